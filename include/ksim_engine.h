@@ -1,0 +1,296 @@
+/*
+ * ksim_engine.h — C ABI of the MI355X scheduling-cycle engine (libksim_engine.so).
+ *
+ * This is the drop-in boundary described in SURVEY.md §8(b).  In the reference
+ * (ThomasK33/kube-scheduler-simulator) the per-pod scheduling cycle runs the
+ * in-tree plugins through the simulator's wrapper:
+ *
+ *   factory closure        simulator/scheduler/plugin/plugins.go:75-87
+ *     r(configuration, f)  -> original in-tree plugin   (replaced by this engine)
+ *     NewWrappedPlugin(..) -> result recording          (kept, unchanged)
+ *   wrappedPlugin.PreFilter/Filter/PreScore/Score/NormalizeScore/Reserve
+ *                          simulator/scheduler/plugin/wrappedplugin.go:356-516,583-612
+ *
+ * A cgo package would bind exactly these entry points.
+ * All types are plain C: fixed-width integers, pointers and sizes.  No Go
+ * pointer is retained after a call returns (cgo rule); every input is copied
+ * during the call, every output is written into caller-provided memory.
+ *
+ * Semantics follow upstream k8s.io/kubernetes v1.26.2 (pinned in
+ * simulator/go.mod:53) as restated in SURVEY.md Appendix A and in DESIGN.md.
+ */
+#ifndef KSIM_ENGINE_H
+#define KSIM_ENGINE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSIM_ABI_VERSION 1
+
+/* ---- limits ------------------------------------------------------------ */
+#define KSIM_MAX_NODES        (1 << 18)  /* tie-break key packs the node index in 18 bits */
+#define KSIM_MAX_NODE_TAINTS  8          /* taints per node, node.Spec.Taints order */
+#define KSIM_TAINT_WORDS      4          /* taint vocabulary <= 256 ids (id 0 = none) */
+#define KSIM_MAX_SCALAR       4          /* scalar (extended) resource columns */
+#define KSIM_MAX_LABEL_COLS   32         /* node label keys known to the engine */
+#define KSIM_EXPR_VALS        6          /* values per node-selector requirement */
+#define KSIM_MAX_FILTER       16
+#define KSIM_MAX_SCORE        8
+#define KSIM_MAX_RES          4          /* resources in a scoring strategy */
+
+/* ---- error codes (SURVEY §8(b) "Errors") -------------------------------- */
+#define KSIM_OK            0
+#define KSIM_E_INVALID    -1
+#define KSIM_E_DEVICE     -2
+#define KSIM_E_OOM        -3
+#define KSIM_E_RCCL       -4
+#define KSIM_E_UNSUPPORTED -5
+
+/* ---- plugin ids.  Names are the upstream in-tree plugin names. ---------- */
+enum ksim_plugin {
+  KSIM_PL_NODE_UNSCHEDULABLE = 0,   /* NodeUnschedulable */
+  KSIM_PL_NODE_NAME,                /* NodeName */
+  KSIM_PL_TAINT_TOLERATION,         /* TaintToleration */
+  KSIM_PL_NODE_AFFINITY,            /* NodeAffinity */
+  KSIM_PL_NODE_PORTS,               /* NodePorts */
+  KSIM_PL_NODE_RESOURCES_FIT,       /* NodeResourcesFit */
+  KSIM_PL_VOLUME_RESTRICTIONS,      /* VolumeRestrictions */
+  KSIM_PL_EBS_LIMITS,               /* EBSLimits */
+  KSIM_PL_GCEPD_LIMITS,             /* GCEPDLimits */
+  KSIM_PL_NODE_VOLUME_LIMITS,       /* NodeVolumeLimits */
+  KSIM_PL_AZURE_DISK_LIMITS,        /* AzureDiskLimits */
+  KSIM_PL_VOLUME_BINDING,           /* VolumeBinding */
+  KSIM_PL_VOLUME_ZONE,              /* VolumeZone */
+  KSIM_PL_POD_TOPOLOGY_SPREAD,      /* PodTopologySpread */
+  KSIM_PL_INTER_POD_AFFINITY,       /* InterPodAffinity */
+  KSIM_PL_BALANCED_ALLOCATION,      /* NodeResourcesBalancedAllocation */
+  KSIM_PL_IMAGE_LOCALITY,           /* ImageLocality */
+  KSIM_PL_COUNT
+};
+
+/* taint effects */
+#define KSIM_EFFECT_NONE               0
+#define KSIM_EFFECT_NO_SCHEDULE        1
+#define KSIM_EFFECT_PREFER_NO_SCHEDULE 2
+#define KSIM_EFFECT_NO_EXECUTE         3
+
+/* resources usable in scoring strategies (ScoringStrategy.Resources) */
+#define KSIM_RES_CPU        0
+#define KSIM_RES_MEMORY     1
+#define KSIM_RES_EPHEMERAL  2
+#define KSIM_RES_SCALAR0    3   /* KSIM_RES_SCALAR0 + k = scalar column k */
+
+/* node flags */
+#define KSIM_NODE_UNSCHEDULABLE  1u   /* node.Spec.Unschedulable */
+
+/* pod flags */
+#define KSIM_POD_TOLERATES_UNSCHEDULABLE 1u  /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
+#define KSIM_POD_HAS_REQUIRED_AFFINITY   2u  /* spec.affinity.nodeAffinity.required != nil */
+#define KSIM_POD_HAS_SCALAR              4u  /* len(request.ScalarResources) > 0 */
+#define KSIM_POD_HAS_HOST_PORTS          8u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
+#define KSIM_POD_HAS_VOLUMES            16u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
+
+/* node-selector requirement operators (k8s NodeSelectorOperator + matchFields) */
+#define KSIM_OP_IN            0
+#define KSIM_OP_NOT_IN        1
+#define KSIM_OP_EXISTS        2
+#define KSIM_OP_DOES_NOT_EXIST 3
+#define KSIM_OP_GT            4
+#define KSIM_OP_LT            5
+#define KSIM_OP_FIELD_IN      6  /* matchFields metadata.name In   (vals = node positions) */
+#define KSIM_OP_FIELD_NOT_IN  7  /* matchFields metadata.name NotIn */
+#define KSIM_OP_FALSE         8  /* requirement that can never match (e.g. unknown value) */
+#define KSIM_OP_TRUE          9  /* requirement that always matches (e.g. NotIn of unknown values) */
+
+/* Filter outcome per node (ksim_eval_out.fail_plugin) */
+#define KSIM_PASSED        0xFF
+#define KSIM_NOT_EVALUATED 0xFE
+
+/* NodeResourcesFit failure reason bits (ksim_eval_out.fail_detail) */
+#define KSIM_FIT_TOO_MANY_PODS   1u
+#define KSIM_FIT_CPU             2u
+#define KSIM_FIT_MEMORY          4u
+#define KSIM_FIT_EPHEMERAL       8u
+#define KSIM_FIT_SCALAR0        16u   /* << k for scalar column k */
+
+/* per-pod cycle status */
+#define KSIM_STATUS_SCHEDULED      0
+#define KSIM_STATUS_UNSCHEDULABLE  1   /* FitError: no feasible node */
+
+/* ---- cluster snapshot (SoA; one entry per node in nodeTree order) -------- */
+/* Mirrors [upstream] framework.NodeInfo: Allocatable, Requested,
+ * NonZeroRequested, len(Pods); node.Spec.{Unschedulable,Taints}; node labels. */
+typedef struct ksim_node_table {
+  int32_t n_nodes;
+  int32_t n_scalar;               /* <= KSIM_MAX_SCALAR */
+  int32_t n_label_cols;           /* <= KSIM_MAX_LABEL_COLS */
+  int32_t _pad0;
+  const int64_t*  alloc_cpu;      /* Allocatable.MilliCPU */
+  const int64_t*  alloc_mem;      /* Allocatable.Memory */
+  const int64_t*  alloc_eph;      /* Allocatable.EphemeralStorage */
+  const int32_t*  alloc_pods;     /* Allocatable.AllowedPodNumber */
+  const int64_t*  alloc_scalar;   /* [n_scalar][n_nodes] */
+  const int64_t*  req_cpu;        /* Requested.* */
+  const int64_t*  req_mem;
+  const int64_t*  req_eph;
+  const int64_t*  req_scalar;     /* [n_scalar][n_nodes] */
+  const int64_t*  nz_cpu;         /* NonZeroRequested.MilliCPU */
+  const int64_t*  nz_mem;         /* NonZeroRequested.Memory */
+  const int32_t*  num_pods;       /* len(NodeInfo.Pods) */
+  const uint32_t* flags;          /* KSIM_NODE_* */
+  const uint16_t* taints;         /* [KSIM_MAX_NODE_TAINTS][n_nodes]; taint vocab id, 0 terminates */
+  const uint32_t* labels;         /* [n_label_cols][n_nodes]; label value id, 0 = key absent */
+} ksim_node_table;
+
+/* Vocabularies the host interned (strings stay on the host). */
+typedef struct ksim_vocab {
+  int32_t n_taints;               /* taint vocabulary size incl. id 0 (<= 64*KSIM_TAINT_WORDS) */
+  int32_t n_label_values;         /* entries of label_num / label_num_ok */
+  const uint8_t* taint_effect;    /* [n_taints] KSIM_EFFECT_* */
+  const int32_t* label_col_offset;/* [n_label_cols]: base index of the column's value ids */
+  const int64_t* label_num;       /* strconv.ParseInt(value,10,64) per (col, value id) */
+  const uint8_t* label_num_ok;    /* 1 if that parse succeeded */
+} ksim_vocab;
+
+/* One NodeSelectorRequirement compiled against the vocabulary. */
+typedef struct ksim_label_expr {
+  int64_t  num;                     /* Gt/Lt operand */
+  uint32_t vals[KSIM_EXPR_VALS];    /* value ids (In/NotIn) or node positions (FIELD_*) */
+  uint16_t col;                     /* node label column */
+  uint8_t  op;                      /* KSIM_OP_* */
+  uint8_t  nvals;
+  uint32_t _pad;
+} ksim_label_expr;                  /* 40 bytes */
+
+/* NodeSelectorTerm = AND of exprs[first .. first+n_expr); n_expr == 0 -> empty
+ * term, which matches nothing (component-helpers nodeSelectorTerm.match). */
+typedef struct ksim_term {
+  int32_t first_expr;
+  int32_t n_expr;
+  int32_t weight;                   /* PreferredSchedulingTerm.Weight (preferred terms only) */
+  int32_t _pad;
+} ksim_term;                        /* 16 bytes */
+
+/* A pod compiled by the host (resources already summed per Fit PreFilter
+ * computePodResourceRequest / NodeInfo calculateResource). */
+typedef struct ksim_pod {
+  int64_t  req_cpu, req_mem, req_eph;        /* requests: max(sum containers, any init) + overhead */
+  int64_t  nz_cpu, nz_mem;                   /* non-zero requests (100m / 200Mi defaults) */
+  int64_t  scalar_req[KSIM_MAX_SCALAR];      /* per node scalar column; 0 = not requested */
+  uint64_t tol_filter[KSIM_TAINT_WORDS];     /* bit t: taint t tolerated by pod.Spec.Tolerations */
+  uint64_t tol_prefer[KSIM_TAINT_WORDS];     /* bit t: tolerated by tolerations with effect "" or PreferNoSchedule */
+  int32_t  node_name;                        /* -1: spec.nodeName empty; -2: unknown node; else node position */
+  uint32_t flags;                            /* KSIM_POD_* */
+  int32_t  sel_first, sel_count;             /* spec.nodeSelector as In{value} exprs (AND) */
+  int32_t  req_term_first, req_term_count;   /* required node affinity terms (OR) */
+  int32_t  pref_term_first, pref_term_count; /* preferred node affinity terms */
+  int32_t  _reserved[8];                     /* topology spread / pod affinity (later ABI rev) */
+} ksim_pod;
+
+typedef struct ksim_pod_set {
+  int32_t n_pods;
+  int32_t n_exprs;
+  int32_t n_terms;
+  int32_t _pad;
+  const ksim_pod* pods;
+  const ksim_label_expr* exprs;
+  const ksim_term* terms;
+} ksim_pod_set;
+
+/* Profile: the converted KubeSchedulerProfile (simulator/scheduler/scheduler.go:199-249,
+ * plugins.go:185-220) restricted to what the cycle needs. */
+typedef struct ksim_profile {
+  int32_t n_filter;
+  int32_t n_score;
+  uint8_t filter[KSIM_MAX_FILTER];     /* ksim_plugin ids, profile Filter order */
+  uint8_t score[KSIM_MAX_SCORE];       /* ksim_plugin ids, profile Score order */
+  int32_t score_weight[KSIM_MAX_SCORE];/* profile weights; 0 is treated as 1 (framework) */
+  int32_t percentage_of_nodes_to_score;/* 0 = adaptive (simulator default), 100 = all */
+  /* NodeResourcesFit ScoringStrategy (LeastAllocated) */
+  int32_t fit_n_res;
+  int32_t fit_res[KSIM_MAX_RES];       /* KSIM_RES_* */
+  int64_t fit_res_weight[KSIM_MAX_RES];
+  /* NodeResourcesBalancedAllocation resources */
+  int32_t ba_n_res;
+  int32_t ba_res[KSIM_MAX_RES];
+  int64_t ba_res_weight[KSIM_MAX_RES];
+  int32_t hard_pod_affinity_weight;    /* InterPodAffinityArgs (default 1) */
+  int32_t _pad;
+  uint64_t tiebreak_seed;              /* selectHost fixed-seed tie-break TB(seed) */
+} ksim_profile;
+
+/* Full per-node outputs of one scheduling cycle (compat mode: what the
+ * wrapper records into the result store).  Any pointer may be NULL. */
+typedef struct ksim_eval_out {
+  uint8_t*  fail_plugin;   /* [n_nodes] filter-order index of the first failing plugin,
+                              KSIM_PASSED, or KSIM_NOT_EVALUATED (ADAPT scan never reached it) */
+  uint32_t* fail_detail;   /* [n_nodes] reason detail (Fit bits, taint id, ...) */
+  uint8_t*  scored;        /* [n_nodes] 1 if the node was in the list passed to Score */
+  int64_t*  raw;           /* [n_score][n_nodes] Score() result for scored nodes */
+  int64_t*  norm;          /* [n_score][n_nodes] after NormalizeScore (raw if the plugin has none) */
+  int64_t*  total;         /* [n_nodes] sum of norm * profile weight */
+  int32_t chosen;          /* node position, -1 if unschedulable */
+  int32_t status;          /* KSIM_STATUS_* */
+  int32_t n_feasible;      /* feasible nodes kept (<= K) */
+  int32_t n_evaluated;     /* nodes whose filter chain ran */
+  int32_t n_processed;     /* feasible + failed (nextStartNodeIndex advance) */
+  int32_t k_to_find;       /* numFeasibleNodesToFind */
+  int32_t next_start;      /* nextStartNodeIndex after this cycle */
+  int32_t _pad;
+} ksim_eval_out;
+
+typedef struct ksim_batch_stats {
+  int64_t pods;            /* cycles run */
+  int64_t scheduled;
+  int64_t unschedulable;
+  int64_t evals;           /* pod x node filter evaluations (SURVEY §8(d) definition) */
+  double  device_ms;       /* device time of the batch (HIP events) */
+} ksim_batch_stats;
+
+typedef struct ksim_handle ksim_handle;
+
+/* ---- lifecycle ----------------------------------------------------------- */
+int  ksim_abi_version(void);
+/* sizeof() of the ABI structs, for binding-layout checks: which = 0 node_table,
+ * 1 vocab, 2 label_expr, 3 term, 4 pod, 5 pod_set, 6 profile, 7 eval_out, 8 batch_stats */
+size_t ksim_abi_sizeof(int which);
+int  ksim_create(int device, ksim_handle** out);
+void ksim_destroy(ksim_handle* h);
+const char* ksim_last_error(const ksim_handle* h);
+
+/* ---- configuration / snapshot ------------------------------------------- */
+int ksim_set_profile(ksim_handle* h, const ksim_profile* p);
+/* Replace the whole snapshot (nodes already in nodeTree order). Resets nextStartNodeIndex. */
+int ksim_set_cluster(ksim_handle* h, const ksim_node_table* nodes, const ksim_vocab* vocab);
+/* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
+int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
+                        int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods);
+int ksim_get_next_start(ksim_handle* h, int32_t* next_start);
+int ksim_set_next_start(ksim_handle* h, int32_t next_start);
+/* Pod sequence number used by the tie-break (advances once per cycle). */
+int ksim_set_pod_seq(ksim_handle* h, int64_t seq);
+
+/* ---- scheduling cycles --------------------------------------------------- */
+/* One full cycle for pod `pod_index` of `pods` (compat mode) incl. assume/bind. */
+int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
+/* Assume/forget a pod on a node (NodeInfo.AddPod / RemovePod). */
+int ksim_assume(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
+int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
+
+/* Batch mode: upload a pod set once (device-resident), then schedule a range
+ * of it in queue order; chosen[i] = node position or -1.  */
+int ksim_load_pods(ksim_handle* h, const ksim_pod_set* pods);
+int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count,
+                         int32_t* chosen, ksim_batch_stats* stats);
+/* Convenience: load + schedule all. */
+int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* pods, int32_t* chosen,
+                        ksim_batch_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSIM_ENGINE_H */

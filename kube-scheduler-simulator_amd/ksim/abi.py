@@ -1,0 +1,235 @@
+"""ctypes / numpy mirror of include/ksim_engine.h (the C-ABI boundary).
+
+The structs are the ones a cgo package would pass across the boundary
+(SURVEY.md §8(b)); tests check every size against ``ksim_abi_sizeof``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+ABI_VERSION = 1
+
+MAX_NODES = 1 << 18
+MAX_NODE_TAINTS = 8
+TAINT_WORDS = 4
+MAX_SCALAR = 4
+MAX_LABEL_COLS = 32
+EXPR_VALS = 6
+MAX_FILTER = 16
+MAX_SCORE = 8
+MAX_RES = 4
+
+OK = 0
+E_INVALID = -1
+E_DEVICE = -2
+E_OOM = -3
+E_RCCL = -4
+E_UNSUPPORTED = -5
+
+# plugin ids (enum ksim_plugin); names are the upstream in-tree plugin names
+PLUGINS = [
+    "NodeUnschedulable",
+    "NodeName",
+    "TaintToleration",
+    "NodeAffinity",
+    "NodePorts",
+    "NodeResourcesFit",
+    "VolumeRestrictions",
+    "EBSLimits",
+    "GCEPDLimits",
+    "NodeVolumeLimits",
+    "AzureDiskLimits",
+    "VolumeBinding",
+    "VolumeZone",
+    "PodTopologySpread",
+    "InterPodAffinity",
+    "NodeResourcesBalancedAllocation",
+    "ImageLocality",
+]
+PLUGIN_ID = {n: i for i, n in enumerate(PLUGINS)}
+PL_NODE_UNSCHEDULABLE = 0
+PL_NODE_NAME = 1
+PL_TAINT_TOLERATION = 2
+PL_NODE_AFFINITY = 3
+PL_NODE_PORTS = 4
+PL_NODE_RESOURCES_FIT = 5
+PL_POD_TOPOLOGY_SPREAD = 13
+PL_INTER_POD_AFFINITY = 14
+PL_BALANCED_ALLOCATION = 15
+PL_IMAGE_LOCALITY = 16
+
+EFFECT_NONE = 0
+EFFECT_NO_SCHEDULE = 1
+EFFECT_PREFER_NO_SCHEDULE = 2
+EFFECT_NO_EXECUTE = 3
+EFFECT_ID = {"": EFFECT_NONE, "NoSchedule": EFFECT_NO_SCHEDULE,
+             "PreferNoSchedule": EFFECT_PREFER_NO_SCHEDULE, "NoExecute": EFFECT_NO_EXECUTE}
+
+RES_CPU = 0
+RES_MEMORY = 1
+RES_EPHEMERAL = 2
+RES_SCALAR0 = 3
+
+NODE_UNSCHEDULABLE = 1
+
+POD_TOLERATES_UNSCHEDULABLE = 1
+POD_HAS_REQUIRED_AFFINITY = 2
+POD_HAS_SCALAR = 4
+POD_HAS_HOST_PORTS = 8
+POD_HAS_VOLUMES = 16
+
+OP_IN = 0
+OP_NOT_IN = 1
+OP_EXISTS = 2
+OP_DOES_NOT_EXIST = 3
+OP_GT = 4
+OP_LT = 5
+OP_FIELD_IN = 6
+OP_FIELD_NOT_IN = 7
+OP_FALSE = 8
+OP_TRUE = 9
+
+PASSED = 0xFF
+NOT_EVALUATED = 0xFE
+
+FIT_TOO_MANY_PODS = 1
+FIT_CPU = 2
+FIT_MEMORY = 4
+FIT_EPHEMERAL = 8
+FIT_SCALAR0 = 16
+
+STATUS_SCHEDULED = 0
+STATUS_UNSCHEDULABLE = 1
+
+# ---- numpy dtypes (align=True reproduces the C layout) -------------------
+LABEL_EXPR_DTYPE = np.dtype(
+    [("num", "<i8"), ("vals", "<u4", (EXPR_VALS,)), ("col", "<u2"), ("op", "u1"),
+     ("nvals", "u1"), ("_pad", "<u4")], align=True)
+TERM_DTYPE = np.dtype(
+    [("first_expr", "<i4"), ("n_expr", "<i4"), ("weight", "<i4"), ("_pad", "<i4")], align=True)
+POD_DTYPE = np.dtype(
+    [("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_eph", "<i8"),
+     ("nz_cpu", "<i8"), ("nz_mem", "<i8"),
+     ("scalar_req", "<i8", (MAX_SCALAR,)),
+     ("tol_filter", "<u8", (TAINT_WORDS,)), ("tol_prefer", "<u8", (TAINT_WORDS,)),
+     ("node_name", "<i4"), ("flags", "<u4"),
+     ("sel_first", "<i4"), ("sel_count", "<i4"),
+     ("req_term_first", "<i4"), ("req_term_count", "<i4"),
+     ("pref_term_first", "<i4"), ("pref_term_count", "<i4"),
+     ("_reserved", "<i4", (8,))], align=True)
+
+
+def _p(arr):
+    """Pointer to a numpy array's data (None for None / empty)."""
+    if arr is None:
+        return None
+    return ctypes.c_void_p(arr.ctypes.data) if arr.size else None
+
+
+class NodeTable(ctypes.Structure):
+    _fields_ = [
+        ("n_nodes", ctypes.c_int32), ("n_scalar", ctypes.c_int32),
+        ("n_label_cols", ctypes.c_int32), ("_pad0", ctypes.c_int32),
+        ("alloc_cpu", ctypes.c_void_p), ("alloc_mem", ctypes.c_void_p),
+        ("alloc_eph", ctypes.c_void_p), ("alloc_pods", ctypes.c_void_p),
+        ("alloc_scalar", ctypes.c_void_p),
+        ("req_cpu", ctypes.c_void_p), ("req_mem", ctypes.c_void_p),
+        ("req_eph", ctypes.c_void_p), ("req_scalar", ctypes.c_void_p),
+        ("nz_cpu", ctypes.c_void_p), ("nz_mem", ctypes.c_void_p),
+        ("num_pods", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+        ("taints", ctypes.c_void_p), ("labels", ctypes.c_void_p),
+    ]
+
+
+class Vocab(ctypes.Structure):
+    _fields_ = [
+        ("n_taints", ctypes.c_int32), ("n_label_values", ctypes.c_int32),
+        ("taint_effect", ctypes.c_void_p), ("label_col_offset", ctypes.c_void_p),
+        ("label_num", ctypes.c_void_p), ("label_num_ok", ctypes.c_void_p),
+    ]
+
+
+class PodSet(ctypes.Structure):
+    _fields_ = [
+        ("n_pods", ctypes.c_int32), ("n_exprs", ctypes.c_int32),
+        ("n_terms", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("pods", ctypes.c_void_p), ("exprs", ctypes.c_void_p), ("terms", ctypes.c_void_p),
+    ]
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [
+        ("n_filter", ctypes.c_int32), ("n_score", ctypes.c_int32),
+        ("filter", ctypes.c_uint8 * MAX_FILTER), ("score", ctypes.c_uint8 * MAX_SCORE),
+        ("score_weight", ctypes.c_int32 * MAX_SCORE),
+        ("percentage_of_nodes_to_score", ctypes.c_int32),
+        ("fit_n_res", ctypes.c_int32), ("fit_res", ctypes.c_int32 * MAX_RES),
+        ("fit_res_weight", ctypes.c_int64 * MAX_RES),
+        ("ba_n_res", ctypes.c_int32), ("ba_res", ctypes.c_int32 * MAX_RES),
+        ("ba_res_weight", ctypes.c_int64 * MAX_RES),
+        ("hard_pod_affinity_weight", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("tiebreak_seed", ctypes.c_uint64),
+    ]
+
+
+class EvalOut(ctypes.Structure):
+    _fields_ = [
+        ("fail_plugin", ctypes.c_void_p), ("fail_detail", ctypes.c_void_p),
+        ("scored", ctypes.c_void_p), ("raw", ctypes.c_void_p), ("norm", ctypes.c_void_p),
+        ("total", ctypes.c_void_p),
+        ("chosen", ctypes.c_int32), ("status", ctypes.c_int32),
+        ("n_feasible", ctypes.c_int32), ("n_evaluated", ctypes.c_int32),
+        ("n_processed", ctypes.c_int32), ("k_to_find", ctypes.c_int32),
+        ("next_start", ctypes.c_int32), ("_pad", ctypes.c_int32),
+    ]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [
+        ("pods", ctypes.c_int64), ("scheduled", ctypes.c_int64),
+        ("unschedulable", ctypes.c_int64), ("evals", ctypes.c_int64),
+        ("device_ms", ctypes.c_double),
+    ]
+
+
+STRUCT_ORDER = [NodeTable, Vocab, LABEL_EXPR_DTYPE, TERM_DTYPE, POD_DTYPE, PodSet, Profile,
+                EvalOut, BatchStats]
+
+
+def struct_size(s) -> int:
+    return s.itemsize if isinstance(s, np.dtype) else ctypes.sizeof(s)
+
+
+class EvalBuffers:
+    """Caller-owned output arrays for one compat-mode cycle (ksim_eval_out)."""
+
+    def __init__(self, n_nodes: int, n_score: int):
+        self.fail_plugin = np.zeros(n_nodes, np.uint8)
+        self.fail_detail = np.zeros(n_nodes, np.uint32)
+        self.scored = np.zeros(n_nodes, np.uint8)
+        self.raw = np.zeros((max(n_score, 1), n_nodes), np.int64)
+        self.norm = np.zeros((max(n_score, 1), n_nodes), np.int64)
+        self.total = np.zeros(n_nodes, np.int64)
+        self.out = EvalOut()
+        self.out.fail_plugin = _p(self.fail_plugin)
+        self.out.fail_detail = _p(self.fail_detail)
+        self.out.scored = _p(self.scored)
+        self.out.raw = _p(self.raw)
+        self.out.norm = _p(self.norm)
+        self.out.total = _p(self.total)
+
+    def result(self) -> dict:
+        o = self.out
+        return dict(chosen=o.chosen, status=o.status, n_feasible=o.n_feasible,
+                    n_evaluated=o.n_evaluated, n_processed=o.n_processed,
+                    k_to_find=o.k_to_find, next_start=o.next_start,
+                    fail_plugin=self.fail_plugin.copy(), fail_detail=self.fail_detail.copy(),
+                    scored=self.scored.copy(), raw=self.raw.copy(), norm=self.norm.copy(),
+                    total=self.total.copy())
+
+
+def repo_root() -> str:
+    return os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))

@@ -1,0 +1,479 @@
+"""Host snapshot encoder: Node/Pod objects -> the engine's SoA buffers.
+
+Mirrors what [upstream] internal/cache does before each cycle (snapshot in
+nodeTree order, NodeInfo aggregates) and what each plugin's PreFilter/PreScore
+precomputes per pod (request sums, toleration sets, compiled affinity), so
+the device only sees integer ids (SURVEY.md §2.3 "Host snapshot encoder").
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .model import (Node, Pod, Taint, Toleration, quantity_milli_value, quantity_value)
+
+LABEL_HOSTNAME = "kubernetes.io/hostname"
+LABEL_ZONE = "topology.kubernetes.io/zone"
+LABEL_REGION = "topology.kubernetes.io/region"
+LABEL_ZONE_BETA = "failure-domain.beta.kubernetes.io/zone"
+LABEL_REGION_BETA = "failure-domain.beta.kubernetes.io/region"
+TAINT_NODE_UNSCHEDULABLE = "node.kubernetes.io/unschedulable"
+
+DEFAULT_MILLI_CPU_REQUEST = 100                 # schedutil.DefaultMilliCPURequest
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024      # schedutil.DefaultMemoryRequest
+_NATIVE = ("cpu", "memory", "ephemeral-storage", "pods")
+
+
+class EncodeError(ValueError):
+    pass
+
+
+def zone_key(labels: Dict[str, str]) -> str:
+    """component-helpers node/topology GetZoneKey."""
+    zone = labels.get(LABEL_ZONE, labels.get(LABEL_ZONE_BETA, ""))
+    region = labels.get(LABEL_REGION, labels.get(LABEL_REGION_BETA, ""))
+    if region == "" and zone == "":
+        return ""
+    return region + ":\x00:" + zone
+
+
+def node_tree_order(zone_keys: Sequence[str]) -> List[int]:
+    """[upstream] internal/cache/node_tree.go nodeTree.list(): round-robin over
+    zones (zone insertion order), insertion order inside each zone."""
+    zones: List[str] = []
+    tree: Dict[str, List[int]] = {}
+    for i, z in enumerate(zone_keys):
+        if z not in tree:
+            zones.append(z)
+            tree[z] = []
+        tree[z].append(i)
+    out: List[int] = []
+    idx = 0
+    n = len(zone_keys)
+    while len(out) < n:
+        for z in zones:
+            lst = tree[z]
+            if idx < len(lst):
+                out.append(lst[idx])
+        idx += 1
+    return out
+
+
+# ---- pod resource sums ------------------------------------------------------
+def _res(requests: Dict[str, str], name: str) -> int:
+    q = requests.get(name)
+    if q is None:
+        return 0
+    return quantity_milli_value(q) if name == "cpu" else quantity_value(q)
+
+
+def pod_requests(pod: Pod) -> Dict[str, int]:
+    """computePodResourceRequest ([upstream] noderesources/fit.go) ==
+    NodeInfo calculateResource 'res': sum containers, max init, + overhead."""
+    names = set()
+    for c in pod.containers + pod.init_containers:
+        names.update(c.requests)
+    names.update(pod.overhead)
+    out = {}
+    for n in names:
+        if n == "pods":
+            continue
+        v = sum(_res(c.requests, n) for c in pod.containers)
+        for ic in pod.init_containers:
+            v = max(v, _res(ic.requests, n))
+        v += _res(pod.overhead, n)
+        out[n] = v
+    return out
+
+
+def _nonzero(requests: Dict[str, str]) -> Tuple[int, int]:
+    """schedutil.GetNonzeroRequests."""
+    cpu = DEFAULT_MILLI_CPU_REQUEST if "cpu" not in requests else _res(requests, "cpu")
+    mem = DEFAULT_MEMORY_REQUEST if "memory" not in requests else _res(requests, "memory")
+    return cpu, mem
+
+
+def pod_nonzero_requests(pod: Pod) -> Tuple[int, int]:
+    """NodeInfo calculateResource non0CPU/non0Mem (== the LeastAllocated pod
+    request computed with nonZero=true)."""
+    cpu = mem = 0
+    for c in pod.containers:
+        a, b = _nonzero(c.requests)
+        cpu += a
+        mem += b
+    for ic in pod.init_containers:
+        a, b = _nonzero(ic.requests)
+        cpu = max(cpu, a)
+        mem = max(mem, b)
+    if "cpu" in pod.overhead:
+        cpu += _res(pod.overhead, "cpu")
+    if "memory" in pod.overhead:
+        mem += _res(pod.overhead, "memory")
+    return cpu, mem
+
+
+# ---- encoded buffers --------------------------------------------------------
+@dataclass
+class EncodedCluster:
+    n_nodes: int
+    n_scalar: int
+    alloc_cpu: np.ndarray
+    alloc_mem: np.ndarray
+    alloc_eph: np.ndarray
+    alloc_pods: np.ndarray
+    alloc_scalar: np.ndarray          # [n_scalar][N]
+    req_cpu: np.ndarray
+    req_mem: np.ndarray
+    req_eph: np.ndarray
+    req_scalar: np.ndarray            # [n_scalar][N]
+    nz_cpu: np.ndarray
+    nz_mem: np.ndarray
+    num_pods: np.ndarray
+    flags: np.ndarray
+    taints: np.ndarray                # [MAX_NODE_TAINTS][N] uint16
+    labels: np.ndarray                # [L][N] uint32
+    taint_effect: np.ndarray          # [V] uint8
+    label_col_offset: np.ndarray      # [L] int32
+    label_num: np.ndarray             # int64
+    label_num_ok: np.ndarray          # uint8
+    # host metadata (strings never cross the boundary)
+    node_names: List[str] = field(default_factory=list)
+    label_keys: List[str] = field(default_factory=list)
+    label_values: List[List[str]] = field(default_factory=list)   # per col: [vid] -> value
+    taint_vocab: List[Taint] = field(default_factory=list)        # [tid] (tid 0 = None)
+    scalar_names: List[str] = field(default_factory=list)
+
+    @property
+    def n_label_cols(self) -> int:
+        return int(self.labels.shape[0])
+
+    def node_table(self) -> abi.NodeTable:
+        t = abi.NodeTable()
+        t.n_nodes = self.n_nodes
+        t.n_scalar = self.n_scalar
+        t.n_label_cols = self.n_label_cols
+        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "alloc_scalar",
+                  "req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem",
+                  "num_pods", "flags", "taints", "labels"):
+            setattr(t, f, abi._p(getattr(self, f)))
+        return t
+
+    def vocab(self) -> abi.Vocab:
+        v = abi.Vocab()
+        v.n_taints = int(self.taint_effect.size)
+        v.n_label_values = int(self.label_num.size)
+        v.taint_effect = abi._p(self.taint_effect)
+        v.label_col_offset = abi._p(self.label_col_offset)
+        v.label_num = abi._p(self.label_num)
+        v.label_num_ok = abi._p(self.label_num_ok)
+        return v
+
+    def label_col(self, key: str) -> int:
+        return self.label_keys.index(key) if key in self.label_keys else -1
+
+    def value_id(self, col: int, value: str) -> int:
+        if col < 0:
+            return 0
+        try:
+            return self.label_values[col].index(value)
+        except ValueError:
+            return 0
+
+    def copy_state(self) -> "EncodedCluster":
+        import copy
+        c = copy.copy(self)
+        for f in ("req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem", "num_pods"):
+            setattr(c, f, getattr(self, f).copy())
+        return c
+
+
+@dataclass
+class EncodedPods:
+    pods: np.ndarray                  # POD_DTYPE
+    exprs: np.ndarray                 # LABEL_EXPR_DTYPE
+    terms: np.ndarray                 # TERM_DTYPE
+    names: List[Tuple[str, str]] = field(default_factory=list)   # (namespace, name)
+
+    @property
+    def n_pods(self) -> int:
+        return int(self.pods.size)
+
+    def pod_set(self) -> abi.PodSet:
+        s = abi.PodSet()
+        s.n_pods = int(self.pods.size)
+        s.n_exprs = int(self.exprs.size)
+        s.n_terms = int(self.terms.size)
+        s.pods = abi._p(self.pods)
+        s.exprs = abi._p(self.exprs)
+        s.terms = abi._p(self.terms)
+        return s
+
+    def subset(self, first: int, count: int) -> "EncodedPods":
+        return EncodedPods(self.pods[first:first + count].copy(), self.exprs, self.terms,
+                           self.names[first:first + count])
+
+
+# ---- cluster encoder --------------------------------------------------------
+def _parse_int64(s: str) -> Optional[int]:
+    """strconv.ParseInt(s, 10, 64)."""
+    t = s[1:] if s[:1] in "+-" else s
+    if not t or not t.isdigit():
+        return None
+    v = int(s)
+    if v < -(2 ** 63) or v > 2 ** 63 - 1:
+        return None
+    return v
+
+
+def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
+                   extra_scalar: Sequence[str] = ()) -> Tuple[EncodedCluster, List[int]]:
+    """Encode nodes in nodeTree order.  Returns (cluster, order) where
+    order[position] = index into ``nodes``.  ``bound_pods`` (spec.nodeName set)
+    are added to their node's aggregates like NodeInfo.AddPod."""
+    order = node_tree_order([zone_key(n.labels) for n in nodes])
+    ns = [nodes[i] for i in order]
+    N = len(ns)
+    if N > abi.MAX_NODES:
+        raise EncodeError("too many nodes")
+    # scalar resources: every non-native allocatable / requested name
+    scalar: List[str] = []
+    for n in ns:
+        for k in n.allocatable:
+            if k not in _NATIVE and k not in scalar:
+                scalar.append(k)
+    for k in extra_scalar:
+        if k not in scalar:
+            scalar.append(k)
+    if len(scalar) > abi.MAX_SCALAR:
+        raise EncodeError("too many scalar resources")
+    S = len(scalar)
+    # label columns
+    keys: List[str] = []
+    for n in ns:
+        for k in n.labels:
+            if k not in keys:
+                keys.append(k)
+    if len(keys) > abi.MAX_LABEL_COLS:
+        raise EncodeError("too many label keys")
+    values: List[List[str]] = [[""] for _ in keys]
+    vindex: List[Dict[str, int]] = [{} for _ in keys]
+    labels = np.zeros((max(len(keys), 0), N), np.uint32)
+    for pos, n in enumerate(ns):
+        for k, v in n.labels.items():
+            c = keys.index(k)
+            vid = vindex[c].get(v)
+            if vid is None:
+                vid = len(values[c])
+                values[c].append(v)
+                vindex[c][v] = vid
+            labels[c, pos] = vid
+    offs = np.zeros(len(keys), np.int32)
+    nums, oks = [], []
+    for c in range(len(keys)):
+        offs[c] = len(nums)
+        for v in values[c]:
+            pv = _parse_int64(v) if v != "" else None
+            nums.append(pv if pv is not None else 0)
+            oks.append(1 if pv is not None else 0)
+    # taints
+    tvocab: List[Taint] = [None]  # type: ignore[list-item]
+    tindex: Dict[Tuple[str, str, str], int] = {}
+    taints = np.zeros((abi.MAX_NODE_TAINTS, N), np.uint16)
+    for pos, n in enumerate(ns):
+        if len(n.taints) > abi.MAX_NODE_TAINTS:
+            raise EncodeError(f"node {n.name}: more than {abi.MAX_NODE_TAINTS} taints")
+        for k, t in enumerate(n.taints):
+            key = (t.key, t.value, t.effect)
+            tid = tindex.get(key)
+            if tid is None:
+                tid = len(tvocab)
+                tvocab.append(Taint(t.key, t.value, t.effect))
+                tindex[key] = tid
+            taints[k, pos] = tid
+    if len(tvocab) > 64 * abi.TAINT_WORDS:
+        raise EncodeError("taint vocabulary too large")
+    effect = np.array([0] + [abi.EFFECT_ID.get(t.effect, 0) for t in tvocab[1:]], np.uint8)
+
+    def col(name):
+        return np.array([_res(n.allocatable, name) for n in ns], np.int64)
+
+    c = EncodedCluster(
+        n_nodes=N, n_scalar=S,
+        alloc_cpu=col("cpu"), alloc_mem=col("memory"), alloc_eph=col("ephemeral-storage"),
+        alloc_pods=np.array([_res(n.allocatable, "pods") for n in ns], np.int32),
+        alloc_scalar=np.array([[_res(n.allocatable, s) for n in ns] for s in scalar], np.int64).reshape(S, N),
+        req_cpu=np.zeros(N, np.int64), req_mem=np.zeros(N, np.int64), req_eph=np.zeros(N, np.int64),
+        req_scalar=np.zeros((S, N), np.int64),
+        nz_cpu=np.zeros(N, np.int64), nz_mem=np.zeros(N, np.int64),
+        num_pods=np.zeros(N, np.int32),
+        flags=np.array([abi.NODE_UNSCHEDULABLE if n.unschedulable else 0 for n in ns], np.uint32),
+        taints=taints, labels=labels, taint_effect=effect, label_col_offset=offs,
+        label_num=np.array(nums, np.int64), label_num_ok=np.array(oks, np.uint8),
+        node_names=[n.name for n in ns], label_keys=keys, label_values=values,
+        taint_vocab=tvocab, scalar_names=scalar,
+    )
+    pos_of = {name: i for i, name in enumerate(c.node_names)}
+    for p in bound_pods:
+        if p.node_name not in pos_of:
+            continue
+        i = pos_of[p.node_name]
+        r = pod_requests(p)
+        nz = pod_nonzero_requests(p)
+        c.req_cpu[i] += r.get("cpu", 0)
+        c.req_mem[i] += r.get("memory", 0)
+        c.req_eph[i] += r.get("ephemeral-storage", 0)
+        for k, s in enumerate(scalar):
+            c.req_scalar[k, i] += r.get(s, 0)
+        c.nz_cpu[i] += nz[0]
+        c.nz_mem[i] += nz[1]
+        c.num_pods[i] += 1
+    return c, order
+
+
+# ---- pod encoder --------------------------------------------------------------
+class _PodBuilder:
+    def __init__(self, cluster: EncodedCluster):
+        self.c = cluster
+        self.exprs: List[np.void] = []
+        self.terms: List[Tuple[int, int, int]] = []
+        self.pos_of = {n: i for i, n in enumerate(cluster.node_names)}
+
+    def _expr(self, col=0, op=abi.OP_FALSE, vals=(), num=0):
+        if len(vals) > abi.EXPR_VALS:
+            raise EncodeError("requirement has too many values after vocabulary filtering")
+        e = np.zeros((), abi.LABEL_EXPR_DTYPE)
+        e["col"] = max(col, 0)
+        e["op"] = op
+        e["nvals"] = len(vals)
+        for i, v in enumerate(vals):
+            e["vals"][i] = v
+        e["num"] = num
+        self.exprs.append(e)
+
+    def requirement(self, r) -> None:
+        """nodeSelectorRequirementsAsSelector / fields selector, compiled to ids.
+        Invalid requirements compile to OP_FALSE (LazyErrorNodeSelector drops
+        the term, so it can never match)."""
+        c = self.c
+        col = c.label_col(r.key)
+        op = r.operator
+        if op in ("In", "NotIn"):
+            if not r.values:
+                return self._expr()
+            vids = sorted({c.value_id(col, v) for v in r.values} - {0})
+            if op == "In":
+                return self._expr(col, abi.OP_IN, vids) if vids else self._expr()
+            if not vids:
+                return self._expr(0, abi.OP_TRUE)
+            return self._expr(col, abi.OP_NOT_IN, vids)
+        if op in ("Exists", "DoesNotExist"):
+            if r.values:
+                return self._expr()
+            if col < 0:
+                # key unknown on every node: Exists never, DoesNotExist always
+                return self._expr() if op == "Exists" else self._expr(0, abi.OP_TRUE)
+            return self._expr(col, abi.OP_EXISTS if op == "Exists" else abi.OP_DOES_NOT_EXIST)
+        if op in ("Gt", "Lt"):
+            if len(r.values) != 1:
+                return self._expr()
+            v = _parse_int64(r.values[0])
+            if v is None or col < 0:
+                return self._expr()
+            return self._expr(col, abi.OP_GT if op == "Gt" else abi.OP_LT, [], v)
+        return self._expr()
+
+    def field_requirement(self, r) -> None:
+        # nodeSelectorRequirementsAsFieldSelector: metadata.name In/NotIn with
+        # exactly one value; anything else is a parse error (term dropped).
+        if r.key != "metadata.name" or r.operator not in ("In", "NotIn") or len(r.values) != 1:
+            return self._expr()
+        pos = [self.pos_of[r.values[0]]] if r.values[0] in self.pos_of else []
+        if r.operator == "In":
+            return self._expr(0, abi.OP_FIELD_IN, pos) if pos else self._expr()
+        return self._expr(0, abi.OP_FIELD_NOT_IN, pos) if pos else self._expr(0, abi.OP_TRUE)
+
+    def term(self, t, weight=0) -> None:
+        first = len(self.exprs)
+        for r in t.match_expressions:
+            self.requirement(r)
+        for r in t.match_fields:
+            self.field_requirement(r)
+        self.terms.append((first, len(self.exprs) - first, weight))
+
+
+def _tol_bits(tolerations: Sequence[Toleration], vocab: Sequence[Taint]) -> np.ndarray:
+    w = np.zeros(abi.TAINT_WORDS, np.uint64)
+    for tid in range(1, len(vocab)):
+        if any(t.tolerates(vocab[tid]) for t in tolerations):
+            w[tid >> 6] |= np.uint64(1) << np.uint64(tid & 63)
+    return w
+
+
+def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
+    """Compile pods against the cluster vocabulary (the per-pod PreFilter /
+    PreScore precomputation of Fit, TaintToleration and NodeAffinity)."""
+    b = _PodBuilder(cluster)
+    arr = np.zeros(len(pods), abi.POD_DTYPE)
+    names = []
+    for i, p in enumerate(pods):
+        r = pod_requests(p)
+        nz = pod_nonzero_requests(p)
+        rec = arr[i]
+        rec["req_cpu"] = r.get("cpu", 0)
+        rec["req_mem"] = r.get("memory", 0)
+        rec["req_eph"] = r.get("ephemeral-storage", 0)
+        rec["nz_cpu"], rec["nz_mem"] = nz
+        flags = 0
+        scal = [k for k in r if k not in _NATIVE]
+        if scal:
+            flags |= abi.POD_HAS_SCALAR
+        for k in scal:
+            if k not in cluster.scalar_names:
+                # no node offers it: allocatable 0 everywhere -> needs a column
+                raise EncodeError(f"scalar resource {k} unknown to the cluster encoder (pass extra_scalar)")
+            rec["scalar_req"][cluster.scalar_names.index(k)] = r[k]
+        rec["tol_filter"] = _tol_bits(p.tolerations, cluster.taint_vocab)
+        prefer = [t for t in p.tolerations if t.effect in ("", "PreferNoSchedule")]
+        rec["tol_prefer"] = _tol_bits(prefer, cluster.taint_vocab)
+        if any(t.tolerates(Taint(TAINT_NODE_UNSCHEDULABLE, "", "NoSchedule")) for t in p.tolerations):
+            flags |= abi.POD_TOLERATES_UNSCHEDULABLE
+        if p.node_name:
+            rec["node_name"] = b.pos_of.get(p.node_name, -2)
+        else:
+            rec["node_name"] = -1
+        # spec.nodeSelector -> labels.SelectorFromSet (Equals requirements)
+        rec["sel_first"] = len(b.exprs)
+        for k, v in p.node_selector.items():
+            col = cluster.label_col(k)
+            vid = cluster.value_id(col, v)
+            if vid:
+                b._expr(col, abi.OP_IN, [vid])
+            else:
+                b._expr()
+        rec["sel_count"] = len(b.exprs) - rec["sel_first"]
+        if p.required_terms is not None:
+            flags |= abi.POD_HAS_REQUIRED_AFFINITY
+            rec["req_term_first"] = len(b.terms)
+            for t in p.required_terms:
+                b.term(t)
+            rec["req_term_count"] = len(b.terms) - rec["req_term_first"]
+        rec["pref_term_first"] = len(b.terms)
+        for pt in p.preferred_terms:
+            if pt.weight == 0:
+                continue
+            b.term(pt.term, pt.weight)
+        rec["pref_term_count"] = len(b.terms) - rec["pref_term_first"]
+        if any(c.host_ports for c in p.containers + p.init_containers):
+            flags |= abi.POD_HAS_HOST_PORTS
+        if p.has_volumes:
+            flags |= abi.POD_HAS_VOLUMES
+        rec["flags"] = flags
+        names.append((p.namespace, p.name))
+    exprs = np.array(b.exprs, abi.LABEL_EXPR_DTYPE) if b.exprs else np.zeros(0, abi.LABEL_EXPR_DTYPE)
+    terms = np.zeros(len(b.terms), abi.TERM_DTYPE)
+    for i, (f, n, w) in enumerate(b.terms):
+        terms[i]["first_expr"], terms[i]["n_expr"], terms[i]["weight"] = f, n, w
+    return EncodedPods(arr, exprs, terms, names)

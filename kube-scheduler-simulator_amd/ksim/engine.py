@@ -1,0 +1,150 @@
+"""Binding of libksim_engine.so (the product path).
+
+Fails loudly when the HIP library is missing or no GPU is present: there is no
+CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libksim_engine.so")
+_LIB = None
+
+# Exported symbols declared in include/ksim_engine.h (checked by tests).
+EXPORTS = [
+    "ksim_abi_version", "ksim_abi_sizeof", "ksim_create", "ksim_destroy", "ksim_last_error",
+    "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_next_start",
+    "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
+    "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch",
+]
+
+
+class KsimError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ksim error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C kube-scheduler-simulator_amd/csrc` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.ksim_abi_version.restype = ctypes.c_int
+        L.ksim_abi_sizeof.restype = ctypes.c_size_t
+        L.ksim_abi_sizeof.argtypes = [ctypes.c_int]
+        L.ksim_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.ksim_destroy.argtypes = [vp]
+        L.ksim_destroy.restype = None
+        L.ksim_last_error.argtypes = [vp]
+        L.ksim_last_error.restype = ctypes.c_char_p
+        L.ksim_set_profile.argtypes = [vp, vp]
+        L.ksim_set_cluster.argtypes = [vp, vp, vp]
+        L.ksim_get_node_state.argtypes = [vp] * 7
+        L.ksim_get_next_start.argtypes = [vp, vp]
+        L.ksim_set_next_start.argtypes = [vp, i32]
+        L.ksim_set_pod_seq.argtypes = [vp, i64]
+        L.ksim_eval_pod.argtypes = [vp, vp, i32, vp]
+        L.ksim_assume.argtypes = [vp, vp, i32, i32]
+        L.ksim_forget.argtypes = [vp, vp, i32, i32]
+        L.ksim_load_pods.argtypes = [vp, vp]
+        L.ksim_schedule_loaded.argtypes = [vp, i32, i32, vp, vp]
+        L.ksim_schedule_batch.argtypes = [vp, vp, vp, vp]
+        _LIB = L
+    return _LIB
+
+
+class Engine:
+    """One engine handle on one GPU (one scheduler profile, one snapshot)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        rc = lib().ksim_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise KsimError(rc, f"ksim_create(device={device}) failed (no GPU / HIP runtime?)")
+        self.h = h
+        self.n_nodes = 0
+        self.n_score = 0
+        self._keep = []
+
+    def _chk(self, rc: int):
+        if rc != 0:
+            raise KsimError(rc, lib().ksim_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ksim_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def set_profile(self, prof: abi.Profile):
+        self._chk(lib().ksim_set_profile(self.h, ctypes.byref(prof)))
+        self.n_score = prof.n_score
+
+    def set_cluster(self, cluster):
+        nt, vo = cluster.node_table(), cluster.vocab()
+        self._chk(lib().ksim_set_cluster(self.h, ctypes.byref(nt), ctypes.byref(vo)))
+        self.n_nodes = cluster.n_nodes
+
+    def eval_pod(self, pods, index: int) -> dict:
+        buf = abi.EvalBuffers(self.n_nodes, self.n_score)
+        ps = pods.pod_set()
+        self._chk(lib().ksim_eval_pod(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        return buf.result()
+
+    def assume(self, pods, index: int, node: int):
+        ps = pods.pod_set()
+        self._chk(lib().ksim_assume(self.h, ctypes.byref(ps), index, node))
+
+    def forget(self, pods, index: int, node: int):
+        ps = pods.pod_set()
+        self._chk(lib().ksim_forget(self.h, ctypes.byref(ps), index, node))
+
+    def load_pods(self, pods):
+        ps = pods.pod_set()
+        self._chk(lib().ksim_load_pods(self.h, ctypes.byref(ps)))
+        self._keep = [pods]
+
+    def schedule_loaded(self, first: int, count: int, want_chosen: bool = True):
+        chosen = np.zeros(count, np.int32) if want_chosen else None
+        st = abi.BatchStats()
+        self._chk(lib().ksim_schedule_loaded(
+            self.h, first, count, chosen.ctypes.data_as(ctypes.c_void_p) if chosen is not None else None,
+            ctypes.byref(st)))
+        return chosen, st
+
+    def schedule_batch(self, pods):
+        self.load_pods(pods)
+        return self.schedule_loaded(0, pods.n_pods)
+
+    def node_state(self) -> dict:
+        n = self.n_nodes
+        out = {k: np.zeros(n, np.int64) for k in ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem")}
+        out["num_pods"] = np.zeros(n, np.int32)
+        a = [out[k].ctypes.data_as(ctypes.c_void_p) for k in
+             ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")]
+        self._chk(lib().ksim_get_node_state(self.h, *a))
+        return out
+
+    @property
+    def next_start(self) -> int:
+        v = ctypes.c_int32()
+        self._chk(lib().ksim_get_next_start(self.h, ctypes.byref(v)))
+        return v.value
+
+    def set_next_start(self, s: int):
+        self._chk(lib().ksim_set_next_start(self.h, s))
+
+    def set_pod_seq(self, s: int):
+        self._chk(lib().ksim_set_pod_seq(self.h, s))

@@ -1,0 +1,183 @@
+"""Deterministic synthetic clusters for BASELINE.json's configs.
+
+SplitMix64 streams with the seeds 0x4B53494D0001..0005.  Config 1 is built as
+Node/Pod objects (it exercises the encoder); configs 2/4/5 are emitted straight
+into the engine's SoA buffers (vectorised, 100k nodes / 1M pods in seconds).
+Node/pod shapes start from the UI templates web/components/lib/templates/
+{node,pod}.yaml (cpu 4 / 32Gi / 110 pods; pod 100m / 16Gi).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import numpy as np
+
+from . import abi
+from .encode import EncodedCluster, EncodedPods, encode_cluster, encode_pods
+from .model import (Container, Node, NodeSelectorTerm, Pod, PreferredTerm, Requirement, Taint,
+                    Toleration)
+
+M64 = (1 << 64) - 1
+GOLDEN = 0x9E3779B97F4A7C15
+SEEDS = {1: 0x4B53494D0001, 2: 0x4B53494D0002, 3: 0x4B53494D0003, 4: 0x4B53494D0004,
+         5: 0x4B53494D0005}
+GI = 1 << 30
+MI = 1 << 20
+
+
+def mix64(z: int) -> int:
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+class Rng:
+    """SplitMix64 stream."""
+
+    def __init__(self, seed: int):
+        self.s = seed & M64
+
+    def next(self) -> int:
+        self.s = (self.s + GOLDEN) & M64
+        return mix64(self.s)
+
+    def below(self, n: int) -> int:
+        return (self.next() >> 11) % n
+
+    def chance(self, pct: int) -> bool:
+        return self.below(100) < pct
+
+
+def _mix_np(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def stream(seed: int, tag: int, n: int) -> np.ndarray:
+    """n values of the SplitMix64 stream seeded with mix64(seed ^ tag)."""
+    s = np.uint64(mix64((seed ^ tag) & M64))
+    with np.errstate(over="ignore"):
+        idx = np.arange(1, n + 1, dtype=np.uint64)
+        return _mix_np(s + idx * np.uint64(GOLDEN))
+
+
+def below(x: np.ndarray, n: int) -> np.ndarray:
+    return ((x >> np.uint64(11)) % np.uint64(n)).astype(np.int64)
+
+
+# ---- config 1: 100 nodes x 1,000 pods, resources + taints + node affinity ----
+POOLS = ["a", "b", "c", "d"]
+DISKS = ["ssd", "hdd"]
+NOSCHED = [Taint("dedicated", "gpu", "NoSchedule"), Taint("dedicated", "infra", "NoSchedule")]
+PREFER = [Taint("spot", "true", "PreferNoSchedule"), Taint("old", "true", "PreferNoSchedule")]
+
+
+def config1_objects(n_nodes: int = 100, n_pods: int = 1000,
+                    seed: int = SEEDS[1]) -> Tuple[List[Node], List[Pod]]:
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        cores = [4, 8, 16, 32][r.below(4)]
+        mem = [16, 32, 64, 128][r.below(4)]
+        taints = []
+        if r.chance(10):
+            taints.append(NOSCHED[r.below(2)])
+        if r.chance(20):
+            taints.append(PREFER[r.below(2)])
+        nodes.append(Node(
+            name=f"node-{i:05d}",
+            labels={"kubernetes.io/hostname": f"node-{i:05d}",
+                    "topology.kubernetes.io/zone": f"z{i % 3}",
+                    "pool": POOLS[r.below(4)], "disk": DISKS[r.below(2)]},
+            taints=taints,
+            allocatable={"cpu": str(cores), "memory": f"{mem}Gi", "pods": "110"}))
+    pods = []
+    all_taints = NOSCHED + PREFER
+    for j in range(n_pods):
+        cpu = 100 * (1 + r.below(20))
+        mem = 128 * (1 << r.below(7))
+        p = Pod(name=f"pod-{j:06d}", containers=[Container({"cpu": f"{cpu}m", "memory": f"{mem}Mi"})])
+        if r.chance(30):
+            t = all_taints[r.below(4)]
+            p.tolerations = [Toleration(t.key, "Equal", t.value, t.effect)]
+        if r.chance(30):
+            k = 1 + r.below(2)
+            vals = sorted({POOLS[r.below(4)] for _ in range(k)})
+            p.required_terms = [NodeSelectorTerm([Requirement("pool", "In", vals)])]
+        if r.chance(30):
+            terms = []
+            for _ in range(1 + r.below(2)):
+                w = 1 + r.below(100)
+                if r.chance(50):
+                    req = Requirement("pool", "In", [POOLS[r.below(4)]])
+                else:
+                    req = Requirement("disk", "In", ["ssd"])
+                terms.append(PreferredTerm(w, NodeSelectorTerm([req])))
+            p.preferred_terms = terms
+        pods.append(p)
+    return nodes, pods
+
+
+def config1(n_nodes: int = 100, n_pods: int = 1000, seed: int = SEEDS[1]):
+    nodes, pods = config1_objects(n_nodes, n_pods, seed)
+    cluster, _ = encode_cluster(nodes)
+    return cluster, encode_pods(cluster, pods)
+
+
+# ---- configs 2/4/5: bare pods, NodeResourcesFit + BalancedAllocation dominated --
+def bare_cluster(n_nodes: int, seed: int) -> EncodedCluster:
+    """Nodes cpu in {8,16,32,64} cores, memory in {32,64,128,256} Gi, 110 pods,
+    3 zones (node i in z{i%3}: nodeTree order is the identity)."""
+    N = n_nodes
+    cores = np.array([8, 16, 32, 64], np.int64)[below(stream(seed, 1, N), 4)]
+    mem = np.array([32, 64, 128, 256], np.int64)[below(stream(seed, 2, N), 4)] * GI
+    hostnames = [f"node-{i:06d}" for i in range(N)]
+    labels = np.zeros((2, N), np.uint32)
+    labels[0] = np.arange(1, N + 1, dtype=np.uint32)          # kubernetes.io/hostname
+    labels[1] = (np.arange(N) % 3 + 1).astype(np.uint32)       # topology.kubernetes.io/zone
+    z = np.zeros(N, np.int64)
+    return EncodedCluster(
+        n_nodes=N, n_scalar=0,
+        alloc_cpu=cores * 1000, alloc_mem=mem, alloc_eph=z.copy(),
+        alloc_pods=np.full(N, 110, np.int32), alloc_scalar=np.zeros((0, N), np.int64),
+        req_cpu=z.copy(), req_mem=z.copy(), req_eph=z.copy(), req_scalar=np.zeros((0, N), np.int64),
+        nz_cpu=z.copy(), nz_mem=z.copy(), num_pods=np.zeros(N, np.int32),
+        flags=np.zeros(N, np.uint32), taints=np.zeros((abi.MAX_NODE_TAINTS, N), np.uint16),
+        labels=labels, taint_effect=np.zeros(1, np.uint8),
+        label_col_offset=np.array([0, N + 1], np.int32),
+        label_num=np.zeros(N + 1 + 4, np.int64), label_num_ok=np.zeros(N + 1 + 4, np.uint8),
+        node_names=hostnames,
+        label_keys=["kubernetes.io/hostname", "topology.kubernetes.io/zone"],
+        label_values=[[""] + hostnames, ["", "z0", "z1", "z2"]],
+        taint_vocab=[None], scalar_names=[])
+
+
+def bare_pods(n_pods: int, seed: int, cpu_steps: int = 10, mem_steps: int = 16) -> EncodedPods:
+    """Pods with one container: cpu 100m..1000m (step 100m), memory
+    256Mi..4Gi (step 256Mi); requests set, so non-zero == requests."""
+    P = n_pods
+    cpu = 100 * (1 + below(stream(seed, 11, P), cpu_steps))
+    mem = 256 * MI * (1 + below(stream(seed, 12, P), mem_steps))
+    pods = np.zeros(P, abi.POD_DTYPE)
+    pods["req_cpu"] = cpu
+    pods["req_mem"] = mem
+    pods["nz_cpu"] = cpu
+    pods["nz_mem"] = mem
+    pods["node_name"] = -1
+    return EncodedPods(pods, np.zeros(0, abi.LABEL_EXPR_DTYPE), np.zeros(0, abi.TERM_DTYPE),
+                       [("default", f"pod-{j:07d}") for j in range(P)] if P <= 200000 else [])
+
+
+def config2(n_nodes: int = 5000, n_pods: int = 50000, seed: int = SEEDS[2]):
+    return bare_cluster(n_nodes, seed), bare_pods(n_pods, seed)
+
+
+def config4(n_nodes: int = 100000, n_pods: int = 1000000, seed: int = SEEDS[4]):
+    return bare_cluster(n_nodes, seed), bare_pods(n_pods, seed)
+
+
+def config5_weights(n: int = 1024, seed: int = SEEDS[5]) -> np.ndarray:
+    """1,024 score-weight vectors w in {1..10}^7 (profile Score order)."""
+    x = stream(seed, 21, n * 7)
+    return (1 + below(x, 10)).reshape(n, 7).astype(np.int32)

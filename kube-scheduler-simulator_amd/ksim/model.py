@@ -1,0 +1,182 @@
+"""Minimal Kubernetes object model for the hot path (Node, Pod and the fields
+the six north-star plugins read), plus resource.Quantity parsing.
+
+Objects can be built directly or parsed from v1 JSON/YAML dicts (the shape of
+``ResourcesForImport`` in simulator/export/export.go:56-65).
+"""
+from __future__ import annotations
+
+import math
+import re
+from dataclasses import dataclass, field
+from fractions import Fraction
+from typing import Dict, List, Optional
+
+# ---- resource.Quantity ----------------------------------------------------
+_BIN = {"Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40, "Pi": 2 ** 50, "Ei": 2 ** 60}
+_DEC = {"n": Fraction(1, 10 ** 9), "u": Fraction(1, 10 ** 6), "m": Fraction(1, 1000), "": 1,
+        "k": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9, "T": 10 ** 12, "P": 10 ** 15, "E": 10 ** 18}
+_QRE = re.compile(r"^([+-]?(?:\d+\.?\d*|\.\d+))(?:(Ki|Mi|Gi|Ti|Pi|Ei|[numkMGTPE])|[eE]([+-]?\d+))?$")
+
+
+def parse_quantity(q) -> Fraction:
+    """Exact value of a k8s resource.Quantity string (or number)."""
+    if isinstance(q, (int, Fraction)):
+        return Fraction(q)
+    if isinstance(q, float):
+        return Fraction(str(q))
+    s = str(q).strip()
+    m = _QRE.match(s)
+    if not m:
+        raise ValueError(f"invalid quantity {q!r}")
+    num = Fraction(m.group(1))
+    if m.group(2):
+        suf = m.group(2)
+        num *= _BIN[suf] if suf in _BIN else _DEC[suf]
+    elif m.group(3):
+        num *= Fraction(10) ** int(m.group(3))
+    return num
+
+
+def quantity_value(q) -> int:
+    """resource.Quantity.Value(): rounds up to an integer."""
+    return math.ceil(parse_quantity(q))
+
+
+def quantity_milli_value(q) -> int:
+    """resource.Quantity.MilliValue(): value*1000 rounded up."""
+    return math.ceil(parse_quantity(q) * 1000)
+
+
+# ---- objects --------------------------------------------------------------
+@dataclass
+class Taint:
+    key: str
+    value: str = ""
+    effect: str = "NoSchedule"
+
+
+@dataclass
+class Toleration:
+    key: str = ""
+    operator: str = ""          # "" == Equal
+    value: str = ""
+    effect: str = ""
+
+    def tolerates(self, t: Taint) -> bool:
+        """k8s.io/api core/v1 Toleration.ToleratesTaint."""
+        if self.effect and self.effect != t.effect:
+            return False
+        if self.key and self.key != t.key:
+            return False
+        if self.operator in ("", "Equal"):
+            return self.value == t.value
+        if self.operator == "Exists":
+            return True
+        return False
+
+
+@dataclass
+class Requirement:
+    key: str
+    operator: str               # In NotIn Exists DoesNotExist Gt Lt
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class NodeSelectorTerm:
+    match_expressions: List[Requirement] = field(default_factory=list)
+    match_fields: List[Requirement] = field(default_factory=list)
+
+
+@dataclass
+class PreferredTerm:
+    weight: int
+    term: NodeSelectorTerm
+
+
+@dataclass
+class Container:
+    requests: Dict[str, str] = field(default_factory=dict)
+    host_ports: List[int] = field(default_factory=list)
+
+
+@dataclass
+class Node:
+    name: str
+    labels: Dict[str, str] = field(default_factory=dict)
+    taints: List[Taint] = field(default_factory=list)
+    allocatable: Dict[str, str] = field(default_factory=dict)
+    unschedulable: bool = False
+
+
+@dataclass
+class Pod:
+    name: str
+    namespace: str = "default"
+    labels: Dict[str, str] = field(default_factory=dict)
+    containers: List[Container] = field(default_factory=list)
+    init_containers: List[Container] = field(default_factory=list)
+    overhead: Dict[str, str] = field(default_factory=dict)
+    node_selector: Dict[str, str] = field(default_factory=dict)
+    required_terms: Optional[List[NodeSelectorTerm]] = None   # None: no required affinity
+    preferred_terms: List[PreferredTerm] = field(default_factory=list)
+    tolerations: List[Toleration] = field(default_factory=list)
+    node_name: str = ""
+    has_volumes: bool = False
+    priority: int = 0
+
+
+# ---- v1 dict parsing --------------------------------------------------------
+# Volume sources the volume filter plugins (VolumeRestrictions, *Limits,
+# VolumeBinding, VolumeZone) act on; pods with none of them pass all of those.
+_VOLUME_SOURCES = ("persistentVolumeClaim", "gcePersistentDisk", "awsElasticBlockStore",
+                   "azureDisk", "csi", "rbd", "iscsi", "cinder", "ephemeral")
+
+def _req(d) -> Requirement:
+    return Requirement(d["key"], d["operator"], list(d.get("values") or []))
+
+
+def _term(d) -> NodeSelectorTerm:
+    return NodeSelectorTerm([_req(x) for x in (d.get("matchExpressions") or [])],
+                            [_req(x) for x in (d.get("matchFields") or [])])
+
+
+def node_from_dict(d: dict) -> Node:
+    md, spec, status = d.get("metadata", {}), d.get("spec", {}) or {}, d.get("status", {}) or {}
+    return Node(
+        name=md.get("name", ""),
+        labels=dict(md.get("labels") or {}),
+        taints=[Taint(t["key"], t.get("value", ""), t.get("effect", "")) for t in (spec.get("taints") or [])],
+        allocatable={k: str(v) for k, v in (status.get("allocatable") or {}).items()},
+        unschedulable=bool(spec.get("unschedulable", False)),
+    )
+
+
+def _container(c) -> Container:
+    res = c.get("resources") or {}
+    return Container({k: str(v) for k, v in (res.get("requests") or {}).items()},
+                     [p["hostPort"] for p in (c.get("ports") or []) if p.get("hostPort")])
+
+
+def pod_from_dict(d: dict) -> Pod:
+    md, spec = d.get("metadata", {}), d.get("spec", {}) or {}
+    aff = (spec.get("affinity") or {}).get("nodeAffinity") or {}
+    req = aff.get("requiredDuringSchedulingIgnoredDuringExecution")
+    pref = aff.get("preferredDuringSchedulingIgnoredDuringExecution") or []
+    return Pod(
+        name=md.get("name", ""),
+        namespace=md.get("namespace", "default"),
+        labels=dict(md.get("labels") or {}),
+        containers=[_container(c) for c in (spec.get("containers") or [])],
+        init_containers=[_container(c) for c in (spec.get("initContainers") or [])],
+        overhead={k: str(v) for k, v in (spec.get("overhead") or {}).items()},
+        node_selector=dict(spec.get("nodeSelector") or {}),
+        required_terms=None if req is None else [_term(t) for t in (req.get("nodeSelectorTerms") or [])],
+        preferred_terms=[PreferredTerm(int(p.get("weight", 0)), _term(p.get("preference") or {})) for p in pref],
+        tolerations=[Toleration(t.get("key", ""), t.get("operator", ""), t.get("value", ""), t.get("effect", ""))
+                     for t in (spec.get("tolerations") or [])],
+        node_name=spec.get("nodeName", "") or "",
+        has_volumes=any(any(k in v for k in _VOLUME_SOURCES) for v in (spec.get("volumes") or [])),
+        priority=int(spec.get("priority") or 0),
+    )

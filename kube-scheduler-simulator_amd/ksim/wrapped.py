@@ -1,0 +1,107 @@
+"""Engine-backed plugins behind the simulator's wrapper contract.
+
+``record_cycle`` replays one engine cycle into a result Store exactly as the
+simulator's wrappedPlugin records the original plugins during that cycle
+(simulator/scheduler/plugin/wrappedplugin.go):
+
+  PreFilter      -> AddPreFilterResult(plugin, "success"|msg, result)   :459-486
+  Filter         -> AddFilterResult(node, plugin, "passed"|msg)          :491-516
+                    (only plugins the framework ran: up to the first failure)
+  PostFilter     -> AddPostFilterResult(nominated, plugin, nodes)        :518-544
+  PreScore       -> AddPreScoreResult(plugin, "success"|msg)             :427-454
+  Score          -> AddScoreResult(node, plugin, raw)                    :388-413
+  NormalizeScore -> AddNormalizedScoreResult(node, plugin, normalized)   :356-383
+  Reserve        -> AddSelectedNode(node) + AddReserveResult             :583-612
+  PreBind/Bind   -> AddPreBindResult / AddBindResult
+Keys are the ORIGINAL plugin names (wrappedplugin.go:374,406,447,479,510).
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+from . import abi
+from .encode import EncodedCluster
+from .profile import SchedulerProfile, original_name
+from .resultstore import PASSED_FILTER_MESSAGE, SUCCESS_MESSAGE, Store
+
+# Plugins with a ScoreExtensions (NormalizeScore) in v1.26.
+HAS_NORMALIZE = {"TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity"}
+
+# Upstream error reasons.
+ERR_UNSCHEDULABLE = "node(s) were unschedulable"                        # nodeunschedulable
+ERR_NODE_NAME = "node(s) didn't match the requested node name"          # nodename
+ERR_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"  # nodeaffinity ErrReasonPod
+
+
+def filter_message(cluster: EncodedCluster, plugin: str, detail: int) -> str:
+    """framework.Status.Message() of a failing in-tree Filter."""
+    if plugin == "NodeUnschedulable":
+        return ERR_UNSCHEDULABLE
+    if plugin == "NodeName":
+        return ERR_NODE_NAME
+    if plugin == "TaintToleration":
+        t = cluster.taint_vocab[detail]
+        return f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
+    if plugin == "NodeAffinity":
+        return ERR_NODE_AFFINITY
+    if plugin == "NodeResourcesFit":
+        reasons = []
+        if detail & abi.FIT_TOO_MANY_PODS:
+            reasons.append("Too many pods")
+        if detail & abi.FIT_CPU:
+            reasons.append("Insufficient cpu")
+        if detail & abi.FIT_MEMORY:
+            reasons.append("Insufficient memory")
+        if detail & abi.FIT_EPHEMERAL:
+            reasons.append("Insufficient ephemeral-storage")
+        for k, name in enumerate(cluster.scalar_names):
+            if detail & (abi.FIT_SCALAR0 << k):
+                reasons.append(f"Insufficient {name}")
+        return ", ".join(reasons)
+    return f"{plugin} failed"
+
+
+def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, ns: str, name: str,
+                 res: Dict) -> None:
+    """Feed ``store`` with one compat-mode cycle result (engine or oracle)."""
+    names = cluster.node_names
+    for p in prof.plugins["preFilter"].enabled:
+        store.add_pre_filter_result(ns, name, original_name(p.name), SUCCESS_MESSAGE, None)
+    forder = prof.filter_order()
+    fp, fd = res["fail_plugin"], res["fail_detail"]
+    for node in range(cluster.n_nodes):
+        r = int(fp[node])
+        if r == abi.NOT_EVALUATED:
+            continue
+        last = len(forder) if r == abi.PASSED else r + 1
+        for f in range(last):
+            if f == r:
+                store.add_filter_result(ns, name, names[node], forder[f],
+                                        filter_message(cluster, forder[f], int(fd[node])))
+            else:
+                store.add_filter_result(ns, name, names[node], forder[f], PASSED_FILTER_MESSAGE)
+    if res["status"] == abi.STATUS_UNSCHEDULABLE:
+        failed = [names[i] for i in range(cluster.n_nodes) if fp[i] not in (abi.PASSED, abi.NOT_EVALUATED)]
+        for p in prof.plugins["postFilter"].enabled:
+            store.add_post_filter_result(ns, name, "", original_name(p.name), failed)
+        return
+    if res["n_feasible"] > 1:
+        for p in prof.plugins["preScore"].enabled:
+            store.add_pre_score_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+        scored = [i for i in range(cluster.n_nodes) if res["scored"][i]]
+        splugins = prof.score_plugins()
+        for i in scored:
+            for k, pl in enumerate(splugins):
+                store.add_score_result(ns, name, names[i], pl.name, int(res["raw"][k][i]))
+        for k, pl in enumerate(splugins):
+            if pl.name in HAS_NORMALIZE:
+                for i in scored:
+                    store.add_normalized_score_result(ns, name, names[i], pl.name, int(res["norm"][k][i]))
+    chosen = names[res["chosen"]]
+    for p in prof.plugins["reserve"].enabled:
+        store.add_selected_node(ns, name, chosen)
+        store.add_reserve_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+    for p in prof.plugins["preBind"].enabled:
+        store.add_pre_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+    for p in prof.plugins["bind"].enabled:
+        store.add_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)

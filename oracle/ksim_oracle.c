@@ -1,0 +1,649 @@
+/*
+ * ksim_oracle.c — CPU restatement (ORACLE) of the per-pod scheduling cycle.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ksim_oracle.h): the checker for the HIP engine
+ * and the CPU baseline timed by bench.py.  Never linked by libksim_engine.so.
+ *
+ * Every function names the upstream k8s.io/kubernetes v1.26.2 function it
+ * restates ([upstream] path, absent from /root/reference; pinned at
+ * simulator/go.mod:53) and the SURVEY.md §8(a) row it covers.  Simulator-side
+ * behaviour cites /root/reference files directly.
+ *
+ * Build: gcc -O2 -fPIC -shared -fopenmp -ffp-contract=off (oracle/Makefile).
+ * -ffp-contract=off matches Go on GOAMD64=v1 (simulator/Dockerfile:1 golang:1.19),
+ * which never fuses float64 multiply-add.
+ */
+#include "ksim_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define MAX_NODE_SCORE 100   /* framework.MaxNodeScore */
+#define MIN_NODE_SCORE 0     /* framework.MinNodeScore */
+#define MIN_FEASIBLE_NODES_TO_FIND 100            /* schedule_one.go minFeasibleNodesToFind */
+#define MIN_FEASIBLE_NODES_PERCENTAGE_TO_FIND 5   /* schedule_one.go minFeasibleNodesPercentageToFind */
+
+struct ksim_oracle {
+  ksim_profile prof;
+  int32_t n, n_scalar, n_label_cols;
+  /* static node columns */
+  int64_t *alloc_cpu, *alloc_mem, *alloc_eph, *alloc_scalar;
+  int32_t *alloc_pods;
+  uint32_t *flags;
+  uint16_t *taints;
+  uint32_t *labels;
+  /* dynamic node columns (NodeInfo.Requested / NonZeroRequested / Pods) */
+  int64_t *req_cpu, *req_mem, *req_eph, *req_scalar, *nz_cpu, *nz_mem;
+  int32_t *num_pods;
+  /* vocab */
+  int32_t n_taints, n_label_values;
+  uint8_t *taint_effect;
+  int32_t *label_col_offset;
+  int64_t *label_num;
+  uint8_t *label_num_ok;
+  /* scheduler state */
+  int32_t next_start;   /* sched.nextStartNodeIndex */
+  int64_t pod_seq;      /* tie-break sequence */
+  /* scratch */
+  uint8_t *fail;
+  uint32_t *detail;
+  int32_t *flist;
+  int64_t *raw;         /* [KSIM_MAX_SCORE][n] */
+};
+
+/* ------------------------------------------------------------------------ */
+static void* dupbuf(const void* src, size_t bytes) {
+  void* p = malloc(bytes ? bytes : 1);
+  if (p && src && bytes) memcpy(p, src, bytes);
+  else if (p) memset(p, 0, bytes ? bytes : 1);
+  return p;
+}
+
+ksim_oracle* ksim_oracle_create(const ksim_node_table* t, const ksim_vocab* v,
+                                const ksim_profile* prof) {
+  if (!t || !v || !prof || t->n_nodes < 0 || t->n_nodes > KSIM_MAX_NODES) return NULL;
+  ksim_oracle* o = (ksim_oracle*)calloc(1, sizeof(*o));
+  size_t n = (size_t)t->n_nodes;
+  o->prof = *prof;
+  o->n = t->n_nodes;
+  o->n_scalar = t->n_scalar;
+  o->n_label_cols = t->n_label_cols;
+  o->alloc_cpu = dupbuf(t->alloc_cpu, n * 8);
+  o->alloc_mem = dupbuf(t->alloc_mem, n * 8);
+  o->alloc_eph = dupbuf(t->alloc_eph, n * 8);
+  o->alloc_pods = dupbuf(t->alloc_pods, n * 4);
+  o->alloc_scalar = dupbuf(t->alloc_scalar, n * 8 * (size_t)t->n_scalar);
+  o->req_cpu = dupbuf(t->req_cpu, n * 8);
+  o->req_mem = dupbuf(t->req_mem, n * 8);
+  o->req_eph = dupbuf(t->req_eph, n * 8);
+  o->req_scalar = dupbuf(t->req_scalar, n * 8 * (size_t)t->n_scalar);
+  o->nz_cpu = dupbuf(t->nz_cpu, n * 8);
+  o->nz_mem = dupbuf(t->nz_mem, n * 8);
+  o->num_pods = dupbuf(t->num_pods, n * 4);
+  o->flags = dupbuf(t->flags, n * 4);
+  o->taints = dupbuf(t->taints, n * 2 * KSIM_MAX_NODE_TAINTS);
+  o->labels = dupbuf(t->labels, n * 4 * (size_t)t->n_label_cols);
+  o->n_taints = v->n_taints;
+  o->n_label_values = v->n_label_values;
+  o->taint_effect = dupbuf(v->taint_effect, (size_t)v->n_taints);
+  o->label_col_offset = dupbuf(v->label_col_offset, 4 * (size_t)t->n_label_cols);
+  o->label_num = dupbuf(v->label_num, 8 * (size_t)v->n_label_values);
+  o->label_num_ok = dupbuf(v->label_num_ok, (size_t)v->n_label_values);
+  o->fail = malloc(n + 1);
+  o->detail = malloc(4 * n + 4);
+  o->flist = malloc(4 * n + 4);
+  o->raw = malloc(8 * n * KSIM_MAX_SCORE + 8);
+  return o;
+}
+
+void ksim_oracle_destroy(ksim_oracle* o) {
+  if (!o) return;
+  void* ps[] = {o->alloc_cpu, o->alloc_mem, o->alloc_eph, o->alloc_pods, o->alloc_scalar,
+                o->req_cpu, o->req_mem, o->req_eph, o->req_scalar, o->nz_cpu, o->nz_mem,
+                o->num_pods, o->flags, o->taints, o->labels, o->taint_effect,
+                o->label_col_offset, o->label_num, o->label_num_ok, o->fail, o->detail,
+                o->flist, o->raw};
+  for (size_t i = 0; i < sizeof(ps) / sizeof(ps[0]); i++) free(ps[i]);
+  free(o);
+}
+
+/* ---- tie-break TB(seed), SURVEY §8(b) "Determinism modes" ---------------- */
+static uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* key = total<<44 | hash26<<18 | (2^18-1-node): one u64 max replaces the
+ * reservoir sampling of [upstream] schedule_one.go selectHost (global math/rand). */
+uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node) {
+  uint64_t h = splitmix64(seed ^ ((uint64_t)pod_seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
+  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)((KSIM_MAX_NODES - 1) - node);
+}
+
+/* [upstream] schedule_one.go (*Scheduler).numFeasibleNodesToFind — §8(a) a16 */
+int32_t ksim_oracle_num_feasible_nodes_to_find(int32_t percentage, int32_t num_all_nodes) {
+  if (num_all_nodes < MIN_FEASIBLE_NODES_TO_FIND || percentage >= 100) return num_all_nodes;
+  int32_t adaptive = percentage;
+  if (adaptive <= 0) {
+    adaptive = 50 - num_all_nodes / 125;
+    if (adaptive < MIN_FEASIBLE_NODES_PERCENTAGE_TO_FIND) adaptive = MIN_FEASIBLE_NODES_PERCENTAGE_TO_FIND;
+  }
+  int32_t num = num_all_nodes * adaptive / 100;
+  if (num < MIN_FEASIBLE_NODES_TO_FIND) return MIN_FEASIBLE_NODES_TO_FIND;
+  return num;
+}
+
+/* ---- NodeAffinity (component-helpers nodeaffinity + apimachinery labels) - */
+static inline uint32_t node_label(const ksim_oracle* o, int col, int32_t node) {
+  return o->labels[(size_t)col * o->n + node];
+}
+
+/* labels.Requirement.Matches / fields selector for metadata.name — §8(a) a26 */
+static int label_req_matches(const ksim_oracle* o, const ksim_label_expr* e, int32_t node) {
+  uint32_t v = (e->op <= KSIM_OP_LT) ? node_label(o, e->col, node) : 0;
+  switch (e->op) {
+    case KSIM_OP_IN:
+      if (!v) return 0;
+      for (int k = 0; k < e->nvals; k++) if (e->vals[k] == v) return 1;
+      return 0;
+    case KSIM_OP_NOT_IN:
+      if (!v) return 1;
+      for (int k = 0; k < e->nvals; k++) if (e->vals[k] == v) return 0;
+      return 1;
+    case KSIM_OP_EXISTS: return v != 0;
+    case KSIM_OP_DOES_NOT_EXIST: return v == 0;
+    case KSIM_OP_GT:
+    case KSIM_OP_LT: {
+      if (!v) return 0;
+      int32_t idx = o->label_col_offset[e->col] + (int32_t)v;
+      if (idx < 0 || idx >= o->n_label_values || !o->label_num_ok[idx]) return 0;
+      return e->op == KSIM_OP_GT ? (o->label_num[idx] > e->num) : (o->label_num[idx] < e->num);
+    }
+    case KSIM_OP_FIELD_IN:
+      for (int k = 0; k < e->nvals; k++) if ((int32_t)e->vals[k] == node) return 1;
+      return 0;
+    case KSIM_OP_FIELD_NOT_IN:
+      for (int k = 0; k < e->nvals; k++) if ((int32_t)e->vals[k] == node) return 0;
+      return 1;
+    case KSIM_OP_TRUE: return 1;
+    default: return 0;
+  }
+}
+
+/* nodeSelectorTerm.match: empty term matches nothing; AND of requirements. */
+static int term_matches(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_term* t,
+                        int32_t node) {
+  if (t->n_expr <= 0) return 0;
+  for (int i = 0; i < t->n_expr; i++)
+    if (!label_req_matches(o, &ps->exprs[t->first_expr + i], node)) return 0;
+  return 1;
+}
+
+/* RequiredNodeAffinity.Match: nodeSelector (labels.SelectorFromSet) AND
+ * (OR of required terms) — [upstream] nodeaffinity.Filter, §8(a) a26 */
+static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set* ps,
+                                        const ksim_pod* p, int32_t node) {
+  for (int i = 0; i < p->sel_count; i++)
+    if (!label_req_matches(o, &ps->exprs[p->sel_first + i], node)) return 0;
+  if (p->flags & KSIM_POD_HAS_REQUIRED_AFFINITY) {
+    for (int i = 0; i < p->req_term_count; i++)
+      if (term_matches(o, ps, &ps->terms[p->req_term_first + i], node)) return 1;
+    return 0;
+  }
+  return 1;
+}
+
+/* PreferredSchedulingTerms.Score — [upstream] nodeaffinity.Score */
+static int64_t preferred_node_affinity_score(const ksim_oracle* o, const ksim_pod_set* ps,
+                                             const ksim_pod* p, int32_t node) {
+  int64_t count = 0;
+  for (int i = 0; i < p->pref_term_count; i++) {
+    const ksim_term* t = &ps->terms[p->pref_term_first + i];
+    if (t->weight == 0) continue;
+    if (term_matches(o, ps, t, node)) count += t->weight;
+  }
+  return count;
+}
+
+/* ---- TaintToleration ---------------------------------------------------- */
+static inline int bit_set(const uint64_t* w, uint32_t id) {
+  return (int)((w[id >> 6] >> (id & 63)) & 1u);
+}
+
+/* v1helper.FindMatchingUntoleratedTaint with DoNotScheduleTaintsFilterFunc —
+ * [upstream] tainttoleration.Filter, §8(a) a25.  Returns taint id or 0. */
+static uint32_t find_matching_untolerated_taint(const ksim_oracle* o, const ksim_pod* p,
+                                                int32_t node) {
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) {
+    uint32_t tid = o->taints[(size_t)k * o->n + node];
+    if (!tid) break;
+    uint8_t eff = o->taint_effect[tid];
+    if ((eff == KSIM_EFFECT_NO_SCHEDULE || eff == KSIM_EFFECT_NO_EXECUTE) &&
+        !bit_set(p->tol_filter, tid))
+      return tid;
+  }
+  return 0;
+}
+
+/* countIntolerableTaintsPreferNoSchedule — [upstream] tainttoleration.Score */
+static int64_t count_intolerable_prefer_no_schedule(const ksim_oracle* o, const ksim_pod* p,
+                                                    int32_t node) {
+  int64_t c = 0;
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) {
+    uint32_t tid = o->taints[(size_t)k * o->n + node];
+    if (!tid) break;
+    if (o->taint_effect[tid] != KSIM_EFFECT_PREFER_NO_SCHEDULE) continue;
+    if (!bit_set(p->tol_prefer, tid)) c++;
+  }
+  return c;
+}
+
+/* ---- NodeResourcesFit --------------------------------------------------- */
+/* fitsRequest — [upstream] noderesources/fit.go, §8(a) a22.  Reason bits in
+ * the order upstream appends them (pods, cpu, memory, ephemeral, scalars). */
+static uint32_t fits_request(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+  uint32_t r = 0;
+  if (o->num_pods[node] + 1 > o->alloc_pods[node]) r |= KSIM_FIT_TOO_MANY_PODS;
+  if (p->req_cpu == 0 && p->req_mem == 0 && p->req_eph == 0 && !(p->flags & KSIM_POD_HAS_SCALAR))
+    return r;
+  if (p->req_cpu > o->alloc_cpu[node] - o->req_cpu[node]) r |= KSIM_FIT_CPU;
+  if (p->req_mem > o->alloc_mem[node] - o->req_mem[node]) r |= KSIM_FIT_MEMORY;
+  if (p->req_eph > o->alloc_eph[node] - o->req_eph[node]) r |= KSIM_FIT_EPHEMERAL;
+  for (int k = 0; k < o->n_scalar; k++) {
+    int64_t q = p->scalar_req[k];
+    if (q == 0) continue;
+    size_t ix = (size_t)k * o->n + node;
+    if (q > o->alloc_scalar[ix] - o->req_scalar[ix]) r |= (KSIM_FIT_SCALAR0 << k);
+  }
+  return r;
+}
+
+/* resourceAllocationScorer.calculateResourceAllocatableRequest — a23/a24.
+ * use_requested: BalancedAllocation (true) vs Fit LeastAllocated (false). */
+static void calc_alloc_req(const ksim_oracle* o, const ksim_pod* p, int32_t node, int32_t res,
+                           int use_requested, int64_t* alloc, int64_t* req) {
+  *alloc = 0; *req = 0;
+  switch (res) {
+    case KSIM_RES_CPU: {
+      int64_t pr = use_requested ? p->req_cpu : p->nz_cpu;
+      *alloc = o->alloc_cpu[node];
+      *req = (use_requested ? o->req_cpu[node] : o->nz_cpu[node]) + pr;
+      return;
+    }
+    case KSIM_RES_MEMORY: {
+      int64_t pr = use_requested ? p->req_mem : p->nz_mem;
+      *alloc = o->alloc_mem[node];
+      *req = (use_requested ? o->req_mem[node] : o->nz_mem[node]) + pr;
+      return;
+    }
+    case KSIM_RES_EPHEMERAL:
+      *alloc = o->alloc_eph[node];
+      *req = o->req_eph[node] + p->req_eph;   /* always nodeInfo.Requested */
+      return;
+    default: {
+      int k = res - KSIM_RES_SCALAR0;
+      if (k < 0 || k >= o->n_scalar) return;
+      int64_t pr = p->scalar_req[k];
+      if (pr == 0) return;                    /* scalar not requested: bypass */
+      size_t ix = (size_t)k * o->n + node;
+      *alloc = o->alloc_scalar[ix];
+      *req = o->req_scalar[ix] + pr;
+      return;
+    }
+  }
+}
+
+/* leastRequestedScore — [upstream] noderesources/least_allocated.go */
+int64_t ksim_oracle_least_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
+}
+
+/* leastResourceScorer over resourceAllocationScorer.score — a23 */
+static int64_t fit_least_allocated_score(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+  int64_t node_score = 0, weight_sum = 0;
+  for (int i = 0; i < o->prof.fit_n_res; i++) {
+    int64_t a, r;
+    calc_alloc_req(o, p, node, o->prof.fit_res[i], 0, &a, &r);
+    if (a == 0) continue;
+    node_score += ksim_oracle_least_requested_score(r, a) * o->prof.fit_res_weight[i];
+    weight_sum += o->prof.fit_res_weight[i];
+  }
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
+/* balancedResourceScorer — [upstream] noderesources/balanced_allocation.go, a24 */
+int64_t ksim_oracle_balanced_score(int32_t n, const int64_t* requested, const int64_t* allocatable) {
+  double fr[KSIM_MAX_RES];
+  int nf = 0;
+  double total = 0;
+  for (int i = 0; i < n && i < KSIM_MAX_RES; i++) {
+    if (allocatable[i] == 0) continue;
+    double f = (double)requested[i] / (double)allocatable[i];
+    if (f > 1) f = 1;
+    total += f;
+    fr[nf++] = f;
+  }
+  double std = 0.0;
+  if (nf == 2) {
+    std = fabs((fr[0] - fr[1]) / 2);
+  } else if (nf > 2) {
+    double mean = total / (double)nf;
+    double sum = 0;
+    for (int i = 0; i < nf; i++) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+    std = sqrt(sum / (double)nf);
+  }
+  return (int64_t)((1 - std) * (double)MAX_NODE_SCORE);
+}
+
+static int64_t balanced_allocation_score(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+  int64_t req[KSIM_MAX_RES], alloc[KSIM_MAX_RES];
+  int m = 0;
+  for (int i = 0; i < o->prof.ba_n_res && i < KSIM_MAX_RES; i++) {
+    int64_t a, r;
+    calc_alloc_req(o, p, node, o->prof.ba_res[i], 1, &a, &r);
+    if (a == 0) continue;
+    alloc[m] = a; req[m] = r; m++;
+  }
+  return ksim_oracle_balanced_score(m, req, alloc);
+}
+
+/* ---- helper.DefaultNormalizeScore — a31 ---------------------------------- */
+void ksim_oracle_default_normalize(int64_t max_priority, int reverse, int32_t n, int64_t* s) {
+  int64_t max_count = 0;
+  for (int i = 0; i < n; i++) if (s[i] > max_count) max_count = s[i];
+  if (max_count == 0) {
+    if (reverse) for (int i = 0; i < n; i++) s[i] = max_priority;
+    return;
+  }
+  for (int i = 0; i < n; i++) {
+    int64_t v = max_priority * s[i] / max_count;
+    if (reverse) v = max_priority - v;
+    s[i] = v;
+  }
+}
+
+/* ---- framework: RunFilterPlugins — a17 ---------------------------------- */
+/* Runs the profile's filter plugins in order and stops at the first failure
+ * (runAllFilters=false).  Returns the filter-order index of the failing plugin
+ * or KSIM_PASSED; *detail gets the reason payload. */
+static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
+                                  int32_t node, uint32_t* detail) {
+  *detail = 0;
+  for (int f = 0; f < o->prof.n_filter; f++) {
+    switch (o->prof.filter[f]) {
+      case KSIM_PL_NODE_UNSCHEDULABLE:   /* nodeunschedulable.Filter */
+        if ((o->flags[node] & KSIM_NODE_UNSCHEDULABLE) &&
+            !(p->flags & KSIM_POD_TOLERATES_UNSCHEDULABLE))
+          return (uint8_t)f;
+        break;
+      case KSIM_PL_NODE_NAME:            /* nodename.Filter */
+        if (p->node_name != -1 && p->node_name != node) return (uint8_t)f;
+        break;
+      case KSIM_PL_TAINT_TOLERATION: {
+        uint32_t tid = find_matching_untolerated_taint(o, p, node);
+        if (tid) { *detail = tid; return (uint8_t)f; }
+        break;
+      }
+      case KSIM_PL_NODE_AFFINITY:
+        if (!required_node_affinity_match(o, ps, p, node)) return (uint8_t)f;
+        break;
+      case KSIM_PL_NODE_RESOURCES_FIT: {
+        uint32_t r = fits_request(o, p, node);
+        if (r) { *detail = r; return (uint8_t)f; }
+        break;
+      }
+      /* PodTopologySpread / InterPodAffinity: pods without constraints or
+       * affinity terms, and no existing pods with (anti)affinity, pass.
+       * NodePorts / volume plugins: pods without host ports or volumes pass. */
+      default:
+        break;
+    }
+  }
+  return KSIM_PASSED;
+}
+
+static int64_t score_plugin_raw(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
+                                int plugin, int32_t node) {
+  switch (plugin) {
+    case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(o, p, node);
+    case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(o, p, node);
+    case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer_no_schedule(o, p, node);
+    case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(o, ps, p, node);
+    /* ImageLocality: nodes carry no image list -> calculatePriority(0) = 0.
+     * PodTopologySpread / InterPodAffinity: no constraints/terms -> 0. */
+    default: return 0;
+  }
+}
+
+/* NormalizeScore of each plugin over the scored list (in place). */
+static void normalize_plugin(int plugin, int32_t n, int64_t* s) {
+  switch (plugin) {
+    case KSIM_PL_TAINT_TOLERATION:        /* tainttoleration.NormalizeScore (reverse) */
+      ksim_oracle_default_normalize(MAX_NODE_SCORE, 1, n, s);
+      return;
+    case KSIM_PL_NODE_AFFINITY:           /* nodeaffinity.NormalizeScore */
+      ksim_oracle_default_normalize(MAX_NODE_SCORE, 0, n, s);
+      return;
+    case KSIM_PL_POD_TOPOLOGY_SPREAD: {   /* podtopologyspread.NormalizeScore, no ignored nodes */
+      int64_t mn = INT64_MAX, mx = 0;
+      for (int i = 0; i < n; i++) { if (s[i] < mn) mn = s[i]; if (s[i] > mx) mx = s[i]; }
+      for (int i = 0; i < n; i++)
+        s[i] = (mx == 0) ? MAX_NODE_SCORE : MAX_NODE_SCORE * (mx + mn - s[i]) / mx;
+      return;
+    }
+    case KSIM_PL_INTER_POD_AFFINITY:      /* topologyScore empty -> scores left unchanged */
+    default:
+      return;                              /* Fit / BalancedAllocation / ImageLocality: none */
+  }
+}
+
+static int has_normalize(int plugin) {
+  return plugin == KSIM_PL_TAINT_TOLERATION || plugin == KSIM_PL_NODE_AFFINITY ||
+         plugin == KSIM_PL_POD_TOPOLOGY_SPREAD || plugin == KSIM_PL_INTER_POD_AFFINITY;
+}
+
+/* NodeInfo.AddPod restricted to the aggregates the plugins read — a20 */
+static void assume_pod(ksim_oracle* o, const ksim_pod* p, int32_t node, int sign) {
+  o->req_cpu[node] += sign * p->req_cpu;
+  o->req_mem[node] += sign * p->req_mem;
+  o->req_eph[node] += sign * p->req_eph;
+  for (int k = 0; k < o->n_scalar; k++) o->req_scalar[(size_t)k * o->n + node] += sign * p->scalar_req[k];
+  o->nz_cpu[node] += sign * p->nz_cpu;
+  o->nz_mem[node] += sign * p->nz_mem;
+  o->num_pods[node] += sign;
+}
+
+/* ---- schedulePod: findNodesThatFitPod + prioritizeNodes + selectHost ----- */
+/* Sequential (parallelism 1) semantics of [upstream] schedule_one.go — a15-a19. */
+int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_eval_out* out) {
+  if (!o || !ps || pi < 0 || pi >= ps->n_pods || !out) return KSIM_E_INVALID;
+  const ksim_pod* p = &ps->pods[pi];
+  const int32_t N = o->n;
+  if (N == 0) return KSIM_E_INVALID;                      /* ErrNoNodesAvailable */
+  const int64_t seq = o->pod_seq++;
+  const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, N);
+  const int32_t start = o->next_start;
+  const int S = o->prof.n_score;
+
+  if (out->fail_plugin) memset(out->fail_plugin, KSIM_NOT_EVALUATED, (size_t)N);
+  if (out->fail_detail) memset(out->fail_detail, 0, 4 * (size_t)N);
+  if (out->scored) memset(out->scored, 0, (size_t)N);
+  if (out->raw) memset(out->raw, 0, 8 * (size_t)N * S);
+  if (out->norm) memset(out->norm, 0, 8 * (size_t)N * S);
+  if (out->total) memset(out->total, 0, 8 * (size_t)N);
+
+  /* findNodesThatPassFilters */
+  int32_t nf = 0, nfailed = 0, evaluated = 0;
+  for (int32_t i = 0; i < N; i++) {
+    int32_t node = (start + i) % N;
+    uint32_t det;
+    uint8_t r = run_filter_plugins(o, ps, p, node, &det);
+    evaluated++;
+    if (out->fail_plugin) out->fail_plugin[node] = r;
+    if (out->fail_detail) out->fail_detail[node] = det;
+    if (r == KSIM_PASSED) {
+      if (nf == K) break;          /* the (K+1)-th feasible node: recorded, not kept */
+      o->flist[nf++] = node;
+    } else {
+      nfailed++;
+    }
+  }
+  int32_t processed = nf + nfailed;
+  o->next_start = (start + processed) % N;
+
+  out->k_to_find = K;
+  out->n_feasible = nf;
+  out->n_evaluated = evaluated;
+  out->n_processed = processed;
+  out->next_start = o->next_start;
+
+  if (nf == 0) {
+    out->chosen = -1;
+    out->status = KSIM_STATUS_UNSCHEDULABLE;
+    return KSIM_OK;
+  }
+  int32_t chosen;
+  if (nf == 1) {
+    chosen = o->flist[0];          /* single feasible node: no scoring at all */
+  } else {
+    /* RunScorePlugins: raw scores, NormalizeScore per plugin, weights */
+    int64_t* tmp = (int64_t*)malloc(8 * (size_t)nf);
+    int64_t* totals = (int64_t*)calloc((size_t)nf, 8);
+    for (int s = 0; s < S; s++) {
+      int pl = o->prof.score[s];
+      for (int32_t j = 0; j < nf; j++) tmp[j] = score_plugin_raw(o, ps, p, pl, o->flist[j]);
+      if (out->raw) for (int32_t j = 0; j < nf; j++) out->raw[(size_t)s * N + o->flist[j]] = tmp[j];
+      if (has_normalize(pl)) normalize_plugin(pl, nf, tmp);
+      int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
+      for (int32_t j = 0; j < nf; j++) {
+        if (out->norm) out->norm[(size_t)s * N + o->flist[j]] = tmp[j];
+        totals[j] += tmp[j] * w;
+      }
+    }
+    if (S == 0) for (int32_t j = 0; j < nf; j++) totals[j] = 1;  /* prioritizeNodes: no score plugins */
+    uint64_t best = 0;
+    chosen = -1;
+    for (int32_t j = 0; j < nf; j++) {
+      int32_t node = o->flist[j];
+      if (out->total) out->total[node] = totals[j];
+      if (out->scored) out->scored[node] = 1;
+      uint64_t key = ksim_oracle_tb_key(totals[j], o->prof.tiebreak_seed, seq, node);
+      if (chosen < 0 || key > best) { best = key; chosen = node; }
+    }
+    free(tmp);
+    free(totals);
+  }
+  out->chosen = chosen;
+  out->status = KSIM_STATUS_SCHEDULED;
+  assume_pod(o, p, chosen, 1);
+  return KSIM_OK;
+}
+
+/* ---- timing mode: same cycle, node loop fanned out (Parallelizer analogue) */
+int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, int32_t count,
+                         int32_t* chosen_out, int nthreads, ksim_batch_stats* st) {
+  if (!o || !ps || first < 0 || count < 0 || first + count > ps->n_pods) return KSIM_E_INVALID;
+  const int32_t N = o->n;
+  if (N == 0) return KSIM_E_INVALID;
+  if (nthreads < 1) nthreads = 1;
+  const int S = o->prof.n_score;
+  int64_t evals = 0, sched = 0, unsched = 0;
+  uint8_t* feas = o->fail;   /* 1 = passed all filters */
+  int64_t* raw = o->raw;     /* [S][N] */
+  int64_t* totals = (int64_t*)malloc(8 * (size_t)N);
+
+  for (int32_t c = 0; c < count; c++) {
+    const int32_t pi = first + c;
+    const ksim_pod* p = &ps->pods[pi];
+    const int64_t seq = o->pod_seq++;
+    const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, N);
+    const int32_t start = o->next_start;
+    int32_t nf = 0, nfailed = 0, evaluated = 0;
+    int32_t chosen = -1;
+
+#pragma omp parallel num_threads(nthreads) if (nthreads > 1)
+    {
+#pragma omp for schedule(static)
+      for (int32_t node = 0; node < N; node++) {
+        uint32_t det;
+        feas[node] = run_filter_plugins(o, ps, p, node, &det) == KSIM_PASSED;
+      }
+#pragma omp single
+      {
+        for (int32_t i = 0; i < N; i++) {
+          int32_t node = (start + i) % N;
+          evaluated++;
+          if (feas[node]) {
+            if (nf == K) break;
+            o->flist[nf++] = node;
+          } else {
+            nfailed++;
+          }
+        }
+      }
+      if (nf > 1) {
+#pragma omp for schedule(static)
+        for (int32_t j = 0; j < nf; j++)
+          for (int s = 0; s < S; s++)
+            raw[(size_t)s * N + j] = score_plugin_raw(o, ps, p, o->prof.score[s], o->flist[j]);
+#pragma omp single
+        {
+          for (int32_t j = 0; j < nf; j++) totals[j] = (S == 0) ? 1 : 0;
+          for (int s = 0; s < S; s++) {
+            int pl = o->prof.score[s];
+            int64_t* v = raw + (size_t)s * N;
+            if (has_normalize(pl)) normalize_plugin(pl, nf, v);
+            int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
+            for (int32_t j = 0; j < nf; j++) totals[j] += v[j] * w;
+          }
+          uint64_t best = 0;
+          for (int32_t j = 0; j < nf; j++) {
+            uint64_t key = ksim_oracle_tb_key(totals[j], o->prof.tiebreak_seed, seq, o->flist[j]);
+            if (chosen < 0 || key > best) { best = key; chosen = o->flist[j]; }
+          }
+        }
+      }
+    }
+    if (nf == 1) chosen = o->flist[0];
+    o->next_start = (start + nf + nfailed) % N;
+    evals += evaluated;
+    if (chosen >= 0) { assume_pod(o, p, chosen, 1); sched++; } else { unsched++; }
+    if (chosen_out) chosen_out[c] = chosen;
+  }
+  free(totals);
+  if (st) {
+    st->pods = count;
+    st->scheduled = sched;
+    st->unschedulable = unsched;
+    st->evals = evals;
+    st->device_ms = 0;
+  }
+  return KSIM_OK;
+}
+
+int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* req_mem,
+                               int64_t* req_eph, int64_t* nz_cpu, int64_t* nz_mem,
+                               int32_t* num_pods) {
+  if (!o) return KSIM_E_INVALID;
+  size_t n = (size_t)o->n;
+  if (req_cpu) memcpy(req_cpu, o->req_cpu, 8 * n);
+  if (req_mem) memcpy(req_mem, o->req_mem, 8 * n);
+  if (req_eph) memcpy(req_eph, o->req_eph, 8 * n);
+  if (nz_cpu) memcpy(nz_cpu, o->nz_cpu, 8 * n);
+  if (nz_mem) memcpy(nz_mem, o->nz_mem, 8 * n);
+  if (num_pods) memcpy(num_pods, o->num_pods, 4 * n);
+  return KSIM_OK;
+}
+
+int32_t ksim_oracle_next_start(const ksim_oracle* o) { return o->next_start; }
+void ksim_oracle_set_next_start(ksim_oracle* o, int32_t s) { o->next_start = s; }
+void ksim_oracle_set_pod_seq(ksim_oracle* o, int64_t seq) { o->pod_seq = seq; }

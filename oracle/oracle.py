@@ -1,0 +1,109 @@
+"""ctypes binding of libksim_oracle.so — the CPU restatement.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product path never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libksim_oracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.ksim_oracle_create.restype = vp
+        L.ksim_oracle_create.argtypes = [vp, vp, vp]
+        L.ksim_oracle_destroy.argtypes = [vp]
+        L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
+        L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
+        L.ksim_oracle_get_node_state.argtypes = [vp] * 7
+        L.ksim_oracle_next_start.argtypes = [vp]
+        L.ksim_oracle_next_start.restype = i32
+        L.ksim_oracle_set_next_start.argtypes = [vp, i32]
+        L.ksim_oracle_set_pod_seq.argtypes = [vp, i64]
+        L.ksim_oracle_num_feasible_nodes_to_find.argtypes = [i32, i32]
+        L.ksim_oracle_num_feasible_nodes_to_find.restype = i32
+        L.ksim_oracle_least_requested_score.argtypes = [i64, i64]
+        L.ksim_oracle_least_requested_score.restype = i64
+        L.ksim_oracle_balanced_score.argtypes = [i32, vp, vp]
+        L.ksim_oracle_balanced_score.restype = i64
+        L.ksim_oracle_default_normalize.argtypes = [i64, ctypes.c_int, i32, vp]
+        L.ksim_oracle_tb_key.argtypes = [i64, ctypes.c_uint64, i64, i32]
+        L.ksim_oracle_tb_key.restype = ctypes.c_uint64
+        _LIB = L
+    return _LIB
+
+
+class Oracle:
+    """One simulated scheduler over an encoded cluster (CPU restatement)."""
+
+    def __init__(self, cluster, profile):
+        from ksim import abi  # noqa: F401
+        self._keep = (cluster, profile)
+        self.cluster = cluster
+        self.profile = profile
+        self._nt = cluster.node_table()
+        self._vo = cluster.vocab()
+        self.h = lib().ksim_oracle_create(ctypes.byref(self._nt), ctypes.byref(self._vo),
+                                          ctypes.byref(profile))
+        if not self.h:
+            raise RuntimeError("ksim_oracle_create failed")
+
+    def close(self):
+        if self.h:
+            lib().ksim_oracle_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def cycle(self, pods, index: int) -> dict:
+        from ksim import abi
+        buf = abi.EvalBuffers(self.cluster.n_nodes, self.profile.n_score)
+        ps = pods.pod_set()
+        rc = lib().ksim_oracle_cycle(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out))
+        if rc != 0:
+            raise RuntimeError(f"oracle cycle failed: {rc}")
+        return buf.result()
+
+    def schedule(self, pods, first=0, count=None, nthreads=1):
+        from ksim import abi
+        count = pods.n_pods - first if count is None else count
+        chosen = np.zeros(count, np.int32)
+        st = abi.BatchStats()
+        ps = pods.pod_set()
+        rc = lib().ksim_oracle_schedule(self.h, ctypes.byref(ps), first, count,
+                                        chosen.ctypes.data_as(ctypes.c_void_p), nthreads,
+                                        ctypes.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle schedule failed: {rc}")
+        return chosen, st
+
+    def node_state(self) -> dict:
+        n = self.cluster.n_nodes
+        out = {k: np.zeros(n, np.int64) for k in ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem")}
+        out["num_pods"] = np.zeros(n, np.int32)
+        a = [out[k].ctypes.data_as(ctypes.c_void_p) for k in
+             ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")]
+        lib().ksim_oracle_get_node_state(self.h, *a)
+        return out
+
+    @property
+    def next_start(self) -> int:
+        return lib().ksim_oracle_next_start(self.h)
+
+    def set_next_start(self, s: int):
+        lib().ksim_oracle_set_next_start(self.h, s)
+
+    def set_pod_seq(self, s: int):
+        lib().ksim_oracle_set_pod_seq(self.h, s)

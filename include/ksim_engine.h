@@ -32,7 +32,8 @@ extern "C" {
 #define KSIM_ABI_VERSION 1
 
 /* ---- limits ------------------------------------------------------------ */
-#define KSIM_MAX_NODES        (1 << 18)  /* tie-break key packs the node index in 18 bits */
+#define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
+#define KSIM_MAX_NODES        KSIM_KEY_NODE_MASK
 #define KSIM_MAX_NODE_TAINTS  8          /* taints per node, node.Spec.Taints order */
 #define KSIM_TAINT_WORDS      4          /* taint vocabulary <= 256 ids (id 0 = none) */
 #define KSIM_MAX_SCALAR       4          /* scalar (extended) resource columns */
@@ -249,6 +250,9 @@ typedef struct ksim_batch_stats {
   int64_t unschedulable;
   int64_t evals;           /* pod x node filter evaluations (SURVEY §8(d) definition) */
   double  device_ms;       /* device time of the batch (HIP events) */
+  int64_t batches;         /* speculative batches run (batch path) */
+  int64_t truncations;     /* batches cut short by an exhausted candidate list */
+  int64_t perpod_cycles;   /* cycles run on the per-pod path */
 } ksim_batch_stats;
 
 typedef struct ksim_handle ksim_handle;
@@ -289,6 +293,24 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count,
 /* Convenience: load + schedule all. */
 int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* pods, int32_t* chosen,
                         ksim_batch_stats* stats);
+
+/* Restore the dynamic node state (Requested / NonZeroRequested / len(Pods)) to
+ * the snapshot given at ksim_set_cluster, and nextStartNodeIndex / pod
+ * sequence to 0 (device-side copy; used by sweeps and the bench). */
+int ksim_reset_cluster(ksim_handle* h);
+
+/* ---- measurement ----------------------------------------------------------- */
+/* Schedule loaded pods [first, first+count) exactly as ksim_schedule_loaded
+ * would, with a HIP event between every kernel on the engine's stream.
+ * avg_ms[k] = mean duration of kernel k over its launches that did work
+ * (0 if never launched); launches[k] = that count.  Kernel k is named by
+ * ksim_kernel_name(k).  Returns the number of kernel kinds (<= cap). */
+int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms,
+                      int64_t* launches, int32_t cap);
+const char* ksim_kernel_name(int32_t k);
+/* Batch-path diagnostics of the last ksim_schedule_loaded: out[0] batches,
+ * out[1] truncations, out[2] speculation rounds of the repair kernel.  Returns the number of values written (<= n). */
+int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 
 #ifdef __cplusplus
 }

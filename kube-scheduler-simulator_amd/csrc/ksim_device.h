@@ -5,6 +5,10 @@
 // compose them.  Compiled with -ffp-contract=off and no fast-math so float64
 // division / sqrt are IEEE correctly rounded and nothing is fused (Go on
 // GOAMD64=v1 never fuses), which makes BalancedAllocation bit-exact.
+//
+// The per-node arithmetic works on a NodeRow held in registers: the node's
+// NodeInfo aggregates, loaded once from the HBM columns (or from an LDS slot
+// in the batch repair kernel), so one evaluation never re-reads a field.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,7 +26,7 @@ constexpr int kMaxNodeScore = 100;
 // the bind step of every cycle (NodeInfo.AddPod), never re-uploaded.
 struct DevCluster {
   int32_t n, n_scalar, n_label_cols, n_taints;
-  int32_t n_label_values, _pad[3];
+  int32_t n_label_values, n_prefer_taints, _pad[2];
   const int64_t* alloc_cpu;
   const int64_t* alloc_mem;
   const int64_t* alloc_eph;
@@ -48,6 +52,7 @@ struct DevPods {
   const ksim_pod* pods;
   const ksim_label_expr* exprs;
   const ksim_term* terms;
+  const int32_t* norm_const;     // [n_pods] batch path: constant sum of weighted normalized scores
   int32_t n_pods, n_exprs, n_terms, _pad;
 };
 
@@ -57,14 +62,18 @@ struct DevState {
   int32_t cursor;        // pod index of the next cycle
   int32_t end;           // one past the last pod of the current run
   int32_t next_start;    // nextStartNodeIndex
-  int32_t _pad0;
+  int32_t truncations;   // batch path: batches cut short by an exhausted candidate list
   int64_t pod_seq;       // tie-break sequence (one per cycle)
   int64_t evals;         // pod x node filter evaluations
   int64_t scheduled;
   int64_t unschedulable;
   // scalars of the last cycle
-  int32_t chosen, status, n_feasible, n_evaluated, n_processed, k_to_find, next_start_after, _pad1;
+  int32_t chosen, status, n_feasible, n_evaluated, n_processed, k_to_find, next_start_after, batches;
+  // batch-path diagnostics: speculation rounds of k_batch_repair
+  int64_t rounds;
 };
+
+struct BRow;
 
 // Per-cycle scratch written by the filter/score kernel, read by finalize.
 struct DevScratch {
@@ -72,6 +81,11 @@ struct DevScratch {
   uint32_t* detail;      // [n]
   int64_t* raw;          // [KSIM_MAX_SCORE][n] raw scores (normalized slots; all in compat)
   int64_t* part;         // [n] sum of weighted raw of slots without NormalizeScore
+  uint64_t* cand;        // batch path: [B][n_tiles][kTileCand] per-tile best keys
+  uint64_t* topk;        // batch path: [B][T] merged top keys, descending
+  int32_t* topk_cnt;     // batch path: [B] valid merged keys
+  int32_t* topk_complete;// batch path: [B] 1 if every S0-feasible node is in the list
+  BRow* rows;            // batch path: [B][T] S0 rows of the listed nodes
 };
 
 // Compat-mode outputs (ksim_eval_out), device copies.
@@ -85,7 +99,7 @@ struct DevEvalOut {
 // Normalization kind of a score slot.
 enum NormKind : int32_t { kNormNone = 0, kNormDefault = 1, kNormDefaultReverse = 2, kNormPTS = 3, kNormIPA = 4 };
 
-__host__ __device__ inline int32_t norm_kind(int plugin) {
+__host__ __device__ __forceinline__ int32_t norm_kind(int plugin) {
   switch (plugin) {
     case KSIM_PL_TAINT_TOLERATION: return kNormDefaultReverse;
     case KSIM_PL_NODE_AFFINITY: return kNormDefault;
@@ -96,7 +110,7 @@ __host__ __device__ inline int32_t norm_kind(int plugin) {
 }
 
 // [upstream] schedule_one.go numFeasibleNodesToFind
-__host__ __device__ inline int32_t num_feasible_nodes_to_find(int32_t pct, int32_t n) {
+__host__ __device__ __forceinline__ int32_t num_feasible_nodes_to_find(int32_t pct, int32_t n) {
   if (n < 100 || pct >= 100) return n;
   int32_t a = pct;
   if (a <= 0) {
@@ -107,7 +121,7 @@ __host__ __device__ inline int32_t num_feasible_nodes_to_find(int32_t pct, int32
   return k < 100 ? 100 : k;
 }
 
-__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -115,17 +129,81 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
 }
 
 // selectHost tie-break TB(seed): a single u64 max over (total, hash, node).
-__host__ __device__ inline uint64_t tb_key(int64_t total, uint64_t seed, int64_t seq, int32_t node) {
+// node < KSIM_MAX_NODES = KSIM_KEY_NODE_MASK keeps the low field >= 1: a valid key is never 0.
+__host__ __device__ __forceinline__ uint64_t tb_key(int64_t total, uint64_t seed, int64_t seq, int32_t node) {
   uint64_t h = splitmix64(seed ^ ((uint64_t)seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
-  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)((KSIM_MAX_NODES - 1) - node);
+  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
+}
+__host__ __device__ __forceinline__ int32_t key_node(uint64_t key) {
+  return (int32_t)(KSIM_KEY_NODE_MASK - (int32_t)(key & KSIM_KEY_NODE_MASK));
 }
 
-__device__ __forceinline__ int bit_set(const uint64_t* w, uint32_t id) {
-  return (int)((w[id >> 6] >> (id & 63)) & 1ull);
+// NodeInfo aggregates of one node, in registers.
+struct NodeRow {
+  int64_t alloc_cpu, alloc_mem, alloc_eph;
+  int64_t req_cpu, req_mem, req_eph;
+  int64_t nz_cpu, nz_mem;
+  int64_t alloc_sc[KSIM_MAX_SCALAR], req_sc[KSIM_MAX_SCALAR];
+  int32_t alloc_pods, num_pods;
+  uint32_t flags;
+  int32_t node;
+  uint32_t taints[KSIM_MAX_NODE_TAINTS / 2];   // taint ids, two u16 per word, node.Spec.Taints order
+};
+
+__device__ __forceinline__ uint32_t row_taint(const NodeRow& r, int k) {
+  return (r.taints[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+}
+
+__device__ __forceinline__ NodeRow load_row(const DevCluster& c, int32_t node) {
+  NodeRow r;
+  r.node = node;
+  r.alloc_cpu = c.alloc_cpu[node];
+  r.alloc_mem = c.alloc_mem[node];
+  r.alloc_eph = c.alloc_eph[node];
+  r.req_cpu = c.req_cpu[node];
+  r.req_mem = c.req_mem[node];
+  r.req_eph = c.req_eph[node];
+  r.nz_cpu = c.nz_cpu[node];
+  r.nz_mem = c.nz_mem[node];
+  r.alloc_pods = c.alloc_pods[node];
+  r.num_pods = c.num_pods[node];
+  r.flags = c.flags[node];
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) {
+    const bool on = k < c.n_scalar;
+    r.alloc_sc[k] = on ? c.alloc_scalar[(size_t)k * c.n + node] : 0;
+    r.req_sc[k] = on ? c.req_scalar[(size_t)k * c.n + node] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++)
+    r.taints[k] = (uint32_t)c.taints[(size_t)(2 * k) * c.n + node] |
+                  ((uint32_t)c.taints[(size_t)(2 * k + 1) * c.n + node] << 16);
+  return r;
+}
+
+// floor(a / b) for a >= 0, b > 0.  Below 2^52 the correctly rounded f64
+// quotient is within 1 of the true one, so one correction step makes it exact;
+// this replaces the ~100-instruction 64-bit integer division sequence.
+__device__ __forceinline__ int64_t div_floor_nonneg(int64_t a, int64_t b) {
+  if (a >= (1ll << 52) || b >= (1ll << 52)) return a / b;
+  int64_t q = (int64_t)((double)a / (double)b);
+  if (q * b > a) q--;
+  else if ((q + 1) * b <= a) q++;
+  return q;
+}
+
+// Bit `id` of a KSIM_TAINT_WORDS-word set.  The word is picked with selects,
+// never a runtime array index, so a pod record copied into registers stays in
+// registers (a dynamic index would move it to scratch memory).
+__device__ __forceinline__ int bit_set(const uint64_t (&w)[KSIM_TAINT_WORDS], uint32_t id) {
+  static_assert(KSIM_TAINT_WORDS == 4, "bit_set assumes 4 words");
+  const uint32_t q = id >> 6;
+  const uint64_t x = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+  return (int)((x >> (id & 63)) & 1ull);
 }
 
 // labels.Requirement.Matches / metadata.name field selector
-__device__ inline bool label_req_matches(const DevCluster& c, const ksim_label_expr& e, int32_t node) {
+__device__ __forceinline__ bool label_req_matches(const DevCluster& c, const ksim_label_expr& e, int32_t node) {
   const uint8_t op = e.op;
   uint32_t v = 0;
   if (op <= KSIM_OP_LT) v = c.labels[(size_t)e.col * c.n + node];
@@ -162,7 +240,7 @@ __device__ inline bool label_req_matches(const DevCluster& c, const ksim_label_e
   }
 }
 
-__device__ inline bool term_matches(const DevCluster& c, const DevPods& P, const ksim_term& t, int32_t node) {
+__device__ __forceinline__ bool term_matches(const DevCluster& c, const DevPods& P, const ksim_term& t, int32_t node) {
   if (t.n_expr <= 0) return false;
   for (int i = 0; i < t.n_expr; i++)
     if (!label_req_matches(c, P.exprs[t.first_expr + i], node)) return false;
@@ -170,7 +248,7 @@ __device__ inline bool term_matches(const DevCluster& c, const DevPods& P, const
 }
 
 // nodeaffinity RequiredNodeAffinity.Match
-__device__ inline bool required_node_affinity_match(const DevCluster& c, const DevPods& P,
+__device__ __forceinline__ bool required_node_affinity_match(const DevCluster& c, const DevPods& P,
                                                     const ksim_pod& p, int32_t node) {
   for (int i = 0; i < p.sel_count; i++)
     if (!label_req_matches(c, P.exprs[p.sel_first + i], node)) return false;
@@ -183,7 +261,7 @@ __device__ inline bool required_node_affinity_match(const DevCluster& c, const D
 }
 
 // nodeaffinity PreferredSchedulingTerms.Score
-__device__ inline int64_t preferred_node_affinity_score(const DevCluster& c, const DevPods& P,
+__device__ __forceinline__ int64_t preferred_node_affinity_score(const DevCluster& c, const DevPods& P,
                                                         const ksim_pod& p, int32_t node) {
   int64_t count = 0;
   for (int i = 0; i < p.pref_term_count; i++) {
@@ -195,9 +273,10 @@ __device__ inline int64_t preferred_node_affinity_score(const DevCluster& c, con
 }
 
 // v1helper.FindMatchingUntoleratedTaint (NoSchedule|NoExecute)
-__device__ inline uint32_t find_matching_untolerated_taint(const DevCluster& c, const ksim_pod& p, int32_t node) {
+__device__ __forceinline__ uint32_t find_matching_untolerated_taint(const DevCluster& c, const ksim_pod& p, const NodeRow& r) {
+#pragma unroll
   for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) {
-    uint32_t tid = c.taints[(size_t)k * c.n + node];
+    uint32_t tid = row_taint(r, k);
     if (!tid) break;
     uint8_t eff = c.taint_effect[tid];
     if ((eff == KSIM_EFFECT_NO_SCHEDULE || eff == KSIM_EFFECT_NO_EXECUTE) && !bit_set(p.tol_filter, tid))
@@ -207,10 +286,11 @@ __device__ inline uint32_t find_matching_untolerated_taint(const DevCluster& c, 
 }
 
 // tainttoleration countIntolerableTaintsPreferNoSchedule
-__device__ inline int64_t count_intolerable_prefer(const DevCluster& c, const ksim_pod& p, int32_t node) {
+__device__ __forceinline__ int64_t count_intolerable_prefer(const DevCluster& c, const ksim_pod& p, const NodeRow& r) {
   int64_t n = 0;
+#pragma unroll
   for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) {
-    uint32_t tid = c.taints[(size_t)k * c.n + node];
+    uint32_t tid = row_taint(r, k);
     if (!tid) break;
     if (c.taint_effect[tid] != KSIM_EFFECT_PREFER_NO_SCHEDULE) continue;
     if (!bit_set(p.tol_prefer, tid)) n++;
@@ -219,44 +299,44 @@ __device__ inline int64_t count_intolerable_prefer(const DevCluster& c, const ks
 }
 
 // noderesources fitsRequest -> reason bits
-__device__ inline uint32_t fits_request(const DevCluster& c, const ksim_pod& p, int32_t node) {
-  uint32_t r = 0;
-  if (c.num_pods[node] + 1 > c.alloc_pods[node]) r |= KSIM_FIT_TOO_MANY_PODS;
-  if (p.req_cpu == 0 && p.req_mem == 0 && p.req_eph == 0 && !(p.flags & KSIM_POD_HAS_SCALAR)) return r;
-  if (p.req_cpu > c.alloc_cpu[node] - c.req_cpu[node]) r |= KSIM_FIT_CPU;
-  if (p.req_mem > c.alloc_mem[node] - c.req_mem[node]) r |= KSIM_FIT_MEMORY;
-  if (p.req_eph > c.alloc_eph[node] - c.req_eph[node]) r |= KSIM_FIT_EPHEMERAL;
-  for (int k = 0; k < c.n_scalar; k++) {
-    int64_t q = p.scalar_req[k];
-    if (q == 0) continue;
-    size_t ix = (size_t)k * c.n + node;
-    if (q > c.alloc_scalar[ix] - c.req_scalar[ix]) r |= (KSIM_FIT_SCALAR0 << k);
+__device__ __forceinline__ uint32_t fits_request(const NodeRow& r, const ksim_pod& p, int n_scalar) {
+  uint32_t bits = 0;
+  if (r.num_pods + 1 > r.alloc_pods) bits |= KSIM_FIT_TOO_MANY_PODS;
+  if (p.req_cpu == 0 && p.req_mem == 0 && p.req_eph == 0 && !(p.flags & KSIM_POD_HAS_SCALAR)) return bits;
+  if (p.req_cpu > r.alloc_cpu - r.req_cpu) bits |= KSIM_FIT_CPU;
+  if (p.req_mem > r.alloc_mem - r.req_mem) bits |= KSIM_FIT_MEMORY;
+  if (p.req_eph > r.alloc_eph - r.req_eph) bits |= KSIM_FIT_EPHEMERAL;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) {
+    if (k >= n_scalar) break;
+    const int64_t q = p.scalar_req[k];
+    if (q != 0 && q > r.alloc_sc[k] - r.req_sc[k]) bits |= (KSIM_FIT_SCALAR0 << k);
   }
-  return r;
+  return bits;
 }
 
 // resourceAllocationScorer.calculateResourceAllocatableRequest
-__device__ inline void calc_alloc_req(const DevCluster& c, const ksim_pod& p, int32_t node, int32_t res,
-                                      bool use_requested, int64_t& alloc, int64_t& req) {
+__device__ __forceinline__ void calc_alloc_req(const NodeRow& r, const ksim_pod& p, int32_t res, bool use_requested,
+                                               int n_scalar, int64_t& alloc, int64_t& req) {
   alloc = 0;
   req = 0;
   if (res == KSIM_RES_CPU) {
-    alloc = c.alloc_cpu[node];
-    req = (use_requested ? c.req_cpu[node] : c.nz_cpu[node]) + (use_requested ? p.req_cpu : p.nz_cpu);
+    alloc = r.alloc_cpu;
+    req = use_requested ? r.req_cpu + p.req_cpu : r.nz_cpu + p.nz_cpu;
   } else if (res == KSIM_RES_MEMORY) {
-    alloc = c.alloc_mem[node];
-    req = (use_requested ? c.req_mem[node] : c.nz_mem[node]) + (use_requested ? p.req_mem : p.nz_mem);
+    alloc = r.alloc_mem;
+    req = use_requested ? r.req_mem + p.req_mem : r.nz_mem + p.nz_mem;
   } else if (res == KSIM_RES_EPHEMERAL) {
-    alloc = c.alloc_eph[node];
-    req = c.req_eph[node] + p.req_eph;
+    alloc = r.alloc_eph;
+    req = r.req_eph + p.req_eph;
   } else {
-    int k = res - KSIM_RES_SCALAR0;
-    if (k < 0 || k >= c.n_scalar) return;
-    int64_t pr = p.scalar_req[k];
-    if (pr == 0) return;
-    size_t ix = (size_t)k * c.n + node;
-    alloc = c.alloc_scalar[ix];
-    req = c.req_scalar[ix] + pr;
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCALAR; k++) {
+      if (res == KSIM_RES_SCALAR0 + k && k < n_scalar && p.scalar_req[k] != 0) {
+        alloc = r.alloc_sc[k];
+        req = r.req_sc[k] + p.scalar_req[k];
+      }
+    }
   }
 }
 
@@ -264,65 +344,85 @@ __device__ inline void calc_alloc_req(const DevCluster& c, const ksim_pod& p, in
 __device__ __forceinline__ int64_t least_requested_score(int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (requested > capacity) return 0;
-  return ((capacity - requested) * kMaxNodeScore) / capacity;
+  if (capacity < 0 || requested > capacity) return ((capacity - requested) * kMaxNodeScore) / capacity;
+  return div_floor_nonneg((capacity - requested) * kMaxNodeScore, capacity);
 }
 
-__device__ inline int64_t fit_least_allocated_score(const DevCluster& c, const ksim_profile& prof,
-                                                    const ksim_pod& p, int32_t node) {
+__device__ __forceinline__ int64_t fit_least_allocated_score(const NodeRow& r, const ksim_profile& prof, const ksim_pod& p,
+                                                    int n_scalar) {
   int64_t node_score = 0, weight_sum = 0;
-  for (int i = 0; i < prof.fit_n_res; i++) {
-    int64_t a, r;
-    calc_alloc_req(c, p, node, prof.fit_res[i], false, a, r);
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_RES; i++) {
+    if (i >= prof.fit_n_res) break;
+    int64_t a, q;
+    calc_alloc_req(r, p, prof.fit_res[i], false, n_scalar, a, q);
     if (a == 0) continue;
-    node_score += least_requested_score(r, a) * prof.fit_res_weight[i];
+    node_score += least_requested_score(q, a) * prof.fit_res_weight[i];
     weight_sum += prof.fit_res_weight[i];
   }
   if (weight_sum == 0) return 0;
-  return node_score / weight_sum;
+  if (node_score < 0 || weight_sum < 0) return node_score / weight_sum;
+  return div_floor_nonneg(node_score, weight_sum);
 }
 
-// balanced_allocation.go balancedResourceScorer (float64, unfused)
-__device__ inline int64_t balanced_allocation_score(const DevCluster& c, const ksim_profile& prof,
-                                                    const ksim_pod& p, int32_t node) {
-  double fr[KSIM_MAX_RES];
+// balanced_allocation.go balancedResourceScorer (float64, unfused).  The
+// fractions are recomputed in the second pass instead of being stored in a
+// dynamically indexed array (which would live in scratch memory); the
+// recomputation is bitwise identical.
+__device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, const ksim_profile& prof, const ksim_pod& p,
+                                                    int n_scalar) {
   int nf = 0;
-  double total = 0;
-  for (int i = 0; i < prof.ba_n_res && i < KSIM_MAX_RES; i++) {
-    int64_t a, r;
-    calc_alloc_req(c, p, node, prof.ba_res[i], true, a, r);
+  double total = 0, f0 = 0, f1 = 0;
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_RES; i++) {
+    if (i >= prof.ba_n_res) break;
+    int64_t a, q;
+    calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
     if (a == 0) continue;
-    double f = (double)r / (double)a;
+    double f = (double)q / (double)a;
     if (f > 1) f = 1;
     total += f;
-    fr[nf++] = f;
+    if (nf == 0) f0 = f;
+    else if (nf == 1) f1 = f;
+    nf++;
   }
   double std = 0.0;
   if (nf == 2) {
-    std = fabs((fr[0] - fr[1]) / 2);
+    std = fabs((f0 - f1) / 2);
   } else if (nf > 2) {
-    double mean = total / (double)nf;
+    const double mean = total / (double)nf;
     double sum = 0;
-    for (int i = 0; i < nf; i++) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_RES; i++) {
+      if (i >= prof.ba_n_res) break;
+      int64_t a, q;
+      calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
+      if (a == 0) continue;
+      double f = (double)q / (double)a;
+      if (f > 1) f = 1;
+      sum = sum + (f - mean) * (f - mean);
+    }
     std = sqrt(sum / (double)nf);
   }
   return (int64_t)((1 - std) * (double)kMaxNodeScore);
 }
 
 // frameworkImpl.RunFilterPlugins (stop at first failure)
-__device__ inline uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                             const ksim_pod& p, int32_t node, uint32_t& detail) {
+__device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                             const ksim_pod& p, const NodeRow& r, uint32_t& detail) {
   detail = 0;
+  const int32_t node = r.node;
   for (int f = 0; f < prof.n_filter; f++) {
     switch (prof.filter[f]) {
       case KSIM_PL_NODE_UNSCHEDULABLE:
-        if ((c.flags[node] & KSIM_NODE_UNSCHEDULABLE) && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE))
+        if ((r.flags & KSIM_NODE_UNSCHEDULABLE) && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE))
           return (uint8_t)f;
         break;
       case KSIM_PL_NODE_NAME:
         if (p.node_name != -1 && p.node_name != node) return (uint8_t)f;
         break;
       case KSIM_PL_TAINT_TOLERATION: {
-        uint32_t tid = find_matching_untolerated_taint(c, p, node);
+        uint32_t tid = find_matching_untolerated_taint(c, p, r);
         if (tid) { detail = tid; return (uint8_t)f; }
         break;
       }
@@ -330,8 +430,8 @@ __device__ inline uint8_t run_filter_plugins(const DevCluster& c, const DevPods&
         if (!required_node_affinity_match(c, P, p, node)) return (uint8_t)f;
         break;
       case KSIM_PL_NODE_RESOURCES_FIT: {
-        uint32_t r = fits_request(c, p, node);
-        if (r) { detail = r; return (uint8_t)f; }
+        uint32_t bits = fits_request(r, p, c.n_scalar);
+        if (bits) { detail = bits; return (uint8_t)f; }
         break;
       }
       default:
@@ -341,18 +441,161 @@ __device__ inline uint8_t run_filter_plugins(const DevCluster& c, const DevPods&
   return KSIM_PASSED;
 }
 
-__device__ inline int64_t score_plugin_raw(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                           const ksim_pod& p, int plugin, int32_t node) {
+__device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                           const ksim_pod& p, int plugin, const NodeRow& r) {
   switch (plugin) {
-    case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(c, prof, p, node);
-    case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(c, prof, p, node);
-    case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, node);
-    case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, node);
+    case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(r, prof, p, c.n_scalar);
+    case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(r, prof, p, c.n_scalar);
+    case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
+    case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
     default: return 0;   // ImageLocality (no images), PTS/IPA without constraints/terms
   }
 }
 
-__device__ inline void assume_pod(const DevCluster& c, const ksim_pod& p, int32_t node, int sign) {
+// Sum of weighted raw scores of the slots without NormalizeScore.
+__device__ __forceinline__ int64_t partial_total(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                        const ksim_pod& p, const NodeRow& r) {
+  int64_t part = 0;
+  for (int k = 0; k < prof.n_score; k++) {
+    const int pl = prof.score[k];
+    if (norm_kind(pl) != kNormNone) continue;
+    const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
+    part += score_plugin_raw(c, P, prof, p, pl, r) * w;
+  }
+  return part;
+}
+
+// ---- batch path: the profile compiled down to what batchable pods need -----
+// Batchable pods (see pod_batchable in ksim_engine.cpp) pass every filter
+// plugin except the ones listed here, and their normalized scores are a
+// per-pod constant, so a key is
+//   static filters (bind-invariant) -> Fit filter -> w_fit*LeastAllocated +
+//   w_ba*BalancedAllocation + constant -> TB key.
+struct BatchProg {
+  int32_t n_static;                        // static (bind-invariant) filters, profile order
+  uint8_t static_filter[KSIM_MAX_FILTER];
+  int32_t has_fit_filter;
+  int32_t _pad;
+  int64_t w_fit, w_ba;                     // summed profile weights of the Fit / BA score slots
+};
+
+// Compact row for the batch repair's LDS staging: the NodeRow fields a
+// batchable pod can read (batchable pods request no scalar resources and the
+// scoring strategies use cpu / memory / ephemeral-storage only).  96 bytes.
+struct BRow {
+  int64_t alloc_cpu, alloc_mem, alloc_eph;
+  int64_t req_cpu, req_mem, req_eph;
+  int64_t nz_cpu, nz_mem;
+  int32_t alloc_pods, num_pods;
+  uint32_t flags;
+  int32_t node;
+  uint32_t taints[KSIM_MAX_NODE_TAINTS / 2];
+};
+static_assert(sizeof(BRow) == 96, "BRow layout");
+
+__device__ __forceinline__ BRow to_brow(const NodeRow& r) {
+  BRow b;
+  b.alloc_cpu = r.alloc_cpu; b.alloc_mem = r.alloc_mem; b.alloc_eph = r.alloc_eph;
+  b.req_cpu = r.req_cpu; b.req_mem = r.req_mem; b.req_eph = r.req_eph;
+  b.nz_cpu = r.nz_cpu; b.nz_mem = r.nz_mem;
+  b.alloc_pods = r.alloc_pods; b.num_pods = r.num_pods; b.flags = r.flags; b.node = r.node;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++) b.taints[k] = r.taints[k];
+  return b;
+}
+
+__device__ __forceinline__ NodeRow from_brow(const BRow& b) {
+  NodeRow r;
+  r.alloc_cpu = b.alloc_cpu; r.alloc_mem = b.alloc_mem; r.alloc_eph = b.alloc_eph;
+  r.req_cpu = b.req_cpu; r.req_mem = b.req_mem; r.req_eph = b.req_eph;
+  r.nz_cpu = b.nz_cpu; r.nz_mem = b.nz_mem;
+  r.alloc_pods = b.alloc_pods; r.num_pods = b.num_pods; r.flags = b.flags; r.node = b.node;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) { r.alloc_sc[k] = 0; r.req_sc[k] = 0; }
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++) r.taints[k] = b.taints[k];
+  return r;
+}
+
+__device__ __forceinline__ void brow_add_pod(BRow& r, const ksim_pod& p) {
+  r.req_cpu += p.req_cpu;
+  r.req_mem += p.req_mem;
+  r.req_eph += p.req_eph;
+  r.nz_cpu += p.nz_cpu;
+  r.nz_mem += p.nz_mem;
+  r.num_pods += 1;
+}
+
+// dst = src + pod (NodeInfo.AddPod), field by field (src may alias dst).
+__device__ __forceinline__ void brow_assign_add(BRow& dst, const BRow& src, const ksim_pod& p) {
+  const int64_t rc = src.req_cpu + p.req_cpu, rm = src.req_mem + p.req_mem, re = src.req_eph + p.req_eph;
+  const int64_t zc = src.nz_cpu + p.nz_cpu, zm = src.nz_mem + p.nz_mem;
+  const int64_t ac = src.alloc_cpu, am = src.alloc_mem, ae = src.alloc_eph;
+  const int32_t ap = src.alloc_pods, np = src.num_pods + 1, nd = src.node;
+  const uint32_t fl = src.flags, t0 = src.taints[0], t1 = src.taints[1], t2 = src.taints[2], t3 = src.taints[3];
+  dst.alloc_cpu = ac; dst.alloc_mem = am; dst.alloc_eph = ae;
+  dst.req_cpu = rc; dst.req_mem = rm; dst.req_eph = re;
+  dst.nz_cpu = zc; dst.nz_mem = zm;
+  dst.alloc_pods = ap; dst.num_pods = np; dst.flags = fl; dst.node = nd;
+  dst.taints[0] = t0; dst.taints[1] = t1; dst.taints[2] = t2; dst.taints[3] = t3;
+}
+
+__device__ __forceinline__ void store_brow_dynamic(const DevCluster& c, const BRow& r) {
+  const int32_t node = r.node;
+  c.req_cpu[node] = r.req_cpu;
+  c.req_mem[node] = r.req_mem;
+  c.req_eph[node] = r.req_eph;
+  c.nz_cpu[node] = r.nz_cpu;
+  c.nz_mem[node] = r.nz_mem;
+  c.num_pods[node] = r.num_pods;
+}
+
+__device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const DevPods& P, const BatchProg& bp,
+                                           const ksim_pod& p, const NodeRow& r) {
+  for (int f = 0; f < bp.n_static; f++) {
+    switch (bp.static_filter[f]) {
+      case KSIM_PL_NODE_UNSCHEDULABLE:
+        if ((r.flags & KSIM_NODE_UNSCHEDULABLE) && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE)) return false;
+        break;
+      case KSIM_PL_NODE_NAME:
+        if (p.node_name != -1 && p.node_name != r.node) return false;
+        break;
+      case KSIM_PL_TAINT_TOLERATION:
+        if (find_matching_untolerated_taint(c, p, r)) return false;
+        break;
+      case KSIM_PL_NODE_AFFINITY:
+        if (!required_node_affinity_match(c, P, p, r.node)) return false;
+        break;
+      default:
+        break;
+    }
+  }
+  return true;
+}
+
+// Key of a batchable pod on a row whose static filters passed (0 = infeasible).
+__device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
+                                            int32_t norm_const, const NodeRow& r, int n_scalar, int64_t seq) {
+  if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
+  int64_t tot = norm_const;
+  if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);
+  if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, n_scalar);
+  if (prof.n_score == 0) tot = 1;
+  return tb_key(tot, prof.tiebreak_seed, seq, r.node);
+}
+
+__device__ __forceinline__ void row_add_pod(NodeRow& r, const ksim_pod& p, int sign) {
+  r.req_cpu += sign * p.req_cpu;
+  r.req_mem += sign * p.req_mem;
+  r.req_eph += sign * p.req_eph;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) r.req_sc[k] += sign * p.scalar_req[k];
+  r.nz_cpu += sign * p.nz_cpu;
+  r.nz_mem += sign * p.nz_mem;
+  r.num_pods += sign;
+}
+
+__device__ __forceinline__ void assume_pod(const DevCluster& c, const ksim_pod& p, int32_t node, int sign) {
   c.req_cpu[node] += sign * p.req_cpu;
   c.req_mem[node] += sign * p.req_mem;
   c.req_eph[node] += sign * p.req_eph;
@@ -360,6 +603,17 @@ __device__ inline void assume_pod(const DevCluster& c, const ksim_pod& p, int32_
   c.nz_cpu[node] += sign * p.nz_cpu;
   c.nz_mem[node] += sign * p.nz_mem;
   c.num_pods[node] += sign;
+}
+
+__device__ __forceinline__ void store_row_dynamic(const DevCluster& c, const NodeRow& r) {
+  const int32_t node = r.node;
+  c.req_cpu[node] = r.req_cpu;
+  c.req_mem[node] = r.req_mem;
+  c.req_eph[node] = r.req_eph;
+  for (int k = 0; k < c.n_scalar; k++) c.req_scalar[(size_t)k * c.n + node] = r.req_sc[k];
+  c.nz_cpu[node] = r.nz_cpu;
+  c.nz_mem[node] = r.nz_mem;
+  c.num_pods[node] = r.num_pods;
 }
 
 }  // namespace ksim

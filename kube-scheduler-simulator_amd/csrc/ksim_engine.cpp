@@ -1,10 +1,12 @@
 // ksim_engine.cpp — host runtime behind the C ABI (include/ksim_engine.h).
 //
 // Owns the HBM-resident snapshot (SoA node columns, vocabularies), the pod
-// queue, the per-cycle scratch, one HIP stream and a captured hipGraph of G
-// back-to-back cycles that is replayed for batch runs.  Every input is
-// validated on the host before any kernel sees it (a bad index must never
-// reach the device), copied during the call, and never retained (cgo rule).
+// queue, the per-cycle scratch and one HIP stream.  Batch runs are split into
+// maximal runs of pods the speculative batch path can take (P100 and no
+// node-varying normalized score) and runs that need the per-pod path; each
+// path is a captured hipGraph replayed until the run's cursor is consumed.
+// Every input is validated on the host before any kernel sees it (a bad index
+// must never reach the device), copied during the call, never retained.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,7 +21,8 @@ using namespace ksim;
 
 namespace {
 
-constexpr int kGraphCycles = 128;   // cycles per captured graph
+constexpr int kGraphCycles = 128;      // per-pod cycles per captured graph
+constexpr int kGraphBatches = 16;      // speculative batches per captured graph
 
 struct DevBuf {
   void* p = nullptr;
@@ -36,10 +39,18 @@ struct ksim_handle {
 
   bool has_profile = false;
   ksim_profile prof{};
+  BatchProg bp{};
 
   bool has_cluster = false;
   DevCluster dc{};
   std::vector<DevBuf> cluster_bufs;
+  std::vector<uint8_t> taint_effect;    // host copy (batchability analysis)
+
+  // device copy of the uploaded dynamic columns (ksim_reset_cluster)
+  struct {
+    int64_t *req_cpu, *req_mem, *req_eph, *req_scalar, *nz_cpu, *nz_mem;
+    int32_t* num_pods;
+  } init{};
 
   DevScratch sc{};
   DevEvalOut eo{};
@@ -52,13 +63,13 @@ struct ksim_handle {
   DevPods dp{};
   int32_t* d_chosen = nullptr;
   std::vector<DevBuf> pod_bufs;
+  std::vector<uint8_t> batchable;       // per loaded pod
 
   // compat-mode single pod
-  DevPods dp1{};
   std::vector<DevBuf> pod1_bufs;
 
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t graph_exec = nullptr;
+  hipGraphExec_t graph_cycle = nullptr;
+  hipGraphExec_t graph_batch = nullptr;
 };
 
 namespace {
@@ -73,9 +84,9 @@ int hip_fail(ksim_handle* h, hipError_t e, const char* what) {
   return set_err(h, code, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIPCHK(h, expr)                                   \
-  do {                                                    \
-    hipError_t _e = (expr);                               \
+#define HIPCHK(h, expr)                                    \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
     if (_e != hipSuccess) return hip_fail((h), _e, #expr); \
   } while (0)
 
@@ -102,11 +113,11 @@ int upload(ksim_handle* h, std::vector<DevBuf>& owner, const void* src, size_t b
   return KSIM_OK;
 }
 
-void drop_graph(ksim_handle* h) {
-  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
-  if (h->graph) (void)hipGraphDestroy(h->graph);
-  h->graph_exec = nullptr;
-  h->graph = nullptr;
+void drop_graphs(ksim_handle* h) {
+  if (h->graph_cycle) (void)hipGraphExecDestroy(h->graph_cycle);
+  if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
+  h->graph_cycle = nullptr;
+  h->graph_batch = nullptr;
 }
 
 bool plugin_supported(int id) { return id >= 0 && id < KSIM_PL_COUNT; }
@@ -143,6 +154,44 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
   return KSIM_OK;
 }
 
+// Batch-path eligibility of a pod and the constant it adds to every total.
+// The batch path needs P100 (every feasible node is kept, so no window) and
+// every normalized plugin constant over nodes:
+//   TaintToleration: no PreferNoSchedule taint the pod does not tolerate ->
+//                    all raw 0 -> DefaultNormalizeScore(reverse) = 100
+//   NodeAffinity:    no preferred terms -> raw 0 -> 0
+//   PodTopologySpread: no constraints (this ABI revision) -> 100
+//   InterPodAffinity:  no terms -> topologyScore empty -> 0
+bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
+  const ksim_profile& prof = h->prof;
+  if (num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, h->dc.n) != h->dc.n) return false;
+  if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
+  int64_t acc = 0;
+  for (int k = 0; k < prof.n_score; k++) {
+    const int pl = prof.score[k];
+    const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
+    switch (norm_kind(pl)) {
+      case kNormDefaultReverse: {
+        for (size_t t = 1; t < h->taint_effect.size(); t++)
+          if (h->taint_effect[t] == KSIM_EFFECT_PREFER_NO_SCHEDULE && !((p.tol_prefer[t >> 6] >> (t & 63)) & 1ull))
+            return false;
+        acc += 100 * w;
+        break;
+      }
+      case kNormDefault:
+        if (p.pref_term_count > 0) return false;
+        break;
+      case kNormPTS:
+        acc += 100 * w;
+        break;
+      default:
+        break;
+    }
+  }
+  norm_const = (int32_t)acc;
+  return true;
+}
+
 int ensure_ready(ksim_handle* h) {
   if (!h) return KSIM_E_INVALID;
   if (!h->has_profile) return set_err(h, KSIM_E_INVALID, "profile not set");
@@ -156,6 +205,7 @@ LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen) {
   a.c = h->dc;
   a.P = P;
   a.prof = h->prof;
+  a.bp = h->bp;
   a.st = h->st;
   a.s = h->sc;
   a.o = h->eo;
@@ -167,6 +217,69 @@ int set_run(ksim_handle* h, int32_t first, int32_t end) {
   h->run_hdr[0] = first;
   h->run_hdr[1] = end;
   HIPCHK(h, hipMemcpyAsync(h->st, h->run_hdr, sizeof(h->run_hdr), hipMemcpyHostToDevice, h->stream));
+  return KSIM_OK;
+}
+
+int read_state(ksim_handle* h, DevState& st) {
+  HIPCHK(h, hipMemcpyAsync(&st, h->st, sizeof(st), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return KSIM_OK;
+}
+
+int capture(ksim_handle* h, bool batch, hipGraphExec_t* out) {
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  LaunchArgs a = make_args(h, h->dp, h->d_chosen);
+  hipGraph_t g = nullptr;
+  HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  if (batch)
+    for (int i = 0; i < kGraphBatches; i++) launch_batch(a, h->stream);
+  else
+    for (int i = 0; i < kGraphCycles; i++) launch_cycle(a, h->stream, false);
+  hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return hip_fail(h, e, "hipGraphInstantiate");
+  return KSIM_OK;
+}
+
+// Run pods [a, b) on one path (all of them share the path).
+int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch) {
+  int rc;
+  if ((rc = set_run(h, a, b))) return rc;
+  if (!batch) {
+    if (!h->graph_cycle && (rc = capture(h, false, &h->graph_cycle))) return rc;
+    for (int32_t done = a; done < b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(h->graph_cycle, h->stream));
+    return KSIM_OK;
+  }
+  if (!h->graph_batch && (rc = capture(h, true, &h->graph_batch))) return rc;
+  // every batch commits >= 1 pod, nearly always kBatchPods: replay until consumed
+  int32_t cursor = a;
+  while (cursor < b) {
+    const int32_t left = b - cursor;
+    const int reps = std::max(1, left / (kBatchPods * kGraphBatches));
+    for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(h->graph_batch, h->stream));
+    DevState st;
+    if ((rc = read_state(h, st))) return rc;
+    if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "batch path made no progress");
+    cursor = st.cursor;
+  }
+  return KSIM_OK;
+}
+
+// Split [first, first+count) into maximal same-path runs.
+template <typename F>
+int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
+  int32_t i = first;
+  const int32_t end = first + count;
+  while (i < end) {
+    const bool b = h->batchable[i] != 0;
+    int32_t j = i + 1;
+    while (j < end && (h->batchable[j] != 0) == b) j++;
+    int rc = fn(i, j, b);
+    if (rc) return rc;
+    i = j;
+  }
   return KSIM_OK;
 }
 
@@ -199,11 +312,9 @@ int ksim_create(int device, ksim_handle** out) {
   if (device < 0 || device >= ndev) return KSIM_E_INVALID;
   auto* h = new ksim_handle();
   h->device = device;
-  if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-      hipMalloc(&h->st, sizeof(DevState)) != hipSuccess ||
-      hipMemset(h->st, 0, sizeof(DevState)) != hipSuccess) {
+      hipMalloc(&h->st, sizeof(DevState)) != hipSuccess || hipMemset(h->st, 0, sizeof(DevState)) != hipSuccess) {
     delete h;
     return KSIM_E_DEVICE;
   }
@@ -215,7 +326,7 @@ void ksim_destroy(ksim_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  drop_graph(h);
+  drop_graphs(h);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
   free_bufs(h->pod_bufs);
@@ -242,9 +353,29 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   }
   if (p->fit_n_res < 0 || p->fit_n_res > KSIM_MAX_RES || p->ba_n_res < 0 || p->ba_n_res > KSIM_MAX_RES)
     return set_err(h, KSIM_E_INVALID, "scoring resources out of range");
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
   h->prof = *p;
   h->has_profile = true;
-  drop_graph(h);
+  // the profile compiled for batchable pods (see BatchProg in ksim_device.h)
+  BatchProg bp{};
+  for (int i = 0; i < p->n_filter; i++) {
+    const int f = p->filter[i];
+    if (f == KSIM_PL_NODE_UNSCHEDULABLE || f == KSIM_PL_NODE_NAME || f == KSIM_PL_TAINT_TOLERATION ||
+        f == KSIM_PL_NODE_AFFINITY)
+      bp.static_filter[bp.n_static++] = (uint8_t)f;
+    if (f == KSIM_PL_NODE_RESOURCES_FIT) bp.has_fit_filter = 1;
+  }
+  for (int k = 0; k < p->n_score; k++) {
+    const int64_t w = p->score_weight[k] == 0 ? 1 : p->score_weight[k];
+    if (p->score[k] == KSIM_PL_NODE_RESOURCES_FIT) bp.w_fit += w;
+    if (p->score[k] == KSIM_PL_BALANCED_ALLOCATION) bp.w_ba += w;
+  }
+  h->bp = bp;
+  drop_graphs(h);
+  // batchability depends on the profile: a loaded queue must be reloaded
+  free_bufs(h->pod_bufs);
+  h->dp = DevPods{};
+  h->batchable.clear();
   return KSIM_OK;
 }
 
@@ -256,20 +387,23 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   if (t->n_scalar < 0 || t->n_scalar > KSIM_MAX_SCALAR) return set_err(h, KSIM_E_INVALID, "n_scalar out of range");
   if (t->n_label_cols < 0 || t->n_label_cols > KSIM_MAX_LABEL_COLS)
     return set_err(h, KSIM_E_INVALID, "n_label_cols out of range");
-  if (v->n_taints < 1 || v->n_taints > 64 * KSIM_TAINT_WORDS) return set_err(h, KSIM_E_INVALID, "n_taints out of range");
-  if (n > 0 && (!t->alloc_cpu || !t->alloc_mem || !t->alloc_eph || !t->alloc_pods || !t->req_cpu ||
-                !t->req_mem || !t->req_eph || !t->nz_cpu || !t->nz_mem || !t->num_pods || !t->flags ||
-                !t->taints || (t->n_label_cols > 0 && !t->labels) ||
-                (t->n_scalar > 0 && (!t->alloc_scalar || !t->req_scalar))))
+  if (v->n_taints < 1 || v->n_taints > 64 * KSIM_TAINT_WORDS || !v->taint_effect)
+    return set_err(h, KSIM_E_INVALID, "n_taints out of range");
+  if (n > 0 && (!t->alloc_cpu || !t->alloc_mem || !t->alloc_eph || !t->alloc_pods || !t->req_cpu || !t->req_mem ||
+                !t->req_eph || !t->nz_cpu || !t->nz_mem || !t->num_pods || !t->flags || !t->taints ||
+                (t->n_label_cols > 0 && !t->labels) || (t->n_scalar > 0 && (!t->alloc_scalar || !t->req_scalar))))
     return set_err(h, KSIM_E_INVALID, "null node column");
   for (size_t i = 0; i < (size_t)n * KSIM_MAX_NODE_TAINTS; i++)
     if (t->taints[i] >= v->n_taints) return set_err(h, KSIM_E_INVALID, "taint id out of vocabulary");
   if (t->n_label_cols > 0 && (!v->label_col_offset || (v->n_label_values > 0 && (!v->label_num || !v->label_num_ok))))
     return set_err(h, KSIM_E_INVALID, "null label vocabulary");
   (void)hipStreamSynchronize(h->stream);
-  drop_graph(h);
+  drop_graphs(h);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
+  free_bufs(h->pod_bufs);
+  h->dp = DevPods{};
+  h->batchable.clear();
   h->has_cluster = false;
 
   DevCluster c{};
@@ -280,11 +414,11 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   c.n_label_values = v->n_label_values;
   const size_t N = (size_t)n;
   int rc;
-#define UP(field, src, bytes)                                                       \
-  do {                                                                              \
-    void* _p = nullptr;                                                             \
+#define UP(field, src, bytes)                                                         \
+  do {                                                                                \
+    void* _p = nullptr;                                                               \
     if ((rc = upload(h, h->cluster_bufs, (src), (bytes), &_p)) != KSIM_OK) return rc; \
-    c.field = reinterpret_cast<decltype(c.field)>(_p);                              \
+    c.field = reinterpret_cast<decltype(c.field)>(_p);                                \
   } while (0)
   UP(alloc_cpu, t->alloc_cpu, 8 * N);
   UP(alloc_mem, t->alloc_mem, 8 * N);
@@ -307,42 +441,61 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   UP(label_num_ok, v->label_num_ok, (size_t)std::max(v->n_label_values, 0));
 #undef UP
   h->dc = c;
+  h->taint_effect.assign(v->taint_effect, v->taint_effect + v->n_taints);
+  {
+    void* q = nullptr;
+#define SNAP(field, bytes)                                                                 \
+  do {                                                                                     \
+    if ((rc = upload(h, h->cluster_bufs, nullptr, (bytes), &q)) != KSIM_OK) return rc;     \
+    h->init.field = reinterpret_cast<decltype(h->init.field)>(q);                          \
+    HIPCHK(h, hipMemcpyAsync(q, c.field, (bytes), hipMemcpyDeviceToDevice, h->stream));     \
+  } while (0)
+    SNAP(req_cpu, 8 * N);
+    SNAP(req_mem, 8 * N);
+    SNAP(req_eph, 8 * N);
+    SNAP(req_scalar, 8 * N * t->n_scalar);
+    SNAP(nz_cpu, 8 * N);
+    SNAP(nz_mem, 8 * N);
+    SNAP(num_pods, 4 * N);
+#undef SNAP
+  }
 
   DevScratch s{};
   DevEvalOut o{};
+  const size_t n_tiles = (N + kTileNodes - 1) / kTileNodes;
   void* p = nullptr;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, N, &p))) return rc;
-  s.fail = (uint8_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 4 * N, &p))) return rc;
-  s.detail = (uint32_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 8 * N * KSIM_MAX_SCORE, &p))) return rc;
-  s.raw = (int64_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 8 * N, &p))) return rc;
-  s.part = (int64_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, N, &p))) return rc;
-  o.scored = (uint8_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 8 * N * KSIM_MAX_SCORE, &p))) return rc;
-  o.raw = (int64_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 8 * N * KSIM_MAX_SCORE, &p))) return rc;
-  o.norm = (int64_t*)p;
-  if ((rc = upload(h, h->scratch_bufs, nullptr, 8 * N, &p))) return rc;
-  o.total = (int64_t*)p;
+#define SCR(dst, type, bytes)                                                         \
+  do {                                                                                \
+    if ((rc = upload(h, h->scratch_bufs, nullptr, (bytes), &p)) != KSIM_OK) return rc; \
+    dst = (type)p;                                                                    \
+  } while (0)
+  SCR(s.fail, uint8_t*, N);
+  SCR(s.detail, uint32_t*, 4 * N);
+  SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
+  SCR(s.part, int64_t*, 8 * N);
+  SCR(s.cand, uint64_t*, 8 * (size_t)kBatchPods * n_tiles * kTileCand);
+  SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kTopT);
+  SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods);
+  SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
+  SCR(s.rows, BRow*, sizeof(BRow) * (size_t)kBatchPods * kTopT);
+  SCR(o.scored, uint8_t*, N);
+  SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
+  SCR(o.norm, int64_t*, 8 * N * KSIM_MAX_SCORE);
+  SCR(o.total, int64_t*, 8 * N);
+#undef SCR
   h->sc = s;
   h->eo = o;
   DevState zero{};
   HIPCHK(h, hipMemcpyAsync(h->st, &zero, sizeof(zero), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->has_cluster = true;
-  // a loaded pod queue was validated against the previous cluster
-  free_bufs(h->pod_bufs);
-  h->dp = DevPods{};
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   h->d_chosen = nullptr;
   return KSIM_OK;
 }
 
-int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
-                        int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods) {
+int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
+                        int64_t* nz_mem, int32_t* num_pods) {
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   HIPCHK(h, hipSetDevice(h->device));
   const size_t N = (size_t)h->dc.n;
@@ -383,16 +536,15 @@ int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
 static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std::vector<ksim_label_expr>& ex,
                            std::vector<ksim_term>& tm) {
   pod = ps->pods[i];
-  auto copy_expr = [&](int32_t e) { ex.push_back(ps->exprs[e]); };
   int32_t sel0 = (int32_t)ex.size();
-  for (int32_t k = 0; k < pod.sel_count; k++) copy_expr(pod.sel_first + k);
+  for (int32_t k = 0; k < pod.sel_count; k++) ex.push_back(ps->exprs[pod.sel_first + k]);
   pod.sel_first = sel0;
   auto copy_terms = [&](int32_t& first, int32_t count) {
     int32_t t0 = (int32_t)tm.size();
     for (int32_t t = 0; t < count; t++) {
       ksim_term x = ps->terms[first + t];
       int32_t e0 = (int32_t)ex.size();
-      for (int32_t k = 0; k < x.n_expr; k++) copy_expr(x.first_expr + k);
+      for (int32_t k = 0; k < x.n_expr; k++) ex.push_back(ps->exprs[x.first_expr + k]);
       x.first_expr = e0;
       tm.push_back(x);
     }
@@ -423,10 +575,11 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksi
   P.exprs = (const ksim_label_expr*)p;
   if ((rc = upload(h, h->pod1_bufs, tm.data(), tm.size() * sizeof(ksim_term), &p))) return rc;
   P.terms = (const ksim_term*)p;
+  if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
+  P.norm_const = (const int32_t*)p;
   P.n_pods = 1;
   P.n_exprs = (int32_t)ex.size();
   P.n_terms = (int32_t)tm.size();
-  h->dp1 = P;
   if ((rc = set_run(h, 0, 1))) return rc;
   launch_cycle(make_args(h, P, nullptr), h->stream, true);
   HIPCHK(h, hipGetLastError());
@@ -481,10 +634,13 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     if ((rc = validate_pod(h, ps, i))) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  drop_graph(h);
+  drop_graphs(h);
   free_bufs(h->pod_bufs);
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   h->d_chosen = nullptr;
+  std::vector<int32_t> nc((size_t)std::max(ps->n_pods, 1), 0);
+  h->batchable.assign((size_t)ps->n_pods, 0);
+  for (int32_t i = 0; i < ps->n_pods; i++) h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
   DevPods P{};
   void* p = nullptr;
   if ((rc = upload(h, h->pod_bufs, ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return rc;
@@ -493,6 +649,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.exprs = (const ksim_label_expr*)p;
   if ((rc = upload(h, h->pod_bufs, ps->terms, sizeof(ksim_term) * ps->n_terms, &p))) return rc;
   P.terms = (const ksim_term*)p;
+  if ((rc = upload(h, h->pod_bufs, nc.data(), 4 * nc.size(), &p))) return rc;
+  P.norm_const = (const int32_t*)p;
   P.n_pods = ps->n_pods;
   P.n_exprs = ps->n_exprs;
   P.n_terms = ps->n_terms;
@@ -503,35 +661,30 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   return KSIM_OK;
 }
 
-static int build_graph(ksim_handle* h) {
-  drop_graph(h);
-  LaunchArgs a = make_args(h, h->dp, h->d_chosen);
-  HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < kGraphCycles; i++) launch_cycle(a, h->stream, false);
-  hipError_t e = hipStreamEndCapture(h->stream, &h->graph);
-  if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
-  HIPCHK(h, hipGraphInstantiate(&h->graph_exec, h->graph, nullptr, nullptr, 0));
-  return KSIM_OK;
-}
-
 int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* chosen, ksim_batch_stats* stats) {
   int rc = ensure_ready(h);
   if (rc) return rc;
   if (!h->dp.pods && count > 0) return set_err(h, KSIM_E_INVALID, "no pods loaded");
   if (first < 0 || count < 0 || first + count > h->dp.n_pods) return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
   HIPCHK(h, hipSetDevice(h->device));
-  if (!h->graph_exec && (rc = build_graph(h))) return rc;
-  if ((rc = set_run(h, first, first + count))) return rc;
+  HIPCHK(h, hipMemsetAsync(&h->st->truncations, 0, 4, h->stream));
   HIPCHK(h, hipMemsetAsync(&h->st->evals, 0, 3 * sizeof(int64_t), h->stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->rounds, 0, 8, h->stream));
+  int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  for (int32_t done = 0; done < count; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(h->graph_exec, h->stream));
+  rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch) {
+    if (!batch) perpod += b - a;
+    return run_range(h, a, b, batch);
+  });
+  if (rc) return rc;
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   HIPCHK(h, hipGetLastError());
   if (chosen && count) HIPCHK(h, hipMemcpy(chosen, h->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
   if (stats) {
     DevState st;
-    HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+    if ((rc = read_state(h, st))) return rc;
     float ms = 0;
     HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
     stats->pods = count;
@@ -539,6 +692,9 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
     stats->unschedulable = st.unschedulable;
     stats->evals = st.evals;
     stats->device_ms = ms;
+    stats->batches = st.batches;
+    stats->truncations = st.truncations;
+    stats->perpod_cycles = perpod;
   }
   return KSIM_OK;
 }
@@ -549,4 +705,95 @@ int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* ps, int32_t* chosen,
   return ksim_schedule_loaded(h, 0, ps->n_pods, chosen, stats);
 }
 
+int ksim_reset_cluster(ksim_handle* h) {
+  if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t N = (size_t)h->dc.n;
+  const DevCluster& c = h->dc;
+  HIPCHK(h, hipMemcpyAsync(c.req_cpu, h->init.req_cpu, 8 * N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.req_mem, h->init.req_mem, 8 * N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.req_eph, h->init.req_eph, 8 * N, hipMemcpyDeviceToDevice, h->stream));
+  if (c.n_scalar)
+    HIPCHK(h, hipMemcpyAsync(c.req_scalar, h->init.req_scalar, 8 * N * c.n_scalar, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.nz_cpu, h->init.nz_cpu, 8 * N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.nz_mem, h->init.nz_mem, 8 * N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.num_pods, h->init.num_pods, 4 * N, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->st, 0, sizeof(DevState), h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return KSIM_OK;
+}
+
+const char* ksim_kernel_name(int32_t k) {
+  if (k >= 0 && k < kKernelsPerCycle) return kKernelNames[k];
+  k -= kKernelsPerCycle;
+  if (k >= 0 && k < kKernelsPerBatch) return kBatchKernelNames[k];
+  return nullptr;
+}
+
+int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms, int64_t* launches, int32_t cap) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch;
+  if (!avg_ms || cap < kKinds) return set_err(h, KSIM_E_INVALID, "avg_ms too small");
+  if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
+    return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
+  HIPCHK(h, hipSetDevice(h->device));
+  double sum[kKinds] = {0};
+  int64_t n[kKinds] = {0};
+  LaunchArgs a = make_args(h, h->dp, h->d_chosen);
+  rc = for_each_run(h, first, count, [&](int32_t lo, int32_t hi, bool batch) -> int {
+    int r;
+    if ((r = set_run(h, lo, hi))) return r;
+    const int per = batch ? kKernelsPerBatch : kKernelsPerCycle;
+    const int base = batch ? kKernelsPerCycle : 0;
+    int32_t cursor = lo;
+    while (cursor < hi) {
+      const int32_t iters = batch ? std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods) : std::min(512, hi - cursor);
+      std::vector<hipEvent_t> evs((size_t)iters * (per + 1));
+      for (auto& e : evs) HIPCHK(h, hipEventCreate(&e));
+      if (batch) HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
+      for (int32_t i = 0; i < iters; i++) {
+        if (batch)
+          launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
+        else
+          launch_cycle(a, h->stream, false, &evs[(size_t)i * (per + 1)]);
+      }
+      HIPCHK(h, hipGetLastError());
+      DevState st;
+      if ((r = read_state(h, st))) return r;
+      // iterations past the end exit at once; count only those that did work
+      const int32_t did = batch ? std::min<int32_t>(iters, st.batches) : std::min(iters, st.cursor - cursor);
+      for (int32_t i = 0; i < did; i++)
+        for (int k = 0; k < per; k++) {
+          float ms = 0;
+          const size_t b = (size_t)i * (per + 1);
+          HIPCHK(h, hipEventElapsedTime(&ms, evs[b + k], evs[b + k + 1]));
+          sum[base + k] += ms;
+          n[base + k] += 1;
+        }
+      for (auto& e : evs) (void)hipEventDestroy(e);
+      if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "no progress while timing");
+      cursor = st.cursor;
+    }
+    return KSIM_OK;
+  });
+  if (rc) return rc;
+  for (int k = 0; k < kKinds; k++) {
+    avg_ms[k] = n[k] ? sum[k] / n[k] : 0.0;
+    if (launches) launches[k] = n[k];
+  }
+  return kKinds;
+}
+
 }  // extern "C"
+
+extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
+  if (!h || !out || n < 0) return KSIM_E_INVALID;
+  DevState st;
+  int rc = read_state(h, st);
+  if (rc) return rc;
+  const int64_t v[3] = {st.batches, st.truncations, st.rounds};
+  const int32_t m = n < 3 ? n : 3;
+  for (int32_t i = 0; i < m; i++) out[i] = v[i];
+  return m;
+}

@@ -6,18 +6,36 @@
 
 namespace ksim {
 
+// Batch path geometry.
+constexpr int kBatchPods = 64;     // B: pods per speculative batch (= one wave64 in the repair)
+constexpr int kTopT = 16;
+constexpr int kRepairThreads = 512;   // k_batch_repair block size          // T: candidate keys kept per pod
+constexpr int kPodsPerGroup = 4;   // pods evaluated per node row load in k_batch_eval
+constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
+constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
+constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
+
 struct LaunchArgs {
   DevCluster c;
   DevPods P;
   ksim_profile prof;
+  BatchProg bp;
   DevState* st;
   DevScratch s;
   DevEvalOut o;
   int32_t* chosen;   // [n_pods] device, may be null
 };
 
+constexpr int kKernelsPerCycle = 2;
+extern const char* const kKernelNames[kKernelsPerCycle];
+constexpr int kKernelsPerBatch = 3;
+extern const char* const kBatchKernelNames[kKernelsPerBatch];
+
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat);
+// evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.
+void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, hipEvent_t* evs = nullptr);
+// One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
+void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_assume(const DevCluster& c, const ksim_pod& p, int32_t node, int sign, hipStream_t stream);
 
 }  // namespace ksim

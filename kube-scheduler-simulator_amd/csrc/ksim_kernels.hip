@@ -1,21 +1,18 @@
-// ksim_kernels.hip — HIP kernels of the per-pod scheduling cycle (gfx950).
+// ksim_kernels.hip — HIP kernels of the scheduling cycle (gfx950).
 //
-// One cycle = two launches, both reading the pod index from device state so a
-// captured hipGraph of G cycles can be replayed back to back:
+// Two execution paths produce identical placements (both bit-exact with the
+// oracle):
 //
-//   k_filter_score  grid over nodes (256 threads = 4 wave64 per block).
-//                   RunFilterPlugins for every node (SURVEY §8(a) a17, a22,
-//                   a25, a26) and, for feasible nodes, the raw Score of every
-//                   profile score plugin (a23, a24, a25, a26).  Node columns are
-//                   read coalesced (SoA), the pod record through the scalar
-//                   cache (wave-uniform).
-//   k_finalize      one 1024-thread block: findNodesThatPassFilters' window
-//                   (numFeasibleNodesToFind + rotated first-K scan, a16) by a
-//                   block prefix scan, per-plugin NormalizeScore extrema over
-//                   the kept list (a31, a28, a30), weighted totals (a18),
-//                   selectHost as a packed-u64 argmax (a19, TB tie-break),
-//                   then NodeInfo.AddPod on the chosen row (a20) and the
-//                   nextStartNodeIndex update.
+// A. Per-pod path (compat mode, and pods the batch path cannot take):
+//    k_filter_score  grid over nodes: RunFilterPlugins (SURVEY §8(a) a17, a22,
+//                    a25, a26) and, for feasible nodes, every raw Score (a23-a26).
+//    k_finalize      one 1024-thread block: numFeasibleNodesToFind window by a
+//                    block prefix scan (a16), NormalizeScore extrema (a31),
+//                    weighted totals (a18), selectHost as a packed-u64 argmax
+//                    (a19, TB tie-break), NodeInfo.AddPod (a20).
+//
+// B. Batch path (P100, pods whose normalized plugins are constant over
+//    nodes): ksim_batch.hip.
 #include "ksim_device.h"
 #include "ksim_internal.h"
 
@@ -56,10 +53,8 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
   return v;
 }
 
-constexpr int kFinalThreads = 1024;
-constexpr int kFinalWaves = kFinalThreads / 64;
-
-// Block max over u64 (all threads get the result).
+// Block max over u64 for a block of NW waves (all threads get the result).
+template <int NW>
 __device__ uint64_t block_max_u64(uint64_t v, uint64_t* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   v = wave_max_u64(v);
@@ -67,9 +62,13 @@ __device__ uint64_t block_max_u64(uint64_t v, uint64_t* sh) {
   if (lane == 0) sh[w] = v;
   __syncthreads();
   uint64_t r = sh[0];
-  for (int i = 1; i < kFinalWaves; i++) r = sh[i] > r ? sh[i] : r;
+#pragma unroll
+  for (int i = 1; i < NW; i++) r = sh[i] > r ? sh[i] : r;
   return r;
 }
+
+constexpr int kFinalThreads = 1024;
+constexpr int kFinalWaves = kFinalThreads / 64;
 
 __device__ int64_t block_max_i64(int64_t v, int64_t* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -139,7 +138,7 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
   }
 }
 
-// ---- kernel 1: filter + raw score per node ------------------------------------
+// ==== A. per-pod path ===========================================================
 template <bool COMPAT>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, ksim_profile prof,
                                                       const DevState* __restrict__ st, DevScratch s) {
@@ -148,15 +147,16 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
   if (node >= c.n) return;
   const ksim_pod& p = P.pods[pi];
+  const NodeRow r = load_row(c, node);
   uint32_t det;
-  const uint8_t r = run_filter_plugins(c, P, prof, p, node, det);
-  s.fail[node] = r;
+  const uint8_t res = run_filter_plugins(c, P, prof, p, r, det);
+  s.fail[node] = res;
   if (COMPAT) s.detail[node] = det;
-  if (r != KSIM_PASSED) return;
+  if (res != KSIM_PASSED) return;
   int64_t part = 0;
   for (int k = 0; k < prof.n_score; k++) {
     const int pl = prof.score[k];
-    const int64_t v = score_plugin_raw(c, P, prof, p, pl, node);
+    const int64_t v = score_plugin_raw(c, P, prof, p, pl, r);
     if (norm_kind(pl) == kNormNone) {
       const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
       part += v * w;
@@ -168,7 +168,6 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
   s.part[node] = part;
 }
 
-// ---- kernel 2: window, normalize, select, bind --------------------------------
 template <bool COMPAT>
 __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPods P, ksim_profile prof,
                                                             DevState* __restrict__ st, DevScratch s,
@@ -288,8 +287,8 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
       const uint64_t key = tb_key(tot, prof.tiebreak_seed, seq, node);
       best = key > best ? key : best;
     }
-    best = block_max_u64(best, shu);
-    chosen = (int32_t)((KSIM_MAX_NODES - 1) - (int32_t)(best & (KSIM_MAX_NODES - 1)));
+    best = block_max_u64<kFinalWaves>(best, shu);
+    chosen = key_node(best);
   }
 
   // Phase D: assume/bind + scheduler state.
@@ -323,15 +322,21 @@ __global__ void k_assume(DevCluster c, ksim_pod p, int32_t node, int sign) {
 }
 
 // ---- launchers ----------------------------------------------------------------
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat) {
+const char* const kKernelNames[kKernelsPerCycle] = {"k_filter_score", "k_finalize"};
+
+void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, hipEvent_t* evs) {
   const int blocks = (a.c.n + 255) / 256;
-  if (compat) {
+  if (evs) (void)hipEventRecord(evs[0], stream);
+  if (compat)
     k_filter_score<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-    k_finalize<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
-  } else {
+  else
     k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  if (compat)
+    k_finalize<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
+  else
     k_finalize<false><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
-  }
+  if (evs) (void)hipEventRecord(evs[2], stream);
 }
 
 void launch_assume(const DevCluster& c, const ksim_pod& p, int32_t node, int sign, hipStream_t stream) {

@@ -1,0 +1,56 @@
+// ksim_wave.h — wave64 primitives for gfx950.
+//
+// wave_max_u64_dpp: the DPP reduction (quad_perm xor1, xor2, row_ror 4, 8
+// inside each 16-lane row, then row_bcast15 / row_bcast31 across rows, result
+// in lane 63, broadcast by readlane).  It never touches the LDS, unlike the
+// __shfl_xor form (ds_bpermute) — on the repair kernel's single-wave critical
+// path that difference is several hundred cycles per reduction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ksim {
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false);
+  return ((uint64_t)(uint32_t)hi2 << 32) | (uint32_t)lo2;
+}
+
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Wave max over u64; all 64 lanes must be active.
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+  v = umax64(v, dpp_u64<0xb1, 0xf>(v));    // quad_perm [1,0,3,2]
+  v = umax64(v, dpp_u64<0x4e, 0xf>(v));    // quad_perm [2,3,0,1]
+  v = umax64(v, dpp_u64<0x124, 0xf>(v));   // row_ror:4
+  v = umax64(v, dpp_u64<0x128, 0xf>(v));   // row_ror:8
+  v = umax64(v, dpp_u64<0x142, 0xa>(v));   // row_bcast:15 -> rows 1, 3
+  v = umax64(v, dpp_u64<0x143, 0xc>(v));   // row_bcast:31 -> rows 2, 3
+  return readlane_u64(v, 63);
+}
+
+__device__ __forceinline__ void cswap_desc(uint64_t& a, uint64_t& b) {
+  const uint64_t hi = a > b ? a : b, lo = a > b ? b : a;
+  a = hi;
+  b = lo;
+}
+
+// Order LDS accesses of one wave without a workgroup barrier (which would
+// also wait for every outstanding global memory operation).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace ksim

@@ -12,7 +12,7 @@ import numpy as np
 
 ABI_VERSION = 1
 
-MAX_NODES = 1 << 18
+MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
 TAINT_WORDS = 4
 MAX_SCALAR = 4
@@ -191,7 +191,8 @@ class BatchStats(ctypes.Structure):
     _fields_ = [
         ("pods", ctypes.c_int64), ("scheduled", ctypes.c_int64),
         ("unschedulable", ctypes.c_int64), ("evals", ctypes.c_int64),
-        ("device_ms", ctypes.c_double),
+        ("device_ms", ctypes.c_double), ("batches", ctypes.c_int64),
+        ("truncations", ctypes.c_int64), ("perpod_cycles", ctypes.c_int64),
     ]
 
 

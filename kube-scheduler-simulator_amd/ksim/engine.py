@@ -22,7 +22,8 @@ EXPORTS = [
     "ksim_abi_version", "ksim_abi_sizeof", "ksim_create", "ksim_destroy", "ksim_last_error",
     "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_next_start",
     "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
-    "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch",
+    "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
+    "ksim_time_kernels", "ksim_kernel_name", "ksim_get_diag",
 ]
 
 
@@ -60,6 +61,11 @@ def lib():
         L.ksim_load_pods.argtypes = [vp, vp]
         L.ksim_schedule_loaded.argtypes = [vp, i32, i32, vp, vp]
         L.ksim_schedule_batch.argtypes = [vp, vp, vp, vp]
+        L.ksim_reset_cluster.argtypes = [vp]
+        L.ksim_time_kernels.argtypes = [vp, i32, i32, vp, vp, i32]
+        L.ksim_kernel_name.argtypes = [i32]
+        L.ksim_kernel_name.restype = ctypes.c_char_p
+        L.ksim_get_diag.argtypes = [vp, vp, i32]
         _LIB = L
     return _LIB
 
@@ -82,9 +88,9 @@ class Engine:
             raise KsimError(rc, lib().ksim_last_error(self.h).decode())
 
     def close(self):
-        if getattr(self, "h", None):
-            lib().ksim_destroy(self.h)
-            self.h = None
+        if getattr(self, "h", None) and _LIB is not None:
+            _LIB.ksim_destroy(self.h)
+        self.h = None
 
     __del__ = close
 
@@ -148,3 +154,28 @@ class Engine:
 
     def set_pod_seq(self, s: int):
         self._chk(lib().ksim_set_pod_seq(self.h, s))
+
+    def reset_cluster(self):
+        """Restore the uploaded snapshot's dynamic node state (device-side copy)."""
+        self._chk(lib().ksim_reset_cluster(self.h))
+
+    def diag(self) -> dict:
+        """Batch-path diagnostics of the last schedule_loaded call."""
+        out = np.zeros(3, np.int64)
+        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 3)
+        if n < 0:
+            self._chk(n)
+        return {"batches": int(out[0]), "truncations": int(out[1]), "rounds": int(out[2])}
+
+    def time_kernels(self, first: int, count: int) -> dict:
+        """Schedule loaded pods [first, first+count) with HIP events between the
+        kernels on the engine's own stream.  Returns {kernel: (mean ms, launches)}
+        for every kernel that ran."""
+        out = np.zeros(16, np.float64)
+        cnt = np.zeros(16, np.int64)
+        n = lib().ksim_time_kernels(self.h, first, count, out.ctypes.data_as(ctypes.c_void_p),
+                                    cnt.ctypes.data_as(ctypes.c_void_p), 16)
+        if n < 0:
+            self._chk(n)
+        return {lib().ksim_kernel_name(k).decode(): (float(out[k]), int(cnt[k]))
+                for k in range(n) if cnt[k] > 0}

@@ -123,7 +123,7 @@ static uint64_t splitmix64(uint64_t x) {
  * reservoir sampling of [upstream] schedule_one.go selectHost (global math/rand). */
 uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node) {
   uint64_t h = splitmix64(seed ^ ((uint64_t)pod_seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
-  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)((KSIM_MAX_NODES - 1) - node);
+  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
 }
 
 /* [upstream] schedule_one.go (*Scheduler).numFeasibleNodesToFind — §8(a) a16 */

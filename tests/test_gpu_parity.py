@@ -75,3 +75,70 @@ def test_config2_slice_batch(pct):
     es, os_ = eng.node_state(), ora.node_state()
     for k in es:
         np.testing.assert_array_equal(es[k], os_[k])
+
+
+def _batch_vs_oracle(cluster, pods, pct=100, seed=0x4B53494D):
+    prof = _prof(pct, seed)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+    return st
+
+
+@pytest.mark.parametrize("n_nodes", [1, 7, 64, 65, 300])
+def test_batch_small_clusters(n_nodes):
+    """Ragged node counts (partial wave tiles, single node), pod count not a
+    multiple of the batch size, and pods that stop fitting (unschedulable)."""
+    cluster, _ = gen.config2(n_nodes=n_nodes, n_pods=1)
+    pods = gen.bare_pods(n_nodes * 40 + 37, seed=99)
+    st = _batch_vs_oracle(cluster, pods)
+    assert st.perpod_cycles == 0 and st.batches > 0
+
+
+def test_batch_truncation_identical_pods():
+    """Identical pods on identical nodes: every pod's top-T overlaps the nodes
+    already bound in the batch, forcing truncated batches; placements must still
+    equal the one-by-one oracle."""
+    cluster, _ = gen.config2(n_nodes=40, n_pods=1)
+    cluster.alloc_cpu[:] = 64000
+    cluster.alloc_mem[:] = 256 << 30
+    pods = gen.bare_pods(3000, seed=5, cpu_steps=1, mem_steps=1)
+    st = _batch_vs_oracle(cluster, pods)
+    assert st.truncations > 0
+
+
+def test_batch_mixed_runs_config1_p100():
+    """Config-1 pods on config-1 nodes without PreferNoSchedule taints: pods
+    with preferred node affinity take the per-pod path, the rest the batch
+    path; the segmented runs stay exact."""
+    from ksim.encode import encode_cluster, encode_pods
+    nodes, pods = gen.config1_objects()
+    for n in nodes:
+        n.taints = [t for t in n.taints if t.effect != "PreferNoSchedule"]
+    cluster, _ = encode_cluster(nodes)
+    st = _batch_vs_oracle(cluster, encode_pods(cluster, pods))
+    assert st.perpod_cycles > 0 and st.batches > 0
+
+
+def test_batch_weights_sweep():
+    """Config-5 style weight vectors over a config-2 slice."""
+    cluster, pods = gen.config2(n_nodes=1000, n_pods=3000)
+    ws = gen.config5_weights()[:3]
+    for w in ws:
+        sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+        names = [p.name for p in sp.score_plugins()]
+        prof = profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, w)}))
+        eng = Engine(0)
+        eng.set_profile(prof)
+        eng.set_cluster(cluster)
+        chosen, _ = eng.schedule_batch(pods)
+        ochosen, _ = Oracle(cluster, prof).schedule(pods)
+        np.testing.assert_array_equal(chosen, ochosen)

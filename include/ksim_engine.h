@@ -309,7 +309,8 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
                       int64_t* launches, int32_t cap);
 const char* ksim_kernel_name(int32_t k);
 /* Batch-path diagnostics of the last ksim_schedule_loaded: out[0] batches,
- * out[1] truncations, out[2] speculation rounds of the repair kernel.  Returns the number of values written (<= n). */
+ * out[1] truncations (an exhausted candidate list ended a batch), out[2] cuts
+ * (a pod's exact choice was a node bound earlier in its batch, ending it).  Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 
 #ifdef __cplusplus

@@ -69,8 +69,9 @@ struct DevState {
   int64_t unschedulable;
   // scalars of the last cycle
   int32_t chosen, status, n_feasible, n_evaluated, n_processed, k_to_find, next_start_after, batches;
-  // batch-path diagnostics: speculation rounds of k_batch_repair
-  int64_t rounds;
+  // batch path: batches ended early because a pod's best node was one bound
+  // earlier in the batch (its guess was not its exact choice)
+  int64_t cuts;
 };
 
 struct BRow;
@@ -85,7 +86,10 @@ struct DevScratch {
   uint64_t* topk;        // batch path: [B][T] merged top keys, descending
   int32_t* topk_cnt;     // batch path: [B] valid merged keys
   int32_t* topk_complete;// batch path: [B] 1 if every S0-feasible node is in the list
-  BRow* rows;            // batch path: [B][T] S0 rows of the listed nodes
+  uint64_t* gkey;        // batch path: [B] key of each pod's greedy guess (0: none)
+  int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
+  uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
+  uint32_t* done;        // batch path: k_batch_pairs blocks finished (last-block election)
 };
 
 // Compat-mode outputs (ksim_eval_out), device copies.

@@ -477,7 +477,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kTopT);
   SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
-  SCR(s.rows, BRow*, sizeof(BRow) * (size_t)kBatchPods * kTopT);
+  SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
+  SCR(s.chain_end, int32_t*, 4);
+  SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
+  SCR(s.done, uint32_t*, 4);
   SCR(o.scored, uint8_t*, N);
   SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(o.norm, int64_t*, 8 * N * KSIM_MAX_SCORE);
@@ -670,7 +673,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   HIPCHK(h, hipMemsetAsync(&h->st->truncations, 0, 4, h->stream));
   HIPCHK(h, hipMemsetAsync(&h->st->evals, 0, 3 * sizeof(int64_t), h->stream));
   HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
-  HIPCHK(h, hipMemsetAsync(&h->st->rounds, 0, 8, h->stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->cuts, 0, 8, h->stream));
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch) {
@@ -792,7 +795,7 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  const int64_t v[3] = {st.batches, st.truncations, st.rounds};
+  const int64_t v[3] = {st.batches, st.truncations, st.cuts};
   const int32_t m = n < 3 ? n : 3;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;

@@ -7,10 +7,9 @@
 namespace ksim {
 
 // Batch path geometry.
-constexpr int kBatchPods = 64;     // B: pods per speculative batch (= one wave64 in the repair)
-constexpr int kTopT = 16;
-constexpr int kRepairThreads = 512;   // k_batch_repair block size          // T: candidate keys kept per pod
-constexpr int kPodsPerGroup = 4;   // pods evaluated per node row load in k_batch_eval
+constexpr int kBatchPods = 256;    // B: pods per speculative batch
+constexpr int kTopT = 8;           // T: candidate keys kept per pod (<= 64: one lane per entry in the chain)
+static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch geometry");
 constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
 constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
 constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
@@ -28,7 +27,7 @@ struct LaunchArgs {
 
 constexpr int kKernelsPerCycle = 2;
 extern const char* const kKernelNames[kKernelsPerCycle];
-constexpr int kKernelsPerBatch = 3;
+constexpr int kKernelsPerBatch = 4;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).

@@ -165,7 +165,7 @@ class Engine:
         n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 3)
         if n < 0:
             self._chk(n)
-        return {"batches": int(out[0]), "truncations": int(out[1]), "rounds": int(out[2])}
+        return {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2])}
 
     def time_kernels(self, first: int, count: int) -> dict:
         """Schedule loaded pods [first, first+count) with HIP events between the

@@ -142,3 +142,27 @@ def test_batch_weights_sweep():
         chosen, _ = eng.schedule_batch(pods)
         ochosen, _ = Oracle(cluster, prof).schedule(pods)
         np.testing.assert_array_equal(chosen, ochosen)
+
+
+def test_batch_cuts_balanced_heavy():
+    """BalancedAllocation-heavy weights with skewed pods: binding a pod can
+    raise a node's balance score for a later pod of the same batch, so some
+    pods' exact choice is a node bound earlier in the batch (a cut).  The cut
+    path must stay exact."""
+    cluster, _ = gen.config2(n_nodes=300, n_pods=1)
+    pods = gen.bare_pods(4000, seed=17, cpu_steps=20, mem_steps=2)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    names = [p.name for p in sp.score_plugins()]
+    w = {n: (10 if n == "NodeResourcesBalancedAllocation" else 1) for n in names}
+    prof = profile.compile_profile(sp.with_weights(w))
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    d = eng.diag()
+    print("diag", d)
+    assert d["cuts"] > 0

@@ -35,24 +35,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-BATCH_PODS, TOP_T = 64, 16   # csrc/ksim_internal.h kBatchPods, kTopT
-ROW_BYTES = 88               # NodeRow fields a bind reads + writes back
-
-
-def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int) -> int:
-    """Algorithmic bytes per launch of each kernel."""
-    tiles = (n_nodes + 63) // 64
+def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
+    """Algorithmic HBM bytes per launch of each kernel:
+    the node rows an evaluation kernel must read once per pod it evaluates;
+    the small bookkeeping kernels are priced by the keys they move."""
+    B, T = geom["pods_per_batch"], geom["top_t"]
+    tiles = (n_nodes + geom["tile_nodes"] - 1) // geom["tile_nodes"]
     if name == "k_filter_score":
-        return B_EVAL * n_nodes                      # one node row per pod x node eval
+        return B_EVAL * n_nodes                       # one node row per pod x node eval
     if name == "k_finalize":
-        return n_nodes * (1 + 8 + 8 * n_norm)        # fail code + partial total + normalized raws
+        return n_nodes * (1 + 8 + 8 * n_norm)         # fail code + partial total + normalized raws
     if name == "k_batch_eval":
-        return B_EVAL * n_nodes * BATCH_PODS         # B pods x N nodes evals per launch
+        return B_EVAL * n_nodes * B                   # B pods x N nodes evals per launch
     if name == "k_batch_merge":
-        return 8 * BATCH_PODS * (tiles * TOP_T + TOP_T)
-    if name == "k_batch_repair":
-        return 8 * BATCH_PODS * TOP_T + 2 * ROW_BYTES * BATCH_PODS
+        return 8 * B * (tiles * geom["tile_cand"] + T)
+    if name == "k_batch_chain":
+        return 8 * B * T * 2
+    if name == "k_batch_pairs":
+        return B * (B - 1) // 2 * B_EVAL + 8 * B * 3      # one bound-row re-eval per pod pair
     return 0
+
+
+# the kernel that carries the pod x node evaluations on each path
+EVAL_KERNELS = ("k_batch_eval", "k_filter_score")
 
 
 def cpu_baseline(cluster, pods, sp, seconds: float, threads: int) -> dict:
@@ -156,10 +161,12 @@ def main():
     # Roofline of the dominant kernel: per-kernel HIP events on the engine stream.
     eng.reset_cluster()
     kt = eng.time_kernels(0, min(pods.n_pods, 8192))
-    dominant = max(kt, key=lambda k: kt[k][0] * kt[k][1])     # largest share of device time
+    geom = engine.batch_geometry()
+    by_time = max(kt, key=lambda k: kt[k][0] * kt[k][1])      # largest share of device time
+    dominant = next((k for k in EVAL_KERNELS if k in kt), by_time)
     n_norm = sum(1 for p in sp.score_plugins()
                  if p.name in ("TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity"))
-    alg = kernel_alg_bytes(dominant, cluster.n_nodes, n_norm)
+    alg = kernel_alg_bytes(dominant, cluster.n_nodes, n_norm, geom)
     achieved = alg / (kt[dominant][0] * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -167,7 +174,7 @@ def main():
         try:
             tj = json.load(open(tpath))
             if tj.get("kernel") == dominant and tj.get("nodes") == cluster.n_nodes:
-                traffic = tj.get("bytes_per_launch")
+                traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
@@ -190,13 +197,15 @@ def main():
                    "parallelism": "replicas (per-GPU score-weight profiles)" if world > 1 else "single GPU"},
         "pods_per_s": cycles / elapsed,
         "kernels": {k: {"avg_ms": v[0], "launches": v[1],
-                        "alg_GBps": kernel_alg_bytes(k, cluster.n_nodes, n_norm) / (v[0] * 1e-3) / 1e9}
+                        "alg_GBps": kernel_alg_bytes(k, cluster.n_nodes, n_norm, geom) / (v[0] * 1e-3) / 1e9}
                     for k, v in kt.items()},
         "batch_stats": {"batches": st.batches, "truncations": st.truncations,
                         "perpod_cycles": st.perpod_cycles},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": alg},
+                     "alg_bytes_per_launch": alg, "avg_launch_ms": kt[dominant][0],
+                     "dominant_by_time": by_time},
+        "batch_geometry": geom,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         log("[rank 0] cpu baseline ...")

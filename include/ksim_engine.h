@@ -312,6 +312,10 @@ const char* ksim_kernel_name(int32_t k);
  * out[1] truncations (an exhausted candidate list ended a batch), out[2] cuts
  * (a pod's exact choice was a node bound earlier in its batch, ending it).  Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
+/* Batch-path geometry compiled into the library: out[0] pods per batch (B),
+ * out[1] candidate keys kept per pod (T), out[2] nodes per wave tile,
+ * out[3] keys a tile keeps per pod.  Returns the number written (<= n). */
+int ksim_batch_geometry(int32_t* out, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -247,18 +247,33 @@ int capture(ksim_handle* h, bool batch, hipGraphExec_t* out) {
 int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch) {
   int rc;
   if ((rc = set_run(h, a, b))) return rc;
+  // No launch is ever issued past the end of the run (a launch there would
+  // exit at once and skew per-kernel averages): whole graphs while they fit,
+  // then single launches for the remainder.
+  LaunchArgs la = make_args(h, h->dp, h->d_chosen);
   if (!batch) {
     if (!h->graph_cycle && (rc = capture(h, false, &h->graph_cycle))) return rc;
-    for (int32_t done = a; done < b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(h->graph_cycle, h->stream));
+    int32_t done = a;
+    for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(h->graph_cycle, h->stream));
+    for (; done < b; done++) launch_cycle(la, h->stream, false);
+    HIPCHK(h, hipGetLastError());
     return KSIM_OK;
   }
   if (!h->graph_batch && (rc = capture(h, true, &h->graph_batch))) return rc;
-  // every batch commits >= 1 pod, nearly always kBatchPods: replay until consumed
+  // every batch commits between 1 and kBatchPods pods: a graph of
+  // kGraphBatches batches never overshoots while left >= kBatchPods * kGraphBatches,
+  // and ceil(left / kBatchPods) single batches never overshoot either
   int32_t cursor = a;
   while (cursor < b) {
     const int32_t left = b - cursor;
-    const int reps = std::max(1, left / (kBatchPods * kGraphBatches));
-    for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(h->graph_batch, h->stream));
+    if (left >= kBatchPods * kGraphBatches) {
+      const int reps = left / (kBatchPods * kGraphBatches);
+      for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(h->graph_batch, h->stream));
+    } else {
+      const int n1 = (left + kBatchPods - 1) / kBatchPods;
+      for (int r = 0; r < n1; r++) launch_batch(la, h->stream);
+      HIPCHK(h, hipGetLastError());
+    }
     DevState st;
     if ((rc = read_state(h, st))) return rc;
     if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "batch path made no progress");
@@ -797,6 +812,14 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   if (rc) return rc;
   const int64_t v[3] = {st.batches, st.truncations, st.cuts};
   const int32_t m = n < 3 ? n : 3;
+  for (int32_t i = 0; i < m; i++) out[i] = v[i];
+  return m;
+}
+
+extern "C" int ksim_batch_geometry(int32_t* out, int32_t n) {
+  if (!out || n < 0) return KSIM_E_INVALID;
+  const int32_t v[4] = {kBatchPods, kTopT, kTileNodes, kTileCand};
+  const int32_t m = n < 4 ? n : 4;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }

@@ -23,7 +23,7 @@ EXPORTS = [
     "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_next_start",
     "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
-    "ksim_time_kernels", "ksim_kernel_name", "ksim_get_diag",
+    "ksim_time_kernels", "ksim_kernel_name", "ksim_get_diag", "ksim_batch_geometry",
 ]
 
 
@@ -66,8 +66,17 @@ def lib():
         L.ksim_kernel_name.argtypes = [i32]
         L.ksim_kernel_name.restype = ctypes.c_char_p
         L.ksim_get_diag.argtypes = [vp, vp, i32]
+        L.ksim_batch_geometry.argtypes = [vp, i32]
         _LIB = L
     return _LIB
+
+
+def batch_geometry() -> dict:
+    """Batch-path geometry compiled into libksim_engine.so (no GPU needed)."""
+    out = np.zeros(4, np.int32)
+    lib().ksim_batch_geometry(out.ctypes.data_as(ctypes.c_void_p), 4)
+    return {"pods_per_batch": int(out[0]), "top_t": int(out[1]), "tile_nodes": int(out[2]),
+            "tile_cand": int(out[3])}
 
 
 class Engine:

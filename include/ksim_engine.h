@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 1
+#define KSIM_ABI_VERSION 2
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -42,6 +42,9 @@ extern "C" {
 #define KSIM_MAX_FILTER       16
 #define KSIM_MAX_SCORE        8
 #define KSIM_MAX_RES          4          /* resources in a scoring strategy */
+#define KSIM_MAX_USES         16         /* topology uses per pod (PTS constraints + IPA terms) */
+#define KSIM_MAX_CLASSES      4096       /* count classes (see ksim_topo_use) */
+#define KSIM_COL_NONE         0xFFFF     /* topology key carried by no node */
 
 /* ---- error codes (SURVEY §8(b) "Errors") -------------------------------- */
 #define KSIM_OK            0
@@ -95,6 +98,9 @@ enum ksim_plugin {
 #define KSIM_POD_HAS_HOST_PORTS          8u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
 #define KSIM_POD_HAS_VOLUMES            16u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
 
+/* pod topo_flags */
+#define KSIM_POD_IPA_SELF_AFFINITY 1u  /* podMatchesAllAffinityTerms(required affinity terms, pod) */
+
 /* node-selector requirement operators (k8s NodeSelectorOperator + matchFields) */
 #define KSIM_OP_IN            0
 #define KSIM_OP_NOT_IN        1
@@ -117,6 +123,13 @@ enum ksim_plugin {
 #define KSIM_FIT_MEMORY          4u
 #define KSIM_FIT_EPHEMERAL       8u
 #define KSIM_FIT_SCALAR0        16u   /* << k for scalar column k */
+
+/* PodTopologySpread / InterPodAffinity failure details (ksim_eval_out.fail_detail) */
+#define KSIM_PTS_MISSING_LABEL   1u   /* ErrReasonNodeLabelNotMatch (UnschedulableAndUnresolvable) */
+#define KSIM_PTS_SKEW            2u   /* ErrReasonConstraintsNotMatch */
+#define KSIM_IPA_AFFINITY        1u   /* ErrReasonAffinityRulesNotMatch (UnschedulableAndUnresolvable) */
+#define KSIM_IPA_ANTI_AFFINITY   2u   /* ErrReasonAntiAffinityRulesNotMatch */
+#define KSIM_IPA_EXISTING_ANTI   3u   /* ErrReasonExistingAntiAffinityRulesNotMatch */
 
 /* per-pod cycle status */
 #define KSIM_STATUS_SCHEDULED      0
@@ -145,6 +158,10 @@ typedef struct ksim_node_table {
   const uint32_t* flags;          /* KSIM_NODE_* */
   const uint16_t* taints;         /* [KSIM_MAX_NODE_TAINTS][n_nodes]; taint vocab id, 0 terminates */
   const uint32_t* labels;         /* [n_label_cols][n_nodes]; label value id, 0 = key absent */
+  int32_t n_classes;              /* <= KSIM_MAX_CLASSES */
+  int32_t _pad1;
+  const int32_t* class_count;     /* [n_classes][n_nodes]: pods (or term weights) of each count
+                                     class on each node, from the pods already bound */
 } ksim_node_table;
 
 /* Vocabularies the host interned (strings stay on the host). */
@@ -155,6 +172,10 @@ typedef struct ksim_vocab {
   const int32_t* label_col_offset;/* [n_label_cols]: base index of the column's value ids */
   const int64_t* label_num;       /* strconv.ParseInt(value,10,64) per (col, value id) */
   const uint8_t* label_num_ok;    /* 1 if that parse succeeded */
+  int32_t n_topo_log;             /* >= n_nodes + 1 when any pod spreads with ScheduleAnyway */
+  int32_t _pad;
+  const double* topo_log;         /* [size] = math.Log(float64(size + 2)) (PTS topologyNormalizingWeight),
+                                     computed by the host so the device never evaluates log */
 } ksim_vocab;
 
 /* One NodeSelectorRequirement compiled against the vocabulary. */
@@ -189,8 +210,51 @@ typedef struct ksim_pod {
   int32_t  sel_first, sel_count;             /* spec.nodeSelector as In{value} exprs (AND) */
   int32_t  req_term_first, req_term_count;   /* required node affinity terms (OR) */
   int32_t  pref_term_first, pref_term_count; /* preferred node affinity terms */
-  int32_t  _reserved[8];                     /* topology spread / pod affinity (later ABI rev) */
+  int32_t  use_first, use_count;             /* topology uses (PodTopologySpread / InterPodAffinity) */
+  int32_t  add_first, add_count;             /* count-class contributions once bound (NodeInfo.AddPod) */
+  uint32_t topo_flags;                       /* KSIM_POD_IPA_* */
+  int32_t  _reserved[3];
 } ksim_pod;
+
+/* Count classes.  The host evaluates every label selector / affinity term
+ * against pod namespaces and labels once (that string work does not depend
+ * on placement) and hands the device integer classes:
+ *   class_count[c][node] = sum over pods bound to node of their multiplicity in c.
+ * A "use" tells the device which class to aggregate over which topology key
+ * and in which role ([upstream] podtopologyspread / interpodaffinity):
+ *   PTS_HARD           DoNotSchedule constraint: TpPairToMatchNum over eligible nodes,
+ *                      skew vs the critical-path minimum (Filter)
+ *   PTS_SOFT           ScheduleAnyway constraint: TopologyPairToPodCounts (PreScore/Score)
+ *   IPA_EXISTING_ANTI  existingAntiAffinityCounts of a carried required anti-affinity term
+ *   IPA_AFFINITY       affinityCounts of one incoming required affinity term
+ *   IPA_ANTI           antiAffinityCounts of one incoming required anti-affinity term
+ *   IPA_SCORE          topologyScore += arg x domain count
+ *   IPA_SCORE_HARD     topologyScore += hardPodAffinityWeight x domain count */
+#define KSIM_USE_PTS_HARD           0
+#define KSIM_USE_PTS_SOFT           1
+#define KSIM_USE_IPA_EXISTING_ANTI  2
+#define KSIM_USE_IPA_AFFINITY       3
+#define KSIM_USE_IPA_ANTI           4
+#define KSIM_USE_IPA_SCORE          5
+#define KSIM_USE_IPA_SCORE_HARD     6
+#define KSIM_USEF_SELF_MATCH        1u   /* PTS: constraint selector matches the pod itself */
+#define KSIM_USEF_HONOR_AFFINITY    2u   /* PTS: nodeAffinityPolicy Honor (default) */
+#define KSIM_USEF_HONOR_TAINTS      4u   /* PTS: nodeTaintsPolicy Honor (default Ignore) */
+#define KSIM_USEF_HOSTNAME          8u   /* PTS: topologyKey == kubernetes.io/hostname */
+
+typedef struct ksim_topo_use {
+  int32_t  cls;                     /* count class; -1 = counts no pod */
+  int32_t  arg;                     /* PTS: maxSkew; IPA_SCORE: signed weight */
+  uint16_t col;                     /* topology key label column, KSIM_COL_NONE if no node has it */
+  uint8_t  kind;                    /* KSIM_USE_* */
+  uint8_t  flags;                   /* KSIM_USEF_* */
+  int32_t  _pad;
+} ksim_topo_use;                    /* 16 bytes */
+
+typedef struct ksim_class_add {
+  int32_t cls;
+  int32_t count;
+} ksim_class_add;
 
 typedef struct ksim_pod_set {
   int32_t n_pods;
@@ -200,6 +264,10 @@ typedef struct ksim_pod_set {
   const ksim_pod* pods;
   const ksim_label_expr* exprs;
   const ksim_term* terms;
+  int32_t n_uses;
+  int32_t n_adds;
+  const ksim_topo_use* uses;
+  const ksim_class_add* adds;
 } ksim_pod_set;
 
 /* Profile: the converted KubeSchedulerProfile (simulator/scheduler/scheduler.go:199-249,
@@ -260,7 +328,8 @@ typedef struct ksim_handle ksim_handle;
 /* ---- lifecycle ----------------------------------------------------------- */
 int  ksim_abi_version(void);
 /* sizeof() of the ABI structs, for binding-layout checks: which = 0 node_table,
- * 1 vocab, 2 label_expr, 3 term, 4 pod, 5 pod_set, 6 profile, 7 eval_out, 8 batch_stats */
+ * 1 vocab, 2 label_expr, 3 term, 4 pod, 5 pod_set, 6 profile, 7 eval_out, 8 batch_stats,
+ * 9 topo_use, 10 class_add */
 size_t ksim_abi_sizeof(int which);
 int  ksim_create(int device, ksim_handle** out);
 void ksim_destroy(ksim_handle* h);
@@ -273,6 +342,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* nodes, const ksim_vo
 /* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
                         int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods);
+/* Read back the count classes [n_classes][n_nodes] (PodTopologySpread / InterPodAffinity state). */
+int ksim_get_class_count(ksim_handle* h, int32_t* out);
 int ksim_get_next_start(ksim_handle* h, int32_t* next_start);
 int ksim_set_next_start(ksim_handle* h, int32_t next_start);
 /* Pod sequence number used by the tie-break (advances once per cycle). */

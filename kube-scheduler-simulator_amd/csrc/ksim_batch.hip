@@ -256,8 +256,8 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
     if (chosen_out) chosen_out[base + tid] = node;
     atomicAdd(node >= 0 ? &s_sched : &s_unsched, 1);
     if (tid < istar && gj) {                            // bound nodes are distinct: one writer each
-      assume_pod(c, P.pods[base + tid], node, 1);
-      if (node == inode) assume_pod(c, P.pods[base + istar], node, 1);
+      assume_pod(c, P, P.pods[base + tid], node, 1);
+      if (node == inode) assume_pod(c, P, P.pods[base + istar], node, 1);
     }
   }
   __syncthreads();

@@ -46,6 +46,11 @@ struct DevCluster {
   const int32_t* label_col_offset;
   const int64_t* label_num;
   const uint8_t* label_num_ok;
+  // PodTopologySpread / InterPodAffinity count classes (ksim_engine.h "Count classes")
+  int32_t n_classes, n_topo_log, vmax, _pad2;
+  int32_t* cnt;                  // [n_classes][n], updated by every bind
+  const double* topo_log;        // [n_topo_log] = log(size + 2), host-computed
+  const int32_t* col_nvals;      // [n_label_cols] value ids per column (domain table sizes)
 };
 
 struct DevPods {
@@ -53,7 +58,9 @@ struct DevPods {
   const ksim_label_expr* exprs;
   const ksim_term* terms;
   const int32_t* norm_const;     // [n_pods] batch path: constant sum of weighted normalized scores
-  int32_t n_pods, n_exprs, n_terms, _pad;
+  const ksim_topo_use* uses;
+  const ksim_class_add* adds;
+  int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, _pad[3];
 };
 
 // Scheduler state that survives across cycles (sched.nextStartNodeIndex,
@@ -72,7 +79,19 @@ struct DevState {
   // batch path: batches ended early because a pod's best node was one bound
   // earlier in the batch (its guess was not its exact choice)
   int64_t cuts;
+  // per-pod topology flags of the current cycle (kTopo*), reset by k_finalize
+  uint32_t topo_flags;
+  int32_t _pad;
 };
+
+// DevState.topo_flags
+constexpr uint32_t kTopoAffinityNonEmpty = 1u;   // len(state.affinityCounts) > 0
+constexpr uint32_t kTopoScoreNonEmpty = 2u;      // len(state.topologyScore) > 0
+
+// PTS hard: a domain entry carries its pods in the low bits and one marker per
+// eligible node above them (TpPairToMatchNum has the pair iff a marker is set).
+constexpr int kDomMarkShift = 40;
+constexpr int64_t kDomCountMask = (1ll << kDomMarkShift) - 1;
 
 struct BRow;
 
@@ -90,6 +109,8 @@ struct DevScratch {
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
   uint32_t* done;        // batch path: k_batch_pairs blocks finished (last-block election)
+  int64_t* dom;          // [KSIM_MAX_USES][vmax] topology-pair sums of the current pod (zero between pods)
+  int64_t* min_match;    // [KSIM_MAX_USES] PTS hard: critical-path minimum
 };
 
 // Compat-mode outputs (ksim_eval_out), device copies.
@@ -412,7 +433,16 @@ __device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, c
 }
 
 // frameworkImpl.RunFilterPlugins (stop at first failure)
+struct DevScratch;
+__device__ __forceinline__ uint32_t pts_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                               const ksim_pod& p, int32_t node);
+__device__ __forceinline__ uint32_t ipa_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                               const ksim_pod& p, uint32_t topo_flags, int32_t node);
+__device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                             const ksim_profile& prof, const ksim_pod& p, int32_t node);
+
 __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                             const DevScratch& s, uint32_t topo_flags,
                                              const ksim_pod& p, const NodeRow& r, uint32_t& detail) {
   detail = 0;
   const int32_t node = r.node;
@@ -438,6 +468,16 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (bits) { detail = bits; return (uint8_t)f; }
         break;
       }
+      case KSIM_PL_POD_TOPOLOGY_SPREAD: {
+        const uint32_t why = p.use_count ? pts_filter(c, P, s, p, node) : 0;
+        if (why) { detail = why; return (uint8_t)f; }
+        break;
+      }
+      case KSIM_PL_INTER_POD_AFFINITY: {
+        const uint32_t why = p.use_count ? ipa_filter(c, P, s, p, topo_flags, node) : 0;
+        if (why) { detail = why; return (uint8_t)f; }
+        break;
+      }
       default:
         break;
     }
@@ -445,28 +485,161 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
   return KSIM_PASSED;
 }
 
+// PodTopologySpread's raw score needs the feasible list (k_finalize computes it).
 __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                           const ksim_pod& p, int plugin, const NodeRow& r) {
+                                           const DevScratch& s, const ksim_pod& p, int plugin, const NodeRow& r) {
   switch (plugin) {
     case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(r, prof, p, c.n_scalar);
     case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(r, prof, p, c.n_scalar);
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
-    default: return 0;   // ImageLocality (no images), PTS/IPA without constraints/terms
+    case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(c, P, s, prof, p, r.node) : 0;
+    default: return 0;   // ImageLocality (no images); PodTopologySpread: k_finalize
   }
 }
 
 // Sum of weighted raw scores of the slots without NormalizeScore.
-__device__ __forceinline__ int64_t partial_total(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                        const ksim_pod& p, const NodeRow& r) {
-  int64_t part = 0;
-  for (int k = 0; k < prof.n_score; k++) {
-    const int pl = prof.score[k];
-    if (norm_kind(pl) != kNormNone) continue;
-    const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
-    part += score_plugin_raw(c, P, prof, p, pl, r) * w;
+
+
+// ---- PodTopologySpread / InterPodAffinity -------------
+// Same structure as oracle/ksim_oracle.c: upstream's topology-pair maps are
+// domain tables dom[u][value id of the use's key column] in HBM, filled by
+// k_topo_prefilter (atomics, LDS-staged for small key vocabularies).
+__device__ __forceinline__ uint32_t use_value(const DevCluster& c, const ksim_topo_use& u, int32_t node) {
+  return u.col == KSIM_COL_NONE ? 0u : c.labels[(size_t)u.col * c.n + node];
+}
+__device__ __forceinline__ int64_t class_count(const DevCluster& c, int32_t cls, int32_t node) {
+  return cls < 0 ? 0 : (int64_t)c.cnt[(size_t)cls * c.n + node];
+}
+__device__ __forceinline__ const int64_t* dom_of(const DevCluster& c, const DevScratch& s, int u) {
+  return s.dom + (size_t)u * c.vmax;
+}
+
+// FindMatchingUntoleratedTaint straight from the taint columns (no NodeRow).
+__device__ __forceinline__ bool node_has_untolerated_taint(const DevCluster& c, const ksim_pod& p, int32_t node) {
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) {
+    const uint32_t tid = c.taints[(size_t)k * c.n + node];
+    if (!tid) break;
+    const uint8_t eff = c.taint_effect[tid];
+    if ((eff == KSIM_EFFECT_NO_SCHEDULE || eff == KSIM_EFFECT_NO_EXECUTE) && !bit_set(p.tol_filter, tid)) return true;
   }
-  return part;
+  return false;
+}
+
+// topologySpreadConstraint.matchNodeInclusionPolicies
+__device__ __forceinline__ bool match_node_inclusion(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                     const ksim_topo_use& u, int32_t node) {
+  if ((u.flags & KSIM_USEF_HONOR_AFFINITY) && !required_node_affinity_match(c, P, p, node)) return false;
+  if ((u.flags & KSIM_USEF_HONOR_TAINTS) && node_has_untolerated_taint(c, p, node)) return false;
+  return true;
+}
+
+// nodeLabelsMatchSpreadConstraints over the pod's uses of one kind
+__device__ __forceinline__ bool node_has_all_keys(const DevCluster& c, const DevPods& P, const ksim_pod& p, int kind,
+                                                  int32_t node) {
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind == kind && use_value(c, u, node) == 0) return false;
+  }
+  return true;
+}
+
+// podtopologyspread Filter -> 0 or KSIM_PTS_*
+__device__ __forceinline__ uint32_t pts_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                               const ksim_pod& p, int32_t node) {
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_PTS_HARD) continue;
+    const uint32_t v = use_value(c, u, node);
+    if (v == 0) return KSIM_PTS_MISSING_LABEL;
+    const int64_t self = (u.flags & KSIM_USEF_SELF_MATCH) ? 1 : 0;
+    const int64_t match = dom_of(c, s, i)[v] & kDomCountMask;     // absent pair: 0
+    if (match + self - s.min_match[i] > (int64_t)u.arg) return KSIM_PTS_SKEW;
+  }
+  return 0;
+}
+
+// interpodaffinity Filter -> 0 or KSIM_IPA_*
+__device__ __forceinline__ uint32_t ipa_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                               const ksim_pod& p, uint32_t topo_flags, int32_t node) {
+  bool pods_exist = true, any_aff = false;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_IPA_AFFINITY) continue;
+    any_aff = true;
+    const uint32_t v = use_value(c, u, node);
+    if (v == 0) return KSIM_IPA_AFFINITY;
+    if (dom_of(c, s, i)[v] <= 0) pods_exist = false;
+  }
+  if (any_aff && !pods_exist &&
+      !(!(topo_flags & kTopoAffinityNonEmpty) && (p.topo_flags & KSIM_POD_IPA_SELF_AFFINITY)))
+    return KSIM_IPA_AFFINITY;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_IPA_ANTI) continue;
+    const uint32_t v = use_value(c, u, node);
+    if (v != 0 && dom_of(c, s, i)[v] > 0) return KSIM_IPA_ANTI_AFFINITY;
+  }
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_IPA_EXISTING_ANTI) continue;
+    const uint32_t v = use_value(c, u, node);
+    if (v != 0 && dom_of(c, s, i)[v] > 0) return KSIM_IPA_EXISTING_ANTI;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ bool use_has_kind(const DevPods& P, const ksim_pod& p, int k0, int k1 = -1, int k2 = -1) {
+  for (int i = 0; i < p.use_count; i++) {
+    const int k = P.uses[p.use_first + i].kind;
+    if (k == k0 || k == k1 || k == k2) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ int64_t ipa_coef(const ksim_profile& prof, const ksim_topo_use& u) {
+  if (u.kind == KSIM_USE_IPA_SCORE) return u.arg;
+  if (u.kind == KSIM_USE_IPA_SCORE_HARD) return prof.hard_pod_affinity_weight > 0 ? prof.hard_pod_affinity_weight : 0;
+  return 0;
+}
+
+// interpodaffinity Score
+__device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                             const ksim_profile& prof, const ksim_pod& p, int32_t node) {
+  int64_t sc = 0;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    const int64_t coef = ipa_coef(prof, u);
+    if (coef == 0) continue;
+    const uint32_t v = use_value(c, u, node);
+    if (v != 0) sc += coef * dom_of(c, s, i)[v];
+  }
+  return sc;
+}
+
+// podtopologyspread Score before NormalizeScore (weight[i] = topologyNormalizingWeight)
+__device__ __forceinline__ int64_t pts_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                             const ksim_pod& p, const double* weight, int32_t node) {
+  double score = 0;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_PTS_SOFT) continue;
+    const uint32_t v = use_value(c, u, node);
+    if (v == 0) continue;
+    const int64_t cnt = (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node) : dom_of(c, s, i)[v];
+    score = score + ((double)cnt * weight[i] + (double)(u.arg - 1));    // scoreForCount, unfused
+  }
+  return (int64_t)round(score);                                          // math.Round
+}
+
+// NodeInfo.AddPod / RemovePod on the count classes
+__device__ __forceinline__ void apply_adds(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
+                                           int sign) {
+  for (int i = 0; i < p.add_count; i++) {
+    const ksim_class_add a = P.adds[p.add_first + i];
+    c.cnt[(size_t)a.cls * c.n + node] += sign * a.count;
+  }
 }
 
 // ---- batch path: the profile compiled down to what batchable pods need -----
@@ -599,7 +772,9 @@ __device__ __forceinline__ void row_add_pod(NodeRow& r, const ksim_pod& p, int s
   r.num_pods += sign;
 }
 
-__device__ __forceinline__ void assume_pod(const DevCluster& c, const ksim_pod& p, int32_t node, int sign) {
+__device__ __forceinline__ void assume_pod(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
+                                           int sign) {
+  apply_adds(c, P, p, node, sign);
   c.req_cpu[node] += sign * p.req_cpu;
   c.req_mem[node] += sign * p.req_mem;
   c.req_eph[node] += sign * p.req_eph;

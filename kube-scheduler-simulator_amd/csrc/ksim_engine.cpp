@@ -49,8 +49,9 @@ struct ksim_handle {
   // device copy of the uploaded dynamic columns (ksim_reset_cluster)
   struct {
     int64_t *req_cpu, *req_mem, *req_eph, *req_scalar, *nz_cpu, *nz_mem;
-    int32_t* num_pods;
+    int32_t *num_pods, *cnt;
   } init{};
+  std::vector<int32_t> col_nvals;       // host copy (pod validation)
 
   DevScratch sc{};
   DevEvalOut eo{};
@@ -64,11 +65,13 @@ struct ksim_handle {
   int32_t* d_chosen = nullptr;
   std::vector<DevBuf> pod_bufs;
   std::vector<uint8_t> batchable;       // per loaded pod
+  std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
 
-  hipGraphExec_t graph_cycle = nullptr;
+  hipGraphExec_t graph_cycle = nullptr;        // per-pod cycles, pods without topology uses
+  hipGraphExec_t graph_cycle_topo = nullptr;   // per-pod cycles incl. the topology kernels
   hipGraphExec_t graph_batch = nullptr;
 };
 
@@ -115,8 +118,10 @@ int upload(ksim_handle* h, std::vector<DevBuf>& owner, const void* src, size_t b
 
 void drop_graphs(ksim_handle* h) {
   if (h->graph_cycle) (void)hipGraphExecDestroy(h->graph_cycle);
+  if (h->graph_cycle_topo) (void)hipGraphExecDestroy(h->graph_cycle_topo);
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   h->graph_cycle = nullptr;
+  h->graph_cycle_topo = nullptr;
   h->graph_batch = nullptr;
 }
 
@@ -151,6 +156,24 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
     if (!check_expr(p.sel_first + k)) return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad nodeSelector expr");
   if (!check_terms(p.req_term_first, p.req_term_count) || !check_terms(p.pref_term_first, p.pref_term_count))
     return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad affinity term range");
+  const std::string who = "pod " + std::to_string(i) + ": ";
+  if (p.use_count < 0 || p.use_count > KSIM_MAX_USES ||
+      (p.use_count > 0 && (!ps->uses || p.use_first < 0 || p.use_first + p.use_count > ps->n_uses)))
+    return set_err(h, KSIM_E_INVALID, who + "bad topology use range");
+  for (int32_t k = 0; k < p.use_count; k++) {
+    const ksim_topo_use& u = ps->uses[p.use_first + k];
+    if (u.kind > KSIM_USE_IPA_SCORE_HARD) return set_err(h, KSIM_E_INVALID, who + "bad topology use kind");
+    if (u.cls < -1 || u.cls >= c.n_classes) return set_err(h, KSIM_E_INVALID, who + "topology use class out of range");
+    if (u.col != KSIM_COL_NONE && u.col >= c.n_label_cols)
+      return set_err(h, KSIM_E_INVALID, who + "topology key column out of range");
+    if (u.kind == KSIM_USE_PTS_SOFT && c.n_topo_log < c.n + 1)
+      return set_err(h, KSIM_E_INVALID, who + "ScheduleAnyway spread needs topo_log[0..n_nodes]");
+  }
+  if (p.add_count < 0 || (p.add_count > 0 && (!ps->adds || p.add_first < 0 || p.add_first + p.add_count > ps->n_adds)))
+    return set_err(h, KSIM_E_INVALID, who + "bad class add range");
+  for (int32_t k = 0; k < p.add_count; k++)
+    if (ps->adds[p.add_first + k].cls < 0 || ps->adds[p.add_first + k].cls >= c.n_classes)
+      return set_err(h, KSIM_E_INVALID, who + "class add out of range");
   return KSIM_OK;
 }
 
@@ -160,11 +183,14 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
 //   TaintToleration: no PreferNoSchedule taint the pod does not tolerate ->
 //                    all raw 0 -> DefaultNormalizeScore(reverse) = 100
 //   NodeAffinity:    no preferred terms -> raw 0 -> 0
-//   PodTopologySpread: no constraints (this ABI revision) -> 100
-//   InterPodAffinity:  no terms -> topologyScore empty -> 0
+//   PodTopologySpread: no constraints -> 100
+//   InterPodAffinity:  no uses -> topologyScore empty -> 0
+// A pod with topology uses reads the count classes, which binds of earlier
+// pods of a batch change, so it always takes the per-pod path.
 bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
   const ksim_profile& prof = h->prof;
   if (num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, h->dc.n) != h->dc.n) return false;
+  if (p.use_count > 0) return false;
   if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
   int64_t acc = 0;
   for (int k = 0; k < prof.n_score; k++) {
@@ -226,7 +252,7 @@ int read_state(ksim_handle* h, DevState& st) {
   return KSIM_OK;
 }
 
-int capture(ksim_handle* h, bool batch, hipGraphExec_t* out) {
+int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   hipGraph_t g = nullptr;
@@ -234,7 +260,7 @@ int capture(ksim_handle* h, bool batch, hipGraphExec_t* out) {
   if (batch)
     for (int i = 0; i < kGraphBatches; i++) launch_batch(a, h->stream);
   else
-    for (int i = 0; i < kGraphCycles; i++) launch_cycle(a, h->stream, false);
+    for (int i = 0; i < kGraphCycles; i++) launch_cycle(a, h->stream, false, topo);
   hipError_t e = hipStreamEndCapture(h->stream, &g);
   if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
@@ -244,7 +270,7 @@ int capture(ksim_handle* h, bool batch, hipGraphExec_t* out) {
 }
 
 // Run pods [a, b) on one path (all of them share the path).
-int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch) {
+int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   int rc;
   if ((rc = set_run(h, a, b))) return rc;
   // No launch is ever issued past the end of the run (a launch there would
@@ -252,14 +278,15 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch) {
   // then single launches for the remainder.
   LaunchArgs la = make_args(h, h->dp, h->d_chosen);
   if (!batch) {
-    if (!h->graph_cycle && (rc = capture(h, false, &h->graph_cycle))) return rc;
+    hipGraphExec_t& g = topo ? h->graph_cycle_topo : h->graph_cycle;
+    if (!g && (rc = capture(h, false, topo, &g))) return rc;
     int32_t done = a;
-    for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(h->graph_cycle, h->stream));
-    for (; done < b; done++) launch_cycle(la, h->stream, false);
+    for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(g, h->stream));
+    for (; done < b; done++) launch_cycle(la, h->stream, false, topo);
     HIPCHK(h, hipGetLastError());
     return KSIM_OK;
   }
-  if (!h->graph_batch && (rc = capture(h, true, &h->graph_batch))) return rc;
+  if (!h->graph_batch && (rc = capture(h, true, false, &h->graph_batch))) return rc;
   // every batch commits between 1 and kBatchPods pods: a graph of
   // kGraphBatches batches never overshoots while left >= kBatchPods * kGraphBatches,
   // and ceil(left / kBatchPods) single batches never overshoot either
@@ -282,16 +309,18 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch) {
   return KSIM_OK;
 }
 
-// Split [first, first+count) into maximal same-path runs.
+// Split [first, first+count) into maximal same-path runs (batch / per-pod,
+// per-pod runs further by whether a pod carries topology uses).
 template <typename F>
 int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
   int32_t i = first;
   const int32_t end = first + count;
   while (i < end) {
     const bool b = h->batchable[i] != 0;
+    const bool t = h->topo[i] != 0;
     int32_t j = i + 1;
-    while (j < end && (h->batchable[j] != 0) == b) j++;
-    int rc = fn(i, j, b);
+    while (j < end && (h->batchable[j] != 0) == b && (h->topo[j] != 0) == t) j++;
+    int rc = fn(i, j, b, t);
     if (rc) return rc;
     i = j;
   }
@@ -315,6 +344,8 @@ size_t ksim_abi_sizeof(int which) {
     case 6: return sizeof(ksim_profile);
     case 7: return sizeof(ksim_eval_out);
     case 8: return sizeof(ksim_batch_stats);
+    case 9: return sizeof(ksim_topo_use);
+    case 10: return sizeof(ksim_class_add);
     default: return 0;
   }
 }
@@ -412,6 +443,25 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     if (t->taints[i] >= v->n_taints) return set_err(h, KSIM_E_INVALID, "taint id out of vocabulary");
   if (t->n_label_cols > 0 && (!v->label_col_offset || (v->n_label_values > 0 && (!v->label_num || !v->label_num_ok))))
     return set_err(h, KSIM_E_INVALID, "null label vocabulary");
+  // value ids per label column: every label id must index its column's domain
+  // tables (device atomics use it as an address)
+  std::vector<int32_t> col_nvals((size_t)t->n_label_cols, 0);
+  int32_t vmax = 1;
+  for (int k = 0; k < t->n_label_cols; k++) {
+    const int32_t end = k + 1 < t->n_label_cols ? v->label_col_offset[k + 1] : v->n_label_values;
+    col_nvals[k] = end - v->label_col_offset[k];
+    if (v->label_col_offset[k] < 0 || col_nvals[k] < 1 || end > v->n_label_values)
+      return set_err(h, KSIM_E_INVALID, "label_col_offset not increasing within n_label_values");
+    if (col_nvals[k] > KSIM_MAX_NODES + 1) return set_err(h, KSIM_E_INVALID, "label column vocabulary too large");
+    vmax = std::max(vmax, col_nvals[k]);
+    for (int32_t i = 0; i < n; i++)
+      if (t->labels[(size_t)k * n + i] >= (uint32_t)col_nvals[k])
+        return set_err(h, KSIM_E_INVALID, "label value id out of its column's vocabulary");
+  }
+  if (t->n_classes < 0 || t->n_classes > KSIM_MAX_CLASSES || (t->n_classes > 0 && n > 0 && !t->class_count))
+    return set_err(h, KSIM_E_INVALID, "n_classes out of range / null class_count");
+  if (v->n_topo_log < 0 || (v->n_topo_log > 0 && !v->topo_log))
+    return set_err(h, KSIM_E_INVALID, "bad topo_log");
   (void)hipStreamSynchronize(h->stream);
   drop_graphs(h);
   free_bufs(h->cluster_bufs);
@@ -419,9 +469,13 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   free_bufs(h->pod_bufs);
   h->dp = DevPods{};
   h->batchable.clear();
+  h->topo.clear();
   h->has_cluster = false;
 
   DevCluster c{};
+  c.n_classes = t->n_classes;
+  c.n_topo_log = v->n_topo_log;
+  c.vmax = vmax;
   c.n = n;
   c.n_scalar = t->n_scalar;
   c.n_label_cols = t->n_label_cols;
@@ -454,7 +508,11 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   UP(label_col_offset, v->label_col_offset, 4 * (size_t)t->n_label_cols);
   UP(label_num, v->label_num, 8 * (size_t)std::max(v->n_label_values, 0));
   UP(label_num_ok, v->label_num_ok, (size_t)std::max(v->n_label_values, 0));
+  UP(cnt, t->class_count, 4 * N * (size_t)t->n_classes);
+  UP(topo_log, v->topo_log, 8 * (size_t)v->n_topo_log);
+  UP(col_nvals, col_nvals.data(), 4 * col_nvals.size());
 #undef UP
+  h->col_nvals = col_nvals;
   h->dc = c;
   h->taint_effect.assign(v->taint_effect, v->taint_effect + v->n_taints);
   {
@@ -472,6 +530,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     SNAP(nz_cpu, 8 * N);
     SNAP(nz_mem, 8 * N);
     SNAP(num_pods, 4 * N);
+    SNAP(cnt, 4 * N * (size_t)t->n_classes);
 #undef SNAP
   }
 
@@ -496,6 +555,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.chain_end, int32_t*, 4);
   SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.done, uint32_t*, 4);
+  SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
+  SCR(s.min_match, int64_t*, 8 * (size_t)KSIM_MAX_USES);
   SCR(o.scored, uint8_t*, N);
   SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(o.norm, int64_t*, 8 * N * KSIM_MAX_SCORE);
@@ -527,6 +588,15 @@ int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int6
   return KSIM_OK;
 }
 
+int ksim_get_class_count(ksim_handle* h, int32_t* out) {
+  if (!h || !h->has_cluster || !out) return set_err(h, KSIM_E_INVALID, "cluster not set / null out");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->dc.n_classes)
+    HIPCHK(h, hipMemcpy(out, h->dc.cnt, 4 * (size_t)h->dc.n * h->dc.n_classes, hipMemcpyDeviceToHost));
+  return KSIM_OK;
+}
+
 int ksim_get_next_start(ksim_handle* h, int32_t* next_start) {
   if (!h || !next_start) return KSIM_E_INVALID;
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -552,8 +622,13 @@ int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
 
 // Re-based copy of one pod with only the expressions/terms it references.
 static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std::vector<ksim_label_expr>& ex,
-                           std::vector<ksim_term>& tm) {
+                           std::vector<ksim_term>& tm, std::vector<ksim_topo_use>& us,
+                           std::vector<ksim_class_add>& ad) {
   pod = ps->pods[i];
+  us.assign(ps->uses + pod.use_first, ps->uses + pod.use_first + pod.use_count);
+  ad.assign(ps->adds + pod.add_first, ps->adds + pod.add_first + pod.add_count);
+  pod.use_first = 0;
+  pod.add_first = 0;
   int32_t sel0 = (int32_t)ex.size();
   for (int32_t k = 0; k < pod.sel_count; k++) ex.push_back(ps->exprs[pod.sel_first + k]);
   pod.sel_first = sel0;
@@ -572,21 +647,19 @@ static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std
   copy_terms(pod.pref_term_first, pod.pref_term_count);
 }
 
-int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
-  int rc = ensure_ready(h);
-  if (rc) return rc;
-  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
-    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
-  if ((rc = validate_pod(h, ps, pod_index))) return rc;
-  HIPCHK(h, hipSetDevice(h->device));
+// Upload one pod (re-based) as a device pod set of its own.
+static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P) {
   ksim_pod pod;
   std::vector<ksim_label_expr> ex;
   std::vector<ksim_term> tm;
-  single_pod_set(ps, pod_index, pod, ex, tm);
+  std::vector<ksim_topo_use> us;
+  std::vector<ksim_class_add> ad;
+  single_pod_set(ps, pod_index, pod, ex, tm, us, ad);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_bufs(h->pod1_bufs);
-  DevPods P{};
+  P = DevPods{};
   void* p = nullptr;
+  int rc;
   if ((rc = upload(h, h->pod1_bufs, &pod, sizeof(pod), &p))) return rc;
   P.pods = (const ksim_pod*)p;
   if ((rc = upload(h, h->pod1_bufs, ex.data(), ex.size() * sizeof(ksim_label_expr), &p))) return rc;
@@ -595,11 +668,29 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksi
   P.terms = (const ksim_term*)p;
   if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
   P.norm_const = (const int32_t*)p;
+  if ((rc = upload(h, h->pod1_bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
+  P.uses = (const ksim_topo_use*)p;
+  if ((rc = upload(h, h->pod1_bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
+  P.adds = (const ksim_class_add*)p;
   P.n_pods = 1;
   P.n_exprs = (int32_t)ex.size();
   P.n_terms = (int32_t)tm.size();
+  P.n_uses = (int32_t)us.size();
+  P.n_adds = (int32_t)ad.size();
+  return KSIM_OK;
+}
+
+int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
+    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  DevPods P;
+  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
   if ((rc = set_run(h, 0, 1))) return rc;
-  launch_cycle(make_args(h, P, nullptr), h->stream, true);
+  launch_cycle(make_args(h, P, nullptr), h->stream, true, ps->pods[pod_index].use_count > 0);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const size_t N = (size_t)h->dc.n;
@@ -626,10 +717,13 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksi
 static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  if (!ps || pod_index < 0 || pod_index >= ps->n_pods || node < 0 || node >= h->dc.n)
+  if (!ps || !ps->pods || pod_index < 0 || pod_index >= ps->n_pods || node < 0 || node >= h->dc.n)
     return set_err(h, KSIM_E_INVALID, "bad pod / node");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  launch_assume(h->dc, ps->pods[pod_index], node, sign, h->stream);
+  DevPods P;
+  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
+  launch_assume(h->dc, P, 0, node, sign, h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return KSIM_OK;
@@ -658,7 +752,11 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->d_chosen = nullptr;
   std::vector<int32_t> nc((size_t)std::max(ps->n_pods, 1), 0);
   h->batchable.assign((size_t)ps->n_pods, 0);
-  for (int32_t i = 0; i < ps->n_pods; i++) h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
+  h->topo.assign((size_t)ps->n_pods, 0);
+  for (int32_t i = 0; i < ps->n_pods; i++) {
+    h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
+    h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
+  }
   DevPods P{};
   void* p = nullptr;
   if ((rc = upload(h, h->pod_bufs, ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return rc;
@@ -669,6 +767,12 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.terms = (const ksim_term*)p;
   if ((rc = upload(h, h->pod_bufs, nc.data(), 4 * nc.size(), &p))) return rc;
   P.norm_const = (const int32_t*)p;
+  if ((rc = upload(h, h->pod_bufs, ps->uses, sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0), &p))) return rc;
+  P.uses = (const ksim_topo_use*)p;
+  if ((rc = upload(h, h->pod_bufs, ps->adds, sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0), &p))) return rc;
+  P.adds = (const ksim_class_add*)p;
+  P.n_uses = ps->n_uses;
+  P.n_adds = ps->n_adds;
   P.n_pods = ps->n_pods;
   P.n_exprs = ps->n_exprs;
   P.n_terms = ps->n_terms;
@@ -691,9 +795,9 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   HIPCHK(h, hipMemsetAsync(&h->st->cuts, 0, 8, h->stream));
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch) {
+  rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
     if (!batch) perpod += b - a;
-    return run_range(h, a, b, batch);
+    return run_range(h, a, b, batch, topo);
   });
   if (rc) return rc;
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
@@ -736,6 +840,8 @@ int ksim_reset_cluster(ksim_handle* h) {
   HIPCHK(h, hipMemcpyAsync(c.nz_cpu, h->init.nz_cpu, 8 * N, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(c.nz_mem, h->init.nz_mem, 8 * N, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(c.num_pods, h->init.num_pods, 4 * N, hipMemcpyDeviceToDevice, h->stream));
+  if (c.n_classes)
+    HIPCHK(h, hipMemcpyAsync(c.cnt, h->init.cnt, 4 * N * c.n_classes, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->st, 0, sizeof(DevState), h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return KSIM_OK;
@@ -759,7 +865,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
   double sum[kKinds] = {0};
   int64_t n[kKinds] = {0};
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
-  rc = for_each_run(h, first, count, [&](int32_t lo, int32_t hi, bool batch) -> int {
+  rc = for_each_run(h, first, count, [&](int32_t lo, int32_t hi, bool batch, bool topo) -> int {
     int r;
     if ((r = set_run(h, lo, hi))) return r;
     const int per = batch ? kKernelsPerBatch : kKernelsPerCycle;
@@ -774,7 +880,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
         if (batch)
           launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else
-          launch_cycle(a, h->stream, false, &evs[(size_t)i * (per + 1)]);
+          launch_cycle(a, h->stream, false, topo, &evs[(size_t)i * (per + 1)]);
       }
       HIPCHK(h, hipGetLastError());
       DevState st;

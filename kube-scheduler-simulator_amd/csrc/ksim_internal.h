@@ -25,16 +25,18 @@ struct LaunchArgs {
   int32_t* chosen;   // [n_pods] device, may be null
 };
 
-constexpr int kKernelsPerCycle = 2;
+constexpr int kKernelsPerCycle = 4;
 extern const char* const kKernelNames[kKernelsPerCycle];
 constexpr int kKernelsPerBatch = 4;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).
 // evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, hipEvent_t* evs = nullptr);
+// topo: the pod may carry PodTopologySpread / InterPodAffinity uses (adds the
+// two topology kernels; they exit at once for a pod without uses).
+void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
-void launch_assume(const DevCluster& c, const ksim_pod& p, int32_t node, int sign, hipStream_t stream);
+void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream);
 
 }  // namespace ksim

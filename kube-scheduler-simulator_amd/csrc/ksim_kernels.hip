@@ -113,12 +113,41 @@ __device__ void block_scan_i32(int32_t v, int32_t& excl, int32_t& total, int32_t
   total = tot;
 }
 
+// Block-wide min over NW waves (all threads get the result).
+template <int NW>
+__device__ int64_t block_min_i64_nw(int64_t v, int64_t* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_min_i64(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  int64_t r = sh[0];
+#pragma unroll
+  for (int i = 1; i < NW; i++) r = sh[i] < r ? sh[i] : r;
+  return r;
+}
+
+template <int NW>
+__device__ int32_t block_sum_i32_nw(int32_t v, int32_t* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  int32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < NW; i++) r += sh[i];
+  return r;
+}
+
 // ---- normalization ----------------------------------------------------------
 // Extrema a slot needs, merged over the kept feasible list:
 //   DefaultNormalizeScore: maxCount = max(0, max)          (helper/normalize_score.go)
-//   PodTopologySpread:     maxScore = max(0, max), minScore = min
-//   InterPodAffinity:      min / max (only when topologyScore is non-empty)
-__device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int64_t gmax, int64_t gmin) {
+//   PodTopologySpread:     maxScore = max(0, max), minScore = min, IgnoredNodes excluded
+//   InterPodAffinity:      min / max, only when topologyScore is non-empty
+__device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int64_t gmax, int64_t gmin,
+                                                   bool ipa_nonempty) {
   switch (kind) {
     case kNormDefault: {
       int64_t m = gmax > 0 ? gmax : 0;
@@ -132,13 +161,113 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
       int64_t mx = gmax > 0 ? gmax : 0;
       return mx == 0 ? (int64_t)kMaxNodeScore : (int64_t)kMaxNodeScore * (mx + gmin - v) / mx;
     }
-    case kNormIPA:   // topologyScore empty for pods without terms: scores left unchanged
+    case kNormIPA: {
+      if (!ipa_nonempty) return v;
+      const int64_t diff = gmax - gmin;
+      double f = 0;
+      if (diff > 0) f = (double)kMaxNodeScore * ((double)(v - gmin) / (double)diff);
+      return (int64_t)f;
+    }
     default:
       return v;
   }
 }
 
 // ==== A. per-pod path ===========================================================
+constexpr int kLdsDom = 128;   // domain tables of key columns with <= kLdsDom value ids are LDS-staged
+
+// PreFilter of PodTopologySpread / InterPodAffinity plus the domain sums their
+// PreScore needs: one thread per node, adds into the pod's domain tables.
+__global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P, ksim_profile prof,
+                                                        DevState* __restrict__ st, DevScratch s) {
+  __shared__ unsigned long long s_dom[KSIM_MAX_USES][kLdsDom];
+  __shared__ uint32_t s_flags;
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const ksim_pod& p = P.pods[pi];
+  const int nu = p.use_count;
+  if (nu == 0) return;
+  const int tid = threadIdx.x;
+  for (int x = tid; x < nu * kLdsDom; x += blockDim.x) s_dom[x / kLdsDom][x % kLdsDom] = 0;
+  if (tid == 0) s_flags = 0;
+  __syncthreads();
+  const int32_t node = blockIdx.x * blockDim.x + tid;
+  uint32_t flags = 0;
+  if (node < c.n) {
+    const bool all_hard = node_has_all_keys(c, P, p, KSIM_USE_PTS_HARD, node);
+    const bool all_soft = node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      const uint32_t v = use_value(c, u, node);
+      if (v == 0) continue;                        // the node has no pair for this key
+      const int64_t cnt = class_count(c, u.cls, node);
+      int64_t add = 0;
+      switch (u.kind) {
+        case KSIM_USE_PTS_HARD:                     // TpPairToMatchNum[pair] += count (+ presence mark)
+          if (all_hard && match_node_inclusion(c, P, p, u, node)) add = cnt + (1ll << kDomMarkShift);
+          break;
+        case KSIM_USE_PTS_SOFT:                     // TopologyPairToPodCounts (hostname: per node in Score)
+          if (!(u.flags & KSIM_USEF_HOSTNAME) && all_soft && match_node_inclusion(c, P, p, u, node)) add = cnt;
+          break;
+        case KSIM_USE_IPA_AFFINITY:
+          if (cnt > 0) flags |= kTopoAffinityNonEmpty;
+          add = cnt;
+          break;
+        case KSIM_USE_IPA_EXISTING_ANTI:
+        case KSIM_USE_IPA_ANTI:
+          add = cnt;
+          break;
+        default:                                    // IPA score: topologyScore[key][value]
+          if (ipa_coef(prof, u) != 0 && cnt != 0) {
+            flags |= kTopoScoreNonEmpty;
+            add = cnt;
+          }
+          break;
+      }
+      if (add == 0) continue;
+      if (c.col_nvals[u.col] <= kLdsDom)
+        atomicAdd(&s_dom[i][v], (unsigned long long)add);
+      else
+        atomicAdd(reinterpret_cast<unsigned long long*>(s.dom + (size_t)i * c.vmax + v), (unsigned long long)add);
+    }
+  }
+  if (flags) atomicOr(&s_flags, flags);
+  __syncthreads();
+  for (int x = tid; x < nu * kLdsDom; x += blockDim.x) {
+    const unsigned long long v = s_dom[x / kLdsDom][x % kLdsDom];
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(s.dom + (size_t)(x / kLdsDom) * c.vmax + x % kLdsDom), v);
+  }
+  if (tid == 0 && s_flags) atomicOr(&st->topo_flags, s_flags);
+}
+
+// TpKeyToCriticalPaths: per hard constraint, the minimum over its present pairs
+// (math.MaxInt32 when no eligible node carries the key).
+__global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, const DevState* __restrict__ st,
+                                                  DevScratch s) {
+  __shared__ int64_t sh[4];
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const ksim_pod& p = P.pods[pi];
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_PTS_HARD) continue;
+    int64_t mn = 2147483647;
+    if (u.col != KSIM_COL_NONE) {
+      const int32_t V = c.col_nvals[u.col];
+      const int64_t* d = s.dom + (size_t)i * c.vmax;
+      for (int32_t v = threadIdx.x; v < V; v += blockDim.x) {
+        const int64_t x = d[v];
+        if ((x >> kDomMarkShift) != 0) {
+          const int64_t m = x & kDomCountMask;
+          mn = m < mn ? m : mn;
+        }
+      }
+    }
+    mn = block_min_i64_nw<4>(mn, sh);
+    if (threadIdx.x == 0) s.min_match[i] = mn;
+  }
+}
+
 template <bool COMPAT>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, ksim_profile prof,
                                                       const DevState* __restrict__ st, DevScratch s) {
@@ -147,16 +276,17 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
   if (node >= c.n) return;
   const ksim_pod& p = P.pods[pi];
+  const uint32_t tf = p.use_count ? st->topo_flags : 0u;
   const NodeRow r = load_row(c, node);
   uint32_t det;
-  const uint8_t res = run_filter_plugins(c, P, prof, p, r, det);
+  const uint8_t res = run_filter_plugins(c, P, prof, s, tf, p, r, det);
   s.fail[node] = res;
   if (COMPAT) s.detail[node] = det;
   if (res != KSIM_PASSED) return;
   int64_t part = 0;
   for (int k = 0; k < prof.n_score; k++) {
     const int pl = prof.score[k];
-    const int64_t v = score_plugin_raw(c, P, prof, p, pl, r);
+    const int64_t v = score_plugin_raw(c, P, prof, s, p, pl, r);
     if (norm_kind(pl) == kNormNone) {
       const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
       part += v * w;
@@ -168,6 +298,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
   s.part[node] = part;
 }
 
+constexpr int kBmWords = (KSIM_MAX_NODES + 1 + 31) / 32;   // value-id bitmap (PTS pair registration)
+
 template <bool COMPAT>
 __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPods P, ksim_profile prof,
                                                             DevState* __restrict__ st, DevScratch s,
@@ -177,6 +309,8 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   __shared__ int32_t sh32[kFinalWaves];
   __shared__ int32_t s_cut, s_single;
   __shared__ int64_t s_gmax[KSIM_MAX_SCORE], s_gmin[KSIM_MAX_SCORE];
+  __shared__ uint32_t s_bm[kBmWords];
+  __shared__ double s_w[KSIM_MAX_USES];
 
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
@@ -187,6 +321,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   const int64_t seq = st->pod_seq;
   const int32_t chunk = (N + kFinalThreads - 1) / kFinalThreads;
   const int32_t lo = min(N, tid * chunk), hi = min(N, lo + chunk);
+  const ksim_pod& p = P.pods[pi];
 
   // Phase A: feasible count per rotated chunk, block scan, locate the (K+1)-th.
   int32_t cnt = 0;
@@ -231,6 +366,45 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     }
   }
 
+  // Phase A2: PodTopologySpread PreScore over the kept list: IgnoredNodes,
+  // pair registration and topologyNormalizingWeight per soft constraint.
+  const bool has_soft = nf > 1 && p.use_count > 0 && use_has_kind(P, p, KSIM_USE_PTS_SOFT);
+  if (has_soft) {
+    int32_t nign = 0;
+    for (int32_t r = lo; r < whi; r++) {
+      int32_t node = start + r;
+      if (node >= N) node -= N;
+      if (s.fail[node] == KSIM_PASSED && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node)) nign++;
+    }
+    nign = block_sum_i32_nw<kFinalWaves>(nign, sh32);
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (u.kind != KSIM_USE_PTS_SOFT) continue;
+      int32_t size;
+      if (u.flags & KSIM_USEF_HOSTNAME) {
+        size = nf - nign;
+      } else {
+        const int32_t words = u.col == KSIM_COL_NONE ? 1 : (c.col_nvals[u.col] + 31) / 32;
+        for (int x = tid; x < words; x += kFinalThreads) s_bm[x] = 0;
+        __syncthreads();
+        for (int32_t r = lo; r < whi; r++) {
+          int32_t node = start + r;
+          if (node >= N) node -= N;
+          if (s.fail[node] != KSIM_PASSED || !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node)) continue;
+          const uint32_t v = use_value(c, u, node);
+          atomicOr(&s_bm[v >> 5], 1u << (v & 31));
+        }
+        __syncthreads();
+        int32_t bits = 0;
+        for (int x = tid; x < words; x += kFinalThreads) bits += __popc(s_bm[x]);
+        size = block_sum_i32_nw<kFinalWaves>(bits, sh32);
+      }
+      if (tid == 0) s_w[i] = c.topo_log[size];
+    }
+    __syncthreads();
+  }
+  const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
+
   int32_t chosen = -1;
   if (nf == 1) {
     for (int32_t r = lo; r < whi; r++) {
@@ -241,7 +415,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     __syncthreads();
     chosen = s_single;
   } else if (nf > 1) {
-    // Phase B: NormalizeScore extrema over the kept feasible list.
+    // Phase B: PodTopologySpread raw scores, NormalizeScore extrema over the kept list.
     for (int k = 0; k < S; k++) {
       const int32_t kind = norm_kind(prof.score[k]);
       if (kind == kNormNone) continue;
@@ -250,7 +424,13 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         int32_t node = start + r;
         if (node >= N) node -= N;
         if (s.fail[node] != KSIM_PASSED) continue;
-        const int64_t v = s.raw[(size_t)k * N + node];
+        int64_t v = s.raw[(size_t)k * N + node];
+        if (kind == kNormPTS) {
+          const bool ign = has_soft && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
+          v = (has_soft && !ign) ? pts_score(c, P, s, p, s_w, node) : 0;
+          s.raw[(size_t)k * N + node] = v;
+          if (ign) continue;                       // invalidScore: not in min / max
+        }
         mx = v > mx ? v : mx;
         mn = v < mn ? v : mn;
       }
@@ -271,7 +451,10 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         const int64_t raw = s.raw[(size_t)k * N + node];
         int64_t nv = raw;
         if (kind != kNormNone) {
-          nv = normalize_value(kind, raw, s_gmax[k], s_gmin[k]);
+          if (kind == kNormPTS && has_soft && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node))
+            nv = 0;
+          else
+            nv = normalize_value(kind, raw, s_gmax[k], s_gmin[k], ipa_nonempty);
           const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
           tot += nv * w;
         }
@@ -291,15 +474,30 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     chosen = key_node(best);
   }
 
+  // Restore the all-zero domain tables for the next pod (every entry this
+  // pod touched is the value of some node's key).
+  if (p.use_count) {
+    __syncthreads();
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (u.col == KSIM_COL_NONE || (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME))) continue;
+      int64_t* d = s.dom + (size_t)i * c.vmax;
+      if (c.col_nvals[u.col] <= 4 * kFinalThreads) {
+        for (int32_t v = tid; v < c.col_nvals[u.col]; v += kFinalThreads) d[v] = 0;
+      } else {
+        for (int32_t node = lo; node < hi; node++) d[use_value(c, u, node)] = 0;
+      }
+    }
+  }
+
   // Phase D: assume/bind + scheduler state.
   if (tid == 0) {
-    const ksim_pod& p = P.pods[pi];
     int32_t ns = start + (cut < N ? cut : N);
     ns %= N;
     st->next_start = ns;
     st->evals += evaluated;
     if (chosen >= 0) {
-      assume_pod(c, p, chosen, 1);
+      assume_pod(c, P, p, chosen, 1);
       st->scheduled += 1;
     } else {
       st->unschedulable += 1;
@@ -313,34 +511,40 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     st->k_to_find = K;
     st->next_start_after = ns;
     st->pod_seq = seq + 1;
+    st->topo_flags = 0;
     st->cursor = pi + 1;
   }
 }
 
-__global__ void k_assume(DevCluster c, ksim_pod p, int32_t node, int sign) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) assume_pod(c, p, node, sign);
+__global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int sign) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) assume_pod(c, P, P.pods[pod], node, sign);
 }
 
 // ---- launchers ----------------------------------------------------------------
-const char* const kKernelNames[kKernelsPerCycle] = {"k_filter_score", "k_finalize"};
+const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_min", "k_filter_score",
+                                                    "k_finalize"};
 
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, hipEvent_t* evs) {
+void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
   const int blocks = (a.c.n + 255) / 256;
   if (evs) (void)hipEventRecord(evs[0], stream);
+  if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  if (topo) k_topo_min<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[2], stream);
   if (compat)
     k_filter_score<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   else
     k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  if (evs) (void)hipEventRecord(evs[1], stream);
+  if (evs) (void)hipEventRecord(evs[3], stream);
   if (compat)
     k_finalize<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
   else
     k_finalize<false><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
-  if (evs) (void)hipEventRecord(evs[2], stream);
+  if (evs) (void)hipEventRecord(evs[4], stream);
 }
 
-void launch_assume(const DevCluster& c, const ksim_pod& p, int32_t node, int sign, hipStream_t stream) {
-  k_assume<<<1, 64, 0, stream>>>(c, p, node, sign);
+void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
+  k_assume<<<1, 64, 0, stream>>>(c, P, pod, node, sign);
 }
 
 }  // namespace ksim

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -21,6 +21,9 @@ EXPR_VALS = 6
 MAX_FILTER = 16
 MAX_SCORE = 8
 MAX_RES = 4
+MAX_USES = 16
+MAX_CLASSES = 4096
+COL_NONE = 0xFFFF
 
 OK = 0
 E_INVALID = -1
@@ -81,6 +84,29 @@ POD_HAS_SCALAR = 4
 POD_HAS_HOST_PORTS = 8
 POD_HAS_VOLUMES = 16
 
+# pod topo_flags
+POD_IPA_SELF_AFFINITY = 1
+
+# topology uses (ksim_topo_use.kind)
+USE_PTS_HARD = 0
+USE_PTS_SOFT = 1
+USE_IPA_EXISTING_ANTI = 2
+USE_IPA_AFFINITY = 3
+USE_IPA_ANTI = 4
+USE_IPA_SCORE = 5
+USE_IPA_SCORE_HARD = 6
+USEF_SELF_MATCH = 1
+USEF_HONOR_AFFINITY = 2
+USEF_HONOR_TAINTS = 4
+USEF_HOSTNAME = 8
+
+# PodTopologySpread / InterPodAffinity filter failure details
+PTS_MISSING_LABEL = 1
+PTS_SKEW = 2
+IPA_AFFINITY = 1
+IPA_ANTI_AFFINITY = 2
+IPA_EXISTING_ANTI = 3
+
 OP_IN = 0
 OP_NOT_IN = 1
 OP_EXISTS = 2
@@ -119,7 +145,12 @@ POD_DTYPE = np.dtype(
      ("sel_first", "<i4"), ("sel_count", "<i4"),
      ("req_term_first", "<i4"), ("req_term_count", "<i4"),
      ("pref_term_first", "<i4"), ("pref_term_count", "<i4"),
-     ("_reserved", "<i4", (8,))], align=True)
+     ("use_first", "<i4"), ("use_count", "<i4"), ("add_first", "<i4"), ("add_count", "<i4"),
+     ("topo_flags", "<u4"), ("_reserved", "<i4", (3,))], align=True)
+TOPO_USE_DTYPE = np.dtype(
+    [("cls", "<i4"), ("arg", "<i4"), ("col", "<u2"), ("kind", "u1"), ("flags", "u1"), ("_pad", "<i4")],
+    align=True)
+CLASS_ADD_DTYPE = np.dtype([("cls", "<i4"), ("count", "<i4")], align=True)
 
 
 def _p(arr):
@@ -141,6 +172,8 @@ class NodeTable(ctypes.Structure):
         ("nz_cpu", ctypes.c_void_p), ("nz_mem", ctypes.c_void_p),
         ("num_pods", ctypes.c_void_p), ("flags", ctypes.c_void_p),
         ("taints", ctypes.c_void_p), ("labels", ctypes.c_void_p),
+        ("n_classes", ctypes.c_int32), ("_pad1", ctypes.c_int32),
+        ("class_count", ctypes.c_void_p),
     ]
 
 
@@ -149,6 +182,8 @@ class Vocab(ctypes.Structure):
         ("n_taints", ctypes.c_int32), ("n_label_values", ctypes.c_int32),
         ("taint_effect", ctypes.c_void_p), ("label_col_offset", ctypes.c_void_p),
         ("label_num", ctypes.c_void_p), ("label_num_ok", ctypes.c_void_p),
+        ("n_topo_log", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("topo_log", ctypes.c_void_p),
     ]
 
 
@@ -157,6 +192,8 @@ class PodSet(ctypes.Structure):
         ("n_pods", ctypes.c_int32), ("n_exprs", ctypes.c_int32),
         ("n_terms", ctypes.c_int32), ("_pad", ctypes.c_int32),
         ("pods", ctypes.c_void_p), ("exprs", ctypes.c_void_p), ("terms", ctypes.c_void_p),
+        ("n_uses", ctypes.c_int32), ("n_adds", ctypes.c_int32),
+        ("uses", ctypes.c_void_p), ("adds", ctypes.c_void_p),
     ]
 
 
@@ -197,7 +234,7 @@ class BatchStats(ctypes.Structure):
 
 
 STRUCT_ORDER = [NodeTable, Vocab, LABEL_EXPR_DTYPE, TERM_DTYPE, POD_DTYPE, PodSet, Profile,
-                EvalOut, BatchStats]
+                EvalOut, BatchStats, TOPO_USE_DTYPE, CLASS_ADD_DTYPE]
 
 
 def struct_size(s) -> int:

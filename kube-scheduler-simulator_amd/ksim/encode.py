@@ -14,6 +14,7 @@ import numpy as np
 
 from . import abi
 from .model import (Node, Pod, Taint, Toleration, quantity_milli_value, quantity_value)
+from .topology import TopologyError, TopologyIndex, pod_uses, register_pod_classes, topo_log_table
 
 LABEL_HOSTNAME = "kubernetes.io/hostname"
 LABEL_ZONE = "topology.kubernetes.io/zone"
@@ -145,6 +146,22 @@ class EncodedCluster:
     label_values: List[List[str]] = field(default_factory=list)   # per col: [vid] -> value
     taint_vocab: List[Taint] = field(default_factory=list)        # [tid] (tid 0 = None)
     scalar_names: List[str] = field(default_factory=list)
+    # count classes of PodTopologySpread / InterPodAffinity (ksim/topology.py)
+    topo: Optional[TopologyIndex] = None
+    class_count: Optional[np.ndarray] = None          # [C][N] int32
+    topo_log: Optional[np.ndarray] = None             # [N+1] float64
+
+    def __post_init__(self):
+        if self.topo is None:
+            self.topo = TopologyIndex(self.n_nodes)
+        if self.class_count is None:
+            self.class_count = self.topo.class_count_array()
+        if self.topo_log is None:
+            self.topo_log = topo_log_table(self.n_nodes)
+
+    def refresh_classes(self) -> None:
+        """Re-materialise class_count after classes were registered."""
+        self.class_count = self.topo.class_count_array()
 
     @property
     def n_label_cols(self) -> int:
@@ -159,6 +176,8 @@ class EncodedCluster:
                   "req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem",
                   "num_pods", "flags", "taints", "labels"):
             setattr(t, f, abi._p(getattr(self, f)))
+        t.n_classes = int(self.class_count.shape[0])
+        t.class_count = abi._p(self.class_count)
         return t
 
     def vocab(self) -> abi.Vocab:
@@ -169,6 +188,8 @@ class EncodedCluster:
         v.label_col_offset = abi._p(self.label_col_offset)
         v.label_num = abi._p(self.label_num)
         v.label_num_ok = abi._p(self.label_num_ok)
+        v.n_topo_log = int(self.topo_log.size)
+        v.topo_log = abi._p(self.topo_log)
         return v
 
     def label_col(self, key: str) -> int:
@@ -185,7 +206,8 @@ class EncodedCluster:
     def copy_state(self) -> "EncodedCluster":
         import copy
         c = copy.copy(self)
-        for f in ("req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem", "num_pods"):
+        for f in ("req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem", "num_pods",
+                  "class_count"):
             setattr(c, f, getattr(self, f).copy())
         return c
 
@@ -196,6 +218,8 @@ class EncodedPods:
     exprs: np.ndarray                 # LABEL_EXPR_DTYPE
     terms: np.ndarray                 # TERM_DTYPE
     names: List[Tuple[str, str]] = field(default_factory=list)   # (namespace, name)
+    uses: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.TOPO_USE_DTYPE))
+    adds: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.CLASS_ADD_DTYPE))
 
     @property
     def n_pods(self) -> int:
@@ -209,11 +233,15 @@ class EncodedPods:
         s.pods = abi._p(self.pods)
         s.exprs = abi._p(self.exprs)
         s.terms = abi._p(self.terms)
+        s.n_uses = int(self.uses.size)
+        s.n_adds = int(self.adds.size)
+        s.uses = abi._p(self.uses)
+        s.adds = abi._p(self.adds)
         return s
 
     def subset(self, first: int, count: int) -> "EncodedPods":
         return EncodedPods(self.pods[first:first + count].copy(), self.exprs, self.terms,
-                           self.names[first:first + count])
+                           self.names[first:first + count], self.uses, self.adds)
 
 
 # ---- cluster encoder --------------------------------------------------------
@@ -229,10 +257,13 @@ def _parse_int64(s: str) -> Optional[int]:
 
 
 def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
-                   extra_scalar: Sequence[str] = ()) -> Tuple[EncodedCluster, List[int]]:
+                   extra_scalar: Sequence[str] = (),
+                   namespaces: Optional[Dict[str, Dict[str, str]]] = None) -> Tuple[EncodedCluster, List[int]]:
     """Encode nodes in nodeTree order.  Returns (cluster, order) where
     order[position] = index into ``nodes``.  ``bound_pods`` (spec.nodeName set)
-    are added to their node's aggregates like NodeInfo.AddPod."""
+    are added to their node's aggregates like NodeInfo.AddPod (and to the
+    PodTopologySpread / InterPodAffinity count classes).  ``namespaces`` maps
+    namespace name -> labels (for namespaceSelector terms)."""
     order = node_tree_order([zone_key(n.labels) for n in nodes])
     ns = [nodes[i] for i in order]
     N = len(ns)
@@ -315,10 +346,15 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
         node_names=[n.name for n in ns], label_keys=keys, label_values=values,
         taint_vocab=tvocab, scalar_names=scalar,
     )
+    c.topo = TopologyIndex(N, namespaces)
     pos_of = {name: i for i, name in enumerate(c.node_names)}
+    for p in bound_pods:
+        if p.node_name in pos_of:
+            c.topo.carried_terms(p)          # classes of every carried term exist first
     for p in bound_pods:
         if p.node_name not in pos_of:
             continue
+        c.topo.add_bound(p, pos_of[p.node_name])
         i = pos_of[p.node_name]
         r = pod_requests(p)
         nz = pod_nonzero_requests(p)
@@ -330,6 +366,7 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
         c.nz_cpu[i] += nz[0]
         c.nz_mem[i] += nz[1]
         c.num_pods[i] += 1
+    c.refresh_classes()
     return c, order
 
 
@@ -418,6 +455,14 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
     b = _PodBuilder(cluster)
     arr = np.zeros(len(pods), abi.POD_DTYPE)
     names = []
+    topo = cluster.topo
+    try:
+        for p in pods:                        # pass 1: every class exists before any adds
+            register_pod_classes(topo, p)
+    except TopologyError as e:
+        raise EncodeError(str(e)) from e
+    uses: List[tuple] = []
+    adds: List[Tuple[int, int]] = []
     for i, p in enumerate(pods):
         r = pod_requests(p)
         nz = pod_nonzero_requests(p)
@@ -471,9 +516,27 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         if p.has_volumes:
             flags |= abi.POD_HAS_VOLUMES
         rec["flags"] = flags
+        try:
+            u, tflags = pod_uses(topo, cluster, p)
+        except TopologyError as e:
+            raise EncodeError(str(e)) from e
+        rec["use_first"], rec["use_count"] = len(uses), len(u)
+        uses.extend(u)
+        a = topo.adds(p)
+        rec["add_first"], rec["add_count"] = len(adds), len(a)
+        adds.extend(a)
+        rec["topo_flags"] = tflags
         names.append((p.namespace, p.name))
     exprs = np.array(b.exprs, abi.LABEL_EXPR_DTYPE) if b.exprs else np.zeros(0, abi.LABEL_EXPR_DTYPE)
     terms = np.zeros(len(b.terms), abi.TERM_DTYPE)
     for i, (f, n, w) in enumerate(b.terms):
         terms[i]["first_expr"], terms[i]["n_expr"], terms[i]["weight"] = f, n, w
-    return EncodedPods(arr, exprs, terms, names)
+    uarr = np.zeros(len(uses), abi.TOPO_USE_DTYPE)
+    for i, (cls, arg, col, kind, fl) in enumerate(uses):
+        uarr[i]["cls"], uarr[i]["arg"], uarr[i]["col"], uarr[i]["kind"], uarr[i]["flags"] = cls, arg, col, kind, fl
+    aarr = np.zeros(len(adds), abi.CLASS_ADD_DTYPE)
+    if adds:
+        aarr["cls"] = [x[0] for x in adds]
+        aarr["count"] = [x[1] for x in adds]
+    cluster.refresh_classes()
+    return EncodedPods(arr, exprs, terms, names, uarr, aarr)

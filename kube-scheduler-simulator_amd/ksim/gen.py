@@ -181,3 +181,73 @@ def config5_weights(n: int = 1024, seed: int = SEEDS[5]) -> np.ndarray:
     """1,024 score-weight vectors w in {1..10}^7 (profile Score order)."""
     x = stream(seed, 21, n * 7)
     return (1 + below(x, 10)).reshape(n, 7).astype(np.int32)
+
+
+# ---- config 3: PodTopologySpread + InterPodAffinity heavy ---------------------
+N_APPS = 64
+
+
+def config3_objects(n_nodes: int = 10000, pods_per_node: int = 10, n_incoming: int = 10000,
+                    seed: int = SEEDS[3], zone_anti_every: int = 1000):
+    """nodes in 3 zones (round-robin), ``pods_per_node``
+    existing pods per node, each with app=a<k> (64 values) carrying a required
+    anti-affinity term against a random app (topologyKey hostname; every
+    ``zone_anti_every``-th one instead zone-wide against app + tier=critical)
+    and a preferred affinity term (zone, weight 1..100) to a random app.
+    Incoming pods (app=a<x>, 5 % tier=critical) spread with maxSkew 1 over
+    zones (DoNotSchedule) and maxSkew 2 over hostnames (ScheduleAnyway) on
+    their own app, and prefer (weight 50) not to share a host with it."""
+    from .model import (LabelSelector, PodAffinityTerm, TopologySpreadConstraint, WeightedPodAffinityTerm)
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        cores = [16, 32, 64][r.below(3)]
+        mem = [64, 128, 256][r.below(3)]
+        nodes.append(Node(
+            name=f"node-{i:06d}",
+            labels={"kubernetes.io/hostname": f"node-{i:06d}", "topology.kubernetes.io/zone": f"z{i % 3}"},
+            allocatable={"cpu": str(cores), "memory": f"{mem}Gi", "pods": "110"}))
+    bound = []
+    j = 0
+    for i in range(n_nodes):
+        for _ in range(pods_per_node):
+            app = f"a{r.below(N_APPS)}"
+            cpu = 100 * (1 + r.below(5))
+            mem = 256 * (1 + r.below(8))
+            p = Pod(name=f"existing-{j:07d}", labels={"app": app, "tier": "web"},
+                    containers=[Container({"cpu": f"{cpu}m", "memory": f"{mem}Mi"})],
+                    node_name=nodes[i].name)
+            target = f"a{r.below(N_APPS)}"
+            if zone_anti_every and j % zone_anti_every == zone_anti_every - 1:
+                p.pod_anti_affinity_required = [PodAffinityTerm(
+                    "topology.kubernetes.io/zone", LabelSelector({"app": target, "tier": "critical"}))]
+            else:
+                p.pod_anti_affinity_required = [PodAffinityTerm(
+                    "kubernetes.io/hostname", LabelSelector({"app": target}))]
+            p.pod_affinity_preferred = [WeightedPodAffinityTerm(1 + r.below(100), PodAffinityTerm(
+                "topology.kubernetes.io/zone", LabelSelector({"app": f"a{r.below(N_APPS)}"})))]
+            bound.append(p)
+            j += 1
+    incoming = []
+    for k in range(n_incoming):
+        app = f"a{r.below(N_APPS)}"
+        tier = "critical" if r.chance(5) else "web"
+        cpu = 100 * (1 + r.below(10))
+        mem = 256 * (1 + r.below(16))
+        sel = LabelSelector({"app": app})
+        p = Pod(name=f"pod-{k:07d}", labels={"app": app, "tier": tier},
+                containers=[Container({"cpu": f"{cpu}m", "memory": f"{mem}Mi"})],
+                topology_spread=[
+                    TopologySpreadConstraint(1, "topology.kubernetes.io/zone", "DoNotSchedule", sel),
+                    TopologySpreadConstraint(2, "kubernetes.io/hostname", "ScheduleAnyway", sel)],
+                pod_anti_affinity_preferred=[WeightedPodAffinityTerm(50, PodAffinityTerm(
+                    "kubernetes.io/hostname", LabelSelector({"app": app})))])
+        incoming.append(p)
+    return nodes, bound, incoming
+
+
+def config3(n_nodes: int = 10000, pods_per_node: int = 10, n_incoming: int = 10000, seed: int = SEEDS[3],
+            zone_anti_every: int = 1000):
+    nodes, bound, incoming = config3_objects(n_nodes, pods_per_node, n_incoming, seed, zone_anti_every)
+    cluster, _ = encode_cluster(nodes, bound)
+    return cluster, encode_pods(cluster, incoming)

@@ -96,6 +96,84 @@ class PreferredTerm:
 
 
 @dataclass
+class LabelSelector:
+    """metav1.LabelSelector.  A pod-side field holding ``None`` is a nil
+    selector (labels.Nothing() after LabelSelectorAsSelector); a LabelSelector
+    with no requirements is labels.Everything()."""
+    match_labels: Dict[str, str] = field(default_factory=dict)
+    match_expressions: List[Requirement] = field(default_factory=list)
+
+    def empty(self) -> bool:
+        return not self.match_labels and not self.match_expressions
+
+    def matches(self, labels: Dict[str, str]) -> bool:
+        """labels.Selector.Matches of LabelSelectorAsSelector(self).  Invalid
+        requirements (an operator this model does not know, or In/NotIn
+        without values) make the selector match nothing (the conversion errs
+        and callers treat the error as a non-match)."""
+        for k, v in self.match_labels.items():
+            if labels.get(k) != v:
+                return False
+        for r in self.match_expressions:
+            has = r.key in labels
+            if r.operator == "In":
+                if not r.values or not has or labels[r.key] not in r.values:
+                    return False
+            elif r.operator == "NotIn":
+                if not r.values:
+                    return False
+                if has and labels[r.key] in r.values:
+                    return False
+            elif r.operator == "Exists":
+                if r.values or not has:
+                    return False
+            elif r.operator == "DoesNotExist":
+                if r.values or has:
+                    return False
+            else:
+                return False
+        return True
+
+    def key(self):
+        """Canonical, hashable form (requirement order does not change the
+        selector: labels.Requirements are sorted by key)."""
+        return (tuple(sorted(self.match_labels.items())),
+                tuple(sorted((r.key, r.operator, tuple(sorted(r.values))) for r in self.match_expressions)))
+
+
+def selector_matches(sel: "Optional[LabelSelector]", labels: Dict[str, str]) -> bool:
+    """LabelSelectorAsSelector(sel).Matches(labels): nil -> Nothing."""
+    return sel is not None and sel.matches(labels)
+
+
+@dataclass
+class TopologySpreadConstraint:
+    """v1.TopologySpreadConstraint (fields read by [upstream] podtopologyspread)."""
+    max_skew: int
+    topology_key: str
+    when_unsatisfiable: str = "DoNotSchedule"      # or ScheduleAnyway
+    label_selector: Optional[LabelSelector] = None
+    min_domains: Optional[int] = None
+    node_affinity_policy: Optional[str] = None     # nil -> Honor
+    node_taints_policy: Optional[str] = None       # nil -> Ignore
+
+
+@dataclass
+class PodAffinityTerm:
+    """v1.PodAffinityTerm."""
+    topology_key: str
+    label_selector: Optional[LabelSelector] = None
+    namespaces: List[str] = field(default_factory=list)
+    namespace_selector: Optional[LabelSelector] = None
+
+
+@dataclass
+class WeightedPodAffinityTerm:
+    weight: int
+    term: PodAffinityTerm
+
+
+@dataclass
 class Container:
     requests: Dict[str, str] = field(default_factory=dict)
     host_ports: List[int] = field(default_factory=list)
@@ -125,6 +203,16 @@ class Pod:
     node_name: str = ""
     has_volumes: bool = False
     priority: int = 0
+    topology_spread: List[TopologySpreadConstraint] = field(default_factory=list)
+    pod_affinity_required: List[PodAffinityTerm] = field(default_factory=list)
+    pod_affinity_preferred: List[WeightedPodAffinityTerm] = field(default_factory=list)
+    pod_anti_affinity_required: List[PodAffinityTerm] = field(default_factory=list)
+    pod_anti_affinity_preferred: List[WeightedPodAffinityTerm] = field(default_factory=list)
+
+    def has_pod_affinity(self) -> bool:
+        """PodInfo: pods with any (anti)affinity term (NodeInfo.PodsWithAffinity)."""
+        return bool(self.pod_affinity_required or self.pod_affinity_preferred or
+                    self.pod_anti_affinity_required or self.pod_anti_affinity_preferred)
 
 
 # ---- v1 dict parsing --------------------------------------------------------
@@ -140,6 +228,29 @@ def _req(d) -> Requirement:
 def _term(d) -> NodeSelectorTerm:
     return NodeSelectorTerm([_req(x) for x in (d.get("matchExpressions") or [])],
                             [_req(x) for x in (d.get("matchFields") or [])])
+
+
+def _selector(d) -> Optional[LabelSelector]:
+    if d is None:
+        return None
+    return LabelSelector(dict(d.get("matchLabels") or {}),
+                         [_req(x) for x in (d.get("matchExpressions") or [])])
+
+
+def _pod_term(d) -> PodAffinityTerm:
+    return PodAffinityTerm(d.get("topologyKey", ""), _selector(d.get("labelSelector")),
+                           list(d.get("namespaces") or []), _selector(d.get("namespaceSelector")))
+
+
+def _weighted(d) -> WeightedPodAffinityTerm:
+    return WeightedPodAffinityTerm(int(d.get("weight", 0)), _pod_term(d.get("podAffinityTerm") or {}))
+
+
+def _spread(d) -> TopologySpreadConstraint:
+    return TopologySpreadConstraint(int(d.get("maxSkew", 1)), d.get("topologyKey", ""),
+                                    d.get("whenUnsatisfiable", "DoNotSchedule"),
+                                    _selector(d.get("labelSelector")), d.get("minDomains"),
+                                    d.get("nodeAffinityPolicy"), d.get("nodeTaintsPolicy"))
 
 
 def node_from_dict(d: dict) -> Node:
@@ -161,7 +272,10 @@ def _container(c) -> Container:
 
 def pod_from_dict(d: dict) -> Pod:
     md, spec = d.get("metadata", {}), d.get("spec", {}) or {}
-    aff = (spec.get("affinity") or {}).get("nodeAffinity") or {}
+    affinity = spec.get("affinity") or {}
+    aff = affinity.get("nodeAffinity") or {}
+    pa = affinity.get("podAffinity") or {}
+    paa = affinity.get("podAntiAffinity") or {}
     req = aff.get("requiredDuringSchedulingIgnoredDuringExecution")
     pref = aff.get("preferredDuringSchedulingIgnoredDuringExecution") or []
     return Pod(
@@ -179,4 +293,11 @@ def pod_from_dict(d: dict) -> Pod:
         node_name=spec.get("nodeName", "") or "",
         has_volumes=any(any(k in v for k in _VOLUME_SOURCES) for v in (spec.get("volumes") or [])),
         priority=int(spec.get("priority") or 0),
+        topology_spread=[_spread(c) for c in (spec.get("topologySpreadConstraints") or [])],
+        pod_affinity_required=[_pod_term(t) for t in (pa.get("requiredDuringSchedulingIgnoredDuringExecution") or [])],
+        pod_affinity_preferred=[_weighted(t) for t in (pa.get("preferredDuringSchedulingIgnoredDuringExecution") or [])],
+        pod_anti_affinity_required=[_pod_term(t) for t in
+                                    (paa.get("requiredDuringSchedulingIgnoredDuringExecution") or [])],
+        pod_anti_affinity_preferred=[_weighted(t) for t in
+                                     (paa.get("preferredDuringSchedulingIgnoredDuringExecution") or [])],
     )

@@ -1,0 +1,329 @@
+"""Host compiler for PodTopologySpread and InterPodAffinity.
+
+Upstream evaluates label selectors and affinity terms against every existing
+pod in PreFilter / PreScore ([upstream] podtopologyspread/filtering.go
+calPreFilterState, scoring.go PreScore; interpodaffinity/filtering.go
+getExistingAntiAffinityCounts / getIncomingAffinityAntiAffinityCounts,
+scoring.go processExistingPod).  All of that string work depends only on the
+pods' namespaces and labels, never on where pods are bound, so the host does
+it once and the device keeps integer COUNT CLASSES:
+
+  cnt[c][node] = sum over pods bound to node of mult(pod, c)
+
+* selector class  — a pod matcher (namespace predicate + label selector);
+                    mult = 1 if the pod matches.  Used by the incoming pod's
+                    spread constraints and (anti)affinity terms.
+* carried class   — (kind, matcher, topology key) of a term some pod CARRIES
+                    (required anti-affinity, required affinity, preferred
+                    affinity / anti-affinity); mult = number of such terms
+                    (required) or the sum of their weights (preferred).  Used
+                    when the incoming pod matches the carried term.
+
+Every plugin quantity is then a domain sum of one class over the nodes sharing
+the node's value of a topology key, which the engine computes on the device:
+  PTS  TpPairToMatchNum[(k, v)]          = sum over eligible nodes with k=v of cnt[sel]
+  IPA  existingAntiAffinityCounts[(k,v)] = sum over nodes with k=v of cnt[carried anti]
+       affinityCounts / antiAffinityCounts, topologyScore[k][v] likewise.
+A pod's "uses" (ksim_topo_use) list which class / key / role it needs; its
+"adds" (ksim_class_add) are what its bind contributes to cnt (NodeInfo.AddPod).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .model import LabelSelector, Pod, PodAffinityTerm
+
+LABEL_HOSTNAME = "kubernetes.io/hostname"
+
+# carried-term kinds
+CARRY_REQ_ANTI = "req_anti"
+CARRY_REQ_AFF = "req_aff"
+CARRY_PREF_AFF = "pref_aff"
+CARRY_PREF_ANTI = "pref_anti"
+
+
+class TopologyError(ValueError):
+    pass
+
+
+@dataclass(frozen=True)
+class Matcher:
+    """framework.AffinityTerm.Matches / countPodsMatchSelector as a predicate
+    over (namespace, labels).  ``selector`` is LabelSelector.key() or None
+    (nil selector -> labels.Nothing())."""
+    namespaces: frozenset
+    all_namespaces: bool
+    selector: Optional[tuple]
+
+
+def _validate_selector(sel: Optional[LabelSelector]) -> None:
+    """LabelSelectorAsSelector errors make upstream PreFilter fail the cycle;
+    the engine rejects such pods instead of diverging silently."""
+    if sel is None:
+        return
+    for r in sel.match_expressions:
+        if r.operator in ("In", "NotIn") and not r.values:
+            raise TopologyError(f"selector requirement {r.key} {r.operator} needs values")
+        if r.operator in ("Exists", "DoesNotExist") and r.values:
+            raise TopologyError(f"selector requirement {r.key} {r.operator} must not have values")
+        if r.operator not in ("In", "NotIn", "Exists", "DoesNotExist"):
+            raise TopologyError(f"selector operator {r.operator} not supported")
+
+
+class TopologyIndex:
+    """Count classes of one cluster (kept on EncodedCluster.topo)."""
+
+    def __init__(self, n_nodes: int, namespaces: Optional[Dict[str, Dict[str, str]]] = None):
+        self.n = n_nodes
+        self.ns_labels: Dict[str, Dict[str, str]] = dict(namespaces or {})
+        self.selectors: Dict[tuple, LabelSelector] = {}
+        self.keys: List[tuple] = []                 # class id -> identity
+        self.ids: Dict[tuple, int] = {}
+        self.counts: List[np.ndarray] = []          # class id -> int32[N]
+        # bound pods grouped by (namespace, labels) signature: sig -> node positions
+        self.bound_sigs: Dict[tuple, List[int]] = {}
+        self.sig_pods: Dict[tuple, Pod] = {}
+        self._match_cache: Dict[Tuple[tuple, Matcher], bool] = {}
+        self.sel_ids: List[int] = []                # selector classes (subset of ids)
+        self.carry_ids: List[int] = []              # carried classes
+        self._carry_uses: Dict[tuple, List[tuple]] = {}   # signature -> carried uses (valid for a class count)
+
+    # ---- matchers ------------------------------------------------------------
+    def _sel_key(self, sel: Optional[LabelSelector]) -> Optional[tuple]:
+        if sel is None:
+            return None
+        _validate_selector(sel)
+        k = sel.key()
+        self.selectors.setdefault(k, sel)
+        return k
+
+    def note_namespace(self, ns: str) -> None:
+        self.ns_labels.setdefault(ns, {})
+
+    def term_matcher(self, owner: Pod, t: PodAffinityTerm) -> Matcher:
+        """newAffinityTerm + getNamespacesFromPodAffinityTerm, with a non-empty
+        namespaceSelector resolved over the known namespaces
+        (mergeAffinityTermNamespacesIfNotEmpty); an empty one ({}) matches every
+        namespace, a nil one none."""
+        names = set(t.namespaces)
+        all_ns = False
+        if not t.namespaces and t.namespace_selector is None:
+            names.add(owner.namespace)
+        if t.namespace_selector is not None:
+            _validate_selector(t.namespace_selector)
+            if t.namespace_selector.empty():
+                all_ns = True
+            else:
+                names.update(ns for ns, lab in self.ns_labels.items() if t.namespace_selector.matches(lab))
+        return Matcher(frozenset(names), all_ns, self._sel_key(t.label_selector))
+
+    def matches(self, m: Matcher, ns: str, labels: Dict[str, str]) -> bool:
+        if not (m.all_namespaces or ns in m.namespaces):
+            return False
+        return m.selector is not None and self.selectors[m.selector].matches(labels)
+
+    def _pod_matches(self, m, pod: Pod) -> bool:
+        sig = (pod.namespace, tuple(sorted(pod.labels.items())))
+        return self._sig_matches(m, sig, pod)
+
+    def _sig_matches(self, m, sig, pod: Pod) -> bool:
+        ck = (sig, m)
+        v = self._match_cache.get(ck)
+        if v is None:
+            if isinstance(m, tuple) and m and m[0] == "all":
+                v = all(self.matches(x, pod.namespace, pod.labels) for x in m[1])
+            else:
+                v = self.matches(m, pod.namespace, pod.labels)
+            self._match_cache[ck] = v
+        return v
+
+    # ---- classes -------------------------------------------------------------
+    def _new_class(self, key: tuple, counts: np.ndarray) -> int:
+        cid = len(self.keys)
+        if cid >= abi.MAX_CLASSES:
+            raise TopologyError("too many count classes")
+        self.keys.append(key)
+        self.ids[key] = cid
+        self.counts.append(counts)
+        (self.sel_ids if key[0] == "sel" else self.carry_ids).append(cid)
+        return cid
+
+    def selector_class(self, m) -> int:
+        """Class of pods matching ``m`` (a Matcher, or ("all", (Matcher, ...))
+        for podMatchesAllAffinityTerms).  Counts come from the bound pods."""
+        key = ("sel", m)
+        cid = self.ids.get(key)
+        if cid is not None:
+            return cid
+        cnt = np.zeros(self.n, np.int32)
+        for sig, positions in self.bound_sigs.items():
+            if self._sig_matches(m, sig, self.sig_pods[sig]):
+                np.add.at(cnt, np.asarray(positions, np.int64), 1)
+        return self._new_class(key, cnt)
+
+    def carried_class(self, kind: str, m: Matcher, topology_key: str) -> int:
+        key = ("carry", kind, m, topology_key)
+        cid = self.ids.get(key)
+        if cid is None:
+            cid = self._new_class(key, np.zeros(self.n, np.int32))
+        return cid
+
+    def carried_terms(self, pod: Pod) -> List[Tuple[int, int]]:
+        """(class, multiplicity) of the terms ``pod`` carries once bound."""
+        out: Dict[int, int] = {}
+        for t in pod.pod_anti_affinity_required:
+            c = self.carried_class(CARRY_REQ_ANTI, self.term_matcher(pod, t), t.topology_key)
+            out[c] = out.get(c, 0) + 1
+        for t in pod.pod_affinity_required:
+            c = self.carried_class(CARRY_REQ_AFF, self.term_matcher(pod, t), t.topology_key)
+            out[c] = out.get(c, 0) + 1
+        for w in pod.pod_affinity_preferred:
+            c = self.carried_class(CARRY_PREF_AFF, self.term_matcher(pod, w.term), w.term.topology_key)
+            out[c] = out.get(c, 0) + w.weight
+        for w in pod.pod_anti_affinity_preferred:
+            c = self.carried_class(CARRY_PREF_ANTI, self.term_matcher(pod, w.term), w.term.topology_key)
+            out[c] = out.get(c, 0) + w.weight
+        return sorted(out.items())
+
+    def add_bound(self, pod: Pod, pos: int) -> None:
+        """An existing pod bound at node position ``pos`` (NodeInfo.AddPod)."""
+        self.note_namespace(pod.namespace)
+        for c, mult in self.carried_terms(pod):
+            self.counts[c][pos] += mult
+        for cid in self.sel_ids:
+            if self._pod_matches(self.keys[cid][1], pod):
+                self.counts[cid][pos] += 1
+        sig = (pod.namespace, tuple(sorted(pod.labels.items())))
+        self.bound_sigs.setdefault(sig, []).append(pos)
+        self.sig_pods.setdefault(sig, pod)
+
+    def adds(self, pod: Pod) -> List[Tuple[int, int]]:
+        """(class, count) this pod contributes when bound: its carried terms
+        plus every selector class it matches."""
+        out = dict(self.carried_terms(pod))
+        for cid in self.sel_ids:
+            if self._pod_matches(self.keys[cid][1], pod):
+                out[cid] = out.get(cid, 0) + 1
+        return sorted(out.items())
+
+    def carried_uses(self, cluster, pod: Pod) -> List[tuple]:
+        """Uses of the carried classes whose term matches ``pod`` (cached per
+        (namespace, labels) signature and class count)."""
+        ck = (pod.namespace, tuple(sorted(pod.labels.items())), len(self.carry_ids))
+        hit = self._carry_uses.get(ck)
+        if hit is not None:
+            return hit
+        out = []
+        for cid in self.carry_ids:
+            _, kind, m, tk = self.keys[cid]
+            if not self.matches(m, pod.namespace, pod.labels):
+                continue
+            col = _col(cluster, tk)
+            if kind == CARRY_REQ_ANTI:
+                out.append(_use(abi.USE_IPA_EXISTING_ANTI, cid, col))
+            elif kind == CARRY_REQ_AFF:
+                out.append(_use(abi.USE_IPA_SCORE_HARD, cid, col, 1))
+            elif kind == CARRY_PREF_AFF:
+                out.append(_use(abi.USE_IPA_SCORE, cid, col, 1))
+            else:
+                out.append(_use(abi.USE_IPA_SCORE, cid, col, -1))
+        self._carry_uses[ck] = out
+        return out
+
+    def class_count_array(self) -> np.ndarray:
+        if not self.counts:
+            return np.zeros((0, self.n), np.int32)
+        return np.stack(self.counts).astype(np.int32)
+
+
+# ---- per-pod compilation -------------------------------------------------------
+def _col(cluster, key: str) -> int:
+    c = cluster.label_col(key)
+    return abi.COL_NONE if c < 0 else c
+
+
+def register_pod_classes(topo: TopologyIndex, pod: Pod) -> None:
+    """Pass 1: every class the pod will use or carry exists before any pod's
+    adds are computed (so a later queue pod's selector counts earlier ones)."""
+    topo.note_namespace(pod.namespace)
+    topo.carried_terms(pod)
+    for c in pod.topology_spread:
+        _validate_selector(c.label_selector)
+        if c.label_selector is not None and not c.label_selector.empty():
+            topo.selector_class(Matcher(frozenset([pod.namespace]), False, topo._sel_key(c.label_selector)))
+    if pod.pod_affinity_required:
+        topo.selector_class(("all", tuple(topo.term_matcher(pod, t) for t in pod.pod_affinity_required)))
+    for t in pod.pod_anti_affinity_required:
+        topo.selector_class(topo.term_matcher(pod, t))
+    for w in pod.pod_affinity_preferred + pod.pod_anti_affinity_preferred:
+        topo.selector_class(topo.term_matcher(pod, w.term))
+
+
+def _use(kind, cls, col, arg=0, flags=0):
+    return (cls, arg, col, kind, flags)
+
+
+def pod_uses(topo: TopologyIndex, cluster, pod: Pod) -> Tuple[List[tuple], int]:
+    """Pass 2: the pod's uses (ksim_topo_use rows) and topo flags."""
+    uses: List[tuple] = []
+    flags = 0
+    # --- PodTopologySpread: filterTopologySpreadConstraints (hard, then soft) ---
+    seen = {"DoNotSchedule": set(), "ScheduleAnyway": set()}
+    for c in pod.topology_spread:
+        if c.when_unsatisfiable not in seen:
+            raise TopologyError(f"whenUnsatisfiable {c.when_unsatisfiable} not supported")
+        if c.topology_key in seen[c.when_unsatisfiable]:
+            raise TopologyError("duplicate topologyKey/whenUnsatisfiable (rejected by API validation)")
+        seen[c.when_unsatisfiable].add(c.topology_key)
+        if c.max_skew < 1:
+            raise TopologyError("maxSkew must be >= 1")
+        sel = c.label_selector
+        cls = -1
+        if sel is not None and not sel.empty():       # countPodsMatchSelector: Empty() counts 0
+            cls = topo.selector_class(Matcher(frozenset([pod.namespace]), False, topo._sel_key(sel)))
+        f = 0
+        if sel is not None and sel.matches(pod.labels):   # c.Selector.Matches(podLabelSet)
+            f |= abi.USEF_SELF_MATCH
+        if (c.node_affinity_policy or "Honor") == "Honor":
+            f |= abi.USEF_HONOR_AFFINITY
+        if (c.node_taints_policy or "Ignore") == "Honor":
+            f |= abi.USEF_HONOR_TAINTS
+        if c.topology_key == LABEL_HOSTNAME:
+            f |= abi.USEF_HOSTNAME
+        kind = abi.USE_PTS_HARD if c.when_unsatisfiable == "DoNotSchedule" else abi.USE_PTS_SOFT
+        uses.append(_use(kind, cls, _col(cluster, c.topology_key), c.max_skew, f))
+    # --- InterPodAffinity filter: incoming required affinity (all terms) ---
+    if pod.pod_affinity_required:
+        ms = tuple(topo.term_matcher(pod, t) for t in pod.pod_affinity_required)
+        cls = topo.selector_class(("all", ms))
+        for t in pod.pod_affinity_required:
+            uses.append(_use(abi.USE_IPA_AFFINITY, cls, _col(cluster, t.topology_key)))
+        if all(topo.matches(m, pod.namespace, pod.labels) for m in ms):
+            flags |= abi.POD_IPA_SELF_AFFINITY
+    for t in pod.pod_anti_affinity_required:
+        cls = topo.selector_class(topo.term_matcher(pod, t))
+        uses.append(_use(abi.USE_IPA_ANTI, cls, _col(cluster, t.topology_key)))
+    # --- carried terms of other pods that match this pod ---
+    uses.extend(topo.carried_uses(cluster, pod))
+    # --- incoming preferred (anti)affinity terms (score) ---
+    for w in pod.pod_affinity_preferred:
+        uses.append(_use(abi.USE_IPA_SCORE, topo.selector_class(topo.term_matcher(pod, w.term)),
+                         _col(cluster, w.term.topology_key), w.weight))
+    for w in pod.pod_anti_affinity_preferred:
+        uses.append(_use(abi.USE_IPA_SCORE, topo.selector_class(topo.term_matcher(pod, w.term)),
+                         _col(cluster, w.term.topology_key), -w.weight))
+    if len(uses) > abi.MAX_USES:
+        raise TopologyError(f"pod {pod.name}: {len(uses)} topology uses > {abi.MAX_USES}")
+    return uses, flags
+
+
+def topo_log_table(n_nodes: int) -> np.ndarray:
+    """topologyNormalizingWeight(size) = math.Log(float64(size + 2)) for
+    size = 0..n_nodes, computed on the host (the simulator's Go host would
+    use math.Log) so the device never evaluates log."""
+    import math
+    return np.array([math.log(float(s + 2)) for s in range(n_nodes + 1)], np.float64)

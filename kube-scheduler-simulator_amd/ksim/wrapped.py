@@ -31,6 +31,11 @@ HAS_NORMALIZE = {"TaintToleration", "NodeAffinity", "PodTopologySpread", "InterP
 ERR_UNSCHEDULABLE = "node(s) were unschedulable"                        # nodeunschedulable
 ERR_NODE_NAME = "node(s) didn't match the requested node name"          # nodename
 ERR_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"  # nodeaffinity ErrReasonPod
+ERR_PTS = "node(s) didn't match pod topology spread constraints"        # podtopologyspread ErrReasonConstraintsNotMatch
+ERR_PTS_LABEL = ERR_PTS + " (missing required label)"                   # ErrReasonNodeLabelNotMatch
+ERR_IPA = {abi.IPA_AFFINITY: "node(s) didn't match pod affinity rules",
+           abi.IPA_ANTI_AFFINITY: "node(s) didn't match pod anti-affinity rules",
+           abi.IPA_EXISTING_ANTI: "node(s) didn't satisfy existing pods anti-affinity rules"}
 
 
 def filter_message(cluster: EncodedCluster, plugin: str, detail: int) -> str:
@@ -58,6 +63,10 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int) -> str:
             if detail & (abi.FIT_SCALAR0 << k):
                 reasons.append(f"Insufficient {name}")
         return ", ".join(reasons)
+    if plugin == "PodTopologySpread":
+        return ERR_PTS_LABEL if detail == abi.PTS_MISSING_LABEL else ERR_PTS
+    if plugin == "InterPodAffinity":
+        return ERR_IPA[detail]
     return f"{plugin} failed"
 
 

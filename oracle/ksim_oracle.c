@@ -45,6 +45,13 @@ struct ksim_oracle {
   int32_t *label_col_offset;
   int64_t *label_num;
   uint8_t *label_num_ok;
+  /* PodTopologySpread / InterPodAffinity count classes (ksim_engine.h) */
+  int32_t n_classes;
+  int32_t *cnt;         /* [n_classes][n] dynamic */
+  int32_t n_topo_log;
+  double *topo_log;
+  int32_t *col_nvals;   /* value ids per label column */
+  int32_t vmax;
   /* scheduler state */
   int32_t next_start;   /* sched.nextStartNodeIndex */
   int64_t pod_seq;      /* tie-break sequence */
@@ -53,6 +60,9 @@ struct ksim_oracle {
   uint32_t *detail;
   int32_t *flist;
   int64_t *raw;         /* [KSIM_MAX_SCORE][n] */
+  int64_t *dom;         /* [KSIM_MAX_USES][vmax] topology-pair sums */
+  uint8_t *present;     /* [KSIM_MAX_USES][vmax] pair present (PTS) / registered (PTS soft) */
+  uint8_t *ignored;     /* [n] PTS IgnoredNodes */
 };
 
 /* ------------------------------------------------------------------------ */
@@ -97,6 +107,20 @@ ksim_oracle* ksim_oracle_create(const ksim_node_table* t, const ksim_vocab* v,
   o->detail = malloc(4 * n + 4);
   o->flist = malloc(4 * n + 4);
   o->raw = malloc(8 * n * KSIM_MAX_SCORE + 8);
+  o->n_classes = t->n_classes;
+  o->cnt = dupbuf(t->class_count, 4 * n * (size_t)(t->n_classes > 0 ? t->n_classes : 0));
+  o->n_topo_log = v->n_topo_log;
+  o->topo_log = dupbuf(v->topo_log, 8 * (size_t)(v->n_topo_log > 0 ? v->n_topo_log : 0));
+  o->col_nvals = malloc(4 * (size_t)t->n_label_cols + 4);
+  o->vmax = 1;
+  for (int k = 0; k < t->n_label_cols; k++) {
+    int32_t end = (k + 1 < t->n_label_cols) ? v->label_col_offset[k + 1] : v->n_label_values;
+    o->col_nvals[k] = end - v->label_col_offset[k];
+    if (o->col_nvals[k] > o->vmax) o->vmax = o->col_nvals[k];
+  }
+  o->dom = malloc(8 * (size_t)KSIM_MAX_USES * o->vmax);
+  o->present = malloc((size_t)KSIM_MAX_USES * o->vmax);
+  o->ignored = malloc(n + 1);
   return o;
 }
 
@@ -106,7 +130,8 @@ void ksim_oracle_destroy(ksim_oracle* o) {
                 o->req_cpu, o->req_mem, o->req_eph, o->req_scalar, o->nz_cpu, o->nz_mem,
                 o->num_pods, o->flags, o->taints, o->labels, o->taint_effect,
                 o->label_col_offset, o->label_num, o->label_num_ok, o->fail, o->detail,
-                o->flist, o->raw};
+                o->flist, o->raw, o->cnt, o->topo_log, o->col_nvals, o->dom, o->present,
+                o->ignored};
   for (size_t i = 0; i < sizeof(ps) / sizeof(ps[0]); i++) free(ps[i]);
   free(o);
 }
@@ -371,12 +396,241 @@ void ksim_oracle_default_normalize(int64_t max_priority, int reverse, int32_t n,
   }
 }
 
+/* ---- PodTopologySpread / InterPodAffinity (a27-a30) ---------------------- */
+/* The host compiled every selector / term into count classes (ksim_engine.h
+ * "Count classes"); upstream's topology-pair maps become arrays indexed by the
+ * label value id of the use's key column:  pair (key, value) -> dom[u][value]. */
+typedef struct topo_ctx {
+  int n;                                 /* uses of the pod */
+  const ksim_topo_use* u[KSIM_MAX_USES];
+  int64_t min_match[KSIM_MAX_USES];      /* PTS hard: TpKeyToCriticalPaths[key][0].MatchNum */
+  double weight[KSIM_MAX_USES];          /* PTS soft: TopologyNormalizingWeight */
+  int has_hard, has_soft, has_ipa_filter, has_ipa_score;
+  int affinity_counts_empty;             /* len(state.affinityCounts) == 0 */
+  int topology_score_empty;              /* len(state.topologyScore) == 0 */
+} topo_ctx;
+
+static inline int64_t* dom_of(const ksim_oracle* o, int u) { return o->dom + (size_t)u * o->vmax; }
+static inline uint8_t* present_of(const ksim_oracle* o, int u) { return o->present + (size_t)u * o->vmax; }
+
+static inline uint32_t use_value(const ksim_oracle* o, const ksim_topo_use* u, int32_t node) {
+  return u->col == KSIM_COL_NONE ? 0u : node_label(o, u->col, node);   /* 0 = key absent */
+}
+static inline int64_t class_count(const ksim_oracle* o, int32_t cls, int32_t node) {
+  return cls < 0 ? 0 : o->cnt[(size_t)cls * o->n + node];
+}
+
+static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set* ps,
+                                        const ksim_pod* p, int32_t node);
+static uint32_t find_matching_untolerated_taint(const ksim_oracle* o, const ksim_pod* p, int32_t node);
+
+/* topologySpreadConstraint.matchNodeInclusionPolicies */
+static int match_node_inclusion_policies(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
+                                         const ksim_topo_use* u, int32_t node) {
+  if ((u->flags & KSIM_USEF_HONOR_AFFINITY) && !required_node_affinity_match(o, ps, p, node)) return 0;
+  if ((u->flags & KSIM_USEF_HONOR_TAINTS) && find_matching_untolerated_taint(o, p, node)) return 0;
+  return 1;
+}
+
+/* nodeLabelsMatchSpreadConstraints over the uses of one kind */
+static int node_has_all_keys(const ksim_oracle* o, const topo_ctx* t, int kind, int32_t node) {
+  for (int i = 0; i < t->n; i++)
+    if (t->u[i]->kind == kind && use_value(o, t->u[i], node) == 0) return 0;
+  return 1;
+}
+
+/* PreFilter of PodTopologySpread (calPreFilterState) and InterPodAffinity
+ * (getExistingAntiAffinityCounts, getIncomingAffinityAntiAffinityCounts). */
+static void topo_prefilter(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p, topo_ctx* t) {
+  memset(t, 0, sizeof(*t));
+  t->n = p->use_count;
+  for (int i = 0; i < t->n; i++) {
+    t->u[i] = &ps->uses[p->use_first + i];
+    int k = t->u[i]->kind;
+    if (k == KSIM_USE_PTS_HARD) t->has_hard = 1;
+    else if (k == KSIM_USE_PTS_SOFT) t->has_soft = 1;
+    else if (k == KSIM_USE_IPA_EXISTING_ANTI || k == KSIM_USE_IPA_AFFINITY || k == KSIM_USE_IPA_ANTI) t->has_ipa_filter = 1;
+    else t->has_ipa_score = 1;
+    memset(dom_of(o, i), 0, 8 * (size_t)o->vmax);
+    memset(present_of(o, i), 0, (size_t)o->vmax);
+  }
+  t->affinity_counts_empty = 1;
+  for (int32_t node = 0; node < o->n; node++) {
+    int all_hard = t->has_hard ? node_has_all_keys(o, t, KSIM_USE_PTS_HARD, node) : 0;
+    for (int i = 0; i < t->n; i++) {
+      const ksim_topo_use* u = t->u[i];
+      uint32_t v = use_value(o, u, node);
+      switch (u->kind) {
+        case KSIM_USE_PTS_HARD:
+          if (!all_hard || !match_node_inclusion_policies(o, ps, p, u, node)) break;
+          dom_of(o, i)[v] += class_count(o, u->cls, node);      /* TpPairToMatchNum[pair] += count */
+          present_of(o, i)[v] = 1;
+          break;
+        case KSIM_USE_IPA_EXISTING_ANTI:
+        case KSIM_USE_IPA_AFFINITY:
+        case KSIM_USE_IPA_ANTI:
+          if (v == 0) break;                                     /* topologyToMatchedTermCount.update */
+          dom_of(o, i)[v] += class_count(o, u->cls, node);
+          if (u->kind == KSIM_USE_IPA_AFFINITY && class_count(o, u->cls, node) > 0) t->affinity_counts_empty = 0;
+          break;
+        default:
+          break;
+      }
+    }
+  }
+  /* TpKeyToCriticalPaths: the minimum over the key's pairs (math.MaxInt32 if none) */
+  for (int i = 0; i < t->n; i++) {
+    if (t->u[i]->kind != KSIM_USE_PTS_HARD) continue;
+    int64_t mn = 2147483647;
+    for (int32_t v = 0; v < o->vmax; v++)
+      if (present_of(o, i)[v] && dom_of(o, i)[v] < mn) mn = dom_of(o, i)[v];
+    t->min_match[i] = mn;
+  }
+}
+
+/* podtopologyspread Filter -> 0 or KSIM_PTS_* */
+static uint32_t pts_filter(const ksim_oracle* o, const topo_ctx* t, int32_t node) {
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_PTS_HARD) continue;
+    uint32_t v = use_value(o, u, node);
+    if (v == 0) return KSIM_PTS_MISSING_LABEL;
+    int64_t self = (u->flags & KSIM_USEF_SELF_MATCH) ? 1 : 0;
+    int64_t match = present_of(o, i)[v] ? dom_of(o, i)[v] : 0;
+    int64_t skew = match + self - t->min_match[i];
+    if (skew > (int64_t)u->arg) return KSIM_PTS_SKEW;
+  }
+  return 0;
+}
+
+/* interpodaffinity Filter -> 0 or KSIM_IPA_* */
+static uint32_t ipa_filter(const ksim_oracle* o, const ksim_pod* p, const topo_ctx* t, int32_t node) {
+  /* satisfyPodAffinity */
+  int pods_exist = 1, any_aff = 0;
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_IPA_AFFINITY) continue;
+    any_aff = 1;
+    uint32_t v = use_value(o, u, node);
+    if (v == 0) return KSIM_IPA_AFFINITY;            /* all topology labels must exist */
+    if (dom_of(o, i)[v] <= 0) pods_exist = 0;
+  }
+  if (any_aff && !pods_exist &&
+      !(t->affinity_counts_empty && (p->topo_flags & KSIM_POD_IPA_SELF_AFFINITY)))
+    return KSIM_IPA_AFFINITY;
+  /* satisfyPodAntiAffinity */
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_IPA_ANTI) continue;
+    uint32_t v = use_value(o, u, node);
+    if (v != 0 && dom_of(o, i)[v] > 0) return KSIM_IPA_ANTI_AFFINITY;
+  }
+  /* satisfyExistingPodsAntiAffinity */
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_IPA_EXISTING_ANTI) continue;
+    uint32_t v = use_value(o, u, node);
+    if (v != 0 && dom_of(o, i)[v] > 0) return KSIM_IPA_EXISTING_ANTI;
+  }
+  return 0;
+}
+
+/* PreScore of PodTopologySpread (initPreScoreState + PreScore) and
+ * InterPodAffinity (processExistingPod over all nodes), over the feasible list. */
+static void topo_prescore(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p, const int32_t* flist,
+                          int32_t nf, topo_ctx* t) {
+  /* PTS: IgnoredNodes = feasible nodes missing a soft key; pair registration; topoSize */
+  int32_t n_ignored = 0;
+  for (int i = 0; i < t->n; i++)
+    if (t->u[i]->kind == KSIM_USE_PTS_SOFT) {
+      memset(dom_of(o, i), 0, 8 * (size_t)o->vmax);
+      memset(present_of(o, i), 0, (size_t)o->vmax);
+    }
+  if (t->has_soft) {
+    int32_t size[KSIM_MAX_USES] = {0};
+    for (int32_t j = 0; j < nf; j++) {
+      int32_t node = flist[j];
+      o->ignored[node] = !node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node);
+      if (o->ignored[node]) { n_ignored++; continue; }
+      for (int i = 0; i < t->n; i++) {
+        const ksim_topo_use* u = t->u[i];
+        if (u->kind != KSIM_USE_PTS_SOFT || (u->flags & KSIM_USEF_HOSTNAME)) continue;
+        uint32_t v = use_value(o, u, node);
+        if (!present_of(o, i)[v]) { present_of(o, i)[v] = 1; size[i]++; }
+      }
+    }
+    for (int i = 0; i < t->n; i++) {
+      const ksim_topo_use* u = t->u[i];
+      if (u->kind != KSIM_USE_PTS_SOFT) continue;
+      int32_t sz = (u->flags & KSIM_USEF_HOSTNAME) ? nf - n_ignored : size[i];
+      t->weight[i] = o->topo_log[sz];                 /* topologyNormalizingWeight(sz) = log(sz + 2) */
+    }
+    for (int32_t node = 0; node < o->n; node++) {     /* processAllNode */
+      if (!node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node)) continue;
+      for (int i = 0; i < t->n; i++) {
+        const ksim_topo_use* u = t->u[i];
+        if (u->kind != KSIM_USE_PTS_SOFT || (u->flags & KSIM_USEF_HOSTNAME)) continue;
+        if (!match_node_inclusion_policies(o, ps, p, u, node)) continue;
+        uint32_t v = use_value(o, u, node);
+        if (!present_of(o, i)[v]) continue;           /* pair not associated with a candidate node */
+        dom_of(o, i)[v] += class_count(o, u->cls, node);
+      }
+    }
+  }
+  /* IPA: topologyScore[key][value] = sum of weighted counts over the nodes of the pair */
+  t->topology_score_empty = 1;
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_IPA_SCORE && u->kind != KSIM_USE_IPA_SCORE_HARD) continue;
+    memset(dom_of(o, i), 0, 8 * (size_t)o->vmax);
+    if (u->kind == KSIM_USE_IPA_SCORE_HARD && o->prof.hard_pod_affinity_weight <= 0) continue;
+    for (int32_t node = 0; node < o->n; node++) {
+      uint32_t v = use_value(o, u, node);
+      int64_t c = class_count(o, u->cls, node);
+      if (v == 0 || c == 0) continue;
+      dom_of(o, i)[v] += c;
+      t->topology_score_empty = 0;
+    }
+  }
+}
+
+/* podtopologyspread Score (before NormalizeScore); ignored nodes score 0 */
+static int64_t pts_score(const ksim_oracle* o, const topo_ctx* t, int32_t node) {
+  if (!t->has_soft || o->ignored[node]) return 0;
+  double score = 0;
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    if (u->kind != KSIM_USE_PTS_SOFT) continue;
+    uint32_t v = use_value(o, u, node);
+    if (v == 0) continue;
+    int64_t cnt = (u->flags & KSIM_USEF_HOSTNAME) ? class_count(o, u->cls, node) : dom_of(o, i)[v];
+    score += (double)cnt * t->weight[i] + (double)(u->arg - 1);   /* scoreForCount, unfused */
+  }
+  return (int64_t)round(score);                                   /* math.Round: half away from zero */
+}
+
+/* interpodaffinity Score */
+static int64_t ipa_score(const ksim_oracle* o, const topo_ctx* t, int32_t node) {
+  int64_t s = 0;
+  for (int i = 0; i < t->n; i++) {
+    const ksim_topo_use* u = t->u[i];
+    int64_t coef;
+    if (u->kind == KSIM_USE_IPA_SCORE) coef = u->arg;
+    else if (u->kind == KSIM_USE_IPA_SCORE_HARD) coef = o->prof.hard_pod_affinity_weight;
+    else continue;
+    if (coef == 0) continue;
+    uint32_t v = use_value(o, u, node);
+    if (v != 0) s += coef * dom_of(o, i)[v];
+  }
+  return s;
+}
+
 /* ---- framework: RunFilterPlugins — a17 ---------------------------------- */
 /* Runs the profile's filter plugins in order and stops at the first failure
  * (runAllFilters=false).  Returns the filter-order index of the failing plugin
  * or KSIM_PASSED; *detail gets the reason payload. */
 static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
-                                  int32_t node, uint32_t* detail) {
+                                  const topo_ctx* t, int32_t node, uint32_t* detail) {
   *detail = 0;
   for (int f = 0; f < o->prof.n_filter; f++) {
     switch (o->prof.filter[f]) {
@@ -401,9 +655,17 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
         if (r) { *detail = r; return (uint8_t)f; }
         break;
       }
-      /* PodTopologySpread / InterPodAffinity: pods without constraints or
-       * affinity terms, and no existing pods with (anti)affinity, pass.
-       * NodePorts / volume plugins: pods without host ports or volumes pass. */
+      case KSIM_PL_POD_TOPOLOGY_SPREAD: {
+        uint32_t r = t->has_hard ? pts_filter(o, t, node) : 0;
+        if (r) { *detail = r; return (uint8_t)f; }
+        break;
+      }
+      case KSIM_PL_INTER_POD_AFFINITY: {
+        uint32_t r = t->has_ipa_filter ? ipa_filter(o, p, t, node) : 0;
+        if (r) { *detail = r; return (uint8_t)f; }
+        break;
+      }
+      /* NodePorts / volume plugins: pods without host ports or volumes pass. */
       default:
         break;
     }
@@ -412,20 +674,22 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
 }
 
 static int64_t score_plugin_raw(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
-                                int plugin, int32_t node) {
+                                const topo_ctx* t, int plugin, int32_t node) {
   switch (plugin) {
     case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(o, p, node);
     case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(o, p, node);
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer_no_schedule(o, p, node);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(o, ps, p, node);
-    /* ImageLocality: nodes carry no image list -> calculatePriority(0) = 0.
-     * PodTopologySpread / InterPodAffinity: no constraints/terms -> 0. */
+    case KSIM_PL_POD_TOPOLOGY_SPREAD: return pts_score(o, t, node);
+    case KSIM_PL_INTER_POD_AFFINITY: return t->has_ipa_score ? ipa_score(o, t, node) : 0;
+    /* ImageLocality: nodes carry no image list -> calculatePriority(0) = 0. */
     default: return 0;
   }
 }
 
-/* NormalizeScore of each plugin over the scored list (in place). */
-static void normalize_plugin(int plugin, int32_t n, int64_t* s) {
+/* NormalizeScore of each plugin over the scored list (in place).  ign[j]:
+ * node j of the list is in PodTopologySpread's IgnoredNodes. */
+static void normalize_plugin(int plugin, const topo_ctx* t, const uint8_t* ign, int32_t n, int64_t* s) {
   switch (plugin) {
     case KSIM_PL_TAINT_TOLERATION:        /* tainttoleration.NormalizeScore (reverse) */
       ksim_oracle_default_normalize(MAX_NODE_SCORE, 1, n, s);
@@ -433,14 +697,31 @@ static void normalize_plugin(int plugin, int32_t n, int64_t* s) {
     case KSIM_PL_NODE_AFFINITY:           /* nodeaffinity.NormalizeScore */
       ksim_oracle_default_normalize(MAX_NODE_SCORE, 0, n, s);
       return;
-    case KSIM_PL_POD_TOPOLOGY_SPREAD: {   /* podtopologyspread.NormalizeScore, no ignored nodes */
+    case KSIM_PL_POD_TOPOLOGY_SPREAD: {   /* podtopologyspread.NormalizeScore */
       int64_t mn = INT64_MAX, mx = 0;
-      for (int i = 0; i < n; i++) { if (s[i] < mn) mn = s[i]; if (s[i] > mx) mx = s[i]; }
-      for (int i = 0; i < n; i++)
-        s[i] = (mx == 0) ? MAX_NODE_SCORE : MAX_NODE_SCORE * (mx + mn - s[i]) / mx;
+      for (int i = 0; i < n; i++) {
+        if (ign[i]) continue;               /* invalidScore: excluded from min / max */
+        if (s[i] < mn) mn = s[i];
+        if (s[i] > mx) mx = s[i];
+      }
+      for (int i = 0; i < n; i++) {
+        if (ign[i]) s[i] = 0;
+        else s[i] = (mx == 0) ? MAX_NODE_SCORE : MAX_NODE_SCORE * (mx + mn - s[i]) / mx;
+      }
       return;
     }
-    case KSIM_PL_INTER_POD_AFFINITY:      /* topologyScore empty -> scores left unchanged */
+    case KSIM_PL_INTER_POD_AFFINITY: {    /* interpodaffinity.NormalizeScore */
+      if (t->topology_score_empty) return;
+      int64_t mn = INT64_MAX, mx = INT64_MIN;
+      for (int i = 0; i < n; i++) { if (s[i] > mx) mx = s[i]; if (s[i] < mn) mn = s[i]; }
+      int64_t diff = mx - mn;
+      for (int i = 0; i < n; i++) {
+        double f = 0;
+        if (diff > 0) f = (double)MAX_NODE_SCORE * ((double)(s[i] - mn) / (double)diff);
+        s[i] = (int64_t)f;
+      }
+      return;
+    }
     default:
       return;                              /* Fit / BalancedAllocation / ImageLocality: none */
   }
@@ -452,7 +733,7 @@ static int has_normalize(int plugin) {
 }
 
 /* NodeInfo.AddPod restricted to the aggregates the plugins read — a20 */
-static void assume_pod(ksim_oracle* o, const ksim_pod* p, int32_t node, int sign) {
+static void assume_pod(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p, int32_t node, int sign) {
   o->req_cpu[node] += sign * p->req_cpu;
   o->req_mem[node] += sign * p->req_mem;
   o->req_eph[node] += sign * p->req_eph;
@@ -460,6 +741,10 @@ static void assume_pod(ksim_oracle* o, const ksim_pod* p, int32_t node, int sign
   o->nz_cpu[node] += sign * p->nz_cpu;
   o->nz_mem[node] += sign * p->nz_mem;
   o->num_pods[node] += sign;
+  for (int i = 0; i < p->add_count; i++) {            /* pod counts / carried terms */
+    const ksim_class_add* a = &ps->adds[p->add_first + i];
+    o->cnt[(size_t)a->cls * o->n + node] += sign * a->count;
+  }
 }
 
 /* ---- schedulePod: findNodesThatFitPod + prioritizeNodes + selectHost ----- */
@@ -481,12 +766,14 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_e
   if (out->norm) memset(out->norm, 0, 8 * (size_t)N * S);
   if (out->total) memset(out->total, 0, 8 * (size_t)N);
 
-  /* findNodesThatPassFilters */
+  /* PreFilter (PodTopologySpread / InterPodAffinity state), then findNodesThatPassFilters */
+  topo_ctx tc;
+  topo_prefilter(o, ps, p, &tc);
   int32_t nf = 0, nfailed = 0, evaluated = 0;
   for (int32_t i = 0; i < N; i++) {
     int32_t node = (start + i) % N;
     uint32_t det;
-    uint8_t r = run_filter_plugins(o, ps, p, node, &det);
+    uint8_t r = run_filter_plugins(o, ps, p, &tc, node, &det);
     evaluated++;
     if (out->fail_plugin) out->fail_plugin[node] = r;
     if (out->fail_detail) out->fail_detail[node] = det;
@@ -518,11 +805,14 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_e
     /* RunScorePlugins: raw scores, NormalizeScore per plugin, weights */
     int64_t* tmp = (int64_t*)malloc(8 * (size_t)nf);
     int64_t* totals = (int64_t*)calloc((size_t)nf, 8);
+    uint8_t* ign = (uint8_t*)calloc((size_t)nf, 1);
+    topo_prescore(o, ps, p, o->flist, nf, &tc);
+    if (tc.has_soft) for (int32_t j = 0; j < nf; j++) ign[j] = o->ignored[o->flist[j]];
     for (int s = 0; s < S; s++) {
       int pl = o->prof.score[s];
-      for (int32_t j = 0; j < nf; j++) tmp[j] = score_plugin_raw(o, ps, p, pl, o->flist[j]);
+      for (int32_t j = 0; j < nf; j++) tmp[j] = score_plugin_raw(o, ps, p, &tc, pl, o->flist[j]);
       if (out->raw) for (int32_t j = 0; j < nf; j++) out->raw[(size_t)s * N + o->flist[j]] = tmp[j];
-      if (has_normalize(pl)) normalize_plugin(pl, nf, tmp);
+      if (has_normalize(pl)) normalize_plugin(pl, &tc, ign, nf, tmp);
       int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
       for (int32_t j = 0; j < nf; j++) {
         if (out->norm) out->norm[(size_t)s * N + o->flist[j]] = tmp[j];
@@ -541,10 +831,11 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_e
     }
     free(tmp);
     free(totals);
+    free(ign);
   }
   out->chosen = chosen;
   out->status = KSIM_STATUS_SCHEDULED;
-  assume_pod(o, p, chosen, 1);
+  assume_pod(o, ps, p, chosen, 1);
   return KSIM_OK;
 }
 
@@ -560,6 +851,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
   uint8_t* feas = o->fail;   /* 1 = passed all filters */
   int64_t* raw = o->raw;     /* [S][N] */
   int64_t* totals = (int64_t*)malloc(8 * (size_t)N);
+  uint8_t* ign_buf = (uint8_t*)malloc((size_t)N);
 
   for (int32_t c = 0; c < count; c++) {
     const int32_t pi = first + c;
@@ -569,13 +861,15 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
     const int32_t start = o->next_start;
     int32_t nf = 0, nfailed = 0, evaluated = 0;
     int32_t chosen = -1;
+    topo_ctx tc;
+    topo_prefilter(o, ps, p, &tc);
 
 #pragma omp parallel num_threads(nthreads) if (nthreads > 1)
     {
 #pragma omp for schedule(static)
       for (int32_t node = 0; node < N; node++) {
         uint32_t det;
-        feas[node] = run_filter_plugins(o, ps, p, node, &det) == KSIM_PASSED;
+        feas[node] = run_filter_plugins(o, ps, p, &tc, node, &det) == KSIM_PASSED;
       }
 #pragma omp single
       {
@@ -591,17 +885,20 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
         }
       }
       if (nf > 1) {
+#pragma omp single
+        topo_prescore(o, ps, p, o->flist, nf, &tc);
 #pragma omp for schedule(static)
         for (int32_t j = 0; j < nf; j++)
           for (int s = 0; s < S; s++)
-            raw[(size_t)s * N + j] = score_plugin_raw(o, ps, p, o->prof.score[s], o->flist[j]);
+            raw[(size_t)s * N + j] = score_plugin_raw(o, ps, p, &tc, o->prof.score[s], o->flist[j]);
 #pragma omp single
         {
           for (int32_t j = 0; j < nf; j++) totals[j] = (S == 0) ? 1 : 0;
+          for (int32_t j = 0; j < nf; j++) ign_buf[j] = tc.has_soft ? o->ignored[o->flist[j]] : 0;
           for (int s = 0; s < S; s++) {
             int pl = o->prof.score[s];
             int64_t* v = raw + (size_t)s * N;
-            if (has_normalize(pl)) normalize_plugin(pl, nf, v);
+            if (has_normalize(pl)) normalize_plugin(pl, &tc, ign_buf, nf, v);
             int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
             for (int32_t j = 0; j < nf; j++) totals[j] += v[j] * w;
           }
@@ -616,10 +913,11 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
     if (nf == 1) chosen = o->flist[0];
     o->next_start = (start + nf + nfailed) % N;
     evals += evaluated;
-    if (chosen >= 0) { assume_pod(o, p, chosen, 1); sched++; } else { unsched++; }
+    if (chosen >= 0) { assume_pod(o, ps, p, chosen, 1); sched++; } else { unsched++; }
     if (chosen_out) chosen_out[c] = chosen;
   }
   free(totals);
+  free(ign_buf);
   if (st) {
     st->pods = count;
     st->scheduled = sched;
@@ -647,3 +945,9 @@ int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* 
 int32_t ksim_oracle_next_start(const ksim_oracle* o) { return o->next_start; }
 void ksim_oracle_set_next_start(ksim_oracle* o, int32_t s) { o->next_start = s; }
 void ksim_oracle_set_pod_seq(ksim_oracle* o, int64_t seq) { o->pod_seq = seq; }
+
+int ksim_oracle_get_class_count(const ksim_oracle* o, int32_t* out) {
+  if (!o || !out) return KSIM_E_INVALID;
+  memcpy(out, o->cnt, 4 * (size_t)o->n * (size_t)(o->n_classes > 0 ? o->n_classes : 0));
+  return KSIM_OK;
+}

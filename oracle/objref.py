@@ -1,0 +1,565 @@
+"""Object-level restatement of the scheduling cycle in pure Python (ORACLE).
+
+TEST INFRASTRUCTURE ONLY (like ksim_oracle.c): used by tests/ to pin the C
+oracle AND the host encoder (ksim/encode.py, ksim/topology.py) on small
+clusters.  It works on the Node / Pod objects with string labels and Go-style
+maps, following the structure of the upstream k8s.io/kubernetes v1.26.2
+plugins (pinned at simulator/go.mod:53; absent from /root/reference, restated
+per SURVEY.md Appendix A and the notes in DESIGN.md), so it shares no code
+with the encoder or the C restatement except the Quantity / toleration /
+selector helpers of ksim.model and the nodeTree order of ksim.encode.
+
+Pure-Python loops: small cases only (tens of nodes, hundreds of pods).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+from ksim.encode import node_tree_order, pod_nonzero_requests, pod_requests, zone_key
+from ksim.model import LabelSelector, Node, Pod, PodAffinityTerm, Taint, selector_matches
+
+MAX_NODE_SCORE = 100
+LABEL_HOSTNAME = "kubernetes.io/hostname"
+M64 = (1 << 64) - 1
+KEY_NODE_MASK = (1 << 18) - 1
+
+# filter failure messages (framework.Status.Message())
+PTS_MISSING = "node(s) didn't match pod topology spread constraints (missing required label)"
+PTS_SKEW = "node(s) didn't match pod topology spread constraints"
+IPA_AFF = "node(s) didn't match pod affinity rules"
+IPA_ANTI = "node(s) didn't match pod anti-affinity rules"
+IPA_EXIST = "node(s) didn't satisfy existing pods anti-affinity rules"
+
+
+def splitmix64(x: int) -> int:
+    z = (x + 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def tb_key(total: int, seed: int, seq: int, node: int) -> int:
+    """selectHost tie-break TB(seed)."""
+    h = splitmix64((seed ^ ((seq << 20) & M64) ^ node) & M64) >> 38
+    return (((total & M64) << 44) | (h << 18) | (KEY_NODE_MASK - node)) & M64
+
+
+def num_feasible_nodes_to_find(pct: int, n: int) -> int:
+    if n < 100 or pct >= 100:
+        return n
+    a = pct if pct > 0 else max(5, 50 - n // 125)
+    return max(n * a // 100, 100)
+
+
+def go_div(a: int, b: int) -> int:
+    """Go integer division (truncates toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+# ---- affinity terms ------------------------------------------------------------
+class AffinityTerm:
+    """framework.AffinityTerm (newAffinityTerm + getNamespacesFromPodAffinityTerm)."""
+
+    def __init__(self, owner: Pod, t: PodAffinityTerm, weight: int = 0):
+        self.namespaces = set(t.namespaces)
+        if not t.namespaces and t.namespace_selector is None:
+            self.namespaces.add(owner.namespace)
+        self.ns_selector: Optional[LabelSelector] = t.namespace_selector
+        self.selector: Optional[LabelSelector] = t.label_selector
+        self.topology_key = t.topology_key
+        self.weight = weight
+
+    def matches(self, pod: Pod, ns_labels: Optional[Dict[str, str]]) -> bool:
+        """AffinityTerm.Matches: namespace listed, or the namespace selector
+        (nil = Nothing, {} = Everything) matches ns_labels; then the selector."""
+        ns_ok = pod.namespace in self.namespaces or selector_matches(self.ns_selector, ns_labels or {})
+        return ns_ok and selector_matches(self.selector, pod.labels)
+
+
+class PodInfo:
+    def __init__(self, pod: Pod):
+        self.pod = pod
+        self.required_affinity = [AffinityTerm(pod, t) for t in pod.pod_affinity_required]
+        self.required_anti = [AffinityTerm(pod, t) for t in pod.pod_anti_affinity_required]
+        self.preferred_affinity = [AffinityTerm(pod, w.term, w.weight) for w in pod.pod_affinity_preferred]
+        self.preferred_anti = [AffinityTerm(pod, w.term, w.weight) for w in pod.pod_anti_affinity_preferred]
+
+
+class NodeInfo:
+    def __init__(self, node: Node):
+        self.node = node
+        self.alloc = {"cpu": 0, "memory": 0, "ephemeral-storage": 0, "pods": 0}
+        from ksim.model import quantity_milli_value, quantity_value
+        for k, v in node.allocatable.items():
+            self.alloc[k] = quantity_milli_value(v) if k == "cpu" else quantity_value(v)
+        self.requested: Dict[str, int] = {}
+        self.nz_cpu = 0
+        self.nz_mem = 0
+        self.pods: List[PodInfo] = []
+
+    def add_pod(self, pod: Pod) -> None:
+        for k, v in pod_requests(pod).items():
+            self.requested[k] = self.requested.get(k, 0) + v
+        c, m = pod_nonzero_requests(pod)
+        self.nz_cpu += c
+        self.nz_mem += m
+        self.pods.append(PodInfo(pod))
+
+
+class ObjScheduler:
+    """One simulated scheduler (sequential semantics, TB tie-break)."""
+
+    def __init__(self, nodes: List[Node], bound: List[Pod] = (), namespaces: Optional[Dict[str, Dict]] = None,
+                 pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
+                 hard_pod_affinity_weight: int = 1):
+        order = node_tree_order([zone_key(n.labels) for n in nodes])
+        self.nodes = [NodeInfo(nodes[i]) for i in order]
+        self.by_name = {ni.node.name: ni for ni in self.nodes}
+        for p in bound:
+            if p.node_name in self.by_name:
+                self.by_name[p.node_name].add_pod(p)
+        self.ns_labels = dict(namespaces or {})
+        self.pct = pct
+        self.weights = weights or {"NodeResourcesBalancedAllocation": 1, "ImageLocality": 1, "InterPodAffinity": 1,
+                                   "NodeResourcesFit": 1, "NodeAffinity": 1, "PodTopologySpread": 2,
+                                   "TaintToleration": 1}
+        self.score_order = ["NodeResourcesBalancedAllocation", "ImageLocality", "InterPodAffinity",
+                            "NodeResourcesFit", "NodeAffinity", "PodTopologySpread", "TaintToleration"]
+        self.filter_order = ["NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodePorts",
+                             "NodeResourcesFit", "VolumeRestrictions", "EBSLimits", "GCEPDLimits",
+                             "NodeVolumeLimits", "AzureDiskLimits", "VolumeBinding", "VolumeZone",
+                             "PodTopologySpread", "InterPodAffinity"]
+        self.seed = seed
+        self.hard_w = hard_pod_affinity_weight
+        self.next_start = 0
+        self.seq = 0
+
+    # ---- NodeAffinity / taints (component-helpers, v1helper) -------------------
+    @staticmethod
+    def _req_match(r, labels: Dict[str, str]) -> bool:
+        has = r.key in labels
+        if r.operator == "In":
+            return bool(r.values) and has and labels[r.key] in r.values
+        if r.operator == "NotIn":
+            return bool(r.values) and (not has or labels[r.key] not in r.values)
+        if r.operator == "Exists":
+            return not r.values and has
+        if r.operator == "DoesNotExist":
+            return not r.values and not has
+        if r.operator in ("Gt", "Lt"):
+            if len(r.values) != 1 or not has:
+                return False
+            try:
+                a, b = int(labels[r.key]), int(r.values[0])
+            except ValueError:
+                return False
+            return a > b if r.operator == "Gt" else a < b
+        return False
+
+    def _term_match(self, t, node: Node) -> bool:
+        if not t.match_expressions and not t.match_fields:
+            return False
+        for r in t.match_expressions:
+            if not self._req_match(r, node.labels):
+                return False
+        for r in t.match_fields:
+            if r.key != "metadata.name" or r.operator not in ("In", "NotIn") or len(r.values) != 1:
+                return False
+            if (node.name in r.values) != (r.operator == "In"):
+                return False
+        return True
+
+    def required_node_affinity(self, pod: Pod, node: Node) -> bool:
+        for k, v in pod.node_selector.items():
+            if node.labels.get(k) != v:
+                return False
+        if pod.required_terms is not None:
+            return any(self._term_match(t, node) for t in pod.required_terms)
+        return True
+
+    @staticmethod
+    def untolerated_taint(pod: Pod, node: Node, effects=("NoSchedule", "NoExecute")):
+        for t in node.taints:
+            if t.effect in effects and not any(tol.tolerates(t) for tol in pod.tolerations):
+                return t
+        return None
+
+    # ---- PodTopologySpread (filtering.go / scoring.go) ---------------------------
+    def _constraints(self, pod: Pod, when: str):
+        out = []
+        for c in pod.topology_spread:
+            if c.when_unsatisfiable == when:
+                out.append(c)
+        return out
+
+    @staticmethod
+    def _count_match(ni: NodeInfo, sel: Optional[LabelSelector], ns: str) -> int:
+        if sel is None or sel.empty():          # Nothing / selector.Empty() -> 0
+            return 0
+        return sum(1 for pi in ni.pods if pi.pod.namespace == ns and sel.matches(pi.pod.labels))
+
+    def _inclusion(self, c, pod: Pod, node: Node) -> bool:
+        if (c.node_affinity_policy or "Honor") == "Honor" and not self.required_node_affinity(pod, node):
+            return False
+        if (c.node_taints_policy or "Ignore") == "Honor" and self.untolerated_taint(pod, node) is not None:
+            return False
+        return True
+
+    def pts_prefilter(self, pod: Pod):
+        cons = self._constraints(pod, "DoNotSchedule")
+        pair_num: Dict[Tuple[str, str], int] = {}
+        for ni in self.nodes:
+            node = ni.node
+            if not all(c.topology_key in node.labels for c in cons):
+                continue
+            tp: Dict[Tuple[str, str], int] = {}
+            for c in cons:
+                if not self._inclusion(c, pod, node):
+                    continue
+                tp[(c.topology_key, node.labels[c.topology_key])] = self._count_match(ni, c.label_selector,
+                                                                                      pod.namespace)
+            for k, v in tp.items():
+                pair_num[k] = pair_num.get(k, 0) + v
+        crit = {c.topology_key: 2 ** 31 - 1 for c in cons}
+        for (k, v), num in pair_num.items():
+            crit[k] = min(crit[k], num)
+        return cons, pair_num, crit
+
+    def pts_filter(self, pod: Pod, state, node: Node) -> Optional[str]:
+        cons, pair_num, crit = state
+        for c in cons:
+            if c.topology_key not in node.labels:
+                return PTS_MISSING
+            self_match = 1 if selector_matches(c.label_selector, pod.labels) else 0
+            match = pair_num.get((c.topology_key, node.labels[c.topology_key]), 0)
+            if match + self_match - crit[c.topology_key] > c.max_skew:
+                return PTS_SKEW
+        return None
+
+    def pts_prescore(self, pod: Pod, filtered: List[NodeInfo]):
+        cons = self._constraints(pod, "ScheduleAnyway")
+        ignored = set()
+        pair_counts: Dict[Tuple[str, str], int] = {}
+        weights = []
+        if not cons:
+            return cons, ignored, pair_counts, weights
+        topo_size = [0] * len(cons)
+        for ni in filtered:
+            node = ni.node
+            if not all(c.topology_key in node.labels for c in cons):
+                ignored.add(node.name)
+                continue
+            for i, c in enumerate(cons):
+                if c.topology_key == LABEL_HOSTNAME:
+                    continue
+                pair = (c.topology_key, node.labels[c.topology_key])
+                if pair not in pair_counts:
+                    pair_counts[pair] = 0
+                    topo_size[i] += 1
+        for i, c in enumerate(cons):
+            sz = topo_size[i]
+            if c.topology_key == LABEL_HOSTNAME:
+                sz = len(filtered) - len(ignored)
+            weights.append(math.log(float(sz + 2)))
+        for ni in self.nodes:
+            node = ni.node
+            if not all(c.topology_key in node.labels for c in cons):
+                continue
+            for c in cons:
+                if not self._inclusion(c, pod, node):
+                    continue
+                pair = (c.topology_key, node.labels[c.topology_key])
+                if pair not in pair_counts:
+                    continue
+                pair_counts[pair] += self._count_match(ni, c.label_selector, pod.namespace)
+        return cons, ignored, pair_counts, weights
+
+    def pts_score(self, pod: Pod, state, ni: NodeInfo) -> int:
+        cons, ignored, pair_counts, weights = state
+        if ni.node.name in ignored:
+            return 0
+        score = 0.0
+        for i, c in enumerate(cons):
+            if c.topology_key in ni.node.labels:
+                if c.topology_key == LABEL_HOSTNAME:
+                    cnt = self._count_match(ni, c.label_selector, pod.namespace)
+                else:
+                    cnt = pair_counts[(c.topology_key, ni.node.labels[c.topology_key])]
+                score += float(cnt) * weights[i] + float(c.max_skew - 1)
+        return int(math.floor(score + 0.5)) if score >= 0 else -int(math.floor(-score + 0.5))
+
+    @staticmethod
+    def pts_normalize(state, names: List[str], scores: List[int]) -> List[int]:
+        _, ignored, _, _ = state
+        mn, mx = 2 ** 63 - 1, 0
+        for n, s in zip(names, scores):
+            if n in ignored:
+                continue
+            mn, mx = min(mn, s), max(mx, s)
+        out = []
+        for n, s in zip(names, scores):
+            if n in ignored:
+                out.append(0)
+            elif mx == 0:
+                out.append(MAX_NODE_SCORE)
+            else:
+                out.append(go_div(MAX_NODE_SCORE * (mx + mn - s), mx))
+        return out
+
+    # ---- InterPodAffinity (filtering.go / scoring.go) ----------------------------
+    def _nslabels(self, ns: str) -> Dict[str, str]:
+        return self.ns_labels.get(ns, {})
+
+    def _merge_ns(self, t: AffinityTerm) -> AffinityTerm:
+        """mergeAffinityTermNamespacesIfNotEmpty (incoming pod's terms)."""
+        if t.ns_selector is None or t.ns_selector.empty():
+            return t
+        import copy
+        t = copy.copy(t)
+        t.namespaces = set(t.namespaces) | {n for n, lab in self.ns_labels.items() if t.ns_selector.matches(lab)}
+        t.ns_selector = None                     # labels.Nothing()
+        return t
+
+    def ipa_prefilter(self, pod: Pod):
+        info = PodInfo(pod)
+        req_aff = [self._merge_ns(t) for t in info.required_affinity]
+        req_anti = [self._merge_ns(t) for t in info.required_anti]
+        ns_labels = self._nslabels(pod.namespace)
+        existing: Dict[Tuple[str, str], int] = {}
+        for ni in self.nodes:
+            for epi in ni.pods:
+                for t in epi.required_anti:
+                    if t.matches(pod, ns_labels) and t.topology_key in ni.node.labels:
+                        pair = (t.topology_key, ni.node.labels[t.topology_key])
+                        existing[pair] = existing.get(pair, 0) + 1
+        aff: Dict[Tuple[str, str], int] = {}
+        anti: Dict[Tuple[str, str], int] = {}
+        for ni in self.nodes:
+            for epi in ni.pods:
+                if req_aff and all(t.matches(epi.pod, None) for t in req_aff):
+                    for t in req_aff:
+                        if t.topology_key in ni.node.labels:
+                            pair = (t.topology_key, ni.node.labels[t.topology_key])
+                            aff[pair] = aff.get(pair, 0) + 1
+                for t in req_anti:
+                    if t.matches(epi.pod, None) and t.topology_key in ni.node.labels:
+                        pair = (t.topology_key, ni.node.labels[t.topology_key])
+                        anti[pair] = anti.get(pair, 0) + 1
+        self_match = bool(req_aff) and all(t.matches(pod, None) for t in req_aff)
+        return req_aff, req_anti, existing, aff, anti, self_match
+
+    @staticmethod
+    def ipa_filter(state, node: Node) -> Optional[str]:
+        req_aff, req_anti, existing, aff, anti, self_match = state
+        pods_exist = True
+        for t in req_aff:
+            if t.topology_key in node.labels:
+                if aff.get((t.topology_key, node.labels[t.topology_key]), 0) <= 0:
+                    pods_exist = False
+            else:
+                return IPA_AFF
+        if not pods_exist and not (len(aff) == 0 and self_match):
+            return IPA_AFF
+        if anti:
+            for t in req_anti:
+                if t.topology_key in node.labels and anti.get((t.topology_key, node.labels[t.topology_key]), 0) > 0:
+                    return IPA_ANTI
+        if existing:
+            for k, v in node.labels.items():
+                if existing.get((k, v), 0) > 0:
+                    return IPA_EXIST
+        return None
+
+    def ipa_prescore(self, pod: Pod) -> Dict[str, Dict[str, int]]:
+        info = PodInfo(pod)
+        pref_aff = [self._merge_ns(t) for t in info.preferred_affinity]
+        pref_anti = [self._merge_ns(t) for t in info.preferred_anti]
+        ns_labels = self._nslabels(pod.namespace)
+        topo: Dict[str, Dict[str, int]] = {}
+
+        def process(t: AffinityTerm, weight: int, target: Pod, nsl, node: Node, mult: int):
+            if t.matches(target, nsl) and t.topology_key in node.labels:
+                d = topo.setdefault(t.topology_key, {})
+                v = node.labels[t.topology_key]
+                d[v] = d.get(v, 0) + weight * mult
+
+        for ni in self.nodes:
+            node = ni.node
+            for epi in ni.pods:
+                if not node.labels:
+                    continue
+                for t in pref_aff:
+                    process(t, t.weight, epi.pod, None, node, 1)
+                for t in pref_anti:
+                    process(t, t.weight, epi.pod, None, node, -1)
+                if self.hard_w > 0:
+                    for t in epi.required_affinity:
+                        process(t, self.hard_w, pod, ns_labels, node, 1)
+                for t in epi.preferred_affinity:
+                    process(t, t.weight, pod, ns_labels, node, 1)
+                for t in epi.preferred_anti:
+                    process(t, t.weight, pod, ns_labels, node, -1)
+        return topo
+
+    @staticmethod
+    def ipa_score(topo, node: Node) -> int:
+        s = 0
+        for k, vals in topo.items():
+            if k in node.labels:
+                s += vals.get(node.labels[k], 0)
+        return s
+
+    @staticmethod
+    def ipa_normalize(topo, scores: List[int]) -> List[int]:
+        if not topo:
+            return list(scores)
+        mn, mx = min(scores), max(scores)
+        d = mx - mn
+        return [int(float(MAX_NODE_SCORE) * (float(s - mn) / float(d))) if d > 0 else 0 for s in scores]
+
+    # ---- resources -------------------------------------------------------------------
+    @staticmethod
+    def fit_filter(pod: Pod, ni: NodeInfo) -> Optional[str]:
+        req = pod_requests(pod)
+        reasons = []
+        if len(ni.pods) + 1 > ni.alloc.get("pods", 0):
+            reasons.append("Too many pods")
+        if any(v for v in req.values()) or any(k not in ("cpu", "memory", "ephemeral-storage") for k in req):
+            for r in ("cpu", "memory", "ephemeral-storage"):
+                if req.get(r, 0) > ni.alloc.get(r, 0) - ni.requested.get(r, 0):
+                    reasons.append(f"Insufficient {r}")
+        return ", ".join(reasons) if reasons else None
+
+    @staticmethod
+    def least_allocated(pod: Pod, ni: NodeInfo) -> int:
+        ncpu, nmem = pod_nonzero_requests(pod)
+        score = wsum = 0
+        for alloc, req in ((ni.alloc["cpu"], ni.nz_cpu + ncpu), (ni.alloc["memory"], ni.nz_mem + nmem)):
+            if alloc == 0:
+                continue
+            s = 0 if req > alloc else go_div((alloc - req) * MAX_NODE_SCORE, alloc)
+            score += s
+            wsum += 1
+        return go_div(score, wsum) if wsum else 0
+
+    @staticmethod
+    def balanced(pod: Pod, ni: NodeInfo) -> int:
+        req = pod_requests(pod)
+        fr = []
+        for r in ("cpu", "memory"):
+            a = ni.alloc[r]
+            if a == 0:
+                continue
+            f = float(ni.requested.get(r, 0) + req.get(r, 0)) / float(a)
+            fr.append(1.0 if f > 1 else f)
+        std = abs((fr[0] - fr[1]) / 2) if len(fr) == 2 else 0.0
+        return int((1 - std) * MAX_NODE_SCORE)
+
+    @staticmethod
+    def default_normalize(scores: List[int], reverse: bool) -> List[int]:
+        m = max([0] + scores)
+        if m == 0:
+            return [MAX_NODE_SCORE] * len(scores) if reverse else list(scores)
+        out = [go_div(MAX_NODE_SCORE * s, m) for s in scores]
+        return [MAX_NODE_SCORE - s for s in out] if reverse else out
+
+    # ---- the cycle ---------------------------------------------------------------------
+    def filter_node(self, pod: Pod, ni: NodeInfo, pts, ipa) -> Tuple[Optional[str], Optional[str]]:
+        node = ni.node
+        for pl in self.filter_order:
+            msg = None
+            if pl == "NodeUnschedulable":
+                if node.unschedulable and not any(
+                        t.tolerates(Taint("node.kubernetes.io/unschedulable", "", "NoSchedule"))
+                        for t in pod.tolerations):
+                    msg = "node(s) were unschedulable"
+            elif pl == "NodeName":
+                if pod.node_name and pod.node_name != node.name:
+                    msg = "node(s) didn't match the requested node name"
+            elif pl == "TaintToleration":
+                t = self.untolerated_taint(pod, node)
+                if t is not None:
+                    msg = f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
+            elif pl == "NodeAffinity":
+                if not self.required_node_affinity(pod, node):
+                    msg = "node(s) didn't match Pod's node affinity/selector"
+            elif pl == "NodeResourcesFit":
+                msg = self.fit_filter(pod, ni)
+            elif pl == "PodTopologySpread":
+                msg = self.pts_filter(pod, pts, node)
+            elif pl == "InterPodAffinity":
+                msg = self.ipa_filter(ipa, node)
+            if msg:
+                return pl, msg
+        return None, None
+
+    def cycle(self, pod: Pod) -> dict:
+        N = len(self.nodes)
+        seq = self.seq
+        self.seq += 1
+        K = num_feasible_nodes_to_find(self.pct, N)
+        pts = self.pts_prefilter(pod)
+        ipa = self.ipa_prefilter(pod)
+        filt: Dict[str, Tuple[Optional[str], Optional[str]]] = {}
+        feasible: List[NodeInfo] = []
+        failed = 0
+        for i in range(N):
+            ni = self.nodes[(self.next_start + i) % N]
+            pl, msg = self.filter_node(pod, ni, pts, ipa)
+            filt[ni.node.name] = (pl, msg)
+            if pl is None:
+                if len(feasible) == K:
+                    break
+                feasible.append(ni)
+            else:
+                failed += 1
+        self.next_start = (self.next_start + len(feasible) + failed) % N
+        res = {"filter": filt, "n_feasible": len(feasible), "raw": {}, "norm": {}, "total": {}}
+        if not feasible:
+            res["chosen"] = None
+            return res
+        if len(feasible) == 1:
+            chosen = feasible[0]
+        else:
+            names = [ni.node.name for ni in feasible]
+            pstate = self.pts_prescore(pod, feasible)
+            topo = self.ipa_prescore(pod)
+            totals = [0] * len(feasible)
+            for pl in self.score_order:
+                if pl == "NodeResourcesBalancedAllocation":
+                    raw = [self.balanced(pod, ni) for ni in feasible]
+                    norm = raw
+                elif pl == "ImageLocality":
+                    raw = [0] * len(feasible)
+                    norm = raw
+                elif pl == "InterPodAffinity":
+                    raw = [self.ipa_score(topo, ni.node) for ni in feasible]
+                    norm = self.ipa_normalize(topo, raw)
+                elif pl == "NodeResourcesFit":
+                    raw = [self.least_allocated(pod, ni) for ni in feasible]
+                    norm = raw
+                elif pl == "NodeAffinity":
+                    raw = [sum(t.weight for t in pod.preferred_terms if t.weight and self._term_match(t.term, ni.node))
+                           for ni in feasible]
+                    norm = self.default_normalize(raw, False)
+                elif pl == "PodTopologySpread":
+                    raw = [self.pts_score(pod, pstate, ni) for ni in feasible]
+                    norm = self.pts_normalize(pstate, names, raw)
+                else:   # TaintToleration
+                    raw = [sum(1 for t in ni.node.taints if t.effect == "PreferNoSchedule" and not any(
+                        tol.tolerates(t) for tol in pod.tolerations if tol.effect in ("", "PreferNoSchedule")))
+                        for ni in feasible]
+                    norm = self.default_normalize(raw, True)
+                w = self.weights.get(pl, 0) or 1
+                res["raw"][pl] = dict(zip(names, raw))
+                res["norm"][pl] = dict(zip(names, norm))
+                totals = [a + b * w for a, b in zip(totals, norm)]
+            res["total"] = dict(zip(names, totals))
+            index = {ni.node.name: i for i, ni in enumerate(self.nodes)}
+            best = max(range(len(feasible)), key=lambda j: tb_key(totals[j], self.seed, seq, index[names[j]]))
+            chosen = feasible[best]
+        chosen.add_pod(pod)
+        res["chosen"] = chosen.node.name
+        return res

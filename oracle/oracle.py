@@ -28,6 +28,7 @@ def lib():
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
+        L.ksim_oracle_get_class_count.argtypes = [vp, vp]
         L.ksim_oracle_next_start.argtypes = [vp]
         L.ksim_oracle_next_start.restype = i32
         L.ksim_oracle_set_next_start.argtypes = [vp, i32]
@@ -96,6 +97,11 @@ class Oracle:
         a = [out[k].ctypes.data_as(ctypes.c_void_p) for k in
              ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")]
         lib().ksim_oracle_get_node_state(self.h, *a)
+        return out
+
+    def class_count(self) -> np.ndarray:
+        out = np.zeros((self.cluster.class_count.shape[0], self.cluster.n_nodes), np.int32)
+        lib().ksim_oracle_get_class_count(self.h, out.ctypes.data_as(ctypes.c_void_p))
         return out
 
     @property

@@ -166,3 +166,86 @@ def test_batch_cuts_balanced_heavy():
     d = eng.diag()
     print("diag", d)
     assert d["cuts"] > 0
+
+
+# ---- PodTopologySpread + InterPodAffinity (config 3 shapes) ----------------------
+def _engine(cluster, prof):
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    return eng
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_config3_compat_cycles(pct):
+    """Per-node outputs of every cycle (filter codes incl. PTS / IPA details,
+    raw + normalized scores, totals) and the count classes afterwards."""
+    cluster, pods = gen.config3(n_nodes=300, pods_per_node=10, n_incoming=300, seed=11, zone_anti_every=50)
+    prof = _prof(pct)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(pods.n_pods):
+        _compare_cycle(eng.eval_pod(pods, i), ora.cycle(pods, i), f"pod {i}")
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_config3_batch(pct):
+    cluster, pods = gen.config3(n_nodes=1000, pods_per_node=10, n_incoming=1500, seed=12)
+    prof = _prof(pct)
+    eng = _engine(cluster, prof)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+
+
+def test_topology_mixed_with_batchable_pods():
+    """Bare pods carrying app labels (batch path; their binds add to the
+    selector classes) interleaved with spread / affinity pods (per-pod path)."""
+    from ksim.encode import encode_cluster, encode_pods
+    from ksim.model import Container, Pod
+    nodes, bound, inc = gen.config3_objects(n_nodes=400, pods_per_node=5, n_incoming=600, seed=13)
+    bare = [Pod(f"bare-{k}", labels={"app": f"a{k % 64}", "tier": "web"},
+                containers=[Container({"cpu": "200m", "memory": "512Mi"})]) for k in range(1200)]
+    queue = []
+    for k in range(600):
+        queue.append(inc[k])
+        queue.extend(bare[2 * k:2 * k + 2])
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, queue)
+    prof = _prof(100)
+    eng = _engine(cluster, prof)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, _ = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    assert st.perpod_cycles == 600 and st.batches > 0
+
+
+def test_topology_hand_cases_vs_oracle():
+    """The object-level cases of tests/test_topology.py through the engine."""
+    import test_topology as tt
+    from ksim.encode import encode_cluster, encode_pods
+    cases = []
+    nodes = [tt._node(i, f"z{i % 3}") for i in range(9)]
+    term = tt.PodAffinityTerm("topology.kubernetes.io/zone", tt.LabelSelector({"app": "db"}))
+    cases.append((nodes, [], [tt._pod(f"db{i}", {"app": "db"}, pod_affinity_required=[term]) for i in range(4)]))
+    nodes2 = [tt._node(i, f"z{i % 2}") for i in range(6)]
+    bound2 = [tt._pod("e0", {"app": "x"}, node="n0", pod_anti_affinity_required=[
+        tt.PodAffinityTerm("topology.kubernetes.io/zone", tt.LabelSelector({"app": "y"}))])]
+    cases.append((nodes2, bound2, [tt._pod("y0", {"app": "y"}), tt._pod("x1", {"app": "z"}, pod_anti_affinity_required=[
+        tt.PodAffinityTerm("kubernetes.io/hostname", tt.LabelSelector({"app": "x"}))])]))
+    for nodes, bound, pods in cases:
+        cluster, _ = encode_cluster(nodes, bound)
+        enc = encode_pods(cluster, pods)
+        for pct in (0, 100):
+            prof = _prof(pct)
+            eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+            for i in range(enc.n_pods):
+                _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")

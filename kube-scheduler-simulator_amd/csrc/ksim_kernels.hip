@@ -356,7 +356,10 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     for (int32_t r = lo; r < hi; r++) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (r >= evaluated) s.fail[node] = KSIM_NOT_EVALUATED;
+      if (r >= evaluated) {
+        s.fail[node] = KSIM_NOT_EVALUATED;
+        s.detail[node] = 0;
+      }
       o.scored[node] = 0;
       o.total[node] = 0;
       for (int k = 0; k < S; k++) {

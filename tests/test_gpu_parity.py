@@ -206,10 +206,16 @@ def test_config3_batch(pct):
 
 def test_topology_mixed_with_batchable_pods():
     """Bare pods carrying app labels (batch path; their binds add to the
-    selector classes) interleaved with spread / affinity pods (per-pod path)."""
+    spread constraints' selector classes) interleaved with spread pods
+    (per-pod path).  No pod carries an affinity term, so the bare pods have
+    no topology uses of their own and stay batchable."""
     from ksim.encode import encode_cluster, encode_pods
     from ksim.model import Container, Pod
     nodes, bound, inc = gen.config3_objects(n_nodes=400, pods_per_node=5, n_incoming=600, seed=13)
+    for p in bound:
+        p.pod_anti_affinity_required, p.pod_affinity_preferred = [], []
+    for p in inc:
+        p.pod_anti_affinity_preferred = []
     bare = [Pod(f"bare-{k}", labels={"app": f"a{k % 64}", "tier": "web"},
                 containers=[Container({"cpu": "200m", "memory": "512Mi"})]) for k in range(1200)]
     queue = []

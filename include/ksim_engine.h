@@ -370,6 +370,27 @@ int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* pods, int32_t* chose
  * sequence to 0 (device-side copy; used by sweeps and the bench). */
 int ksim_reset_cluster(ksim_handle* h);
 
+/* ---- node sharding (multi-GPU) -------------------------------
+ * A cluster of n_total nodes (nodeTree order) is split into contiguous shards.
+ * A shard handle holds global positions [node_base, node_base + n_nodes) of
+ * the table given to ksim_set_cluster; tie-break keys, spec.nodeName,
+ * metadata.name selectors and chosen[] use GLOBAL positions.  Sharded runs
+ * take batchable pods (P100, no topology uses) and exchange, per batch of 256
+ * pods, one all-gather of the shards' candidate records (18 KB per shard)
+ * and one all-reduce (max) of 256 pair keys. */
+#define KSIM_COMM_ID_BYTES 128
+/* Must precede ksim_set_cluster. */
+int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total);
+/* One process per GPU over RCCL: rank 0 creates the id (ncclGetUniqueId),
+ * every rank passes the same bytes; ksim_schedule_loaded then runs sharded. */
+int ksim_comm_unique_id(uint8_t* id /* [KSIM_COMM_ID_BYTES] */);
+int ksim_comm_init(ksim_handle* h, int32_t rank, int32_t world, const uint8_t* id);
+/* An in-process group of shard handles on one device (exchanges by device
+ * copies): the same protocol without a communicator.  hs[i] must tile the
+ * cluster in order; chosen / stats as ksim_schedule_loaded (evals summed). */
+int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32_t count,
+                               int32_t* chosen, ksim_batch_stats* stats);
+
 /* ---- measurement ----------------------------------------------------------- */
 /* Schedule loaded pods [first, first+count) exactly as ksim_schedule_loaded
  * would, with a HIP event between every kernel on the engine's stream.

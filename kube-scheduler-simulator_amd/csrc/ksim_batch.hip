@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
     uint64_t kk = 0;
     if (node < c.n) {
       const NodeRow r = load_row(c, node);
-      if (static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq);
+      if (static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
     }
     a[k] = kk;
   }
@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
 __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict__ st,
                                                      const uint64_t* __restrict__ cand, int32_t n_tiles,
                                                      uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
-                                                     int32_t* __restrict__ topk_complete) {
+                                                     int32_t* __restrict__ topk_complete,
+                                                     uint64_t* __restrict__ xsend) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_m[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int32_t j = blockIdx.x * 4 + w;
@@ -122,6 +123,56 @@ __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict_
     topk_cnt[j] = cnt;
     topk_complete[j] = complete;
   }
+  if (xsend) {                                       // sharded: this shard's record for the all-gather
+    uint64_t* x = xsend + (size_t)j * kXRec;
+    if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
+    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)cnt | ((uint64_t)complete << 32);
+  }
+}
+
+// Sharded: merge the R shard records of pod j (all-gathered, [R][B][kXRec])
+// into the pod's global top-T.  Lane l holds entry l % T of shard l / T.  A key
+// is provably in the global order if it is >= the last listed key of every
+// incomplete shard (every key a shard did not list is below its last listed
+// one); the list is complete when every shard was and nothing was dropped.
+__global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict__ st,
+                                                      const uint64_t* __restrict__ xrecv, int32_t world,
+                                                      uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                                      int32_t* __restrict__ topk_complete) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t j = blockIdx.x * 4 + w;
+  const int32_t base = st->cursor;
+  if (base + j >= min(st->end, base + kBatchPods)) return;   // wave-uniform
+  const int sh = lane / kTopT, e = lane % kTopT;
+  uint64_t key = 0, meta = 0;
+  if (sh < world) {
+    const uint64_t* x = xrecv + ((size_t)sh * kBatchPods + j) * kXRec;
+    meta = x[kTopT];
+    key = x[e];
+  }
+  const int32_t cnt = (int32_t)(uint32_t)meta;
+  const bool complete = (meta >> 32) != 0;
+  if (e >= cnt) key = 0;
+  // threshold: the largest "last listed key" over incomplete shards
+  const uint64_t last = (sh < world && !complete && cnt > 0 && e == cnt - 1) ? key : 0;
+  const uint64_t thr = wave_max_u64_dpp(last);
+  const bool all_complete = __ballot(sh < world && e == 0 && !complete) == 0;
+  const bool valid = key != 0 && key >= thr;
+  const uint64_t vm = __ballot(valid);
+  const int nvalid = __popcll(vm);
+  // rank of a valid key among the valid keys (keys are unique: one per node)
+  int rank = 0;
+  for (int l = 0; l < 64; l++) {
+    const uint64_t o = readlane_u64(key, l);
+    if (((vm >> l) & 1ull) && o > key) rank++;
+  }
+  if (valid && rank < kTopT) topk[(size_t)j * kTopT + rank] = key;
+  const int n = nvalid < kTopT ? nvalid : kTopT;
+  if (lane >= n && lane < kTopT) topk[(size_t)j * kTopT + lane] = 0;
+  if (lane == 0) {
+    topk_cnt[j] = n;
+    topk_complete[j] = (all_complete && nvalid <= kTopT) ? 1 : 0;
+  }
 }
 
 // The greedy chain in one wave.  Lanes e < kTopT hold pod i's list entries;
@@ -129,7 +180,7 @@ __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict_
 // read before step i marks its guess (so the read is off the critical path)
 // and patched with that guess by one compare; the list of step i+2 is read
 // two steps ahead.  A step is then a ballot, s_ff1 and readlane.
-__global__ __launch_bounds__(256) void k_batch_chain(const DevState* __restrict__ st, int32_t n_nodes,
+__global__ __launch_bounds__(256) void k_batch_chain(const DevState* __restrict__ st, int32_t n_nodes /* global */,
                                                      const uint64_t* __restrict__ topk,
                                                      const int32_t* __restrict__ topk_cnt,
                                                      const int32_t* __restrict__ topk_complete,
@@ -191,9 +242,60 @@ __global__ __launch_bounds__(256) void k_batch_chain(const DevState* __restrict_
     gkey[i] = (i < nchain && s_gpos[i] >= 0) ? topk[i * kTopT + s_gpos[i]] : 0;
 }
 
+// Validate the chain against M (pmax) and commit (one block of kBatchPods
+// threads).  Binds are applied by the shard that owns the node.
+__device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
+                                             const uint64_t* __restrict__ gkey, const uint64_t* __restrict__ pmax,
+                                             int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
+                                             int32_t* s_sched, int32_t* s_unsched) {
+  const int tid = threadIdx.x;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  const int64_t seq0 = st->pod_seq;
+  if (tid == 0) {
+    *s_istar = nchain;
+    *s_sched = 0;
+    *s_unsched = 0;
+  }
+  __syncthreads();
+  const uint64_t gj = tid < nchain ? __builtin_nontemporal_load(&gkey[tid]) : 0;
+  const uint64_t mj = tid < nchain ? __builtin_nontemporal_load(&pmax[tid]) : 0;
+  if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
+  __syncthreads();
+  const int32_t istar = *s_istar;
+  const int32_t committed = istar < nchain ? istar + 1 : nchain;
+  const int32_t inode = istar < nchain ? key_node(__builtin_nontemporal_load(&pmax[istar])) : -1;
+  if (tid < committed) {
+    const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);     // global position
+    if (chosen_out) chosen_out[base + tid] = node;
+    atomicAdd(node >= 0 ? s_sched : s_unsched, 1);
+    const int32_t local = node - c.base;
+    if (tid < istar && gj && local >= 0 && local < c.n) {   // bound nodes are distinct: one writer each
+      assume_pod(c, P, P.pods[base + tid], local, 1);
+      if (node == inode) assume_pod(c, P, P.pods[base + istar], local, 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    st->cursor = base + committed;
+    st->pod_seq = seq0 + committed;
+    st->evals += (int64_t)committed * c.n;
+    st->scheduled += *s_sched;
+    st->unschedulable += *s_unsched;
+    st->batches += 1;
+    if (committed < nb) {
+      if (istar < nchain) st->cuts += 1;
+      else st->truncations += 1;
+    }
+  }
+}
+
 // Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
-// bound there; M_j = the block max.  The last block to finish validates the
-// chain against M and commits the batch.
+// bound there; M_j = the block max.  Unsharded, the last block to finish
+// validates the chain against M and commits the batch; sharded (SHARDED),
+// each shard scores the guesses it owns and M is all-reduced (max) before
+// k_batch_commit.
+template <bool SHARDED>
 __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
                                                             DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ gkey,
@@ -212,11 +314,13 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
   uint64_t v = 0;
   if (j < nchain && k < j) {
     const uint64_t gk = gkey[k];
-    if (gk) {
-      NodeRow r = load_row(c, key_node(gk));
+    const int32_t local = gk ? key_node(gk) - c.base : -1;
+    if (local >= 0 && local < c.n) {
+      NodeRow r = load_row(c, local);
       row_add_pod(r, P.pods[base + k], 1);
       const ksim_pod& p = P.pods[base + j];
-      if (static_filters_pass(c, P, bp, p, r)) v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j);
+      if (static_filters_pass(c, P, bp, p, r))
+        v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j, c.base);
     }
   }
   if (j < nchain && __syncthreads_or(k < j)) {
@@ -231,48 +335,33 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
   } else if (tid == 0) {
     pmax[j] = 0;
   }
+  if (SHARDED) return;
   // last block: validate and commit
   __threadfence();
   if (tid == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!s_last) return;
   __threadfence();
-  if (tid == 0) {
-    s_istar = nchain;
-    s_sched = 0;
-    s_unsched = 0;
-    *done = 0;                                          // re-arm for the next batch
-  }
-  __syncthreads();
-  const uint64_t gj = tid < nchain ? __builtin_nontemporal_load(&gkey[tid]) : 0;
-  const uint64_t mj = tid < nchain ? __builtin_nontemporal_load(&pmax[tid]) : 0;
-  if (tid < nchain && mj > gj) atomicMin(&s_istar, tid);   // keys are unique per node: never equal unless 0
-  __syncthreads();
-  const int32_t istar = s_istar;
-  const int32_t committed = istar < nchain ? istar + 1 : nchain;
-  const int32_t inode = istar < nchain ? key_node(__builtin_nontemporal_load(&pmax[istar])) : -1;
-  if (tid < committed) {
-    const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);
-    if (chosen_out) chosen_out[base + tid] = node;
-    atomicAdd(node >= 0 ? &s_sched : &s_unsched, 1);
-    if (tid < istar && gj) {                            // bound nodes are distinct: one writer each
-      assume_pod(c, P, P.pods[base + tid], node, 1);
-      if (node == inode) assume_pod(c, P, P.pods[base + istar], node, 1);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    st->cursor = base + committed;
-    st->pod_seq = seq0 + committed;
-    st->evals += (int64_t)committed * c.n;
-    st->scheduled += s_sched;
-    st->unschedulable += s_unsched;
-    st->batches += 1;
-    if (committed < nb) {
-      if (istar < nchain) st->cuts += 1;
-      else st->truncations += 1;
-    }
-  }
+  if (tid == 0) *done = 0;                              // re-arm for the next batch
+  batch_commit(c, P, st, gkey, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched);
+}
+
+__global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
+                                                             const uint64_t* __restrict__ gkey,
+                                                             const int32_t* __restrict__ chain_end,
+                                                             const uint64_t* __restrict__ pmax,
+                                                             int32_t* __restrict__ chosen_out) {
+  __shared__ int32_t s_istar, s_sched, s_unsched;
+  if (min(kBatchPods, st->end - st->cursor) <= 0) return;
+  batch_commit(c, P, st, gkey, pmax, *chain_end, chosen_out, &s_istar, &s_sched, &s_unsched);
+}
+
+// In-process shard group: M = max over the group's pmax arrays, written back to each.
+__global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {
+  const int j = threadIdx.x;
+  uint64_t m = 0;
+  for (int r = 0; r < g.n; r++) m = umax64(m, g.p[r][j]);
+  for (int r = 0; r < g.n; r++) g.p[r][j] = m;
 }
 
 const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_eval", "k_batch_merge", "k_batch_chain",
@@ -286,14 +375,38 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[1], stream);
   const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
-                                                               a.s.topk_complete);
+                                                               a.s.topk_complete, nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_batch_chain<<<1, 256, 0, stream>>>(a.st, a.c.n, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+  k_batch_chain<<<1, 256, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
                                        a.s.chain_end);
   if (evs) (void)hipEventRecord(evs[3], stream);
-  k_batch_pairs<<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
-                                                       a.s.pmax, a.s.done, a.chosen);
+  k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+                                                              a.s.pmax, a.s.done, a.chosen);
   if (evs) (void)hipEventRecord(evs[4], stream);
 }
+
+void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
+  const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
+  const dim3 g1((n_tiles + 3) / 4, kBatchPods);
+  k_batch_eval<<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
+  k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
+                                                               a.s.topk_complete, a.s.xsend);
+}
+
+void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {
+  k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
+                                                     a.s.topk_complete);
+  k_batch_chain<<<1, 256, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                       a.s.chain_end);
+  k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+                                                             a.s.pmax, a.s.done, a.chosen);
+}
+
+void launch_shard_commit(const LaunchArgs& a, hipStream_t stream) {
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+}
+
+void launch_group_max(const GroupPtrs& g, hipStream_t stream) { k_group_max<<<1, kBatchPods, 0, stream>>>(g); }
 
 }  // namespace ksim

@@ -26,7 +26,10 @@ constexpr int kMaxNodeScore = 100;
 // the bind step of every cycle (NodeInfo.AddPod), never re-uploaded.
 struct DevCluster {
   int32_t n, n_scalar, n_label_cols, n_taints;
-  int32_t n_label_values, n_prefer_taints, _pad[2];
+  // node sharding: this snapshot holds global positions [base, base + n) of
+  // n_total nodes.  Memory is indexed by the LOCAL position; tie-break keys,
+  // spec.nodeName and metadata.name field selectors use the GLOBAL one.
+  int32_t n_label_values, n_prefer_taints, base, n_total;
   const int64_t* alloc_cpu;
   const int64_t* alloc_mem;
   const int64_t* alloc_eph;
@@ -109,6 +112,8 @@ struct DevScratch {
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
   uint32_t* done;        // batch path: k_batch_pairs blocks finished (last-block election)
+  uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
+  uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records
   int64_t* dom;          // [KSIM_MAX_USES][vmax] topology-pair sums of the current pod (zero between pods)
   int64_t* min_match;    // [KSIM_MAX_USES] PTS hard: critical-path minimum
 };
@@ -253,11 +258,11 @@ __device__ __forceinline__ bool label_req_matches(const DevCluster& c, const ksi
       return op == KSIM_OP_GT ? (c.label_num[idx] > e.num) : (c.label_num[idx] < e.num);
     }
     case KSIM_OP_FIELD_IN: {
-      for (int k = 0; k < e.nvals; k++) if ((int32_t)e.vals[k] == node) return true;
+      for (int k = 0; k < e.nvals; k++) if ((int32_t)e.vals[k] == c.base + node) return true;
       return false;
     }
     case KSIM_OP_FIELD_NOT_IN: {
-      for (int k = 0; k < e.nvals; k++) if ((int32_t)e.vals[k] == node) return false;
+      for (int k = 0; k < e.nvals; k++) if ((int32_t)e.vals[k] == c.base + node) return false;
       return true;
     }
     case KSIM_OP_TRUE: return true;
@@ -453,7 +458,7 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
           return (uint8_t)f;
         break;
       case KSIM_PL_NODE_NAME:
-        if (p.node_name != -1 && p.node_name != node) return (uint8_t)f;
+        if (p.node_name != -1 && p.node_name != c.base + node) return (uint8_t)f;
         break;
       case KSIM_PL_TAINT_TOLERATION: {
         uint32_t tid = find_matching_untolerated_taint(c, p, r);
@@ -735,7 +740,7 @@ __device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const D
         if ((r.flags & KSIM_NODE_UNSCHEDULABLE) && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE)) return false;
         break;
       case KSIM_PL_NODE_NAME:
-        if (p.node_name != -1 && p.node_name != r.node) return false;
+        if (p.node_name != -1 && p.node_name != c.base + r.node) return false;
         break;
       case KSIM_PL_TAINT_TOLERATION:
         if (find_matching_untolerated_taint(c, p, r)) return false;
@@ -752,13 +757,14 @@ __device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const D
 
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).
 __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
-                                            int32_t norm_const, const NodeRow& r, int n_scalar, int64_t seq) {
+                                            int32_t norm_const, const NodeRow& r, int n_scalar, int64_t seq,
+                                            int32_t base) {
   if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
   int64_t tot = norm_const;
   if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);
   if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, n_scalar);
   if (prof.n_score == 0) tot = 1;
-  return tb_key(tot, prof.tiebreak_seed, seq, r.node);
+  return tb_key(tot, prof.tiebreak_seed, seq, base + r.node);
 }
 
 __device__ __forceinline__ void row_add_pod(NodeRow& r, const ksim_pod& p, int sign) {

@@ -7,7 +7,9 @@
 // path is a captured hipGraph replayed until the run's cursor is consumed.
 // Every input is validated on the host before any kernel sees it (a bad index
 // must never reach the device), copied during the call, never retained.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -22,6 +24,39 @@ using namespace ksim;
 namespace {
 
 constexpr int kGraphCycles = 128;      // per-pod cycles per captured graph
+
+// RCCL, resolved at run time: the process may already hold torch's librccl
+// (RTLD_NOLOAD finds it first, so both share one RCCL and one HIP runtime).
+struct Rccl {
+  bool ok = false;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* lib = nullptr;
+    for (const char* name : {"librccl.so", "librccl.so.1"})
+      if (!lib) lib = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if (!lib) lib = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+    if (!lib) return x;
+    x.get_unique_id = (decltype(x.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+    x.comm_init_rank = (decltype(x.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+    x.comm_destroy = (decltype(x.comm_destroy))dlsym(lib, "ncclCommDestroy");
+    x.all_gather = (decltype(x.all_gather))dlsym(lib, "ncclAllGather");
+    x.all_reduce = (decltype(x.all_reduce))dlsym(lib, "ncclAllReduce");
+    x.error_string = (decltype(x.error_string))dlsym(lib, "ncclGetErrorString");
+    x.ok = x.get_unique_id && x.comm_init_rank && x.comm_destroy && x.all_gather && x.all_reduce && x.error_string;
+    return x;
+  }();
+  return r;
+}
 constexpr int kGraphBatches = 16;      // speculative batches per captured graph
 
 struct DevBuf {
@@ -69,6 +104,11 @@ struct ksim_handle {
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
+
+  // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
+  int32_t shard_base = 0, shard_total = 0;
+  int32_t rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
 
   hipGraphExec_t graph_cycle = nullptr;        // per-pod cycles, pods without topology uses
   hipGraphExec_t graph_cycle_topo = nullptr;   // per-pod cycles incl. the topology kernels
@@ -132,7 +172,7 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
   const DevCluster& c = h->dc;
   if (p.flags & (KSIM_POD_HAS_HOST_PORTS | KSIM_POD_HAS_VOLUMES))
     return set_err(h, KSIM_E_UNSUPPORTED, "pod " + std::to_string(i) + ": host ports / volumes not supported by the engine");
-  if (p.node_name < -2 || p.node_name >= c.n)
+  if (p.node_name < -2 || p.node_name >= c.n_total)
     return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": node_name out of range");
   auto check_expr = [&](int32_t e) -> bool {
     if (e < 0 || e >= ps->n_exprs) return false;
@@ -327,6 +367,79 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
   return KSIM_OK;
 }
 
+// ---- node-sharded batch path ----------------------------------
+// One batch on every shard of a group, phases separated by the two exchanges:
+// all-gather of the per-shard candidate records, all-reduce (max) of the pair
+// keys.  `hs` is either {this rank's handle} with an RCCL communicator (one
+// process per GPU) or an in-process group of shard handles on one device
+// (exchanges by device copies).  Everything runs on `stream`, asynchronously.
+int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+  const int R = (int)hs.size();
+  ksim_handle* h0 = hs[0];
+  const size_t rec = (size_t)kBatchPods * kXRec;            // u64 per shard
+  for (auto* h : hs) launch_shard_eval(make_args(h, h->dp, h->d_chosen), stream);
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+  } else {
+    for (int src = 0; src < R; src++)
+      for (int dst = 0; dst < R; dst++)
+        HIPCHK(h0, hipMemcpyAsync(hs[dst]->sc.xrecv + (size_t)src * rec, hs[src]->sc.xsend, 8 * rec,
+                                  hipMemcpyDeviceToDevice, stream));
+  }
+  const int32_t world = h0->comm ? h0->world : R;
+  for (auto* h : hs) launch_shard_chain(make_args(h, h->dp, h->d_chosen), world, stream);
+  if (h0->comm) {
+    const ncclResult_t r =
+        rccl().all_reduce(h0->sc.pmax, h0->sc.pmax, kBatchPods, ncclUint64, ncclMax, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllReduce: ") + rccl().error_string(r));
+  } else if (R > 1) {
+    GroupPtrs g{};
+    g.n = R;
+    for (int i = 0; i < R; i++) g.p[i] = hs[i]->sc.pmax;
+    launch_group_max(g, stream);
+  }
+  for (auto* h : hs) launch_shard_commit(make_args(h, h->dp, h->d_chosen), stream);
+  HIPCHK(h0, hipGetLastError());
+  return KSIM_OK;
+}
+
+// Pods [a, b) on the sharded batch path (every pod must be batchable).  No
+// batch is ever issued past the run's end (each commits 1..kBatchPods pods).
+int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
+  ksim_handle* h0 = hs[0];
+  hipStream_t stream = h0->stream;
+  for (auto* h : hs) {
+    int rc;
+    if ((rc = set_run(h, a, b))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  int32_t cursor = a;
+  while (cursor < b) {
+    const int32_t n = std::max(1, (b - cursor) / kBatchPods);
+    for (int32_t i = 0; i < n; i++) {
+      int rc = shard_batch(hs, stream);
+      if (rc) return rc;
+    }
+    DevState st;
+    HIPCHK(h0, hipMemcpyAsync(&st, h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));
+    HIPCHK(h0, hipStreamSynchronize(stream));
+    if (st.cursor <= cursor) return set_err(h0, KSIM_E_DEVICE, "sharded batch path made no progress");
+    cursor = st.cursor;
+  }
+  return KSIM_OK;
+}
+
+bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
+
+int reset_counters(ksim_handle* h, hipStream_t stream) {
+  HIPCHK(h, hipMemsetAsync(&h->st->truncations, 0, 4, stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->evals, 0, 3 * sizeof(int64_t), stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, stream));
+  HIPCHK(h, hipMemsetAsync(&h->st->cuts, 0, 8, stream));
+  return KSIM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -373,6 +486,7 @@ void ksim_destroy(ksim_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   drop_graphs(h);
+  if (h->comm && rccl().ok) (void)rccl().comm_destroy(h->comm);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
   free_bufs(h->pod_bufs);
@@ -472,7 +586,12 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   h->topo.clear();
   h->has_cluster = false;
 
+  const int32_t n_total = h->shard_total ? h->shard_total : n;
+  if (h->shard_base < 0 || h->shard_base + n > n_total || n_total > KSIM_MAX_NODES)
+    return set_err(h, KSIM_E_INVALID, "shard range outside the cluster (ksim_set_shard)");
   DevCluster c{};
+  c.base = h->shard_base;
+  c.n_total = n_total;
   c.n_classes = t->n_classes;
   c.n_topo_log = v->n_topo_log;
   c.vmax = vmax;
@@ -556,6 +675,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.done, uint32_t*, 4);
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
+  SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);
+  SCR(s.xrecv, uint64_t*, 8 * (size_t)kMaxShards * kBatchPods * kXRec);
   SCR(s.min_match, int64_t*, 8 * (size_t)KSIM_MAX_USES);
   SCR(o.scored, uint8_t*, N);
   SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
@@ -789,16 +910,20 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   if (!h->dp.pods && count > 0) return set_err(h, KSIM_E_INVALID, "no pods loaded");
   if (first < 0 || count < 0 || first + count > h->dp.n_pods) return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemsetAsync(&h->st->truncations, 0, 4, h->stream));
-  HIPCHK(h, hipMemsetAsync(&h->st->evals, 0, 3 * sizeof(int64_t), h->stream));
-  HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
-  HIPCHK(h, hipMemsetAsync(&h->st->cuts, 0, 8, h->stream));
+  if ((rc = reset_counters(h, h->stream))) return rc;
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
-    if (!batch) perpod += b - a;
-    return run_range(h, a, b, batch, topo);
-  });
+  if (is_sharded(h)) {
+    for (int32_t i = first; i < first + count; i++)
+      if (!h->batchable[i])
+        return set_err(h, KSIM_E_UNSUPPORTED, "node-sharded runs take batchable pods only (P100, no topology uses)");
+    if (count && (rc = shard_run({h}, first, first + count))) return rc;
+  } else {
+    rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
+      if (!batch) perpod += b - a;
+      return run_range(h, a, b, batch, topo);
+    });
+  }
   if (rc) return rc;
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -817,6 +942,95 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
     stats->batches = st.batches;
     stats->truncations = st.truncations;
     stats->perpod_cycles = perpod;
+  }
+  return KSIM_OK;
+}
+
+int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total) {
+  if (!h) return KSIM_E_INVALID;
+  if (node_base < 0 || n_total < 0 || n_total > KSIM_MAX_NODES || node_base > n_total)
+    return set_err(h, KSIM_E_INVALID, "bad shard range");
+  if (h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_set_shard must precede ksim_set_cluster");
+  h->shard_base = node_base;
+  h->shard_total = n_total;
+  return KSIM_OK;
+}
+
+int ksim_comm_unique_id(uint8_t* id) {
+  if (!id) return KSIM_E_INVALID;
+  if (!rccl().ok) return KSIM_E_RCCL;
+  ncclUniqueId u;
+  if (rccl().get_unique_id(&u) != ncclSuccess) return KSIM_E_RCCL;
+  std::memcpy(id, u.internal, KSIM_COMM_ID_BYTES);
+  return KSIM_OK;
+}
+
+int ksim_comm_init(ksim_handle* h, int32_t rank, int32_t world, const uint8_t* id) {
+  if (!h || !id) return KSIM_E_INVALID;
+  if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
+    return set_err(h, KSIM_E_INVALID, "world must be 1.." + std::to_string(kMaxShards));
+  if (!rccl().ok) return set_err(h, KSIM_E_RCCL, "librccl not found");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (h->comm) (void)rccl().comm_destroy(h->comm);
+  h->comm = nullptr;
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, KSIM_COMM_ID_BYTES);
+  const ncclResult_t r = rccl().comm_init_rank(&h->comm, world, u, rank);
+  if (r != ncclSuccess) {
+    h->comm = nullptr;
+    return set_err(h, KSIM_E_RCCL, std::string("ncclCommInitRank: ") + rccl().error_string(r));
+  }
+  h->rank = rank;
+  h->world = world;
+  return KSIM_OK;
+}
+
+int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32_t count, int32_t* chosen,
+                               ksim_batch_stats* stats) {
+  if (!hs || n < 1 || n > kMaxShards) return KSIM_E_INVALID;
+  ksim_handle* h0 = hs[0];
+  std::vector<ksim_handle*> v(hs, hs + n);
+  int32_t expect = 0;
+  for (auto* h : v) {
+    int rc = ensure_ready(h);
+    if (rc) return rc;
+    if (h->comm) return set_err(h0, KSIM_E_INVALID, "group handles must not hold a communicator");
+    if (h->device != h0->device) return set_err(h0, KSIM_E_INVALID, "group handles must share one device");
+    if (!h->dp.pods || h->dp.n_pods != h0->dp.n_pods) return set_err(h0, KSIM_E_INVALID, "pods not loaded alike");
+    if (h->dc.n_total != h0->dc.n_total || h->dc.base != expect)
+      return set_err(h0, KSIM_E_INVALID, "shards must tile the cluster in order");
+    expect += h->dc.n;
+  }
+  if (expect != h0->dc.n_total) return set_err(h0, KSIM_E_INVALID, "shards must tile the cluster");
+  if (first < 0 || count < 0 || first + count > h0->dp.n_pods) return set_err(h0, KSIM_E_INVALID, "range out of loaded pods");
+  for (int32_t i = first; i < first + count; i++)
+    if (!h0->batchable[i]) return set_err(h0, KSIM_E_UNSUPPORTED, "node-sharded runs take batchable pods only");
+  HIPCHK(h0, hipSetDevice(h0->device));
+  int rc;
+  for (auto* h : v)
+    if ((rc = reset_counters(h, h->stream))) return rc;
+  HIPCHK(h0, hipEventRecord(h0->ev0, h0->stream));
+  if (count && (rc = shard_run(v, first, first + count))) return rc;
+  HIPCHK(h0, hipEventRecord(h0->ev1, h0->stream));
+  HIPCHK(h0, hipEventSynchronize(h0->ev1));
+  if (chosen && count) HIPCHK(h0, hipMemcpy(chosen, h0->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    for (auto* h : v) {
+      DevState st;
+      if ((rc = read_state(h, st))) return rc;
+      stats->evals += st.evals;                // each shard counts its own nodes
+      if (h == h0) {
+        stats->scheduled = st.scheduled;
+        stats->unschedulable = st.unschedulable;
+        stats->batches = st.batches;
+        stats->truncations = st.truncations;
+      }
+    }
+    float ms = 0;
+    HIPCHK(h0, hipEventElapsedTime(&ms, h0->ev0, h0->ev1));
+    stats->pods = count;
+    stats->device_ms = ms;
   }
   return KSIM_OK;
 }

@@ -13,6 +13,15 @@ static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch 
 constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
 constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
 constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
+constexpr int kXRec = kTopT + 1;   // sharded exchange record per pod: T keys + (count | complete << 32)
+constexpr int kMaxShards = 64 / kTopT;   // k_batch_gmerge holds every shard's list in one wave
+static_assert(kTopT * kMaxShards <= 64, "gmerge geometry");
+
+// In-process shard group (one device): the pmax arrays of up to kMaxShards handles.
+struct GroupPtrs {
+  uint64_t* p[kMaxShards];
+  int32_t n;
+};
 
 struct LaunchArgs {
   DevCluster c;
@@ -37,6 +46,16 @@ extern const char* const kBatchKernelNames[kKernelsPerBatch];
 void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+// Sharded batch (node shards; the caller exchanges between the phases):
+//   launch_shard_eval    eval + merge; writes this shard's records to s.xsend
+//   (all-gather s.xsend -> s.xrecv [world][kBatchPods][kXRec])
+//   launch_shard_chain   global merge + chain + pair keys of owned guesses -> s.pmax
+//   (all-reduce max s.pmax)
+//   launch_shard_commit  validate + commit (owner shard binds)
+void launch_shard_eval(const LaunchArgs& a, hipStream_t stream);
+void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream);
+void launch_shard_commit(const LaunchArgs& a, hipStream_t stream);
+void launch_group_max(const GroupPtrs& g, hipStream_t stream);
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream);
 
 }  // namespace ksim

@@ -470,11 +470,11 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         o.total[node] = tot;
         o.scored[node] = 1;
       }
-      const uint64_t key = tb_key(tot, prof.tiebreak_seed, seq, node);
+      const uint64_t key = tb_key(tot, prof.tiebreak_seed, seq, c.base + node);
       best = key > best ? key : best;
     }
     best = block_max_u64<kFinalWaves>(best, shu);
-    chosen = key_node(best);
+    chosen = key_node(best) - c.base;               // the per-pod path is never sharded: base == 0
   }
 
   // Restore the all-zero domain tables for the next pod (every entry this
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     } else {
       st->unschedulable += 1;
     }
-    if (chosen_out) chosen_out[pi] = chosen;
+    if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : -1;
     st->chosen = chosen;
     st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : KSIM_STATUS_UNSCHEDULABLE;
     st->n_feasible = nf;

@@ -192,6 +192,22 @@ class EncodedCluster:
         v.topo_log = abi._p(self.topo_log)
         return v
 
+    def shard(self, base: int, count: int) -> "EncodedCluster":
+        """Nodes [base, base + count) as a shard snapshot: the
+        same vocabularies, the node columns sliced.  Positions stay global
+        (the engine is told the base by ksim_set_shard)."""
+        import copy
+        sl = slice(base, base + count)
+        c = copy.copy(self)
+        c.n_nodes = count
+        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "req_eph",
+                  "nz_cpu", "nz_mem", "num_pods", "flags"):
+            setattr(c, f, np.ascontiguousarray(getattr(self, f)[sl]))
+        for f in ("alloc_scalar", "req_scalar", "taints", "labels", "class_count"):
+            setattr(c, f, np.ascontiguousarray(getattr(self, f)[:, sl]))
+        c.node_names = self.node_names[sl]
+        return c
+
     def label_col(self, key: str) -> int:
         return self.label_keys.index(key) if key in self.label_keys else -1
 

@@ -24,6 +24,7 @@ EXPORTS = [
     "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
     "ksim_time_kernels", "ksim_kernel_name", "ksim_get_diag", "ksim_batch_geometry",
+    "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
 ]
 
 
@@ -68,6 +69,10 @@ def lib():
         L.ksim_kernel_name.restype = ctypes.c_char_p
         L.ksim_get_diag.argtypes = [vp, vp, i32]
         L.ksim_batch_geometry.argtypes = [vp, i32]
+        L.ksim_set_shard.argtypes = [vp, i32, i32]
+        L.ksim_comm_unique_id.argtypes = [vp]
+        L.ksim_comm_init.argtypes = [vp, i32, i32, vp]
+        L.ksim_group_schedule_loaded.argtypes = [vp, i32, i32, i32, vp, vp]
         _LIB = L
     return _LIB
 
@@ -78,6 +83,30 @@ def batch_geometry() -> dict:
     lib().ksim_batch_geometry(out.ctypes.data_as(ctypes.c_void_p), 4)
     return {"pods_per_batch": int(out[0]), "top_t": int(out[1]), "tile_nodes": int(out[2]),
             "tile_cand": int(out[3])}
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId through the engine (rank 0 of a node-sharded run)."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    rc = lib().ksim_comm_unique_id(buf)
+    if rc != 0:
+        raise KsimError(rc, "ksim_comm_unique_id failed (librccl?)")
+    return bytes(buf)
+
+
+def group_schedule_loaded(engines, first: int, count: int):
+    """In-process shard group on one device (ksim_group_schedule_loaded)."""
+    arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+    chosen = np.zeros(count, np.int32)
+    st = abi.BatchStats()
+    rc = lib().ksim_group_schedule_loaded(arr, len(engines), first, count,
+                                          chosen.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+    if rc != 0:
+        raise KsimError(rc, lib().ksim_last_error(engines[0].h).decode())
+    return chosen, st
 
 
 class Engine:
@@ -103,6 +132,14 @@ class Engine:
         self.h = None
 
     __del__ = close
+
+    def set_shard(self, node_base: int, n_total: int):
+        """This handle holds global node positions [node_base, node_base + n) of n_total."""
+        self._chk(lib().ksim_set_shard(self.h, node_base, n_total))
+
+    def comm_init(self, rank: int, world: int, uid: bytes):
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        self._chk(lib().ksim_comm_init(self.h, rank, world, buf))
 
     def set_profile(self, prof: abi.Profile):
         self._chk(lib().ksim_set_profile(self.h, ctypes.byref(prof)))

@@ -1,0 +1,102 @@
+"""Node-sharded batch path on the GPU, bit-exact vs the oracle
+on the whole cluster.  One MI355X: the in-process shard group exercises the
+full exchange protocol (candidate all-gather, pair-key max all-reduce, owner
+binds); the RCCL communicator is exercised with world = 1."""
+import numpy as np
+import pytest
+
+from ksim import engine, gen, profile
+from ksim.engine import Engine, group_schedule_loaded
+from ksim.shard import partition
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _prof(weights=None, seed=0x4B53494D):
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100, tiebreak_seed=seed)
+    if weights:
+        sp = sp.with_weights(weights)
+    return profile.compile_profile(sp)
+
+
+def _group(cluster, pods, prof, world):
+    engines = []
+    for base, cnt in partition(cluster.n_nodes, world):
+        e = Engine(0)
+        e.set_shard(base, cluster.n_nodes)
+        e.set_profile(prof)
+        e.set_cluster(cluster.shard(base, cnt))
+        e.load_pods(pods)
+        engines.append(e)
+    return engines
+
+
+def _node_state(engines):
+    parts = [e.node_state() for e in engines]
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_group_config2_slice(world):
+    cluster, pods = gen.config2(n_nodes=2000, n_pods=3000)
+    prof = _prof()
+    engines = _group(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    es, os_ = _node_state(engines), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+
+
+@pytest.mark.parametrize("n_nodes,world", [(9, 2), (65, 4), (300, 3), (1031, 8)])
+def test_group_ragged_until_full(n_nodes, world):
+    """Ragged shards, pods that stop fitting (unschedulable), batches cut short."""
+    cluster, _ = gen.config2(n_nodes=n_nodes, n_pods=1)
+    pods = gen.bare_pods(n_nodes * 120 + 37, seed=99)    # > 110 pods per node: some never fit
+    prof = _prof()
+    engines = _group(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.unschedulable == ost.unschedulable and st.unschedulable > 0
+
+
+def test_group_truncation_and_cuts():
+    cluster, _ = gen.config2(n_nodes=300, n_pods=1)
+    pods = gen.bare_pods(4000, seed=17, cpu_steps=20, mem_steps=2)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    w = {p.name: (10 if p.name == "NodeResourcesBalancedAllocation" else 1) for p in sp.score_plugins()}
+    prof = profile.compile_profile(sp.with_weights(w))
+    engines = _group(cluster, pods, prof, 4)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ochosen, _ = Oracle(cluster, prof).schedule(pods)
+    np.testing.assert_array_equal(chosen, ochosen)
+    cluster2, _ = gen.config2(n_nodes=40, n_pods=1)
+    cluster2.alloc_cpu[:] = 64000
+    cluster2.alloc_mem[:] = 256 << 30
+    pods2 = gen.bare_pods(3000, seed=5, cpu_steps=1, mem_steps=1)
+    engines = _group(cluster2, pods2, _prof(), 3)
+    chosen, st = group_schedule_loaded(engines, 0, pods2.n_pods)
+    np.testing.assert_array_equal(chosen, Oracle(cluster2, _prof()).schedule(pods2)[0])
+    assert st.truncations > 0
+
+
+def test_rccl_world1():
+    """ksim_comm_init + the RCCL exchange calls with a single rank."""
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=2000)
+    prof = _prof()
+    uid = engine.comm_unique_id()
+    e = Engine(0)
+    e.set_shard(0, cluster.n_nodes)
+    e.set_profile(prof)
+    e.set_cluster(cluster)
+    e.comm_init(0, 1, uid)
+    e.load_pods(pods)
+    chosen, st = e.schedule_loaded(0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals

@@ -1,18 +1,25 @@
 #!/usr/bin/env python3
 """bench.py — pod x node filter+score evaluations/s of the scheduling cycle on MI355X.
 
-Metric and config: BASELINE.json ("pod x node filter+score evals/sec and pods
-scheduled/sec"; configs[1] = default profile, 5,000 nodes x 50,000 pods on one
-MI355X).  One step = one full pass of that workload: reset the node snapshot
-to empty (device-side copy) and run all 50,000 scheduling cycles (Filter over
-every node, Score, NormalizeScore, weights, selectHost, bind) on the engine.
+Metric (BASELINE.json): pod x node filter+score evals/sec (pods scheduled/sec
+reported beside it).  One step = one full pass of the workload on the engine:
+reset the node snapshot (device-side copy) and run every scheduling cycle
+(Filter over every node, Score, NormalizeScore, weights, selectHost, bind).
 Inputs (cluster SoA + pod queue) are resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W] [--mode p100|adapt]
+  python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5] [--mode p100|adapt]
 
-N > 1 (torch.distributed.run, one rank per GPU): every rank runs the same
-workload under its own score-weight vector (config 5 policy sweep: independent
-profiles per GPU, no data-path collective) -> "scaling": "weak".
+Workloads:
+  config 2 (default)  N = 1: 5,000 nodes x 50,000 pods, default profile, P100.
+                      N > 1: node-sharded weak scaling, --nodes-per-gpu (5,000)
+                      x N nodes, the same 50,000 pods; one process per GPU, per
+                      batch an RCCL all-gather of candidates + all-reduce (max).
+  config 3            PodTopologySpread + InterPodAffinity heavy (10k nodes, 3
+                      zones, 100k existing pods with anti-affinity terms), per-pod
+                      path; N > 1 runs independent replicas.
+  config 4            100,000 nodes x 1M pods, node-sharded over N GPUs (strong).
+  config 5            policy sweep: 1,024 score-weight vectors over config 2
+                      (first 10,000 pods), vectors split over the N GPUs.
 """
 from __future__ import annotations
 
@@ -60,7 +67,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 EVAL_KERNELS = ("k_batch_eval", "k_filter_score")
 
 
-def cpu_baseline(cluster, pods, sp, seconds: float, threads: int) -> dict:
+def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) -> dict:
     """The CPU restatement (oracle, OpenMP over nodes) on a bounded sample."""
     from ksim import profile
     from oracle.oracle import Oracle
@@ -75,9 +82,42 @@ def cpu_baseline(cluster, pods, sp, seconds: float, threads: int) -> dict:
     dt2 = time.perf_counter() - t
     return {"value": st2.evals / dt2, "unit": "pod x node evals/s", "cores": threads, "kind": "port",
             "pods_per_s": n / dt2,
-            "sample": f"config-2 pods 100..{100 + n} ({n} cycles, {st2.evals} evals) after 100 warm cycles "
+            "sample": f"{label} pods 100..{100 + n} ({n} cycles, {st2.evals} evals) after 100 warm cycles "
                       f"from the empty cluster, same profile/mode, oracle/ksim_oracle.c OpenMP {threads} threads, "
                       f"{dt2:.1f} s"}
+
+
+def build(cfg: int, args, rank: int, world: int):
+    """(cluster, pods, profile, description, sharded, scaling) for one rank."""
+    from ksim import gen, profile
+    pct = 100 if args.mode == "p100" else 0
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=pct)
+    if cfg == 2:
+        n = args.nodes if world == 1 else args.nodes_per_gpu * world
+        cluster, pods = gen.config2(n, args.pods)
+        desc = f"config2: default profile, {n} nodes x {pods.n_pods} pods, {args.mode.upper()}"
+        if world > 1:
+            desc += f", node-sharded {world} x {args.nodes_per_gpu} nodes (weak scaling)"
+        return cluster, pods, sp, desc, world > 1, "weak"
+    if cfg == 4:
+        cluster, pods = gen.config4(args.nodes4, args.pods4)
+        desc = f"config4: default profile, {cluster.n_nodes} nodes x {pods.n_pods} pods, {args.mode.upper()}, " \
+               f"node-sharded over {world} GPU(s)"
+        return cluster, pods, sp, desc, world > 1, "strong"
+    if cfg == 3:
+        cluster, pods = gen.config3(n_nodes=args.nodes3, n_incoming=args.pods3)
+        desc = (f"config3: default profile, {cluster.n_nodes} nodes / 3 zones, "
+                f"{int(cluster.num_pods.sum())} existing pods with anti-affinity terms, {pods.n_pods} incoming "
+                f"pods with spread constraints + preferred anti-affinity, {args.mode.upper()}")
+        if world > 1:
+            desc += f", {world} independent replicas"
+        return cluster, pods, sp, desc, False, "weak"
+    if cfg == 5:
+        cluster, pods = gen.config2(5000, 10000)
+        desc = f"config5: {args.sweep} score-weight vectors over 5000 nodes x 10000 pods, {args.mode.upper()}, " \
+               f"vectors split over {world} GPU(s)"
+        return cluster, pods, sp, desc, False, "strong"
+    raise SystemExit(f"unknown config {cfg}")
 
 
 def main():
@@ -85,9 +125,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--mode", choices=["p100", "adapt"], default="p100")
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=50000)
+    ap.add_argument("--nodes-per-gpu", type=int, default=5000)
+    ap.add_argument("--nodes3", type=int, default=10000)
+    ap.add_argument("--pods3", type=int, default=10000)
+    ap.add_argument("--nodes4", type=int, default=100000)
+    ap.add_argument("--pods4", type=int, default=1000000)
+    ap.add_argument("--sweep", type=int, default=1024)
+    ap.add_argument("--force-shard", action="store_true",
+                    help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
@@ -107,26 +156,50 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-    from ksim import engine, gen, profile
+    from ksim import engine, gen, profile, shard
+
     engine.lib()
-
-    cluster, pods = gen.config2(args.nodes, args.pods)
-    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100 if args.mode == "p100" else 0)
-    if world > 1:
-        w = gen.config5_weights()[rank % 1024]
-        names = [p.name for p in sp.score_plugins()]
-        sp = sp.with_weights({n: int(x) for n, x in zip(names, w)})
+    cfg = args.config
+    cluster, pods, sp, desc, sharded, scaling = build(cfg, args, rank, world)
     prof = profile.compile_profile(sp)
+    if args.force_shard and cfg in (2, 4):
+        sharded = True
+        desc += " [sharded path forced]"
 
-    eng = engine.Engine(local)
-    eng.set_profile(prof)
-    eng.set_cluster(cluster)
+    if sharded:
+        uid = shard.broadcast_unique_id(dist, rank) if world > 1 else engine.comm_unique_id()
+        eng = shard.sharded_engine(cluster, prof, rank, world, local, uid)
+    else:
+        eng = engine.Engine(local)
+        eng.set_profile(prof)
+        eng.set_cluster(cluster)
     eng.load_pods(pods)
 
-    def step():
-        eng.reset_cluster()
-        _, st = eng.schedule_loaded(0, pods.n_pods, want_chosen=False)
-        return st
+    if cfg == 5:
+        weights = gen.config5_weights(args.sweep)[rank::world]
+        names = [p.name for p in sp.score_plugins()]
+        profs = [profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, w)})) for w in weights]
+
+        def step():
+            agg = None
+            for pr in profs:
+                eng.set_profile(pr)
+                eng.load_pods(pods)
+                eng.reset_cluster()
+                _, st = eng.schedule_loaded(0, pods.n_pods, want_chosen=False)
+                if agg is None:
+                    agg = st
+                else:
+                    for f in ("pods", "scheduled", "unschedulable", "evals", "batches", "truncations",
+                              "perpod_cycles"):
+                        setattr(agg, f, getattr(agg, f) + getattr(st, f))
+                    agg.device_ms += st.device_ms
+            return agg
+    else:
+        def step():
+            eng.reset_cluster()
+            _, st = eng.schedule_loaded(0, pods.n_pods, want_chosen=False)
+            return st
 
     for i in range(args.warmup):
         st = step()
@@ -156,28 +229,41 @@ def main():
         elapsed = float(t.item())
         c = torch.tensor([evals, cycles], dtype=torch.float64, device="cuda")
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        evals, cycles = int(c[0].item()), int(c[1].item())
+        evals = int(c[0].item())
+        # sharded: every rank ran the same cycles (count them once)
+        cycles = int(c[1].item()) // (world if sharded else 1)
 
-    # Roofline of the dominant kernel: per-kernel HIP events on the engine stream.
-    eng.reset_cluster()
-    kt = eng.time_kernels(0, min(pods.n_pods, 8192))
+    # Roofline of the evaluation kernel: per-kernel HIP events on an engine
+    # stream, over this rank's nodes (a sharded rank times its own shard).
     geom = engine.batch_geometry()
+    if sharded:
+        base, cnt = shard.partition(cluster.n_nodes, world)[rank]
+        keng = engine.Engine(local)
+        keng.set_profile(profile.compile_profile(sp if cfg != 5 else sp))
+        keng.set_cluster(cluster.shard(base, cnt))
+        keng.load_pods(pods)
+        knodes = cnt
+    else:
+        keng, knodes = eng, cluster.n_nodes
+        keng.reset_cluster()
+    kt = keng.time_kernels(0, min(pods.n_pods, 50000 if cfg != 3 else 2000))
     by_time = max(kt, key=lambda k: kt[k][0] * kt[k][1])      # largest share of device time
     dominant = next((k for k in EVAL_KERNELS if k in kt), by_time)
     n_norm = sum(1 for p in sp.score_plugins()
                  if p.name in ("TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity"))
-    alg = kernel_alg_bytes(dominant, cluster.n_nodes, n_norm, geom)
+    alg = kernel_alg_bytes(dominant, knodes, n_norm, geom)
     achieved = alg / (kt[dominant][0] * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("kernel") == dominant and tj.get("nodes") == cluster.n_nodes:
+            if tj.get("kernel") == dominant and tj.get("nodes") == knodes:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
+    seeds = {2: "0x4B53494D0002", 3: "0x4B53494D0003", 4: "0x4B53494D0004", 5: "0x4B53494D0002/0005"}
     result = {
         "metric": "pod x node filter+score evals/sec",
         "value": evals / elapsed,
@@ -187,29 +273,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int64",
-        "data": "synthetic (SplitMix64 seed 0x4B53494D0002)",
-        "config": {"workload": f"config2: default profile, {cluster.n_nodes} nodes x {pods.n_pods} pods, "
-                               f"{args.mode.upper()} (percentageOfNodesToScore={prof.percentage_of_nodes_to_score})",
-                   "nodes": cluster.n_nodes, "pods": pods.n_pods, "mode": args.mode,
-                   "parallelism": "replicas (per-GPU score-weight profiles)" if world > 1 else "single GPU"},
+        "data": f"synthetic (SplitMix64 seed {seeds[cfg]})",
+        "config": {"workload": desc, "nodes": cluster.n_nodes, "pods": pods.n_pods, "mode": args.mode,
+                   "parallelism": (f"node-sharded over {world} GPUs (RCCL)" if sharded else
+                                   f"{world} independent replicas" if world > 1 else "single GPU")},
         "pods_per_s": cycles / elapsed,
         "kernels": {k: {"avg_ms": v[0], "launches": v[1],
-                        "alg_GBps": kernel_alg_bytes(k, cluster.n_nodes, n_norm, geom) / (v[0] * 1e-3) / 1e9}
+                        "alg_GBps": kernel_alg_bytes(k, knodes, n_norm, geom) / (v[0] * 1e-3) / 1e9}
                     for k, v in kt.items()},
         "batch_stats": {"batches": st.batches, "truncations": st.truncations,
                         "perpod_cycles": st.perpod_cycles},
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": alg, "avg_launch_ms": kt[dominant][0],
+                     "alg_bytes_per_launch": alg, "avg_launch_ms": kt[dominant][0], "kernel_nodes": knodes,
                      "dominant_by_time": by_time},
         "batch_geometry": geom,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         log("[rank 0] cpu baseline ...")
-        result["cpu_baseline"] = cpu_baseline(cluster, pods, sp, args.cpu_seconds, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline(cluster, pods, sp, args.cpu_seconds, args.cpu_threads,
+                                              f"config-{cfg}")
         result["vs_cpu"] = result["value"] / result["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -1,0 +1,171 @@
+"""Numpy model of the node-sharded batch protocol.
+
+TEST INFRASTRUCTURE ONLY: tests/test_shard_cpu.py runs it on world_size-2
+``gloo`` process groups on the CPU and checks its placements against the C
+oracle on the whole cluster.  It restates, rank by rank, what
+csrc/ksim_batch.hip does between the two exchanges:
+
+  per shard : keys of B pods x local nodes under the batch-start snapshot
+              -> sorted top-T per pod + "complete" (every feasible node listed)
+  all-gather: every shard's lists                        (ncclAllGather)
+  global    : keys >= the last listed key of every incomplete shard are the
+              provable global prefix (k_batch_gmerge)
+  chain     : pod i guesses its best node not guessed earlier (k_batch_chain)
+  pairs     : key of pod j on pod k's guess after pod k binds, owner shard only
+  all-reduce: max over shards                             (ncclAllReduce MAX)
+  commit    : up to the first pod whose exact choice is not its guess; the
+              owner shard applies the binds (k_batch_commit)
+
+Batchable pods only (bare pods: Fit filter + LeastAllocated +
+BalancedAllocation vary over nodes, every normalized plugin is constant).
+Keys stay below 2^63 (totals < 2^19), so int64 tensors carry them.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+NODE_MASK = (1 << 18) - 1
+
+
+def _splitmix(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def tb_keys(total: np.ndarray, seed: int, seq: int, nodes: np.ndarray) -> np.ndarray:
+    x = np.uint64(seed) ^ (np.uint64(seq) << np.uint64(20)) ^ nodes.astype(np.uint64)
+    h = _splitmix(x) >> np.uint64(38)
+    return ((total.astype(np.uint64) << np.uint64(44)) | (h << np.uint64(18)) |
+            (np.uint64(NODE_MASK) - nodes.astype(np.uint64)))
+
+
+class Shard:
+    """One rank's nodes [base, base + n) of a bare config-2 style cluster."""
+
+    def __init__(self, cluster, base: int, count: int):
+        sl = slice(base, base + count)
+        self.base, self.n = base, count
+        self.alloc_cpu = cluster.alloc_cpu[sl].astype(np.int64)
+        self.alloc_mem = cluster.alloc_mem[sl].astype(np.int64)
+        self.alloc_pods = cluster.alloc_pods[sl].astype(np.int64)
+        self.req_cpu = cluster.req_cpu[sl].astype(np.int64).copy()
+        self.req_mem = cluster.req_mem[sl].astype(np.int64).copy()
+        self.nz_cpu = cluster.nz_cpu[sl].astype(np.int64).copy()
+        self.nz_mem = cluster.nz_mem[sl].astype(np.int64).copy()
+        self.num_pods = cluster.num_pods[sl].astype(np.int64).copy()
+
+    def keys(self, pod, rows, seed, seq, const, w_fit, w_ba, extra=None) -> np.ndarray:
+        """TB keys of ``pod`` on local ``rows`` (0 = infeasible).  ``extra``:
+        (row, pod) already bound there (the pair check)."""
+        rc, rm = self.req_cpu[rows].copy(), self.req_mem[rows].copy()
+        zc, zm = self.nz_cpu[rows].copy(), self.nz_mem[rows].copy()
+        npods = self.num_pods[rows].copy()
+        if extra is not None:
+            rc += extra["req_cpu"]
+            rm += extra["req_mem"]
+            zc += extra["nz_cpu"]
+            zm += extra["nz_mem"]
+            npods += 1
+        ac, am = self.alloc_cpu[rows], self.alloc_mem[rows]
+        fits = (npods + 1 <= self.alloc_pods[rows]) & (pod["req_cpu"] <= ac - rc) & (pod["req_mem"] <= am - rm)
+        la = np.zeros(len(rows), np.int64)
+        cnt = np.zeros(len(rows), np.int64)
+        for alloc, req in ((ac, zc + pod["nz_cpu"]), (am, zm + pod["nz_mem"])):
+            ok = alloc != 0
+            s = np.where(req > alloc, 0, ((alloc - req) * 100) // np.where(ok, alloc, 1))
+            la += np.where(ok, s, 0)
+            cnt += ok
+        la = np.where(cnt > 0, la // np.maximum(cnt, 1), 0)
+        f0 = np.minimum(1.0, (rc + pod["req_cpu"]).astype(np.float64) / ac.astype(np.float64))
+        f1 = np.minimum(1.0, (rm + pod["req_mem"]).astype(np.float64) / am.astype(np.float64))
+        ba = ((1 - np.abs((f0 - f1) / 2)) * 100).astype(np.int64)
+        total = const + w_fit * la + w_ba * ba
+        k = tb_keys(total, seed, seq, self.base + np.asarray(rows, np.int64))
+        return np.where(fits, k, np.uint64(0))
+
+    def bind(self, row: int, pod) -> None:
+        self.req_cpu[row] += pod["req_cpu"]
+        self.req_mem[row] += pod["req_mem"]
+        self.nz_cpu[row] += pod["nz_cpu"]
+        self.nz_mem[row] += pod["nz_mem"]
+        self.num_pods[row] += 1
+
+
+def global_merge(lists, completes, T: int):
+    """k_batch_gmerge: lists[s] = shard s's keys (descending, <= T)."""
+    thr = 0
+    for keys, comp in zip(lists, completes):
+        if not comp and len(keys):
+            thr = max(thr, int(keys[-1]))
+    allk = sorted((int(k) for keys in lists for k in keys if int(k) >= thr and int(k) != 0), reverse=True)
+    complete = all(completes) and len(allk) <= T
+    return allk[:T], complete
+
+
+def schedule(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed: int, const: int,
+             w_fit: int = 1, w_ba: int = 1, B: int = 16, T: int = 3):
+    """Run every pod through the sharded protocol; returns global placements."""
+    import torch
+    P = pods.n_pods
+    chosen = np.full(P, -1, np.int64)
+    cursor, seq0 = 0, 0
+    rows = np.arange(shard.n)
+    while cursor < P:
+        nb = min(B, P - cursor)
+        # per shard: top-T per pod under the batch-start snapshot
+        rec = np.zeros((nb, T + 1), np.int64)
+        for j in range(nb):
+            k = shard.keys(pods.pods[cursor + j], rows, seed, seq0 + j, const, w_fit, w_ba)
+            order = np.sort(k[k != 0])[::-1]
+            rec[j, :min(T, len(order))] = order[:T].astype(np.int64)
+            rec[j, T] = min(T, len(order)) | ((1 if len(order) <= T else 0) << 32)
+        gathered = [torch.zeros(nb * (T + 1), dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(rec.reshape(-1)))
+        g = [x.numpy().reshape(nb, T + 1) for x in gathered]
+        # global lists + chain (identical on every rank)
+        guessed, gkey, nchain = set(), [0] * nb, nb
+        for j in range(nb):
+            lists = [g[s][j, :g[s][j, T] & 0xFFFFFFFF] for s in range(world)]
+            comps = [bool(g[s][j, T] >> 32) for s in range(world)]
+            glist, gcomplete = global_merge(lists, comps, T)
+            pick = next((k for k in glist if NODE_MASK - (k & NODE_MASK) not in guessed), None)
+            if pick is None:
+                if not gcomplete:
+                    nchain = j
+                    break
+                continue
+            guessed.add(NODE_MASK - (pick & NODE_MASK))
+            gkey[j] = pick
+        # pair keys of owned guesses, max over shards
+        pmax = np.zeros(nb, np.int64)
+        for j in range(nchain):
+            for k in range(j):
+                if not gkey[k]:
+                    continue
+                row = NODE_MASK - (gkey[k] & NODE_MASK) - shard.base
+                if 0 <= row < shard.n:
+                    v = shard.keys(pods.pods[cursor + j], np.array([row]), seed, seq0 + j, const, w_fit, w_ba,
+                                   extra=pods.pods[cursor + k])[0]
+                    pmax[j] = max(pmax[j], int(v))
+        t = torch.from_numpy(pmax)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        pmax = t.numpy()
+        istar = next((j for j in range(nchain) if pmax[j] > gkey[j]), nchain)
+        committed = istar + 1 if istar < nchain else nchain
+        inode = NODE_MASK - (int(pmax[istar]) & NODE_MASK) if istar < nchain else -1
+        for j in range(committed):
+            node = inode if j == istar else (NODE_MASK - (gkey[j] & NODE_MASK) if gkey[j] else -1)
+            chosen[cursor + j] = node
+            if j < istar and gkey[j]:
+                row = node - shard.base
+                if 0 <= row < shard.n:
+                    shard.bind(row, pods.pods[cursor + j])
+                    if node == inode:
+                        shard.bind(row, pods.pods[cursor + istar])
+        cursor += committed
+        seq0 += committed
+    return chosen

@@ -1,0 +1,75 @@
+"""The node-sharded protocol on world_size-2/3 ``gloo`` process groups (CPU).
+
+oracle/shard_model.py restates per rank what the sharded HIP path does
+between its two exchanges; placements must equal the C oracle's on the whole
+cluster.  Also covers the partition every rank computes and the unique-id
+broadcast helper's wiring (bench.py's N > 1 plumbing)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from ksim.shard import partition
+
+
+def test_partition_tiles_cluster():
+    for n, w in [(10, 3), (5000, 8), (100000, 8), (7, 7)]:
+        parts = partition(n, w)
+        assert parts[0][0] == 0 and sum(c for _, c in parts) == n
+        assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+        assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+    with pytest.raises(ValueError):
+        partition(3, 4)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "kube-scheduler-simulator_amd")]
+    import torch.distributed as dist
+    from ksim import gen, profile
+    from ksim.shard import partition
+    from oracle import shard_model
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=n_pods, seed=seed)
+        sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+        if weights:
+            sp = sp.with_weights(weights)
+        w = {p.name: (p.weight or 1) for p in sp.score_plugins()}
+        const = 100 * w["TaintToleration"] + 100 * w["PodTopologySpread"]
+        base, cnt = partition(n_nodes, world)[rank]
+        shard = shard_model.Shard(cluster, base, cnt)
+        chosen = shard_model.schedule(pods, shard, rank, world, dist, n_nodes, sp.tiebreak_seed, const,
+                                      w["NodeResourcesFit"], w["NodeResourcesBalancedAllocation"], B=B, T=T)
+        if rank == 0:
+            from oracle.oracle import Oracle
+            ochosen, _ = Oracle(cluster, profile.compile_profile(sp)).schedule(pods)
+            np.testing.assert_array_equal(chosen, ochosen)
+        # every rank must hold the same placements
+        import torch
+        t = torch.from_numpy(chosen.astype(np.int64))
+        ref = t.clone()
+        dist.broadcast(ref, src=0)
+        assert torch.equal(t, ref)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_nodes,n_pods,T,B,weights", [
+    (2, 60, 500, 3, 16, None),
+    (3, 40, 400, 2, 24, {"NodeResourcesBalancedAllocation": 10}),
+    (2, 12, 700, 4, 32, None),          # pods stop fitting: unschedulable pods
+])
+def test_sharded_protocol_gloo(world, n_nodes, n_pods, T, B, weights):
+    mp.spawn(_worker, args=(world, _free_port(), n_nodes, n_pods, 7, T, B, weights), nprocs=world, join=True)

@@ -402,7 +402,10 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
 const char* ksim_kernel_name(int32_t k);
 /* Batch-path diagnostics of the last ksim_schedule_loaded: out[0] batches,
  * out[1] truncations (an exhausted candidate list ended a batch), out[2] cuts
- * (a pod's exact choice was a node bound earlier in its batch, ending it).  Returns the number of values written (<= n). */
+ * (a pod's exact choice was a node bound earlier in its batch, ending it);
+ * out[3..18] device phase-clock accumulators since ksim_set_cluster (100 MHz
+ * ticks: [3] chain prologue, [4] chain loop, [5] chain epilogue, [6] chain
+ * launches).  Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),
  * out[1] candidate keys kept per pod (T), out[2] nodes per wave tile,

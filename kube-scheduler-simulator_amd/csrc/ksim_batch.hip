@@ -175,71 +175,94 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
   }
 }
 
-// The greedy chain in one wave.  Lanes e < kTopT hold pod i's list entries;
-// "guessed" is a bitmap over node ids in LDS.  The bitmap word of step i+1 is
-// read before step i marks its guess (so the read is off the critical path)
-// and patched with that guess by one compare; the list of step i+2 is read
-// two steps ahead.  A step is then a ballot, s_ff1 and readlane.
-__global__ __launch_bounds__(256) void k_batch_chain(const DevState* __restrict__ st, int32_t n_nodes /* global */,
-                                                     const uint64_t* __restrict__ topk,
-                                                     const int32_t* __restrict__ topk_cnt,
-                                                     const int32_t* __restrict__ topk_complete,
-                                                     uint64_t* __restrict__ gkey, int32_t* __restrict__ chain_end) {
-  __shared__ uint32_t s_bm[(KSIM_KEY_NODE_MASK + 32) / 32];   // 32 KB: guessed nodes
-  __shared__ int32_t s_node[kBatchPods + 2][kTopT];
-  __shared__ int32_t s_gpos[kBatchPods];
-  __shared__ uint32_t s_incomplete[kBatchPods / 32];
-  const int tid = threadIdx.x, lane = tid & 63;
+// The greedy chain (pod i guesses the first entry of its list that no earlier
+// pod of the batch guessed), computed by parallel relaxation instead of 256
+// dependent steps: every pod holds a current guess; a round lets each pod
+// re-pick the first entry not held by an earlier pod under the previous
+// round's guesses.  Pod i's pick depends only on pods < i, so once pods
+// 0..q-1 are unchanged by a round they are exact (the serial chain's
+// result); the batch keeps that exact prefix.  Node ids are mapped to slots of
+// an LDS hash table, and "held by an earlier pod" is an LDS atomicMin of pod
+// indices per slot.  Rounds needed = the depth of the conflict chain.
+constexpr int kHashSlots = 4096;               // >= 2 x kBatchPods x kTopT list entries
+constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
+static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
+
+__global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __restrict__ st,
+                                                            int32_t n_nodes /* global */,
+                                                            const uint64_t* __restrict__ topk,
+                                                            const int32_t* __restrict__ topk_cnt,
+                                                            const int32_t* __restrict__ topk_complete,
+                                                            uint64_t* __restrict__ gkey,
+                                                            int32_t* __restrict__ chain_end,
+                                                            unsigned long long* __restrict__ dbg) {
+  __shared__ int32_t s_key[kHashSlots];        // node id in the slot, -1 = empty
+  __shared__ int32_t s_hold[kHashSlots];       // lowest pod index holding the slot this round
+  __shared__ int16_t s_rep[kBatchPods][kTopT]; // slot of each list entry
+  __shared__ int32_t s_first, s_cut;
+  // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int i = threadIdx.x;                   // one pod per thread
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return;
-  const int words = (n_nodes + 31) >> 5;
-  for (int x = tid; x < words; x += blockDim.x) s_bm[x] = 0;
-  for (int x = tid; x < (kBatchPods + 2) * kTopT; x += blockDim.x) {
-    const int i = x / kTopT, e = x % kTopT;
-    s_node[i][e] = (i < nb && e < topk_cnt[i]) ? key_node(topk[x]) : -1;
+  for (int x = i; x < kHashSlots; x += kBatchPods) {
+    s_key[x] = -1;
+    s_hold[x] = kBatchPods;
   }
-  if (tid < kBatchPods / 32) s_incomplete[tid] = 0;
+  const int cnt = i < nb ? topk_cnt[i] : 0;
+  const bool incomplete = i < nb && !topk_complete[i];
   __syncthreads();
-  if (tid < nb && !topk_complete[tid]) atomicOr(&s_incomplete[tid >> 5], 1u << (tid & 31));
-  __syncthreads();
-  if (tid < 64) {
-    const bool act = lane < kTopT;
-    int32_t n0 = act ? s_node[0][lane] : -1;
-    uint32_t w0 = n0 >= 0 ? s_bm[n0 >> 5] : 0u;
-    int32_t n1 = act ? s_node[1][lane] : -1;
-    int32_t gprev = -1, nchain = nb;
-    for (int i = 0; i < nb; i++) {
-      const int32_t n2 = act ? s_node[i + 2][lane] : -1;          // rows nb.. are -1
-      const uint32_t w1 = n1 >= 0 ? s_bm[n1 >> 5] : 0u;            // misses only guess i
-      const bool fr = n0 >= 0 && n0 != gprev && !((w0 >> (n0 & 31)) & 1u);
-      const uint64_t m = __ballot(fr);
-      int32_t g = -1;
-      if (m) {
-        const int p = (int)__builtin_ctzll(m);
-        g = __builtin_amdgcn_readlane(n0, p);
-        if (lane == 0) {
-          atomicOr(&s_bm[g >> 5], 1u << (g & 31));
-          s_gpos[i] = p;
-        }
-      } else {
-        if ((s_incomplete[i >> 5] >> (i & 31)) & 1u) {            // exhausted, incomplete: cut
-          nchain = i;
-          break;
-        }
-        if (lane == 0) s_gpos[i] = -1;                              // no feasible node at all
+  for (int e = 0; e < kTopT; e++) {
+    int16_t slot = -1;
+    if (e < cnt) {
+      const int32_t node = key_node(topk[(size_t)i * kTopT + e]);
+      uint32_t h = ((uint32_t)node * 2654435761u) >> 20;        // 12-bit hash
+      while (true) {
+        const int32_t prev = atomicCAS(&s_key[h], -1, node);
+        if (prev == -1 || prev == node) break;
+        h = (h + 1) & (kHashSlots - 1);
       }
-      gprev = g;
-      n0 = n1;
-      w0 = w1;
-      n1 = n2;
+      slot = (int16_t)h;
     }
-    if (lane == 0) *chain_end = nchain;
+    s_rep[i][e] = slot;
   }
   __syncthreads();
-  const int32_t nchain = *chain_end;
-  for (int i = tid; i < nb; i += blockDim.x)
-    gkey[i] = (i < nchain && s_gpos[i] >= 0) ? topk[i * kTopT + s_gpos[i]] : 0;
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
+  int first = kBatchPods, rounds = 0;
+  for (; rounds < kChainRounds; rounds++) {
+    if (i == 0) s_first = kBatchPods;
+    if (a >= 0) atomicMin(&s_hold[s_rep[i][a]], i);
+    __syncthreads();
+    int na = -1;
+    for (int e = 0; e < cnt; e++)
+      if (s_hold[s_rep[i][e]] >= i) { na = e; break; }   // not held by an earlier pod
+    __syncthreads();
+    if (a >= 0) s_hold[s_rep[i][a]] = kBatchPods;       // reset for the next round
+    if (na != a) atomicMin(&s_first, i);
+    a = na;
+    __syncthreads();
+    first = s_first;
+    if (first == kBatchPods) break;            // a fixpoint: every pod exact
+  }
+  // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
+  if (i == 0) s_cut = first < nb ? first : nb;
+  __syncthreads();
+  if (i < first && i < nb && a < 0 && incomplete) atomicMin(&s_cut, i);
+  __syncthreads();
+  const int32_t nchain = s_cut;
+  const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+  if (i < nb) gkey[i] = (i < nchain && a >= 0) ? topk[(size_t)i * kTopT + a] : 0;
+  if (i == 0) *chain_end = nchain;
+  if (i == 0 && dbg) {
+    const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&dbg[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&dbg[1], (unsigned long long)(t2 - t1));
+    atomicAdd(&dbg[2], (unsigned long long)(t3 - t2));
+    atomicAdd(&dbg[3], 1ull);
+    atomicAdd(&dbg[4], (unsigned long long)(rounds + 1));
+  }
 }
 
 // Validate the chain against M (pmax) and commit (one block of kBatchPods
@@ -377,8 +400,8 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
                                                                a.s.topk_complete, nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_batch_chain<<<1, 256, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                       a.s.chain_end);
+  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+                                              a.s.gkey, a.s.chain_end, a.s.dbg);
   if (evs) (void)hipEventRecord(evs[3], stream);
   k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
                                                               a.s.pmax, a.s.done, a.chosen);
@@ -397,8 +420,8 @@ void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {
   k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
                                                      a.s.topk_complete);
-  k_batch_chain<<<1, 256, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                       a.s.chain_end);
+  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+                                              a.s.gkey, a.s.chain_end, a.s.dbg);
   k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
                                                              a.s.pmax, a.s.done, a.chosen);
 }

@@ -112,6 +112,7 @@ struct DevScratch {
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
   uint32_t* done;        // batch path: k_batch_pairs blocks finished (last-block election)
+  unsigned long long* dbg;   // [16] diagnostic accumulators (ksim_get_diag), e.g. chain phase times
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
   uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records
   int64_t* dom;          // [KSIM_MAX_USES][vmax] topology-pair sums of the current pod (zero between pods)

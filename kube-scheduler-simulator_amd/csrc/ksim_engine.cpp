@@ -675,6 +675,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.done, uint32_t*, 4);
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
+  SCR(s.dbg, unsigned long long*, 8 * 16);
   SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);
   SCR(s.xrecv, uint64_t*, 8 * (size_t)kMaxShards * kBatchPods * kXRec);
   SCR(s.min_match, int64_t*, 8 * (size_t)KSIM_MAX_USES);
@@ -1130,8 +1131,9 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  const int64_t v[3] = {st.batches, st.truncations, st.cuts};
-  const int32_t m = n < 3 ? n : 3;
+  int64_t v[3 + 16] = {st.batches, st.truncations, st.cuts};
+  if (h->has_cluster) HIPCHK(h, hipMemcpy(v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
+  const int32_t m = n < 19 ? n : 19;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }

@@ -311,6 +311,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   __shared__ int64_t s_gmax[KSIM_MAX_SCORE], s_gmin[KSIM_MAX_SCORE];
   __shared__ uint32_t s_bm[kBmWords];
   __shared__ double s_w[KSIM_MAX_USES];
+  __shared__ ksim_topo_use s_use[KSIM_MAX_USES];
 
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
@@ -322,6 +323,8 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   const int32_t chunk = (N + kFinalThreads - 1) / kFinalThreads;
   const int32_t lo = min(N, tid * chunk), hi = min(N, lo + chunk);
   const ksim_pod& p = P.pods[pi];
+  const int nu = p.use_count;
+  if (tid < nu) s_use[tid] = P.uses[p.use_first + tid];   // visible after block_scan's barriers
 
   // Phase A: feasible count per rotated chunk, block scan, locate the (K+1)-th.
   int32_t cnt = 0;
@@ -349,11 +352,14 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   const int32_t cut = s_cut;                         // rotated position of the (K+1)-th feasible, or N
   const int32_t evaluated = cut < N ? cut + 1 : N;
   const int32_t nf = total < K ? total : K;
-  const int32_t whi = min(hi, cut);
   const int S = prof.n_score;
 
+  // From here on thread t walks the rotated positions t, t + 1024, ... so a
+  // wave's loads of per-node columns are coalesced; kept = position < kend
+  // with a PASSED filter result.
+  const int32_t kend = cut < N ? cut : N;
   if (COMPAT) {
-    for (int32_t r = lo; r < hi; r++) {
+    for (int32_t r = tid; r < N; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
       if (r >= evaluated) {
@@ -371,17 +377,24 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
 
   // Phase A2: PodTopologySpread PreScore over the kept list: IgnoredNodes,
   // pair registration and topologyNormalizingWeight per soft constraint.
-  const bool has_soft = nf > 1 && p.use_count > 0 && use_has_kind(P, p, KSIM_USE_PTS_SOFT);
+  bool any_soft = false;
+  for (int i = 0; i < nu; i++) any_soft = any_soft || s_use[i].kind == KSIM_USE_PTS_SOFT;
+  const bool has_soft = nf > 1 && any_soft;
+  auto lacks_soft_key = [&](int32_t node) -> bool {
+    for (int i = 0; i < nu; i++)
+      if (s_use[i].kind == KSIM_USE_PTS_SOFT && use_value(c, s_use[i], node) == 0) return true;
+    return false;
+  };
   if (has_soft) {
     int32_t nign = 0;
-    for (int32_t r = lo; r < whi; r++) {
+    for (int32_t r = tid; r < kend; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (s.fail[node] == KSIM_PASSED && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node)) nign++;
+      if (s.fail[node] == KSIM_PASSED && lacks_soft_key(node)) nign++;
     }
     nign = block_sum_i32_nw<kFinalWaves>(nign, sh32);
-    for (int i = 0; i < p.use_count; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use u = s_use[i];
       if (u.kind != KSIM_USE_PTS_SOFT) continue;
       int32_t size;
       if (u.flags & KSIM_USEF_HOSTNAME) {
@@ -390,10 +403,10 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         const int32_t words = u.col == KSIM_COL_NONE ? 1 : (c.col_nvals[u.col] + 31) / 32;
         for (int x = tid; x < words; x += kFinalThreads) s_bm[x] = 0;
         __syncthreads();
-        for (int32_t r = lo; r < whi; r++) {
+        for (int32_t r = tid; r < kend; r += kFinalThreads) {
           int32_t node = start + r;
           if (node >= N) node -= N;
-          if (s.fail[node] != KSIM_PASSED || !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node)) continue;
+          if (s.fail[node] != KSIM_PASSED || lacks_soft_key(node)) continue;
           const uint32_t v = use_value(c, u, node);
           atomicOr(&s_bm[v >> 5], 1u << (v & 31));
         }
@@ -407,10 +420,24 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     __syncthreads();
   }
   const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
+  // podtopologyspread Score from the LDS copy of the uses (ignored nodes: 0)
+  auto pts_raw = [&](int32_t node) -> int64_t {
+    double score = 0;
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use& u = s_use[i];
+      if (u.kind != KSIM_USE_PTS_SOFT) continue;
+      const uint32_t v = use_value(c, u, node);
+      if (v == 0) continue;
+      const int64_t n_match = (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node)
+                                                              : s.dom[(size_t)i * c.vmax + v];
+      score = score + ((double)n_match * s_w[i] + (double)(u.arg - 1));   // scoreForCount, unfused
+    }
+    return (int64_t)round(score);                                          // math.Round
+  };
 
   int32_t chosen = -1;
   if (nf == 1) {
-    for (int32_t r = lo; r < whi; r++) {
+    for (int32_t r = tid; r < kend; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
       if (s.fail[node] == KSIM_PASSED) s_single = node;
@@ -418,43 +445,55 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     __syncthreads();
     chosen = s_single;
   } else if (nf > 1) {
-    // Phase B: PodTopologySpread raw scores, NormalizeScore extrema over the kept list.
-    for (int k = 0; k < S; k++) {
-      const int32_t kind = norm_kind(prof.score[k]);
-      if (kind == kNormNone) continue;
-      int64_t mx = INT64_MIN, mn = INT64_MAX;
-      for (int32_t r = lo; r < whi; r++) {
-        int32_t node = start + r;
-        if (node >= N) node -= N;
-        if (s.fail[node] != KSIM_PASSED) continue;
-        int64_t v = s.raw[(size_t)k * N + node];
+    // Phase B: one pass over the kept list: PodTopologySpread raw scores and
+    // the NormalizeScore extrema of every normalized slot.
+    int64_t mx[KSIM_MAX_SCORE], mn[KSIM_MAX_SCORE];
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCORE; k++) { mx[k] = INT64_MIN; mn[k] = INT64_MAX; }
+    for (int32_t r = tid; r < kend; r += kFinalThreads) {
+      int32_t node = start + r;
+      if (node >= N) node -= N;
+      if (s.fail[node] != KSIM_PASSED) continue;
+      const bool ign = has_soft && lacks_soft_key(node);
+#pragma unroll
+      for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+        if (k >= S) break;
+        const int32_t kind = norm_kind(prof.score[k]);
+        if (kind == kNormNone) continue;
+        int64_t v;
         if (kind == kNormPTS) {
-          const bool ign = has_soft && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
-          v = (has_soft && !ign) ? pts_score(c, P, s, p, s_w, node) : 0;
+          v = (has_soft && !ign) ? pts_raw(node) : 0;
           s.raw[(size_t)k * N + node] = v;
           if (ign) continue;                       // invalidScore: not in min / max
+        } else {
+          v = s.raw[(size_t)k * N + node];
         }
-        mx = v > mx ? v : mx;
-        mn = v < mn ? v : mn;
+        mx[k] = v > mx[k] ? v : mx[k];
+        mn[k] = v < mn[k] ? v : mn[k];
       }
-      mx = block_max_i64(mx, sh64);
-      mn = block_min_i64(mn, sh64);
-      if (tid == 0) { s_gmax[k] = mx; s_gmin[k] = mn; }
+    }
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+      if (k >= S || norm_kind(prof.score[k]) == kNormNone) continue;
+      const int64_t gx = block_max_i64(mx[k], sh64);
+      const int64_t gn = block_min_i64(mn[k], sh64);
+      if (tid == 0) { s_gmax[k] = gx; s_gmin[k] = gn; }
     }
     __syncthreads();
     // Phase C: weighted totals and the tie-break argmax.
     uint64_t best = 0;
-    for (int32_t r = lo; r < whi; r++) {
+    for (int32_t r = tid; r < kend; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
       if (s.fail[node] != KSIM_PASSED) continue;
+      const bool ign = has_soft && lacks_soft_key(node);
       int64_t tot = S == 0 ? 1 : s.part[node];
       for (int k = 0; k < S; k++) {
         const int32_t kind = norm_kind(prof.score[k]);
         const int64_t raw = s.raw[(size_t)k * N + node];
         int64_t nv = raw;
         if (kind != kNormNone) {
-          if (kind == kNormPTS && has_soft && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node))
+          if (kind == kNormPTS && ign)
             nv = 0;
           else
             nv = normalize_value(kind, raw, s_gmax[k], s_gmin[k], ipa_nonempty);
@@ -479,16 +518,16 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
 
   // Restore the all-zero domain tables for the next pod (every entry this
   // pod touched is the value of some node's key).
-  if (p.use_count) {
+  if (nu) {
     __syncthreads();
-    for (int i = 0; i < p.use_count; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use u = s_use[i];
       if (u.col == KSIM_COL_NONE || (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME))) continue;
       int64_t* d = s.dom + (size_t)i * c.vmax;
       if (c.col_nvals[u.col] <= 4 * kFinalThreads) {
         for (int32_t v = tid; v < c.col_nvals[u.col]; v += kFinalThreads) d[v] = 0;
       } else {
-        for (int32_t node = lo; node < hi; node++) d[use_value(c, u, node)] = 0;
+        for (int32_t node = tid; node < N; node += kFinalThreads) d[use_value(c, u, node)] = 0;
       }
     }
   }

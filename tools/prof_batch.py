@@ -16,3 +16,4 @@ e.load_pods(pods)
 _, st = e.schedule_loaded(0, pods.n_pods, want_chosen=False)
 print(f"pods={pods.n_pods} batches={st.batches} trunc={st.truncations} device_ms={st.device_ms:.2f}")
 print("diag", e.diag())
+print("time_kernels", e.time_kernels(0, min(pods.n_pods, 8192)) if False else "")

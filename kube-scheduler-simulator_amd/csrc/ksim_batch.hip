@@ -44,24 +44,25 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
   if (tile >= n_tiles) return;                       // wave-uniform
   const ksim_pod& p = P.pods[pi];
   const int32_t nc = P.norm_const[pi];
+  const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
   const int64_t seq = st->pod_seq + j;
-  uint64_t a[kNodesPerLane];
-#pragma unroll
+  // The lane's kNodesPerLane keys, kept sorted (descending) by insertion; the
+  // node loop is not unrolled so the kernel stays small (instruction cache).
+  uint64_t a[kNodesPerLane] = {0, 0, 0, 0};
+  static_assert(kNodesPerLane == 4 && kTileCand == 4, "insertion below is for 4 keys");
+#pragma unroll 1
   for (int k = 0; k < kNodesPerLane; k++) {
     const int32_t node = tile * kTileNodes + k * 64 + lane;
     uint64_t kk = 0;
     if (node < c.n) {
       const NodeRow r = load_row(c, node);
-      if (static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
+      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
     }
-    a[k] = kk;
+    a[3] = umax64(a[3], kk);
+    cswap_desc(a[2], a[3]);
+    cswap_desc(a[1], a[2]);
+    cswap_desc(a[0], a[1]);
   }
-  static_assert(kNodesPerLane == 4 && kTileCand == 4, "sorting network below is for 4 keys");
-  cswap_desc(a[0], a[1]);
-  cswap_desc(a[2], a[3]);
-  cswap_desc(a[0], a[2]);
-  cswap_desc(a[1], a[3]);
-  cswap_desc(a[1], a[2]);
   uint64_t* out = cand + ((size_t)j * n_tiles + tile) * kTileCand;
 #pragma unroll
   for (int t = 0; t < kTileCand; t++) {
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
       NodeRow r = load_row(c, local);
       row_add_pod(r, P.pods[base + k], 1);
       const ksim_pod& p = P.pods[base + j];
-      if (static_filters_pass(c, P, bp, p, r))
+      if ((P.bflags[base + j] & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r))
         v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j, c.base);
     }
   }

@@ -61,6 +61,7 @@ struct DevPods {
   const ksim_label_expr* exprs;
   const ksim_term* terms;
   const int32_t* norm_const;     // [n_pods] batch path: constant sum of weighted normalized scores
+  const int32_t* bflags;         // [n_pods] batch path: kBatch* flags
   const ksim_topo_use* uses;
   const ksim_class_add* adds;
   int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, _pad[3];
@@ -658,9 +659,13 @@ struct BatchProg {
   int32_t n_static;                        // static (bind-invariant) filters, profile order
   uint8_t static_filter[KSIM_MAX_FILTER];
   int32_t has_fit_filter;
-  int32_t _pad;
+  int32_t cpu_mem;                         // both scoring strategies are exactly {cpu, memory}
   int64_t w_fit, w_ba;                     // summed profile weights of the Fit / BA score slots
+  int64_t fit_w_cpu, fit_w_mem;            // cpu_mem: LeastAllocated resource weights
 };
+
+// DevPods.bflags (batch path, per pod)
+constexpr int32_t kBatchStaticTrivial = 1; // every static filter passes on every node (host-proven)
 
 // Compact row for the batch repair's LDS staging: the NodeRow fields a
 // batchable pod can read (batchable pods request no scalar resources and the
@@ -756,10 +761,61 @@ __device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const D
   return true;
 }
 
+// dyn_key for the default scoring strategies ({cpu, memory} for both
+// LeastAllocated and BalancedAllocation; batchable pods request no scalars):
+// the same arithmetic as the generic functions with the resource loops
+// resolved, so the batch kernels stay small.
+__device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, const BatchProg& bp,
+                                                    const ksim_pod& p, int32_t norm_const, const NodeRow& r,
+                                                    int64_t seq, int32_t base) {
+  if (bp.has_fit_filter) {
+    if (r.num_pods + 1 > r.alloc_pods) return 0;
+    if (p.req_cpu != 0 || p.req_mem != 0 || p.req_eph != 0) {
+      if (p.req_cpu > r.alloc_cpu - r.req_cpu || p.req_mem > r.alloc_mem - r.req_mem ||
+          p.req_eph > r.alloc_eph - r.req_eph)
+        return 0;
+    }
+  }
+  int64_t tot = norm_const;
+  if (bp.w_fit) {                              // leastResourceScorer over {cpu, memory}
+    int64_t ns = 0, ws = 0;
+    if (r.alloc_cpu != 0) {
+      ns += least_requested_score(r.nz_cpu + p.nz_cpu, r.alloc_cpu) * bp.fit_w_cpu;
+      ws += bp.fit_w_cpu;
+    }
+    if (r.alloc_mem != 0) {
+      ns += least_requested_score(r.nz_mem + p.nz_mem, r.alloc_mem) * bp.fit_w_mem;
+      ws += bp.fit_w_mem;
+    }
+    const int64_t la = ws == 0 ? 0 : (ns < 0 || ws < 0) ? ns / ws : div_floor_nonneg(ns, ws);
+    tot += bp.w_fit * la;
+  }
+  if (bp.w_ba) {                               // balancedResourceScorer over {cpu, memory}
+    double f0 = 0, f1 = 0;
+    int nf = 0;
+    if (r.alloc_cpu != 0) {
+      double f = (double)(r.req_cpu + p.req_cpu) / (double)r.alloc_cpu;
+      f0 = f > 1 ? 1 : f;
+      nf++;
+    }
+    if (r.alloc_mem != 0) {
+      double f = (double)(r.req_mem + p.req_mem) / (double)r.alloc_mem;
+      if (nf == 0) f0 = f > 1 ? 1 : f;
+      else f1 = f > 1 ? 1 : f;
+      nf++;
+    }
+    const double std = nf == 2 ? fabs((f0 - f1) / 2) : 0.0;
+    tot += bp.w_ba * (int64_t)((1 - std) * (double)kMaxNodeScore);
+  }
+  if (prof.n_score == 0) tot = 1;
+  return tb_key(tot, prof.tiebreak_seed, seq, base + r.node);
+}
+
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).
 __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
                                             int32_t norm_const, const NodeRow& r, int n_scalar, int64_t seq,
                                             int32_t base) {
+  if (bp.cpu_mem) return dyn_key_cpu_mem(prof, bp, p, norm_const, r, seq, base);
   if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
   int64_t tot = norm_const;
   if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);

@@ -80,6 +80,8 @@ struct ksim_handle {
   DevCluster dc{};
   std::vector<DevBuf> cluster_bufs;
   std::vector<uint8_t> taint_effect;    // host copy (batchability analysis)
+  std::vector<uint16_t> hard_taints;    // taint ids with effect NoSchedule/NoExecute on some node
+  bool any_unschedulable = false;       // some node has spec.unschedulable
 
   // device copy of the uploaded dynamic columns (ksim_reset_cluster)
   struct {
@@ -227,6 +229,18 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
 //   InterPodAffinity:  no uses -> topologyScore empty -> 0
 // A pod with topology uses reads the count classes, which binds of earlier
 // pods of a batch change, so it always takes the per-pod path.
+// Every static filter of the batch path passes on every node for this pod:
+// no spec.nodeName, no nodeSelector / required node affinity, every
+// NoSchedule/NoExecute taint in the cluster tolerated, no unschedulable node
+// (or tolerated).  The batch kernels then skip the static filters.
+bool static_trivial(const ksim_handle* h, const ksim_pod& p) {
+  if (p.node_name != -1 || p.sel_count > 0 || (p.flags & KSIM_POD_HAS_REQUIRED_AFFINITY)) return false;
+  if (h->any_unschedulable && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE)) return false;
+  for (uint16_t id : h->hard_taints)
+    if (!((p.tol_filter[id >> 6] >> (id & 63)) & 1ull)) return false;
+  return true;
+}
+
 bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
   const ksim_profile& prof = h->prof;
   if (num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, h->dc.n) != h->dc.n) return false;
@@ -518,6 +532,10 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   h->has_profile = true;
   // the profile compiled for batchable pods (see BatchProg in ksim_device.h)
   BatchProg bp{};
+  bp.cpu_mem = p->fit_n_res == 2 && p->fit_res[0] == KSIM_RES_CPU && p->fit_res[1] == KSIM_RES_MEMORY &&
+               p->ba_n_res == 2 && p->ba_res[0] == KSIM_RES_CPU && p->ba_res[1] == KSIM_RES_MEMORY;
+  bp.fit_w_cpu = p->fit_res_weight[0];
+  bp.fit_w_mem = p->fit_res_weight[1];
   for (int i = 0; i < p->n_filter; i++) {
     const int f = p->filter[i];
     if (f == KSIM_PL_NODE_UNSCHEDULABLE || f == KSIM_PL_NODE_NAME || f == KSIM_PL_TAINT_TOLERATION ||
@@ -634,6 +652,16 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   h->col_nvals = col_nvals;
   h->dc = c;
   h->taint_effect.assign(v->taint_effect, v->taint_effect + v->n_taints);
+  {
+    std::vector<uint8_t> seen((size_t)v->n_taints, 0);
+    for (size_t i = 0; i < (size_t)n * KSIM_MAX_NODE_TAINTS; i++) seen[t->taints[i]] = 1;
+    h->hard_taints.clear();
+    for (int id = 1; id < v->n_taints; id++)
+      if (seen[id] && (v->taint_effect[id] == KSIM_EFFECT_NO_SCHEDULE || v->taint_effect[id] == KSIM_EFFECT_NO_EXECUTE))
+        h->hard_taints.push_back((uint16_t)id);
+    h->any_unschedulable = false;
+    for (int32_t i = 0; i < n; i++) h->any_unschedulable = h->any_unschedulable || (t->flags[i] & KSIM_NODE_UNSCHEDULABLE);
+  }
   {
     void* q = nullptr;
 #define SNAP(field, bytes)                                                                 \
@@ -790,6 +818,8 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   P.terms = (const ksim_term*)p;
   if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
   P.norm_const = (const int32_t*)p;
+  if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
+  P.bflags = (const int32_t*)p;
   if ((rc = upload(h, h->pod1_bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
   if ((rc = upload(h, h->pod1_bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
@@ -873,11 +903,13 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   h->d_chosen = nullptr;
   std::vector<int32_t> nc((size_t)std::max(ps->n_pods, 1), 0);
+  std::vector<int32_t> bf((size_t)std::max(ps->n_pods, 1), 0);
   h->batchable.assign((size_t)ps->n_pods, 0);
   h->topo.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
     h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
+    bf[i] = static_trivial(h, ps->pods[i]) ? kBatchStaticTrivial : 0;
   }
   DevPods P{};
   void* p = nullptr;
@@ -889,6 +921,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.terms = (const ksim_term*)p;
   if ((rc = upload(h, h->pod_bufs, nc.data(), 4 * nc.size(), &p))) return rc;
   P.norm_const = (const int32_t*)p;
+  if ((rc = upload(h, h->pod_bufs, bf.data(), 4 * bf.size(), &p))) return rc;
+  P.bflags = (const int32_t*)p;
   if ((rc = upload(h, h->pod_bufs, ps->uses, sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
   if ((rc = upload(h, h->pod_bufs, ps->adds, sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0), &p))) return rc;

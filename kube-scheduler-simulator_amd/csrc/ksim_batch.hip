@@ -404,8 +404,11 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
   if (evs) (void)hipEventRecord(evs[3], stream);
-  k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
-                                                              a.s.pmax, a.s.done, a.chosen);
+  // pair keys, then a separate one-block commit: cheaper than every block of
+  // the pairs kernel fencing for a last-block election
+  k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+                                                             a.s.pmax, a.s.done, a.chosen);
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
   if (evs) (void)hipEventRecord(evs[4], stream);
 }
 

@@ -50,7 +50,9 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
     tiles = (n_nodes + geom["tile_nodes"] - 1) // geom["tile_nodes"]
     if name == "k_filter_score":
         return B_EVAL * n_nodes                       # one node row per pod x node eval
-    if name == "k_finalize":
+    if name == "k_extrema":
+        return n_nodes * (1 + 8 * n_norm)             # fail code + normalized raws
+    if name == "k_select":
         return n_nodes * (1 + 8 + 8 * n_norm)         # fail code + partial total + normalized raws
     if name == "k_batch_eval":
         return B_EVAL * n_nodes * B                   # B pods x N nodes evals per launch

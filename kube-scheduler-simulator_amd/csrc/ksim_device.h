@@ -83,7 +83,7 @@ struct DevState {
   // batch path: batches ended early because a pod's best node was one bound
   // earlier in the batch (its guess was not its exact choice)
   int64_t cuts;
-  // per-pod topology flags of the current cycle (kTopo*), reset by k_finalize
+  // per-pod topology flags of the current cycle (kTopo*), reset by k_bind
   uint32_t topo_flags;
   int32_t _pad;
 };
@@ -99,9 +99,19 @@ constexpr int64_t kDomCountMask = (1ll << kDomMarkShift) - 1;
 
 struct BRow;
 
-// Per-cycle scratch written by the filter/score kernel, read by finalize.
+// Selection state of one per-pod cycle (k_window -> k_extrema -> k_select -> k_bind).
+struct WinState {
+  int32_t cut, kend, nf, evaluated, k, has_soft, single, _pad;
+  double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
+  uint64_t ext[2 * KSIM_MAX_SCORE];      // per score slot: max image, min image (atomicMax)
+  uint64_t best;                         // TB argmax key
+};
+
+// Per-cycle scratch written by the filter/score kernel, read by the selection.
 struct DevScratch {
   uint8_t* fail;         // [n] filter-order index of first failure or KSIM_PASSED
+  uint8_t* ign;          // [n] feasible node missing a ScheduleAnyway spread key (IgnoredNodes)
+  WinState* win;
   uint32_t* detail;      // [n]
   int64_t* raw;          // [KSIM_MAX_SCORE][n] raw scores (normalized slots; all in compat)
   int64_t* part;         // [n] sum of weighted raw of slots without NormalizeScore
@@ -492,7 +502,7 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
   return KSIM_PASSED;
 }
 
-// PodTopologySpread's raw score needs the feasible list (k_finalize computes it).
+// PodTopologySpread's raw score needs the feasible list (k_extrema computes it).
 __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                            const DevScratch& s, const ksim_pod& p, int plugin, const NodeRow& r) {
   switch (plugin) {
@@ -501,7 +511,7 @@ __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const D
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
     case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(c, P, s, prof, p, r.node) : 0;
-    default: return 0;   // ImageLocality (no images); PodTopologySpread: k_finalize
+    default: return 0;   // ImageLocality (no images); PodTopologySpread: k_extrema
   }
 }
 

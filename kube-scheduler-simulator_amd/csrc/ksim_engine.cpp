@@ -691,6 +691,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     dst = (type)p;                                                                    \
   } while (0)
   SCR(s.fail, uint8_t*, N);
+  SCR(s.ign, uint8_t*, N);
+  SCR(s.win, WinState*, sizeof(WinState));
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);

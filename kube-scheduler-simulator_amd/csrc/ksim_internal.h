@@ -34,7 +34,7 @@ struct LaunchArgs {
   int32_t* chosen;   // [n_pods] device, may be null
 };
 
-constexpr int kKernelsPerCycle = 4;
+constexpr int kKernelsPerCycle = 7;
 extern const char* const kKernelNames[kKernelsPerCycle];
 constexpr int kKernelsPerBatch = 4;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];

@@ -15,6 +15,7 @@
 //    nodes): ksim_batch.hip.
 #include "ksim_device.h"
 #include "ksim_internal.h"
+#include "ksim_wave.h"
 
 namespace ksim {
 
@@ -283,6 +284,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
   s.fail[node] = res;
   if (COMPAT) s.detail[node] = det;
   if (res != KSIM_PASSED) return;
+  // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
+  s.ign[node] = p.use_count && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
   int64_t part = 0;
   for (int k = 0; k < prof.n_score; k++) {
     const int pl = prof.score[k];
@@ -300,33 +303,40 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
 
 constexpr int kBmWords = (KSIM_MAX_NODES + 1 + 31) / 32;   // value-id bitmap (PTS pair registration)
 
-template <bool COMPAT>
-__global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPods P, ksim_profile prof,
-                                                            DevState* __restrict__ st, DevScratch s,
-                                                            DevEvalOut o, int32_t* __restrict__ chosen_out) {
-  __shared__ int64_t sh64[kFinalWaves];
-  __shared__ uint64_t shu[kFinalWaves];
-  __shared__ int32_t sh32[kFinalWaves];
-  __shared__ int32_t s_cut, s_single;
-  __shared__ int64_t s_gmax[KSIM_MAX_SCORE], s_gmin[KSIM_MAX_SCORE];
-  __shared__ uint32_t s_bm[kBmWords];
-  __shared__ double s_w[KSIM_MAX_USES];
-  __shared__ ksim_topo_use s_use[KSIM_MAX_USES];
+// Order-preserving u64 images of an int64 so extrema are atomicMax on u64:
+// max image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both.
+__device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
+__device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
+__device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
+__device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
 
+// The selection after the filters, as four launches (a single block cannot
+// hide the latency of 10^4 nodes' loads):
+//   k_window   1 block: numFeasibleNodesToFind window (block scan), the
+//              PodTopologySpread PreScore (IgnoredNodes, pair registration,
+//              topologyNormalizingWeight); resets the extrema / argmax slots
+//   k_extrema  grid: PodTopologySpread raw scores, NormalizeScore extrema
+//   k_select   grid: normalized weighted totals, TB argmax (atomicMax), and
+//              the domain tables re-zeroed for the next pod
+//   k_bind     1 wave: selectHost result, NodeInfo.AddPod, scheduler state
+template <bool COMPAT>
+__global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods P, ksim_profile prof,
+                                                          DevState* __restrict__ st, DevScratch s) {
+  __shared__ int32_t sh32[kFinalWaves];
+  __shared__ int32_t s_cut;
+  __shared__ uint32_t s_bm[kBmWords];
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const int tid = threadIdx.x;
   const int32_t N = c.n;
   const int32_t K = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, N);
   const int32_t start = st->next_start;
-  const int64_t seq = st->pod_seq;
   const int32_t chunk = (N + kFinalThreads - 1) / kFinalThreads;
   const int32_t lo = min(N, tid * chunk), hi = min(N, lo + chunk);
   const ksim_pod& p = P.pods[pi];
-  const int nu = p.use_count;
-  if (tid < nu) s_use[tid] = P.uses[p.use_first + tid];   // visible after block_scan's barriers
+  WinState* win = s.win;
 
-  // Phase A: feasible count per rotated chunk, block scan, locate the (K+1)-th.
+  // feasible count per rotated chunk, block scan, locate the (K+1)-th
   int32_t cnt = 0;
   for (int32_t r = lo; r < hi; r++) {
     int32_t node = start + r;
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
   }
   int32_t excl, total;
   block_scan_i32(cnt, excl, total, sh32);
-  if (tid == 0) { s_cut = N; s_single = -1; }
+  if (tid == 0) s_cut = N;
   __syncthreads();
   if (total > K && excl <= K && K < excl + cnt) {
     int32_t run = excl;
@@ -349,52 +359,31 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
     }
   }
   __syncthreads();
-  const int32_t cut = s_cut;                         // rotated position of the (K+1)-th feasible, or N
+  const int32_t cut = s_cut;
+  const int32_t kend = cut < N ? cut : N;
   const int32_t evaluated = cut < N ? cut + 1 : N;
   const int32_t nf = total < K ? total : K;
-  const int S = prof.n_score;
-
-  // From here on thread t walks the rotated positions t, t + 1024, ... so a
-  // wave's loads of per-node columns are coalesced; kept = position < kend
-  // with a PASSED filter result.
-  const int32_t kend = cut < N ? cut : N;
   if (COMPAT) {
-    for (int32_t r = tid; r < N; r += kFinalThreads) {
+    for (int32_t r = evaluated + tid; r < N; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (r >= evaluated) {
-        s.fail[node] = KSIM_NOT_EVALUATED;
-        s.detail[node] = 0;
-      }
-      o.scored[node] = 0;
-      o.total[node] = 0;
-      for (int k = 0; k < S; k++) {
-        o.raw[(size_t)k * N + node] = 0;
-        o.norm[(size_t)k * N + node] = 0;
-      }
+      s.fail[node] = KSIM_NOT_EVALUATED;
+      s.detail[node] = 0;
     }
   }
-
-  // Phase A2: PodTopologySpread PreScore over the kept list: IgnoredNodes,
-  // pair registration and topologyNormalizingWeight per soft constraint.
   bool any_soft = false;
-  for (int i = 0; i < nu; i++) any_soft = any_soft || s_use[i].kind == KSIM_USE_PTS_SOFT;
+  for (int i = 0; i < p.use_count; i++) any_soft = any_soft || P.uses[p.use_first + i].kind == KSIM_USE_PTS_SOFT;
   const bool has_soft = nf > 1 && any_soft;
-  auto lacks_soft_key = [&](int32_t node) -> bool {
-    for (int i = 0; i < nu; i++)
-      if (s_use[i].kind == KSIM_USE_PTS_SOFT && use_value(c, s_use[i], node) == 0) return true;
-    return false;
-  };
   if (has_soft) {
     int32_t nign = 0;
     for (int32_t r = tid; r < kend; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (s.fail[node] == KSIM_PASSED && lacks_soft_key(node)) nign++;
+      nign += s.fail[node] == KSIM_PASSED && s.ign[node];
     }
     nign = block_sum_i32_nw<kFinalWaves>(nign, sh32);
-    for (int i = 0; i < nu; i++) {
-      const ksim_topo_use u = s_use[i];
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
       if (u.kind != KSIM_USE_PTS_SOFT) continue;
       int32_t size;
       if (u.flags & KSIM_USEF_HOSTNAME) {
@@ -406,7 +395,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         for (int32_t r = tid; r < kend; r += kFinalThreads) {
           int32_t node = start + r;
           if (node >= N) node -= N;
-          if (s.fail[node] != KSIM_PASSED || lacks_soft_key(node)) continue;
+          if (s.fail[node] != KSIM_PASSED || s.ign[node]) continue;
           const uint32_t v = use_value(c, u, node);
           atomicOr(&s_bm[v >> 5], 1u << (v & 31));
         }
@@ -415,78 +404,129 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         for (int x = tid; x < words; x += kFinalThreads) bits += __popc(s_bm[x]);
         size = block_sum_i32_nw<kFinalWaves>(bits, sh32);
       }
-      if (tid == 0) s_w[i] = c.topo_log[size];
+      if (tid == 0) win->w[i] = c.topo_log[size];
     }
-    __syncthreads();
   }
-  const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
-  // podtopologyspread Score from the LDS copy of the uses (ignored nodes: 0)
-  auto pts_raw = [&](int32_t node) -> int64_t {
-    double score = 0;
-    for (int i = 0; i < nu; i++) {
-      const ksim_topo_use& u = s_use[i];
-      if (u.kind != KSIM_USE_PTS_SOFT) continue;
-      const uint32_t v = use_value(c, u, node);
-      if (v == 0) continue;
-      const int64_t n_match = (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node)
-                                                              : s.dom[(size_t)i * c.vmax + v];
-      score = score + ((double)n_match * s_w[i] + (double)(u.arg - 1));   // scoreForCount, unfused
-    }
-    return (int64_t)round(score);                                          // math.Round
-  };
-
-  int32_t chosen = -1;
+  if (tid < 2 * KSIM_MAX_SCORE) win->ext[tid] = 0;
+  if (tid == 0) {
+    win->cut = cut;
+    win->kend = kend;
+    win->nf = nf;
+    win->evaluated = evaluated;
+    win->has_soft = has_soft;
+    win->k = K;
+    win->best = 0;
+    win->single = -1;
+  }
   if (nf == 1) {
     for (int32_t r = tid; r < kend; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (s.fail[node] == KSIM_PASSED) s_single = node;
+      if (s.fail[node] == KSIM_PASSED) win->single = node;
     }
-    __syncthreads();
-    chosen = s_single;
-  } else if (nf > 1) {
-    // Phase B: one pass over the kept list: PodTopologySpread raw scores and
-    // the NormalizeScore extrema of every normalized slot.
-    int64_t mx[KSIM_MAX_SCORE], mn[KSIM_MAX_SCORE];
+  }
+}
+
+// Rotated scan position of a node and whether it is in the kept list.
+__device__ __forceinline__ bool kept_node(const DevScratch& s, int32_t node, int32_t start, int32_t n,
+                                          int32_t kend) {
+  int32_t r = node - start;
+  if (r < 0) r += n;
+  return r < kend && s.fail[node] == KSIM_PASSED;
+}
+
+__global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_profile prof,
+                                                 const DevState* __restrict__ st, DevScratch s) {
+  __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
+  __shared__ ksim_topo_use s_use[KSIM_MAX_USES];
+  __shared__ double s_w[KSIM_MAX_USES];
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  WinState* win = s.win;
+  if (win->nf <= 1) return;                       // no scoring
+  const ksim_pod& p = P.pods[pi];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nu = p.use_count;
+  const bool has_soft = win->has_soft != 0;
+  if (tid < nu) {
+    s_use[tid] = P.uses[p.use_first + tid];
+    s_w[tid] = win->w[tid];
+  }
+  __syncthreads();
+  const int32_t node = blockIdx.x * blockDim.x + tid;
+  const int32_t N = c.n;
+  const bool kept = node < N && kept_node(s, node, st->next_start, N, win->kend);
+  const int S = prof.n_score;
 #pragma unroll
-    for (int k = 0; k < KSIM_MAX_SCORE; k++) { mx[k] = INT64_MIN; mn[k] = INT64_MAX; }
-    for (int32_t r = tid; r < kend; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
-      if (s.fail[node] != KSIM_PASSED) continue;
-      const bool ign = has_soft && lacks_soft_key(node);
-#pragma unroll
-      for (int k = 0; k < KSIM_MAX_SCORE; k++) {
-        if (k >= S) break;
-        const int32_t kind = norm_kind(prof.score[k]);
-        if (kind == kNormNone) continue;
-        int64_t v;
-        if (kind == kNormPTS) {
-          v = (has_soft && !ign) ? pts_raw(node) : 0;
-          s.raw[(size_t)k * N + node] = v;
-          if (ign) continue;                       // invalidScore: not in min / max
-        } else {
-          v = s.raw[(size_t)k * N + node];
+  for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+    if (k >= S) break;
+    const int32_t kind = norm_kind(prof.score[k]);
+    if (kind == kNormNone) continue;
+    uint64_t ix = 0, in = 0;
+    if (kept) {
+      int64_t v;
+      bool counted = true;
+      if (kind == kNormPTS) {
+        const bool ign = has_soft && s.ign[node];
+        v = 0;
+        if (has_soft && !ign) {                   // podtopologyspread Score
+          double score = 0;
+          for (int i = 0; i < nu; i++) {
+            const ksim_topo_use& u = s_use[i];
+            if (u.kind != KSIM_USE_PTS_SOFT) continue;
+            const uint32_t val = use_value(c, u, node);
+            if (val == 0) continue;
+            const int64_t n_match = (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node)
+                                                                    : s.dom[(size_t)i * c.vmax + val];
+            score = score + ((double)n_match * s_w[i] + (double)(u.arg - 1));   // scoreForCount, unfused
+          }
+          v = (int64_t)round(score);              // math.Round
         }
-        mx[k] = v > mx[k] ? v : mx[k];
-        mn[k] = v < mn[k] ? v : mn[k];
+        s.raw[(size_t)k * N + node] = v;
+        counted = !ign;                           // invalidScore: not in min / max
+      } else {
+        v = s.raw[(size_t)k * N + node];
+      }
+      if (counted) {
+        ix = max_image(v);
+        in = min_image(v);
       }
     }
-#pragma unroll
-    for (int k = 0; k < KSIM_MAX_SCORE; k++) {
-      if (k >= S || norm_kind(prof.score[k]) == kNormNone) continue;
-      const int64_t gx = block_max_i64(mx[k], sh64);
-      const int64_t gn = block_min_i64(mn[k], sh64);
-      if (tid == 0) { s_gmax[k] = gx; s_gmin[k] = gn; }
+    ix = wave_max_u64_dpp(ix);
+    in = wave_max_u64_dpp(in);
+    if (lane == 0) {
+      s_red[wv][2 * k] = ix;
+      s_red[wv][2 * k + 1] = in;
     }
-    __syncthreads();
-    // Phase C: weighted totals and the tie-break argmax.
-    uint64_t best = 0;
-    for (int32_t r = tid; r < kend; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
-      if (s.fail[node] != KSIM_PASSED) continue;
-      const bool ign = has_soft && lacks_soft_key(node);
+  }
+  __syncthreads();
+  if (tid < 2 * KSIM_MAX_SCORE && tid < 2 * S && norm_kind(prof.score[tid >> 1]) != kNormNone) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
+    if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->ext[tid]), (unsigned long long)m);
+  }
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_profile prof,
+                                                const DevState* __restrict__ st, DevScratch s, DevEvalOut o) {
+  __shared__ uint64_t s_best[4];
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  WinState* win = s.win;
+  const ksim_pod& p = P.pods[pi];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t node = blockIdx.x * blockDim.x + tid;
+  const int32_t N = c.n;
+  const int S = prof.n_score;
+  const int32_t nf = win->nf;
+  uint64_t key = 0;
+  if (node < N) {
+    const bool kept = nf > 1 && kept_node(s, node, st->next_start, N, win->kend);
+    if (kept) {
+      const bool ign = win->has_soft && s.ign[node];
+      const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
       int64_t tot = S == 0 ? 1 : s.part[node];
       for (int k = 0; k < S; k++) {
         const int32_t kind = norm_kind(prof.score[k]);
@@ -496,7 +536,8 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
           if (kind == kNormPTS && ign)
             nv = 0;
           else
-            nv = normalize_value(kind, raw, s_gmax[k], s_gmin[k], ipa_nonempty);
+            nv = normalize_value(kind, raw, from_max_image(win->ext[2 * k]), from_min_image(win->ext[2 * k + 1]),
+                                 ipa_nonempty);
           const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
           tot += nv * w;
         }
@@ -509,53 +550,63 @@ __global__ __launch_bounds__(kFinalThreads) void k_finalize(DevCluster c, DevPod
         o.total[node] = tot;
         o.scored[node] = 1;
       }
-      const uint64_t key = tb_key(tot, prof.tiebreak_seed, seq, c.base + node);
-      best = key > best ? key : best;
-    }
-    best = block_max_u64<kFinalWaves>(best, shu);
-    chosen = key_node(best) - c.base;               // the per-pod path is never sharded: base == 0
-  }
-
-  // Restore the all-zero domain tables for the next pod (every entry this
-  // pod touched is the value of some node's key).
-  if (nu) {
-    __syncthreads();
-    for (int i = 0; i < nu; i++) {
-      const ksim_topo_use u = s_use[i];
-      if (u.col == KSIM_COL_NONE || (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME))) continue;
-      int64_t* d = s.dom + (size_t)i * c.vmax;
-      if (c.col_nvals[u.col] <= 4 * kFinalThreads) {
-        for (int32_t v = tid; v < c.col_nvals[u.col]; v += kFinalThreads) d[v] = 0;
-      } else {
-        for (int32_t node = tid; node < N; node += kFinalThreads) d[use_value(c, u, node)] = 0;
+      key = tb_key(tot, prof.tiebreak_seed, st->pod_seq, c.base + node);
+    } else if (COMPAT) {
+      o.total[node] = 0;
+      o.scored[node] = 0;
+      for (int k = 0; k < S; k++) {
+        o.raw[(size_t)k * N + node] = 0;
+        o.norm[(size_t)k * N + node] = 0;
       }
     }
-  }
-
-  // Phase D: assume/bind + scheduler state.
-  if (tid == 0) {
-    int32_t ns = start + (cut < N ? cut : N);
-    ns %= N;
-    st->next_start = ns;
-    st->evals += evaluated;
-    if (chosen >= 0) {
-      assume_pod(c, P, p, chosen, 1);
-      st->scheduled += 1;
-    } else {
-      st->unschedulable += 1;
+    // the domain tables are read no more this cycle: re-zero what this node's
+    // values touched (every touched entry is some node's value)
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (u.col == KSIM_COL_NONE || (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME))) continue;
+      s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
     }
-    if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : -1;
-    st->chosen = chosen;
-    st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : KSIM_STATUS_UNSCHEDULABLE;
-    st->n_feasible = nf;
-    st->n_evaluated = evaluated;
-    st->n_processed = cut < N ? cut : N;
-    st->k_to_find = K;
-    st->next_start_after = ns;
-    st->pod_seq = seq + 1;
-    st->topo_flags = 0;
-    st->cursor = pi + 1;
   }
+  key = wave_max_u64_dpp(key);
+  if (lane == 0) s_best[wv] = key;
+  __syncthreads();
+  if (tid == 0) {
+    const uint64_t m = umax64(umax64(s_best[0], s_best[1]), umax64(s_best[2], s_best[3]));
+    if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->best), (unsigned long long)m);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
+                                             int32_t* __restrict__ chosen_out) {
+  const int32_t pi = st->cursor;
+  if (pi >= st->end || threadIdx.x != 0) return;
+  const WinState* win = s.win;
+  const int32_t N = c.n, nf = win->nf, cut = win->cut;
+  int32_t chosen = -1;
+  if (nf == 1) chosen = win->single;
+  else if (nf > 1) chosen = key_node(win->best) - c.base;   // the per-pod path is never sharded: base == 0
+  const ksim_pod& p = P.pods[pi];
+  int32_t ns = st->next_start + (cut < N ? cut : N);
+  ns %= N;
+  st->next_start = ns;
+  st->evals += win->evaluated;
+  if (chosen >= 0) {
+    assume_pod(c, P, p, chosen, 1);
+    st->scheduled += 1;
+  } else {
+    st->unschedulable += 1;
+  }
+  if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : -1;
+  st->chosen = chosen;
+  st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : KSIM_STATUS_UNSCHEDULABLE;
+  st->n_feasible = nf;
+  st->n_evaluated = win->evaluated;
+  st->n_processed = cut < N ? cut : N;
+  st->k_to_find = win->k;
+  st->next_start_after = ns;
+  st->pod_seq += 1;
+  st->topo_flags = 0;
+  st->cursor = pi + 1;
 }
 
 __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int sign) {
@@ -564,7 +615,7 @@ __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int
 
 // ---- launchers ----------------------------------------------------------------
 const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_min", "k_filter_score",
-                                                    "k_finalize"};
+                                                    "k_window", "k_extrema", "k_select", "k_bind"};
 
 void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
   const int blocks = (a.c.n + 255) / 256;
@@ -579,10 +630,19 @@ void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool top
     k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[3], stream);
   if (compat)
-    k_finalize<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
+    k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   else
-    k_finalize<false><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, a.chosen);
+    k_window<false><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[4], stream);
+  k_extrema<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[5], stream);
+  if (compat)
+    k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  else
+    k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  if (evs) (void)hipEventRecord(evs[6], stream);
+  k_bind<<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+  if (evs) (void)hipEventRecord(evs[7], stream);
 }
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {

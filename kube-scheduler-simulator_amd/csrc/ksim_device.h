@@ -100,10 +100,14 @@ constexpr int64_t kDomCountMask = (1ll << kDomMarkShift) - 1;
 struct BRow;
 
 // Selection state of one per-pod cycle (k_window -> k_extrema -> k_select -> k_bind).
+// ext[kExtCut] (sharded cycles): 1 + the scan position of the cut node on the
+// shard that holds it, 0 elsewhere; all-reduced (max) together with the extrema.
+constexpr int kExtCut = 2 * KSIM_MAX_SCORE;
+constexpr int kExtWords = kExtCut + 1;
 struct WinState {
-  int32_t cut, kend, nf, evaluated, k, has_soft, single, _pad;
+  int32_t cut, kend, nf, evaluated, k, has_soft;
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
-  uint64_t ext[2 * KSIM_MAX_SCORE];      // per score slot: max image, min image (atomicMax)
+  uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
   uint64_t best;                         // TB argmax key
 };
 
@@ -112,6 +116,8 @@ struct DevScratch {
   uint8_t* fail;         // [n] filter-order index of first failure or KSIM_PASSED
   uint8_t* ign;          // [n] feasible node missing a ScheduleAnyway spread key (IgnoredNodes)
   WinState* win;
+  int64_t* xdom;         // sharded cycle: packed domain sums (all-reduced, sum)
+  int64_t* xreg;         // sharded cycle: IgnoredNodes count + per-value registrations (all-reduced, sum)
   uint32_t* detail;      // [n]
   int64_t* raw;          // [KSIM_MAX_SCORE][n] raw scores (normalized slots; all in compat)
   int64_t* part;         // [n] sum of weighted raw of slots without NormalizeScore
@@ -530,6 +536,15 @@ __device__ __forceinline__ int64_t class_count(const DevCluster& c, int32_t cls,
 }
 __device__ __forceinline__ const int64_t* dom_of(const DevCluster& c, const DevScratch& s, int u) {
   return s.dom + (size_t)u * c.vmax;
+}
+// A use whose domain table k_topo_prefilter fills (PTS soft on hostname reads
+// the node's own count instead).
+__host__ __device__ __forceinline__ bool use_needs_dom(const ksim_topo_use& u) {
+  return u.col != KSIM_COL_NONE && !(u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME));
+}
+// A PTS soft use that registers its topology pairs by value (not hostname).
+__host__ __device__ __forceinline__ bool use_registers_values(const ksim_topo_use& u) {
+  return u.kind == KSIM_USE_PTS_SOFT && u.col != KSIM_COL_NONE && !(u.flags & KSIM_USEF_HOSTNAME);
 }
 
 // FindMatchingUntoleratedTaint straight from the taint columns (no NodeRow).

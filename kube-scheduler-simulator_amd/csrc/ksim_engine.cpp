@@ -103,6 +103,8 @@ struct ksim_handle {
   std::vector<DevBuf> pod_bufs;
   std::vector<uint8_t> batchable;       // per loaded pod
   std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
+  std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
+  std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
@@ -444,6 +446,87 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   return KSIM_OK;
 }
 
+// ---- node-sharded per-pod cycle (C1 extrema, C2 argmax, C3 window) ----
+// Element-wise all-reduce of a per-handle device buffer of `count` 8-byte words:
+// sum (int64) or max (uint64).  RCCL across processes, a group kernel in-process.
+template <typename F>
+int x_allreduce(const std::vector<ksim_handle*>& hs, F&& ptr, int64_t count, bool op_max, hipStream_t stream) {
+  if (count <= 0) return KSIM_OK;
+  ksim_handle* h0 = hs[0];
+  if (h0->comm) {
+    void* b = (void*)ptr(h0);
+    const ncclResult_t r = rccl().all_reduce(b, b, (size_t)count, op_max ? ncclUint64 : ncclInt64,
+                                             op_max ? ncclMax : ncclSum, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllReduce: ") + rccl().error_string(r));
+  } else if (hs.size() > 1) {
+    GroupPtrs g{};
+    g.n = (int32_t)hs.size();
+    for (size_t i = 0; i < hs.size(); i++) g.p[i] = (uint64_t*)ptr(hs[i]);
+    launch_group_reduce(g, count, op_max, stream);
+  }
+  return KSIM_OK;
+}
+
+// One per-pod cycle (the pod at the shards' common cursor) across node shards.
+int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t stream) {
+  ksim_handle* h0 = hs[0];
+  const int R = (int)hs.size();
+  const bool topo = h0->topo[pod] != 0;
+  const int64_t xdom = h0->xdom_len[pod], xreg = h0->xreg_len[pod];
+  int rc;
+  if (topo) {
+    for (auto* h : hs) launch_pshard_topo(make_args(h, h->dp, h->d_chosen), stream);
+    if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.xdom; }, xdom, false, stream))) return rc;
+  }
+  for (auto* h : hs) launch_pshard_filter(make_args(h, h->dp, h->d_chosen), topo, stream);
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, 2, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+  } else {
+    GroupPtrs src{}, dst{};
+    src.n = dst.n = R;
+    for (int i = 0; i < R; i++) {
+      src.p[i] = hs[i]->sc.xsend;
+      dst.p[i] = hs[i]->sc.xrecv;
+    }
+    launch_group_gather(src, dst, 2, stream);
+  }
+  const int32_t world = h0->comm ? h0->world : R;
+  for (int i = 0; i < R; i++)
+    launch_pshard_window(make_args(hs[i], hs[i]->dp, hs[i]->d_chosen), h0->comm ? h0->rank : i, world, stream);
+  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.xreg; }, xreg, false, stream))) return rc;
+  for (auto* h : hs) launch_pshard_extrema(make_args(h, h->dp, h->d_chosen), xreg > 0, stream);
+  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.win->ext; }, kExtWords, true, stream))) return rc;
+  for (auto* h : hs) launch_pshard_select(make_args(h, h->dp, h->d_chosen), stream);
+  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return &h->sc.win->best; }, 1, true, stream))) return rc;
+  for (auto* h : hs) launch_pshard_bind(make_args(h, h->dp, h->d_chosen), stream);
+  HIPCHK(h0, hipGetLastError());
+  return KSIM_OK;
+}
+
+// Pods [a, b) on the sharded per-pod path, one cycle each.
+int shard_run_perpod(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
+  ksim_handle* h0 = hs[0];
+  hipStream_t stream = h0->stream;
+  for (auto* h : hs) {
+    int rc;
+    if ((rc = set_run(h, a, b))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  for (int32_t i = a; i < b; i++) {
+    int rc = shard_cycle(hs, i, stream);
+    if (rc) return rc;
+  }
+  return KSIM_OK;
+}
+
+// A sharded run: batchable stretches on the batch protocol, the rest cycle by cycle.
+int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t count) {
+  return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool) {
+    return batch ? shard_run(hs, a, b) : shard_run_perpod(hs, a, b);
+  });
+}
+
 bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
 
 int reset_counters(ksim_handle* h, hipStream_t stream) {
@@ -709,6 +792,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);
   SCR(s.xrecv, uint64_t*, 8 * (size_t)kMaxShards * kBatchPods * kXRec);
   SCR(s.min_match, int64_t*, 8 * (size_t)KSIM_MAX_USES);
+  SCR(s.xdom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
+  SCR(s.xreg, int64_t*, 8 * (1 + (size_t)KSIM_MAX_USES * vmax));
   SCR(o.scored, uint8_t*, N);
   SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(o.norm, int64_t*, 8 * N * KSIM_MAX_SCORE);
@@ -908,9 +993,21 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   std::vector<int32_t> bf((size_t)std::max(ps->n_pods, 1), 0);
   h->batchable.assign((size_t)ps->n_pods, 0);
   h->topo.assign((size_t)ps->n_pods, 0);
+  h->xdom_len.assign((size_t)ps->n_pods, 0);
+  h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
     h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
+    // sharded-cycle exchange sizes, laid out as k_dom_pack / k_window_sh do
+    bool soft = false;
+    int64_t xr = 1;
+    for (int32_t k = 0; k < ps->pods[i].use_count; k++) {
+      const ksim_topo_use& u = ps->uses[ps->pods[i].use_first + k];
+      if (use_needs_dom(u)) h->xdom_len[i] += h->col_nvals[u.col];
+      if (use_registers_values(u)) xr += h->col_nvals[u.col];
+      soft = soft || u.kind == KSIM_USE_PTS_SOFT;
+    }
+    h->xreg_len[i] = soft ? xr : 0;
     bf[i] = static_trivial(h, ps->pods[i]) ? kBatchStaticTrivial : 0;
   }
   DevPods P{};
@@ -951,10 +1048,8 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   if (is_sharded(h)) {
-    for (int32_t i = first; i < first + count; i++)
-      if (!h->batchable[i])
-        return set_err(h, KSIM_E_UNSUPPORTED, "node-sharded runs take batchable pods only (P100, no topology uses)");
-    if (count && (rc = shard_run({h}, first, first + count))) return rc;
+    for (int32_t i = first; i < first + count; i++) perpod += h->batchable[i] ? 0 : 1;
+    rc = shard_schedule({h}, first, count);
   } else {
     rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
       if (!batch) perpod += b - a;
@@ -1040,14 +1135,12 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
   }
   if (expect != h0->dc.n_total) return set_err(h0, KSIM_E_INVALID, "shards must tile the cluster");
   if (first < 0 || count < 0 || first + count > h0->dp.n_pods) return set_err(h0, KSIM_E_INVALID, "range out of loaded pods");
-  for (int32_t i = first; i < first + count; i++)
-    if (!h0->batchable[i]) return set_err(h0, KSIM_E_UNSUPPORTED, "node-sharded runs take batchable pods only");
   HIPCHK(h0, hipSetDevice(h0->device));
   int rc;
   for (auto* h : v)
     if ((rc = reset_counters(h, h->stream))) return rc;
   HIPCHK(h0, hipEventRecord(h0->ev0, h0->stream));
-  if (count && (rc = shard_run(v, first, first + count))) return rc;
+  if (count && (rc = shard_schedule(v, first, count))) return rc;
   HIPCHK(h0, hipEventRecord(h0->ev1, h0->stream));
   HIPCHK(h0, hipEventSynchronize(h0->ev1));
   if (chosen && count) HIPCHK(h0, hipMemcpy(chosen, h0->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));

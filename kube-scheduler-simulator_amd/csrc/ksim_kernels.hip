@@ -243,12 +243,41 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P,
 
 // TpKeyToCriticalPaths: per hard constraint, the minimum over its present pairs
 // (math.MaxInt32 when no eligible node carries the key).
-__global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, const DevState* __restrict__ st,
-                                                  DevScratch s) {
+// Sharded (SHARDED): first unpack the all-reduced domain sums (s.xdom, packed by
+// k_dom_pack) into the domain tables and re-derive the two topology flags from
+// them (every class count is >= 0, so a domain sum is non-zero exactly when
+// some node's count is).
+template <bool SHARDED>
+__global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_profile prof,
+                                                  DevState* __restrict__ st, DevScratch s) {
   __shared__ int64_t sh[4];
+  __shared__ uint32_t s_flags;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const ksim_pod& p = P.pods[pi];
+  if (SHARDED) {
+    if (threadIdx.x == 0) s_flags = 0;
+    __syncthreads();
+    uint32_t flags = 0;
+    int64_t off = 0;
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (!use_needs_dom(u)) continue;
+      const int32_t V = c.col_nvals[u.col];
+      int64_t* d = s.dom + (size_t)i * c.vmax;
+      const bool aff = u.kind == KSIM_USE_IPA_AFFINITY, sc = ipa_coef(prof, u) != 0;
+      for (int32_t v = threadIdx.x; v < V; v += blockDim.x) {
+        const int64_t x = s.xdom[off + v];
+        d[v] = x;
+        if (aff && x > 0) flags |= kTopoAffinityNonEmpty;
+        if (sc && x != 0) flags |= kTopoScoreNonEmpty;
+      }
+      off += V;
+    }
+    if (flags) atomicOr(&s_flags, flags);
+    __syncthreads();
+    if (threadIdx.x == 0) st->topo_flags = s_flags;
+  }
   for (int i = 0; i < p.use_count; i++) {
     const ksim_topo_use u = P.uses[p.use_first + i];
     if (u.kind != KSIM_USE_PTS_HARD) continue;
@@ -407,7 +436,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
       if (tid == 0) win->w[i] = c.topo_log[size];
     }
   }
-  if (tid < 2 * KSIM_MAX_SCORE) win->ext[tid] = 0;
+  if (tid < kExtWords) win->ext[tid] = 0;
   if (tid == 0) {
     win->cut = cut;
     win->kend = kend;
@@ -416,23 +445,18 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     win->has_soft = has_soft;
     win->k = K;
     win->best = 0;
-    win->single = -1;
-  }
-  if (nf == 1) {
-    for (int32_t r = tid; r < kend; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
-      if (s.fail[node] == KSIM_PASSED) win->single = node;
-    }
   }
 }
 
-// Rotated scan position of a node and whether it is in the kept list.
-__device__ __forceinline__ bool kept_node(const DevScratch& s, int32_t node, int32_t start, int32_t n,
+// Position of global node g in the scan from nextStartNodeIndex, and whether a
+// (local) node is in the kept list (feasible and scanned before the cut).
+__device__ __forceinline__ int32_t rot_pos(int32_t g, int32_t start, int32_t n_total) {
+  const int32_t r = g - start;
+  return r < 0 ? r + n_total : r;
+}
+__device__ __forceinline__ bool kept_node(const DevCluster& c, const DevScratch& s, int32_t node, int32_t start,
                                           int32_t kend) {
-  int32_t r = node - start;
-  if (r < 0) r += n;
-  return r < kend && s.fail[node] == KSIM_PASSED;
+  return rot_pos(c.base + node, start, c.n_total) < kend && s.fail[node] == KSIM_PASSED;
 }
 
 __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_profile prof,
@@ -455,7 +479,7 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
   __syncthreads();
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
-  const bool kept = node < N && kept_node(s, node, st->next_start, N, win->kend);
+  const bool kept = node < N && kept_node(c, s, node, st->next_start, win->kend);
   const int S = prof.n_score;
 #pragma unroll
   for (int k = 0; k < KSIM_MAX_SCORE; k++) {
@@ -523,8 +547,8 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_pr
   const int32_t nf = win->nf;
   uint64_t key = 0;
   if (node < N) {
-    const bool kept = nf > 1 && kept_node(s, node, st->next_start, N, win->kend);
-    if (kept) {
+    const bool kept = nf >= 1 && kept_node(c, s, node, st->next_start, win->kend);
+    if (kept && nf > 1) {
       const bool ign = win->has_soft && s.ign[node];
       const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
       int64_t tot = S == 0 ? 1 : s.part[node];
@@ -551,12 +575,16 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_pr
         o.scored[node] = 1;
       }
       key = tb_key(tot, prof.tiebreak_seed, st->pod_seq, c.base + node);
-    } else if (COMPAT) {
+    } else {
+      // one feasible node: schedulePod returns it without scoring
+      if (kept) key = tb_key(0, prof.tiebreak_seed, st->pod_seq, c.base + node);
+      if (COMPAT) {
       o.total[node] = 0;
       o.scored[node] = 0;
       for (int k = 0; k < S; k++) {
         o.raw[(size_t)k * N + node] = 0;
         o.norm[(size_t)k * N + node] = 0;
+      }
       }
     }
     // the domain tables are read no more this cycle: re-zero what this node's
@@ -582,9 +610,7 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   if (pi >= st->end || threadIdx.x != 0) return;
   const WinState* win = s.win;
   const int32_t N = c.n, nf = win->nf, cut = win->cut;
-  int32_t chosen = -1;
-  if (nf == 1) chosen = win->single;
-  else if (nf > 1) chosen = key_node(win->best) - c.base;   // the per-pod path is never sharded: base == 0
+  const int32_t chosen = win->best ? key_node(win->best) : -1;   // unsharded: base == 0
   const ksim_pod& p = P.pods[pi];
   int32_t ns = st->next_start + (cut < N ? cut : N);
   ns %= N;
@@ -613,6 +639,275 @@ __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int
   if (threadIdx.x == 0 && blockIdx.x == 0) assume_pod(c, P, P.pods[pod], node, sign);
 }
 
+// ==== C. node-sharded per-pod cycle ================================
+// Each shard holds the nodes [c.base, c.base + c.n) of c.n_total.  A cycle is
+// the unsharded one with exchanges at its grid-wide seams (the host issues
+// them between these launches; ksim_engine.cpp shard_cycle):
+//   k_topo_prefilter, k_dom_pack  -> all-reduce (sum) of the packed domain sums
+//   k_topo_min<true>               unpack, flags, critical paths
+//   k_filter_score, k_wcount_sh    -> all-gather of (feasible >= start, feasible < start)
+//   k_window_sh                    global cut / kept rule / IgnoredNodes and pair
+//                                  registrations -> all-reduce (sum) of s.xreg
+//   k_wfinal_sh, k_extrema         -> all-reduce (max) of the extrema images + cut
+//   k_select                       -> all-reduce (max) of the TB key
+//   k_bind_sh                      the owner shard binds; every shard advances
+// Scan order is the global rotated order, so a shard's nodes form at most two
+// contiguous runs of it: "hi" (global index >= start) and "lo" (< start).
+
+// Pack the domain rows a sharded exchange sums: use i's row (col_nvals entries)
+// at the running offset, uses in order (the host sizes the exchange the same way).
+__global__ __launch_bounds__(256) void k_dom_pack(DevCluster c, DevPods P, const DevState* __restrict__ st,
+                                                  DevScratch s) {
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const ksim_pod& p = P.pods[pi];
+  int64_t off = 0;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use u = P.uses[p.use_first + i];
+    if (!use_needs_dom(u)) continue;
+    const int32_t V = c.col_nvals[u.col];
+    const int64_t* d = s.dom + (size_t)i * c.vmax;
+    for (int32_t v = threadIdx.x; v < V; v += blockDim.x) s.xdom[off + v] = d[v];
+    off += V;
+  }
+}
+
+// Local feasible counts of the two runs -> s.xsend[0..1]; zeroes s.xreg for k_window_sh.
+__global__ __launch_bounds__(kFinalThreads) void k_wcount_sh(DevCluster c, DevPods P, const DevState* __restrict__ st,
+                                                             DevScratch s) {
+  __shared__ int32_t sh32[kFinalWaves];
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const int tid = threadIdx.x;
+  const int32_t n = c.n;
+  const int32_t split = min(n, max(0, st->next_start - c.base));   // local [split, n) is "hi"
+  int32_t hi = 0, lo = 0;
+  for (int32_t x = tid; x < n; x += kFinalThreads) {
+    const bool f = s.fail[x] == KSIM_PASSED;
+    if (x >= split) hi += f; else lo += f;
+  }
+  hi = block_sum_i32_nw<kFinalWaves>(hi, sh32);
+  lo = block_sum_i32_nw<kFinalWaves>(lo, sh32);
+  if (tid == 0) {
+    s.xsend[0] = (uint64_t)hi;
+    s.xsend[1] = (uint64_t)lo;
+  }
+  const ksim_pod& p = P.pods[pi];
+  int64_t len = 1;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use u = P.uses[p.use_first + i];
+    if (use_registers_values(u)) len += c.col_nvals[u.col];
+  }
+  bool any_soft = false;
+  for (int i = 0; i < p.use_count; i++) any_soft = any_soft || P.uses[p.use_first + i].kind == KSIM_USE_PTS_SOFT;
+  if (any_soft)
+    for (int64_t x = tid; x < len; x += kFinalThreads) s.xreg[x] = 0;
+}
+
+// The j-th (0-based) feasible node of local [lo, hi) in node order (block-wide).
+__device__ int32_t block_nth_feasible(const uint8_t* __restrict__ fail, int32_t lo, int32_t hi, int32_t j,
+                                      int32_t* sh32, int32_t* s_out) {
+  const int tid = threadIdx.x;
+  const int32_t len = hi - lo, chunk = (len + kFinalThreads - 1) / kFinalThreads;
+  const int32_t a = lo + min(len, tid * chunk), b = min(hi, a + chunk);
+  int32_t cnt = 0;
+  for (int32_t x = a; x < b; x++) cnt += fail[x] == KSIM_PASSED;
+  int32_t excl, total;
+  block_scan_i32(cnt, excl, total, sh32);
+  if (tid == 0) *s_out = -1;
+  __syncthreads();
+  if (excl <= j && j < excl + cnt) {
+    int32_t run = excl;
+    for (int32_t x = a; x < b; x++) {
+      if (fail[x] == KSIM_PASSED) {
+        if (run == j) {
+          *s_out = x;
+          break;
+        }
+        run++;
+      }
+    }
+  }
+  __syncthreads();
+  return *s_out;
+}
+
+// Global numFeasibleNodesToFind window from the gathered counts (s.xrecv[world][2]):
+// the cut is the K-th (0-based) feasible node of the global scan; this shard's
+// kept rule is "scan position < win->kend".  Then this shard's IgnoredNodes
+// count and pair registrations over its kept nodes -> s.xreg.
+__global__ __launch_bounds__(kFinalThreads) void k_window_sh(DevCluster c, DevPods P, ksim_profile prof,
+                                                             const DevState* __restrict__ st, DevScratch s,
+                                                             int32_t rank, int32_t world) {
+  __shared__ int32_t sh32[kFinalWaves];
+  __shared__ int32_t s_out;
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const int tid = threadIdx.x;
+  const ksim_pod& p = P.pods[pi];
+  WinState* win = s.win;
+  const int32_t N = c.n_total, n = c.n, base = c.base;
+  const int32_t K = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, N);
+  const int32_t start = st->next_start;
+  int64_t T = 0, all_hi = 0, bhi = 0, blo = 0, fhi = 0, flo = 0;
+  for (int t = 0; t < world; t++) {
+    const int64_t h = (int64_t)s.xrecv[2 * t], l = (int64_t)s.xrecv[2 * t + 1];
+    T += h + l;
+    all_hi += h;
+    if (t < rank) {
+      bhi += h;
+      blo += l;
+    }
+    if (t == rank) {
+      fhi = h;
+      flo = l;
+    }
+  }
+  blo += all_hi;
+  const int32_t split = min(n, max(0, start - base));
+  int32_t kend, cutslot = 0;
+  if (T <= K) {
+    kend = N;
+  } else if (bhi <= K && K < bhi + fhi) {
+    const int32_t x = block_nth_feasible(s.fail, split, n, (int32_t)(K - bhi), sh32, &s_out);
+    kend = base + x - start;
+    cutslot = kend + 1;
+  } else if (blo <= K && K < blo + flo) {
+    const int32_t x = block_nth_feasible(s.fail, 0, split, (int32_t)(K - blo), sh32, &s_out);
+    kend = base + x - start + N;
+    cutslot = kend + 1;
+  } else if (blo + flo <= K) {
+    kend = N;                                  // both runs before the cut
+  } else if (bhi + fhi <= K && split < n) {
+    kend = base + n - start;                   // the hi run before the cut, the lo run after
+  } else {
+    kend = 0;
+  }
+  const int32_t nf = (int32_t)(T < K ? T : K);
+  bool any_soft = false;
+  for (int i = 0; i < p.use_count; i++) any_soft = any_soft || P.uses[p.use_first + i].kind == KSIM_USE_PTS_SOFT;
+  if (any_soft) {
+    int32_t nign = 0;
+    for (int32_t x = tid; x < n; x += kFinalThreads) {
+      if (!kept_node(c, s, x, start, kend)) continue;
+      if (s.ign[x]) {
+        nign++;
+        continue;
+      }
+      int64_t off = 1;
+      for (int i = 0; i < p.use_count; i++) {
+        const ksim_topo_use u = P.uses[p.use_first + i];
+        if (!use_registers_values(u)) continue;
+        atomicAdd(reinterpret_cast<unsigned long long*>(s.xreg + off + use_value(c, u, x)), 1ull);
+        off += c.col_nvals[u.col];
+      }
+    }
+    nign = block_sum_i32_nw<kFinalWaves>(nign, sh32);
+    if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(s.xreg), (unsigned long long)nign);
+  }
+  if (tid < kExtWords) win->ext[tid] = tid == kExtCut ? (uint64_t)cutslot : 0ull;
+  if (tid == 0) {
+    win->kend = kend;
+    win->nf = nf;
+    win->k = K;
+    win->has_soft = nf > 1 && any_soft;
+    win->best = 0;
+  }
+}
+
+// topologyNormalizingWeight from the all-reduced registrations.
+__global__ __launch_bounds__(256) void k_wfinal_sh(DevCluster c, DevPods P, const DevState* __restrict__ st,
+                                                   DevScratch s) {
+  __shared__ int32_t sh32[4];
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  WinState* win = s.win;
+  if (!win->has_soft) return;
+  const ksim_pod& p = P.pods[pi];
+  const int64_t nign = (int64_t)s.xreg[0];
+  int64_t off = 1;
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use u = P.uses[p.use_first + i];
+    if (u.kind != KSIM_USE_PTS_SOFT) continue;
+    int32_t size = 0;
+    if (u.flags & KSIM_USEF_HOSTNAME) {
+      size = (int32_t)(win->nf - nign);
+    } else if (u.col != KSIM_COL_NONE) {
+      const int32_t V = c.col_nvals[u.col];
+      int32_t cnt = 0;
+      for (int32_t v = threadIdx.x; v < V; v += blockDim.x) cnt += v != 0 && s.xreg[off + v] > 0;
+      size = block_sum_i32_nw<4>(cnt, sh32);
+      off += V;
+    }
+    if (threadIdx.x == 0) win->w[i] = c.topo_log[size];
+  }
+}
+
+// selectHost result (global), the owner shard's bind, scheduler state on every shard.
+__global__ __launch_bounds__(256) void k_bind_sh(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
+                                                 int32_t* __restrict__ chosen_out) {
+  const int32_t pi = st->cursor;
+  if (pi >= st->end) return;
+  const ksim_pod& p = P.pods[pi];
+  // the exchanged domain rows hold other shards' values too: re-zero them whole
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use u = P.uses[p.use_first + i];
+    if (!use_needs_dom(u)) continue;
+    const int32_t V = c.col_nvals[u.col];
+    for (int32_t v = threadIdx.x; v < V; v += blockDim.x) s.dom[(size_t)i * c.vmax + v] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const WinState* win = s.win;
+  const int32_t N = c.n_total, n = c.n, base = c.base, start = st->next_start;
+  const int32_t chosen = win->best ? key_node(win->best) : -1;
+  const int32_t local = chosen - base;
+  const int64_t cs = (int64_t)win->ext[kExtCut];
+  const int32_t processed = cs ? (int32_t)(cs - 1) : N;
+  const int32_t evaluated = cs ? (int32_t)cs : N;
+  // this shard's nodes among the evaluated scan prefix
+  const int32_t split = min(n, max(0, start - base));
+  auto in_prefix = [&](int32_t r0, int32_t len) { return min(max(evaluated - r0, 0), len); };
+  const int32_t local_eval = in_prefix(base + split - start, n - split) + in_prefix(base - start + N, split);
+  const int32_t ns = (int32_t)(((int64_t)start + processed) % N);
+  st->next_start = ns;
+  st->evals += local_eval;
+  if (chosen >= 0 && local >= 0 && local < n) assume_pod(c, P, p, local, 1);
+  if (chosen >= 0)
+    st->scheduled += 1;
+  else
+    st->unschedulable += 1;
+  if (chosen_out) chosen_out[pi] = chosen;
+  st->chosen = chosen;
+  st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : KSIM_STATUS_UNSCHEDULABLE;
+  st->n_feasible = win->nf;
+  st->n_evaluated = evaluated;
+  st->n_processed = processed;
+  st->k_to_find = win->k;
+  st->next_start_after = ns;
+  st->pod_seq += 1;
+  st->topo_flags = 0;
+  st->cursor = pi + 1;
+}
+
+// In-process shard group exchanges (one device): element-wise sum / max over
+// the group's buffers written back to every member, and the all-gather.
+__global__ __launch_bounds__(256) void k_group_reduce(GroupPtrs g, int64_t count, int32_t op_max) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t acc = g.p[0][i];
+    for (int r = 1; r < g.n; r++) acc = op_max ? umax64(acc, g.p[r][i]) : acc + g.p[r][i];
+    for (int r = 0; r < g.n; r++) g.p[r][i] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_group_gather(GroupPtrs src, GroupPtrs dst, int32_t words) {
+  const int32_t total = src.n * src.n * words;
+  for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int32_t r = i / (src.n * words), q = (i / words) % src.n, w = i % words;
+    dst.p[r][q * words + w] = src.p[q][w];
+  }
+}
+
 // ---- launchers ----------------------------------------------------------------
 const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_min", "k_filter_score",
                                                     "k_window", "k_extrema", "k_select", "k_bind"};
@@ -622,7 +917,7 @@ void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool top
   if (evs) (void)hipEventRecord(evs[0], stream);
   if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  if (topo) k_topo_min<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s);
+  if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[2], stream);
   if (compat)
     k_filter_score<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
@@ -647,6 +942,48 @@ void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool top
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
   k_assume<<<1, 64, 0, stream>>>(c, P, pod, node, sign);
+}
+
+void launch_pshard_topo(const LaunchArgs& a, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_dom_pack<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s);
+}
+
+void launch_pshard_filter(const LaunchArgs& a, bool topo, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  if (topo) k_topo_min<true><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_wcount_sh<<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.st, a.s);
+}
+
+void launch_pshard_window(const LaunchArgs& a, int32_t rank, int32_t world, hipStream_t stream) {
+  k_window_sh<<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, rank, world);
+}
+
+void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  if (soft) k_wfinal_sh<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s);
+  k_extrema<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+}
+
+void launch_pshard_select(const LaunchArgs& a, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+}
+
+void launch_pshard_bind(const LaunchArgs& a, hipStream_t stream) {
+  k_bind_sh<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+}
+
+void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStream_t stream) {
+  if (count <= 0) return;
+  const int blocks = (int)std::min<int64_t>((count + 255) / 256, 1024);
+  k_group_reduce<<<blocks, 256, 0, stream>>>(g, count, op_max ? 1 : 0);
+}
+
+void launch_group_gather(const GroupPtrs& src, const GroupPtrs& dst, int32_t words, hipStream_t stream) {
+  k_group_gather<<<1, 256, 0, stream>>>(src, dst, words);
 }
 
 }  // namespace ksim

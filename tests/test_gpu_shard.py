@@ -100,3 +100,62 @@ def test_rccl_world1():
     ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals
+
+
+# ---- sharded per-pod cycle (ADAPT window, per-node normalized scores, topology) ----
+
+def _check_group(cluster, pods, prof, world):
+    engines = _group(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled and st.unschedulable == ost.unschedulable
+    for e in engines:
+        assert e.next_start == ora.next_start
+    es, os_ = _node_state(engines), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+    return engines, ora
+
+
+@pytest.mark.parametrize("pct,world", [(0, 2), (100, 3), (0, 8)])
+def test_group_perpod_config1(pct, world):
+    """Taints, node affinity, per-node-varying normalized scores; ADAPT windows
+    that cut inside and across shards; P100 runs mixing batch and per-pod pods."""
+    cluster, pods = gen.config1()
+    _check_group(cluster, pods, _prof_pct(pct), world)
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_group_adapt_config2(world):
+    cluster, pods = gen.config2(n_nodes=1200, n_pods=1500)
+    _check_group(cluster, pods, _prof_pct(0), world)
+
+
+@pytest.mark.parametrize("pct,world", [(0, 2), (100, 4), (0, 8)])
+def test_group_config3(pct, world):
+    """PodTopologySpread + InterPodAffinity: domain sums exchanged, global
+    critical paths, IgnoredNodes and pair registrations over the global kept list."""
+    cluster, pods = gen.config3(n_nodes=600, pods_per_node=10, n_incoming=700, seed=21, zone_anti_every=50)
+    engines, ora = _check_group(cluster, pods, _prof_pct(pct), world)
+    np.testing.assert_array_equal(np.concatenate([e.class_count() for e in engines], axis=1), ora.class_count())
+
+
+def test_rccl_world1_perpod():
+    cluster, pods = gen.config3(n_nodes=500, pods_per_node=10, n_incoming=400, seed=22)
+    prof = _prof_pct(0)
+    e = Engine(0)
+    e.set_shard(0, cluster.n_nodes)
+    e.set_profile(prof)
+    e.set_cluster(cluster)
+    e.comm_init(0, 1, engine.comm_unique_id())
+    e.load_pods(pods)
+    chosen, st = e.schedule_loaded(0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals
+
+
+def _prof_pct(pct, seed=0x4B53494D):
+    return profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=pct, tiebreak_seed=seed))

@@ -169,3 +169,79 @@ def schedule(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed
         cursor += committed
         seq0 += committed
     return chosen
+
+
+def num_feasible_nodes_to_find(n: int, pct: int) -> int:
+    """numFeasibleNodesToFind."""
+    if n < 100 or pct >= 100:
+        return n
+    p = pct if pct > 0 else max(5, 50 - n // 125)
+    return max(n * p // 100, 100)
+
+
+def window(counts, rank: int, n_total: int, K: int, base: int, n: int, start: int, fail_ok: np.ndarray):
+    """k_window_sh: the global cut from every shard's (feasible >= start,
+    feasible < start) counts.  Returns (kend, cutslot): this shard keeps its
+    feasible nodes at scan position < kend; cutslot = 1 + the cut's scan
+    position on the shard that holds it, else 0."""
+    T = int(counts.sum())
+    all_hi = int(counts[:, 0].sum())
+    bhi = int(counts[:rank, 0].sum())
+    blo = all_hi + int(counts[:rank, 1].sum())
+    fhi, flo = int(counts[rank, 0]), int(counts[rank, 1])
+    split = min(n, max(0, start - base))
+    if T <= K:
+        return n_total, 0
+    if bhi <= K < bhi + fhi:
+        x = split + int(np.flatnonzero(fail_ok[split:])[K - bhi])
+        return base + x - start, base + x - start + 1
+    if blo <= K < blo + flo:
+        x = int(np.flatnonzero(fail_ok[:split])[K - blo])
+        return base + x - start + n_total, base + x - start + n_total + 1
+    if blo + flo <= K:
+        return n_total, 0
+    if bhi + fhi <= K and split < n:
+        return base + n - start, 0
+    return 0, 0
+
+
+def schedule_perpod(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed: int, const: int,
+                    w_fit: int, w_ba: int, pct: int):
+    """The sharded per-pod cycle (csrc/ksim_kernels.hip §C) for bare pods:
+    all-gather of the two run counts -> global window; all-reduce (max) of
+    (TB key, cutslot); the owner binds.  Returns (placements, local evals,
+    nextStartNodeIndex)."""
+    import torch
+    K = num_feasible_nodes_to_find(n_total, pct)
+    chosen = np.full(pods.n_pods, -1, np.int64)
+    rows = np.arange(shard.n)
+    g = shard.base + rows
+    start, evals = 0, 0
+    for j in range(pods.n_pods):
+        pod = pods.pods[j]
+        keys = shard.keys(pod, rows, seed, j, const, w_fit, w_ba)
+        ok = keys != 0
+        split = min(shard.n, max(0, start - shard.base))
+        mine = torch.tensor([int(ok[split:].sum()), int(ok[:split].sum())], dtype=torch.int64)
+        gathered = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        counts = torch.stack(gathered).numpy()
+        kend, cutslot = window(counts, rank, n_total, K, shard.base, shard.n, start, ok)
+        nf = min(int(counts.sum()), K)
+        pos = (g - start) % n_total
+        kept = ok & (pos < kend)
+        if nf == 1:        # schedulePod: the single feasible node, unscored
+            keys = tb_keys(np.zeros(shard.n, np.int64), seed, j, g)
+        best = int(keys[kept].max()) if kept.any() else 0
+        t = torch.tensor([best, cutslot], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        best, cutslot = int(t[0]), int(t[1])
+        evaluated = cutslot if cutslot else n_total
+        evals += int((pos < evaluated).sum())
+        start = (start + (cutslot - 1 if cutslot else n_total)) % n_total
+        if best:
+            node = NODE_MASK - (best & NODE_MASK)
+            chosen[j] = node
+            if shard.base <= node < shard.base + shard.n:
+                shard.bind(node - shard.base, pod)
+    return chosen, evals, start

@@ -73,3 +73,45 @@ def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights):
 ])
 def test_sharded_protocol_gloo(world, n_nodes, n_pods, T, B, weights):
     mp.spawn(_worker, args=(world, _free_port(), n_nodes, n_pods, 7, T, B, weights), nprocs=world, join=True)
+
+
+def _worker_perpod(rank, world, port, n_nodes, n_pods, seed, pct):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "kube-scheduler-simulator_amd")]
+    import torch
+    import torch.distributed as dist
+    from ksim import gen, profile
+    from ksim.shard import partition
+    from oracle import shard_model
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=n_pods, seed=seed)
+        sp = profile.SchedulerProfile(percentage_of_nodes_to_score=pct)
+        w = {p.name: (p.weight or 1) for p in sp.score_plugins()}
+        const = 100 * w["TaintToleration"] + 100 * w["PodTopologySpread"]
+        base, cnt = partition(n_nodes, world)[rank]
+        shard = shard_model.Shard(cluster, base, cnt)
+        chosen, evals, start = shard_model.schedule_perpod(pods, shard, rank, world, dist, n_nodes, sp.tiebreak_seed,
+                                                           const, w["NodeResourcesFit"],
+                                                           w["NodeResourcesBalancedAllocation"], pct)
+        t = torch.tensor([evals], dtype=torch.int64)
+        dist.all_reduce(t)
+        if rank == 0:
+            from oracle.oracle import Oracle
+            ora = Oracle(cluster, profile.compile_profile(sp))
+            ochosen, ost = ora.schedule(pods)
+            np.testing.assert_array_equal(chosen, ochosen)
+            assert int(t[0]) == ost.evals and start == ora.next_start
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_nodes,n_pods,pct", [
+    (2, 250, 400, 0),      # ADAPT: K = 100 of 250, cuts inside and across shards
+    (3, 301, 300, 0),
+    (3, 12, 500, 100),     # P100, pods stop fitting
+])
+def test_sharded_perpod_gloo(world, n_nodes, n_pods, pct):
+    """The sharded per-pod cycle's window / argmax exchanges across processes."""
+    mp.spawn(_worker_perpod, args=(world, _free_port(), n_nodes, n_pods, 9, pct), nprocs=world, join=True)

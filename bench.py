@@ -112,8 +112,8 @@ def build(cfg: int, args, rank: int, world: int):
                 f"{int(cluster.num_pods.sum())} existing pods with anti-affinity terms, {pods.n_pods} incoming "
                 f"pods with spread constraints + preferred anti-affinity, {args.mode.upper()}")
         if world > 1:
-            desc += f", {world} independent replicas"
-        return cluster, pods, sp, desc, False, "weak"
+            desc += f", node-sharded over {world} GPUs"
+        return cluster, pods, sp, desc, world > 1, "strong"
     if cfg == 5:
         cluster, pods = gen.config2(5000, 10000)
         desc = f"config5: {args.sweep} score-weight vectors over 5000 nodes x 10000 pods, {args.mode.upper()}, " \
@@ -144,6 +144,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
 
+    # The JSON line goes to the original stdout; native libraries (RCCL's
+    # version banner) that write to fd 1 land on stderr instead.
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -164,7 +169,7 @@ def main():
     cfg = args.config
     cluster, pods, sp, desc, sharded, scaling = build(cfg, args, rank, world)
     prof = profile.compile_profile(sp)
-    if args.force_shard and cfg in (2, 4):
+    if args.force_shard and cfg in (2, 3, 4):
         sharded = True
         desc += " [sharded path forced]"
 
@@ -300,7 +305,7 @@ def main():
                                               f"config-{cfg}")
         result["vs_cpu"] = result["value"] / result["cpu_baseline"]["value"]
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -61,7 +61,9 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
     if name == "k_batch_chain":
         return 8 * B * T * 2
     if name == "k_batch_pairs":
-        return B * (B - 1) // 2 * B_EVAL + 8 * B * 3      # one bound-row re-eval per pod pair
+        return B * (B - 1) // 2 * B_EVAL                  # one bound-row re-eval per pod pair
+    if name == "k_batch_commit":
+        return 8 * B * 3                                  # guesses, pair maxima, placements
     return 0
 
 

@@ -3,7 +3,7 @@
 // For B = kBatchPods consecutive pods of the queue that are "batchable" (P100,
 // every normalized score constant over nodes, no scalar requests; see
 // pod_batchable in ksim_engine.cpp), placements equal running the cycle pod by
-// pod (bit-exact with the oracle), in four launches per batch:
+// pod (bit-exact with the oracle), in five launches per batch:
 //
 //   k_batch_eval   grid (node tiles, pods): every pod x node pair against the
 //                  batch-start snapshot S0 — static filters, Fit filter,
@@ -12,11 +12,12 @@
 //                  of DPP wave-max keep the tile's 4 best keys.
 //   k_batch_merge  one wave per pod: merge the sorted tile lists into the
 //                  pod's top-T under S0 (a prefix that is provably exact).
-//   k_batch_chain  one wave: the greedy chain — pod i guesses the first entry
-//                  of its list not guessed by an earlier pod of the batch.
+//   k_batch_chain  one block: the greedy chain — pod i guesses the first entry
+//                  of its list not guessed by an earlier pod of the batch —
+//                  by parallel relaxation (see the kernel), keeping its exact prefix.
 //   k_batch_pairs  block j, thread k < j: key of pod j on pod k's guess after
-//                  pod k is bound there; the block max M_j.  The last block to
-//                  finish validates and commits.
+//                  pod k is bound there; the block max M_j.
+//   k_batch_commit one block: validates the chain and commits.
 //
 // Exactness: pods 0..i-1 took their guesses (distinct nodes), so before pod i
 // only those nodes differ from S0.  Pod i's guess is the best node still at
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {
 }
 
 const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_eval", "k_batch_merge", "k_batch_chain",
-                                                         "k_batch_pairs"};
+                                                         "k_batch_pairs", "k_batch_commit"};
 
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
@@ -408,8 +409,9 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   // the pairs kernel fencing for a last-block election
   k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
                                                              a.s.pmax, a.s.done, a.chosen);
-  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
   if (evs) (void)hipEventRecord(evs[4], stream);
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+  if (evs) (void)hipEventRecord(evs[5], stream);
 }
 
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {

@@ -36,7 +36,7 @@ struct LaunchArgs {
 
 constexpr int kKernelsPerCycle = 7;
 extern const char* const kKernelNames[kKernelsPerCycle];
-constexpr int kKernelsPerBatch = 4;
+constexpr int kKernelsPerBatch = 5;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).

@@ -62,13 +62,17 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
         return 8 * B * T * 2
     if name == "k_batch_pairs":
         return B * (B - 1) // 2 * B_EVAL                  # one bound-row re-eval per pod pair
+    if name == "k_adapt_mask":
+        return B_EVAL * n_nodes * B                   # filter columns of every node row, per pod
+    if name == "k_adapt_top":
+        return B_EVAL * geom.get("adapt_k", n_nodes) * B  # the K kept rows scored per pod
     if name == "k_batch_commit":
         return 8 * B * 3                                  # guesses, pair maxima, placements
     return 0
 
 
 # the kernel that carries the pod x node evaluations on each path
-EVAL_KERNELS = ("k_batch_eval", "k_filter_score")
+EVAL_KERNELS = ("k_batch_eval", "k_adapt_mask", "k_filter_score")
 
 
 def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) -> dict:
@@ -245,6 +249,8 @@ def main():
     # Roofline of the evaluation kernel: per-kernel HIP events on an engine
     # stream, over this rank's nodes (a sharded rank times its own shard).
     geom = engine.batch_geometry()
+    from ksim.profile import num_feasible_nodes_to_find
+    geom["adapt_k"] = num_feasible_nodes_to_find(cluster.n_nodes, sp.percentage_of_nodes_to_score)
     if sharded:
         base, cnt = shard.partition(cluster.n_nodes, world)[rank]
         keng = engine.Engine(local)

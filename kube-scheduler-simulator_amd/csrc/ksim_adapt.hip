@@ -1,0 +1,299 @@
+// ksim_adapt.hip — the speculative batch path under ADAPT (gfx950).
+//
+// ADAPT is the simulator's forced default (percentageOfNodesToScore = 0): a pod
+// scans nodes in nodeTree order from nextStartNodeIndex and keeps the first K =
+// numFeasibleNodesToFind(N) feasible ones; the scan start of pod i+1 is pod i's
+// start plus the nodes pod i processed.  For a batch of B
+// batchable pods (same class of pods as ksim_batch.hip) six launches give the
+// placements of the pod-by-pod cycle, bit-exact:
+//
+//   k_adapt_mask    grid (64-node words, pods): the S0 feasibility bitmap of
+//                   every pod (static filters + Fit filter; one ballot per word).
+//   k_adapt_window  one block, one thread per pod: the scan windows.  Pod i's
+//                   start depends on every earlier pod's processed count, so the
+//                   starts are found by relaxation: guess s_i = s_0 + i*K, let
+//                   every pod find its cut (the K-th feasible node from s_i) in
+//                   its bitmap, re-derive the starts as the prefix sum of the
+//                   processed counts, repeat.  Pod 0's start is exact and each
+//                   round extends the exact prefix; a fixpoint is exact.
+//   k_adapt_top     one wave per pod: TB keys of the kept nodes (the first K
+//                   feasible of its window), the pod's exact top-T.
+//   k_batch_chain   the greedy chain of ksim_batch.hip on those lists.
+//   k_adapt_pairs   block j, thread k < j: pod j on pod k's guessed node once pod
+//                   k is bound there, if the node lies in pod j's window: the key
+//                   (M_j = max) and whether a node feasible under S0 became
+//                   infeasible at or before the cut ("broken": pod j's window, and
+//                   every later start, would shift).
+//   k_adapt_commit  one block: the chain is cut at the first broken pod, then
+//                   validated against M and committed as on the P100 path; the
+//                   scheduler state advances to the start after the last committed pod.
+//
+// Exactness: binds only remove capacity, so feasibility under the current state
+// is S0 feasibility minus flips on bound nodes (static filters never change).
+// Bound nodes are the guesses of earlier pods of the batch.  Up to the first
+// broken pod no window differs from the serial one; the chain argument of
+// ksim_batch.hip then applies within each window.
+#include "ksim_device.h"
+#include "ksim_internal.h"
+#include "ksim_wave.h"
+#include "ksim_commit.h"
+
+namespace ksim {
+
+// Filter outcome of a batchable pod on a node: static filters and Fit only.
+__device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPods& P, const BatchProg& bp,
+                                               const ksim_pod& p, const NodeRow& r, bool trivial) {
+  if (!trivial && !static_filters_pass(c, P, bp, p, r)) return false;
+  return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar);
+}
+
+__global__ __launch_bounds__(256) void k_adapt_mask(DevCluster c, DevPods P, BatchProg bp,
+                                                    const DevState* __restrict__ st, uint64_t* __restrict__ amask,
+                                                    int32_t n_words) {
+  const int32_t base = st->cursor;
+  const int32_t j = blockIdx.y;
+  const int32_t pi = base + j;
+  if (pi >= min(st->end, base + kBatchPods)) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_words) return;                          // wave-uniform
+  const int32_t node = w * 64 + lane;
+  bool f = false;
+  if (node < c.n) {
+    const NodeRow r = load_row(c, node);
+    f = batch_feasible(c, P, bp, P.pods[pi], r, (P.bflags[pi] & kBatchStaticTrivial) != 0);
+  }
+  const uint64_t m = __ballot(f);
+  if (lane == 0) amask[(size_t)j * n_words + w] = m;
+}
+
+// Rotated offset of the K-th (0-based) set bit of `mask` counting from node s,
+// or -1 when the bitmap holds at most K set bits.
+__device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_t n, int32_t k) {
+  int32_t need = k, off = 0, pos = s;
+  while (off < n) {
+    const int32_t w = pos >> 6, b = pos & 63;
+    int32_t len = min((w + 1) * 64, n) - pos;
+    if (len > n - off) len = n - off;                // back at s's word after the wrap
+    uint64_t bits = mask[w] >> b;
+    if (len < 64) bits &= (1ull << len) - 1;
+    const int cnt = __popcll(bits);
+    if (need < cnt) {
+      for (int t = 0; t < need; t++) bits &= bits - 1;
+      return off + __builtin_ctzll(bits);
+    }
+    need -= cnt;
+    off += len;
+    pos += len;
+    if (pos >= n) pos = 0;
+  }
+  return -1;
+}
+
+constexpr int kWindowRounds = 48;   // exact prefix kept if not converged by then
+
+// awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
+// feasible node kept and all N processed); *aexact = pods with exact windows.
+__global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
+                                                             const uint64_t* __restrict__ amask, int32_t n_words,
+                                                             int32_t n, int32_t k, int32_t* __restrict__ awin,
+                                                             int32_t* __restrict__ aexact) {
+  __shared__ int64_t sh[kBatchPods / 64];
+  __shared__ int32_t s_first;
+  const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  if (nb <= 0) return;
+  const int32_t s0 = st->next_start;
+  int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
+  int32_t cut = -1, exact = 0;
+  for (int round = 0; round < kWindowRounds; round++) {
+    cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
+    const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
+    // exclusive prefix sum of the processed counts
+    int64_t x = proc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    if (j == 0) s_first = kBatchPods;
+    __syncthreads();
+    int64_t before = 0;
+    for (int w = 0; w < wv; w++) before += sh[w];
+    const int32_t ns = (int32_t)(((int64_t)s0 + before + x - proc) % n);
+    if (j < nb && ns != s) atomicMin(&s_first, j);
+    __syncthreads();
+    const int32_t f = s_first;
+    __syncthreads();                                 // sh / s_first are rewritten next round
+    if (f == kBatchPods) {                           // fixpoint: every window exact
+      exact = nb;
+      break;
+    }
+    exact = f;                                       // pods < f: start and cut exact
+    if (j >= f) s = ns;                              // pods <= f now hold exact starts
+  }
+  if (j < nb) {
+    awin[2 * j] = s;
+    awin[2 * j + 1] = cut;
+  }
+  if (j == 0) *aexact = exact;
+}
+
+// One wave per pod: the kept nodes' TB keys -> the pod's top-T (complete when
+// it lists every kept node).  Pods past the exact windows get an empty
+// incomplete list, which ends the chain there.
+__global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+                                                   const DevState* __restrict__ st,
+                                                   const uint64_t* __restrict__ amask, int32_t n_words,
+                                                   const int32_t* __restrict__ awin,
+                                                   const int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
+                                                   int32_t* __restrict__ topk_cnt,
+                                                   int32_t* __restrict__ topk_complete) {
+  const int lane = threadIdx.x & 63;
+  const int32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int32_t base = st->cursor;
+  if (j >= min(kBatchPods, st->end - base)) return;   // wave-uniform
+  if (j >= *aexact) {
+    if (lane == 0) {
+      topk_cnt[j] = 0;
+      topk_complete[j] = 0;
+    }
+    return;
+  }
+  const int32_t n = c.n, s = awin[2 * j], cut = awin[2 * j + 1];
+  const int32_t kend = cut >= 0 ? cut : n;
+  const int32_t pi = base + j;
+  const ksim_pod& p = P.pods[pi];
+  const int32_t nc = P.norm_const[pi];
+  const int64_t seq = st->pod_seq + j;
+  const uint64_t* mask = amask + (size_t)j * n_words;
+  uint64_t a[kTopT];
+#pragma unroll
+  for (int t = 0; t < kTopT; t++) a[t] = 0;
+  int32_t kept = 0;
+#pragma unroll 1
+  for (int32_t off = lane; off < kend; off += 64) {
+    int32_t node = s + off;
+    if (node >= n) node -= n;
+    if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
+    kept++;
+    const NodeRow r = load_row(c, node);
+    a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base));
+#pragma unroll
+    for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+  }
+  // a lane can be popped at most T times and holds its T best: no early stop
+  uint64_t mine = 0;
+  int32_t cnt = 0;
+  for (int t = 0; t < kTopT; t++) {
+    const uint64_t m = wave_max_u64_dpp(a[0]);
+    if (m == 0) break;
+    if (lane == t) mine = m;
+    cnt = t + 1;
+    if (a[0] == m) {
+#pragma unroll
+      for (int q = 0; q < kTopT - 1; q++) a[q] = a[q + 1];
+      a[kTopT - 1] = 0;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
+  if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
+  if (lane == 0) {
+    topk_cnt[j] = cnt;
+    topk_complete[j] = kept <= kTopT ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+                                                            const DevState* __restrict__ st,
+                                                            const uint64_t* __restrict__ amask, int32_t n_words,
+                                                            const int32_t* __restrict__ awin,
+                                                            const uint64_t* __restrict__ gkey,
+                                                            const int32_t* __restrict__ chain_end,
+                                                            uint64_t* __restrict__ pmax,
+                                                            int32_t* __restrict__ abroken) {
+  __shared__ uint64_t s_wmax[kBatchPods / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  if (nb <= 0) return;
+  const int32_t nchain = *chain_end;
+  const int j = blockIdx.x, k = tid;
+  uint64_t v = 0;
+  bool brk = false;
+  if (j < nchain && k < j) {
+    const uint64_t gk = gkey[k];
+    const int32_t node = gk ? key_node(gk) - c.base : -1;
+    if (node >= 0 && node < c.n) {
+      const int32_t n = c.n, s = awin[2 * j], cut = awin[2 * j + 1];
+      int32_t off = node - s;
+      if (off < 0) off += n;
+      const int32_t kend = cut >= 0 ? cut : n;
+      if (off < kend || off == cut) {
+        NodeRow r = load_row(c, node);
+        row_add_pod(r, P.pods[base + k], 1);
+        const ksim_pod& p = P.pods[base + j];
+        const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
+        const bool was = (amask[(size_t)j * n_words + (node >> 6)] >> (node & 63)) & 1ull;
+        if (cut >= 0 && was && !now) brk = true;
+        if (off < kend && now) v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, st->pod_seq + j, c.base);
+      }
+    }
+  }
+  const bool any_brk = __syncthreads_or(brk);
+  v = wave_max_u64_dpp(v);
+  if (lane == 0) s_wmax[wave] = v;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t m = 0;
+    for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
+    pmax[j] = j < nchain ? m : 0;
+    abroken[j] = j < nchain && any_brk ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
+                                                             const uint64_t* __restrict__ gkey,
+                                                             const int32_t* __restrict__ chain_end,
+                                                             const uint64_t* __restrict__ pmax,
+                                                             const int32_t* __restrict__ abroken,
+                                                             const int32_t* __restrict__ awin,
+                                                             int32_t* __restrict__ chosen_out) {
+  __shared__ int32_t s_fb, s_istar, s_sched, s_unsched;
+  if (min(kBatchPods, st->end - st->cursor) <= 0) return;
+  const int32_t nchain0 = *chain_end;
+  if (threadIdx.x == 0) s_fb = nchain0;
+  __syncthreads();
+  if ((int32_t)threadIdx.x < nchain0 && abroken[threadIdx.x]) atomicMin(&s_fb, (int32_t)threadIdx.x);
+  __syncthreads();
+  batch_commit(c, P, st, gkey, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, awin);
+}
+
+const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",
+                                                         "k_batch_chain", "k_adapt_pairs", "k_adapt_commit"};
+
+void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
+  const int32_t n_words = (a.c.n + 63) / 64;
+  const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
+  if (evs) (void)hipEventRecord(evs[0], stream);
+  k_adapt_mask<<<dim3((n_words + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.bp, a.st, a.s.amask, n_words);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  if (evs) (void)hipEventRecord(evs[2], stream);
+  k_adapt_top<<<kBatchPods / 4, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
+                                                  a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete);
+  if (evs) (void)hipEventRecord(evs[3], stream);
+  launch_chain(a, stream);
+  if (evs) (void)hipEventRecord(evs[4], stream);
+  k_adapt_pairs<<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
+                                                       a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
+  if (evs) (void)hipEventRecord(evs[5], stream);
+  k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,
+                                               a.s.awin, a.chosen);
+  if (evs) (void)hipEventRecord(evs[6], stream);
+}
+
+}  // namespace ksim

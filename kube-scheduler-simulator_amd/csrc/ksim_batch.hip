@@ -29,6 +29,7 @@
 #include "ksim_device.h"
 #include "ksim_internal.h"
 #include "ksim_wave.h"
+#include "ksim_commit.h"
 
 namespace ksim {
 
@@ -267,54 +268,6 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   }
 }
 
-// Validate the chain against M (pmax) and commit (one block of kBatchPods
-// threads).  Binds are applied by the shard that owns the node.
-__device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
-                                             const uint64_t* __restrict__ gkey, const uint64_t* __restrict__ pmax,
-                                             int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
-                                             int32_t* s_sched, int32_t* s_unsched) {
-  const int tid = threadIdx.x;
-  const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
-  const int64_t seq0 = st->pod_seq;
-  if (tid == 0) {
-    *s_istar = nchain;
-    *s_sched = 0;
-    *s_unsched = 0;
-  }
-  __syncthreads();
-  const uint64_t gj = tid < nchain ? __builtin_nontemporal_load(&gkey[tid]) : 0;
-  const uint64_t mj = tid < nchain ? __builtin_nontemporal_load(&pmax[tid]) : 0;
-  if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
-  __syncthreads();
-  const int32_t istar = *s_istar;
-  const int32_t committed = istar < nchain ? istar + 1 : nchain;
-  const int32_t inode = istar < nchain ? key_node(__builtin_nontemporal_load(&pmax[istar])) : -1;
-  if (tid < committed) {
-    const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);     // global position
-    if (chosen_out) chosen_out[base + tid] = node;
-    atomicAdd(node >= 0 ? s_sched : s_unsched, 1);
-    const int32_t local = node - c.base;
-    if (tid < istar && gj && local >= 0 && local < c.n) {   // bound nodes are distinct: one writer each
-      assume_pod(c, P, P.pods[base + tid], local, 1);
-      if (node == inode) assume_pod(c, P, P.pods[base + istar], local, 1);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    st->cursor = base + committed;
-    st->pod_seq = seq0 + committed;
-    st->evals += (int64_t)committed * c.n;
-    st->scheduled += *s_sched;
-    st->unschedulable += *s_unsched;
-    st->batches += 1;
-    if (committed < nb) {
-      if (istar < nchain) st->cuts += 1;
-      else st->truncations += 1;
-    }
-  }
-}
-
 // Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
 // bound there; M_j = the block max.  Unsharded, the last block to finish
 // validates the chain against M and commits the batch; sharded (SHARDED),
@@ -412,6 +365,11 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[4], stream);
   k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
   if (evs) (void)hipEventRecord(evs[5], stream);
+}
+
+void launch_chain(const LaunchArgs& a, hipStream_t stream) {
+  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+                                              a.s.gkey, a.s.chain_end, a.s.dbg);
 }
 
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {

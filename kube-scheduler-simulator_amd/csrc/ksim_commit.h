@@ -1,0 +1,73 @@
+// ksim_commit.h — the batch commit shared by the P100 (ksim_batch.hip) and
+// ADAPT (ksim_adapt.hip) batch paths.
+#pragma once
+
+#include "ksim_device.h"
+#include "ksim_internal.h"
+
+namespace ksim {
+
+// Validate the chain against M (pmax) and commit (one block of kBatchPods
+// threads).  Binds are applied by the shard that owns the node.  awin (ADAPT
+// batch, unsharded): per pod {scan start, cut offset or -1}; the evaluated
+// counts and nextStartNodeIndex follow the committed pods' windows.
+__device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
+                                             const uint64_t* __restrict__ gkey, const uint64_t* __restrict__ pmax,
+                                             int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
+                                             int32_t* s_sched, int32_t* s_unsched,
+                                             const int32_t* __restrict__ awin = nullptr) {
+  __shared__ int32_t s_evals;
+  const int tid = threadIdx.x;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  const int64_t seq0 = st->pod_seq;
+  if (tid == 0) {
+    *s_istar = nchain;
+    *s_sched = 0;
+    *s_unsched = 0;
+    s_evals = 0;
+  }
+  __syncthreads();
+  const uint64_t gj = tid < nchain ? __builtin_nontemporal_load(&gkey[tid]) : 0;
+  const uint64_t mj = tid < nchain ? __builtin_nontemporal_load(&pmax[tid]) : 0;
+  if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
+  __syncthreads();
+  const int32_t istar = *s_istar;
+  const int32_t committed = istar < nchain ? istar + 1 : nchain;
+  const int32_t inode = istar < nchain ? key_node(__builtin_nontemporal_load(&pmax[istar])) : -1;
+  if (tid < committed) {
+    const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);     // global position
+    if (chosen_out) chosen_out[base + tid] = node;
+    atomicAdd(node >= 0 ? s_sched : s_unsched, 1);
+    const int32_t local = node - c.base;
+    if (tid < istar && gj && local >= 0 && local < c.n) {   // bound nodes are distinct: one writer each
+      assume_pod(c, P, P.pods[base + tid], local, 1);
+      if (node == inode) assume_pod(c, P, P.pods[base + istar], local, 1);
+    }
+  }
+  if (awin && tid < committed) {
+    const int32_t cut = awin[2 * tid + 1];
+    atomicAdd(&s_evals, cut >= 0 ? cut + 1 : c.n);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (awin) {
+      const int32_t cut = awin[2 * (committed - 1) + 1];
+      st->next_start = (int32_t)(((int64_t)awin[2 * (committed - 1)] + (cut >= 0 ? cut : c.n)) % c.n);
+      st->evals += s_evals;
+    } else {
+      st->evals += (int64_t)committed * c.n;
+    }
+    st->cursor = base + committed;
+    st->pod_seq = seq0 + committed;
+    st->scheduled += *s_sched;
+    st->unschedulable += *s_unsched;
+    st->batches += 1;
+    if (committed < nb) {
+      if (istar < nchain) st->cuts += 1;
+      else st->truncations += 1;
+    }
+  }
+}
+
+}  // namespace ksim

@@ -116,6 +116,10 @@ struct DevScratch {
   uint8_t* fail;         // [n] filter-order index of first failure or KSIM_PASSED
   uint8_t* ign;          // [n] feasible node missing a ScheduleAnyway spread key (IgnoredNodes)
   WinState* win;
+  uint64_t* amask;       // ADAPT batch: S0 feasibility bitmaps [kBatchPods][ceil(n / 64)]
+  int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
+  int32_t* aexact;       // ADAPT batch: pods whose windows are exact
+  int32_t* abroken;      // ADAPT batch: a bound node flipped feasibility inside the pod's window
   int64_t* xdom;         // sharded cycle: packed domain sums (all-reduced, sum)
   int64_t* xreg;         // sharded cycle: IgnoredNodes count + per-value registrations (all-reduced, sum)
   uint32_t* detail;      // [n]

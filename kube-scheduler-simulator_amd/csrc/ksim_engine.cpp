@@ -243,9 +243,15 @@ bool static_trivial(const ksim_handle* h, const ksim_pod& p) {
   return true;
 }
 
+bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
+
+// ADAPT: the profile keeps fewer than all nodes (K < N over the whole cluster).
+bool adapt_mode(const ksim_handle* h) {
+  return num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->dc.n_total) < h->dc.n_total;
+}
+
 bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
   const ksim_profile& prof = h->prof;
-  if (num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, h->dc.n) != h->dc.n) return false;
   if (p.use_count > 0) return false;
   if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
   int64_t acc = 0;
@@ -314,7 +320,12 @@ int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   if (batch)
-    for (int i = 0; i < kGraphBatches; i++) launch_batch(a, h->stream);
+    for (int i = 0; i < kGraphBatches; i++) {
+      if (adapt_mode(h))
+        launch_batch_adapt(a, h->stream);
+      else
+        launch_batch(a, h->stream);
+    }
   else
     for (int i = 0; i < kGraphCycles; i++) launch_cycle(a, h->stream, false, topo);
   hipError_t e = hipStreamEndCapture(h->stream, &g);
@@ -354,7 +365,12 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
       for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(h->graph_batch, h->stream));
     } else {
       const int n1 = (left + kBatchPods - 1) / kBatchPods;
-      for (int r = 0; r < n1; r++) launch_batch(la, h->stream);
+      for (int r = 0; r < n1; r++) {
+        if (adapt_mode(h))
+          launch_batch_adapt(la, h->stream);
+        else
+          launch_batch(la, h->stream);
+      }
       HIPCHK(h, hipGetLastError());
     }
     DevState st;
@@ -372,10 +388,12 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
   int32_t i = first;
   const int32_t end = first + count;
   while (i < end) {
-    const bool b = h->batchable[i] != 0;
+    // the ADAPT batch path is unsharded: sharded ADAPT runs cycle by cycle
+    const bool batch_ok = !(adapt_mode(h) && is_sharded(h));
+    const bool b = batch_ok && h->batchable[i] != 0;
     const bool t = h->topo[i] != 0;
     int32_t j = i + 1;
-    while (j < end && (h->batchable[j] != 0) == b && (h->topo[j] != 0) == t) j++;
+    while (j < end && (batch_ok && h->batchable[j] != 0) == b && (h->topo[j] != 0) == t) j++;
     int rc = fn(i, j, b, t);
     if (rc) return rc;
     i = j;
@@ -527,7 +545,7 @@ int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t c
   });
 }
 
-bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
+
 
 int reset_counters(ksim_handle* h, hipStream_t stream) {
   HIPCHK(h, hipMemsetAsync(&h->st->truncations, 0, 4, stream));
@@ -793,6 +811,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.xrecv, uint64_t*, 8 * (size_t)kMaxShards * kBatchPods * kXRec);
   SCR(s.min_match, int64_t*, 8 * (size_t)KSIM_MAX_USES);
   SCR(s.xdom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
+  SCR(s.amask, uint64_t*, 8 * (size_t)kBatchPods * ((N + 63) / 64));
+  SCR(s.awin, int32_t*, 4 * 2 * (size_t)kBatchPods);
+  SCR(s.aexact, int32_t*, 4);
+  SCR(s.abroken, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.xreg, int64_t*, 8 * (1 + (size_t)KSIM_MAX_USES * vmax));
   SCR(o.scored, uint8_t*, N);
   SCR(o.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
@@ -1195,13 +1217,15 @@ const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerCycle) return kKernelNames[k];
   k -= kKernelsPerCycle;
   if (k >= 0 && k < kKernelsPerBatch) return kBatchKernelNames[k];
+  k -= kKernelsPerBatch;
+  if (k >= 0 && k < kKernelsPerAdapt) return kAdaptKernelNames[k];
   return nullptr;
 }
 
 int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms, int64_t* launches, int32_t cap) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch;
+  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt;
   if (!avg_ms || cap < kKinds) return set_err(h, KSIM_E_INVALID, "avg_ms too small");
   if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
@@ -1212,8 +1236,9 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
   rc = for_each_run(h, first, count, [&](int32_t lo, int32_t hi, bool batch, bool topo) -> int {
     int r;
     if ((r = set_run(h, lo, hi))) return r;
-    const int per = batch ? kKernelsPerBatch : kKernelsPerCycle;
-    const int base = batch ? kKernelsPerCycle : 0;
+    const bool adapt = batch && adapt_mode(h);
+    const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
+    const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
     int32_t cursor = lo;
     while (cursor < hi) {
       const int32_t iters = batch ? std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods) : std::min(512, hi - cursor);
@@ -1221,7 +1246,9 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
       for (auto& e : evs) HIPCHK(h, hipEventCreate(&e));
       if (batch) HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
       for (int32_t i = 0; i < iters; i++) {
-        if (batch)
+        if (adapt)
+          launch_batch_adapt(a, h->stream, &evs[(size_t)i * (per + 1)]);
+        else if (batch)
           launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else
           launch_cycle(a, h->stream, false, topo, &evs[(size_t)i * (per + 1)]);

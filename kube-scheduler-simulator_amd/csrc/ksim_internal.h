@@ -38,6 +38,8 @@ constexpr int kKernelsPerCycle = 7;
 extern const char* const kKernelNames[kKernelsPerCycle];
 constexpr int kKernelsPerBatch = 5;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
+constexpr int kKernelsPerAdapt = 6;
+extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).
 // evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.
@@ -46,6 +48,9 @@ extern const char* const kBatchKernelNames[kKernelsPerBatch];
 void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+// The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
+void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // Sharded batch (node shards; the caller exchanges between the phases):
 //   launch_shard_eval    eval + merge; writes this shard's records to s.xsend
 //   (all-gather s.xsend -> s.xrecv [world][kBatchPods][kXRec])

@@ -229,10 +229,10 @@ class Engine:
         """Schedule loaded pods [first, first+count) with HIP events between the
         kernels on the engine's own stream.  Returns {kernel: (mean ms, launches)}
         for every kernel that ran."""
-        out = np.zeros(16, np.float64)
-        cnt = np.zeros(16, np.int64)
+        out = np.zeros(32, np.float64)
+        cnt = np.zeros(32, np.int64)
         n = lib().ksim_time_kernels(self.h, first, count, out.ctypes.data_as(ctypes.c_void_p),
-                                    cnt.ctypes.data_as(ctypes.c_void_p), 16)
+                                    cnt.ctypes.data_as(ctypes.c_void_p), 32)
         if n < 0:
             self._chk(n)
         return {lib().ksim_kernel_name(k).decode(): (float(out[k]), int(cnt[k]))

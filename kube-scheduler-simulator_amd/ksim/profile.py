@@ -224,3 +224,12 @@ def compile_profile(prof: SchedulerProfile, scalar_names: List[str] = ()) -> abi
     p.hard_pod_affinity_weight = prof.hard_pod_affinity_weight
     p.tiebreak_seed = prof.tiebreak_seed & (2 ** 64 - 1)
     return p
+
+
+def num_feasible_nodes_to_find(n: int, pct: int) -> int:
+    """numFeasibleNodesToFind (upstream schedule_one.go): the
+    feasible nodes a cycle keeps.  pct 0 is the adaptive default."""
+    if n < 100 or pct >= 100:
+        return n
+    p = pct if pct > 0 else max(5, 50 - n // 125)
+    return max(n * p // 100, 100)

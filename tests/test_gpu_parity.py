@@ -87,10 +87,41 @@ def _batch_vs_oracle(cluster, pods, pct=100, seed=0x4B53494D):
     ochosen, ost = ora.schedule(pods)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert eng.next_start == ora.next_start
     es, os_ = eng.node_state(), ora.node_state()
     for k in es:
         np.testing.assert_array_equal(es[k], os_[k])
     return st
+
+
+# ---- ADAPT batch path (ksim_adapt.hip): windows by relaxation, broken windows ----
+
+@pytest.mark.parametrize("n_nodes", [101, 150, 257, 1000])
+def test_adapt_batch_until_full(n_nodes):
+    """K < N; nodes fill up (feasibility flips inside windows, unschedulable pods)."""
+    cluster, _ = gen.config2(n_nodes=n_nodes, n_pods=1)
+    pods = gen.bare_pods(n_nodes * 60 + 37, seed=31)
+    st = _batch_vs_oracle(cluster, pods, pct=0)
+    assert st.perpod_cycles == 0 and st.batches > 0
+
+
+def test_adapt_batch_config2_and_pct():
+    cluster, pods = gen.config2(n_nodes=5000, n_pods=6000)
+    _batch_vs_oracle(cluster, pods, pct=0)
+    cluster, pods = gen.config2(n_nodes=3000, n_pods=4000, seed=77)
+    _batch_vs_oracle(cluster, pods, pct=30)
+
+
+def test_adapt_batch_mixed_runs():
+    """Config-1 objects on 400 nodes (K = 100 < N): batch and per-pod runs
+    interleave and hand nextStartNodeIndex to each other."""
+    from ksim.encode import encode_cluster, encode_pods
+    nodes, pods = gen.config1_objects(n_nodes=400, n_pods=2000)
+    for n in nodes:
+        n.taints = [t for t in n.taints if t.effect != "PreferNoSchedule"]
+    cluster, _ = encode_cluster(nodes)
+    st = _batch_vs_oracle(cluster, encode_pods(cluster, pods), pct=0)
+    assert st.perpod_cycles > 0 and st.batches > 0
 
 
 @pytest.mark.parametrize("n_nodes", [1, 7, 64, 65, 300])

@@ -35,6 +35,7 @@ for _p in (ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd")):
         sys.path.insert(0, _p)
 
 B_EVAL = 112            # algorithmic HBM bytes per pod x node evaluation
+B_FILTER = 60           # the filter columns of a row: allocatable 28 + requested 24 + pods 4 + flags 4
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 
 
@@ -63,7 +64,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
     if name == "k_batch_pairs":
         return B * (B - 1) // 2 * B_EVAL                  # one bound-row re-eval per pod pair
     if name == "k_adapt_mask":
-        return B_EVAL * n_nodes * B                   # filter columns of every node row, per pod
+        return B_FILTER * n_nodes * B                 # filter columns of every node row, per pod
     if name == "k_adapt_top":
         return B_EVAL * geom.get("adapt_k", n_nodes) * B  # the K kept rows scored per pod
     if name == "k_batch_commit":
@@ -72,7 +73,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 
 
 # the kernel that carries the pod x node evaluations on each path
-EVAL_KERNELS = ("k_batch_eval", "k_adapt_mask", "k_filter_score")
+EVAL_KERNELS = ("k_batch_eval", "k_adapt_top", "k_filter_score")
 
 
 def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) -> dict:

@@ -16,7 +16,7 @@
 //                   its bitmap, re-derive the starts as the prefix sum of the
 //                   processed counts, repeat.  Pod 0's start is exact and each
 //                   round extends the exact prefix; a fixpoint is exact.
-//   k_adapt_top     one wave per pod: TB keys of the kept nodes (the first K
+//   k_adapt_top     one block per pod: TB keys of the kept nodes (the first K
 //                   feasible of its window), the pod's exact top-T.
 //   k_batch_chain   the greedy chain of ksim_batch.hip on those lists.
 //   k_adapt_pairs   block j, thread k < j: pod j on pod k's guessed node once pod
@@ -141,9 +141,10 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
   if (j == 0) *aexact = exact;
 }
 
-// One wave per pod: the kept nodes' TB keys -> the pod's top-T (complete when
-// it lists every kept node).  Pods past the exact windows get an empty
-// incomplete list, which ends the chain there.
+// One block (4 waves) per pod: the kept nodes' TB keys -> the pod's top-T
+// (complete when it lists every kept node).  Each wave keeps its lanes' best T
+// keys and extracts its own top-T; wave 0 merges the four lists.  Pods past
+// the exact windows get an empty incomplete list, which ends the chain there.
 __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
                                                    const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words,
@@ -151,12 +152,14 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
                                                    const int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
                                                    int32_t* __restrict__ topk_cnt,
                                                    int32_t* __restrict__ topk_complete) {
-  const int lane = threadIdx.x & 63;
-  const int32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ uint64_t s_top[4][kTopT];
+  __shared__ int32_t s_kept[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t j = blockIdx.x;
   const int32_t base = st->cursor;
-  if (j >= min(kBatchPods, st->end - base)) return;   // wave-uniform
+  if (j >= min(kBatchPods, st->end - base)) return;   // block-uniform
   if (j >= *aexact) {
-    if (lane == 0) {
+    if (tid == 0) {
       topk_cnt[j] = 0;
       topk_complete[j] = 0;
     }
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
   for (int t = 0; t < kTopT; t++) a[t] = 0;
   int32_t kept = 0;
 #pragma unroll 1
-  for (int32_t off = lane; off < kend; off += 64) {
+  for (int32_t off = tid; off < kend; off += 256) {
     int32_t node = s + off;
     if (node >= n) node -= n;
     if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
@@ -184,15 +187,12 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
 #pragma unroll
     for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
   }
-  // a lane can be popped at most T times and holds its T best: no early stop
-  uint64_t mine = 0;
-  int32_t cnt = 0;
+  // per wave: a lane can be popped at most T times and holds its T best, so
+  // the wave's top-T is exact
   for (int t = 0; t < kTopT; t++) {
     const uint64_t m = wave_max_u64_dpp(a[0]);
-    if (m == 0) break;
-    if (lane == t) mine = m;
-    cnt = t + 1;
-    if (a[0] == m) {
+    if (lane == 0) s_top[wv][t] = m;
+    if (m != 0 && a[0] == m) {
 #pragma unroll
       for (int q = 0; q < kTopT - 1; q++) a[q] = a[q + 1];
       a[kTopT - 1] = 0;
@@ -200,10 +200,25 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
+  if (lane == 0) s_kept[wv] = kept;
+  __syncthreads();
+  if (wv != 0) return;
+  // merge: lane l < 4T holds entry l % T of wave l / T (keys are unique per node)
+  uint64_t key = lane < 4 * kTopT ? s_top[lane / kTopT][lane % kTopT] : 0;
+  uint64_t mine = 0;
+  int32_t cnt = 0;
+  for (int t = 0; t < kTopT; t++) {
+    const uint64_t m = wave_max_u64_dpp(key);
+    if (m == 0) break;
+    if (lane == t) mine = m;
+    cnt = t + 1;
+    if (key == m) key = 0;
+  }
+  const int32_t total = s_kept[0] + s_kept[1] + s_kept[2] + s_kept[3];
   if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
   if (lane == 0) {
     topk_cnt[j] = cnt;
-    topk_complete[j] = kept <= kTopT ? 1 : 0;
+    topk_complete[j] = total <= kTopT ? 1 : 0;
   }
 }
 
@@ -283,7 +298,7 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_adapt_top<<<kBatchPods / 4, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
+  k_adapt_top<<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
                                                   a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete);
   if (evs) (void)hipEventRecord(evs[3], stream);
   launch_chain(a, stream);

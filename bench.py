@@ -10,13 +10,16 @@ Inputs (cluster SoA + pod queue) are resident in HBM before the timed region.
   python bench.py [--gpus N --steps K --warmup W] [--config 2|3|4|5] [--mode p100|adapt]
 
 Workloads:
-  config 2 (default)  N = 1: 5,000 nodes x 50,000 pods, default profile, P100.
+  config 2 (default)  N = 1: 5,000 nodes x 50,000 pods, default profile, P100;
+                      the same workload under ADAPT (the simulator's forced
+                      default, percentageOfNodesToScore 0) is timed beside it
+                      ("adapt" in the JSON line).
                       N > 1: node-sharded weak scaling, --nodes-per-gpu (5,000)
                       x N nodes, the same 50,000 pods; one process per GPU, per
                       batch an RCCL all-gather of candidates + all-reduce (max).
   config 3            PodTopologySpread + InterPodAffinity heavy (10k nodes, 3
                       zones, 100k existing pods with anti-affinity terms), per-pod
-                      path; N > 1 runs independent replicas.
+                      path; N > 1 node-shards the one cluster (strong scaling).
   config 4            100,000 nodes x 1M pods, node-sharded over N GPUs (strong).
   config 5            policy sweep: 1,024 score-weight vectors over config 2
                       (first 10,000 pods), vectors split over the N GPUs.
@@ -37,6 +40,11 @@ for _p in (ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd")):
 B_EVAL = 112            # algorithmic HBM bytes per pod x node evaluation
 B_FILTER = 60           # the filter columns of a row: allocatable 28 + requested 24 + pods 4 + flags 4
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def _k_adapt(n: int) -> int:
+    from ksim.profile import num_feasible_nodes_to_find
+    return num_feasible_nodes_to_find(n, 0)
 
 
 def log(*a):
@@ -147,6 +155,7 @@ def main():
     ap.add_argument("--force-shard", action="store_true",
                     help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-adapt", action="store_true", help="skip the secondary ADAPT measurement (config 2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     args = ap.parse_args()
@@ -308,6 +317,30 @@ def main():
                      "dominant_by_time": by_time},
         "batch_geometry": geom,
     }
+    if cfg == 2 and world == 1 and args.mode == "p100" and not args.no_adapt:
+        # the simulator's forced default (percentageOfNodesToScore = 0) on the
+        # same cluster and pods, timed the same way: a secondary line item
+        asp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+        aeng = engine.Engine(local)
+        aeng.set_profile(profile.compile_profile(asp))
+        aeng.set_cluster(cluster)
+        aeng.load_pods(pods)
+        aeng.schedule_loaded(0, pods.n_pods, want_chosen=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        aev = 0
+        for _ in range(args.steps):
+            aeng.reset_cluster()
+            _, ast = aeng.schedule_loaded(0, pods.n_pods, want_chosen=False)
+            aev += ast.evals
+        torch.cuda.synchronize()
+        adt = time.perf_counter() - t0
+        result["adapt"] = {"mode": "ADAPT (percentageOfNodesToScore 0, K = %d of %d nodes)" %
+                           (_k_adapt(cluster.n_nodes), cluster.n_nodes),
+                           "value": aev / adt, "unit": "evals/s", "pods_per_s": pods.n_pods * args.steps / adt,
+                           "ms_per_step": adt / args.steps * 1e3, "batches": ast.batches,
+                           "perpod_cycles": ast.perpod_cycles}
+        log(f"[rank 0] adapt: {aev / adt:.3e} evals/s")
     if rank == 0 and world == 1 and not args.no_cpu:
         log("[rank 0] cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(cluster, pods, sp, args.cpu_seconds, args.cpu_threads,

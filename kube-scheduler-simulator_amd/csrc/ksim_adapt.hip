@@ -60,8 +60,9 @@ __global__ __launch_bounds__(256) void k_adapt_mask(DevCluster c, DevPods P, Bat
   const int32_t node = w * 64 + lane;
   bool f = false;
   if (node < c.n) {
-    const NodeRow r = load_row(c, node);
-    f = batch_feasible(c, P, bp, P.pods[pi], r, (P.bflags[pi] & kBatchStaticTrivial) != 0);
+    const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;      // block-uniform
+    const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+    f = batch_feasible(c, P, bp, P.pods[pi], r, trivial);
   }
   const uint64_t m = __ballot(f);
   if (lane == 0) amask[(size_t)j * n_words + w] = m;
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
     if (node >= n) node -= n;
     if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
     kept++;
-    const NodeRow r = load_row(c, node);
+    const NodeRow r = load_res_row(c, node);      // scores read the resource columns only
     a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base));
 #pragma unroll
     for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);

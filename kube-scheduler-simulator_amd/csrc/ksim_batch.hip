@@ -57,7 +57,9 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
     const int32_t node = tile * kTileNodes + k * 64 + lane;
     uint64_t kk = 0;
     if (node < c.n) {
-      const NodeRow r = load_row(c, node);
+      // trivial: the static filters pass everywhere and the pod requests no
+      // scalar resources, so only the resource columns are read
+      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
       if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
     }
     a[3] = umax64(a[3], kk);

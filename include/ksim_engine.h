@@ -95,7 +95,7 @@ enum ksim_plugin {
 #define KSIM_POD_TOLERATES_UNSCHEDULABLE 1u  /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
 #define KSIM_POD_HAS_REQUIRED_AFFINITY   2u  /* spec.affinity.nodeAffinity.required != nil */
 #define KSIM_POD_HAS_SCALAR              4u  /* len(request.ScalarResources) > 0 */
-#define KSIM_POD_HAS_HOST_PORTS          8u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
+#define KSIM_POD_HAS_HOST_PORTS          8u  /* ports not compiled to KSIM_USE_NODE_PORT uses -> KSIM_E_UNSUPPORTED */
 #define KSIM_POD_HAS_VOLUMES            16u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
 
 /* pod topo_flags */
@@ -237,6 +237,7 @@ typedef struct ksim_pod {
 #define KSIM_USE_IPA_ANTI           4
 #define KSIM_USE_IPA_SCORE          5
 #define KSIM_USE_IPA_SCORE_HARD     6
+#define KSIM_USE_NODE_PORT          7   /* NodePorts: the node must hold no pod of class cls (col unused) */
 #define KSIM_USEF_SELF_MATCH        1u   /* PTS: constraint selector matches the pod itself */
 #define KSIM_USEF_HONOR_AFFINITY    2u   /* PTS: nodeAffinityPolicy Honor (default) */
 #define KSIM_USEF_HONOR_TAINTS      4u   /* PTS: nodeTaintsPolicy Honor (default Ignore) */

@@ -490,6 +490,8 @@ __device__ __forceinline__ uint32_t ipa_filter(const DevCluster& c, const DevPod
                                                const ksim_pod& p, uint32_t topo_flags, int32_t node);
 __device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
                                              const ksim_profile& prof, const ksim_pod& p, int32_t node);
+__device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                   int32_t node);
 
 __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                              const DevScratch& s, uint32_t topo_flags,
@@ -518,6 +520,9 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (bits) { detail = bits; return (uint8_t)f; }
         break;
       }
+      case KSIM_PL_NODE_PORTS:
+        if (p.use_count && node_port_conflict(c, P, p, node)) return (uint8_t)f;
+        break;
       case KSIM_PL_POD_TOPOLOGY_SPREAD: {
         const uint32_t why = p.use_count ? pts_filter(c, P, s, p, node) : 0;
         if (why) { detail = why; return (uint8_t)f; }
@@ -602,6 +607,18 @@ __device__ __forceinline__ bool node_has_all_keys(const DevCluster& c, const Dev
     if (u.kind == kind && use_value(c, u, node) == 0) return false;
   }
   return true;
+}
+
+// nodeports Filter: HostPortInfo.CheckConflict of every wanted port, compiled
+// by the host to "class of pods using a conflicting (ip, protocol, port) is
+// empty on the node" (ksim/topology.py port classes)
+__device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                   int32_t node) {
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind == KSIM_USE_NODE_PORT && class_count(c, u.cls, node) > 0) return true;
+  }
+  return false;
 }
 
 // podtopologyspread Filter -> 0 or KSIM_PTS_*

@@ -527,8 +527,6 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
                 continue
             b.term(pt.term, pt.weight)
         rec["pref_term_count"] = len(b.terms) - rec["pref_term_first"]
-        if any(c.host_ports for c in p.containers + p.init_containers):
-            flags |= abi.POD_HAS_HOST_PORTS
         if p.has_volumes:
             flags |= abi.POD_HAS_VOLUMES
         rec["flags"] = flags

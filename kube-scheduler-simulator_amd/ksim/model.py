@@ -174,9 +174,21 @@ class WeightedPodAffinityTerm:
 
 
 @dataclass
+class ContainerPort:
+    """v1.ContainerPort fields NodePorts reads (hostPort 0: not a host port)."""
+    host_port: int = 0
+    protocol: str = "TCP"
+    host_ip: str = ""
+
+
+@dataclass
 class Container:
     requests: Dict[str, str] = field(default_factory=dict)
-    host_ports: List[int] = field(default_factory=list)
+    ports: List[ContainerPort] = field(default_factory=list)
+
+    @property
+    def host_ports(self) -> List[int]:
+        return [p.host_port for p in self.ports if p.host_port > 0]
 
 
 @dataclass
@@ -267,7 +279,8 @@ def node_from_dict(d: dict) -> Node:
 def _container(c) -> Container:
     res = c.get("resources") or {}
     return Container({k: str(v) for k, v in (res.get("requests") or {}).items()},
-                     [p["hostPort"] for p in (c.get("ports") or []) if p.get("hostPort")])
+                     [ContainerPort(int(p.get("hostPort") or 0), p.get("protocol") or "TCP", p.get("hostIP") or "")
+                      for p in (c.get("ports") or [])])
 
 
 def pod_from_dict(d: dict) -> Pod:

@@ -90,6 +90,8 @@ class TopologyIndex:
         self._match_cache: Dict[Tuple[tuple, Matcher], bool] = {}
         self.sel_ids: List[int] = []                # selector classes (subset of ids)
         self.carry_ids: List[int] = []              # carried classes
+        self.port_ids: List[int] = []               # host-port classes (NodePorts)
+        self.bound_ports: List[Tuple[int, tuple]] = []   # (node position, (ip, protocol, port)) of bound pods
         self._carry_uses: Dict[tuple, List[tuple]] = {}   # signature -> carried uses (valid for a class count)
 
     # ---- matchers ------------------------------------------------------------
@@ -149,8 +151,46 @@ class TopologyIndex:
         self.keys.append(key)
         self.ids[key] = cid
         self.counts.append(counts)
-        (self.sel_ids if key[0] == "sel" else self.carry_ids).append(cid)
+        {"sel": self.sel_ids, "carry": self.carry_ids, "port": self.port_ids}[key[0]].append(cid)
         return cid
+
+    # ---- NodePorts: HostPortInfo as count classes -------------------------------
+    # A class ("port", ip, protocol, port) counts the pods on a node using that
+    # exact triple; ("port", "*", protocol, port) those using it on any ip.
+    # HostPortInfo.CheckConflict(ip, protocol, port): ip 0.0.0.0 conflicts
+    # with the (protocol, port) pair on any ip, another ip with itself and 0.0.0.0.
+    def port_class(self, ip: str, protocol: str, port: int) -> int:
+        key = ("port", ip, protocol, port)
+        cid = self.ids.get(key)
+        if cid is not None:
+            return cid
+        cnt = np.zeros(self.n, np.int32)
+        for pos, (bip, bproto, bport) in self.bound_ports:
+            if bproto == protocol and bport == port and (ip == "*" or ip == bip):
+                cnt[pos] += 1
+        return self._new_class(key, cnt)
+
+    def port_check_classes(self, pod: Pod) -> List[int]:
+        """Classes whose presence on a node fails NodePorts for ``pod`` (fitsPorts)."""
+        out: List[int] = []
+        for ip, proto, port in pod_host_ports(pod):
+            keys = [("*", proto, port)] if ip == DEFAULT_BIND_ALL_HOST_IP else \
+                [(DEFAULT_BIND_ALL_HOST_IP, proto, port), (ip, proto, port)]
+            for k in keys:
+                c = self.port_class(*k)
+                if c not in out:
+                    out.append(c)
+        return out
+
+    def port_adds(self, pod: Pod) -> Dict[int, int]:
+        """NodeInfo.AddPod -> UsedPorts.Add of each host port, on the registered classes."""
+        out: Dict[int, int] = {}
+        for ip, proto, port in pod_host_ports(pod):
+            for k in (("port", "*", proto, port), ("port", ip, proto, port)):
+                c = self.ids.get(k)
+                if c is not None:
+                    out[c] = out.get(c, 0) + 1
+        return out
 
     def selector_class(self, m) -> int:
         """Class of pods matching ``m`` (a Matcher, or ("all", (Matcher, ...))
@@ -197,6 +237,9 @@ class TopologyIndex:
         for cid in self.sel_ids:
             if self._pod_matches(self.keys[cid][1], pod):
                 self.counts[cid][pos] += 1
+        for c, k in self.port_adds(pod).items():
+            self.counts[c][pos] += k
+        self.bound_ports.extend((pos, t) for t in pod_host_ports(pod))
         sig = (pod.namespace, tuple(sorted(pod.labels.items())))
         self.bound_sigs.setdefault(sig, []).append(pos)
         self.sig_pods.setdefault(sig, pod)
@@ -208,6 +251,8 @@ class TopologyIndex:
         for cid in self.sel_ids:
             if self._pod_matches(self.keys[cid][1], pod):
                 out[cid] = out.get(cid, 0) + 1
+        for cid, k in self.port_adds(pod).items():
+            out[cid] = out.get(cid, 0) + k
         return sorted(out.items())
 
     def carried_uses(self, cluster, pod: Pod) -> List[tuple]:
@@ -241,6 +286,21 @@ class TopologyIndex:
 
 
 # ---- per-pod compilation -------------------------------------------------------
+DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
+
+
+def pod_host_ports(pod: Pod) -> List[tuple]:
+    """(ip, protocol, port) of the pod's containers' host ports, sanitized as
+    HostPortInfo does (empty ip -> 0.0.0.0, empty protocol -> TCP); port <= 0
+    is no host port.  Init containers' ports are not host ports of the pod."""
+    out = []
+    for c in pod.containers:
+        for p in c.ports:
+            if p.host_port > 0:
+                out.append((p.host_ip or DEFAULT_BIND_ALL_HOST_IP, p.protocol or "TCP", int(p.host_port)))
+    return out
+
+
 def _col(cluster, key: str) -> int:
     c = cluster.label_col(key)
     return abi.COL_NONE if c < 0 else c
@@ -261,6 +321,7 @@ def register_pod_classes(topo: TopologyIndex, pod: Pod) -> None:
         topo.selector_class(topo.term_matcher(pod, t))
     for w in pod.pod_affinity_preferred + pod.pod_anti_affinity_preferred:
         topo.selector_class(topo.term_matcher(pod, w.term))
+    topo.port_check_classes(pod)
 
 
 def _use(kind, cls, col, arg=0, flags=0):
@@ -316,6 +377,9 @@ def pod_uses(topo: TopologyIndex, cluster, pod: Pod) -> Tuple[List[tuple], int]:
     for w in pod.pod_anti_affinity_preferred:
         uses.append(_use(abi.USE_IPA_SCORE, topo.selector_class(topo.term_matcher(pod, w.term)),
                          _col(cluster, w.term.topology_key), -w.weight))
+    # --- NodePorts: a conflicting host port on the node fails the filter ---
+    for cls in topo.port_check_classes(pod):
+        uses.append(_use(abi.USE_NODE_PORT, cls, abi.COL_NONE))
     if len(uses) > abi.MAX_USES:
         raise TopologyError(f"pod {pod.name}: {len(uses)} topology uses > {abi.MAX_USES}")
     return uses, flags

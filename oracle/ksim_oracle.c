@@ -420,6 +420,17 @@ static inline int64_t class_count(const ksim_oracle* o, int32_t cls, int32_t nod
   return cls < 0 ? 0 : o->cnt[(size_t)cls * o->n + node];
 }
 
+/* nodeports fitsPorts: HostPortInfo.CheckConflict(ip, protocol, port) of each
+ * wanted port; the host compiled each check to the classes of pods holding a
+ * conflicting (ip, protocol, port) on a node (0.0.0.0 conflicts with every ip). */
+static int node_port_conflict(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p, int32_t node) {
+  for (int32_t i = 0; i < p->use_count; i++) {
+    const ksim_topo_use* u = &ps->uses[p->use_first + i];
+    if (u->kind == KSIM_USE_NODE_PORT && class_count(o, u->cls, node) > 0) return 1;
+  }
+  return 0;
+}
+
 static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set* ps,
                                         const ksim_pod* p, int32_t node);
 static uint32_t find_matching_untolerated_taint(const ksim_oracle* o, const ksim_pod* p, int32_t node);
@@ -665,7 +676,10 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
         if (r) { *detail = r; return (uint8_t)f; }
         break;
       }
-      /* NodePorts / volume plugins: pods without host ports or volumes pass. */
+      case KSIM_PL_NODE_PORTS:           /* nodeports.Filter -> fitsPorts */
+        if (node_port_conflict(o, ps, p, node)) return (uint8_t)f;
+        break;
+      /* volume plugins: pods without volumes pass. */
       default:
         break;
     }

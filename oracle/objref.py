@@ -98,8 +98,15 @@ class NodeInfo:
         self.nz_cpu = 0
         self.nz_mem = 0
         self.pods: List[PodInfo] = []
+        self.used_ports: Dict[str, set] = {}     # HostPortInfo: ip -> {(protocol, port)}
 
     def add_pod(self, pod: Pod) -> None:
+        for c in pod.containers:                 # NodeInfo.updateUsedPorts (Spec.Containers)
+            for p in c.ports:
+                if p.host_port <= 0:
+                    continue
+                ip, proto = p.host_ip or "0.0.0.0", p.protocol or "TCP"
+                self.used_ports.setdefault(ip, set()).add((proto, p.host_port))
         for k, v in pod_requests(pod).items():
             self.requested[k] = self.requested.get(k, 0) + v
         c, m = pod_nonzero_requests(pod)
@@ -465,6 +472,21 @@ class ObjScheduler:
         out = [go_div(MAX_NODE_SCORE * s, m) for s in scores]
         return [MAX_NODE_SCORE - s for s in out] if reverse else out
 
+    # ---- NodePorts (nodeports.fitsPorts, HostPortInfo.CheckConflict) -----------------
+    @staticmethod
+    def fits_ports(pod: Pod, ni: NodeInfo) -> bool:
+        for c in pod.containers:                 # getContainerPorts
+            for p in c.ports:
+                if p.host_port <= 0:
+                    continue
+                ip, pp = p.host_ip or "0.0.0.0", (p.protocol or "TCP", p.host_port)
+                if ip == "0.0.0.0":
+                    if any(pp in m for m in ni.used_ports.values()):
+                        return False
+                elif any(pp in ni.used_ports.get(k, ()) for k in ("0.0.0.0", ip)):
+                    return False
+        return True
+
     # ---- the cycle ---------------------------------------------------------------------
     def filter_node(self, pod: Pod, ni: NodeInfo, pts, ipa) -> Tuple[Optional[str], Optional[str]]:
         node = ni.node
@@ -485,6 +507,9 @@ class ObjScheduler:
             elif pl == "NodeAffinity":
                 if not self.required_node_affinity(pod, node):
                     msg = "node(s) didn't match Pod's node affinity/selector"
+            elif pl == "NodePorts":
+                if not self.fits_ports(pod, ni):
+                    msg = "node(s) didn't have free ports for the requested pod ports"
             elif pl == "NodeResourcesFit":
                 msg = self.fit_filter(pod, ni)
             elif pl == "PodTopologySpread":

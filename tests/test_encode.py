@@ -129,8 +129,11 @@ def test_from_dict_roundtrip():
     assert p.required_terms[0].match_expressions[0].values == ["b"]
     assert p.containers[0].host_ports == [8080] and p.has_volumes
     c, _ = encode_cluster([n])
-    rec = encode_pods(c, [p]).pods[0]
-    assert rec["flags"] & abi.POD_HAS_HOST_PORTS and rec["flags"] & abi.POD_HAS_VOLUMES
+    e = encode_pods(c, [p])
+    rec = e.pods[0]
+    # host ports compile to a NodePorts use (class of pods on 0.0.0.0:8080/TCP); volumes stay unsupported
+    assert not rec["flags"] & abi.POD_HAS_HOST_PORTS and rec["flags"] & abi.POD_HAS_VOLUMES
+    assert rec["use_count"] == 1 and e.uses[rec["use_first"]]["kind"] == abi.USE_NODE_PORT
 
 
 def test_bound_pods_fill_node_info():

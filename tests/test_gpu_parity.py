@@ -286,3 +286,23 @@ def test_topology_hand_cases_vs_oracle():
             eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
             for i in range(enc.n_pods):
                 _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_node_ports_vs_oracle(pct):
+    """NodePorts on the device: per-node codes of every cycle, then a batch run
+    mixing port pods (per-pod path) and batchable pods."""
+    from ksim.encode import encode_cluster, encode_pods
+    from ksim.model import ContainerPort
+    nodes, pods = gen.config1_objects(n_nodes=150, n_pods=900)
+    for i, p in enumerate(pods):
+        if i % 3 == 0:
+            p.containers[0].ports = [ContainerPort(8000 + i % 7, "TCP" if i % 4 else "UDP",
+                                                   "" if i % 2 else "10.1.0.%d" % (i % 4))]
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods)
+    prof = _prof(pct)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(300):
+        _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
+    _batch_vs_oracle(cluster, enc, pct=pct)

@@ -191,3 +191,42 @@ def test_invalid_selector_rejected():
     cluster, _ = encode_cluster(nodes)
     with pytest.raises(ValueError):
         encode_pods(cluster, [bad])
+
+
+# ---- NodePorts: HostPortInfo as count classes -------------------
+
+def _port_pod(name, ports, node="", **kw):
+    from ksim.model import ContainerPort
+    return Pod(name, node_name=node, containers=[
+        Container({"cpu": "100m", "memory": "128Mi"}, [ContainerPort(*p) for p in ports])], **kw)
+
+
+def test_node_ports_conflicts_vs_objref():
+    """0.0.0.0 conflicts with the (protocol, port) pair on every ip, a specific ip
+    with itself and 0.0.0.0; protocols differ; hostPort 0 is no host port;
+    bound pods' ports and earlier queue pods' binds both count."""
+    nodes = [_node(i, f"z{i % 2}") for i in range(4)]
+    bound = [_port_pod("b0", [(80, "TCP", "")], node="n0"),
+             _port_pod("b1", [(80, "TCP", "10.0.0.1"), (53, "UDP", "")], node="n1"),
+             _port_pod("b2", [(8080, "TCP", "10.0.0.2")], node="n2")]
+    pods = [_port_pod("p0", [(80, "TCP", "")]),                # conflicts n0 (0.0.0.0) and n1 (10.0.0.1)
+            _port_pod("p1", [(80, "TCP", "10.0.0.3")]),        # conflicts n0 (0.0.0.0) only
+            _port_pod("p2", [(53, "TCP", "")]),                # UDP 53 on n1 does not conflict
+            _port_pod("p3", [(53, "UDP", "10.0.0.9")]),        # n1 holds UDP 53 on 0.0.0.0
+            _port_pod("p4", [(8080, "TCP", "10.0.0.2"), (0, "TCP", "")]),
+            _port_pod("p5", [(80, "TCP", ""), (53, "UDP", "")]),
+            _port_pod("p6", [(9000, "", "")])]                 # empty protocol -> TCP
+    pods += [_port_pod(f"q{i}", [(7000 + i % 3, "TCP", "")]) for i in range(8)]   # fill: later pods conflict
+    for pct in (0, 100):
+        run_both(nodes, bound, pods, pct=pct)
+
+
+def test_node_ports_config1_mixed():
+    """Config-1 objects with host ports on a third of the pods (per-pod path),
+    the rest batchable: the C oracle equals the object-level restatement."""
+    from ksim.model import ContainerPort
+    nodes, pods = gen.config1_objects(n_nodes=30, n_pods=240)
+    for i, p in enumerate(pods):
+        if i % 3 == 0:
+            p.containers[0].ports = [ContainerPort(8000 + i % 5, "TCP", "" if i % 2 else "10.1.0.%d" % (i % 4))]
+    run_both(nodes, [], pods, pct=0, check_state=False)

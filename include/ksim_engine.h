@@ -238,6 +238,7 @@ typedef struct ksim_pod {
 #define KSIM_USE_IPA_SCORE          5
 #define KSIM_USE_IPA_SCORE_HARD     6
 #define KSIM_USE_NODE_PORT          7   /* NodePorts: the node must hold no pod of class cls (col unused) */
+#define KSIM_USE_IMAGE              8   /* ImageLocality: raw score = class count (per node, static) */
 #define KSIM_USEF_SELF_MATCH        1u   /* PTS: constraint selector matches the pod itself */
 #define KSIM_USEF_HONOR_AFFINITY    2u   /* PTS: nodeAffinityPolicy Honor (default) */
 #define KSIM_USEF_HONOR_TAINTS      4u   /* PTS: nodeTaintsPolicy Honor (default Ignore) */

@@ -492,6 +492,8 @@ __device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods&
                                              const ksim_profile& prof, const ksim_pod& p, int32_t node);
 __device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const DevPods& P, const ksim_pod& p,
                                                    int32_t node);
+__device__ __forceinline__ int64_t image_locality_score(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                        int32_t node);
 
 __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                              const DevScratch& s, uint32_t topo_flags,
@@ -549,7 +551,8 @@ __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const D
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
     case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(c, P, s, prof, p, r.node) : 0;
-    default: return 0;   // ImageLocality (no images); PodTopologySpread: k_extrema
+    case KSIM_PL_IMAGE_LOCALITY: return p.use_count ? image_locality_score(c, P, p, r.node) : 0;
+    default: return 0;   // PodTopologySpread: k_extrema
   }
 }
 
@@ -619,6 +622,18 @@ __device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const De
     if (u.kind == KSIM_USE_NODE_PORT && class_count(c, u.cls, node) > 0) return true;
   }
   return false;
+}
+
+// imagelocality Score: calculatePriority(sumImageScores) depends only on the
+// node's static image list and the pod's container images, so the host
+// compiles it per image signature to a static class (ksim/topology.py).
+__device__ __forceinline__ int64_t image_locality_score(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                        int32_t node) {
+  for (int i = 0; i < p.use_count; i++) {
+    const ksim_topo_use& u = P.uses[p.use_first + i];
+    if (u.kind == KSIM_USE_IMAGE) return class_count(c, u.cls, node);
+  }
+  return 0;
 }
 
 // podtopologyspread Filter -> 0 or KSIM_PTS_*

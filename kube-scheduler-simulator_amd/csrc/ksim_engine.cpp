@@ -206,7 +206,7 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
     return set_err(h, KSIM_E_INVALID, who + "bad topology use range");
   for (int32_t k = 0; k < p.use_count; k++) {
     const ksim_topo_use& u = ps->uses[p.use_first + k];
-    if (u.kind > KSIM_USE_NODE_PORT) return set_err(h, KSIM_E_INVALID, who + "bad topology use kind");
+    if (u.kind > KSIM_USE_IMAGE) return set_err(h, KSIM_E_INVALID, who + "bad topology use kind");
     if (u.cls < -1 || u.cls >= c.n_classes) return set_err(h, KSIM_E_INVALID, who + "topology use class out of range");
     if (u.col != KSIM_COL_NONE && u.col >= c.n_label_cols)
       return set_err(h, KSIM_E_INVALID, who + "topology key column out of range");

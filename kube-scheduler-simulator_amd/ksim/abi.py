@@ -96,6 +96,7 @@ USE_IPA_ANTI = 4
 USE_IPA_SCORE = 5
 USE_IPA_SCORE_HARD = 6
 USE_NODE_PORT = 7
+USE_IMAGE = 8
 USEF_SELF_MATCH = 1
 USEF_HONOR_AFFINITY = 2
 USEF_HONOR_TAINTS = 4

@@ -364,6 +364,7 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
     )
     c.topo = TopologyIndex(N, namespaces)
     pos_of = {name: i for i, name in enumerate(c.node_names)}
+    c.topo.set_images(nodes, pos_of)                 # input order = the order nodes were added
     for p in bound_pods:
         if p.node_name in pos_of:
             c.topo.carried_terms(p)          # classes of every carried term exist first

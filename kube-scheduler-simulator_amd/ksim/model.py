@@ -10,7 +10,7 @@ import math
 import re
 from dataclasses import dataclass, field
 from fractions import Fraction
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 # ---- resource.Quantity ----------------------------------------------------
 _BIN = {"Ki": 2 ** 10, "Mi": 2 ** 20, "Gi": 2 ** 30, "Ti": 2 ** 40, "Pi": 2 ** 50, "Ei": 2 ** 60}
@@ -185,6 +185,7 @@ class ContainerPort:
 class Container:
     requests: Dict[str, str] = field(default_factory=dict)
     ports: List[ContainerPort] = field(default_factory=list)
+    image: str = ""
 
     @property
     def host_ports(self) -> List[int]:
@@ -198,6 +199,7 @@ class Node:
     taints: List[Taint] = field(default_factory=list)
     allocatable: Dict[str, str] = field(default_factory=dict)
     unschedulable: bool = False
+    images: List[Tuple[List[str], int]] = field(default_factory=list)   # status.images: (names, sizeBytes)
 
 
 @dataclass
@@ -273,6 +275,7 @@ def node_from_dict(d: dict) -> Node:
         taints=[Taint(t["key"], t.get("value", ""), t.get("effect", "")) for t in (spec.get("taints") or [])],
         allocatable={k: str(v) for k, v in (status.get("allocatable") or {}).items()},
         unschedulable=bool(spec.get("unschedulable", False)),
+        images=[(list(im.get("names") or []), int(im.get("sizeBytes") or 0)) for im in (status.get("images") or [])],
     )
 
 
@@ -280,7 +283,7 @@ def _container(c) -> Container:
     res = c.get("resources") or {}
     return Container({k: str(v) for k, v in (res.get("requests") or {}).items()},
                      [ContainerPort(int(p.get("hostPort") or 0), p.get("protocol") or "TCP", p.get("hostIP") or "")
-                      for p in (c.get("ports") or [])])
+                      for p in (c.get("ports") or [])], c.get("image") or "")
 
 
 def pod_from_dict(d: dict) -> Pod:

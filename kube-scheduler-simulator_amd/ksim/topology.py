@@ -91,6 +91,8 @@ class TopologyIndex:
         self.sel_ids: List[int] = []                # selector classes (subset of ids)
         self.carry_ids: List[int] = []              # carried classes
         self.port_ids: List[int] = []               # host-port classes (NodePorts)
+        self.image_ids: List[int] = []              # image-signature classes (ImageLocality)
+        self.images: Dict[str, Tuple[int, np.ndarray]] = {}   # image name -> (size, node mask)
         self.bound_ports: List[Tuple[int, tuple]] = []   # (node position, (ip, protocol, port)) of bound pods
         self._carry_uses: Dict[tuple, List[tuple]] = {}   # signature -> carried uses (valid for a class count)
 
@@ -151,7 +153,8 @@ class TopologyIndex:
         self.keys.append(key)
         self.ids[key] = cid
         self.counts.append(counts)
-        {"sel": self.sel_ids, "carry": self.carry_ids, "port": self.port_ids}[key[0]].append(cid)
+        {"sel": self.sel_ids, "carry": self.carry_ids, "port": self.port_ids,
+         "image": self.image_ids}[key[0]].append(cid)
         return cid
 
     # ---- NodePorts: HostPortInfo as count classes -------------------------------
@@ -181,6 +184,43 @@ class TopologyIndex:
                 if c not in out:
                     out.append(c)
         return out
+
+    # ---- ImageLocality: static per-node scores per image signature ----------------
+    def set_images(self, nodes_in_add_order, pos_of: Dict[str, int]) -> None:
+        """cache.addNodeImageStates over the nodes in the order they were added:
+        an image name's size is the one of the first node listing it, its
+        NumNodes the nodes listing it (ImageStateSummary)."""
+        for n in nodes_in_add_order:
+            for names, size in n.images:
+                for name in names:
+                    st = self.images.get(name)
+                    if st is None:
+                        st = (int(size), np.zeros(self.n, bool))
+                        self.images[name] = st
+                    st[1][pos_of[n.name]] = True
+
+    def image_class(self, pod: Pod) -> Optional[int]:
+        """Class whose count on a node is imagelocality.Score(pod, node):
+        calculatePriority(sumImageScores(node, containers, N), len(containers))."""
+        names = tuple(normalized_image_name(c.image) for c in pod.containers)
+        if not any(nm in self.images for nm in names):
+            return None                                  # 0 on every node: no use needed
+        key = ("image", names)
+        cid = self.ids.get(key)
+        if cid is not None:
+            return cid
+        total = np.zeros(self.n, np.int64)
+        for nm in names:
+            st = self.images.get(nm)
+            if st is None:
+                continue
+            size, mask = st
+            spread = float(int(mask.sum())) / float(self.n)       # float64(NumNodes) / float64(totalNumNodes)
+            total += np.where(mask, int(float(size) * spread), 0)   # int64(float64(Size) * spread)
+        max_t = IMAGE_MAX_CONTAINER_THRESHOLD * len(names)
+        s = np.minimum(np.maximum(total, IMAGE_MIN_THRESHOLD), max_t)
+        score = (100 * (s - IMAGE_MIN_THRESHOLD)) // (max_t - IMAGE_MIN_THRESHOLD)
+        return self._new_class(key, score.astype(np.int32))
 
     def port_adds(self, pod: Pod) -> Dict[int, int]:
         """NodeInfo.AddPod -> UsedPorts.Add of each host port, on the registered classes."""
@@ -287,6 +327,16 @@ class TopologyIndex:
 
 # ---- per-pod compilation -------------------------------------------------------
 DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
+_MB = 1024 * 1024
+IMAGE_MIN_THRESHOLD = 23 * _MB                 # imagelocality minThreshold
+IMAGE_MAX_CONTAINER_THRESHOLD = 1000 * _MB     # imagelocality maxContainerThreshold
+
+
+def normalized_image_name(name: str) -> str:
+    """imagelocality normalizedImageName: a name without a tag gets ":latest"."""
+    if name.rfind(":") <= name.rfind("/"):
+        name = name + ":latest"
+    return name
 
 
 def pod_host_ports(pod: Pod) -> List[tuple]:
@@ -322,6 +372,7 @@ def register_pod_classes(topo: TopologyIndex, pod: Pod) -> None:
     for w in pod.pod_affinity_preferred + pod.pod_anti_affinity_preferred:
         topo.selector_class(topo.term_matcher(pod, w.term))
     topo.port_check_classes(pod)
+    topo.image_class(pod)
 
 
 def _use(kind, cls, col, arg=0, flags=0):
@@ -377,6 +428,10 @@ def pod_uses(topo: TopologyIndex, cluster, pod: Pod) -> Tuple[List[tuple], int]:
     for w in pod.pod_anti_affinity_preferred:
         uses.append(_use(abi.USE_IPA_SCORE, topo.selector_class(topo.term_matcher(pod, w.term)),
                          _col(cluster, w.term.topology_key), -w.weight))
+    # --- ImageLocality: the pod's image-signature score class ---
+    ic = topo.image_class(pod)
+    if ic is not None:
+        uses.append(_use(abi.USE_IMAGE, ic, abi.COL_NONE))
     # --- NodePorts: a conflicting host port on the node fails the filter ---
     for cls in topo.port_check_classes(pod):
         uses.append(_use(abi.USE_NODE_PORT, cls, abi.COL_NONE))

@@ -696,7 +696,13 @@ static int64_t score_plugin_raw(const ksim_oracle* o, const ksim_pod_set* ps, co
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(o, ps, p, node);
     case KSIM_PL_POD_TOPOLOGY_SPREAD: return pts_score(o, t, node);
     case KSIM_PL_INTER_POD_AFFINITY: return t->has_ipa_score ? ipa_score(o, t, node) : 0;
-    /* ImageLocality: nodes carry no image list -> calculatePriority(0) = 0. */
+    case KSIM_PL_IMAGE_LOCALITY: {     /* imagelocality.Score, compiled per image signature */
+      for (int32_t i = 0; i < p->use_count; i++) {
+        const ksim_topo_use* u = &ps->uses[p->use_first + i];
+        if (u->kind == KSIM_USE_IMAGE) return class_count(o, u->cls, node);
+      }
+      return 0;
+    }
     default: return 0;
   }
 }

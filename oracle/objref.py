@@ -123,6 +123,12 @@ class ObjScheduler:
                  hard_pod_affinity_weight: int = 1):
         order = node_tree_order([zone_key(n.labels) for n in nodes])
         self.nodes = [NodeInfo(nodes[i]) for i in order]
+        # cache.addNodeImageStates, nodes in the order they were added: name -> [size, {node names}]
+        self.image_states: Dict[str, list] = {}
+        for n in nodes:
+            for names, size in n.images:
+                for name in names:
+                    self.image_states.setdefault(name, [int(size), set()])[1].add(n.name)
         self.by_name = {ni.node.name: ni for ni in self.nodes}
         for p in bound:
             if p.node_name in self.by_name:
@@ -472,6 +478,27 @@ class ObjScheduler:
         out = [go_div(MAX_NODE_SCORE * s, m) for s in scores]
         return [MAX_NODE_SCORE - s for s in out] if reverse else out
 
+    # ---- ImageLocality (imagelocality.Score) ----------------------------------------
+    def image_locality(self, pod: Pod, node: Node) -> int:
+        mb = 1024 * 1024
+        min_t, max_t = 23 * mb, 1000 * mb * len(pod.containers)
+        total_nodes = len(self.nodes)
+        have = {nm for names, _ in node.images for nm in names}
+        s = 0
+        for c in pod.containers:                  # sumImageScores
+            name = c.image
+            if name.rfind(":") <= name.rfind("/"):
+                name += ":latest"                 # normalizedImageName
+            if name in have:
+                size, on = self.image_states[name]
+                spread = float(len(on)) / float(total_nodes)
+                s += int(float(size) * spread)    # scaledImageScore
+        if s < min_t:                             # calculatePriority
+            s = min_t
+        elif s > max_t:
+            s = max_t
+        return go_div(MAX_NODE_SCORE * (s - min_t), max_t - min_t)
+
     # ---- NodePorts (nodeports.fitsPorts, HostPortInfo.CheckConflict) -----------------
     @staticmethod
     def fits_ports(pod: Pod, ni: NodeInfo) -> bool:
@@ -557,7 +584,7 @@ class ObjScheduler:
                     raw = [self.balanced(pod, ni) for ni in feasible]
                     norm = raw
                 elif pl == "ImageLocality":
-                    raw = [0] * len(feasible)
+                    raw = [self.image_locality(pod, ni.node) for ni in feasible]
                     norm = raw
                 elif pl == "InterPodAffinity":
                     raw = [self.ipa_score(topo, ni.node) for ni in feasible]

@@ -306,3 +306,28 @@ def test_node_ports_vs_oracle(pct):
     for i in range(300):
         _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
     _batch_vs_oracle(cluster, enc, pct=pct)
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_image_locality_vs_oracle(pct):
+    """ImageLocality on the device: nodes with image lists, pods with container
+    images (per-pod path) mixed with image-less batchable pods."""
+    from ksim.encode import encode_cluster, encode_pods
+    mb = 1024 * 1024
+    nodes, pods = gen.config1_objects(n_nodes=160, n_pods=800)
+    for i, n in enumerate(nodes):
+        n.images = [(["app:%d" % (i % 4)], (60 + 90 * (i % 5)) * mb)]
+        if i % 7 == 0:
+            n.images.append((["base/os"], 1500 * mb))
+    for i, p in enumerate(pods):
+        if i % 2 == 0:
+            p.containers[0].image = "app:%d" % (i % 5)
+        if i % 6 == 0:
+            p.containers[0].image = "base/os:latest"
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods)
+    prof = _prof(pct)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(200):
+        _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
+    _batch_vs_oracle(cluster, enc, pct=pct)

@@ -230,3 +230,35 @@ def test_node_ports_config1_mixed():
         if i % 3 == 0:
             p.containers[0].ports = [ContainerPort(8000 + i % 5, "TCP", "" if i % 2 else "10.1.0.%d" % (i % 4))]
     run_both(nodes, [], pods, pct=0, check_state=False)
+
+
+# ---- ImageLocality -------------------------------------------------
+
+def test_image_locality_vs_objref():
+    """Node image lists with sizes around the 23 MB / 1000 MB x containers
+    thresholds, images spread over some nodes, untagged names (":latest"),
+    multi-container pods, pods whose images no node has."""
+    mb = 1024 * 1024
+    nodes = []
+    for i in range(12):
+        n = _node(i, f"z{i % 3}")
+        imgs = []
+        if i % 2 == 0:
+            imgs.append((["nginx:latest", "docker.io/library/nginx:latest"], 180 * mb))
+        if i % 3 == 0:
+            imgs.append((["redis:7"], 40 * mb + i))
+        if i % 4 == 1:
+            imgs.append((["big/model:v1"], 3000 * mb))
+        if i == 5:
+            imgs.append((["tiny:1"], 5 * mb))
+        n.images = imgs
+        nodes.append(n)
+
+    def ipod(name, images):
+        return Pod(name, containers=[Container({"cpu": "100m", "memory": "64Mi"}, image=im) for im in images])
+    pods = [ipod("a", ["nginx"]), ipod("b", ["redis:7", "nginx:latest"]), ipod("c", ["big/model:v1"]),
+            ipod("d", ["tiny:1"]), ipod("e", ["absent:1"]), ipod("f", ["big/model:v1", "redis:7", "nginx"]),
+            ipod("g", ["docker.io/library/nginx"])]
+    pods = pods * 3
+    for pct in (0, 100):
+        run_both(nodes, [], pods, pct=pct)

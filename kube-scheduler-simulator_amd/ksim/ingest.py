@@ -1,0 +1,157 @@
+"""Snapshot ingest: the simulator's import/export document -> engine inputs
+(SURVEY §8(f) 2).
+
+The reference moves whole cluster states as ``ResourcesForImport`` /
+``ResourcesForExport`` JSON (simulator/export/export.go:43-65): pods, nodes,
+pvs, pvcs, storageClasses, priorityClasses, schedulerConfig, namespaces.  This
+module turns one such document into what the engine runs:
+
+* nodes in nodeTree order (ksim.encode), bound pods (``spec.nodeName`` set)
+  added to their node's aggregates and count classes like NodeInfo.AddPod;
+* the pending pods in scheduling-queue order: PrioritySort (higher
+  ``.spec.priority`` first, the priority resolved from ``priorityClassName`` /
+  the globalDefault class as the Priority admission plugin does), ties by
+  creationTimestamp then document order;
+* the scheduler profiles of ``schedulerConfig`` converted the way the simulator
+  does it (scheduler.go:199-249 convertConfigurationForSimulator): plugins merged
+  over the in-tree defaults (plugins.go:185-288), plugin args over the defaults
+  (plugins.go:103-179), every non-profile field reset to the default, so
+  percentageOfNodesToScore is 0 (ADAPT) whatever the document says.
+
+PVs, PVCs and StorageClasses are carried but not evaluated: pods that mount
+volumes of the volume plugins' kinds are reported in ``unsupported`` and left
+out of the queue (the engine's volume filters only cover pods without them).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+from . import profile as prof_mod
+from .model import Node, Pod, node_from_dict, pod_from_dict
+
+
+@dataclass
+class Snapshot:
+    nodes: List[Node]
+    bound: List[Pod]
+    pending: List[Pod]                       # scheduling-queue order
+    namespaces: Dict[str, Dict[str, str]]
+    profiles: List[Tuple[str, prof_mod.SchedulerProfile]]   # (schedulerName, profile)
+    unsupported: List[Tuple[str, str, str]] = field(default_factory=list)   # (namespace, name, why)
+    counts: Dict[str, int] = field(default_factory=dict)
+
+
+# ---- priority (admission: priority from PriorityClass) -------------------------------
+def _priority(spec: dict, classes: Dict[str, int], default: int) -> int:
+    if spec.get("priority") is not None:
+        return int(spec["priority"])
+    name = spec.get("priorityClassName") or ""
+    if name:
+        if name not in classes:
+            raise ValueError(f"priorityClassName {name!r} not found")
+        return classes[name]
+    return default
+
+
+def _priority_classes(items: List[dict]) -> Tuple[Dict[str, int], int]:
+    classes, default = {}, 0
+    # the built-in classes the apiserver always has (scheduling/v1 SystemPriorityClasses)
+    classes["system-node-critical"] = 2000001000
+    classes["system-cluster-critical"] = 2000000000
+    for pc in items or []:
+        name = (pc.get("metadata") or {}).get("name", "")
+        classes[name] = int(pc.get("value") or 0)
+        if pc.get("globalDefault"):
+            default = int(pc.get("value") or 0)
+    return classes, default
+
+
+# ---- scheduler configuration ---------------------------------------------------------
+def _plugin_set(d: Optional[dict]) -> prof_mod.PluginSet:
+    d = d or {}
+    return prof_mod.PluginSet([prof_mod.Plugin(p["name"], int(p.get("weight") or 0)) for p in d.get("enabled") or []],
+                              [prof_mod.Plugin(p["name"]) for p in d.get("disabled") or []])
+
+
+_EXT_JSON = {"queueSort": "queueSort", "preFilter": "preFilter", "filter": "filter", "postFilter": "postFilter",
+             "preScore": "preScore", "score": "score", "reserve": "reserve", "permit": "permit",
+             "preBind": "preBind", "bind": "bind", "postBind": "postBind"}
+
+
+def profile_from_config(p: dict) -> prof_mod.SchedulerProfile:
+    """One v1beta2 KubeSchedulerProfile -> the converted SchedulerProfile."""
+    plugins = {}
+    for key, ext in _EXT_JSON.items():
+        if key in (p.get("plugins") or {}):
+            plugins[ext] = _plugin_set(p["plugins"][key])
+    sp = prof_mod.SchedulerProfile(plugins=prof_mod.convert_for_simulator(plugins))
+    # NewPluginConfig: user args override the defaults (Object over Raw: JSON carries the object)
+    for pc in p.get("pluginConfig") or []:
+        name, args = pc.get("name", ""), pc.get("args") or {}
+        if name == "NodeResourcesFit":
+            ss = args.get("scoringStrategy") or {}
+            if ss.get("type", "LeastAllocated") != "LeastAllocated":
+                raise ValueError(f"NodeResourcesFit scoringStrategy {ss.get('type')} not supported by the engine")
+            if ss.get("resources"):
+                sp.fit = prof_mod.FitArgs("LeastAllocated", [(r["name"], int(r.get("weight") or 1))
+                                                             for r in ss["resources"]])
+        elif name == "NodeResourcesBalancedAllocation":
+            if args.get("resources"):
+                sp.balanced = prof_mod.BalancedAllocationArgs([(r["name"], int(r.get("weight") or 1))
+                                                               for r in args["resources"]])
+        elif name == "InterPodAffinity":
+            if args.get("hardPodAffinityWeight") is not None:
+                sp.hard_pod_affinity_weight = int(args["hardPodAffinityWeight"])
+    sp.percentage_of_nodes_to_score = 0      # non-profile fields are reset to the defaults
+    return sp
+
+
+def profiles_from_config(cfg: Optional[dict]) -> List[Tuple[str, prof_mod.SchedulerProfile]]:
+    profiles = (cfg or {}).get("profiles") or [{"schedulerName": "default-scheduler"}]
+    return [(p.get("schedulerName") or "default-scheduler", profile_from_config(p)) for p in profiles]
+
+
+# ---- the document ----------------------------------------------------------------------
+def load(doc: dict) -> Snapshot:
+    """A ResourcesForImport / ResourcesForExport document (already JSON-decoded)."""
+    classes, default_prio = _priority_classes(doc.get("priorityClasses") or [])
+    namespaces = {}
+    for ns in doc.get("namespaces") or []:
+        md = ns.get("metadata") or {}
+        namespaces[md.get("name", "")] = dict(md.get("labels") or {})
+    nodes = [node_from_dict(n) for n in doc.get("nodes") or []]
+    names = {n.name for n in nodes}
+    if len(names) != len(nodes):
+        raise ValueError("duplicate node names")
+    bound, pending, unsupported = [], [], []
+    keyed = []
+    for idx, d in enumerate(doc.get("pods") or []):
+        pod = pod_from_dict(d)
+        spec = d.get("spec") or {}
+        pod.priority = _priority(spec, classes, default_prio)
+        namespaces.setdefault(pod.namespace, {})
+        if pod.node_name:
+            if pod.node_name in names:
+                bound.append(pod)
+            continue
+        if pod.has_volumes:
+            unsupported.append((pod.namespace, pod.name, "volumes"))
+            continue
+        ts = (d.get("metadata") or {}).get("creationTimestamp") or ""
+        keyed.append((-pod.priority, ts, idx, pod))
+    keyed.sort(key=lambda t: t[:3])           # PrioritySort, then queue arrival
+    pending = [t[3] for t in keyed]
+    return Snapshot(nodes, bound, pending, namespaces, profiles_from_config(doc.get("schedulerConfig")),
+                    unsupported,
+                    {k: len(doc.get(k) or []) for k in ("pods", "nodes", "pvs", "pvcs", "storageClasses",
+                                                         "priorityClasses", "namespaces")})
+
+
+def encode(snap: Snapshot, profile_index: int = 0):
+    """(EncodedCluster, EncodedPods of the pending queue, compiled profile)."""
+    from .encode import encode_cluster, encode_pods
+    cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces)
+    pods = encode_pods(cluster, snap.pending)
+    sp = snap.profiles[profile_index][1]
+    return cluster, pods, prof_mod.compile_profile(sp, cluster.scalar_names)

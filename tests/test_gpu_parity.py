@@ -331,3 +331,12 @@ def test_image_locality_vs_oracle(pct):
     for i in range(200):
         _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
     _batch_vs_oracle(cluster, enc, pct=pct)
+
+
+def test_ingested_template_cluster():
+    """The reference's import document + UI templates through ksim.ingest, on the device."""
+    import test_ingest
+    from ksim import ingest
+    snap = ingest.load(test_ingest._template_cluster(n_nodes=160, n_pods=2000))
+    cluster, enc, _ = ingest.encode(snap)
+    _batch_vs_oracle(cluster, enc, pct=0)

@@ -1,0 +1,109 @@
+"""Snapshot ingest: the reference's import/export documents
+and UI object templates (tests/golden/reference/, extracted by
+tools/make_ref_fixtures.py) -> engine inputs."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ksim import abi, ingest, profile
+from oracle.objref import ObjScheduler
+from oracle.oracle import Oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference")
+
+
+def _doc(name):
+    return json.load(open(os.path.join(GOLD, name)))
+
+
+def _same_profile(a, b):
+    for f in ("n_filter", "n_score", "fit_n_res", "ba_n_res", "hard_pod_affinity_weight", "percentage_of_nodes_to_score"):
+        assert getattr(a, f) == getattr(b, f), f
+    assert list(a.filter[:a.n_filter]) == list(b.filter[:b.n_filter])
+    assert list(a.score[:a.n_score]) == list(b.score[:b.n_score])
+    assert list(a.score_weight[:a.n_score]) == list(b.score_weight[:b.n_score])
+    assert list(a.fit_res[:a.fit_n_res]) == list(b.fit_res[:b.fit_n_res])
+    assert list(a.ba_res[:a.ba_n_res]) == list(b.ba_res[:b.ba_n_res])
+
+
+@pytest.mark.parametrize("name", ["export_case1.json", "export_case2.json", "import_case1.json"])
+def test_reference_documents_profiles(name):
+    """The exported default configuration converts to the default profile
+    (order, weights, args; percentageOfNodesToScore forced to 0)."""
+    snap = ingest.load(_doc(name))
+    assert [n for n, _ in snap.profiles] == ["default-scheduler"]
+    _same_profile(profile.compile_profile(snap.profiles[0][1]), profile.compile_profile(profile.SchedulerProfile()))
+    assert snap.counts["pvs"] == len(_doc(name)["pvs"])
+
+
+def test_priority_classes_and_queue_order():
+    doc = _doc("export_case2.json")
+    pc = _doc("template_priorityclass.json")
+    pc = dict(pc, metadata={"name": "tmpl"})                 # globalDefault, value 1000
+    doc["priorityClasses"] = doc["priorityClasses"] + [pc]
+    tmpl = _doc("template_pod.json")
+    pods = []
+    for i, (prio_kw, ts) in enumerate([({}, "2022-01-01T00:00:03Z"), ({"priorityClassName": "system-node-critical"},
+                                       "2022-01-01T00:00:05Z"), ({"priority": 5}, "2022-01-01T00:00:01Z"),
+                                      ({}, "2022-01-01T00:00:02Z")]):
+        p = copy.deepcopy(tmpl)
+        p["metadata"] = {"name": f"p{i}", "namespace": "default", "creationTimestamp": ts}
+        p["spec"].update(prio_kw)
+        pods.append(p)
+    doc["pods"] = pods
+    snap = ingest.load(doc)
+    assert [p.name for p in snap.pending] == ["p1", "p3", "p0", "p2"]
+    assert [p.priority for p in snap.pending] == [2000001000, 1000, 1000, 5]
+
+
+def _template_cluster(n_nodes=40, n_pods=300, bound_every=4):
+    node_t, pod_t = _doc("template_node.json"), _doc("template_pod.json")
+    nodes, pods = [], []
+    for i in range(n_nodes):
+        n = copy.deepcopy(node_t)
+        n["metadata"] = {"name": f"node-{i}", "labels": {"kubernetes.io/hostname": f"node-{i}",
+                                                         "topology.kubernetes.io/zone": f"z{i % 3}"}}
+        n["status"]["allocatable"]["cpu"] = str(4 * (1 + i % 4))
+        nodes.append(n)
+    for i in range(n_pods):
+        p = copy.deepcopy(pod_t)
+        p["metadata"] = {"name": f"pod-{i}", "namespace": "default", "labels": {"app": f"a{i % 5}"},
+                         "creationTimestamp": "2022-01-01T00:00:00Z"}
+        req = p["spec"]["containers"][0]["resources"]["requests"]
+        req["cpu"] = f"{100 * (1 + i % 10)}m"
+        req["memory"] = f"{1 + i % 8}Gi"
+        if i % bound_every == 0 and i < n_pods // 2:
+            p["spec"]["nodeName"] = f"node-{(7 * i) % n_nodes}"
+        pods.append(p)
+    vol = copy.deepcopy(pod_t)
+    vol["metadata"] = {"name": "with-pvc", "namespace": "default"}
+    vol["spec"]["volumes"] = [{"name": "v", "persistentVolumeClaim": {"claimName": "pvc1"}}]
+    pods.append(vol)
+    doc = _doc("import_case1.json")
+    doc["nodes"], doc["pods"] = nodes, pods
+    return doc
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_template_cluster_schedules_like_objref(pct):
+    """UI templates (node.yaml / pod.yaml) -> ingest -> C oracle placements
+    equal the object-level restatement on the same objects; bound pods fill
+    their nodes; pods with PVC volumes are reported, not scheduled."""
+    snap = ingest.load(_template_cluster())
+    assert snap.unsupported == [("default", "with-pvc", "volumes")]
+    assert len(snap.bound) == 38 and len(snap.pending) == 300 - 38
+    cluster, enc, prof = ingest.encode(snap)
+    assert cluster.alloc_cpu.sum() == sum(4000 * (1 + i % 4) for i in range(40))
+    assert cluster.req_mem.sum() == sum((1 + i % 8) << 30 for i in range(0, 150, 4))
+    sp = copy.deepcopy(snap.profiles[0][1])
+    sp.percentage_of_nodes_to_score = pct
+    prof = profile.compile_profile(sp, cluster.scalar_names)
+    ochosen, _ = Oracle(cluster, prof).schedule(enc)
+    ref = ObjScheduler(snap.nodes, snap.bound, namespaces=snap.namespaces, pct=pct, seed=sp.tiebreak_seed)
+    names = cluster.node_names
+    for i, pod in enumerate(snap.pending):
+        got = ref.cycle(pod)["chosen"]
+        assert (names[ochosen[i]] if ochosen[i] >= 0 else None) == got, f"pod {i}"

@@ -33,6 +33,11 @@
 
 namespace ksim {
 
+// FAST: every pod of the run is trivial (host-proven static filters) and the
+// scoring strategies are {cpu, memory}: the loop reads the resource columns
+// and runs the cpu/memory key only (no static-filter or generic code, which
+// keeps the kernel small and its registers few).
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
                                                     const DevState* __restrict__ st, uint64_t* __restrict__ cand,
                                                     int32_t n_tiles) {
@@ -50,8 +55,8 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
   const int64_t seq = st->pod_seq + j;
   // The lane's kNodesPerLane keys, kept sorted (descending) by insertion; the
   // node loop is not unrolled so the kernel stays small (instruction cache).
-  uint64_t a[kNodesPerLane] = {0, 0, 0, 0};
-  static_assert(kNodesPerLane == 4 && kTileCand == 4, "insertion below is for 4 keys");
+  uint64_t a[kTileCand] = {0, 0, 0, 0};
+  static_assert(kTileCand == 4, "insertion below is for 4 keys");
 #pragma unroll 1
   for (int k = 0; k < kNodesPerLane; k++) {
     const int32_t node = tile * kTileNodes + k * 64 + lane;
@@ -59,8 +64,12 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksi
     if (node < c.n) {
       // trivial: the static filters pass everywhere and the pod requests no
       // scalar resources, so only the resource columns are read
-      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
+      if constexpr (FAST) {
+        kk = dyn_key_cpu_mem(prof, bp, p, nc, load_res_row(c, node), seq, c.base);
+      } else {
+        const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
+      }
     }
     a[3] = umax64(a[3], kk);
     cswap_desc(a[2], a[3]);
@@ -351,7 +360,10 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
   const dim3 g1((n_tiles + 3) / 4, kBatchPods);
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_batch_eval<<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  if (a.fast)
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  else
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
   if (evs) (void)hipEventRecord(evs[1], stream);
   const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
@@ -377,7 +389,10 @@ void launch_chain(const LaunchArgs& a, hipStream_t stream) {
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
   const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
   const dim3 g1((n_tiles + 3) / 4, kBatchPods);
-  k_batch_eval<<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  if (a.fast)
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  else
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
   const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
                                                                a.s.topk_complete, a.s.xsend);

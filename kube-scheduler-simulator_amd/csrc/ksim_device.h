@@ -267,6 +267,17 @@ __device__ __forceinline__ int64_t div_floor_nonneg(int64_t a, int64_t b) {
   return q;
 }
 
+// floor(a / b) for 0 <= a <= 100 * b, b > 0 (a score-sized quotient): an f32
+// reciprocal estimate is within 100 * 2^-20 of a / b, so its truncation is
+// off by at most one, which one exact integer remainder test repairs.
+__device__ __forceinline__ int64_t div_q100(int64_t a, int64_t b) {
+  int32_t q = (int32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
+  const int64_t rem = a - (int64_t)q * b;
+  q -= rem < 0;
+  q += rem >= b;
+  return q;
+}
+
 // Bit `id` of a KSIM_TAINT_WORDS-word set.  The word is picked with selects,
 // never a runtime array index, so a pod record copied into registers stays in
 // registers (a dynamic index would move it to scratch memory).
@@ -421,6 +432,13 @@ __device__ __forceinline__ int64_t least_requested_score(int64_t requested, int6
   if (requested > capacity) return 0;
   if (capacity < 0 || requested > capacity) return ((capacity - requested) * kMaxNodeScore) / capacity;
   return div_floor_nonneg((capacity - requested) * kMaxNodeScore, capacity);
+}
+
+// leastRequestedScore for capacity > 0 (the quotient is in [0, 100]).
+__device__ __forceinline__ int64_t least_requested_q100(int64_t requested, int64_t capacity) {
+  if (capacity < 0) return least_requested_score(requested, capacity);
+  if (requested > capacity) return 0;
+  return div_q100((capacity - requested) * kMaxNodeScore, capacity);
 }
 
 __device__ __forceinline__ int64_t fit_least_allocated_score(const NodeRow& r, const ksim_profile& prof, const ksim_pod& p,
@@ -864,14 +882,15 @@ __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, co
   if (bp.w_fit) {                              // leastResourceScorer over {cpu, memory}
     int64_t ns = 0, ws = 0;
     if (r.alloc_cpu != 0) {
-      ns += least_requested_score(r.nz_cpu + p.nz_cpu, r.alloc_cpu) * bp.fit_w_cpu;
+      ns += least_requested_q100(r.nz_cpu + p.nz_cpu, r.alloc_cpu) * bp.fit_w_cpu;
       ws += bp.fit_w_cpu;
     }
     if (r.alloc_mem != 0) {
-      ns += least_requested_score(r.nz_mem + p.nz_mem, r.alloc_mem) * bp.fit_w_mem;
+      ns += least_requested_q100(r.nz_mem + p.nz_mem, r.alloc_mem) * bp.fit_w_mem;
       ws += bp.fit_w_mem;
     }
-    const int64_t la = ws == 0 ? 0 : (ns < 0 || ws < 0) ? ns / ws : div_floor_nonneg(ns, ws);
+    // the weighted mean of scores in [0, 100] is a score-sized quotient
+    const int64_t la = ws == 0 ? 0 : (ns < 0 || ws < 0) ? ns / ws : div_q100(ns, ws);
     tot += bp.w_fit * la;
   }
   if (bp.w_ba) {                               // balancedResourceScorer over {cpu, memory}

@@ -103,6 +103,7 @@ struct ksim_handle {
   std::vector<DevBuf> pod_bufs;
   std::vector<uint8_t> batchable;       // per loaded pod
   std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
+  std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
@@ -117,6 +118,7 @@ struct ksim_handle {
   hipGraphExec_t graph_cycle = nullptr;        // per-pod cycles, pods without topology uses
   hipGraphExec_t graph_cycle_topo = nullptr;   // per-pod cycles incl. the topology kernels
   hipGraphExec_t graph_batch = nullptr;
+  hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
 };
 
 namespace {
@@ -164,6 +166,8 @@ void drop_graphs(ksim_handle* h) {
   if (h->graph_cycle) (void)hipGraphExecDestroy(h->graph_cycle);
   if (h->graph_cycle_topo) (void)hipGraphExecDestroy(h->graph_cycle_topo);
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
+  if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
+  h->graph_batch_fast = nullptr;
   h->graph_cycle = nullptr;
   h->graph_cycle_topo = nullptr;
   h->graph_batch = nullptr;
@@ -245,6 +249,13 @@ bool static_trivial(const ksim_handle* h, const ksim_pod& p) {
 
 bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
 
+bool run_fast(const ksim_handle* h, int32_t a, int32_t b) {
+  if (!h->bp.cpu_mem) return false;
+  for (int32_t i = a; i < b; i++)
+    if (!h->trivial[i]) return false;
+  return true;
+}
+
 // ADAPT: the profile keeps fewer than all nodes (K < N over the whole cluster).
 bool adapt_mode(const ksim_handle* h) {
   return num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->dc.n_total) < h->dc.n_total;
@@ -314,9 +325,10 @@ int read_state(ksim_handle* h, DevState& st) {
   return KSIM_OK;
 }
 
-int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out) {
+int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
+  a.fast = fast;
   hipGraph_t g = nullptr;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   if (batch)
@@ -336,6 +348,7 @@ int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out) {
   return KSIM_OK;
 }
 
+
 // Run pods [a, b) on one path (all of them share the path).
 int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   int rc;
@@ -353,7 +366,10 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
     HIPCHK(h, hipGetLastError());
     return KSIM_OK;
   }
-  if (!h->graph_batch && (rc = capture(h, true, false, &h->graph_batch))) return rc;
+  // the FAST evaluation kernel when every pod of the run is trivial with cpu/memory scoring
+  la.fast = run_fast(h, a, b);
+  hipGraphExec_t& gb = la.fast ? h->graph_batch_fast : h->graph_batch;
+  if (!gb && (rc = capture(h, true, false, &gb, la.fast))) return rc;
   // every batch commits between 1 and kBatchPods pods: a graph of
   // kGraphBatches batches never overshoots while left >= kBatchPods * kGraphBatches,
   // and ceil(left / kBatchPods) single batches never overshoot either
@@ -362,7 +378,7 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
     const int32_t left = b - cursor;
     if (left >= kBatchPods * kGraphBatches) {
       const int reps = left / (kBatchPods * kGraphBatches);
-      for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(h->graph_batch, h->stream));
+      for (int r = 0; r < reps; r++) HIPCHK(h, hipGraphLaunch(gb, h->stream));
     } else {
       const int n1 = (left + kBatchPods - 1) / kBatchPods;
       for (int r = 0; r < n1; r++) {
@@ -407,11 +423,15 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
 // keys.  `hs` is either {this rank's handle} with an RCCL communicator (one
 // process per GPU) or an in-process group of shard handles on one device
 // (exchanges by device copies).  Everything runs on `stream`, asynchronously.
-int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fast) {
   const int R = (int)hs.size();
   ksim_handle* h0 = hs[0];
   const size_t rec = (size_t)kBatchPods * kXRec;            // u64 per shard
-  for (auto* h : hs) launch_shard_eval(make_args(h, h->dp, h->d_chosen), stream);
+  for (auto* h : hs) {
+    LaunchArgs la = make_args(h, h->dp, h->d_chosen);
+    la.fast = fast;
+    launch_shard_eval(la, stream);
+  }
   if (h0->comm) {
     const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
     if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
@@ -443,6 +463,7 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
 int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   ksim_handle* h0 = hs[0];
   hipStream_t stream = h0->stream;
+  const bool fast = run_fast(h0, a, b);
   for (auto* h : hs) {
     int rc;
     if ((rc = set_run(h, a, b))) return rc;
@@ -452,7 +473,7 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   while (cursor < b) {
     const int32_t n = std::max(1, (b - cursor) / kBatchPods);
     for (int32_t i = 0; i < n; i++) {
-      int rc = shard_batch(hs, stream);
+      int rc = shard_batch(hs, stream, fast);
       if (rc) return rc;
     }
     DevState st;
@@ -1016,6 +1037,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->batchable.assign((size_t)ps->n_pods, 0);
   h->topo.assign((size_t)ps->n_pods, 0);
   h->xdom_len.assign((size_t)ps->n_pods, 0);
+  h->trivial.assign((size_t)ps->n_pods, 0);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
@@ -1031,6 +1053,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     }
     h->xreg_len[i] = soft ? xr : 0;
     bf[i] = static_trivial(h, ps->pods[i]) ? kBatchStaticTrivial : 0;
+    h->trivial[i] = bf[i] ? 1 : 0;
   }
   DevPods P{};
   void* p = nullptr;

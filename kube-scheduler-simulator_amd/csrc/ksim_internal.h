@@ -32,6 +32,7 @@ struct LaunchArgs {
   DevScratch s;
   DevEvalOut o;
   int32_t* chosen;   // [n_pods] device, may be null
+  bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
 };
 
 constexpr int kKernelsPerCycle = 7;

@@ -280,19 +280,16 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
 }
 
 // Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
-// bound there; M_j = the block max.  Unsharded, the last block to finish
-// validates the chain against M and commits the batch; sharded (SHARDED),
-// each shard scores the guesses it owns and M is all-reduced (max) before
-// k_batch_commit.
-template <bool SHARDED>
+// bound there; M_j = the block max.  Sharded, each shard scores the guesses
+// it owns and M is all-reduced (max) before k_batch_commit.  FAST: as in
+// k_batch_eval (trivial pods, cpu/memory scoring).
+template <bool FAST>
 __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
-                                                            DevState* __restrict__ st,
+                                                            const DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ gkey,
                                                             const int32_t* __restrict__ chain_end,
-                                                            uint64_t* __restrict__ pmax, uint32_t* __restrict__ done,
-                                                            int32_t* __restrict__ chosen_out) {
+                                                            uint64_t* __restrict__ pmax) {
   __shared__ uint64_t s_wmax[kBatchPods / 64];
-  __shared__ int32_t s_last, s_istar, s_sched, s_unsched;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
@@ -300,39 +297,36 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
   const int32_t nchain = *chain_end;
   const int64_t seq0 = st->pod_seq;
   const int j = blockIdx.x, k = tid;
+  if (j >= nchain) {                                 // block-uniform
+    if (tid == 0) pmax[j] = 0;
+    return;
+  }
   uint64_t v = 0;
-  if (j < nchain && k < j) {
+  if (k < j) {
     const uint64_t gk = gkey[k];
     const int32_t local = gk ? key_node(gk) - c.base : -1;
     if (local >= 0 && local < c.n) {
-      NodeRow r = load_row(c, local);
-      row_add_pod(r, P.pods[base + k], 1);
       const ksim_pod& p = P.pods[base + j];
-      if ((P.bflags[base + j] & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r))
-        v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j, c.base);
+      if constexpr (FAST) {
+        NodeRow r = load_res_row(c, local);
+        row_add_pod(r, P.pods[base + k], 1);
+        v = dyn_key_cpu_mem(prof, bp, p, P.norm_const[base + j], r, seq0 + j, c.base);
+      } else {
+        NodeRow r = load_row(c, local);
+        row_add_pod(r, P.pods[base + k], 1);
+        if ((P.bflags[base + j] & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r))
+          v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j, c.base);
+      }
     }
   }
-  if (j < nchain && __syncthreads_or(k < j)) {
-    v = wave_max_u64_dpp(v);
-    if (lane == 0) s_wmax[wave] = v;
-    __syncthreads();
-    if (tid == 0) {
-      uint64_t m = 0;
-      for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
-      pmax[j] = m;
-    }
-  } else if (tid == 0) {
-    pmax[j] = 0;
-  }
-  if (SHARDED) return;
-  // last block: validate and commit
-  __threadfence();
-  if (tid == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  v = wave_max_u64_dpp(v);
+  if (lane == 0) s_wmax[wave] = v;
   __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  if (tid == 0) *done = 0;                              // re-arm for the next batch
-  batch_commit(c, P, st, gkey, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched);
+  if (tid == 0) {
+    uint64_t m = 0;
+    for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
+    pmax[j] = m;
+  }
 }
 
 __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
@@ -374,8 +368,12 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[3], stream);
   // pair keys, then a separate one-block commit: cheaper than every block of
   // the pairs kernel fencing for a last-block election
-  k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
-                                                             a.s.pmax, a.s.done, a.chosen);
+  if (a.fast)
+    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+                                                               a.s.pmax);
+  else
+    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey,
+                                                                a.s.chain_end, a.s.pmax);
   if (evs) (void)hipEventRecord(evs[4], stream);
   k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
   if (evs) (void)hipEventRecord(evs[5], stream);
@@ -403,8 +401,12 @@ void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) 
                                                      a.s.topk_complete);
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
-  k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
-                                                             a.s.pmax, a.s.done, a.chosen);
+  if (a.fast)
+    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+                                                               a.s.pmax);
+  else
+    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey,
+                                                                a.s.chain_end, a.s.pmax);
 }
 
 void launch_shard_commit(const LaunchArgs& a, hipStream_t stream) {

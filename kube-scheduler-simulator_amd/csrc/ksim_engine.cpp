@@ -442,7 +442,11 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
                                   hipMemcpyDeviceToDevice, stream));
   }
   const int32_t world = h0->comm ? h0->world : R;
-  for (auto* h : hs) launch_shard_chain(make_args(h, h->dp, h->d_chosen), world, stream);
+  for (auto* h : hs) {
+    LaunchArgs la = make_args(h, h->dp, h->d_chosen);
+    la.fast = fast;
+    launch_shard_chain(la, world, stream);
+  }
   if (h0->comm) {
     const ncclResult_t r =
         rccl().all_reduce(h0->sc.pmax, h0->sc.pmax, kBatchPods, ncclUint64, ncclMax, h0->comm, stream);

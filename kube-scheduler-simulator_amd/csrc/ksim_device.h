@@ -106,6 +106,7 @@ constexpr int kExtCut = 2 * KSIM_MAX_SCORE;
 constexpr int kExtWords = kExtCut + 1;
 struct WinState {
   int32_t cut, kend, nf, evaluated, k, has_soft;
+  int32_t nfeas, nign;                   // no-window cycles (K = N): counted by k_filter_score
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
   uint64_t best;                         // TB argmax key
@@ -120,6 +121,7 @@ struct DevScratch {
   int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
   int32_t* aexact;       // ADAPT batch: pods whose windows are exact
   int32_t* abroken;      // ADAPT batch: a bound node flipped feasibility inside the pod's window
+  uint32_t* regbm;       // no-window cycles: PTS pair registration bitmaps [KSIM_MAX_USES][(vmax + 31) / 32]
   int64_t* xdom;         // sharded cycle: packed domain sums (all-reduced, sum)
   int64_t* xreg;         // sharded cycle: IgnoredNodes count + per-value registrations (all-reduced, sum)
   uint32_t* detail;      // [n]

@@ -104,6 +104,7 @@ struct ksim_handle {
   std::vector<uint8_t> batchable;       // per loaded pod
   std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
+  std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
@@ -117,6 +118,7 @@ struct ksim_handle {
 
   hipGraphExec_t graph_cycle = nullptr;        // per-pod cycles, pods without topology uses
   hipGraphExec_t graph_cycle_topo = nullptr;   // per-pod cycles incl. the topology kernels
+  hipGraphExec_t graph_cycle_topo_fused = nullptr;   // ... with the critical paths in the filter pass
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
 };
@@ -165,6 +167,8 @@ int upload(ksim_handle* h, std::vector<DevBuf>& owner, const void* src, size_t b
 void drop_graphs(ksim_handle* h) {
   if (h->graph_cycle) (void)hipGraphExecDestroy(h->graph_cycle);
   if (h->graph_cycle_topo) (void)hipGraphExecDestroy(h->graph_cycle_topo);
+  if (h->graph_cycle_topo_fused) (void)hipGraphExecDestroy(h->graph_cycle_topo_fused);
+  h->graph_cycle_topo_fused = nullptr;
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   h->graph_batch_fast = nullptr;
@@ -316,6 +320,9 @@ int set_run(ksim_handle* h, int32_t first, int32_t end) {
   h->run_hdr[0] = first;
   h->run_hdr[1] = end;
   HIPCHK(h, hipMemcpyAsync(h->st, h->run_hdr, sizeof(h->run_hdr), hipMemcpyHostToDevice, h->stream));
+  // per-cycle selection state starts from zero (the no-window cycle keeps it
+  // zero between its own cycles; other paths leave extrema behind)
+  HIPCHK(h, hipMemsetAsync(h->sc.win, 0, sizeof(WinState), h->stream));
   return KSIM_OK;
 }
 
@@ -325,10 +332,11 @@ int read_state(ksim_handle* h, DevState& st) {
   return KSIM_OK;
 }
 
-int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false) {
+int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false, bool fuse_min = false) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = fast;
+  a.fuse_min = fuse_min;
   hipGraph_t g = nullptr;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   if (batch)
@@ -358,8 +366,10 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   // then single launches for the remainder.
   LaunchArgs la = make_args(h, h->dp, h->d_chosen);
   if (!batch) {
-    hipGraphExec_t& g = topo ? h->graph_cycle_topo : h->graph_cycle;
-    if (!g && (rc = capture(h, false, topo, &g))) return rc;
+    la.fuse_min = topo;
+    for (int32_t i = a; i < b && la.fuse_min; i++) la.fuse_min = h->hard_small[i] != 0;
+    hipGraphExec_t& g = !topo ? h->graph_cycle : la.fuse_min ? h->graph_cycle_topo_fused : h->graph_cycle_topo;
+    if (!g && (rc = capture(h, false, topo, &g, false, la.fuse_min))) return rc;
     int32_t done = a;
     for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(g, h->stream));
     for (; done < b; done++) launch_cycle(la, h->stream, false, topo);
@@ -819,6 +829,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.fail, uint8_t*, N);
   SCR(s.ign, uint8_t*, N);
   SCR(s.win, WinState*, sizeof(WinState));
+  SCR(s.regbm, uint32_t*, 4 * (size_t)KSIM_MAX_USES * ((vmax + 31) / 32));
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
@@ -1042,6 +1053,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->topo.assign((size_t)ps->n_pods, 0);
   h->xdom_len.assign((size_t)ps->n_pods, 0);
   h->trivial.assign((size_t)ps->n_pods, 0);
+  h->hard_small.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
@@ -1052,6 +1064,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     for (int32_t k = 0; k < ps->pods[i].use_count; k++) {
       const ksim_topo_use& u = ps->uses[ps->pods[i].use_first + k];
       if (use_needs_dom(u)) h->xdom_len[i] += h->col_nvals[u.col];
+      if (u.kind == KSIM_USE_PTS_HARD && u.col != KSIM_COL_NONE && h->col_nvals[u.col] > kFuseMinValues) h->hard_small[i] = 0;
       if (use_registers_values(u)) xr += h->col_nvals[u.col];
       soft = soft || u.kind == KSIM_USE_PTS_SOFT;
     }

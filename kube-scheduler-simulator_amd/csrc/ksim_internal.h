@@ -33,9 +33,11 @@ struct LaunchArgs {
   DevEvalOut o;
   int32_t* chosen;   // [n_pods] device, may be null
   bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
+  bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
 };
 
 constexpr int kKernelsPerCycle = 7;
+constexpr int kFuseMinValues = 256;   // k_filter_score computes the PTS critical paths itself up to this many values
 extern const char* const kKernelNames[kKernelsPerCycle];
 constexpr int kKernelsPerBatch = 5;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];

@@ -298,36 +298,95 @@ __global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_
   }
 }
 
-template <bool COMPAT>
+// NOWIN (K = N: every feasible node is kept, no cut): the filter pass also
+// counts the feasible nodes and does PodTopologySpread's PreScore pair
+// registration and IgnoredNodes count (wave-aggregated atomics), so the cycle
+// needs no k_window.
+// fuse_min: every hard spread constraint of the run keys a column of at most
+// kFuseMinValues values, so each block derives the critical paths itself
+// (k_topo_min's work, a few LDS reductions) instead of a separate launch.
+
+template <bool COMPAT, bool NOWIN>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, ksim_profile prof,
-                                                      const DevState* __restrict__ st, DevScratch s) {
+                                                      const DevState* __restrict__ st, DevScratch s,
+                                                      int32_t fuse_min) {
+  __shared__ int64_t s_min[KSIM_MAX_USES];
+  __shared__ int64_t sh64[4];
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
-  if (node >= c.n) return;
   const ksim_pod& p = P.pods[pi];
-  const uint32_t tf = p.use_count ? st->topo_flags : 0u;
-  const NodeRow r = load_row(c, node);
-  uint32_t det;
-  const uint8_t res = run_filter_plugins(c, P, prof, s, tf, p, r, det);
-  s.fail[node] = res;
-  if (COMPAT) s.detail[node] = det;
-  if (res != KSIM_PASSED) return;
-  // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
-  s.ign[node] = p.use_count && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
-  int64_t part = 0;
-  for (int k = 0; k < prof.n_score; k++) {
-    const int pl = prof.score[k];
-    const int64_t v = score_plugin_raw(c, P, prof, s, p, pl, r);
-    if (norm_kind(pl) == kNormNone) {
-      const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
-      part += v * w;
-      if (COMPAT) s.raw[(size_t)k * c.n + node] = v;
-    } else {
-      s.raw[(size_t)k * c.n + node] = v;
+  if (fuse_min && p.use_count) {                 // block-uniform
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (u.kind != KSIM_USE_PTS_HARD) continue;
+      int64_t mn = 2147483647;
+      if (u.col != KSIM_COL_NONE) {
+        const int32_t V = c.col_nvals[u.col];
+        const int64_t* d = s.dom + (size_t)i * c.vmax;
+        for (int32_t v = threadIdx.x; v < V; v += blockDim.x) {
+          const int64_t x = d[v];
+          if ((x >> kDomMarkShift) != 0) mn = min(mn, x & kDomCountMask);
+        }
+      }
+      mn = block_min_i64_nw<4>(mn, sh64);
+      if (threadIdx.x == 0) s_min[i] = mn;
+    }
+    __syncthreads();
+    s.min_match = s_min;                          // pts_filter reads the block's copy
+  }
+  bool feasible = false, ign = false;
+  if (node < c.n) {
+    const uint32_t tf = p.use_count ? st->topo_flags : 0u;
+    const NodeRow r = load_row(c, node);
+    uint32_t det;
+    const uint8_t res = run_filter_plugins(c, P, prof, s, tf, p, r, det);
+    s.fail[node] = res;
+    if (COMPAT) s.detail[node] = det;
+    feasible = res == KSIM_PASSED;
+    if (feasible) {
+      // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
+      ign = p.use_count && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
+      s.ign[node] = ign;
+      int64_t part = 0;
+      for (int k = 0; k < prof.n_score; k++) {
+        const int pl = prof.score[k];
+        const int64_t v = score_plugin_raw(c, P, prof, s, p, pl, r);
+        if (norm_kind(pl) == kNormNone) {
+          const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
+          part += v * w;
+          if (COMPAT) s.raw[(size_t)k * c.n + node] = v;
+        } else {
+          s.raw[(size_t)k * c.n + node] = v;
+        }
+      }
+      s.part[node] = part;
     }
   }
-  s.part[node] = part;
+  if (NOWIN) {
+    const int lane = threadIdx.x & 63;
+    WinState* win = s.win;
+    const uint64_t fm = __ballot(feasible), im = __ballot(feasible && ign);
+    if (lane == 0 && fm) atomicAdd(&win->nfeas, (int32_t)__popcll(fm));
+    if (lane == 0 && im) atomicAdd(&win->nign, (int32_t)__popcll(im));
+    const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+    for (int i = 0; i < p.use_count; i++) {
+      const ksim_topo_use u = P.uses[p.use_first + i];
+      if (!use_registers_values(u)) continue;
+      const bool reg = feasible && !ign;
+      const uint32_t v = reg ? use_value(c, u, node) : 0u;
+      uint32_t* bm = s.regbm + (size_t)i * vwords;
+      if (c.col_nvals[u.col] <= 64) {            // few values: OR the wave's values first
+        uint64_t bits = reg ? 1ull << v : 0ull;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) bits |= __shfl_xor(bits, d, 64);
+        if (lane == 0 && (uint32_t)bits) atomicOr(&bm[0], (uint32_t)bits);
+        if (lane == 0 && (uint32_t)(bits >> 32)) atomicOr(&bm[1], (uint32_t)(bits >> 32));
+      } else if (reg) {
+        atomicOr(&bm[v >> 5], 1u << (v & 31));
+      }
+    }
+  }
 }
 
 constexpr int kBmWords = (KSIM_MAX_NODES + 1 + 31) / 32;   // value-id bitmap (PTS pair registration)
@@ -459,27 +518,70 @@ __device__ __forceinline__ bool kept_node(const DevCluster& c, const DevScratch&
   return rot_pos(c.base + node, start, c.n_total) < kend && s.fail[node] == KSIM_PASSED;
 }
 
+// NOWIN: the window state is derived here from k_filter_score's counters and
+// registration bitmaps (every block alike; block 0 publishes it for k_select
+// and k_bind).
+template <bool NOWIN>
 __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_profile prof,
                                                  const DevState* __restrict__ st, DevScratch s) {
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
   __shared__ ksim_topo_use s_use[KSIM_MAX_USES];
   __shared__ double s_w[KSIM_MAX_USES];
+  __shared__ int32_t sh32[4];
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
-  if (win->nf <= 1) return;                       // no scoring
   const ksim_pod& p = P.pods[pi];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nu = p.use_count;
-  const bool has_soft = win->has_soft != 0;
-  if (tid < nu) {
-    s_use[tid] = P.uses[p.use_first + tid];
-    s_w[tid] = win->w[tid];
+  bool has_soft;
+  if (NOWIN) {
+    const int32_t nf = win->nfeas;
+    bool any_soft = false;
+    for (int i = 0; i < nu; i++) any_soft = any_soft || P.uses[p.use_first + i].kind == KSIM_USE_PTS_SOFT;
+    has_soft = nf > 1 && any_soft;
+    if (tid < nu) s_use[tid] = P.uses[p.use_first + tid];
+    if (has_soft) {
+      const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+      const int32_t nign = win->nign;
+      for (int i = 0; i < nu; i++) {
+        const ksim_topo_use u = P.uses[p.use_first + i];
+        if (u.kind != KSIM_USE_PTS_SOFT) continue;
+        int32_t size = 0;
+        if (u.flags & KSIM_USEF_HOSTNAME) {
+          size = nf - nign;
+        } else if (u.col != KSIM_COL_NONE) {
+          const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
+          int32_t bits = 0;
+          for (int x = tid; x < words; x += blockDim.x) bits += __popc(s.regbm[(size_t)i * vwords + x]);
+          size = block_sum_i32_nw<4>(bits, sh32);
+        }
+        if (tid == 0) s_w[i] = c.topo_log[size];
+      }
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+      win->nf = nf;
+      win->kend = c.n;
+      win->cut = c.n;
+      win->evaluated = c.n;
+      win->k = c.n;
+      win->has_soft = has_soft;
+      for (int i = 0; i < nu; i++) win->w[i] = s_w[i];
+    }
+    __syncthreads();
+    if (nf <= 1) return;                          // no scoring
+  } else {
+    if (win->nf <= 1) return;                     // no scoring
+    has_soft = win->has_soft != 0;
+    if (tid < nu) {
+      s_use[tid] = P.uses[p.use_first + tid];
+      s_w[tid] = win->w[tid];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
-  const bool kept = node < N && kept_node(c, s, node, st->next_start, win->kend);
+  const bool kept = node < N && kept_node(c, s, node, st->next_start, NOWIN ? N : win->kend);
   const int S = prof.n_score;
 #pragma unroll
   for (int k = 0; k < KSIM_MAX_SCORE; k++) {
@@ -604,11 +706,26 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_pr
   }
 }
 
+// NOWIN also returns the counters, registration bitmaps and extrema slots to
+// zero for the next cycle (k_window resets its own otherwise).
+template <bool NOWIN>
 __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
                                              int32_t* __restrict__ chosen_out) {
   const int32_t pi = st->cursor;
-  if (pi >= st->end || threadIdx.x != 0) return;
-  const WinState* win = s.win;
+  if (pi >= st->end) return;
+  WinState* win = s.win;
+  if (NOWIN) {
+    const ksim_pod& pp = P.pods[pi];
+    const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+    for (int i = 0; i < pp.use_count; i++) {
+      const ksim_topo_use u = P.uses[pp.use_first + i];
+      if (!use_registers_values(u)) continue;
+      const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
+      for (int x = threadIdx.x; x < words; x += blockDim.x) s.regbm[(size_t)i * vwords + x] = 0;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const int32_t N = c.n, nf = win->nf, cut = win->cut;
   const int32_t chosen = win->best ? key_node(win->best) : -1;   // unsharded: base == 0
   const ksim_pod& p = P.pods[pi];
@@ -632,6 +749,12 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   st->next_start_after = ns;
   st->pod_seq += 1;
   st->topo_flags = 0;
+  if (NOWIN) {
+    win->nfeas = 0;
+    win->nign = 0;
+    for (int t = 0; t < kExtWords; t++) win->ext[t] = 0;
+    win->best = 0;
+  }
   st->cursor = pi + 1;
 }
 
@@ -912,32 +1035,37 @@ __global__ __launch_bounds__(256) void k_group_gather(GroupPtrs src, GroupPtrs d
 const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_min", "k_filter_score",
                                                     "k_window", "k_extrema", "k_select", "k_bind"};
 
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
+template <bool COMPAT, bool NOWIN>
+void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent_t* evs) {
   const int blocks = (a.c.n + 255) / 256;
   if (evs) (void)hipEventRecord(evs[0], stream);
   if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (topo && !a.fuse_min) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  if (compat)
-    k_filter_score<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  else
-    k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, topo && a.fuse_min);
   if (evs) (void)hipEventRecord(evs[3], stream);
-  if (compat)
-    k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  else
-    k_window<false><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (!NOWIN) k_window<COMPAT><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_extrema<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_extrema<NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[5], stream);
-  if (compat)
-    k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
-  else
-    k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
   if (evs) (void)hipEventRecord(evs[6], stream);
-  k_bind<<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+  k_bind<NOWIN><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
   if (evs) (void)hipEventRecord(evs[7], stream);
+}
+
+// K = N (percentageOfNodesToScore >= 100 or fewer than 100 nodes): no
+// window, so the window state comes from the filter pass (no k_window).
+void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
+  const bool nowin = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n) >= a.c.n;
+  if (compat) {
+    if (nowin) launch_cycle_t<true, true>(a, stream, topo, evs);
+    else launch_cycle_t<true, false>(a, stream, topo, evs);
+  } else {
+    if (nowin) launch_cycle_t<false, true>(a, stream, topo, evs);
+    else launch_cycle_t<false, false>(a, stream, topo, evs);
+  }
 }
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
@@ -953,7 +1081,7 @@ void launch_pshard_topo(const LaunchArgs& a, hipStream_t stream) {
 void launch_pshard_filter(const LaunchArgs& a, bool topo, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   if (topo) k_topo_min<true><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_filter_score<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
   k_wcount_sh<<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.st, a.s);
 }
 
@@ -964,7 +1092,7 @@ void launch_pshard_window(const LaunchArgs& a, int32_t rank, int32_t world, hipS
 void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   if (soft) k_wfinal_sh<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s);
-  k_extrema<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
 }
 
 void launch_pshard_select(const LaunchArgs& a, hipStream_t stream) {

@@ -145,10 +145,11 @@ __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict_
 }
 
 // Sharded: merge the R shard records of pod j (all-gathered, [R][B][kXRec])
-// into the pod's global top-T.  Lane l holds entry l % T of shard l / T.  A key
-// is provably in the global order if it is >= the last listed key of every
-// incomplete shard (every key a shard did not list is below its last listed
-// one); the list is complete when every shard was and nothing was dropped.
+// into the pod's global top-T.  Entry x = s * T + e (shard s, entry e) sits in
+// lane x % 64, slot x / 64.  A key is provably in the global order if it is
+// >= the last listed key of every incomplete shard (every key a shard did not
+// list is below its last listed one); the list is complete when every shard
+// was and nothing was dropped.
 __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict__ st,
                                                       const uint64_t* __restrict__ xrecv, int32_t world,
                                                       uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
@@ -157,30 +158,45 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
   const int32_t j = blockIdx.x * 4 + w;
   const int32_t base = st->cursor;
   if (base + j >= min(st->end, base + kBatchPods)) return;   // wave-uniform
-  const int sh = lane / kTopT, e = lane % kTopT;
-  uint64_t key = 0, meta = 0;
-  if (sh < world) {
-    const uint64_t* x = xrecv + ((size_t)sh * kBatchPods + j) * kXRec;
-    meta = x[kTopT];
-    key = x[e];
+  uint64_t key[kGmergeSlots], last = 0;
+  bool valid[kGmergeSlots];
+  bool incomplete_shard = false;
+#pragma unroll
+  for (int q = 0; q < kGmergeSlots; q++) {
+    const int x = q * 64 + lane, sh = x / kTopT, e = x % kTopT;
+    key[q] = 0;
+    if (sh < world) {
+      const uint64_t* rec = xrecv + ((size_t)sh * kBatchPods + j) * kXRec;
+      const uint64_t meta = rec[kTopT];
+      const int32_t cnt = (int32_t)(uint32_t)meta;
+      const bool complete = (meta >> 32) != 0;
+      if (e < cnt) key[q] = rec[e];
+      if (!complete && cnt > 0 && e == cnt - 1) last = umax64(last, key[q]);
+      if (!complete && e == 0) incomplete_shard = true;
+    }
   }
-  const int32_t cnt = (int32_t)(uint32_t)meta;
-  const bool complete = (meta >> 32) != 0;
-  if (e >= cnt) key = 0;
-  // threshold: the largest "last listed key" over incomplete shards
-  const uint64_t last = (sh < world && !complete && cnt > 0 && e == cnt - 1) ? key : 0;
-  const uint64_t thr = wave_max_u64_dpp(last);
-  const bool all_complete = __ballot(sh < world && e == 0 && !complete) == 0;
-  const bool valid = key != 0 && key >= thr;
-  const uint64_t vm = __ballot(valid);
-  const int nvalid = __popcll(vm);
-  // rank of a valid key among the valid keys (keys are unique: one per node)
-  int rank = 0;
-  for (int l = 0; l < 64; l++) {
-    const uint64_t o = readlane_u64(key, l);
-    if (((vm >> l) & 1ull) && o > key) rank++;
+  const uint64_t thr = wave_max_u64_dpp(last);     // the largest "last listed key" of an incomplete shard
+  const bool all_complete = __ballot(incomplete_shard) == 0;
+  int nvalid = 0;
+  uint64_t vm[kGmergeSlots];
+#pragma unroll
+  for (int q = 0; q < kGmergeSlots; q++) {
+    valid[q] = key[q] != 0 && key[q] >= thr;
+    vm[q] = __ballot(valid[q]);
+    nvalid += __popcll(vm[q]);
   }
-  if (valid && rank < kTopT) topk[(size_t)j * kTopT + rank] = key;
+  // rank of each valid key among the valid keys (keys are unique: one per node)
+#pragma unroll
+  for (int q = 0; q < kGmergeSlots; q++) {
+    int rank = 0;
+#pragma unroll
+    for (int q2 = 0; q2 < kGmergeSlots; q2++)
+      for (int l = 0; l < 64; l++) {
+        const uint64_t o = readlane_u64(key[q2], l);
+        if (((vm[q2] >> l) & 1ull) && o > key[q]) rank++;
+      }
+    if (valid[q] && rank < kTopT) topk[(size_t)j * kTopT + rank] = key[q];
+  }
   const int n = nvalid < kTopT ? nvalid : kTopT;
   if (lane >= n && lane < kTopT) topk[(size_t)j * kTopT + lane] = 0;
   if (lane == 0) {
@@ -198,7 +214,8 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
 // result); the batch keeps that exact prefix.  Node ids are mapped to slots of
 // an LDS hash table, and "held by an earlier pod" is an LDS atomicMin of pod
 // indices per slot.  Rounds needed = the depth of the conflict chain.
-constexpr int kHashSlots = 4096;               // >= 2 x kBatchPods x kTopT list entries
+constexpr int kHashBits = kTopT <= 8 ? 12 : 13;
+constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
 
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
     int16_t slot = -1;
     if (e < cnt) {
       const int32_t node = key_node(topk[(size_t)i * kTopT + e]);
-      uint32_t h = ((uint32_t)node * 2654435761u) >> 20;        // 12-bit hash
+      uint32_t h = ((uint32_t)node * 2654435761u) >> (32 - kHashBits);
       while (true) {
         const int32_t prev = atomicCAS(&s_key[h], -1, node);
         if (prev == -1 || prev == node) break;

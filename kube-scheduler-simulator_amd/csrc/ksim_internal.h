@@ -8,14 +8,15 @@ namespace ksim {
 
 // Batch path geometry.
 constexpr int kBatchPods = 256;    // B: pods per speculative batch
-constexpr int kTopT = 8;           // T: candidate keys kept per pod (<= 64: one lane per entry in the chain)
+constexpr int kTopT = 8;           // T: candidate keys kept per pod (16 measured: fewer truncations, slower merge/chain)
 static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch geometry");
 constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
 constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
 constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
 constexpr int kXRec = kTopT + 1;   // sharded exchange record per pod: T keys + (count | complete << 32)
-constexpr int kMaxShards = 64 / kTopT;   // k_batch_gmerge holds every shard's list in one wave
-static_assert(kTopT * kMaxShards <= 64, "gmerge geometry");
+constexpr int kMaxShards = 8;      // shards of one simulation (one per GPU of a node)
+constexpr int kGmergeSlots = (kTopT * kMaxShards + 63) / 64;   // list entries per lane in k_batch_gmerge
+static_assert(kGmergeSlots <= 2, "gmerge geometry");
 
 // In-process shard group (one device): the pmax arrays of up to kMaxShards handles.
 struct GroupPtrs {

@@ -314,7 +314,11 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg, "avg_launch_ms": kt[dominant][0], "kernel_nodes": knodes,
-                     "dominant_by_time": by_time},
+                     "dominant_by_time": by_time,
+                     "note": ("algorithmic bytes = 112 B per pod x node evaluation (SURVEY 8(d)); the node table "
+                              "stays in L2 while the launch's pods sweep it, so HBM traffic ('traffic', PMC) is far "
+                              "below the algorithmic bytes and frac can exceed 1; the kernel is bound by its "
+                              "int64/f64 VALU work (profiles/README)")},
         "batch_geometry": geom,
     }
     if cfg == 2 and world == 1 and args.mode == "p100" and not args.no_adapt:

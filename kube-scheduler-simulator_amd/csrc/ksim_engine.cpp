@@ -1277,6 +1277,10 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     int r;
     if ((r = set_run(h, lo, hi))) return r;
     const bool adapt = batch && adapt_mode(h);
+    // the same kernel variants the run itself would launch
+    a.fast = batch && run_fast(h, lo, hi);
+    a.fuse_min = !batch && topo;
+    for (int32_t i = lo; i < hi && a.fuse_min; i++) a.fuse_min = h->hard_small[i] != 0;
     const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
     const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
     int32_t cursor = lo;

@@ -402,6 +402,14 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
 int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms,
                       int64_t* launches, int32_t cap);
 const char* ksim_kernel_name(int32_t k);
+/* The evaluation kernel of the path pod `first` takes (P100 batch path:
+ * k_batch_eval over the batch starting at `first`; per-pod path:
+ * k_filter_score of pod `first`), launched `reps` times back to back on the
+ * engine's stream between two HIP events, against the current snapshot
+ * (the kernel only writes scratch).  *avg_ms = elapsed / reps; the kernel's
+ * ksim_kernel_name index goes to *kernel.  KSIM_E_UNSUPPORTED for the ADAPT
+ * batch path (its evaluations span two kernels). */
+int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, int32_t* kernel);
 /* Batch-path diagnostics of the last ksim_schedule_loaded: out[0] batches,
  * out[1] truncations (an exhausted candidate list ended a batch), out[2] cuts
  * (a pod's exact choice was a node bound earlier in its batch, ending it);

@@ -396,6 +396,15 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[5], stream);
 }
 
+void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
+  const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
+  const dim3 g1((n_tiles + 3) / 4, kBatchPods);
+  if (a.fast)
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+  else
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+}
+
 void launch_chain(const LaunchArgs& a, hipStream_t stream) {
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);

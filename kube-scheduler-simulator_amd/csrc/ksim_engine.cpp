@@ -1253,6 +1253,35 @@ int ksim_reset_cluster(ksim_handle* h) {
   return KSIM_OK;
 }
 
+int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, int32_t* kernel) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!avg_ms || reps < 1 || !h->dp.pods || first < 0 || first >= h->dp.n_pods)
+    return set_err(h, KSIM_E_INVALID, "bad ksim_time_eval arguments");
+  const bool batch = h->batchable[first] && !is_sharded(h);
+  if (batch && adapt_mode(h)) return set_err(h, KSIM_E_UNSUPPORTED, "ADAPT batch evaluations span two kernels");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int32_t end = batch ? std::min(h->dp.n_pods, first + kBatchPods) : first + 1;
+  if ((rc = set_run(h, first, end))) return rc;
+  LaunchArgs a = make_args(h, h->dp, h->d_chosen);
+  a.fast = batch && run_fast(h, first, end);
+  auto launch = [&] {
+    if (batch) launch_batch_eval_only(a, h->stream);
+    else launch_filter_only(a, h->stream);
+  };
+  launch();                                          // warm (code object, caches)
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  for (int32_t i = 0; i < reps; i++) launch();
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  HIPCHK(h, hipGetLastError());
+  float ms = 0;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  *avg_ms = ms / reps;
+  if (kernel) *kernel = batch ? kKernelsPerCycle : 2;   // k_batch_eval / k_filter_score
+  return KSIM_OK;
+}
+
 const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerCycle) return kKernelNames[k];
   k -= kKernelsPerCycle;

@@ -55,6 +55,9 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nul
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
 void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_chain(const LaunchArgs& a, hipStream_t stream);
+// The evaluation kernels alone (ksim_time_eval).
+void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream);
+void launch_filter_only(const LaunchArgs& a, hipStream_t stream);
 // Sharded batch (node shards; the caller exchanges between the phases):
 //   launch_shard_eval    eval + merge; writes this shard's records to s.xsend
 //   (all-gather s.xsend -> s.xrecv [world][kBatchPods][kXRec])

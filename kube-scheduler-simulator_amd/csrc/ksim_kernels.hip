@@ -1068,6 +1068,11 @@ void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool top
   }
 }
 
+void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {
+  // the window-free variant writes counters: time the windowed one (same work per node)
+  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
+}
+
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
   k_assume<<<1, 64, 0, stream>>>(c, P, pod, node, sign);
 }

@@ -23,7 +23,7 @@ EXPORTS = [
     "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_class_count", "ksim_get_next_start",
     "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
-    "ksim_time_kernels", "ksim_kernel_name", "ksim_get_diag", "ksim_batch_geometry",
+    "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
 ]
 
@@ -66,6 +66,7 @@ def lib():
         L.ksim_reset_cluster.argtypes = [vp]
         L.ksim_time_kernels.argtypes = [vp, i32, i32, vp, vp, i32]
         L.ksim_kernel_name.argtypes = [i32]
+        L.ksim_time_eval.argtypes = [vp, i32, i32, vp, vp]
         L.ksim_kernel_name.restype = ctypes.c_char_p
         L.ksim_get_diag.argtypes = [vp, vp, i32]
         L.ksim_batch_geometry.argtypes = [vp, i32]
@@ -224,6 +225,13 @@ class Engine:
             d["chain_us"] = {"setup": out[3] / out[6] / 100.0, "rounds": out[4] / out[6] / 100.0,
                              "epilogue": out[5] / out[6] / 100.0, "rounds_per_batch": out[7] / out[6]}
         return d
+
+    def time_eval(self, first: int, reps: int = 200):
+        """(kernel name, mean ms) of the evaluation kernel launched back to back (ksim_time_eval)."""
+        ms = ctypes.c_double()
+        k = ctypes.c_int32()
+        self._chk(lib().ksim_time_eval(self.h, first, reps, ctypes.byref(ms), ctypes.byref(k)))
+        return lib().ksim_kernel_name(k.value).decode(), ms.value
 
     def time_kernels(self, first: int, count: int) -> dict:
         """Schedule loaded pods [first, first+count) with HIP events between the

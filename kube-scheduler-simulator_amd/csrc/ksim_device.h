@@ -770,6 +770,7 @@ struct BatchProg {
 
 // DevPods.bflags (batch path, per pod)
 constexpr int32_t kBatchStaticTrivial = 1; // every static filter passes on every node (host-proven)
+constexpr int32_t kPodRegistersValues = 2; // has a ScheduleAnyway spread keyed by a non-hostname column
 
 // Compact row for the batch repair's LDS staging: the NodeRow fields a
 // batchable pod can read (batchable pods request no scalar resources and the

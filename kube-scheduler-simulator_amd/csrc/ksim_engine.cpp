@@ -963,7 +963,10 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   P.terms = (const ksim_term*)p;
   if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
   P.norm_const = (const int32_t*)p;
-  if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
+  int32_t bflag[4] = {0, 0, 0, 0};
+  for (const auto& u : us)
+    if (use_registers_values(u)) bflag[0] |= kPodRegistersValues;
+  if ((rc = upload(h, h->pod1_bufs, bflag, sizeof(bflag), &p))) return rc;
   P.bflags = (const int32_t*)p;
   if ((rc = upload(h, h->pod1_bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
@@ -1065,12 +1068,15 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
       const ksim_topo_use& u = ps->uses[ps->pods[i].use_first + k];
       if (use_needs_dom(u)) h->xdom_len[i] += h->col_nvals[u.col];
       if (u.kind == KSIM_USE_PTS_HARD && u.col != KSIM_COL_NONE && h->col_nvals[u.col] > kFuseMinValues) h->hard_small[i] = 0;
-      if (use_registers_values(u)) xr += h->col_nvals[u.col];
+      if (use_registers_values(u)) {
+        xr += h->col_nvals[u.col];
+        bf[i] |= kPodRegistersValues;
+      }
       soft = soft || u.kind == KSIM_USE_PTS_SOFT;
     }
     h->xreg_len[i] = soft ? xr : 0;
-    bf[i] = static_trivial(h, ps->pods[i]) ? kBatchStaticTrivial : 0;
-    h->trivial[i] = bf[i] ? 1 : 0;
+    if (static_trivial(h, ps->pods[i])) bf[i] |= kBatchStaticTrivial;
+    h->trivial[i] = (bf[i] & kBatchStaticTrivial) ? 1 : 0;
   }
   DevPods P{};
   void* p = nullptr;

@@ -370,7 +370,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, k
     if (lane == 0 && fm) atomicAdd(&win->nfeas, (int32_t)__popcll(fm));
     if (lane == 0 && im) atomicAdd(&win->nign, (int32_t)__popcll(im));
     const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
-    for (int i = 0; i < p.use_count; i++) {
+    const int nreg = (P.bflags[pi] & kPodRegistersValues) ? p.use_count : 0;
+    for (int i = 0; i < nreg; i++) {
       const ksim_topo_use u = P.uses[p.use_first + i];
       if (!use_registers_values(u)) continue;
       const bool reg = feasible && !ign;

@@ -422,6 +422,36 @@ int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
  * out[3] keys a tile keeps per pod.  Returns the number written (<= n). */
 int ksim_batch_geometry(int32_t* out, int32_t n);
 
+/* ---- result emission ------------------------------------- */
+/* One cycle's outputs (ksim_eval_out or the oracle's) plus the names the
+ * annotations use.  messages[msg_id[i]] is the failure reason of node i when
+ * fail_plugin[i] is a filter index (the host builds the few distinct reasons,
+ * e.g. ksim/wrapped.py filter_message). */
+typedef struct ksim_emit_input {
+  int32_t n_nodes, n_filter, n_score, n_messages;
+  const char* const* node_names;       /* [n_nodes] nodeTree order */
+  const char* const* filter_names;     /* [n_filter] profile order, original plugin names */
+  const char* const* score_names;      /* [n_score] profile order, original plugin names */
+  const int32_t* score_weight;         /* [n_score] the store's scorePluginWeight (registry default) */
+  const uint8_t* has_normalize;        /* [n_score] plugin has a NormalizeScore extension */
+  const uint8_t* fail_plugin;          /* [n_nodes] KSIM_PASSED / KSIM_NOT_EVALUATED / filter index */
+  const int32_t* msg_id;               /* [n_nodes] index into messages (failed nodes) */
+  const char* const* messages;         /* [n_messages] */
+  const uint8_t* scored;               /* [n_nodes] */
+  const int64_t* raw;                  /* [n_score][n_nodes] */
+  const int64_t* norm;                 /* [n_score][n_nodes] */
+} ksim_emit_input;
+
+/* The filter-result, score-result and finalscore-result annotation values
+ * (annotation.go:3-30) of the cycle, exactly as resultstore.AddStoredResultToPod
+ * encodes the maps the wrapped plugins fill (store.go:129-190, 418-502): Go
+ * encoding/json text, NUL-terminated, into the three caller buffers.  lens[3]
+ * receives the lengths; a buffer smaller than its length + 1 gets nothing
+ * and the call returns KSIM_E_INVALID (retry with lens[k] + 1 bytes).  Host
+ * code only: no device, no handle. */
+int ksim_emit_cycle_json(const ksim_emit_input* in, char* filter_json, int64_t filter_cap, char* score_json,
+                         int64_t score_cap, char* final_json, int64_t final_cap, int64_t* lens);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,7 @@ EXPORTS = [
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
     "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
+    "ksim_emit_cycle_json",
 ]
 
 
@@ -66,6 +67,7 @@ def lib():
         L.ksim_reset_cluster.argtypes = [vp]
         L.ksim_time_kernels.argtypes = [vp, i32, i32, vp, vp, i32]
         L.ksim_kernel_name.argtypes = [i32]
+        L.ksim_emit_cycle_json.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp]
         L.ksim_time_eval.argtypes = [vp, i32, i32, vp, vp]
         L.ksim_kernel_name.restype = ctypes.c_char_p
         L.ksim_get_diag.argtypes = [vp, vp, i32]
@@ -245,3 +247,55 @@ class Engine:
             self._chk(n)
         return {lib().ksim_kernel_name(k).decode(): (float(out[k]), int(cnt[k]))
                 for k in range(n) if cnt[k] > 0}
+
+
+# ---- result emission (ksim_emit_cycle_json) -------------------------------------------
+class _EmitInput(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32), ("n_filter", ctypes.c_int32), ("n_score", ctypes.c_int32),
+                ("n_messages", ctypes.c_int32),
+                ("node_names", ctypes.c_void_p), ("filter_names", ctypes.c_void_p),
+                ("score_names", ctypes.c_void_p), ("score_weight", ctypes.c_void_p),
+                ("has_normalize", ctypes.c_void_p), ("fail_plugin", ctypes.c_void_p),
+                ("msg_id", ctypes.c_void_p), ("messages", ctypes.c_void_p), ("scored", ctypes.c_void_p),
+                ("raw", ctypes.c_void_p), ("norm", ctypes.c_void_p)]
+
+
+def _cstrs(names):
+    arr = (ctypes.c_char_p * max(len(names), 1))()
+    for i, n in enumerate(names):
+        arr[i] = n.encode()
+    return arr
+
+
+def emit_cycle_json(node_names, filter_names, score_names, score_weight, has_normalize, fail_plugin, msg_id,
+                    messages, scored, raw, norm):
+    """(filter-result, score-result, finalscore-result) annotation values of one
+    cycle, encoded natively (host C++, no GPU)."""
+    keep = []
+
+    def arr(a, dt):
+        a = np.ascontiguousarray(a, dt)
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.c_void_p)
+
+    names = [_cstrs(node_names), _cstrs(filter_names), _cstrs(score_names), _cstrs(messages)]
+    e = _EmitInput(len(node_names), len(filter_names), len(score_names), len(messages),
+                   ctypes.cast(names[0], ctypes.c_void_p), ctypes.cast(names[1], ctypes.c_void_p),
+                   ctypes.cast(names[2], ctypes.c_void_p), arr(score_weight, np.int32),
+                   arr(has_normalize, np.uint8), arr(fail_plugin, np.uint8), arr(msg_id, np.int32),
+                   ctypes.cast(names[3], ctypes.c_void_p), arr(scored, np.uint8), arr(raw, np.int64),
+                   arr(norm, np.int64))
+    lens = np.zeros(3, np.int64)
+    n = max(len(node_names), 1)
+    caps = [n * (32 + 48 * len(filter_names)) + 64, n * (32 + 48 * len(score_names)) + 64,
+            n * (32 + 48 * len(score_names)) + 64]
+    for _ in range(2):
+        bufs = [ctypes.create_string_buffer(c) for c in caps]
+        rc = lib().ksim_emit_cycle_json(ctypes.byref(e), bufs[0], caps[0], bufs[1], caps[1], bufs[2], caps[2],
+                                        lens.ctypes.data_as(ctypes.c_void_p))
+        if rc == 0:
+            return tuple(b.value.decode() for b in bufs)
+        if all(lens[k] + 1 <= caps[k] for k in range(3)):
+            raise KsimError(rc, "ksim_emit_cycle_json: invalid input")
+        caps = [int(n) + 1 for n in lens]
+    raise KsimError(rc, "ksim_emit_cycle_json failed")

@@ -117,3 +117,35 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
         store.add_pre_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
     for p in prof.plugins["bind"].enabled:
         store.add_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+
+
+def emit_cycle_annotations(cluster: EncodedCluster, prof: SchedulerProfile, res: Dict,
+                           score_plugin_weight: Dict[str, int]) -> Dict[str, str]:
+    """The three large annotation values of one cycle from the native emitter
+    (ksim_emit_cycle_json): what record_cycle + Store.add_stored_result_to_pod
+    produce for them, without building the maps."""
+    import numpy as np
+    from . import engine
+    from .resultstore import FILTER_RESULT, FINALSCORE_RESULT, SCORE_RESULT
+    forder = prof.filter_order()
+    fp = np.asarray(res["fail_plugin"], np.uint8)
+    fd = np.asarray(res["fail_detail"])
+    failed = (fp != abi.PASSED) & (fp != abi.NOT_EVALUATED)
+    pairs = sorted({(int(a), int(b)) for a, b in zip(fp[failed], fd[failed])})
+    index = {pr: k for k, pr in enumerate(pairs)}
+    messages = [filter_message(cluster, forder[a], b) for a, b in pairs]
+    msg_id = np.zeros(cluster.n_nodes, np.int32)
+    for i in np.nonzero(failed)[0]:
+        msg_id[i] = index[(int(fp[i]), int(fd[i]))]
+    splugins = prof.score_plugins()
+    snames = [p.name for p in splugins]
+    scored = np.asarray(res["scored"], np.uint8) if res["n_feasible"] > 1 else np.zeros(cluster.n_nodes, np.uint8)
+    if res["status"] == abi.STATUS_UNSCHEDULABLE:
+        scored = np.zeros(cluster.n_nodes, np.uint8)
+    raw = np.asarray(res["raw"], np.int64).reshape(len(snames), cluster.n_nodes) if snames else \
+        np.zeros((0, cluster.n_nodes), np.int64)
+    norm = np.asarray(res["norm"], np.int64).reshape(len(snames), cluster.n_nodes) if snames else raw
+    f, s, g = engine.emit_cycle_json(
+        cluster.node_names, forder, snames, [int(score_plugin_weight.get(n, 0)) for n in snames],
+        [1 if n in HAS_NORMALIZE else 0 for n in snames], fp, msg_id, messages, scored, raw, norm)
+    return {FILTER_RESULT: f, SCORE_RESULT: s, FINALSCORE_RESULT: g}

@@ -116,6 +116,7 @@ enum ksim_plugin {
 /* Filter outcome per node (ksim_eval_out.fail_plugin) */
 #define KSIM_PASSED        0xFF
 #define KSIM_NOT_EVALUATED 0xFE
+#define KSIM_FAIL_EXTENDER 0xFD  /* passed the plugins, filtered out by an extender (findNodesThatPassExtenders) */
 
 /* NodeResourcesFit failure reason bits (ksim_eval_out.fail_detail) */
 #define KSIM_FIT_TOO_MANY_PODS   1u
@@ -354,6 +355,25 @@ int ksim_set_pod_seq(ksim_handle* h, int64_t seq);
 /* ---- scheduling cycles --------------------------------------------------- */
 /* One full cycle for pod `pod_index` of `pods` (compat mode) incl. assume/bind. */
 int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
+
+/* The same cycle around the host's extender round trip (SURVEY §8(f) 4;
+ * schedule_one.go findNodesThatPassExtenders / prioritizeNodes):
+ *   ksim_eval_pod_filter  PreFilter, Filter and the numFeasibleNodesToFind
+ *                         window.  fail_plugin / fail_detail and the scalars
+ *                         (n_feasible, n_evaluated, n_processed, k_to_find,
+ *                         next_start) are filled; the kept nodes are the ones
+ *                         with fail_plugin == KSIM_PASSED.  The host sends them
+ *                         to its extenders.
+ *   ksim_eval_pod_finish  ext_fail[n] nonzero: an extender filtered the kept
+ *                         node out (fail_plugin = KSIM_FAIL_EXTENDER).
+ *                         ext_score[n]: the extenders' combined weighted scores,
+ *                         added to the plugin totals.  Either may be NULL.
+ *                         Score, NormalizeScore over the remaining nodes,
+ *                         selectHost and the bind; every output as ksim_eval_pod.
+ * nextStartNodeIndex advances by the filter pass, as upstream (before the
+ * extenders).  Unsharded handles only. */
+int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
+int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t* ext_score, ksim_eval_out* out);
 /* Assume/forget a pod on a node (NodeInfo.AddPod / RemovePod). */
 int ksim_assume(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
 int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);

@@ -121,6 +121,8 @@ struct DevScratch {
   int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
   int32_t* aexact;       // ADAPT batch: pods whose windows are exact
   int32_t* abroken;      // ADAPT batch: a bound node flipped feasibility inside the pod's window
+  const uint8_t* ext_fail;   // extender pass only (else null): nodes an extender filtered out
+  const int64_t* ext_score;  // extender pass only (else null): the extenders' combined scores
   uint32_t* regbm;       // no-window cycles: PTS pair registration bitmaps [KSIM_MAX_USES][(vmax + 31) / 32]
   int64_t* xdom;         // sharded cycle: packed domain sums (all-reduced, sum)
   int64_t* xreg;         // sharded cycle: IgnoredNodes count + per-value registrations (all-reduced, sum)

@@ -110,6 +110,11 @@ struct ksim_handle {
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
+  // extender round trip (ksim_eval_pod_filter -> ksim_eval_pod_finish)
+  DevPods pod1{};
+  bool ext_pending = false;
+  uint8_t* ext_fail = nullptr;     // device [n]
+  int64_t* ext_score = nullptr;    // device [n]
 
   // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
   int32_t shard_base = 0, shard_total = 0;
@@ -830,6 +835,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.ign, uint8_t*, N);
   SCR(s.win, WinState*, sizeof(WinState));
   SCR(s.regbm, uint32_t*, 4 * (size_t)KSIM_MAX_USES * ((vmax + 31) / 32));
+  SCR(h->ext_fail, uint8_t*, N);
+  SCR(h->ext_score, int64_t*, 8 * N);
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
@@ -980,19 +987,8 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   return KSIM_OK;
 }
 
-int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
-  int rc = ensure_ready(h);
-  if (rc) return rc;
-  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
-    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
-  if ((rc = validate_pod(h, ps, pod_index))) return rc;
-  HIPCHK(h, hipSetDevice(h->device));
-  DevPods P;
-  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
-  if ((rc = set_run(h, 0, 1))) return rc;
-  launch_cycle(make_args(h, P, nullptr), h->stream, true, ps->pods[pod_index].use_count > 0);
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+// Copy one compat cycle's per-node outputs and scalars to the caller.
+static int copy_eval_out(ksim_handle* h, ksim_eval_out* out) {
   const size_t N = (size_t)h->dc.n;
   const int S = h->prof.n_score;
   if (out->fail_plugin) HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
@@ -1012,6 +1008,81 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksi
   out->next_start = st.next_start_after;
   if (out->scored && out->n_feasible <= 1) std::memset(out->scored, 0, N);
   return KSIM_OK;
+}
+
+int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
+    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  h->ext_pending = false;
+  DevPods P;
+  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
+  if ((rc = set_run(h, 0, 1))) return rc;
+  launch_cycle(make_args(h, P, nullptr), h->stream, true, ps->pods[pod_index].use_count > 0);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return copy_eval_out(h, out);
+}
+
+int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
+    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if (is_sharded(h)) return set_err(h, KSIM_E_UNSUPPORTED, "extender cycles run on unsharded handles");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  if ((rc = upload_single(h, ps, pod_index, h->pod1))) return rc;
+  if ((rc = set_run(h, 0, 1))) return rc;
+  launch_cycle_filter(make_args(h, h->pod1, nullptr), h->stream, ps->pods[pod_index].use_count > 0);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const size_t N = (size_t)h->dc.n;
+  if (out->fail_plugin) HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+  if (out->fail_detail) HIPCHK(h, hipMemcpy(out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
+  WinState w;
+  DevState st;
+  HIPCHK(h, hipMemcpy(&w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+  const int32_t n = h->dc.n;
+  const int32_t processed = w.cut < n ? w.cut : n;
+  out->chosen = -1;
+  out->status = 0;
+  out->n_feasible = w.nf;
+  out->n_evaluated = w.evaluated;
+  out->n_processed = processed;
+  out->k_to_find = w.k;
+  out->next_start = (int32_t)(((int64_t)st.next_start + processed) % n);
+  h->ext_pending = true;
+  return KSIM_OK;
+}
+
+int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t* ext_score, ksim_eval_out* out) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!out) return set_err(h, KSIM_E_INVALID, "out is null");
+  if (!h->ext_pending) return set_err(h, KSIM_E_INVALID, "ksim_eval_pod_finish without ksim_eval_pod_filter");
+  h->ext_pending = false;
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t N = (size_t)h->dc.n;
+  if (ext_fail)
+    HIPCHK(h, hipMemcpyAsync(h->ext_fail, ext_fail, N, hipMemcpyHostToDevice, h->stream));
+  else
+    HIPCHK(h, hipMemsetAsync(h->ext_fail, 0, N, h->stream));
+  if (ext_score)
+    HIPCHK(h, hipMemcpyAsync(h->ext_score, ext_score, 8 * N, hipMemcpyHostToDevice, h->stream));
+  else
+    HIPCHK(h, hipMemsetAsync(h->ext_score, 0, 8 * N, h->stream));
+  LaunchArgs a = make_args(h, h->pod1, nullptr);
+  a.s.ext_fail = h->ext_fail;
+  a.s.ext_score = h->ext_score;
+  launch_cycle_finish(a, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return copy_eval_out(h, out);
 }
 
 static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {

@@ -55,6 +55,10 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nul
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
 void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_chain(const LaunchArgs& a, hipStream_t stream);
+// Compat cycle around the host's extender round trip (ksim_eval_pod_filter / _finish):
+// the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.
+void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
+void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
 // The evaluation kernels alone (ksim_time_eval).
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream);
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream);

@@ -425,34 +425,57 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   const ksim_pod& p = P.pods[pi];
   WinState* win = s.win;
 
-  // feasible count per rotated chunk, block scan, locate the (K+1)-th
-  int32_t cnt = 0;
-  for (int32_t r = lo; r < hi; r++) {
-    int32_t node = start + r;
-    if (node >= N) node -= N;
-    cnt += s.fail[node] == KSIM_PASSED;
-  }
-  int32_t excl, total;
-  block_scan_i32(cnt, excl, total, sh32);
-  if (tid == 0) s_cut = N;
-  __syncthreads();
-  if (total > K && excl <= K && K < excl + cnt) {
-    int32_t run = excl;
+  // Extender pass (s.ext_fail set, ksim_eval_pod_finish): the window of the
+  // filter pass stands (nextStartNodeIndex moved before the extenders ran);
+  // the kept nodes an extender dropped are marked and the list recounted.
+  const bool ext = s.ext_fail != nullptr;
+  int32_t cut, nf;
+  if (ext) {
+    cut = win->cut;
+    const int32_t kend0 = cut < N ? cut : N;
+    int32_t kept = 0;
+    for (int32_t r = tid; r < kend0; r += kFinalThreads) {   // the stride the loops below use
+      int32_t node = start + r;
+      if (node >= N) node -= N;
+      if (s.fail[node] != KSIM_PASSED) continue;
+      if (s.ext_fail[node]) {
+        s.fail[node] = KSIM_FAIL_EXTENDER;
+        if (COMPAT) s.detail[node] = 0;
+      } else {
+        kept++;
+      }
+    }
+    nf = block_sum_i32_nw<kFinalWaves>(kept, sh32);
+  } else {
+    // feasible count per rotated chunk, block scan, locate the (K+1)-th
+    int32_t cnt = 0;
     for (int32_t r = lo; r < hi; r++) {
       int32_t node = start + r;
       if (node >= N) node -= N;
-      if (s.fail[node] == KSIM_PASSED) {
-        if (run == K) { s_cut = r; break; }
-        run++;
+      cnt += s.fail[node] == KSIM_PASSED;
+    }
+    int32_t excl, total;
+    block_scan_i32(cnt, excl, total, sh32);
+    if (tid == 0) s_cut = N;
+    __syncthreads();
+    if (total > K && excl <= K && K < excl + cnt) {
+      int32_t run = excl;
+      for (int32_t r = lo; r < hi; r++) {
+        int32_t node = start + r;
+        if (node >= N) node -= N;
+        if (s.fail[node] == KSIM_PASSED) {
+          if (run == K) { s_cut = r; break; }
+          run++;
+        }
       }
     }
+    __syncthreads();
+    cut = s_cut;
+    nf = total < K ? total : K;
   }
-  __syncthreads();
-  const int32_t cut = s_cut;
   const int32_t kend = cut < N ? cut : N;
   const int32_t evaluated = cut < N ? cut + 1 : N;
-  const int32_t nf = total < K ? total : K;
-  if (COMPAT) {
+  if (COMPAT && !ext) {
     for (int32_t r = evaluated + tid; r < N; r += kFinalThreads) {
       int32_t node = start + r;
       if (node >= N) node -= N;
@@ -654,7 +677,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_pr
     if (kept && nf > 1) {
       const bool ign = win->has_soft && s.ign[node];
       const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
-      int64_t tot = S == 0 ? 1 : s.part[node];
+      // prioritizeNodes: no score plugins and no extenders -> 1; the extenders'
+      // combined scores are added to the plugin total
+      int64_t tot = S == 0 ? (s.ext_score ? 0 : 1) : s.part[node];
+      if (s.ext_score) tot += s.ext_score[node];
       for (int k = 0; k < S; k++) {
         const int32_t kind = norm_kind(prof.score[k]);
         const int64_t raw = s.raw[(size_t)k * N + node];
@@ -1067,6 +1093,22 @@ void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool top
     if (nowin) launch_cycle_t<false, true>(a, stream, topo, evs);
     else launch_cycle_t<false, false>(a, stream, topo, evs);
   }
+}
+
+void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo) {
+  const int blocks = (a.c.n + 255) / 256;
+  if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
+  k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+}
+
+void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  k_bind<false><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
 }
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {

@@ -122,6 +122,7 @@ OP_TRUE = 9
 
 PASSED = 0xFF
 NOT_EVALUATED = 0xFE
+FAIL_EXTENDER = 0xFD
 
 FIT_TOO_MANY_PODS = 1
 FIT_CPU = 2

@@ -25,7 +25,7 @@ EXPORTS = [
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
     "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
-    "ksim_emit_cycle_json",
+    "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
 ]
 
 
@@ -59,6 +59,8 @@ def lib():
         L.ksim_set_next_start.argtypes = [vp, i32]
         L.ksim_set_pod_seq.argtypes = [vp, i64]
         L.ksim_eval_pod.argtypes = [vp, vp, i32, vp]
+        L.ksim_eval_pod_filter.argtypes = [vp, vp, i32, vp]
+        L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
         L.ksim_assume.argtypes = [vp, vp, i32, i32]
         L.ksim_forget.argtypes = [vp, vp, i32, i32]
         L.ksim_load_pods.argtypes = [vp, vp]
@@ -165,6 +167,22 @@ class Engine:
         ps = pods.pod_set()
         self._chk(lib().ksim_eval_pod(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
         return buf.result()
+
+    def eval_pod_extenders(self, pods, index: int, extender) -> dict:
+        """A compat cycle around an extender round trip: ``extender(filter
+        result) -> (ext_fail[n] or None, ext_score[n] or None)`` sees the filter
+        pass (kept nodes: fail_plugin == PASSED)."""
+        buf = abi.EvalBuffers(self.n_nodes, self.n_score)
+        ps = pods.pod_set()
+        self._chk(lib().ksim_eval_pod_filter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        ef, es = extender(buf.result())
+        ef = None if ef is None else np.ascontiguousarray(ef, np.uint8)
+        es = None if es is None else np.ascontiguousarray(es, np.int64)
+        buf2 = abi.EvalBuffers(self.n_nodes, self.n_score)
+        self._chk(lib().ksim_eval_pod_finish(self.h, None if ef is None else ef.ctypes.data_as(ctypes.c_void_p),
+                                             None if es is None else es.ctypes.data_as(ctypes.c_void_p),
+                                             ctypes.byref(buf2.out)))
+        return buf2.result()
 
     def assume(self, pods, index: int, node: int):
         ps = pods.pod_set()

@@ -770,6 +770,16 @@ static void assume_pod(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p
 /* ---- schedulePod: findNodesThatFitPod + prioritizeNodes + selectHost ----- */
 /* Sequential (parallelism 1) semantics of [upstream] schedule_one.go — a15-a19. */
 int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_eval_out* out) {
+  return ksim_oracle_cycle_ext(o, ps, pi, NULL, NULL, out);
+}
+
+/* The cycle with extenders (schedule_one.go findNodesThatPassExtenders and the
+ * extender part of prioritizeNodes): ext_fail[node] nonzero removes a kept
+ * node after the window (nextStartNodeIndex has already advanced);
+ * ext_score[node] (the extenders' combined weighted scores) is added to the
+ * plugin total before selectHost.  Either may be NULL. */
+int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, const uint8_t* ext_fail,
+                          const int64_t* ext_score, ksim_eval_out* out) {
   if (!o || !ps || pi < 0 || pi >= ps->n_pods || !out) return KSIM_E_INVALID;
   const ksim_pod* p = &ps->pods[pi];
   const int32_t N = o->n;
@@ -806,6 +816,18 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_e
   }
   int32_t processed = nf + nfailed;
   o->next_start = (start + processed) % N;
+  if (ext_fail) {                  /* findNodesThatPassExtenders over the kept list */
+    int32_t m = 0;
+    for (int32_t j = 0; j < nf; j++) {
+      const int32_t node = o->flist[j];
+      if (ext_fail[node]) {
+        if (out->fail_plugin) out->fail_plugin[node] = KSIM_FAIL_EXTENDER;
+      } else {
+        o->flist[m++] = node;
+      }
+    }
+    nf = m;
+  }
 
   out->k_to_find = K;
   out->n_feasible = nf;
@@ -839,7 +861,9 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_e
         totals[j] += tmp[j] * w;
       }
     }
-    if (S == 0) for (int32_t j = 0; j < nf; j++) totals[j] = 1;  /* prioritizeNodes: no score plugins */
+    /* prioritizeNodes: no score plugins and no extenders -> every node scores 1 */
+    if (S == 0 && !ext_score) for (int32_t j = 0; j < nf; j++) totals[j] = 1;
+    if (ext_score) for (int32_t j = 0; j < nf; j++) totals[j] += ext_score[o->flist[j]];
     uint64_t best = 0;
     chosen = -1;
     for (int32_t j = 0; j < nf; j++) {

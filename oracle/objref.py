@@ -547,7 +547,9 @@ class ObjScheduler:
                 return pl, msg
         return None, None
 
-    def cycle(self, pod: Pod) -> dict:
+    def cycle(self, pod: Pod, extender=None) -> dict:
+        """``extender(kept node names) -> (filtered-out names, {name: combined weighted score})``
+        models the scheduler's extenders (findNodesThatPassExtenders, prioritizeNodes)."""
         N = len(self.nodes)
         seq = self.seq
         self.seq += 1
@@ -568,6 +570,12 @@ class ObjScheduler:
             else:
                 failed += 1
         self.next_start = (self.next_start + len(feasible) + failed) % N
+        ext_scores: Dict[str, int] = {}
+        if extender is not None:
+            out, ext_scores = extender([ni.node.name for ni in feasible])
+            for name in out:
+                filt[name] = ("extender", "filtered out by an extender")
+            feasible = [ni for ni in feasible if ni.node.name not in out]
         res = {"filter": filt, "n_feasible": len(feasible), "raw": {}, "norm": {}, "total": {}}
         if not feasible:
             res["chosen"] = None
@@ -608,6 +616,8 @@ class ObjScheduler:
                 res["raw"][pl] = dict(zip(names, raw))
                 res["norm"][pl] = dict(zip(names, norm))
                 totals = [a + b * w for a, b in zip(totals, norm)]
+            if extender is not None:
+                totals = [t + ext_scores.get(nm, 0) for t, nm in zip(totals, names)]
             res["total"] = dict(zip(names, totals))
             index = {ni.node.name: i for i, ni in enumerate(self.nodes)}
             best = max(range(len(feasible)), key=lambda j: tb_key(totals[j], self.seed, seq, index[names[j]]))

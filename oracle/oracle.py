@@ -26,6 +26,7 @@ def lib():
         L.ksim_oracle_create.argtypes = [vp, vp, vp]
         L.ksim_oracle_destroy.argtypes = [vp]
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
+        L.ksim_oracle_cycle_ext.argtypes = [vp, vp, i32, vp, vp, vp]
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
         L.ksim_oracle_get_class_count.argtypes = [vp, vp]
@@ -68,11 +69,17 @@ class Oracle:
 
     __del__ = close
 
-    def cycle(self, pods, index: int) -> dict:
+    def cycle(self, pods, index: int, ext_fail=None, ext_score=None) -> dict:
+        """One compat cycle; ext_fail / ext_score (per node) model the extenders."""
         from ksim import abi
         buf = abi.EvalBuffers(self.cluster.n_nodes, self.profile.n_score)
         ps = pods.pod_set()
-        rc = lib().ksim_oracle_cycle(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out))
+        ef = None if ext_fail is None else np.ascontiguousarray(ext_fail, np.uint8)
+        es = None if ext_score is None else np.ascontiguousarray(ext_score, np.int64)
+        rc = lib().ksim_oracle_cycle_ext(self.h, ctypes.byref(ps), index,
+                                         None if ef is None else ef.ctypes.data_as(ctypes.c_void_p),
+                                         None if es is None else es.ctypes.data_as(ctypes.c_void_p),
+                                         ctypes.byref(buf.out))
         if rc != 0:
             raise RuntimeError(f"oracle cycle failed: {rc}")
         return buf.result()

@@ -340,3 +340,27 @@ def test_ingested_template_cluster():
     snap = ingest.load(test_ingest._template_cluster(n_nodes=160, n_pods=2000))
     cluster, enc, _ = ingest.encode(snap)
     _batch_vs_oracle(cluster, enc, pct=0)
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_extender_cycles_vs_oracle(pct):
+    """ksim_eval_pod_filter / _finish around a deterministic extender, cycle by
+    cycle against the oracle's extender cycle (configs 1 and 3 shapes)."""
+    import test_extender
+    for cluster, pods in (gen.config1(n_nodes=160, n_pods=120),
+                          gen.config3(n_nodes=200, pods_per_node=10, n_incoming=80, seed=3, zone_anti_every=20)):
+        fail, score = test_extender.extender_model(cluster.node_names)
+        prof = _prof(pct)
+        eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+        seen = set()
+
+        def ext(filtered):
+            kept = filtered["fail_plugin"] == abi.PASSED
+            seen.add(int(kept.sum()))
+            return fail, score
+
+        for i in range(pods.n_pods):
+            _compare_cycle(eng.eval_pod_extenders(pods, i, ext), ora.cycle(pods, i, fail, score), f"pod {i}")
+        es, os_ = eng.node_state(), ora.node_state()
+        for k in es:
+            np.testing.assert_array_equal(es[k], os_[k])

@@ -136,7 +136,6 @@ struct DevScratch {
   uint64_t* gkey;        // batch path: [B] key of each pod's greedy guess (0: none)
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
-  uint32_t* done;        // batch path: k_batch_pairs blocks finished (last-block election)
   unsigned long long* dbg;   // [16] diagnostic accumulators (ksim_get_diag), e.g. chain phase times
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
   uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records

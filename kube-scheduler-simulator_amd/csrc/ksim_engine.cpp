@@ -847,7 +847,6 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.chain_end, int32_t*, 4);
   SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
-  SCR(s.done, uint32_t*, 4);
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
   SCR(s.dbg, unsigned long long*, 8 * 16);
   SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);

@@ -1,18 +1,23 @@
 // ksim_kernels.hip — HIP kernels of the scheduling cycle (gfx950).
 //
-// Two execution paths produce identical placements (both bit-exact with the
+// Three execution paths produce identical placements (each bit-exact with the
 // oracle):
 //
-// A. Per-pod path (compat mode, and pods the batch path cannot take):
+// A. Per-pod path (compat mode, and pods the batch paths cannot take), one
+//    cycle per pod:
+//    k_topo_prefilter / k_topo_min  PodTopologySpread / InterPodAffinity
+//                    PreFilter maps as domain sums (a27, a29)
 //    k_filter_score  grid over nodes: RunFilterPlugins (SURVEY §8(a) a17, a22,
-//                    a25, a26) and, for feasible nodes, every raw Score (a23-a26).
-//    k_finalize      one 1024-thread block: numFeasibleNodesToFind window by a
-//                    block prefix scan (a16), NormalizeScore extrema (a31),
-//                    weighted totals (a18), selectHost as a packed-u64 argmax
-//                    (a19, TB tie-break), NodeInfo.AddPod (a20).
-//
-// B. Batch path (P100, pods whose normalized plugins are constant over
-//    nodes): ksim_batch.hip.
+//                    a25-a29) and, for feasible nodes, every raw Score (a23-a30)
+//    k_window        numFeasibleNodesToFind window by a block prefix scan (a16)
+//                    and PTS PreScore (a28); not launched when K = N
+//    k_extrema       NormalizeScore extrema (a31) and PTS raw scores
+//    k_select        weighted totals (a18), selectHost as a packed-u64 argmax
+//                    (a19, TB tie-break)
+//    k_bind          NodeInfo.AddPod (a20) and the scheduler state
+// B. Batch paths (pods whose normalized plugins are constant over nodes):
+//    ksim_batch.hip (P100), ksim_adapt.hip (ADAPT).
+// C. The node-sharded per-pod cycle (below).
 #include "ksim_device.h"
 #include "ksim_internal.h"
 #include "ksim_wave.h"

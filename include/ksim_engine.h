@@ -442,6 +442,48 @@ int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
  * out[3] keys a tile keeps per pod.  Returns the number written (<= n). */
 int ksim_batch_geometry(int32_t* out, int32_t n);
 
+/* ---- PostFilter: DefaultPreemption ----------------------- */
+/* The bound pods preemption may evict: per pod its node, priority, start
+ * time (any monotone unit) and the requests it holds on the node
+ * (cpu, memory, ephemeral-storage, then the scalar columns). */
+#define KSIM_PREEMPT_REQ (3 + KSIM_MAX_SCALAR)
+typedef struct ksim_bound_pods {
+  int32_t n, _pad;
+  const int32_t* node;        /* [n] node position */
+  const int32_t* priority;    /* [n] .spec.priority */
+  const int64_t* start_time;  /* [n] status.startTime */
+  const int64_t* req;         /* [n][KSIM_PREEMPT_REQ] */
+} ksim_bound_pods;
+
+typedef struct ksim_preempt_out {
+  int32_t nominated;          /* node position; -1: preemption cannot help */
+  int32_t n_victims;          /* victims on the nominated node (may exceed victims_cap) */
+  int32_t n_potential;        /* nodesWherePreemptionMightHelp */
+  int32_t n_candidates;       /* candidates the dry run kept (<= numCandidates) */
+  int32_t* victims;           /* [victims_cap] bound-pod indices, reprieve (importance) order */
+  int32_t victims_cap, _pad;
+} ksim_preempt_out;
+
+/* Replace the bound-pod table (copied; the engine orders it per node by
+ * importance: priority desc, start time asc). */
+int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b);
+/* DefaultPreemption's PostFilter for an unschedulable pod of `priority`
+ * (default_preemption.go / preemption.go, v1.26) on the current snapshot,
+ * without changing it:
+ *   potential nodes  the nodes whose filter status is Unschedulable, i.e. the
+ *                    ones that failed NodeResourcesFit (the plugins before it
+ *                    return UnschedulableAndUnresolvable);
+ *   dry run          SelectVictimsOnNode on each, in nodeTree order from
+ *                    offset 0 (upstream draws a random offset), keeping the
+ *                    first numCandidates = max(10 % of them, 100) candidates;
+ *   selection        pickOneNodeForPreemption: lowest highest-victim
+ *                    priority, lowest sum of (priority + 2^31), fewest
+ *                    victims, latest earliest start among the highest-
+ *                    priority victims, then the first candidate (no PDBs).
+ * The pod must carry no topology / port / image uses (KSIM_E_UNSUPPORTED). */
+int ksim_preempt(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
+                 ksim_preempt_out* out);
+
 /* ---- result emission ------------------------------------- */
 /* One cycle's outputs (ksim_eval_out or the oracle's) plus the names the
  * annotations use.  messages[msg_id[i]] is the failure reason of node i when

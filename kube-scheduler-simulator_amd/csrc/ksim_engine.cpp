@@ -110,6 +110,11 @@ struct ksim_handle {
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
+  // DefaultPreemption: bound pods per node in importance order
+  std::vector<DevBuf> pre_bufs;
+  DevPreempt pre{};
+  std::vector<int32_t> pre_index;       // CSR position -> bound-pod table index
+  int32_t pre_n = 0;
   // extender round trip (ksim_eval_pod_filter -> ksim_eval_pod_finish)
   DevPods pod1{};
   bool ext_pending = false;
@@ -646,6 +651,7 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->scratch_bufs);
   free_bufs(h->pod_bufs);
   free_bufs(h->pod1_bufs);
+  free_bufs(h->pre_bufs);
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   if (h->st) (void)hipFree(h->st);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -1449,4 +1455,99 @@ extern "C" int ksim_batch_geometry(int32_t* out, int32_t n) {
   const int32_t m = n < 4 ? n : 4;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
+}
+
+
+// ---- PostFilter: DefaultPreemption (ksim_preempt.hip) ------------------------------
+extern "C" int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!b || b->n < 0 || (b->n > 0 && (!b->node || !b->priority || !b->start_time || !b->req)))
+    return set_err(h, KSIM_E_INVALID, "bad bound-pod table");
+  const int32_t N = h->dc.n, n = b->n;
+  for (int32_t i = 0; i < n; i++)
+    if (b->node[i] < 0 || b->node[i] >= N) return set_err(h, KSIM_E_INVALID, "bound pod on a node out of range");
+  // per node, util.MoreImportantPod order (priority desc, start asc), then table order
+  std::vector<int32_t> ix((size_t)n);
+  for (int32_t i = 0; i < n; i++) ix[i] = i;
+  std::sort(ix.begin(), ix.end(), [&](int32_t x, int32_t y) {
+    if (b->node[x] != b->node[y]) return b->node[x] < b->node[y];
+    if (b->priority[x] != b->priority[y]) return b->priority[x] > b->priority[y];
+    if (b->start_time[x] != b->start_time[y]) return b->start_time[x] < b->start_time[y];
+    return x < y;
+  });
+  std::vector<int32_t> off((size_t)N + 1, 0), prio((size_t)std::max(n, 1));
+  std::vector<int64_t> start((size_t)std::max(n, 1)), req((size_t)std::max(n, 1) * KSIM_PREEMPT_REQ);
+  for (int32_t i = 0; i < n; i++) off[b->node[i] + 1]++;
+  for (int32_t v = 0; v < N; v++) off[v + 1] += off[v];
+  for (int32_t k = 0; k < n; k++) {
+    const int32_t i = ix[k];
+    prio[k] = b->priority[i];
+    start[k] = b->start_time[i];
+    for (int q = 0; q < KSIM_PREEMPT_REQ; q++) req[(size_t)k * KSIM_PREEMPT_REQ + q] = b->req[(size_t)i * KSIM_PREEMPT_REQ + q];
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  free_bufs(h->pre_bufs);
+  DevPreempt d{};
+  void* p = nullptr;
+  if ((rc = upload(h, h->pre_bufs, off.data(), 4 * off.size(), &p))) return rc;
+  d.off = (const int32_t*)p;
+  if ((rc = upload(h, h->pre_bufs, prio.data(), 4 * prio.size(), &p))) return rc;
+  d.prio = (const int32_t*)p;
+  if ((rc = upload(h, h->pre_bufs, start.data(), 8 * start.size(), &p))) return rc;
+  d.start = (const int64_t*)p;
+  if ((rc = upload(h, h->pre_bufs, req.data(), 8 * req.size(), &p))) return rc;
+  d.req = (const int64_t*)p;
+  if ((rc = upload(h, h->pre_bufs, nullptr, (size_t)std::max(n, 1), &p))) return rc;
+  d.vflag = (uint8_t*)p;
+  if ((rc = upload(h, h->pre_bufs, nullptr, sizeof(PreemptNode) * (size_t)N, &p))) return rc;
+  d.res = (PreemptNode*)p;
+  if ((rc = upload(h, h->pre_bufs, nullptr, 16, &p))) return rc;
+  d.pick = (int32_t*)p;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->pre = d;
+  h->pre_index = ix;
+  h->pre_n = n;
+  return KSIM_OK;
+}
+
+extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t priority,
+                            ksim_preempt_out* out) {
+  int rc = ensure_ready(h);
+  if (rc) return rc;
+  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
+    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if (!h->pre.off) return set_err(h, KSIM_E_INVALID, "ksim_set_bound_pods first");
+  if (is_sharded(h)) return set_err(h, KSIM_E_UNSUPPORTED, "preemption runs on unsharded handles");
+  if (ps->pods[pod_index].use_count > 0)
+    return set_err(h, KSIM_E_UNSUPPORTED, "preemption for pods with topology / port / image uses");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  int32_t fit = -1;
+  for (int f = 0; f < h->prof.n_filter; f++)
+    if (h->prof.filter[f] == KSIM_PL_NODE_RESOURCES_FIT) fit = f;
+  HIPCHK(h, hipSetDevice(h->device));
+  DevPods P;
+  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
+  if ((rc = set_run(h, 0, 1))) return rc;
+  launch_preempt(make_args(h, P, nullptr), h->pre, fit, priority, h->stream);
+  HIPCHK(h, hipGetLastError());
+  int32_t pick[4];
+  HIPCHK(h, hipMemcpyAsync(pick, h->pre.pick, sizeof(pick), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  out->nominated = pick[0];
+  out->n_victims = pick[1];
+  out->n_potential = pick[2];
+  out->n_candidates = pick[3];
+  if (pick[0] >= 0 && out->victims && out->victims_cap > 0) {
+    std::vector<int32_t> off(2);
+    HIPCHK(h, hipMemcpy(off.data(), h->pre.off + pick[0], 8, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> flag((size_t)std::max(off[1] - off[0], 1));
+    if (off[1] > off[0])
+      HIPCHK(h, hipMemcpy(flag.data(), h->pre.vflag + off[0], (size_t)(off[1] - off[0]), hipMemcpyDeviceToHost));
+    int32_t k = 0;
+    for (int32_t j = off[0]; j < off[1] && k < out->victims_cap; j++)
+      if (flag[j - off[0]]) out->victims[k++] = h->pre_index[j];
+  }
+  return KSIM_OK;
 }

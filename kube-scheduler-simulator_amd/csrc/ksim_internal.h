@@ -59,6 +59,23 @@ void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.
 void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
 void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
+// DefaultPreemption dry run (ksim_preempt.hip): the bound pods per node in
+// importance order (CSR over nodes), per-node results, the pick.
+struct PreemptNode {
+  int32_t potential, cand, nv, high;   // potential node, candidate, victims, highest victim priority
+  int64_t sum, early;                  // sum of (priority + 2^31), earliest start of the highest-priority victims
+};
+struct DevPreempt {
+  const int32_t* off;                  // [n + 1]
+  const int32_t* prio;                 // [n_bound] CSR order
+  const int64_t* start;                // [n_bound]
+  const int64_t* req;                  // [n_bound][KSIM_PREEMPT_REQ]
+  uint8_t* vflag;                      // [n_bound] victim of its node's dry run
+  PreemptNode* res;                    // [n]
+  int32_t* pick;                       // [4] nominated, victims, potential, candidates
+};
+void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_index, int32_t prio, hipStream_t stream);
+
 // The evaluation kernels alone (ksim_time_eval).
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream);
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream);

@@ -272,5 +272,42 @@ class EvalBuffers:
                     total=self.total.copy())
 
 
+# ---- PostFilter: DefaultPreemption ----------------------------------------------
+PREEMPT_REQ = 3 + MAX_SCALAR
+
+
+class _BoundPodsC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("_pad", ctypes.c_int32), ("node", ctypes.c_void_p),
+                ("priority", ctypes.c_void_p), ("start_time", ctypes.c_void_p), ("req", ctypes.c_void_p)]
+
+
+class BoundPods:
+    """ksim_bound_pods over numpy arrays (kept alive by this object)."""
+
+    def __init__(self, node, priority, start_time, req):
+        self.node = np.ascontiguousarray(node, np.int32)
+        self.priority = np.ascontiguousarray(priority, np.int32)
+        self.start_time = np.ascontiguousarray(start_time, np.int64)
+        self.req = np.ascontiguousarray(np.asarray(req, np.int64).reshape(-1, PREEMPT_REQ))
+        self.n = int(self.node.size)
+        self.c = _BoundPodsC(self.n, 0, _p(self.node), _p(self.priority), _p(self.start_time), _p(self.req))
+
+
+class _PreemptOutC(ctypes.Structure):
+    _fields_ = [("nominated", ctypes.c_int32), ("n_victims", ctypes.c_int32), ("n_potential", ctypes.c_int32),
+                ("n_candidates", ctypes.c_int32), ("victims", ctypes.c_void_p), ("victims_cap", ctypes.c_int32),
+                ("_pad", ctypes.c_int32)]
+
+
+class PreemptOut:
+    def __init__(self, cap: int):
+        self.victims = np.zeros(max(cap, 1), np.int32)
+        self.c = _PreemptOutC(-1, 0, 0, 0, _p(self.victims), int(self.victims.size), 0)
+
+    def result(self) -> tuple:
+        n = min(self.c.n_victims, self.c.victims_cap)
+        return self.c.nominated, [int(v) for v in self.victims[:n]], self.c.n_potential, self.c.n_candidates
+
+
 def repo_root() -> str:
     return os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))

@@ -26,6 +26,7 @@ EXPORTS = [
     "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
+    "ksim_set_bound_pods", "ksim_preempt",
 ]
 
 
@@ -60,6 +61,8 @@ def lib():
         L.ksim_set_pod_seq.argtypes = [vp, i64]
         L.ksim_eval_pod.argtypes = [vp, vp, i32, vp]
         L.ksim_eval_pod_filter.argtypes = [vp, vp, i32, vp]
+        L.ksim_set_bound_pods.argtypes = [vp, vp]
+        L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
         L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
         L.ksim_assume.argtypes = [vp, vp, i32, i32]
         L.ksim_forget.argtypes = [vp, vp, i32, i32]
@@ -183,6 +186,19 @@ class Engine:
                                              None if es is None else es.ctypes.data_as(ctypes.c_void_p),
                                              ctypes.byref(buf2.out)))
         return buf2.result()
+
+    def set_bound_pods(self, bound):
+        """The bound-pod table DefaultPreemption may evict (ksim.abi.BoundPods)."""
+        self._bound_n = bound.n
+        self._chk(lib().ksim_set_bound_pods(self.h, ctypes.byref(bound.c)))
+
+    def preempt(self, pods, index: int, priority: int) -> tuple:
+        """DefaultPreemption PostFilter dry run: (nominated node or -1, victim
+        indices into the bound-pod table, potential nodes, candidates)."""
+        out = abi.PreemptOut(max(getattr(self, "_bound_n", 1), 1))
+        ps = pods.pod_set()
+        self._chk(lib().ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
+        return out.result()
 
     def assume(self, pods, index: int, node: int):
         ps = pods.pod_set()

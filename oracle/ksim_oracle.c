@@ -995,3 +995,122 @@ int ksim_oracle_get_class_count(const ksim_oracle* o, int32_t* out) {
   memcpy(out, o->cnt, 4 * (size_t)o->n * (size_t)(o->n_classes > 0 ? o->n_classes : 0));
   return KSIM_OK;
 }
+
+
+/* ---- PostFilter: DefaultPreemption (preemption.go / default_preemption.go,
+ * v1.26), deterministic: offset 0, candidates in nodeTree order. ----------- */
+typedef struct { int32_t idx, prio; int64_t start; } victim_rec;
+
+static int victim_cmp(const void* a, const void* b) {       /* util.MoreImportantPod, then index */
+  const victim_rec* x = (const victim_rec*)a;
+  const victim_rec* y = (const victim_rec*)b;
+  if (x->prio != y->prio) return x->prio > y->prio ? -1 : 1;
+  if (x->start != y->start) return x->start < y->start ? -1 : 1;
+  return x->idx - y->idx;
+}
+
+/* fitsRequest with the node's requested aggregates adjusted by delta[] / dpods */
+static int fits_adjusted(const ksim_oracle* o, const ksim_pod* p, int32_t node, const int64_t* delta, int64_t dpods) {
+  if (o->num_pods[node] + dpods + 1 > o->alloc_pods[node]) return 0;
+  if (p->req_cpu == 0 && p->req_mem == 0 && p->req_eph == 0 && !(p->flags & KSIM_POD_HAS_SCALAR)) return 1;
+  if (p->req_cpu > o->alloc_cpu[node] - (o->req_cpu[node] + delta[0])) return 0;
+  if (p->req_mem > o->alloc_mem[node] - (o->req_mem[node] + delta[1])) return 0;
+  if (p->req_eph > o->alloc_eph[node] - (o->req_eph[node] + delta[2])) return 0;
+  for (int k = 0; k < o->n_scalar; k++) {
+    const int64_t q = p->scalar_req[k];
+    const size_t ix = (size_t)k * o->n + node;
+    if (q != 0 && q > o->alloc_scalar[ix] - (o->req_scalar[ix] + delta[3 + k])) return 0;
+  }
+  return 1;
+}
+
+/* SelectVictimsOnNode: 1 + victims written to vout (importance order), or 0 */
+static int32_t select_victims(const ksim_oracle* o, const ksim_pod* p, int32_t prio, const ksim_bound_pods* b,
+                              int32_t node, victim_rec* buf, int32_t* vout) {
+  int32_t m = 0;
+  for (int32_t i = 0; i < b->n; i++)
+    if (b->node[i] == node && b->priority[i] < prio) {
+      buf[m].idx = i;
+      buf[m].prio = b->priority[i];
+      buf[m].start = b->start_time[i];
+      m++;
+    }
+  qsort(buf, (size_t)m, sizeof(victim_rec), victim_cmp);
+  int64_t delta[KSIM_PREEMPT_REQ] = {0};
+  for (int32_t j = 0; j < m; j++)
+    for (int k = 0; k < KSIM_PREEMPT_REQ; k++) delta[k] -= b->req[(size_t)buf[j].idx * KSIM_PREEMPT_REQ + k];
+  int64_t dpods = -m;
+  if (!fits_adjusted(o, p, node, delta, dpods)) return 0;
+  int32_t nv = 0;
+  for (int32_t j = 0; j < m; j++) {                      /* reprievePod, most important first */
+    const int64_t* r = b->req + (size_t)buf[j].idx * KSIM_PREEMPT_REQ;
+    for (int k = 0; k < KSIM_PREEMPT_REQ; k++) delta[k] += r[k];
+    dpods++;
+    if (!fits_adjusted(o, p, node, delta, dpods)) {
+      for (int k = 0; k < KSIM_PREEMPT_REQ; k++) delta[k] -= r[k];
+      dpods--;
+      vout[nv++] = buf[j].idx;
+    }
+  }
+  return 1 + nv;
+}
+
+int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32_t prio, const ksim_bound_pods* b,
+                        ksim_preempt_out* out) {
+  if (!o || !ps || !b || !out || pi < 0 || pi >= ps->n_pods) return KSIM_E_INVALID;
+  const ksim_pod* p = &ps->pods[pi];
+  if (p->use_count > 0) return KSIM_E_UNSUPPORTED;
+  const int32_t N = o->n;
+  int fit = -1;
+  for (int f = 0; f < o->prof.n_filter; f++)
+    if (o->prof.filter[f] == KSIM_PL_NODE_RESOURCES_FIT) fit = f;
+  topo_ctx tc;
+  topo_prefilter(o, ps, p, &tc);
+  int32_t* potential = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  int32_t np = 0;
+  for (int32_t node = 0; node < N; node++) {            /* nodesWherePreemptionMightHelp */
+    uint32_t det;
+    if (fit >= 0 && run_filter_plugins(o, ps, p, &tc, node, &det) == (uint8_t)fit) potential[np++] = node;
+  }
+  int32_t want = np * 10 / 100;                         /* GetOffsetAndNumCandidates */
+  if (want < 100) want = 100;
+  if (want > np) want = np;
+  victim_rec* buf = (victim_rec*)malloc(sizeof(victim_rec) * (size_t)(b->n > 0 ? b->n : 1));
+  int32_t* vic = (int32_t*)malloc(sizeof(int32_t) * (size_t)(b->n > 0 ? b->n : 1));
+  int32_t* best_v = (int32_t*)malloc(sizeof(int32_t) * (size_t)(b->n > 0 ? b->n : 1));
+  int32_t ncand = 0, best = -1, best_nv = 0;
+  int32_t best_high = 0;
+  int64_t best_sum = 0, best_start = 0;
+  for (int32_t i = 0; i < np && ncand < want; i++) {
+    const int32_t node = potential[i];
+    const int32_t r = select_victims(o, p, prio, b, node, buf, vic);
+    if (r == 0) continue;
+    ncand++;
+    const int32_t nv = r - 1;
+    /* pickOneNodeForPreemption criteria (no PDBs: no violations anywhere) */
+    const int32_t high = nv ? b->priority[vic[0]] : INT32_MIN;
+    int64_t sum = 0, early = INT64_MAX;
+    for (int32_t j = 0; j < nv; j++) sum += (int64_t)b->priority[vic[j]] + ((int64_t)INT32_MAX + 1);
+    for (int32_t j = 0; j < nv; j++)                    /* GetEarliestPodStartTime */
+      if (b->priority[vic[j]] == high && b->start_time[vic[j]] < early) early = b->start_time[vic[j]];
+    int better = best < 0;
+    if (!better) {
+      if (high != best_high) better = high < best_high;
+      else if (sum != best_sum) better = sum < best_sum;
+      else if (nv != best_nv) better = nv < best_nv;
+      else if (early != best_start) better = early > best_start;
+    }
+    if (better) {
+      best = node; best_nv = nv; best_high = high; best_sum = sum; best_start = early;
+      memcpy(best_v, vic, sizeof(int32_t) * (size_t)nv);
+    }
+  }
+  out->nominated = best;
+  out->n_victims = best >= 0 ? best_nv : 0;
+  out->n_potential = np;
+  out->n_candidates = ncand;
+  if (out->victims)
+    for (int32_t j = 0; j < out->n_victims && j < out->victims_cap; j++) out->victims[j] = best_v[j];
+  free(potential); free(buf); free(vic); free(best_v);
+  return KSIM_OK;
+}

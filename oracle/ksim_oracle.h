@@ -33,6 +33,8 @@ void ksim_oracle_destroy(ksim_oracle* o);
  * (parallelism 1), then assume/bind of the chosen node. */
 int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index,
                       ksim_eval_out* out);
+int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
+                        const ksim_bound_pods* b, ksim_preempt_out* out);
 int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, const uint8_t* ext_fail,
                           const int64_t* ext_score, ksim_eval_out* out);
 

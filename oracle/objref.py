@@ -478,6 +478,67 @@ class ObjScheduler:
         out = [go_div(MAX_NODE_SCORE * s, m) for s in scores]
         return [MAX_NODE_SCORE - s for s in out] if reverse else out
 
+    # ---- DefaultPreemption (preemption.go / default_preemption.go) -------------------
+    def preempt(self, pod: Pod, priority: int, start_time: Dict[str, int], order: Dict[str, int]):
+        """PostFilter for an unschedulable pod, deterministic (offset 0, candidates
+        in nodeTree order).  start_time / order: per bound pod name (order breaks
+        MoreImportantPod ties).  Returns (nominated node name or None, victim names)."""
+        pts, ipa = self.pts_prefilter(pod), self.ipa_prefilter(pod)
+        potential = [ni for ni in self.nodes if self.filter_node(pod, ni, pts, ipa)[0] == "NodeResourcesFit"]
+        want = min(max(len(potential) * 10 // 100, 100), len(potential))
+        want_req = pod_requests(pod)
+        nothing = not any(want_req.values())
+
+        def fits(ni, req, npods):
+            if npods + 1 > ni.alloc.get("pods", 0):
+                return False
+            if nothing:
+                return True
+            return all(want_req.get(r, 0) <= ni.alloc.get(r, 0) - req.get(r, 0)
+                       for r in set(want_req) | {"cpu", "memory", "ephemeral-storage"} if want_req.get(r, 0))
+
+        def select_victims(ni):
+            lower = [pi.pod for pi in ni.pods if pi.pod.priority < priority]
+            lower.sort(key=lambda q: (-q.priority, start_time[q.name], order[q.name]))   # MoreImportantPod
+            req = dict(ni.requested)
+            n = len(ni.pods) - len(lower)
+            for q in lower:
+                for k, v in pod_requests(q).items():
+                    req[k] = req.get(k, 0) - v
+            if not fits(ni, req, n):
+                return None
+            victims = []
+            for q in lower:                        # reprievePod
+                qr = pod_requests(q)
+                for k, v in qr.items():
+                    req[k] = req.get(k, 0) + v
+                n += 1
+                if not fits(ni, req, n):
+                    for k, v in qr.items():
+                        req[k] -= v
+                    n -= 1
+                    victims.append(q)
+            return victims
+
+        cands = []
+        for ni in potential:
+            if len(cands) >= want:
+                break
+            v = select_victims(ni)
+            if v is not None:
+                cands.append((ni, v))
+        if not cands:
+            return None, []
+
+        def criteria(c):                           # pickOneNodeForPreemption (no PDBs)
+            v = c[1]
+            high = v[0].priority if v else -(2 ** 31)
+            total = sum(q.priority + 2 ** 31 for q in v)
+            early = min((start_time[q.name] for q in v if q.priority == high), default=2 ** 63)
+            return (high, total, len(v), -early)
+        best = min(range(len(cands)), key=lambda i: (criteria(cands[i]), i))
+        return cands[best][0].node.name, [q.name for q in cands[best][1]]
+
     # ---- ImageLocality (imagelocality.Score) ----------------------------------------
     def image_locality(self, pod: Pod, node: Node) -> int:
         mb = 1024 * 1024

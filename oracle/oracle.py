@@ -27,6 +27,7 @@ def lib():
         L.ksim_oracle_destroy.argtypes = [vp]
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_cycle_ext.argtypes = [vp, vp, i32, vp, vp, vp]
+        L.ksim_oracle_preempt.argtypes = [vp, vp, i32, i32, vp, vp]
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
         L.ksim_oracle_get_class_count.argtypes = [vp, vp]
@@ -83,6 +84,18 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle cycle failed: {rc}")
         return buf.result()
+
+    def preempt(self, pods, index: int, priority: int, bound) -> tuple:
+        """DefaultPreemption PostFilter (ksim_oracle_preempt).  ``bound`` is a
+        ksim.abi.BoundPods.  Returns (nominated node position or -1, victim indices)."""
+        from ksim import abi
+        out = abi.PreemptOut(max(bound.n, 1))
+        ps = pods.pod_set()
+        rc = lib().ksim_oracle_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(bound.c),
+                                       ctypes.byref(out.c))
+        if rc != 0:
+            raise RuntimeError(f"oracle preempt failed: {rc}")
+        return out.result()
 
     def schedule(self, pods, first=0, count=None, nthreads=1):
         from ksim import abi

@@ -364,3 +364,33 @@ def test_extender_cycles_vs_oracle(pct):
         es, os_ = eng.node_state(), ora.node_state()
         for k in es:
             np.testing.assert_array_equal(es[k], os_[k])
+
+
+@pytest.mark.parametrize("n_nodes", [40, 1500])
+def test_preemption_vs_oracle(n_nodes):
+    """DefaultPreemption dry run on the device (ksim_preempt) against the oracle:
+    nominated node, victims in reprieve order, potential nodes, candidates kept
+    (1,500 nodes: more than 100 candidates, so numCandidates cuts the scan)."""
+    import test_preemption
+    from ksim.encode import encode_cluster, encode_pods
+    from ksim.model import Container, Pod
+    from ksim.preemption import bound_table
+    nodes, bound, start, order = test_preemption.crowded(n_nodes=n_nodes, seed=7)
+    cluster, _ = encode_cluster(nodes, bound)
+    table = bound_table(cluster, bound, start)
+    rng = np.random.default_rng(11)
+    pods = [Pod(f"p{i}", priority=int(rng.choice([0, 5, 50, 500, 5000])),
+                containers=[Container({"cpu": f"{int(rng.integers(10, 400)) * 100}m",
+                                       "memory": f"{int(rng.integers(4, 40))}Gi"})]) for i in range(40)]
+    enc = encode_pods(cluster, pods)
+    prof = _prof(100)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    eng.set_bound_pods(table)
+    many = 0
+    for i, pod in enumerate(pods):
+        got = eng.preempt(enc, i, pod.priority)
+        want = ora.preempt(enc, i, pod.priority, table)
+        assert got == want, f"pod {i}: engine {got[:1]} {got[2:]} oracle {want[:1]} {want[2:]}"
+        many += want[3] >= 100
+    if n_nodes > 1000:
+        assert many > 0

@@ -1,0 +1,54 @@
+"""DefaultPreemption PostFilter: the C oracle's dry run
+(ksim_oracle_preempt) against the object-level restatement (oracle/objref.py
+ObjScheduler.preempt) on crowded clusters with mixed priorities."""
+import numpy as np
+import pytest
+
+from ksim import gen
+from ksim.encode import encode_cluster, encode_pods
+from ksim.model import Container, Pod
+from ksim.preemption import bound_table
+from ksim import profile
+from oracle.objref import ObjScheduler
+from oracle.oracle import Oracle
+
+
+def crowded(n_nodes=40, per_node=6, seed=3):
+    """Config-1 nodes, each holding bound pods of mixed priorities and start times."""
+    rng = np.random.default_rng(seed)
+    nodes, _ = gen.config1_objects(n_nodes=n_nodes, n_pods=1)
+    bound, start, order = [], {}, {}
+    for ni, n in enumerate(nodes):
+        for k in range(per_node):
+            name = f"b{ni}-{k}"
+            p = Pod(name, node_name=n.name, priority=int(rng.choice([0, 10, 100, 1000])),
+                    containers=[Container({"cpu": f"{int(rng.integers(2, 12)) * 100}m",
+                                           "memory": f"{int(rng.integers(1, 6))}Gi"})])
+            bound.append(p)
+            start[name] = int(rng.integers(0, 50))       # ties on purpose
+            order[name] = len(order)
+    return nodes, bound, start, order
+
+
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_preempt_oracle_vs_objref(seed):
+    nodes, bound, start, order = crowded(seed=seed)
+    cluster, _ = encode_cluster(nodes, bound)
+    table = bound_table(cluster, bound, start)
+    rng = np.random.default_rng(seed + 100)
+    pods = [Pod(f"p{i}", priority=int(rng.choice([0, 5, 50, 500, 5000])),
+                containers=[Container({"cpu": f"{int(rng.integers(10, 400)) * 100}m",
+                                       "memory": f"{int(rng.integers(4, 40))}Gi"})]) for i in range(30)]
+    enc = encode_pods(cluster, pods)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    ora = Oracle(cluster, profile.compile_profile(sp))
+    ref = ObjScheduler(nodes, bound, pct=100, seed=sp.tiebreak_seed)
+    nominated = 0
+    for i, pod in enumerate(pods):
+        node, victims, n_pot, n_cand = ora.preempt(enc, i, pod.priority, table)
+        rnode, rvictims = ref.preempt(pod, pod.priority, start, order)
+        got = cluster.node_names[node] if node >= 0 else None
+        assert got == rnode, f"pod {i}"
+        assert [bound[v].name for v in victims] == rvictims, f"pod {i}"
+        nominated += node >= 0
+    assert 0 < nominated < len(pods)

@@ -279,13 +279,15 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
                                                              const int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ chosen_out) {
   __shared__ int32_t s_fb, s_istar, s_sched, s_unsched;
+  const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
+  const int32_t brk = abroken[threadIdx.x];
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
   const int32_t nchain0 = *chain_end;
   if (threadIdx.x == 0) s_fb = nchain0;
   __syncthreads();
-  if ((int32_t)threadIdx.x < nchain0 && abroken[threadIdx.x]) atomicMin(&s_fb, (int32_t)threadIdx.x);
+  if ((int32_t)threadIdx.x < nchain0 && brk) atomicMin(&s_fb, (int32_t)threadIdx.x);
   __syncthreads();
-  batch_commit(c, P, st, gkey, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, awin);
+  batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, awin);
 }
 
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",

@@ -100,15 +100,15 @@ __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict_
                                                      uint64_t* __restrict__ xsend) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_m[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int32_t j = blockIdx.x * 4 + w;
-  const int32_t base = st->cursor;
-  if (base + j >= min(st->end, base + kBatchPods)) return;   // wave-uniform; no block barrier below
+  const int32_t j = blockIdx.x * 4 + w;               // < kBatchPods: the grid is kBatchPods / 4 blocks
   const int32_t per = n_tiles * kTileCand;
   uint64_t* lst = s_m + (size_t)w * (per + (n_tiles + 7) / 8);
   uint8_t* head = reinterpret_cast<uint8_t*>(lst + per);
   const uint64_t* src = cand + (size_t)j * per;
-  for (int x = lane; x < per; x += 64) lst[x] = src[x];
+  for (int x = lane; x < per; x += 64) lst[x] = src[x];   // issued before the state load it does not need
   for (int l = lane; l < n_tiles; l += 64) head[l] = 0;
+  const int32_t base = st->cursor;
+  if (base + j >= min(st->end, base + kBatchPods)) return;   // wave-uniform; no block barrier below
   wave_lds_sync();
   uint64_t mine = 0;                                 // lane t keeps merged key t
   int32_t cnt = 0, complete = 0;
@@ -234,6 +234,13 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int i = threadIdx.x;                   // one pod per thread
+  // the pod's list, count and state in flight together (independent loads;
+  // the buffers hold kBatchPods entries, so no bound check is needed yet)
+  uint64_t lst[kTopT];
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
+  const int cnt0 = topk_cnt[i];
+  const int complete0 = topk_complete[i];
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return;
@@ -241,13 +248,14 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
     s_key[x] = -1;
     s_hold[x] = kBatchPods;
   }
-  const int cnt = i < nb ? topk_cnt[i] : 0;
-  const bool incomplete = i < nb && !topk_complete[i];
+  const int cnt = i < nb ? cnt0 : 0;
+  const bool incomplete = i < nb && !complete0;
   __syncthreads();
+#pragma unroll
   for (int e = 0; e < kTopT; e++) {
     int16_t slot = -1;
     if (e < cnt) {
-      const int32_t node = key_node(topk[(size_t)i * kTopT + e]);
+      const int32_t node = key_node(lst[e]);
       uint32_t h = ((uint32_t)node * 2654435761u) >> (32 - kHashBits);
       while (true) {
         const int32_t prev = atomicCAS(&s_key[h], -1, node);
@@ -259,18 +267,30 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
     s_rep[i][e] = slot;
   }
   __syncthreads();
+  // this pod's slots in registers (selects below, never a dynamic index)
+  int32_t rep[kTopT];
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) rep[e] = s_rep[i][e];
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
   int first = kBatchPods, rounds = 0;
   for (; rounds < kChainRounds; rounds++) {
     if (i == 0) s_first = kBatchPods;
-    if (a >= 0) atomicMin(&s_hold[s_rep[i][a]], i);
+    int32_t ra = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
+    if (a >= 0) atomicMin(&s_hold[ra], i);
     __syncthreads();
+    // every entry's holder at once, then the first one not held by an earlier pod
+    int32_t held[kTopT];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) held[e] = e < cnt ? s_hold[rep[e]] : 0;
     int na = -1;
-    for (int e = 0; e < cnt; e++)
-      if (s_hold[s_rep[i][e]] >= i) { na = e; break; }   // not held by an earlier pod
+#pragma unroll
+    for (int e = kTopT - 1; e >= 0; e--)
+      if (e < cnt && held[e] >= i) na = e;
     __syncthreads();
-    if (a >= 0) s_hold[s_rep[i][a]] = kBatchPods;       // reset for the next round
+    if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
     if (na != a) atomicMin(&s_first, i);
     a = na;
     __syncthreads();
@@ -284,7 +304,10 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   __syncthreads();
   const int32_t nchain = s_cut;
   const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
-  if (i < nb) gkey[i] = (i < nchain && a >= 0) ? topk[(size_t)i * kTopT + a] : 0;
+  uint64_t ga = 0;
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) ga = e == a ? lst[e] : ga;   // register select, no dynamic index
+  if (i < nb) gkey[i] = (i < nchain && a >= 0) ? ga : 0;
   if (i == 0) *chain_end = nchain;
   if (i == 0 && dbg) {
     const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
@@ -308,19 +331,19 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
                                                             uint64_t* __restrict__ pmax) {
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x, k = tid;
+  const uint64_t gk = gkey[k];                       // in flight with the state loads
+  const int32_t nchain = *chain_end;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return;
-  const int32_t nchain = *chain_end;
   const int64_t seq0 = st->pod_seq;
-  const int j = blockIdx.x, k = tid;
   if (j >= nchain) {                                 // block-uniform
     if (tid == 0) pmax[j] = 0;
     return;
   }
   uint64_t v = 0;
   if (k < j) {
-    const uint64_t gk = gkey[k];
     const int32_t local = gk ? key_node(gk) - c.base : -1;
     if (local >= 0 && local < c.n) {
       const ksim_pod& p = P.pods[base + j];
@@ -352,8 +375,10 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPo
                                                              const uint64_t* __restrict__ pmax,
                                                              int32_t* __restrict__ chosen_out) {
   __shared__ int32_t s_istar, s_sched, s_unsched;
+  const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
+  const int32_t nchain = *chain_end;
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
-  batch_commit(c, P, st, gkey, pmax, *chain_end, chosen_out, &s_istar, &s_sched, &s_unsched);
+  batch_commit(c, P, st, g, m, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.

@@ -11,8 +11,10 @@ namespace ksim {
 // threads).  Binds are applied by the shard that owns the node.  awin (ADAPT
 // batch, unsharded): per pod {scan start, cut offset or -1}; the evaluated
 // counts and nextStartNodeIndex follow the committed pods' windows.
+// g_own / m_own: this thread's gkey / pmax entries, loaded by the caller at
+// kernel start (before the state load they do not depend on).
 __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
-                                             const uint64_t* __restrict__ gkey, const uint64_t* __restrict__ pmax,
+                                             uint64_t g_own, uint64_t m_own, const uint64_t* __restrict__ pmax,
                                              int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
                                              int32_t* s_sched, int32_t* s_unsched,
                                              const int32_t* __restrict__ awin = nullptr) {
@@ -28,8 +30,8 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     s_evals = 0;
   }
   __syncthreads();
-  const uint64_t gj = tid < nchain ? __builtin_nontemporal_load(&gkey[tid]) : 0;
-  const uint64_t mj = tid < nchain ? __builtin_nontemporal_load(&pmax[tid]) : 0;
+  const uint64_t gj = tid < nchain ? g_own : 0;
+  const uint64_t mj = tid < nchain ? m_own : 0;
   if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
   __syncthreads();
   const int32_t istar = *s_istar;

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 2
+#define KSIM_ABI_VERSION 3
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -73,6 +73,8 @@ enum ksim_plugin {
   KSIM_PL_INTER_POD_AFFINITY,       /* InterPodAffinity */
   KSIM_PL_BALANCED_ALLOCATION,      /* NodeResourcesBalancedAllocation */
   KSIM_PL_IMAGE_LOCALITY,           /* ImageLocality */
+  KSIM_PL_NETWORK_BANDWIDTH,        /* NetworkBandwidth (the simulator's out-of-tree plugin,
+                                       simulator/scheduler/plugin/networkbandwidth/plugin.go) */
   KSIM_PL_COUNT
 };
 
@@ -90,6 +92,8 @@ enum ksim_plugin {
 
 /* node flags */
 #define KSIM_NODE_UNSCHEDULABLE  1u   /* node.Spec.Unschedulable */
+#define KSIM_NODE_NB_LIMIT       2u   /* NetworkBandwidth: the node-limit annotation is present */
+#define KSIM_NODE_NB_LIMIT_BAD   4u   /* ... and does not parse as a resource.Quantity */
 
 /* pod flags */
 #define KSIM_POD_TOLERATES_UNSCHEDULABLE 1u  /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
@@ -97,6 +101,10 @@ enum ksim_plugin {
 #define KSIM_POD_HAS_SCALAR              4u  /* len(request.ScalarResources) > 0 */
 #define KSIM_POD_HAS_HOST_PORTS          8u  /* ports not compiled to KSIM_USE_NODE_PORT uses -> KSIM_E_UNSUPPORTED */
 #define KSIM_POD_HAS_VOLUMES            16u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
+
+/* pod nb_flags (NetworkBandwidth request annotations) */
+#define KSIM_POD_NB_INGRESS_BAD 1u   /* the ingress request annotation does not parse */
+#define KSIM_POD_NB_EGRESS_BAD  2u   /* the egress request annotation does not parse */
 
 /* pod topo_flags */
 #define KSIM_POD_IPA_SELF_AFFINITY 1u  /* podMatchesAllAffinityTerms(required affinity terms, pod) */
@@ -135,6 +143,18 @@ enum ksim_plugin {
 /* per-pod cycle status */
 #define KSIM_STATUS_SCHEDULED      0
 #define KSIM_STATUS_UNSCHEDULABLE  1   /* FitError: no feasible node */
+#define KSIM_STATUS_ERROR          2   /* a plugin returned a status other than Success /
+                                          Unschedulable: the cycle fails with framework.Error,
+                                          no node is chosen (chosen[] = KSIM_CHOSEN_ERROR) */
+#define KSIM_CHOSEN_ERROR         -2
+
+/* NetworkBandwidth fail_detail (plugin.go:52-102, in the order Filter checks) */
+#define KSIM_NB_INSUFFICIENT   1u   /* Unschedulable: allocated + request > limit */
+#define KSIM_NB_NO_LIMIT       2u   /* Skip: node has no limit annotation       -> Error */
+#define KSIM_NB_LIMIT_BAD      3u   /* Error: node limit does not parse */
+#define KSIM_NB_INGRESS_BAD    4u   /* Error: pod ingress request does not parse */
+#define KSIM_NB_EGRESS_BAD     5u   /* Error: pod egress request does not parse */
+#define KSIM_NB_NO_REQUEST     6u   /* Skip: pod requests no bandwidth          -> Error */
 
 /* ---- cluster snapshot (SoA; one entry per node in nodeTree order) -------- */
 /* Mirrors [upstream] framework.NodeInfo: Allocatable, Requested,
@@ -163,6 +183,9 @@ typedef struct ksim_node_table {
   int32_t _pad1;
   const int32_t* class_count;     /* [n_classes][n_nodes]: pods (or term weights) of each count
                                      class on each node, from the pods already bound */
+  /* NetworkBandwidth (NULL when no node carries the limit annotation), milli-units */
+  const int64_t* nb_limit;        /* the node-limit annotation's quantity */
+  const int64_t* nb_alloc;        /* getNodeAllocatedAmount over the pods already bound */
 } ksim_node_table;
 
 /* Vocabularies the host interned (strings stay on the host). */
@@ -214,7 +237,13 @@ typedef struct ksim_pod {
   int32_t  use_first, use_count;             /* topology uses (PodTopologySpread / InterPodAffinity) */
   int32_t  add_first, add_count;             /* count-class contributions once bound (NodeInfo.AddPod) */
   uint32_t topo_flags;                       /* KSIM_POD_IPA_* */
-  int32_t  _reserved[3];
+  uint32_t nb_flags;                         /* KSIM_POD_NB_* */
+  int32_t  _reserved;
+  int64_t  nb_req;                           /* NetworkBandwidth Filter request (milli): ingress
+                                                + egress request annotations, each falling back
+                                                to the *-bandwidth annotation */
+  int64_t  nb_add;                           /* added to the node's allocated amount once bound
+                                                (request annotations only, unparsable ones skipped) */
 } ksim_pod;
 
 /* Count classes.  The host evaluates every label selector / affinity term
@@ -345,6 +374,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* nodes, const ksim_vo
 /* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
                         int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods);
+/* Read back NetworkBandwidth's allocated amount per node (milli-units). */
+int ksim_get_nb_alloc(ksim_handle* h, int64_t* out);
 /* Read back the count classes [n_classes][n_nodes] (PodTopologySpread / InterPodAffinity state). */
 int ksim_get_class_count(ksim_handle* h, int32_t* out);
 int ksim_get_next_start(ksim_handle* h, int32_t* next_start);

@@ -54,6 +54,10 @@ struct DevCluster {
   int32_t* cnt;                  // [n_classes][n], updated by every bind
   const double* topo_log;        // [n_topo_log] = log(size + 2), host-computed
   const int32_t* col_nvals;      // [n_label_cols] value ids per column (domain table sizes)
+  // NetworkBandwidth (milli-units): the node-limit annotation and the bound
+  // pods' request annotations (getNodeAllocatedAmount), updated by every bind
+  const int64_t* nb_limit;
+  int64_t* nb_alloc;
 };
 
 struct DevPods {
@@ -107,6 +111,8 @@ constexpr int kExtWords = kExtCut + 1;
 struct WinState {
   int32_t cut, kend, nf, evaluated, k, has_soft;
   int32_t nfeas, nign;                   // no-window cycles (K = N): counted by k_filter_score
+  int32_t error;                         // kCycleError*: the cycle fails with framework.Error
+  int32_t _pad;
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
   uint64_t best;                         // TB argmax key
@@ -152,7 +158,10 @@ struct DevEvalOut {
 };
 
 // Normalization kind of a score slot.
-enum NormKind : int32_t { kNormNone = 0, kNormDefault = 1, kNormDefaultReverse = 2, kNormPTS = 3, kNormIPA = 4 };
+enum NormKind : int32_t {
+  kNormNone = 0, kNormDefault = 1, kNormDefaultReverse = 2, kNormPTS = 3, kNormIPA = 4,
+  kNormMinMax = 5   // NetworkBandwidth: IPA's min-max form without the empty-state shortcut
+};
 
 __host__ __device__ __forceinline__ int32_t norm_kind(int plugin) {
   switch (plugin) {
@@ -160,6 +169,7 @@ __host__ __device__ __forceinline__ int32_t norm_kind(int plugin) {
     case KSIM_PL_NODE_AFFINITY: return kNormDefault;
     case KSIM_PL_POD_TOPOLOGY_SPREAD: return kNormPTS;
     case KSIM_PL_INTER_POD_AFFINITY: return kNormIPA;
+    case KSIM_PL_NETWORK_BANDWIDTH: return kNormMinMax;
     default: return kNormNone;
   }
 }
@@ -503,6 +513,51 @@ __device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, c
   return (int64_t)((1 - std) * (double)kMaxNodeScore);
 }
 
+// ---- NetworkBandwidth (simulator/scheduler/plugin/networkbandwidth/plugin.go) --
+// A Filter status other than Success / Unschedulable (its Skip and Error
+// returns) makes [upstream] RunFilterPlugins return framework.Error, and the
+// cycle fails.  Such a node's fail code carries kFailError next to the plugin's
+// filter index; the window decides whether the scan reached it.
+constexpr uint8_t kFailError = 0x80;
+constexpr int32_t kCycleErrorFilter = 1;   // an erroring node inside the scanned window
+constexpr int32_t kCycleErrorScore = 2;    // Score returned Skip / Error for a kept node
+
+__host__ __device__ __forceinline__ bool nb_error_detail(uint32_t d) { return d >= KSIM_NB_NO_LIMIT; }
+__host__ __device__ __forceinline__ bool fail_is_error(uint8_t f) { return (f & kFailError) && f < KSIM_FAIL_EXTENDER; }
+__host__ __device__ __forceinline__ bool prof_has_filter(const ksim_profile& prof, int plugin) {
+  for (int f = 0; f < prof.n_filter; f++)
+    if (prof.filter[f] == plugin) return true;
+  return false;
+}
+__host__ __device__ __forceinline__ bool prof_has_score(const ksim_profile& prof, int plugin) {
+  for (int k = 0; k < prof.n_score; k++)
+    if (prof.score[k] == plugin) return true;
+  return false;
+}
+
+// Filter, plugin.go:52-102, checks in its order (quantities in milli-units)
+__device__ __forceinline__ uint32_t nb_filter(const DevCluster& c, const ksim_pod& p, uint32_t flags, int32_t node) {
+  if (!(flags & KSIM_NODE_NB_LIMIT)) return KSIM_NB_NO_LIMIT;            // :54-57 Skip
+  if (flags & KSIM_NODE_NB_LIMIT_BAD) return KSIM_NB_LIMIT_BAD;          // :58-61 Error
+  if (p.nb_flags & KSIM_POD_NB_INGRESS_BAD) return KSIM_NB_INGRESS_BAD;  // :72-76 Error
+  if (p.nb_flags & KSIM_POD_NB_EGRESS_BAD) return KSIM_NB_EGRESS_BAD;    // :84-88 Error
+  if (p.nb_req == 0) return KSIM_NB_NO_REQUEST;                           // :92-94 Skip
+  return c.nb_alloc[node] + p.nb_req > c.nb_limit[node] ? KSIM_NB_INSUFFICIENT : 0u;   // :97-99
+}
+
+// Score, plugin.go:128-149: (limit - allocated).Value(), resource.Quantity's
+// integer value, which rounds a fraction away from zero
+__device__ __forceinline__ int64_t nb_score(const DevCluster& c, int32_t node) {
+  const int64_t d = c.nb_limit[node] - c.nb_alloc[node];
+  return d >= 0 ? (d + 999) / 1000 : -((-d + 999) / 1000);
+}
+
+// Score returns Skip (no limit annotation) or Error (unparsable limit): the
+// framework's RunScorePlugins fails the cycle
+__host__ __device__ __forceinline__ bool nb_score_error(uint32_t flags) {
+  return !(flags & KSIM_NODE_NB_LIMIT) || (flags & KSIM_NODE_NB_LIMIT_BAD);
+}
+
 // frameworkImpl.RunFilterPlugins (stop at first failure)
 struct DevScratch;
 __device__ __forceinline__ uint32_t pts_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
@@ -556,6 +611,14 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (why) { detail = why; return (uint8_t)f; }
         break;
       }
+      case KSIM_PL_NETWORK_BANDWIDTH: {
+        const uint32_t why = nb_filter(c, p, r.flags, node);
+        if (why) {
+          detail = why;
+          return (uint8_t)(f | (nb_error_detail(why) ? kFailError : 0));
+        }
+        break;
+      }
       default:
         break;
     }
@@ -573,6 +636,7 @@ __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const D
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
     case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(c, P, s, prof, p, r.node) : 0;
     case KSIM_PL_IMAGE_LOCALITY: return p.use_count ? image_locality_score(c, P, p, r.node) : 0;
+    case KSIM_PL_NETWORK_BANDWIDTH: return nb_score_error(r.flags) ? 0 : nb_score(c, r.node);
     default: return 0;   // PodTopologySpread: k_extrema
   }
 }
@@ -952,6 +1016,7 @@ __device__ __forceinline__ void assume_pod(const DevCluster& c, const DevPods& P
   c.nz_cpu[node] += sign * p.nz_cpu;
   c.nz_mem[node] += sign * p.nz_mem;
   c.num_pods[node] += sign;
+  if (p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
 }
 
 __device__ __forceinline__ void store_row_dynamic(const DevCluster& c, const NodeRow& r) {

@@ -87,6 +87,7 @@ struct ksim_handle {
   struct {
     int64_t *req_cpu, *req_mem, *req_eph, *req_scalar, *nz_cpu, *nz_mem;
     int32_t *num_pods, *cnt;
+    int64_t* nb_alloc;
   } init{};
   std::vector<int32_t> col_nvals;       // host copy (pod validation)
 
@@ -275,9 +276,17 @@ bool adapt_mode(const ksim_handle* h) {
   return num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->dc.n_total) < h->dc.n_total;
 }
 
+// NetworkBandwidth in the profile (Filter or Score)
+bool profile_nb(const ksim_profile& p) {
+  return prof_has_filter(p, KSIM_PL_NETWORK_BANDWIDTH) || prof_has_score(p, KSIM_PL_NETWORK_BANDWIDTH);
+}
+
 bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
   const ksim_profile& prof = h->prof;
   if (p.use_count > 0) return false;
+  // NetworkBandwidth runs on the per-pod path (its error statuses end cycles),
+  // and so do pods that add to a node's allocated bandwidth
+  if (profile_nb(prof) || p.nb_add != 0) return false;
   if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
   int64_t acc = 0;
   for (int k = 0; k < prof.n_score; k++) {
@@ -585,6 +594,8 @@ int shard_run_perpod(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) 
 
 // A sharded run: batchable stretches on the batch protocol, the rest cycle by cycle.
 int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t count) {
+  if (profile_nb(hs[0]->prof))
+    return set_err(hs[0], KSIM_E_UNSUPPORTED, "NetworkBandwidth profiles run on unsharded handles");
   return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool) {
     return batch ? shard_run(hs, a, b) : shard_run_perpod(hs, a, b);
   });
@@ -795,6 +806,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   UP(cnt, t->class_count, 4 * N * (size_t)t->n_classes);
   UP(topo_log, v->topo_log, 8 * (size_t)v->n_topo_log);
   UP(col_nvals, col_nvals.data(), 4 * col_nvals.size());
+  UP(nb_limit, t->nb_limit, 8 * N);                      // zeros when no node has the annotation
+  UP(nb_alloc, t->nb_alloc, 8 * N);
 #undef UP
   h->col_nvals = col_nvals;
   h->dc = c;
@@ -825,6 +838,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     SNAP(nz_mem, 8 * N);
     SNAP(num_pods, 4 * N);
     SNAP(cnt, 4 * N * (size_t)t->n_classes);
+    SNAP(nb_alloc, 8 * N);
 #undef SNAP
   }
 
@@ -892,6 +906,14 @@ int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int6
   if (nz_cpu) HIPCHK(h, hipMemcpy(nz_cpu, h->dc.nz_cpu, 8 * N, hipMemcpyDeviceToHost));
   if (nz_mem) HIPCHK(h, hipMemcpy(nz_mem, h->dc.nz_mem, 8 * N, hipMemcpyDeviceToHost));
   if (num_pods) HIPCHK(h, hipMemcpy(num_pods, h->dc.num_pods, 4 * N, hipMemcpyDeviceToHost));
+  return KSIM_OK;
+}
+
+int ksim_get_nb_alloc(ksim_handle* h, int64_t* out) {
+  if (!h || !h->has_cluster || !out) return set_err(h, KSIM_E_INVALID, "cluster not set / null out");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(out, h->dc.nb_alloc, 8 * (size_t)h->dc.n, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
 
@@ -993,10 +1015,21 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
 }
 
 // Copy one compat cycle's per-node outputs and scalars to the caller.
+// The device marks a node whose Filter status was an error with kFailError
+// next to the plugin index; the ABI reports the plugin index alone (the cycle
+// status says the cycle failed).
+static void strip_fail_errors(uint8_t* f, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (fail_is_error(f[i])) f[i] &= (uint8_t)~kFailError;
+}
+
 static int copy_eval_out(ksim_handle* h, ksim_eval_out* out) {
   const size_t N = (size_t)h->dc.n;
   const int S = h->prof.n_score;
-  if (out->fail_plugin) HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+  if (out->fail_plugin) {
+    HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+    strip_fail_errors(out->fail_plugin, N);
+  }
   if (out->fail_detail) HIPCHK(h, hipMemcpy(out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
   if (out->scored) HIPCHK(h, hipMemcpy(out->scored, h->eo.scored, N, hipMemcpyDeviceToHost));
   if (out->raw && S) HIPCHK(h, hipMemcpy(out->raw, h->eo.raw, 8 * N * S, hipMemcpyDeviceToHost));
@@ -1021,6 +1054,8 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksi
   if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
     return set_err(h, KSIM_E_INVALID, "bad pod set / index");
   if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  if (is_sharded(h) && profile_nb(h->prof))
+    return set_err(h, KSIM_E_UNSUPPORTED, "NetworkBandwidth profiles run on unsharded handles");
   HIPCHK(h, hipSetDevice(h->device));
   h->ext_pending = false;
   DevPods P;
@@ -1046,7 +1081,10 @@ int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const size_t N = (size_t)h->dc.n;
-  if (out->fail_plugin) HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+  if (out->fail_plugin) {
+    HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+    strip_fail_errors(out->fail_plugin, N);
+  }
   if (out->fail_detail) HIPCHK(h, hipMemcpy(out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
   WinState w;
   DevState st;
@@ -1054,8 +1092,8 @@ int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
   const int32_t n = h->dc.n;
   const int32_t processed = w.cut < n ? w.cut : n;
-  out->chosen = -1;
-  out->status = 0;
+  out->chosen = w.error ? KSIM_CHOSEN_ERROR : -1;
+  out->status = w.error ? KSIM_STATUS_ERROR : 0;
   out->n_feasible = w.nf;
   out->n_evaluated = w.evaluated;
   out->n_processed = processed;
@@ -1330,6 +1368,7 @@ int ksim_reset_cluster(ksim_handle* h) {
   HIPCHK(h, hipMemcpyAsync(c.num_pods, h->init.num_pods, 4 * N, hipMemcpyDeviceToDevice, h->stream));
   if (c.n_classes)
     HIPCHK(h, hipMemcpyAsync(c.cnt, h->init.cnt, 4 * N * c.n_classes, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.nb_alloc, h->init.nb_alloc, 8 * N, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->st, 0, sizeof(DevState), h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return KSIM_OK;
@@ -1520,6 +1559,8 @@ extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_
     return set_err(h, KSIM_E_INVALID, "bad pod set / index");
   if (!h->pre.off) return set_err(h, KSIM_E_INVALID, "ksim_set_bound_pods first");
   if (is_sharded(h)) return set_err(h, KSIM_E_UNSUPPORTED, "preemption runs on unsharded handles");
+  if (prof_has_filter(h->prof, KSIM_PL_NETWORK_BANDWIDTH))
+    return set_err(h, KSIM_E_UNSUPPORTED, "preemption dry runs re-run Fit only, not NetworkBandwidth");
   if (ps->pods[pod_index].use_count > 0)
     return set_err(h, KSIM_E_UNSUPPORTED, "preemption for pods with topology / port / image uses");
   if ((rc = validate_pod(h, ps, pod_index))) return rc;

@@ -167,8 +167,9 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
       int64_t mx = gmax > 0 ? gmax : 0;
       return mx == 0 ? (int64_t)kMaxNodeScore : (int64_t)kMaxNodeScore * (mx + gmin - v) / mx;
     }
-    case kNormIPA: {
-      if (!ipa_nonempty) return v;
+    case kNormIPA:
+    case kNormMinMax: {
+      if (kind == kNormIPA && !ipa_nonempty) return v;
       const int64_t diff = gmax - gmin;
       double f = 0;
       if (diff > 0) f = (double)kMaxNodeScore * ((double)(v - gmin) / (double)diff);
@@ -434,9 +435,12 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   // filter pass stands (nextStartNodeIndex moved before the extenders ran);
   // the kept nodes an extender dropped are marked and the list recounted.
   const bool ext = s.ext_fail != nullptr;
-  int32_t cut, nf;
+  const bool nb_filter_on = prof_has_filter(prof, KSIM_PL_NETWORK_BANDWIDTH);
+  const bool nb_score_on = prof_has_score(prof, KSIM_PL_NETWORK_BANDWIDTH);
+  int32_t cut, nf, error = 0;
   if (ext) {
     cut = win->cut;
+    error = win->error;                            // the filter pass already failed
     const int32_t kend0 = cut < N ? cut : N;
     int32_t kept = 0;
     for (int32_t r = tid; r < kend0; r += kFinalThreads) {   // the stride the loops below use
@@ -477,6 +481,29 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     __syncthreads();
     cut = s_cut;
     nf = total < K ? total : K;
+    if (nb_filter_on) {
+      // the first node in scan order whose Filter status was an error; the
+      // scan fails there if it comes before the (K+1)-th feasible node
+      int64_t first = N;
+      for (int32_t r = lo; r < hi; r++) {
+        int32_t node = start + r;
+        if (node >= N) node -= N;
+        if (fail_is_error(s.fail[node])) { first = r; break; }
+      }
+      __shared__ int64_t sh64[kFinalWaves];
+      const int32_t err = (int32_t)block_min_i64(first, sh64);
+      if (err < (cut < N ? cut + 1 : N)) {
+        error = kCycleErrorFilter;
+        int32_t before = 0;                        // feasible nodes found before it
+        for (int32_t r = lo; r < hi && r < err; r++) {
+          int32_t node = start + r;
+          if (node >= N) node -= N;
+          before += s.fail[node] == KSIM_PASSED;
+        }
+        nf = block_sum_i32_nw<kFinalWaves>(before, sh32);
+        cut = err;                                 // processed = the nodes before it
+      }
+    }
   }
   const int32_t kend = cut < N ? cut : N;
   const int32_t evaluated = cut < N ? cut + 1 : N;
@@ -488,9 +515,18 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
       s.detail[node] = 0;
     }
   }
+  if (!error && nb_score_on && nf > 1) {
+    int32_t bad = 0;                               // kept nodes whose Score returns Skip / Error
+    for (int32_t r = tid; r < kend; r += kFinalThreads) {
+      int32_t node = start + r;
+      if (node >= N) node -= N;
+      bad += s.fail[node] == KSIM_PASSED && nb_score_error(c.flags[node]);
+    }
+    if (block_sum_i32_nw<kFinalWaves>(bad, sh32) > 0) error = kCycleErrorScore;
+  }
   bool any_soft = false;
   for (int i = 0; i < p.use_count; i++) any_soft = any_soft || P.uses[p.use_first + i].kind == KSIM_USE_PTS_SOFT;
-  const bool has_soft = nf > 1 && any_soft;
+  const bool has_soft = !error && nf > 1 && any_soft;
   if (has_soft) {
     int32_t nign = 0;
     for (int32_t r = tid; r < kend; r += kFinalThreads) {
@@ -533,6 +569,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     win->has_soft = has_soft;
     win->k = K;
     win->best = 0;
+    win->error = error;
   }
 }
 
@@ -600,7 +637,7 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
     __syncthreads();
     if (nf <= 1) return;                          // no scoring
   } else {
-    if (win->nf <= 1) return;                     // no scoring
+    if (win->nf <= 1 || win->error) return;       // no scoring
     has_soft = win->has_soft != 0;
     if (tid < nu) {
       s_use[tid] = P.uses[p.use_first + tid];
@@ -678,7 +715,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_pr
   const int32_t nf = win->nf;
   uint64_t key = 0;
   if (node < N) {
-    const bool kept = nf >= 1 && kept_node(c, s, node, st->next_start, win->kend);
+    const bool kept = nf >= 1 && !win->error && kept_node(c, s, node, st->next_start, win->kend);
     if (kept && nf > 1) {
       const bool ign = win->has_soft && s.ign[node];
       const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
@@ -758,8 +795,8 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const int32_t N = c.n, nf = win->nf, cut = win->cut;
-  const int32_t chosen = win->best ? key_node(win->best) : -1;   // unsharded: base == 0
+  const int32_t N = c.n, nf = win->nf, cut = win->cut, error = win->error;
+  const int32_t chosen = win->best && !error ? key_node(win->best) : -1;   // unsharded: base == 0
   const ksim_pod& p = P.pods[pi];
   int32_t ns = st->next_start + (cut < N ? cut : N);
   ns %= N;
@@ -771,9 +808,10 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   } else {
     st->unschedulable += 1;
   }
-  if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : -1;
-  st->chosen = chosen;
-  st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : KSIM_STATUS_UNSCHEDULABLE;
+  if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : error ? KSIM_CHOSEN_ERROR : -1;
+  st->chosen = chosen >= 0 ? chosen : error ? KSIM_CHOSEN_ERROR : -1;
+  st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : error ? KSIM_STATUS_ERROR : KSIM_STATUS_UNSCHEDULABLE;
+  win->error = 0;
   st->n_feasible = nf;
   st->n_evaluated = win->evaluated;
   st->n_processed = cut < N ? cut : N;
@@ -1089,8 +1127,12 @@ void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent
 
 // K = N (percentageOfNodesToScore >= 100 or fewer than 100 nodes): no
 // window, so the window state comes from the filter pass (no k_window).
+// NetworkBandwidth's error statuses are resolved in k_window, so its profiles
+// always take the windowed cycle.
 void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
-  const bool nowin = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n) >= a.c.n;
+  const bool nowin = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n) >= a.c.n &&
+                     !prof_has_filter(a.prof, KSIM_PL_NETWORK_BANDWIDTH) &&
+                     !prof_has_score(a.prof, KSIM_PL_NETWORK_BANDWIDTH);
   if (compat) {
     if (nowin) launch_cycle_t<true, true>(a, stream, topo, evs);
     else launch_cycle_t<true, false>(a, stream, topo, evs);

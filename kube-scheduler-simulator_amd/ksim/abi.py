@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -51,6 +51,7 @@ PLUGINS = [
     "InterPodAffinity",
     "NodeResourcesBalancedAllocation",
     "ImageLocality",
+    "NetworkBandwidth",
 ]
 PLUGIN_ID = {n: i for i, n in enumerate(PLUGINS)}
 PL_NODE_UNSCHEDULABLE = 0
@@ -63,6 +64,7 @@ PL_POD_TOPOLOGY_SPREAD = 13
 PL_INTER_POD_AFFINITY = 14
 PL_BALANCED_ALLOCATION = 15
 PL_IMAGE_LOCALITY = 16
+PL_NETWORK_BANDWIDTH = 17
 
 EFFECT_NONE = 0
 EFFECT_NO_SCHEDULE = 1
@@ -77,12 +79,18 @@ RES_EPHEMERAL = 2
 RES_SCALAR0 = 3
 
 NODE_UNSCHEDULABLE = 1
+NODE_NB_LIMIT = 2
+NODE_NB_LIMIT_BAD = 4
 
 POD_TOLERATES_UNSCHEDULABLE = 1
 POD_HAS_REQUIRED_AFFINITY = 2
 POD_HAS_SCALAR = 4
 POD_HAS_HOST_PORTS = 8
 POD_HAS_VOLUMES = 16
+
+# pod nb_flags
+POD_NB_INGRESS_BAD = 1
+POD_NB_EGRESS_BAD = 2
 
 # pod topo_flags
 POD_IPA_SELF_AFFINITY = 1
@@ -132,6 +140,16 @@ FIT_SCALAR0 = 16
 
 STATUS_SCHEDULED = 0
 STATUS_UNSCHEDULABLE = 1
+STATUS_ERROR = 2
+CHOSEN_ERROR = -2
+
+# NetworkBandwidth fail details
+NB_INSUFFICIENT = 1
+NB_NO_LIMIT = 2
+NB_LIMIT_BAD = 3
+NB_INGRESS_BAD = 4
+NB_EGRESS_BAD = 5
+NB_NO_REQUEST = 6
 
 # ---- numpy dtypes (align=True reproduces the C layout) -------------------
 LABEL_EXPR_DTYPE = np.dtype(
@@ -149,7 +167,8 @@ POD_DTYPE = np.dtype(
      ("req_term_first", "<i4"), ("req_term_count", "<i4"),
      ("pref_term_first", "<i4"), ("pref_term_count", "<i4"),
      ("use_first", "<i4"), ("use_count", "<i4"), ("add_first", "<i4"), ("add_count", "<i4"),
-     ("topo_flags", "<u4"), ("_reserved", "<i4", (3,))], align=True)
+     ("topo_flags", "<u4"), ("nb_flags", "<u4"), ("_reserved", "<i4"),
+     ("nb_req", "<i8"), ("nb_add", "<i8")], align=True)
 TOPO_USE_DTYPE = np.dtype(
     [("cls", "<i4"), ("arg", "<i4"), ("col", "<u2"), ("kind", "u1"), ("flags", "u1"), ("_pad", "<i4")],
     align=True)
@@ -177,6 +196,7 @@ class NodeTable(ctypes.Structure):
         ("taints", ctypes.c_void_p), ("labels", ctypes.c_void_p),
         ("n_classes", ctypes.c_int32), ("_pad1", ctypes.c_int32),
         ("class_count", ctypes.c_void_p),
+        ("nb_limit", ctypes.c_void_p), ("nb_alloc", ctypes.c_void_p),
     ]
 
 

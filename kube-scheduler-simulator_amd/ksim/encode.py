@@ -12,7 +12,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import abi
+from . import abi, netbw
 from .model import (Node, Pod, Taint, Toleration, quantity_milli_value, quantity_value)
 from .topology import TopologyError, TopologyIndex, pod_uses, register_pod_classes, topo_log_table
 
@@ -150,6 +150,10 @@ class EncodedCluster:
     topo: Optional[TopologyIndex] = None
     class_count: Optional[np.ndarray] = None          # [C][N] int32
     topo_log: Optional[np.ndarray] = None             # [N+1] float64
+    # NetworkBandwidth (ksim/netbw.py), milli-units
+    nb_limit: Optional[np.ndarray] = None             # [N] int64
+    nb_alloc: Optional[np.ndarray] = None             # [N] int64
+    nb_args: netbw.NetworkBandwidthArgs = field(default_factory=netbw.NetworkBandwidthArgs)
 
     def __post_init__(self):
         if self.topo is None:
@@ -158,6 +162,10 @@ class EncodedCluster:
             self.class_count = self.topo.class_count_array()
         if self.topo_log is None:
             self.topo_log = topo_log_table(self.n_nodes)
+        if self.nb_limit is None:
+            self.nb_limit = np.zeros(self.n_nodes, np.int64)
+        if self.nb_alloc is None:
+            self.nb_alloc = np.zeros(self.n_nodes, np.int64)
 
     def refresh_classes(self) -> None:
         """Re-materialise class_count after classes were registered."""
@@ -178,6 +186,8 @@ class EncodedCluster:
             setattr(t, f, abi._p(getattr(self, f)))
         t.n_classes = int(self.class_count.shape[0])
         t.class_count = abi._p(self.class_count)
+        t.nb_limit = abi._p(self.nb_limit)
+        t.nb_alloc = abi._p(self.nb_alloc)
         return t
 
     def vocab(self) -> abi.Vocab:
@@ -201,7 +211,7 @@ class EncodedCluster:
         c = copy.copy(self)
         c.n_nodes = count
         for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "req_eph",
-                  "nz_cpu", "nz_mem", "num_pods", "flags"):
+                  "nz_cpu", "nz_mem", "num_pods", "flags", "nb_limit", "nb_alloc"):
             setattr(c, f, np.ascontiguousarray(getattr(self, f)[sl]))
         for f in ("alloc_scalar", "req_scalar", "taints", "labels", "class_count"):
             setattr(c, f, np.ascontiguousarray(getattr(self, f)[:, sl]))
@@ -223,7 +233,7 @@ class EncodedCluster:
         import copy
         c = copy.copy(self)
         for f in ("req_cpu", "req_mem", "req_eph", "req_scalar", "nz_cpu", "nz_mem", "num_pods",
-                  "class_count"):
+                  "class_count", "nb_alloc"):
             setattr(c, f, getattr(self, f).copy())
         return c
 
@@ -274,7 +284,8 @@ def _parse_int64(s: str) -> Optional[int]:
 
 def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
                    extra_scalar: Sequence[str] = (),
-                   namespaces: Optional[Dict[str, Dict[str, str]]] = None) -> Tuple[EncodedCluster, List[int]]:
+                   namespaces: Optional[Dict[str, Dict[str, str]]] = None,
+                   nb_args: Optional[netbw.NetworkBandwidthArgs] = None) -> Tuple[EncodedCluster, List[int]]:
     """Encode nodes in nodeTree order.  Returns (cluster, order) where
     order[position] = index into ``nodes``.  ``bound_pods`` (spec.nodeName set)
     are added to their node's aggregates like NodeInfo.AddPod (and to the
@@ -347,6 +358,17 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
     def col(name):
         return np.array([_res(n.allocatable, name) for n in ns], np.int64)
 
+    nb_args = nb_args or netbw.NetworkBandwidthArgs()
+    flags = np.array([abi.NODE_UNSCHEDULABLE if n.unschedulable else 0 for n in ns], np.uint32)
+    nb_limit = np.zeros(N, np.int64)
+    try:
+        for pos, n in enumerate(ns):
+            fl, q = netbw.node_limit(n.annotations, nb_args)
+            flags[pos] |= fl
+            nb_limit[pos] = q
+    except netbw.QuantityError as e:
+        raise EncodeError(str(e)) from e
+
     c = EncodedCluster(
         n_nodes=N, n_scalar=S,
         alloc_cpu=col("cpu"), alloc_mem=col("memory"), alloc_eph=col("ephemeral-storage"),
@@ -356,11 +378,12 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
         req_scalar=np.zeros((S, N), np.int64),
         nz_cpu=np.zeros(N, np.int64), nz_mem=np.zeros(N, np.int64),
         num_pods=np.zeros(N, np.int32),
-        flags=np.array([abi.NODE_UNSCHEDULABLE if n.unschedulable else 0 for n in ns], np.uint32),
+        flags=flags,
         taints=taints, labels=labels, taint_effect=effect, label_col_offset=offs,
         label_num=np.array(nums, np.int64), label_num_ok=np.array(oks, np.uint8),
         node_names=[n.name for n in ns], label_keys=keys, label_values=values,
         taint_vocab=tvocab, scalar_names=scalar,
+        nb_limit=nb_limit, nb_alloc=np.zeros(N, np.int64), nb_args=nb_args,
     )
     c.topo = TopologyIndex(N, namespaces)
     pos_of = {name: i for i, name in enumerate(c.node_names)}
@@ -383,6 +406,10 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
         c.nz_cpu[i] += nz[0]
         c.nz_mem[i] += nz[1]
         c.num_pods[i] += 1
+        try:
+            c.nb_alloc[i] += netbw.pod_allocated(p.annotations, nb_args)
+        except netbw.QuantityError as e:
+            raise EncodeError(str(e)) from e
     c.refresh_classes()
     return c, order
 
@@ -541,6 +568,11 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         rec["add_first"], rec["add_count"] = len(adds), len(a)
         adds.extend(a)
         rec["topo_flags"] = tflags
+        try:
+            rec["nb_flags"], rec["nb_req"] = netbw.pod_request(p.annotations, cluster.nb_args)
+            rec["nb_add"] = netbw.pod_allocated(p.annotations, cluster.nb_args)
+        except netbw.QuantityError as e:
+            raise EncodeError(f"pod {p.namespace}/{p.name}: {e}") from e
         names.append((p.namespace, p.name))
     exprs = np.array(b.exprs, abi.LABEL_EXPR_DTYPE) if b.exprs else np.zeros(0, abi.LABEL_EXPR_DTYPE)
     terms = np.zeros(len(b.terms), abi.TERM_DTYPE)

@@ -20,7 +20,7 @@ _LIB = None
 # Exported symbols declared in include/ksim_engine.h (checked by tests).
 EXPORTS = [
     "ksim_abi_version", "ksim_abi_sizeof", "ksim_create", "ksim_destroy", "ksim_last_error",
-    "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_class_count", "ksim_get_next_start",
+    "ksim_set_profile", "ksim_set_cluster", "ksim_get_node_state", "ksim_get_class_count", "ksim_get_nb_alloc", "ksim_get_next_start",
     "ksim_set_next_start", "ksim_set_pod_seq", "ksim_eval_pod", "ksim_assume", "ksim_forget",
     "ksim_load_pods", "ksim_schedule_loaded", "ksim_schedule_batch", "ksim_reset_cluster",
     "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
@@ -56,6 +56,7 @@ def lib():
         L.ksim_set_cluster.argtypes = [vp, vp, vp]
         L.ksim_get_node_state.argtypes = [vp] * 7
         L.ksim_get_class_count.argtypes = [vp, vp]
+        L.ksim_get_nb_alloc.argtypes = [vp, vp]
         L.ksim_get_next_start.argtypes = [vp, vp]
         L.ksim_set_next_start.argtypes = [vp, i32]
         L.ksim_set_pod_seq.argtypes = [vp, i64]
@@ -163,6 +164,12 @@ class Engine:
         """Count classes [n_classes][n_nodes] as the device holds them now."""
         out = np.zeros((self.n_classes, self.n_nodes), np.int32)
         self._chk(lib().ksim_get_class_count(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    def nb_alloc(self) -> np.ndarray:
+        """NetworkBandwidth allocated amount per node (milli-units), as the device holds it."""
+        out = np.zeros(self.n_nodes, np.int64)
+        self._chk(lib().ksim_get_nb_alloc(self.h, out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
     def eval_pod(self, pods, index: int) -> dict:

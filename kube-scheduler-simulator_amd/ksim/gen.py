@@ -251,3 +251,57 @@ def config3(n_nodes: int = 10000, pods_per_node: int = 10, n_incoming: int = 100
     nodes, bound, incoming = config3_objects(n_nodes, pods_per_node, n_incoming, seed, zone_anti_every)
     cluster, _ = encode_cluster(nodes, bound)
     return cluster, encode_pods(cluster, incoming)
+
+
+# ---- NetworkBandwidth scenarios (the simulator's out-of-tree plugin) ----------
+NB_LIMITS = ["1G", "2G", "5G", "10G", "1Gi", "2500M", "750M", "1500000k"]
+NB_REQS = ["50M", "100M", "250M", "400M", "1G", "120Mi", "0.5G", "1500m", "1e8"]
+
+
+def netbw_objects(n_nodes: int = 120, n_pods: int = 300, seed: int = SEEDS[1] ^ 0x4E42,
+                  node_errors: bool = False, pod_errors: bool = False,
+                  n_bound: int = 60) -> Tuple[List[Node], List[Pod], List[Pod]]:
+    """config1-shaped nodes with network-limit annotations, bound pods holding
+    request annotations (the nodes' allocated amounts), and pending pods whose
+    requests come from the request annotations or the *-bandwidth fallbacks.
+    ``node_errors``: some nodes lack the limit or carry an unparsable one;
+    ``pod_errors``: some pods request nothing or carry an unparsable request."""
+    from .netbw import EGRESS_BANDWIDTH, INGRESS_BANDWIDTH, NetworkBandwidthArgs
+    a = NetworkBandwidthArgs()
+    nodes, pods = config1_objects(n_nodes, n_pods + n_bound, seed)
+    r = Rng(seed ^ 0xB0)
+    for n in nodes:
+        if node_errors and r.chance(4):
+            continue                                         # no limit annotation
+        if node_errors and r.chance(3):
+            n.annotations[a.node_limit_annotation] = "ten-gigabit"
+        else:
+            n.annotations[a.node_limit_annotation] = NB_LIMITS[r.below(len(NB_LIMITS))]
+    bound, pending = pods[:n_bound], pods[n_bound:]
+    for p in bound:
+        p.node_name = nodes[r.below(n_nodes)].name
+        p.tolerations, p.required_terms, p.preferred_terms = [], None, []
+        if r.chance(70):
+            p.annotations[a.ingress_request_annotation] = NB_REQS[r.below(len(NB_REQS))]
+        if r.chance(50):
+            p.annotations[a.egress_request_annotation] = NB_REQS[r.below(len(NB_REQS))]
+        if r.chance(10):
+            p.annotations[a.egress_request_annotation] = "lots"      # skipped by getNodeAllocatedAmount
+        if r.chance(20):
+            p.annotations[INGRESS_BANDWIDTH] = NB_REQS[r.below(len(NB_REQS))]   # not counted as allocated
+    for p in pending:
+        k = r.below(4)
+        if k == 0:
+            p.annotations[a.ingress_request_annotation] = NB_REQS[r.below(len(NB_REQS))]
+        elif k == 1:
+            p.annotations[INGRESS_BANDWIDTH] = NB_REQS[r.below(len(NB_REQS))]
+        elif k == 2:
+            p.annotations[a.egress_request_annotation] = NB_REQS[r.below(len(NB_REQS))]
+            p.annotations[INGRESS_BANDWIDTH] = NB_REQS[r.below(len(NB_REQS))]
+        else:
+            p.annotations[EGRESS_BANDWIDTH] = NB_REQS[r.below(len(NB_REQS))]
+        if pod_errors and r.chance(3):
+            p.annotations = {}                                 # requests nothing: Skip -> Error
+        elif pod_errors and r.chance(3):
+            p.annotations[a.egress_request_annotation] = "fast"
+    return nodes, bound, pending

@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Tuple
 
 from . import profile as prof_mod
 from .model import Node, Pod, node_from_dict, pod_from_dict
+from .netbw import NetworkBandwidthArgs
 
 
 @dataclass
@@ -103,6 +104,8 @@ def profile_from_config(p: dict) -> prof_mod.SchedulerProfile:
         elif name == "InterPodAffinity":
             if args.get("hardPodAffinityWeight") is not None:
                 sp.hard_pod_affinity_weight = int(args["hardPodAffinityWeight"])
+        elif name == "NetworkBandwidth":
+            sp.network_bandwidth = NetworkBandwidthArgs.from_config(args)
     sp.percentage_of_nodes_to_score = 0      # non-profile fields are reset to the defaults
     return sp
 
@@ -151,7 +154,7 @@ def load(doc: dict) -> Snapshot:
 def encode(snap: Snapshot, profile_index: int = 0):
     """(EncodedCluster, EncodedPods of the pending queue, compiled profile)."""
     from .encode import encode_cluster, encode_pods
-    cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces)
-    pods = encode_pods(cluster, snap.pending)
     sp = snap.profiles[profile_index][1]
+    cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces, nb_args=sp.network_bandwidth)
+    pods = encode_pods(cluster, snap.pending)
     return cluster, pods, prof_mod.compile_profile(sp, cluster.scalar_names)

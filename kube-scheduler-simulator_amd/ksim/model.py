@@ -200,6 +200,7 @@ class Node:
     allocatable: Dict[str, str] = field(default_factory=dict)
     unschedulable: bool = False
     images: List[Tuple[List[str], int]] = field(default_factory=list)   # status.images: (names, sizeBytes)
+    annotations: Dict[str, str] = field(default_factory=dict)
 
 
 @dataclass
@@ -222,6 +223,7 @@ class Pod:
     pod_affinity_preferred: List[WeightedPodAffinityTerm] = field(default_factory=list)
     pod_anti_affinity_required: List[PodAffinityTerm] = field(default_factory=list)
     pod_anti_affinity_preferred: List[WeightedPodAffinityTerm] = field(default_factory=list)
+    annotations: Dict[str, str] = field(default_factory=dict)
 
     def has_pod_affinity(self) -> bool:
         """PodInfo: pods with any (anti)affinity term (NodeInfo.PodsWithAffinity)."""
@@ -276,6 +278,7 @@ def node_from_dict(d: dict) -> Node:
         allocatable={k: str(v) for k, v in (status.get("allocatable") or {}).items()},
         unschedulable=bool(spec.get("unschedulable", False)),
         images=[(list(im.get("names") or []), int(im.get("sizeBytes") or 0)) for im in (status.get("images") or [])],
+        annotations={k: str(v) for k, v in (md.get("annotations") or {}).items()},
     )
 
 
@@ -316,4 +319,5 @@ def pod_from_dict(d: dict) -> Pod:
                                     (paa.get("requiredDuringSchedulingIgnoredDuringExecution") or [])],
         pod_anti_affinity_preferred=[_weighted(t) for t in
                                      (paa.get("preferredDuringSchedulingIgnoredDuringExecution") or [])],
+        annotations={k: str(v) for k, v in (md.get("annotations") or {}).items()},
     )

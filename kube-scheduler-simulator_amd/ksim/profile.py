@@ -15,6 +15,7 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
 from . import abi
+from .netbw import NetworkBandwidthArgs
 
 SUFFIX = "Wrapped"                    # wrappedplugin.go:239 pluginSuffix
 
@@ -153,6 +154,7 @@ class SchedulerProfile:
     fit: FitArgs = field(default_factory=FitArgs)
     balanced: BalancedAllocationArgs = field(default_factory=BalancedAllocationArgs)
     hard_pod_affinity_weight: int = 1
+    network_bandwidth: NetworkBandwidthArgs = field(default_factory=NetworkBandwidthArgs)
     percentage_of_nodes_to_score: int = 0      # simulator forces the default (scheduler.go:231-241)
     tiebreak_seed: int = 0x4B53494D
 
@@ -185,7 +187,8 @@ def _res_id(name: str, scalar_names: List[str]) -> int:
 
 SUPPORTED_FILTER = set(abi.PLUGINS)
 SUPPORTED_SCORE = {"NodeResourcesBalancedAllocation", "ImageLocality", "InterPodAffinity",
-                   "NodeResourcesFit", "NodeAffinity", "PodTopologySpread", "TaintToleration"}
+                   "NodeResourcesFit", "NodeAffinity", "PodTopologySpread", "TaintToleration",
+                   "NetworkBandwidth"}
 
 
 def compile_profile(prof: SchedulerProfile, scalar_names: List[str] = ()) -> abi.Profile:

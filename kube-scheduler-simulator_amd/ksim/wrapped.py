@@ -25,7 +25,7 @@ from .profile import SchedulerProfile, original_name
 from .resultstore import PASSED_FILTER_MESSAGE, SUCCESS_MESSAGE, Store
 
 # Plugins with a ScoreExtensions (NormalizeScore) in v1.26.
-HAS_NORMALIZE = {"TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity"}
+HAS_NORMALIZE = {"TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity", "NetworkBandwidth"}
 
 # Upstream error reasons.
 ERR_UNSCHEDULABLE = "node(s) were unschedulable"                        # nodeunschedulable
@@ -39,8 +39,12 @@ ERR_IPA = {abi.IPA_AFFINITY: "node(s) didn't match pod affinity rules",
            abi.IPA_EXISTING_ANTI: "node(s) didn't satisfy existing pods anti-affinity rules"}
 
 
-def filter_message(cluster: EncodedCluster, plugin: str, detail: int) -> str:
-    """framework.Status.Message() of a failing in-tree Filter."""
+def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str = "", pod: str = "") -> str:
+    """framework.Status.Message() of a failing Filter (NetworkBandwidth's name
+    the node and the pod)."""
+    if plugin == "NetworkBandwidth":
+        from .netbw import filter_message as nb_message
+        return nb_message(detail, node, pod, cluster.nb_args)
     if plugin == "NodeUnschedulable":
         return ERR_UNSCHEDULABLE
     if plugin == "NodeName":
@@ -89,9 +93,19 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
         for f in range(last):
             if f == r:
                 store.add_filter_result(ns, name, names[node], forder[f],
-                                        filter_message(cluster, forder[f], int(fd[node])))
+                                        filter_message(cluster, forder[f], int(fd[node]), names[node], name))
             else:
                 store.add_filter_result(ns, name, names[node], forder[f], PASSED_FILTER_MESSAGE)
+    if res["status"] == abi.STATUS_ERROR:
+        # framework.Error: a Filter error ends the scan; a Score error ends the
+        # cycle after PreScore (which partial Score records survive the
+        # cancelled parallel run is not deterministic upstream: none are kept)
+        filter_error = any(int(fp[i]) < len(forder) and forder[int(fp[i])] == "NetworkBandwidth" and
+                           int(fd[i]) >= abi.NB_NO_LIMIT for i in range(cluster.n_nodes))
+        if not filter_error:
+            for p in prof.plugins["preScore"].enabled:
+                store.add_pre_score_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+        return
     if res["status"] == abi.STATUS_UNSCHEDULABLE:
         failed = [names[i] for i in range(cluster.n_nodes) if fp[i] not in (abi.PASSED, abi.NOT_EVALUATED)]
         for p in prof.plugins["postFilter"].enabled:
@@ -120,7 +134,7 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
 
 
 def emit_cycle_annotations(cluster: EncodedCluster, prof: SchedulerProfile, res: Dict,
-                           score_plugin_weight: Dict[str, int]) -> Dict[str, str]:
+                           score_plugin_weight: Dict[str, int], pod_name: str = "") -> Dict[str, str]:
     """The three large annotation values of one cycle from the native emitter
     (ksim_emit_cycle_json): what record_cycle + Store.add_stored_result_to_pod
     produce for them, without building the maps."""
@@ -131,16 +145,20 @@ def emit_cycle_annotations(cluster: EncodedCluster, prof: SchedulerProfile, res:
     fp = np.asarray(res["fail_plugin"], np.uint8)
     fd = np.asarray(res["fail_detail"])
     failed = (fp != abi.PASSED) & (fp != abi.NOT_EVALUATED)
-    pairs = sorted({(int(a), int(b)) for a, b in zip(fp[failed], fd[failed])})
+    names = cluster.node_names
+    # one message per (plugin, detail); NetworkBandwidth's also name the node
+    keys = [(int(fp[i]), int(fd[i]), names[i] if int(fp[i]) < len(forder) and forder[fp[i]] == "NetworkBandwidth" else "")
+            for i in np.nonzero(failed)[0]]
+    pairs = sorted(set(keys))
     index = {pr: k for k, pr in enumerate(pairs)}
-    messages = [filter_message(cluster, forder[a], b) for a, b in pairs]
+    messages = [filter_message(cluster, forder[a], b, nd, pod_name) for a, b, nd in pairs]
     msg_id = np.zeros(cluster.n_nodes, np.int32)
-    for i in np.nonzero(failed)[0]:
-        msg_id[i] = index[(int(fp[i]), int(fd[i]))]
+    for i, key in zip(np.nonzero(failed)[0], keys):
+        msg_id[i] = index[key]
     splugins = prof.score_plugins()
     snames = [p.name for p in splugins]
     scored = np.asarray(res["scored"], np.uint8) if res["n_feasible"] > 1 else np.zeros(cluster.n_nodes, np.uint8)
-    if res["status"] == abi.STATUS_UNSCHEDULABLE:
+    if res["status"] in (abi.STATUS_UNSCHEDULABLE, abi.STATUS_ERROR):
         scored = np.zeros(cluster.n_nodes, np.uint8)
     raw = np.asarray(res["raw"], np.int64).reshape(len(snames), cluster.n_nodes) if snames else \
         np.zeros((0, cluster.n_nodes), np.int64)

@@ -52,6 +52,8 @@ struct ksim_oracle {
   double *topo_log;
   int32_t *col_nvals;   /* value ids per label column */
   int32_t vmax;
+  /* NetworkBandwidth: node limit (static) and allocated amount (dynamic), milli-units */
+  int64_t *nb_limit, *nb_alloc;
   /* scheduler state */
   int32_t next_start;   /* sched.nextStartNodeIndex */
   int64_t pod_seq;      /* tie-break sequence */
@@ -121,6 +123,8 @@ ksim_oracle* ksim_oracle_create(const ksim_node_table* t, const ksim_vocab* v,
   o->dom = malloc(8 * (size_t)KSIM_MAX_USES * o->vmax);
   o->present = malloc((size_t)KSIM_MAX_USES * o->vmax);
   o->ignored = malloc(n + 1);
+  o->nb_limit = dupbuf(t->nb_limit, n * 8);
+  o->nb_alloc = dupbuf(t->nb_alloc, n * 8);
   return o;
 }
 
@@ -131,7 +135,7 @@ void ksim_oracle_destroy(ksim_oracle* o) {
                 o->num_pods, o->flags, o->taints, o->labels, o->taint_effect,
                 o->label_col_offset, o->label_num, o->label_num_ok, o->fail, o->detail,
                 o->flist, o->raw, o->cnt, o->topo_log, o->col_nvals, o->dom, o->present,
-                o->ignored};
+                o->ignored, o->nb_limit, o->nb_alloc};
   for (size_t i = 0; i < sizeof(ps) / sizeof(ps[0]); i++) free(ps[i]);
   free(o);
 }
@@ -637,6 +641,45 @@ static int64_t ipa_score(const ksim_oracle* o, const topo_ctx* t, int32_t node) 
 }
 
 /* ---- framework: RunFilterPlugins — a17 ---------------------------------- */
+/* ---- NetworkBandwidth, the simulator's out-of-tree plugin -----------------
+ * simulator/scheduler/plugin/networkbandwidth/plugin.go.  Quantities are
+ * milli-units (the host rejects finer ones).  Filter's Skip / Error returns are
+ * neither Success nor Unschedulable, so [upstream] RunFilterPlugins turns them
+ * into framework.Error and the scheduling cycle fails (nb_error). */
+static uint32_t nb_filter(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+  const uint32_t fl = o->flags[node];
+  if (!(fl & KSIM_NODE_NB_LIMIT)) return KSIM_NB_NO_LIMIT;               /* :54-57 Skip */
+  if (fl & KSIM_NODE_NB_LIMIT_BAD) return KSIM_NB_LIMIT_BAD;             /* :58-61 Error */
+  if (p->nb_flags & KSIM_POD_NB_INGRESS_BAD) return KSIM_NB_INGRESS_BAD; /* :72-76 Error */
+  if (p->nb_flags & KSIM_POD_NB_EGRESS_BAD) return KSIM_NB_EGRESS_BAD;   /* :84-88 Error */
+  if (p->nb_req == 0) return KSIM_NB_NO_REQUEST;                          /* :92-94 Skip */
+  return o->nb_alloc[node] + p->nb_req > o->nb_limit[node] ? KSIM_NB_INSUFFICIENT : 0; /* :97-99 */
+}
+static int nb_error(const ksim_oracle* o, uint8_t r, uint32_t detail) {
+  return r != KSIM_PASSED && o->prof.filter[r] == KSIM_PL_NETWORK_BANDWIDTH && detail >= KSIM_NB_NO_LIMIT;
+}
+/* Score :128-149: (limit - allocated).Value(), rounding a fraction away from zero */
+static int64_t nb_score(const ksim_oracle* o, int32_t node) {
+  const int64_t d = o->nb_limit[node] - o->nb_alloc[node];
+  return d >= 0 ? (d + 999) / 1000 : -((-d + 999) / 1000);
+}
+/* Score returns Skip (no limit annotation) or Error (limit does not parse) */
+static int nb_score_fails(const ksim_oracle* o, int32_t node) {
+  return !(o->flags[node] & KSIM_NODE_NB_LIMIT) || (o->flags[node] & KSIM_NODE_NB_LIMIT_BAD);
+}
+static int has_score_plugin(const ksim_oracle* o, int plugin) {
+  for (int k = 0; k < o->prof.n_score; k++)
+    if (o->prof.score[k] == plugin) return 1;
+  return 0;
+}
+/* RunScorePlugins fails when NetworkBandwidth's Score fails on a kept node */
+static int nb_score_error(const ksim_oracle* o, const int32_t* flist, int32_t nf) {
+  if (nf <= 1 || !has_score_plugin(o, KSIM_PL_NETWORK_BANDWIDTH)) return 0;
+  for (int32_t j = 0; j < nf; j++)
+    if (nb_score_fails(o, flist[j])) return 1;
+  return 0;
+}
+
 /* Runs the profile's filter plugins in order and stops at the first failure
  * (runAllFilters=false).  Returns the filter-order index of the failing plugin
  * or KSIM_PASSED; *detail gets the reason payload. */
@@ -679,6 +722,11 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
       case KSIM_PL_NODE_PORTS:           /* nodeports.Filter -> fitsPorts */
         if (node_port_conflict(o, ps, p, node)) return (uint8_t)f;
         break;
+      case KSIM_PL_NETWORK_BANDWIDTH: {
+        uint32_t r = nb_filter(o, p, node);
+        if (r) { *detail = r; return (uint8_t)f; }
+        break;
+      }
       /* volume plugins: pods without volumes pass. */
       default:
         break;
@@ -703,6 +751,7 @@ static int64_t score_plugin_raw(const ksim_oracle* o, const ksim_pod_set* ps, co
       }
       return 0;
     }
+    case KSIM_PL_NETWORK_BANDWIDTH: return nb_score_fails(o, node) ? 0 : nb_score(o, node);
     default: return 0;
   }
 }
@@ -730,8 +779,9 @@ static void normalize_plugin(int plugin, const topo_ctx* t, const uint8_t* ign, 
       }
       return;
     }
-    case KSIM_PL_INTER_POD_AFFINITY: {    /* interpodaffinity.NormalizeScore */
-      if (t->topology_score_empty) return;
+    case KSIM_PL_INTER_POD_AFFINITY:      /* interpodaffinity.NormalizeScore */
+    case KSIM_PL_NETWORK_BANDWIDTH: {     /* networkbandwidth NormalizeScore, plugin.go:159-186 */
+      if (plugin == KSIM_PL_INTER_POD_AFFINITY && t->topology_score_empty) return;
       int64_t mn = INT64_MAX, mx = INT64_MIN;
       for (int i = 0; i < n; i++) { if (s[i] > mx) mx = s[i]; if (s[i] < mn) mn = s[i]; }
       int64_t diff = mx - mn;
@@ -749,7 +799,8 @@ static void normalize_plugin(int plugin, const topo_ctx* t, const uint8_t* ign, 
 
 static int has_normalize(int plugin) {
   return plugin == KSIM_PL_TAINT_TOLERATION || plugin == KSIM_PL_NODE_AFFINITY ||
-         plugin == KSIM_PL_POD_TOPOLOGY_SPREAD || plugin == KSIM_PL_INTER_POD_AFFINITY;
+         plugin == KSIM_PL_POD_TOPOLOGY_SPREAD || plugin == KSIM_PL_INTER_POD_AFFINITY ||
+         plugin == KSIM_PL_NETWORK_BANDWIDTH;
 }
 
 /* NodeInfo.AddPod restricted to the aggregates the plugins read — a20 */
@@ -761,6 +812,7 @@ static void assume_pod(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p
   o->nz_cpu[node] += sign * p->nz_cpu;
   o->nz_mem[node] += sign * p->nz_mem;
   o->num_pods[node] += sign;
+  o->nb_alloc[node] += sign * p->nb_add;
   for (int i = 0; i < p->add_count; i++) {            /* pod counts / carried terms */
     const ksim_class_add* a = &ps->adds[p->add_first + i];
     o->cnt[(size_t)a->cls * o->n + node] += sign * a->count;
@@ -799,7 +851,7 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
   /* PreFilter (PodTopologySpread / InterPodAffinity state), then findNodesThatPassFilters */
   topo_ctx tc;
   topo_prefilter(o, ps, p, &tc);
-  int32_t nf = 0, nfailed = 0, evaluated = 0;
+  int32_t nf = 0, nfailed = 0, evaluated = 0, error = 0;
   for (int32_t i = 0; i < N; i++) {
     int32_t node = (start + i) % N;
     uint32_t det;
@@ -807,6 +859,10 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
     evaluated++;
     if (out->fail_plugin) out->fail_plugin[node] = r;
     if (out->fail_detail) out->fail_detail[node] = det;
+    if (nb_error(o, r, det)) {     /* checkNode: errCh.SendErrorWithCancel; not in the status map */
+      error = 1;
+      break;
+    }
     if (r == KSIM_PASSED) {
       if (nf == K) break;          /* the (K+1)-th feasible node: recorded, not kept */
       o->flist[nf++] = node;
@@ -835,6 +891,11 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
   out->n_processed = processed;
   out->next_start = o->next_start;
 
+  if (error || nb_score_error(o, o->flist, nf)) {   /* the cycle fails with framework.Error */
+    out->chosen = KSIM_CHOSEN_ERROR;
+    out->status = KSIM_STATUS_ERROR;
+    return KSIM_OK;
+  }
   if (nf == 0) {
     out->chosen = -1;
     out->status = KSIM_STATUS_UNSCHEDULABLE;
@@ -903,7 +964,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
     const int64_t seq = o->pod_seq++;
     const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, N);
     const int32_t start = o->next_start;
-    int32_t nf = 0, nfailed = 0, evaluated = 0;
+    int32_t nf = 0, nfailed = 0, evaluated = 0, error = 0;
     int32_t chosen = -1;
     topo_ctx tc;
     topo_prefilter(o, ps, p, &tc);
@@ -913,13 +974,18 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
 #pragma omp for schedule(static)
       for (int32_t node = 0; node < N; node++) {
         uint32_t det;
-        feas[node] = run_filter_plugins(o, ps, p, &tc, node, &det) == KSIM_PASSED;
+        const uint8_t r = run_filter_plugins(o, ps, p, &tc, node, &det);
+        feas[node] = r == KSIM_PASSED ? 1 : nb_error(o, r, det) ? 2 : 0;
       }
 #pragma omp single
       {
         for (int32_t i = 0; i < N; i++) {
           int32_t node = (start + i) % N;
           evaluated++;
+          if (feas[node] == 2) {
+            error = 1;
+            break;
+          }
           if (feas[node]) {
             if (nf == K) break;
             o->flist[nf++] = node;
@@ -927,8 +993,9 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
             nfailed++;
           }
         }
+        if (!error && nb_score_error(o, o->flist, nf)) error = 1;
       }
-      if (nf > 1) {
+      if (nf > 1 && !error) {
 #pragma omp single
         topo_prescore(o, ps, p, o->flist, nf, &tc);
 #pragma omp for schedule(static)
@@ -954,11 +1021,11 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
         }
       }
     }
-    if (nf == 1) chosen = o->flist[0];
+    if (nf == 1 && !error) chosen = o->flist[0];
     o->next_start = (start + nf + nfailed) % N;
     evals += evaluated;
     if (chosen >= 0) { assume_pod(o, ps, p, chosen, 1); sched++; } else { unsched++; }
-    if (chosen_out) chosen_out[c] = chosen;
+    if (chosen_out) chosen_out[c] = error ? KSIM_CHOSEN_ERROR : chosen;
   }
   free(totals);
   free(ign_buf);
@@ -983,6 +1050,12 @@ int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* 
   if (nz_cpu) memcpy(nz_cpu, o->nz_cpu, 8 * n);
   if (nz_mem) memcpy(nz_mem, o->nz_mem, 8 * n);
   if (num_pods) memcpy(num_pods, o->num_pods, 4 * n);
+  return KSIM_OK;
+}
+
+int ksim_oracle_get_nb_alloc(const ksim_oracle* o, int64_t* out) {
+  if (!o || !out) return KSIM_E_INVALID;
+  memcpy(out, o->nb_alloc, 8 * (size_t)o->n);
   return KSIM_OK;
 }
 
@@ -1062,6 +1135,8 @@ int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int3
   if (p->use_count > 0) return KSIM_E_UNSUPPORTED;
   const int32_t N = o->n;
   int fit = -1;
+  for (int f = 0; f < o->prof.n_filter; f++)           /* the dry run re-runs Fit only */
+    if (o->prof.filter[f] == KSIM_PL_NETWORK_BANDWIDTH) return KSIM_E_UNSUPPORTED;
   for (int f = 0; f < o->prof.n_filter; f++)
     if (o->prof.filter[f] == KSIM_PL_NODE_RESOURCES_FIT) fit = f;
   topo_ctx tc;

@@ -49,6 +49,7 @@ int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* 
                                int64_t* req_eph, int64_t* nz_cpu, int64_t* nz_mem,
                                int32_t* num_pods);
 int ksim_oracle_get_class_count(const ksim_oracle* o, int32_t* out);
+int ksim_oracle_get_nb_alloc(const ksim_oracle* o, int64_t* out);
 int32_t ksim_oracle_next_start(const ksim_oracle* o);
 void ksim_oracle_set_next_start(ksim_oracle* o, int32_t s);
 void ksim_oracle_set_pod_seq(ksim_oracle* o, int64_t seq);

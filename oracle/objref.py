@@ -17,7 +17,7 @@ import math
 from typing import Dict, List, Optional, Tuple
 
 from ksim.encode import node_tree_order, pod_nonzero_requests, pod_requests, zone_key
-from ksim.model import LabelSelector, Node, Pod, PodAffinityTerm, Taint, selector_matches
+from ksim.model import LabelSelector, Node, Pod, PodAffinityTerm, Taint, parse_quantity, selector_matches
 
 MAX_NODE_SCORE = 100
 LABEL_HOSTNAME = "kubernetes.io/hostname"
@@ -120,7 +120,8 @@ class ObjScheduler:
 
     def __init__(self, nodes: List[Node], bound: List[Pod] = (), namespaces: Optional[Dict[str, Dict]] = None,
                  pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
-                 hard_pod_affinity_weight: int = 1):
+                 hard_pod_affinity_weight: int = 1, network_bandwidth=None, nb_filter: bool = True,
+                 nb_score: bool = True):
         order = node_tree_order([zone_key(n.labels) for n in nodes])
         self.nodes = [NodeInfo(nodes[i]) for i in order]
         # cache.addNodeImageStates, nodes in the order they were added: name -> [size, {node names}]
@@ -144,6 +145,14 @@ class ObjScheduler:
                              "NodeResourcesFit", "VolumeRestrictions", "EBSLimits", "GCEPDLimits",
                              "NodeVolumeLimits", "AzureDiskLimits", "VolumeBinding", "VolumeZone",
                              "PodTopologySpread", "InterPodAffinity"]
+        # NetworkBandwidth (out-of-tree, enabled by a profile): appended after the
+        # in-tree plugins, as mergePluginSet places a user-enabled plugin
+        self.nb = network_bandwidth
+        if self.nb is not None:
+            if nb_filter:
+                self.filter_order.append("NetworkBandwidth")
+            if nb_score:
+                self.score_order.append("NetworkBandwidth")
         self.seed = seed
         self.hard_w = hard_pod_affinity_weight
         self.next_start = 0
@@ -432,6 +441,71 @@ class ObjScheduler:
         d = mx - mn
         return [int(float(MAX_NODE_SCORE) * (float(s - mn) / float(d))) if d > 0 else 0 for s in scores]
 
+    # ---- NetworkBandwidth (simulator/scheduler/plugin/networkbandwidth/plugin.go) ------
+    # Exact quantities (Fractions); the node's allocated amount is summed from the
+    # pods on it each time, as getNodeAllocatedAmount does.
+    @staticmethod
+    def _q(s):
+        try:
+            return parse_quantity(s)
+        except ValueError:
+            return None
+
+    def _nb_allocated(self, ni: NodeInfo):
+        a = self.nb
+        total = 0
+        for key in (a.ingress_request_annotation, a.egress_request_annotation):   # :107-120
+            for pi in ni.pods:
+                if key in pi.pod.annotations:
+                    q = self._q(pi.pod.annotations[key])
+                    if q is not None:
+                        total += q
+        return total
+
+    def nb_filter(self, pod: Pod, ni: NodeInfo):
+        """(status, message): status None (Success), "unschedulable", "skip" or "error"."""
+        a, node = self.nb, ni.node
+        if a.node_limit_annotation not in node.annotations:
+            return "skip", f"Node {node.name} does not have {a.node_limit_annotation} annotation present"
+        limit = self._q(node.annotations[a.node_limit_annotation])
+        if limit is None:
+            return "error", f"Node {node.name} has an incorrect quantity in {a.node_limit_annotation} annotation present"
+        allocated = self._nb_allocated(ni)
+        req = 0
+        for key, fallback in ((a.ingress_request_annotation, "kubernetes.io/ingress-bandwidth"),
+                              (a.egress_request_annotation, "kubernetes.io/egress-bandwidth")):
+            s = pod.annotations.get(key)
+            if s is None:
+                s = pod.annotations.get(fallback)
+            if s is not None:
+                q = self._q(s)
+                if q is None:
+                    return "error", f"Could not parse quantity from pod {pod.name} {key} annotations"
+                req += q
+        if req == 0:
+            return "skip", (f"Pod {pod.name} does not have network bandwidth request annotations set. "
+                            f"(Missing {a.ingress_request_annotation} or {a.egress_request_annotation})")
+        if allocated + req > limit:
+            return "unschedulable", f"Node {node.name} does not have enough network bandwidth capacity to schedule pod"
+        return None, None
+
+    def nb_score(self, ni: NodeInfo) -> Optional[int]:
+        """Score's value, or None when it returns Skip / Error."""
+        a, node = self.nb, ni.node
+        if a.node_limit_annotation not in node.annotations:
+            return None
+        limit = self._q(node.annotations[a.node_limit_annotation])
+        if limit is None:
+            return None
+        d = limit - self._nb_allocated(ni)
+        return math.ceil(d) if d >= 0 else -math.ceil(-d)     # Quantity.Value(): away from zero
+
+    @staticmethod
+    def nb_normalize(scores: List[int]) -> List[int]:
+        mn, mx = min(scores), max(scores)
+        d = mx - mn
+        return [int(float(MAX_NODE_SCORE) * (float(s - mn) / float(d))) if d > 0 else 0 for s in scores]
+
     # ---- resources -------------------------------------------------------------------
     @staticmethod
     def fit_filter(pod: Pod, ni: NodeInfo) -> Optional[str]:
@@ -577,9 +651,18 @@ class ObjScheduler:
 
     # ---- the cycle ---------------------------------------------------------------------
     def filter_node(self, pod: Pod, ni: NodeInfo, pts, ipa) -> Tuple[Optional[str], Optional[str]]:
+        """(failing plugin, message); the plugin is "NetworkBandwidth!" when its
+        status was Skip / Error (RunFilterPlugins: framework.Error)."""
         node = ni.node
         for pl in self.filter_order:
             msg = None
+            if pl == "NetworkBandwidth":
+                st, msg = self.nb_filter(pod, ni)
+                if st in ("skip", "error"):
+                    return pl + "!", msg
+                if st:
+                    return pl, msg
+                continue
             if pl == "NodeUnschedulable":
                 if node.unschedulable and not any(
                         t.tolerates(Taint("node.kubernetes.io/unschedulable", "", "NoSchedule"))
@@ -620,9 +703,14 @@ class ObjScheduler:
         filt: Dict[str, Tuple[Optional[str], Optional[str]]] = {}
         feasible: List[NodeInfo] = []
         failed = 0
+        error = None
         for i in range(N):
             ni = self.nodes[(self.next_start + i) % N]
             pl, msg = self.filter_node(pod, ni, pts, ipa)
+            if pl is not None and pl.endswith("!"):        # checkNode: the error ends the scan
+                filt[ni.node.name] = (pl[:-1], msg)
+                error = "filter"
+                break
             filt[ni.node.name] = (pl, msg)
             if pl is None:
                 if len(feasible) == K:
@@ -637,8 +725,11 @@ class ObjScheduler:
             for name in out:
                 filt[name] = ("extender", "filtered out by an extender")
             feasible = [ni for ni in feasible if ni.node.name not in out]
-        res = {"filter": filt, "n_feasible": len(feasible), "raw": {}, "norm": {}, "total": {}}
-        if not feasible:
+        res = {"filter": filt, "n_feasible": len(feasible), "raw": {}, "norm": {}, "total": {}, "error": error}
+        if error is None and len(feasible) > 1 and "NetworkBandwidth" in self.score_order and \
+                any(self.nb_score(ni) is None for ni in feasible):
+            error = res["error"] = "score"                 # RunScorePlugins fails
+        if error or not feasible:
             res["chosen"] = None
             return res
         if len(feasible) == 1:
@@ -668,6 +759,9 @@ class ObjScheduler:
                 elif pl == "PodTopologySpread":
                     raw = [self.pts_score(pod, pstate, ni) for ni in feasible]
                     norm = self.pts_normalize(pstate, names, raw)
+                elif pl == "NetworkBandwidth":
+                    raw = [self.nb_score(ni) for ni in feasible]
+                    norm = self.nb_normalize(raw)
                 else:   # TaintToleration
                     raw = [sum(1 for t in ni.node.taints if t.effect == "PreferNoSchedule" and not any(
                         tol.tolerates(t) for tol in pod.tolerations if tol.effect in ("", "PreferNoSchedule")))

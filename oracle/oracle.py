@@ -31,6 +31,7 @@ def lib():
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
         L.ksim_oracle_get_class_count.argtypes = [vp, vp]
+        L.ksim_oracle_get_nb_alloc.argtypes = [vp, vp]
         L.ksim_oracle_next_start.argtypes = [vp]
         L.ksim_oracle_next_start.restype = i32
         L.ksim_oracle_set_next_start.argtypes = [vp, i32]
@@ -122,6 +123,11 @@ class Oracle:
     def class_count(self) -> np.ndarray:
         out = np.zeros((self.cluster.class_count.shape[0], self.cluster.n_nodes), np.int32)
         lib().ksim_oracle_get_class_count(self.h, out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+    def nb_alloc(self) -> np.ndarray:
+        out = np.zeros(self.cluster.n_nodes, np.int64)
+        lib().ksim_oracle_get_nb_alloc(self.h, out.ctypes.data_as(ctypes.c_void_p))
         return out
 
     @property

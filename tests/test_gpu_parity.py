@@ -394,3 +394,51 @@ def test_preemption_vs_oracle(n_nodes):
         many += want[3] >= 100
     if n_nodes > 1000:
         assert many > 0
+
+
+# ---- NetworkBandwidth (the simulator's out-of-tree plugin) -------------------------
+def _nb_case(pct, node_errors, pod_errors, filt=True, score=True, n_nodes=150, n_pods=300):
+    import test_netbw
+    from ksim.encode import encode_cluster, encode_pods
+    nodes, bound, pending = gen.netbw_objects(n_nodes=n_nodes, n_pods=n_pods, node_errors=node_errors,
+                                              pod_errors=pod_errors)
+    sp = test_netbw.nb_profile(pct, filt=filt, score=score)
+    cluster, _ = encode_cluster(nodes, bound, nb_args=sp.network_bandwidth)
+    return cluster, encode_pods(cluster, pending), profile.compile_profile(sp)
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+@pytest.mark.parametrize("errors", [False, True])
+def test_network_bandwidth_compat_cycles(pct, errors):
+    cluster, pods, prof = _nb_case(pct, errors, errors)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    statuses = set()
+    for i in range(pods.n_pods):
+        e, o = eng.eval_pod(pods, i), ora.cycle(pods, i)
+        _compare_cycle(e, o, f"pod {i}")
+        statuses.add(o["status"])
+    np.testing.assert_array_equal(eng.nb_alloc(), ora.nb_alloc())
+    assert (abi.STATUS_ERROR in statuses) == errors
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_network_bandwidth_batch_and_score_only(pct):
+    for filt, score in ((True, True), (False, True), (True, False)):
+        cluster, pods, prof = _nb_case(pct, True, True, filt, score, n_nodes=300, n_pods=600)
+        eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+        chosen, st = eng.schedule_batch(pods)
+        want, ost = ora.schedule(pods)
+        np.testing.assert_array_equal(chosen, want, err_msg=f"filter={filt} score={score}")
+        assert st.evals == ost.evals and eng.next_start == ora.next_start
+        assert (chosen == abi.CHOSEN_ERROR).any()
+        np.testing.assert_array_equal(eng.nb_alloc(), ora.nb_alloc())
+
+
+def test_network_bandwidth_extender_cycles():
+    import test_extender
+    cluster, pods, prof = _nb_case(0, True, True, n_pods=120)
+    fail, score = test_extender.extender_model(cluster.node_names)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(pods.n_pods):
+        _compare_cycle(eng.eval_pod_extenders(pods, i, lambda f: (fail, score)), ora.cycle(pods, i, fail, score),
+                       f"pod {i}")

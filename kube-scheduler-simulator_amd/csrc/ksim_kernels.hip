@@ -183,15 +183,44 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
 // ==== A. per-pod path ===========================================================
 constexpr int kLdsDom = 128;   // domain tables of key columns with <= kLdsDom value ids are LDS-staged
 
+// The cycle's pod record and topology uses staged in LDS (use_first rebased to
+// 0).  The per-node loops over the uses then read LDS instead of issuing a
+// global load that depends on the pod record for every use.  Every thread of
+// the block must call it (two barriers).
+struct PodStage {
+  ksim_pod pod;
+  ksim_topo_use uses[KSIM_MAX_USES];
+};
+static_assert(sizeof(ksim_pod) % 8 == 0, "pod record copied as 8-byte words");
+
+__device__ __forceinline__ DevPods stage_pod(const DevPods& P, int32_t pi, PodStage& sp) {
+  constexpr int kWords = (int)(sizeof(ksim_pod) / 8);
+  const ksim_pod& g = P.pods[pi];
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(&g);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(&sp.pod);
+  const int t = threadIdx.x;
+  if (t < kWords) dst[t] = src[t];
+  const int32_t nu = g.use_count;
+  if (t < nu) sp.uses[t] = P.uses[g.use_first + t];
+  __syncthreads();
+  if (t == 0) sp.pod.use_first = 0;
+  __syncthreads();
+  DevPods L = P;
+  L.uses = sp.uses;
+  return L;
+}
+
 // PreFilter of PodTopologySpread / InterPodAffinity plus the domain sums their
 // PreScore needs: one thread per node, adds into the pod's domain tables.
-__global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P, ksim_profile prof,
+__global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0, ksim_profile prof,
                                                         DevState* __restrict__ st, DevScratch s) {
   __shared__ unsigned long long s_dom[KSIM_MAX_USES][kLdsDom];
   __shared__ uint32_t s_flags;
+  __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
-  const ksim_pod& p = P.pods[pi];
+  const DevPods P = stage_pod(P0, pi, s_stage);
+  const ksim_pod& p = s_stage.pod;
   const int nu = p.use_count;
   if (nu == 0) return;
   const int tid = threadIdx.x;
@@ -313,15 +342,17 @@ __global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_
 // (k_topo_min's work, a few LDS reductions) instead of a separate launch.
 
 template <bool COMPAT, bool NOWIN>
-__global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P, ksim_profile prof,
+__global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, ksim_profile prof,
                                                       const DevState* __restrict__ st, DevScratch s,
                                                       int32_t fuse_min) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ int64_t sh64[4];
+  __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
-  const ksim_pod& p = P.pods[pi];
+  const DevPods P = stage_pod(P0, pi, s_stage);
+  const ksim_pod& p = s_stage.pod;
   if (fuse_min && p.use_count) {                 // block-uniform
     for (int i = 0; i < p.use_count; i++) {
       const ksim_topo_use u = P.uses[p.use_first + i];
@@ -701,13 +732,15 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
 }
 
 template <bool COMPAT>
-__global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P, ksim_profile prof,
+__global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_profile prof,
                                                 const DevState* __restrict__ st, DevScratch s, DevEvalOut o) {
   __shared__ uint64_t s_best[4];
+  __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
-  const ksim_pod& p = P.pods[pi];
+  const DevPods P = stage_pod(P0, pi, s_stage);
+  const ksim_pod& p = s_stage.pod;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;

@@ -106,6 +106,7 @@ struct ksim_handle {
   std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
+  std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
   std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
@@ -127,9 +128,9 @@ struct ksim_handle {
   int32_t rank = 0, world = 1;
   ncclComm_t comm = nullptr;
 
-  hipGraphExec_t graph_cycle = nullptr;        // per-pod cycles, pods without topology uses
-  hipGraphExec_t graph_cycle_topo = nullptr;   // per-pod cycles incl. the topology kernels
-  hipGraphExec_t graph_cycle_topo_fused = nullptr;   // ... with the critical paths in the filter pass
+  // per-pod cycles, by variant: topology kernels (1) | critical paths in the
+  // filter pass (2) | NormalizeScore extrema in the filter pass (4)
+  hipGraphExec_t graph_cycle[8] = {};
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
 };
@@ -176,15 +177,13 @@ int upload(ksim_handle* h, std::vector<DevBuf>& owner, const void* src, size_t b
 }
 
 void drop_graphs(ksim_handle* h) {
-  if (h->graph_cycle) (void)hipGraphExecDestroy(h->graph_cycle);
-  if (h->graph_cycle_topo) (void)hipGraphExecDestroy(h->graph_cycle_topo);
-  if (h->graph_cycle_topo_fused) (void)hipGraphExecDestroy(h->graph_cycle_topo_fused);
-  h->graph_cycle_topo_fused = nullptr;
+  for (auto& g : h->graph_cycle) {
+    if (g) (void)hipGraphExecDestroy(g);
+    g = nullptr;
+  }
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   h->graph_batch_fast = nullptr;
-  h->graph_cycle = nullptr;
-  h->graph_cycle_topo = nullptr;
   h->graph_batch = nullptr;
 }
 
@@ -351,11 +350,13 @@ int read_state(ksim_handle* h, DevState& st) {
   return KSIM_OK;
 }
 
-int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false, bool fuse_min = false) {
+int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false, bool fuse_min = false,
+            bool fuse_ext = false) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = fast;
   a.fuse_min = fuse_min;
+  a.fuse_ext = fuse_ext;
   hipGraph_t g = nullptr;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   if (batch)
@@ -387,8 +388,10 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   if (!batch) {
     la.fuse_min = topo;
     for (int32_t i = a; i < b && la.fuse_min; i++) la.fuse_min = h->hard_small[i] != 0;
-    hipGraphExec_t& g = !topo ? h->graph_cycle : la.fuse_min ? h->graph_cycle_topo_fused : h->graph_cycle_topo;
-    if (!g && (rc = capture(h, false, topo, &g, false, la.fuse_min))) return rc;
+    la.fuse_ext = true;
+    for (int32_t i = a; i < b && la.fuse_ext; i++) la.fuse_ext = h->soft_le1[i] != 0;
+    hipGraphExec_t& g = h->graph_cycle[(topo ? 1 : 0) | (la.fuse_min ? 2 : 0) | (la.fuse_ext ? 4 : 0)];
+    if (!g && (rc = capture(h, false, topo, &g, false, la.fuse_min, la.fuse_ext))) return rc;
     int32_t done = a;
     for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(g, h->stream));
     for (; done < b; done++) launch_cycle(la, h->stream, false, topo);
@@ -1171,12 +1174,14 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->xdom_len.assign((size_t)ps->n_pods, 0);
   h->trivial.assign((size_t)ps->n_pods, 0);
   h->hard_small.assign((size_t)ps->n_pods, 1);
+  h->soft_le1.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
     h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
     // sharded-cycle exchange sizes, laid out as k_dom_pack / k_window_sh do
     bool soft = false;
+    int n_soft = 0;
     int64_t xr = 1;
     for (int32_t k = 0; k < ps->pods[i].use_count; k++) {
       const ksim_topo_use& u = ps->uses[ps->pods[i].use_first + k];
@@ -1187,7 +1192,9 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
         bf[i] |= kPodRegistersValues;
       }
       soft = soft || u.kind == KSIM_USE_PTS_SOFT;
+      n_soft += u.kind == KSIM_USE_PTS_SOFT ? 1 : 0;
     }
+    h->soft_le1[i] = n_soft <= 1 ? 1 : 0;
     h->xreg_len[i] = soft ? xr : 0;
     if (static_trivial(h, ps->pods[i])) bf[i] |= kBatchStaticTrivial;
     h->trivial[i] = (bf[i] & kBatchStaticTrivial) ? 1 : 0;
@@ -1431,6 +1438,8 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     a.fast = batch && run_fast(h, lo, hi);
     a.fuse_min = !batch && topo;
     for (int32_t i = lo; i < hi && a.fuse_min; i++) a.fuse_min = h->hard_small[i] != 0;
+    a.fuse_ext = !batch;
+    for (int32_t i = lo; i < hi && a.fuse_ext; i++) a.fuse_ext = h->soft_le1[i] != 0;
     const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
     const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
     int32_t cursor = lo;

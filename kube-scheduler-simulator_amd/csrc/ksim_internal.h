@@ -35,6 +35,7 @@ struct LaunchArgs {
   int32_t* chosen;   // [n_pods] device, may be null
   bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
   bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
+  bool fuse_ext = false;  // per-pod runs: every pod has <= 1 ScheduleAnyway spread constraint (K = N: no k_extrema)
 };
 
 constexpr int kKernelsPerCycle = 7;

@@ -340,13 +340,71 @@ __global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_
 // fuse_min: every hard spread constraint of the run keys a column of at most
 // kFuseMinValues values, so each block derives the critical paths itself
 // (k_topo_min's work, a few LDS reductions) instead of a separate launch.
+// fuse_ext (NOWIN runs whose pods carry at most one ScheduleAnyway spread
+// constraint): the NormalizeScore extrema are taken here, so the cycle needs
+// no k_extrema.  PodTopologySpread's raw score is then a non-decreasing
+// function of one count (round(count * w + maxSkew - 1), w > 0 known only
+// after the pass), so its slots hold the count extrema and k_select maps them.
+
+// Order-preserving u64 images of an int64 so extrema are atomicMax on u64:
+// max image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both.
+__device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
+__device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
+__device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
+__device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
+
+// Per-slot extrema images of this block's values -> one atomicMax per slot.
+__device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState* win, const uint64_t (&ix)[KSIM_MAX_SCORE],
+                                              const uint64_t (&in)[KSIM_MAX_SCORE], uint64_t (*s_red)[2 * KSIM_MAX_SCORE]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int S = prof.n_score;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+    if (k >= S) break;
+    if (norm_kind(prof.score[k]) == kNormNone) continue;
+    const uint64_t a = wave_max_u64_dpp(ix[k]), b = wave_max_u64_dpp(in[k]);
+    if (lane == 0) {
+      s_red[wv][2 * k] = a;
+      s_red[wv][2 * k + 1] = b;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * KSIM_MAX_SCORE && tid < 2 * S && norm_kind(prof.score[tid >> 1]) != kNormNone) {
+    uint64_t m = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
+    if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->ext[tid]), (unsigned long long)m);
+  }
+}
+
+// The pod's one ScheduleAnyway spread use (index into its uses), or -1.
+__device__ __forceinline__ int soft_use(const ksim_topo_use* U, int nu) {
+  int soft = -1;
+  for (int i = 0; i < nu; i++)
+    if (U[i].kind == KSIM_USE_PTS_SOFT) soft = i;
+  return soft;
+}
+// PodTopologySpread's count for the soft use on node (TopologyPairToPodCounts,
+// or the node's own count on hostname)
+__device__ __forceinline__ int64_t soft_count(const DevCluster& c, const DevScratch& s, const ksim_topo_use& u,
+                                              int soft, int32_t node) {
+  return (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node)
+                                        : s.dom[(size_t)soft * c.vmax + use_value(c, u, node)];
+}
+// scoreForCount with a single constraint (k_extrema's sum from 0, unfused)
+__device__ __forceinline__ int64_t soft_score(int64_t cnt, double w, int32_t max_skew) {
+  double score = 0;
+  score = score + ((double)cnt * w + (double)(max_skew - 1));
+  return (int64_t)round(score);
+}
 
 template <bool COMPAT, bool NOWIN>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, ksim_profile prof,
                                                       const DevState* __restrict__ st, DevScratch s,
-                                                      int32_t fuse_min) {
+                                                      int32_t fuse_min, int32_t fuse_ext) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ int64_t sh64[4];
+  __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
   __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
@@ -424,17 +482,37 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
         atomicOr(&bm[v >> 5], 1u << (v & 31));
       }
     }
+    if (fuse_ext) {                                // block-uniform
+      const int soft = soft_use(P.uses, p.use_count);
+      uint64_t ix[KSIM_MAX_SCORE], in[KSIM_MAX_SCORE];
+#pragma unroll
+      for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+        ix[k] = in[k] = 0;
+        if (k >= prof.n_score) continue;
+        const int32_t kind = norm_kind(prof.score[k]);
+        if (kind == kNormNone || !feasible) continue;
+        int64_t v = 0;
+        bool counted = true;
+        if (kind == kNormPTS) {
+          if (soft >= 0) {
+            counted = !ign;                        // IgnoredNodes: not in min / max
+            if (counted) v = soft_count(c, s, P.uses[soft], soft, node);
+          }
+        } else {
+          v = s.raw[(size_t)k * c.n + node];
+        }
+        if (counted) {
+          ix[k] = max_image(v);
+          in[k] = min_image(v);
+        }
+      }
+      block_extrema(prof, s.win, ix, in, s_red);
+    }
   }
 }
 
 constexpr int kBmWords = (KSIM_MAX_NODES + 1 + 31) / 32;   // value-id bitmap (PTS pair registration)
 
-// Order-preserving u64 images of an int64 so extrema are atomicMax on u64:
-// max image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both.
-__device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
-__device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
-__device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
-__device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
 
 // The selection after the filters, as four launches (a single block cannot
 // hide the latency of 10^4 nodes' loads):
@@ -731,10 +809,16 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
   }
 }
 
+// fuse_ext: k_extrema did not run (see k_filter_score).  Every block derives
+// the window state from the filter pass's counters, as k_extrema<true> does,
+// and block 0 publishes it for k_bind; PodTopologySpread's raw scores and
+// extrema come from the soft use's counts.
 template <bool COMPAT>
 __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_profile prof,
-                                                const DevState* __restrict__ st, DevScratch s, DevEvalOut o) {
+                                                const DevState* __restrict__ st, DevScratch s, DevEvalOut o,
+                                                int32_t fuse_ext) {
   __shared__ uint64_t s_best[4];
+  __shared__ int32_t sh32[4];
   __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
@@ -745,12 +829,48 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
   const int S = prof.n_score;
-  const int32_t nf = win->nf;
+  int32_t nf, kend;
+  bool has_soft;
+  int soft = -1;
+  double w_soft = 0;
+  if (fuse_ext) {                                  // block-uniform
+    nf = win->nfeas;
+    kend = N;
+    soft = soft_use(P.uses, p.use_count);
+    has_soft = nf > 1 && soft >= 0;
+    if (has_soft) {                                // topologyNormalizingWeight of the one soft use
+      const ksim_topo_use& u = P.uses[soft];
+      int32_t size = 0;
+      if (u.flags & KSIM_USEF_HOSTNAME) {
+        size = nf - win->nign;
+      } else if (u.col != KSIM_COL_NONE) {
+        const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+        const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
+        int32_t bits = 0;
+        for (int x = tid; x < words; x += blockDim.x) bits += __popc(s.regbm[(size_t)soft * vwords + x]);
+        size = block_sum_i32_nw<4>(bits, sh32);
+      }
+      w_soft = c.topo_log[size];
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+      win->nf = nf;
+      win->kend = N;
+      win->cut = N;
+      win->evaluated = N;
+      win->k = N;
+      win->has_soft = has_soft;
+      if (soft >= 0) win->w[soft] = w_soft;
+    }
+  } else {
+    nf = win->nf;
+    kend = win->kend;
+    has_soft = win->has_soft != 0;
+  }
   uint64_t key = 0;
   if (node < N) {
-    const bool kept = nf >= 1 && !win->error && kept_node(c, s, node, st->next_start, win->kend);
+    const bool kept = nf >= 1 && !win->error && kept_node(c, s, node, st->next_start, kend);
     if (kept && nf > 1) {
-      const bool ign = win->has_soft && s.ign[node];
+      const bool ign = has_soft && s.ign[node];
       const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
       // prioritizeNodes: no score plugins and no extenders -> 1; the extenders'
       // combined scores are added to the plugin total
@@ -758,14 +878,28 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       if (s.ext_score) tot += s.ext_score[node];
       for (int k = 0; k < S; k++) {
         const int32_t kind = norm_kind(prof.score[k]);
-        const int64_t raw = s.raw[(size_t)k * N + node];
+        int64_t raw, gmax = 0, gmin = 0;
+        if (kind != kNormNone) {
+          gmax = from_max_image(win->ext[2 * k]);
+          gmin = from_min_image(win->ext[2 * k + 1]);
+        }
+        if (fuse_ext && kind == kNormPTS) {
+          raw = 0;
+          if (has_soft) {                          // counts -> scores (a non-decreasing map)
+            const int32_t ms = P.uses[soft].arg;
+            if (!ign) raw = soft_score(soft_count(c, s, P.uses[soft], soft, node), w_soft, ms);
+            if (win->ext[2 * k]) gmax = soft_score(gmax, w_soft, ms);
+            if (win->ext[2 * k + 1]) gmin = soft_score(gmin, w_soft, ms);
+          }
+        } else {
+          raw = s.raw[(size_t)k * N + node];
+        }
         int64_t nv = raw;
         if (kind != kNormNone) {
           if (kind == kNormPTS && ign)
             nv = 0;
           else
-            nv = normalize_value(kind, raw, from_max_image(win->ext[2 * k]), from_min_image(win->ext[2 * k + 1]),
-                                 ipa_nonempty);
+            nv = normalize_value(kind, raw, gmax, gmin, ipa_nonempty);
           const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
           tot += nv * w;
         }
@@ -1146,13 +1280,14 @@ void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent
   if (evs) (void)hipEventRecord(evs[1], stream);
   if (topo && !a.fuse_min) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, topo && a.fuse_min);
+  const int32_t fx = NOWIN && !COMPAT && a.fuse_ext;   // extrema in the filter pass, no k_extrema
+  k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, topo && a.fuse_min, fx);
   if (evs) (void)hipEventRecord(evs[3], stream);
   if (!NOWIN) k_window<COMPAT><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_extrema<NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (!fx) k_extrema<NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[5], stream);
-  k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, fx);
   if (evs) (void)hipEventRecord(evs[6], stream);
   k_bind<NOWIN><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
   if (evs) (void)hipEventRecord(evs[7], stream);
@@ -1179,7 +1314,7 @@ void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo) {
   const int blocks = (a.c.n + 255) / 256;
   if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
+  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
   k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
 }
 
@@ -1187,13 +1322,13 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0);
   k_bind<false><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
 }
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {
   // the window-free variant writes counters: time the windowed one (same work per node)
-  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
+  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
 }
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
@@ -1209,7 +1344,7 @@ void launch_pshard_topo(const LaunchArgs& a, hipStream_t stream) {
 void launch_pshard_filter(const LaunchArgs& a, bool topo, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   if (topo) k_topo_min<true><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0);
+  k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
   k_wcount_sh<<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.st, a.s);
 }
 
@@ -1225,7 +1360,7 @@ void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream) {
 
 void launch_pshard_select(const LaunchArgs& a, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
-  k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o);
+  k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0);
 }
 
 void launch_pshard_bind(const LaunchArgs& a, hipStream_t stream) {

@@ -226,6 +226,17 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0
   const int tid = threadIdx.x;
   for (int x = tid; x < nu * kLdsDom; x += blockDim.x) s_dom[x / kLdsDom][x % kLdsDom] = 0;
   if (tid == 0) s_flags = 0;
+  // the PTS pair-registration rows the no-window filter pass fills for this
+  // pod start empty (k_bind used to clear them after the cycle)
+  if (blockIdx.x == 0 && (P0.bflags[pi] & kPodRegistersValues)) {
+    const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use u = P.uses[i];           // staged: use_first == 0
+      if (!use_registers_values(u)) continue;
+      const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
+      for (int x = tid; x < words; x += blockDim.x) s.regbm[(size_t)i * vwords + x] = 0;
+    }
+  }
   __syncthreads();
   const int32_t node = blockIdx.x * blockDim.x + tid;
   uint32_t flags = 0;
@@ -942,25 +953,15 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   }
 }
 
-// NOWIN also returns the counters, registration bitmaps and extrema slots to
-// zero for the next cycle (k_window resets its own otherwise).
+// NOWIN also returns the counters and extrema slots to zero for the next
+// cycle (k_window resets its own otherwise; k_topo_prefilter clears the
+// registration rows).
 template <bool NOWIN>
 __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
                                              int32_t* __restrict__ chosen_out) {
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
-  if (NOWIN) {
-    const ksim_pod& pp = P.pods[pi];
-    const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
-    for (int i = 0; i < pp.use_count; i++) {
-      const ksim_topo_use u = P.uses[pp.use_first + i];
-      if (!use_registers_values(u)) continue;
-      const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
-      for (int x = threadIdx.x; x < words; x += blockDim.x) s.regbm[(size_t)i * vwords + x] = 0;
-    }
-  }
-  __syncthreads();
   if (threadIdx.x != 0) return;
   const int32_t N = c.n, nf = win->nf, cut = win->cut, error = win->error;
   const int32_t chosen = win->best && !error ? key_node(win->best) : -1;   // unsharded: base == 0

@@ -293,9 +293,10 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("kernel") == dominant and tj.get("nodes") == knodes:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+            for entry in (tj if isinstance(tj, list) else [tj]):    # PMC measurements, by kernel and size
+                if entry.get("kernel") == dominant and entry.get("nodes") == knodes:
+                    traffic = entry.get("hbm_bytes_per_launch")
+        except (OSError, ValueError, AttributeError):
             traffic = None
 
     seeds = {2: "0x4B53494D0002", 3: "0x4B53494D0003", 4: "0x4B53494D0004", 5: "0x4B53494D0002/0005"}

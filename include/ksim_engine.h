@@ -368,8 +368,16 @@ void ksim_destroy(ksim_handle* h);
 const char* ksim_last_error(const ksim_handle* h);
 
 /* ---- configuration / snapshot ------------------------------------------- */
+/* The compiled profile: plugin order and enable bits, score weights, plugin
+ * args.  Replaces what the simulator hands upstream scheduler.New after
+ * convertConfigurationForSimulator (simulator/scheduler/scheduler.go:199-249),
+ * ConvertForSimulator (scheduler/plugin/plugins.go:185-288) and NewPluginConfig
+ * (plugins.go:103-179). */
 int ksim_set_profile(ksim_handle* h, const ksim_profile* p);
-/* Replace the whole snapshot (nodes already in nodeTree order). Resets nextStartNodeIndex. */
+/* Replace the whole snapshot (nodes already in nodeTree order). Resets
+ * nextStartNodeIndex.  The device-side counterpart of the scheduler cache's
+ * Snapshot / UpdateSnapshot that the wrapped plugins read through
+ * framework.NodeInfo (scheduler/plugin/wrappedplugin.go:491, 388). */
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* nodes, const ksim_vocab* vocab);
 /* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
@@ -384,7 +392,14 @@ int ksim_set_next_start(ksim_handle* h, int32_t next_start);
 int ksim_set_pod_seq(ksim_handle* h, int64_t seq);
 
 /* ---- scheduling cycles --------------------------------------------------- */
-/* One full cycle for pod `pod_index` of `pods` (compat mode) incl. assume/bind. */
+/* One full cycle for pod `pod_index` of `pods` (compat mode) incl. assume/bind.
+ * It replaces the original-plugin calls inside the wrapped plugins: PreFilter
+ * (scheduler/plugin/wrappedplugin.go:459-486), Filter (:491-516), PreScore
+ * (:427-454), Score (:388-413), NormalizeScore (:346-383), and the selected
+ * node that Reserve records (:583-612).  fail_plugin / fail_detail, raw /
+ * norm and total are what those wrappers pass to Store.AddFilterResult,
+ * AddScoreResult and AddNormalizedScoreResult
+ * (scheduler/plugin/resultstore/store.go:418-502). */
 int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
 
 /* The same cycle around the host's extender round trip (SURVEY §8(f) 4;
@@ -403,14 +418,19 @@ int ksim_eval_pod(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, k
  *                         selectHost and the bind; every output as ksim_eval_pod.
  * nextStartNodeIndex advances by the filter pass, as upstream (before the
  * extenders).  Unsharded handles only. */
+/* The simulator's extender service forwards these calls to the extenders
+ * (scheduler/extender/extender.go:122-148, Filter and Prioritize). */
 int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
 int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t* ext_score, ksim_eval_out* out);
-/* Assume/forget a pod on a node (NodeInfo.AddPod / RemovePod). */
+/* Assume/forget a pod on a node (NodeInfo.AddPod / RemovePod): the state change
+ * behind Reserve / Unreserve (scheduler/plugin/wrappedplugin.go:583, 617). */
 int ksim_assume(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
 int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
 
 /* Batch mode: upload a pod set once (device-resident), then schedule a range
- * of it in queue order; chosen[i] = node position or -1.  */
+ * of it in queue order; chosen[i] = node position or -1.  The whole-cycle
+ * entry point of SURVEY §8(b) (ksim_schedule_batch): the same placements as
+ * running the wrapped plugins pod by pod, without a Go call per node. */
 int ksim_load_pods(ksim_handle* h, const ksim_pod_set* pods);
 int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count,
                          int32_t* chosen, ksim_batch_stats* stats);
@@ -500,7 +520,9 @@ typedef struct ksim_preempt_out {
 int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b);
 /* DefaultPreemption's PostFilter for an unschedulable pod of `priority`
  * (default_preemption.go / preemption.go, v1.26) on the current snapshot,
- * without changing it:
+ * without changing it.  It replaces the original plugin's PostFilter that the
+ * wrapper calls and records (scheduler/plugin/wrappedplugin.go:518-544,
+ * Store.AddPostFilterResult store.go:437):
  *   potential nodes  the nodes whose filter status is Unschedulable, i.e. the
  *                    ones that failed NodeResourcesFit (the plugins before it
  *                    return UnschedulableAndUnresolvable);

@@ -47,9 +47,10 @@ __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPod
   return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar);
 }
 
-__global__ __launch_bounds__(256) void k_adapt_mask(DevCluster c, DevPods P, BatchProg bp,
+__global__ __launch_bounds__(256) void k_adapt_mask(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
                                                     const DevState* __restrict__ st, uint64_t* __restrict__ amask,
                                                     int32_t n_words) {
+  const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
   const int32_t j = blockIdx.y;
   const int32_t pi = base + j;
@@ -146,13 +147,16 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
 // (complete when it lists every kept node).  Each wave keeps its lanes' best T
 // keys and extracts its own top-T; wave 0 merges the four lists.  Pods past
 // the exact windows get an empty incomplete list, which ends the chain there.
-__global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+__global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
+                                                   const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words,
                                                    const int32_t* __restrict__ awin,
                                                    const int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
                                                    int32_t* __restrict__ topk_cnt,
                                                    int32_t* __restrict__ topk_complete) {
+  const ksim_profile& prof = *prof_p;
+  const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_top[4][kTopT];
   __shared__ int32_t s_kept[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -223,7 +227,9 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, ksim
   }
 }
 
-__global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+__global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P,
+                                                            const ksim_profile* __restrict__ prof_p,
+                                                            const BatchProg* __restrict__ bp_p,
                                                             const DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ amask, int32_t n_words,
                                                             const int32_t* __restrict__ awin,
@@ -231,6 +237,8 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
                                                             const int32_t* __restrict__ chain_end,
                                                             uint64_t* __restrict__ pmax,
                                                             int32_t* __restrict__ abroken) {
+  const ksim_profile& prof = *prof_p;
+  const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t base = st->cursor;
@@ -297,16 +305,16 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   const int32_t n_words = (a.c.n + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_adapt_mask<<<dim3((n_words + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.bp, a.st, a.s.amask, n_words);
+  k_adapt_mask<<<dim3((n_words + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st, a.s.amask, n_words);
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_adapt_top<<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
+  k_adapt_top<<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
                                                   a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete);
   if (evs) (void)hipEventRecord(evs[3], stream);
   launch_chain(a, stream);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_adapt_pairs<<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.amask, n_words, a.s.awin,
+  k_adapt_pairs<<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
                                                        a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
   if (evs) (void)hipEventRecord(evs[5], stream);
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,

@@ -38,9 +38,12 @@ namespace ksim {
 // and runs the cpu/memory key only (no static-filter or generic code, which
 // keeps the kernel small and its registers few).
 template <bool FAST>
-__global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+__global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
+                                                    const BatchProg* __restrict__ bp_p,
                                                     const DevState* __restrict__ st, uint64_t* __restrict__ cand,
                                                     int32_t n_tiles) {
+  const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
+  const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
   const int32_t end = min(st->end, base + kBatchPods);
   const int32_t j = blockIdx.y;                      // one pod of the batch per grid row
@@ -324,11 +327,15 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
 // it owns and M is all-reduced (max) before k_batch_commit.  FAST: as in
 // k_batch_eval (trivial pods, cpu/memory scoring).
 template <bool FAST>
-__global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P, ksim_profile prof, BatchProg bp,
+__global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P,
+                                                            const ksim_profile* __restrict__ prof_p,
+                                                            const BatchProg* __restrict__ bp_p,
                                                             const DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ gkey,
                                                             const int32_t* __restrict__ chain_end,
                                                             uint64_t* __restrict__ pmax) {
+  const ksim_profile& prof = *prof_p;
+  const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
@@ -397,9 +404,9 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const dim3 g1((n_tiles + 3) / 4, kBatchPods);
   if (evs) (void)hipEventRecord(evs[0], stream);
   if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   if (evs) (void)hipEventRecord(evs[1], stream);
   const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
@@ -411,10 +418,10 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   // pair keys, then a separate one-block commit: cheaper than every block of
   // the pairs kernel fencing for a last-block election
   if (a.fast)
-    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
                                                                a.s.pmax);
   else
-    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey,
+    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
                                                                 a.s.chain_end, a.s.pmax);
   if (evs) (void)hipEventRecord(evs[4], stream);
   k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
@@ -425,9 +432,9 @@ void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
   const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
   const dim3 g1((n_tiles + 3) / 4, kBatchPods);
   if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
 }
 
 void launch_chain(const LaunchArgs& a, hipStream_t stream) {
@@ -439,9 +446,9 @@ void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
   const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
   const dim3 g1((n_tiles + 3) / 4, kBatchPods);
   if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.cand, n_tiles);
+    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
   k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
                                                                a.s.topk_complete, a.s.xsend);
@@ -453,10 +460,10 @@ void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) 
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
   if (a.fast)
-    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey, a.s.chain_end,
+    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
                                                                a.s.pmax);
   else
-    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.prof, a.bp, a.st, a.s.gkey,
+    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
                                                                 a.s.chain_end, a.s.pmax);
 }
 

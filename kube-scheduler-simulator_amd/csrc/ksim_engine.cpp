@@ -75,6 +75,11 @@ struct ksim_handle {
   bool has_profile = false;
   ksim_profile prof{};
   BatchProg bp{};
+  // device copies of prof / bp, read by the batch-path kernels: a captured
+  // batch graph then survives a weight change (ksim_set_profile)
+  ksim_profile* d_prof = nullptr;
+  BatchProg* d_bp = nullptr;
+  std::vector<size_t> pod_buf_bytes;    // sizes of pod_bufs (ksim_load_pods reuses same-sized buffers)
 
   bool has_cluster = false;
   DevCluster dc{};
@@ -176,11 +181,16 @@ int upload(ksim_handle* h, std::vector<DevBuf>& owner, const void* src, size_t b
   return KSIM_OK;
 }
 
-void drop_graphs(ksim_handle* h) {
+// The per-pod cycle graphs (their kernels take the profile by value).
+void drop_cycle_graphs(ksim_handle* h) {
   for (auto& g : h->graph_cycle) {
     if (g) (void)hipGraphExecDestroy(g);
     g = nullptr;
   }
+}
+
+void drop_graphs(ksim_handle* h) {
+  drop_cycle_graphs(h);
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   h->graph_batch_fast = nullptr;
@@ -327,6 +337,8 @@ LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen) {
   a.P = P;
   a.prof = h->prof;
   a.bp = h->bp;
+  a.dprof = h->d_prof;
+  a.dbp = h->d_bp;
   a.st = h->st;
   a.s = h->sc;
   a.o = h->eo;
@@ -647,7 +659,11 @@ int ksim_create(int device, ksim_handle** out) {
   h->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
-      hipMalloc(&h->st, sizeof(DevState)) != hipSuccess || hipMemset(h->st, 0, sizeof(DevState)) != hipSuccess) {
+      hipMalloc(&h->st, sizeof(DevState)) != hipSuccess || hipMemset(h->st, 0, sizeof(DevState)) != hipSuccess ||
+      // written only by ksim_set_profile, on the engine's stream (a null-stream
+      // memset here would not be ordered before that copy)
+      hipMalloc(&h->d_prof, sizeof(ksim_profile)) != hipSuccess ||
+      hipMalloc(&h->d_bp, sizeof(BatchProg)) != hipSuccess) {
     delete h;
     return KSIM_E_DEVICE;
   }
@@ -668,6 +684,8 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->pre_bufs);
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   if (h->st) (void)hipFree(h->st);
+  if (h->d_prof) (void)hipFree(h->d_prof);
+  if (h->d_bp) (void)hipFree(h->d_bp);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -689,6 +707,10 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   if (p->fit_n_res < 0 || p->fit_n_res > KSIM_MAX_RES || p->ba_n_res < 0 || p->ba_n_res > KSIM_MAX_RES)
     return set_err(h, KSIM_E_INVALID, "scoring resources out of range");
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
+  // window size K is captured by value (from percentageOfNodesToScore)
+  const bool keep_batch_graphs = h->has_profile &&
+                                 h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score;
   h->prof = *p;
   h->has_profile = true;
   // the profile compiled for batchable pods (see BatchProg in ksim_device.h)
@@ -710,9 +732,16 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
     if (p->score[k] == KSIM_PL_BALANCED_ALLOCATION) bp.w_ba += w;
   }
   h->bp = bp;
-  drop_graphs(h);
-  // batchability depends on the profile: a loaded queue must be reloaded
-  free_bufs(h->pod_bufs);
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(h->d_prof, &h->prof, sizeof(ksim_profile), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d_bp, &h->bp, sizeof(BatchProg), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (keep_batch_graphs)
+    drop_cycle_graphs(h);
+  else
+    drop_graphs(h);
+  // batchability depends on the profile: a loaded queue must be reloaded (its
+  // buffers stay allocated for ksim_load_pods to reuse)
   h->dp = DevPods{};
   h->batchable.clear();
   return KSIM_OK;
@@ -760,6 +789,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
   free_bufs(h->pod_bufs);
+  h->pod_buf_bytes.clear();
   h->dp = DevPods{};
   h->batchable.clear();
   h->topo.clear();
@@ -1163,10 +1193,35 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     if ((rc = validate_pod(h, ps, i))) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  drop_graphs(h);
-  free_bufs(h->pod_bufs);
-  if (h->d_chosen) (void)hipFree(h->d_chosen);
-  h->d_chosen = nullptr;
+  // A queue with the same array sizes as the loaded one (a policy sweep
+  // reloading its pods under each profile) is copied into the same buffers:
+  // the device pointers, and so every captured graph, stay valid.
+  const size_t np1 = (size_t)std::max(ps->n_pods, 1);
+  const std::vector<size_t> bytes = {sizeof(ksim_pod) * (size_t)ps->n_pods,
+                                     sizeof(ksim_label_expr) * (size_t)ps->n_exprs,
+                                     sizeof(ksim_term) * (size_t)ps->n_terms,
+                                     4 * np1,
+                                     4 * np1,
+                                     sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0),
+                                     sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0)};
+  const bool reuse = h->d_chosen && h->pod_bufs.size() == bytes.size() && h->pod_buf_bytes == bytes;
+  if (!reuse) {
+    drop_graphs(h);
+    free_bufs(h->pod_bufs);
+    h->pod_buf_bytes.clear();
+    if (h->d_chosen) (void)hipFree(h->d_chosen);
+    h->d_chosen = nullptr;
+  }
+  size_t next_buf = 0;
+  auto put = [&](const void* src, size_t nbytes, void** out) -> int {
+    if (!reuse) return upload(h, h->pod_bufs, src, nbytes, out);
+    DevBuf& b = h->pod_bufs[next_buf++];
+    const hipError_t e = (src && nbytes) ? hipMemcpyAsync(b.p, src, nbytes, hipMemcpyHostToDevice, h->stream)
+                                         : hipMemsetAsync(b.p, 0, b.bytes, h->stream);
+    if (e != hipSuccess) return hip_fail(h, e, "pod upload");
+    *out = b.p;
+    return KSIM_OK;
+  };
   std::vector<int32_t> nc((size_t)std::max(ps->n_pods, 1), 0);
   std::vector<int32_t> bf((size_t)std::max(ps->n_pods, 1), 0);
   h->batchable.assign((size_t)ps->n_pods, 0);
@@ -1201,27 +1256,30 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   }
   DevPods P{};
   void* p = nullptr;
-  if ((rc = upload(h, h->pod_bufs, ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return rc;
+  if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return rc;
   P.pods = (const ksim_pod*)p;
-  if ((rc = upload(h, h->pod_bufs, ps->exprs, sizeof(ksim_label_expr) * ps->n_exprs, &p))) return rc;
+  if ((rc = put(ps->exprs, sizeof(ksim_label_expr) * ps->n_exprs, &p))) return rc;
   P.exprs = (const ksim_label_expr*)p;
-  if ((rc = upload(h, h->pod_bufs, ps->terms, sizeof(ksim_term) * ps->n_terms, &p))) return rc;
+  if ((rc = put(ps->terms, sizeof(ksim_term) * ps->n_terms, &p))) return rc;
   P.terms = (const ksim_term*)p;
-  if ((rc = upload(h, h->pod_bufs, nc.data(), 4 * nc.size(), &p))) return rc;
+  if ((rc = put(nc.data(), 4 * nc.size(), &p))) return rc;
   P.norm_const = (const int32_t*)p;
-  if ((rc = upload(h, h->pod_bufs, bf.data(), 4 * bf.size(), &p))) return rc;
+  if ((rc = put(bf.data(), 4 * bf.size(), &p))) return rc;
   P.bflags = (const int32_t*)p;
-  if ((rc = upload(h, h->pod_bufs, ps->uses, sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0), &p))) return rc;
+  if ((rc = put(ps->uses, sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
-  if ((rc = upload(h, h->pod_bufs, ps->adds, sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0), &p))) return rc;
+  if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0), &p))) return rc;
   P.adds = (const ksim_class_add*)p;
   P.n_uses = ps->n_uses;
   P.n_adds = ps->n_adds;
   P.n_pods = ps->n_pods;
   P.n_exprs = ps->n_exprs;
   P.n_terms = ps->n_terms;
-  HIPCHK(h, hipMalloc(&h->d_chosen, 4 * (size_t)std::max(ps->n_pods, 1)));
-  HIPCHK(h, hipMemsetAsync(h->d_chosen, 0xff, 4 * (size_t)std::max(ps->n_pods, 1), h->stream));
+  if (!reuse) {
+    HIPCHK(h, hipMalloc(&h->d_chosen, 4 * np1));
+    h->pod_buf_bytes = bytes;
+  }
+  HIPCHK(h, hipMemsetAsync(h->d_chosen, 0xff, 4 * np1, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->dp = P;
   return KSIM_OK;

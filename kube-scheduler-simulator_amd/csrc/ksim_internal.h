@@ -33,6 +33,8 @@ struct LaunchArgs {
   DevScratch s;
   DevEvalOut o;
   int32_t* chosen;   // [n_pods] device, may be null
+  const ksim_profile* dprof = nullptr;   // device copies of prof / bp (the batch kernels read these)
+  const BatchProg* dbp = nullptr;
   bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
   bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
   bool fuse_ext = false;  // per-pod runs: every pod has <= 1 ScheduleAnyway spread constraint (K = N: no k_extrema)

@@ -147,6 +147,78 @@ __global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict_
   }
 }
 
+// The same merge with the pod's tile lists in registers (n_tiles * kTileCand
+// <= 64 * NREG, e.g. 5,000 nodes: 80 keys, NREG = 2), one 64-lane block per
+// pod.  Key x = s * 64 + lane is entry x % kTileCand of tile x / kTileCand.
+// Tile lists are sorted and keys are distinct (the node is in the key), so
+// the max over all remaining keys is the max over the tile heads the LDS
+// version scans; consuming entry kTileCand - 1 of a tile ends the prefix.
+template <int NREG>
+__global__ __launch_bounds__(64) void k_batch_merge_reg(const DevState* __restrict__ st,
+                                                        const uint64_t* __restrict__ cand, int32_t n_tiles,
+                                                        uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                                        int32_t* __restrict__ topk_complete,
+                                                        uint64_t* __restrict__ xsend) {
+  const int lane = threadIdx.x;
+  const int32_t j = blockIdx.x;
+  const int32_t per = n_tiles * kTileCand;
+  const uint64_t* src = cand + (size_t)j * per;
+  uint64_t v[NREG];
+#pragma unroll
+  for (int s = 0; s < NREG; s++) v[s] = s * 64 + lane < per ? src[s * 64 + lane] : 0;   // before the state load
+  const int32_t base = st->cursor;
+  if (base + j >= min(st->end, base + kBatchPods)) return;   // block-uniform
+  uint64_t mine = 0;
+  int32_t cnt = 0, complete = 0;
+  for (int t = 0; t < kTopT; t++) {
+    uint64_t best = v[0];
+#pragma unroll
+    for (int s = 1; s < NREG; s++) best = umax64(best, v[s]);
+    const uint64_t m = wave_max_u64_dpp(best);
+    if (m == 0) { complete = 1; break; }
+    if (lane == t) mine = m;
+    cnt = t + 1;
+    bool stop = false;
+    if (best == m) {
+#pragma unroll
+      for (int s = 0; s < NREG; s++)
+        if (v[s] == m) {
+          v[s] = 0;
+          stop = ((s * 64 + lane) % kTileCand) == kTileCand - 1;
+        }
+    }
+    if (__ballot(stop)) break;
+  }
+  if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
+  if (lane == 0) {
+    topk_cnt[j] = cnt;
+    topk_complete[j] = complete;
+  }
+  if (xsend) {
+    uint64_t* x = xsend + (size_t)j * kXRec;
+    if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
+    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)cnt | ((uint64_t)complete << 32);
+  }
+}
+
+// Merge launcher: registers for small tile counts, LDS otherwise.
+static void launch_merge(const DevState* st, const uint64_t* cand, int32_t n_tiles, uint64_t* topk,
+                         int32_t* topk_cnt, int32_t* topk_complete, uint64_t* xsend, hipStream_t stream) {
+  const int32_t per = n_tiles * kTileCand;
+  static const bool force_lds = getenv("KSIM_MERGE_LDS") != nullptr;   // A/B switch
+  if (force_lds || per > 256) {
+    const size_t per_wave = (size_t)per * 8 + (size_t)((n_tiles + 7) / 8) * 8;
+    k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete,
+                                                                 xsend);
+  } else if (per <= 64) {
+    k_batch_merge_reg<1><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
+  } else if (per <= 128) {
+    k_batch_merge_reg<2><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
+  } else {
+    k_batch_merge_reg<4><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
+  }
+}
+
 // Sharded: merge the R shard records of pod j (all-gathered, [R][B][kXRec])
 // into the pod's global top-T.  Entry x = s * T + e (shard s, entry e) sits in
 // lane x % 64, slot x / 64.  A key is provably in the global order if it is
@@ -408,9 +480,7 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   else
     k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
-  k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
-                                                               a.s.topk_complete, nullptr);
+  launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, stream);
   if (evs) (void)hipEventRecord(evs[2], stream);
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
@@ -449,9 +519,7 @@ void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
     k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
   else
     k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  const size_t per_wave = (size_t)n_tiles * kTileCand * 8 + (size_t)((n_tiles + 7) / 8) * 8;
-  k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt,
-                                                               a.s.topk_complete, a.s.xsend);
+  launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend, stream);
 }
 
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {

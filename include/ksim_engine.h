@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 3
+#define KSIM_ABI_VERSION 4
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -101,6 +101,19 @@ enum ksim_plugin {
 #define KSIM_POD_HAS_SCALAR              4u  /* len(request.ScalarResources) > 0 */
 #define KSIM_POD_HAS_HOST_PORTS          8u  /* ports not compiled to KSIM_USE_NODE_PORT uses -> KSIM_E_UNSUPPORTED */
 #define KSIM_POD_HAS_VOLUMES            16u  /* unsupported by the engine -> KSIM_E_UNSUPPORTED */
+/* NodeAffinity's PreFilterResult (nodeaffinity.PreFilter: the union over the
+ * required terms of the intersection of each term's metadata.name In
+ * matchFields; a term without one means all nodes, i.e. no flag).  The cycle
+ * scans only those nodes: nn[nn_first .. nn_first + nn_count) of the pod set,
+ * node positions in increasing (nodeTree) order, from nextStartNodeIndex mod
+ * nn_count (schedule_one.go findNodesThatFitPod / findNodesThatPassFilters,
+ * where upstream visits the set in Go map order).  nn_count == 0: the terms
+ * conflict, the pod is unschedulable without any Filter call ("pod affinity
+ * terms conflict"); nextStartNodeIndex stays. */
+#define KSIM_POD_NODE_NAMES             32u
+/* ... and a listed name is not a node of the snapshot: NodeInfos().Get fails
+ * and the cycle fails with framework.Error before any Filter call. */
+#define KSIM_POD_NODE_NAMES_UNKNOWN     64u
 
 /* pod nb_flags (NetworkBandwidth request annotations) */
 #define KSIM_POD_NB_INGRESS_BAD 1u   /* the ingress request annotation does not parse */
@@ -238,7 +251,7 @@ typedef struct ksim_pod {
   int32_t  add_first, add_count;             /* count-class contributions once bound (NodeInfo.AddPod) */
   uint32_t topo_flags;                       /* KSIM_POD_IPA_* */
   uint32_t nb_flags;                         /* KSIM_POD_NB_* */
-  int32_t  _reserved;
+  int32_t  nn_first, nn_count;               /* PreFilterResult.NodeNames (KSIM_POD_NODE_NAMES) */
   int64_t  nb_req;                           /* NetworkBandwidth Filter request (milli): ingress
                                                 + egress request annotations, each falling back
                                                 to the *-bandwidth annotation */
@@ -300,6 +313,9 @@ typedef struct ksim_pod_set {
   int32_t n_adds;
   const ksim_topo_use* uses;
   const ksim_class_add* adds;
+  int32_t n_nn;                     /* entries of nn */
+  int32_t _pad2;
+  const int32_t* nn;                /* PreFilterResult node positions (see KSIM_POD_NODE_NAMES) */
 } ksim_pod_set;
 
 /* Profile: the converted KubeSchedulerProfile (simulator/scheduler/scheduler.go:199-249,
@@ -486,7 +502,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
  * (a pod's exact choice was a node bound earlier in its batch, ending it);
  * out[3..18] device phase-clock accumulators since ksim_set_cluster (100 MHz
  * ticks: [3] chain prologue, [4] chain loop, [5] chain epilogue, [6] chain
- * launches).  Returns the number of values written (<= n). */
+ * launches); out[19] hipGraphs captured since ksim_create (a weight sweep that
+ * keeps its graphs across ksim_set_profile captures none).  Returns the number
+ * of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),
  * out[1] candidate keys kept per pod (T), out[2] nodes per wave tile,

@@ -174,7 +174,6 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   const int32_t kend = cut >= 0 ? cut : n;
   const int32_t pi = base + j;
   const ksim_pod& p = P.pods[pi];
-  const int32_t nc = P.norm_const[pi];
   const int64_t seq = st->pod_seq + j;
   const uint64_t* mask = amask + (size_t)j * n_words;
   uint64_t a[kTopT];
@@ -188,7 +187,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
     if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
     kept++;
     const NodeRow r = load_res_row(c, node);      // scores read the resource columns only
-    a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base));
+    a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
 #pragma unroll
     for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
   }
@@ -263,7 +262,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
         const bool was = (amask[(size_t)j * n_words + (node >> 6)] >> (node & 63)) & 1ull;
         if (cut >= 0 && was && !now) brk = true;
-        if (off < kend && now) v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, st->pod_seq + j, c.base);
+        if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base);
       }
     }
   }

@@ -53,7 +53,6 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
   const int32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tile >= n_tiles) return;                       // wave-uniform
   const ksim_pod& p = P.pods[pi];
-  const int32_t nc = P.norm_const[pi];
   const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
   const int64_t seq = st->pod_seq + j;
   // The lane's kNodesPerLane keys, kept sorted (descending) by insertion; the
@@ -68,10 +67,10 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
       // trivial: the static filters pass everywhere and the pod requests no
       // scalar resources, so only the resource columns are read
       if constexpr (FAST) {
-        kk = dyn_key_cpu_mem(prof, bp, p, nc, load_res_row(c, node), seq, c.base);
+        kk = dyn_key_cpu_mem(prof, bp, p, load_res_row(c, node), seq, c.base);
       } else {
         const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, nc, r, c.n_scalar, seq, c.base);
+        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
       }
     }
     a[3] = umax64(a[3], kk);
@@ -429,12 +428,12 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
       if constexpr (FAST) {
         NodeRow r = load_res_row(c, local);
         row_add_pod(r, P.pods[base + k], 1);
-        v = dyn_key_cpu_mem(prof, bp, p, P.norm_const[base + j], r, seq0 + j, c.base);
+        v = dyn_key_cpu_mem(prof, bp, p, r, seq0 + j, c.base);
       } else {
         NodeRow r = load_row(c, local);
         row_add_pod(r, P.pods[base + k], 1);
         if ((P.bflags[base + j] & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r))
-          v = dyn_key(prof, bp, p, P.norm_const[base + j], r, c.n_scalar, seq0 + j, c.base);
+          v = dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base);
       }
     }
   }

@@ -64,11 +64,11 @@ struct DevPods {
   const ksim_pod* pods;
   const ksim_label_expr* exprs;
   const ksim_term* terms;
-  const int32_t* norm_const;     // [n_pods] batch path: constant sum of weighted normalized scores
+  const int32_t* nn;             // PreFilterResult.NodeNames positions (KSIM_POD_NODE_NAMES), sorted per pod
   const int32_t* bflags;         // [n_pods] batch path: kBatch* flags
   const ksim_topo_use* uses;
   const ksim_class_add* adds;
-  int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, _pad[3];
+  int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, _pad[2];
 };
 
 // Scheduler state that survives across cycles (sched.nextStartNodeIndex,
@@ -112,17 +112,69 @@ struct WinState {
   int32_t cut, kend, nf, evaluated, k, has_soft;
   int32_t nfeas, nign;                   // no-window cycles (K = N): counted by k_filter_score
   int32_t error;                         // kCycleError*: the cycle fails with framework.Error
-  int32_t _pad;
+  int32_t nscan;                         // nodes the cycle scans (ScanSet.n): nextStartNodeIndex modulus
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
-  uint64_t best;                         // TB argmax key
 };
+
+// The nodes one cycle scans, in scan order: every node of
+// the cluster in nodeTree order from nextStartNodeIndex, or only NodeAffinity's
+// PreFilterResult.NodeNames (KSIM_POD_NODE_NAMES; [upstream] findNodesThatFitPod
+// then scans that list from nextStartNodeIndex mod its length and advances
+// nextStartNodeIndex mod its length).  Positions are global (sharded handles
+// scan the whole cluster's order).
+struct ScanSet {
+  const int32_t* list;   // sorted global positions; nullptr: every one of n nodes
+  int32_t n;             // scan length (0: PreFilter rejected the pod, nothing is scanned)
+  int32_t start;         // first scan position's index (nextStartNodeIndex mod n)
+};
+
+__device__ __forceinline__ ScanSet scan_set(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                            int32_t next_start) {
+  ScanSet s;
+  if (p.flags & KSIM_POD_NODE_NAMES) {
+    s.list = P.nn + p.nn_first;
+    s.n = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 0 : p.nn_count;
+  } else {
+    s.list = nullptr;
+    s.n = c.n_total;
+  }
+  s.start = s.n > 0 ? next_start % s.n : 0;
+  return s;
+}
+
+// Global position of scan position r (0 <= r < s.n).
+__device__ __forceinline__ int32_t scan_node(const ScanSet& s, int32_t r) {
+  int32_t x = s.start + r;
+  if (x >= s.n) x -= s.n;
+  return s.list ? s.list[x] : x;
+}
+
+// Scan position of global node g, or -1 when the cycle does not scan it.
+__device__ __forceinline__ int32_t scan_pos(const ScanSet& s, int32_t g) {
+  int32_t idx = g;
+  if (s.list) {
+    int32_t lo = 0, hi = s.n;                      // lower_bound over the sorted list
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (s.list[mid] < g) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= s.n || s.list[lo] != g) return -1;
+    idx = lo;
+  } else if (s.n == 0) {
+    return -1;
+  }
+  const int32_t r = idx - s.start;
+  return r < 0 ? r + s.n : r;
+}
 
 // Per-cycle scratch written by the filter/score kernel, read by the selection.
 struct DevScratch {
   uint8_t* fail;         // [n] filter-order index of first failure or KSIM_PASSED
   uint8_t* ign;          // [n] feasible node missing a ScheduleAnyway spread key (IgnoredNodes)
   WinState* win;
+  uint64_t* bbest;       // [2 * blocks] k_select: each block's best (max image of the total, TB lo word)
   uint64_t* amask;       // ADAPT batch: S0 feasibility bitmaps [kBatchPods][ceil(n / 64)]
   int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
   int32_t* aexact;       // ADAPT batch: pods whose windows are exact
@@ -193,15 +245,28 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-// selectHost tie-break TB(seed): a single u64 max over (total, hash, node).
-// node < KSIM_MAX_NODES = KSIM_KEY_NODE_MASK keeps the low field >= 1: a valid key is never 0.
+// selectHost tie-break TB(seed): the max of (total, hash26, node) in
+// lexicographic order, total a full int64.  lo = hash26 << 18 | (mask - node)
+// is the tie-break word; node < KSIM_MAX_NODES = KSIM_KEY_NODE_MASK keeps its
+// low field >= 1, so a valid lo is never 0.
+__host__ __device__ __forceinline__ uint64_t tb_lo(uint64_t seed, int64_t seq, int32_t node) {
+  const uint64_t h = splitmix64(seed ^ ((uint64_t)seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
+  return (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
+}
+// One-word key for a total known to lie in [0, 2^20) (kKeyTotalLimit): the
+// batch paths key a pod's nodes by total minus a per-pod constant, which the
+// host proves fits (pod_batchable); the order is the same as (total, lo).
+constexpr int64_t kKeyTotalLimit = 1ll << 20;
 __host__ __device__ __forceinline__ uint64_t tb_key(int64_t total, uint64_t seed, int64_t seq, int32_t node) {
-  uint64_t h = splitmix64(seed ^ ((uint64_t)seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
-  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
+  return ((uint64_t)total << 44) | tb_lo(seed, seq, node);
 }
 __host__ __device__ __forceinline__ int32_t key_node(uint64_t key) {
   return (int32_t)(KSIM_KEY_NODE_MASK - (int32_t)(key & KSIM_KEY_NODE_MASK));
 }
+// Order-preserving u64 image of an int64 (max image), so (total, lo) pairs
+// compare as two u64 words; 0 is below every image of a real total > INT64_MIN.
+__host__ __device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
+__host__ __device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
 
 // NodeInfo aggregates of one node, in registers.
 struct NodeRow {
@@ -439,17 +504,21 @@ __device__ __forceinline__ void calc_alloc_req(const NodeRow& r, const ksim_pod&
   }
 }
 
-// least_allocated.go leastRequestedScore
+// least_allocated.go leastRequestedScore.  (capacity - requested) * 100 is Go
+// int64 arithmetic, which wraps for capacities past 2^56: the product is formed
+// unsigned (defined wrap), and such a quotient is taken exactly (a / b).
 __device__ __forceinline__ int64_t least_requested_score(int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (requested > capacity) return 0;
-  if (capacity < 0 || requested > capacity) return ((capacity - requested) * kMaxNodeScore) / capacity;
-  return div_floor_nonneg((capacity - requested) * kMaxNodeScore, capacity);
+  const int64_t prod = (int64_t)((uint64_t)(capacity - requested) * (uint64_t)kMaxNodeScore);
+  if (capacity < 0 || prod < 0) return prod / capacity;
+  return div_floor_nonneg(prod, capacity);
 }
 
-// leastRequestedScore for capacity > 0 (the quotient is in [0, 100]).
+// leastRequestedScore for 0 < capacity < 2^52 (no wrap; the quotient is in
+// [0, 100]), the general form otherwise.
 __device__ __forceinline__ int64_t least_requested_q100(int64_t requested, int64_t capacity) {
-  if (capacity < 0) return least_requested_score(requested, capacity);
+  if (capacity < 0 || capacity >= (1ll << 52)) return least_requested_score(requested, capacity);
   if (requested > capacity) return 0;
   return div_q100((capacity - requested) * kMaxNodeScore, capacity);
 }
@@ -521,6 +590,7 @@ __device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, c
 constexpr uint8_t kFailError = 0x80;
 constexpr int32_t kCycleErrorFilter = 1;   // an erroring node inside the scanned window
 constexpr int32_t kCycleErrorScore = 2;    // Score returned Skip / Error for a kept node
+constexpr int32_t kCycleErrorPrefilter = 3; // PreFilterResult names a node the snapshot lacks (KSIM_POD_NODE_NAMES_UNKNOWN)
 
 __host__ __device__ __forceinline__ bool nb_error_detail(uint32_t d) { return d >= KSIM_NB_NO_LIMIT; }
 __host__ __device__ __forceinline__ bool fail_is_error(uint8_t f) { return (f & kFailError) && f < KSIM_FAIL_EXTENDER; }
@@ -934,9 +1004,11 @@ __device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const D
 // dyn_key for the default scoring strategies ({cpu, memory} for both
 // LeastAllocated and BalancedAllocation; batchable pods request no scalars):
 // the same arithmetic as the generic functions with the resource loops
-// resolved, so the batch kernels stay small.
+// resolved, so the batch kernels stay small.  The key's total leaves out the
+// pod's constant normalized scores (the same on every node), so it lies in
+// [0, 100 * (w_fit + w_ba)] < kKeyTotalLimit (pod_batchable checks the bound).
 __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, const BatchProg& bp,
-                                                    const ksim_pod& p, int32_t norm_const, const NodeRow& r,
+                                                    const ksim_pod& p, const NodeRow& r,
                                                     int64_t seq, int32_t base) {
   if (bp.has_fit_filter) {
     if (r.num_pods + 1 > r.alloc_pods) return 0;
@@ -946,7 +1018,7 @@ __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, co
         return 0;
     }
   }
-  int64_t tot = norm_const;
+  int64_t tot = 0;
   if (bp.w_fit) {                              // leastResourceScorer over {cpu, memory}
     int64_t ns = 0, ws = 0;
     if (r.alloc_cpu != 0) {
@@ -957,8 +1029,9 @@ __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, co
       ns += least_requested_q100(r.nz_mem + p.nz_mem, r.alloc_mem) * bp.fit_w_mem;
       ws += bp.fit_w_mem;
     }
-    // the weighted mean of scores in [0, 100] is a score-sized quotient
-    const int64_t la = ws == 0 ? 0 : (ns < 0 || ws < 0) ? ns / ws : div_q100(ns, ws);
+    // the weighted mean of scores in [0, 100] is a score-sized quotient (a
+    // wrapped leastRequestedScore of a capacity past 2^56 may leave that range)
+    const int64_t la = ws == 0 ? 0 : (ns < 0 || ws <= 0 || ns > kMaxNodeScore * ws) ? ns / ws : div_q100(ns, ws);
     tot += bp.w_fit * la;
   }
   if (bp.w_ba) {                               // balancedResourceScorer over {cpu, memory}
@@ -984,11 +1057,10 @@ __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, co
 
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).
 __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
-                                            int32_t norm_const, const NodeRow& r, int n_scalar, int64_t seq,
-                                            int32_t base) {
-  if (bp.cpu_mem) return dyn_key_cpu_mem(prof, bp, p, norm_const, r, seq, base);
+                                            const NodeRow& r, int n_scalar, int64_t seq, int32_t base) {
+  if (bp.cpu_mem) return dyn_key_cpu_mem(prof, bp, p, r, seq, base);
   if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
-  int64_t tot = norm_const;
+  int64_t tot = 0;
   if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);
   if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, n_scalar);
   if (prof.n_score == 0) tot = 1;

@@ -138,6 +138,7 @@ struct ksim_handle {
   hipGraphExec_t graph_cycle[8] = {};
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
+  int64_t graph_captures = 0;                  // graphs captured since ksim_create (ksim_get_diag)
 };
 
 namespace {
@@ -198,6 +199,7 @@ void drop_graphs(ksim_handle* h) {
 }
 
 bool plugin_supported(int id) { return id >= 0 && id < KSIM_PL_COUNT; }
+bool is_sharded(const ksim_handle* h);
 
 int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
   const ksim_pod& p = ps->pods[i];
@@ -246,6 +248,18 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
   for (int32_t k = 0; k < p.add_count; k++)
     if (ps->adds[p.add_first + k].cls < 0 || ps->adds[p.add_first + k].cls >= c.n_classes)
       return set_err(h, KSIM_E_INVALID, who + "class add out of range");
+  if (p.flags & KSIM_POD_NODE_NAMES) {
+    if (p.nn_count < 0 || (p.nn_count > 0 && (!ps->nn || p.nn_first < 0 ||
+                                              (int64_t)p.nn_first + p.nn_count > (int64_t)ps->n_nn)))
+      return set_err(h, KSIM_E_INVALID, who + "bad PreFilterResult node range");
+    for (int32_t k = 0; k < p.nn_count; k++) {
+      const int32_t v = ps->nn[p.nn_first + k];
+      if (v < 0 || v >= c.n_total || (k > 0 && v <= ps->nn[p.nn_first + k - 1]))
+        return set_err(h, KSIM_E_INVALID, who + "PreFilterResult nodes must be increasing node positions");
+    }
+    if (is_sharded(h))
+      return set_err(h, KSIM_E_UNSUPPORTED, who + "a PreFilterResult node restriction runs on unsharded handles");
+  }
   return KSIM_OK;
 }
 
@@ -290,36 +304,34 @@ bool profile_nb(const ksim_profile& p) {
   return prof_has_filter(p, KSIM_PL_NETWORK_BANDWIDTH) || prof_has_score(p, KSIM_PL_NETWORK_BANDWIDTH);
 }
 
-bool pod_batchable(const ksim_handle* h, const ksim_pod& p, int32_t& norm_const) {
+// The batch keys carry a pod's total minus its constant normalized part in
+// 20 bits (tb_key): 100 * (w_fit + w_ba) must stay below kKeyTotalLimit, or
+// the pods take the per-pod path, whose (total, TB) pairs are exact for any
+// int64 total.  Pods that NodeAffinity's PreFilterResult restricts scan a node
+// list of their own: per-pod path.
+bool pod_batchable(const ksim_handle* h, const ksim_pod& p) {
   const ksim_profile& prof = h->prof;
   if (p.use_count > 0) return false;
+  if (p.flags & KSIM_POD_NODE_NAMES) return false;
   // NetworkBandwidth runs on the per-pod path (its error statuses end cycles),
   // and so do pods that add to a node's allocated bandwidth
   if (profile_nb(prof) || p.nb_add != 0) return false;
   if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
-  int64_t acc = 0;
+  if ((int64_t)kMaxNodeScore * (h->bp.w_fit + h->bp.w_ba) >= kKeyTotalLimit) return false;
   for (int k = 0; k < prof.n_score; k++) {
-    const int pl = prof.score[k];
-    const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
-    switch (norm_kind(pl)) {
-      case kNormDefaultReverse: {
+    switch (norm_kind(prof.score[k])) {
+      case kNormDefaultReverse:
         for (size_t t = 1; t < h->taint_effect.size(); t++)
           if (h->taint_effect[t] == KSIM_EFFECT_PREFER_NO_SCHEDULE && !((p.tol_prefer[t >> 6] >> (t & 63)) & 1ull))
             return false;
-        acc += 100 * w;
-        break;
-      }
+        break;                                          // every node 100
       case kNormDefault:
-        if (p.pref_term_count > 0) return false;
+        if (p.pref_term_count > 0) return false;        // else every node 0
         break;
-      case kNormPTS:
-        acc += 100 * w;
-        break;
-      default:
+      default:                                          // PodTopologySpread 100, InterPodAffinity 0
         break;
     }
   }
-  norm_const = (int32_t)acc;
   return true;
 }
 
@@ -385,6 +397,7 @@ int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fas
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) return hip_fail(h, e, "hipGraphInstantiate");
+  h->graph_captures++;
   return KSIM_OK;
 }
 
@@ -554,39 +567,46 @@ int x_allreduce(const std::vector<ksim_handle*>& hs, F&& ptr, int64_t count, boo
   return KSIM_OK;
 }
 
+// All-gather of two words per shard: s.xsend[0..1] -> s.xrecv[world][2].
+int x_allgather2(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+  ksim_handle* h0 = hs[0];
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, 2, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+    return KSIM_OK;
+  }
+  GroupPtrs src{}, dst{};
+  src.n = dst.n = (int32_t)hs.size();
+  for (size_t i = 0; i < hs.size(); i++) {
+    src.p[i] = hs[i]->sc.xsend;
+    dst.p[i] = hs[i]->sc.xrecv;
+  }
+  launch_group_gather(src, dst, 2, stream);
+  return KSIM_OK;
+}
+
 // One per-pod cycle (the pod at the shards' common cursor) across node shards.
 int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t stream) {
   ksim_handle* h0 = hs[0];
   const int R = (int)hs.size();
   const bool topo = h0->topo[pod] != 0;
   const int64_t xdom = h0->xdom_len[pod], xreg = h0->xreg_len[pod];
+  const int32_t world = h0->comm ? h0->world : R;
   int rc;
   if (topo) {
     for (auto* h : hs) launch_pshard_topo(make_args(h, h->dp, h->d_chosen), stream);
     if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.xdom; }, xdom, false, stream))) return rc;
   }
   for (auto* h : hs) launch_pshard_filter(make_args(h, h->dp, h->d_chosen), topo, stream);
-  if (h0->comm) {
-    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, 2, ncclUint64, h0->comm, stream);
-    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
-  } else {
-    GroupPtrs src{}, dst{};
-    src.n = dst.n = R;
-    for (int i = 0; i < R; i++) {
-      src.p[i] = hs[i]->sc.xsend;
-      dst.p[i] = hs[i]->sc.xrecv;
-    }
-    launch_group_gather(src, dst, 2, stream);
-  }
-  const int32_t world = h0->comm ? h0->world : R;
+  if ((rc = x_allgather2(hs, stream))) return rc;      // C3: feasible counts per shard
   for (int i = 0; i < R; i++)
     launch_pshard_window(make_args(hs[i], hs[i]->dp, hs[i]->d_chosen), h0->comm ? h0->rank : i, world, stream);
   if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.xreg; }, xreg, false, stream))) return rc;
   for (auto* h : hs) launch_pshard_extrema(make_args(h, h->dp, h->d_chosen), xreg > 0, stream);
   if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.win->ext; }, kExtWords, true, stream))) return rc;
   for (auto* h : hs) launch_pshard_select(make_args(h, h->dp, h->d_chosen), stream);
-  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return &h->sc.win->best; }, 1, true, stream))) return rc;
-  for (auto* h : hs) launch_pshard_bind(make_args(h, h->dp, h->d_chosen), stream);
+  if ((rc = x_allgather2(hs, stream))) return rc;      // C2: every shard's (total, TB) best
+  for (auto* h : hs) launch_pshard_bind(make_args(h, h->dp, h->d_chosen), world, stream);
   HIPCHK(h0, hipGetLastError());
   return KSIM_OK;
 }
@@ -706,13 +726,6 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   }
   if (p->fit_n_res < 0 || p->fit_n_res > KSIM_MAX_RES || p->ba_n_res < 0 || p->ba_n_res > KSIM_MAX_RES)
     return set_err(h, KSIM_E_INVALID, "scoring resources out of range");
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
-  // window size K is captured by value (from percentageOfNodesToScore)
-  const bool keep_batch_graphs = h->has_profile &&
-                                 h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score;
-  h->prof = *p;
-  h->has_profile = true;
   // the profile compiled for batchable pods (see BatchProg in ksim_device.h)
   BatchProg bp{};
   bp.cpu_mem = p->fit_n_res == 2 && p->fit_res[0] == KSIM_RES_CPU && p->fit_res[1] == KSIM_RES_MEMORY &&
@@ -731,19 +744,33 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
     if (p->score[k] == KSIM_PL_NODE_RESOURCES_FIT) bp.w_fit += w;
     if (p->score[k] == KSIM_PL_BALANCED_ALLOCATION) bp.w_ba += w;
   }
-  h->bp = bp;
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(h->d_prof, &h->prof, sizeof(ksim_profile), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->d_bp, &h->bp, sizeof(BatchProg), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (keep_batch_graphs)
-    drop_cycle_graphs(h);
-  else
-    drop_graphs(h);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
+  // window size K is captured by value (from percentageOfNodesToScore)
+  const bool keep_batch_graphs = h->has_profile &&
+                                 h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score;
   // batchability depends on the profile: a loaded queue must be reloaded (its
   // buffers stay allocated for ksim_load_pods to reuse)
   h->dp = DevPods{};
   h->batchable.clear();
+  // device copies first: if one fails the handle holds no profile at all (never
+  // a host profile the device copies and the kept graphs disagree with)
+  hipError_t e = hipMemcpyAsync(h->d_prof, p, sizeof(ksim_profile), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->d_bp, &bp, sizeof(BatchProg), hipMemcpyHostToDevice, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) {
+    drop_graphs(h);
+    h->has_profile = false;
+    return hip_fail(h, e, "profile upload");
+  }
+  h->prof = *p;
+  h->bp = bp;
+  h->has_profile = true;
+  if (keep_batch_graphs)
+    drop_cycle_graphs(h);
+  else
+    drop_graphs(h);
   return KSIM_OK;
 }
 
@@ -887,6 +914,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.fail, uint8_t*, N);
   SCR(s.ign, uint8_t*, N);
   SCR(s.win, WinState*, sizeof(WinState));
+  SCR(s.bbest, uint64_t*, 16 * ((N + 255) / 256));
   SCR(s.regbm, uint32_t*, 4 * (size_t)KSIM_MAX_USES * ((vmax + 31) / 32));
   SCR(h->ext_fail, uint8_t*, N);
   SCR(h->ext_score, int64_t*, 8 * N);
@@ -985,12 +1013,15 @@ int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
 // Re-based copy of one pod with only the expressions/terms it references.
 static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std::vector<ksim_label_expr>& ex,
                            std::vector<ksim_term>& tm, std::vector<ksim_topo_use>& us,
-                           std::vector<ksim_class_add>& ad) {
+                           std::vector<ksim_class_add>& ad, std::vector<int32_t>& nn) {
   pod = ps->pods[i];
   us.assign(ps->uses + pod.use_first, ps->uses + pod.use_first + pod.use_count);
   ad.assign(ps->adds + pod.add_first, ps->adds + pod.add_first + pod.add_count);
+  if ((pod.flags & KSIM_POD_NODE_NAMES) && pod.nn_count > 0)
+    nn.assign(ps->nn + pod.nn_first, ps->nn + pod.nn_first + pod.nn_count);
   pod.use_first = 0;
   pod.add_first = 0;
+  pod.nn_first = 0;
   int32_t sel0 = (int32_t)ex.size();
   for (int32_t k = 0; k < pod.sel_count; k++) ex.push_back(ps->exprs[pod.sel_first + k]);
   pod.sel_first = sel0;
@@ -1016,7 +1047,8 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   std::vector<ksim_term> tm;
   std::vector<ksim_topo_use> us;
   std::vector<ksim_class_add> ad;
-  single_pod_set(ps, pod_index, pod, ex, tm, us, ad);
+  std::vector<int32_t> nn;
+  single_pod_set(ps, pod_index, pod, ex, tm, us, ad, nn);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_bufs(h->pod1_bufs);
   P = DevPods{};
@@ -1028,8 +1060,9 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   P.exprs = (const ksim_label_expr*)p;
   if ((rc = upload(h, h->pod1_bufs, tm.data(), tm.size() * sizeof(ksim_term), &p))) return rc;
   P.terms = (const ksim_term*)p;
-  if ((rc = upload(h, h->pod1_bufs, nullptr, 16, &p))) return rc;
-  P.norm_const = (const int32_t*)p;
+  if ((rc = upload(h, h->pod1_bufs, nn.data(), 4 * nn.size(), &p))) return rc;
+  P.nn = (const int32_t*)p;
+  P.n_nn = (int32_t)nn.size();
   int32_t bflag[4] = {0, 0, 0, 0};
   for (const auto& u : us)
     if (use_registers_values(u)) bflag[0] |= kPodRegistersValues;
@@ -1123,15 +1156,15 @@ int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   DevState st;
   HIPCHK(h, hipMemcpy(&w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
   HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
-  const int32_t n = h->dc.n;
-  const int32_t processed = w.cut < n ? w.cut : n;
+  const int32_t ns = w.nscan;                      // nodes scanned (PreFilterResult: its node count)
+  const int32_t processed = w.cut < ns ? w.cut : ns;
   out->chosen = w.error ? KSIM_CHOSEN_ERROR : -1;
   out->status = w.error ? KSIM_STATUS_ERROR : 0;
   out->n_feasible = w.nf;
   out->n_evaluated = w.evaluated;
   out->n_processed = processed;
   out->k_to_find = w.k;
-  out->next_start = (int32_t)(((int64_t)st.next_start + processed) % n);
+  out->next_start = ns > 0 ? (int32_t)(((int64_t)st.next_start + processed) % ns) : st.next_start;
   h->ext_pending = true;
   return KSIM_OK;
 }
@@ -1187,31 +1220,42 @@ int ksim_forget(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32
 int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  if (!ps || ps->n_pods < 0 || (ps->n_pods > 0 && !ps->pods) || ps->n_exprs < 0 || ps->n_terms < 0)
+  if (!ps || ps->n_pods < 0 || (ps->n_pods > 0 && !ps->pods) || ps->n_exprs < 0 || ps->n_terms < 0 ||
+      ps->n_uses < 0 || ps->n_adds < 0 || ps->n_nn < 0)
     return set_err(h, KSIM_E_INVALID, "bad pod set");
   for (int32_t i = 0; i < ps->n_pods; i++)
     if ((rc = validate_pod(h, ps, i))) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  // The handle holds no queue until every buffer below is in place: a failure
+  // part-way leaves it empty, never with pointers to freed or half-written
+  // buffers (or graphs captured over them).
+  h->dp = DevPods{};
+  h->batchable.clear();
   // A queue with the same array sizes as the loaded one (a policy sweep
   // reloading its pods under each profile) is copied into the same buffers:
-  // the device pointers, and so every captured graph, stay valid.
+  // the device pointers, and so every captured graph, stay valid.  Every count
+  // a graph captures by value (n_pods, n_exprs, n_terms, n_uses, n_adds,
+  // n_nn) is a byte size over a fixed element size, so equal sizes mean equal
+  // captured values.
   const size_t np1 = (size_t)std::max(ps->n_pods, 1);
   const std::vector<size_t> bytes = {sizeof(ksim_pod) * (size_t)ps->n_pods,
                                      sizeof(ksim_label_expr) * (size_t)ps->n_exprs,
                                      sizeof(ksim_term) * (size_t)ps->n_terms,
+                                     4 * (size_t)ps->n_nn,
                                      4 * np1,
-                                     4 * np1,
-                                     sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0),
-                                     sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0)};
-  const bool reuse = h->d_chosen && h->pod_bufs.size() == bytes.size() && h->pod_buf_bytes == bytes;
-  if (!reuse) {
+                                     sizeof(ksim_topo_use) * (size_t)ps->n_uses,
+                                     sizeof(ksim_class_add) * (size_t)ps->n_adds};
+  const bool reuse = h->d_chosen && h->pod_buf_bytes == bytes;
+  auto drop_queue = [&](int code) {
     drop_graphs(h);
     free_bufs(h->pod_bufs);
     h->pod_buf_bytes.clear();
     if (h->d_chosen) (void)hipFree(h->d_chosen);
     h->d_chosen = nullptr;
-  }
+    return code;
+  };
+  if (!reuse) drop_queue(KSIM_OK);
   size_t next_buf = 0;
   auto put = [&](const void* src, size_t nbytes, void** out) -> int {
     if (!reuse) return upload(h, h->pod_bufs, src, nbytes, out);
@@ -1222,9 +1266,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     *out = b.p;
     return KSIM_OK;
   };
-  std::vector<int32_t> nc((size_t)std::max(ps->n_pods, 1), 0);
-  std::vector<int32_t> bf((size_t)std::max(ps->n_pods, 1), 0);
-  h->batchable.assign((size_t)ps->n_pods, 0);
+  std::vector<int32_t> bf(np1, 0);
+  std::vector<uint8_t> batchable((size_t)ps->n_pods, 0);
   h->topo.assign((size_t)ps->n_pods, 0);
   h->xdom_len.assign((size_t)ps->n_pods, 0);
   h->trivial.assign((size_t)ps->n_pods, 0);
@@ -1232,7 +1275,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->soft_le1.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
-    h->batchable[i] = pod_batchable(h, ps->pods[i], nc[i]) ? 1 : 0;
+    batchable[i] = pod_batchable(h, ps->pods[i]) ? 1 : 0;
     h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
     // sharded-cycle exchange sizes, laid out as k_dom_pack / k_window_sh do
     bool soft = false;
@@ -1256,31 +1299,39 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   }
   DevPods P{};
   void* p = nullptr;
-  if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return rc;
+  if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return drop_queue(rc);
   P.pods = (const ksim_pod*)p;
-  if ((rc = put(ps->exprs, sizeof(ksim_label_expr) * ps->n_exprs, &p))) return rc;
+  if ((rc = put(ps->exprs, sizeof(ksim_label_expr) * ps->n_exprs, &p))) return drop_queue(rc);
   P.exprs = (const ksim_label_expr*)p;
-  if ((rc = put(ps->terms, sizeof(ksim_term) * ps->n_terms, &p))) return rc;
+  if ((rc = put(ps->terms, sizeof(ksim_term) * ps->n_terms, &p))) return drop_queue(rc);
   P.terms = (const ksim_term*)p;
-  if ((rc = put(nc.data(), 4 * nc.size(), &p))) return rc;
-  P.norm_const = (const int32_t*)p;
-  if ((rc = put(bf.data(), 4 * bf.size(), &p))) return rc;
+  if ((rc = put(ps->nn, 4 * (size_t)ps->n_nn, &p))) return drop_queue(rc);
+  P.nn = (const int32_t*)p;
+  if ((rc = put(bf.data(), 4 * bf.size(), &p))) return drop_queue(rc);
   P.bflags = (const int32_t*)p;
-  if ((rc = put(ps->uses, sizeof(ksim_topo_use) * (size_t)std::max(ps->n_uses, 0), &p))) return rc;
+  if ((rc = put(ps->uses, sizeof(ksim_topo_use) * (size_t)ps->n_uses, &p))) return drop_queue(rc);
   P.uses = (const ksim_topo_use*)p;
-  if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)std::max(ps->n_adds, 0), &p))) return rc;
+  if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)ps->n_adds, &p))) return drop_queue(rc);
   P.adds = (const ksim_class_add*)p;
   P.n_uses = ps->n_uses;
   P.n_adds = ps->n_adds;
+  P.n_nn = ps->n_nn;
   P.n_pods = ps->n_pods;
   P.n_exprs = ps->n_exprs;
   P.n_terms = ps->n_terms;
+  hipError_t e = hipSuccess;
   if (!reuse) {
-    HIPCHK(h, hipMalloc(&h->d_chosen, 4 * np1));
+    e = hipMalloc(&h->d_chosen, 4 * np1);
+    if (e != hipSuccess) {
+      h->d_chosen = nullptr;
+      return drop_queue(hip_fail(h, e, "hipMalloc"));
+    }
     h->pod_buf_bytes = bytes;
   }
-  HIPCHK(h, hipMemsetAsync(h->d_chosen, 0xff, 4 * np1, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if ((e = hipMemsetAsync(h->d_chosen, 0xff, 4 * np1, h->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(h->stream)) != hipSuccess)
+    return drop_queue(hip_fail(h, e, "pod queue setup"));
+  h->batchable = std::move(batchable);
   h->dp = P;
   return KSIM_OK;
 }
@@ -1548,9 +1599,10 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  int64_t v[3 + 16] = {st.batches, st.truncations, st.cuts};
+  int64_t v[3 + 16 + 1] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hipMemcpy(v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
-  const int32_t m = n < 19 ? n : 19;
+  v[19] = h->graph_captures;
+  const int32_t m = n < 20 ? n : 20;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }
@@ -1630,6 +1682,8 @@ extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_
     return set_err(h, KSIM_E_UNSUPPORTED, "preemption dry runs re-run Fit only, not NetworkBandwidth");
   if (ps->pods[pod_index].use_count > 0)
     return set_err(h, KSIM_E_UNSUPPORTED, "preemption for pods with topology / port / image uses");
+  if (ps->pods[pod_index].flags & KSIM_POD_NODE_NAMES)
+    return set_err(h, KSIM_E_UNSUPPORTED, "preemption for pods a PreFilterResult restricts");
   if ((rc = validate_pod(h, ps, pod_index))) return rc;
   int32_t fit = -1;
   for (int f = 0; f < h->prof.n_filter; f++)

@@ -98,14 +98,14 @@ void launch_group_max(const GroupPtrs& g, hipStream_t stream);
 //   launch_pshard_filter   [topo min] + filter + counts (all-gather s.xsend[2] -> s.xrecv[world][2])
 //   launch_pshard_window   cut / kept / registrations (all-reduce sum s.xreg; pods with soft spread)
 //   launch_pshard_extrema  weights + extrema            (all-reduce max win->ext[kExtWords])
-//   launch_pshard_select   totals + TB key              (all-reduce max win->best)
-//   launch_pshard_bind
+//   launch_pshard_select   totals + TB pair, shard best  (all-gather s.xsend[2] -> s.xrecv[world][2])
+//   launch_pshard_bind     selectHost over the shards, owner binds
 void launch_pshard_topo(const LaunchArgs& a, hipStream_t stream);
 void launch_pshard_filter(const LaunchArgs& a, bool topo, hipStream_t stream);
 void launch_pshard_window(const LaunchArgs& a, int32_t rank, int32_t world, hipStream_t stream);
 void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream);
 void launch_pshard_select(const LaunchArgs& a, hipStream_t stream);
-void launch_pshard_bind(const LaunchArgs& a, hipStream_t stream);
+void launch_pshard_bind(const LaunchArgs& a, int32_t world, hipStream_t stream);
 void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStream_t stream);
 void launch_group_gather(const GroupPtrs& src, const GroupPtrs& dst, int32_t words, hipStream_t stream);
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream);

@@ -359,10 +359,23 @@ __global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_
 
 // Order-preserving u64 images of an int64 so extrema are atomicMax on u64:
 // max image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both.
-__device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
+// (max_image / from_max_image: ksim_device.h)
 __device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
-__device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
 __device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
+
+// Wave max of (img, lo) pairs in lexicographic order (selectHost over full
+// int64 totals): the max image first, then the max lo among the lanes holding it.
+__device__ __forceinline__ void wave_best2(uint64_t& img, uint64_t& lo) {
+  const uint64_t m = wave_max_u64_dpp(img);
+  lo = wave_max_u64_dpp(img == m ? lo : 0ull);
+  img = m;
+}
+__device__ __forceinline__ void best2_merge(uint64_t& img, uint64_t& lo, uint64_t img2, uint64_t lo2) {
+  if (img2 > img || (img2 == img && lo2 > lo)) {
+    img = img2;
+    lo = lo2;
+  }
+}
 
 // Per-slot extrema images of this block's values -> one atomicMax per slot.
 __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState* win, const uint64_t (&ix)[KSIM_MAX_SCORE],
@@ -442,7 +455,13 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     s.min_match = s_min;                          // pts_filter reads the block's copy
   }
   bool feasible = false, ign = false;
-  if (node < c.n) {
+  bool scanned = true;
+  if (p.flags & KSIM_POD_NODE_NAMES)              // block-uniform: NodeAffinity's PreFilterResult
+    scanned = node < c.n && scan_pos(scan_set(c, P, p, st->next_start), c.base + node) >= 0;
+  if (node < c.n && !scanned) {                   // never handed to Filter
+    s.fail[node] = KSIM_NOT_EVALUATED;
+    if (COMPAT) s.detail[node] = 0;
+  } else if (node < c.n) {
     const uint32_t tf = p.use_count ? st->topo_flags : 0u;
     const NodeRow r = load_row(c, node);
     uint32_t det;
@@ -543,12 +562,14 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const int tid = threadIdx.x;
-  const int32_t N = c.n;
-  const int32_t K = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, N);
-  const int32_t start = st->next_start;
-  const int32_t chunk = (N + kFinalThreads - 1) / kFinalThreads;
-  const int32_t lo = min(N, tid * chunk), hi = min(N, lo + chunk);
   const ksim_pod& p = P.pods[pi];
+  // the scan (unsharded: global positions are local): every node, or the
+  // PreFilterResult's nodes (KSIM_POD_NODE_NAMES)
+  const ScanSet ss = scan_set(c, P, p, st->next_start);
+  const int32_t NS = ss.n;
+  const int32_t K = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, NS);
+  const int32_t chunk = (NS + kFinalThreads - 1) / kFinalThreads;
+  const int32_t lo = min(NS, tid * chunk), hi = min(NS, lo + chunk);
   WinState* win = s.win;
 
   // Extender pass (s.ext_fail set, ksim_eval_pod_finish): the window of the
@@ -561,11 +582,10 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   if (ext) {
     cut = win->cut;
     error = win->error;                            // the filter pass already failed
-    const int32_t kend0 = cut < N ? cut : N;
+    const int32_t kend0 = cut < NS ? cut : NS;
     int32_t kept = 0;
     for (int32_t r = tid; r < kend0; r += kFinalThreads) {   // the stride the loops below use
-      int32_t node = start + r;
-      if (node >= N) node -= N;
+      const int32_t node = scan_node(ss, r);
       if (s.fail[node] != KSIM_PASSED) continue;
       if (s.ext_fail[node]) {
         s.fail[node] = KSIM_FAIL_EXTENDER;
@@ -576,23 +596,17 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     }
     nf = block_sum_i32_nw<kFinalWaves>(kept, sh32);
   } else {
-    // feasible count per rotated chunk, block scan, locate the (K+1)-th
+    // feasible count per scan chunk, block scan, locate the (K+1)-th
     int32_t cnt = 0;
-    for (int32_t r = lo; r < hi; r++) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
-      cnt += s.fail[node] == KSIM_PASSED;
-    }
+    for (int32_t r = lo; r < hi; r++) cnt += s.fail[scan_node(ss, r)] == KSIM_PASSED;
     int32_t excl, total;
     block_scan_i32(cnt, excl, total, sh32);
-    if (tid == 0) s_cut = N;
+    if (tid == 0) s_cut = NS;
     __syncthreads();
     if (total > K && excl <= K && K < excl + cnt) {
       int32_t run = excl;
       for (int32_t r = lo; r < hi; r++) {
-        int32_t node = start + r;
-        if (node >= N) node -= N;
-        if (s.fail[node] == KSIM_PASSED) {
+        if (s.fail[scan_node(ss, r)] == KSIM_PASSED) {
           if (run == K) { s_cut = r; break; }
           run++;
         }
@@ -604,33 +618,28 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     if (nb_filter_on) {
       // the first node in scan order whose Filter status was an error; the
       // scan fails there if it comes before the (K+1)-th feasible node
-      int64_t first = N;
+      int64_t first = NS;
       for (int32_t r = lo; r < hi; r++) {
-        int32_t node = start + r;
-        if (node >= N) node -= N;
-        if (fail_is_error(s.fail[node])) { first = r; break; }
+        if (fail_is_error(s.fail[scan_node(ss, r)])) { first = r; break; }
       }
       __shared__ int64_t sh64[kFinalWaves];
       const int32_t err = (int32_t)block_min_i64(first, sh64);
-      if (err < (cut < N ? cut + 1 : N)) {
+      if (err < (cut < NS ? cut + 1 : NS)) {
         error = kCycleErrorFilter;
         int32_t before = 0;                        // feasible nodes found before it
-        for (int32_t r = lo; r < hi && r < err; r++) {
-          int32_t node = start + r;
-          if (node >= N) node -= N;
-          before += s.fail[node] == KSIM_PASSED;
-        }
+        for (int32_t r = lo; r < hi && r < err; r++) before += s.fail[scan_node(ss, r)] == KSIM_PASSED;
         nf = block_sum_i32_nw<kFinalWaves>(before, sh32);
         cut = err;                                 // processed = the nodes before it
       }
     }
+    // NodeInfos().Get of a PreFilterResult name fails: framework.Error, nothing scanned
+    if (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) error = kCycleErrorPrefilter;
   }
-  const int32_t kend = cut < N ? cut : N;
-  const int32_t evaluated = cut < N ? cut + 1 : N;
+  const int32_t kend = cut < NS ? cut : NS;
+  const int32_t evaluated = cut < NS ? cut + 1 : NS;
   if (COMPAT && !ext) {
-    for (int32_t r = evaluated + tid; r < N; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
+    for (int32_t r = evaluated + tid; r < NS; r += kFinalThreads) {
+      const int32_t node = scan_node(ss, r);
       s.fail[node] = KSIM_NOT_EVALUATED;
       s.detail[node] = 0;
     }
@@ -638,8 +647,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   if (!error && nb_score_on && nf > 1) {
     int32_t bad = 0;                               // kept nodes whose Score returns Skip / Error
     for (int32_t r = tid; r < kend; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
+      const int32_t node = scan_node(ss, r);
       bad += s.fail[node] == KSIM_PASSED && nb_score_error(c.flags[node]);
     }
     if (block_sum_i32_nw<kFinalWaves>(bad, sh32) > 0) error = kCycleErrorScore;
@@ -650,8 +658,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
   if (has_soft) {
     int32_t nign = 0;
     for (int32_t r = tid; r < kend; r += kFinalThreads) {
-      int32_t node = start + r;
-      if (node >= N) node -= N;
+      const int32_t node = scan_node(ss, r);
       nign += s.fail[node] == KSIM_PASSED && s.ign[node];
     }
     nign = block_sum_i32_nw<kFinalWaves>(nign, sh32);
@@ -666,8 +673,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
         for (int x = tid; x < words; x += kFinalThreads) s_bm[x] = 0;
         __syncthreads();
         for (int32_t r = tid; r < kend; r += kFinalThreads) {
-          int32_t node = start + r;
-          if (node >= N) node -= N;
+          const int32_t node = scan_node(ss, r);
           if (s.fail[node] != KSIM_PASSED || s.ign[node]) continue;
           const uint32_t v = use_value(c, u, node);
           atomicOr(&s_bm[v >> 5], 1u << (v & 31));
@@ -688,20 +694,17 @@ __global__ __launch_bounds__(kFinalThreads) void k_window(DevCluster c, DevPods 
     win->evaluated = evaluated;
     win->has_soft = has_soft;
     win->k = K;
-    win->best = 0;
     win->error = error;
+    win->nscan = NS;
   }
 }
 
-// Position of global node g in the scan from nextStartNodeIndex, and whether a
-// (local) node is in the kept list (feasible and scanned before the cut).
-__device__ __forceinline__ int32_t rot_pos(int32_t g, int32_t start, int32_t n_total) {
-  const int32_t r = g - start;
-  return r < 0 ? r + n_total : r;
-}
-__device__ __forceinline__ bool kept_node(const DevCluster& c, const DevScratch& s, int32_t node, int32_t start,
+// Whether a (local) node is in the kept list: feasible and scanned before the cut.
+__device__ __forceinline__ bool kept_node(const DevCluster& c, const DevScratch& s, const ScanSet& ss, int32_t node,
                                           int32_t kend) {
-  return rot_pos(c.base + node, start, c.n_total) < kend && s.fail[node] == KSIM_PASSED;
+  if (s.fail[node] != KSIM_PASSED) return false;
+  const int32_t r = scan_pos(ss, c.base + node);
+  return r >= 0 && r < kend;
 }
 
 // NOWIN: the window state is derived here from k_filter_score's counters and
@@ -720,6 +723,7 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
   const ksim_pod& p = P.pods[pi];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nu = p.use_count;
+  const ScanSet ss = scan_set(c, P, p, st->next_start);
   bool has_soft;
   if (NOWIN) {
     const int32_t nf = win->nfeas;
@@ -745,12 +749,14 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
         if (tid == 0) s_w[i] = c.topo_log[size];
       }
     }
-    if (blockIdx.x == 0 && tid == 0) {
+    if (blockIdx.x == 0 && tid == 0) {            // K = N: every scanned node is kept
       win->nf = nf;
-      win->kend = c.n;
-      win->cut = c.n;
-      win->evaluated = c.n;
-      win->k = c.n;
+      win->kend = ss.n;
+      win->cut = ss.n;
+      win->evaluated = ss.n;
+      win->k = ss.n;
+      win->nscan = ss.n;
+      win->error = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? kCycleErrorPrefilter : 0;
       win->has_soft = has_soft;
       for (int i = 0; i < nu; i++) win->w[i] = s_w[i];
     }
@@ -767,7 +773,7 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
   }
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
-  const bool kept = node < N && kept_node(c, s, node, st->next_start, NOWIN ? N : win->kend);
+  const bool kept = node < N && kept_node(c, s, ss, node, NOWIN ? ss.n : win->kend);
   const int S = prof.n_score;
 #pragma unroll
   for (int k = 0; k < KSIM_MAX_SCORE; k++) {
@@ -828,7 +834,7 @@ template <bool COMPAT>
 __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_profile prof,
                                                 const DevState* __restrict__ st, DevScratch s, DevEvalOut o,
                                                 int32_t fuse_ext) {
-  __shared__ uint64_t s_best[4];
+  __shared__ uint64_t s_best[8];
   __shared__ int32_t sh32[4];
   __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
@@ -844,9 +850,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   bool has_soft;
   int soft = -1;
   double w_soft = 0;
+  const ScanSet ss = scan_set(c, P, p, st->next_start);
   if (fuse_ext) {                                  // block-uniform
     nf = win->nfeas;
-    kend = N;
+    kend = ss.n;
     soft = soft_use(P.uses, p.use_count);
     has_soft = nf > 1 && soft >= 0;
     if (has_soft) {                                // topologyNormalizingWeight of the one soft use
@@ -863,12 +870,14 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       }
       w_soft = c.topo_log[size];
     }
-    if (blockIdx.x == 0 && tid == 0) {
+    if (blockIdx.x == 0 && tid == 0) {            // K = N: every scanned node is kept
       win->nf = nf;
-      win->kend = N;
-      win->cut = N;
-      win->evaluated = N;
-      win->k = N;
+      win->kend = ss.n;
+      win->cut = ss.n;
+      win->evaluated = ss.n;
+      win->k = ss.n;
+      win->nscan = ss.n;
+      win->error = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? kCycleErrorPrefilter : 0;
       win->has_soft = has_soft;
       if (soft >= 0) win->w[soft] = w_soft;
     }
@@ -877,9 +886,9 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     kend = win->kend;
     has_soft = win->has_soft != 0;
   }
-  uint64_t key = 0;
+  uint64_t img = 0, tlo = 0;                       // this node's (total image, TB lo); tlo == 0: no key
   if (node < N) {
-    const bool kept = nf >= 1 && !win->error && kept_node(c, s, node, st->next_start, kend);
+    const bool kept = nf >= 1 && !win->error && kept_node(c, s, ss, node, kend);
     if (kept && nf > 1) {
       const bool ign = has_soft && s.ign[node];
       const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
@@ -923,10 +932,14 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
         o.total[node] = tot;
         o.scored[node] = 1;
       }
-      key = tb_key(tot, prof.tiebreak_seed, st->pod_seq, c.base + node);
+      img = max_image(tot);
+      tlo = tb_lo(prof.tiebreak_seed, st->pod_seq, c.base + node);
     } else {
       // one feasible node: schedulePod returns it without scoring
-      if (kept) key = tb_key(0, prof.tiebreak_seed, st->pod_seq, c.base + node);
+      if (kept) {
+        img = max_image(0);
+        tlo = tb_lo(prof.tiebreak_seed, st->pod_seq, c.base + node);
+      }
       if (COMPAT) {
       o.total[node] = 0;
       o.scored[node] = 0;
@@ -944,13 +957,30 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
     }
   }
-  key = wave_max_u64_dpp(key);
-  if (lane == 0) s_best[wv] = key;
+  // selectHost: the block's best (total, TB) pair -> its record (k_bind reduces the records)
+  wave_best2(img, tlo);
+  if (lane == 0) {
+    s_best[2 * wv] = img;
+    s_best[2 * wv + 1] = tlo;
+  }
   __syncthreads();
   if (tid == 0) {
-    const uint64_t m = umax64(umax64(s_best[0], s_best[1]), umax64(s_best[2], s_best[3]));
-    if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->best), (unsigned long long)m);
+    uint64_t bi = s_best[0], bl = s_best[1];
+#pragma unroll
+    for (int w = 1; w < 4; w++) best2_merge(bi, bl, s_best[2 * w], s_best[2 * w + 1]);
+    s.bbest[2 * blockIdx.x] = bi;
+    s.bbest[2 * blockIdx.x + 1] = bl;
   }
+}
+
+// selectHost over k_select's per-block records (one wave): the winning TB lo
+// word (0: no kept node).
+__device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32_t n_blocks) {
+  const int lane = threadIdx.x & 63;
+  uint64_t img = 0, lo = 0;
+  for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
+  wave_best2(img, lo);
+  return lo;
 }
 
 // NOWIN also returns the counters and extrema slots to zero for the next
@@ -962,12 +992,14 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
+  const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);
   if (threadIdx.x != 0) return;
-  const int32_t N = c.n, nf = win->nf, cut = win->cut, error = win->error;
-  const int32_t chosen = win->best && !error ? key_node(win->best) : -1;   // unsharded: base == 0
+  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, error = win->error;
+  const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
   const ksim_pod& p = P.pods[pi];
-  int32_t ns = st->next_start + (cut < N ? cut : N);
-  ns %= N;
+  // nextStartNodeIndex = (nextStartNodeIndex + processed) % len(scanned nodes);
+  // a pod PreFilter rejected scans nothing and leaves it
+  const int32_t ns = NS > 0 ? (int32_t)(((int64_t)st->next_start + (cut < NS ? cut : NS)) % NS) : st->next_start;
   st->next_start = ns;
   st->evals += win->evaluated;
   if (chosen >= 0) {
@@ -982,7 +1014,7 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
   win->error = 0;
   st->n_feasible = nf;
   st->n_evaluated = win->evaluated;
-  st->n_processed = cut < N ? cut : N;
+  st->n_processed = cut < NS ? cut : NS;
   st->k_to_find = win->k;
   st->next_start_after = ns;
   st->pod_seq += 1;
@@ -991,7 +1023,6 @@ __global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* 
     win->nfeas = 0;
     win->nign = 0;
     for (int t = 0; t < kExtWords; t++) win->ext[t] = 0;
-    win->best = 0;
   }
   st->cursor = pi + 1;
 }
@@ -1126,6 +1157,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window_sh(DevCluster c, DevPo
   }
   blo += all_hi;
   const int32_t split = min(n, max(0, start - base));
+  const ScanSet ss{nullptr, N, start};             // sharded cycles scan every node
   int32_t kend, cutslot = 0;
   if (T <= K) {
     kend = N;
@@ -1150,7 +1182,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window_sh(DevCluster c, DevPo
   if (any_soft) {
     int32_t nign = 0;
     for (int32_t x = tid; x < n; x += kFinalThreads) {
-      if (!kept_node(c, s, x, start, kend)) continue;
+      if (!kept_node(c, s, ss, x, kend)) continue;
       if (s.ign[x]) {
         nign++;
         continue;
@@ -1172,7 +1204,7 @@ __global__ __launch_bounds__(kFinalThreads) void k_window_sh(DevCluster c, DevPo
     win->nf = nf;
     win->k = K;
     win->has_soft = nf > 1 && any_soft;
-    win->best = 0;
+    win->nscan = N;
   }
 }
 
@@ -1205,8 +1237,23 @@ __global__ __launch_bounds__(256) void k_wfinal_sh(DevCluster c, DevPods P, cons
 }
 
 // selectHost result (global), the owner shard's bind, scheduler state on every shard.
+// This shard's best (total image, TB lo) over k_select's block records ->
+// s.xsend[0..1], all-gathered (s.xrecv[world][2]) before k_bind_sh.
+__global__ __launch_bounds__(64) void k_best_pack(DevCluster c, const DevState* __restrict__ st, DevScratch s) {
+  if (st->cursor >= st->end) return;
+  const int32_t n_blocks = (c.n + 255) / 256;
+  const int lane = threadIdx.x;
+  uint64_t img = 0, lo = 0;
+  for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
+  wave_best2(img, lo);
+  if (lane == 0) {
+    s.xsend[0] = img;
+    s.xsend[1] = lo;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_bind_sh(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
-                                                 int32_t* __restrict__ chosen_out) {
+                                                 int32_t world, int32_t* __restrict__ chosen_out) {
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const ksim_pod& p = P.pods[pi];
@@ -1221,7 +1268,9 @@ __global__ __launch_bounds__(256) void k_bind_sh(DevCluster c, DevPods P, DevSta
   if (threadIdx.x != 0) return;
   const WinState* win = s.win;
   const int32_t N = c.n_total, n = c.n, base = c.base, start = st->next_start;
-  const int32_t chosen = win->best ? key_node(win->best) : -1;
+  uint64_t bi = 0, bl = 0;                         // selectHost over the shards' records
+  for (int32_t r = 0; r < world; r++) best2_merge(bi, bl, s.xrecv[2 * r], s.xrecv[2 * r + 1]);
+  const int32_t chosen = bl ? key_node(bl) : -1;
   const int32_t local = chosen - base;
   const int64_t cs = (int64_t)win->ext[kExtCut];
   const int32_t processed = cs ? (int32_t)(cs - 1) : N;
@@ -1362,10 +1411,11 @@ void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream) {
 void launch_pshard_select(const LaunchArgs& a, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0);
+  k_best_pack<<<1, 64, 0, stream>>>(a.c, a.st, a.s);
 }
 
-void launch_pshard_bind(const LaunchArgs& a, hipStream_t stream) {
-  k_bind_sh<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+void launch_pshard_bind(const LaunchArgs& a, int32_t world, hipStream_t stream) {
+  k_bind_sh<<<1, 256, 0, stream>>>(a.c, a.P, a.st, a.s, world, a.chosen);
 }
 
 void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStream_t stream) {

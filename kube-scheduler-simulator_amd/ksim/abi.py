@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -87,6 +87,8 @@ POD_HAS_REQUIRED_AFFINITY = 2
 POD_HAS_SCALAR = 4
 POD_HAS_HOST_PORTS = 8
 POD_HAS_VOLUMES = 16
+POD_NODE_NAMES = 32            # NodeAffinity PreFilterResult restricts the scan (nn_first, nn_count)
+POD_NODE_NAMES_UNKNOWN = 64    # ... and names a node the snapshot lacks: the cycle errors
 
 # pod nb_flags
 POD_NB_INGRESS_BAD = 1
@@ -167,7 +169,7 @@ POD_DTYPE = np.dtype(
      ("req_term_first", "<i4"), ("req_term_count", "<i4"),
      ("pref_term_first", "<i4"), ("pref_term_count", "<i4"),
      ("use_first", "<i4"), ("use_count", "<i4"), ("add_first", "<i4"), ("add_count", "<i4"),
-     ("topo_flags", "<u4"), ("nb_flags", "<u4"), ("_reserved", "<i4"),
+     ("topo_flags", "<u4"), ("nb_flags", "<u4"), ("nn_first", "<i4"), ("nn_count", "<i4"),
      ("nb_req", "<i8"), ("nb_add", "<i8")], align=True)
 TOPO_USE_DTYPE = np.dtype(
     [("cls", "<i4"), ("arg", "<i4"), ("col", "<u2"), ("kind", "u1"), ("flags", "u1"), ("_pad", "<i4")],
@@ -217,6 +219,7 @@ class PodSet(ctypes.Structure):
         ("pods", ctypes.c_void_p), ("exprs", ctypes.c_void_p), ("terms", ctypes.c_void_p),
         ("n_uses", ctypes.c_int32), ("n_adds", ctypes.c_int32),
         ("uses", ctypes.c_void_p), ("adds", ctypes.c_void_p),
+        ("n_nn", ctypes.c_int32), ("_pad2", ctypes.c_int32), ("nn", ctypes.c_void_p),
     ]
 
 

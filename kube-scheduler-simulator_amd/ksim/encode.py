@@ -246,6 +246,10 @@ class EncodedPods:
     names: List[Tuple[str, str]] = field(default_factory=list)   # (namespace, name)
     uses: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.TOPO_USE_DTYPE))
     adds: np.ndarray = field(default_factory=lambda: np.zeros(0, abi.CLASS_ADD_DTYPE))
+    nn: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))   # PreFilterResult node positions
+    # per pod: NodeAffinity's PreFilterResult.NodeNames (sorted names, as the
+    # wrapper records them) or None (all nodes); [] = conflicting terms
+    prefilter_names: List[Optional[List[str]]] = field(default_factory=list)
 
     @property
     def n_pods(self) -> int:
@@ -263,11 +267,14 @@ class EncodedPods:
         s.n_adds = int(self.adds.size)
         s.uses = abi._p(self.uses)
         s.adds = abi._p(self.adds)
+        s.n_nn = int(self.nn.size)
+        s.nn = abi._p(self.nn)
         return s
 
     def subset(self, first: int, count: int) -> "EncodedPods":
         return EncodedPods(self.pods[first:first + count].copy(), self.exprs, self.terms,
-                           self.names[first:first + count], self.uses, self.adds)
+                           self.names[first:first + count], self.uses, self.adds, self.nn,
+                           self.prefilter_names[first:first + count])
 
 
 # ---- cluster encoder --------------------------------------------------------
@@ -485,6 +492,28 @@ class _PodBuilder:
         self.terms.append((first, len(self.exprs) - first, weight))
 
 
+def prefilter_node_names(pod: Pod) -> Optional[List[str]]:
+    """[upstream] nodeaffinity.PreFilter (v1.26) PreFilterResult.NodeNames: over
+    the required node-affinity terms, the union of each term's intersection of
+    its metadata.name In matchFields.  None: every node (no required terms, or
+    a term without such a field); [] : the terms conflict (the plugin returns
+    UnschedulableAndUnresolvable "pod affinity terms conflict").  Sorted, as
+    sets.String.List() hands them to the result store (store.go:517-530)."""
+    if not pod.required_terms:
+        return None
+    names = None
+    for t in pod.required_terms:
+        term_names = None
+        for r in t.match_fields:
+            if r.key == "metadata.name" and r.operator == "In":
+                vals = set(r.values)
+                term_names = vals if term_names is None else term_names & vals
+        if term_names is None:
+            return None
+        names = set(term_names) if names is None else names | term_names
+    return sorted(names)
+
+
 def _tol_bits(tolerations: Sequence[Toleration], vocab: Sequence[Taint]) -> np.ndarray:
     w = np.zeros(abi.TAINT_WORDS, np.uint64)
     for tid in range(1, len(vocab)):
@@ -507,6 +536,8 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         raise EncodeError(str(e)) from e
     uses: List[tuple] = []
     adds: List[Tuple[int, int]] = []
+    nn: List[int] = []
+    pf_names: List[Optional[List[str]]] = []
     for i, p in enumerate(pods):
         r = pod_requests(p)
         nz = pod_nonzero_requests(p)
@@ -557,6 +588,15 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         rec["pref_term_count"] = len(b.terms) - rec["pref_term_first"]
         if p.has_volumes:
             flags |= abi.POD_HAS_VOLUMES
+        pf = prefilter_node_names(p)
+        pf_names.append(pf)
+        if pf is not None:                    # findNodesThatFitPod scans only these nodes
+            flags |= abi.POD_NODE_NAMES
+            known = sorted(b.pos_of[n] for n in pf if n in b.pos_of)
+            if len(known) < len(pf):
+                flags |= abi.POD_NODE_NAMES_UNKNOWN
+            rec["nn_first"], rec["nn_count"] = len(nn), len(known)
+            nn.extend(known)
         rec["flags"] = flags
         try:
             u, tflags = pod_uses(topo, cluster, p)
@@ -586,4 +626,4 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         aarr["cls"] = [x[0] for x in adds]
         aarr["count"] = [x[1] for x in adds]
     cluster.refresh_classes()
-    return EncodedPods(arr, exprs, terms, names, uarr, aarr)
+    return EncodedPods(arr, exprs, terms, names, uarr, aarr, np.array(nn, np.int32), pf_names)

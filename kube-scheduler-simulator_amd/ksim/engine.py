@@ -259,11 +259,12 @@ class Engine:
 
     def diag(self) -> dict:
         """Batch-path diagnostics of the last schedule_loaded call."""
-        out = np.zeros(19, np.int64)
-        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 19)
+        out = np.zeros(20, np.int64)
+        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 20)
         if n < 0:
             self._chk(n)
-        d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2])}
+        d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2]),
+             "graph_captures": int(out[19])}
         if out[6]:
             d["chain_us"] = {"setup": out[3] / out[6] / 100.0, "rounds": out[4] / out[6] / 100.0,
                              "epilogue": out[5] / out[6] / 100.0, "rounds_per_batch": out[7] / out[6]}

@@ -305,3 +305,93 @@ def netbw_objects(n_nodes: int = 120, n_pods: int = 300, seed: int = SEEDS[1] ^ 
         elif pod_errors and r.chance(3):
             p.annotations[a.egress_request_annotation] = "fast"
     return nodes, bound, pending
+
+
+def prefilter_objects(n_nodes: int = 300, n_pods: int = 600, seed: int = SEEDS[1] ^ 0x50464E) \
+        -> Tuple[List[Node], List[Pod]]:
+    """config1-shaped nodes and pods, a third of them with required node
+    affinity on metadata.name matchFields, so NodeAffinity's PreFilterResult
+    restricts their scan: one name; two names as two
+    ORed terms; a long list of single-name terms (more than
+    numFeasibleNodesToFind's window under ADAPT); a term that also carries
+    label expressions; intersecting fields; conflicting fields (no node);
+    an unknown node name (the cycle errors); a two-value requirement (the
+    PreFilter set holds it, the Filter's field selector cannot parse it); a
+    NotIn field (no restriction)."""
+    nodes, pods = config1_objects(n_nodes, n_pods, seed)
+    r = Rng(seed ^ 0x77)
+    names = [n.name for n in nodes]
+
+    def field(op, *vals):
+        return Requirement("metadata.name", op, list(vals))
+
+    for j, p in enumerate(pods):
+        if j % 3:
+            continue
+        k = r.below(10)
+        a, b = names[r.below(n_nodes)], names[r.below(n_nodes)]
+        if k == 0:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a)])]
+        elif k == 1:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a)]),
+                                NodeSelectorTerm(match_fields=[field("In", b)])]
+        elif k == 2:
+            many = sorted({names[r.below(n_nodes)] for _ in range(min(n_nodes, 180))})
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", x)]) for x in many]
+        elif k == 3:
+            p.required_terms = [NodeSelectorTerm([Requirement("pool", "In", [POOLS[r.below(4)]])],
+                                                 [field("In", a)]),
+                                NodeSelectorTerm(match_fields=[field("In", b)])]
+        elif k == 4:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a), field("In", a)])]
+        elif k == 5:
+            c = names[(names.index(a) + 1) % n_nodes]
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a), field("In", c)])]
+        elif k == 6:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", "node-missing")]),
+                                NodeSelectorTerm(match_fields=[field("In", a)])]
+        elif k == 7:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a, b)])]
+        elif k == 8:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("NotIn", a)])]
+        else:
+            p.required_terms = [NodeSelectorTerm(match_fields=[field("In", a)]),
+                                NodeSelectorTerm([Requirement("disk", "In", ["ssd"])])]
+    return nodes, pods
+
+
+def edge_objects(n_pods: int = 160, seed: int = SEEDS[1] ^ 0xED6E) -> Tuple[List[Node], List[Pod], List[Pod]]:
+    """Resource edge cases the plugin arithmetic must get right (SURVEY
+    Appendix A): allocatable 0, requested above allocatable (bound pods
+    overcommit a node), allowed pods 0, quantities at and past 2^52 (the exact
+    division path) and past 2^56 (leastRequestedScore's int64 product wraps
+    in Go), BestEffort pods (non-zero defaults), init containers.  Returns
+    (nodes, bound pods, pending pods)."""
+    r = Rng(seed)
+
+    def node(i, cpu, mem, pods="110"):
+        return Node(f"edge-{i:02d}", {"kubernetes.io/hostname": f"edge-{i:02d}",
+                                      "topology.kubernetes.io/zone": f"z{i % 2}"},
+                    [], {"cpu": cpu, "memory": mem, "pods": pods})
+
+    nodes = [node(0, "0", "0"), node(1, "4", "8Gi"), node(2, "4", "4Pi"), node(3, "100000000000", "1Ei"),
+             node(4, "5000000000000", "3Ei"), node(5, "8", "16Gi", pods="0"), node(6, "16", "64Gi"),
+             node(7, "32", "128Gi"), node(8, "8", "32Gi"), node(9, "64", "4Pi"), node(10, "2", "1Gi"),
+             node(11, "4503599627370", "8191Pi")]
+    bound = [Pod(f"over-{k}", node_name="edge-01", containers=[Container({"cpu": "3", "memory": "6Gi"})])
+             for k in range(2)]
+    bound.append(Pod("big", node_name="edge-03", containers=[Container({"cpu": "1000", "memory": "300Pi"})]))
+    mems = ["0", "64Mi", "1Gi", "6Gi", "2Pi", "700Pi", "1Ei"]
+    cpus = ["0", "100m", "1", "3", "2000", "4000000000000"]
+    pending = []
+    for j in range(n_pods):
+        k = r.below(6)
+        if k == 0:
+            c = Container({})                                         # BestEffort: 100m / 200Mi non-zero
+        else:
+            c = Container({"cpu": cpus[r.below(len(cpus))], "memory": mems[r.below(len(mems))]})
+        p = Pod(f"edge-pod-{j:04d}", containers=[c])
+        if r.chance(15):
+            p.init_containers = [Container({"cpu": cpus[r.below(len(cpus))], "memory": mems[r.below(len(mems))]})]
+        pending.append(p)
+    return nodes, bound, pending

@@ -17,7 +17,7 @@ Keys are the ORIGINAL plugin names (wrappedplugin.go:374,406,447,479,510).
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, List, Optional
 
 from . import abi
 from .encode import EncodedCluster
@@ -34,6 +34,7 @@ ERR_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"  # nodea
 ERR_NODE_PORTS = "node(s) didn't have free ports for the requested pod ports"     # nodeports.ErrReason
 ERR_PTS = "node(s) didn't match pod topology spread constraints"        # podtopologyspread ErrReasonConstraintsNotMatch
 ERR_PTS_LABEL = ERR_PTS + " (missing required label)"                   # ErrReasonNodeLabelNotMatch
+ERR_NODE_AFFINITY_CONFLICT = "pod affinity terms conflict"              # nodeaffinity errReasonConflict (PreFilter)
 ERR_IPA = {abi.IPA_AFFINITY: "node(s) didn't match pod affinity rules",
            abi.IPA_ANTI_AFFINITY: "node(s) didn't match pod anti-affinity rules",
            abi.IPA_EXISTING_ANTI: "node(s) didn't satisfy existing pods anti-affinity rules"}
@@ -78,11 +79,27 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
 
 
 def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, ns: str, name: str,
-                 res: Dict) -> None:
-    """Feed ``store`` with one compat-mode cycle result (engine or oracle)."""
+                 res: Dict, prefilter_names: Optional[List[str]] = None) -> None:
+    """Feed ``store`` with one compat-mode cycle result (engine or oracle).
+    ``prefilter_names``: the pod's NodeAffinity PreFilterResult.NodeNames
+    (EncodedPods.prefilter_names; None = all nodes, [] = conflicting terms)."""
     names = cluster.node_names
+    conflict = prefilter_names is not None and len(prefilter_names) == 0
     for p in prof.plugins["preFilter"].enabled:
-        store.add_pre_filter_result(ns, name, original_name(p.name), SUCCESS_MESSAGE, None)
+        plugin = original_name(p.name)
+        if plugin == "NodeAffinity" and prefilter_names is not None:
+            # wrappedPlugin.PreFilter records the status and result.NodeNames.List()
+            store.add_pre_filter_result(ns, name, plugin, ERR_NODE_AFFINITY_CONFLICT if conflict else SUCCESS_MESSAGE,
+                                        None if conflict else list(prefilter_names))
+            if conflict:
+                break                          # RunPreFilterPlugins stops at a failing plugin
+        else:
+            store.add_pre_filter_result(ns, name, plugin, SUCCESS_MESSAGE, None)
+    if conflict:
+        # findNodesThatFitPod: every node gets the PreFilter status; no Filter runs
+        for p in prof.plugins["postFilter"].enabled:
+            store.add_post_filter_result(ns, name, "", original_name(p.name), list(names))
+        return
     forder = prof.filter_order()
     fp, fd = res["fail_plugin"], res["fail_detail"]
     for node in range(cluster.n_nodes):
@@ -97,9 +114,13 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
             else:
                 store.add_filter_result(ns, name, names[node], forder[f], PASSED_FILTER_MESSAGE)
     if res["status"] == abi.STATUS_ERROR:
-        # framework.Error: a Filter error ends the scan; a Score error ends the
-        # cycle after PreScore (which partial Score records survive the
-        # cancelled parallel run is not deterministic upstream: none are kept)
+        # framework.Error: a PreFilterResult node missing from the snapshot ends
+        # the cycle before any Filter; a Filter error ends the scan; a Score
+        # error ends the cycle after PreScore (which partial Score records
+        # survive the cancelled parallel run is not deterministic upstream:
+        # none are kept)
+        if prefilter_names is not None and res["n_evaluated"] == 0:
+            return
         filter_error = any(int(fp[i]) < len(forder) and forder[int(fp[i])] == "NetworkBandwidth" and
                            int(fd[i]) >= abi.NB_NO_LIMIT for i in range(cluster.n_nodes))
         if not filter_error:

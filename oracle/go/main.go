@@ -193,11 +193,12 @@ func splitmix64(x uint64) uint64 {
 	return z ^ (z >> 31)
 }
 
-// tbKey is SURVEY §8(b)'s TB(seed) selectHost key (ksim_oracle_tb_key).
-func tbKey(total int64, seed uint64, seq int64, node int) uint64 {
+// tbLo is the tie-break word of SURVEY §8(b)'s TB(seed) (ksim_oracle_tb_lo):
+// selectHost takes the max of (total, tbLo) in lexicographic order.
+func tbLo(seed uint64, seq int64, node int) uint64 {
 	const nodeMask = (1 << 18) - 1
 	h := splitmix64(seed^(uint64(seq)<<20)^uint64(node)) >> 38
-	return uint64(total)<<44 | h<<18 | uint64(nodeMask-node)
+	return h<<18 | uint64(nodeMask-node)
 }
 
 // defaultArgs: the v1beta2 defaults the simulator starts from
@@ -264,12 +265,10 @@ func run(f *fixture) ([]cycle, error) {
 	informerFactory.Start(stop)
 	informerFactory.WaitForCacheSync(stop)
 
-	N := len(snap.list)
 	index := map[string]int{}
 	for i, ni := range snap.list {
 		index[ni.Node().Name] = i
 	}
-	K := int(numFeasibleNodesToFind(f.Pct, int32(N)))
 	nextStart := 0
 	var out []cycle
 	for seq := range f.Pods {
@@ -277,18 +276,40 @@ func run(f *fixture) ([]cycle, error) {
 		c := cycle{Pod: pod.Name, Filter: map[string]interface{}{}, Score: map[string]map[string]int64{},
 			Normalized: map[string]map[string]int64{}, Total: map[string]int64{}}
 		state := framework.NewCycleState()
+		var preRes *framework.PreFilterResult
 		for _, name := range preFilterOrder {
 			if p, ok := pl[name].(framework.PreFilterPlugin); ok {
-				if _, st := p.PreFilter(ctx, state, pod); !st.IsSuccess() {
+				r, st := p.PreFilter(ctx, state, pod)
+				if !st.IsSuccess() {
 					return nil, fmt.Errorf("pod %s: PreFilter %s: %s (not modelled)", pod.Name, name, st.Message())
 				}
+				preRes = preRes.Merge(r)
 			}
 		}
+		// findNodesThatFitPod: a PreFilterResult restricts the scan to its nodes,
+		// taken in nodeTree order (upstream ranges over the set in Go map order)
+		scan := snap.list
+		if !preRes.AllNodes() {
+			scan = nil
+			for _, ni := range snap.list {
+				if preRes.NodeNames.Has(ni.Node().Name) {
+					scan = append(scan, ni)
+				}
+			}
+			if len(scan) != len(preRes.NodeNames) {
+				return nil, fmt.Errorf("pod %s: PreFilterResult names a node outside the snapshot (not modelled)", pod.Name)
+			}
+		}
+		N := len(scan)
+		if N == 0 {
+			return nil, fmt.Errorf("pod %s: empty PreFilterResult (not modelled)", pod.Name)
+		}
+		K := int(numFeasibleNodesToFind(f.Pct, int32(N)))
 		// findNodesThatPassFilters, parallelism 1
 		var feasible []*framework.NodeInfo
 		failed := 0
 		for i := 0; i < N; i++ {
-			ni := snap.list[(nextStart+i)%N]
+			ni := scan[(nextStart+i)%N]
 			var rec interface{} = "passed"
 			for _, name := range filterOrder {
 				st := pl[name].(framework.FilterPlugin).Filter(ctx, state, pod, ni)
@@ -361,11 +382,13 @@ func run(f *fixture) ([]cycle, error) {
 				c.Normalized[name] = norm
 			}
 			best := -1
-			var bestKey uint64
+			var bestTotal int64
+			var bestLo uint64
 			for j, n := range nodes {
 				c.Total[n.Name] = totals[j]
-				if k := tbKey(totals[j], f.Seed, int64(seq), index[n.Name]); best < 0 || k > bestKey {
-					best, bestKey = j, k
+				lo := tbLo(f.Seed, int64(seq), index[n.Name])
+				if best < 0 || totals[j] > bestTotal || (totals[j] == bestTotal && lo > bestLo) {
+					best, bestTotal, bestLo = j, totals[j], lo
 				}
 			}
 			chosen = feasible[best]

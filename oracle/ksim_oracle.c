@@ -148,11 +148,47 @@ static uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-/* key = total<<44 | hash26<<18 | (2^18-1-node): one u64 max replaces the
- * reservoir sampling of [upstream] schedule_one.go selectHost (global math/rand). */
-uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node) {
+/* selectHost picks the max of (total, lo) in lexicographic order, total the
+ * full int64; lo = hash26<<18 | (2^18-1-node).  This replaces the reservoir
+ * sampling of [upstream] schedule_one.go selectHost (global math/rand). */
+uint64_t ksim_oracle_tb_lo(uint64_t seed, int64_t pod_seq, int32_t node) {
   uint64_t h = splitmix64(seed ^ ((uint64_t)pod_seq << 20) ^ (uint64_t)(uint32_t)node) >> 38;
-  return ((uint64_t)total << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
+  return (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - node);
+}
+
+/* The same order packed into one u64 for a total in [0, 2^20): total<<44 | lo. */
+uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node) {
+  return ((uint64_t)total << 44) | ksim_oracle_tb_lo(seed, pod_seq, node);
+}
+
+/* (total, lo) > (best_total, best_lo) */
+static int tb_better(int64_t total, uint64_t lo, int64_t best_total, uint64_t best_lo) {
+  return total > best_total || (total == best_total && lo > best_lo);
+}
+
+/* The nodes findNodesThatFitPod scans (a16): every node, or NodeAffinity's
+ * PreFilterResult.NodeNames (a5: ksim_engine.h KSIM_POD_NODE_NAMES), in
+ * increasing position from nextStartNodeIndex mod their count. */
+typedef struct scan_set {
+  const int32_t* list;   /* NULL: every node */
+  int32_t n, start;
+} scan_set;
+
+static scan_set pod_scan_set(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p) {
+  scan_set s;
+  s.list = NULL;
+  s.n = o->n;
+  if (p->flags & KSIM_POD_NODE_NAMES) {
+    s.list = ps->nn + p->nn_first;
+    s.n = (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 0 : p->nn_count;
+  }
+  s.start = s.n > 0 ? o->next_start % s.n : 0;
+  return s;
+}
+
+static int32_t scan_node_at(const scan_set* s, int32_t i) {
+  const int32_t x = (s->start + i) % s->n;
+  return s->list ? s->list[x] : x;
 }
 
 /* [upstream] schedule_one.go (*Scheduler).numFeasibleNodesToFind — §8(a) a16 */
@@ -332,7 +368,9 @@ static void calc_alloc_req(const ksim_oracle* o, const ksim_pod* p, int32_t node
 int64_t ksim_oracle_least_requested_score(int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (requested > capacity) return 0;
-  return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
+  /* Go's int64 product wraps (capacities past 2^56); C's signed one must not overflow */
+  const int64_t prod = (int64_t)((uint64_t)(capacity - requested) * (uint64_t)MAX_NODE_SCORE);
+  return prod / capacity;
 }
 
 /* leastResourceScorer over resourceAllocationScorer.score — a23 */
@@ -837,8 +875,9 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
   const int32_t N = o->n;
   if (N == 0) return KSIM_E_INVALID;                      /* ErrNoNodesAvailable */
   const int64_t seq = o->pod_seq++;
-  const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, N);
-  const int32_t start = o->next_start;
+  const scan_set ss = pod_scan_set(o, ps, p);
+  const int32_t NS = ss.n;
+  const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, NS);
   const int S = o->prof.n_score;
 
   if (out->fail_plugin) memset(out->fail_plugin, KSIM_NOT_EVALUATED, (size_t)N);
@@ -852,8 +891,11 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
   topo_ctx tc;
   topo_prefilter(o, ps, p, &tc);
   int32_t nf = 0, nfailed = 0, evaluated = 0, error = 0;
-  for (int32_t i = 0; i < N; i++) {
-    int32_t node = (start + i) % N;
+  /* NodeInfos().Get of a PreFilterResult name the snapshot lacks: the cycle
+   * fails with an error before any Filter call */
+  if (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) error = 1;
+  for (int32_t i = 0; i < NS; i++) {
+    int32_t node = scan_node_at(&ss, i);
     uint32_t det;
     uint8_t r = run_filter_plugins(o, ps, p, &tc, node, &det);
     evaluated++;
@@ -871,7 +913,7 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
     }
   }
   int32_t processed = nf + nfailed;
-  o->next_start = (start + processed) % N;
+  if (NS > 0) o->next_start = (int32_t)(((int64_t)o->next_start + processed) % NS);
   if (ext_fail) {                  /* findNodesThatPassExtenders over the kept list */
     int32_t m = 0;
     for (int32_t j = 0; j < nf; j++) {
@@ -925,14 +967,19 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
     /* prioritizeNodes: no score plugins and no extenders -> every node scores 1 */
     if (S == 0 && !ext_score) for (int32_t j = 0; j < nf; j++) totals[j] = 1;
     if (ext_score) for (int32_t j = 0; j < nf; j++) totals[j] += ext_score[o->flist[j]];
-    uint64_t best = 0;
+    int64_t best_total = 0;
+    uint64_t best_lo = 0;
     chosen = -1;
     for (int32_t j = 0; j < nf; j++) {
       int32_t node = o->flist[j];
       if (out->total) out->total[node] = totals[j];
       if (out->scored) out->scored[node] = 1;
-      uint64_t key = ksim_oracle_tb_key(totals[j], o->prof.tiebreak_seed, seq, node);
-      if (chosen < 0 || key > best) { best = key; chosen = node; }
+      const uint64_t lo = ksim_oracle_tb_lo(o->prof.tiebreak_seed, seq, node);
+      if (chosen < 0 || tb_better(totals[j], lo, best_total, best_lo)) {
+        best_total = totals[j];
+        best_lo = lo;
+        chosen = node;
+      }
     }
     free(tmp);
     free(totals);
@@ -962,9 +1009,10 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
     const int32_t pi = first + c;
     const ksim_pod* p = &ps->pods[pi];
     const int64_t seq = o->pod_seq++;
-    const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, N);
-    const int32_t start = o->next_start;
-    int32_t nf = 0, nfailed = 0, evaluated = 0, error = 0;
+    const scan_set ss = pod_scan_set(o, ps, p);
+    const int32_t NS = ss.n;
+    const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, NS);
+    int32_t nf = 0, nfailed = 0, evaluated = 0, error = (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 1 : 0;
     int32_t chosen = -1;
     topo_ctx tc;
     topo_prefilter(o, ps, p, &tc);
@@ -979,8 +1027,8 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
       }
 #pragma omp single
       {
-        for (int32_t i = 0; i < N; i++) {
-          int32_t node = (start + i) % N;
+        for (int32_t i = 0; i < NS; i++) {
+          int32_t node = scan_node_at(&ss, i);
           evaluated++;
           if (feas[node] == 2) {
             error = 1;
@@ -1013,16 +1061,21 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
             int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
             for (int32_t j = 0; j < nf; j++) totals[j] += v[j] * w;
           }
-          uint64_t best = 0;
+          int64_t best_total = 0;
+          uint64_t best_lo = 0;
           for (int32_t j = 0; j < nf; j++) {
-            uint64_t key = ksim_oracle_tb_key(totals[j], o->prof.tiebreak_seed, seq, o->flist[j]);
-            if (chosen < 0 || key > best) { best = key; chosen = o->flist[j]; }
+            const uint64_t lo = ksim_oracle_tb_lo(o->prof.tiebreak_seed, seq, o->flist[j]);
+            if (chosen < 0 || tb_better(totals[j], lo, best_total, best_lo)) {
+              best_total = totals[j];
+              best_lo = lo;
+              chosen = o->flist[j];
+            }
           }
         }
       }
     }
     if (nf == 1 && !error) chosen = o->flist[0];
-    o->next_start = (start + nf + nfailed) % N;
+    if (NS > 0) o->next_start = (int32_t)(((int64_t)o->next_start + nf + nfailed) % NS);
     evals += evaluated;
     if (chosen >= 0) { assume_pod(o, ps, p, chosen, 1); sched++; } else { unsched++; }
     if (chosen_out) chosen_out[c] = error ? KSIM_CHOSEN_ERROR : chosen;

@@ -60,6 +60,7 @@ int64_t ksim_oracle_least_requested_score(int64_t requested, int64_t capacity);
 int64_t ksim_oracle_balanced_score(int32_t n, const int64_t* requested, const int64_t* allocatable);
 void    ksim_oracle_default_normalize(int64_t max_priority, int reverse, int32_t n, int64_t* scores);
 uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node);
+uint64_t ksim_oracle_tb_lo(uint64_t seed, int64_t pod_seq, int32_t node);
 
 #ifdef __cplusplus
 }

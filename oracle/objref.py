@@ -39,10 +39,15 @@ def splitmix64(x: int) -> int:
     return z ^ (z >> 31)
 
 
-def tb_key(total: int, seed: int, seq: int, node: int) -> int:
-    """selectHost tie-break TB(seed)."""
+def tb_lo(seed: int, seq: int, node: int) -> int:
+    """The tie-break word of selectHost's TB(seed)."""
     h = splitmix64((seed ^ ((seq << 20) & M64) ^ node) & M64) >> 38
-    return (((total & M64) << 44) | (h << 18) | (KEY_NODE_MASK - node)) & M64
+    return (h << 18) | (KEY_NODE_MASK - node)
+
+
+def tb_key(total: int, seed: int, seq: int, node: int) -> tuple:
+    """selectHost's order: the max of (total, tie-break word), total a full int64."""
+    return (total, tb_lo(seed, seq, node))
 
 
 def num_feasible_nodes_to_find(pct: int, n: int) -> int:
@@ -50,6 +55,14 @@ def num_feasible_nodes_to_find(pct: int, n: int) -> int:
         return n
     a = pct if pct > 0 else max(5, 50 - n // 125)
     return max(n * a // 100, 100)
+
+
+def go_i64(x: int) -> int:
+    """Go int64 arithmetic wraps: (capacity - requested) * 100 overflows for
+    capacities past 2^56 (leastRequestedScore), and the quotient is of the
+    wrapped product."""
+    x &= M64
+    return x - (1 << 64) if x >> 63 else x
 
 
 def go_div(a: int, b: int) -> int:
@@ -526,7 +539,7 @@ class ObjScheduler:
         for alloc, req in ((ni.alloc["cpu"], ni.nz_cpu + ncpu), (ni.alloc["memory"], ni.nz_mem + nmem)):
             if alloc == 0:
                 continue
-            s = 0 if req > alloc else go_div((alloc - req) * MAX_NODE_SCORE, alloc)
+            s = 0 if req > alloc else go_div(go_i64((alloc - req) * MAX_NODE_SCORE), alloc)
             score += s
             wsum += 1
         return go_div(score, wsum) if wsum else 0
@@ -691,21 +704,51 @@ class ObjScheduler:
                 return pl, msg
         return None, None
 
+    @staticmethod
+    def node_affinity_prefilter(pod: Pod) -> Optional[set]:
+        """nodeaffinity.PreFilter's PreFilterResult.NodeNames (v1.26): None for
+        all nodes; an empty set when the terms conflict."""
+        if not pod.required_terms:
+            return None
+        out = None
+        for t in pod.required_terms:
+            term = None
+            for r in t.match_fields:
+                if r.key == "metadata.name" and r.operator == "In":
+                    term = set(r.values) if term is None else term & set(r.values)
+            if term is None:
+                return None                   # this term admits every node (terms are ORed)
+            out = set(term) if out is None else out | term
+        return out
+
     def cycle(self, pod: Pod, extender=None) -> dict:
         """``extender(kept node names) -> (filtered-out names, {name: combined weighted score})``
         models the scheduler's extenders (findNodesThatPassExtenders, prioritizeNodes)."""
-        N = len(self.nodes)
         seq = self.seq
         self.seq += 1
-        K = num_feasible_nodes_to_find(self.pct, N)
         pts = self.pts_prefilter(pod)
         ipa = self.ipa_prefilter(pod)
         filt: Dict[str, Tuple[Optional[str], Optional[str]]] = {}
+        # findNodesThatFitPod: PreFilterResult.NodeNames restricts the scan to
+        # those nodes (upstream in Go map order; here nodeTree order, the
+        # deterministic stand-in, SURVEY §8(b))
+        names_pf = self.node_affinity_prefilter(pod)
+        scan = self.nodes
+        if names_pf is not None:
+            if any(n not in self.by_name for n in names_pf):      # NodeInfos().Get fails
+                return {"filter": filt, "n_feasible": 0, "raw": {}, "norm": {}, "total": {},
+                        "error": "prefilter", "chosen": None}
+            if not names_pf:                                      # "pod affinity terms conflict"
+                return {"filter": filt, "n_feasible": 0, "raw": {}, "norm": {}, "total": {},
+                        "error": None, "chosen": None}
+            scan = [ni for ni in self.nodes if ni.node.name in names_pf]
+        N = len(scan)
+        K = num_feasible_nodes_to_find(self.pct, N)
         feasible: List[NodeInfo] = []
         failed = 0
         error = None
         for i in range(N):
-            ni = self.nodes[(self.next_start + i) % N]
+            ni = scan[(self.next_start + i) % N]
             pl, msg = self.filter_node(pod, ni, pts, ipa)
             if pl is not None and pl.endswith("!"):        # checkNode: the error ends the scan
                 filt[ni.node.name] = (pl[:-1], msg)

@@ -1,0 +1,294 @@
+"""GPU parity, round-2 cases: the HIP engine (through the C ABI) against the
+oracle, bit-exact.
+
+- NodeAffinity's PreFilterResult restricting the scan;
+- selectHost over full int64 totals: large weights (the batch paths' 20-bit
+  key gate) and extender scores far outside a 20-bit field;
+- a policy sweep on ONE handle exactly as bench.py runs config 5
+  (ksim_set_profile keeping the captured batch graphs, ksim_load_pods reusing
+  the pod buffers);
+- resource edge cases (allocatable 0, overcommitted nodes, quantities past
+  2^52 and 2^56, weight 0);
+- every BASELINE config at full size: config 2 (50,000 pods, both modes),
+  config 3 (10,000 nodes, 100,000 existing pods), config 4 (100,000 nodes as
+  an in-process 8-shard group), config 5 (16 weight vectors);
+- the Go-harness fixtures (tests/golden/go) through the engine.
+"""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from ksim import abi, gen, profile
+from ksim.encode import encode_cluster, encode_pods
+from ksim.engine import Engine, group_schedule_loaded
+from ksim.shard import partition
+from oracle.oracle import Oracle
+from test_gpu_parity import _batch_vs_oracle, _compare_cycle, _prof
+
+pytestmark = pytest.mark.gpu
+
+BIG_W = {"NodeResourcesBalancedAllocation": 900001, "ImageLocality": 1, "InterPodAffinity": 7,
+         "NodeResourcesFit": 1234567, "NodeAffinity": 40000, "PodTopologySpread": 2, "TaintToleration": 3}
+
+
+def _engine(cluster, prof):
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    return eng
+
+
+def _same_state(eng, ora):
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+
+
+# ---- NodeAffinity PreFilterResult ---------------------------------------------------
+@pytest.mark.parametrize("pct", [0, 100])
+def test_prefilter_node_names_compat(pct):
+    nodes, pods = gen.prefilter_objects(n_nodes=300, n_pods=360)
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods)
+    prof = _prof(pct)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    statuses = set()
+    for i in range(enc.n_pods):
+        e, o = eng.eval_pod(enc, i), ora.cycle(enc, i)
+        _compare_cycle(e, o, f"pod {i}")
+        statuses.add(o["status"])
+    _same_state(eng, ora)
+    assert {abi.STATUS_SCHEDULED, abi.STATUS_UNSCHEDULABLE, abi.STATUS_ERROR} <= statuses
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_prefilter_node_names_batch(pct):
+    """Restricted pods (per-pod path) interleaved with batchable ones: the
+    restricted scans move nextStartNodeIndex mod their length."""
+    nodes, pods = gen.prefilter_objects(n_nodes=1200, n_pods=2400)
+    for n in nodes:
+        n.taints = [t for t in n.taints if t.effect != "PreferNoSchedule"]
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods)
+    st = _batch_vs_oracle(cluster, enc, pct=pct)
+    assert st.perpod_cycles > 0 and st.batches > 0
+
+
+# ---- selectHost over full int64 totals ---------------------------------------------
+@pytest.mark.parametrize("pct", [0, 100])
+def test_large_weights_compat(pct):
+    cluster, pods = gen.config1(n_nodes=120, n_pods=200)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=pct).with_weights(BIG_W)
+    prof = profile.compile_profile(sp)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    top = 0
+    for i in range(pods.n_pods):
+        e, o = eng.eval_pod(pods, i), ora.cycle(pods, i)
+        _compare_cycle(e, o, f"pod {i}")
+        top = max(top, int(o["total"].max()))
+    assert top >= 1 << 20
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_large_weights_batch_gate(pct):
+    """100 x (w_fit + w_ba) >= 2^20: the pods leave the batch path for the
+    per-pod path (exact for any total); just below the bound they stay."""
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=2500)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=pct)
+    for w, batched in ((BIG_W, False), ({"NodeResourcesFit": 5000, "NodeResourcesBalancedAllocation": 5485}, True)):
+        prof = profile.compile_profile(sp.with_weights(w))
+        eng = _engine(cluster, prof)
+        chosen, st = eng.schedule_batch(pods)
+        ora = Oracle(cluster, prof)
+        ochosen, ost = ora.schedule(pods, nthreads=8)
+        np.testing.assert_array_equal(chosen, ochosen)
+        assert st.evals == ost.evals and eng.next_start == ora.next_start
+        assert (st.perpod_cycles == 0) == batched and (st.batches > 0) == batched
+
+
+@pytest.mark.parametrize("pct", [0, 100])
+def test_extender_scores_beyond_key_field(pct):
+    import test_extender
+    cluster, pods = gen.config1(n_nodes=160, n_pods=150)
+    fail, score = test_extender.extender_model(cluster.node_names)
+    score = (score - 150) * 10000 * 37                   # weights x 10^4, both signs
+    prof = _prof(pct)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(pods.n_pods):
+        _compare_cycle(eng.eval_pod_extenders(pods, i, lambda f: (fail, score)), ora.cycle(pods, i, fail, score),
+                       f"pod {i}")
+    _same_state(eng, ora)
+
+
+# ---- policy sweep on one handle (config 5 as bench.py runs it) ---------------------
+@pytest.mark.parametrize("case", ["fast", "generic", "adapt"])
+def test_sweep_one_engine_reuses_graphs(case):
+    """set_profile(w_k) -> load_pods (same queue, same buffers) ->
+    reset_cluster -> schedule_loaded, on ONE engine: the batch graphs captured
+    under the first vector replay under every later one (kernels read the
+    profile from device memory) and the placements equal the oracle's."""
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=9000)
+    pct = 0 if case == "adapt" else 100
+    base = profile.SchedulerProfile(percentage_of_nodes_to_score=pct)
+    if case == "generic":                                # bp.cpu_mem off: the generic evaluation kernel
+        base.fit.resources = [("cpu", 2), ("memory", 1), ("ephemeral-storage", 1)]
+    names = [p.name for p in base.score_plugins()]
+    vectors = gen.config5_weights(6)
+    eng = Engine(0)
+    eng.set_profile(profile.compile_profile(base))
+    eng.set_cluster(cluster)
+    caps = None
+    for k, v in enumerate(vectors):
+        prof = profile.compile_profile(base.with_weights({n: int(x) for n, x in zip(names, v)}))
+        eng.set_profile(prof)
+        eng.load_pods(pods)
+        eng.reset_cluster()
+        chosen, st = eng.schedule_loaded(0, pods.n_pods)
+        ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+        np.testing.assert_array_equal(chosen, ochosen, err_msg=f"vector {k}")
+        assert st.evals == ost.evals and st.perpod_cycles == 0
+        if k == 0:
+            caps = eng.diag()["graph_captures"]
+        else:
+            assert eng.diag()["graph_captures"] == caps, "set_profile / load_pods dropped the batch graphs"
+
+
+def test_config5_sweep_as_bench():
+    """bench.py's config-5 loop on the config-5 cluster: 16 vectors, one engine."""
+    cluster, pods = gen.config2(5000, 4500)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    names = [p.name for p in sp.score_plugins()]
+    eng = Engine(0)
+    eng.set_profile(profile.compile_profile(sp))
+    eng.set_cluster(cluster)
+    for k, v in enumerate(gen.config5_weights(16)):
+        prof = profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, v)}))
+        eng.set_profile(prof)
+        eng.load_pods(pods)
+        eng.reset_cluster()
+        chosen, _ = eng.schedule_loaded(0, pods.n_pods)
+        np.testing.assert_array_equal(chosen, Oracle(cluster, prof).schedule(pods, nthreads=16)[0],
+                                      err_msg=f"vector {k}")
+
+
+# ---- resource edge cases -----------------------------------------------------------
+@pytest.mark.parametrize("pct", [0, 100])
+def test_edge_quantities(pct):
+    nodes, bound, pods = gen.edge_objects()
+    cluster, _ = encode_cluster(nodes, bound)
+    enc = encode_pods(cluster, pods)
+    w0 = {"NodeResourcesBalancedAllocation": 0, "ImageLocality": 0, "InterPodAffinity": 0,
+          "NodeResourcesFit": 3, "NodeAffinity": 0, "PodTopologySpread": 0, "TaintToleration": 0}
+    for sp in (profile.SchedulerProfile(percentage_of_nodes_to_score=pct),
+               profile.SchedulerProfile(percentage_of_nodes_to_score=pct).with_weights(w0)):
+        prof = profile.compile_profile(sp)
+        eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+        for i in range(enc.n_pods):
+            _compare_cycle(eng.eval_pod(enc, i), ora.cycle(enc, i), f"pod {i}")
+        _same_state(eng, ora)
+        _batch_vs_oracle(cluster, enc, pct=pct)
+
+
+# ---- every BASELINE config at full size ----------------------------------------------
+@pytest.mark.parametrize("pct", [100, 0])
+def test_config2_full(pct):
+    """Config 2 exactly as bench.py runs it: 5,000 nodes x 50,000 pods."""
+    cluster, pods = gen.config2()
+    prof = _prof(pct)
+    eng = _engine(cluster, prof)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=16)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled and eng.next_start == ora.next_start
+    _same_state(eng, ora)
+
+
+def test_config3_full():
+    """Config 3 at BASELINE size (10,000 nodes, 3 zones, 100,000 existing pods
+    with anti-affinity terms): per-node outputs of the first 300 cycles, then
+    placements and count classes over the next 1,700."""
+    cluster, pods = gen.config3(n_incoming=2000)
+    prof = _prof(100)
+    eng, ora = _engine(cluster, prof), Oracle(cluster, prof)
+    for i in range(300):
+        _compare_cycle(eng.eval_pod(pods, i), ora.cycle(pods, i), f"pod {i}")
+    rest = pods.subset(300, pods.n_pods - 300)
+    chosen, st = eng.schedule_batch(rest)
+    ochosen, ost = ora.schedule(rest, nthreads=16)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    _same_state(eng, ora)
+
+
+def test_config4_group8():
+    """Config 4's cluster (100,000 nodes) as an in-process 8-shard group, the
+    node-sharded exchange protocol on one device, for 20,000 pods."""
+    cluster, pods = gen.config4(n_pods=20000)
+    prof = _prof(100)
+    engines = []
+    for base, cnt in partition(cluster.n_nodes, 8):
+        e = Engine(0)
+        e.set_shard(base, cluster.n_nodes)
+        e.set_profile(prof)
+        e.set_cluster(cluster.shard(base, cnt))
+        e.load_pods(pods)
+        engines.append(e)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=16)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+
+
+# ---- the Go-harness fixtures through the engine --------------------------------------
+GO = sorted(p for p in __import__("glob").glob(os.path.join(os.path.dirname(__file__), "golden", "go", "*.json.gz"))
+            if not p.endswith(".go.json.gz"))
+
+
+@pytest.mark.parametrize("path", GO, ids=[os.path.basename(p).split(".")[0] for p in GO])
+def test_go_fixtures_through_engine(path):
+    """The recorded cycles of each fixture (which a Go run would pin) reproduced
+    by the device: filter outcomes and messages, scores, totals, placement,
+    nextStartNodeIndex."""
+    from ksim.model import node_from_dict, pod_from_dict
+    from ksim.wrapped import filter_message
+    with gzip.open(path, "rb") as f:
+        doc = json.loads(f.read())
+    nodes = [node_from_dict(d) for d in doc["nodes"]]
+    bound = [pod_from_dict(d) for d in doc["boundPods"]]
+    pods = [pod_from_dict(d) for d in doc["pods"]]
+    cluster, _ = encode_cluster(nodes, bound, namespaces=doc["namespaces"])
+    enc = encode_pods(cluster, pods)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=doc["percentageOfNodesToScore"],
+                                  tiebreak_seed=doc["tiebreakSeed"],
+                                  hard_pod_affinity_weight=doc["hardPodAffinityWeight"])
+    eng = _engine(cluster, profile.compile_profile(sp))
+    forder, names = sp.filter_order(), cluster.node_names
+    snames = [p.name for p in sp.score_plugins()]
+    for i, exp in enumerate(doc["expected"]):
+        e = eng.eval_pod(enc, i)
+        where = f"{os.path.basename(path)}: pod {exp['pod']}"
+        for pos, name in enumerate(names):
+            fp = int(e["fail_plugin"][pos])
+            if fp == abi.NOT_EVALUATED:
+                assert name not in exp["filter"], where
+            elif fp == abi.PASSED:
+                assert exp["filter"][name] == "passed", (where, name)
+            else:
+                assert exp["filter"][name] == [forder[fp], filter_message(cluster, forder[fp],
+                                                                          int(e["fail_detail"][pos]))], (where, name)
+        assert e["n_feasible"] == exp["nFeasible"] and e["next_start"] == exp["nextStartNodeIndex"], where
+        if exp["nFeasible"] > 1:
+            for k, pl in enumerate(snames):
+                for name, raw in exp["score"][pl].items():
+                    assert e["raw"][k][names.index(name)] == raw, (where, pl, name)
+                    assert e["norm"][k][names.index(name)] == exp["normalized"][pl][name], (where, pl, name)
+            for name, tot in exp["total"].items():
+                assert e["total"][names.index(name)] == tot, (where, name)
+        got = names[e["chosen"]] if e["chosen"] >= 0 else None
+        assert got == exp["chosen"], where

@@ -74,6 +74,14 @@ def cases():
     hp = [tt._pod("y0", {"app": "y"}), tt._pod("x1", {"app": "z"}, pod_anti_affinity_required=[
         tt.PodAffinityTerm("kubernetes.io/hostname", tt.LabelSelector({"app": "x"}))])]
     yield run_case("ipa_hand_p100", hn, hb, hp, 100)
+    # NodeAffinity's PreFilterResult (metadata.name matchFields) restricting the
+    # scan; the harness models only sets of known nodes, so conflicting and
+    # unknown-name pods are left out
+    from ksim.encode import prefilter_node_names
+    pn, pp = gen.prefilter_objects(n_nodes=150, n_pods=90)
+    known = {n.name for n in pn}
+    keep = [p for p in pp if prefilter_node_names(p) != [] and set(prefilter_node_names(p) or ()) <= known]
+    yield run_case("prefilter_names_adapt", pn, [], keep, 0)
 
 
 def main():

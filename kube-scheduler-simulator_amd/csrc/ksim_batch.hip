@@ -59,19 +59,44 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
   // node loop is not unrolled so the kernel stays small (instruction cache).
   uint64_t a[kTileCand] = {0, 0, 0, 0};
   static_assert(kTileCand == 4, "insertion below is for 4 keys");
+  if constexpr (FAST) {
+    // the lane's kNodesPerLane keys as independent chains (every row load
+    // issued up front), then sorted in
+    const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
+    uint64_t kk[kNodesPerLane];
+    NodeRow rows[kNodesPerLane];
+    double ic[kNodesPerLane], im[kNodesPerLane];
+#pragma unroll
+    for (int k = 0; k < kNodesPerLane; k++) {
+      const int32_t node = tile * kTileNodes + k * 64 + lane;
+      const int32_t x = node < c.n ? node : c.n - 1;
+      rows[k] = load_res_row(c, x);
+      ic[k] = c.inv_cpu[x];
+      im[k] = c.inv_mem[x];
+    }
+    __builtin_amdgcn_sched_barrier(0);        // every row load in flight before the first key
+#pragma unroll
+    for (int k = 0; k < kNodesPerLane; k++) {
+      const int32_t node = tile * kTileNodes + k * 64 + lane;
+      kk[k] = node < c.n ? dyn_key_fast(bp, p, rows[k], ic[k], im[k], hseed, c.base + node) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kNodesPerLane; k++) {
+      a[3] = umax64(a[3], kk[k]);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+    }
+  }
 #pragma unroll 1
-  for (int k = 0; k < kNodesPerLane; k++) {
+  for (int k = 0; k < (FAST ? 0 : kNodesPerLane); k++) {
     const int32_t node = tile * kTileNodes + k * 64 + lane;
     uint64_t kk = 0;
     if (node < c.n) {
       // trivial: the static filters pass everywhere and the pod requests no
       // scalar resources, so only the resource columns are read
-      if constexpr (FAST) {
-        kk = dyn_key_cpu_mem(prof, bp, p, load_res_row(c, node), seq, c.base);
-      } else {
-        const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
-      }
+      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
     }
     a[3] = umax64(a[3], kk);
     cswap_desc(a[2], a[3]);
@@ -89,6 +114,153 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
       a[2] = a[3];
       a[3] = 0;
     }
+  }
+}
+
+// ---- k_batch_top: evaluation and the pod's top-T in one launch -------------------
+// One block per pod of the batch (kTopThreads threads, kTopWaves waves: two per
+// SIMD when every CU holds one block), the nodes strided over its lanes.  Each
+// lane keeps its best kTileCand keys (and counts its feasible nodes); each wave
+// extracts its provably exact top-T prefix from the lane lists; wave 0 merges
+// the wave lists into the pod's top-T.  A list holds only its best keys: once a
+// lane that had more feasible nodes than it kept has given up its last kept key,
+// the next key of its wave cannot be proven, so the wave's prefix ends there
+// (complete = 0); the block merge keeps the keys >= the last listed key of every
+// incomplete wave (every key a wave did not list is below it).  complete = 1:
+// every S0-feasible node is in the pod's list.  This replaces k_batch_eval's
+// per-tile lists and the k_batch_merge launch.
+template <bool FAST, int kTopThreads>
+__global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
+                                                           const ksim_profile* __restrict__ prof_p,
+                                                           const BatchProg* __restrict__ bp_p,
+                                                           const DevState* __restrict__ st,
+                                                           uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                                           int32_t* __restrict__ topk_complete,
+                                                           uint64_t* __restrict__ xsend) {
+  constexpr int kTopWaves = kTopThreads / 64;
+  constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
+  static_assert(kTopSlots <= 2 && kTileCand == 4, "k_batch_top geometry");
+  const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
+  const BatchProg& bp = *bp_p;
+  __shared__ uint64_t s_list[kTopWaves][kTopT];
+  __shared__ int32_t s_cnt[kTopWaves], s_complete[kTopWaves];
+  const int32_t base = st->cursor;
+  const int32_t j = blockIdx.x;
+  const int32_t pi = base + j;
+  if (pi >= min(st->end, base + kBatchPods)) return;        // block-uniform
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const ksim_pod& p = P.pods[pi];
+  const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
+  const int64_t seq = st->pod_seq + j;
+  const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
+  uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
+  int32_t nfeas = 0;
+  if constexpr (FAST) {
+    // two nodes per step as independent chains (both rows loaded up front)
+#pragma unroll 1
+    for (int32_t node = threadIdx.x; node < c.n; node += 2 * kTopThreads) {
+      const int32_t n2 = node + kTopThreads;
+      const int32_t x2 = n2 < c.n ? n2 : node;
+      const NodeRow r1 = load_res_row(c, node), r2 = load_res_row(c, x2);
+      const double c1 = c.inv_cpu[node], m1 = c.inv_mem[node], c2 = c.inv_cpu[x2], m2 = c.inv_mem[x2];
+      __builtin_amdgcn_sched_barrier(0);      // both rows in flight before the first key
+      const uint64_t k1 = dyn_key_fast(bp, p, r1, c1, m1, hseed, c.base + node);
+      const uint64_t k2 = n2 < c.n ? dyn_key_fast(bp, p, r2, c2, m2, hseed, c.base + n2) : 0;
+      nfeas += (k1 != 0) + (k2 != 0);
+      a[3] = umax64(a[3], k1);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+      a[3] = umax64(a[3], k2);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+    }
+  }
+#pragma unroll 1
+  for (int32_t node = threadIdx.x; node < (FAST ? 0 : c.n); node += kTopThreads) {
+    uint64_t kk = 0;
+    {
+      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+    }
+    nfeas += kk != 0;
+    a[3] = umax64(a[3], kk);
+    cswap_desc(a[2], a[3]);
+    cswap_desc(a[1], a[2]);
+    cswap_desc(a[0], a[1]);
+  }
+  // the wave's provable top-T prefix (lane t keeps key t)
+  uint64_t mine = 0;
+  int32_t cnt = 0, complete = 0, popped = 0;
+  for (int t = 0; t < kTopT; t++) {
+    const uint64_t m = wave_max_u64_dpp(a[0]);
+    if (m == 0) { complete = 1; break; }
+    if (lane == t) mine = m;
+    cnt = t + 1;
+    bool stop = false;
+    if (a[0] == m) {                              // keys are unique (the node is in the key)
+      a[0] = a[1];
+      a[1] = a[2];
+      a[2] = a[3];
+      a[3] = 0;
+      stop = ++popped == kTileCand && nfeas > kTileCand;
+    }
+    if (__ballot(stop)) break;
+  }
+  if (lane < kTopT) s_list[wv][lane] = lane < cnt ? mine : 0;
+  if (lane == 0) {
+    s_cnt[wv] = cnt;
+    s_complete[wv] = complete;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  // block merge: entry x = w * kTopT + e sits in lane x % 64, slot x / 64
+  uint64_t key[kTopSlots], last = 0;
+  bool incomplete = false;
+#pragma unroll
+  for (int q = 0; q < kTopSlots; q++) {
+    const int x = q * 64 + lane, w = x / kTopT, e = x % kTopT;
+    key[q] = 0;
+    if (w < kTopWaves) {
+      const int32_t n = s_cnt[w];
+      if (e < n) key[q] = s_list[w][e];
+      if (!s_complete[w] && n > 0 && e == n - 1) last = umax64(last, key[q]);
+      if (!s_complete[w] && e == 0) incomplete = true;
+    }
+  }
+  const uint64_t thr = wave_max_u64_dpp(last);   // the largest "last listed key" of an incomplete wave
+  const bool all_complete = __ballot(incomplete) == 0;
+  int32_t nvalid = 0;
+#pragma unroll
+  for (int q = 0; q < kTopSlots; q++) {
+    if (key[q] < thr) key[q] = 0;                // not provably in the pod's order
+    nvalid += __popcll(__ballot(key[q] != 0));
+  }
+  uint64_t out = 0;
+  int32_t n_out = 0;
+  for (int t = 0; t < kTopT; t++) {
+    uint64_t best = key[0];
+#pragma unroll
+    for (int q = 1; q < kTopSlots; q++) best = umax64(best, key[q]);
+    const uint64_t m = wave_max_u64_dpp(best);
+    if (m == 0) break;
+    if (lane == t) out = m;
+    n_out = t + 1;
+#pragma unroll
+    for (int q = 0; q < kTopSlots; q++)
+      if (key[q] == m) key[q] = 0;
+  }
+  const int32_t cmp = (all_complete && nvalid <= kTopT) ? 1 : 0;
+  if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < n_out ? out : 0;
+  if (lane == 0) {
+    topk_cnt[j] = n_out;
+    topk_complete[j] = cmp;
+  }
+  if (xsend) {                                   // sharded: this shard's record for the all-gather
+    uint64_t* x = xsend + (size_t)j * kXRec;
+    if (lane < kTopT) x[lane] = lane < n_out ? out : 0;
+    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)n_out | ((uint64_t)cmp << 32);
   }
 }
 
@@ -428,7 +600,8 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
       if constexpr (FAST) {
         NodeRow r = load_res_row(c, local);
         row_add_pod(r, P.pods[base + k], 1);
-        v = dyn_key_cpu_mem(prof, bp, p, r, seq0 + j, c.base);
+        v = dyn_key_fast(bp, p, r, c.inv_cpu[local], c.inv_mem[local], prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20),
+                         c.base + local);
       } else {
         NodeRow r = load_row(c, local);
         row_add_pod(r, P.pods[base + k], 1);
@@ -467,19 +640,46 @@ __global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {
   for (int r = 0; r < g.n; r++) g.p[r][j] = m;
 }
 
-const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_eval", "k_batch_merge", "k_batch_chain",
+const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch_merge", "k_batch_chain",
                                                          "k_batch_pairs", "k_batch_commit"};
 
+// A/B switch (read once per process): the round-1 two-launch form, per-tile
+// lists (k_batch_eval) merged by k_batch_merge.
+static bool tile_eval() {
+  static const bool on = getenv("KSIM_BATCH_TILES") != nullptr;
+  return on;
+}
+
+// Evaluation and per-pod top-T (xsend: the sharded record, else null).
+static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream, hipEvent_t* mid = nullptr) {
+  if (tile_eval()) {
+    const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
+    const dim3 g1((n_tiles + 3) / 4, kBatchPods);
+    if (a.fast)
+      k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
+    else
+      k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
+    if (mid) (void)hipEventRecord(*mid, stream);
+    launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, stream);
+    return;
+  }
+  static const int threads = getenv("KSIM_TOP_THREADS") ? atoi(getenv("KSIM_TOP_THREADS")) : 1024;   // A/B
+#define TOP(F, T) k_batch_top<F, T><<<kBatchPods, T, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, \
+                                                                   a.s.topk_cnt, a.s.topk_complete, xsend)
+  if (threads == 512) {
+    if (a.fast) TOP(true, 512);
+    else TOP(false, 512);
+  } else {
+    if (a.fast) TOP(true, 1024);
+    else TOP(false, 1024);
+  }
+#undef TOP
+  if (mid) (void)hipEventRecord(*mid, stream);
+}
+
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
-  const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
-  const dim3 g1((n_tiles + 3) / 4, kBatchPods);
   if (evs) (void)hipEventRecord(evs[0], stream);
-  if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  if (evs) (void)hipEventRecord(evs[1], stream);
-  launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, stream);
+  launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
@@ -498,12 +698,16 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
 }
 
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
-  const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
-  const dim3 g1((n_tiles + 3) / 4, kBatchPods);
-  if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
+  if (tile_eval()) {
+    const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
+    const dim3 g1((n_tiles + 3) / 4, kBatchPods);
+    if (a.fast)
+      k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
+    else
+      k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
+    return;
+  }
+  launch_eval_top(a, nullptr, stream);
 }
 
 void launch_chain(const LaunchArgs& a, hipStream_t stream) {
@@ -511,15 +715,7 @@ void launch_chain(const LaunchArgs& a, hipStream_t stream) {
                                               a.s.gkey, a.s.chain_end, a.s.dbg);
 }
 
-void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) {
-  const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
-  const dim3 g1((n_tiles + 3) / 4, kBatchPods);
-  if (a.fast)
-    k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  else
-    k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-  launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend, stream);
-}
+void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) { launch_eval_top(a, a.s.xsend, stream); }
 
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {
   k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,

@@ -58,6 +58,10 @@ struct DevCluster {
   // pods' request annotations (getNodeAllocatedAmount), updated by every bind
   const int64_t* nb_limit;
   int64_t* nb_alloc;
+  // RN(1 / allocatable) of cpu and memory (0 for allocatable 0), host-computed:
+  // the FAST batch kernels divide by them (div_rn)
+  const double* inv_cpu;
+  const double* inv_mem;
 };
 
 struct DevPods {
@@ -901,6 +905,11 @@ struct BatchProg {
   int32_t cpu_mem;                         // both scoring strategies are exactly {cpu, memory}
   int64_t w_fit, w_ba;                     // summed profile weights of the Fit / BA score slots
   int64_t fit_w_cpu, fit_w_mem;            // cpu_mem: LeastAllocated resource weights
+  int32_t fast_w;                          // cpu_mem with both LeastAllocated weights in [1, 2^31) (dyn_key_fast)
+  int32_t no_score;                        // the profile has no score plugin: every total is 1
+  int32_t fit_w_eq;                        // fast_w and fit_w_cpu == fit_w_mem: the mean is a halving
+  int32_t _pad;
+  double inv_w[3];                         // RN(1 / w) of fit_w_cpu, fit_w_mem, their sum (dyn_key_fast)
 };
 
 // DevPods.bflags (batch path, per pod)
@@ -1053,6 +1062,79 @@ __device__ __forceinline__ uint64_t dyn_key_cpu_mem(const ksim_profile& prof, co
   }
   if (prof.n_score == 0) tot = 1;
   return tb_key(tot, prof.tiebreak_seed, seq, base + r.node);
+}
+
+// The correctly rounded quotient n / d (the IEEE division's result) from
+// y = RN(1 / d): q0 = RN(n y) is within an ulp of n / d, the FMA residual
+// n - q0 d is exact, and one FMA correction rounds correctly (Markstein's
+// theorem; operands here are integers far from overflow and underflow).  The
+// FMAs are explicit: they emulate a division, they do not contract any of the
+// plugins' own float64 expressions (-ffp-contract=off still holds for those).
+__device__ __forceinline__ double div_rn(double n, double d, double y) {
+  const double q0 = n * y;
+  const double e = __builtin_fma(-q0, d, n);
+  return __builtin_fma(e, y, q0);
+}
+
+// The FAST key (k_batch_top<true>, k_batch_pairs<true>): trivial pods (every
+// static filter host-proven to pass), {cpu, memory} strategies with
+// LeastAllocated weights in [1, 2^31) (BatchProg::fast_w), allocatable cpu and
+// memory in [0, 2^46) on every node (checked at ksim_set_cluster).  Then each
+// leastRequestedScore quotient n / d has integers n < 2^53, 0 < d < 2^46, and
+// the truncation of the correctly rounded float64 quotient IS the integer
+// quotient: an integer quotient is exact, any other lies at least 1/d > 2^-46
+// below the next integer while the rounding error of a quotient below 128 is
+// at most 2^-47.  The same bound covers the weighted mean (n < 2^40, d < 2^32).
+// Each division is div_rn with the host's RN(1 / d) (DevCluster inv_cpu /
+// inv_mem, BatchProg inv_w): three float64 operations instead of a 64-bit division and
+// its correction steps, and for BalancedAllocation bit for bit the float64
+// quotient Go computes.  hseed = seed ^ (seq << 20), the pod's part of the
+// tie-break hash.
+__device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+                                                 double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
+  if (bp.has_fit_filter) {
+    if (r.num_pods + 1 > r.alloc_pods) return 0;
+    if ((p.req_cpu != 0 || p.req_mem != 0 || p.req_eph != 0) &&
+        (p.req_cpu > r.alloc_cpu - r.req_cpu || p.req_mem > r.alloc_mem - r.req_mem ||
+         p.req_eph > r.alloc_eph - r.req_eph))
+      return 0;
+  }
+  const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
+  const double ac = (double)r.alloc_cpu, am = (double)r.alloc_mem;
+  int32_t tot = 0;
+  if (bp.w_fit) {                              // leastResourceScorer over {cpu, memory}
+    const int64_t rc = r.nz_cpu + p.nz_cpu, rm = r.nz_mem + p.nz_mem;
+    const int32_t sc = (!hc || rc > r.alloc_cpu) ? 0
+                       : (int32_t)div_rn((double)((r.alloc_cpu - rc) * kMaxNodeScore), ac, inv_c);
+    const int32_t sm = (!hm || rm > r.alloc_mem) ? 0
+                       : (int32_t)div_rn((double)((r.alloc_mem - rm) * kMaxNodeScore), am, inv_m);
+    int32_t la;
+    if (bp.fit_w_eq) {                         // (sc w + sm w) / (2 w)
+      la = (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;
+    } else {
+      const int64_t wc = hc ? bp.fit_w_cpu : 0, wm = hm ? bp.fit_w_mem : 0;
+      const double inv = (hc && hm) ? bp.inv_w[2] : hc ? bp.inv_w[0] : bp.inv_w[1];
+      la = (hc || hm) ? (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv) : 0;
+    }
+    tot += (int32_t)bp.w_fit * la;
+  }
+  if (bp.w_ba) {                               // balancedResourceScorer over {cpu, memory}
+    double f0 = 0, f1 = 0;
+    if (hc) {
+      const double f = div_rn((double)(r.req_cpu + p.req_cpu), ac, inv_c);
+      f0 = f > 1 ? 1 : f;
+    }
+    if (hm) {
+      const double f = div_rn((double)(r.req_mem + p.req_mem), am, inv_m);
+      if (hc) f1 = f > 1 ? 1 : f;
+      else f0 = f > 1 ? 1 : f;
+    }
+    const double std = (hc && hm) ? fabs((f0 - f1) / 2) : 0.0;
+    tot += (int32_t)bp.w_ba * (int32_t)((1 - std) * (double)kMaxNodeScore);
+  }
+  if (bp.no_score) tot = 1;
+  const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
+  return ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);
 }
 
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).

@@ -87,6 +87,7 @@ struct ksim_handle {
   std::vector<uint8_t> taint_effect;    // host copy (batchability analysis)
   std::vector<uint16_t> hard_taints;    // taint ids with effect NoSchedule/NoExecute on some node
   bool any_unschedulable = false;       // some node has spec.unschedulable
+  bool alloc_narrow = false;            // every allocatable cpu / memory in [0, 2^46) (dyn_key_fast)
 
   // device copy of the uploaded dynamic columns (ksim_reset_cluster)
   struct {
@@ -287,8 +288,10 @@ bool static_trivial(const ksim_handle* h, const ksim_pod& p) {
 
 bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_total != 0; }
 
+// The FAST batch kernels (dyn_key_fast): trivial pods, {cpu, memory}
+// strategies with weights in [1, 2^31), allocatable cpu / memory below 2^46.
 bool run_fast(const ksim_handle* h, int32_t a, int32_t b) {
-  if (!h->bp.cpu_mem) return false;
+  if (!h->bp.cpu_mem || !h->bp.fast_w || !h->alloc_narrow) return false;
   for (int32_t i = a; i < b; i++)
     if (!h->trivial[i]) return false;
   return true;
@@ -524,7 +527,8 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
 int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   ksim_handle* h0 = hs[0];
   hipStream_t stream = h0->stream;
-  const bool fast = run_fast(h0, a, b);
+  bool fast = run_fast(h0, a, b);                      // every shard of an in-process group alike
+  for (auto* h : hs) fast = fast && h->alloc_narrow;
   for (auto* h : hs) {
     int rc;
     if ((rc = set_run(h, a, b))) return rc;
@@ -732,6 +736,15 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
                p->ba_n_res == 2 && p->ba_res[0] == KSIM_RES_CPU && p->ba_res[1] == KSIM_RES_MEMORY;
   bp.fit_w_cpu = p->fit_res_weight[0];
   bp.fit_w_mem = p->fit_res_weight[1];
+  bp.fast_w = bp.cpu_mem && bp.fit_w_cpu >= 1 && bp.fit_w_cpu < (1ll << 31) && bp.fit_w_mem >= 1 &&
+              bp.fit_w_mem < (1ll << 31);
+  bp.no_score = p->n_score == 0;
+  bp.fit_w_eq = bp.fast_w && bp.fit_w_cpu == bp.fit_w_mem;
+  if (bp.fast_w) {                                    // RN(1 / w): IEEE division on the host
+    bp.inv_w[0] = 1.0 / (double)bp.fit_w_cpu;
+    bp.inv_w[1] = 1.0 / (double)bp.fit_w_mem;
+    bp.inv_w[2] = 1.0 / (double)(bp.fit_w_cpu + bp.fit_w_mem);
+  }
   for (int i = 0; i < p->n_filter; i++) {
     const int f = p->filter[i];
     if (f == KSIM_PL_NODE_UNSCHEDULABLE || f == KSIM_PL_NODE_NAME || f == KSIM_PL_TAINT_TOLERATION ||
@@ -868,6 +881,15 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   UP(col_nvals, col_nvals.data(), 4 * col_nvals.size());
   UP(nb_limit, t->nb_limit, 8 * N);                      // zeros when no node has the annotation
   UP(nb_alloc, t->nb_alloc, 8 * N);
+  {
+    std::vector<double> ic(N), im(N);                  // RN(1 / allocatable): IEEE division on the host
+    for (size_t i = 0; i < N; i++) {
+      ic[i] = t->alloc_cpu[i] ? 1.0 / (double)t->alloc_cpu[i] : 0.0;
+      im[i] = t->alloc_mem[i] ? 1.0 / (double)t->alloc_mem[i] : 0.0;
+    }
+    UP(inv_cpu, ic.data(), 8 * N);
+    UP(inv_mem, im.data(), 8 * N);
+  }
 #undef UP
   h->col_nvals = col_nvals;
   h->dc = c;
@@ -881,6 +903,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
         h->hard_taints.push_back((uint16_t)id);
     h->any_unschedulable = false;
     for (int32_t i = 0; i < n; i++) h->any_unschedulable = h->any_unschedulable || (t->flags[i] & KSIM_NODE_UNSCHEDULABLE);
+    h->alloc_narrow = true;
+    for (int32_t i = 0; i < n; i++)
+      h->alloc_narrow = h->alloc_narrow && t->alloc_cpu[i] >= 0 && t->alloc_cpu[i] < (1ll << 46) &&
+                        t->alloc_mem[i] >= 0 && t->alloc_mem[i] < (1ll << 46);
   }
   {
     void* q = nullptr;

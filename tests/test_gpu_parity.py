@@ -142,8 +142,13 @@ def test_batch_truncation_identical_pods():
     cluster.alloc_cpu[:] = 64000
     cluster.alloc_mem[:] = 256 << 30
     pods = gen.bare_pods(3000, seed=5, cpu_steps=1, mem_steps=1)
+    prof = _prof(100)
     st = _batch_vs_oracle(cluster, pods)
-    assert st.truncations > 0
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    eng.schedule_batch(pods)
+    assert st.truncations + eng.diag()["cuts"] > 0 and st.batches > pods.n_pods // 256
 
 
 def test_batch_mixed_runs_config1_p100():

@@ -36,8 +36,8 @@ extern "C" {
 #define KSIM_MAX_NODES        KSIM_KEY_NODE_MASK
 #define KSIM_MAX_NODE_TAINTS  8          /* taints per node, node.Spec.Taints order */
 #define KSIM_TAINT_WORDS      4          /* taint vocabulary <= 256 ids (id 0 = none) */
-#define KSIM_MAX_SCALAR       4          /* scalar (extended) resource columns */
-#define KSIM_MAX_LABEL_COLS   32         /* node label keys known to the engine */
+#define KSIM_MAX_SCALAR       8          /* scalar (extended) resource columns */
+#define KSIM_MAX_LABEL_COLS   256        /* node label keys with a column (the keys pods reference) */
 #define KSIM_EXPR_VALS        6          /* values per node-selector requirement */
 #define KSIM_MAX_FILTER       16
 #define KSIM_MAX_SCORE        8
@@ -395,6 +395,25 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p);
  * Snapshot / UpdateSnapshot that the wrapped plugins read through
  * framework.NodeInfo (scheduler/plugin/wrappedplugin.go:491, 388). */
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* nodes, const ksim_vocab* vocab);
+/* Node informer deltas (the scheduler cache's AddNode / UpdateNode /
+ * RemoveNode, then UpdateSnapshot) without losing the binds
+ * the cycles made.  `nodes` is the new snapshot in nodeTree order (static
+ * columns, vocabulary, and the dynamic columns of the pods bound in it);
+ * old_pos[i] is the current position of new node i, or -1 for an added node.
+ * On a kept node the binds made since the last snapshot (the device's dynamic
+ * column minus the snapshot's, at old_pos) are replayed on top of the table,
+ * for the scalar columns and count classes the handle already has; added
+ * nodes, appended scalar columns and appended classes take the table as is.
+ * The table becomes the ksim_reset_cluster snapshot.  Label columns may be
+ * added or dropped (the vocabulary is replaced).  nextStartNodeIndex carries
+ * over mod the new node count ([upstream] the scheduler keeps the index and
+ * scans nodes[(index + i) % numAllNodes]); the pod sequence carries over.
+ * Loaded pods and the bound-pod table refer to node positions and are
+ * dropped.  Unsharded handles only. */
+int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* nodes, const ksim_vocab* vocab, const int32_t* old_pos);
+/* RemoveNode of the node at position `pos` (later nodes move down by one),
+ * from the device-resident snapshot alone. */
+int ksim_remove_node(ksim_handle* h, int32_t pos);
 /* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
                         int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods);

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
                                                            uint64_t* __restrict__ xsend) {
   constexpr int kTopWaves = kTopThreads / 64;
   constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
-  static_assert(kTopSlots <= 2 && kTileCand == 4, "k_batch_top geometry");
+  static_assert(kTopSlots <= 4 && kTileCand == 4, "k_batch_top geometry");
   const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
   const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_list[kTopWaves][kTopT];
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
 // result); the batch keeps that exact prefix.  Node ids are mapped to slots of
 // an LDS hash table, and "held by an earlier pod" is an LDS atomicMin of pod
 // indices per slot.  Rounds needed = the depth of the conflict chain.
-constexpr int kHashBits = kTopT <= 8 ? 12 : 13;
+constexpr int kHashBits = kBatchPods * kTopT <= 2048 ? 12 : kBatchPods * kTopT <= 4096 ? 13 : 14;
 constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");

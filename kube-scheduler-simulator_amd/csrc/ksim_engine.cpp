@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "ksim_internal.h"
@@ -834,6 +835,13 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   h->batchable.clear();
   h->topo.clear();
   h->has_cluster = false;
+  // node positions of the old snapshot: the bound-pod table and a pending
+  // extender round trip do not carry over
+  free_bufs(h->pre_bufs);
+  h->pre = DevPreempt{};
+  h->pre_index.clear();
+  h->pre_n = 0;
+  h->ext_pending = false;
 
   const int32_t n_total = h->shard_total ? h->shard_total : n;
   if (h->shard_base < 0 || h->shard_base + n > n_total || n_total > KSIM_MAX_NODES)
@@ -979,6 +987,182 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   h->d_chosen = nullptr;
   return KSIM_OK;
+}
+
+// Node informer deltas: the new table in nodeTree order, old_pos[i] = the
+// current position of new node i or -1 (added).  The table is the new
+// snapshot (static columns, vocabulary and the dynamic columns of the bound
+// pods); on a kept node the binds the cycles made since the last snapshot
+// (device column - snapshot column at old_pos) are replayed on top of it, for
+// every scalar column / count class the handle already has.  nextStartNodeIndex
+// carries over mod the new node count (upstream keeps the index and scans
+// nodes[(index + i) % numAllNodes]), and so does the tie-break sequence.
+// Loaded pods, the bound-pod table and captured graphs are dropped (node
+// positions changed).
+int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v, const int32_t* old_pos) {
+  if (!h || !t || !v) return KSIM_E_INVALID;
+  if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_upsert_nodes before ksim_set_cluster");
+  if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_upsert_nodes on a shard handle");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int32_t n = t->n_nodes, n0 = h->dc.n;
+  if (n < 0 || n > KSIM_MAX_NODES) return set_err(h, KSIM_E_INVALID, "n_nodes out of range");
+  if (n > 0 && !old_pos) return set_err(h, KSIM_E_INVALID, "null old_pos");
+  const int32_t s0 = h->dc.n_scalar, c0 = h->dc.n_classes;
+  if (t->n_scalar < s0 || t->n_scalar > KSIM_MAX_SCALAR)
+    return set_err(h, KSIM_E_INVALID, "scalar columns may only be appended");
+  if (t->n_classes < c0 || t->n_classes > KSIM_MAX_CLASSES)
+    return set_err(h, KSIM_E_INVALID, "count classes may only be appended");
+  if (n > 0 && (!t->req_cpu || !t->req_mem || !t->req_eph || !t->nz_cpu || !t->nz_mem || !t->num_pods ||
+                (t->n_scalar > 0 && !t->req_scalar) || (t->n_classes > 0 && !t->class_count)))
+    return set_err(h, KSIM_E_INVALID, "null node column");
+  {
+    std::vector<uint8_t> seen((size_t)n0, 0);
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t op = old_pos[i];
+      if (op < -1 || op >= n0 || (op >= 0 && seen[op]++))
+        return set_err(h, KSIM_E_INVALID, "old_pos: out of range or repeated");
+    }
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  DevState st{};
+  HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+  const size_t N = (size_t)n, N0 = (size_t)n0;
+  // out = table + (device - snapshot) at old_pos, rows of n0 -> rows of n
+  auto replay = [&](auto& out, const auto* dev, const auto* snap, const auto* tab, int rows, int rows0) -> int {
+    using T = typename std::remove_reference<decltype(out)>::type::value_type;
+    std::vector<T> a(N0 * (size_t)rows0), b(N0 * (size_t)rows0);
+    if (!a.empty()) {
+      HIPCHK(h, hipMemcpy(a.data(), dev, sizeof(T) * a.size(), hipMemcpyDeviceToHost));
+      HIPCHK(h, hipMemcpy(b.data(), snap, sizeof(T) * b.size(), hipMemcpyDeviceToHost));
+    }
+    out.assign(N * (size_t)rows, 0);
+    for (int k = 0; k < rows; k++)
+      for (size_t i = 0; i < N; i++) {
+        T x = tab ? tab[k * N + i] : 0;
+        if (k < rows0 && old_pos[i] >= 0) x += a[k * N0 + old_pos[i]] - b[k * N0 + old_pos[i]];
+        out[k * N + i] = x;
+      }
+    return KSIM_OK;
+  };
+  std::vector<int64_t> rc_, rm, re, rs, zc, zm, nb;
+  std::vector<int32_t> np, cnt;
+  int rc;
+  const DevCluster& c = h->dc;
+  if ((rc = replay(rc_, c.req_cpu, h->init.req_cpu, t->req_cpu, 1, 1)) ||
+      (rc = replay(rm, c.req_mem, h->init.req_mem, t->req_mem, 1, 1)) ||
+      (rc = replay(re, c.req_eph, h->init.req_eph, t->req_eph, 1, 1)) ||
+      (rc = replay(rs, c.req_scalar, h->init.req_scalar, t->req_scalar, t->n_scalar, s0)) ||
+      (rc = replay(zc, c.nz_cpu, h->init.nz_cpu, t->nz_cpu, 1, 1)) ||
+      (rc = replay(zm, c.nz_mem, h->init.nz_mem, t->nz_mem, 1, 1)) ||
+      (rc = replay(nb, c.nb_alloc, h->init.nb_alloc, t->nb_alloc, 1, 1)) ||
+      (rc = replay(np, c.num_pods, h->init.num_pods, t->num_pods, 1, 1)) ||
+      (rc = replay(cnt, c.cnt, h->init.cnt, t->class_count, t->n_classes, c0)))
+    return rc;
+  // the table becomes the snapshot (ksim_set_cluster copies it to h->init)
+  if ((rc = ksim_set_cluster(h, t, v)) != KSIM_OK) return rc;
+  const DevCluster& d = h->dc;
+  auto put = [&](void* dst, const void* src, size_t bytes) -> int {
+    if (bytes) HIPCHK(h, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return KSIM_OK;
+  };
+  if ((rc = put(d.req_cpu, rc_.data(), 8 * N)) || (rc = put(d.req_mem, rm.data(), 8 * N)) ||
+      (rc = put(d.req_eph, re.data(), 8 * N)) || (rc = put(d.req_scalar, rs.data(), 8 * rs.size())) ||
+      (rc = put(d.nz_cpu, zc.data(), 8 * N)) || (rc = put(d.nz_mem, zm.data(), 8 * N)) ||
+      (rc = put(d.num_pods, np.data(), 4 * N)) || (rc = put(d.cnt, cnt.data(), 4 * cnt.size())) ||
+      (rc = put(d.nb_alloc, nb.data(), 8 * N)))
+    return rc;
+  DevState s2{};
+  s2.next_start = n > 0 ? st.next_start % n : 0;
+  s2.pod_seq = st.pod_seq;
+  HIPCHK(h, hipMemcpy(h->st, &s2, sizeof(s2), hipMemcpyHostToDevice));
+  return KSIM_OK;
+}
+
+// DeleteNode: the node at `pos` leaves; later positions move down by one.  The
+// table handed to ksim_upsert_nodes is the current snapshot without it, so the
+// replay keeps every other node's state.
+int ksim_remove_node(ksim_handle* h, int32_t pos) {
+  if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
+  if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_remove_node on a shard handle");
+  const int32_t n0 = h->dc.n;
+  if (pos < 0 || pos >= n0) return set_err(h, KSIM_E_INVALID, "node position out of range");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const DevCluster& c = h->dc;
+  const int32_t n = n0 - 1;
+  const size_t N0 = (size_t)n0;
+  // the static columns and vocabulary, read back and compacted
+  auto pull = [&](auto& out, const auto* dev, size_t rows) -> int {
+    using T = typename std::remove_reference<decltype(out)>::type::value_type;
+    std::vector<T> all(N0 * rows);
+    if (!all.empty()) HIPCHK(h, hipMemcpy(all.data(), dev, sizeof(T) * all.size(), hipMemcpyDeviceToHost));
+    out.clear();
+    for (size_t k = 0; k < rows; k++)
+      for (size_t i = 0; i < N0; i++)
+        if ((int32_t)i != pos) out.push_back(all[k * N0 + i]);
+    return KSIM_OK;
+  };
+  std::vector<int64_t> ac, am, ae, as, rc_, rm, re, rs, zc, zm, nbl, nba;
+  std::vector<int32_t> ap, np, cnt;
+  std::vector<uint32_t> fl, lb;
+  std::vector<uint16_t> tn;
+  int rc;
+  if ((rc = pull(ac, c.alloc_cpu, 1)) || (rc = pull(am, c.alloc_mem, 1)) || (rc = pull(ae, c.alloc_eph, 1)) ||
+      (rc = pull(as, c.alloc_scalar, (size_t)c.n_scalar)) || (rc = pull(ap, c.alloc_pods, 1)) ||
+      (rc = pull(rc_, h->init.req_cpu, 1)) || (rc = pull(rm, h->init.req_mem, 1)) ||
+      (rc = pull(re, h->init.req_eph, 1)) || (rc = pull(rs, h->init.req_scalar, (size_t)c.n_scalar)) ||
+      (rc = pull(zc, h->init.nz_cpu, 1)) || (rc = pull(zm, h->init.nz_mem, 1)) ||
+      (rc = pull(np, h->init.num_pods, 1)) || (rc = pull(fl, c.flags, 1)) ||
+      (rc = pull(tn, c.taints, KSIM_MAX_NODE_TAINTS)) || (rc = pull(lb, c.labels, (size_t)c.n_label_cols)) ||
+      (rc = pull(cnt, h->init.cnt, (size_t)c.n_classes)) || (rc = pull(nbl, c.nb_limit, 1)) ||
+      (rc = pull(nba, h->init.nb_alloc, 1)))
+    return rc;
+  std::vector<uint8_t> te(h->taint_effect);
+  std::vector<int32_t> lco((size_t)c.n_label_cols);
+  std::vector<int64_t> lnum((size_t)std::max(c.n_label_values, 0));
+  std::vector<uint8_t> lok((size_t)std::max(c.n_label_values, 0));
+  std::vector<double> tlog((size_t)c.n_topo_log);
+  if (!lco.empty()) HIPCHK(h, hipMemcpy(lco.data(), c.label_col_offset, 4 * lco.size(), hipMemcpyDeviceToHost));
+  if (!lnum.empty()) {
+    HIPCHK(h, hipMemcpy(lnum.data(), c.label_num, 8 * lnum.size(), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(lok.data(), c.label_num_ok, lok.size(), hipMemcpyDeviceToHost));
+  }
+  if (!tlog.empty()) HIPCHK(h, hipMemcpy(tlog.data(), c.topo_log, 8 * tlog.size(), hipMemcpyDeviceToHost));
+  ksim_node_table t{};
+  t.n_nodes = n;
+  t.n_scalar = c.n_scalar;
+  t.n_label_cols = c.n_label_cols;
+  t.alloc_cpu = ac.data();
+  t.alloc_mem = am.data();
+  t.alloc_eph = ae.data();
+  t.alloc_pods = ap.data();
+  t.alloc_scalar = as.data();
+  t.req_cpu = rc_.data();
+  t.req_mem = rm.data();
+  t.req_eph = re.data();
+  t.req_scalar = rs.data();
+  t.nz_cpu = zc.data();
+  t.nz_mem = zm.data();
+  t.num_pods = np.data();
+  t.flags = fl.data();
+  t.taints = tn.data();
+  t.labels = lb.data();
+  t.n_classes = c.n_classes;
+  t.class_count = cnt.data();
+  t.nb_limit = nbl.data();
+  t.nb_alloc = nba.data();
+  ksim_vocab v{};
+  v.n_taints = (int32_t)te.size();
+  v.n_label_values = c.n_label_values;
+  v.taint_effect = te.data();
+  v.label_col_offset = lco.data();
+  v.label_num = lnum.data();
+  v.label_num_ok = lok.data();
+  v.n_topo_log = c.n_topo_log;
+  v.topo_log = tlog.data();
+  std::vector<int32_t> old_pos((size_t)std::max(n, 1));
+  for (int32_t i = 0; i < n; i++) old_pos[i] = i < pos ? i : i + 1;
+  return ksim_upsert_nodes(h, &t, &v, old_pos.data());
 }
 
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,

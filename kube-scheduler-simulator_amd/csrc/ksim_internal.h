@@ -7,8 +7,15 @@
 namespace ksim {
 
 // Batch path geometry.
-constexpr int kBatchPods = 256;    // B: pods per speculative batch
-constexpr int kTopT = 8;           // T: candidate keys kept per pod (16 measured: fewer truncations, slower merge/chain)
+// Compile-time overridable for A/B builds (-DKSIM_BATCH_PODS=512 -DKSIM_TOP_T=16).
+#ifndef KSIM_BATCH_PODS
+#define KSIM_BATCH_PODS 256
+#endif
+#ifndef KSIM_TOP_T
+#define KSIM_TOP_T 8
+#endif
+constexpr int kBatchPods = KSIM_BATCH_PODS;   // B: pods per speculative batch
+constexpr int kTopT = KSIM_TOP_T;             // T: candidate keys kept per pod
 static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch geometry");
 constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
 constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile

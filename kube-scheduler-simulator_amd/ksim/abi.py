@@ -15,8 +15,8 @@ ABI_VERSION = 4
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
 TAINT_WORDS = 4
-MAX_SCALAR = 4
-MAX_LABEL_COLS = 32
+MAX_SCALAR = 8
+MAX_LABEL_COLS = 256
 EXPR_VALS = 6
 MAX_FILTER = 16
 MAX_SCORE = 8

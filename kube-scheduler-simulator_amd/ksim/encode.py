@@ -154,6 +154,9 @@ class EncodedCluster:
     nb_limit: Optional[np.ndarray] = None             # [N] int64
     nb_alloc: Optional[np.ndarray] = None             # [N] int64
     nb_args: netbw.NetworkBandwidthArgs = field(default_factory=netbw.NetworkBandwidthArgs)
+    # node labels (nodeTree order): a label key gets a column only once a pod
+    # references it (selector, affinity term, topology key), see label_col
+    node_labels: Optional[List[Dict[str, str]]] = None
 
     def __post_init__(self):
         if self.topo is None:
@@ -216,10 +219,41 @@ class EncodedCluster:
         for f in ("alloc_scalar", "req_scalar", "taints", "labels", "class_count"):
             setattr(c, f, np.ascontiguousarray(getattr(self, f)[:, sl]))
         c.node_names = self.node_names[sl]
+        if self.node_labels is not None:
+            c.node_labels = self.node_labels[sl]
         return c
 
     def label_col(self, key: str) -> int:
-        return self.label_keys.index(key) if key in self.label_keys else -1
+        """The key's label column; a key some node carries gets one on first
+        use (nodes carry many keys, the engine needs only the referenced ones).
+        -1: no node carries the key."""
+        if key in self.label_keys:
+            return self.label_keys.index(key)
+        if self.node_labels is None or not any(key in lb for lb in self.node_labels):
+            return -1
+        if len(self.label_keys) >= abi.MAX_LABEL_COLS:
+            raise EncodeError(f"more than {abi.MAX_LABEL_COLS} referenced label keys")
+        values = [""]
+        index: Dict[str, int] = {}
+        row = np.zeros((1, self.n_nodes), np.uint32)
+        for pos, lb in enumerate(self.node_labels):
+            v = lb.get(key)
+            if v is None:
+                continue
+            vid = index.get(v)
+            if vid is None:
+                vid = index[v] = len(values)
+                values.append(v)
+            row[0, pos] = vid
+        # new lists / arrays (never in place: copies of this cluster share them)
+        self.label_col_offset = np.append(self.label_col_offset, np.int32(self.label_num.size)).astype(np.int32)
+        nums = [_parse_int64(v) if v != "" else None for v in values]
+        self.label_num = np.concatenate([self.label_num, np.array([x if x is not None else 0 for x in nums], np.int64)])
+        self.label_num_ok = np.concatenate([self.label_num_ok, np.array([x is not None for x in nums], np.uint8)])
+        self.labels = np.concatenate([self.labels.reshape(-1, self.n_nodes), row]).astype(np.uint32)
+        self.label_keys = self.label_keys + [key]
+        self.label_values = self.label_values + [values]
+        return len(self.label_keys) - 1
 
     def value_id(self, col: int, value: str) -> int:
         if col < 0:
@@ -292,19 +326,24 @@ def _parse_int64(s: str) -> Optional[int]:
 def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
                    extra_scalar: Sequence[str] = (),
                    namespaces: Optional[Dict[str, Dict[str, str]]] = None,
-                   nb_args: Optional[netbw.NetworkBandwidthArgs] = None) -> Tuple[EncodedCluster, List[int]]:
+                   nb_args: Optional[netbw.NetworkBandwidthArgs] = None,
+                   scalar_order: Sequence[str] = (), classes_from: Optional[TopologyIndex] = None) \
+        -> Tuple[EncodedCluster, List[int]]:
     """Encode nodes in nodeTree order.  Returns (cluster, order) where
     order[position] = index into ``nodes``.  ``bound_pods`` (spec.nodeName set)
     are added to their node's aggregates like NodeInfo.AddPod (and to the
     PodTopologySpread / InterPodAffinity count classes).  ``namespaces`` maps
-    namespace name -> labels (for namespaceSelector terms)."""
+    namespace name -> labels (for namespaceSelector terms).  ``scalar_order``:
+    scalar columns to place first, in this order, and ``classes_from``: a
+    snapshot's TopologyIndex whose count classes are registered first (a re-encoded snapshot keeps the columns and
+    class ids of the one it replaces, ksim.ingest.NodeCache)."""
     order = node_tree_order([zone_key(n.labels) for n in nodes])
     ns = [nodes[i] for i in order]
     N = len(ns)
     if N > abi.MAX_NODES:
         raise EncodeError("too many nodes")
     # scalar resources: every non-native allocatable / requested name
-    scalar: List[str] = []
+    scalar: List[str] = list(scalar_order)
     for n in ns:
         for k in n.allocatable:
             if k not in _NATIVE and k not in scalar:
@@ -315,34 +354,13 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
     if len(scalar) > abi.MAX_SCALAR:
         raise EncodeError("too many scalar resources")
     S = len(scalar)
-    # label columns
+    # label columns are created on first reference (EncodedCluster.label_col)
     keys: List[str] = []
-    for n in ns:
-        for k in n.labels:
-            if k not in keys:
-                keys.append(k)
-    if len(keys) > abi.MAX_LABEL_COLS:
-        raise EncodeError("too many label keys")
-    values: List[List[str]] = [[""] for _ in keys]
-    vindex: List[Dict[str, int]] = [{} for _ in keys]
-    labels = np.zeros((max(len(keys), 0), N), np.uint32)
-    for pos, n in enumerate(ns):
-        for k, v in n.labels.items():
-            c = keys.index(k)
-            vid = vindex[c].get(v)
-            if vid is None:
-                vid = len(values[c])
-                values[c].append(v)
-                vindex[c][v] = vid
-            labels[c, pos] = vid
-    offs = np.zeros(len(keys), np.int32)
-    nums, oks = [], []
-    for c in range(len(keys)):
-        offs[c] = len(nums)
-        for v in values[c]:
-            pv = _parse_int64(v) if v != "" else None
-            nums.append(pv if pv is not None else 0)
-            oks.append(1 if pv is not None else 0)
+    values: List[List[str]] = []
+    labels = np.zeros((0, N), np.uint32)
+    offs = np.zeros(0, np.int32)
+    nums: List[int] = []
+    oks: List[int] = []
     # taints
     tvocab: List[Taint] = [None]  # type: ignore[list-item]
     tindex: Dict[Tuple[str, str, str], int] = {}
@@ -391,10 +409,13 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
         node_names=[n.name for n in ns], label_keys=keys, label_values=values,
         taint_vocab=tvocab, scalar_names=scalar,
         nb_limit=nb_limit, nb_alloc=np.zeros(N, np.int64), nb_args=nb_args,
+        node_labels=[dict(n.labels) for n in ns],
     )
     c.topo = TopologyIndex(N, namespaces)
     pos_of = {name: i for i, name in enumerate(c.node_names)}
     c.topo.set_images(nodes, pos_of)                 # input order = the order nodes were added
+    if classes_from is not None:
+        c.topo.preregister(classes_from)
     for p in bound_pods:
         if p.node_name in pos_of:
             c.topo.carried_terms(p)          # classes of every carried term exist first

@@ -14,7 +14,10 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libksim_engine.so")
+# KSIM_LIB_VARIANT=<tag> loads an A/B build of the batch geometry
+# (csrc/Makefile "variant": libksim_engine_<tag>.so); the default is the product build.
+_VARIANT = os.environ.get("KSIM_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, f"libksim_engine_{_VARIANT}.so" if _VARIANT else "libksim_engine.so")
 _LIB = None
 
 # Exported symbols declared in include/ksim_engine.h (checked by tests).
@@ -26,7 +29,7 @@ EXPORTS = [
     "ksim_time_kernels", "ksim_kernel_name", "ksim_time_eval", "ksim_get_diag", "ksim_batch_geometry",
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
-    "ksim_set_bound_pods", "ksim_preempt",
+    "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
 ]
 
 
@@ -54,6 +57,8 @@ def lib():
         L.ksim_last_error.restype = ctypes.c_char_p
         L.ksim_set_profile.argtypes = [vp, vp]
         L.ksim_set_cluster.argtypes = [vp, vp, vp]
+        L.ksim_upsert_nodes.argtypes = [vp, vp, vp, vp]
+        L.ksim_remove_node.argtypes = [vp, i32]
         L.ksim_get_node_state.argtypes = [vp] * 7
         L.ksim_get_class_count.argtypes = [vp, vp]
         L.ksim_get_nb_alloc.argtypes = [vp, vp]
@@ -130,6 +135,8 @@ class Engine:
         self.n_nodes = 0
         self.n_score = 0
         self._keep = []
+        self.cluster = None
+        self._ran = False
 
     def _chk(self, rc: int):
         if rc != 0:
@@ -157,8 +164,46 @@ class Engine:
     def set_cluster(self, cluster):
         nt, vo = cluster.node_table(), cluster.vocab()
         self._chk(lib().ksim_set_cluster(self.h, ctypes.byref(nt), ctypes.byref(vo)))
+        self._track(cluster, nt)
+        self._ran = False
+
+    def _track(self, cluster, nt):
+        self.cluster = cluster
         self.n_nodes = cluster.n_nodes
         self.n_classes = nt.n_classes
+        self._layout = (cluster.n_label_cols, int(nt.n_classes))
+
+    def upsert_nodes(self, cluster, old_pos):
+        """Node informer deltas (ksim_upsert_nodes): ``cluster`` is the new
+        snapshot, old_pos[i] the current position of its node i or -1."""
+        nt, vo = cluster.node_table(), cluster.vocab()
+        op = np.ascontiguousarray(old_pos, np.int32)
+        if op.size != cluster.n_nodes:
+            raise ValueError("old_pos must have one entry per node of the new snapshot")
+        self._chk(lib().ksim_upsert_nodes(self.h, ctypes.byref(nt), ctypes.byref(vo),
+                                          op.ctypes.data_as(ctypes.c_void_p)))
+        self._track(cluster, nt)
+        self._keep = []
+
+    def remove_node(self, pos: int):
+        """RemoveNode of the node at ``pos`` (ksim_remove_node); the host
+        snapshot object is no longer the engine's (positions moved)."""
+        self._chk(lib().ksim_remove_node(self.h, pos))
+        self.n_nodes -= 1
+        self.cluster = None
+        self._keep = []
+
+    def _sync(self):
+        """Pods encoded after set_cluster may have added label columns (keys a
+        pod references get one on first use) or count classes to the host
+        snapshot: re-send it in place (every node kept)."""
+        c = getattr(self, "cluster", None)
+        if c is None or (c.n_label_cols, int(c.class_count.shape[0])) == self._layout:
+            return
+        if int(c.class_count.shape[0]) != self._layout[1] and self._ran:
+            raise RuntimeError("count classes were registered after cycles ran on this engine: "
+                               "encode every pod before scheduling, or re-send the snapshot (upsert_nodes)")
+        self.upsert_nodes(c, np.arange(c.n_nodes, dtype=np.int32))
 
     def class_count(self) -> np.ndarray:
         """Count classes [n_classes][n_nodes] as the device holds them now."""
@@ -173,6 +218,8 @@ class Engine:
         return out
 
     def eval_pod(self, pods, index: int) -> dict:
+        self._sync()
+        self._ran = True
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
         ps = pods.pod_set()
         self._chk(lib().ksim_eval_pod(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
@@ -182,6 +229,8 @@ class Engine:
         """A compat cycle around an extender round trip: ``extender(filter
         result) -> (ext_fail[n] or None, ext_score[n] or None)`` sees the filter
         pass (kept nodes: fail_plugin == PASSED)."""
+        self._sync()
+        self._ran = True
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
         ps = pods.pod_set()
         self._chk(lib().ksim_eval_pod_filter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
@@ -202,20 +251,27 @@ class Engine:
     def preempt(self, pods, index: int, priority: int) -> tuple:
         """DefaultPreemption PostFilter dry run: (nominated node or -1, victim
         indices into the bound-pod table, potential nodes, candidates)."""
+        self._sync()
+        self._ran = True
         out = abi.PreemptOut(max(getattr(self, "_bound_n", 1), 1))
         ps = pods.pod_set()
         self._chk(lib().ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
         return out.result()
 
     def assume(self, pods, index: int, node: int):
+        self._sync()
+        self._ran = True
         ps = pods.pod_set()
         self._chk(lib().ksim_assume(self.h, ctypes.byref(ps), index, node))
 
     def forget(self, pods, index: int, node: int):
+        self._sync()
+        self._ran = True
         ps = pods.pod_set()
         self._chk(lib().ksim_forget(self.h, ctypes.byref(ps), index, node))
 
     def load_pods(self, pods):
+        self._sync()
         ps = pods.pod_set()
         self._chk(lib().ksim_load_pods(self.h, ctypes.byref(ps)))
         self._keep = [pods]
@@ -223,6 +279,7 @@ class Engine:
     def schedule_loaded(self, first: int, count: int, want_chosen: bool = True):
         chosen = np.zeros(count, np.int32) if want_chosen else None
         st = abi.BatchStats()
+        self._ran = True
         self._chk(lib().ksim_schedule_loaded(
             self.h, first, count, chosen.ctypes.data_as(ctypes.c_void_p) if chosen is not None else None,
             ctypes.byref(st)))

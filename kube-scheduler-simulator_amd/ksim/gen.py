@@ -395,3 +395,97 @@ def edge_objects(n_pods: int = 160, seed: int = SEEDS[1] ^ 0xED6E) -> Tuple[List
             p.init_containers = [Container({"cpu": cpus[r.below(len(cpus))], "memory": mems[r.below(len(mems))]})]
         pending.append(p)
     return nodes, bound, pending
+
+
+def delta_objects(n_nodes: int = 240, n_pods: int = 720, n_keys: int = 60, seed: int = SEEDS[1] ^ 0xDE17A):
+    """A cluster for node informer deltas (ksim.ingest.NodeCache): nodes carry
+    ``n_keys`` label keys (example.com/k00.., three values, each present on 80 %
+    of the nodes) plus hostname / zone (4 zones) and hugepages-2Mi / -1Gi
+    allocatable; bound pods; pending pods with node selectors, required and
+    preferred terms over those keys, hugepages requests, a zone spread and a
+    hostname anti-affinity on their app.  Returns (nodes, bound, pending,
+    deltas) with deltas = (added nodes, updated nodes, removed names): added
+    nodes carry a new label key and a new scalar resource, updates change
+    label values and (for some) the zone, removals hit nodes holding pods."""
+    from .model import LabelSelector, PodAffinityTerm, TopologySpreadConstraint
+    r = Rng(seed)
+    keys = [f"example.com/k{j:02d}" for j in range(n_keys)]
+
+    def node(name, zone):
+        labels = {"kubernetes.io/hostname": name, "topology.kubernetes.io/zone": f"z{zone}"}
+        for k in keys:
+            if r.chance(80):
+                labels[k] = f"v{r.below(3)}"
+        alloc = {"cpu": str([8, 16, 32][r.below(3)]), "memory": f"{[32, 64, 128][r.below(3)]}Gi", "pods": "110"}
+        if r.chance(50):
+            alloc["hugepages-2Mi"] = f"{1 + r.below(4)}Gi"
+        if r.chance(25):
+            alloc["hugepages-1Gi"] = f"{2 + r.below(3)}Gi"
+        return Node(name, labels, [], alloc)
+
+    nodes = [node(f"dn-{i:05d}", i % 4) for i in range(n_nodes)]
+
+    def pod(name):
+        app = f"app{r.below(12)}"
+        req = {"cpu": f"{100 * (1 + r.below(20))}m", "memory": f"{256 * (1 + r.below(16))}Mi"}
+        if r.chance(30):
+            req["hugepages-2Mi"] = f"{256 * (1 + r.below(4))}Mi"
+        if r.chance(10):
+            req["hugepages-1Gi"] = "1Gi"
+        p = Pod(name, labels={"app": app}, containers=[Container(req)])
+        if r.chance(40):
+            p.node_selector = {keys[r.below(n_keys)]: f"v{r.below(3)}" for _ in range(1 + r.below(2))}
+        if r.chance(20):
+            k = keys[r.below(n_keys)]
+            op = ["In", "NotIn", "Exists", "DoesNotExist"][r.below(4)]
+            vals = [f"v{r.below(3)}"] if op in ("In", "NotIn") else []
+            p.required_terms = [NodeSelectorTerm([Requirement(k, op, vals)])]
+        if r.chance(25):
+            p.preferred_terms = [PreferredTerm(1 + r.below(100), NodeSelectorTerm(
+                [Requirement(keys[r.below(n_keys)], "In", [f"v{r.below(3)}"])]))]
+        if r.chance(25):
+            p.topology_spread = [TopologySpreadConstraint(2, "topology.kubernetes.io/zone", "DoNotSchedule",
+                                                          LabelSelector({"app": app}))]
+        if r.chance(15):
+            p.pod_anti_affinity_required = [PodAffinityTerm("kubernetes.io/hostname", LabelSelector({"app": app}))]
+        return p
+
+    bound = []
+    for j in range(n_nodes // 2):
+        p = pod(f"bound-{j:05d}")
+        p.node_selector, p.required_terms, p.topology_spread = {}, None, []
+        p.node_name = nodes[r.below(n_nodes)].name
+        bound.append(p)
+    pending = [pod(f"dpod-{j:05d}") for j in range(n_pods)]
+
+    added = []
+    for i in range(n_nodes // 10):
+        n = node(f"dn-new-{i:04d}", r.below(5))                       # a fifth zone appears
+        n.labels["example.com/new"] = f"v{r.below(2)}"
+        if r.chance(50):
+            n.allocatable["example.com/fpga"] = "2"
+        added.append(n)
+    updated = []
+    for i in r_sample(r, n_nodes, n_nodes // 20):
+        old = nodes[i]
+        labels = dict(old.labels)
+        for k in keys[:8]:
+            labels[k] = f"v{r.below(3)}"
+        if i % 3 == 0:
+            labels["topology.kubernetes.io/zone"] = f"z{(int(labels['topology.kubernetes.io/zone'][1:]) + 1) % 4}"
+        updated.append(Node(old.name, labels, list(old.taints), dict(old.allocatable)))
+    held = sorted({p.node_name for p in bound})
+    removed = [held[r.below(len(held))] for _ in range(n_nodes // 40)]
+    removed += [nodes[r.below(n_nodes)].name for _ in range(n_nodes // 40)]
+    removed = sorted(set(removed) - {n.name for n in updated})
+    return nodes, bound, pending, (added, updated, removed)
+
+
+def r_sample(r: Rng, n: int, k: int) -> List[int]:
+    """k distinct indices below n from the stream r."""
+    out: List[int] = []
+    while len(out) < min(k, n):
+        x = r.below(n)
+        if x not in out:
+            out.append(x)
+    return out

@@ -25,7 +25,9 @@ out of the queue (the engine's volume filters only cover pods without them).
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
 
 from . import profile as prof_mod
 from .model import Node, Pod, node_from_dict, pod_from_dict
@@ -158,3 +160,72 @@ def encode(snap: Snapshot, profile_index: int = 0):
     cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces, nb_args=sp.network_bandwidth)
     pods = encode_pods(cluster, snap.pending)
     return cluster, pods, prof_mod.compile_profile(sp, cluster.scalar_names)
+
+
+# ---- node informer deltas ---------------------------------------------------------------
+class NodeCache:
+    """The node side of the scheduler cache between snapshots ([upstream]
+    pkg/scheduler/internal/cache/cache.go AddNode / UpdateNode / RemoveNode and
+    node_tree.go; the simulator drives them from the node informer of its fake
+    cluster).  Nodes are kept in informer add order, which is the nodeTree's
+    insertion order: an update that moves a node to another zone re-adds it
+    (nodeTree.updateNode = removeNode + addNode), a removed node leaves the tree
+    and the pods bound to it leave the snapshot.
+
+    ``commit(pending)`` re-encodes the snapshot (the same scalar columns and
+    count classes first, label columns for the keys the pods reference) and returns it with ``old_pos`` for ksim_upsert_nodes, which
+    replays the engine's binds since the last snapshot on top of it."""
+
+    def __init__(self, nodes: Sequence[Node], bound: Sequence[Pod] = (),
+                 namespaces: Optional[Dict[str, Dict[str, str]]] = None,
+                 nb_args: Optional[NetworkBandwidthArgs] = None, extra_scalar: Sequence[str] = ()):
+        self.nodes: List[Node] = list(nodes)
+        self.bound: List[Pod] = list(bound)
+        self.namespaces = namespaces
+        self.nb_args = nb_args
+        self.extra_scalar = list(extra_scalar)
+        self.cluster = self._encode((), None)
+
+    def _encode(self, scalar_order, classes_from):
+        from .encode import encode_cluster
+        c, _ = encode_cluster(self.nodes, self.bound, extra_scalar=self.extra_scalar,
+                              namespaces=self.namespaces, nb_args=self.nb_args, scalar_order=scalar_order,
+                              classes_from=classes_from)
+        return c
+
+    def _index(self, name: str) -> int:
+        for i, n in enumerate(self.nodes):
+            if n.name == name:
+                return i
+        raise KeyError(f"node {name!r} not in the cache")
+
+    def add_node(self, node: Node) -> None:
+        if any(n.name == node.name for n in self.nodes):
+            raise ValueError(f"node {node.name!r} already in the cache")
+        self.nodes.append(node)
+
+    def update_node(self, node: Node) -> None:
+        from .encode import zone_key
+        i = self._index(node.name)
+        if zone_key(self.nodes[i].labels) != zone_key(node.labels):
+            del self.nodes[i]
+            self.nodes.append(node)
+        else:
+            self.nodes[i] = node
+
+    def remove_node(self, name: str) -> None:
+        del self.nodes[self._index(name)]
+
+    def commit(self, pending: Sequence[Pod]):
+        """(new EncodedCluster, old_pos, EncodedPods of ``pending``, encoded
+        against the new snapshot; pass the queue still to run)."""
+        from .encode import EncodeError, encode_pods
+        old = self.cluster
+        new = self._encode(old.scalar_names, old.topo)
+        pods = encode_pods(new, pending)
+        if new.topo.keys[:len(old.topo.keys)] != old.topo.keys:
+            raise EncodeError("count classes changed ids across the node delta")
+        pos = {name: i for i, name in enumerate(old.node_names)}
+        old_pos = np.array([pos.get(name, -1) for name in new.node_names], np.int32)
+        self.cluster = new
+        return new, old_pos, pods

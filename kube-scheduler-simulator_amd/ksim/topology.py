@@ -205,6 +205,9 @@ class TopologyIndex:
         names = tuple(normalized_image_name(c.image) for c in pod.containers)
         if not any(nm in self.images for nm in names):
             return None                                  # 0 on every node: no use needed
+        return self._image_class(names)
+
+    def _image_class(self, names: tuple) -> int:
         key = ("image", names)
         cid = self.ids.get(key)
         if cid is not None:
@@ -221,6 +224,22 @@ class TopologyIndex:
         s = np.minimum(np.maximum(total, IMAGE_MIN_THRESHOLD), max_t)
         score = (100 * (s - IMAGE_MIN_THRESHOLD)) // (max_t - IMAGE_MIN_THRESHOLD)
         return self._new_class(key, score.astype(np.int32))
+
+    def preregister(self, src: "TopologyIndex") -> None:
+        """Register the classes of ``src``, in order, before any bound pod is
+        added (a re-encoded snapshot keeps the class ids of the one it
+        replaces, ksim.ingest.NodeCache); the bound pods then count into them."""
+        for k, v in src.selectors.items():
+            self.selectors.setdefault(k, v)
+        for key in src.keys:
+            if key[0] == "carry":
+                self.carried_class(key[1], key[2], key[3])
+            elif key[0] == "sel":
+                self.selector_class(key[1])
+            elif key[0] == "port":
+                self.port_class(*key[1:])
+            else:
+                self._image_class(key[1])
 
     def port_adds(self, pod: Pod) -> Dict[int, int]:
         """NodeInfo.AddPod -> UsedPorts.Add of each host port, on the registered classes."""

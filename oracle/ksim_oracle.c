@@ -54,6 +54,9 @@ struct ksim_oracle {
   int32_t vmax;
   /* NetworkBandwidth: node limit (static) and allocated amount (dynamic), milli-units */
   int64_t *nb_limit, *nb_alloc;
+  /* the dynamic columns as given at create / upsert (ksim_oracle_upsert_nodes) */
+  int64_t *s_req_cpu, *s_req_mem, *s_req_eph, *s_req_scalar, *s_nz_cpu, *s_nz_mem, *s_nb_alloc;
+  int32_t *s_num_pods, *s_cnt;
   /* scheduler state */
   int32_t next_start;   /* sched.nextStartNodeIndex */
   int64_t pod_seq;      /* tie-break sequence */
@@ -125,6 +128,15 @@ ksim_oracle* ksim_oracle_create(const ksim_node_table* t, const ksim_vocab* v,
   o->ignored = malloc(n + 1);
   o->nb_limit = dupbuf(t->nb_limit, n * 8);
   o->nb_alloc = dupbuf(t->nb_alloc, n * 8);
+  o->s_req_cpu = dupbuf(o->req_cpu, n * 8);
+  o->s_req_mem = dupbuf(o->req_mem, n * 8);
+  o->s_req_eph = dupbuf(o->req_eph, n * 8);
+  o->s_req_scalar = dupbuf(o->req_scalar, n * 8 * (size_t)t->n_scalar);
+  o->s_nz_cpu = dupbuf(o->nz_cpu, n * 8);
+  o->s_nz_mem = dupbuf(o->nz_mem, n * 8);
+  o->s_nb_alloc = dupbuf(o->nb_alloc, n * 8);
+  o->s_num_pods = dupbuf(o->num_pods, n * 4);
+  o->s_cnt = dupbuf(o->cnt, 4 * n * (size_t)(t->n_classes > 0 ? t->n_classes : 0));
   return o;
 }
 
@@ -135,10 +147,67 @@ void ksim_oracle_destroy(ksim_oracle* o) {
                 o->num_pods, o->flags, o->taints, o->labels, o->taint_effect,
                 o->label_col_offset, o->label_num, o->label_num_ok, o->fail, o->detail,
                 o->flist, o->raw, o->cnt, o->topo_log, o->col_nvals, o->dom, o->present,
-                o->ignored, o->nb_limit, o->nb_alloc};
+                o->ignored, o->nb_limit, o->nb_alloc, o->s_req_cpu, o->s_req_mem, o->s_req_eph,
+                o->s_req_scalar, o->s_nz_cpu, o->s_nz_mem, o->s_nb_alloc, o->s_num_pods, o->s_cnt};
   for (size_t i = 0; i < sizeof(ps) / sizeof(ps[0]); i++) free(ps[i]);
   free(o);
 }
+
+/* Node informer deltas (ksim_engine.h ksim_upsert_nodes): the table is the
+ * new snapshot; on a kept node the binds since the last snapshot (live -
+ * snapshot at old_pos) are replayed on top of it for the scalar columns /
+ * classes the oracle already has.  nextStartNodeIndex mod the new node count,
+ * the pod sequence carries over. */
+#define REPLAY(T, out, live, snap, tab, rows, rows0)                                    \
+  do {                                                                                 \
+    out = (T*)malloc(sizeof(T) * n * (size_t)(rows) + sizeof(T));                      \
+    for (int k = 0; k < (rows); k++)                                                   \
+      for (size_t i = 0; i < n; i++) {                                                 \
+        T x = (tab) ? (tab)[k * n + i] : 0;                                            \
+        if (k < (rows0) && old_pos[i] >= 0)                                            \
+          x += (live)[k * n0 + (size_t)old_pos[i]] - (snap)[k * n0 + (size_t)old_pos[i]]; \
+        out[k * n + i] = x;                                                            \
+      }                                                                                \
+  } while (0)
+
+int ksim_oracle_upsert_nodes(ksim_oracle* o, const ksim_node_table* t, const ksim_vocab* v,
+                             const int32_t* old_pos) {
+  if (!o || !t || !v || t->n_nodes < 0 || t->n_nodes > KSIM_MAX_NODES) return -1;
+  if (t->n_scalar < o->n_scalar || t->n_classes < o->n_classes || (t->n_nodes > 0 && !old_pos)) return -1;
+  const size_t n = (size_t)t->n_nodes, n0 = (size_t)o->n;
+  for (size_t i = 0; i < n; i++)
+    if (old_pos[i] < -1 || old_pos[i] >= o->n) return -1;
+  ksim_oracle* q = ksim_oracle_create(t, v, &o->prof);     /* snapshot = the table */
+  if (!q) return -1;
+  int64_t *rc, *rm, *re, *zc, *zm, *nb, *rs;
+  int32_t *np, *cnt;
+  REPLAY(int64_t, rc, o->req_cpu, o->s_req_cpu, t->req_cpu, 1, 1);
+  REPLAY(int64_t, rm, o->req_mem, o->s_req_mem, t->req_mem, 1, 1);
+  REPLAY(int64_t, re, o->req_eph, o->s_req_eph, t->req_eph, 1, 1);
+  REPLAY(int64_t, zc, o->nz_cpu, o->s_nz_cpu, t->nz_cpu, 1, 1);
+  REPLAY(int64_t, zm, o->nz_mem, o->s_nz_mem, t->nz_mem, 1, 1);
+  REPLAY(int64_t, nb, o->nb_alloc, o->s_nb_alloc, t->nb_alloc, 1, 1);
+  REPLAY(int64_t, rs, o->req_scalar, o->s_req_scalar, t->req_scalar, t->n_scalar, o->n_scalar);
+  REPLAY(int32_t, np, o->num_pods, o->s_num_pods, t->num_pods, 1, 1);
+  REPLAY(int32_t, cnt, o->cnt, o->s_cnt, t->class_count, t->n_classes, o->n_classes);
+  free(q->req_cpu); q->req_cpu = rc;
+  free(q->req_mem); q->req_mem = rm;
+  free(q->req_eph); q->req_eph = re;
+  free(q->nz_cpu); q->nz_cpu = zc;
+  free(q->nz_mem); q->nz_mem = zm;
+  free(q->nb_alloc); q->nb_alloc = nb;
+  free(q->req_scalar); q->req_scalar = rs;
+  free(q->num_pods); q->num_pods = np;
+  free(q->cnt); q->cnt = cnt;
+  q->next_start = n > 0 ? o->next_start % (int32_t)n : 0;
+  q->pod_seq = o->pod_seq;
+  ksim_oracle swap = *o;
+  *o = *q;
+  *q = swap;
+  ksim_oracle_destroy(q);
+  return 0;
+}
+#undef REPLAY
 
 /* ---- tie-break TB(seed), SURVEY §8(b) "Determinism modes" ---------------- */
 static uint64_t splitmix64(uint64_t x) {

@@ -28,6 +28,9 @@ typedef struct ksim_oracle ksim_oracle;
 ksim_oracle* ksim_oracle_create(const ksim_node_table* nodes, const ksim_vocab* vocab,
                                 const ksim_profile* profile);
 void ksim_oracle_destroy(ksim_oracle* o);
+/* ksim_engine.h ksim_upsert_nodes on the oracle's snapshot (0 on success). */
+int ksim_oracle_upsert_nodes(ksim_oracle* o, const ksim_node_table* t, const ksim_vocab* v,
+                             const int32_t* old_pos);
 
 /* One scheduling cycle with full per-node outputs, sequential semantics
  * (parallelism 1), then assume/bind of the chosen node. */

@@ -25,6 +25,7 @@ def lib():
         L.ksim_oracle_create.restype = vp
         L.ksim_oracle_create.argtypes = [vp, vp, vp]
         L.ksim_oracle_destroy.argtypes = [vp]
+        L.ksim_oracle_upsert_nodes.argtypes = [vp, vp, vp, vp]
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_cycle_ext.argtypes = [vp, vp, i32, vp, vp, vp]
         L.ksim_oracle_preempt.argtypes = [vp, vp, i32, i32, vp, vp]
@@ -63,6 +64,30 @@ class Oracle:
                                           ctypes.byref(profile))
         if not self.h:
             raise RuntimeError("ksim_oracle_create failed")
+        self._layout = (cluster.n_label_cols, int(cluster.class_count.shape[0]))
+        self._ran = False
+
+    def upsert_nodes(self, cluster, old_pos):
+        """ksim_engine.h ksim_upsert_nodes on the oracle (node informer deltas)."""
+        nt, vo = cluster.node_table(), cluster.vocab()
+        op = np.ascontiguousarray(old_pos, np.int32)
+        assert op.size == cluster.n_nodes
+        if lib().ksim_oracle_upsert_nodes(self.h, ctypes.byref(nt), ctypes.byref(vo),
+                                          op.ctypes.data_as(ctypes.c_void_p)) != 0:
+            raise RuntimeError("ksim_oracle_upsert_nodes failed")
+        self.cluster = cluster
+        self._keep = (cluster, self.profile)
+        self._layout = (cluster.n_label_cols, int(cluster.class_count.shape[0]))
+
+    def _sync(self):
+        """As ksim.engine.Engine._sync: label columns / classes added by pods
+        encoded after the oracle was made are re-sent in place."""
+        c = self.cluster
+        if (c.n_label_cols, int(c.class_count.shape[0])) == self._layout:
+            return
+        if int(c.class_count.shape[0]) != self._layout[1] and self._ran:
+            raise RuntimeError("count classes registered after cycles ran on this oracle")
+        self.upsert_nodes(c, np.arange(c.n_nodes, dtype=np.int32))
 
     def close(self):
         if self.h:
@@ -73,6 +98,8 @@ class Oracle:
 
     def cycle(self, pods, index: int, ext_fail=None, ext_score=None) -> dict:
         """One compat cycle; ext_fail / ext_score (per node) model the extenders."""
+        self._sync()
+        self._ran = True
         from ksim import abi
         buf = abi.EvalBuffers(self.cluster.n_nodes, self.profile.n_score)
         ps = pods.pod_set()
@@ -89,6 +116,8 @@ class Oracle:
     def preempt(self, pods, index: int, priority: int, bound) -> tuple:
         """DefaultPreemption PostFilter (ksim_oracle_preempt).  ``bound`` is a
         ksim.abi.BoundPods.  Returns (nominated node position or -1, victim indices)."""
+        self._sync()
+        self._ran = True
         from ksim import abi
         out = abi.PreemptOut(max(bound.n, 1))
         ps = pods.pod_set()
@@ -99,6 +128,8 @@ class Oracle:
         return out.result()
 
     def schedule(self, pods, first=0, count=None, nthreads=1):
+        self._sync()
+        self._ran = True
         from ksim import abi
         count = pods.n_pods - first if count is None else count
         chosen = np.zeros(count, np.int32)

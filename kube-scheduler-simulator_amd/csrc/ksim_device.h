@@ -50,10 +50,13 @@ struct DevCluster {
   const int64_t* label_num;
   const uint8_t* label_num_ok;
   // PodTopologySpread / InterPodAffinity count classes (ksim_engine.h "Count classes")
-  int32_t n_classes, n_topo_log, vmax, _pad2;
+  int32_t n_classes, n_topo_log, vmax;
+  uint32_t cflags;               // kCluster*: facts the per-pod filter plan uses
   int32_t* cnt;                  // [n_classes][n], updated by every bind
   const double* topo_log;        // [n_topo_log] = log(size + 2), host-computed
   const int32_t* col_nvals;      // [n_label_cols] value ids per column (domain table sizes)
+  const uint8_t* col_unique;     // [n_label_cols] every value on at most one node (e.g. hostname);
+                                 // all zero on shard handles
   // NetworkBandwidth (milli-units): the node-limit annotation and the bound
   // pods' request annotations (getNodeAllocatedAmount), updated by every bind
   const int64_t* nb_limit;
@@ -64,6 +67,13 @@ struct DevCluster {
   const double* inv_mem;
 };
 
+// DevCluster.cflags
+constexpr uint32_t kClusterUnschedulable = 1u;   // some node has spec.unschedulable
+constexpr uint32_t kClusterHardTaints = 2u;      // some node has a NoSchedule / NoExecute taint
+constexpr uint32_t kClusterPreferTaints = 4u;    // some node has a PreferNoSchedule taint
+
+struct PodPlan;
+
 struct DevPods {
   const ksim_pod* pods;
   const ksim_label_expr* exprs;
@@ -72,6 +82,7 @@ struct DevPods {
   const int32_t* bflags;         // [n_pods] batch path: kBatch* flags
   const ksim_topo_use* uses;
   const ksim_class_add* adds;
+  const PodPlan* plans;          // [n_pods] per-pod cycle plans (host-compiled, see PodPlan)
   int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, _pad[2];
 };
 
@@ -531,10 +542,9 @@ __device__ __forceinline__ int64_t fit_least_allocated_score(const NodeRow& r, c
                                                     int n_scalar) {
   int64_t node_score = 0, weight_sum = 0;
 #pragma unroll
-  for (int i = 0; i < KSIM_MAX_RES; i++) {
-    if (i >= prof.fit_n_res) break;
-    int64_t a, q;
-    calc_alloc_req(r, p, prof.fit_res[i], false, n_scalar, a, q);
+  for (int i = 0; i < KSIM_MAX_RES; i++) {      // constant indices only (no exit): prof stays in registers
+    int64_t a = 0, q = 0;
+    if (i < prof.fit_n_res) calc_alloc_req(r, p, prof.fit_res[i], false, n_scalar, a, q);
     if (a == 0) continue;
     node_score += least_requested_score(q, a) * prof.fit_res_weight[i];
     weight_sum += prof.fit_res_weight[i];
@@ -554,9 +564,8 @@ __device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, c
   double total = 0, f0 = 0, f1 = 0;
 #pragma unroll
   for (int i = 0; i < KSIM_MAX_RES; i++) {
-    if (i >= prof.ba_n_res) break;
-    int64_t a, q;
-    calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
+    int64_t a = 0, q = 0;
+    if (i < prof.ba_n_res) calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
     if (a == 0) continue;
     double f = (double)q / (double)a;
     if (f > 1) f = 1;
@@ -573,9 +582,8 @@ __device__ __forceinline__ int64_t balanced_allocation_score(const NodeRow& r, c
     double sum = 0;
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_RES; i++) {
-      if (i >= prof.ba_n_res) break;
-      int64_t a, q;
-      calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
+      int64_t a = 0, q = 0;
+      if (i < prof.ba_n_res) calc_alloc_req(r, p, prof.ba_res[i], true, n_scalar, a, q);
       if (a == 0) continue;
       double f = (double)q / (double)a;
       if (f > 1) f = 1;
@@ -598,6 +606,31 @@ constexpr int32_t kCycleErrorPrefilter = 3; // PreFilterResult names a node the 
 
 __host__ __device__ __forceinline__ bool nb_error_detail(uint32_t d) { return d >= KSIM_NB_NO_LIMIT; }
 __host__ __device__ __forceinline__ bool fail_is_error(uint8_t f) { return (f & kFailError) && f < KSIM_FAIL_EXTENDER; }
+// Profile arrays at a runtime (uniform) index, extracted from packed words by
+// shifts: a runtime index into the by-value kernel argument would compile to a
+// select chain over every element at each access.
+__device__ __forceinline__ uint32_t prof_filter(const ksim_profile& prof, int f) {
+  uint64_t w0, w1;
+  memcpy(&w0, prof.filter, 8);
+  memcpy(&w1, prof.filter + 8, 8);
+  return (uint32_t)(((f < 8 ? w0 : w1) >> (8 * (f & 7))) & 0xffu);
+}
+__device__ __forceinline__ uint32_t prof_score(const ksim_profile& prof, int k) {
+  static_assert(KSIM_MAX_SCORE == 8 && KSIM_MAX_FILTER == 16, "packed profile words");
+  uint64_t w;
+  memcpy(&w, prof.score, 8);
+  return (uint32_t)((w >> (8 * k)) & 0xffu);
+}
+// score_weight[k], 0 read as 1 (the framework's default weight)
+__device__ __forceinline__ int64_t prof_weight(const ksim_profile& prof, int k) {
+  uint64_t w[4];
+  memcpy(w, prof.score_weight, 32);
+  const int q = k >> 1;
+  const uint64_t x = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+  const int32_t v = (int32_t)(uint32_t)(x >> (32 * (k & 1)));
+  return v == 0 ? 1 : v;
+}
+
 __host__ __device__ __forceinline__ bool prof_has_filter(const ksim_profile& prof, int plugin) {
   for (int f = 0; f < prof.n_filter; f++)
     if (prof.filter[f] == plugin) return true;
@@ -632,26 +665,86 @@ __host__ __device__ __forceinline__ bool nb_score_error(uint32_t flags) {
   return !(flags & KSIM_NODE_NB_LIMIT) || (flags & KSIM_NODE_NB_LIMIT_BAD);
 }
 
-// frameworkImpl.RunFilterPlugins (stop at first failure)
-struct DevScratch;
-__device__ __forceinline__ uint32_t pts_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                               const ksim_pod& p, int32_t node);
-__device__ __forceinline__ uint32_t ipa_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                               const ksim_pod& p, uint32_t topo_flags, int32_t node);
-__device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                             const ksim_profile& prof, const ksim_pod& p, int32_t node);
-__device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const DevPods& P, const ksim_pod& p,
-                                                   int32_t node);
-__device__ __forceinline__ int64_t image_locality_score(const DevCluster& c, const DevPods& P, const ksim_pod& p,
-                                                        int32_t node);
+// ---- PodTopologySpread / InterPodAffinity / NodePorts / ImageLocality inputs --
+// Internal use flag, set only when a pod's uses are staged on the device (never
+// in the ABI): the use's key column is unique per node (DevCluster.col_unique),
+// so an InterPodAffinity domain sum is the node's own class count and needs no
+// domain table.
+constexpr uint8_t kUseUniqueCol = 0x80;
 
+// The use's per-node number is the node's own class count (no domain table):
+// PodTopologySpread ScheduleAnyway on hostname (upstream counts the node's
+// pods), NodePorts, ImageLocality, and InterPodAffinity on a unique column.
+__host__ __device__ __forceinline__ bool use_node_count(const ksim_topo_use& u) {
+  return (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME)) || u.kind == KSIM_USE_NODE_PORT ||
+         u.kind == KSIM_USE_IMAGE ||
+         ((u.flags & kUseUniqueCol) && u.kind >= KSIM_USE_IPA_EXISTING_ANTI && u.kind <= KSIM_USE_IPA_SCORE_HARD);
+}
+
+// A use record as four dwords: one scalar load when its address is
+// block-uniform (a sub-dword field read alone would take the vector memory
+// path).  Layout: cls, arg, col | kind << 16 | flags << 24, pad.
+static_assert(sizeof(ksim_topo_use) == 16, "ksim_topo_use is four dwords");
+__device__ __forceinline__ ksim_topo_use load_use(const ksim_topo_use* U, int i) {
+  const uint4 w = reinterpret_cast<const uint4*>(U)[i];
+  ksim_topo_use u;
+  u.cls = (int32_t)w.x;
+  u.arg = (int32_t)w.y;
+  u.col = (uint16_t)(w.z & 0xffffu);
+  u.kind = (uint8_t)((w.z >> 16) & 0xffu);
+  u.flags = (uint8_t)(w.z >> 24);
+  u._pad = (int32_t)w.w;
+  return u;
+}
+
+// The pod's uses by role, one bit per use (bit i = use i), built once per
+// thread from scalar loads: the per-node code tests uniform bits instead of
+// re-reading each use's kind inside every plugin.
+struct UseMasks {
+  uint32_t hard, soft, soft_val, aff, anti, exist, score, port, image, node_count, self_match;
+};
+
+// Per-pod plan of the per-pod cycle, compiled by the host when a pod set is
+// uploaded (ksim_load_pods and the single-pod calls; a queue is uploaded again
+// after every ksim_set_profile / ksim_set_cluster, so the plan may depend on
+// both): the filter plugins that can fail for this pod on this cluster (the
+// rest pass every node), and its topology uses by role.  The kernels read it
+// with scalar loads instead of re-deriving it per node.
+struct PodPlan {
+  uint32_t filter_en;            // plugin ids to evaluate (1 << id), FilterPlan.en
+  uint32_t _pad;
+  UseMasks m;
+};
+
+// One node's inputs of every topology use of the cycle's pod, loaded up front:
+// one round of label loads, then one of domain-table / class-count loads, so
+// the plugins below read registers instead of a dependent load pair per use
+// inside each plugin's loop.
+struct TopoRow {
+  uint32_t v[KSIM_MAX_USES];     // value id of the use's key column on the node (0: key absent)
+  int64_t x[KSIM_MAX_USES];      // domain-table entry of that value, or the node's class count
+};
+
+// frameworkImpl.RunFilterPlugins (stop at first failure)
+__device__ __forceinline__ uint32_t pts_filter(const ksim_topo_use* U, const UseMasks& m, const int64_t* min_match,
+                                               const TopoRow& t);
+__device__ __forceinline__ uint32_t ipa_filter(const UseMasks& m, const ksim_pod& p, uint32_t topo_flags,
+                                               const TopoRow& t);
+__device__ __forceinline__ int64_t ipa_score(const ksim_profile& prof, const ksim_topo_use* U, const UseMasks& m,
+                                             const TopoRow& t);
+__device__ __forceinline__ bool node_port_conflict(const UseMasks& m, const TopoRow& t);
+__device__ __forceinline__ int64_t image_locality_score(const UseMasks& m, const TopoRow& t);
+
+// U / m / t: the pod's uses (p.use_count of them), their masks and the node's TopoRow.
 __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                             const DevScratch& s, uint32_t topo_flags,
-                                             const ksim_pod& p, const NodeRow& r, uint32_t& detail) {
+                                             const int64_t* min_match, uint32_t topo_flags, const ksim_pod& p,
+                                             const NodeRow& r, const ksim_topo_use* U, const UseMasks& m,
+                                             const TopoRow& t, uint32_t& detail) {
   detail = 0;
   const int32_t node = r.node;
+  const int nu = p.use_count;
   for (int f = 0; f < prof.n_filter; f++) {
-    switch (prof.filter[f]) {
+    switch (prof_filter(prof, f)) {
       case KSIM_PL_NODE_UNSCHEDULABLE:
         if ((r.flags & KSIM_NODE_UNSCHEDULABLE) && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE))
           return (uint8_t)f;
@@ -673,15 +766,15 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         break;
       }
       case KSIM_PL_NODE_PORTS:
-        if (p.use_count && node_port_conflict(c, P, p, node)) return (uint8_t)f;
+        if (nu && node_port_conflict(m, t)) return (uint8_t)f;
         break;
       case KSIM_PL_POD_TOPOLOGY_SPREAD: {
-        const uint32_t why = p.use_count ? pts_filter(c, P, s, p, node) : 0;
+        const uint32_t why = nu ? pts_filter(U, m, min_match, t) : 0;
         if (why) { detail = why; return (uint8_t)f; }
         break;
       }
       case KSIM_PL_INTER_POD_AFFINITY: {
-        const uint32_t why = p.use_count ? ipa_filter(c, P, s, p, topo_flags, node) : 0;
+        const uint32_t why = nu ? ipa_filter(m, p, topo_flags, t) : 0;
         if (why) { detail = why; return (uint8_t)f; }
         break;
       }
@@ -702,17 +795,170 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
 
 // PodTopologySpread's raw score needs the feasible list (k_extrema computes it).
 __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
-                                           const DevScratch& s, const ksim_pod& p, int plugin, const NodeRow& r) {
+                                           const ksim_pod& p, int plugin, const NodeRow& r,
+                                           const ksim_topo_use* U, const UseMasks& m, const TopoRow& t) {
   switch (plugin) {
     case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(r, prof, p, c.n_scalar);
     case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(r, prof, p, c.n_scalar);
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
-    case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(c, P, s, prof, p, r.node) : 0;
-    case KSIM_PL_IMAGE_LOCALITY: return p.use_count ? image_locality_score(c, P, p, r.node) : 0;
+    case KSIM_PL_INTER_POD_AFFINITY: return p.use_count ? ipa_score(prof, U, m, t) : 0;
+    case KSIM_PL_IMAGE_LOCALITY: return p.use_count ? image_locality_score(m, t) : 0;
     case KSIM_PL_NETWORK_BANDWIDTH: return nb_score_error(r.flags) ? 0 : nb_score(c, r.node);
     default: return 0;   // PodTopologySpread: k_extrema
   }
+}
+
+// ---- per-pod plans: the filter and score chains as straight-line code --------
+// The per-node chain above is a runtime loop over the profile with a switch per
+// plugin; on CDNA every iteration pays the dispatch branches and the spills
+// around the inlined plugin bodies.  The plans below evaluate, in a fixed order,
+// only the plugins that can matter for this pod on this cluster (uniform bits),
+// then pick the first failure by profile position: the same result, because
+// the filter plugins are pure.
+struct FilterPlan {
+  uint64_t rank_lo, rank_hi;   // profile position of each plugin id, 5 bits each (ids 0..11 | 12..)
+  uint32_t en;                 // plugin ids to evaluate (1 << id)
+};
+
+__device__ __forceinline__ uint32_t plan_rank(const FilterPlan& fp, int pl) {
+  return pl < 12 ? (uint32_t)((fp.rank_lo >> (5 * pl)) & 31u) : (uint32_t)((fp.rank_hi >> (5 * (pl - 12))) & 31u);
+}
+
+// FilterPlan.en for one pod (host, at upload): the profile's filter plugins
+// that can fail for this pod on this cluster.  any_unschedulable / hard_taints:
+// some node has spec.unschedulable / a NoSchedule or NoExecute taint.
+inline uint32_t plan_filter_en(const ksim_profile& prof, const ksim_pod& p, const UseMasks& m, bool any_unschedulable,
+                               bool hard_taints) {
+  uint32_t en = 0;
+  for (int f = 0; f < prof.n_filter; f++) {
+    const int pl = prof.filter[f];
+    bool on = false;
+    switch (pl) {        // a plugin left out here passes every node for this pod
+      case KSIM_PL_NODE_UNSCHEDULABLE:
+        on = any_unschedulable && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE);
+        break;
+      case KSIM_PL_NODE_NAME: on = p.node_name != -1; break;
+      case KSIM_PL_TAINT_TOLERATION: on = hard_taints; break;
+      case KSIM_PL_NODE_AFFINITY: on = p.sel_count > 0 || (p.flags & KSIM_POD_HAS_REQUIRED_AFFINITY); break;
+      case KSIM_PL_NODE_PORTS: on = m.port != 0; break;
+      case KSIM_PL_NODE_RESOURCES_FIT: on = true; break;
+      case KSIM_PL_POD_TOPOLOGY_SPREAD: on = m.hard != 0; break;
+      case KSIM_PL_INTER_POD_AFFINITY: on = (m.aff | m.anti | m.exist) != 0; break;
+      case KSIM_PL_NETWORK_BANDWIDTH: on = true; break;
+      default: break;    // the volume plugins: engine pods carry no volumes
+    }
+    if (on) en |= 1u << pl;
+  }
+  return en;
+}
+
+// The profile's filter positions / score slots per plugin id (host, at
+// ksim_set_profile; BatchProg carries them to the kernels).
+inline void plan_profile(const ksim_profile& prof, uint64_t& rank_lo, uint64_t& rank_hi, uint64_t& slot,
+                         uint32_t& slot_hi) {
+  rank_lo = rank_hi = slot = 0;
+  slot_hi = 0;
+  for (int f = 0; f < prof.n_filter; f++) {
+    const int pl = prof.filter[f];
+    if (pl < 12) rank_lo |= (uint64_t)f << (5 * pl);
+    else rank_hi |= (uint64_t)f << (5 * (pl - 12));
+  }
+  for (int k = 0; k < prof.n_score; k++) {
+    const int pl = prof.score[k];
+    if (pl < 16) slot |= (uint64_t)(k + 1) << (4 * pl);
+    else slot_hi |= (uint32_t)(k + 1) << (4 * (pl - 16));
+  }
+}
+
+// frameworkImpl.RunFilterPlugins over the plan: KSIM_PASSED or the profile
+// position of the first failing plugin (| kFailError for an error status).
+__device__ __forceinline__ uint8_t run_filter_plan(const DevCluster& c, const DevPods& P, const FilterPlan& fp,
+                                                   const int64_t* min_match, uint32_t topo_flags, const ksim_pod& p,
+                                                   const NodeRow& r, const ksim_topo_use* U, const UseMasks& m,
+                                                   const TopoRow& t, uint32_t& detail) {
+  uint32_t best = 0xffu, det = 0;
+  bool err = false;
+  auto take = [&](int pl, bool fails, uint32_t d, bool e) {
+    const uint32_t rk = plan_rank(fp, pl);
+    if (fails && rk < best) {
+      best = rk;
+      det = d;
+      err = e;
+    }
+  };
+  const int32_t node = r.node;
+  if (fp.en & (1u << KSIM_PL_NODE_UNSCHEDULABLE))
+    take(KSIM_PL_NODE_UNSCHEDULABLE, (r.flags & KSIM_NODE_UNSCHEDULABLE) != 0, 0, false);
+  if (fp.en & (1u << KSIM_PL_NODE_NAME)) take(KSIM_PL_NODE_NAME, p.node_name != c.base + node, 0, false);
+  if (fp.en & (1u << KSIM_PL_TAINT_TOLERATION)) {
+    const uint32_t tid = find_matching_untolerated_taint(c, p, r);
+    take(KSIM_PL_TAINT_TOLERATION, tid != 0, tid, false);
+  }
+  if (fp.en & (1u << KSIM_PL_NODE_AFFINITY))
+    take(KSIM_PL_NODE_AFFINITY, !required_node_affinity_match(c, P, p, node), 0, false);
+  if (fp.en & (1u << KSIM_PL_NODE_RESOURCES_FIT)) {
+    const uint32_t bits = fits_request(r, p, c.n_scalar);
+    take(KSIM_PL_NODE_RESOURCES_FIT, bits != 0, bits, false);
+  }
+  if (fp.en & (1u << KSIM_PL_NODE_PORTS)) take(KSIM_PL_NODE_PORTS, node_port_conflict(m, t), 0, false);
+  if (fp.en & (1u << KSIM_PL_POD_TOPOLOGY_SPREAD)) {
+    const uint32_t why = pts_filter(U, m, min_match, t);
+    take(KSIM_PL_POD_TOPOLOGY_SPREAD, why != 0, why, false);
+  }
+  if (fp.en & (1u << KSIM_PL_INTER_POD_AFFINITY)) {
+    const uint32_t why = ipa_filter(m, p, topo_flags, t);
+    take(KSIM_PL_INTER_POD_AFFINITY, why != 0, why, false);
+  }
+  if (fp.en & (1u << KSIM_PL_NETWORK_BANDWIDTH)) {
+    const uint32_t why = nb_filter(c, p, r.flags, node);
+    take(KSIM_PL_NETWORK_BANDWIDTH, why != 0, why, nb_error_detail(why));
+  }
+  detail = best == 0xffu ? 0u : det;
+  return best == 0xffu ? (uint8_t)KSIM_PASSED : (uint8_t)(best | (err ? kFailError : 0));
+}
+
+// The score slots of each plugin id: profile position + 1, 4 bits each (0: absent).
+struct ScorePlan {
+  uint64_t slot;               // plugin ids 0..15
+  uint32_t slot_hi;            // plugin ids 16..
+};
+
+__device__ __forceinline__ int plan_slot(const ScorePlan& sp, int pl) {
+  return pl < 16 ? (int)((sp.slot >> (4 * pl)) & 15u) - 1 : (int)((sp.slot_hi >> (4 * (pl - 16))) & 15u) - 1;
+}
+
+// The score plugins' raw scores of one feasible node (PodTopologySpread's is
+// computed after the filter pass: 0 here), stored per slot into raw
+// ([slot][n]); returns the weighted sum of the slots without NormalizeScore.
+// store_plain: also store the raw score of those slots (compat mode).
+__device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                                  const ScorePlan& sp, const ksim_pod& p, const NodeRow& r,
+                                                  const ksim_topo_use* U, const UseMasks& m, const TopoRow& t,
+                                                  int64_t* raw, bool store_plain) {
+  int64_t part = 0;
+  const size_t n = (size_t)c.n;
+  auto put = [&](int pl, int64_t v) {
+    const int k = plan_slot(sp, pl);
+    if (norm_kind(pl) == kNormNone) {
+      part += v * prof_weight(prof, k);
+      if (store_plain) raw[(size_t)k * n + r.node] = v;
+    } else {
+      raw[(size_t)k * n + r.node] = v;
+    }
+  };
+#define KSIM_PUT(pl, expr) \
+  if (plan_slot(sp, pl) >= 0) put(pl, expr)
+  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, fit_least_allocated_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, balanced_allocation_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_TAINT_TOLERATION, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
+  KSIM_PUT(KSIM_PL_NODE_AFFINITY, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
+  KSIM_PUT(KSIM_PL_INTER_POD_AFFINITY, m.score ? ipa_score(prof, U, m, t) : 0);
+  KSIM_PUT(KSIM_PL_IMAGE_LOCALITY, m.image ? image_locality_score(m, t) : 0);
+  KSIM_PUT(KSIM_PL_NETWORK_BANDWIDTH, nb_score_error(r.flags) ? 0 : nb_score(c, r.node));
+  KSIM_PUT(KSIM_PL_POD_TOPOLOGY_SPREAD, 0);
+#undef KSIM_PUT
+  return part;
 }
 
 // Sum of weighted raw scores of the slots without NormalizeScore.
@@ -731,14 +977,60 @@ __device__ __forceinline__ int64_t class_count(const DevCluster& c, int32_t cls,
 __device__ __forceinline__ const int64_t* dom_of(const DevCluster& c, const DevScratch& s, int u) {
   return s.dom + (size_t)u * c.vmax;
 }
-// A use whose domain table k_topo_prefilter fills (PTS soft on hostname reads
-// the node's own count instead).
+// A use whose domain table k_topo_prefilter fills (use_node_count: the node's
+// own count instead).
 __host__ __device__ __forceinline__ bool use_needs_dom(const ksim_topo_use& u) {
-  return u.col != KSIM_COL_NONE && !(u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME));
+  return u.col != KSIM_COL_NONE && !use_node_count(u);
+}
+
+// TopoRow of one node over the pod's uses U[0 .. nu) (block-uniform nu; the
+// domain tables are the ones k_topo_prefilter filled for this cycle).
+template <typename Scratch>
+__device__ __forceinline__ void load_topo_row(const DevCluster& c, const ksim_topo_use* U, int nu,
+                                              const UseMasks& m, const Scratch& s, int32_t node, TopoRow& t) {
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++) {
+    uint32_t v = 0;
+    if (i < nu) {
+      const uint16_t col = load_use(U, i).col;
+      if (col != KSIM_COL_NONE) v = c.labels[(size_t)col * c.n + node];
+    }
+    t.v[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++) {
+    int64_t x = 0;
+    if (i < nu)
+      x = ((m.node_count >> i) & 1u) ? class_count(c, load_use(U, i).cls, node) : s.dom[(size_t)i * c.vmax + t.v[i]];
+    t.x[i] = x;
+  }
 }
 // A PTS soft use that registers its topology pairs by value (not hostname).
 __host__ __device__ __forceinline__ bool use_registers_values(const ksim_topo_use& u) {
   return u.kind == KSIM_USE_PTS_SOFT && u.col != KSIM_COL_NONE && !(u.flags & KSIM_USEF_HOSTNAME);
+}
+
+__host__ __device__ __forceinline__ int64_t ipa_coef(const ksim_profile& prof, const ksim_topo_use& u);
+
+// Host side (PodPlan): U is a host array.
+__host__ __device__ __forceinline__ UseMasks use_masks(const ksim_profile& prof, const ksim_topo_use* U, int nu) {
+  UseMasks m{};
+  for (int i = 0; i < nu; i++) {
+    const ksim_topo_use u = U[i];
+    const uint32_t b = 1u << i;
+    if (u.kind == KSIM_USE_PTS_HARD) m.hard |= b;
+    if (u.kind == KSIM_USE_PTS_SOFT) m.soft |= b;
+    if (use_registers_values(u)) m.soft_val |= b;
+    if (u.kind == KSIM_USE_IPA_AFFINITY) m.aff |= b;
+    if (u.kind == KSIM_USE_IPA_ANTI) m.anti |= b;
+    if (u.kind == KSIM_USE_IPA_EXISTING_ANTI) m.exist |= b;
+    if (ipa_coef(prof, u) != 0) m.score |= b;
+    if (u.kind == KSIM_USE_NODE_PORT) m.port |= b;
+    if (u.kind == KSIM_USE_IMAGE) m.image |= b;
+    if (use_node_count(u)) m.node_count |= b;
+    if (u.flags & KSIM_USEF_SELF_MATCH) m.self_match |= b;
+  }
+  return m;
 }
 
 // FindMatchingUntoleratedTaint straight from the taint columns (no NodeRow).
@@ -761,82 +1053,63 @@ __device__ __forceinline__ bool match_node_inclusion(const DevCluster& c, const 
   return true;
 }
 
-// nodeLabelsMatchSpreadConstraints over the pod's uses of one kind
-__device__ __forceinline__ bool node_has_all_keys(const DevCluster& c, const DevPods& P, const ksim_pod& p, int kind,
-                                                  int32_t node) {
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind == kind && use_value(c, u, node) == 0) return false;
-  }
-  return true;
-}
-
 // nodeports Filter: HostPortInfo.CheckConflict of every wanted port, compiled
 // by the host to "class of pods using a conflicting (ip, protocol, port) is
 // empty on the node" (ksim/topology.py port classes)
-__device__ __forceinline__ bool node_port_conflict(const DevCluster& c, const DevPods& P, const ksim_pod& p,
-                                                   int32_t node) {
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind == KSIM_USE_NODE_PORT && class_count(c, u.cls, node) > 0) return true;
-  }
-  return false;
+__device__ __forceinline__ bool node_port_conflict(const UseMasks& m, const TopoRow& t) {
+  bool hit = false;
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++)
+    if (((m.port >> i) & 1u) && t.x[i] > 0) hit = true;
+  return hit;
 }
 
 // imagelocality Score: calculatePriority(sumImageScores) depends only on the
 // node's static image list and the pod's container images, so the host
 // compiles it per image signature to a static class (ksim/topology.py).
-__device__ __forceinline__ int64_t image_locality_score(const DevCluster& c, const DevPods& P, const ksim_pod& p,
-                                                        int32_t node) {
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind == KSIM_USE_IMAGE) return class_count(c, u.cls, node);
-  }
-  return 0;
+__device__ __forceinline__ int64_t image_locality_score(const UseMasks& m, const TopoRow& t) {
+  int64_t r = 0;
+#pragma unroll
+  for (int i = KSIM_MAX_USES - 1; i >= 0; i--)     // the first image use wins
+    if ((m.image >> i) & 1u) r = t.x[i];
+  return r;
 }
 
 // podtopologyspread Filter -> 0 or KSIM_PTS_*
-__device__ __forceinline__ uint32_t pts_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                               const ksim_pod& p, int32_t node) {
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind != KSIM_USE_PTS_HARD) continue;
-    const uint32_t v = use_value(c, u, node);
-    if (v == 0) return KSIM_PTS_MISSING_LABEL;
-    const int64_t self = (u.flags & KSIM_USEF_SELF_MATCH) ? 1 : 0;
-    const int64_t match = dom_of(c, s, i)[v] & kDomCountMask;     // absent pair: 0
-    if (match + self - s.min_match[i] > (int64_t)u.arg) return KSIM_PTS_SKEW;
+__device__ __forceinline__ uint32_t pts_filter(const ksim_topo_use* U, const UseMasks& m, const int64_t* min_match,
+                                               const TopoRow& t) {
+  uint32_t why = 0;                                               // the first failing constraint's reason
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++) {
+    if (why != 0 || !((m.hard >> i) & 1u)) continue;
+    const int64_t self = (m.self_match >> i) & 1u;
+    const int64_t match = t.x[i] & kDomCountMask;                  // absent pair: 0
+    if (t.v[i] == 0) why = KSIM_PTS_MISSING_LABEL;
+    else if (match + self - min_match[i] > (int64_t)load_use(U, i).arg) why = KSIM_PTS_SKEW;
   }
-  return 0;
+  return why;
 }
 
 // interpodaffinity Filter -> 0 or KSIM_IPA_*
-__device__ __forceinline__ uint32_t ipa_filter(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                               const ksim_pod& p, uint32_t topo_flags, int32_t node) {
-  bool pods_exist = true, any_aff = false;
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind != KSIM_USE_IPA_AFFINITY) continue;
-    any_aff = true;
-    const uint32_t v = use_value(c, u, node);
-    if (v == 0) return KSIM_IPA_AFFINITY;
-    if (dom_of(c, s, i)[v] <= 0) pods_exist = false;
+__device__ __forceinline__ uint32_t ipa_filter(const UseMasks& m, const ksim_pod& p, uint32_t topo_flags,
+                                               const TopoRow& t) {
+  bool pods_exist = true, missing = false, anti = false, existing = false;
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++) {
+    const uint32_t v = t.v[i];
+    if ((m.aff >> i) & 1u) {
+      if (v == 0) missing = true;
+      else if (t.x[i] <= 0) pods_exist = false;
+    }
+    if (((m.anti >> i) & 1u) && v != 0 && t.x[i] > 0) anti = true;
+    if (((m.exist >> i) & 1u) && v != 0 && t.x[i] > 0) existing = true;
   }
-  if (any_aff && !pods_exist &&
+  if (missing) return KSIM_IPA_AFFINITY;
+  if (m.aff && !pods_exist &&
       !(!(topo_flags & kTopoAffinityNonEmpty) && (p.topo_flags & KSIM_POD_IPA_SELF_AFFINITY)))
     return KSIM_IPA_AFFINITY;
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind != KSIM_USE_IPA_ANTI) continue;
-    const uint32_t v = use_value(c, u, node);
-    if (v != 0 && dom_of(c, s, i)[v] > 0) return KSIM_IPA_ANTI_AFFINITY;
-  }
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind != KSIM_USE_IPA_EXISTING_ANTI) continue;
-    const uint32_t v = use_value(c, u, node);
-    if (v != 0 && dom_of(c, s, i)[v] > 0) return KSIM_IPA_EXISTING_ANTI;
-  }
+  if (anti) return KSIM_IPA_ANTI_AFFINITY;
+  if (existing) return KSIM_IPA_EXISTING_ANTI;
   return 0;
 }
 
@@ -848,39 +1121,20 @@ __device__ __forceinline__ bool use_has_kind(const DevPods& P, const ksim_pod& p
   return false;
 }
 
-__device__ __forceinline__ int64_t ipa_coef(const ksim_profile& prof, const ksim_topo_use& u) {
+__host__ __device__ __forceinline__ int64_t ipa_coef(const ksim_profile& prof, const ksim_topo_use& u) {
   if (u.kind == KSIM_USE_IPA_SCORE) return u.arg;
   if (u.kind == KSIM_USE_IPA_SCORE_HARD) return prof.hard_pod_affinity_weight > 0 ? prof.hard_pod_affinity_weight : 0;
   return 0;
 }
 
 // interpodaffinity Score
-__device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                             const ksim_profile& prof, const ksim_pod& p, int32_t node) {
+__device__ __forceinline__ int64_t ipa_score(const ksim_profile& prof, const ksim_topo_use* U, const UseMasks& m,
+                                             const TopoRow& t) {
   int64_t sc = 0;
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    const int64_t coef = ipa_coef(prof, u);
-    if (coef == 0) continue;
-    const uint32_t v = use_value(c, u, node);
-    if (v != 0) sc += coef * dom_of(c, s, i)[v];
-  }
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_USES; i++)
+    if (((m.score >> i) & 1u) && t.v[i] != 0) sc += ipa_coef(prof, load_use(U, i)) * t.x[i];
   return sc;
-}
-
-// podtopologyspread Score before NormalizeScore (weight[i] = topologyNormalizingWeight)
-__device__ __forceinline__ int64_t pts_score(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                             const ksim_pod& p, const double* weight, int32_t node) {
-  double score = 0;
-  for (int i = 0; i < p.use_count; i++) {
-    const ksim_topo_use& u = P.uses[p.use_first + i];
-    if (u.kind != KSIM_USE_PTS_SOFT) continue;
-    const uint32_t v = use_value(c, u, node);
-    if (v == 0) continue;
-    const int64_t cnt = (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node) : dom_of(c, s, i)[v];
-    score = score + ((double)cnt * weight[i] + (double)(u.arg - 1));    // scoreForCount, unfused
-  }
-  return (int64_t)round(score);                                          // math.Round
 }
 
 // NodeInfo.AddPod / RemovePod on the count classes
@@ -910,6 +1164,9 @@ struct BatchProg {
   int32_t fit_w_eq;                        // fast_w and fit_w_cpu == fit_w_mem: the mean is a halving
   int32_t _pad;
   double inv_w[3];                         // RN(1 / w) of fit_w_cpu, fit_w_mem, their sum (dyn_key_fast)
+  // per-pod cycle (plan_profile): filter position / score slot per plugin id
+  uint64_t rank_lo, rank_hi, slot;
+  uint32_t slot_hi, _pad2;
 };
 
 // DevPods.bflags (batch path, per pod)

@@ -97,6 +97,7 @@ struct ksim_handle {
     int64_t* nb_alloc;
   } init{};
   std::vector<int32_t> col_nvals;       // host copy (pod validation)
+  std::vector<uint8_t> col_unique;      // host copy of DevCluster.col_unique (kUseUniqueCol on upload)
 
   DevScratch sc{};
   DevEvalOut eo{};
@@ -723,10 +724,15 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   if (!h || !p) return KSIM_E_INVALID;
   if (p->n_filter < 0 || p->n_filter > KSIM_MAX_FILTER || p->n_score < 0 || p->n_score > KSIM_MAX_SCORE)
     return set_err(h, KSIM_E_INVALID, "plugin count out of range");
-  for (int i = 0; i < p->n_filter; i++)
+  for (int i = 0; i < p->n_filter; i++) {
     if (!plugin_supported(p->filter[i])) return set_err(h, KSIM_E_INVALID, "unknown filter plugin id");
+    for (int j = 0; j < i; j++)
+      if (p->filter[j] == p->filter[i]) return set_err(h, KSIM_E_INVALID, "filter plugin listed twice");
+  }
   for (int i = 0; i < p->n_score; i++) {
     if (!plugin_supported(p->score[i])) return set_err(h, KSIM_E_INVALID, "unknown score plugin id");
+    for (int j = 0; j < i; j++)
+      if (p->score[j] == p->score[i]) return set_err(h, KSIM_E_INVALID, "score plugin listed twice");
     if (p->score_weight[i] < 0) return set_err(h, KSIM_E_INVALID, "negative score weight");
   }
   if (p->fit_n_res < 0 || p->fit_n_res > KSIM_MAX_RES || p->ba_n_res < 0 || p->ba_n_res > KSIM_MAX_RES)
@@ -758,6 +764,7 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
     if (p->score[k] == KSIM_PL_NODE_RESOURCES_FIT) bp.w_fit += w;
     if (p->score[k] == KSIM_PL_BALANCED_ALLOCATION) bp.w_ba += w;
   }
+  plan_profile(*p, bp.rank_lo, bp.rank_hi, bp.slot, bp.slot_hi);
   HIPCHK(h, hipSetDevice(h->device));
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
@@ -887,6 +894,26 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   UP(cnt, t->class_count, 4 * N * (size_t)t->n_classes);
   UP(topo_log, v->topo_log, 8 * (size_t)v->n_topo_log);
   UP(col_nvals, col_nvals.data(), 4 * col_nvals.size());
+  {
+    // label columns whose every value sits on at most one node (hostname):
+    // InterPodAffinity reads the node's own count there (kUseUniqueCol); off
+    // on shard handles, whose domain sums are exchanged as tables
+    std::vector<uint8_t> uniq((size_t)t->n_label_cols, 0);
+    if (!h->shard_total) {
+      std::vector<uint8_t> seen;
+      for (int k = 0; k < t->n_label_cols; k++) {
+        seen.assign((size_t)col_nvals[k], 0);
+        bool u = true;
+        for (int32_t i = 0; i < n && u; i++) {
+          const uint32_t v = t->labels[(size_t)k * n + i];
+          if (v && seen[v]++) u = false;
+        }
+        uniq[k] = u;
+      }
+    }
+    UP(col_unique, uniq.data(), uniq.size());
+    h->col_unique = uniq;
+  }
   UP(nb_limit, t->nb_limit, 8 * N);                      // zeros when no node has the annotation
   UP(nb_alloc, t->nb_alloc, 8 * N);
   {
@@ -911,6 +938,11 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
         h->hard_taints.push_back((uint16_t)id);
     h->any_unschedulable = false;
     for (int32_t i = 0; i < n; i++) h->any_unschedulable = h->any_unschedulable || (t->flags[i] & KSIM_NODE_UNSCHEDULABLE);
+    c.cflags = h->any_unschedulable ? kClusterUnschedulable : 0u;
+    if (!h->hard_taints.empty()) c.cflags |= kClusterHardTaints;
+    for (size_t i = 0; i < (size_t)n * KSIM_MAX_NODE_TAINTS; i++)
+      if (t->taints[i] && v->taint_effect[t->taints[i]] == KSIM_EFFECT_PREFER_NO_SCHEDULE) c.cflags |= kClusterPreferTaints;
+    h->dc.cflags = c.cflags;
     h->alloc_narrow = true;
     for (int32_t i = 0; i < n; i++)
       h->alloc_narrow = h->alloc_narrow && t->alloc_cpu[i] >= 0 && t->alloc_cpu[i] < (1ll << 46) &&
@@ -1220,6 +1252,23 @@ int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
   return KSIM_OK;
 }
 
+// Device copies of topology uses carry kUseUniqueCol when their key column is
+// unique per node (ksim_device.h use_node_count).
+static void mark_unique(const ksim_handle* h, ksim_topo_use* u, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (u[i].col != KSIM_COL_NONE && u[i].col < h->col_unique.size() && h->col_unique[u[i].col])
+      u[i].flags |= kUseUniqueCol;
+}
+
+// The pod's PodPlan against the current profile and cluster (uses: its device
+// copies, kUseUniqueCol marked).
+static PodPlan make_plan(const ksim_handle* h, const ksim_pod& p, const ksim_topo_use* uses) {
+  PodPlan pl{};
+  pl.m = use_masks(h->prof, uses, p.use_count);
+  pl.filter_en = plan_filter_en(h->prof, p, pl.m, h->any_unschedulable, !h->hard_taints.empty());
+  return pl;
+}
+
 // Re-based copy of one pod with only the expressions/terms it references.
 static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std::vector<ksim_label_expr>& ex,
                            std::vector<ksim_term>& tm, std::vector<ksim_topo_use>& us,
@@ -1259,6 +1308,7 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   std::vector<ksim_class_add> ad;
   std::vector<int32_t> nn;
   single_pod_set(ps, pod_index, pod, ex, tm, us, ad, nn);
+  mark_unique(h, us.data(), us.size());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   free_bufs(h->pod1_bufs);
   P = DevPods{};
@@ -1278,6 +1328,9 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
     if (use_registers_values(u)) bflag[0] |= kPodRegistersValues;
   if ((rc = upload(h, h->pod1_bufs, bflag, sizeof(bflag), &p))) return rc;
   P.bflags = (const int32_t*)p;
+  const PodPlan plan = make_plan(h, pod, us.data());
+  if ((rc = upload(h, h->pod1_bufs, &plan, sizeof(plan), &p))) return rc;
+  P.plans = (const PodPlan*)p;
   if ((rc = upload(h, h->pod1_bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
   if ((rc = upload(h, h->pod1_bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
@@ -1455,6 +1508,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
                                      4 * (size_t)ps->n_nn,
                                      4 * np1,
                                      sizeof(ksim_topo_use) * (size_t)ps->n_uses,
+                                     sizeof(PodPlan) * (size_t)ps->n_pods,
                                      sizeof(ksim_class_add) * (size_t)ps->n_adds};
   const bool reuse = h->d_chosen && h->pod_buf_bytes == bytes;
   auto drop_queue = [&](int code) {
@@ -1519,8 +1573,17 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.nn = (const int32_t*)p;
   if ((rc = put(bf.data(), 4 * bf.size(), &p))) return drop_queue(rc);
   P.bflags = (const int32_t*)p;
-  if ((rc = put(ps->uses, sizeof(ksim_topo_use) * (size_t)ps->n_uses, &p))) return drop_queue(rc);
+  std::vector<ksim_topo_use> uses(ps->uses, ps->uses + std::max(ps->n_uses, 0));
+  mark_unique(h, uses.data(), uses.size());
+  if ((rc = put(uses.data(), sizeof(ksim_topo_use) * uses.size(), &p))) return drop_queue(rc);
   P.uses = (const ksim_topo_use*)p;
+  {
+    std::vector<PodPlan> plans((size_t)ps->n_pods);
+    for (int32_t i = 0; i < ps->n_pods; i++)
+      plans[i] = make_plan(h, ps->pods[i], uses.data() + std::max(ps->pods[i].use_first, 0));
+    if ((rc = put(plans.data(), sizeof(PodPlan) * plans.size(), &p))) return drop_queue(rc);
+    P.plans = (const PodPlan*)p;
+  }
   if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)ps->n_adds, &p))) return drop_queue(rc);
   P.adds = (const ksim_class_add*)p;
   P.n_uses = ps->n_uses;

@@ -193,7 +193,7 @@ struct PodStage {
 };
 static_assert(sizeof(ksim_pod) % 8 == 0, "pod record copied as 8-byte words");
 
-__device__ __forceinline__ DevPods stage_pod(const DevPods& P, int32_t pi, PodStage& sp) {
+__device__ __forceinline__ DevPods stage_pod(const DevCluster& c, const DevPods& P, int32_t pi, PodStage& sp) {
   constexpr int kWords = (int)(sizeof(ksim_pod) / 8);
   const ksim_pod& g = P.pods[pi];
   const uint64_t* src = reinterpret_cast<const uint64_t*>(&g);
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0
   __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
-  const DevPods P = stage_pod(P0, pi, s_stage);
+  const DevPods P = stage_pod(c, P0, pi, s_stage);
   const ksim_pod& p = s_stage.pod;
   const int nu = p.use_count;
   if (nu == 0) return;
@@ -241,37 +241,50 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0
   const int32_t node = blockIdx.x * blockDim.x + tid;
   uint32_t flags = 0;
   if (node < c.n) {
-    const bool all_hard = node_has_all_keys(c, P, p, KSIM_USE_PTS_HARD, node);
-    const bool all_soft = node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
-    for (int i = 0; i < nu; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
-      const uint32_t v = use_value(c, u, node);
-      if (v == 0) continue;                        // the node has no pair for this key
-      const int64_t cnt = class_count(c, u.cls, node);
+    const ksim_topo_use* U = P.uses;               // staged: use_first == 0
+    uint32_t val[KSIM_MAX_USES];
+    int64_t cnt[KSIM_MAX_USES];
+    bool all_hard = true, all_soft = true;         // nodeLabelsMatchSpreadConstraints per kind
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_USES; i++) {      // every load of the node first
+      val[i] = i < nu ? use_value(c, U[i], node) : 0u;
+      cnt[i] = i < nu ? class_count(c, U[i].cls, node) : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_USES; i++) {
+      if (i < nu && val[i] == 0 && U[i].kind == KSIM_USE_PTS_HARD) all_hard = false;
+      if (i < nu && val[i] == 0 && U[i].kind == KSIM_USE_PTS_SOFT) all_soft = false;
+    }
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_USES; i++) {
+      const uint32_t v = val[i];
+      if (i >= nu || v == 0) continue;             // the node has no pair for this key
+      const ksim_topo_use u = U[i];
+      const int64_t n_cnt = cnt[i];
       int64_t add = 0;
       switch (u.kind) {
         case KSIM_USE_PTS_HARD:                     // TpPairToMatchNum[pair] += count (+ presence mark)
-          if (all_hard && match_node_inclusion(c, P, p, u, node)) add = cnt + (1ll << kDomMarkShift);
+          if (all_hard && match_node_inclusion(c, P, p, u, node)) add = n_cnt + (1ll << kDomMarkShift);
           break;
         case KSIM_USE_PTS_SOFT:                     // TopologyPairToPodCounts (hostname: per node in Score)
-          if (!(u.flags & KSIM_USEF_HOSTNAME) && all_soft && match_node_inclusion(c, P, p, u, node)) add = cnt;
+          if (!(u.flags & KSIM_USEF_HOSTNAME) && all_soft && match_node_inclusion(c, P, p, u, node)) add = n_cnt;
           break;
         case KSIM_USE_IPA_AFFINITY:
-          if (cnt > 0) flags |= kTopoAffinityNonEmpty;
-          add = cnt;
+          if (n_cnt > 0) flags |= kTopoAffinityNonEmpty;
+          add = n_cnt;
           break;
         case KSIM_USE_IPA_EXISTING_ANTI:
         case KSIM_USE_IPA_ANTI:
-          add = cnt;
+          add = n_cnt;
           break;
         default:                                    // IPA score: topologyScore[key][value]
-          if (ipa_coef(prof, u) != 0 && cnt != 0) {
+          if (ipa_coef(prof, u) != 0 && n_cnt != 0) {
             flags |= kTopoScoreNonEmpty;
-            add = cnt;
+            add = n_cnt;
           }
           break;
       }
-      if (add == 0) continue;
+      if (add == 0 || use_node_count(u)) continue;  // unique column: the node's count is the sum
       if (c.col_nvals[u.col] <= kLdsDom)
         atomicAdd(&s_dom[i][v], (unsigned long long)add);
       else
@@ -422,19 +435,40 @@ __device__ __forceinline__ int64_t soft_score(int64_t cnt, double w, int32_t max
   return (int64_t)round(score);
 }
 
+// KSIM_FS_CLOCKS builds: per-block phase times of k_filter_score (thread 0,
+// 100 MHz realtime) summed into s.dbg[8 + phase], s.dbg[15] = blocks.
+#ifdef KSIM_FS_CLOCKS
+#define FS_CLK(k)                                                          \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      const uint64_t _t = __builtin_amdgcn_s_memrealtime();                \
+      if ((k) > 0) atomicAdd(&s.dbg[8 + (k) - 1], (unsigned long long)(_t - fs_t)); \
+      fs_t = _t;                                                           \
+    }                                                                      \
+  } while (0)
+#else
+#define FS_CLK(k) do {} while (0)
+#endif
+
 template <bool COMPAT, bool NOWIN>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, ksim_profile prof,
+                                                      const BatchProg* __restrict__ bp,
                                                       const DevState* __restrict__ st, DevScratch s,
                                                       int32_t fuse_min, int32_t fuse_ext) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ int64_t sh64[4];
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
-  __shared__ PodStage s_stage;
+#ifdef KSIM_FS_CLOCKS
+  uint64_t fs_t = 0;
+#endif
+  FS_CLK(0);
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
-  const DevPods P = stage_pod(P0, pi, s_stage);
-  const ksim_pod& p = s_stage.pod;
+  // the pod record and its uses sit at a block-uniform address: scalar loads
+  const DevPods& P = P0;
+  const ksim_pod p = P0.pods[pi];
+  FS_CLK(1);
   if (fuse_min && p.use_count) {                 // block-uniform
     for (int i = 0; i < p.use_count; i++) {
       const ksim_topo_use u = P.uses[p.use_first + i];
@@ -454,6 +488,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     __syncthreads();
     s.min_match = s_min;                          // pts_filter reads the block's copy
   }
+  FS_CLK(2);
   bool feasible = false, ign = false;
   bool scanned = true;
   if (p.flags & KSIM_POD_NODE_NAMES)              // block-uniform: NodeAffinity's PreFilterResult
@@ -464,30 +499,43 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   } else if (node < c.n) {
     const uint32_t tf = p.use_count ? st->topo_flags : 0u;
     const NodeRow r = load_row(c, node);
+#ifdef KSIM_FS_CLOCKS
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0) {
+      const uint64_t _t = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&s.dbg[13], (unsigned long long)(_t - fs_t));
+    }
+#endif
+    const ksim_topo_use* U = P.uses + p.use_first;
+    const PodPlan pp = P.plans[pi];                 // block-uniform: scalar loads
+    const UseMasks& m = pp.m;
+    const FilterPlan fp{bp->rank_lo, bp->rank_hi, pp.filter_en};
+    TopoRow t;
+    if (p.use_count) load_topo_row(c, U, p.use_count, m, s, node, t);
+#ifdef KSIM_FS_CLOCKS
+    __builtin_amdgcn_s_waitcnt(0);
+    if (threadIdx.x == 0) {
+      const uint64_t _t = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&s.dbg[14], (unsigned long long)(_t - fs_t));
+    }
+#endif
     uint32_t det;
-    const uint8_t res = run_filter_plugins(c, P, prof, s, tf, p, r, det);
+    const uint8_t res = run_filter_plan(c, P, fp, s.min_match, tf, p, r, U, m, t, det);
+    FS_CLK(3);
     s.fail[node] = res;
     if (COMPAT) s.detail[node] = det;
     feasible = res == KSIM_PASSED;
     if (feasible) {
       // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
-      ign = p.use_count && !node_has_all_keys(c, P, p, KSIM_USE_PTS_SOFT, node);
+#pragma unroll
+      for (int i = 0; i < KSIM_MAX_USES; i++)
+        if (((m.soft >> i) & 1u) && t.v[i] == 0) ign = true;
       s.ign[node] = ign;
-      int64_t part = 0;
-      for (int k = 0; k < prof.n_score; k++) {
-        const int pl = prof.score[k];
-        const int64_t v = score_plugin_raw(c, P, prof, s, p, pl, r);
-        if (norm_kind(pl) == kNormNone) {
-          const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
-          part += v * w;
-          if (COMPAT) s.raw[(size_t)k * c.n + node] = v;
-        } else {
-          s.raw[(size_t)k * c.n + node] = v;
-        }
-      }
+      const int64_t part = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT);
       s.part[node] = part;
     }
   }
+  FS_CLK(4);
   if (NOWIN) {
     const int lane = threadIdx.x & 63;
     WinState* win = s.win;
@@ -513,7 +561,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
       }
     }
     if (fuse_ext) {                                // block-uniform
-      const int soft = soft_use(P.uses, p.use_count);
+      const ksim_topo_use* U = P.uses + p.use_first;
+      const int soft = soft_use(U, p.use_count);
       uint64_t ix[KSIM_MAX_SCORE], in[KSIM_MAX_SCORE];
 #pragma unroll
       for (int k = 0; k < KSIM_MAX_SCORE; k++) {
@@ -526,7 +575,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
         if (kind == kNormPTS) {
           if (soft >= 0) {
             counted = !ign;                        // IgnoredNodes: not in min / max
-            if (counted) v = soft_count(c, s, P.uses[soft], soft, node);
+            if (counted) v = soft_count(c, s, U[soft], soft, node);
           }
         } else {
           v = s.raw[(size_t)k * c.n + node];
@@ -539,6 +588,10 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
       block_extrema(prof, s.win, ix, in, s_red);
     }
   }
+  FS_CLK(5);
+#ifdef KSIM_FS_CLOCKS
+  if (threadIdx.x == 0) atomicAdd(&s.dbg[15], 1ull);
+#endif
 }
 
 constexpr int kBmWords = (KSIM_MAX_NODES + 1 + 31) / 32;   // value-id bitmap (PTS pair registration)
@@ -840,7 +893,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
-  const DevPods P = stage_pod(P0, pi, s_stage);
+  const DevPods P = stage_pod(c, P0, pi, s_stage);
   const ksim_pod& p = s_stage.pod;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t node = blockIdx.x * blockDim.x + tid;
@@ -897,7 +950,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       int64_t tot = S == 0 ? (s.ext_score ? 0 : 1) : s.part[node];
       if (s.ext_score) tot += s.ext_score[node];
       for (int k = 0; k < S; k++) {
-        const int32_t kind = norm_kind(prof.score[k]);
+        const int32_t kind = norm_kind(prof_score(prof, k));
         int64_t raw, gmax = 0, gmin = 0;
         if (kind != kNormNone) {
           gmax = from_max_image(win->ext[2 * k]);
@@ -920,8 +973,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
             nv = 0;
           else
             nv = normalize_value(kind, raw, gmax, gmin, ipa_nonempty);
-          const int64_t w = prof.score_weight[k] == 0 ? 1 : prof.score_weight[k];
-          tot += nv * w;
+          tot += nv * prof_weight(prof, k);
         }
         if (COMPAT) {
           o.raw[(size_t)k * N + node] = raw;
@@ -953,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     // values touched (every touched entry is some node's value)
     for (int i = 0; i < p.use_count; i++) {
       const ksim_topo_use u = P.uses[p.use_first + i];
-      if (u.col == KSIM_COL_NONE || (u.kind == KSIM_USE_PTS_SOFT && (u.flags & KSIM_USEF_HOSTNAME))) continue;
+      if (!use_needs_dom(u)) continue;
       s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
     }
   }
@@ -1331,7 +1383,7 @@ void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent
   if (topo && !a.fuse_min) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[2], stream);
   const int32_t fx = NOWIN && !COMPAT && a.fuse_ext;   // extrema in the filter pass, no k_extrema
-  k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, topo && a.fuse_min, fx);
+  k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, topo && a.fuse_min, fx);
   if (evs) (void)hipEventRecord(evs[3], stream);
   if (!NOWIN) k_window<COMPAT><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[4], stream);
@@ -1364,7 +1416,7 @@ void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo) {
   const int blocks = (a.c.n + 255) / 256;
   if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
+  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, 0, 0);
   k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
 }
 
@@ -1378,7 +1430,7 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {
   // the window-free variant writes counters: time the windowed one (same work per node)
-  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
+  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, 0, 0);
 }
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {
@@ -1394,7 +1446,7 @@ void launch_pshard_topo(const LaunchArgs& a, hipStream_t stream) {
 void launch_pshard_filter(const LaunchArgs& a, bool topo, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   if (topo) k_topo_min<true><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, 0, 0);
+  k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, 0, 0);
   k_wcount_sh<<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.st, a.s);
 }
 

@@ -321,7 +321,7 @@ class Engine:
         if n < 0:
             self._chk(n)
         d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2]),
-             "graph_captures": int(out[19])}
+             "graph_captures": int(out[19]), "dbg": [int(x) for x in out[3:19]]}
         if out[6]:
             d["chain_us"] = {"setup": out[3] / out[6] / 100.0, "rounds": out[4] / out[6] / 100.0,
                              "epilogue": out[5] / out[6] / 100.0, "rounds_per_batch": out[7] / out[6]}

@@ -130,6 +130,7 @@ struct WinState {
   int32_t nscan;                         // nodes the cycle scans (ScanSet.n): nextStartNodeIndex modulus
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
+  int32_t done, _pad;                    // k_select blocks finished (the last one binds; reset by it)
 };
 
 // The nodes one cycle scans, in scan order: every node of
@@ -358,6 +359,15 @@ __device__ __forceinline__ int64_t div_floor_nonneg(int64_t a, int64_t b) {
   if (q * b > a) q--;
   else if ((q + 1) * b <= a) q++;
   return q;
+}
+
+// a / b with Go / C truncation, b > 0 (NormalizeScore's quotients): the
+// f64-quotient path of div_floor_nonneg on |a| (the integer division sequence
+// only past 2^52).
+__device__ __forceinline__ int64_t div_trunc_pos(int64_t a, int64_t b) {
+  if (a >= 0) return div_floor_nonneg(a, b);
+  if (a == INT64_MIN) return a / b;
+  return -div_floor_nonneg(-a, b);
 }
 
 // floor(a / b) for 0 <= a <= 100 * b, b > 0 (a score-sized quotient): an f32
@@ -702,6 +712,8 @@ __device__ __forceinline__ ksim_topo_use load_use(const ksim_topo_use* U, int i)
 // re-reading each use's kind inside every plugin.
 struct UseMasks {
   uint32_t hard, soft, soft_val, aff, anti, exist, score, port, image, node_count, self_match;
+  uint32_t dom;                  // k_topo_prefilter fills the use's domain table (use_needs_dom, and adds)
+  uint32_t honor_aff, honor_taints;   // PTS nodeAffinityPolicy / nodeTaintsPolicy Honor
 };
 
 // Per-pod plan of the per-pod cycle, compiled by the host when a pod set is
@@ -928,14 +940,27 @@ __device__ __forceinline__ int plan_slot(const ScorePlan& sp, int pl) {
   return pl < 16 ? (int)((sp.slot >> (4 * pl)) & 15u) - 1 : (int)((sp.slot_hi >> (4 * (pl - 16))) & 15u) - 1;
 }
 
-// The score plugins' raw scores of one feasible node (PodTopologySpread's is
-// computed after the filter pass: 0 here), stored per slot into raw
+// The raw scores of the plugins with a NormalizeScore (PodTopologySpread's
+// aside), kept in registers for the fused extrema.
+struct RawScores {
+  int64_t taint, aff, ipa, nb;
+  __device__ __forceinline__ int64_t of(int pl) const {
+    return pl == KSIM_PL_TAINT_TOLERATION ? taint : pl == KSIM_PL_NODE_AFFINITY ? aff
+         : pl == KSIM_PL_INTER_POD_AFFINITY ? ipa : pl == KSIM_PL_NETWORK_BANDWIDTH ? nb : 0;
+  }
+};
+
+// The score plugins' raw scores of one feasible node (PodTopologySpread's
+// score needs the whole feasible list: its slot gets pts_count, the node's
+// count for the pod's ScheduleAnyway use, which the fused k_select maps to
+// the score; k_extrema overwrites it otherwise), stored per slot into raw
 // ([slot][n]); returns the weighted sum of the slots without NormalizeScore.
 // store_plain: also store the raw score of those slots (compat mode).
 __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                                   const ScorePlan& sp, const ksim_pod& p, const NodeRow& r,
                                                   const ksim_topo_use* U, const UseMasks& m, const TopoRow& t,
-                                                  int64_t* raw, bool store_plain) {
+                                                  int64_t* raw, bool store_plain, RawScores& rv,
+                                                  int64_t pts_count) {
   int64_t part = 0;
   const size_t n = (size_t)c.n;
   auto put = [&](int pl, int64_t v) {
@@ -947,16 +972,17 @@ __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const Dev
       raw[(size_t)k * n + r.node] = v;
     }
   };
-#define KSIM_PUT(pl, expr) \
-  if (plan_slot(sp, pl) >= 0) put(pl, expr)
-  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, fit_least_allocated_score(r, prof, p, c.n_scalar));
-  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, balanced_allocation_score(r, prof, p, c.n_scalar));
-  KSIM_PUT(KSIM_PL_TAINT_TOLERATION, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
-  KSIM_PUT(KSIM_PL_NODE_AFFINITY, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
-  KSIM_PUT(KSIM_PL_INTER_POD_AFFINITY, m.score ? ipa_score(prof, U, m, t) : 0);
-  KSIM_PUT(KSIM_PL_IMAGE_LOCALITY, m.image ? image_locality_score(m, t) : 0);
-  KSIM_PUT(KSIM_PL_NETWORK_BANDWIDTH, nb_score_error(r.flags) ? 0 : nb_score(c, r.node));
-  KSIM_PUT(KSIM_PL_POD_TOPOLOGY_SPREAD, 0);
+#define KSIM_PUT(pl, dst, expr) \
+  if (plan_slot(sp, pl) >= 0) { dst = (expr); put(pl, dst); }
+  int64_t v;
+  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fit_least_allocated_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, balanced_allocation_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_TAINT_TOLERATION, rv.taint, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
+  KSIM_PUT(KSIM_PL_NODE_AFFINITY, rv.aff, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
+  KSIM_PUT(KSIM_PL_INTER_POD_AFFINITY, rv.ipa, m.score ? ipa_score(prof, U, m, t) : 0);
+  KSIM_PUT(KSIM_PL_IMAGE_LOCALITY, v, m.image ? image_locality_score(m, t) : 0);
+  KSIM_PUT(KSIM_PL_NETWORK_BANDWIDTH, rv.nb, nb_score_error(r.flags) ? 0 : nb_score(c, r.node));
+  KSIM_PUT(KSIM_PL_POD_TOPOLOGY_SPREAD, v, pts_count);   // k_extrema or k_select makes it a score
 #undef KSIM_PUT
   return part;
 }
@@ -1029,7 +1055,12 @@ __host__ __device__ __forceinline__ UseMasks use_masks(const ksim_profile& prof,
     if (u.kind == KSIM_USE_IMAGE) m.image |= b;
     if (use_node_count(u)) m.node_count |= b;
     if (u.flags & KSIM_USEF_SELF_MATCH) m.self_match |= b;
+    if (u.flags & KSIM_USEF_HONOR_AFFINITY) m.honor_aff |= b;
+    if (u.flags & KSIM_USEF_HONOR_TAINTS) m.honor_taints |= b;
   }
+  m.dom = (m.hard | m.soft_val | m.aff | m.anti | m.exist | m.score) & ~m.node_count;
+  for (int i = 0; i < nu; i++)
+    if (U[i].col == KSIM_COL_NONE) m.dom &= ~(1u << i);
   return m;
 }
 
@@ -1428,6 +1459,33 @@ __device__ __forceinline__ void assume_pod(const DevCluster& c, const DevPods& P
   c.nz_mem[node] += sign * p.nz_mem;
   c.num_pods[node] += sign;
   if (p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
+}
+
+// assume_pod by one wave (every lane calls it): one lane per column, so the
+// read-modify-writes are in flight together instead of one after another.
+// A pod's class adds name distinct classes.
+__device__ __forceinline__ void assume_pod_wave(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
+                                                int sign) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) c.req_cpu[node] += sign * p.req_cpu;
+  if (lane == 1) c.req_mem[node] += sign * p.req_mem;
+  if (lane == 2) c.req_eph[node] += sign * p.req_eph;
+  if (lane == 3) c.nz_cpu[node] += sign * p.nz_cpu;
+  if (lane == 4) c.nz_mem[node] += sign * p.nz_mem;
+  if (lane == 5) c.num_pods[node] += sign;
+  if (lane == 6 && p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
+  if (lane >= 8 && lane < 8 + c.n_scalar) {
+    const int k = lane - 8;
+    int64_t q = 0;
+#pragma unroll
+    for (int j = 0; j < KSIM_MAX_SCALAR; j++)
+      if (j == k) q = p.scalar_req[j];
+    c.req_scalar[(size_t)k * c.n + node] += sign * q;
+  }
+  for (int i = lane; i < p.add_count; i += 64) {
+    const ksim_class_add a = P.adds[p.add_first + i];
+    c.cnt[(size_t)a.cls * c.n + node] += sign * a.count;
+  }
 }
 
 __device__ __forceinline__ void store_row_dynamic(const DevCluster& c, const NodeRow& r) {

@@ -157,15 +157,17 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
   switch (kind) {
     case kNormDefault: {
       int64_t m = gmax > 0 ? gmax : 0;
-      return m == 0 ? v : (int64_t)kMaxNodeScore * v / m;
+      return m == 0 ? v : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
     }
     case kNormDefaultReverse: {
       int64_t m = gmax > 0 ? gmax : 0;
-      return m == 0 ? (int64_t)kMaxNodeScore : (int64_t)kMaxNodeScore - (int64_t)kMaxNodeScore * v / m;
+      return m == 0 ? (int64_t)kMaxNodeScore
+                    : (int64_t)kMaxNodeScore - div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
     }
     case kNormPTS: {
       int64_t mx = gmax > 0 ? gmax : 0;
-      return mx == 0 ? (int64_t)kMaxNodeScore : (int64_t)kMaxNodeScore * (mx + gmin - v) / mx;
+      return mx == 0 ? (int64_t)kMaxNodeScore
+                     : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)(mx + gmin - v)), mx);
     }
     case kNormIPA:
     case kNormMinMax: {
@@ -183,57 +185,36 @@ __device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int6
 // ==== A. per-pod path ===========================================================
 constexpr int kLdsDom = 128;   // domain tables of key columns with <= kLdsDom value ids are LDS-staged
 
-// The cycle's pod record and topology uses staged in LDS (use_first rebased to
-// 0).  The per-node loops over the uses then read LDS instead of issuing a
-// global load that depends on the pod record for every use.  Every thread of
-// the block must call it (two barriers).
-struct PodStage {
-  ksim_pod pod;
-  ksim_topo_use uses[KSIM_MAX_USES];
-};
-static_assert(sizeof(ksim_pod) % 8 == 0, "pod record copied as 8-byte words");
-
-__device__ __forceinline__ DevPods stage_pod(const DevCluster& c, const DevPods& P, int32_t pi, PodStage& sp) {
-  constexpr int kWords = (int)(sizeof(ksim_pod) / 8);
-  const ksim_pod& g = P.pods[pi];
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(&g);
-  uint64_t* dst = reinterpret_cast<uint64_t*>(&sp.pod);
-  const int t = threadIdx.x;
-  if (t < kWords) dst[t] = src[t];
-  const int32_t nu = g.use_count;
-  if (t < nu) sp.uses[t] = P.uses[g.use_first + t];
-  __syncthreads();
-  if (t == 0) sp.pod.use_first = 0;
-  __syncthreads();
-  DevPods L = P;
-  L.uses = sp.uses;
-  return L;
-}
-
 // PreFilter of PodTopologySpread / InterPodAffinity plus the domain sums their
-// PreScore needs: one thread per node, adds into the pod's domain tables.
-__global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0, ksim_profile prof,
+// PreScore needs: one thread per node, adds into the pod's domain tables (the
+// pod's plan says which uses have one; LDS-staged for small key vocabularies).
+__global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P, ksim_profile prof,
                                                         DevState* __restrict__ st, DevScratch s) {
   __shared__ unsigned long long s_dom[KSIM_MAX_USES][kLdsDom];
   __shared__ uint32_t s_flags;
-  __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
-  const DevPods P = stage_pod(c, P0, pi, s_stage);
-  const ksim_pod& p = s_stage.pod;
+  const ksim_pod p = P.pods[pi];                  // block-uniform: scalar loads
   const int nu = p.use_count;
   if (nu == 0) return;
+  const PodPlan pp = P.plans[pi];
+  const UseMasks& m = pp.m;
+  const ksim_topo_use* U = P.uses + p.use_first;
+  uint32_t lds = 0;                                // uses whose table is staged in LDS
+  for (uint32_t b = m.dom; b; b &= b - 1) {
+    const int i = __builtin_ctz(b);
+    if (c.col_nvals[load_use(U, i).col] <= kLdsDom) lds |= 1u << i;
+  }
   const int tid = threadIdx.x;
   for (int x = tid; x < nu * kLdsDom; x += blockDim.x) s_dom[x / kLdsDom][x % kLdsDom] = 0;
   if (tid == 0) s_flags = 0;
   // the PTS pair-registration rows the no-window filter pass fills for this
   // pod start empty (k_bind used to clear them after the cycle)
-  if (blockIdx.x == 0 && (P0.bflags[pi] & kPodRegistersValues)) {
+  if (blockIdx.x == 0 && m.soft_val) {
     const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
-    for (int i = 0; i < nu; i++) {
-      const ksim_topo_use u = P.uses[i];           // staged: use_first == 0
-      if (!use_registers_values(u)) continue;
-      const int32_t words = (c.col_nvals[u.col] + 31) >> 5;
+    for (uint32_t b = m.soft_val; b; b &= b - 1) {
+      const int i = __builtin_ctz(b);
+      const int32_t words = (c.col_nvals[load_use(U, i).col] + 31) >> 5;
       for (int x = tid; x < words; x += blockDim.x) s.regbm[(size_t)i * vwords + x] = 0;
     }
   }
@@ -241,51 +222,42 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0
   const int32_t node = blockIdx.x * blockDim.x + tid;
   uint32_t flags = 0;
   if (node < c.n) {
-    const ksim_topo_use* U = P.uses;               // staged: use_first == 0
     uint32_t val[KSIM_MAX_USES];
     int64_t cnt[KSIM_MAX_USES];
-    bool all_hard = true, all_soft = true;         // nodeLabelsMatchSpreadConstraints per kind
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_USES; i++) {      // every load of the node first
-      val[i] = i < nu ? use_value(c, U[i], node) : 0u;
-      cnt[i] = i < nu ? class_count(c, U[i].cls, node) : 0;
+      val[i] = 0;
+      cnt[i] = 0;
+      if (i < nu) {
+        const ksim_topo_use u = load_use(U, i);
+        if (u.col != KSIM_COL_NONE) val[i] = c.labels[(size_t)u.col * c.n + node];
+        cnt[i] = class_count(c, u.cls, node);
+      }
     }
+    bool all_hard = true, all_soft = true;         // nodeLabelsMatchSpreadConstraints per kind
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_USES; i++) {
-      if (i < nu && val[i] == 0 && U[i].kind == KSIM_USE_PTS_HARD) all_hard = false;
-      if (i < nu && val[i] == 0 && U[i].kind == KSIM_USE_PTS_SOFT) all_soft = false;
+      if (((m.hard >> i) & 1u) && val[i] == 0) all_hard = false;
+      if (((m.soft >> i) & 1u) && val[i] == 0) all_soft = false;
+      if (((m.aff >> i) & 1u) && val[i] != 0 && cnt[i] > 0) flags |= kTopoAffinityNonEmpty;
+      if (((m.score >> i) & 1u) && val[i] != 0 && cnt[i] != 0) flags |= kTopoScoreNonEmpty;
     }
+    // matchNodeInclusionPolicies, once per node for every spread use
+    const uint32_t spread = m.hard | m.soft_val;
+    const bool aff_ok = (m.honor_aff & spread) ? required_node_affinity_match(c, P, p, node) : true;
+    const bool taint_ok = (m.honor_taints & spread) ? !node_has_untolerated_taint(c, p, node) : true;
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_USES; i++) {
       const uint32_t v = val[i];
-      if (i >= nu || v == 0) continue;             // the node has no pair for this key
-      const ksim_topo_use u = U[i];
-      const int64_t n_cnt = cnt[i];
-      int64_t add = 0;
-      switch (u.kind) {
-        case KSIM_USE_PTS_HARD:                     // TpPairToMatchNum[pair] += count (+ presence mark)
-          if (all_hard && match_node_inclusion(c, P, p, u, node)) add = n_cnt + (1ll << kDomMarkShift);
-          break;
-        case KSIM_USE_PTS_SOFT:                     // TopologyPairToPodCounts (hostname: per node in Score)
-          if (!(u.flags & KSIM_USEF_HOSTNAME) && all_soft && match_node_inclusion(c, P, p, u, node)) add = n_cnt;
-          break;
-        case KSIM_USE_IPA_AFFINITY:
-          if (n_cnt > 0) flags |= kTopoAffinityNonEmpty;
-          add = n_cnt;
-          break;
-        case KSIM_USE_IPA_EXISTING_ANTI:
-        case KSIM_USE_IPA_ANTI:
-          add = n_cnt;
-          break;
-        default:                                    // IPA score: topologyScore[key][value]
-          if (ipa_coef(prof, u) != 0 && n_cnt != 0) {
-            flags |= kTopoScoreNonEmpty;
-            add = n_cnt;
-          }
-          break;
-      }
-      if (add == 0 || use_node_count(u)) continue;  // unique column: the node's count is the sum
-      if (c.col_nvals[u.col] <= kLdsDom)
+      if (!((m.dom >> i) & 1u) || v == 0) continue;   // no table, or the node has no pair for this key
+      const bool incl = (!((m.honor_aff >> i) & 1u) || aff_ok) && (!((m.honor_taints >> i) & 1u) || taint_ok);
+      int64_t add = cnt[i];
+      if ((m.hard >> i) & 1u)                      // TpPairToMatchNum[pair] += count (+ presence mark)
+        add = all_hard && incl ? add + (1ll << kDomMarkShift) : 0;
+      else if ((m.soft_val >> i) & 1u)             // TopologyPairToPodCounts
+        add = all_soft && incl ? add : 0;
+      if (add == 0) continue;
+      if ((lds >> i) & 1u)
         atomicAdd(&s_dom[i][v], (unsigned long long)add);
       else
         atomicAdd(reinterpret_cast<unsigned long long*>(s.dom + (size_t)i * c.vmax + v), (unsigned long long)add);
@@ -294,6 +266,7 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P0
   if (flags) atomicOr(&s_flags, flags);
   __syncthreads();
   for (int x = tid; x < nu * kLdsDom; x += blockDim.x) {
+    if (!((lds >> (x / kLdsDom)) & 1u)) continue;
     const unsigned long long v = s_dom[x / kLdsDom][x % kLdsDom];
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(s.dom + (size_t)(x / kLdsDom) * c.vmax + x % kLdsDom), v);
   }
@@ -414,20 +387,6 @@ __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState
   }
 }
 
-// The pod's one ScheduleAnyway spread use (index into its uses), or -1.
-__device__ __forceinline__ int soft_use(const ksim_topo_use* U, int nu) {
-  int soft = -1;
-  for (int i = 0; i < nu; i++)
-    if (U[i].kind == KSIM_USE_PTS_SOFT) soft = i;
-  return soft;
-}
-// PodTopologySpread's count for the soft use on node (TopologyPairToPodCounts,
-// or the node's own count on hostname)
-__device__ __forceinline__ int64_t soft_count(const DevCluster& c, const DevScratch& s, const ksim_topo_use& u,
-                                              int soft, int32_t node) {
-  return (u.flags & KSIM_USEF_HOSTNAME) ? class_count(c, u.cls, node)
-                                        : s.dom[(size_t)soft * c.vmax + use_value(c, u, node)];
-}
 // scoreForCount with a single constraint (k_extrema's sum from 0, unfused)
 __device__ __forceinline__ int64_t soft_score(int64_t cnt, double w, int32_t max_skew) {
   double score = 0;
@@ -456,7 +415,6 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
                                                       const DevState* __restrict__ st, DevScratch s,
                                                       int32_t fuse_min, int32_t fuse_ext) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
-  __shared__ int64_t sh64[4];
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
 #ifdef KSIM_FS_CLOCKS
   uint64_t fs_t = 0;
@@ -468,28 +426,36 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   // the pod record and its uses sit at a block-uniform address: scalar loads
   const DevPods& P = P0;
   const ksim_pod p = P0.pods[pi];
+  const PodPlan pp = P0.plans[pi];                 // block-uniform: scalar loads
+  const UseMasks& m = pp.m;
+  const ksim_topo_use* U = P.uses + p.use_first;
   FS_CLK(1);
-  if (fuse_min && p.use_count) {                 // block-uniform
-    for (int i = 0; i < p.use_count; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
-      if (u.kind != KSIM_USE_PTS_HARD) continue;
-      int64_t mn = 2147483647;
-      if (u.col != KSIM_COL_NONE) {
-        const int32_t V = c.col_nvals[u.col];
-        const int64_t* d = s.dom + (size_t)i * c.vmax;
-        for (int32_t v = threadIdx.x; v < V; v += blockDim.x) {
-          const int64_t x = d[v];
-          if ((x >> kDomMarkShift) != 0) mn = min(mn, x & kDomCountMask);
+  if (fuse_min && m.hard) {                        // block-uniform: the critical paths, one wave
+    if (threadIdx.x < 64) {
+      for (uint32_t b = m.hard; b; b &= b - 1) {
+        const int i = __builtin_ctz(b);
+        const ksim_topo_use u = load_use(U, i);
+        int64_t mn = 2147483647;
+        if (u.col != KSIM_COL_NONE) {
+          const int32_t V = c.col_nvals[u.col];
+          const int64_t* d = s.dom + (size_t)i * c.vmax;
+          for (int32_t v = threadIdx.x; v < V; v += 64) {
+            const int64_t x = d[v];
+            if ((x >> kDomMarkShift) != 0) mn = min(mn, x & kDomCountMask);
+          }
         }
+        mn = wave_min_i64(mn);
+        if (threadIdx.x == 0) s_min[i] = mn;
       }
-      mn = block_min_i64_nw<4>(mn, sh64);
-      if (threadIdx.x == 0) s_min[i] = mn;
     }
     __syncthreads();
     s.min_match = s_min;                          // pts_filter reads the block's copy
   }
   FS_CLK(2);
   bool feasible = false, ign = false;
+  RawScores rv{};                                  // normalized plugins' raw scores (fused extrema)
+  int64_t soft_cnt = 0;                            // PodTopologySpread: the node's count for the soft use
+  const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;   // the pod's last ScheduleAnyway use
   bool scanned = true;
   if (p.flags & KSIM_POD_NODE_NAMES)              // block-uniform: NodeAffinity's PreFilterResult
     scanned = node < c.n && scan_pos(scan_set(c, P, p, st->next_start), c.base + node) >= 0;
@@ -506,9 +472,6 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
       atomicAdd(&s.dbg[13], (unsigned long long)(_t - fs_t));
     }
 #endif
-    const ksim_topo_use* U = P.uses + p.use_first;
-    const PodPlan pp = P.plans[pi];                 // block-uniform: scalar loads
-    const UseMasks& m = pp.m;
     const FilterPlan fp{bp->rank_lo, bp->rank_hi, pp.filter_en};
     TopoRow t;
     if (p.use_count) load_topo_row(c, U, p.use_count, m, s, node, t);
@@ -528,11 +491,13 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     if (feasible) {
       // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
 #pragma unroll
-      for (int i = 0; i < KSIM_MAX_USES; i++)
+      for (int i = 0; i < KSIM_MAX_USES; i++) {
         if (((m.soft >> i) & 1u) && t.v[i] == 0) ign = true;
+        if (i == soft) soft_cnt = t.x[i];          // soft_count: the node's own count or the domain sum
+      }
       s.ign[node] = ign;
-      const int64_t part = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT);
-      s.part[node] = part;
+      s.part[node] = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT, rv,
+                                    soft_cnt);
     }
   }
   FS_CLK(4);
@@ -542,43 +507,40 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     const uint64_t fm = __ballot(feasible), im = __ballot(feasible && ign);
     if (lane == 0 && fm) atomicAdd(&win->nfeas, (int32_t)__popcll(fm));
     if (lane == 0 && im) atomicAdd(&win->nign, (int32_t)__popcll(im));
-    const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
-    const int nreg = (P.bflags[pi] & kPodRegistersValues) ? p.use_count : 0;
-    for (int i = 0; i < nreg; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
-      if (!use_registers_values(u)) continue;
-      const bool reg = feasible && !ign;
-      const uint32_t v = reg ? use_value(c, u, node) : 0u;
-      uint32_t* bm = s.regbm + (size_t)i * vwords;
-      if (c.col_nvals[u.col] <= 64) {            // few values: OR the wave's values first
-        uint64_t bits = reg ? 1ull << v : 0ull;
+    if (P.bflags[pi] & kPodRegistersValues) {
+      const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
+      for (uint32_t b = m.soft_val; b; b &= b - 1) {
+        const int i = __builtin_ctz(b);
+        const ksim_topo_use u = load_use(U, i);
+        const bool reg = feasible && !ign && node < c.n;
+        const uint32_t v = reg ? use_value(c, u, node) : 0u;
+        uint32_t* bm = s.regbm + (size_t)i * vwords;
+        if (c.col_nvals[u.col] <= 64) {            // few values: OR the wave's values first
+          uint64_t bits = reg ? 1ull << v : 0ull;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) bits |= __shfl_xor(bits, d, 64);
-        if (lane == 0 && (uint32_t)bits) atomicOr(&bm[0], (uint32_t)bits);
-        if (lane == 0 && (uint32_t)(bits >> 32)) atomicOr(&bm[1], (uint32_t)(bits >> 32));
-      } else if (reg) {
-        atomicOr(&bm[v >> 5], 1u << (v & 31));
+          for (int d = 32; d >= 1; d >>= 1) bits |= __shfl_xor(bits, d, 64);
+          if (lane == 0 && (uint32_t)bits) atomicOr(&bm[0], (uint32_t)bits);
+          if (lane == 0 && (uint32_t)(bits >> 32)) atomicOr(&bm[1], (uint32_t)(bits >> 32));
+        } else if (reg) {
+          atomicOr(&bm[v >> 5], 1u << (v & 31));
+        }
       }
     }
     if (fuse_ext) {                                // block-uniform
-      const ksim_topo_use* U = P.uses + p.use_first;
-      const int soft = soft_use(U, p.use_count);
       uint64_t ix[KSIM_MAX_SCORE], in[KSIM_MAX_SCORE];
 #pragma unroll
       for (int k = 0; k < KSIM_MAX_SCORE; k++) {
         ix[k] = in[k] = 0;
-        if (k >= prof.n_score) continue;
-        const int32_t kind = norm_kind(prof.score[k]);
-        if (kind == kNormNone || !feasible) continue;
+        if (k >= prof.n_score || !feasible) continue;
+        const int pl = (int)prof_score(prof, k);
+        if (norm_kind(pl) == kNormNone) continue;
         int64_t v = 0;
         bool counted = true;
-        if (kind == kNormPTS) {
-          if (soft >= 0) {
-            counted = !ign;                        // IgnoredNodes: not in min / max
-            if (counted) v = soft_count(c, s, U[soft], soft, node);
-          }
+        if (pl == KSIM_PL_POD_TOPOLOGY_SPREAD) {
+          counted = soft < 0 || !ign;              // IgnoredNodes: not in min / max
+          v = soft < 0 ? 0 : soft_cnt;
         } else {
-          v = s.raw[(size_t)k * c.n + node];
+          v = rv.of(pl);
         }
         if (counted) {
           ix[k] = max_image(v);
@@ -883,18 +845,76 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
 // the window state from the filter pass's counters, as k_extrema<true> does,
 // and block 0 publishes it for k_bind; PodTopologySpread's raw scores and
 // extrema come from the soft use's counts.
+// selectHost over k_select's per-block records (one wave): the winning TB lo
+// word (0: no kept node).
+__device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32_t n_blocks) {
+  const int lane = threadIdx.x & 63;
+  uint64_t img = 0, lo = 0;
+  for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
+  wave_best2(img, lo);
+  return lo;
+}
+
+// The bind step of a per-pod cycle, by one wave: selectHost over k_select's
+// block records, NodeInfo.AddPod on the chosen node (one column per lane) and
+// the scheduler state (thread 0).  NOWIN also returns the counters and extrema
+// slots to zero for the next cycle (k_window resets its own otherwise;
+// k_topo_prefilter clears the registration rows).
+__device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
+                                           const DevScratch& s, int32_t* __restrict__ chosen_out, int32_t pi,
+                                           bool nowin) {
+  WinState* win = s.win;
+  const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);   // every lane
+  const int32_t error = win->error;
+  const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
+  const ksim_pod p = P.pods[pi];
+  if (chosen >= 0) assume_pod_wave(c, P, p, chosen, 1);         // NodeInfo.AddPod, one column per lane
+  if ((threadIdx.x & 63) != 0) return;
+  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
+  DevState S = *st;                                // one read, one write back: no load-store chain
+  // nextStartNodeIndex = (nextStartNodeIndex + processed) % len(scanned nodes);
+  // a pod PreFilter rejected scans nothing and leaves it
+  const int32_t ns = NS > 0 ? (int32_t)(((int64_t)S.next_start + (cut < NS ? cut : NS)) % NS) : S.next_start;
+  S.next_start = ns;
+  S.evals += evaluated;
+  if (chosen >= 0) S.scheduled += 1;
+  else S.unschedulable += 1;
+  if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : error ? KSIM_CHOSEN_ERROR : -1;
+  S.chosen = chosen >= 0 ? chosen : error ? KSIM_CHOSEN_ERROR : -1;
+  S.status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : error ? KSIM_STATUS_ERROR : KSIM_STATUS_UNSCHEDULABLE;
+  S.n_feasible = nf;
+  S.n_evaluated = evaluated;
+  S.n_processed = cut < NS ? cut : NS;
+  S.k_to_find = k;
+  S.next_start_after = ns;
+  S.pod_seq += 1;
+  S.topo_flags = 0;
+  S.cursor = pi + 1;
+  *st = S;
+  win->error = 0;
+  if (nowin) {
+    win->nfeas = 0;
+    win->nign = 0;
+    for (int t = 0; t < kExtWords; t++) win->ext[t] = 0;
+  }
+}
+
 template <bool COMPAT>
+// bind_mode (unsharded cycles): 1 / 2 = the last block to finish runs the bind
+// step (bind_cycle, windowed / NOWIN), which saves k_bind's launch.
 __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_profile prof,
-                                                const DevState* __restrict__ st, DevScratch s, DevEvalOut o,
-                                                int32_t fuse_ext) {
+                                                DevState* __restrict__ st, DevScratch s, DevEvalOut o,
+                                                int32_t fuse_ext, int32_t bind_mode, int32_t* __restrict__ chosen_out) {
   __shared__ uint64_t s_best[8];
   __shared__ int32_t sh32[4];
-  __shared__ PodStage s_stage;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
-  const DevPods P = stage_pod(c, P0, pi, s_stage);
-  const ksim_pod& p = s_stage.pod;
+  const DevPods& P = P0;
+  const ksim_pod p = P0.pods[pi];                 // block-uniform: scalar loads
+  const PodPlan pp = P0.plans[pi];
+  const UseMasks& m = pp.m;
+  const ksim_topo_use* U = P.uses + p.use_first;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
@@ -907,10 +927,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   if (fuse_ext) {                                  // block-uniform
     nf = win->nfeas;
     kend = ss.n;
-    soft = soft_use(P.uses, p.use_count);
+    soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;   // the pod's one ScheduleAnyway use
     has_soft = nf > 1 && soft >= 0;
     if (has_soft) {                                // topologyNormalizingWeight of the one soft use
-      const ksim_topo_use& u = P.uses[soft];
+      const ksim_topo_use u = load_use(U, soft);
       int32_t size = 0;
       if (u.flags & KSIM_USEF_HOSTNAME) {
         size = nf - win->nign;
@@ -959,8 +979,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
         if (fuse_ext && kind == kNormPTS) {
           raw = 0;
           if (has_soft) {                          // counts -> scores (a non-decreasing map)
-            const int32_t ms = P.uses[soft].arg;
-            if (!ign) raw = soft_score(soft_count(c, s, P.uses[soft], soft, node), w_soft, ms);
+            const int32_t ms = load_use(U, soft).arg;
+            // the filter pass left the node's count in the slot (the domain
+            // tables are being re-zeroed by this kernel)
+            if (!ign) raw = soft_score(s.raw[(size_t)k * N + node], w_soft, ms);
             if (win->ext[2 * k]) gmax = soft_score(gmax, w_soft, ms);
             if (win->ext[2 * k + 1]) gmin = soft_score(gmin, w_soft, ms);
           }
@@ -1002,13 +1024,20 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       }
     }
     // the domain tables are read no more this cycle: re-zero what this node's
-    // values touched (every touched entry is some node's value)
-    for (int i = 0; i < p.use_count; i++) {
-      const ksim_topo_use u = P.uses[p.use_first + i];
-      if (!use_needs_dom(u)) continue;
-      s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
+    // values touched (every touched entry is some node's value); small tables
+    // are cleared whole by block 0 below
+    for (uint32_t b = m.dom; b; b &= b - 1) {
+      const int i = __builtin_ctz(b);
+      const ksim_topo_use u = load_use(U, i);
+      if (c.col_nvals[u.col] > kLdsDom) s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
     }
   }
+  if (blockIdx.x == 0)
+    for (uint32_t b = m.dom; b; b &= b - 1) {
+      const int i = __builtin_ctz(b);
+      const int32_t V = c.col_nvals[load_use(U, i).col];
+      if (V <= kLdsDom && tid < V) s.dom[(size_t)i * c.vmax + tid] = 0;
+    }
   // selectHost: the block's best (total, TB) pair -> its record (k_bind reduces the records)
   wave_best2(img, tlo);
   if (lane == 0) {
@@ -1023,60 +1052,20 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     s.bbest[2 * blockIdx.x] = bi;
     s.bbest[2 * blockIdx.x + 1] = bl;
   }
-}
-
-// selectHost over k_select's per-block records (one wave): the winning TB lo
-// word (0: no kept node).
-__device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32_t n_blocks) {
-  const int lane = threadIdx.x & 63;
-  uint64_t img = 0, lo = 0;
-  for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
-  wave_best2(img, lo);
-  return lo;
-}
-
-// NOWIN also returns the counters and extrema slots to zero for the next
-// cycle (k_window resets its own otherwise; k_topo_prefilter clears the
-// registration rows).
-template <bool NOWIN>
-__global__ __launch_bounds__(64) void k_bind(DevCluster c, DevPods P, DevState* __restrict__ st, DevScratch s,
-                                             int32_t* __restrict__ chosen_out) {
-  const int32_t pi = st->cursor;
-  if (pi >= st->end) return;
-  WinState* win = s.win;
-  const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);
-  if (threadIdx.x != 0) return;
-  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, error = win->error;
-  const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
-  const ksim_pod& p = P.pods[pi];
-  // nextStartNodeIndex = (nextStartNodeIndex + processed) % len(scanned nodes);
-  // a pod PreFilter rejected scans nothing and leaves it
-  const int32_t ns = NS > 0 ? (int32_t)(((int64_t)st->next_start + (cut < NS ? cut : NS)) % NS) : st->next_start;
-  st->next_start = ns;
-  st->evals += win->evaluated;
-  if (chosen >= 0) {
-    assume_pod(c, P, p, chosen, 1);
-    st->scheduled += 1;
-  } else {
-    st->unschedulable += 1;
+  if (bind_mode) {
+    // the last block: its acquire sees every block's record (and block 0's
+    // window fields) released by their own increments
+    __shared__ int32_t s_last;
+    if (tid == 0) {
+      const int32_t done = __hip_atomic_fetch_add(&win->done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = done == (int32_t)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_last && tid < 64) {
+      if (tid == 0) win->done = 0;
+      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2);
+    }
   }
-  if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : error ? KSIM_CHOSEN_ERROR : -1;
-  st->chosen = chosen >= 0 ? chosen : error ? KSIM_CHOSEN_ERROR : -1;
-  st->status = chosen >= 0 ? KSIM_STATUS_SCHEDULED : error ? KSIM_STATUS_ERROR : KSIM_STATUS_UNSCHEDULABLE;
-  win->error = 0;
-  st->n_feasible = nf;
-  st->n_evaluated = win->evaluated;
-  st->n_processed = cut < NS ? cut : NS;
-  st->k_to_find = win->k;
-  st->next_start_after = ns;
-  st->pod_seq += 1;
-  st->topo_flags = 0;
-  if (NOWIN) {
-    win->nfeas = 0;
-    win->nign = 0;
-    for (int t = 0; t < kExtWords; t++) win->ext[t] = 0;
-  }
-  st->cursor = pi + 1;
 }
 
 __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int sign) {
@@ -1389,9 +1378,9 @@ void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent
   if (evs) (void)hipEventRecord(evs[4], stream);
   if (!fx) k_extrema<NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[5], stream);
-  k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, fx);
+  // the last k_select block binds (no k_bind launch)
+  k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, fx, NOWIN ? 2 : 1, a.chosen);
   if (evs) (void)hipEventRecord(evs[6], stream);
-  k_bind<NOWIN><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
   if (evs) (void)hipEventRecord(evs[7], stream);
 }
 
@@ -1424,8 +1413,7 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
   k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0);
-  k_bind<false><<<1, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 1, a.chosen);
 }
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {
@@ -1462,7 +1450,7 @@ void launch_pshard_extrema(const LaunchArgs& a, bool soft, hipStream_t stream) {
 
 void launch_pshard_select(const LaunchArgs& a, hipStream_t stream) {
   const int blocks = (a.c.n + 255) / 256;
-  k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0);
+  k_select<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 0, nullptr);
   k_best_pack<<<1, 64, 0, stream>>>(a.c, a.st, a.s);
 }
 

@@ -40,6 +40,9 @@ for _p in (ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd")):
 B_EVAL = 112            # algorithmic HBM bytes per pod x node evaluation
 B_FILTER = 60           # the filter columns of a row: allocatable 28 + requested 24 + pods 4 + flags 4
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 vector instruction holds a SIMD
+# for 2 cycles (MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz
+VALU_PEAK_G = 256 * 4 * 0.5 * 2.4          # G wave-instructions / s
 
 
 def _k_adapt(n: int) -> int:
@@ -63,7 +66,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
         return n_nodes * (1 + 8 * n_norm)             # fail code + normalized raws
     if name == "k_select":
         return n_nodes * (1 + 8 + 8 * n_norm)         # fail code + partial total + normalized raws
-    if name == "k_batch_eval":
+    if name in ("k_batch_top", "k_batch_eval"):
         return B_EVAL * n_nodes * B                   # B pods x N nodes evals per launch
     if name == "k_batch_merge":
         return 8 * B * (tiles * geom["tile_cand"] + T)
@@ -81,7 +84,33 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 
 
 # the kernel that carries the pod x node evaluations on each path
-EVAL_KERNELS = ("k_batch_eval", "k_adapt_top", "k_filter_score")
+EVAL_KERNELS = ("k_batch_top", "k_batch_eval", "k_adapt_top", "k_filter_score")
+
+
+def _profile_entry(fname: str, kernel: str, nodes: int):
+    """The committed PMC measurement (profiles/<fname>) of a kernel at a size."""
+    path = os.path.join(ROOT, "profiles", fname)
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for entry in (tj if isinstance(tj, list) else [tj]):
+        if isinstance(entry, dict) and entry.get("kernel") == kernel and entry.get("nodes") == nodes:
+            return entry
+    return None
+
+
+def host_cpu() -> dict:
+    """What the CPU baseline ran on: logical CPUs and the model name."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
 
 
 def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) -> dict:
@@ -98,7 +127,7 @@ def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) ->
     _, st2 = o.schedule(pods, 100, n, nthreads=threads)
     dt2 = time.perf_counter() - t
     return {"value": st2.evals / dt2, "unit": "pod x node evals/s", "cores": threads, "kind": "port",
-            "pods_per_s": n / dt2,
+            "pods_per_s": n / dt2, "host": host_cpu(),
             "sample": f"{label} pods 100..{100 + n} ({n} cycles, {st2.evals} evals) after 100 warm cycles "
                       f"from the empty cluster, same profile/mode, oracle/ksim_oracle.c OpenMP {threads} threads, "
                       f"{dt2:.1f} s"}
@@ -288,16 +317,19 @@ def main():
     except engine.KsimError:
         pass
     achieved = alg / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            for entry in (tj if isinstance(tj, list) else [tj]):    # PMC measurements, by kernel and size
-                if entry.get("kernel") == dominant and entry.get("nodes") == knodes:
-                    traffic = entry.get("hbm_bytes_per_launch")
-        except (OSError, ValueError, AttributeError):
-            traffic = None
+    # PMC measurements committed under profiles/ (by kernel and size): HBM
+    # bytes per launch (traffic.json) and vector instructions per launch
+    # (valu.json), priced with this run's launch time
+    te = _profile_entry("traffic.json", dominant, knodes)
+    traffic = te.get("hbm_bytes_per_launch") if te else None
+    ve = _profile_entry("valu.json", dominant, knodes)
+    valu = None
+    if ve and ve.get("valu_insts_per_launch"):
+        g = ve["valu_insts_per_launch"] / (avg_ms * 1e-3) / 1e9
+        valu = {"achieved": g, "peak": VALU_PEAK_G, "unit": "G wave-instructions/s", "frac": g / VALU_PEAK_G,
+                "valu_insts_per_launch": ve["valu_insts_per_launch"],
+                "salu_insts_per_launch": ve.get("salu_insts_per_launch"),
+                "valu_insts_per_eval_lane": ve.get("valu_insts_per_eval_lane"), "source": ve.get("source")}
 
     seeds = {2: "0x4B53494D0002", 3: "0x4B53494D0003", 4: "0x4B53494D0004", 5: "0x4B53494D0002/0005"}
     result = {
@@ -325,11 +357,12 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg, "avg_launch_ms": avg_ms, "timing": timing, "kernel_nodes": knodes,
-                     "dominant_by_time": by_time,
+                     "dominant_by_time": by_time, "valu": valu,
                      "note": ("algorithmic bytes = 112 B per pod x node evaluation (SURVEY 8(d)); the node table "
                               "stays in L2 while the launch's pods sweep it, so HBM traffic ('traffic', PMC) is far "
                               "below the algorithmic bytes and frac can exceed 1; the kernel is bound by its "
-                              "int64/f64 VALU work (profiles/README)")},
+                              "int64/f64 vector work: 'valu' prices its PMC instruction count against the VALU "
+                              "issue peak (profiles/README)")},
         "batch_geometry": geom,
     }
     if cfg == 2 and world == 1 and args.mode == "p100" and not args.no_adapt:

@@ -1775,6 +1775,8 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   if ((rc = set_run(h, first, end))) return rc;
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = batch && run_fast(h, first, end);
+  a.fuse_min = !batch && h->topo[first] && h->hard_small[first];
+  a.fuse_ext = !batch && h->soft_le1[first];
   auto launch = [&] {
     if (batch) launch_batch_eval_only(a, h->stream);
     else launch_filter_only(a, h->stream);
@@ -1788,7 +1790,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   float ms = 0;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
   *avg_ms = ms / reps;
-  if (kernel) *kernel = batch ? kKernelsPerCycle : 2;   // k_batch_eval / k_filter_score
+  // the timed no-window filter passes added into the window counters
+  if (!batch) HIPCHK(h, hipMemset(h->sc.win, 0, sizeof(WinState)));
+  if (kernel) *kernel = batch ? kKernelsPerCycle : 2;   // k_batch_top / k_filter_score
   return KSIM_OK;
 }
 
@@ -1825,6 +1829,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
     const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
     int32_t cursor = lo;
+    uint32_t launched = (1u << per) - 1;         // batch paths launch every kernel of a batch
     while (cursor < hi) {
       const int32_t iters = batch ? std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods) : std::min(512, hi - cursor);
       std::vector<hipEvent_t> evs((size_t)iters * (per + 1));
@@ -1836,7 +1841,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
         else if (batch)
           launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else
-          launch_cycle(a, h->stream, false, topo, &evs[(size_t)i * (per + 1)]);
+          launched = launch_cycle(a, h->stream, false, topo, &evs[(size_t)i * (per + 1)]);
       }
       HIPCHK(h, hipGetLastError());
       DevState st;
@@ -1845,6 +1850,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
       const int32_t did = batch ? std::min<int32_t>(iters, st.batches) : std::min(iters, st.cursor - cursor);
       for (int32_t i = 0; i < did; i++)
         for (int k = 0; k < per; k++) {
+          if (!((launched >> k) & 1u)) continue;   // an empty event pair, not a kernel
           float ms = 0;
           const size_t b = (size_t)i * (per + 1);
           HIPCHK(h, hipEventElapsedTime(&ms, evs[b + k], evs[b + k + 1]));

@@ -59,7 +59,9 @@ extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 // evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.
 // topo: the pod may carry PodTopologySpread / InterPodAffinity uses (adds the
 // two topology kernels; they exit at once for a pod without uses).
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
+// Returns the kernel slots it launched (bit k: kernel k of the cycle), so a
+// timing run counts only those.
+uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.

@@ -1364,40 +1364,46 @@ const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_
                                                     "k_window", "k_extrema", "k_select", "k_bind"};
 
 template <bool COMPAT, bool NOWIN>
-void launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent_t* evs) {
+uint32_t launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipEvent_t* evs) {
+  uint32_t mask = 0;
   const int blocks = (a.c.n + 255) / 256;
   if (evs) (void)hipEventRecord(evs[0], stream);
   if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (topo) mask |= 1u << 0;
   if (evs) (void)hipEventRecord(evs[1], stream);
   if (topo && !a.fuse_min) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (topo && !a.fuse_min) mask |= 1u << 1;
   if (evs) (void)hipEventRecord(evs[2], stream);
   const int32_t fx = NOWIN && !COMPAT && a.fuse_ext;   // extrema in the filter pass, no k_extrema
   k_filter_score<COMPAT, NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, topo && a.fuse_min, fx);
+  mask |= 1u << 2;
   if (evs) (void)hipEventRecord(evs[3], stream);
   if (!NOWIN) k_window<COMPAT><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (!NOWIN) mask |= 1u << 3;
   if (evs) (void)hipEventRecord(evs[4], stream);
   if (!fx) k_extrema<NOWIN><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (!fx) mask |= 1u << 4;
   if (evs) (void)hipEventRecord(evs[5], stream);
   // the last k_select block binds (no k_bind launch)
   k_select<COMPAT><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, fx, NOWIN ? 2 : 1, a.chosen);
+  mask |= 1u << 5;
   if (evs) (void)hipEventRecord(evs[6], stream);
   if (evs) (void)hipEventRecord(evs[7], stream);
+  return mask;
 }
 
 // K = N (percentageOfNodesToScore >= 100 or fewer than 100 nodes): no
 // window, so the window state comes from the filter pass (no k_window).
 // NetworkBandwidth's error statuses are resolved in k_window, so its profiles
 // always take the windowed cycle.
-void launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
+uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs) {
   const bool nowin = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n) >= a.c.n &&
                      !prof_has_filter(a.prof, KSIM_PL_NETWORK_BANDWIDTH) &&
                      !prof_has_score(a.prof, KSIM_PL_NETWORK_BANDWIDTH);
   if (compat) {
-    if (nowin) launch_cycle_t<true, true>(a, stream, topo, evs);
-    else launch_cycle_t<true, false>(a, stream, topo, evs);
+    return nowin ? launch_cycle_t<true, true>(a, stream, topo, evs) : launch_cycle_t<true, false>(a, stream, topo, evs);
   } else {
-    if (nowin) launch_cycle_t<false, true>(a, stream, topo, evs);
-    else launch_cycle_t<false, false>(a, stream, topo, evs);
+    return nowin ? launch_cycle_t<false, true>(a, stream, topo, evs) : launch_cycle_t<false, false>(a, stream, topo, evs);
   }
 }
 
@@ -1417,8 +1423,16 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
 }
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {
-  // the window-free variant writes counters: time the windowed one (same work per node)
-  k_filter_score<false, false><<<(a.c.n + 255) / 256, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, 0, 0);
+  // the variant the cycle launches (launch_cycle_t); the no-window one adds
+  // into the window counters, which the caller clears afterwards
+  const int blocks = (a.c.n + 255) / 256;
+  const bool nowin = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n) >= a.c.n &&
+                     !prof_has_filter(a.prof, KSIM_PL_NETWORK_BANDWIDTH) &&
+                     !prof_has_score(a.prof, KSIM_PL_NETWORK_BANDWIDTH);
+  if (nowin)
+    k_filter_score<false, true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, a.fuse_min, a.fuse_ext);
+  else
+    k_filter_score<false, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, a.fuse_min, 0);
 }
 
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream) {

@@ -147,6 +147,10 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
 // (complete when it lists every kept node).  Each wave keeps its lanes' best T
 // keys and extracts its own top-T; wave 0 merges the four lists.  Pods past
 // the exact windows get an empty incomplete list, which ends the chain there.
+// SH (node-sharded): amask / awin are global (n_total nodes); the block scores
+// the kept nodes this shard holds and writes the pod's record (xsend: its T
+// best keys and count | complete << 32) for the all-gather instead of topk.
+template <bool SH>
 __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
@@ -154,7 +158,8 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
                                                    const int32_t* __restrict__ awin,
                                                    const int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
                                                    int32_t* __restrict__ topk_cnt,
-                                                   int32_t* __restrict__ topk_complete) {
+                                                   int32_t* __restrict__ topk_complete,
+                                                   uint64_t* __restrict__ xsend) {
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_top[4][kTopT];
@@ -164,13 +169,15 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   const int32_t base = st->cursor;
   if (j >= min(kBatchPods, st->end - base)) return;   // block-uniform
   if (j >= *aexact) {
-    if (tid == 0) {
+    if (SH) {
+      if (tid <= kTopT) xsend[(size_t)j * kXRec + tid] = 0;   // empty, incomplete
+    } else if (tid == 0) {
       topk_cnt[j] = 0;
       topk_complete[j] = 0;
     }
     return;
   }
-  const int32_t n = c.n, s = awin[2 * j], cut = awin[2 * j + 1];
+  const int32_t n = SH ? c.n_total : c.n, s = awin[2 * j], cut = awin[2 * j + 1];
   const int32_t kend = cut >= 0 ? cut : n;
   const int32_t pi = base + j;
   const ksim_pod& p = P.pods[pi];
@@ -180,16 +187,35 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
 #pragma unroll
   for (int t = 0; t < kTopT; t++) a[t] = 0;
   int32_t kept = 0;
+  if (SH) {
+    // the window [s, s + kend) (circular, global) as two linear pieces, each
+    // clipped to this shard's [base, base + c.n)
+    const int32_t lo = c.base, hi = c.base + c.n;
+    const int32_t e1 = s + kend <= n ? s + kend : n, e2 = s + kend <= n ? 0 : s + kend - n;
+    const int32_t a0 = max(s, lo), a1 = min(e1, hi), b0 = max(0, lo), b1 = min(e2, hi);
+    const int32_t len1 = a1 > a0 ? a1 - a0 : 0, len2 = b1 > b0 ? b1 - b0 : 0;
 #pragma unroll 1
-  for (int32_t off = tid; off < kend; off += 256) {
-    int32_t node = s + off;
-    if (node >= n) node -= n;
-    if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
-    kept++;
-    const NodeRow r = load_res_row(c, node);      // scores read the resource columns only
-    a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
+    for (int32_t i = tid; i < len1 + len2; i += 256) {
+      const int32_t g = i < len1 ? a0 + i : b0 + (i - len1);
+      if (!((mask[g >> 6] >> (g & 63)) & 1ull)) continue;
+      kept++;
+      const NodeRow r = load_res_row(c, g - c.base);
+      a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
 #pragma unroll
-    for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+      for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+    }
+  } else {
+#pragma unroll 1
+    for (int32_t off = tid; off < kend; off += 256) {
+      int32_t node = s + off;
+      if (node >= n) node -= n;
+      if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
+      kept++;
+      const NodeRow r = load_res_row(c, node);      // scores read the resource columns only
+      a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
+#pragma unroll
+      for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+    }
   }
   // per wave: a lane can be popped at most T times and holds its T best, so
   // the wave's top-T is exact
@@ -219,6 +245,12 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
     if (key == m) key = 0;
   }
   const int32_t total = s_kept[0] + s_kept[1] + s_kept[2] + s_kept[3];
+  if (SH) {
+    uint64_t* x = xsend + (size_t)j * kXRec;
+    if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
+    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)cnt | ((uint64_t)(total <= kTopT ? 1 : 0) << 32);
+    return;
+  }
   if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
   if (lane == 0) {
     topk_cnt[j] = cnt;
@@ -226,6 +258,9 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   }
 }
 
+// SH: windows and bitmaps are global; a shard scores only the guesses on its
+// own nodes; pmax[kBatchPods + j] carries the broken flag (all-reduced with M).
+template <bool SH>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P,
                                                             const ksim_profile* __restrict__ prof_p,
                                                             const BatchProg* __restrict__ bp_p,
@@ -251,8 +286,9 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
     const uint64_t gk = gkey[k];
     const int32_t node = gk ? key_node(gk) - c.base : -1;
     if (node >= 0 && node < c.n) {
-      const int32_t n = c.n, s = awin[2 * j], cut = awin[2 * j + 1];
-      int32_t off = node - s;
+      const int32_t g = node + c.base;              // global position (== node unsharded)
+      const int32_t n = SH ? c.n_total : c.n, s = awin[2 * j], cut = awin[2 * j + 1];
+      int32_t off = g - s;
       if (off < 0) off += n;
       const int32_t kend = cut >= 0 ? cut : n;
       if (off < kend || off == cut) {
@@ -260,7 +296,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         row_add_pod(r, P.pods[base + k], 1);
         const ksim_pod& p = P.pods[base + j];
         const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
-        const bool was = (amask[(size_t)j * n_words + (node >> 6)] >> (node & 63)) & 1ull;
+        const bool was = (amask[(size_t)j * n_words + (g >> 6)] >> (g & 63)) & 1ull;
         if (cut >= 0 && was && !now) brk = true;
         if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base);
       }
@@ -274,10 +310,12 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
     uint64_t m = 0;
     for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
     pmax[j] = j < nchain ? m : 0;
-    abroken[j] = j < nchain && any_brk ? 1 : 0;
+    if (SH) pmax[kBatchPods + j] = j < nchain && any_brk ? 1 : 0;
+    else abroken[j] = j < nchain && any_brk ? 1 : 0;
   }
 }
 
+// abroken null (sharded): the broken flags follow M in pmax[kBatchPods + j].
 __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ gkey,
                                                              const int32_t* __restrict__ chain_end,
@@ -287,7 +325,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
                                                              int32_t* __restrict__ chosen_out) {
   __shared__ int32_t s_fb, s_istar, s_sched, s_unsched;
   const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
-  const int32_t brk = abroken[threadIdx.x];
+  const int32_t brk = abroken ? abroken[threadIdx.x] : (int32_t)pmax[kBatchPods + threadIdx.x];
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
   const int32_t nchain0 = *chain_end;
   if (threadIdx.x == 0) s_fb = nchain0;
@@ -308,17 +346,65 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_adapt_top<<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
-                                                  a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete);
+  k_adapt_top<false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
+                                                         a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr);
   if (evs) (void)hipEventRecord(evs[3], stream);
   launch_chain(a, stream);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_adapt_pairs<<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
-                                                       a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
+  k_adapt_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
+                                                              a.s.awin, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
   if (evs) (void)hipEventRecord(evs[5], stream);
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,
                                                a.s.awin, a.chosen);
   if (evs) (void)hipEventRecord(evs[6], stream);
+}
+
+// ---- node-sharded ADAPT batch -----------------------------------
+// Shards hold 64-aligned node ranges (adapt_shard_chunk), so shard r's bitmap
+// words are the global words [r * W, r * W + W).  Per batch: every shard's
+// S0 bitmaps of its own nodes are all-gathered ([R][B][W] words) and unpacked
+// into the global bitmap; the windows follow from it identically on every
+// shard; each shard lists the top-T of the kept nodes it holds (a record as
+// on the P100 path), the records are all-gathered and merged, the chain runs;
+// each shard scores the guesses on its nodes (pair keys and broken flags),
+// those are all-reduced (max) and every shard commits, binding its own nodes.
+__global__ __launch_bounds__(256) void k_adapt_unpack(const DevState* __restrict__ st,
+                                                      const uint64_t* __restrict__ recv, int32_t W, int32_t nw,
+                                                      uint64_t* __restrict__ amask) {
+  const int32_t j = blockIdx.y;
+  const int32_t base = st->cursor;
+  if (base + j >= min(st->end, base + kBatchPods)) return;   // block-uniform
+  for (int32_t w = blockIdx.x * 256 + threadIdx.x; w < nw; w += gridDim.x * 256) {
+    const int32_t r = w / W;
+    amask[(size_t)j * nw + w] = recv[((size_t)r * kBatchPods + j) * W + (w - r * W)];
+  }
+}
+
+void launch_adapt_sh_mask(const LaunchArgs& a, uint64_t* send, int32_t W, hipStream_t stream) {
+  k_adapt_mask<<<dim3((W + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st, send, W);
+}
+
+void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W, uint64_t* gmask,
+                            hipStream_t stream) {
+  const int32_t N = a.c.n_total, nw = (N + 63) / 64;
+  const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
+  k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
+  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
+  k_adapt_top<true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin, a.s.aexact,
+                                                        a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend);
+}
+
+void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream) {
+  const int32_t nw = (a.c.n_total + 63) / 64;
+  k_batch_gmerge_launch(a, world, stream);
+  launch_chain(a, stream);
+  k_adapt_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
+                                                             a.s.gkey, a.s.chain_end, a.s.pmax, nullptr);
+}
+
+void launch_adapt_sh_commit(const LaunchArgs& a, hipStream_t stream) {
+  k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, nullptr, a.s.awin,
+                                               a.chosen);
 }
 
 }  // namespace ksim

@@ -717,6 +717,10 @@ void launch_chain(const LaunchArgs& a, hipStream_t stream) {
 
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) { launch_eval_top(a, a.s.xsend, stream); }
 
+void k_batch_gmerge_launch(const LaunchArgs& a, int32_t world, hipStream_t stream) {
+  k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
+                                                     a.s.topk_complete);
+}
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {
   k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
                                                      a.s.topk_complete);

@@ -7,6 +7,19 @@
 
 namespace ksim {
 
+// Nodes of the circular scan window [s, s + len) of the cluster's n_total
+// nodes that lie on this snapshot ([base, base + n)): the evaluations a shard
+// ran for the window (all of them on an unsharded handle).
+__device__ __forceinline__ int64_t window_local(const DevCluster& c, int32_t s, int64_t len) {
+  const int64_t N = c.n_total, lo = c.base, hi = (int64_t)c.base + c.n;
+  auto ov = [&](int64_t a, int64_t b) -> int64_t {   // |[a, b) n [lo, hi)|
+    const int64_t x = a > lo ? a : lo, y = b < hi ? b : hi;
+    return y > x ? y - x : 0;
+  };
+  if (s + len <= N) return ov(s, s + len);
+  return ov(s, N) + ov(0, s + len - N);
+}
+
 // Validate the chain against M (pmax) and commit (one block of kBatchPods
 // threads).  Binds are applied by the shard that owns the node.  awin (ADAPT
 // batch, unsharded): per pod {scan start, cut offset or -1}; the evaluated
@@ -49,13 +62,13 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   }
   if (awin && tid < committed) {
     const int32_t cut = awin[2 * tid + 1];
-    atomicAdd(&s_evals, cut >= 0 ? cut + 1 : c.n);
+    atomicAdd(&s_evals, (int32_t)window_local(c, awin[2 * tid], cut >= 0 ? (int64_t)cut + 1 : c.n_total));
   }
   __syncthreads();
   if (tid == 0) {
-    if (awin) {
+    if (awin && committed > 0) {
       const int32_t cut = awin[2 * (committed - 1) + 1];
-      st->next_start = (int32_t)(((int64_t)awin[2 * (committed - 1)] + (cut >= 0 ? cut : c.n)) % c.n);
+      st->next_start = (int32_t)(((int64_t)awin[2 * (committed - 1)] + (cut >= 0 ? cut : c.n_total)) % c.n_total);
       st->evals += s_evals;
     } else {
       st->evals += (int64_t)committed * c.n;

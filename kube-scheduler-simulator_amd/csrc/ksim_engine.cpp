@@ -141,6 +141,11 @@ struct ksim_handle {
   hipGraphExec_t graph_cycle[8] = {};
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
+  // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
+  // the global bitmap (allocated at the first such run)
+  std::vector<DevBuf> ash_bufs;
+  uint64_t *ash_send = nullptr, *ash_recv = nullptr, *ash_gmask = nullptr;
+  int32_t ash_world = 0, ash_w = 0;
   int64_t graph_captures = 0;                  // graphs captured since ksim_create (ksim_get_diag)
 };
 
@@ -461,13 +466,14 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
 
 // Split [first, first+count) into maximal same-path runs (batch / per-pod,
 // per-pod runs further by whether a pod carries topology uses).
+// adapt_sharded: sharded handles whose shards follow adapt_shard_chunk, so
+// ADAPT may take the sharded batch path (otherwise it runs cycle by cycle).
 template <typename F>
-int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn) {
+int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn, bool adapt_sharded = false) {
   int32_t i = first;
   const int32_t end = first + count;
   while (i < end) {
-    // the ADAPT batch path is unsharded: sharded ADAPT runs cycle by cycle
-    const bool batch_ok = !(adapt_mode(h) && is_sharded(h));
+    const bool batch_ok = !(adapt_mode(h) && is_sharded(h)) || adapt_sharded;
     const bool b = batch_ok && h->batchable[i] != 0;
     const bool t = h->topo[i] != 0;
     int32_t j = i + 1;
@@ -633,13 +639,120 @@ int shard_run_perpod(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) 
   return KSIM_OK;
 }
 
+// ---- node-sharded ADAPT batch path (ksim_adapt.hip "node-sharded ADAPT batch") ----
+// The shard layout it needs: R shards of chunk = ceil(ceil(N / R) / 64) * 64
+// nodes each (the last one the rest, non-empty), in order (ksim/shard.py
+// partition follows it whenever it can).
+int32_t adapt_shard_chunk(int32_t n_total, int32_t world) {
+  const int32_t q = (n_total + world - 1) / world;
+  return (q + 63) / 64 * 64;
+}
+
+bool adapt_shard_layout(const std::vector<ksim_handle*>& hs) {
+  const ksim_handle* h0 = hs[0];
+  const int32_t world = h0->comm ? h0->world : (int32_t)hs.size();
+  const int32_t N = h0->dc.n_total, chunk = adapt_shard_chunk(N, world);
+  if ((int64_t)(world - 1) * chunk >= N) return false;
+  for (size_t i = 0; i < hs.size(); i++) {
+    const int32_t r = h0->comm ? h0->rank : (int32_t)i;
+    const int32_t base = r * chunk, n = std::min(chunk, N - base);
+    if (hs[i]->dc.base != base || hs[i]->dc.n != n) return false;
+  }
+  return true;
+}
+
+int adapt_shard_buffers(ksim_handle* h, int32_t world, int32_t W) {
+  if (h->ash_world == world && h->ash_w == W) return KSIM_OK;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  free_bufs(h->ash_bufs);
+  const size_t nw = (size_t)(h->dc.n_total + 63) / 64;
+  void* p = nullptr;
+  int rc;
+  if ((rc = upload(h, h->ash_bufs, nullptr, 8 * (size_t)kBatchPods * W, &p))) return rc;
+  h->ash_send = (uint64_t*)p;
+  if ((rc = upload(h, h->ash_bufs, nullptr, 8 * (size_t)world * kBatchPods * W, &p))) return rc;
+  h->ash_recv = (uint64_t*)p;
+  if ((rc = upload(h, h->ash_bufs, nullptr, 8 * (size_t)kBatchPods * nw, &p))) return rc;
+  h->ash_gmask = (uint64_t*)p;
+  h->ash_world = world;
+  h->ash_w = W;
+  return KSIM_OK;
+}
+
+// One ADAPT batch on every shard of a group (exchanges: bitmaps, records, M).
+int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+  const int R = (int)hs.size();
+  ksim_handle* h0 = hs[0];
+  const int32_t world = h0->comm ? h0->world : R;
+  const int32_t W = adapt_shard_chunk(h0->dc.n_total, world) / 64;
+  const size_t mw = (size_t)kBatchPods * W;                   // bitmap words per shard
+  for (auto* h : hs) launch_adapt_sh_mask(make_args(h, h->dp, h->d_chosen), h->ash_send, W, stream);
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->ash_send, h0->ash_recv, mw, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+  } else {
+    for (int src = 0; src < R; src++)
+      for (int dst = 0; dst < R; dst++)
+        HIPCHK(h0, hipMemcpyAsync(hs[dst]->ash_recv + (size_t)src * mw, hs[src]->ash_send, 8 * mw,
+                                  hipMemcpyDeviceToDevice, stream));
+  }
+  for (auto* h : hs) launch_adapt_sh_window(make_args(h, h->dp, h->d_chosen), h->ash_recv, W, h->ash_gmask, stream);
+  const size_t rec = (size_t)kBatchPods * kXRec;
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+  } else {
+    for (int src = 0; src < R; src++)
+      for (int dst = 0; dst < R; dst++)
+        HIPCHK(h0, hipMemcpyAsync(hs[dst]->sc.xrecv + (size_t)src * rec, hs[src]->sc.xsend, 8 * rec,
+                                  hipMemcpyDeviceToDevice, stream));
+  }
+  for (auto* h : hs) launch_adapt_sh_pairs(make_args(h, h->dp, h->d_chosen), h->ash_gmask, world, stream);
+  int rc;
+  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.pmax; }, 2 * kBatchPods, true, stream))) return rc;
+  for (auto* h : hs) launch_adapt_sh_commit(make_args(h, h->dp, h->d_chosen), stream);
+  HIPCHK(h0, hipGetLastError());
+  return KSIM_OK;
+}
+
+// Pods [a, b) on the sharded ADAPT batch path.
+int shard_run_adapt(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
+  ksim_handle* h0 = hs[0];
+  hipStream_t stream = h0->stream;
+  const int32_t world = h0->comm ? h0->world : (int32_t)hs.size();
+  const int32_t W = adapt_shard_chunk(h0->dc.n_total, world) / 64;
+  for (auto* h : hs) {
+    int rc;
+    if ((rc = adapt_shard_buffers(h, world, W))) return rc;
+    if ((rc = set_run(h, a, b))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  int32_t cursor = a;
+  while (cursor < b) {
+    const int32_t n = std::max(1, (b - cursor) / kBatchPods);
+    for (int32_t i = 0; i < n; i++) {
+      int rc = shard_batch_adapt(hs, stream);
+      if (rc) return rc;
+    }
+    DevState st;
+    HIPCHK(h0, hipMemcpyAsync(&st, h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));
+    HIPCHK(h0, hipStreamSynchronize(stream));
+    if (st.cursor <= cursor) return set_err(h0, KSIM_E_DEVICE, "sharded ADAPT batch path made no progress");
+    cursor = st.cursor;
+  }
+  return KSIM_OK;
+}
+
 // A sharded run: batchable stretches on the batch protocol, the rest cycle by cycle.
 int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t count) {
   if (profile_nb(hs[0]->prof))
     return set_err(hs[0], KSIM_E_UNSUPPORTED, "NetworkBandwidth profiles run on unsharded handles");
+  const bool adapt = adapt_mode(hs[0]);
+  const bool adapt_batch = adapt && adapt_shard_layout(hs);
   return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool) {
-    return batch ? shard_run(hs, a, b) : shard_run_perpod(hs, a, b);
-  });
+    if (!batch) return shard_run_perpod(hs, a, b);
+    return adapt ? shard_run_adapt(hs, a, b) : shard_run(hs, a, b);
+  }, adapt_batch);
 }
 
 
@@ -705,6 +818,7 @@ void ksim_destroy(ksim_handle* h) {
   if (h->comm && rccl().ok) (void)rccl().comm_destroy(h->comm);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
+  free_bufs(h->ash_bufs);
   free_bufs(h->pod_bufs);
   free_bufs(h->pod1_bufs);
   free_bufs(h->pre_bufs);
@@ -836,6 +950,9 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   drop_graphs(h);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
+  free_bufs(h->ash_bufs);
+  h->ash_send = h->ash_recv = h->ash_gmask = nullptr;
+  h->ash_world = h->ash_w = 0;
   free_bufs(h->pod_bufs);
   h->pod_buf_bytes.clear();
   h->dp = DevPods{};
@@ -993,7 +1110,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.chain_end, int32_t*, 4);
-  SCR(s.pmax, uint64_t*, 8 * (size_t)kBatchPods);
+  SCR(s.pmax, uint64_t*, 8 * 2 * (size_t)kBatchPods);   // [M | sharded ADAPT broken flags]
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
   SCR(s.dbg, unsigned long long*, 8 * 16);
   SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);

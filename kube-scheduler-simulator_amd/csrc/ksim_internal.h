@@ -98,6 +98,15 @@ void launch_filter_only(const LaunchArgs& a, hipStream_t stream);
 //   (all-reduce max s.pmax)
 //   launch_shard_commit  validate + commit (owner shard binds)
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream);
+// records all-gathered in s.xrecv ([world][kBatchPods][kXRec]) -> per-pod global top-T
+void k_batch_gmerge_launch(const LaunchArgs& a, int32_t world, hipStream_t stream);
+// node-sharded ADAPT batch (ksim_adapt.hip): shard bitmaps of W words per pod
+// -> all-gather -> windows + this shard's records -> all-gather -> chain +
+// pairs (s.pmax: [M | broken]) -> all-reduce (max) -> commit
+void launch_adapt_sh_mask(const LaunchArgs& a, uint64_t* send, int32_t W, hipStream_t stream);
+void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W, uint64_t* gmask, hipStream_t stream);
+void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream);
+void launch_adapt_sh_commit(const LaunchArgs& a, hipStream_t stream);
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream);
 void launch_shard_commit(const LaunchArgs& a, hipStream_t stream);
 void launch_group_max(const GroupPtrs& g, hipStream_t stream);

@@ -11,10 +11,23 @@ from __future__ import annotations
 from typing import List, Tuple
 
 
+def adapt_chunk(n_total: int, world: int) -> int:
+    """Shard size of the 64-aligned layout: ceil(ceil(N / R) / 64) * 64 nodes
+    (the engine's adapt_shard_chunk; the last shard holds the rest)."""
+    q = -(-n_total // world)
+    return -(-q // 64) * 64
+
+
 def partition(n_total: int, world: int) -> List[Tuple[int, int]]:
-    """Contiguous (base, count) per rank; the first n_total % world ranks get one more."""
+    """Contiguous (base, count) per rank.  The 64-aligned layout (adapt_chunk)
+    whenever every shard stays non-empty: the node-sharded ADAPT batch path
+    needs it (its shards exchange whole 64-node bitmap words); otherwise the
+    first n_total % world ranks get one node more."""
     if world < 1 or n_total < world:
         raise ValueError("need at least one node per shard")
+    chunk = adapt_chunk(n_total, world)
+    if (world - 1) * chunk < n_total:
+        return [(r * chunk, min(chunk, n_total - r * chunk)) for r in range(world)]
     q, r = divmod(n_total, world)
     out, base = [], 0
     for i in range(world):

@@ -245,3 +245,127 @@ def schedule_perpod(pods, shard: Shard, rank: int, world: int, dist, n_total: in
             if shard.base <= node < shard.base + shard.n:
                 shard.bind(node - shard.base, pod)
     return chosen, evals, start
+
+
+def _find_cut(mask: np.ndarray, s: int, k: int) -> int:
+    """find_cut (csrc/ksim_adapt.hip): offset from s (circular) of the k-th
+    (0-based) feasible node of the boolean node mask, or -1."""
+    order = np.concatenate([np.arange(s, len(mask)), np.arange(0, s)])
+    idx = np.flatnonzero(mask[order])
+    return int(idx[k]) if len(idx) > k else -1
+
+
+def schedule_adapt(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed: int, const: int,
+                   w_fit: int = 1, w_ba: int = 1, B: int = 16, T: int = 3):
+    """The node-sharded ADAPT batch (csrc/ksim_adapt.hip "node-sharded ADAPT
+    batch"), rank by rank: each shard's S0 feasibility of its nodes is
+    all-gathered into the global bitmap; the scan windows follow from it
+    (pod j+1 starts where pod j's scan stopped); each shard lists the top-T of
+    the kept nodes it holds; lists all-gathered and merged, the chain run; each
+    shard scores the guesses it owns (pair key, and "broken" when the bind
+    makes an S0-feasible node at or before the cut infeasible: that pod's
+    window would shift); max all-reduce of both; the commit stops before the
+    first broken pod and validates the rest as on the P100 path.  Returns
+    (global placements, evaluations on this shard, nextStartNodeIndex)."""
+    import torch
+    P = pods.n_pods
+    K = num_feasible_nodes_to_find(n_total, 0)
+    chosen = np.full(P, -1, np.int64)
+    cursor, seq0, start, evals = 0, 0, 0, 0
+    rows = np.arange(shard.n)
+    lo, hi = shard.base, shard.base + shard.n
+    while cursor < P:
+        nb = min(B, P - cursor)
+        # S0 bitmaps: this shard's nodes, all-gathered into the global order
+        sizes = _shard_sizes(dist, shard.n, world)
+        cmax = max(sizes)                          # equal-size all-gather: padded rows (the W words)
+        loc = np.zeros((nb, cmax), np.int64)
+        for j in range(nb):
+            loc[j, :shard.n] = shard.keys(pods.pods[cursor + j], rows, seed, seq0 + j, const, w_fit, w_ba) != 0
+        parts = [torch.zeros(nb * cmax, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(loc.reshape(-1)))
+        gmask = np.concatenate([x.numpy().reshape(nb, cmax)[:, :sizes[r]] for r, x in enumerate(parts)],
+                               axis=1).astype(bool)
+        # windows (every rank alike)
+        wins, s = [], start
+        for j in range(nb):
+            cut = _find_cut(gmask[j], s, K)
+            wins.append((s, cut))
+            s = (s + (cut if cut >= 0 else n_total)) % n_total
+        # this shard's kept nodes -> its top-T record per pod
+        rec = np.zeros((nb, T + 1), np.int64)
+        for j, (s, cut) in enumerate(wins):
+            kend = cut if cut >= 0 else n_total
+            g = (s + np.arange(kend)) % n_total
+            g = g[(g >= lo) & (g < hi)]
+            g = g[gmask[j][g]]
+            k = shard.keys(pods.pods[cursor + j], g - lo, seed, seq0 + j, const, w_fit, w_ba) if len(g) else \
+                np.zeros(0, np.uint64)
+            order = np.sort(k[k != 0])[::-1]
+            rec[j, :min(T, len(order))] = order[:T].astype(np.int64)
+            rec[j, T] = min(T, len(order)) | ((1 if len(order) <= T else 0) << 32)
+        gathered = [torch.zeros(nb * (T + 1), dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(rec.reshape(-1)))
+        gr = [x.numpy().reshape(nb, T + 1) for x in gathered]
+        guessed, gkey, nchain = set(), [0] * nb, nb
+        for j in range(nb):
+            lists = [gr[r][j, :gr[r][j, T] & 0xFFFFFFFF] for r in range(world)]
+            comps = [bool(gr[r][j, T] >> 32) for r in range(world)]
+            glist, gcomplete = global_merge(lists, comps, T)
+            pick = next((k for k in glist if NODE_MASK - (k & NODE_MASK) not in guessed), None)
+            if pick is None:
+                if not gcomplete:
+                    nchain = j
+                    break
+                continue
+            guessed.add(NODE_MASK - (pick & NODE_MASK))
+            gkey[j] = pick
+        # owned guesses: pair keys and broken flags, max over shards
+        px = np.zeros(2 * nb, np.int64)
+        for j in range(nchain):
+            s, cut = wins[j]
+            kend = cut if cut >= 0 else n_total
+            for k in range(j):
+                if not gkey[k]:
+                    continue
+                node = NODE_MASK - (gkey[k] & NODE_MASK)
+                if not lo <= node < hi:
+                    continue
+                off = (node - s) % n_total
+                if off < kend or off == cut:
+                    v = int(shard.keys(pods.pods[cursor + j], np.array([node - lo]), seed, seq0 + j, const, w_fit,
+                                       w_ba, extra=pods.pods[cursor + k])[0])
+                    if cut >= 0 and gmask[j][node] and v == 0:
+                        px[nb + j] = 1
+                    if off < kend:
+                        px[j] = max(px[j], v)
+        t = torch.from_numpy(px)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        px = t.numpy()
+        nchain = next((j for j in range(nchain) if px[nb + j]), nchain)
+        istar = next((j for j in range(nchain) if px[j] > gkey[j]), nchain)
+        committed = istar + 1 if istar < nchain else nchain
+        inode = NODE_MASK - (int(px[istar]) & NODE_MASK) if istar < nchain else -1
+        for j in range(committed):
+            node = inode if j == istar else (NODE_MASK - (gkey[j] & NODE_MASK) if gkey[j] else -1)
+            chosen[cursor + j] = node
+            s, cut = wins[j]
+            g = (s + np.arange(cut + 1 if cut >= 0 else n_total)) % n_total
+            evals += int(((g >= lo) & (g < hi)).sum())
+            if j < istar and gkey[j] and lo <= node < hi:
+                shard.bind(node - lo, pods.pods[cursor + j])
+                if node == inode:
+                    shard.bind(node - lo, pods.pods[cursor + istar])
+        if committed:
+            s, cut = wins[committed - 1]
+            start = (s + (cut if cut >= 0 else n_total)) % n_total
+        cursor += committed
+        seq0 += committed
+    return chosen, evals, start
+
+
+def _shard_sizes(dist, n: int, world: int):
+    import torch
+    t = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(t, torch.tensor([n], dtype=torch.int64))
+    return [int(x[0]) for x in t]

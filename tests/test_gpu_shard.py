@@ -161,3 +161,59 @@ def test_rccl_world1_perpod():
 
 def _prof_pct(pct, seed=0x4B53494D):
     return profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=pct, tiebreak_seed=seed))
+
+
+def _adapt_prof(seed=0x4B53494D):
+    return profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=0, tiebreak_seed=seed))
+
+
+@pytest.mark.parametrize("n_nodes,world", [(2000, 2), (3000, 4), (5000, 8), (1031, 3)])
+def test_group_adapt_batch(n_nodes, world):
+    """ADAPT (the simulator's default) on node shards: the sharded ADAPT batch
+    path (bitmap all-gather, global windows, shard records, broken flags in
+    the max all-reduce) matches the oracle on the whole cluster, including
+    nextStartNodeIndex and the evaluation count."""
+    cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=3000)
+    prof = _adapt_prof()
+    assert partition(n_nodes, world)[1][0] % 64 == 0          # the aligned layout
+    engines = _group(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert st.batches > 0 and st.perpod_cycles == 0             # the batch path ran
+    assert all(e.next_start == ora.next_start for e in engines)
+    es, os_ = _node_state(engines), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+
+
+def test_group_adapt_until_full():
+    """ADAPT shards while pods stop fitting: windows that wrap, fewer than K
+    feasible nodes, unschedulable pods."""
+    cluster, _ = gen.config2(n_nodes=700, n_pods=1)
+    pods = gen.bare_pods(700 * 112, seed=7)
+    prof = _adapt_prof()
+    engines = _group(cluster, pods, prof, 4)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert (chosen == -1).sum() > 0 and st.evals == ost.evals
+
+
+def test_rccl_world1_adapt():
+    """The RCCL exchange calls of the sharded ADAPT batch with a single rank."""
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=2000)
+    prof = _adapt_prof()
+    e = Engine(0)
+    e.set_shard(0, cluster.n_nodes)
+    e.set_profile(prof)
+    e.set_cluster(cluster)
+    e.comm_init(0, 1, engine.comm_unique_id())
+    e.load_pods(pods)
+    chosen, st = e.schedule_loaded(0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.batches > 0

@@ -15,11 +15,18 @@ from ksim.shard import partition
 
 
 def test_partition_tiles_cluster():
-    for n, w in [(10, 3), (5000, 8), (100000, 8), (7, 7)]:
+    from ksim.shard import adapt_chunk
+    for n, w in [(10, 3), (5000, 8), (100000, 8), (7, 7), (1031, 3), (65, 4)]:
         parts = partition(n, w)
         assert parts[0][0] == 0 and sum(c for _, c in parts) == n
         assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))
-        assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+        assert all(c > 0 for _, c in parts)
+        chunk = adapt_chunk(n, w)
+        if (w - 1) * chunk < n:      # the 64-aligned layout (sharded ADAPT batch path)
+            assert all(b == r * chunk for r, (b, _) in enumerate(parts))
+        else:                        # too few nodes for it: balanced to one node
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+    assert partition(100000, 8)[1] == (12544, 12544) and partition(100000, 8)[7] == (87808, 12192)
     with pytest.raises(ValueError):
         partition(3, 4)
 
@@ -115,3 +122,47 @@ def _worker_perpod(rank, world, port, n_nodes, n_pods, seed, pct):
 def test_sharded_perpod_gloo(world, n_nodes, n_pods, pct):
     """The sharded per-pod cycle's window / argmax exchanges across processes."""
     mp.spawn(_worker_perpod, args=(world, _free_port(), n_nodes, n_pods, 9, pct), nprocs=world, join=True)
+
+
+def _worker_adapt(rank, world, port, n_nodes, n_pods, seed, T, B):
+    import sys
+    root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+    sys.path[:0] = [root, os.path.join(root, "kube-scheduler-simulator_amd")]
+    import torch
+    import torch.distributed as dist
+    from ksim import gen, profile
+    from ksim.shard import partition
+    from oracle import shard_model
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=n_pods, seed=seed)
+        sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+        w = {p.name: (p.weight or 1) for p in sp.score_plugins()}
+        const = 100 * w["TaintToleration"] + 100 * w["PodTopologySpread"]
+        base, cnt = partition(n_nodes, world)[rank]
+        shard = shard_model.Shard(cluster, base, cnt)
+        chosen, evals, start = shard_model.schedule_adapt(pods, shard, rank, world, dist, n_nodes, sp.tiebreak_seed,
+                                                          const, w["NodeResourcesFit"],
+                                                          w["NodeResourcesBalancedAllocation"], B=B, T=T)
+        t = torch.tensor([evals], dtype=torch.int64)
+        dist.all_reduce(t)
+        if rank == 0:
+            from oracle.oracle import Oracle
+            ora = Oracle(cluster, profile.compile_profile(sp))
+            ochosen, ost = ora.schedule(pods)
+            np.testing.assert_array_equal(chosen, ochosen)
+            assert int(t[0]) == ost.evals and start == ora.next_start
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_nodes,n_pods,T,B", [
+    (2, 250, 500, 3, 16),     # ADAPT: K = 100 of 250, windows across the shard boundary
+    (3, 301, 400, 4, 24),
+    (2, 130, 1500, 3, 32),    # pods stop fitting: fewer than K feasible, unschedulable pods
+])
+def test_sharded_adapt_batch_gloo(world, n_nodes, n_pods, T, B):
+    """The node-sharded ADAPT batch protocol (bitmap all-gather, global windows,
+    shard records, pair keys + broken flags under one max all-reduce) across
+    processes, against the C oracle on the whole cluster."""
+    mp.spawn(_worker_adapt, args=(world, _free_port(), n_nodes, n_pods, 11, T, B), nprocs=world, join=True)

@@ -47,26 +47,41 @@ __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPod
   return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar);
 }
 
-__global__ __launch_bounds__(256) void k_adapt_mask(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
-                                                    const DevState* __restrict__ st, uint64_t* __restrict__ amask,
-                                                    int32_t n_words) {
+// The S0 feasibility bitmaps, node-stationary: a block of 256 threads holds
+// one node per thread (its row loaded once) and sweeps kMaskPods pods of the
+// batch, one ballot per pod and 64-node word.  (A pod-per-block form re-reads
+// every node row once per pod: B x the node table from L2 / MALL per batch,
+// ~190 us at 100k nodes; here a row is read once per mp pods.)  mp shrinks on
+// small clusters so the grid still fills the chip (mask_pods).
+__host__ __device__ inline int32_t mask_pods(int32_t n_words) {
+  const int32_t wb = (n_words + 3) / 4;            // 4 words (waves) per block
+  const int32_t mp = wb / 8;                       // about 2,048 blocks over B pods
+  return mp < 1 ? 1 : mp > 32 ? 32 : mp;
+}
+
+__global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
+                                                       const DevState* __restrict__ st, uint64_t* __restrict__ amask,
+                                                       int32_t n_words, int32_t mp) {
   const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
-  const int32_t j = blockIdx.y;
-  const int32_t pi = base + j;
-  if (pi >= min(st->end, base + kBatchPods)) return;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t j0 = blockIdx.y * mp;
+  if (j0 >= nb) return;                              // block-uniform
   const int lane = threadIdx.x & 63;
   const int32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= n_words) return;                          // wave-uniform
   const int32_t node = w * 64 + lane;
-  bool f = false;
-  if (node < c.n) {
-    const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;      // block-uniform
-    const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-    f = batch_feasible(c, P, bp, P.pods[pi], r, trivial);
+  const bool on = node < c.n;
+  const NodeRow r = load_row(c, on ? node : 0);
+  const int32_t j1 = min(j0 + mp, nb);
+#pragma unroll 1
+  for (int32_t j = j0; j < j1; j++) {
+    const int32_t pi = base + j;
+    const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // uniform
+    const bool f = on && batch_feasible(c, P, bp, P.pods[pi], r, trivial);
+    const uint64_t m = __ballot(f);
+    if (lane == 0) amask[(size_t)j * n_words + w] = m;
   }
-  const uint64_t m = __ballot(f);
-  if (lane == 0) amask[(size_t)j * n_words + w] = m;
 }
 
 // Rotated offset of the K-th (0-based) set bit of `mask` counting from node s,
@@ -150,7 +165,9 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
 // SH (node-sharded): amask / awin are global (n_total nodes); the block scores
 // the kept nodes this shard holds and writes the pod's record (xsend: its T
 // best keys and count | complete << 32) for the all-gather instead of topk.
-template <bool SH>
+// FAST: the narrow-arithmetic keys (dyn_key_fast; trivial cpu/memory pods, see
+// ksim_batch.hip).
+template <bool SH, bool FAST>
 __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
@@ -182,6 +199,12 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   const int32_t pi = base + j;
   const ksim_pod& p = P.pods[pi];
   const int64_t seq = st->pod_seq + j;
+  const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
+  auto node_key = [&](int32_t local) -> uint64_t {
+    const NodeRow r = load_res_row(c, local);       // scores read the resource columns only
+    if constexpr (FAST) return dyn_key_fast(bp, p, r, c.inv_cpu[local], c.inv_mem[local], hseed, c.base + local);
+    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+  };
   const uint64_t* mask = amask + (size_t)j * n_words;
   uint64_t a[kTopT];
 #pragma unroll
@@ -199,8 +222,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
       const int32_t g = i < len1 ? a0 + i : b0 + (i - len1);
       if (!((mask[g >> 6] >> (g & 63)) & 1ull)) continue;
       kept++;
-      const NodeRow r = load_res_row(c, g - c.base);
-      a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
+      a[kTopT - 1] = umax64(a[kTopT - 1], node_key(g - c.base));
 #pragma unroll
       for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
     }
@@ -211,8 +233,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
       if (node >= n) node -= n;
       if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
       kept++;
-      const NodeRow r = load_res_row(c, node);      // scores read the resource columns only
-      a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base));
+      a[kTopT - 1] = umax64(a[kTopT - 1], node_key(node));
 #pragma unroll
       for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
     }
@@ -342,12 +363,20 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   const int32_t n_words = (a.c.n + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_adapt_mask<<<dim3((n_words + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st, a.s.amask, n_words);
+  const int32_t mp = mask_pods(n_words);
+  k_adapt_mask_ns<<<dim3((n_words + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st,
+                                                                                          a.s.amask, n_words, mp);
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_adapt_top<false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin,
-                                                         a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr);
+  if (a.fast)
+    k_adapt_top<false, true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
+                                                             a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt,
+                                                             a.s.topk_complete, nullptr);
+  else
+    k_adapt_top<false, false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
+                                                              a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt,
+                                                              a.s.topk_complete, nullptr);
   if (evs) (void)hipEventRecord(evs[3], stream);
   launch_chain(a, stream);
   if (evs) (void)hipEventRecord(evs[4], stream);
@@ -381,7 +410,9 @@ __global__ __launch_bounds__(256) void k_adapt_unpack(const DevState* __restrict
 }
 
 void launch_adapt_sh_mask(const LaunchArgs& a, uint64_t* send, int32_t W, hipStream_t stream) {
-  k_adapt_mask<<<dim3((W + 3) / 4, kBatchPods), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st, send, W);
+  const int32_t mp = mask_pods(W);
+  k_adapt_mask_ns<<<dim3((W + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st, send, W,
+                                                                                     mp);
 }
 
 void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W, uint64_t* gmask,
@@ -390,8 +421,14 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
   k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
-  k_adapt_top<true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin, a.s.aexact,
-                                                        a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend);
+  if (a.fast)
+    k_adapt_top<true, true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
+                                                            a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+                                                            a.s.xsend);
+  else
+    k_adapt_top<true, false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
+                                                             a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+                                                             a.s.xsend);
 }
 
 void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream) {

@@ -680,13 +680,18 @@ int adapt_shard_buffers(ksim_handle* h, int32_t world, int32_t W) {
 }
 
 // One ADAPT batch on every shard of a group (exchanges: bitmaps, records, M).
-int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fast) {
+  auto args = [&](ksim_handle* h) {
+    LaunchArgs la = make_args(h, h->dp, h->d_chosen);
+    la.fast = fast;
+    return la;
+  };
   const int R = (int)hs.size();
   ksim_handle* h0 = hs[0];
   const int32_t world = h0->comm ? h0->world : R;
   const int32_t W = adapt_shard_chunk(h0->dc.n_total, world) / 64;
   const size_t mw = (size_t)kBatchPods * W;                   // bitmap words per shard
-  for (auto* h : hs) launch_adapt_sh_mask(make_args(h, h->dp, h->d_chosen), h->ash_send, W, stream);
+  for (auto* h : hs) launch_adapt_sh_mask(args(h), h->ash_send, W, stream);
   if (h0->comm) {
     const ncclResult_t r = rccl().all_gather(h0->ash_send, h0->ash_recv, mw, ncclUint64, h0->comm, stream);
     if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
@@ -696,7 +701,7 @@ int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
         HIPCHK(h0, hipMemcpyAsync(hs[dst]->ash_recv + (size_t)src * mw, hs[src]->ash_send, 8 * mw,
                                   hipMemcpyDeviceToDevice, stream));
   }
-  for (auto* h : hs) launch_adapt_sh_window(make_args(h, h->dp, h->d_chosen), h->ash_recv, W, h->ash_gmask, stream);
+  for (auto* h : hs) launch_adapt_sh_window(args(h), h->ash_recv, W, h->ash_gmask, stream);
   const size_t rec = (size_t)kBatchPods * kXRec;
   if (h0->comm) {
     const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
@@ -707,10 +712,10 @@ int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
         HIPCHK(h0, hipMemcpyAsync(hs[dst]->sc.xrecv + (size_t)src * rec, hs[src]->sc.xsend, 8 * rec,
                                   hipMemcpyDeviceToDevice, stream));
   }
-  for (auto* h : hs) launch_adapt_sh_pairs(make_args(h, h->dp, h->d_chosen), h->ash_gmask, world, stream);
+  for (auto* h : hs) launch_adapt_sh_pairs(args(h), h->ash_gmask, world, stream);
   int rc;
   if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.pmax; }, 2 * kBatchPods, true, stream))) return rc;
-  for (auto* h : hs) launch_adapt_sh_commit(make_args(h, h->dp, h->d_chosen), stream);
+  for (auto* h : hs) launch_adapt_sh_commit(args(h), stream);
   HIPCHK(h0, hipGetLastError());
   return KSIM_OK;
 }
@@ -721,6 +726,8 @@ int shard_run_adapt(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   hipStream_t stream = h0->stream;
   const int32_t world = h0->comm ? h0->world : (int32_t)hs.size();
   const int32_t W = adapt_shard_chunk(h0->dc.n_total, world) / 64;
+  bool fast = run_fast(h0, a, b);                      // every shard alike
+  for (auto* h : hs) fast = fast && h->alloc_narrow;
   for (auto* h : hs) {
     int rc;
     if ((rc = adapt_shard_buffers(h, world, W))) return rc;
@@ -731,7 +738,7 @@ int shard_run_adapt(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   while (cursor < b) {
     const int32_t n = std::max(1, (b - cursor) / kBatchPods);
     for (int32_t i = 0; i < n; i++) {
-      int rc = shard_batch_adapt(hs, stream);
+      int rc = shard_batch_adapt(hs, stream, fast);
       if (rc) return rc;
     }
     DevState st;

@@ -677,7 +677,7 @@ static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t st
   if (mid) (void)hipEventRecord(*mid, stream);
 }
 
-void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
+uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[0], stream);
   launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
@@ -695,6 +695,7 @@ void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[4], stream);
   k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
   if (evs) (void)hipEventRecord(evs[5], stream);
+  return tile_eval() ? 0x1fu : 0x1du;   // k_batch_top leaves the merge slot empty
 }
 
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {

@@ -1963,7 +1963,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
         if (adapt)
           launch_batch_adapt(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else if (batch)
-          launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
+          launched = launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else
           launched = launch_cycle(a, h->stream, false, topo, &evs[(size_t)i * (per + 1)]);
       }

@@ -63,7 +63,8 @@ extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 // timing run counts only those.
 uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
-void launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+// Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
+uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
 void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_chain(const LaunchArgs& a, hipStream_t stream);

@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   // per wave: a lane can be popped at most T times and holds its T best, so
   // the wave's top-T is exact
   for (int t = 0; t < kTopT; t++) {
-    const uint64_t m = wave_max_u64_dpp(a[0]);
+    const uint64_t m = wave_max_u64_hi(a[0]);
     if (lane == 0) s_top[wv][t] = m;
     if (m != 0 && a[0] == m) {
 #pragma unroll
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   uint64_t mine = 0;
   int32_t cnt = 0;
   for (int t = 0; t < kTopT; t++) {
-    const uint64_t m = wave_max_u64_dpp(key);
+    const uint64_t m = wave_max_u64_hi(key);
     if (m == 0) break;
     if (lane == t) mine = m;
     cnt = t + 1;

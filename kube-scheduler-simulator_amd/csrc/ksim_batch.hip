@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   uint64_t mine = 0;
   int32_t cnt = 0, complete = 0, popped = 0;
   for (int t = 0; t < kTopT; t++) {
-    const uint64_t m = wave_max_u64_dpp(a[0]);
+    const uint64_t m = wave_max_u64_hi(a[0]);
     if (m == 0) { complete = 1; break; }
     if (lane == t) mine = m;
     cnt = t + 1;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     uint64_t best = key[0];
 #pragma unroll
     for (int q = 1; q < kTopSlots; q++) best = umax64(best, key[q]);
-    const uint64_t m = wave_max_u64_dpp(best);
+    const uint64_t m = wave_max_u64_hi(best);
     if (m == 0) break;
     if (lane == t) out = m;
     n_out = t + 1;

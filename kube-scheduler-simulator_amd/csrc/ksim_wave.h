@@ -39,6 +39,41 @@ __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
   return readlane_u64(v, 63);
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t v) {
+  // old = 0 (the identity of unsigned max) for disabled rows and lanes, so the
+  // move folds into v_max_u32 with a DPP operand
+  const uint32_t w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
+  return v > w ? v : w;
+}
+
+// Wave max over u32; all 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+  v = dpp_max_u32<0xb1, 0xf>(v);
+  v = dpp_max_u32<0x4e, 0xf>(v);
+  v = dpp_max_u32<0x124, 0xf>(v);
+  v = dpp_max_u32<0x128, 0xf>(v);
+  v = dpp_max_u32<0x142, 0xa>(v);
+  v = dpp_max_u32<0x143, 0xc>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Wave max over u64 keys, high words first: one 32-bit reduction, and when a
+// single lane holds the maximal high word (the common case for tie-break keys,
+// whose high word carries hash bits) its low word by one readlane; otherwise a
+// second 32-bit reduction over the low words of the lanes holding it.
+__device__ __forceinline__ uint64_t wave_max_u64_hi(uint64_t v) {
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  const uint32_t mh = wave_max_u32_dpp(hi);
+  const uint64_t tie = __ballot(hi == mh);
+  uint32_t ml;
+  if ((tie & (tie - 1)) == 0)
+    ml = (uint32_t)__builtin_amdgcn_readlane((int)lo, __builtin_ctzll(tie));
+  else
+    ml = wave_max_u32_dpp(hi == mh ? lo : 0u);
+  return ((uint64_t)mh << 32) | ml;
+}
+
 __device__ __forceinline__ void cswap_desc(uint64_t& a, uint64_t& b) {
   const uint64_t hi = a > b ? a : b, lo = a > b ? b : a;
   a = hi;

@@ -6,6 +6,7 @@ Objects can be built directly or parsed from v1 JSON/YAML dicts (the shape of
 """
 from __future__ import annotations
 
+import functools
 import math
 import re
 from dataclasses import dataclass, field
@@ -25,7 +26,13 @@ def parse_quantity(q) -> Fraction:
         return Fraction(q)
     if isinstance(q, float):
         return Fraction(str(q))
-    s = str(q).strip()
+    return _parse_quantity_str(str(q))
+
+
+@functools.lru_cache(maxsize=65536)
+def _parse_quantity_str(q: str) -> Fraction:
+    # clusters repeat a few quantity strings many times (Fractions are immutable)
+    s = q.strip()
     m = _QRE.match(s)
     if not m:
         raise ValueError(f"invalid quantity {q!r}")
@@ -40,12 +47,26 @@ def parse_quantity(q) -> Fraction:
 
 def quantity_value(q) -> int:
     """resource.Quantity.Value(): rounds up to an integer."""
+    if isinstance(q, str):
+        return _quantity_value_str(q)
     return math.ceil(parse_quantity(q))
 
 
 def quantity_milli_value(q) -> int:
     """resource.Quantity.MilliValue(): value*1000 rounded up."""
+    if isinstance(q, str):
+        return _quantity_milli_str(q)
     return math.ceil(parse_quantity(q) * 1000)
+
+
+@functools.lru_cache(maxsize=65536)
+def _quantity_value_str(q: str) -> int:
+    return math.ceil(_parse_quantity_str(q))
+
+
+@functools.lru_cache(maxsize=65536)
+def _quantity_milli_str(q: str) -> int:
+    return math.ceil(_parse_quantity_str(q) * 1000)
 
 
 # ---- objects --------------------------------------------------------------

@@ -83,8 +83,22 @@ struct DevPods {
   const ksim_topo_use* uses;
   const ksim_class_add* adds;
   const PodPlan* plans;          // [n_pods] per-pod cycle plans (host-compiled, see PodPlan)
-  int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, _pad[2];
+  // Persistent domain tables: for the (count class, key column)
+  // pairs the queue's topology uses read, the class's domain sums over the
+  // column's values, built once per queue / reset (k_ptab_init) and kept by
+  // every bind (ptab_add), so a pod whose plan carries kPlanPtab needs no
+  // per-cycle PreFilter pass.  Null on shard handles.
+  int64_t* ptab;                 // table entries; a use's table starts at its device copy's _pad
+  const int4* ptab_ent;          // [n_ptab] {class, column, kind (kPtab*), first entry}
+  const int32_t* ptab_cfirst;    // [n_classes + 1] the tables of each class: ptab_cidx[cfirst[c] .. cfirst[c+1])
+  const int32_t* ptab_cidx;
+  int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, n_ptab, _pad;
 };
+
+// Persistent table kinds (DevPods.ptab_ent .z)
+constexpr int32_t kPtabPlain = 0;    // sum[v] = class count over the nodes with value v
+constexpr int32_t kPtabMark = 1;     // plus one kDomMarkShift marker per node with value v (PTS hard)
+constexpr int32_t kPtabTotal = 2;    // one entry: the class count over every node carrying the key
 
 // Scheduler state that survives across cycles (sched.nextStartNodeIndex,
 // the tie-break sequence) plus the run cursor and counters.
@@ -714,6 +728,8 @@ struct UseMasks {
   uint32_t hard, soft, soft_val, aff, anti, exist, score, port, image, node_count, self_match;
   uint32_t dom;                  // k_topo_prefilter fills the use's domain table (use_needs_dom, and adds)
   uint32_t honor_aff, honor_taints;   // PTS nodeAffinityPolicy / nodeTaintsPolicy Honor
+  uint32_t ptab;                 // dom uses read from a persistent table (kPlanPtab pods)
+  uint32_t _pad;
 };
 
 // Per-pod plan of the per-pod cycle, compiled by the host when a pod set is
@@ -724,9 +740,16 @@ struct UseMasks {
 // with scalar loads instead of re-deriving it per node.
 struct PodPlan {
   uint32_t filter_en;            // plugin ids to evaluate (1 << id), FilterPlan.en
-  uint32_t _pad;
+  uint32_t flags;                // kPlan*
   UseMasks m;
 };
+// PodPlan.flags
+// kPlanPtab: every domain sum the pod reads is a persistent table (its device
+// use copies carry the table's first entry in _pad, DevPods.ptab), and so is
+// every InterPodAffinity emptiness test (a kPtabTotal table for key columns
+// unique per node): the cycle runs no k_topo_prefilter, and k_filter_score
+// derives the topology flags from the tables.
+constexpr uint32_t kPlanPtab = 1u;
 
 // One node's inputs of every topology use of the cycle's pod, loaded up front:
 // one round of label loads, then one of domain-table / class-count loads, so
@@ -1013,7 +1036,8 @@ __host__ __device__ __forceinline__ bool use_needs_dom(const ksim_topo_use& u) {
 // domain tables are the ones k_topo_prefilter filled for this cycle).
 template <typename Scratch>
 __device__ __forceinline__ void load_topo_row(const DevCluster& c, const ksim_topo_use* U, int nu,
-                                              const UseMasks& m, const Scratch& s, int32_t node, TopoRow& t) {
+                                              const UseMasks& m, const Scratch& s, const int64_t* ptab,
+                                              int32_t node, TopoRow& t) {
 #pragma unroll
   for (int i = 0; i < KSIM_MAX_USES; i++) {
     uint32_t v = 0;
@@ -1026,8 +1050,12 @@ __device__ __forceinline__ void load_topo_row(const DevCluster& c, const ksim_to
 #pragma unroll
   for (int i = 0; i < KSIM_MAX_USES; i++) {
     int64_t x = 0;
-    if (i < nu)
-      x = ((m.node_count >> i) & 1u) ? class_count(c, load_use(U, i).cls, node) : s.dom[(size_t)i * c.vmax + t.v[i]];
+    if (i < nu) {
+      const ksim_topo_use u = load_use(U, i);
+      x = ((m.node_count >> i) & 1u) ? class_count(c, u.cls, node)
+          : ((m.ptab >> i) & 1u)     ? ptab[u._pad + t.v[i]]
+                                     : s.dom[(size_t)i * c.vmax + t.v[i]];
+    }
     t.x[i] = x;
   }
 }
@@ -1168,12 +1196,27 @@ __device__ __forceinline__ int64_t ipa_score(const ksim_profile& prof, const ksi
   return sc;
 }
 
+// The persistent domain tables of class cls follow a change of its count on
+// node (concurrent binds of one batch may share a table entry: atomics).
+__device__ __forceinline__ void ptab_add(const DevCluster& c, const DevPods& P, int32_t cls, int32_t node,
+                                         int64_t delta) {
+  if (!P.ptab_cfirst) return;
+  const int32_t e1 = P.ptab_cfirst[cls + 1];
+  for (int32_t e = P.ptab_cfirst[cls]; e < e1; e++) {
+    const int4 t = P.ptab_ent[P.ptab_cidx[e]];
+    const uint32_t v = c.labels[(size_t)t.y * c.n + node];
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(P.ptab + t.w + (t.z == kPtabTotal ? 0u : v)),
+                     (unsigned long long)delta);
+  }
+}
+
 // NodeInfo.AddPod / RemovePod on the count classes
 __device__ __forceinline__ void apply_adds(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
                                            int sign) {
   for (int i = 0; i < p.add_count; i++) {
     const ksim_class_add a = P.adds[p.add_first + i];
     c.cnt[(size_t)a.cls * c.n + node] += sign * a.count;
+    ptab_add(c, P, a.cls, node, (int64_t)sign * a.count);
   }
 }
 
@@ -1485,6 +1528,7 @@ __device__ __forceinline__ void assume_pod_wave(const DevCluster& c, const DevPo
   for (int i = lane; i < p.add_count; i += 64) {
     const ksim_class_add a = P.adds[p.add_first + i];
     c.cnt[(size_t)a.cls * c.n + node] += sign * a.count;
+    ptab_add(c, P, a.cls, node, (int64_t)sign * a.count);
   }
 }
 

@@ -13,8 +13,11 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
+#include <tuple>
 #include <type_traits>
 #include <vector>
 
@@ -98,6 +101,7 @@ struct ksim_handle {
   } init{};
   std::vector<int32_t> col_nvals;       // host copy (pod validation)
   std::vector<uint8_t> col_unique;      // host copy of DevCluster.col_unique (kUseUniqueCol on upload)
+  std::vector<uint8_t> col_total;       // per label column: every node carries the key
 
   DevScratch sc{};
   DevEvalOut eo{};
@@ -111,7 +115,8 @@ struct ksim_handle {
   int32_t* d_chosen = nullptr;
   std::vector<DevBuf> pod_bufs;
   std::vector<uint8_t> batchable;       // per loaded pod
-  std::vector<uint8_t> topo;            // per loaded pod: carries topology uses
+  std::vector<uint8_t> topo;            // per loaded pod: 0 no topology uses, 1 uses (k_topo_prefilter), 2 uses
+                                        // read from persistent tables (kPlanPtab)
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
@@ -138,7 +143,7 @@ struct ksim_handle {
 
   // per-pod cycles, by variant: topology kernels (1) | critical paths in the
   // filter pass (2) | NormalizeScore extrema in the filter pass (4)
-  hipGraphExec_t graph_cycle[8] = {};
+  hipGraphExec_t graph_cycle[16] = {};   // | persistent tables (8)
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
@@ -385,12 +390,13 @@ int read_state(ksim_handle* h, DevState& st) {
 }
 
 int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false, bool fuse_min = false,
-            bool fuse_ext = false) {
+            bool fuse_ext = false, bool ptab = false) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = fast;
   a.fuse_min = fuse_min;
   a.fuse_ext = fuse_ext;
+  a.ptab = ptab;
   hipGraph_t g = nullptr;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
   if (batch)
@@ -425,8 +431,10 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
     for (int32_t i = a; i < b && la.fuse_min; i++) la.fuse_min = h->hard_small[i] != 0;
     la.fuse_ext = true;
     for (int32_t i = a; i < b && la.fuse_ext; i++) la.fuse_ext = h->soft_le1[i] != 0;
-    hipGraphExec_t& g = h->graph_cycle[(topo ? 1 : 0) | (la.fuse_min ? 2 : 0) | (la.fuse_ext ? 4 : 0)];
-    if (!g && (rc = capture(h, false, topo, &g, false, la.fuse_min, la.fuse_ext))) return rc;
+    la.ptab = h->topo[a] == 2;                     // runs are uniform in topo (for_each_run)
+    hipGraphExec_t& g =
+        h->graph_cycle[(topo ? 1 : 0) | (la.fuse_min ? 2 : 0) | (la.fuse_ext ? 4 : 0) | (la.ptab ? 8 : 0)];
+    if (!g && (rc = capture(h, false, topo, &g, false, la.fuse_min, la.fuse_ext, la.ptab))) return rc;
     int32_t done = a;
     for (; done + kGraphCycles <= b; done += kGraphCycles) HIPCHK(h, hipGraphLaunch(g, h->stream));
     for (; done < b; done++) launch_cycle(la, h->stream, false, topo);
@@ -477,7 +485,7 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn, bool adap
     const bool b = batch_ok && h->batchable[i] != 0;
     const bool t = h->topo[i] != 0;
     int32_t j = i + 1;
-    while (j < end && (batch_ok && h->batchable[j] != 0) == b && (h->topo[j] != 0) == t) j++;
+    while (j < end && (batch_ok && h->batchable[j] != 0) == b && h->topo[j] == h->topo[i]) j++;
     int rc = fn(i, j, b, t);
     if (rc) return rc;
     i = j;
@@ -1037,6 +1045,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     }
     UP(col_unique, uniq.data(), uniq.size());
     h->col_unique = uniq;
+    h->col_total.assign((size_t)t->n_label_cols, 1);
+    for (int k = 0; k < t->n_label_cols; k++)
+      for (int32_t i = 0; i < n && h->col_total[k]; i++)
+        if (!t->labels[(size_t)k * n + i]) h->col_total[k] = 0;
   }
   UP(nb_limit, t->nb_limit, 8 * N);                      // zeros when no node has the annotation
   UP(nb_alloc, t->nb_alloc, 8 * N);
@@ -1462,6 +1474,12 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   P.n_pods = 1;
   P.n_exprs = (int32_t)ex.size();
   P.n_terms = (int32_t)tm.size();
+  // this pod's binds keep the loaded queue's persistent tables (its plan reads
+  // none of them: no kPlanPtab on single uploads)
+  P.ptab = h->dp.ptab;
+  P.ptab_ent = h->dp.ptab_ent;
+  P.ptab_cfirst = h->dp.ptab_cfirst;
+  P.ptab_cidx = h->dp.ptab_cidx;
   P.n_uses = (int32_t)us.size();
   P.n_adds = (int32_t)ad.size();
   return KSIM_OK;
@@ -1604,6 +1622,87 @@ int ksim_forget(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32
   return assume_common(h, ps, pod_index, node, -1);
 }
 
+// Persistent domain tables of a queue: which pods read every
+// domain sum from a table kept by the binds, and the tables they need.
+struct PtabRegistry {
+  std::vector<int4> ent;                 // {class, column, kind, first entry}
+  std::vector<int32_t> cfirst, cidx;     // CSR by class
+  int64_t len = 0;                       // int64 entries
+  std::vector<uint8_t> pod;              // per pod: kPlanPtab
+  std::vector<uint32_t> mask;            // per pod: UseMasks.ptab
+};
+
+// uses: the queue's device use copies (kUseUniqueCol marked); their _pad
+// becomes the first entry of the use's table.  A pod qualifies when each of
+// its domain sums is independent of the pod beyond (class, column): PTS hard
+// constraints on keys every node carries with nodeInclusionPolicies that
+// filter nothing here, InterPodAffinity terms; value-keyed ScheduleAnyway
+// constraints keep k_topo_prefilter (k_extrema reads their sums).  Shard
+// handles exchange per-cycle sums and build no tables.
+static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector<ksim_topo_use>& uses,
+                       PtabRegistry& R) {
+  R = PtabRegistry{};
+  R.pod.assign((size_t)ps->n_pods, 0);
+  R.mask.assign((size_t)ps->n_pods, 0);
+  if (is_sharded(h) || getenv("KSIM_NO_PTAB")) return;   // A/B switch: per-cycle PreFilter sums
+  std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> index;
+  for (int32_t i = 0; i < ps->n_pods; i++) {
+    const ksim_pod& p = ps->pods[i];
+    if (p.use_count <= 0) continue;
+    ksim_topo_use* U = uses.data() + p.use_first;
+    const UseMasks m = use_masks(h->prof, U, p.use_count);
+    const bool pod_aff = p.sel_count > 0 || (p.flags & KSIM_POD_HAS_REQUIRED_AFFINITY);
+    int32_t kind[KSIM_MAX_USES];
+    bool ok = true;
+    for (int k = 0; k < p.use_count && ok; k++) {
+      const ksim_topo_use& u = U[k];
+      const uint32_t b = 1u << k;
+      kind[k] = -1;
+      if (u.col == KSIM_COL_NONE) continue;
+      if (use_node_count(u)) {                   // the node's own count; a total for the emptiness test
+        if ((m.aff | m.score) & b && u.cls >= 0) kind[k] = kPtabTotal;
+        continue;
+      }
+      if (u.kind == KSIM_USE_PTS_SOFT) {
+        ok = false;
+      } else if (u.kind == KSIM_USE_PTS_HARD) {
+        ok = h->col_total[u.col] && h->col_nvals[u.col] <= kFuseMinValues &&
+             !((u.flags & KSIM_USEF_HONOR_AFFINITY) && pod_aff) &&
+             !((u.flags & KSIM_USEF_HONOR_TAINTS) && !h->hard_taints.empty());
+        kind[k] = kPtabMark;
+      } else {
+        ok = !((m.aff | m.score) & b) || h->col_nvals[u.col] <= kFuseMinValues;   // emptiness scans
+        kind[k] = kPtabPlain;
+      }
+    }
+    if (!ok) continue;
+    for (int k = 0; k < p.use_count; k++) {
+      if (kind[k] < 0) continue;
+      ksim_topo_use& u = U[k];
+      const auto key = std::make_tuple(u.cls, (int32_t)u.col, kind[k]);
+      auto it = index.find(key);
+      if (it == index.end()) {
+        it = index.emplace(key, (int32_t)R.ent.size()).first;
+        R.ent.push_back(make_int4(u.cls, (int32_t)u.col, kind[k], (int32_t)R.len));
+        R.len += kind[k] == kPtabTotal ? 1 : h->col_nvals[u.col];
+      }
+      u._pad = R.ent[(size_t)it->second].w;
+      if (kind[k] != kPtabTotal) R.mask[i] |= 1u << k;
+    }
+    R.pod[i] = 1;
+  }
+  if (R.ent.empty()) return;
+  const int32_t C = h->dc.n_classes;
+  R.cfirst.assign((size_t)C + 1, 0);
+  for (const int4& e : R.ent)
+    if (e.x >= 0) R.cfirst[(size_t)e.x + 1]++;
+  for (int32_t c = 0; c < C; c++) R.cfirst[(size_t)c + 1] += R.cfirst[(size_t)c];
+  R.cidx.assign((size_t)R.cfirst[(size_t)C], 0);
+  std::vector<int32_t> fill(R.cfirst.begin(), R.cfirst.end() - 1);
+  for (size_t e = 0; e < R.ent.size(); e++)
+    if (R.ent[e].x >= 0) R.cidx[(size_t)fill[(size_t)R.ent[e].x]++] = (int32_t)e;
+}
+
 int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   int rc = ensure_ready(h);
   if (rc) return rc;
@@ -1626,7 +1725,13 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   // n_nn) is a byte size over a fixed element size, so equal sizes mean equal
   // captured values.
   const size_t np1 = (size_t)std::max(ps->n_pods, 1);
+  std::vector<ksim_topo_use> uses(ps->uses, ps->uses + std::max(ps->n_uses, 0));
+  mark_unique(h, uses.data(), uses.size());
+  PtabRegistry R;
+  build_ptab(h, ps, uses, R);
   const std::vector<size_t> bytes = {sizeof(ksim_pod) * (size_t)ps->n_pods,
+                                     sizeof(int4) * R.ent.size(), 4 * R.cfirst.size(), 4 * R.cidx.size(),
+                                     8 * (size_t)R.len,
                                      sizeof(ksim_label_expr) * (size_t)ps->n_exprs,
                                      sizeof(ksim_term) * (size_t)ps->n_terms,
                                      4 * (size_t)ps->n_nn,
@@ -1664,7 +1769,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     batchable[i] = pod_batchable(h, ps->pods[i]) ? 1 : 0;
-    h->topo[i] = ps->pods[i].use_count > 0 ? 1 : 0;
+    h->topo[i] = ps->pods[i].use_count > 0 ? (R.pod[i] ? 2 : 1) : 0;
     // sharded-cycle exchange sizes, laid out as k_dom_pack / k_window_sh do
     bool soft = false;
     int n_soft = 0;
@@ -1697,19 +1802,31 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.nn = (const int32_t*)p;
   if ((rc = put(bf.data(), 4 * bf.size(), &p))) return drop_queue(rc);
   P.bflags = (const int32_t*)p;
-  std::vector<ksim_topo_use> uses(ps->uses, ps->uses + std::max(ps->n_uses, 0));
-  mark_unique(h, uses.data(), uses.size());
   if ((rc = put(uses.data(), sizeof(ksim_topo_use) * uses.size(), &p))) return drop_queue(rc);
   P.uses = (const ksim_topo_use*)p;
   {
     std::vector<PodPlan> plans((size_t)ps->n_pods);
-    for (int32_t i = 0; i < ps->n_pods; i++)
+    for (int32_t i = 0; i < ps->n_pods; i++) {
       plans[i] = make_plan(h, ps->pods[i], uses.data() + std::max(ps->pods[i].use_first, 0));
+      if (R.pod[i]) {
+        plans[i].flags |= kPlanPtab;
+        plans[i].m.ptab = R.mask[i];
+      }
+    }
     if ((rc = put(plans.data(), sizeof(PodPlan) * plans.size(), &p))) return drop_queue(rc);
     P.plans = (const PodPlan*)p;
   }
   if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)ps->n_adds, &p))) return drop_queue(rc);
   P.adds = (const ksim_class_add*)p;
+  if ((rc = put(R.ent.data(), sizeof(int4) * R.ent.size(), &p))) return drop_queue(rc);
+  P.ptab_ent = (const int4*)p;
+  if ((rc = put(R.cfirst.data(), 4 * R.cfirst.size(), &p))) return drop_queue(rc);
+  P.ptab_cfirst = R.cfirst.empty() ? nullptr : (const int32_t*)p;
+  if ((rc = put(R.cidx.data(), 4 * R.cidx.size(), &p))) return drop_queue(rc);
+  P.ptab_cidx = (const int32_t*)p;
+  if ((rc = put(nullptr, 8 * (size_t)R.len, &p))) return drop_queue(rc);   // filled by k_ptab_init
+  P.ptab = (int64_t*)p;
+  P.n_ptab = (int32_t)R.ent.size();
   P.n_uses = ps->n_uses;
   P.n_adds = ps->n_adds;
   P.n_nn = ps->n_nn;
@@ -1730,6 +1847,11 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     return drop_queue(hip_fail(h, e, "pod queue setup"));
   h->batchable = std::move(batchable);
   h->dp = P;
+  launch_ptab_init(h->dc, P, h->stream);
+  if ((e = hipGetLastError()) != hipSuccess || (e = hipStreamSynchronize(h->stream)) != hipSuccess) {
+    h->dp = DevPods{};
+    return drop_queue(hip_fail(h, e, "persistent tables"));
+  }
   return KSIM_OK;
 }
 
@@ -1883,6 +2005,8 @@ int ksim_reset_cluster(ksim_handle* h) {
     HIPCHK(h, hipMemcpyAsync(c.cnt, h->init.cnt, 4 * N * c.n_classes, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(c.nb_alloc, h->init.nb_alloc, 8 * N, hipMemcpyDeviceToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->st, 0, sizeof(DevState), h->stream));
+  launch_ptab_init(h->dc, h->dp, h->stream);        // the queue's persistent tables follow the counts
+  HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return KSIM_OK;
 }
@@ -1901,6 +2025,7 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   a.fast = batch && run_fast(h, first, end);
   a.fuse_min = !batch && h->topo[first] && h->hard_small[first];
   a.fuse_ext = !batch && h->soft_le1[first];
+  a.ptab = !batch && h->topo[first] == 2;
   auto launch = [&] {
     if (batch) launch_batch_eval_only(a, h->stream);
     else launch_filter_only(a, h->stream);
@@ -1950,6 +2075,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     for (int32_t i = lo; i < hi && a.fuse_min; i++) a.fuse_min = h->hard_small[i] != 0;
     a.fuse_ext = !batch;
     for (int32_t i = lo; i < hi && a.fuse_ext; i++) a.fuse_ext = h->soft_le1[i] != 0;
+    a.ptab = !batch && h->topo[lo] == 2;
     const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
     const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
     int32_t cursor = lo;

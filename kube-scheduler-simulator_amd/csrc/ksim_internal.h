@@ -45,6 +45,7 @@ struct LaunchArgs {
   bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
   bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
   bool fuse_ext = false;  // per-pod runs: every pod has <= 1 ScheduleAnyway spread constraint (K = N: no k_extrema)
+  bool ptab = false;      // per-pod topology runs: every pod carries kPlanPtab (no k_topo_prefilter)
 };
 
 constexpr int kKernelsPerCycle = 7;
@@ -127,6 +128,8 @@ void launch_pshard_select(const LaunchArgs& a, hipStream_t stream);
 void launch_pshard_bind(const LaunchArgs& a, int32_t world, hipStream_t stream);
 void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStream_t stream);
 void launch_group_gather(const GroupPtrs& src, const GroupPtrs& dst, int32_t words, hipStream_t stream);
+// Persistent domain tables of a loaded queue (DevPods.ptab) from the class counts.
+void launch_ptab_init(const DevCluster& c, const DevPods& P, hipStream_t stream);
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream);
 
 }  // namespace ksim

@@ -198,6 +198,7 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P,
   const int nu = p.use_count;
   if (nu == 0) return;
   const PodPlan pp = P.plans[pi];
+  if (pp.flags & kPlanPtab) return;                // persistent tables: nothing to sum
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
   uint32_t lds = 0;                                // uses whose table is staged in LDS
@@ -412,10 +413,11 @@ __device__ __forceinline__ int64_t soft_score(int64_t cnt, double w, int32_t max
 template <bool COMPAT, bool NOWIN>
 __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, ksim_profile prof,
                                                       const BatchProg* __restrict__ bp,
-                                                      const DevState* __restrict__ st, DevScratch s,
+                                                      DevState* __restrict__ st, DevScratch s,
                                                       int32_t fuse_min, int32_t fuse_ext) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
+  __shared__ uint32_t s_tf;
 #ifdef KSIM_FS_CLOCKS
   uint64_t fs_t = 0;
 #endif
@@ -430,15 +432,16 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
   FS_CLK(1);
-  if (fuse_min && m.hard) {                        // block-uniform: the critical paths, one wave
-    if (threadIdx.x < 64) {
+  const bool pt = (pp.flags & kPlanPtab) != 0;    // block-uniform: persistent tables
+  if ((fuse_min && m.hard) || (pt && (m.aff | m.score))) {
+    if (threadIdx.x < 64 && fuse_min) {            // the critical paths, one wave
       for (uint32_t b = m.hard; b; b &= b - 1) {
         const int i = __builtin_ctz(b);
         const ksim_topo_use u = load_use(U, i);
         int64_t mn = 2147483647;
         if (u.col != KSIM_COL_NONE) {
           const int32_t V = c.col_nvals[u.col];
-          const int64_t* d = s.dom + (size_t)i * c.vmax;
+          const int64_t* d = pt ? P0.ptab + u._pad : s.dom + (size_t)i * c.vmax;
           for (int32_t v = threadIdx.x; v < V; v += 64) {
             const int64_t x = d[v];
             if ((x >> kDomMarkShift) != 0) mn = min(mn, x & kDomCountMask);
@@ -447,9 +450,29 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
         mn = wave_min_i64(mn);
         if (threadIdx.x == 0) s_min[i] = mn;
       }
+    } else if (threadIdx.x >= 64 && threadIdx.x < 128 && pt) {
+      // len(affinityCounts) > 0 / len(topologyScore) > 0 from the tables
+      // (k_topo_prefilter's flags): some node with the key and a count
+      uint32_t f = 0;
+      for (uint32_t b = m.aff | m.score; b; b &= b - 1) {
+        const int i = __builtin_ctz(b);
+        const ksim_topo_use u = load_use(U, i);
+        if (u.col == KSIM_COL_NONE || u.cls < 0) continue;
+        const bool total = (m.node_count >> i) & 1u;   // a kPtabTotal table
+        const int32_t V = total ? 1 : c.col_nvals[u.col];
+        const int64_t* d = P0.ptab + u._pad;
+        bool nz = false;
+        for (int32_t v = (int32_t)threadIdx.x - 64 + (total ? 0 : 1); v < V; v += 64) nz = nz || d[v] != 0;
+        if (__ballot(nz))
+          f |= (((m.aff >> i) & 1u) ? kTopoAffinityNonEmpty : 0u) | (((m.score >> i) & 1u) ? kTopoScoreNonEmpty : 0u);
+      }
+      if (threadIdx.x == 64) {
+        s_tf = f;
+        if (blockIdx.x == 0) st->topo_flags = f;    // k_select's normalization reads it
+      }
     }
     __syncthreads();
-    s.min_match = s_min;                          // pts_filter reads the block's copy
+    if (fuse_min && m.hard) s.min_match = s_min;   // pts_filter reads the block's copy
   }
   FS_CLK(2);
   bool feasible = false, ign = false;
@@ -463,7 +486,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     s.fail[node] = KSIM_NOT_EVALUATED;
     if (COMPAT) s.detail[node] = 0;
   } else if (node < c.n) {
-    const uint32_t tf = p.use_count ? st->topo_flags : 0u;
+    const uint32_t tf = !p.use_count ? 0u : pt ? ((m.aff | m.score) ? s_tf : 0u) : st->topo_flags;
     const NodeRow r = load_row(c, node);
 #ifdef KSIM_FS_CLOCKS
     __builtin_amdgcn_s_waitcnt(0);
@@ -474,7 +497,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
 #endif
     const FilterPlan fp{bp->rank_lo, bp->rank_hi, pp.filter_en};
     TopoRow t;
-    if (p.use_count) load_topo_row(c, U, p.use_count, m, s, node, t);
+    if (p.use_count) load_topo_row(c, U, p.use_count, m, s, P0.ptab, node, t);
 #ifdef KSIM_FS_CLOCKS
     __builtin_amdgcn_s_waitcnt(0);
     if (threadIdx.x == 0) {
@@ -1026,14 +1049,14 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     // the domain tables are read no more this cycle: re-zero what this node's
     // values touched (every touched entry is some node's value); small tables
     // are cleared whole by block 0 below
-    for (uint32_t b = m.dom; b; b &= b - 1) {
+    for (uint32_t b = m.dom & ~m.ptab; b; b &= b - 1) {
       const int i = __builtin_ctz(b);
       const ksim_topo_use u = load_use(U, i);
       if (c.col_nvals[u.col] > kLdsDom) s.dom[(size_t)i * c.vmax + use_value(c, u, node)] = 0;
     }
   }
   if (blockIdx.x == 0)
-    for (uint32_t b = m.dom; b; b &= b - 1) {
+    for (uint32_t b = m.dom & ~m.ptab; b; b &= b - 1) {
       const int i = __builtin_ctz(b);
       const int32_t V = c.col_nvals[load_use(U, i).col];
       if (V <= kLdsDom && tid < V) s.dom[(size_t)i * c.vmax + tid] = 0;
@@ -1066,6 +1089,39 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2);
     }
   }
+}
+
+// The persistent domain tables from the class counts (a queue's upload, a
+// snapshot reset): one block per table, LDS sums over the column's values.
+constexpr int kPtabLds = 2048;
+__global__ __launch_bounds__(256) void k_ptab_init(DevCluster c, DevPods P) {
+  __shared__ unsigned long long s_sum[kPtabLds];
+  const int4 t = P.ptab_ent[blockIdx.x];
+  const int32_t V = t.z == kPtabTotal ? 1 : c.col_nvals[t.y];
+  int64_t* out = P.ptab + t.w;
+  const bool lds = V <= kPtabLds;
+  for (int32_t v = threadIdx.x; v < V; v += blockDim.x) {
+    if (lds) s_sum[v] = 0;
+    else out[v] = 0;
+  }
+  __syncthreads();
+  const uint32_t* lab = c.labels + (size_t)t.y * c.n;
+  for (int32_t n = threadIdx.x; n < c.n; n += blockDim.x) {
+    const uint32_t v = lab[n];
+    if (!v) continue;
+    const int64_t add = (t.x >= 0 ? (int64_t)c.cnt[(size_t)t.x * c.n + n] : 0) + (t.z == kPtabMark ? (1ll << kDomMarkShift) : 0);
+    const uint32_t x = t.z == kPtabTotal ? 0u : v;
+    if (!add) continue;
+    if (lds) atomicAdd(&s_sum[x], (unsigned long long)add);
+    else atomicAdd(reinterpret_cast<unsigned long long*>(out + x), (unsigned long long)add);
+  }
+  __syncthreads();
+  if (lds)
+    for (int32_t v = threadIdx.x; v < V; v += blockDim.x) out[v] = (int64_t)s_sum[v];
+}
+
+void launch_ptab_init(const DevCluster& c, const DevPods& P, hipStream_t stream) {
+  if (P.n_ptab > 0) k_ptab_init<<<P.n_ptab, 256, 0, stream>>>(c, P);
 }
 
 __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int sign) {
@@ -1368,8 +1424,9 @@ uint32_t launch_cycle_t(const LaunchArgs& a, hipStream_t stream, bool topo, hipE
   uint32_t mask = 0;
   const int blocks = (a.c.n + 255) / 256;
   if (evs) (void)hipEventRecord(evs[0], stream);
-  if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
-  if (topo) mask |= 1u << 0;
+  const bool pre = topo && !a.ptab;                // persistent tables: no PreFilter pass
+  if (pre) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (pre) mask |= 1u << 0;
   if (evs) (void)hipEventRecord(evs[1], stream);
   if (topo && !a.fuse_min) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   if (topo && !a.fuse_min) mask |= 1u << 1;

@@ -1,6 +1,6 @@
 // ksim_wave.h — wave64 primitives for gfx950.
 //
-// wave_max_u64_dpp: the DPP reduction (quad_perm xor1, xor2, row_ror 4, 8
+// wave_max_u64_dpp64: the DPP reduction (quad_perm xor1, xor2, row_ror 4, 8
 // inside each 16-lane row, then row_bcast15 / row_bcast31 across rows, result
 // in lane 63, broadcast by readlane).  It never touches the LDS, unlike the
 // __shfl_xor form (ds_bpermute) — on the repair kernel's single-wave critical
@@ -28,8 +28,8 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Wave max over u64; all 64 lanes must be active.
-__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+// Wave max over u64 by 64-bit DPP steps; all 64 lanes must be active.
+__device__ __forceinline__ uint64_t wave_max_u64_dpp64(uint64_t v) {
   v = umax64(v, dpp_u64<0xb1, 0xf>(v));    // quad_perm [1,0,3,2]
   v = umax64(v, dpp_u64<0x4e, 0xf>(v));    // quad_perm [2,3,0,1]
   v = umax64(v, dpp_u64<0x124, 0xf>(v));   // row_ror:4
@@ -73,6 +73,9 @@ __device__ __forceinline__ uint64_t wave_max_u64_hi(uint64_t v) {
     ml = wave_max_u32_dpp(hi == mh ? lo : 0u);
   return ((uint64_t)mh << 32) | ml;
 }
+
+// Wave max over u64 (all 64 lanes active): the high-word-first form.
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) { return wave_max_u64_hi(v); }
 
 __device__ __forceinline__ void cswap_desc(uint64_t& a, uint64_t& b) {
   const uint64_t hi = a > b ? a : b, lo = a > b ? b : a;

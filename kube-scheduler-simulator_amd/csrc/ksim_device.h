@@ -92,6 +92,8 @@ struct DevPods {
   const int4* ptab_ent;          // [n_ptab] {class, column, kind (kPtab*), first entry}
   const int32_t* ptab_cfirst;    // [n_classes + 1] the tables of each class: ptab_cidx[cfirst[c] .. cfirst[c+1])
   const int32_t* ptab_cidx;
+  const int4* ptab_padd;         // per pod (PodPlan.tadd_*): {first entry, column, kind, count} of
+                                 // every table its adds change, so a bind skips the class lookup
   int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, n_ptab, _pad;
 };
 
@@ -742,6 +744,7 @@ struct PodPlan {
   uint32_t filter_en;            // plugin ids to evaluate (1 << id), FilterPlan.en
   uint32_t flags;                // kPlan*
   UseMasks m;
+  int32_t tadd_first, tadd_count;   // kPlanTadds: the pod's persistent-table updates (DevPods.ptab_padd)
 };
 // PodPlan.flags
 // kPlanPtab: every domain sum the pod reads is a persistent table (its device
@@ -750,6 +753,9 @@ struct PodPlan {
 // unique per node): the cycle runs no k_topo_prefilter, and k_filter_score
 // derives the topology flags from the tables.
 constexpr uint32_t kPlanPtab = 1u;
+// kPlanTadds: tadd_first / tadd_count list every persistent-table update of
+// the pod's binds (queue pods; single uploads go through the class index).
+constexpr uint32_t kPlanTadds = 2u;
 
 // One node's inputs of every topology use of the cycle's pod, loaded up front:
 // one round of label loads, then one of domain-table / class-count loads, so
@@ -1508,7 +1514,7 @@ __device__ __forceinline__ void assume_pod(const DevCluster& c, const DevPods& P
 // read-modify-writes are in flight together instead of one after another.
 // A pod's class adds name distinct classes.
 __device__ __forceinline__ void assume_pod_wave(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
-                                                int sign) {
+                                                int sign, bool tables = true) {
   const int lane = threadIdx.x & 63;
   if (lane == 0) c.req_cpu[node] += sign * p.req_cpu;
   if (lane == 1) c.req_mem[node] += sign * p.req_mem;
@@ -1528,7 +1534,7 @@ __device__ __forceinline__ void assume_pod_wave(const DevCluster& c, const DevPo
   for (int i = lane; i < p.add_count; i += 64) {
     const ksim_class_add a = P.adds[p.add_first + i];
     c.cnt[(size_t)a.cls * c.n + node] += sign * a.count;
-    ptab_add(c, P, a.cls, node, (int64_t)sign * a.count);
+    if (tables) ptab_add(c, P, a.cls, node, (int64_t)sign * a.count);
   }
 }
 

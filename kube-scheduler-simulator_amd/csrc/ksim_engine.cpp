@@ -1630,6 +1630,8 @@ struct PtabRegistry {
   int64_t len = 0;                       // int64 entries
   std::vector<uint8_t> pod;              // per pod: kPlanPtab
   std::vector<uint32_t> mask;            // per pod: UseMasks.ptab
+  std::vector<int4> padd;                // per pod: the table updates of its adds
+  std::vector<int32_t> padd_first, padd_count;
 };
 
 // uses: the queue's device use copies (kUseUniqueCol marked); their _pad
@@ -1691,6 +1693,8 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
     }
     R.pod[i] = 1;
   }
+  R.padd_first.assign((size_t)ps->n_pods, 0);
+  R.padd_count.assign((size_t)ps->n_pods, 0);
   if (R.ent.empty()) return;
   const int32_t C = h->dc.n_classes;
   R.cfirst.assign((size_t)C + 1, 0);
@@ -1701,6 +1705,18 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   std::vector<int32_t> fill(R.cfirst.begin(), R.cfirst.end() - 1);
   for (size_t e = 0; e < R.ent.size(); e++)
     if (R.ent[e].x >= 0) R.cidx[(size_t)fill[(size_t)R.ent[e].x]++] = (int32_t)e;
+  for (int32_t i = 0; i < ps->n_pods; i++) {
+    const ksim_pod& p = ps->pods[i];
+    R.padd_first[(size_t)i] = (int32_t)R.padd.size();
+    for (int32_t a = 0; a < p.add_count; a++) {
+      const ksim_class_add& ad = ps->adds[p.add_first + a];
+      for (int32_t e = R.cfirst[(size_t)ad.cls]; e < R.cfirst[(size_t)ad.cls + 1]; e++) {
+        const int4& t = R.ent[(size_t)R.cidx[(size_t)e]];
+        R.padd.push_back(make_int4(t.w, t.y, t.z, ad.count));
+      }
+    }
+    R.padd_count[(size_t)i] = (int32_t)R.padd.size() - R.padd_first[(size_t)i];
+  }
 }
 
 int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
@@ -1731,7 +1747,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   build_ptab(h, ps, uses, R);
   const std::vector<size_t> bytes = {sizeof(ksim_pod) * (size_t)ps->n_pods,
                                      sizeof(int4) * R.ent.size(), 4 * R.cfirst.size(), 4 * R.cidx.size(),
-                                     8 * (size_t)R.len,
+                                     8 * (size_t)R.len, sizeof(int4) * R.padd.size(),
                                      sizeof(ksim_label_expr) * (size_t)ps->n_exprs,
                                      sizeof(ksim_term) * (size_t)ps->n_terms,
                                      4 * (size_t)ps->n_nn,
@@ -1812,6 +1828,11 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
         plans[i].flags |= kPlanPtab;
         plans[i].m.ptab = R.mask[i];
       }
+      if (!R.padd_first.empty() && !getenv("KSIM_NO_TADDS")) {   // the table updates of its binds, listed
+        plans[i].flags |= kPlanTadds;
+        plans[i].tadd_first = R.padd_first[(size_t)i];
+        plans[i].tadd_count = R.padd_count[(size_t)i];
+      }
     }
     if ((rc = put(plans.data(), sizeof(PodPlan) * plans.size(), &p))) return drop_queue(rc);
     P.plans = (const PodPlan*)p;
@@ -1827,6 +1848,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   if ((rc = put(nullptr, 8 * (size_t)R.len, &p))) return drop_queue(rc);   // filled by k_ptab_init
   P.ptab = (int64_t*)p;
   P.n_ptab = (int32_t)R.ent.size();
+  if ((rc = put(R.padd.data(), sizeof(int4) * R.padd.size(), &p))) return drop_queue(rc);
+  P.ptab_padd = (const int4*)p;
   P.n_uses = ps->n_uses;
   P.n_adds = ps->n_adds;
   P.n_nn = ps->n_nn;

@@ -422,12 +422,15 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   uint64_t fs_t = 0;
 #endif
   FS_CLK(0);
+  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
+  // the node's row does not depend on the cycle: its loads go out before the
+  // state / pod / plan chain
+  const NodeRow r = load_row(c, node < c.n ? node : c.n - 1);
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
-  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
   // the pod record and its uses sit at a block-uniform address: scalar loads
   const DevPods& P = P0;
-  const ksim_pod p = P0.pods[pi];
+  const ksim_pod& p = P0.pods[pi];                // block-uniform address: scalar loads where used
   const PodPlan pp = P0.plans[pi];                 // block-uniform: scalar loads
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
@@ -487,7 +490,6 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     if (COMPAT) s.detail[node] = 0;
   } else if (node < c.n) {
     const uint32_t tf = !p.use_count ? 0u : pt ? ((m.aff | m.score) ? s_tf : 0u) : st->topo_flags;
-    const NodeRow r = load_row(c, node);
 #ifdef KSIM_FS_CLOCKS
     __builtin_amdgcn_s_waitcnt(0);
     if (threadIdx.x == 0) {
@@ -885,14 +887,28 @@ __device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32
 // k_topo_prefilter clears the registration rows).
 __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
                                            const DevScratch& s, int32_t* __restrict__ chosen_out, int32_t pi,
-                                           bool nowin) {
+                                           bool nowin, const PodPlan& pp) {
   WinState* win = s.win;
+  // the pod's persistent-table updates, loaded ahead of the selection they do not depend on
+  const int lane = threadIdx.x & 63;
+  const bool tadds = (pp.flags & kPlanTadds) != 0;
+  int4 ta = make_int4(0, 0, 0, 0);
+  if (tadds && lane < pp.tadd_count) ta = P.ptab_padd[pp.tadd_first + lane];
   const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);   // every lane
   const int32_t error = win->error;
   const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
   const ksim_pod p = P.pods[pi];
-  if (chosen >= 0) assume_pod_wave(c, P, p, chosen, 1);         // NodeInfo.AddPod, one column per lane
-  if ((threadIdx.x & 63) != 0) return;
+  if (chosen >= 0) {
+    assume_pod_wave(c, P, p, chosen, 1, !tadds);                // NodeInfo.AddPod, one column per lane
+    if (tadds)
+      for (int32_t i = lane; i < pp.tadd_count; i += 64) {
+        const int4 t = i == lane ? ta : P.ptab_padd[pp.tadd_first + i];
+        const uint32_t v = c.labels[(size_t)t.y * c.n + chosen];
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(P.ptab + t.x + (t.z == kPtabTotal ? 0u : v)),
+                         (unsigned long long)(int64_t)t.w);
+      }
+  }
+  if (lane != 0) return;
   const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
   DevState S = *st;                                // one read, one write back: no load-store chain
   // nextStartNodeIndex = (nextStartNodeIndex + processed) % len(scanned nodes);
@@ -930,6 +946,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
                                                 int32_t fuse_ext, int32_t bind_mode, int32_t* __restrict__ chosen_out) {
   __shared__ uint64_t s_best[8];
   __shared__ int32_t sh32[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t node = blockIdx.x * blockDim.x + tid;
+  const int32_t N = c.n;
+  const int S = prof.n_score;
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   WinState* win = s.win;
@@ -938,10 +958,6 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   const PodPlan pp = P0.plans[pi];
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int32_t node = blockIdx.x * blockDim.x + tid;
-  const int32_t N = c.n;
-  const int S = prof.n_score;
   int32_t nf, kend;
   bool has_soft;
   int soft = -1;
@@ -1086,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     __syncthreads();
     if (s_last && tid < 64) {
       if (tid == 0) win->done = 0;
-      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2);
+      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp);
     }
   }
 }

@@ -71,6 +71,7 @@ struct DevCluster {
 constexpr uint32_t kClusterUnschedulable = 1u;   // some node has spec.unschedulable
 constexpr uint32_t kClusterHardTaints = 2u;      // some node has a NoSchedule / NoExecute taint
 constexpr uint32_t kClusterPreferTaints = 4u;    // some node has a PreferNoSchedule taint
+constexpr uint32_t kClusterNarrow = 8u;          // every allocatable cpu / memory in [0, 2^46) (fast quotients)
 
 struct PodPlan;
 
@@ -985,11 +986,20 @@ struct RawScores {
 // the score; k_extrema overwrites it otherwise), stored per slot into raw
 // ([slot][n]); returns the weighted sum of the slots without NormalizeScore.
 // store_plain: also store the raw score of those slots (compat mode).
+struct BatchProg;
+__device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+                                                        double inv_c, double inv_m);
+__device__ __forceinline__ int32_t fast_balanced_allocation(const ksim_pod& p, const NodeRow& r, double inv_c,
+                                                            double inv_m);
+
+// fast (non-null): BatchProg::fast_w on a kClusterNarrow cluster, so the
+// cpu / memory strategies take the host-reciprocal quotients (inv_c, inv_m).
 __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                                   const ScorePlan& sp, const ksim_pod& p, const NodeRow& r,
                                                   const ksim_topo_use* U, const UseMasks& m, const TopoRow& t,
                                                   int64_t* raw, bool store_plain, RawScores& rv,
-                                                  int64_t pts_count) {
+                                                  int64_t pts_count, const BatchProg* fast = nullptr,
+                                                  double inv_c = 0, double inv_m = 0) {
   int64_t part = 0;
   const size_t n = (size_t)c.n;
   auto put = [&](int pl, int64_t v) {
@@ -1004,8 +1014,10 @@ __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const Dev
 #define KSIM_PUT(pl, dst, expr) \
   if (plan_slot(sp, pl) >= 0) { dst = (expr); put(pl, dst); }
   int64_t v;
-  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fit_least_allocated_score(r, prof, p, c.n_scalar));
-  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, balanced_allocation_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fast ? (int64_t)fast_least_allocated(*fast, p, r, inv_c, inv_m)
+                                                : fit_least_allocated_score(r, prof, p, c.n_scalar));
+  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(p, r, inv_c, inv_m)
+                                                : balanced_allocation_score(r, prof, p, c.n_scalar));
   KSIM_PUT(KSIM_PL_TAINT_TOLERATION, rv.taint, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
   KSIM_PUT(KSIM_PL_NODE_AFFINITY, rv.aff, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
   KSIM_PUT(KSIM_PL_INTER_POD_AFFINITY, rv.ipa, m.score ? ipa_score(prof, U, m, t) : 0);
@@ -1427,6 +1439,39 @@ __device__ __forceinline__ double div_rn(double n, double d, double y) {
 // its correction steps, and for BalancedAllocation bit for bit the float64
 // quotient Go computes.  hseed = seed ^ (seq << 20), the pod's part of the
 // tie-break hash.
+// leastResourceScorer over {cpu, memory} (BatchProg::fast_w, kClusterNarrow)
+__device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+                                                        double inv_c, double inv_m) {
+  const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
+  const int64_t rc = r.nz_cpu + p.nz_cpu, rm = r.nz_mem + p.nz_mem;
+  const int32_t sc = (!hc || rc > r.alloc_cpu) ? 0
+                     : (int32_t)div_rn((double)((r.alloc_cpu - rc) * kMaxNodeScore), (double)r.alloc_cpu, inv_c);
+  const int32_t sm = (!hm || rm > r.alloc_mem) ? 0
+                     : (int32_t)div_rn((double)((r.alloc_mem - rm) * kMaxNodeScore), (double)r.alloc_mem, inv_m);
+  if (bp.fit_w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
+  const int64_t wc = hc ? bp.fit_w_cpu : 0, wm = hm ? bp.fit_w_mem : 0;
+  const double inv = (hc && hm) ? bp.inv_w[2] : hc ? bp.inv_w[0] : bp.inv_w[1];
+  return (hc || hm) ? (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv) : 0;
+}
+
+// balancedResourceScorer over {cpu, memory}: the float64 quotients Go computes
+__device__ __forceinline__ int32_t fast_balanced_allocation(const ksim_pod& p, const NodeRow& r, double inv_c,
+                                                            double inv_m) {
+  const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
+  double f0 = 0, f1 = 0;
+  if (hc) {
+    const double f = div_rn((double)(r.req_cpu + p.req_cpu), (double)r.alloc_cpu, inv_c);
+    f0 = f > 1 ? 1 : f;
+  }
+  if (hm) {
+    const double f = div_rn((double)(r.req_mem + p.req_mem), (double)r.alloc_mem, inv_m);
+    if (hc) f1 = f > 1 ? 1 : f;
+    else f0 = f > 1 ? 1 : f;
+  }
+  const double std = (hc && hm) ? fabs((f0 - f1) / 2) : 0.0;
+  return (int32_t)((1 - std) * (double)kMaxNodeScore);
+}
+
 __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
                                                  double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
   if (bp.has_fit_filter) {
@@ -1436,39 +1481,9 @@ __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim
          p.req_eph > r.alloc_eph - r.req_eph))
       return 0;
   }
-  const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
-  const double ac = (double)r.alloc_cpu, am = (double)r.alloc_mem;
   int32_t tot = 0;
-  if (bp.w_fit) {                              // leastResourceScorer over {cpu, memory}
-    const int64_t rc = r.nz_cpu + p.nz_cpu, rm = r.nz_mem + p.nz_mem;
-    const int32_t sc = (!hc || rc > r.alloc_cpu) ? 0
-                       : (int32_t)div_rn((double)((r.alloc_cpu - rc) * kMaxNodeScore), ac, inv_c);
-    const int32_t sm = (!hm || rm > r.alloc_mem) ? 0
-                       : (int32_t)div_rn((double)((r.alloc_mem - rm) * kMaxNodeScore), am, inv_m);
-    int32_t la;
-    if (bp.fit_w_eq) {                         // (sc w + sm w) / (2 w)
-      la = (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;
-    } else {
-      const int64_t wc = hc ? bp.fit_w_cpu : 0, wm = hm ? bp.fit_w_mem : 0;
-      const double inv = (hc && hm) ? bp.inv_w[2] : hc ? bp.inv_w[0] : bp.inv_w[1];
-      la = (hc || hm) ? (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv) : 0;
-    }
-    tot += (int32_t)bp.w_fit * la;
-  }
-  if (bp.w_ba) {                               // balancedResourceScorer over {cpu, memory}
-    double f0 = 0, f1 = 0;
-    if (hc) {
-      const double f = div_rn((double)(r.req_cpu + p.req_cpu), ac, inv_c);
-      f0 = f > 1 ? 1 : f;
-    }
-    if (hm) {
-      const double f = div_rn((double)(r.req_mem + p.req_mem), am, inv_m);
-      if (hc) f1 = f > 1 ? 1 : f;
-      else f0 = f > 1 ? 1 : f;
-    }
-    const double std = (hc && hm) ? fabs((f0 - f1) / 2) : 0.0;
-    tot += (int32_t)bp.w_ba * (int32_t)((1 - std) * (double)kMaxNodeScore);
-  }
+  if (bp.w_fit) tot += (int32_t)bp.w_fit * fast_least_allocated(bp, p, r, inv_c, inv_m);
+  if (bp.w_ba) tot += (int32_t)bp.w_ba * fast_balanced_allocation(p, r, inv_c, inv_m);
   if (bp.no_score) tot = 1;
   const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
   return ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);

@@ -1083,6 +1083,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
     for (int32_t i = 0; i < n; i++)
       h->alloc_narrow = h->alloc_narrow && t->alloc_cpu[i] >= 0 && t->alloc_cpu[i] < (1ll << 46) &&
                         t->alloc_mem[i] >= 0 && t->alloc_mem[i] < (1ll << 46);
+    if (h->alloc_narrow) h->dc.cflags |= kClusterNarrow;
   }
   {
     void* q = nullptr;

@@ -425,7 +425,9 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
   // the node's row does not depend on the cycle: its loads go out before the
   // state / pod / plan chain
-  const NodeRow r = load_row(c, node < c.n ? node : c.n - 1);
+  const int32_t xr = node < c.n ? node : c.n - 1;
+  const NodeRow r = load_row(c, xr);
+  const double inv_c = c.inv_cpu[xr], inv_m = c.inv_mem[xr];
   const int32_t pi = st->cursor;
   if (pi >= st->end) return;
   // the pod record and its uses sit at a block-uniform address: scalar loads
@@ -521,8 +523,9 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
         if (i == soft) soft_cnt = t.x[i];          // soft_count: the node's own count or the domain sum
       }
       s.ign[node] = ign;
+      const BatchProg* fast = (bp->fast_w && (c.cflags & kClusterNarrow)) ? bp : nullptr;
       s.part[node] = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT, rv,
-                                    soft_cnt);
+                                    soft_cnt, fast, inv_c, inv_m);
     }
   }
   FS_CLK(4);

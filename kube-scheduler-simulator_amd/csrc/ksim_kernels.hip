@@ -365,14 +365,18 @@ __device__ __forceinline__ void best2_merge(uint64_t& img, uint64_t& lo, uint64_
 }
 
 // Per-slot extrema images of this block's values -> one atomicMax per slot.
+// zmask: slots whose raw score is 0 on every node for this pod; their extrema
+// are (0, 0) whenever some node is feasible (and unread otherwise), so block 0
+// stores them without a reduction.
 __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState* win, const uint64_t (&ix)[KSIM_MAX_SCORE],
-                                              const uint64_t (&in)[KSIM_MAX_SCORE], uint64_t (*s_red)[2 * KSIM_MAX_SCORE]) {
+                                              const uint64_t (&in)[KSIM_MAX_SCORE], uint64_t (*s_red)[2 * KSIM_MAX_SCORE],
+                                              uint32_t zmask = 0) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int S = prof.n_score;
 #pragma unroll
   for (int k = 0; k < KSIM_MAX_SCORE; k++) {
     if (k >= S) break;
-    if (norm_kind(prof.score[k]) == kNormNone) continue;
+    if (norm_kind(prof.score[k]) == kNormNone || ((zmask >> k) & 1u)) continue;
     const uint64_t a = wave_max_u64_dpp(ix[k]), b = wave_max_u64_dpp(in[k]);
     if (lane == 0) {
       s_red[wv][2 * k] = a;
@@ -382,8 +386,12 @@ __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState
   __syncthreads();
   if (tid < 2 * KSIM_MAX_SCORE && tid < 2 * S && norm_kind(prof.score[tid >> 1]) != kNormNone) {
     uint64_t m = 0;
+    if ((zmask >> (tid >> 1)) & 1u) {
+      m = blockIdx.x == 0 ? ((tid & 1) ? ~(1ull << 63) : (1ull << 63)) : 0ull;   // min_image(0) / max_image(0)
+    } else {
 #pragma unroll
-    for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
+      for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
+    }
     if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->ext[tid]), (unsigned long long)m);
   }
 }
@@ -575,7 +583,18 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
           in[k] = min_image(v);
         }
       }
-      block_extrema(prof, s.win, ix, in, s_red);
+      uint32_t zmask = 0;                          // slots constant 0 for this pod
+#pragma unroll
+      for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+        if (k >= prof.n_score) continue;
+        const int pl = (int)prof_score(prof, k);
+        const bool z = (pl == KSIM_PL_TAINT_TOLERATION && !(c.cflags & kClusterPreferTaints)) ||
+                       (pl == KSIM_PL_NODE_AFFINITY && p.pref_term_count == 0) ||
+                       (pl == KSIM_PL_INTER_POD_AFFINITY && m.score == 0) ||
+                       (pl == KSIM_PL_POD_TOPOLOGY_SPREAD && soft < 0);
+        if (z) zmask |= 1u << k;
+      }
+      block_extrema(prof, s.win, ix, in, s_red, zmask);
     }
   }
   FS_CLK(5);
@@ -897,6 +916,10 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   const bool tadds = (pp.flags & kPlanTadds) != 0;
   int4 ta = make_int4(0, 0, 0, 0);
   if (tadds && lane < pp.tadd_count) ta = P.ptab_padd[pp.tadd_first + lane];
+  // the window scalars and the scheduler state do not depend on the choice
+  // either (the row stores below could alias them for the compiler: load first)
+  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
+  DevState S = *st;                                // one read, one write back: no load-store chain
   const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);   // every lane
   const int32_t error = win->error;
   const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
@@ -912,8 +935,6 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
       }
   }
   if (lane != 0) return;
-  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
-  DevState S = *st;                                // one read, one write back: no load-store chain
   // nextStartNodeIndex = (nextStartNodeIndex + processed) % len(scanned nodes);
   // a pod PreFilter rejected scans nothing and leaves it
   const int32_t ns = NS > 0 ? (int32_t)(((int64_t)S.next_start + (cut < NS ? cut : NS)) % NS) : S.next_start;

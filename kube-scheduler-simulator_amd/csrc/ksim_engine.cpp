@@ -152,6 +152,13 @@ struct ksim_handle {
   uint64_t *ash_send = nullptr, *ash_recv = nullptr, *ash_gmask = nullptr;
   int32_t ash_world = 0, ash_w = 0;
   int64_t graph_captures = 0;                  // graphs captured since ksim_create (ksim_get_diag)
+  // node-sharded per-pod cycles (group leader): graphs of kGraphCycles cycles
+  // per shape (topology, exchange lengths), valid while every handle of the
+  // group keeps the graph generation it had at capture
+  int64_t graph_gen = 0;                       // bumped whenever this handle's cycle graphs are dropped
+  std::vector<std::pair<const ksim_handle*, int64_t>> sg_sig;
+  std::map<std::tuple<bool, int64_t, int64_t>, hipGraphExec_t> sg_graphs;
+  bool sg_off = false;                         // capture failed once (e.g. a collective that cannot be captured)
 };
 
 namespace {
@@ -201,6 +208,9 @@ void drop_cycle_graphs(ksim_handle* h) {
     if (g) (void)hipGraphExecDestroy(g);
     g = nullptr;
   }
+  for (auto& kv : h->sg_graphs) (void)hipGraphExecDestroy(kv.second);
+  h->sg_graphs.clear();
+  h->graph_gen++;
 }
 
 void drop_graphs(ksim_handle* h) {
@@ -605,12 +615,12 @@ int x_allgather2(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
   return KSIM_OK;
 }
 
-// One per-pod cycle (the pod at the shards' common cursor) across node shards.
-int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t stream) {
+// One per-pod cycle (the pod at the shards' common cursor) across node shards,
+// with exchanges of xdom / xreg words (at least the pod's own lengths: words
+// past them are summed but never read).
+int shard_cycle(const std::vector<ksim_handle*>& hs, bool topo, int64_t xdom, int64_t xreg, hipStream_t stream) {
   ksim_handle* h0 = hs[0];
   const int R = (int)hs.size();
-  const bool topo = h0->topo[pod] != 0;
-  const int64_t xdom = h0->xdom_len[pod], xreg = h0->xreg_len[pod];
   const int32_t world = h0->comm ? h0->world : R;
   int rc;
   if (topo) {
@@ -631,7 +641,50 @@ int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t st
   return KSIM_OK;
 }
 
-// Pods [a, b) on the sharded per-pod path, one cycle each.
+int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t stream) {
+  const ksim_handle* h0 = hs[0];
+  return shard_cycle(hs, h0->topo[pod] != 0, h0->xdom_len[pod], h0->xreg_len[pod], stream);
+}
+
+// kGraphCycles sharded cycles of one shape as a graph on the leader (its
+// stream carries every shard's kernels and the collectives), or nullptr when
+// capture is off or fails (the caller runs the cycles eagerly).
+hipGraphExec_t shard_graph(const std::vector<ksim_handle*>& hs, bool topo, int64_t xdom, int64_t xreg) {
+  ksim_handle* h0 = hs[0];
+  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  std::vector<std::pair<const ksim_handle*, int64_t>> sig;
+  for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
+  if (sig != h0->sg_sig) {                     // another group, or some handle dropped its graphs
+    for (auto& kv : h0->sg_graphs) (void)hipGraphExecDestroy(kv.second);
+    h0->sg_graphs.clear();
+    h0->sg_sig = sig;
+  }
+  const auto key = std::make_tuple(topo, xdom, xreg);
+  auto it = h0->sg_graphs.find(key);
+  if (it != h0->sg_graphs.end()) return it->second;
+  hipStream_t stream = h0->stream;
+  if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  for (int i = 0; ok && i < kGraphCycles; i++) ok = shard_cycle(hs, topo, xdom, xreg, stream) == KSIM_OK;
+  const hipError_t e = hipStreamEndCapture(stream, &g);   // ends a capture even after a failed launch
+  ok = ok && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  if (!ok) {
+    h0->sg_off = true;
+    h0->err.clear();
+    return nullptr;
+  }
+  h0->graph_captures++;
+  h0->sg_graphs.emplace(key, ge);
+  return ge;
+}
+
+// Pods [a, b) on the sharded per-pod path, one cycle each: whole graphs of
+// kGraphCycles cycles shaped for the run's largest exchanges, then single
+// cycles for the rest.
 int shard_run_perpod(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   ksim_handle* h0 = hs[0];
   hipStream_t stream = h0->stream;
@@ -640,7 +693,18 @@ int shard_run_perpod(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) 
     if ((rc = set_run(h, a, b))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
-  for (int32_t i = a; i < b; i++) {
+  int32_t i = a;
+  if (b - a >= kGraphCycles) {
+    const bool topo = h0->topo[a] != 0;          // runs are uniform in topo (for_each_run)
+    int64_t xdom = 0, xreg = 0;
+    for (int32_t k = a; k < b; k++) {
+      xdom = std::max(xdom, h0->xdom_len[k]);
+      xreg = std::max(xreg, h0->xreg_len[k]);
+    }
+    if (hipGraphExec_t g = shard_graph(hs, topo, xdom, xreg))
+      for (; i + kGraphCycles <= b; i += kGraphCycles) HIPCHK(h0, hipGraphLaunch(g, stream));
+  }
+  for (; i < b; i++) {
     int rc = shard_cycle(hs, i, stream);
     if (rc) return rc;
   }

@@ -75,34 +75,57 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
   const NodeRow r = load_row(c, on ? node : 0);
   const int32_t j1 = min(j0 + mp, nb);
 #pragma unroll 1
-  for (int32_t j = j0; j < j1; j++) {
-    const int32_t pi = base + j;
-    const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // uniform
-    const bool f = on && batch_feasible(c, P, bp, P.pods[pi], r, trivial);
-    const uint64_t m = __ballot(f);
-    if (lane == 0) amask[(size_t)j * n_words + w] = m;
+  for (int32_t j = j0; j < j1; j += 2) {           // two pods per step: both records' loads in flight
+    const int32_t jb = j + 1 < j1 ? j + 1 : j;
+    const bool ta = (P.bflags[base + j] & kBatchStaticTrivial) != 0;   // uniform
+    const bool tb = (P.bflags[base + jb] & kBatchStaticTrivial) != 0;
+    const bool fa = on && batch_feasible(c, P, bp, P.pods[base + j], r, ta);
+    const bool fb = on && batch_feasible(c, P, bp, P.pods[base + jb], r, tb);
+    const uint64_t ma = __ballot(fa), mb = __ballot(fb);
+    if (lane == 0) {
+      amask[(size_t)j * n_words + w] = ma;
+      if (jb != j) amask[(size_t)jb * n_words + w] = mb;
+    }
   }
 }
 
 // Rotated offset of the K-th (0-based) set bit of `mask` counting from node s,
 // or -1 when the bitmap holds at most K set bits.
+// Eight word segments per step: their loads do not depend on the counts, so
+// they go out together (one memory round trip per 512 nodes scanned instead of
+// one per 64).
 __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_t n, int32_t k) {
+  constexpr int kAhead = 8;
   int32_t need = k, off = 0, pos = s;
   while (off < n) {
-    const int32_t w = pos >> 6, b = pos & 63;
-    int32_t len = min((w + 1) * 64, n) - pos;
-    if (len > n - off) len = n - off;                // back at s's word after the wrap
-    uint64_t bits = mask[w] >> b;
-    if (len < 64) bits &= (1ull << len) - 1;
-    const int cnt = __popcll(bits);
-    if (need < cnt) {
-      for (int t = 0; t < need; t++) bits &= bits - 1;
-      return off + __builtin_ctzll(bits);
+    uint64_t bits[kAhead];
+    int32_t len[kAhead];
+    int32_t p = pos, o = off;
+#pragma unroll
+    for (int t = 0; t < kAhead; t++) {
+      const int32_t w = p >> 6, b = p & 63;
+      int32_t l = min((w + 1) * 64, n) - p;
+      if (l > n - o) l = n - o;                     // back at s's word after the wrap (0: past the end)
+      uint64_t x = mask[w] >> b;                     // p < n: w is in range
+      if (l < 64) x &= (1ull << l) - 1;
+      bits[t] = x;
+      len[t] = l;
+      o += l;
+      p += l;
+      if (p >= n) p = 0;
     }
-    need -= cnt;
-    off += len;
-    pos += len;
-    if (pos >= n) pos = 0;
+#pragma unroll
+    for (int t = 0; t < kAhead; t++) {
+      const int cnt = __popcll(bits[t]);
+      if (need < cnt) {
+        uint64_t x = bits[t];
+        for (int q = 0; q < need; q++) x &= x - 1;
+        return off + __builtin_ctzll(x);
+      }
+      need -= cnt;
+      off += len[t];
+    }
+    pos = p;
   }
   return -1;
 }
@@ -225,6 +248,32 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
       a[kTopT - 1] = umax64(a[kTopT - 1], node_key(g - c.base));
 #pragma unroll
       for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+    }
+  } else if constexpr (FAST) {
+    // two nodes per step, every load of both (bitmap words, rows) issued first
+#pragma unroll 1
+    for (int32_t off = tid; off < kend; off += 512) {
+      int32_t n1 = s + off, n2 = s + off + 256;
+      if (n1 >= n) n1 -= n;
+      if (n2 >= n) n2 -= n;
+      const bool v2 = off + 256 < kend;
+      if (!v2) n2 = n1;
+      const uint64_t w1 = mask[n1 >> 6], w2 = mask[n2 >> 6];
+      const NodeRow r1 = load_res_row(c, n1), r2 = load_res_row(c, n2);
+      const double c1 = c.inv_cpu[n1], m1 = c.inv_mem[n1], c2 = c.inv_cpu[n2], m2 = c.inv_mem[n2];
+      __builtin_amdgcn_sched_barrier(0);
+      if ((w1 >> (n1 & 63)) & 1ull) {
+        kept++;
+        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast(bp, p, r1, c1, m1, hseed, c.base + n1));
+#pragma unroll
+        for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+      }
+      if (v2 && ((w2 >> (n2 & 63)) & 1ull)) {
+        kept++;
+        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast(bp, p, r2, c2, m2, hseed, c.base + n2));
+#pragma unroll
+        for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+      }
     }
   } else {
 #pragma unroll 1

@@ -142,6 +142,8 @@ def test_group_config3(pct, world):
     cluster, pods = gen.config3(n_nodes=600, pods_per_node=10, n_incoming=700, seed=21, zone_anti_every=50)
     engines, ora = _check_group(cluster, pods, _prof_pct(pct), world)
     np.testing.assert_array_equal(np.concatenate([e.class_count() for e in engines], axis=1), ora.class_count())
+    # the 700 topology pods ran as graphs of 128 sharded cycles on the leader
+    assert engines[0].diag()["graph_captures"] >= 1
 
 
 def test_rccl_world1_perpod():
@@ -153,10 +155,13 @@ def test_rccl_world1_perpod():
     e.set_cluster(cluster)
     e.comm_init(0, 1, engine.comm_unique_id())
     e.load_pods(pods)
+    g0 = e.diag()["graph_captures"]
     chosen, st = e.schedule_loaded(0, pods.n_pods)
     ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals
+    # RCCL collectives captured with the cycles' kernels (graphs of 128 cycles)
+    assert e.diag()["graph_captures"] > g0
 
 
 def _prof_pct(pct, seed=0x4B53494D):

@@ -74,6 +74,43 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
   const bool on = node < c.n;
   const NodeRow r = load_row(c, on ? node : 0);
   const int32_t j1 = min(j0 + mp, nb);
+  // The group's request fields, one pod per lane (mp <= 32), read back per pod
+  // by readlane: no scalar memory round trip inside the pod loop.  Trivial
+  // pods only (every static filter host-proven to pass; batchable pods
+  // request no scalar resources).
+  int64_t qc = 0, qm = 0, qe = 0;
+  uint32_t qf = 0;
+  bool nontriv = false;
+  if (lane < j1 - j0) {
+    const ksim_pod& q = P.pods[base + j0 + lane];
+    qc = q.req_cpu;
+    qm = q.req_mem;
+    qe = q.req_eph;
+    qf = q.flags;
+    nontriv = !(P.bflags[base + j0 + lane] & kBatchStaticTrivial);
+  }
+  if (__ballot(nontriv) == 0) {                    // wave-uniform
+    const bool fit = bp.has_fit_filter != 0;
+    const bool room = r.num_pods + 1 <= r.alloc_pods;
+    const int64_t fc = r.alloc_cpu - r.req_cpu, fm = r.alloc_mem - r.req_mem, fe = r.alloc_eph - r.req_eph;
+#pragma unroll 1
+    for (int32_t j = j0; j < j1; j++) {
+      const int l = j - j0;
+      const int64_t c0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qc >> 32), l) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)qc, l));
+      const int64_t m0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qm >> 32), l) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)qm, l));
+      const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qe >> 32), l) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)qe, l));
+      const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)qf, l);
+      // fits_request: the pod count, then the requests unless the pod requests nothing
+      const bool none = c0 == 0 && m0 == 0 && e0 == 0 && !(f0 & KSIM_POD_HAS_SCALAR);
+      const bool ok = !fit || (room && (none || (c0 <= fc && m0 <= fm && e0 <= fe)));
+      const uint64_t m = __ballot(on && ok);
+      if (lane == 0) amask[(size_t)j * n_words + w] = m;
+    }
+    return;
+  }
 #pragma unroll 1
   for (int32_t j = j0; j < j1; j += 2) {           // two pods per step: both records' loads in flight
     const int32_t jb = j + 1 < j1 ? j + 1 : j;

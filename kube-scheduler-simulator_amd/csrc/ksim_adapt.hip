@@ -167,7 +167,8 @@ __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_
   return -1;
 }
 
-constexpr int kWindowRounds = 48;   // exact prefix kept if not converged by then
+constexpr int kWindowRounds = 48;
+constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length   // exact prefix kept if not converged by then
 
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
@@ -227,8 +228,10 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
 // best keys and count | complete << 32) for the all-gather instead of topk.
 // FAST: the narrow-arithmetic keys (dyn_key_fast; trivial cpu/memory pods, see
 // ksim_batch.hip).
-template <bool SH, bool FAST>
-__global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
+// NT threads per block: 256, or 1024 for long windows (K >= kTopWideK), so
+// the block's waves fill their SIMDs (every CU holds one pod's block).
+template <bool SH, bool FAST, int NT>
+__global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words,
@@ -239,8 +242,10 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
                                                    uint64_t* __restrict__ xsend) {
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
-  __shared__ uint64_t s_top[4][kTopT];
-  __shared__ int32_t s_kept[4];
+  constexpr int W = NT / 64;
+  constexpr int kSlots = (W * kTopT + 63) / 64;     // merge entries per lane
+  __shared__ uint64_t s_top[W][kTopT];
+  __shared__ int32_t s_kept[W];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t j = blockIdx.x;
   const int32_t base = st->cursor;
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
     const int32_t a0 = max(s, lo), a1 = min(e1, hi), b0 = max(0, lo), b1 = min(e2, hi);
     const int32_t len1 = a1 > a0 ? a1 - a0 : 0, len2 = b1 > b0 ? b1 - b0 : 0;
 #pragma unroll 1
-    for (int32_t i = tid; i < len1 + len2; i += 256) {
+    for (int32_t i = tid; i < len1 + len2; i += NT) {
       const int32_t g = i < len1 ? a0 + i : b0 + (i - len1);
       if (!((mask[g >> 6] >> (g & 63)) & 1ull)) continue;
       kept++;
@@ -289,11 +294,11 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   } else if constexpr (FAST) {
     // two nodes per step, every load of both (bitmap words, rows) issued first
 #pragma unroll 1
-    for (int32_t off = tid; off < kend; off += 512) {
-      int32_t n1 = s + off, n2 = s + off + 256;
+    for (int32_t off = tid; off < kend; off += 2 * NT) {
+      int32_t n1 = s + off, n2 = s + off + NT;
       if (n1 >= n) n1 -= n;
       if (n2 >= n) n2 -= n;
-      const bool v2 = off + 256 < kend;
+      const bool v2 = off + NT < kend;
       if (!v2) n2 = n1;
       const uint64_t w1 = mask[n1 >> 6], w2 = mask[n2 >> 6];
       const NodeRow r1 = load_res_row(c, n1), r2 = load_res_row(c, n2);
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
     }
   } else {
 #pragma unroll 1
-    for (int32_t off = tid; off < kend; off += 256) {
+    for (int32_t off = tid; off < kend; off += NT) {
       int32_t node = s + off;
       if (node >= n) node -= n;
       if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
@@ -340,18 +345,30 @@ __global__ __launch_bounds__(256) void k_adapt_top(DevCluster c, DevPods P, cons
   if (lane == 0) s_kept[wv] = kept;
   __syncthreads();
   if (wv != 0) return;
-  // merge: lane l < 4T holds entry l % T of wave l / T (keys are unique per node)
-  uint64_t key = lane < 4 * kTopT ? s_top[lane / kTopT][lane % kTopT] : 0;
+  // merge: entry x = w * T + e (keys are unique per node) sits in lane x % 64, slot x / 64
+  uint64_t key[kSlots];
+#pragma unroll
+  for (int q = 0; q < kSlots; q++) {
+    const int x = q * 64 + lane;
+    key[q] = x < W * kTopT ? s_top[x / kTopT][x % kTopT] : 0;
+  }
   uint64_t mine = 0;
   int32_t cnt = 0;
   for (int t = 0; t < kTopT; t++) {
-    const uint64_t m = wave_max_u64_hi(key);
+    uint64_t best = key[0];
+#pragma unroll
+    for (int q = 1; q < kSlots; q++) best = umax64(best, key[q]);
+    const uint64_t m = wave_max_u64_hi(best);
     if (m == 0) break;
     if (lane == t) mine = m;
     cnt = t + 1;
-    if (key == m) key = 0;
+#pragma unroll
+    for (int q = 0; q < kSlots; q++)
+      if (key[q] == m) key[q] = 0;
   }
-  const int32_t total = s_kept[0] + s_kept[1] + s_kept[2] + s_kept[3];
+  int32_t total = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) total += s_kept[w];
   if (SH) {
     uint64_t* x = xsend + (size_t)j * kXRec;
     if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
@@ -455,14 +472,16 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  if (a.fast)
-    k_adapt_top<false, true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
-                                                             a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, nullptr);
-  else
-    k_adapt_top<false, false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
-                                                              a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt,
-                                                              a.s.topk_complete, nullptr);
+#define TOP(F, NT) k_adapt_top<false, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
+    a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr)
+  if (k >= kTopWideK) {
+    if (a.fast) TOP(true, 1024);
+    else TOP(false, 1024);
+  } else {
+    if (a.fast) TOP(true, 256);
+    else TOP(false, 256);
+  }
+#undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
   launch_chain(a, stream);
   if (evs) (void)hipEventRecord(evs[4], stream);
@@ -507,14 +526,16 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
   k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
   k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
-  if (a.fast)
-    k_adapt_top<true, true><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
-                                                            a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                                            a.s.xsend);
-  else
-    k_adapt_top<true, false><<<kBatchPods, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
-                                                             a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                                             a.s.xsend);
+#define TOP(F, NT) k_adapt_top<true, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, \
+    nw, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend)
+  if (k >= kTopWideK) {
+    if (a.fast) TOP(true, 1024);
+    else TOP(false, 1024);
+  } else {
+    if (a.fast) TOP(true, 256);
+    else TOP(false, 256);
+  }
+#undef TOP
 }
 
 void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream) {

@@ -245,6 +245,36 @@ def test_config4_group8():
     assert st.evals == ost.evals and st.scheduled == ost.scheduled
 
 
+@pytest.mark.parametrize("world", [1, 8])
+def test_config4_adapt(world):
+    """Config 4's cluster in the simulator's own mode (percentageOfNodesToScore
+    0: K = 5,000 of 100,000, the wide k_adapt_top), 6,000 pods, on one handle
+    and as an in-process 8-shard group (the node-sharded ADAPT batch protocol)."""
+    cluster, pods = gen.config4(n_pods=6000)
+    prof = _prof(0)
+    if world == 1:
+        eng = _engine(cluster, prof)
+        chosen, st = eng.schedule_batch(pods)
+        starts = [eng.next_start]
+    else:
+        engines = []
+        for base, cnt in partition(cluster.n_nodes, world):
+            e = Engine(0)
+            e.set_shard(base, cluster.n_nodes)
+            e.set_profile(prof)
+            e.set_cluster(cluster.shard(base, cnt))
+            e.load_pods(pods)
+            engines.append(e)
+        chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+        starts = [e.next_start for e in engines]
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=16)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert all(s == ora.next_start for s in starts)
+    assert st.perpod_cycles == 0                     # every pod on the ADAPT batch path
+
+
 # ---- the Go-harness fixtures through the engine --------------------------------------
 GO = sorted(p for p in __import__("glob").glob(os.path.join(os.path.dirname(__file__), "golden", "go", "*.json.gz"))
             if not p.endswith(".go.json.gz"))

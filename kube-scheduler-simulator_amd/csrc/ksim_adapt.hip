@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
     const bool fit = bp.has_fit_filter != 0;
     const bool room = r.num_pods + 1 <= r.alloc_pods;
     const int64_t fc = r.alloc_cpu - r.req_cpu, fm = r.alloc_mem - r.req_mem, fe = r.alloc_eph - r.req_eph;
+    uint64_t word = 0;                             // lane l: pod j0 + l's ballot
 #pragma unroll 1
     for (int32_t j = j0; j < j1; j++) {
       const int l = j - j0;
@@ -107,8 +108,9 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
       const bool none = c0 == 0 && m0 == 0 && e0 == 0 && !(f0 & KSIM_POD_HAS_SCALAR);
       const bool ok = !fit || (room && (none || (c0 <= fc && m0 <= fm && e0 <= fe)));
       const uint64_t m = __ballot(on && ok);
-      if (lane == 0) amask[(size_t)j * n_words + w] = m;
+      word = lane == l ? m : word;
     }
+    if (lane < j1 - j0) amask[(size_t)(j0 + lane) * n_words + w] = word;   // one store instruction per wave
     return;
   }
 #pragma unroll 1

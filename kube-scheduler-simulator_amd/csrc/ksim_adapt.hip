@@ -48,7 +48,7 @@ __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPod
 }
 
 // The S0 feasibility bitmaps, node-stationary: a block of 256 threads holds
-// one node per thread (its row loaded once) and sweeps kMaskPods pods of the
+// one node per thread (its row loaded once) and sweeps mp <= 64 pods of the
 // batch, one ballot per pod and 64-node word.  (A pod-per-block form re-reads
 // every node row once per pod: B x the node table from L2 / MALL per batch,
 // ~190 us at 100k nodes; here a row is read once per mp pods.)  mp shrinks on
@@ -56,7 +56,7 @@ __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPod
 __host__ __device__ inline int32_t mask_pods(int32_t n_words) {
   const int32_t wb = (n_words + 3) / 4;            // 4 words (waves) per block
   const int32_t mp = wb / 8;                       // about 2,048 blocks over B pods
-  return mp < 1 ? 1 : mp > 32 ? 32 : mp;
+  return mp < 1 ? 1 : mp > 64 ? 64 : mp;
 }
 
 __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
@@ -72,9 +72,9 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
   if (w >= n_words) return;                          // wave-uniform
   const int32_t node = w * 64 + lane;
   const bool on = node < c.n;
-  const NodeRow r = load_row(c, on ? node : 0);
+  const int32_t x = on ? node : 0;
   const int32_t j1 = min(j0 + mp, nb);
-  // The group's request fields, one pod per lane (mp <= 32), read back per pod
+  // The group's request fields, one pod per lane (mp <= 64), read back per pod
   // by readlane: no scalar memory round trip inside the pod loop.  Trivial
   // pods only (every static filter host-proven to pass; batchable pods
   // request no scalar resources).
@@ -90,9 +90,16 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
     nontriv = !(P.bflags[base + j0 + lane] & kBatchStaticTrivial);
   }
   if (__ballot(nontriv) == 0) {                    // wave-uniform
+    // only the Fit filter's columns (the table is re-read once per pod group)
     const bool fit = bp.has_fit_filter != 0;
-    const bool room = r.num_pods + 1 <= r.alloc_pods;
-    const int64_t fc = r.alloc_cpu - r.req_cpu, fm = r.alloc_mem - r.req_mem, fe = r.alloc_eph - r.req_eph;
+    bool room = true;
+    int64_t fc = 0, fm = 0, fe = 0;
+    if (fit) {
+      room = c.num_pods[x] + 1 <= c.alloc_pods[x];
+      fc = c.alloc_cpu[x] - c.req_cpu[x];
+      fm = c.alloc_mem[x] - c.req_mem[x];
+      fe = c.alloc_eph[x] - c.req_eph[x];
+    }
     uint64_t word = 0;                             // lane l: pod j0 + l's ballot
 #pragma unroll 1
     for (int32_t j = j0; j < j1; j++) {
@@ -113,6 +120,7 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
     if (lane < j1 - j0) amask[(size_t)(j0 + lane) * n_words + w] = word;   // one store instruction per wave
     return;
   }
+  const NodeRow r = load_row(c, x);
 #pragma unroll 1
   for (int32_t j = j0; j < j1; j += 2) {           // two pods per step: both records' loads in flight
     const int32_t jb = j + 1 < j1 ? j + 1 : j;

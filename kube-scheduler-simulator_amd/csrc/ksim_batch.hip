@@ -129,6 +129,12 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
 // incomplete wave (every key a wave did not list is below it).  complete = 1:
 // every S0-feasible node is in the pod's list.  This replaces k_batch_eval's
 // per-tile lists and the k_batch_merge launch.
+#ifndef KSIM_TOP_STEP
+#define KSIM_TOP_STEP 2
+#endif
+constexpr int kTopStep = KSIM_TOP_STEP;   // nodes per lane per step of the FAST loop
+
+
 template <bool FAST, int kTopThreads>
 __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
@@ -156,25 +162,30 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
   int32_t nfeas = 0;
   if constexpr (FAST) {
-    // two nodes per step as independent chains (both rows loaded up front)
+    // kTopStep nodes per step as independent chains (every row loaded up front)
 #pragma unroll 1
-    for (int32_t node = threadIdx.x; node < c.n; node += 2 * kTopThreads) {
-      const int32_t n2 = node + kTopThreads;
-      const int32_t x2 = n2 < c.n ? n2 : node;
-      const NodeRow r1 = load_res_row(c, node), r2 = load_res_row(c, x2);
-      const double c1 = c.inv_cpu[node], m1 = c.inv_mem[node], c2 = c.inv_cpu[x2], m2 = c.inv_mem[x2];
-      __builtin_amdgcn_sched_barrier(0);      // both rows in flight before the first key
-      const uint64_t k1 = dyn_key_fast(bp, p, r1, c1, m1, hseed, c.base + node);
-      const uint64_t k2 = n2 < c.n ? dyn_key_fast(bp, p, r2, c2, m2, hseed, c.base + n2) : 0;
-      nfeas += (k1 != 0) + (k2 != 0);
-      a[3] = umax64(a[3], k1);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
-      a[3] = umax64(a[3], k2);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
+    for (int32_t node = threadIdx.x; node < c.n; node += kTopStep * kTopThreads) {
+      NodeRow r[kTopStep];
+      double ic[kTopStep], im[kTopStep];
+#pragma unroll
+      for (int u = 0; u < kTopStep; u++) {
+        const int32_t nu = node + u * kTopThreads;
+        const int32_t x = nu < c.n ? nu : node;
+        r[u] = load_res_row(c, x);
+        ic[u] = c.inv_cpu[x];
+        im[u] = c.inv_mem[x];
+      }
+      __builtin_amdgcn_sched_barrier(0);      // every row in flight before the first key
+#pragma unroll
+      for (int u = 0; u < kTopStep; u++) {
+        const int32_t nu = node + u * kTopThreads;
+        const uint64_t k = nu < c.n ? dyn_key_fast(bp, p, r[u], ic[u], im[u], hseed, c.base + nu) : 0;
+        nfeas += k != 0;
+        a[3] = umax64(a[3], k);
+        cswap_desc(a[2], a[3]);
+        cswap_desc(a[1], a[2]);
+        cswap_desc(a[0], a[1]);
+      }
     }
   }
 #pragma unroll 1

@@ -1,0 +1,144 @@
+// Package engine is the cgo binding of libksim_engine.so (include/ksim_engine.h)
+// that a maintainer would add to the simulator as simulator/scheduler/engine,
+// next to the plugin factory it serves (simulator/scheduler/plugin/plugins.go:75-87:
+// the closure builds the original in-tree plugin `p` and wraps it with
+// NewWrappedPlugin; an engine-backed plugin takes the place of `p`).
+//
+// NOT BUILT HERE: the build container has no Go toolchain.  The declarations
+// follow the C header one to one; INTEGRATION.md describes the call sequence.
+//
+// Every call copies its inputs before returning and keeps no Go pointer, which
+// satisfies the cgo pointer-passing rules.  CGO_ENABLED=0 in
+// simulator/Dockerfile:5 must become 1, and libamdhip64.so must be present
+// next to libksim_engine.so.
+package engine
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../kube-scheduler-simulator_amd/ksim -lksim_engine -Wl,-rpath,${SRCDIR}/../../../kube-scheduler-simulator_amd/ksim
+#include <stdlib.h>
+#include "ksim_engine.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+)
+
+// ABIVersion is the header version this binding was written against.
+const ABIVersion = 4
+
+// Engine owns one device handle (one GPU, or one node shard of a cluster).
+type Engine struct{ h *C.ksim_handle }
+
+// New opens the engine on a HIP device; it fails when no GPU is present (the
+// engine has no CPU fallback).
+func New(device int) (*Engine, error) {
+	if v := int(C.ksim_abi_version()); v != ABIVersion {
+		return nil, fmt.Errorf("libksim_engine ABI %d, binding %d", v, ABIVersion)
+	}
+	var h *C.ksim_handle
+	if rc := C.ksim_create(C.int(device), &h); rc != C.KSIM_OK {
+		return nil, fmt.Errorf("ksim_create: %d", int(rc))
+	}
+	return &Engine{h: h}, nil
+}
+
+// Close releases the handle and its device memory.
+func (e *Engine) Close() { C.ksim_destroy(e.h) }
+
+func (e *Engine) err(rc C.int) error {
+	if rc == C.KSIM_OK {
+		return nil
+	}
+	return fmt.Errorf("ksim %d: %s", int(rc), C.GoString(C.ksim_last_error(e.h)))
+}
+
+// SetProfile installs the converted KubeSchedulerProfile
+// (convertConfigurationForSimulator, simulator/scheduler/scheduler.go:199-249).
+func (e *Engine) SetProfile(p *C.ksim_profile) error { return e.err(C.ksim_set_profile(e.h, p)) }
+
+// SetCluster uploads the whole snapshot in nodeTree order (resets
+// nextStartNodeIndex).  t's column pointers point into Go memory pinned for
+// the call only.
+func (e *Engine) SetCluster(t *C.ksim_node_table, v *C.ksim_vocab) error {
+	return e.err(C.ksim_set_cluster(e.h, t, v))
+}
+
+// UpsertNodes applies node informer events (AddNode / UpdateNode / RemoveNode)
+// without losing the binds the cycles made: t is the new snapshot, oldPos[i]
+// the previous position of new node i or -1.  Reload the pod queue afterwards.
+func (e *Engine) UpsertNodes(t *C.ksim_node_table, v *C.ksim_vocab, oldPos []int32) error {
+	var p *C.int32_t
+	if len(oldPos) > 0 {
+		p = (*C.int32_t)(unsafe.Pointer(&oldPos[0]))
+	}
+	return e.err(C.ksim_upsert_nodes(e.h, t, v, p))
+}
+
+// RemoveNode removes the node at position pos (later nodes move down by one).
+func (e *Engine) RemoveNode(pos int) error { return e.err(C.ksim_remove_node(e.h, C.int32_t(pos))) }
+
+// EvalPod runs one full cycle for pod idx of ps (PreFilter .. bind) and fills
+// the per-node outputs the wrapped plugins record (out's slices are Go-owned:
+// n_nodes entries, n_score x n_nodes for the score matrices).
+func (e *Engine) EvalPod(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
+	return e.err(C.ksim_eval_pod(e.h, ps, C.int32_t(idx), out))
+}
+
+// Assume / Forget: NodeInfo.AddPod / RemovePod of a bound pod (informer pod
+// events, Unreserve), count classes included.
+func (e *Engine) Assume(ps *C.ksim_pod_set, idx, node int) error {
+	return e.err(C.ksim_assume(e.h, ps, C.int32_t(idx), C.int32_t(node)))
+}
+
+func (e *Engine) Forget(ps *C.ksim_pod_set, idx, node int) error {
+	return e.err(C.ksim_forget(e.h, ps, C.int32_t(idx), C.int32_t(node)))
+}
+
+// LoadPods uploads a pending queue in PrioritySort order for ScheduleLoaded.
+func (e *Engine) LoadPods(ps *C.ksim_pod_set) error { return e.err(C.ksim_load_pods(e.h, ps)) }
+
+// ScheduleLoaded schedules loaded pods [first, first+count) on the device
+// (batch, ADAPT batch or per-pod cycles; placements identical to cycle by
+// cycle).  chosen[i] receives the node position of pod first+i, or -1.
+func (e *Engine) ScheduleLoaded(first, count int, chosen []int32) (C.ksim_batch_stats, error) {
+	var st C.ksim_batch_stats
+	var p *C.int32_t
+	if len(chosen) > 0 {
+		p = (*C.int32_t)(unsafe.Pointer(&chosen[0]))
+	}
+	rc := C.ksim_schedule_loaded(e.h, C.int32_t(first), C.int32_t(count), p, &st)
+	return st, e.err(rc)
+}
+
+// ResetCluster restores the snapshot of the last SetCluster / UpsertNodes.
+func (e *Engine) ResetCluster() error { return e.err(C.ksim_reset_cluster(e.h)) }
+
+// NextStart is the scheduler's nextStartNodeIndex.
+func (e *Engine) NextStart() (int, error) {
+	var v C.int32_t
+	rc := C.ksim_get_next_start(e.h, &v)
+	return int(v), e.err(rc)
+}
+
+// Multi-GPU: one process per GPU.  SetShard (before SetCluster) gives this
+// handle the contiguous node range [base, base+count) of nTotal; rank 0 makes
+// the communicator id with CommUniqueID, the ranks share it over any side
+// channel, and each calls CommInit.
+func (e *Engine) SetShard(base, nTotal int) error {
+	return e.err(C.ksim_set_shard(e.h, C.int32_t(base), C.int32_t(nTotal)))
+}
+
+func CommUniqueID() ([C.KSIM_COMM_ID_BYTES]byte, error) {
+	var id [C.KSIM_COMM_ID_BYTES]byte
+	if rc := C.ksim_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&id[0]))); rc != C.KSIM_OK {
+		return id, fmt.Errorf("ksim_comm_unique_id: %d", int(rc))
+	}
+	return id, nil
+}
+
+func (e *Engine) CommInit(rank, world int, id [C.KSIM_COMM_ID_BYTES]byte) error {
+	return e.err(C.ksim_comm_init(e.h, C.int32_t(rank), C.int32_t(world), (*C.uint8_t)(unsafe.Pointer(&id[0]))))
+}

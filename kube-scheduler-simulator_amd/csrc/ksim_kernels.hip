@@ -445,6 +445,10 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
   FS_CLK(1);
+  // the node's topology inputs depend on the pod's uses only: their loads go
+  // out before the critical-path phase and its barrier
+  TopoRow t;
+  if (p.use_count) load_topo_row(c, U, p.use_count, m, s, P0.ptab, xr, t);
   const bool pt = (pp.flags & kPlanPtab) != 0;    // block-uniform: persistent tables
   if ((fuse_min && m.hard) || (pt && (m.aff | m.score))) {
     if (threadIdx.x < 64 && fuse_min) {            // the critical paths, one wave
@@ -508,8 +512,6 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     }
 #endif
     const FilterPlan fp{bp->rank_lo, bp->rank_hi, pp.filter_en};
-    TopoRow t;
-    if (p.use_count) load_topo_row(c, U, p.use_count, m, s, P0.ptab, node, t);
 #ifdef KSIM_FS_CLOCKS
     __builtin_amdgcn_s_waitcnt(0);
     if (threadIdx.x == 0) {

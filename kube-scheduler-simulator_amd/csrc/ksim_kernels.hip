@@ -368,9 +368,11 @@ __device__ __forceinline__ void best2_merge(uint64_t& img, uint64_t& lo, uint64_
 // zmask: slots whose raw score is 0 on every node for this pod; their extrema
 // are (0, 0) whenever some node is feasible (and unread otherwise), so block 0
 // stores them without a reduction.
+// s_cnt (optional): per wave {feasible, ignored} counts, added to the window
+// counters once per block after the barrier (one atomic per block, not per wave).
 __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState* win, const uint64_t (&ix)[KSIM_MAX_SCORE],
                                               const uint64_t (&in)[KSIM_MAX_SCORE], uint64_t (*s_red)[2 * KSIM_MAX_SCORE],
-                                              uint32_t zmask = 0) {
+                                              uint32_t zmask = 0, const int32_t (*s_cnt)[2] = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int S = prof.n_score;
 #pragma unroll
@@ -393,6 +395,11 @@ __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState
       for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
     }
     if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->ext[tid]), (unsigned long long)m);
+  }
+  if (s_cnt && (tid == 64 || tid == 65)) {
+    const int q = tid - 64;
+    const int32_t v = s_cnt[0][q] + s_cnt[1][q] + s_cnt[2][q] + s_cnt[3][q];
+    if (v) atomicAdd(q ? &win->nign : &win->nfeas, v);
   }
 }
 
@@ -425,6 +432,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
                                                       int32_t fuse_min, int32_t fuse_ext) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
+  __shared__ int32_t s_cnt[4][2];
   __shared__ uint32_t s_tf;
 #ifdef KSIM_FS_CLOCKS
   uint64_t fs_t = 0;
@@ -543,8 +551,13 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     const int lane = threadIdx.x & 63;
     WinState* win = s.win;
     const uint64_t fm = __ballot(feasible), im = __ballot(feasible && ign);
-    if (lane == 0 && fm) atomicAdd(&win->nfeas, (int32_t)__popcll(fm));
-    if (lane == 0 && im) atomicAdd(&win->nign, (int32_t)__popcll(im));
+    if (!fuse_ext) {                               // block-uniform
+      if (lane == 0 && fm) atomicAdd(&win->nfeas, (int32_t)__popcll(fm));
+      if (lane == 0 && im) atomicAdd(&win->nign, (int32_t)__popcll(im));
+    } else if (lane == 0) {                        // summed per block by block_extrema
+      s_cnt[threadIdx.x >> 6][0] = (int32_t)__popcll(fm);
+      s_cnt[threadIdx.x >> 6][1] = (int32_t)__popcll(im);
+    }
     if (P.bflags[pi] & kPodRegistersValues) {
       const uint32_t vwords = (uint32_t)(c.vmax + 31) >> 5;
       for (uint32_t b = m.soft_val; b; b &= b - 1) {
@@ -596,7 +609,7 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
                        (pl == KSIM_PL_POD_TOPOLOGY_SPREAD && soft < 0);
         if (z) zmask |= 1u << k;
       }
-      block_extrema(prof, s.win, ix, in, s_red, zmask);
+      block_extrema(prof, s.win, ix, in, s_red, zmask, s_cnt);
     }
   }
   FS_CLK(5);

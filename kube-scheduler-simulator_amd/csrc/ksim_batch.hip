@@ -651,6 +651,13 @@ __global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {
   for (int r = 0; r < g.n; r++) g.p[r][j] = m;
 }
 
+// k_batch_chain's phase clocks (diag "dbg" words 0-4) only when asked for
+// (KSIM_CHAIN_CLOCKS): the five device atomics sit at the end of every chain.
+static unsigned long long* chain_clock(const LaunchArgs& a) {
+  static const bool on = getenv("KSIM_CHAIN_CLOCKS") != nullptr;
+  return on ? a.s.dbg : nullptr;
+}
+
 const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch_merge", "k_batch_chain",
                                                          "k_batch_pairs", "k_batch_commit"};
 
@@ -693,7 +700,7 @@ uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) 
   launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, a.s.dbg);
+                                              a.s.gkey, a.s.chain_end, chain_clock(a));
   if (evs) (void)hipEventRecord(evs[3], stream);
   // pair keys, then a separate one-block commit: cheaper than every block of
   // the pairs kernel fencing for a last-block election
@@ -724,7 +731,7 @@ void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
 
 void launch_chain(const LaunchArgs& a, hipStream_t stream) {
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, a.s.dbg);
+                                              a.s.gkey, a.s.chain_end, chain_clock(a));
 }
 
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) { launch_eval_top(a, a.s.xsend, stream); }
@@ -737,7 +744,7 @@ void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) 
   k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
                                                      a.s.topk_complete);
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, a.s.dbg);
+                                              a.s.gkey, a.s.chain_end, chain_clock(a));
   if (a.fast)
     k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
                                                                a.s.pmax);

@@ -275,6 +275,46 @@ def test_config4_adapt(world):
     assert st.perpod_cycles == 0                     # every pod on the ADAPT batch path
 
 
+def test_persistent_tables_under_assume_forget():
+    """The persistent domain tables follow binds made outside the loaded queue
+    (ksim_assume / ksim_forget of single uploads: the class-index update path)
+    and snapshot resets: an engine reading the tables must place every later
+    pod exactly as one that recomputes the domain sums per cycle
+    (k_topo_prefilter, KSIM_NO_PTAB), and both as the oracle before the binds."""
+    cluster, pods = gen.config3(n_nodes=800, pods_per_node=6, n_incoming=900, seed=31, zone_anti_every=40)
+    extra = pods.subset(800, 60)                     # same encoding: their adds name this cluster's classes
+    prof = _prof(100)
+    a = _engine(cluster, prof)
+    a.load_pods(pods)
+    os.environ["KSIM_NO_PTAB"] = "1"
+    try:
+        b = _engine(cluster, prof)
+        b.load_pods(pods)
+    finally:
+        del os.environ["KSIM_NO_PTAB"]
+    ca, _ = a.schedule_loaded(0, 300)
+    cb, _ = b.schedule_loaded(0, 300)
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(ca, Oracle(cluster, prof).schedule(pods.subset(0, 300))[0])
+    nodes = [(i * 37) % cluster.n_nodes for i in range(extra.n_pods)]
+    for e in (a, b):
+        for i, n in enumerate(nodes):
+            e.assume(extra, i, n)
+        for i in range(0, extra.n_pods, 3):
+            e.forget(extra, i, nodes[i])
+    ca, _ = a.schedule_loaded(300, pods.n_pods - 300)
+    cb, _ = b.schedule_loaded(300, pods.n_pods - 300)
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_array_equal(a.class_count(), b.class_count())
+    # a reset rebuilds the tables from the snapshot counts: the run repeats
+    for e in (a, b):
+        e.reset_cluster()
+    ca2, _ = a.schedule_loaded(0, pods.n_pods)
+    cb2, _ = b.schedule_loaded(0, pods.n_pods)
+    np.testing.assert_array_equal(ca2, cb2)
+    np.testing.assert_array_equal(ca2, Oracle(cluster, prof).schedule(pods)[0])
+
+
 # ---- the Go-harness fixtures through the engine --------------------------------------
 GO = sorted(p for p in __import__("glob").glob(os.path.join(os.path.dirname(__file__), "golden", "go", "*.json.gz"))
             if not p.endswith(".go.json.gz"))

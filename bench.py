@@ -176,7 +176,7 @@ def build(cfg: int, args, rank: int, world: int):
     if cfg == 5:
         cluster, pods = gen.config2(5000, 10000)
         desc = f"config5: {args.sweep} score-weight vectors over 5000 nodes x 10000 pods, {args.mode.upper()}, " \
-               f"vectors split over {world} GPU(s)"
+               f"vectors split over {world} GPU(s), {args.sweep_streams} concurrent engines per GPU"
         return cluster, pods, sp, desc, False, "strong"
     raise SystemExit(f"unknown config {cfg}")
 
@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--nodes4", type=int, default=100000)
     ap.add_argument("--pods4", type=int, default=1000000)
     ap.add_argument("--sweep", type=int, default=1024)
+    ap.add_argument("--sweep-streams", type=int, default=8,
+                    help="config 5: engines (streams) sweeping weight vectors concurrently per GPU")
     ap.add_argument("--force-shard", action="store_true",
                     help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -246,14 +248,26 @@ def main():
         weights = gen.config5_weights(args.sweep)[rank::world]
         names = [p.name for p in sp.score_plugins()]
         profs = [profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, w)})) for w in weights]
+        # Independent weight vectors run concurrently: one engine (own stream,
+        # own copy of the 5,000-node snapshot) per host thread, so one sweep's
+        # latency-bound batch kernels overlap another's (ctypes releases the GIL).
+        engs = [eng]
+        for _ in range(max(1, args.sweep_streams) - 1):
+            e = engine.Engine(local)
+            e.set_profile(prof)
+            e.set_cluster(cluster)
+            e.load_pods(pods)
+            engs.append(e)
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(len(engs))
 
-        def step():
-            agg = None
-            for pr in profs:
-                eng.set_profile(pr)
-                eng.load_pods(pods)
-                eng.reset_cluster()
-                _, st = eng.schedule_loaded(0, pods.n_pods, want_chosen=False)
+        def run_part(j):
+            e, agg = engs[j], None
+            for pr in profs[j::len(engs)]:
+                e.set_profile(pr)
+                e.load_pods(pods)
+                e.reset_cluster()
+                _, st = e.schedule_loaded(0, pods.n_pods, want_chosen=False)
                 if agg is None:
                     agg = st
                 else:
@@ -261,6 +275,15 @@ def main():
                               "perpod_cycles"):
                         setattr(agg, f, getattr(agg, f) + getattr(st, f))
                     agg.device_ms += st.device_ms
+            return agg
+
+        def step():
+            parts = [p for p in pool.map(run_part, range(len(engs))) if p is not None]
+            agg = parts[0]
+            for st in parts[1:]:
+                for f in ("pods", "scheduled", "unschedulable", "evals", "batches", "truncations", "perpod_cycles"):
+                    setattr(agg, f, getattr(agg, f) + getattr(st, f))
+                agg.device_ms += st.device_ms
             return agg
     else:
         def step():

@@ -275,6 +275,41 @@ def test_config4_adapt(world):
     assert st.perpod_cycles == 0                     # every pod on the ADAPT batch path
 
 
+def test_sweep_concurrent_engines():
+    """bench.py config 5's concurrent form: weight vectors split over engines
+    driven from host threads (own streams, own graphs); every vector's
+    placements equal the sequential one-engine sweep's."""
+    from concurrent.futures import ThreadPoolExecutor
+    cluster, pods = gen.config2(n_nodes=1000, n_pods=2000)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    names = [p.name for p in sp.score_plugins()]
+    profs = [profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, w)}))
+             for w in gen.config5_weights(16)]
+    ref = _engine(cluster, profs[0])
+    want = []
+    for pr in profs:
+        ref.set_profile(pr)
+        want.append(ref.schedule_batch(pods)[0])
+        ref.reset_cluster()
+    engs = [_engine(cluster, profs[0]) for _ in range(4)]
+
+    def run(j):
+        out = {}
+        for v in range(j, len(profs), len(engs)):
+            engs[j].set_profile(profs[v])
+            engs[j].load_pods(pods)
+            engs[j].reset_cluster()
+            out[v] = engs[j].schedule_loaded(0, pods.n_pods)[0]
+        return out
+
+    got = {}
+    with ThreadPoolExecutor(len(engs)) as ex:
+        for part in ex.map(run, range(len(engs))):
+            got.update(part)
+    for v in range(len(profs)):
+        np.testing.assert_array_equal(got[v], want[v], err_msg=f"vector {v}")
+
+
 def test_persistent_tables_under_assume_forget():
     """The persistent domain tables follow binds made outside the loaded queue
     (ksim_assume / ksim_forget of single uploads: the class-index update path)

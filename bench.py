@@ -136,6 +136,23 @@ def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) ->
 HOST_COMPILE = {}
 
 
+class TimedMatcher:
+    """DeviceMatcher with its wall time per call (host CSR build + device call)
+    and the device time of the ksim_match_terms kernels (HIP events)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.seconds = []
+        self.device_ms = []
+
+    def match(self, mp):
+        t = time.perf_counter()
+        r = self.inner.match(mp)
+        self.seconds.append(time.perf_counter() - t)
+        self.device_ms.append(self.inner.engine.last_match_ms())
+        return r
+
+
 def build(cfg: int, args, rank: int, world: int):
     """(cluster, pods, profile, description, sharded, scaling) for one rank."""
     from ksim import gen, profile
@@ -156,8 +173,15 @@ def build(cfg: int, args, rank: int, world: int):
     if cfg == 3:
         from ksim.encode import encode_cluster, encode_pods
         nodes, bound, incoming = gen.config3_objects(n_nodes=args.nodes3, n_incoming=args.pods3)
+        matcher = None
+        if not args.host_match:
+            # selector / term matching of the count classes on the device
+            # (ksim_match_terms, int8 MFMA contraction)
+            from ksim.engine import Engine
+            from ksim.termmatch import DeviceMatcher
+            matcher = TimedMatcher(DeviceMatcher(Engine(int(os.environ.get("LOCAL_RANK", "0")))))
         t0 = time.perf_counter()
-        cluster, _ = encode_cluster(nodes, bound)
+        cluster, _ = encode_cluster(nodes, bound, matcher=matcher)
         t1 = time.perf_counter()
         pods = encode_pods(cluster, incoming)
         t2 = time.perf_counter()
@@ -165,8 +189,14 @@ def build(cfg: int, args, rank: int, world: int):
         # scans over existing pods (done once here, outside the timed region).
         HOST_COMPILE.update({"encode_cluster_s": t1 - t0, "encode_pods_s": t2 - t1,
                              "existing_pods": len(bound), "incoming_pods": len(incoming),
-                             "note": "host count-class compile (ksim/encode.py + ksim/topology.py, Python), "
-                                     "once per snapshot/queue, not in the timed region"})
+                             "term_matching": "host (Python)" if matcher is None else
+                             "device (ksim_match_terms)",
+                             "note": "count-class compile (ksim/encode.py + ksim/topology.py), once per "
+                                     "snapshot/queue, not in the timed region"})
+        if matcher is not None:
+            HOST_COMPILE["match_calls_s"] = matcher.seconds
+            HOST_COMPILE["match_device_ms"] = matcher.device_ms
+            matcher.inner.engine.close()
         desc = (f"config3: default profile, {cluster.n_nodes} nodes / 3 zones, "
                 f"{int(cluster.num_pods.sum())} existing pods with anti-affinity terms, {pods.n_pods} incoming "
                 f"pods with spread constraints + preferred anti-affinity, {args.mode.upper()}")
@@ -201,6 +231,8 @@ def main():
     ap.add_argument("--force-shard", action="store_true",
                     help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--host-match", action="store_true",
+                    help="config 3: match the count classes' selectors on the host instead of ksim_match_terms")
     ap.add_argument("--no-adapt", action="store_true", help="skip the secondary ADAPT measurement (config 2)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 4
+#define KSIM_ABI_VERSION 5
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -522,7 +522,8 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
  * out[3..18] device phase-clock accumulators since ksim_set_cluster (100 MHz
  * ticks: [3] chain prologue, [4] chain loop, [5] chain epilogue, [6] chain
  * launches); out[19] hipGraphs captured since ksim_create (a weight sweep that
- * keeps its graphs across ksim_set_profile captures none).  Returns the number
+ * keeps its graphs across ksim_set_profile captures none); out[20] device
+ * time of the last ksim_match_terms in ns (HIP events).  Returns the number
  * of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),
@@ -573,6 +574,45 @@ int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b);
  * The pod must carry no topology / port / image uses (KSIM_E_UNSUPPORTED). */
 int ksim_preempt(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
                  ksim_preempt_out* out);
+
+/* ---- selector / affinity-term matching -------------------- */
+/* The pod-matching half of PodTopologySpread's and InterPodAffinity's
+ * PreFilter / PreScore: upstream countPodsMatchSelector,
+ * getExistingAntiAffinityCounts, getIncomingAffinityAntiAffinityCounts and
+ * processExistingPod run every selector / term against every existing pod,
+ * reached per pod through the wrapped plugins' PreFilter / PreScore
+ * (scheduler/plugin/wrappedplugin.go:427-486).  The engine keeps the answers
+ * as count classes (ksim_node_table.class_count); this call computes them.
+ *
+ * The host reduces each matcher to requirements over a feature vocabulary
+ * (a namespace, a label key=value pair, a label key): In / Exists name the
+ * features that satisfy them, NotIn / DoesNotExist (neg = 1) the features
+ * that break them; a namespace predicate is an In over namespaces; a nil
+ * selector is a positive requirement naming no feature.  A signature is the
+ * feature set of a (namespace, labels) pair.  On the device:
+ *   hits[s][r]  = |features(s) & features(r)|   (int8 MFMA contraction)
+ *   match[s][m] = AND over r in m of (hits > 0) != neg[r]
+ *   counts[c][node] = #{bound pods p on node : match[sig(p)][class_matcher[c]]}
+ * Limits: n_reqs <= 4096, n_feat <= 65536 (KSIM_E_UNSUPPORTED beyond). */
+typedef struct ksim_match_problem {
+  int32_t n_sigs, n_feat, n_reqs, n_matchers;
+  const int32_t* sig_feat_off;     /* [n_sigs + 1] CSR over sig_feat */
+  const int32_t* sig_feat;         /* feature ids < n_feat */
+  const int32_t* req_feat_off;     /* [n_reqs + 1] CSR over req_feat */
+  const int32_t* req_feat;
+  const uint8_t* req_neg;          /* [n_reqs] */
+  const int32_t* m_req_off;        /* [n_matchers + 1] CSR over m_req (requirement ids, AND) */
+  const int32_t* m_req;
+  int32_t n_pods, n_nodes, n_classes, _pad;
+  const int32_t* pod_sig;          /* [n_pods] signature of each bound pod */
+  const int32_t* pod_node;         /* [n_pods] its node position */
+  const int32_t* class_matcher;    /* [n_classes] matcher of each output class */
+} ksim_match_problem;
+
+/* match_bits: [n_sigs][ceil(n_matchers / 32)] (bit m of row s: signature s
+ * matches matcher m); counts (may be NULL when n_classes == 0):
+ * [n_classes][n_nodes].  Needs no cluster or profile on the handle. */
+int ksim_match_terms(ksim_handle* h, const ksim_match_problem* mp, uint32_t* match_bits, int32_t* counts);
 
 /* ---- result emission ------------------------------------- */
 /* One cycle's outputs (ksim_eval_out or the oracle's) plus the names the

@@ -159,6 +159,7 @@ struct ksim_handle {
   std::vector<std::pair<const ksim_handle*, int64_t>> sg_sig;
   std::map<std::tuple<bool, int64_t, int64_t>, hipGraphExec_t> sg_graphs;
   bool sg_off = false;                         // capture failed once (e.g. a collective that cannot be captured)
+  int64_t match_ns = 0;                        // device time of the last ksim_match_terms (HIP events)
 };
 
 namespace {
@@ -863,6 +864,7 @@ size_t ksim_abi_sizeof(int which) {
     case 8: return sizeof(ksim_batch_stats);
     case 9: return sizeof(ksim_topo_use);
     case 10: return sizeof(ksim_class_add);
+    case 11: return sizeof(ksim_match_problem);
     default: return 0;
   }
 }
@@ -2216,10 +2218,11 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  int64_t v[3 + 16 + 1] = {st.batches, st.truncations, st.cuts};
+  int64_t v[3 + 16 + 2] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hipMemcpy(v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   v[19] = h->graph_captures;
-  const int32_t m = n < 20 ? n : 20;
+  v[20] = h->match_ns;
+  const int32_t m = n < 21 ? n : 21;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }
@@ -2328,5 +2331,106 @@ extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_
     for (int32_t j = off[0]; j < off[1] && k < out->victims_cap; j++)
       if (flag[j - off[0]]) out->victims[k++] = h->pre_index[j];
   }
+  return KSIM_OK;
+}
+
+// ---- selector / affinity-term matching (ksim_match.hip) ------
+extern "C" int ksim_match_terms(ksim_handle* h, const ksim_match_problem* mp, uint32_t* match_bits, int32_t* counts) {
+  if (!h || !mp || !match_bits) return set_err(h, KSIM_E_INVALID, "null argument");
+  const ksim_match_problem& q = *mp;
+  if (q.n_sigs < 0 || q.n_feat < 0 || q.n_reqs < 0 || q.n_matchers < 0 || q.n_pods < 0 || q.n_nodes < 0 ||
+      q.n_classes < 0)
+    return set_err(h, KSIM_E_INVALID, "negative size");
+  if (q.n_reqs > kMatchMaxReqs || q.n_feat > kMatchMaxFeat)
+    return set_err(h, KSIM_E_UNSUPPORTED, "match problem exceeds 4096 requirements or 65536 features");
+  if (q.n_classes > 0 && !counts) return set_err(h, KSIM_E_INVALID, "counts buffer missing");
+  if (!q.sig_feat_off || !q.req_feat_off || (!q.req_neg && q.n_reqs > 0) || !q.m_req_off)
+    return set_err(h, KSIM_E_INVALID, "null CSR");
+  // host validation: every index the kernels follow is in range
+  auto csr_ok = [](const int32_t* off, int32_t rows, const int32_t* v, int32_t bound) {
+    if (off[0] != 0) return false;
+    for (int32_t i = 0; i < rows; i++)
+      if (off[i + 1] < off[i]) return false;
+    if (off[rows] > 0 && !v) return false;
+    for (int32_t j = 0; j < off[rows]; j++)
+      if (v[j] < 0 || v[j] >= bound) return false;
+    return true;
+  };
+  if (!csr_ok(q.sig_feat_off, q.n_sigs, q.sig_feat, q.n_feat) ||
+      !csr_ok(q.req_feat_off, q.n_reqs, q.req_feat, q.n_feat) ||
+      !csr_ok(q.m_req_off, q.n_matchers, q.m_req, q.n_reqs))
+    return set_err(h, KSIM_E_INVALID, "feature / requirement index out of range");
+  if (q.n_classes > 0) {
+    if (!q.class_matcher) return set_err(h, KSIM_E_INVALID, "class_matcher missing");
+    for (int32_t c = 0; c < q.n_classes; c++)
+      if (q.class_matcher[c] < 0 || q.class_matcher[c] >= q.n_matchers)
+        return set_err(h, KSIM_E_INVALID, "class matcher out of range");
+    if (q.n_pods > 0 && (!q.pod_sig || !q.pod_node)) return set_err(h, KSIM_E_INVALID, "bound pod arrays missing");
+    for (int32_t p = 0; p < q.n_pods; p++)
+      if (q.pod_sig[p] < 0 || q.pod_sig[p] >= q.n_sigs || q.pod_node[p] < 0 || q.pod_node[p] >= q.n_nodes)
+        return set_err(h, KSIM_E_INVALID, "bound pod signature / node out of range");
+  }
+  if (q.n_sigs == 0) return KSIM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  DevMatch m{};
+  m.s = q.n_sigs;
+  m.sp = (q.n_sigs + 15) / 16 * 16;
+  m.fp = std::max(64, (q.n_feat + 63) / 64 * 64);
+  m.r = q.n_reqs;
+  m.rp = std::max(16, (q.n_reqs + 15) / 16 * 16);
+  m.m = q.n_matchers;
+  m.w = (q.n_matchers + 31) / 32;
+  m.c = q.n_classes;
+  m.cw = (q.n_classes + 31) / 32;
+  m.p = q.n_classes > 0 ? q.n_pods : 0;
+  m.n = q.n_nodes;
+  std::vector<DevBuf> bufs;
+  struct Guard {
+    std::vector<DevBuf>& b;
+    ~Guard() { free_bufs(b); }
+  } guard{bufs};
+  int rc;
+  void* p;
+  std::vector<uint8_t> neg((size_t)m.rp, 0);
+  std::copy(q.req_neg, q.req_neg + q.n_reqs, neg.begin());
+  if ((rc = upload(h, bufs, nullptr, (size_t)m.sp * m.fp, &p))) return rc;
+  m.a = (int8_t*)p;
+  if ((rc = upload(h, bufs, nullptr, (size_t)m.rp * m.fp, &p))) return rc;
+  m.bt = (int8_t*)p;
+  if ((rc = upload(h, bufs, neg.data(), neg.size(), &p))) return rc;
+  m.neg = (uint8_t*)p;
+  auto put = [&](const int32_t* src, int64_t n, const int32_t** dst) {
+    void* d;
+    int r = upload(h, bufs, src, (size_t)std::max<int64_t>(n, 0) * 4, &d);
+    *dst = (const int32_t*)d;
+    return r;
+  };
+  if ((rc = put(q.sig_feat_off, q.n_sigs + 1, &m.sig_off)) || (rc = put(q.sig_feat, q.sig_feat_off[q.n_sigs], &m.sig_feat)) ||
+      (rc = put(q.req_feat_off, q.n_reqs + 1, &m.req_off)) || (rc = put(q.req_feat, q.req_feat_off[q.n_reqs], &m.req_feat)) ||
+      (rc = put(q.m_req_off, q.n_matchers + 1, &m.m_off)) || (rc = put(q.m_req, q.m_req_off[q.n_matchers], &m.m_req)))
+    return rc;
+  if ((rc = upload(h, bufs, nullptr, (size_t)m.s * std::max(m.w, 1) * 4, &p))) return rc;
+  m.bits = (uint32_t*)p;
+  if (m.c > 0) {
+    if ((rc = put(q.class_matcher, m.c, &m.cls_matcher)) || (rc = put(q.pod_sig, m.p, &m.pod_sig)) ||
+        (rc = put(q.pod_node, m.p, &m.pod_node)))
+      return rc;
+    if ((rc = upload(h, bufs, nullptr, (size_t)m.s * m.cw * 4, &p))) return rc;
+    m.cls_bits = (uint32_t*)p;
+    if ((rc = upload(h, bufs, nullptr, (size_t)m.c * std::max(m.n, 1) * 4, &p))) return rc;
+    m.cnt = (int32_t*)p;
+  }
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  launch_match(m, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  if (m.w > 0)
+    HIPCHK(h, hipMemcpyAsync(match_bits, m.bits, (size_t)m.s * m.w * 4, hipMemcpyDeviceToHost, h->stream));
+  if (m.c > 0 && m.n > 0)
+    HIPCHK(h, hipMemcpyAsync(counts, m.cnt, (size_t)m.c * m.n * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  h->match_ns = (int64_t)(ms * 1e6);
   return KSIM_OK;
 }

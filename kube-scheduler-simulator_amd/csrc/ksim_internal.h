@@ -130,6 +130,23 @@ void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStre
 void launch_group_gather(const GroupPtrs& src, const GroupPtrs& dst, int32_t words, hipStream_t stream);
 // Persistent domain tables of a loaded queue (DevPods.ptab) from the class counts.
 void launch_ptab_init(const DevCluster& c, const DevPods& P, hipStream_t stream);
+
+// Selector / term matching as an int8 contraction (ksim_match.hip, ksim_match_terms).
+constexpr int kMatchMaxReqs = 4096;     // requirement columns (LDS: 16 rows x 4096 bits)
+constexpr int kMatchMaxFeat = 65536;    // feature vocabulary (K of the contraction)
+struct DevMatch {
+  const int8_t* a;          // [sp][fp] signature one-hot rows (zeroed before the scatter)
+  const int8_t* bt;         // [rp][fp] requirement rows (B transposed)
+  const uint8_t* neg;       // [rp] 1: satisfied when no feature hits
+  const int32_t *sig_off, *sig_feat, *req_off, *req_feat;   // CSR feature lists
+  const int32_t *m_off, *m_req;                               // CSR requirement lists per matcher
+  const int32_t *pod_sig, *pod_node, *cls_matcher;
+  uint32_t* bits;           // [s][w] matcher bits per signature
+  uint32_t* cls_bits;       // [s][cw] class bits per signature
+  int32_t* cnt;             // [c][n] class counts over the bound pods (zeroed)
+  int32_t s, sp, fp, r, rp, m, w, c, cw, p, n;
+};
+void launch_match(const DevMatch& m, hipStream_t stream);
 void launch_assume(const DevCluster& c, const DevPods& P, int32_t pod, int32_t node, int sign, hipStream_t stream);
 
 }  // namespace ksim

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -259,8 +259,23 @@ class BatchStats(ctypes.Structure):
     ]
 
 
+class MatchProblem(ctypes.Structure):
+    """ksim_match_problem: selectors / terms as requirements over a feature
+    vocabulary, signatures as feature sets (ksim/termmatch.py)."""
+    _fields_ = [
+        ("n_sigs", ctypes.c_int32), ("n_feat", ctypes.c_int32),
+        ("n_reqs", ctypes.c_int32), ("n_matchers", ctypes.c_int32),
+        ("sig_feat_off", ctypes.c_void_p), ("sig_feat", ctypes.c_void_p),
+        ("req_feat_off", ctypes.c_void_p), ("req_feat", ctypes.c_void_p),
+        ("req_neg", ctypes.c_void_p), ("m_req_off", ctypes.c_void_p), ("m_req", ctypes.c_void_p),
+        ("n_pods", ctypes.c_int32), ("n_nodes", ctypes.c_int32),
+        ("n_classes", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("pod_sig", ctypes.c_void_p), ("pod_node", ctypes.c_void_p), ("class_matcher", ctypes.c_void_p),
+    ]
+
+
 STRUCT_ORDER = [NodeTable, Vocab, LABEL_EXPR_DTYPE, TERM_DTYPE, POD_DTYPE, PodSet, Profile,
-                EvalOut, BatchStats, TOPO_USE_DTYPE, CLASS_ADD_DTYPE]
+                EvalOut, BatchStats, TOPO_USE_DTYPE, CLASS_ADD_DTYPE, MatchProblem]
 
 
 def struct_size(s) -> int:

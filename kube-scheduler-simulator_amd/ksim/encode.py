@@ -327,8 +327,8 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
                    extra_scalar: Sequence[str] = (),
                    namespaces: Optional[Dict[str, Dict[str, str]]] = None,
                    nb_args: Optional[netbw.NetworkBandwidthArgs] = None,
-                   scalar_order: Sequence[str] = (), classes_from: Optional[TopologyIndex] = None) \
-        -> Tuple[EncodedCluster, List[int]]:
+                   scalar_order: Sequence[str] = (), classes_from: Optional[TopologyIndex] = None,
+                   matcher=None) -> Tuple[EncodedCluster, List[int]]:
     """Encode nodes in nodeTree order.  Returns (cluster, order) where
     order[position] = index into ``nodes``.  ``bound_pods`` (spec.nodeName set)
     are added to their node's aggregates like NodeInfo.AddPod (and to the
@@ -336,7 +336,8 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
     namespace name -> labels (for namespaceSelector terms).  ``scalar_order``:
     scalar columns to place first, in this order, and ``classes_from``: a
     snapshot's TopologyIndex whose count classes are registered first (a re-encoded snapshot keeps the columns and
-    class ids of the one it replaces, ksim.ingest.NodeCache)."""
+    class ids of the one it replaces, ksim.ingest.NodeCache).  ``matcher``: match the count classes' selectors
+    on the device (ksim.termmatch.DeviceMatcher, ksim_match_terms); encode_pods uses it as well."""
     order = node_tree_order([zone_key(n.labels) for n in nodes])
     ns = [nodes[i] for i in order]
     N = len(ns)
@@ -414,15 +415,16 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
     c.topo = TopologyIndex(N, namespaces)
     pos_of = {name: i for i, name in enumerate(c.node_names)}
     c.topo.set_images(nodes, pos_of)                 # input order = the order nodes were added
+    c.topo.matcher = matcher
+    c.topo.deferred = matcher is not None
     if classes_from is not None:
         c.topo.preregister(classes_from)
-    for p in bound_pods:
-        if p.node_name in pos_of:
-            c.topo.carried_terms(p)          # classes of every carried term exist first
-    for p in bound_pods:
+    carried = [c.topo.carried_terms(p) if p.node_name in pos_of else None   # every carried class exists first
+               for p in bound_pods]
+    for p, ct in zip(bound_pods, carried):
         if p.node_name not in pos_of:
             continue
-        c.topo.add_bound(p, pos_of[p.node_name])
+        c.topo.add_bound(p, pos_of[p.node_name], ct)
         i = pos_of[p.node_name]
         r = pod_requests(p)
         nz = pod_nonzero_requests(p)
@@ -438,6 +440,8 @@ def encode_cluster(nodes: Sequence[Node], bound_pods: Sequence[Pod] = (),
             c.nb_alloc[i] += netbw.pod_allocated(p.annotations, nb_args)
         except netbw.QuantityError as e:
             raise EncodeError(str(e)) from e
+    if c.topo.deferred:
+        c.topo.resolve()
     c.refresh_classes()
     return c, order
 
@@ -550,11 +554,14 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
     arr = np.zeros(len(pods), abi.POD_DTYPE)
     names = []
     topo = cluster.topo
+    topo.deferred = topo.matcher is not None
     try:
         for p in pods:                        # pass 1: every class exists before any adds
             register_pod_classes(topo, p)
     except TopologyError as e:
         raise EncodeError(str(e)) from e
+    if topo.deferred:                         # the new classes' counts, the pods' matches (device)
+        topo.resolve(pods)
     uses: List[tuple] = []
     adds: List[Tuple[int, int]] = []
     nn: List[int] = []

@@ -30,6 +30,7 @@ EXPORTS = [
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
     "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
+    "ksim_match_terms",
 ]
 
 
@@ -70,6 +71,7 @@ def lib():
         L.ksim_set_bound_pods.argtypes = [vp, vp]
         L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
         L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
+        L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
         L.ksim_assume.argtypes = [vp, vp, i32, i32]
         L.ksim_forget.argtypes = [vp, vp, i32, i32]
         L.ksim_load_pods.argtypes = [vp, vp]
@@ -258,6 +260,18 @@ class Engine:
         self._chk(lib().ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
         return out.result()
 
+    def match_terms(self, mp: abi.MatchProblem, n_words: int, counts: Optional[np.ndarray]) -> np.ndarray:
+        """ksim_match_terms: [n_sigs][n_words] matcher bits; ``counts``
+        ([n_classes][n_nodes] int32, or None) receives the class counts."""
+        bits = np.zeros((max(mp.n_sigs, 1), max(n_words, 1)), np.uint32)
+        cp = None if counts is None else counts.ctypes.data_as(ctypes.c_void_p)
+        self._chk(lib().ksim_match_terms(self.h, ctypes.byref(mp), bits.ctypes.data_as(ctypes.c_void_p), cp))
+        return bits[:mp.n_sigs, :n_words]
+
+    def last_match_ms(self) -> float:
+        """Device time of the last match_terms call (its kernels, HIP events)."""
+        return self.diag()["match_ns"] / 1e6
+
     def assume(self, pods, index: int, node: int):
         self._sync()
         self._ran = True
@@ -316,12 +330,12 @@ class Engine:
 
     def diag(self) -> dict:
         """Batch-path diagnostics of the last schedule_loaded call."""
-        out = np.zeros(20, np.int64)
-        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 20)
+        out = np.zeros(21, np.int64)
+        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 21)
         if n < 0:
             self._chk(n)
         d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2]),
-             "graph_captures": int(out[19]), "dbg": [int(x) for x in out[3:19]]}
+             "graph_captures": int(out[19]), "dbg": [int(x) for x in out[3:19]], "match_ns": int(out[20])}
         if out[6]:
             d["chain_us"] = {"setup": out[3] / out[6] / 100.0, "rounds": out[4] / out[6] / 100.0,
                              "epilogue": out[5] / out[6] / 100.0, "rounds_per_batch": out[7] / out[6]}

@@ -95,6 +95,14 @@ class TopologyIndex:
         self.images: Dict[str, Tuple[int, np.ndarray]] = {}   # image name -> (size, node mask)
         self.bound_ports: List[Tuple[int, tuple]] = []   # (node position, (ip, protocol, port)) of bound pods
         self._carry_uses: Dict[tuple, List[tuple]] = {}   # signature -> carried uses (valid for a class count)
+        # Device matching (ksim.termmatch): with a ``matcher`` the
+        # selector classes are matched against the bound pods in one
+        # ksim_match_terms call per ``resolve``; while ``deferred`` no class is
+        # matched on the host.
+        self.matcher = None
+        self.deferred = False
+        self._sig_sel: Dict[tuple, List[int]] = {}        # signature -> selector classes it matches
+        self._sig_sel_n = -1                              # len(sel_ids) when _sig_sel was filled
 
     # ---- matchers ------------------------------------------------------------
     def _sel_key(self, sel: Optional[LabelSelector]) -> Optional[tuple]:
@@ -259,9 +267,10 @@ class TopologyIndex:
         if cid is not None:
             return cid
         cnt = np.zeros(self.n, np.int32)
-        for sig, positions in self.bound_sigs.items():
-            if self._sig_matches(m, sig, self.sig_pods[sig]):
-                np.add.at(cnt, np.asarray(positions, np.int64), 1)
+        if not self.deferred:                          # deferred: counted by resolve()
+            for sig, positions in self.bound_sigs.items():
+                if self._sig_matches(m, sig, self.sig_pods[sig]):
+                    np.add.at(cnt, np.asarray(positions, np.int64), 1)
         return self._new_class(key, cnt)
 
     def carried_class(self, kind: str, m: Matcher, topology_key: str) -> int:
@@ -288,14 +297,16 @@ class TopologyIndex:
             out[c] = out.get(c, 0) + w.weight
         return sorted(out.items())
 
-    def add_bound(self, pod: Pod, pos: int) -> None:
-        """An existing pod bound at node position ``pos`` (NodeInfo.AddPod)."""
+    def add_bound(self, pod: Pod, pos: int, carried: Optional[List[Tuple[int, int]]] = None) -> None:
+        """An existing pod bound at node position ``pos`` (NodeInfo.AddPod).
+        ``carried``: its carried_terms, when the caller has them already."""
         self.note_namespace(pod.namespace)
-        for c, mult in self.carried_terms(pod):
+        for c, mult in (self.carried_terms(pod) if carried is None else carried):
             self.counts[c][pos] += mult
-        for cid in self.sel_ids:
-            if self._pod_matches(self.keys[cid][1], pod):
-                self.counts[cid][pos] += 1
+        if not self.deferred:
+            for cid in self.sel_ids:
+                if self._pod_matches(self.keys[cid][1], pod):
+                    self.counts[cid][pos] += 1
         for c, k in self.port_adds(pod).items():
             self.counts[c][pos] += k
         self.bound_ports.extend((pos, t) for t in pod_host_ports(pod))
@@ -307,9 +318,12 @@ class TopologyIndex:
         """(class, count) this pod contributes when bound: its carried terms
         plus every selector class it matches."""
         out = dict(self.carried_terms(pod))
-        for cid in self.sel_ids:
-            if self._pod_matches(self.keys[cid][1], pod):
-                out[cid] = out.get(cid, 0) + 1
+        sig = (pod.namespace, tuple(sorted(pod.labels.items())))
+        sel = self._sig_sel.get(sig) if self._sig_sel_n == len(self.sel_ids) else None
+        if sel is None:
+            sel = [cid for cid in self.sel_ids if self._sig_matches(self.keys[cid][1], sig, pod)]
+        for cid in sel:
+            out[cid] = out.get(cid, 0) + 1
         for cid, k in self.port_adds(pod).items():
             out[cid] = out.get(cid, 0) + k
         return sorted(out.items())
@@ -322,9 +336,10 @@ class TopologyIndex:
         if hit is not None:
             return hit
         out = []
+        sig = ck[:2]
         for cid in self.carry_ids:
             _, kind, m, tk = self.keys[cid]
-            if not self.matches(m, pod.namespace, pod.labels):
+            if not self._sig_matches(m, sig, pod):
                 continue
             col = _col(cluster, tk)
             if kind == CARRY_REQ_ANTI:
@@ -337,6 +352,40 @@ class TopologyIndex:
                 out.append(_use(abi.USE_IPA_SCORE, cid, col, -1))
         self._carry_uses[ck] = out
         return out
+
+    def resolve(self, pods: Sequence[Pod] = ()) -> None:
+        """Match every selector and carried class against the bound pods'
+        signatures and those of ``pods`` on the device (``self.matcher``,
+        ksim_match_terms), set the selector classes' counts over the bound
+        pods, and end the deferred state."""
+        self.deferred = False
+        if self.matcher is None:
+            return
+        from .termmatch import MatchProblem
+        sigs = list(self.bound_sigs)
+        index = {sig: i for i, sig in enumerate(sigs)}
+        for p in pods:
+            sig = (p.namespace, tuple(sorted(p.labels.items())))
+            if sig not in index:
+                index[sig] = len(sigs)
+                sigs.append(sig)
+        ms = [self.keys[c][1] for c in self.sel_ids] + [self.keys[c][2] for c in self.carry_ids]
+        mp = MatchProblem(self, ms, sigs)
+        lens = [len(v) for v in self.bound_sigs.values()]
+        pod_sig = np.repeat(np.arange(len(lens), dtype=np.int32), lens)
+        pod_node = np.fromiter((x for v in self.bound_sigs.values() for x in v), np.int32, int(sum(lens)))
+        mp.set_counts(pod_sig, pod_node, self.n, range(len(self.sel_ids)))
+        hit, counts = self.matcher.match(mp)
+        for j, cid in enumerate(self.sel_ids):
+            self.counts[cid] = counts[j].copy()
+        ns = len(self.sel_ids)
+        self._sig_sel = {sig: [self.sel_ids[j] for j in np.flatnonzero(hit[i, :ns])] for i, sig in enumerate(sigs)}
+        self._sig_sel_n = ns
+        for j, cid in enumerate(self.carry_ids):
+            m = self.keys[cid][2]
+            col = hit[:, ns + j]
+            for i, sig in enumerate(sigs):
+                self._match_cache[(sig, m)] = bool(col[i])
 
     def class_count_array(self) -> np.ndarray:
         if not self.counts:

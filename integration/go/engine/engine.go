@@ -80,6 +80,20 @@ func (e *Engine) UpsertNodes(t *C.ksim_node_table, v *C.ksim_vocab, oldPos []int
 // RemoveNode removes the node at position pos (later nodes move down by one).
 func (e *Engine) RemoveNode(pos int) error { return e.err(C.ksim_remove_node(e.h, C.int32_t(pos))) }
 
+// MatchTerms answers every (signature, matcher) pair of the count classes'
+// selectors and terms on the device (the existing-pod scans of
+// PodTopologySpread / InterPodAffinity PreFilter and PreScore):
+// bits[s*words+m/32] bit m%32 = signature s matches matcher m, and
+// counts[c*nNodes+node] = bound pods on node whose signature matches
+// classMatcher[c] (counts may be empty when mp.n_classes == 0).
+func (e *Engine) MatchTerms(mp *C.ksim_match_problem, bits []uint32, counts []int32) error {
+	var cp *C.int32_t
+	if len(counts) > 0 {
+		cp = (*C.int32_t)(unsafe.Pointer(&counts[0]))
+	}
+	return e.err(C.ksim_match_terms(e.h, mp, (*C.uint32_t)(unsafe.Pointer(&bits[0])), cp))
+}
+
 // EvalPod runs one full cycle for pod idx of ps (PreFilter .. bind) and fills
 // the per-node outputs the wrapped plugins record (out's slices are Go-owned:
 // n_nodes entries, n_score x n_nodes for the score matrices).

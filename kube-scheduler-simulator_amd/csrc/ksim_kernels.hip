@@ -931,6 +931,8 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   const bool tadds = (pp.flags & kPlanTadds) != 0;
   int4 ta = make_int4(0, 0, 0, 0);
   if (tadds && lane < pp.tadd_count) ta = P.ptab_padd[pp.tadd_first + lane];
+  ksim_class_add add0{};                           // this lane's first class add, likewise
+  if (lane < P.pods[pi].add_count) add0 = P.adds[P.pods[pi].add_first + lane];
   // the window scalars and the scheduler state do not depend on the choice
   // either (the row stores below could alias them for the compiler: load first)
   const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
@@ -940,7 +942,7 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
   const ksim_pod p = P.pods[pi];
   if (chosen >= 0) {
-    assume_pod_wave(c, P, p, chosen, 1, !tadds);                // NodeInfo.AddPod, one column per lane
+    assume_pod_wave(c, P, p, chosen, 1, !tadds, &add0);         // NodeInfo.AddPod, one column per lane
     if (tadds)
       for (int32_t i = lane; i < pp.tadd_count; i += 64) {
         const int4 t = i == lane ? ta : P.ptab_padd[pp.tadd_first + i];
@@ -977,6 +979,23 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   }
 }
 
+// KSIM_SEL_CLOCKS builds: per-block phase times of k_select (thread 0, 100 MHz
+// realtime) summed into s.dbg[phase - 1] (1 prologue, 2 totals, 3 block
+// record, 4 arrival), s.dbg[4] = blocks, s.dbg[5] = the last block's bind,
+// s.dbg[6] = bind steps.
+#ifdef KSIM_SEL_CLOCKS
+#define SEL_CLK(k)                                                         \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      const uint64_t _t = __builtin_amdgcn_s_memrealtime();                \
+      if ((k) > 0) atomicAdd(&s.dbg[(k) - 1], (unsigned long long)(_t - sel_t)); \
+      sel_t = _t;                                                          \
+    }                                                                      \
+  } while (0)
+#else
+#define SEL_CLK(k) do {} while (0)
+#endif
+
 template <bool COMPAT>
 // bind_mode (unsharded cycles): 1 / 2 = the last block to finish runs the bind
 // step (bind_cycle, windowed / NOWIN), which saves k_bind's launch.
@@ -985,6 +1004,10 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
                                                 int32_t fuse_ext, int32_t bind_mode, int32_t* __restrict__ chosen_out) {
   __shared__ uint64_t s_best[8];
   __shared__ int32_t sh32[4];
+#ifdef KSIM_SEL_CLOCKS
+  uint64_t sel_t = 0;
+#endif
+  SEL_CLK(0);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t node = blockIdx.x * blockDim.x + tid;
   const int32_t N = c.n;
@@ -1037,6 +1060,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     kend = win->kend;
     has_soft = win->has_soft != 0;
   }
+  SEL_CLK(1);
   uint64_t img = 0, tlo = 0;                       // this node's (total image, TB lo); tlo == 0: no key
   if (node < N) {
     const bool kept = nf >= 1 && !win->error && kept_node(c, s, ss, node, kend);
@@ -1116,6 +1140,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       const int32_t V = c.col_nvals[load_use(U, i).col];
       if (V <= kLdsDom && tid < V) s.dom[(size_t)i * c.vmax + tid] = 0;
     }
+  SEL_CLK(2);
   // selectHost: the block's best (total, TB) pair -> its record (k_bind reduces the records)
   wave_best2(img, tlo);
   if (lane == 0) {
@@ -1130,6 +1155,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     s.bbest[2 * blockIdx.x] = bi;
     s.bbest[2 * blockIdx.x + 1] = bl;
   }
+  SEL_CLK(3);
   if (bind_mode) {
     // the last block: its acquire sees every block's record (and block 0's
     // window fields) released by their own increments
@@ -1139,11 +1165,21 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
       s_last = done == (int32_t)gridDim.x - 1;
     }
     __syncthreads();
+    SEL_CLK(4);
     if (s_last && tid < 64) {
       if (tid == 0) win->done = 0;
       bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp);
+#ifdef KSIM_SEL_CLOCKS
+      if (tid == 0) {
+        atomicAdd(&s.dbg[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - sel_t));
+        atomicAdd(&s.dbg[6], 1ull);
+      }
+#endif
     }
   }
+#ifdef KSIM_SEL_CLOCKS
+  if (tid == 0) atomicAdd(&s.dbg[4], 1ull);
+#endif
 }
 
 // The persistent domain tables from the class counts (a queue's upload, a

@@ -549,8 +549,12 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
   return KSIM_OK;
 }
 
+hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast);
+
 // Pods [a, b) on the sharded batch path (every pod must be batchable).  No
-// batch is ever issued past the run's end (each commits 1..kBatchPods pods).
+// batch is ever issued past the run's end (each commits 1..kBatchPods pods):
+// whole graphs of kGraphBatches batches while at least kBatchPods *
+// kGraphBatches pods are left, then left / kBatchPods single batches.
 int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   ksim_handle* h0 = hs[0];
   hipStream_t stream = h0->stream;
@@ -561,12 +565,19 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
     if ((rc = set_run(h, a, b))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_batch_graph(hs, fast) : nullptr;
   int32_t cursor = a;
   while (cursor < b) {
-    const int32_t n = std::max(1, (b - cursor) / kBatchPods);
-    for (int32_t i = 0; i < n; i++) {
-      int rc = shard_batch(hs, stream, fast);
-      if (rc) return rc;
+    const int32_t left = b - cursor;
+    if (g && left >= kBatchPods * kGraphBatches) {
+      const int reps = left / (kBatchPods * kGraphBatches);
+      for (int r = 0; r < reps; r++) HIPCHK(h0, hipGraphLaunch(g, stream));
+    } else {
+      const int32_t n = std::max(1, left / kBatchPods);
+      for (int32_t i = 0; i < n; i++) {
+        int rc = shard_batch(hs, stream, fast);
+        if (rc) return rc;
+      }
     }
     DevState st;
     HIPCHK(h0, hipMemcpyAsync(&st, h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));
@@ -670,6 +681,42 @@ hipGraphExec_t shard_graph(const std::vector<ksim_handle*>& hs, bool topo, int64
   bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
   for (int i = 0; ok && i < kGraphCycles; i++) ok = shard_cycle(hs, topo, xdom, xreg, stream) == KSIM_OK;
   const hipError_t e = hipStreamEndCapture(stream, &g);   // ends a capture even after a failed launch
+  ok = ok && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  if (!ok) {
+    h0->sg_off = true;
+    h0->err.clear();
+    return nullptr;
+  }
+  h0->graph_captures++;
+  h0->sg_graphs.emplace(key, ge);
+  return ge;
+}
+
+// kGraphBatches sharded batches (every shard's kernels and the exchanges on
+// the leader's stream, RCCL collectives included) as a graph, cached with the
+// per-pod shard graphs; nullptr when capture is off or fails (eager batches).
+hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast) {
+  ksim_handle* h0 = hs[0];
+  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  std::vector<std::pair<const ksim_handle*, int64_t>> sig;
+  for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
+  if (sig != h0->sg_sig) {
+    for (auto& kv : h0->sg_graphs) (void)hipGraphExecDestroy(kv.second);
+    h0->sg_graphs.clear();
+    h0->sg_sig = sig;
+  }
+  const auto key = std::make_tuple(fast, (int64_t)-1, (int64_t)-1);   // per-pod keys have lengths >= 0
+  auto it = h0->sg_graphs.find(key);
+  if (it != h0->sg_graphs.end()) return it->second;
+  hipStream_t stream = h0->stream;
+  if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  for (int i = 0; ok && i < kGraphBatches; i++) ok = shard_batch(hs, stream, fast) == KSIM_OK;
+  const hipError_t e = hipStreamEndCapture(stream, &g);
   ok = ok && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
   if (g) (void)hipGraphDestroy(g);
   (void)hipGetLastError();

@@ -39,10 +39,11 @@ def _node_state(engines):
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_group_config2_slice(world):
-    cluster, pods = gen.config2(n_nodes=2000, n_pods=3000)
+    cluster, pods = gen.config2(n_nodes=2000, n_pods=6000)
     prof = _prof()
     engines = _group(cluster, pods, prof, world)
     chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    assert engines[0].diag()["graph_captures"] >= 1      # batches replayed as hipGraphs of 16
     ora = Oracle(cluster, prof)
     ochosen, ost = ora.schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
@@ -89,7 +90,7 @@ def test_group_truncation_and_cuts():
 
 def test_rccl_world1():
     """ksim_comm_init + the RCCL exchange calls with a single rank."""
-    cluster, pods = gen.config2(n_nodes=1500, n_pods=2000)
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=6000)
     prof = _prof()
     uid = engine.comm_unique_id()
     e = Engine(0)
@@ -99,6 +100,7 @@ def test_rccl_world1():
     e.comm_init(0, 1, uid)
     e.load_pods(pods)
     chosen, st = e.schedule_loaded(0, pods.n_pods)
+    assert e.diag()["graph_captures"] >= 1               # RCCL collectives captured in the batch graphs
     ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals

@@ -549,7 +549,7 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
   return KSIM_OK;
 }
 
-hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast);
+hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast, bool adapt);
 
 // Pods [a, b) on the sharded batch path (every pod must be batchable).  No
 // batch is ever issued past the run's end (each commits 1..kBatchPods pods):
@@ -565,7 +565,7 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
     if ((rc = set_run(h, a, b))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
-  const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_batch_graph(hs, fast) : nullptr;
+  const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_batch_graph(hs, fast, false) : nullptr;
   int32_t cursor = a;
   while (cursor < b) {
     const int32_t left = b - cursor;
@@ -697,7 +697,9 @@ hipGraphExec_t shard_graph(const std::vector<ksim_handle*>& hs, bool topo, int64
 // kGraphBatches sharded batches (every shard's kernels and the exchanges on
 // the leader's stream, RCCL collectives included) as a graph, cached with the
 // per-pod shard graphs; nullptr when capture is off or fails (eager batches).
-hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast) {
+int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fast);
+
+hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast, bool adapt) {
   ksim_handle* h0 = hs[0];
   if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
@@ -707,7 +709,7 @@ hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast)
     h0->sg_graphs.clear();
     h0->sg_sig = sig;
   }
-  const auto key = std::make_tuple(fast, (int64_t)-1, (int64_t)-1);   // per-pod keys have lengths >= 0
+  const auto key = std::make_tuple(fast, (int64_t)(adapt ? -2 : -1), (int64_t)-1);   // per-pod keys: lengths >= 0
   auto it = h0->sg_graphs.find(key);
   if (it != h0->sg_graphs.end()) return it->second;
   hipStream_t stream = h0->stream;
@@ -715,7 +717,8 @@ hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast)
   hipGraph_t g = nullptr;
   hipGraphExec_t ge = nullptr;
   bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
-  for (int i = 0; ok && i < kGraphBatches; i++) ok = shard_batch(hs, stream, fast) == KSIM_OK;
+  for (int i = 0; ok && i < kGraphBatches; i++)
+    ok = (adapt ? shard_batch_adapt(hs, stream, fast) : shard_batch(hs, stream, fast)) == KSIM_OK;
   const hipError_t e = hipStreamEndCapture(stream, &g);
   ok = ok && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
   if (g) (void)hipGraphDestroy(g);
@@ -784,6 +787,7 @@ bool adapt_shard_layout(const std::vector<ksim_handle*>& hs) {
 int adapt_shard_buffers(ksim_handle* h, int32_t world, int32_t W) {
   if (h->ash_world == world && h->ash_w == W) return KSIM_OK;
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  drop_cycle_graphs(h);                           // shard batch graphs captured over the old buffers
   free_bufs(h->ash_bufs);
   const size_t nw = (size_t)(h->dc.n_total + 63) / 64;
   void* p = nullptr;
@@ -854,12 +858,19 @@ int shard_run_adapt(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
     if ((rc = set_run(h, a, b))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_batch_graph(hs, fast, true) : nullptr;
   int32_t cursor = a;
   while (cursor < b) {
-    const int32_t n = std::max(1, (b - cursor) / kBatchPods);
-    for (int32_t i = 0; i < n; i++) {
-      int rc = shard_batch_adapt(hs, stream, fast);
-      if (rc) return rc;
+    const int32_t left = b - cursor;
+    if (g && left >= kBatchPods * kGraphBatches) {   // as shard_run
+      const int reps = left / (kBatchPods * kGraphBatches);
+      for (int r = 0; r < reps; r++) HIPCHK(h0, hipGraphLaunch(g, stream));
+    } else {
+      const int32_t n = std::max(1, left / kBatchPods);
+      for (int32_t i = 0; i < n; i++) {
+        int rc = shard_batch_adapt(hs, stream, fast);
+        if (rc) return rc;
+      }
     }
     DevState st;
     HIPCHK(h0, hipMemcpyAsync(&st, h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));

@@ -208,11 +208,12 @@ def test_group_adapt_until_full():
     ochosen, ost = ora.schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert (chosen == -1).sum() > 0 and st.evals == ost.evals
+    assert engines[0].diag()["graph_captures"] >= 1      # ADAPT batches replayed as hipGraphs of 16
 
 
 def test_rccl_world1_adapt():
     """The RCCL exchange calls of the sharded ADAPT batch with a single rank."""
-    cluster, pods = gen.config2(n_nodes=1500, n_pods=2000)
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=6000)
     prof = _adapt_prof()
     e = Engine(0)
     e.set_shard(0, cluster.n_nodes)
@@ -224,3 +225,4 @@ def test_rccl_world1_adapt():
     ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.batches > 0
+    assert e.diag()["graph_captures"] >= 1

@@ -134,6 +134,7 @@ def cpu_baseline(cluster, pods, sp, seconds: float, threads: int, label: str) ->
 
 
 HOST_COMPILE = {}
+SWEEP = {}
 
 
 class TimedMatcher:
@@ -298,7 +299,8 @@ def main():
     eng.load_pods(pods)
 
     if cfg == 5:
-        weights = gen.config5_weights(args.sweep)[rank::world]
+        from ksim import sweep
+        weights = gen.config5_weights(args.sweep)[sweep.rank_vectors(args.sweep, rank, world)]
         names = [p.name for p in sp.score_plugins()]
         profs = [profile.compile_profile(sp.with_weights({n: int(x) for n, x in zip(names, w)})) for w in weights]
         # Independent weight vectors run concurrently: one engine (own stream,
@@ -315,12 +317,13 @@ def main():
         pool = ThreadPoolExecutor(len(engs))
 
         def run_part(j):
-            e, agg = engs[j], None
+            e, agg, rows = engs[j], None, []
             for pr in profs[j::len(engs)]:
                 e.set_profile(pr)
                 e.load_pods(pods)
                 e.reset_cluster()
-                _, st = e.schedule_loaded(0, pods.n_pods, want_chosen=False)
+                chosen, st = e.schedule_loaded(0, pods.n_pods)       # the placements of this vector
+                rows.append(chosen)
                 if agg is None:
                     agg = st
                 else:
@@ -328,10 +331,15 @@ def main():
                               "perpod_cycles"):
                         setattr(agg, f, getattr(agg, f) + getattr(st, f))
                     agg.device_ms += st.device_ms
-            return agg
+            return agg, rows
 
         def step():
-            parts = [p for p in pool.map(run_part, range(len(engs))) if p is not None]
+            res = list(pool.map(run_part, range(len(engs))))
+            # C4: every vector's placements, gathered to rank 0 in global order
+            local_rows = sweep.order_engine_results([r for _, r in res], len(profs))
+            SWEEP["placements"] = sweep.gather_placements(local_rows, rank, world, args.sweep, dist,
+                                                          "cuda" if dist is not None else None)
+            parts = [p for p, _ in res if p is not None]
             agg = parts[0]
             for st in parts[1:]:
                 for f in ("pods", "scheduled", "unschedulable", "evals", "batches", "truncations", "perpod_cycles"):
@@ -450,6 +458,13 @@ def main():
     }
     if HOST_COMPILE:
         result["host_compile"] = HOST_COMPILE
+    if SWEEP.get("placements") is not None:
+        from ksim import sweep
+        pl = SWEEP["placements"]
+        result["sweep"] = {"vectors": int(pl.shape[0]), "pods": int(pl.shape[1]),
+                           "placements_gathered": "rank 0, [vectors][pods] int32, one all-gather per step (C4)",
+                           "scheduled_per_vector_mean": float((pl >= 0).sum(axis=1).mean()),
+                           "digest": sweep.placement_digest(pl)}
     if cfg == 2 and world == 1 and args.mode == "p100" and not args.no_adapt:
         # the simulator's forced default (percentageOfNodesToScore = 0) on the
         # same cluster and pods, timed the same way: a secondary line item

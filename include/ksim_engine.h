@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 5
+#define KSIM_ABI_VERSION 6
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -252,12 +252,32 @@ typedef struct ksim_pod {
   uint32_t topo_flags;                       /* KSIM_POD_IPA_* */
   uint32_t nb_flags;                         /* KSIM_POD_NB_* */
   int32_t  nn_first, nn_count;               /* PreFilterResult.NodeNames (KSIM_POD_NODE_NAMES) */
+  /* Bound PersistentVolumeClaims (see "volume groups" below): VolumeBinding's
+   * PV node affinity and VolumeZone's PV topology labels as groups of terms. */
+  int32_t  vb_first, vb_count;               /* VolumeBinding groups: terms [vb_first, +vb_count) */
+  int32_t  vz_first, vz_count;               /* VolumeZone groups: terms [vz_first, +vz_count) */
   int64_t  nb_req;                           /* NetworkBandwidth Filter request (milli): ingress
                                                 + egress request annotations, each falling back
                                                 to the *-bandwidth annotation */
   int64_t  nb_add;                           /* added to the node's allocated amount once bound
                                                 (request annotations only, unparsable ones skipped) */
 } ksim_pod;
+
+/* Volume groups.  A pod's PersistentVolumeClaims bound to PersistentVolumes
+ * become node-label requirements (host compile, ksim/encode.py):
+ *   VolumeBinding  (binder.go checkBoundClaims -> volumeutil.CheckNodeAffinity)
+ *                  one group per PV with spec.nodeAffinity.required: its
+ *                  NodeSelectorTerms (OR), evaluated on a node that has only
+ *                  labels (a matchFields metadata.name requirement sees "");
+ *   VolumeZone     (volume_zone.go Filter) one group per PV topology label
+ *                  (topology.kubernetes.io/zone|region and the beta
+ *                  failure-domain keys): the terms {key In LabelZonesToSet(v)}
+ *                  and {every topology key DoesNotExist} (a node without any
+ *                  topology label passes).
+ * Terms of a list are consecutive ksim_term entries of the pod set; a term's
+ * `weight` is its group index (0, 0, 1, 2, 2, ... non-decreasing).  The filter
+ * passes iff every group has a matching term.  Failure reasons: "node(s) had
+ * volume node affinity conflict" / "node(s) had no available volume zone". */
 
 /* Count classes.  The host evaluates every label selector / affinity term
  * against pod namespaces and labels once (that string work does not depend

@@ -466,6 +466,25 @@ __device__ __forceinline__ bool required_node_affinity_match(const DevCluster& c
   return true;
 }
 
+// VolumeBinding / VolumeZone (ksim_engine.h "Volume groups"): terms
+// [first, first + count) of the pod set in groups (ksim_term.weight = group
+// index, non-decreasing); true iff every group has a matching term.
+__device__ __forceinline__ bool volume_groups_match(const DevCluster& c, const DevPods& P, int32_t first,
+                                                    int32_t count, int32_t node) {
+  int32_t group = -1;
+  bool ok = true;                                  // the current group has a match
+  for (int i = 0; i < count; i++) {
+    const ksim_term& t = P.terms[first + i];
+    if (t.weight != group) {
+      if (!ok) return false;
+      group = t.weight;
+      ok = false;
+    }
+    if (!ok && term_matches(c, P, t, node)) ok = true;
+  }
+  return ok;
+}
+
 // nodeaffinity PreferredSchedulingTerms.Score
 __device__ __forceinline__ int64_t preferred_node_affinity_score(const DevCluster& c, const DevPods& P,
                                                         const ksim_pod& p, int32_t node) {
@@ -802,6 +821,12 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
       case KSIM_PL_NODE_AFFINITY:
         if (!required_node_affinity_match(c, P, p, node)) return (uint8_t)f;
         break;
+      case KSIM_PL_VOLUME_BINDING:
+        if (p.vb_count && !volume_groups_match(c, P, p.vb_first, p.vb_count, node)) return (uint8_t)f;
+        break;
+      case KSIM_PL_VOLUME_ZONE:
+        if (p.vz_count && !volume_groups_match(c, P, p.vz_first, p.vz_count, node)) return (uint8_t)f;
+        break;
       case KSIM_PL_NODE_RESOURCES_FIT: {
         uint32_t bits = fits_request(r, p, c.n_scalar);
         if (bits) { detail = bits; return (uint8_t)f; }
@@ -888,7 +913,9 @@ inline uint32_t plan_filter_en(const ksim_profile& prof, const ksim_pod& p, cons
       case KSIM_PL_POD_TOPOLOGY_SPREAD: on = m.hard != 0; break;
       case KSIM_PL_INTER_POD_AFFINITY: on = (m.aff | m.anti | m.exist) != 0; break;
       case KSIM_PL_NETWORK_BANDWIDTH: on = true; break;
-      default: break;    // the volume plugins: engine pods carry no volumes
+      case KSIM_PL_VOLUME_BINDING: on = p.vb_count > 0; break;
+      case KSIM_PL_VOLUME_ZONE: on = p.vz_count > 0; break;
+      default: break;    // the other volume plugins pass (bound PVCs of unlimited kinds)
     }
     if (on) en |= 1u << pl;
   }
@@ -939,6 +966,10 @@ __device__ __forceinline__ uint8_t run_filter_plan(const DevCluster& c, const De
   }
   if (fp.en & (1u << KSIM_PL_NODE_AFFINITY))
     take(KSIM_PL_NODE_AFFINITY, !required_node_affinity_match(c, P, p, node), 0, false);
+  if (fp.en & (1u << KSIM_PL_VOLUME_BINDING))
+    take(KSIM_PL_VOLUME_BINDING, !volume_groups_match(c, P, p.vb_first, p.vb_count, node), 0, false);
+  if (fp.en & (1u << KSIM_PL_VOLUME_ZONE))
+    take(KSIM_PL_VOLUME_ZONE, !volume_groups_match(c, P, p.vz_first, p.vz_count, node), 0, false);
   if (fp.en & (1u << KSIM_PL_NODE_RESOURCES_FIT)) {
     const uint32_t bits = fits_request(r, p, c.n_scalar);
     take(KSIM_PL_NODE_RESOURCES_FIT, bits != 0, bits, false);

@@ -255,6 +255,15 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
   if (!check_terms(p.req_term_first, p.req_term_count) || !check_terms(p.pref_term_first, p.pref_term_count))
     return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad affinity term range");
   const std::string who = "pod " + std::to_string(i) + ": ";
+  for (const auto& vl : {std::make_pair(p.vb_first, p.vb_count), std::make_pair(p.vz_first, p.vz_count)}) {
+    if (vl.second == 0) continue;
+    if (!check_terms(vl.first, vl.second)) return set_err(h, KSIM_E_INVALID, who + "bad volume term range");
+    for (int32_t k = 0; k < vl.second; k++) {   // group indices: non-negative, non-decreasing
+      const int32_t g = ps->terms[vl.first + k].weight;
+      if (g < 0 || (k > 0 && g < ps->terms[vl.first + k - 1].weight))
+        return set_err(h, KSIM_E_INVALID, who + "volume term groups must be non-decreasing");
+    }
+  }
   if (p.use_count < 0 || p.use_count > KSIM_MAX_USES ||
       (p.use_count > 0 && (!ps->uses || p.use_first < 0 || p.use_first + p.use_count > ps->n_uses)))
     return set_err(h, KSIM_E_INVALID, who + "bad topology use range");
@@ -339,6 +348,7 @@ bool pod_batchable(const ksim_handle* h, const ksim_pod& p) {
   const ksim_profile& prof = h->prof;
   if (p.use_count > 0) return false;
   if (p.flags & KSIM_POD_NODE_NAMES) return false;
+  if (p.vb_count > 0 || p.vz_count > 0) return false;   // volume groups: the per-pod filter chain
   // NetworkBandwidth runs on the per-pod path (its error statuses end cycles),
   // and so do pods that add to a node's allocated bandwidth
   if (profile_nb(prof) || p.nb_add != 0) return false;
@@ -1558,6 +1568,8 @@ static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std
   };
   copy_terms(pod.req_term_first, pod.req_term_count);
   copy_terms(pod.pref_term_first, pod.pref_term_count);
+  copy_terms(pod.vb_first, pod.vb_count);
+  copy_terms(pod.vz_first, pod.vz_count);
 }
 
 // Upload one pod (re-based) as a device pod set of its own.

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -170,6 +170,7 @@ POD_DTYPE = np.dtype(
      ("pref_term_first", "<i4"), ("pref_term_count", "<i4"),
      ("use_first", "<i4"), ("use_count", "<i4"), ("add_first", "<i4"), ("add_count", "<i4"),
      ("topo_flags", "<u4"), ("nb_flags", "<u4"), ("nn_first", "<i4"), ("nn_count", "<i4"),
+     ("vb_first", "<i4"), ("vb_count", "<i4"), ("vz_first", "<i4"), ("vz_count", "<i4"),
      ("nb_req", "<i8"), ("nb_add", "<i8")], align=True)
 TOPO_USE_DTYPE = np.dtype(
     [("cls", "<i4"), ("arg", "<i4"), ("col", "<u2"), ("kind", "u1"), ("flags", "u1"), ("_pad", "<i4")],

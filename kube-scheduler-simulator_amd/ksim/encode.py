@@ -15,6 +15,7 @@ import numpy as np
 from . import abi, netbw
 from .model import (Node, Pod, Taint, Toleration, quantity_milli_value, quantity_value)
 from .topology import TopologyError, TopologyIndex, pod_uses, register_pod_classes, topo_log_table
+from .volumes import VolumeUnsupported
 
 LABEL_HOSTNAME = "kubernetes.io/hostname"
 LABEL_ZONE = "topology.kubernetes.io/zone"
@@ -501,6 +502,10 @@ class _PodBuilder:
     def field_requirement(self, r) -> None:
         # nodeSelectorRequirementsAsFieldSelector: metadata.name In/NotIn with
         # exactly one value; anything else is a parse error (term dropped).
+        # ksim.volumes hands PV terms over already decided ("__true__" /
+        # "__false__": CheckNodeAffinity's node has no name).
+        if r.operator in ("__true__", "__false__"):
+            return self._expr(0, abi.OP_TRUE) if r.operator == "__true__" else self._expr()
         if r.key != "metadata.name" or r.operator not in ("In", "NotIn") or len(r.values) != 1:
             return self._expr()
         pos = [self.pos_of[r.values[0]]] if r.values[0] in self.pos_of else []
@@ -547,9 +552,12 @@ def _tol_bits(tolerations: Sequence[Toleration], vocab: Sequence[Taint]) -> np.n
     return w
 
 
-def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
+def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None) -> EncodedPods:
     """Compile pods against the cluster vocabulary (the per-pod PreFilter /
-    PreScore precomputation of Fit, TaintToleration and NodeAffinity)."""
+    PreScore precomputation of Fit, TaintToleration and NodeAffinity).
+    ``volumes``: a ksim.volumes.VolumeIndex for pods with PersistentVolumeClaims
+    (VolumeBinding / VolumeZone groups); without one such pods are flagged
+    KSIM_POD_HAS_VOLUMES (the engine refuses them)."""
     b = _PodBuilder(cluster)
     arr = np.zeros(len(pods), abi.POD_DTYPE)
     names = []
@@ -616,6 +624,22 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod]) -> EncodedPods:
         rec["pref_term_count"] = len(b.terms) - rec["pref_term_first"]
         if p.has_volumes:
             flags |= abi.POD_HAS_VOLUMES
+        elif p.pvc_claims:
+            groups = None
+            if volumes is not None:
+                try:
+                    groups = volumes.groups(p)
+                except VolumeUnsupported:
+                    groups = None
+            if groups is None:
+                flags |= abi.POD_HAS_VOLUMES
+            else:
+                for key, terms_of in (("vb", groups[0]), ("vz", groups[1])):
+                    rec[f"{key}_first"] = len(b.terms)
+                    for g, ts in enumerate(terms_of):
+                        for t in ts:
+                            b.term(t, g)
+                    rec[f"{key}_count"] = len(b.terms) - rec[f"{key}_first"]
         pf = prefilter_node_names(p)
         pf_names.append(pf)
         if pf is not None:                    # findNodesThatFitPod scans only these nodes

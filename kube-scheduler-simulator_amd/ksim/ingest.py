@@ -18,9 +18,11 @@ module turns one such document into what the engine runs:
   (plugins.go:103-179), every non-profile field reset to the default, so
   percentageOfNodesToScore is 0 (ADAPT) whatever the document says.
 
-PVs, PVCs and StorageClasses are carried but not evaluated: pods that mount
-volumes of the volume plugins' kinds are reported in ``unsupported`` and left
-out of the queue (the engine's volume filters only cover pods without them).
+PVs and PVCs feed VolumeBinding and VolumeZone for claims bound to a PV
+(ksim.volumes: PV node affinity, PV topology labels).  Pods with volumes the
+engine does not model (inline disks, CSI inline, ephemeral, unbound or missing
+claims, ReadWriteOncePod, PVs counted against node volume limits) are reported
+in ``unsupported`` and left out of the queue.
 """
 from __future__ import annotations
 
@@ -30,7 +32,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import profile as prof_mod
-from .model import Node, Pod, node_from_dict, pod_from_dict
+from .model import Node, Pod, node_from_dict, pod_from_dict, pv_from_dict, pvc_from_dict
+from .volumes import VolumeIndex, VolumeUnsupported
 from .netbw import NetworkBandwidthArgs
 
 
@@ -42,6 +45,7 @@ class Snapshot:
     namespaces: Dict[str, Dict[str, str]]
     profiles: List[Tuple[str, prof_mod.SchedulerProfile]]   # (schedulerName, profile)
     unsupported: List[Tuple[str, str, str]] = field(default_factory=list)   # (namespace, name, why)
+    volumes: Optional[VolumeIndex] = None    # the document's PVs / PVCs (VolumeBinding, VolumeZone)
     counts: Dict[str, int] = field(default_factory=dict)
 
 
@@ -129,6 +133,8 @@ def load(doc: dict) -> Snapshot:
     names = {n.name for n in nodes}
     if len(names) != len(nodes):
         raise ValueError("duplicate node names")
+    volumes = VolumeIndex.from_nodes(nodes, [pv_from_dict(d) for d in doc.get("pvs") or []],
+                                     [pvc_from_dict(d) for d in doc.get("pvcs") or []])
     bound, pending, unsupported = [], [], []
     keyed = []
     for idx, d in enumerate(doc.get("pods") or []):
@@ -143,12 +149,18 @@ def load(doc: dict) -> Snapshot:
         if pod.has_volumes:
             unsupported.append((pod.namespace, pod.name, "volumes"))
             continue
+        if pod.pvc_claims:
+            try:
+                volumes.groups(pod)
+            except VolumeUnsupported as e:
+                unsupported.append((pod.namespace, pod.name, f"volumes: {e}"))
+                continue
         ts = (d.get("metadata") or {}).get("creationTimestamp") or ""
         keyed.append((-pod.priority, ts, idx, pod))
     keyed.sort(key=lambda t: t[:3])           # PrioritySort, then queue arrival
     pending = [t[3] for t in keyed]
     return Snapshot(nodes, bound, pending, namespaces, profiles_from_config(doc.get("schedulerConfig")),
-                    unsupported,
+                    unsupported, volumes,
                     {k: len(doc.get(k) or []) for k in ("pods", "nodes", "pvs", "pvcs", "storageClasses",
                                                          "priorityClasses", "namespaces")})
 
@@ -158,7 +170,7 @@ def encode(snap: Snapshot, profile_index: int = 0):
     from .encode import encode_cluster, encode_pods
     sp = snap.profiles[profile_index][1]
     cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces, nb_args=sp.network_bandwidth)
-    pods = encode_pods(cluster, snap.pending)
+    pods = encode_pods(cluster, snap.pending, volumes=snap.volumes)
     return cluster, pods, prof_mod.compile_profile(sp, cluster.scalar_names)
 
 

@@ -237,7 +237,8 @@ class Pod:
     preferred_terms: List[PreferredTerm] = field(default_factory=list)
     tolerations: List[Toleration] = field(default_factory=list)
     node_name: str = ""
-    has_volumes: bool = False
+    has_volumes: bool = False          # a volume the engine does not model (inline disks, CSI, ephemeral, ...)
+    pvc_claims: List[str] = field(default_factory=list)   # persistentVolumeClaim.claimName of each such volume
     priority: int = 0
     topology_spread: List[TopologySpreadConstraint] = field(default_factory=list)
     pod_affinity_required: List[PodAffinityTerm] = field(default_factory=list)
@@ -252,11 +253,51 @@ class Pod:
                     self.pod_anti_affinity_required or self.pod_anti_affinity_preferred)
 
 
+@dataclass
+class PersistentVolume:
+    """v1.PersistentVolume fields VolumeBinding / VolumeZone read for a bound claim."""
+    name: str
+    labels: Dict[str, str] = field(default_factory=dict)
+    node_affinity: Optional[List[NodeSelectorTerm]] = None   # spec.nodeAffinity.required.nodeSelectorTerms
+    source: str = ""                                        # the spec key of its volume source (csi, local, ...)
+    access_modes: List[str] = field(default_factory=list)
+
+
+@dataclass
+class PersistentVolumeClaim:
+    name: str
+    namespace: str = "default"
+    volume_name: str = ""                                    # spec.volumeName ("" = unbound)
+    access_modes: List[str] = field(default_factory=list)
+
+
 # ---- v1 dict parsing --------------------------------------------------------
 # Volume sources the volume filter plugins (VolumeRestrictions, *Limits,
 # VolumeBinding, VolumeZone) act on; pods with none of them pass all of those.
+# persistentVolumeClaim volumes are kept as claims (Pod.pvc_claims); the others
+# mark the pod has_volumes (not modelled).
 _VOLUME_SOURCES = ("persistentVolumeClaim", "gcePersistentDisk", "awsElasticBlockStore",
                    "azureDisk", "csi", "rbd", "iscsi", "cinder", "ephemeral")
+_PV_SOURCES = ("csi", "local", "hostPath", "nfs", "awsElasticBlockStore", "gcePersistentDisk", "azureDisk",
+               "azureFile", "cinder", "rbd", "iscsi", "fc", "cephfs", "glusterfs", "portworxVolume",
+               "vsphereVolume", "flexVolume", "flocker", "quobyte", "scaleIO", "storageos", "photonPersistentDisk")
+
+
+def pv_from_dict(d: dict) -> PersistentVolume:
+    md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
+    req = ((spec.get("nodeAffinity") or {}).get("required"))
+    return PersistentVolume(
+        name=md.get("name", ""), labels=dict(md.get("labels") or {}),
+        node_affinity=None if req is None else [_term(t) for t in (req.get("nodeSelectorTerms") or [])],
+        source=next((k for k in _PV_SOURCES if k in spec), ""),
+        access_modes=list(spec.get("accessModes") or []))
+
+
+def pvc_from_dict(d: dict) -> PersistentVolumeClaim:
+    md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
+    return PersistentVolumeClaim(name=md.get("name", ""), namespace=md.get("namespace", "default") or "default",
+                                 volume_name=spec.get("volumeName", "") or "",
+                                 access_modes=list(spec.get("accessModes") or []))
 
 def _req(d) -> Requirement:
     return Requirement(d["key"], d["operator"], list(d.get("values") or []))
@@ -331,7 +372,10 @@ def pod_from_dict(d: dict) -> Pod:
         tolerations=[Toleration(t.get("key", ""), t.get("operator", ""), t.get("value", ""), t.get("effect", ""))
                      for t in (spec.get("tolerations") or [])],
         node_name=spec.get("nodeName", "") or "",
-        has_volumes=any(any(k in v for k in _VOLUME_SOURCES) for v in (spec.get("volumes") or [])),
+        has_volumes=any(any(k in v for k in _VOLUME_SOURCES if k != "persistentVolumeClaim")
+                        for v in (spec.get("volumes") or [])),
+        pvc_claims=[(v.get("persistentVolumeClaim") or {}).get("claimName", "")
+                    for v in (spec.get("volumes") or []) if "persistentVolumeClaim" in v],
         priority=int(spec.get("priority") or 0),
         topology_spread=[_spread(c) for c in (spec.get("topologySpreadConstraints") or [])],
         pod_affinity_required=[_pod_term(t) for t in (pa.get("requiredDuringSchedulingIgnoredDuringExecution") or [])],

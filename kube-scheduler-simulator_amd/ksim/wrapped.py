@@ -75,6 +75,12 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
         return ERR_PTS_LABEL if detail == abi.PTS_MISSING_LABEL else ERR_PTS
     if plugin == "InterPodAffinity":
         return ERR_IPA[detail]
+    if plugin == "VolumeBinding":
+        from .volumes import MSG_VOLUME_BINDING
+        return MSG_VOLUME_BINDING
+    if plugin == "VolumeZone":
+        from .volumes import MSG_VOLUME_ZONE
+        return MSG_VOLUME_ZONE
     return f"{plugin} failed"
 
 

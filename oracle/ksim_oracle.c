@@ -319,6 +319,27 @@ static int term_matches(const ksim_oracle* o, const ksim_pod_set* ps, const ksim
   return 1;
 }
 
+/* VolumeBinding (binder.go checkBoundClaims -> volumeutil.CheckNodeAffinity,
+ * one group per bound PV with required node affinity) and VolumeZone
+ * (volume_zone.go Filter, one group per PV topology label): every group of
+ * terms [first, first + count) (ksim_term.weight = group index) has a
+ * matching term.  The groups are compiled by ksim/encode.py (see the header). */
+static int volume_groups_match(const ksim_oracle* o, const ksim_pod_set* ps, int32_t first, int32_t count,
+                               int32_t node) {
+  int32_t group = -1;
+  int ok = 1;
+  for (int32_t i = 0; i < count; i++) {
+    const ksim_term* t = &ps->terms[first + i];
+    if (t->weight != group) {
+      if (!ok) return 0;
+      group = t->weight;
+      ok = 0;
+    }
+    if (!ok && term_matches(o, ps, t, node)) ok = 1;
+  }
+  return ok;
+}
+
 /* RequiredNodeAffinity.Match: nodeSelector (labels.SelectorFromSet) AND
  * (OR of required terms) — [upstream] nodeaffinity.Filter, §8(a) a26 */
 static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set* ps,
@@ -811,6 +832,12 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
       case KSIM_PL_NODE_AFFINITY:
         if (!required_node_affinity_match(o, ps, p, node)) return (uint8_t)f;
         break;
+      case KSIM_PL_VOLUME_BINDING:       /* bound claims: PV node affinity */
+        if (!volume_groups_match(o, ps, p->vb_first, p->vb_count, node)) return (uint8_t)f;
+        break;
+      case KSIM_PL_VOLUME_ZONE:          /* bound claims: PV topology labels */
+        if (!volume_groups_match(o, ps, p->vz_first, p->vz_count, node)) return (uint8_t)f;
+        break;
       case KSIM_PL_NODE_RESOURCES_FIT: {
         uint32_t r = fits_request(o, p, node);
         if (r) { *detail = r; return (uint8_t)f; }
@@ -834,7 +861,7 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
         if (r) { *detail = r; return (uint8_t)f; }
         break;
       }
-      /* volume plugins: pods without volumes pass. */
+      /* the other volume plugins: bound claims of unlimited kinds pass. */
       default:
         break;
     }

@@ -134,7 +134,7 @@ class ObjScheduler:
     def __init__(self, nodes: List[Node], bound: List[Pod] = (), namespaces: Optional[Dict[str, Dict]] = None,
                  pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
                  hard_pod_affinity_weight: int = 1, network_bandwidth=None, nb_filter: bool = True,
-                 nb_score: bool = True):
+                 nb_score: bool = True, pvs=(), pvcs=()):
         order = node_tree_order([zone_key(n.labels) for n in nodes])
         self.nodes = [NodeInfo(nodes[i]) for i in order]
         # cache.addNodeImageStates, nodes in the order they were added: name -> [size, {node names}]
@@ -168,6 +168,9 @@ class ObjScheduler:
                 self.score_order.append("NetworkBandwidth")
         self.seed = seed
         self.hard_w = hard_pod_affinity_weight
+        # the snapshot's PersistentVolumes and PersistentVolumeClaims (VolumeBinding / VolumeZone)
+        self.pvs = {pv.name: pv for pv in pvs}
+        self.pvcs = {(c.namespace, c.name): c for c in pvcs}
         self.next_start = 0
         self.seq = 0
 
@@ -213,6 +216,39 @@ class ObjScheduler:
         if pod.required_terms is not None:
             return any(self._term_match(t, node) for t in pod.required_terms)
         return True
+
+    # ---- VolumeBinding / VolumeZone for bound claims (v1.26) ---------------------
+    TOPOLOGY_LABELS = ("failure-domain.beta.kubernetes.io/zone", "failure-domain.beta.kubernetes.io/region",
+                       "topology.kubernetes.io/zone", "topology.kubernetes.io/region")
+
+    def _bound_pvs(self, pod: Pod):
+        return [self.pvs[self.pvcs[(pod.namespace, c)].volume_name] for c in pod.pvc_claims]
+
+    def volume_binding_ok(self, pod: Pod, node: Node) -> bool:
+        """binder.go checkBoundClaims: volumeutil.CheckNodeAffinity(pv, node.Labels)
+        for every bound claim; the node it builds carries labels only."""
+        labels_only = Node(name="", labels=node.labels)
+        for pv in self._bound_pvs(pod):
+            if pv.node_affinity is None:
+                continue
+            if not any(self._term_match(t, labels_only) for t in pv.node_affinity):
+                return False
+        return True
+
+    def volume_zone_ok(self, pod: Pod, node: Node) -> bool:
+        """volume_zone.go getPVbyPod + Filter."""
+        tops = []
+        for pv in self._bound_pvs(pod):
+            for k, v in pv.labels.items():
+                if k not in self.TOPOLOGY_LABELS:
+                    continue
+                zones = [z.strip() for z in v.split("__")]
+                if any(not z for z in zones):
+                    continue                      # LabelZonesToSet error: the label is ignored
+                tops.append((k, set(zones)))
+        if not any(k in node.labels for k in self.TOPOLOGY_LABELS):
+            return True                           # the node has no zone constraints
+        return all(k in node.labels and node.labels[k] in zs for k, zs in tops)
 
     @staticmethod
     def untolerated_taint(pod: Pod, node: Node, effects=("NoSchedule", "NoExecute")):
@@ -700,6 +736,12 @@ class ObjScheduler:
                 msg = self.pts_filter(pod, pts, node)
             elif pl == "InterPodAffinity":
                 msg = self.ipa_filter(ipa, node)
+            elif pl == "VolumeBinding":
+                if pod.pvc_claims and not self.volume_binding_ok(pod, node):
+                    msg = "node(s) had volume node affinity conflict"
+            elif pl == "VolumeZone":
+                if pod.pvc_claims and not self.volume_zone_ok(pod, node):
+                    msg = "node(s) had no available volume zone"
             if msg:
                 return pl, msg
         return None, None

@@ -127,11 +127,12 @@ def test_from_dict_roundtrip():
                                         {"key": "a", "operator": "In", "values": ["b"]}]}]}}},
                                 "volumes": [{"name": "x", "persistentVolumeClaim": {"claimName": "c"}}]}})
     assert p.required_terms[0].match_expressions[0].values == ["b"]
-    assert p.containers[0].host_ports == [8080] and p.has_volumes
+    assert p.containers[0].host_ports == [8080] and p.pvc_claims == ["c"] and not p.has_volumes
     c, _ = encode_cluster([n])
     e = encode_pods(c, [p])
     rec = e.pods[0]
-    # host ports compile to a NodePorts use (class of pods on 0.0.0.0:8080/TCP); volumes stay unsupported
+    # host ports compile to a NodePorts use (class of pods on 0.0.0.0:8080/TCP); a claim without a
+    # VolumeIndex (no PVs / PVCs given) stays unsupported
     assert not rec["flags"] & abi.POD_HAS_HOST_PORTS and rec["flags"] & abi.POD_HAS_VOLUMES
     assert rec["use_count"] == 1 and e.uses[rec["use_first"]]["kind"] == abi.USE_NODE_PORT
 

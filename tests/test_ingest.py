@@ -91,10 +91,13 @@ def _template_cluster(n_nodes=40, n_pods=300, bound_every=4):
 def test_template_cluster_schedules_like_objref(pct):
     """UI templates (node.yaml / pod.yaml) -> ingest -> C oracle placements
     equal the object-level restatement on the same objects; bound pods fill
-    their nodes; pods with PVC volumes are reported, not scheduled."""
+    their nodes; the pod with a PVC (the sample's pvc1, bound to the hostPath
+    PV pv1) is scheduled with VolumeBinding / VolumeZone (no node affinity, no
+    topology labels: every node passes)."""
     snap = ingest.load(_template_cluster())
-    assert snap.unsupported == [("default", "with-pvc", "volumes")]
-    assert len(snap.bound) == 38 and len(snap.pending) == 300 - 38
+    assert snap.unsupported == []
+    assert len(snap.bound) == 38 and len(snap.pending) == 300 - 38 + 1
+    assert [p.name for p in snap.pending if p.pvc_claims] == ["with-pvc"]
     cluster, enc, prof = ingest.encode(snap)
     assert cluster.alloc_cpu.sum() == sum(4000 * (1 + i % 4) for i in range(40))
     assert cluster.req_mem.sum() == sum((1 + i % 8) << 30 for i in range(0, 150, 4))
@@ -102,7 +105,8 @@ def test_template_cluster_schedules_like_objref(pct):
     sp.percentage_of_nodes_to_score = pct
     prof = profile.compile_profile(sp, cluster.scalar_names)
     ochosen, _ = Oracle(cluster, prof).schedule(enc)
-    ref = ObjScheduler(snap.nodes, snap.bound, namespaces=snap.namespaces, pct=pct, seed=sp.tiebreak_seed)
+    ref = ObjScheduler(snap.nodes, snap.bound, namespaces=snap.namespaces, pct=pct, seed=sp.tiebreak_seed,
+                       pvs=snap.volumes.pvs.values(), pvcs=snap.volumes.pvcs.values())
     names = cluster.node_names
     for i, pod in enumerate(snap.pending):
         got = ref.cycle(pod)["chosen"]

@@ -1020,8 +1020,8 @@ struct RawScores {
 struct BatchProg;
 __device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m);
-__device__ __forceinline__ int32_t fast_balanced_allocation(const ksim_pod& p, const NodeRow& r, double inv_c,
-                                                            double inv_m);
+__device__ __forceinline__ int32_t fast_balanced_allocation(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+                                                            double inv_c, double inv_m);
 
 // fast (non-null): BatchProg::fast_w on a kClusterNarrow cluster, so the
 // cpu / memory strategies take the host-reciprocal quotients (inv_c, inv_m).
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const Dev
   int64_t v;
   KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fast ? (int64_t)fast_least_allocated(*fast, p, r, inv_c, inv_m)
                                                 : fit_least_allocated_score(r, prof, p, c.n_scalar));
-  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(p, r, inv_c, inv_m)
+  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(*fast, p, r, inv_c, inv_m)
                                                 : balanced_allocation_score(r, prof, p, c.n_scalar));
   KSIM_PUT(KSIM_PL_TAINT_TOLERATION, rv.taint, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
   KSIM_PUT(KSIM_PL_NODE_AFFINITY, rv.aff, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
@@ -1470,32 +1470,48 @@ __device__ __forceinline__ double div_rn(double n, double d, double y) {
 // its correction steps, and for BalancedAllocation bit for bit the float64
 // quotient Go computes.  hseed = seed ^ (seq << 20), the pod's part of the
 // tie-break hash.
-// leastResourceScorer over {cpu, memory} (BatchProg::fast_w, kClusterNarrow)
+// An integer in [0, 2^52) as a double, exactly: the bits of 2^52 + x minus
+// 2^52 (one OR and one add, where the general int64 conversion takes two
+// conversions, a scale and an add).  Every value the FAST keys convert is
+// below 2^46 (kClusterNarrow allocatables; sums bounded by them, see callers).
+__device__ __forceinline__ double u52_to_f64(int64_t x) {
+  return __longlong_as_double(x | 0x4330000000000000LL) - 4503599627370496.0;
+}
+
+// leastResourceScorer over {cpu, memory} (BatchProg::fast_w, kClusterNarrow).
+// (alloc - requested) * 100 is an integer below 2^53, so the double product of
+// the converted difference and 100 is exact, as the int64 product converted is.
 __device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m) {
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
   const int64_t rc = r.nz_cpu + p.nz_cpu, rm = r.nz_mem + p.nz_mem;
+  const double ac = u52_to_f64(r.alloc_cpu), am = u52_to_f64(r.alloc_mem);
   const int32_t sc = (!hc || rc > r.alloc_cpu) ? 0
-                     : (int32_t)div_rn((double)((r.alloc_cpu - rc) * kMaxNodeScore), (double)r.alloc_cpu, inv_c);
+                     : (int32_t)div_rn(u52_to_f64(r.alloc_cpu - rc) * (double)kMaxNodeScore, ac, inv_c);
   const int32_t sm = (!hm || rm > r.alloc_mem) ? 0
-                     : (int32_t)div_rn((double)((r.alloc_mem - rm) * kMaxNodeScore), (double)r.alloc_mem, inv_m);
+                     : (int32_t)div_rn(u52_to_f64(r.alloc_mem - rm) * (double)kMaxNodeScore, am, inv_m);
   if (bp.fit_w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
   const int64_t wc = hc ? bp.fit_w_cpu : 0, wm = hm ? bp.fit_w_mem : 0;
   const double inv = (hc && hm) ? bp.inv_w[2] : hc ? bp.inv_w[0] : bp.inv_w[1];
   return (hc || hm) ? (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv) : 0;
 }
 
-// balancedResourceScorer over {cpu, memory}: the float64 quotients Go computes
-__device__ __forceinline__ int32_t fast_balanced_allocation(const ksim_pod& p, const NodeRow& r, double inv_c,
-                                                            double inv_m) {
+// balancedResourceScorer over {cpu, memory}: the float64 quotients Go computes.
+// With a Fit filter in the profile it passed, so requested + request <=
+// allocatable < 2^46 and the short conversion is exact (without one the sums
+// are unbounded and take the general conversion).
+__device__ __forceinline__ int32_t fast_balanced_allocation(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+                                                            double inv_c, double inv_m) {
+  const bool fit = bp.has_fit_filter != 0;
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
+  const int64_t qc = r.req_cpu + p.req_cpu, qm = r.req_mem + p.req_mem;
   double f0 = 0, f1 = 0;
   if (hc) {
-    const double f = div_rn((double)(r.req_cpu + p.req_cpu), (double)r.alloc_cpu, inv_c);
+    const double f = div_rn(fit ? u52_to_f64(qc) : (double)qc, u52_to_f64(r.alloc_cpu), inv_c);
     f0 = f > 1 ? 1 : f;
   }
   if (hm) {
-    const double f = div_rn((double)(r.req_mem + p.req_mem), (double)r.alloc_mem, inv_m);
+    const double f = div_rn(fit ? u52_to_f64(qm) : (double)qm, u52_to_f64(r.alloc_mem), inv_m);
     if (hc) f1 = f > 1 ? 1 : f;
     else f0 = f > 1 ? 1 : f;
   }
@@ -1514,7 +1530,7 @@ __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim
   }
   int32_t tot = 0;
   if (bp.w_fit) tot += (int32_t)bp.w_fit * fast_least_allocated(bp, p, r, inv_c, inv_m);
-  if (bp.w_ba) tot += (int32_t)bp.w_ba * fast_balanced_allocation(p, r, inv_c, inv_m);
+  if (bp.w_ba) tot += (int32_t)bp.w_ba * fast_balanced_allocation(bp, p, r, inv_c, inv_m);
   if (bp.no_score) tot = 1;
   const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
   return ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);

@@ -253,6 +253,9 @@ def main():
     ap.add_argument("--force-shard", action="store_true",
                     help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--shard-mode", choices=["replicated", "nodes"], default="replicated",
+                    help="config 2 over N > 1 GPUs: replicated snapshot with the evaluation split by node range "
+                         "(one collective per batch), or node shards (two)")
     ap.add_argument("--host-match", action="store_true",
                     help="config 3: match the count classes' selectors on the host instead of ksim_match_terms")
     ap.add_argument("--no-adapt", action="store_true", help="skip the secondary ADAPT measurement (config 2)")
@@ -291,7 +294,13 @@ def main():
 
     if sharded:
         uid = shard.broadcast_unique_id(dist, rank) if world > 1 else engine.comm_unique_id()
-        eng = shard.sharded_engine(cluster, prof, rank, world, local, uid)
+        if cfg == 2 and args.shard_mode == "replicated":
+            # every rank holds the whole snapshot, the batch top-T is split:
+            # one all-gather per batch instead of an all-gather + all-reduce
+            eng = shard.replicated_engine(cluster, prof, rank, world, local, uid)
+            desc += ", replicated snapshot (evaluation split by node range)"
+        else:
+            eng = shard.sharded_engine(cluster, prof, rank, world, local, uid)
     else:
         eng = engine.Engine(local)
         eng.set_profile(prof)

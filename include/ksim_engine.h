@@ -511,6 +511,16 @@ int ksim_reset_cluster(ksim_handle* h);
 int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total);
 /* One process per GPU over RCCL: rank 0 creates the id (ncclGetUniqueId),
  * every rank passes the same bytes; ksim_schedule_loaded then runs sharded. */
+/* Replicated node sharding (an alternative to ksim_set_shard for the P100
+ * batch path): the handle holds EVERY node (ksim_set_cluster with the whole
+ * snapshot) and its batch top-T evaluates only local positions [eval_lo,
+ * eval_hi); the ranks' ranges tile the cluster in rank order.  Each batch then
+ * needs one exchange (the all-gather of the per-rank candidate records): the
+ * pair keys of every guess are computed locally and every rank binds every
+ * placement, so the replicas stay equal.  Other runs (per-pod cycles, ADAPT)
+ * execute whole on every replica.  Call after ksim_set_cluster (a new
+ * snapshot clears it) and before ksim_comm_init / the group call. */
+int ksim_set_eval_range(ksim_handle* h, int32_t eval_lo, int32_t eval_hi);
 int ksim_comm_unique_id(uint8_t* id /* [KSIM_COMM_ID_BYTES] */);
 int ksim_comm_init(ksim_handle* h, int32_t rank, int32_t world, const uint8_t* id);
 /* An in-process group of shard handles on one device (exchanges by device

@@ -164,13 +164,13 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   if constexpr (FAST) {
     // kTopStep nodes per step as independent chains (every row loaded up front)
 #pragma unroll 1
-    for (int32_t node = threadIdx.x; node < c.n; node += kTopStep * kTopThreads) {
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
       NodeRow r[kTopStep];
       double ic[kTopStep], im[kTopStep];
 #pragma unroll
       for (int u = 0; u < kTopStep; u++) {
         const int32_t nu = node + u * kTopThreads;
-        const int32_t x = nu < c.n ? nu : node;
+        const int32_t x = nu < c.eval_hi ? nu : node;
         r[u] = load_res_row(c, x);
         ic[u] = c.inv_cpu[x];
         im[u] = c.inv_mem[x];
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
 #pragma unroll
       for (int u = 0; u < kTopStep; u++) {
         const int32_t nu = node + u * kTopThreads;
-        const uint64_t k = nu < c.n ? dyn_key_fast(bp, p, r[u], ic[u], im[u], hseed, c.base + nu) : 0;
+        const uint64_t k = nu < c.eval_hi ? dyn_key_fast(bp, p, r[u], ic[u], im[u], hseed, c.base + nu) : 0;
         nfeas += k != 0;
         a[3] = umax64(a[3], k);
         cswap_desc(a[2], a[3]);
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     }
   }
 #pragma unroll 1
-  for (int32_t node = threadIdx.x; node < (FAST ? 0 : c.n); node += kTopThreads) {
+  for (int32_t node = c.eval_lo + threadIdx.x; node < (FAST ? 0 : c.eval_hi); node += kTopThreads) {
     uint64_t kk = 0;
     {
       const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
@@ -670,7 +670,7 @@ static bool tile_eval() {
 
 // Evaluation and per-pod top-T (xsend: the sharded record, else null).
 static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream, hipEvent_t* mid = nullptr) {
-  if (tile_eval()) {
+  if (tile_eval() && a.c.eval_lo == 0 && a.c.eval_hi == a.c.n) {   // the tile form evaluates every node
     const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
     const dim3 g1((n_tiles + 3) / 4, kBatchPods);
     if (a.fast)

@@ -71,7 +71,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
       st->next_start = (int32_t)(((int64_t)awin[2 * (committed - 1)] + (cut >= 0 ? cut : c.n_total)) % c.n_total);
       st->evals += s_evals;
     } else {
-      st->evals += (int64_t)committed * c.n;
+      st->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);   // the nodes this handle evaluated
     }
     st->cursor = base + committed;
     st->pod_seq = seq0 + committed;

@@ -30,6 +30,10 @@ struct DevCluster {
   // n_total nodes.  Memory is indexed by the LOCAL position; tie-break keys,
   // spec.nodeName and metadata.name field selectors use the GLOBAL one.
   int32_t n_label_values, n_prefer_taints, base, n_total;
+  // the nodes k_batch_top evaluates (local positions [eval_lo, eval_hi)): all
+  // of them, except on replicated handles (ksim_set_eval_range), which hold
+  // every node and evaluate one range of them
+  int32_t eval_lo, eval_hi;
   const int64_t* alloc_cpu;
   const int64_t* alloc_mem;
   const int64_t* alloc_eph;

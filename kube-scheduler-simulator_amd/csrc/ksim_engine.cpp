@@ -138,6 +138,11 @@ struct ksim_handle {
 
   // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
   int32_t shard_base = 0, shard_total = 0;
+  // replicated handle (ksim_set_eval_range): holds every node, evaluates
+  // [eval_lo, eval_hi) in the P100 batch top-T and keeps its replica by
+  // binding every placement: one exchange per batch (the records' all-gather)
+  bool replicated = false;
+  int32_t eval_lo = 0, eval_hi = 0;
   int32_t rank = 0, world = 1;
   ncclComm_t comm = nullptr;
 
@@ -382,6 +387,8 @@ int ensure_ready(ksim_handle* h) {
 LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen) {
   LaunchArgs a;
   a.c = h->dc;
+  a.c.eval_lo = 0;                       // every node (replicated shard batches narrow it, shard_batch)
+  a.c.eval_hi = a.c.n;
   a.P = P;
   a.prof = h->prof;
   a.bp = h->bp;
@@ -520,15 +527,24 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn, bool adap
 // keys.  `hs` is either {this rank's handle} with an RCCL communicator (one
 // process per GPU) or an in-process group of shard handles on one device
 // (exchanges by device copies).  Everything runs on `stream`, asynchronously.
+// Replicated handles hold every node: each evaluates its range, and the pair
+// keys and binds of every guess are local, so the pair-key all-reduce is not
+// needed (one exchange per batch).
+LaunchArgs shard_args(ksim_handle* h, bool fast) {
+  LaunchArgs la = make_args(h, h->dp, h->d_chosen);
+  la.fast = fast;
+  if (h->replicated) {
+    la.c.eval_lo = h->eval_lo;
+    la.c.eval_hi = h->eval_hi;
+  }
+  return la;
+}
+
 int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fast) {
   const int R = (int)hs.size();
   ksim_handle* h0 = hs[0];
   const size_t rec = (size_t)kBatchPods * kXRec;            // u64 per shard
-  for (auto* h : hs) {
-    LaunchArgs la = make_args(h, h->dp, h->d_chosen);
-    la.fast = fast;
-    launch_shard_eval(la, stream);
-  }
+  for (auto* h : hs) launch_shard_eval(shard_args(h, fast), stream);
   if (h0->comm) {
     const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
     if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
@@ -539,12 +555,10 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
                                   hipMemcpyDeviceToDevice, stream));
   }
   const int32_t world = h0->comm ? h0->world : R;
-  for (auto* h : hs) {
-    LaunchArgs la = make_args(h, h->dp, h->d_chosen);
-    la.fast = fast;
-    launch_shard_chain(la, world, stream);
-  }
-  if (h0->comm) {
+  for (auto* h : hs) launch_shard_chain(shard_args(h, fast), world, stream);
+  if (h0->replicated) {
+    // every guess is local: the pair maxima are complete on every handle
+  } else if (h0->comm) {
     const ncclResult_t r =
         rccl().all_reduce(h0->sc.pmax, h0->sc.pmax, kBatchPods, ncclUint64, ncclMax, h0->comm, stream);
     if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllReduce: ") + rccl().error_string(r));
@@ -554,7 +568,7 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
     for (int i = 0; i < R; i++) g.p[i] = hs[i]->sc.pmax;
     launch_group_max(g, stream);
   }
-  for (auto* h : hs) launch_shard_commit(make_args(h, h->dp, h->d_chosen), stream);
+  for (auto* h : hs) launch_shard_commit(shard_args(h, fast), stream);
   HIPCHK(h0, hipGetLastError());
   return KSIM_OK;
 }
@@ -895,6 +909,19 @@ int shard_run_adapt(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
 int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t count) {
   if (profile_nb(hs[0]->prof))
     return set_err(hs[0], KSIM_E_UNSUPPORTED, "NetworkBandwidth profiles run on unsharded handles");
+  if (hs[0]->replicated) {
+    // P100 batch stretches on the replicated exchange; everything else runs
+    // whole on every replica (the same cycles, so the replicas stay equal)
+    const bool adapt = adapt_mode(hs[0]);
+    return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
+      if (batch && !adapt) return shard_run(hs, a, b);
+      for (auto* h : hs) {
+        int rc = run_range(h, a, b, batch, topo);
+        if (rc) return rc;
+      }
+      return (int)KSIM_OK;
+    }, true);
+  }
   const bool adapt = adapt_mode(hs[0]);
   const bool adapt_batch = adapt && adapt_shard_layout(hs);
   return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool) {
@@ -1059,6 +1086,7 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
 }
 
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v) {
+  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
   if (!h || !t || !v) return KSIM_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));
   const int32_t n = t->n_nodes;
@@ -1303,6 +1331,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
 // Loaded pods, the bound-pod table and captured graphs are dropped (node
 // positions changed).
 int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v, const int32_t* old_pos) {
+  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
   if (!h || !t || !v) return KSIM_E_INVALID;
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_upsert_nodes before ksim_set_cluster");
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_upsert_nodes on a shard handle");
@@ -1385,6 +1414,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
 // table handed to ksim_upsert_nodes is the current snapshot without it, so the
 // replay keeps every other node's state.
 int ksim_remove_node(ksim_handle* h, int32_t pos) {
+  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_remove_node on a shard handle");
   const int32_t n0 = h->dc.n;
@@ -2065,6 +2095,19 @@ int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total) {
   return KSIM_OK;
 }
 
+int ksim_set_eval_range(ksim_handle* h, int32_t eval_lo, int32_t eval_hi) {
+  if (!h) return KSIM_E_INVALID;
+  if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_set_eval_range needs the cluster (ksim_set_cluster)");
+  if (h->shard_total != 0) return set_err(h, KSIM_E_INVALID, "a node-shard handle holds only its nodes: no eval range");
+  if (eval_lo < 0 || eval_hi < eval_lo || eval_hi > h->dc.n) return set_err(h, KSIM_E_INVALID, "bad eval range");
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  drop_cycle_graphs(h);                        // shard batch graphs captured with the old range
+  h->replicated = true;
+  h->eval_lo = eval_lo;
+  h->eval_hi = eval_hi;
+  return KSIM_OK;
+}
+
 int ksim_comm_unique_id(uint8_t* id) {
   if (!id) return KSIM_E_INVALID;
   if (!rccl().ok) return KSIM_E_RCCL;
@@ -2106,6 +2149,13 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
     if (h->comm) return set_err(h0, KSIM_E_INVALID, "group handles must not hold a communicator");
     if (h->device != h0->device) return set_err(h0, KSIM_E_INVALID, "group handles must share one device");
     if (!h->dp.pods || h->dp.n_pods != h0->dp.n_pods) return set_err(h0, KSIM_E_INVALID, "pods not loaded alike");
+    if (h->replicated != h0->replicated) return set_err(h0, KSIM_E_INVALID, "mixed replicated / shard handles");
+    if (h->replicated) {                       // replicas: whole clusters, eval ranges tiling it in order
+      if (h->dc.n != h0->dc.n || h->eval_lo != expect)
+        return set_err(h0, KSIM_E_INVALID, "eval ranges must tile the cluster in order");
+      expect = h->eval_hi;
+      continue;
+    }
     if (h->dc.n_total != h0->dc.n_total || h->dc.base != expect)
       return set_err(h0, KSIM_E_INVALID, "shards must tile the cluster in order");
     expect += h->dc.n;

@@ -30,7 +30,7 @@ EXPORTS = [
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
     "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
-    "ksim_match_terms",
+    "ksim_match_terms", "ksim_set_eval_range",
 ]
 
 
@@ -72,6 +72,7 @@ def lib():
         L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
         L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
         L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
+        L.ksim_set_eval_range.argtypes = [vp, i32, i32]
         L.ksim_assume.argtypes = [vp, vp, i32, i32]
         L.ksim_forget.argtypes = [vp, vp, i32, i32]
         L.ksim_load_pods.argtypes = [vp, vp]
@@ -154,6 +155,10 @@ class Engine:
     def set_shard(self, node_base: int, n_total: int):
         """This handle holds global node positions [node_base, node_base + n) of n_total."""
         self._chk(lib().ksim_set_shard(self.h, node_base, n_total))
+
+    def set_eval_range(self, lo: int, hi: int):
+        """Replicated sharding: this handle (whole cluster) evaluates nodes [lo, hi)."""
+        self._chk(lib().ksim_set_eval_range(self.h, lo, hi))
 
     def comm_init(self, rank: int, world: int, uid: bytes):
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)

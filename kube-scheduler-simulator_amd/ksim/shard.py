@@ -55,3 +55,18 @@ def sharded_engine(cluster, prof, rank: int, world: int, device: int, uid: bytes
     eng.set_cluster(cluster.shard(base, cnt))
     eng.comm_init(rank, world, uid)
     return eng
+
+
+def replicated_engine(cluster, prof, rank: int, world: int, device: int, uid: bytes):
+    """This rank's engine in replicated sharding (ksim_set_eval_range): the
+    whole snapshot (a few MB even at 100k nodes, next to 288 GB of HBM), the
+    batch top-T over this rank's range of ``partition``, one all-gather per
+    batch over RCCL."""
+    from .engine import Engine
+    lo, cnt = partition(cluster.n_nodes, world)[rank]
+    eng = Engine(device)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    eng.set_eval_range(lo, lo + cnt)
+    eng.comm_init(rank, world, uid)
+    return eng

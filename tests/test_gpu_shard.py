@@ -226,3 +226,64 @@ def test_rccl_world1_adapt():
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.batches > 0
     assert e.diag()["graph_captures"] >= 1
+
+
+# ---- replicated sharding (ksim_set_eval_range): whole snapshot per handle ----------
+
+def _replicas(cluster, pods, prof, world):
+    engines = []
+    for lo, cnt in partition(cluster.n_nodes, world):
+        e = Engine(0)
+        e.set_profile(prof)
+        e.set_cluster(cluster)
+        e.set_eval_range(lo, lo + cnt)
+        e.load_pods(pods)
+        engines.append(e)
+    return engines
+
+
+@pytest.mark.parametrize("n_nodes,world", [(2000, 2), (1031, 3), (5000, 8)])
+def test_group_replicated(n_nodes, world):
+    """Each replica evaluates its node range in the batch top-T; one exchange
+    per batch (no pair-key all-reduce); every replica binds every placement
+    and ends with the oracle's whole node state."""
+    cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=6000)
+    prof = _prof()
+    engines = _replicas(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert engines[0].diag()["graph_captures"] >= 1
+    os_ = ora.node_state()
+    for e in engines:
+        es = e.node_state()
+        for k in es:
+            np.testing.assert_array_equal(es[k], os_[k])
+
+
+def test_group_replicated_mixed_paths():
+    """Pods the batch path cannot take (taints, node affinity: per-pod cycles)
+    run whole on every replica between replicated batches."""
+    cluster, pods = gen.config1(n_nodes=300, n_pods=3000)
+    prof = _prof()
+    engines = _replicas(cluster, pods, prof, 3)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ochosen, _ = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+
+
+def test_rccl_world1_replicated():
+    cluster, pods = gen.config2(n_nodes=1500, n_pods=6000)
+    prof = _prof()
+    e = Engine(0)
+    e.set_profile(prof)
+    e.set_cluster(cluster)
+    e.set_eval_range(0, cluster.n_nodes)
+    e.comm_init(0, 1, engine.comm_unique_id())
+    e.load_pods(pods)
+    chosen, st = e.schedule_loaded(0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and e.diag()["graph_captures"] >= 1

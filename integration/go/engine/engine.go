@@ -80,6 +80,12 @@ func (e *Engine) UpsertNodes(t *C.ksim_node_table, v *C.ksim_vocab, oldPos []int
 // RemoveNode removes the node at position pos (later nodes move down by one).
 func (e *Engine) RemoveNode(pos int) error { return e.err(C.ksim_remove_node(e.h, C.int32_t(pos))) }
 
+// SetEvalRange makes this handle a replica (whole snapshot) that evaluates
+// nodes [lo, hi) in the batch top-T; the ranks' ranges tile the cluster.
+func (e *Engine) SetEvalRange(lo, hi int) error {
+	return e.err(C.ksim_set_eval_range(e.h, C.int32_t(lo), C.int32_t(hi)))
+}
+
 // MatchTerms answers every (signature, matcher) pair of the count classes'
 // selectors and terms on the device (the existing-pod scans of
 // PodTopologySpread / InterPodAffinity PreFilter and PreScore):

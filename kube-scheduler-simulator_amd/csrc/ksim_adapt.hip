@@ -458,15 +458,18 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
                                                              const int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ chosen_out) {
   __shared__ int32_t s_fb, s_istar, s_sched, s_unsched;
+  __shared__ int2 s_aw[kBatchPods];
   const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
   const int32_t brk = abroken ? abroken[threadIdx.x] : (int32_t)pmax[kBatchPods + threadIdx.x];
+  const int2 aw = reinterpret_cast<const int2*>(awin)[threadIdx.x];   // {scan start, cut}, likewise
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
   const int32_t nchain0 = *chain_end;
+  s_aw[threadIdx.x] = aw;
   if (threadIdx.x == 0) s_fb = nchain0;
   __syncthreads();
   if ((int32_t)threadIdx.x < nchain0 && brk) atomicMin(&s_fb, (int32_t)threadIdx.x);
   __syncthreads();
-  batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, awin);
+  batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw);
 }
 
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",

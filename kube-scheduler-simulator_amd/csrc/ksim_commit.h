@@ -21,16 +21,19 @@ __device__ __forceinline__ int64_t window_local(const DevCluster& c, int32_t s, 
 }
 
 // Validate the chain against M (pmax) and commit (one block of kBatchPods
-// threads).  Binds are applied by the shard that owns the node.  awin (ADAPT
-// batch, unsharded): per pod {scan start, cut offset or -1}; the evaluated
-// counts and nextStartNodeIndex follow the committed pods' windows.
-// g_own / m_own: this thread's gkey / pmax entries, loaded by the caller at
-// kernel start (before the state load they do not depend on).
+// threads).  Binds are applied by the shard that owns the node.  s_aw (ADAPT
+// batch): per pod {scan start, cut offset or -1} (the awin pairs), staged in
+// LDS by the caller from loads issued at kernel start, so neither the
+// evaluation count nor nextStartNodeIndex waits for a global load after the
+// cut is known; the evaluated counts and nextStartNodeIndex follow the
+// committed pods' windows.  g_own / m_own: this thread's gkey / pmax entries,
+// loaded by the caller at kernel start (before the state load they do not
+// depend on).
 __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
                                              uint64_t g_own, uint64_t m_own, const uint64_t* __restrict__ pmax,
                                              int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
                                              int32_t* s_sched, int32_t* s_unsched,
-                                             const int32_t* __restrict__ awin = nullptr) {
+                                             const int2* s_aw = nullptr) {
   __shared__ int32_t s_evals;
   const int tid = threadIdx.x;
   const int32_t base = st->cursor;
@@ -60,15 +63,15 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
       if (node == inode) assume_pod(c, P, P.pods[base + istar], local, 1);
     }
   }
-  if (awin && tid < committed) {
-    const int32_t cut = awin[2 * tid + 1];
-    atomicAdd(&s_evals, (int32_t)window_local(c, awin[2 * tid], cut >= 0 ? (int64_t)cut + 1 : c.n_total));
+  if (s_aw && tid < committed) {
+    const int2 w = s_aw[tid];
+    atomicAdd(&s_evals, (int32_t)window_local(c, w.x, w.y >= 0 ? (int64_t)w.y + 1 : c.n_total));
   }
   __syncthreads();
   if (tid == 0) {
-    if (awin && committed > 0) {
-      const int32_t cut = awin[2 * (committed - 1) + 1];
-      st->next_start = (int32_t)(((int64_t)awin[2 * (committed - 1)] + (cut >= 0 ? cut : c.n_total)) % c.n_total);
+    if (s_aw && committed > 0) {
+      const int2 w = s_aw[committed - 1];
+      st->next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
       st->evals += s_evals;
     } else {
       st->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);   // the nodes this handle evaluated

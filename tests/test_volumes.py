@@ -169,3 +169,29 @@ def test_volume_filters_engine_vs_oracle(pct):
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_volume_filters_sharded(world):
+    """Volume pods on the node-sharded per-pod cycle (in-process shard group)."""
+    from ksim.engine import Engine, group_schedule_loaded
+    from ksim.shard import partition
+    nodes, pods, pvs, pvcs = volume_scenario(seed=5, n_nodes=200, n_pods=500)
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods, volumes=VolumeIndex.from_nodes(nodes, pvs, pvcs))
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=0))
+    engines = []
+    for base, cnt in partition(cluster.n_nodes, world):
+        e = Engine(0)
+        e.set_shard(base, cluster.n_nodes)
+        e.set_profile(prof)
+        e.set_cluster(cluster.shard(base, cnt))
+        e.load_pods(enc)
+        engines.append(e)
+    chosen, st = group_schedule_loaded(engines, 0, enc.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(enc)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals
+    for e in engines:
+        e.close()

@@ -2490,7 +2490,10 @@ extern "C" int ksim_match_terms(ksim_handle* h, const ksim_match_problem* mp, ui
       if (q.pod_sig[p] < 0 || q.pod_sig[p] >= q.n_sigs || q.pod_node[p] < 0 || q.pod_node[p] >= q.n_nodes)
         return set_err(h, KSIM_E_INVALID, "bound pod signature / node out of range");
   }
-  if (q.n_sigs == 0) return KSIM_OK;
+  if (q.n_sigs == 0) {                         // no signature: no bound pod either (pod_sig < n_sigs)
+    if (q.n_classes > 0 && q.n_nodes > 0) std::memset(counts, 0, (size_t)q.n_classes * q.n_nodes * 4);
+    return KSIM_OK;
+  }
   HIPCHK(h, hipSetDevice(h->device));
   DevMatch m{};
   m.s = q.n_sigs;

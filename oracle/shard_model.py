@@ -16,6 +16,10 @@ csrc/ksim_batch.hip does between the two exchanges:
   commit    : up to the first pod whose exact choice is not its guess; the
               owner shard applies the binds (k_batch_commit)
 
+Replicated sharding (ksim_set_eval_range, ``eval_range``): the Shard holds
+every node, the top-T covers the rank's range only, the pair keys of every
+guess are local (no all-reduce) and every rank binds every placement.
+
 Batchable pods only (bare pods: Fit filter + LeastAllocated +
 BalancedAllocation vary over nodes, every normalized plugin is constant).
 Keys stay below 2^63 (totals < 2^19), so int64 tensors carry them.
@@ -107,13 +111,15 @@ def global_merge(lists, completes, T: int):
 
 
 def schedule(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed: int, const: int,
-             w_fit: int = 1, w_ba: int = 1, B: int = 16, T: int = 3):
-    """Run every pod through the sharded protocol; returns global placements."""
+             w_fit: int = 1, w_ba: int = 1, B: int = 16, T: int = 3, eval_range=None):
+    """Run every pod through the sharded protocol; returns global placements.
+    ``eval_range`` = (lo, hi): replicated sharding (the Shard is the whole
+    cluster, this rank's top-T covers rows [lo, hi))."""
     import torch
     P = pods.n_pods
     chosen = np.full(P, -1, np.int64)
     cursor, seq0 = 0, 0
-    rows = np.arange(shard.n)
+    rows = np.arange(shard.n) if eval_range is None else np.arange(*eval_range)
     while cursor < P:
         nb = min(B, P - cursor)
         # per shard: top-T per pod under the batch-start snapshot
@@ -151,9 +157,10 @@ def schedule(pods, shard: Shard, rank: int, world: int, dist, n_total: int, seed
                     v = shard.keys(pods.pods[cursor + j], np.array([row]), seed, seq0 + j, const, w_fit, w_ba,
                                    extra=pods.pods[cursor + k])[0]
                     pmax[j] = max(pmax[j], int(v))
-        t = torch.from_numpy(pmax)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        pmax = t.numpy()
+        if eval_range is None:                          # replicas: every guess is local
+            t = torch.from_numpy(pmax)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pmax = t.numpy()
         istar = next((j for j in range(nchain) if pmax[j] > gkey[j]), nchain)
         committed = istar + 1 if istar < nchain else nchain
         inode = NODE_MASK - (int(pmax[istar]) & NODE_MASK) if istar < nchain else -1

@@ -39,7 +39,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights):
+def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights, replicated=False):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
     sys.path[:0] = [root, os.path.join(root, "kube-scheduler-simulator_amd")]
@@ -56,9 +56,20 @@ def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights):
         w = {p.name: (p.weight or 1) for p in sp.score_plugins()}
         const = 100 * w["TaintToleration"] + 100 * w["PodTopologySpread"]
         base, cnt = partition(n_nodes, world)[rank]
-        shard = shard_model.Shard(cluster, base, cnt)
+        if replicated:                                   # whole cluster, this rank's evaluation range
+            shard = shard_model.Shard(cluster, 0, n_nodes)
+            rng = (base, base + cnt)
+        else:
+            shard = shard_model.Shard(cluster, base, cnt)
+            rng = None
         chosen = shard_model.schedule(pods, shard, rank, world, dist, n_nodes, sp.tiebreak_seed, const,
-                                      w["NodeResourcesFit"], w["NodeResourcesBalancedAllocation"], B=B, T=T)
+                                      w["NodeResourcesFit"], w["NodeResourcesBalancedAllocation"], B=B, T=T,
+                                      eval_range=rng)
+        if replicated:                                   # every replica holds the oracle's node state
+            from oracle.oracle import Oracle
+            ora = Oracle(cluster, profile.compile_profile(sp))
+            ora.schedule(pods)
+            np.testing.assert_array_equal(shard.req_cpu, ora.node_state()["req_cpu"])
         if rank == 0:
             from oracle.oracle import Oracle
             ochosen, _ = Oracle(cluster, profile.compile_profile(sp)).schedule(pods)
@@ -80,6 +91,13 @@ def _worker(rank, world, port, n_nodes, n_pods, seed, T, B, weights):
 ])
 def test_sharded_protocol_gloo(world, n_nodes, n_pods, T, B, weights):
     mp.spawn(_worker, args=(world, _free_port(), n_nodes, n_pods, 7, T, B, weights), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,n_nodes,n_pods,T,B", [(2, 60, 500, 3, 16), (3, 40, 400, 2, 24)])
+def test_replicated_protocol_gloo(world, n_nodes, n_pods, T, B):
+    """Replicated sharding (ksim_set_eval_range): one all-gather per batch, no
+    pair-key all-reduce, every replica ends with the oracle's node state."""
+    mp.spawn(_worker, args=(world, _free_port(), n_nodes, n_pods, 7, T, B, None, True), nprocs=world, join=True)
 
 
 def _worker_perpod(rank, world, port, n_nodes, n_pods, seed, pct):

@@ -111,3 +111,53 @@ def test_template_cluster_schedules_like_objref(pct):
     for i, pod in enumerate(snap.pending):
         got = ref.cycle(pod)["chosen"]
         assert (names[ochosen[i]] if ochosen[i] >= 0 else None) == got, f"pod {i}"
+
+
+def test_volume_documents_schedule_like_objref():
+    """A document whose PVs (the UI's pv.yaml template) carry node affinity and
+    zone labels: pods with claims bound to them are scheduled with
+    VolumeBinding / VolumeZone, and placements equal the object-level
+    restatement on the same PV / PVC objects; an unbound claim is reported."""
+    doc = _template_cluster(n_nodes=30, n_pods=60, bound_every=1000)
+    pv_t, pvc_t, pod_t = _doc("template_pv.json"), _doc("template_pvc.json"), _doc("template_pod.json")
+    pvs, pvcs = [], []
+    for k, (aff, zone) in enumerate([(None, "z1"), (["node-3", "node-4"], None), (None, "z0__z2"), (None, None)]):
+        pv = copy.deepcopy(pv_t)
+        pv["metadata"] = {"name": f"pv-{k}", "labels": ({"topology.kubernetes.io/zone": zone} if zone else {})}
+        pv["spec"].pop("claimRef", None)
+        if aff:
+            pv["spec"]["nodeAffinity"] = {"required": {"nodeSelectorTerms": [{"matchExpressions": [
+                {"key": "kubernetes.io/hostname", "operator": "In", "values": aff}]}]}}
+        pvs.append(pv)
+        pvc = copy.deepcopy(pvc_t)
+        pvc["metadata"] = {"name": f"claim-{k}", "namespace": "default"}
+        pvc["spec"]["volumeName"] = f"pv-{k}"
+        pvcs.append(pvc)
+    unbound = copy.deepcopy(pvc_t)
+    unbound["metadata"] = {"name": "claim-unbound", "namespace": "default"}
+    unbound["spec"].pop("volumeName", None)
+    pvcs.append(unbound)
+    for i in range(40):
+        p = copy.deepcopy(pod_t)
+        p["metadata"] = {"name": f"vol-{i}", "namespace": "default", "creationTimestamp": "2022-01-01T00:00:01Z"}
+        claim = "claim-unbound" if i == 7 else f"claim-{i % 4}"
+        p["spec"]["volumes"] = [{"name": "v", "persistentVolumeClaim": {"claimName": claim}}]
+        doc["pods"].append(p)
+    doc["pvs"], doc["pvcs"] = pvs, pvcs
+    snap = ingest.load(doc)
+    assert [u[1] for u in snap.unsupported] == ["with-pvc", "vol-7"]   # pvc1 is not in this document
+    cluster, enc, _ = ingest.encode(snap)
+    assert (enc.pods["vb_count"] > 0).sum() == 10 and (enc.pods["vz_count"] > 0).sum() == 20
+    sp = copy.deepcopy(snap.profiles[0][1])
+    sp.percentage_of_nodes_to_score = 100
+    prof = profile.compile_profile(sp, cluster.scalar_names)
+    ochosen, _ = Oracle(cluster, prof).schedule(enc)
+    ref = ObjScheduler(snap.nodes, snap.bound, namespaces=snap.namespaces, pct=100, seed=sp.tiebreak_seed,
+                       pvs=snap.volumes.pvs.values(), pvcs=snap.volumes.pvcs.values())
+    names = cluster.node_names
+    for i, pod in enumerate(snap.pending):
+        got = ref.cycle(pod)["chosen"]
+        assert (names[ochosen[i]] if ochosen[i] >= 0 else None) == got, f"pod {i} {pod.name}"
+    placed = {pod.name: names[ochosen[i]] for i, pod in enumerate(snap.pending) if pod.pvc_claims and ochosen[i] >= 0}
+    aff = [placed[f"vol-{i}"] for i in range(1, 40, 4) if f"vol-{i}" in placed]   # pv-1: node-3 / node-4 only
+    assert len(aff) >= 2 and set(aff) <= {"node-3", "node-4"}

@@ -141,8 +141,11 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
 // Eight word segments per step: their loads do not depend on the counts, so
 // they go out together (one memory round trip per 512 nodes scanned instead of
 // one per 64).
+#ifndef KSIM_WIN_AHEAD
+#define KSIM_WIN_AHEAD 8
+#endif
 __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_t n, int32_t k) {
-  constexpr int kAhead = 8;
+  constexpr int kAhead = KSIM_WIN_AHEAD;             // bitmap words per step (their loads are independent)
   int32_t need = k, off = 0, pos = s;
   while (off < n) {
     uint64_t bits[kAhead];

@@ -98,10 +98,13 @@ __global__ __launch_bounds__(256) void k_match_mfma(DevMatch m) {
   }
 }
 
-// Per signature: the classes whose matcher it satisfies, as bit words.
+// Per signature: the classes whose matcher it satisfies, as bit words (one
+// block per (signature, 256 classes), a 1-D grid: signatures may exceed the
+// 65,536 blocks of a grid's y dimension).
 __global__ __launch_bounds__(256) void k_match_classes(DevMatch m) {
-  const int32_t s = blockIdx.y;
-  const int32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t chunks = (m.c + 255) / 256;
+  const int32_t s = blockIdx.x / chunks;
+  const int32_t c = (blockIdx.x % chunks) * blockDim.x + threadIdx.x;
   const bool hit = c < m.c && ((m.bits[(size_t)s * m.w + (m.cls_matcher[c] >> 5)] >> (m.cls_matcher[c] & 31)) & 1);
   const uint64_t w = __ballot(hit);
   const int32_t lane = threadIdx.x & 63;
@@ -130,7 +133,7 @@ void launch_match(const DevMatch& m, hipStream_t stream) {
   k_match_scatter<<<(m.rp + 255) / 256, 256, 0, stream>>>(const_cast<int8_t*>(m.bt), m.r, m.fp, m.req_off, m.req_feat);
   k_match_mfma<<<m.sp / 16, 256, 0, stream>>>(m);
   if (m.c > 0 && m.s > 0) {
-    k_match_classes<<<dim3((m.c + 255) / 256, m.s), 256, 0, stream>>>(m);
+    k_match_classes<<<m.s * ((m.c + 255) / 256), 256, 0, stream>>>(m);
     if (m.p > 0) k_match_count<<<(m.p + 255) / 256, 256, 0, stream>>>(m);
   }
 }

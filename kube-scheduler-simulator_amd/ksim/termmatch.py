@@ -55,9 +55,13 @@ class MatchProblem:
             m_reqs.append(reqs)
         self.n_matchers = len(matchers)
         self.n_words = (self.n_matchers + 31) // 32
-        # signatures: (namespace, sorted label items) -> feature ids in the vocabulary
+        # signatures: (namespace, sorted label items) -> feature ids in the
+        # vocabulary; signatures with the same features (labels no requirement
+        # names differ) share one row of the contraction (sig_row)
+        rows: Dict[tuple, int] = {}
         sig_feats = []
-        for ns, labels in sigs:
+        self.sig_row = np.zeros(len(sigs), np.int32)
+        for i, (ns, labels) in enumerate(sigs):
             f = []
             x = self.feat.get(("ns", ns))
             if x is not None:
@@ -67,12 +71,17 @@ class MatchProblem:
                     x = self.feat.get(key)
                     if x is not None:
                         f.append(x)
-            sig_feats.append(f)
+            t = tuple(sorted(f))
+            r = rows.get(t)
+            if r is None:
+                r = rows[t] = len(sig_feats)
+                sig_feats.append(list(t))
+            self.sig_row[i] = r
         self.sig_off, self.sig_feat = _csr(sig_feats)
         self.req_off, self.req_feat = _csr(self.req_feats)
         self.neg = np.array(self.req_neg, np.uint8)
         self.m_off, self.m_req = _csr(m_reqs)
-        self.n_sigs = len(sigs)
+        self.n_sigs = len(sig_feats)                    # distinct feature sets (rows)
         self.pod_sig = np.zeros(0, np.int32)
         self.pod_node = np.zeros(0, np.int32)
         self.class_matcher = np.zeros(0, np.int32)
@@ -114,8 +123,9 @@ class MatchProblem:
         return out
 
     def set_counts(self, pod_sig: np.ndarray, pod_node: np.ndarray, n_nodes: int, class_matcher: Sequence[int]):
-        """Count classes to accumulate over bound pods (signature, node)."""
-        self.pod_sig = np.ascontiguousarray(pod_sig, np.int32)
+        """Count classes to accumulate over bound pods (signature index into
+        the constructor's ``sigs``, node)."""
+        self.pod_sig = np.ascontiguousarray(self.sig_row[np.asarray(pod_sig, np.int64)], np.int32)
         self.pod_node = np.ascontiguousarray(pod_node, np.int32)
         self.class_matcher = np.ascontiguousarray(class_matcher, np.int32)
         self.n_nodes = int(n_nodes)
@@ -147,6 +157,11 @@ def unpack_bits(words: np.ndarray, n: int) -> np.ndarray:
     return b[:, :n].astype(bool)
 
 
+def expand_rows(mp: MatchProblem, hit: np.ndarray) -> np.ndarray:
+    """[distinct feature sets][matchers] -> [constructor sigs][matchers]."""
+    return hit[mp.sig_row]
+
+
 class DeviceMatcher:
     """TopologyIndex.matcher backed by the engine (ksim_match_terms)."""
 
@@ -159,4 +174,4 @@ class DeviceMatcher:
         counts = np.zeros((mp.class_matcher.size, mp.n_nodes), np.int32) if mp.class_matcher.size else None
         bits = self.engine.match_terms(mp.struct(), mp.n_words, counts)
         self.calls += 1
-        return unpack_bits(bits, mp.n_matchers), counts
+        return expand_rows(mp, unpack_bits(bits, mp.n_matchers)), counts

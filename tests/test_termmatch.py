@@ -15,7 +15,7 @@ from ksim import gen
 from ksim.encode import encode_cluster, encode_pods
 from ksim.model import (Container, LabelSelector, Node, Pod, PodAffinityTerm, Requirement,
                         TopologySpreadConstraint, WeightedPodAffinityTerm)
-from ksim.termmatch import MatchProblem, unpack_bits
+from ksim.termmatch import MatchProblem, expand_rows, unpack_bits
 
 
 class NumpyMatcher:
@@ -41,7 +41,7 @@ class NumpyMatcher:
         counts = np.zeros((mp.class_matcher.size, mp.n_nodes), np.int32)
         for c, m in enumerate(mp.class_matcher):
             np.add.at(counts[c], mp.pod_node[hit[mp.pod_sig, m]], 1)
-        return hit, counts
+        return expand_rows(mp, hit), counts
 
 
 def encode_both(nodes, bound, pods, matcher, namespaces=None):
@@ -205,3 +205,48 @@ def test_device_match_many_requirements(engine):
             for j in range(600)]
     host, dev = encode_both(nodes, bound, pods, DeviceMatcher(engine))
     assert_same(host, dev)
+
+
+def _exists_problem(n_sigs, n_keys=17, seed=0):
+    """Signatures labelled with the keys of the bits of their index (distinct
+    feature sets), matchers Exists(a) AND DoesNotExist(b) over key pairs."""
+    from ksim.topology import Matcher
+    rng = np.random.default_rng(seed)
+    keys = [f"k{i}" for i in range(n_keys)]
+    sigs = [("default", tuple(sorted((keys[b], "v") for b in range(n_keys) if (s >> b) & 1))) for s in range(n_sigs)]
+    ms = []
+    for a in range(n_keys):
+        b = (a * 5 + 3) % n_keys
+        sel = LabelSelector(match_expressions=[Requirement(keys[a], "Exists", []), Requirement(keys[b], "DoesNotExist", [])])
+        ms.append(Matcher(frozenset(["default"]), False, sel.key()))
+    mp = MatchProblem(None, ms, sigs)
+    n_pods, n_nodes = 4 * n_sigs, 50
+    mp.set_counts(rng.integers(0, n_sigs, n_pods), rng.integers(0, n_nodes, n_pods), n_nodes, np.arange(len(ms)))
+    return mp, sigs, ms
+
+
+def test_signatures_with_equal_features_share_a_row():
+    """Labels no requirement names do not split a signature's row."""
+    from ksim.topology import Matcher
+    sel = LabelSelector({"app": "a"})
+    ms = [Matcher(frozenset(["default"]), False, sel.key())]
+    sigs = [("default", (("app", "a"), ("pod", f"x{i}"))) for i in range(100)] + [("default", (("app", "b"),))]
+    mp = MatchProblem(None, ms, sigs)
+    assert mp.n_sigs == 2 and list(mp.sig_row[:3]) == [0, 0, 0] and mp.sig_row[100] == 1
+    mp.set_counts(np.arange(101), np.zeros(101, np.int64), 1, [0])
+    hit, counts = NumpyMatcher().match(mp)
+    assert hit.shape == (101, 1) and hit[:100, 0].all() and not hit[100, 0]
+    assert counts.tolist() == [[100]]
+
+
+@pytest.mark.gpu
+def test_device_match_more_rows_than_grid_y(engine):
+    """70,000 distinct signature rows (more than the 65,536 blocks of a grid's
+    y dimension) and 280,000 bound pods: bits and class counts vs numpy."""
+    from ksim.termmatch import DeviceMatcher
+    mp, _, _ = _exists_problem(70000)
+    assert mp.n_sigs == 70000
+    hd, cd = DeviceMatcher(engine).match(mp)
+    hn, cn = NumpyMatcher().match(mp)
+    np.testing.assert_array_equal(hd, hn)
+    np.testing.assert_array_equal(cd, cn)

@@ -476,18 +476,27 @@ constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linea
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
 
-__global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __restrict__ st,
-                                                            int32_t n_nodes /* global */,
-                                                            const uint64_t* __restrict__ topk,
-                                                            const int32_t* __restrict__ topk_cnt,
-                                                            const int32_t* __restrict__ topk_complete,
-                                                            uint64_t* __restrict__ gkey,
-                                                            int32_t* __restrict__ chain_end,
-                                                            unsigned long long* __restrict__ dbg) {
-  __shared__ int32_t s_key[kHashSlots];        // node id in the slot, -1 = empty
-  __shared__ int32_t s_hold[kHashSlots];       // lowest pod index holding the slot this round
-  __shared__ int16_t s_rep[kBatchPods][kTopT]; // slot of each list entry
-  __shared__ int32_t s_first, s_cut;
+struct ChainLds {
+  int32_t key[kHashSlots];                     // node id in the slot, -1 = empty
+  int32_t hold[kHashSlots];                    // lowest pod index holding the slot this round
+  int16_t rep[kBatchPods][kTopT];              // slot of each list entry
+  int32_t first, cut;
+};
+
+// The chain of one batch in one block of kBatchPods threads (thread i = pod
+// i).  Returns false when the batch is empty (block-uniform); else *gk = pod
+// i's guessed key (0: none, or i past the exact prefix) and *nchain = the
+// prefix length.  A pure function of the lists: every block that runs it gets
+// the same guesses.
+__device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restrict__ st,
+                                            const uint64_t* __restrict__ topk,
+                                            const int32_t* __restrict__ topk_cnt,
+                                            const int32_t* __restrict__ topk_complete, uint64_t* gk,
+                                            int32_t* nchain_out, unsigned long long* __restrict__ dbg) {
+  int32_t* const s_key = L.key;
+  int32_t* const s_hold = L.hold;
+  int32_t& s_first = L.first;
+  int32_t& s_cut = L.cut;
   // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int i = threadIdx.x;                   // one pod per thread
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   const int complete0 = topk_complete[i];
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
-  if (nb <= 0) return;
+  if (nb <= 0) return false;
   for (int x = i; x < kHashSlots; x += kBatchPods) {
     s_key[x] = -1;
     s_hold[x] = kBatchPods;
@@ -521,13 +530,13 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
       }
       slot = (int16_t)h;
     }
-    s_rep[i][e] = slot;
+    L.rep[i][e] = slot;
   }
   __syncthreads();
   // this pod's slots in registers (selects below, never a dynamic index)
   int32_t rep[kTopT];
 #pragma unroll
-  for (int e = 0; e < kTopT; e++) rep[e] = s_rep[i][e];
+  for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
   int first = kBatchPods, rounds = 0;
@@ -564,8 +573,8 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   uint64_t ga = 0;
 #pragma unroll
   for (int e = 0; e < kTopT; e++) ga = e == a ? lst[e] : ga;   // register select, no dynamic index
-  if (i < nb) gkey[i] = (i < nchain && a >= 0) ? ga : 0;
-  if (i == 0) *chain_end = nchain;
+  *gk = (i < nchain && a >= 0) ? ga : 0;
+  *nchain_out = nchain;
   if (i == 0 && dbg) {
     const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
     atomicAdd(&dbg[0], (unsigned long long)(t1 - t0));
@@ -574,30 +583,34 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
     atomicAdd(&dbg[3], 1ull);
     atomicAdd(&dbg[4], (unsigned long long)(rounds + 1));
   }
+  return true;
 }
 
-// Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
-// bound there; M_j = the block max.  Sharded, each shard scores the guesses
-// it owns and M is all-reduced (max) before k_batch_commit.  FAST: as in
-// k_batch_eval (trivial pods, cpu/memory scoring).
+__global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __restrict__ st,
+                                                            int32_t n_nodes /* global */,
+                                                            const uint64_t* __restrict__ topk,
+                                                            const int32_t* __restrict__ topk_cnt,
+                                                            const int32_t* __restrict__ topk_complete,
+                                                            uint64_t* __restrict__ gkey,
+                                                            int32_t* __restrict__ chain_end,
+                                                            unsigned long long* __restrict__ dbg) {
+  __shared__ ChainLds L;
+  uint64_t gk;
+  int32_t nchain;
+  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbg)) return;
+  const int32_t nb = min(kBatchPods, st->end - st->cursor);
+  if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
+  if (threadIdx.x == 0) *chain_end = nchain;
+}
+
+// Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
 template <bool FAST>
-__global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P,
-                                                            const ksim_profile* __restrict__ prof_p,
-                                                            const BatchProg* __restrict__ bp_p,
-                                                            const DevState* __restrict__ st,
-                                                            const uint64_t* __restrict__ gkey,
-                                                            const int32_t* __restrict__ chain_end,
-                                                            uint64_t* __restrict__ pmax) {
-  const ksim_profile& prof = *prof_p;
-  const BatchProg& bp = *bp_p;
-  __shared__ uint64_t s_wmax[kBatchPods / 64];
+__device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                            const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
+                                            int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
-  const uint64_t gk = gkey[k];                       // in flight with the state loads
-  const int32_t nchain = *chain_end;
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
-  if (nb <= 0) return;
   const int64_t seq0 = st->pod_seq;
   if (j >= nchain) {                                 // block-uniform
     if (tid == 0) pmax[j] = 0;
@@ -629,6 +642,54 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
     for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
     pmax[j] = m;
   }
+}
+
+// Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
+// bound there; M_j = the block max.  Sharded, each shard scores the guesses
+// it owns and M is all-reduced (max) before k_batch_commit.  FAST: as in
+// k_batch_eval (trivial pods, cpu/memory scoring).
+template <bool FAST>
+__global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P,
+                                                            const ksim_profile* __restrict__ prof_p,
+                                                            const BatchProg* __restrict__ bp_p,
+                                                            const DevState* __restrict__ st,
+                                                            const uint64_t* __restrict__ gkey,
+                                                            const int32_t* __restrict__ chain_end,
+                                                            uint64_t* __restrict__ pmax) {
+  __shared__ uint64_t s_wmax[kBatchPods / 64];
+  const uint64_t gk = gkey[threadIdx.x];             // in flight with the state loads
+  const int32_t nchain = *chain_end;
+  const int32_t nb = min(kBatchPods, st->end - st->cursor);
+  if (nb <= 0) return;
+  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax);
+}
+
+// The chain and the pair keys in one launch: every block of the pairs grid
+// runs the (deterministic) chain itself, thread k ending with pod k's guess in
+// a register, so the pairs need no chain launch and no gkey round trip.
+// Block 0 also stores the guesses and the prefix length for k_batch_commit.
+template <bool FAST>
+__global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
+                                                                  const ksim_profile* __restrict__ prof_p,
+                                                                  const BatchProg* __restrict__ bp_p,
+                                                                  const DevState* __restrict__ st,
+                                                                  const uint64_t* __restrict__ topk,
+                                                                  const int32_t* __restrict__ topk_cnt,
+                                                                  const int32_t* __restrict__ topk_complete,
+                                                                  uint64_t* __restrict__ gkey,
+                                                                  int32_t* __restrict__ chain_end,
+                                                                  uint64_t* __restrict__ pmax) {
+  __shared__ ChainLds L;
+  __shared__ uint64_t s_wmax[kBatchPods / 64];
+  uint64_t gk;
+  int32_t nchain;
+  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
+  if (blockIdx.x == 0) {
+    const int32_t nb = min(kBatchPods, st->end - st->cursor);
+    if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
+    if (threadIdx.x == 0) *chain_end = nchain;
+  }
+  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax);
 }
 
 __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
@@ -668,6 +729,13 @@ static bool tile_eval() {
   return on;
 }
 
+// A/B switch (read once per process): KSIM_CHAIN_SEPARATE=1 launches the chain
+// as its own one-block kernel ahead of the pairs (the round-2 form).
+static bool chain_fused() {
+  static const bool separate = getenv("KSIM_CHAIN_SEPARATE") != nullptr;
+  return !separate;
+}
+
 // Evaluation and per-pod top-T (xsend: the sharded record, else null).
 static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream, hipEvent_t* mid = nullptr) {
   if (tile_eval() && a.c.eval_lo == 0 && a.c.eval_hi == a.c.n) {   // the tile form evaluates every node
@@ -699,6 +767,22 @@ uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) 
   if (evs) (void)hipEventRecord(evs[0], stream);
   launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
   if (evs) (void)hipEventRecord(evs[2], stream);
+  if (chain_fused() && !chain_clock(a)) {
+    // the chain inside every pairs block (k_batch_chain_pairs), timed in the pairs slot
+    if (evs) (void)hipEventRecord(evs[3], stream);
+    if (a.fast)
+      k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                       a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                                                       a.s.chain_end, a.s.pmax);
+    else
+      k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                        a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                                                        a.s.chain_end, a.s.pmax);
+    if (evs) (void)hipEventRecord(evs[4], stream);
+    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+    if (evs) (void)hipEventRecord(evs[5], stream);
+    return tile_eval() ? 0x1bu : 0x19u;
+  }
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, chain_clock(a));
   if (evs) (void)hipEventRecord(evs[3], stream);

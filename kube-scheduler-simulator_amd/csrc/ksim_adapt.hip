@@ -37,6 +37,7 @@
 #include "ksim_internal.h"
 #include "ksim_wave.h"
 #include "ksim_commit.h"
+#include "ksim_chain.h"
 
 namespace ksim {
 
@@ -397,15 +398,21 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
 
 // SH: windows and bitmaps are global; a shard scores only the guesses on its
 // own nodes; pmax[kBatchPods + j] carries the broken flag (all-reduced with M).
-template <bool SH>
+// CHAIN: every block runs the chain itself from the top-T lists (as
+// k_batch_chain_pairs on the P100 path); block 0 stores gkey / chain_end for
+// the commit.  Otherwise the guesses come from k_batch_chain.
+template <bool SH, bool CHAIN>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P,
                                                             const ksim_profile* __restrict__ prof_p,
                                                             const BatchProg* __restrict__ bp_p,
                                                             const DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ amask, int32_t n_words,
                                                             const int32_t* __restrict__ awin,
-                                                            const uint64_t* __restrict__ gkey,
-                                                            const int32_t* __restrict__ chain_end,
+                                                            const uint64_t* __restrict__ topk,
+                                                            const int32_t* __restrict__ topk_cnt,
+                                                            const int32_t* __restrict__ topk_complete,
+                                                            uint64_t* __restrict__ gkey,
+                                                            int32_t* __restrict__ chain_end,
                                                             uint64_t* __restrict__ pmax,
                                                             int32_t* __restrict__ abroken) {
   const ksim_profile& prof = *prof_p;
@@ -415,12 +422,23 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return;
-  const int32_t nchain = *chain_end;
   const int j = blockIdx.x, k = tid;
+  int32_t nchain;
+  uint64_t gk;
+  if constexpr (CHAIN) {
+    __shared__ ChainLds L;
+    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
+    if (j == 0) {
+      if (k < nb) gkey[k] = gk;
+      if (k == 0) *chain_end = nchain;
+    }
+  } else {
+    nchain = *chain_end;
+    gk = gkey[k];
+  }
   uint64_t v = 0;
   bool brk = false;
   if (j < nchain && k < j) {
-    const uint64_t gk = gkey[k];
     const int32_t node = gk ? key_node(gk) - c.base : -1;
     if (node >= 0 && node < c.n) {
       const int32_t g = node + c.base;              // global position (== node unsharded)
@@ -478,7 +496,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",
                                                          "k_batch_chain", "k_adapt_pairs", "k_adapt_commit"};
 
-void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
+uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const int32_t n_words = (a.c.n + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
   if (evs) (void)hipEventRecord(evs[0], stream);
@@ -499,14 +517,23 @@ void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs
   }
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
-  launch_chain(a, stream);
-  if (evs) (void)hipEventRecord(evs[4], stream);
-  k_adapt_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words,
-                                                              a.s.awin, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
+  if (chain_fused()) {                               // the chain inside the pairs launch, timed in its slot
+    if (evs) (void)hipEventRecord(evs[4], stream);
+    k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+        a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
+  } else {
+    launch_chain(a, stream);
+    if (evs) (void)hipEventRecord(evs[4], stream);
+    k_adapt_pairs<false, false><<<kBatchPods, kBatchPods, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, nullptr, nullptr, nullptr, a.s.gkey,
+        a.s.chain_end, a.s.pmax, a.s.abroken);
+  }
   if (evs) (void)hipEventRecord(evs[5], stream);
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,
                                                a.s.awin, a.chosen);
   if (evs) (void)hipEventRecord(evs[6], stream);
+  return chain_fused() ? 0x37u : 0x3fu;         // fused: the chain slot is an empty event pair
 }
 
 // ---- node-sharded ADAPT batch -----------------------------------
@@ -557,9 +584,17 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
 void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream) {
   const int32_t nw = (a.c.n_total + 63) / 64;
   k_batch_gmerge_launch(a, world, stream);
-  launch_chain(a, stream);
-  k_adapt_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
-                                                             a.s.gkey, a.s.chain_end, a.s.pmax, nullptr);
+  if (chain_fused()) {
+    k_adapt_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw,
+                                                                     a.s.awin, a.s.topk, a.s.topk_cnt,
+                                                                     a.s.topk_complete, a.s.gkey, a.s.chain_end,
+                                                                     a.s.pmax, nullptr);
+  } else {
+    launch_chain(a, stream);
+    k_adapt_pairs<true, false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw,
+                                                                      a.s.awin, nullptr, nullptr, nullptr, a.s.gkey,
+                                                                      a.s.chain_end, a.s.pmax, nullptr);
+  }
 }
 
 void launch_adapt_sh_commit(const LaunchArgs& a, hipStream_t stream) {

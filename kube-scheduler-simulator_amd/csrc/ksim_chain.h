@@ -1,0 +1,124 @@
+// ksim_chain.h — the batch paths' greedy chain (k_batch_chain, and inside the
+// fused chain + pairs launches of the P100 and ADAPT batches).
+#pragma once
+#include "ksim_device.h"
+#include "ksim_internal.h"
+
+namespace ksim {
+
+constexpr int kHashBits = kBatchPods * kTopT <= 2048 ? 12 : kBatchPods * kTopT <= 4096 ? 13 : 14;
+constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
+constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
+static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
+
+struct ChainLds {
+  int32_t key[kHashSlots];                     // node id in the slot, -1 = empty
+  int32_t hold[kHashSlots];                    // lowest pod index holding the slot this round
+  int16_t rep[kBatchPods][kTopT];              // slot of each list entry
+  int32_t first, cut;
+};
+
+// The chain of one batch in one block of kBatchPods threads (thread i = pod
+// i).  Returns false when the batch is empty (block-uniform); else *gk = pod
+// i's guessed key (0: none, or i past the exact prefix) and *nchain = the
+// prefix length.  A pure function of the lists: every block that runs it gets
+// the same guesses.
+__device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restrict__ st,
+                                            const uint64_t* __restrict__ topk,
+                                            const int32_t* __restrict__ topk_cnt,
+                                            const int32_t* __restrict__ topk_complete, uint64_t* gk,
+                                            int32_t* nchain_out, unsigned long long* __restrict__ dbg) {
+  int32_t* const s_key = L.key;
+  int32_t* const s_hold = L.hold;
+  int32_t& s_first = L.first;
+  int32_t& s_cut = L.cut;
+  // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int i = threadIdx.x;                   // one pod per thread
+  // the pod's list, count and state in flight together (independent loads;
+  // the buffers hold kBatchPods entries, so no bound check is needed yet)
+  uint64_t lst[kTopT];
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
+  const int cnt0 = topk_cnt[i];
+  const int complete0 = topk_complete[i];
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  if (nb <= 0) return false;
+  for (int x = i; x < kHashSlots; x += kBatchPods) {
+    s_key[x] = -1;
+    s_hold[x] = kBatchPods;
+  }
+  const int cnt = i < nb ? cnt0 : 0;
+  const bool incomplete = i < nb && !complete0;
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) {
+    int16_t slot = -1;
+    if (e < cnt) {
+      const int32_t node = key_node(lst[e]);
+      uint32_t h = ((uint32_t)node * 2654435761u) >> (32 - kHashBits);
+      while (true) {
+        const int32_t prev = atomicCAS(&s_key[h], -1, node);
+        if (prev == -1 || prev == node) break;
+        h = (h + 1) & (kHashSlots - 1);
+      }
+      slot = (int16_t)h;
+    }
+    L.rep[i][e] = slot;
+  }
+  __syncthreads();
+  // this pod's slots in registers (selects below, never a dynamic index)
+  int32_t rep[kTopT];
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
+  int first = kBatchPods, rounds = 0;
+  for (; rounds < kChainRounds; rounds++) {
+    if (i == 0) s_first = kBatchPods;
+    int32_t ra = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
+    if (a >= 0) atomicMin(&s_hold[ra], i);
+    __syncthreads();
+    // every entry's holder at once, then the first one not held by an earlier pod
+    int32_t held[kTopT];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) held[e] = e < cnt ? s_hold[rep[e]] : 0;
+    int na = -1;
+#pragma unroll
+    for (int e = kTopT - 1; e >= 0; e--)
+      if (e < cnt && held[e] >= i) na = e;
+    __syncthreads();
+    if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
+    if (na != a) atomicMin(&s_first, i);
+    a = na;
+    __syncthreads();
+    first = s_first;
+    if (first == kBatchPods) break;            // a fixpoint: every pod exact
+  }
+  // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
+  if (i == 0) s_cut = first < nb ? first : nb;
+  __syncthreads();
+  if (i < first && i < nb && a < 0 && incomplete) atomicMin(&s_cut, i);
+  __syncthreads();
+  const int32_t nchain = s_cut;
+  const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+  uint64_t ga = 0;
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) ga = e == a ? lst[e] : ga;   // register select, no dynamic index
+  *gk = (i < nchain && a >= 0) ? ga : 0;
+  *nchain_out = nchain;
+  if (i == 0 && dbg) {
+    const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&dbg[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&dbg[1], (unsigned long long)(t2 - t1));
+    atomicAdd(&dbg[2], (unsigned long long)(t3 - t2));
+    atomicAdd(&dbg[3], 1ull);
+    atomicAdd(&dbg[4], (unsigned long long)(rounds + 1));
+  }
+  return true;
+}
+
+}  // namespace ksim

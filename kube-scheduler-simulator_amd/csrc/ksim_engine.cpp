@@ -2297,7 +2297,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
       if (batch) HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
       for (int32_t i = 0; i < iters; i++) {
         if (adapt)
-          launch_batch_adapt(a, h->stream, &evs[(size_t)i * (per + 1)]);
+          launched = launch_batch_adapt(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else if (batch)
           launched = launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else

@@ -65,9 +65,10 @@ extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 // Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
+bool chain_fused();   // KSIM_CHAIN_SEPARATE unset: the chain runs inside the pairs launch
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
-void launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // Compat cycle around the host's extender round trip (ksim_eval_pod_filter / _finish):
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.

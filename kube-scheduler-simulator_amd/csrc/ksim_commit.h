@@ -20,6 +20,12 @@ __device__ __forceinline__ int64_t window_local(const DevCluster& c, int32_t s, 
   return ov(s, N) + ov(0, s + len - N);
 }
 
+// The resource columns of one node row and one pod's requests on them.
+struct ResCols {
+  int64_t cpu, mem, eph, nzc, nzm;
+  int32_t pods;
+};
+
 // Validate the chain against M (pmax) and commit (one block of kBatchPods
 // threads).  Binds are applied by the shard that owns the node.  s_aw (ADAPT
 // batch): per pod {scan start, cut offset or -1} (the awin pairs), staged in
@@ -35,10 +41,27 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
                                              int32_t* s_sched, int32_t* s_unsched,
                                              const int2* s_aw = nullptr) {
   __shared__ int32_t s_evals;
+  __shared__ uint64_t s_m[kBatchPods];
+  __shared__ ResCols s_req[kBatchPods];
   const int tid = threadIdx.x;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   const int64_t seq0 = st->pod_seq;
+  const uint64_t gj = tid < nchain ? g_own : 0;
+  const uint64_t mj = tid < nchain ? m_own : 0;
+  // ahead of the cut: the row of the node this pod guessed (it binds there if
+  // committed; bound nodes are distinct, so this thread is its only writer)
+  // and the pod's requests (in LDS: pod i* may bind on another pod's node)
+  const int32_t glocal = gj ? key_node(gj) - c.base : -1;
+  const bool gown = glocal >= 0 && glocal < c.n;
+  ResCols row{0, 0, 0, 0, 0, 0};
+  if (gown) row = ResCols{c.req_cpu[glocal], c.req_mem[glocal], c.req_eph[glocal], c.nz_cpu[glocal], c.nz_mem[glocal],
+                          c.num_pods[glocal]};
+  if (tid < nchain) {
+    const ksim_pod& p = P.pods[base + tid];
+    s_req[tid] = ResCols{p.req_cpu, p.req_mem, p.req_eph, p.nz_cpu, p.nz_mem, 1};
+  }
+  s_m[tid] = mj;
   if (tid == 0) {
     *s_istar = nchain;
     *s_sched = 0;
@@ -46,21 +69,36 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     s_evals = 0;
   }
   __syncthreads();
-  const uint64_t gj = tid < nchain ? g_own : 0;
-  const uint64_t mj = tid < nchain ? m_own : 0;
   if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
   __syncthreads();
   const int32_t istar = *s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
-  const int32_t inode = istar < nchain ? key_node(__builtin_nontemporal_load(&pmax[istar])) : -1;
+  const int32_t inode = istar < nchain ? key_node(s_m[istar]) : -1;
   if (tid < committed) {
     const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);     // global position
     if (chosen_out) chosen_out[base + tid] = node;
     atomicAdd(node >= 0 ? s_sched : s_unsched, 1);
-    const int32_t local = node - c.base;
-    if (tid < istar && gj && local >= 0 && local < c.n) {   // bound nodes are distinct: one writer each
-      assume_pod(c, P, P.pods[base + tid], local, 1);
-      if (node == inode) assume_pod(c, P, P.pods[base + istar], local, 1);
+    if (tid < istar && gown) {
+      auto add = [&](const ResCols& q) {
+        row.cpu += q.cpu;
+        row.mem += q.mem;
+        row.eph += q.eph;
+        row.nzc += q.nzc;
+        row.nzm += q.nzm;
+        row.pods += q.pods;
+      };
+      add(s_req[tid]);
+      assume_pod_rest(c, P, P.pods[base + tid], glocal, 1);
+      if (node == inode) {
+        add(s_req[istar]);
+        assume_pod_rest(c, P, P.pods[base + istar], glocal, 1);
+      }
+      c.req_cpu[glocal] = row.cpu;
+      c.req_mem[glocal] = row.mem;
+      c.req_eph[glocal] = row.eph;
+      c.nz_cpu[glocal] = row.nzc;
+      c.nz_mem[glocal] = row.nzm;
+      c.num_pods[glocal] = row.pods;
     }
   }
   if (s_aw && tid < committed) {

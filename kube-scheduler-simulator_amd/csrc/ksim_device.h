@@ -1576,6 +1576,15 @@ __device__ __forceinline__ void assume_pod(const DevCluster& c, const DevPods& P
   if (p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
 }
 
+// assume_pod without the six resource columns (the batch commit updates those
+// from a row it loaded ahead): class adds, scalar resources, bandwidth.
+__device__ __forceinline__ void assume_pod_rest(const DevCluster& c, const DevPods& P, const ksim_pod& p, int32_t node,
+                                                int sign) {
+  apply_adds(c, P, p, node, sign);
+  for (int k = 0; k < c.n_scalar; k++) c.req_scalar[(size_t)k * c.n + node] += sign * p.scalar_req[k];
+  if (p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
+}
+
 // Returnless 64-bit atomic add (two's complement: wraps as the plain add does).
 __device__ __forceinline__ void atomic_add_i64(int64_t* x, int64_t v) {
   atomicAdd(reinterpret_cast<unsigned long long*>(x), (unsigned long long)v);

@@ -489,11 +489,27 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   if (threadIdx.x == 0) *chain_end = nchain;
 }
 
+// The request fields the FAST pair key reads (pod j's and the bound pod k's),
+// as a local ksim_pod: a caller can load them before it knows the guesses.
+__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
+  ksim_pod p;
+  p.req_cpu = g.req_cpu;
+  p.req_mem = g.req_mem;
+  p.req_eph = g.req_eph;
+  p.nz_cpu = g.nz_cpu;
+  p.nz_mem = g.nz_mem;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) p.scalar_req[k] = 0;   // trivial pods: no scalar requests
+  return p;
+}
+
 // Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
+// FAST with pj / pk: pod j's and pod k's fields loaded by the caller.
 template <bool FAST>
 __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                             const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
-                                            int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax) {
+                                            int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax,
+                                            const ksim_pod* pj = nullptr, const ksim_pod* pk = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
   const int32_t base = st->cursor;
@@ -509,9 +525,9 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
       const ksim_pod& p = P.pods[base + j];
       if constexpr (FAST) {
         NodeRow r = load_res_row(c, local);
-        row_add_pod(r, P.pods[base + k], 1);
-        v = dyn_key_fast(bp, p, r, c.inv_cpu[local], c.inv_mem[local], prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20),
-                         c.base + local);
+        row_add_pod(r, pk ? *pk : P.pods[base + k], 1);
+        v = dyn_key_fast(bp, pj ? *pj : p, r, c.inv_cpu[local], c.inv_mem[local],
+                         prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
       } else {
         NodeRow r = load_row(c, local);
         row_add_pod(r, P.pods[base + k], 1);
@@ -567,6 +583,14 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
                                                                   uint64_t* __restrict__ pmax) {
   __shared__ ChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
+  // FAST: pod j's and pod k's request fields in flight during the chain
+  ksim_pod pj, pk;
+  if constexpr (FAST) {
+    const int32_t base = st->cursor, nb = min(kBatchPods, st->end - base);
+    const int32_t j = blockIdx.x, k = threadIdx.x;
+    if (j < nb) pj = fast_pod_fields(P.pods[base + j]);
+    if (k < nb) pk = fast_pod_fields(P.pods[base + k]);
+  }
   uint64_t gk;
   int32_t nchain;
   if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
@@ -575,7 +599,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
     if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
     if (threadIdx.x == 0) *chain_end = nchain;
   }
-  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax);
+  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr, FAST ? &pk : nullptr);
 }
 
 __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,

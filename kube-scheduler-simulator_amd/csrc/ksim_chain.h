@@ -15,7 +15,7 @@ struct ChainLds {
   int32_t key[kHashSlots];                     // node id in the slot, -1 = empty
   int32_t hold[kHashSlots];                    // lowest pod index holding the slot this round
   int16_t rep[kBatchPods][kTopT];              // slot of each list entry
-  int32_t first, cut;
+  int32_t first[2], cut;                      // first: one slot per round parity (see the round loop)
 };
 
 // The chain of one batch in one block of kBatchPods threads (thread i = pod
@@ -30,7 +30,6 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
                                             int32_t* nchain_out, unsigned long long* __restrict__ dbg) {
   int32_t* const s_key = L.key;
   int32_t* const s_hold = L.hold;
-  int32_t& s_first = L.first;
   int32_t& s_cut = L.cut;
   // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -49,6 +48,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
     s_key[x] = -1;
     s_hold[x] = kBatchPods;
   }
+  if (i < 2) L.first[i] = kBatchPods;
   const int cnt = i < nb ? cnt0 : 0;
   const bool incomplete = i < nb && !complete0;
   __syncthreads();
@@ -76,12 +76,17 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
   int first = kBatchPods, rounds = 0;
   for (; rounds < kChainRounds; rounds++) {
-    if (i == 0) s_first = kBatchPods;
+    // round r reports in first[r & 1].  The other slot was read at the end of
+    // round r - 1, by every thread before the first barrier below, so it is
+    // reset after that barrier (resetting the current slot at the top of the
+    // round raced with slower waves still reading the previous round's flag).
+    const int par = rounds & 1;
     int32_t ra = 0;
 #pragma unroll
     for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
     if (a >= 0) atomicMin(&s_hold[ra], i);
     __syncthreads();
+    if (i == 0) L.first[par ^ 1] = kBatchPods;
     // every entry's holder at once, then the first one not held by an earlier pod
     int32_t held[kTopT];
 #pragma unroll
@@ -92,10 +97,10 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
       if (e < cnt && held[e] >= i) na = e;
     __syncthreads();
     if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
-    if (na != a) atomicMin(&s_first, i);
+    if (na != a) atomicMin(&L.first[par], i);
     a = na;
     __syncthreads();
-    first = s_first;
+    first = L.first[par];
     if (first == kBatchPods) break;            // a fixpoint: every pod exact
   }
   // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain

@@ -184,18 +184,19 @@ __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_
 constexpr int kWindowRounds = 48;
 constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length   // exact prefix kept if not converged by then
 
-// awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
-// feasible node kept and all N processed); *aexact = pods with exact windows.
-__global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
-                                                             const uint64_t* __restrict__ amask, int32_t n_words,
-                                                             int32_t n, int32_t k, int32_t* __restrict__ awin,
-                                                             int32_t* __restrict__ aexact) {
+// The windows of one batch in one block of kBatchPods threads (thread j = pod
+// j): *s_out = pod j's scan start, *cut_out = its cut offset (-1: no cut),
+// *exact_out = pods with exact windows.  false: the batch is empty
+// (block-uniform).  A pure function of the bitmaps and the state.
+__device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
+                                             int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
+                                             int32_t* cut_out, int32_t* exact_out) {
   __shared__ int64_t sh[kBatchPods / 64];
   __shared__ int32_t s_first;
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
-  if (nb <= 0) return;
+  if (nb <= 0) return false;
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
@@ -226,12 +227,31 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
     exact = f;                                       // pods < f: start and cut exact
     if (j >= f) s = ns;                              // pods <= f now hold exact starts
   }
-  if (j < nb) {
+  *s_out = s;
+  *cut_out = cut;
+  *exact_out = exact;
+  return true;
+}
+
+// awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
+// feasible node kept and all N processed); *aexact = pods with exact windows.
+__global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
+                                                             const uint64_t* __restrict__ amask, int32_t n_words,
+                                                             int32_t n, int32_t k, int32_t* __restrict__ awin,
+                                                             int32_t* __restrict__ aexact) {
+  int32_t s, cut, exact;
+  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact)) return;
+  const int j = threadIdx.x;
+  if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
     awin[2 * j + 1] = cut;
   }
   if (j == 0) *aexact = exact;
 }
+
+// Clusters up to this many bitmap words run the window scan inside k_adapt_top
+// (every block scans all B bitmaps: B x W words from L2 per block).
+constexpr int32_t kWinFusedWords = 256;
 
 // One block (4 waves) per pod: the kept nodes' TB keys -> the pod's top-T
 // (complete when it lists every kept node).  Each wave keeps its lanes' best T
@@ -244,13 +264,16 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
 // ksim_batch.hip).
 // NT threads per block: 256, or 1024 for long windows (K >= kTopWideK), so
 // the block's waves fill their SIMDs (every CU holds one pod's block).
-template <bool SH, bool FAST, int NT>
+// WIN (NT = kBatchPods, unsharded): every block runs the window scan itself
+// (window_block, thread i = pod i) instead of reading k_adapt_window's
+// output; block 0 stores awin / aexact for the pairs and the commit.
+template <bool SH, bool FAST, int NT, bool WIN = false>
 __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words,
-                                                   const int32_t* __restrict__ awin,
-                                                   const int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
+                                                   int32_t* __restrict__ awin,
+                                                   int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
                                                    int32_t* __restrict__ topk_cnt,
                                                    int32_t* __restrict__ topk_complete,
                                                    uint64_t* __restrict__ xsend) {
@@ -264,7 +287,28 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
   const int32_t j = blockIdx.x;
   const int32_t base = st->cursor;
   if (j >= min(kBatchPods, st->end - base)) return;   // block-uniform
-  if (j >= *aexact) {
+  int32_t win_s = 0, win_cut = -1, exact;
+  if constexpr (WIN) {
+    static_assert(!SH && NT == kBatchPods, "fused window: unsharded, one thread per pod");
+    __shared__ int2 s_win;
+    int32_t ws, wc;
+    const int32_t kk = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, c.n);
+    window_block(st, amask, n_words, c.n, kk, &ws, &wc, &exact);   // the batch is not empty (above)
+    if (tid == j) s_win = make_int2(ws, wc);
+    if (j == 0) {
+      if (tid < min(kBatchPods, st->end - base)) {
+        awin[2 * tid] = ws;
+        awin[2 * tid + 1] = wc;
+      }
+      if (tid == 0) *aexact = exact;
+    }
+    __syncthreads();
+    win_s = s_win.x;
+    win_cut = s_win.y;
+  } else {
+    exact = *aexact;
+  }
+  if (j >= exact) {
     if (SH) {
       if (tid <= kTopT) xsend[(size_t)j * kXRec + tid] = 0;   // empty, incomplete
     } else if (tid == 0) {
@@ -273,7 +317,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
     }
     return;
   }
-  const int32_t n = SH ? c.n_total : c.n, s = awin[2 * j], cut = awin[2 * j + 1];
+  const int32_t n = SH ? c.n_total : c.n, s = WIN ? win_s : awin[2 * j], cut = WIN ? win_cut : awin[2 * j + 1];
   const int32_t kend = cut >= 0 ? cut : n;
   const int32_t pi = base + j;
   const ksim_pod& p = P.pods[pi];
@@ -496,6 +540,13 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",
                                                          "k_batch_chain", "k_adapt_pairs", "k_adapt_commit"};
 
+// A/B switch (read once per process): KSIM_WINDOW_SEPARATE=1 launches the
+// window scan as its own one-block kernel at every cluster size.
+static bool window_fused() {
+  static const bool separate = getenv("KSIM_WINDOW_SEPARATE") != nullptr;
+  return !separate;
+}
+
 uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const int32_t n_words = (a.c.n + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
@@ -504,16 +555,20 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   k_adapt_mask_ns<<<dim3((n_words + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st,
                                                                                           a.s.amask, n_words, mp);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  const bool win_fused = window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
+  if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
-#define TOP(F, NT) k_adapt_top<false, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
+#define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr)
   if (k >= kTopWideK) {
-    if (a.fast) TOP(true, 1024);
-    else TOP(false, 1024);
+    if (a.fast) TOP(true, 1024, false);
+    else TOP(false, 1024, false);
+  } else if (win_fused) {
+    if (a.fast) TOP(true, 256, true);
+    else TOP(false, 256, true);
   } else {
-    if (a.fast) TOP(true, 256);
-    else TOP(false, 256);
+    if (a.fast) TOP(true, 256, false);
+    else TOP(false, 256, false);
   }
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
@@ -533,7 +588,9 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,
                                                a.s.awin, a.chosen);
   if (evs) (void)hipEventRecord(evs[6], stream);
-  return chain_fused() ? 0x37u : 0x3fu;         // fused: the chain slot is an empty event pair
+  uint32_t mask = chain_fused() ? 0x37u : 0x3fu;   // fused: the chain slot is an empty event pair
+  if (win_fused) mask &= ~0x2u;                   // likewise the window slot
+  return mask;
 }
 
 // ---- node-sharded ADAPT batch -----------------------------------

@@ -185,6 +185,20 @@ int hip_fail(ksim_handle* h, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail((h), _e, #expr); \
   } while (0)
 
+// Blocking copies on the handle's own non-blocking stream.  A hipMemcpy on the
+// legacy stream is refused while another host thread captures a graph (several
+// engines in one process: bench config 5's concurrent sweep), and stream order
+// is the order the engine relies on anyway.
+static hipError_t hcopy(ksim_handle* h, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, h->stream);
+  return e != hipSuccess ? e : hipStreamSynchronize(h->stream);
+}
+
+static hipError_t hzero(ksim_handle* h, void* dst, size_t bytes) {
+  const hipError_t e = hipMemsetAsync(dst, 0, bytes, h->stream);
+  return e != hipSuccess ? e : hipStreamSynchronize(h->stream);
+}
+
 void free_bufs(std::vector<DevBuf>& v) {
   for (auto& b : v)
     if (b.p) (void)hipFree(b.p);
@@ -1357,15 +1371,15 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   DevState st{};
-  HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, &st, h->st, sizeof(st), hipMemcpyDeviceToHost));
   const size_t N = (size_t)n, N0 = (size_t)n0;
   // out = table + (device - snapshot) at old_pos, rows of n0 -> rows of n
   auto replay = [&](auto& out, const auto* dev, const auto* snap, const auto* tab, int rows, int rows0) -> int {
     using T = typename std::remove_reference<decltype(out)>::type::value_type;
     std::vector<T> a(N0 * (size_t)rows0), b(N0 * (size_t)rows0);
     if (!a.empty()) {
-      HIPCHK(h, hipMemcpy(a.data(), dev, sizeof(T) * a.size(), hipMemcpyDeviceToHost));
-      HIPCHK(h, hipMemcpy(b.data(), snap, sizeof(T) * b.size(), hipMemcpyDeviceToHost));
+      HIPCHK(h, hcopy(h, a.data(), dev, sizeof(T) * a.size(), hipMemcpyDeviceToHost));
+      HIPCHK(h, hcopy(h, b.data(), snap, sizeof(T) * b.size(), hipMemcpyDeviceToHost));
     }
     out.assign(N * (size_t)rows, 0);
     for (int k = 0; k < rows; k++)
@@ -1394,7 +1408,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
   if ((rc = ksim_set_cluster(h, t, v)) != KSIM_OK) return rc;
   const DevCluster& d = h->dc;
   auto put = [&](void* dst, const void* src, size_t bytes) -> int {
-    if (bytes) HIPCHK(h, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    if (bytes) HIPCHK(h, hcopy(h, dst, src, bytes, hipMemcpyHostToDevice));
     return KSIM_OK;
   };
   if ((rc = put(d.req_cpu, rc_.data(), 8 * N)) || (rc = put(d.req_mem, rm.data(), 8 * N)) ||
@@ -1406,7 +1420,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
   DevState s2{};
   s2.next_start = n > 0 ? st.next_start % n : 0;
   s2.pod_seq = st.pod_seq;
-  HIPCHK(h, hipMemcpy(h->st, &s2, sizeof(s2), hipMemcpyHostToDevice));
+  HIPCHK(h, hcopy(h, h->st, &s2, sizeof(s2), hipMemcpyHostToDevice));
   return KSIM_OK;
 }
 
@@ -1428,7 +1442,7 @@ int ksim_remove_node(ksim_handle* h, int32_t pos) {
   auto pull = [&](auto& out, const auto* dev, size_t rows) -> int {
     using T = typename std::remove_reference<decltype(out)>::type::value_type;
     std::vector<T> all(N0 * rows);
-    if (!all.empty()) HIPCHK(h, hipMemcpy(all.data(), dev, sizeof(T) * all.size(), hipMemcpyDeviceToHost));
+    if (!all.empty()) HIPCHK(h, hcopy(h, all.data(), dev, sizeof(T) * all.size(), hipMemcpyDeviceToHost));
     out.clear();
     for (size_t k = 0; k < rows; k++)
       for (size_t i = 0; i < N0; i++)
@@ -1455,12 +1469,12 @@ int ksim_remove_node(ksim_handle* h, int32_t pos) {
   std::vector<int64_t> lnum((size_t)std::max(c.n_label_values, 0));
   std::vector<uint8_t> lok((size_t)std::max(c.n_label_values, 0));
   std::vector<double> tlog((size_t)c.n_topo_log);
-  if (!lco.empty()) HIPCHK(h, hipMemcpy(lco.data(), c.label_col_offset, 4 * lco.size(), hipMemcpyDeviceToHost));
+  if (!lco.empty()) HIPCHK(h, hcopy(h, lco.data(), c.label_col_offset, 4 * lco.size(), hipMemcpyDeviceToHost));
   if (!lnum.empty()) {
-    HIPCHK(h, hipMemcpy(lnum.data(), c.label_num, 8 * lnum.size(), hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy(lok.data(), c.label_num_ok, lok.size(), hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, lnum.data(), c.label_num, 8 * lnum.size(), hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, lok.data(), c.label_num_ok, lok.size(), hipMemcpyDeviceToHost));
   }
-  if (!tlog.empty()) HIPCHK(h, hipMemcpy(tlog.data(), c.topo_log, 8 * tlog.size(), hipMemcpyDeviceToHost));
+  if (!tlog.empty()) HIPCHK(h, hcopy(h, tlog.data(), c.topo_log, 8 * tlog.size(), hipMemcpyDeviceToHost));
   ksim_node_table t{};
   t.n_nodes = n;
   t.n_scalar = c.n_scalar;
@@ -1504,12 +1518,12 @@ int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int6
   HIPCHK(h, hipSetDevice(h->device));
   const size_t N = (size_t)h->dc.n;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (req_cpu) HIPCHK(h, hipMemcpy(req_cpu, h->dc.req_cpu, 8 * N, hipMemcpyDeviceToHost));
-  if (req_mem) HIPCHK(h, hipMemcpy(req_mem, h->dc.req_mem, 8 * N, hipMemcpyDeviceToHost));
-  if (req_eph) HIPCHK(h, hipMemcpy(req_eph, h->dc.req_eph, 8 * N, hipMemcpyDeviceToHost));
-  if (nz_cpu) HIPCHK(h, hipMemcpy(nz_cpu, h->dc.nz_cpu, 8 * N, hipMemcpyDeviceToHost));
-  if (nz_mem) HIPCHK(h, hipMemcpy(nz_mem, h->dc.nz_mem, 8 * N, hipMemcpyDeviceToHost));
-  if (num_pods) HIPCHK(h, hipMemcpy(num_pods, h->dc.num_pods, 4 * N, hipMemcpyDeviceToHost));
+  if (req_cpu) HIPCHK(h, hcopy(h, req_cpu, h->dc.req_cpu, 8 * N, hipMemcpyDeviceToHost));
+  if (req_mem) HIPCHK(h, hcopy(h, req_mem, h->dc.req_mem, 8 * N, hipMemcpyDeviceToHost));
+  if (req_eph) HIPCHK(h, hcopy(h, req_eph, h->dc.req_eph, 8 * N, hipMemcpyDeviceToHost));
+  if (nz_cpu) HIPCHK(h, hcopy(h, nz_cpu, h->dc.nz_cpu, 8 * N, hipMemcpyDeviceToHost));
+  if (nz_mem) HIPCHK(h, hcopy(h, nz_mem, h->dc.nz_mem, 8 * N, hipMemcpyDeviceToHost));
+  if (num_pods) HIPCHK(h, hcopy(h, num_pods, h->dc.num_pods, 4 * N, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
 
@@ -1517,7 +1531,7 @@ int ksim_get_nb_alloc(ksim_handle* h, int64_t* out) {
   if (!h || !h->has_cluster || !out) return set_err(h, KSIM_E_INVALID, "cluster not set / null out");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  HIPCHK(h, hipMemcpy(out, h->dc.nb_alloc, 8 * (size_t)h->dc.n, hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, out, h->dc.nb_alloc, 8 * (size_t)h->dc.n, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
 
@@ -1526,14 +1540,14 @@ int ksim_get_class_count(ksim_handle* h, int32_t* out) {
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->dc.n_classes)
-    HIPCHK(h, hipMemcpy(out, h->dc.cnt, 4 * (size_t)h->dc.n * h->dc.n_classes, hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, out, h->dc.cnt, 4 * (size_t)h->dc.n * h->dc.n_classes, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
 
 int ksim_get_next_start(ksim_handle* h, int32_t* next_start) {
   if (!h || !next_start) return KSIM_E_INVALID;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  HIPCHK(h, hipMemcpy(next_start, &h->st->next_start, 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, next_start, &h->st->next_start, 4, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
 
@@ -1542,14 +1556,14 @@ int ksim_set_next_start(ksim_handle* h, int32_t next_start) {
   if (h->has_cluster && (next_start < 0 || next_start >= std::max(h->dc.n, 1)))
     return set_err(h, KSIM_E_INVALID, "next_start out of range");
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  HIPCHK(h, hipMemcpy(&h->st->next_start, &next_start, 4, hipMemcpyHostToDevice));
+  HIPCHK(h, hcopy(h, &h->st->next_start, &next_start, 4, hipMemcpyHostToDevice));
   return KSIM_OK;
 }
 
 int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
   if (!h) return KSIM_E_INVALID;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  HIPCHK(h, hipMemcpy(&h->st->pod_seq, &seq, 8, hipMemcpyHostToDevice));
+  HIPCHK(h, hcopy(h, &h->st->pod_seq, &seq, 8, hipMemcpyHostToDevice));
   return KSIM_OK;
 }
 
@@ -1665,16 +1679,16 @@ static int copy_eval_out(ksim_handle* h, ksim_eval_out* out) {
   const size_t N = (size_t)h->dc.n;
   const int S = h->prof.n_score;
   if (out->fail_plugin) {
-    HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
     strip_fail_errors(out->fail_plugin, N);
   }
-  if (out->fail_detail) HIPCHK(h, hipMemcpy(out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
-  if (out->scored) HIPCHK(h, hipMemcpy(out->scored, h->eo.scored, N, hipMemcpyDeviceToHost));
-  if (out->raw && S) HIPCHK(h, hipMemcpy(out->raw, h->eo.raw, 8 * N * S, hipMemcpyDeviceToHost));
-  if (out->norm && S) HIPCHK(h, hipMemcpy(out->norm, h->eo.norm, 8 * N * S, hipMemcpyDeviceToHost));
-  if (out->total) HIPCHK(h, hipMemcpy(out->total, h->eo.total, 8 * N, hipMemcpyDeviceToHost));
+  if (out->fail_detail) HIPCHK(h, hcopy(h, out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
+  if (out->scored) HIPCHK(h, hcopy(h, out->scored, h->eo.scored, N, hipMemcpyDeviceToHost));
+  if (out->raw && S) HIPCHK(h, hcopy(h, out->raw, h->eo.raw, 8 * N * S, hipMemcpyDeviceToHost));
+  if (out->norm && S) HIPCHK(h, hcopy(h, out->norm, h->eo.norm, 8 * N * S, hipMemcpyDeviceToHost));
+  if (out->total) HIPCHK(h, hcopy(h, out->total, h->eo.total, 8 * N, hipMemcpyDeviceToHost));
   DevState st;
-  HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, &st, h->st, sizeof(st), hipMemcpyDeviceToHost));
   out->chosen = st.chosen;
   out->status = st.status;
   out->n_feasible = st.n_feasible;
@@ -1720,14 +1734,14 @@ int ksim_eval_pod_filter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const size_t N = (size_t)h->dc.n;
   if (out->fail_plugin) {
-    HIPCHK(h, hipMemcpy(out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, out->fail_plugin, h->sc.fail, N, hipMemcpyDeviceToHost));
     strip_fail_errors(out->fail_plugin, N);
   }
-  if (out->fail_detail) HIPCHK(h, hipMemcpy(out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
+  if (out->fail_detail) HIPCHK(h, hcopy(h, out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
   WinState w;
   DevState st;
-  HIPCHK(h, hipMemcpy(&w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(&st, h->st, sizeof(st), hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, &w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
+  HIPCHK(h, hcopy(h, &st, h->st, sizeof(st), hipMemcpyDeviceToHost));
   const int32_t ns = w.nscan;                      // nodes scanned (PreFilterResult: its node count)
   const int32_t processed = w.cut < ns ? w.cut : ns;
   out->chosen = w.error ? KSIM_CHOSEN_ERROR : -1;
@@ -2067,7 +2081,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   HIPCHK(h, hipGetLastError());
-  if (chosen && count) HIPCHK(h, hipMemcpy(chosen, h->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
+  if (chosen && count) HIPCHK(h, hcopy(h, chosen, h->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
   if (stats) {
     DevState st;
     if ((rc = read_state(h, st))) return rc;
@@ -2170,7 +2184,7 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
   if (count && (rc = shard_schedule(v, first, count))) return rc;
   HIPCHK(h0, hipEventRecord(h0->ev1, h0->stream));
   HIPCHK(h0, hipEventSynchronize(h0->ev1));
-  if (chosen && count) HIPCHK(h0, hipMemcpy(chosen, h0->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
+  if (chosen && count) HIPCHK(h0, hcopy(h0, chosen, h0->d_chosen + first, 4 * (size_t)count, hipMemcpyDeviceToHost));
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
     for (auto* h : v) {
@@ -2250,7 +2264,7 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
   *avg_ms = ms / reps;
   // the timed no-window filter passes added into the window counters
-  if (!batch) HIPCHK(h, hipMemset(h->sc.win, 0, sizeof(WinState)));
+  if (!batch) HIPCHK(h, hzero(h, h->sc.win, sizeof(WinState)));
   if (kernel) *kernel = batch ? kKernelsPerCycle : 2;   // k_batch_top / k_filter_score
   return KSIM_OK;
 }
@@ -2339,7 +2353,7 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   int rc = read_state(h, st);
   if (rc) return rc;
   int64_t v[3 + 16 + 2] = {st.batches, st.truncations, st.cuts};
-  if (h->has_cluster) HIPCHK(h, hipMemcpy(v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
+  if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   v[19] = h->graph_captures;
   v[20] = h->match_ns;
   const int32_t m = n < 21 ? n : 21;
@@ -2443,10 +2457,10 @@ extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_
   out->n_candidates = pick[3];
   if (pick[0] >= 0 && out->victims && out->victims_cap > 0) {
     std::vector<int32_t> off(2);
-    HIPCHK(h, hipMemcpy(off.data(), h->pre.off + pick[0], 8, hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, off.data(), h->pre.off + pick[0], 8, hipMemcpyDeviceToHost));
     std::vector<uint8_t> flag((size_t)std::max(off[1] - off[0], 1));
     if (off[1] > off[0])
-      HIPCHK(h, hipMemcpy(flag.data(), h->pre.vflag + off[0], (size_t)(off[1] - off[0]), hipMemcpyDeviceToHost));
+      HIPCHK(h, hcopy(h, flag.data(), h->pre.vflag + off[0], (size_t)(off[1] - off[0]), hipMemcpyDeviceToHost));
     int32_t k = 0;
     for (int32_t j = off[0]; j < off[1] && k < out->victims_cap; j++)
       if (flag[j - off[0]]) out->victims[k++] = h->pre_index[j];

@@ -1,0 +1,47 @@
+"""The engine's A/B switches keep the pre-fusion launch forms alive
+(KSIM_CHAIN_SEPARATE: the chain as its own one-block launch ahead of the
+pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch).  They
+are read once per process, so each runs in one child process that schedules
+P100 and ADAPT batches and checks them against the oracle (the default forms
+run in every other GPU test)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+CHILD = r'''
+import numpy as np
+from ksim import gen, profile
+from ksim.engine import Engine
+from oracle.oracle import Oracle
+for pct, n_nodes, n_pods in ((100, 2000, 3000), (0, 2000, 3000), (0, 300, 300 * 60 + 11)):
+    cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=n_pods, seed=5)
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=pct))
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and eng.next_start == ora.next_start
+    assert st.batches > 0
+    eng.close()
+print("ok")
+'''
+
+
+@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE"])
+def test_separate_launch_forms_vs_oracle(switch):
+    env = dict(os.environ)
+    env[switch] = "1"
+    env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd"),
+                                         env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", CHILD], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]

@@ -72,8 +72,8 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
         return 8 * B * (tiles * geom["tile_cand"] + T)
     if name == "k_batch_chain":
         return 8 * B * T * 2
-    if name == "k_batch_pairs":
-        return B * (B - 1) // 2 * B_EVAL                  # one bound-row re-eval per pod pair
+    if name == "k_batch_pairs":                           # the chain runs inside this launch (k_batch_chain_pairs)
+        return B * (B - 1) // 2 * B_EVAL + 8 * B * T * 2   # one bound-row re-eval per pod pair + the lists
     if name == "k_adapt_mask":
         return B_FILTER * n_nodes * B                 # filter columns of every node row, per pod
     if name == "k_adapt_top":

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 6
+#define KSIM_ABI_VERSION 7
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -481,6 +481,61 @@ int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t*
  * behind Reserve / Unreserve (scheduler/plugin/wrappedplugin.go:583, 617). */
 int ksim_assume(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
 int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t node);
+
+/* ---- framework-driven compat mode ---------------------------------------------
+ * The simulator runs upstream's framework with parallelism 16 and
+ * percentageOfNodesToScore 0 (simulator/scheduler/scheduler.go:149,153, re-
+ * defaulted at :231-241).  The FRAMEWORK then decides which nodes Filter runs
+ * on (16 racing Parallelizer workers stop after numFeasibleNodesToFind feasible
+ * nodes), which feasible list PreScore / Score / NormalizeScore see, and which
+ * tied node selectHost's reservoir hands to Reserve.  ksim_eval_pod makes those
+ * choices itself (sequential scan, TB tie-break); these calls answer the
+ * engine-backed plugins under the framework's own choices instead:
+ *
+ *   ksim_fw_prefilter  PreFilter, then Filter of EVERY node of the pod's scan
+ *                      set (all nodes, or PreFilterResult.NodeNames), so a
+ *                      worker reaching any node finds its answer: fail_plugin
+ *                      / fail_detail for every node (KSIM_NOT_EVALUATED only
+ *                      for nodes outside PreFilterResult.NodeNames, which the
+ *                      framework never hands to Filter).  n_feasible = nodes
+ *                      passing, n_evaluated = scan-set size, k_to_find =
+ *                      numFeasibleNodesToFind(scan-set size) for the
+ *                      framework's scan.  nextStartNodeIndex and the tie-break
+ *                      sequence are the framework's: untouched.  status
+ *                      KSIM_STATUS_ERROR: a PreFilterResult name is not a node
+ *                      (the framework fails the cycle; no Filter runs).  A
+ *                      NetworkBandwidth Filter Skip / Error shows as its
+ *                      fail_detail (KSIM_NB_NO_LIMIT and above): the framework
+ *                      turns it into framework.Error.
+ *                      Replaces the original plugins' PreFilter and Filter
+ *                      behind wrappedPlugin.PreFilter / Filter
+ *                      (wrappedplugin.go:459-486, 491-516).
+ *   ksim_fw_score      PreScore, Score and NormalizeScore over exactly the
+ *                      framework's feasible list nodes[0..n) (any order; each a
+ *                      node that passed the filter pass, once):
+ *                      PodTopologySpread's IgnoredNodes, pair registration and
+ *                      topologyNormalizingWeight over the list, raw / norm /
+ *                      total / scored for the listed nodes (the same layout as
+ *                      ksim_eval_out).  No selectHost, no bind: chosen = -1
+ *                      (KSIM_CHOSEN_ERROR with status KSIM_STATUS_ERROR when a
+ *                      listed node's NetworkBandwidth Score fails).
+ *                      Replaces PreScore / Score (wrappedplugin.go:427-454,
+ *                      388-413).
+ *   ksim_fw_normalize  NormalizeScore of the plugin at profile score slot
+ *                      `score_slot` over an explicit (node, score) list, e.g.
+ *                      the NodeScoreList the wrapper passes
+ *                      (wrappedplugin.go:356-375), with the PreScore state of
+ *                      the last ksim_fw_score (IgnoredNodes, topologyScore
+ *                      emptiness).  out[j] = normalized score of entry j;
+ *                      plugins without NormalizeScore copy the scores.
+ *   Reserve / Unreserve with the framework's node: ksim_assume / ksim_forget
+ *                      (wrappedplugin.go:583-584, 617).
+ * Any other cycle or snapshot call on the handle ends a framework cycle in
+ * flight.  Unsharded handles only. */
+int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
+int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out* out);
+int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, const int64_t* scores, int32_t n,
+                      int64_t* out);
 
 /* Batch mode: upload a pod set once (device-resident), then schedule a range
  * of it in queue order; chosen[i] = node position or -1.  The whole-cycle

@@ -27,7 +27,7 @@ import (
 )
 
 // ABIVersion is the header version this binding was written against.
-const ABIVersion = 4
+const ABIVersion = 7
 
 // Engine owns one device handle (one GPU, or one node shard of a cluster).
 type Engine struct{ h *C.ksim_handle }
@@ -105,6 +105,55 @@ func (e *Engine) MatchTerms(mp *C.ksim_match_problem, bits []uint32, counts []in
 // n_nodes entries, n_score x n_nodes for the score matrices).
 func (e *Engine) EvalPod(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
 	return e.err(C.ksim_eval_pod(e.h, ps, C.int32_t(idx), out))
+}
+
+// EvalPodFilter / EvalPodFinish split a cycle around the host's extender
+// round trip (findNodesThatPassExtenders, the extender part of prioritizeNodes).
+func (e *Engine) EvalPodFilter(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
+	return e.err(C.ksim_eval_pod_filter(e.h, ps, C.int32_t(idx), out))
+}
+
+func (e *Engine) EvalPodFinish(extFail []uint8, extScore []int64, out *C.ksim_eval_out) error {
+	var f *C.uint8_t
+	var s *C.int64_t
+	if len(extFail) > 0 {
+		f = (*C.uint8_t)(unsafe.Pointer(&extFail[0]))
+	}
+	if len(extScore) > 0 {
+		s = (*C.int64_t)(unsafe.Pointer(&extScore[0]))
+	}
+	return e.err(C.ksim_eval_pod_finish(e.h, f, s, out))
+}
+
+// Framework-driven compat mode (plugins.go uses these through cgo directly):
+// FwPreFilter answers Filter for every node of the pod's scan set, FwScore
+// runs PreScore / Score / NormalizeScore over the framework's list,
+// FwNormalize normalizes one score slot over an explicit list.
+func (e *Engine) FwPreFilter(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
+	return e.err(C.ksim_fw_prefilter(e.h, ps, C.int32_t(idx), out))
+}
+
+func (e *Engine) FwScore(nodes []int32, out *C.ksim_eval_out) error {
+	var p *C.int32_t
+	if len(nodes) > 0 {
+		p = (*C.int32_t)(unsafe.Pointer(&nodes[0]))
+	}
+	return e.err(C.ksim_fw_score(e.h, p, C.int32_t(len(nodes)), out))
+}
+
+func (e *Engine) FwNormalize(slot int, nodes []int32, scores, out []int64) error {
+	if len(nodes) == 0 {
+		return nil
+	}
+	return e.err(C.ksim_fw_normalize(e.h, C.int32_t(slot), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
+		(*C.int64_t)(unsafe.Pointer(&scores[0])), C.int32_t(len(nodes)), (*C.int64_t)(unsafe.Pointer(&out[0]))))
+}
+
+// SetBoundPods / Preempt: DefaultPreemption's dry run over the bound pods.
+func (e *Engine) SetBoundPods(b *C.ksim_bound_pods) error { return e.err(C.ksim_set_bound_pods(e.h, b)) }
+
+func (e *Engine) Preempt(ps *C.ksim_pod_set, idx int, priority int32, out *C.ksim_preempt_out) error {
+	return e.err(C.ksim_preempt(e.h, ps, C.int32_t(idx), C.int32_t(priority), out))
 }
 
 // Assume / Forget: NodeInfo.AddPod / RemovePod of a bound pod (informer pod

@@ -135,6 +135,15 @@ struct ksim_handle {
   bool ext_pending = false;
   uint8_t* ext_fail = nullptr;     // device [n]
   int64_t* ext_score = nullptr;    // device [n]
+  // framework-driven compat cycle (ksim_fw_prefilter -> ksim_fw_score ->
+  // ksim_fw_normalize): the pod in h->pod1, its filter pass on the host for
+  // list validation, the scan-set size
+  bool fw_pending = false, fw_scored = false, fw_dom_dirty = false;
+  int32_t fw_ns = 0;
+  std::vector<uint8_t> fw_fail;
+  int32_t* fw_nodes = nullptr;     // device [n]
+  int64_t* fw_vals = nullptr;      // device [n]
+  int64_t* fw_out = nullptr;       // device [n]
 
   // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
   int32_t shard_base = 0, shard_total = 0;
@@ -390,8 +399,22 @@ bool pod_batchable(const ksim_handle* h, const ksim_pod& p) {
   return true;
 }
 
-int ensure_ready(ksim_handle* h) {
+// A framework-driven cycle left behind by another entry point: its PreFilter
+// domain sums were never re-zeroed by a k_select (no ksim_fw_score ran), and
+// its pod / scratch state is about to be replaced.
+int fw_abandon(ksim_handle* h) {
+  if (h->fw_dom_dirty && h->sc.dom)
+    HIPCHK(h, hipMemsetAsync(h->sc.dom, 0, 8 * (size_t)KSIM_MAX_USES * h->dc.vmax, h->stream));
+  h->fw_dom_dirty = h->fw_pending = h->fw_scored = false;
+  return KSIM_OK;
+}
+
+int ensure_ready(ksim_handle* h, bool fw = false) {
   if (!h) return KSIM_E_INVALID;
+  if (!fw && (h->fw_pending || h->fw_scored || h->fw_dom_dirty)) {
+    const int rc = fw_abandon(h);
+    if (rc) return rc;
+  }
   if (!h->has_profile) return set_err(h, KSIM_E_INVALID, "profile not set");
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   if (h->dc.n <= 0) return set_err(h, KSIM_E_INVALID, "no nodes available");
@@ -1157,6 +1180,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   h->pre_index.clear();
   h->pre_n = 0;
   h->ext_pending = false;
+  h->fw_pending = h->fw_scored = h->fw_dom_dirty = false;   // fresh scratch below
 
   const int32_t n_total = h->shard_total ? h->shard_total : n;
   if (h->shard_base < 0 || h->shard_base + n > n_total || n_total > KSIM_MAX_NODES)
@@ -1297,6 +1321,9 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.regbm, uint32_t*, 4 * (size_t)KSIM_MAX_USES * ((vmax + 31) / 32));
   SCR(h->ext_fail, uint8_t*, N);
   SCR(h->ext_score, int64_t*, 8 * N);
+  SCR(h->fw_nodes, int32_t*, 4 * N);
+  SCR(h->fw_vals, int64_t*, 8 * N);
+  SCR(h->fw_out, int64_t*, 8 * N);
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
@@ -1778,6 +1805,128 @@ int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t*
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return copy_eval_out(h, out);
+}
+
+// ---- framework-driven compat mode (SURVEY §8(b) compat mode) -------------------
+// The simulator runs upstream's framework with parallelism 16 and
+// percentageOfNodesToScore 0 (simulator/scheduler/scheduler.go:149,153,231-241):
+// the framework, not the engine, decides which nodes Filter runs on, the list
+// PreScore / Score / NormalizeScore see and the node Reserve records
+// (wrappedplugin.go:356-375, 491-516, 583-584).  These entry points answer the
+// engine-backed plugins under those choices.
+int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
+  int rc = ensure_ready(h);        // abandons any framework cycle in flight
+  if (rc) return rc;
+  if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
+    return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if (is_sharded(h)) return set_err(h, KSIM_E_UNSUPPORTED, "framework-driven cycles run on unsharded handles");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
+  h->ext_pending = false;
+  if ((rc = upload_single(h, ps, pod_index, h->pod1))) return rc;
+  if ((rc = set_run(h, 0, 1))) return rc;
+  // the two topology flags are OR-ed by the PreFilter pass and reset by a bind,
+  // which a framework cycle does not run
+  HIPCHK(h, hipMemsetAsync(&h->st->topo_flags, 0, sizeof(uint32_t), h->stream));
+  const ksim_pod& p = ps->pods[pod_index];
+  launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, p.use_count > 0);
+  HIPCHK(h, hipGetLastError());
+  h->fw_dom_dirty = p.use_count > 0;
+  const size_t N = (size_t)h->dc.n;
+  h->fw_fail.resize(N);
+  HIPCHK(h, hcopy(h, h->fw_fail.data(), h->sc.fail, N, hipMemcpyDeviceToHost));
+  if (out->fail_detail) HIPCHK(h, hcopy(h, out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
+  int32_t ns = h->dc.n;
+  if (p.flags & KSIM_POD_NODE_NAMES) ns = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 0 : p.nn_count;
+  int32_t nf = 0;
+  for (size_t i = 0; i < N; i++) nf += h->fw_fail[i] == KSIM_PASSED;
+  if (out->fail_plugin) {
+    std::memcpy(out->fail_plugin, h->fw_fail.data(), N);
+    strip_fail_errors(out->fail_plugin, N);
+  }
+  int32_t next = 0;
+  HIPCHK(h, hcopy(h, &next, &h->st->next_start, sizeof(next), hipMemcpyDeviceToHost));
+  const bool unknown = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) != 0;
+  out->chosen = unknown ? KSIM_CHOSEN_ERROR : -1;
+  out->status = unknown ? KSIM_STATUS_ERROR : 0;
+  out->n_feasible = nf;
+  out->n_evaluated = ns;
+  out->n_processed = 0;
+  out->k_to_find = num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, ns);
+  out->next_start = next;
+  h->fw_ns = ns;
+  h->fw_pending = !unknown;
+  return KSIM_OK;
+}
+
+int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out* out) {
+  int rc = ensure_ready(h, true);
+  if (rc) return rc;
+  if (!out || n < 0 || (n > 0 && !nodes)) return set_err(h, KSIM_E_INVALID, "bad node list");
+  if (!h->fw_pending) return set_err(h, KSIM_E_INVALID, "ksim_fw_score without ksim_fw_prefilter");
+  const size_t N = (size_t)h->dc.n;
+  // the list: feasible nodes of the filter pass, each once
+  std::vector<uint8_t> out_of_list(N, 1);
+  for (int32_t j = 0; j < n; j++) {
+    const int32_t x = nodes[j];
+    if (x < 0 || (size_t)x >= N || h->fw_fail[x] != KSIM_PASSED || !out_of_list[x])
+      return set_err(h, KSIM_E_INVALID, "node list: not a feasible node of the filter pass, or repeated");
+    out_of_list[x] = 0;
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(h->ext_fail, out_of_list.data(), N, hipMemcpyHostToDevice, h->stream));
+  // the window of the filter pass covers the whole scan set (k_window's
+  // extender branch keeps it and drops the unlisted nodes)
+  const int32_t cut = h->fw_ns;
+  HIPCHK(h, hipMemcpyAsync(&h->sc.win->cut, &cut, sizeof(cut), hipMemcpyHostToDevice, h->stream));
+  LaunchArgs a = make_args(h, h->pod1, nullptr);
+  a.s.ext_fail = h->ext_fail;
+  a.s.ext_score = nullptr;
+  launch_fw_score(a, h->stream);
+  HIPCHK(h, hipGetLastError());
+  h->fw_pending = false;
+  h->fw_dom_dirty = false;                 // k_select re-zeroed the domain sums
+  h->fw_scored = true;
+  const int S = h->prof.n_score;
+  if (out->scored) HIPCHK(h, hcopy(h, out->scored, h->eo.scored, N, hipMemcpyDeviceToHost));
+  if (out->raw && S) HIPCHK(h, hcopy(h, out->raw, h->eo.raw, 8 * N * S, hipMemcpyDeviceToHost));
+  if (out->norm && S) HIPCHK(h, hcopy(h, out->norm, h->eo.norm, 8 * N * S, hipMemcpyDeviceToHost));
+  if (out->total) HIPCHK(h, hcopy(h, out->total, h->eo.total, 8 * N, hipMemcpyDeviceToHost));
+  WinState w;
+  HIPCHK(h, hcopy(h, &w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
+  if (out->fail_plugin) {                  // the filter pass, unchanged
+    std::memcpy(out->fail_plugin, h->fw_fail.data(), N);
+    strip_fail_errors(out->fail_plugin, N);
+  }
+  out->n_feasible = w.nf;
+  out->n_evaluated = h->fw_ns;
+  out->n_processed = 0;
+  out->k_to_find = num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->fw_ns);
+  out->chosen = w.error ? KSIM_CHOSEN_ERROR : -1;
+  out->status = w.error ? KSIM_STATUS_ERROR : 0;
+  if (out->scored && w.nf <= 1) std::memset(out->scored, 0, N);
+  return KSIM_OK;
+}
+
+int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, const int64_t* scores, int32_t n,
+                      int64_t* out) {
+  int rc = ensure_ready(h, true);
+  if (rc) return rc;
+  if (!h->fw_scored) return set_err(h, KSIM_E_INVALID, "ksim_fw_normalize without ksim_fw_score");
+  if (score_slot < 0 || score_slot >= h->prof.n_score) return set_err(h, KSIM_E_INVALID, "bad score slot");
+  const size_t N = (size_t)h->dc.n;
+  if (n < 0 || (size_t)n > N || (n > 0 && (!nodes || !scores || !out)))
+    return set_err(h, KSIM_E_INVALID, "bad score list");
+  for (int32_t j = 0; j < n; j++)
+    if (nodes[j] < 0 || (size_t)nodes[j] >= N) return set_err(h, KSIM_E_INVALID, "bad node in score list");
+  if (n == 0) return KSIM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(h->fw_nodes, nodes, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->fw_vals, scores, 8 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  launch_fw_normalize(make_args(h, h->pod1, nullptr), score_slot, h->fw_nodes, h->fw_vals, n, h->fw_out, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hcopy(h, out, h->fw_out, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  return KSIM_OK;
 }
 
 static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {

@@ -74,6 +74,13 @@ void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.
 void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
 void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
+// Framework-driven compat cycle (ksim_fw_*): Filter of every scanned node; then
+// PreScore / Score / NormalizeScore over the framework's list (a.s.ext_fail =
+// 1 for unlisted nodes), no bind; NormalizeScore of one slot over an explicit list.
+void launch_fw_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
+void launch_fw_score(const LaunchArgs& a, hipStream_t stream);
+void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,
+                         int64_t* out, hipStream_t stream);
 // DefaultPreemption dry run (ksim_preempt.hip): the bound pods per node in
 // importance order (CSR over nodes), per-node results, the pick.
 struct PreemptNode {

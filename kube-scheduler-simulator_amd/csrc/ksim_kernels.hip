@@ -1506,6 +1506,46 @@ __global__ __launch_bounds__(256) void k_group_gather(GroupPtrs src, GroupPtrs d
   }
 }
 
+// ==== framework-driven compat cycle (ksim_fw_*) ====================================
+// Under the simulator's own settings the upstream framework chooses which nodes
+// Filter runs on, the feasible list PreScore / Score / NormalizeScore see and
+// the node Reserve assumes (ksim_engine.h "Framework-driven compat mode").  The
+// filter pass answers every node of the scan set (k_filter_score without the
+// window); ksim_fw_score runs the extender-style finish with the framework's
+// list as the kept set (k_window's ext branch: unlisted nodes out, PTS PreScore
+// over the list), k_extrema and k_select without the bind.
+//
+// NormalizeScore of one score slot over an explicit (node, score) list, with
+// the PreScore facts of the last ksim_fw_score: PodTopologySpread's
+// IgnoredNodes (s.ign under win->has_soft) and InterPodAffinity's topologyScore
+// emptiness (st->topo_flags).  One block: extrema as order-preserving images.
+__global__ __launch_bounds__(kFinalThreads) void k_fw_normalize(ksim_profile prof, int32_t slot,
+                                                                const DevState* __restrict__ st, DevScratch s,
+                                                                const int32_t* __restrict__ nodes,
+                                                                const int64_t* __restrict__ vals, int32_t n,
+                                                                int64_t* __restrict__ out) {
+  __shared__ uint64_t sh[kFinalWaves];
+  const int32_t kind = norm_kind((int)prof_score(prof, slot));
+  const bool soft = s.win->has_soft != 0;
+  uint64_t ix = 0, in = 0;
+  for (int32_t j = threadIdx.x; j < n; j += kFinalThreads) {
+    const bool ign = kind == kNormPTS && soft && s.ign[nodes[j]];
+    if (!ign) {
+      ix = umax64(ix, max_image(vals[j]));
+      in = umax64(in, min_image(vals[j]));
+    }
+  }
+  const int64_t gmax = from_max_image(block_max_u64<kFinalWaves>(ix, sh));
+  const int64_t gmin = from_min_image(block_max_u64<kFinalWaves>(in, sh));
+  const bool ipa_nonempty = (st->topo_flags & kTopoScoreNonEmpty) != 0;
+  for (int32_t j = threadIdx.x; j < n; j += kFinalThreads) {
+    const int64_t v = vals[j];
+    if (kind == kNormNone) out[j] = v;
+    else if (kind == kNormPTS && soft && s.ign[nodes[j]]) out[j] = 0;
+    else out[j] = normalize_value(kind, v, gmax, gmin, ipa_nonempty);
+  }
+}
+
 // ---- launchers ----------------------------------------------------------------
 const char* const kKernelNames[kKernelsPerCycle] = {"k_topo_prefilter", "k_topo_min", "k_filter_score",
                                                     "k_window", "k_extrema", "k_select", "k_bind"};
@@ -1568,6 +1608,29 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream) {
   k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
   k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 1, a.chosen);
+}
+
+// Framework-driven compat cycle: Filter of every scanned node (no window, no
+// scheduler-state change) ...
+void launch_fw_filter(const LaunchArgs& a, hipStream_t stream, bool topo) {
+  const int blocks = (a.c.n + 255) / 256;
+  if (topo) k_topo_prefilter<<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  if (topo) k_topo_min<false><<<1, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_filter_score<true, false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.dbp, a.st, a.s, 0, 0);
+}
+
+// ... then PreScore / Score / NormalizeScore over the framework's list
+// (a.s.ext_fail: 1 = not in the list), no selectHost bind.
+void launch_fw_score(const LaunchArgs& a, hipStream_t stream) {
+  const int blocks = (a.c.n + 255) / 256;
+  k_window<true><<<1, kFinalThreads, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_extrema<false><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s);
+  k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 0, nullptr);
+}
+
+void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,
+                         int64_t* out, hipStream_t stream) {
+  k_fw_normalize<<<1, kFinalThreads, 0, stream>>>(a.prof, slot, a.st, a.s, nodes, vals, n, out);
 }
 
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream) {

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8

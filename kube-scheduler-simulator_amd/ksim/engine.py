@@ -30,7 +30,7 @@ EXPORTS = [
     "ksim_set_shard", "ksim_comm_unique_id", "ksim_comm_init", "ksim_group_schedule_loaded",
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
     "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
-    "ksim_match_terms", "ksim_set_eval_range",
+    "ksim_match_terms", "ksim_set_eval_range", "ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize",
 ]
 
 
@@ -73,6 +73,9 @@ def lib():
         L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
         L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
         L.ksim_set_eval_range.argtypes = [vp, i32, i32]
+        L.ksim_fw_prefilter.argtypes = [vp, vp, i32, vp]
+        L.ksim_fw_score.argtypes = [vp, vp, i32, vp]
+        L.ksim_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
         L.ksim_assume.argtypes = [vp, vp, i32, i32]
         L.ksim_forget.argtypes = [vp, vp, i32, i32]
         L.ksim_load_pods.argtypes = [vp, vp]
@@ -249,6 +252,37 @@ class Engine:
                                              None if es is None else es.ctypes.data_as(ctypes.c_void_p),
                                              ctypes.byref(buf2.out)))
         return buf2.result()
+
+    # ---- framework-driven compat mode (ksim_fw_*) ----------------------------
+    def fw_prefilter(self, pods, index: int) -> dict:
+        """PreFilter + Filter of every node of the pod's scan set (the framework
+        chooses which of them its workers visit)."""
+        self._sync()
+        self._ran = True
+        buf = abi.EvalBuffers(self.n_nodes, self.n_score)
+        ps = pods.pod_set()
+        self._chk(lib().ksim_fw_prefilter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        return buf.result()
+
+    def fw_score(self, nodes) -> dict:
+        """PreScore / Score / NormalizeScore over exactly the framework's feasible list."""
+        arr = np.ascontiguousarray(nodes, np.int32)
+        buf = abi.EvalBuffers(self.n_nodes, self.n_score)
+        self._chk(lib().ksim_fw_score(self.h, arr.ctypes.data_as(ctypes.c_void_p), arr.size,
+                                      ctypes.byref(buf.out)))
+        return buf.result()
+
+    def fw_normalize(self, slot: int, nodes, scores) -> np.ndarray:
+        """NormalizeScore of score slot ``slot`` over an explicit (node, score) list."""
+        nd = np.ascontiguousarray(nodes, np.int32)
+        sc = np.ascontiguousarray(scores, np.int64)
+        if nd.size != sc.size:
+            raise ValueError("one score per node")
+        out = np.zeros(nd.size, np.int64)
+        self._chk(lib().ksim_fw_normalize(self.h, slot, nd.ctypes.data_as(ctypes.c_void_p),
+                                          sc.ctypes.data_as(ctypes.c_void_p), nd.size,
+                                          out.ctypes.data_as(ctypes.c_void_p)))
+        return out
 
     def set_bound_pods(self, bound):
         """The bound-pod table DefaultPreemption may evict (ksim.abi.BoundPods)."""

@@ -1,0 +1,168 @@
+"""Engine-backed framework plugins: the Python mirror of the Go adapter in
+integration/go/engine/plugins.go.
+
+In the reference every in-tree plugin is built by the factory closure at
+simulator/scheduler/plugin/plugins.go:75-87 and wrapped by NewWrappedPlugin
+(:86).  The engine replaces the ORIGINAL plugin ``p`` of that closure; the
+wrapper (wrappedplugin.go) and the result store stay as they are.  The
+framework, not the engine, then decides:
+
+  * which nodes Filter runs on: 16 racing Parallelizer workers stop after
+    numFeasibleNodesToFind feasible nodes (simulator/scheduler/scheduler.go:
+    149,153 pin parallelism 16 and percentageOfNodesToScore 0);
+  * the feasible list PreScore / Score / NormalizeScore see;
+  * the node Reserve records (selectHost's reservoir over math/rand).
+
+So the plugins answer under those choices (ksim_engine.h "framework-driven
+compat mode"):
+
+  PreFilter       the first wrapped PreFilter of a cycle calls ksim_fw_prefilter:
+                  Filter of every node of the pod's scan set on the device
+                  (wrappedplugin.go:459-486);
+  Filter(node)    a read of that pass: plugin k of the profile's Filter order
+                  fails on the node iff the pass stopped at k (RunFilterPlugins
+                  calls k only after 0..k-1 passed)  (:491-516);
+  PreScore(list)  the first wrapped PreScore calls ksim_fw_score(list)  (:427-454);
+  Score(node)     raw[slot][node]  (:388-413);
+  NormalizeScore  ksim_fw_normalize over the NodeScoreList it is handed  (:356-375);
+  Reserve(node)   ksim_assume on the framework's node; Unreserve ksim_forget
+                  (:583-584, 617);
+  PostFilter      DefaultPreemption's dry run, ksim_preempt: the nominated node
+                  (:518-538, Store.AddPostFilterResult store.go:437-452).
+
+One cycle is in flight at a time (upstream scheduleOne is serial); the wrapped
+plugins of a profile share one ``EnginePlugins``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .profile import SchedulerProfile
+from .wrapped import ERR_NODE_AFFINITY_CONFLICT, filter_message
+
+# framework.Code
+SUCCESS, ERROR, UNSCHEDULABLE, UNSCHEDULABLE_AND_UNRESOLVABLE, SKIP = 0, 1, 2, 3, 6
+
+# filter plugins whose failures are UnschedulableAndUnresolvable in v1.26
+_UNRESOLVABLE = {"NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "VolumeBinding",
+                 "VolumeZone"}
+
+
+class Status:
+    """framework.Status: a code and a message (nil status = SUCCESS)."""
+    __slots__ = ("code", "message", "failed_plugin")
+
+    def __init__(self, code: int = SUCCESS, message: str = "", failed_plugin: str = ""):
+        self.code, self.message, self.failed_plugin = code, message, failed_plugin
+
+    def is_success(self) -> bool:
+        return self.code == SUCCESS
+
+    def __repr__(self):
+        return f"Status({self.code}, {self.message!r})"
+
+
+def filter_code(plugin: str, detail: int) -> int:
+    """The framework.Code of a failing Filter (upstream v1.26 plugin returns)."""
+    if plugin == "NetworkBandwidth":
+        return UNSCHEDULABLE if detail == abi.NB_INSUFFICIENT else ERROR
+    if plugin == "PodTopologySpread":
+        return UNSCHEDULABLE_AND_UNRESOLVABLE if detail == abi.PTS_MISSING_LABEL else UNSCHEDULABLE
+    if plugin == "InterPodAffinity":
+        return UNSCHEDULABLE_AND_UNRESOLVABLE if detail == abi.IPA_AFFINITY else UNSCHEDULABLE
+    return UNSCHEDULABLE_AND_UNRESOLVABLE if plugin in _UNRESOLVABLE else UNSCHEDULABLE
+
+
+class EnginePlugins:
+    """The engine-backed plugin set of one profile.  ``backend`` is a
+    ksim.engine.Engine (the product); tests pass the oracle's framework-mode
+    binding (same method names) to get the reference answers under the same
+    framework choices."""
+
+    def __init__(self, backend, cluster, prof: SchedulerProfile):
+        self.b = backend
+        self.cluster = cluster
+        self.prof = prof
+        self.forder = prof.filter_order()
+        self.snames = [p.name for p in prof.score_plugins()]
+        self.pos = {n: i for i, n in enumerate(cluster.node_names)}
+        self._pods = None
+        self._idx = -1
+        self._filter: Optional[Dict] = None
+        self._score: Optional[Dict] = None
+
+    # ---- PreFilter / Filter ---------------------------------------------------
+    def pre_filter(self, pods, index: int) -> Tuple[Status, Optional[List[str]]]:
+        """The engine's PreFilter pass; returns NodeAffinity's status and
+        PreFilterResult.NodeNames (None = all nodes)."""
+        self._pods, self._idx = pods, index
+        self._score = None
+        names = pods.prefilter_names[index] if pods.prefilter_names else None
+        if names is not None and len(names) == 0:
+            self._filter = None
+            return Status(UNSCHEDULABLE_AND_UNRESOLVABLE, ERR_NODE_AFFINITY_CONFLICT, "NodeAffinity"), []
+        self._filter = self.b.fw_prefilter(pods, index)
+        if self._filter["status"] == abi.STATUS_ERROR:
+            return Status(ERROR, "node in PreFilterResult not found", "NodeAffinity"), names
+        return Status(), names
+
+    def filter(self, plugin: str, node: int) -> Status:
+        """wrappedPlugin.Filter's original-plugin call for ``plugin`` on ``node``."""
+        k = self.forder.index(plugin)
+        r = int(self._filter["fail_plugin"][node])
+        if r == abi.NOT_EVALUATED:
+            raise RuntimeError(f"Filter on node {node} outside the pod's scan set")
+        if r == abi.PASSED or r != k:
+            if r != abi.PASSED and r < k:
+                raise RuntimeError(f"{plugin} called on node {node} after {self.forder[r]} failed")
+            return Status()
+        d = int(self._filter["fail_detail"][node])
+        ns, name = self._pods.names[self._idx]
+        msg = filter_message(self.cluster, plugin, d, self.cluster.node_names[node], name)
+        return Status(filter_code(plugin, d), msg, plugin)
+
+    def run_filter_plugins(self, node: int) -> Tuple[Status, List[Tuple[str, Status]]]:
+        """framework.RunFilterPlugins: the plugins in order up to the first
+        non-success; returns the cycle status and each (plugin, status) run."""
+        ran = []
+        for pl in self.forder:
+            st = self.filter(pl, node)
+            ran.append((pl, st))
+            if not st.is_success():
+                return st, ran
+        return Status(), ran
+
+    # ---- PreScore / Score / NormalizeScore ------------------------------------
+    def pre_score(self, nodes: Sequence[int]) -> Status:
+        self._score = self.b.fw_score(np.asarray(nodes, np.int32))
+        if self._score["status"] == abi.STATUS_ERROR:
+            return Status(ERROR, "NetworkBandwidth Score failed")
+        return Status()
+
+    def score(self, plugin: str, node: int) -> int:
+        return int(self._score["raw"][self.snames.index(plugin)][node])
+
+    def normalize_score(self, plugin: str, nodes: Sequence[int], scores: Sequence[int]) -> List[int]:
+        """NormalizeScore over exactly the NodeScoreList handed in."""
+        return [int(x) for x in self.b.fw_normalize(self.snames.index(plugin), nodes, scores)]
+
+    # ---- Reserve / Unreserve / PostFilter -------------------------------------
+    def reserve(self, node: int) -> Status:
+        self.b.assume(self._pods, self._idx, node)
+        return Status()
+
+    def unreserve(self, node: int) -> None:
+        self.b.forget(self._pods, self._idx, node)
+
+    def post_filter(self, priority: int, bound=None) -> Tuple[Status, int]:
+        """DefaultPreemption.PostFilter: (status, nominated node or -1)."""
+        if bound is None:
+            node, _victims = self.b.preempt(self._pods, self._idx, priority)[:2]
+        else:
+            node, _victims = self.b.preempt(self._pods, self._idx, priority, bound)[:2]
+        if node < 0:
+            return Status(UNSCHEDULABLE, "preemption: 0/... nodes are available"), -1
+        return Status(), int(node)

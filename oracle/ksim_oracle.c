@@ -68,6 +68,10 @@ struct ksim_oracle {
   int64_t *dom;         /* [KSIM_MAX_USES][vmax] topology-pair sums */
   uint8_t *present;     /* [KSIM_MAX_USES][vmax] pair present (PTS) / registered (PTS soft) */
   uint8_t *ignored;     /* [n] PTS IgnoredNodes */
+  /* framework-driven compat mode (ksim_oracle_fw_*): the PreFilter state of
+   * the pod in flight and the PreScore facts NormalizeScore reads */
+  struct topo_ctx *fw_tc;
+  int fw_active, fw_scored;
 };
 
 /* ------------------------------------------------------------------------ */
@@ -148,7 +152,7 @@ void ksim_oracle_destroy(ksim_oracle* o) {
                 o->label_col_offset, o->label_num, o->label_num_ok, o->fail, o->detail,
                 o->flist, o->raw, o->cnt, o->topo_log, o->col_nvals, o->dom, o->present,
                 o->ignored, o->nb_limit, o->nb_alloc, o->s_req_cpu, o->s_req_mem, o->s_req_eph,
-                o->s_req_scalar, o->s_nz_cpu, o->s_nz_mem, o->s_nb_alloc, o->s_num_pods, o->s_cnt};
+                o->s_req_scalar, o->s_nz_cpu, o->s_nz_mem, o->s_nb_alloc, o->s_num_pods, o->s_cnt, o->fw_tc};
   for (size_t i = 0; i < sizeof(ps) / sizeof(ps[0]); i++) free(ps[i]);
   free(o);
 }
@@ -200,7 +204,7 @@ int ksim_oracle_upsert_nodes(ksim_oracle* o, const ksim_node_table* t, const ksi
   free(q->num_pods); q->num_pods = np;
   free(q->cnt); q->cnt = cnt;
   q->next_start = n > 0 ? o->next_start % (int32_t)n : 0;
-  q->pod_seq = o->pod_seq;
+  q->pod_seq = o->pod_seq;   /* a framework cycle in flight does not survive a node delta */
   ksim_oracle swap = *o;
   *o = *q;
   *q = swap;
@@ -1084,6 +1088,136 @@ int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, co
   out->chosen = chosen;
   out->status = KSIM_STATUS_SCHEDULED;
   assume_pod(o, ps, p, chosen, 1);
+  return KSIM_OK;
+}
+
+/* ---- framework-driven compat mode (ksim_engine.h ksim_fw_*) -------------- */
+/* Under the simulator's own settings (parallelism 16, percentageOfNodesToScore
+ * 0: simulator/scheduler/scheduler.go:149,153,231-241) the [upstream]
+ * framework, not the plugins, decides which nodes Filter runs on (16 racing
+ * Parallelizer workers, first numFeasibleNodesToFind feasible), the feasible
+ * list PreScore / Score / NormalizeScore see, and the node selectHost's
+ * reservoir picks for Reserve.  The plugin answers are functions of those
+ * choices alone:
+ *   Filter(node)        the PreFilter state and the snapshot (every node of
+ *                       the scan set answered here);
+ *   PreScore(list)      PodTopologySpread's IgnoredNodes, pair registration
+ *                       and topologyNormalizingWeight over the list
+ *                       (initPreScoreState); InterPodAffinity's topologyScore
+ *                       over all nodes (processExistingPod);
+ *   NormalizeScore(ls)  the plugin's normalization over exactly the list it
+ *                       is handed (wrappedplugin.go:356-375).
+ * Reserve / Unreserve are ksim_oracle_assume with sign +1 / -1. */
+int ksim_oracle_fw_filter(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ksim_eval_out* out) {
+  if (!o || !ps || pi < 0 || pi >= ps->n_pods || !out || o->n == 0) return KSIM_E_INVALID;
+  const ksim_pod* p = &ps->pods[pi];
+  const int32_t N = o->n;
+  const scan_set ss = pod_scan_set(o, ps, p);
+  if (!o->fw_tc) o->fw_tc = (topo_ctx*)calloc(1, sizeof(topo_ctx));
+  topo_prefilter(o, ps, p, o->fw_tc);
+  if (out->fail_plugin) memset(out->fail_plugin, KSIM_NOT_EVALUATED, (size_t)N);
+  if (out->fail_detail) memset(out->fail_detail, 0, 4 * (size_t)N);
+  int32_t nf = 0;
+  const int unknown = (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) != 0;
+  for (int32_t i = 0; i < ss.n; i++) {
+    const int32_t node = scan_node_at(&ss, i);
+    uint32_t det;
+    const uint8_t r = run_filter_plugins(o, ps, p, o->fw_tc, node, &det);
+    if (out->fail_plugin) out->fail_plugin[node] = r;
+    if (out->fail_detail) out->fail_detail[node] = det;
+    nf += r == KSIM_PASSED;
+  }
+  out->chosen = unknown ? KSIM_CHOSEN_ERROR : -1;
+  out->status = unknown ? KSIM_STATUS_ERROR : 0;
+  out->n_feasible = nf;
+  out->n_evaluated = ss.n;
+  out->n_processed = 0;
+  out->k_to_find = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, ss.n);
+  out->next_start = o->next_start;
+  o->fw_active = 1;
+  o->fw_scored = 0;
+  return KSIM_OK;
+}
+
+/* PreScore + Score + NormalizeScore + weights over exactly `nodes` (the
+ * framework's feasible list, any order).  No selectHost, no bind. */
+int ksim_oracle_fw_score(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, const int32_t* nodes, int32_t n,
+                         ksim_eval_out* out) {
+  if (!o || !o->fw_active || !ps || pi < 0 || pi >= ps->n_pods || !out || n < 0 || (n > 0 && !nodes))
+    return KSIM_E_INVALID;
+  const ksim_pod* p = &ps->pods[pi];
+  const int32_t N = o->n;
+  const int S = o->prof.n_score;
+  for (int32_t j = 0; j < n; j++) {
+    if (nodes[j] < 0 || nodes[j] >= N) return KSIM_E_INVALID;
+    o->flist[j] = nodes[j];
+  }
+  if (out->scored) memset(out->scored, 0, (size_t)N);
+  if (out->raw) memset(out->raw, 0, 8 * (size_t)N * S);
+  if (out->norm) memset(out->norm, 0, 8 * (size_t)N * S);
+  if (out->total) memset(out->total, 0, 8 * (size_t)N);
+  topo_ctx* tc = o->fw_tc;
+  out->chosen = -1;
+  out->n_feasible = n;
+  if (nb_score_error(o, o->flist, n)) {
+    out->status = KSIM_STATUS_ERROR;
+    out->chosen = KSIM_CHOSEN_ERROR;
+    return KSIM_OK;
+  }
+  out->status = 0;
+  topo_prescore(o, ps, p, o->flist, n, tc);
+  o->fw_scored = 1;
+  int64_t* tmp = (int64_t*)malloc(8 * (size_t)(n ? n : 1));
+  int64_t* totals = (int64_t*)calloc((size_t)(n ? n : 1), 8);
+  uint8_t* ign = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+  if (tc->has_soft) for (int32_t j = 0; j < n; j++) ign[j] = o->ignored[o->flist[j]];
+  for (int s = 0; s < S; s++) {
+    const int pl = o->prof.score[s];
+    for (int32_t j = 0; j < n; j++) tmp[j] = score_plugin_raw(o, ps, p, tc, pl, o->flist[j]);
+    if (out->raw) for (int32_t j = 0; j < n; j++) out->raw[(size_t)s * N + o->flist[j]] = tmp[j];
+    if (has_normalize(pl)) normalize_plugin(pl, tc, ign, n, tmp);
+    const int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
+    for (int32_t j = 0; j < n; j++) {
+      if (out->norm) out->norm[(size_t)s * N + o->flist[j]] = tmp[j];
+      totals[j] += tmp[j] * w;
+    }
+  }
+  if (S == 0) for (int32_t j = 0; j < n; j++) totals[j] = 1;
+  for (int32_t j = 0; j < n; j++) {
+    if (out->total) out->total[o->flist[j]] = totals[j];
+    if (out->scored) out->scored[o->flist[j]] = 1;
+  }
+  free(tmp);
+  free(totals);
+  free(ign);
+  return KSIM_OK;
+}
+
+/* NormalizeScore of the plugin at profile score slot `slot` over an explicit
+ * (node, score) list, with the PreScore state of the last ksim_oracle_fw_score
+ * (PodTopologySpread's IgnoredNodes, InterPodAffinity's topologyScore). */
+int ksim_oracle_fw_normalize(ksim_oracle* o, int32_t slot, const int32_t* nodes, const int64_t* scores, int32_t n,
+                             int64_t* out) {
+  if (!o || !o->fw_scored || slot < 0 || slot >= o->prof.n_score || n < 0 || (n > 0 && (!nodes || !scores || !out)))
+    return KSIM_E_INVALID;
+  const int pl = o->prof.score[slot];
+  uint8_t* ign = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+  for (int32_t j = 0; j < n; j++) {
+    if (nodes[j] < 0 || nodes[j] >= o->n) { free(ign); return KSIM_E_INVALID; }
+    ign[j] = o->fw_tc->has_soft && o->ignored[nodes[j]];
+    out[j] = scores[j];
+  }
+  if (has_normalize(pl)) normalize_plugin(pl, o->fw_tc, ign, n, out);
+  free(ign);
+  return KSIM_OK;
+}
+
+/* NodeInfo.AddPod / RemovePod of a pod on a node: Reserve / Unreserve
+ * (wrappedplugin.go:583-584, 617), informer pod add / delete. */
+int ksim_oracle_assume(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32_t node, int sign) {
+  if (!o || !ps || pi < 0 || pi >= ps->n_pods || node < 0 || node >= o->n || (sign != 1 && sign != -1))
+    return KSIM_E_INVALID;
+  assume_pod(o, ps, &ps->pods[pi], node, sign);
   return KSIM_OK;
 }
 

@@ -48,6 +48,15 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* pods, int32_t first
                          int32_t count, int32_t* chosen, int nthreads,
                          ksim_batch_stats* stats);
 
+/* Framework-driven compat mode (ksim_engine.h ksim_fw_*): Filter of every
+ * node of the scan set, PreScore / Score / NormalizeScore over the
+ * framework's list, NormalizeScore over an explicit list, assume / forget. */
+int ksim_oracle_fw_filter(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);
+int ksim_oracle_fw_score(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, const int32_t* nodes,
+                         int32_t n, ksim_eval_out* out);
+int ksim_oracle_fw_normalize(ksim_oracle* o, int32_t slot, const int32_t* nodes, const int64_t* scores, int32_t n,
+                             int64_t* out);
+int ksim_oracle_assume(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, int32_t node, int sign);
 int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* req_mem,
                                int64_t* req_eph, int64_t* nz_cpu, int64_t* nz_mem,
                                int32_t* num_pods);

@@ -29,6 +29,10 @@ def lib():
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_cycle_ext.argtypes = [vp, vp, i32, vp, vp, vp]
         L.ksim_oracle_preempt.argtypes = [vp, vp, i32, i32, vp, vp]
+        L.ksim_oracle_fw_filter.argtypes = [vp, vp, i32, vp]
+        L.ksim_oracle_fw_score.argtypes = [vp, vp, i32, vp, i32, vp]
+        L.ksim_oracle_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
+        L.ksim_oracle_assume.argtypes = [vp, vp, i32, i32, ctypes.c_int]
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
         L.ksim_oracle_get_class_count.argtypes = [vp, vp]
@@ -112,6 +116,50 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"oracle cycle failed: {rc}")
         return buf.result()
+
+    # ---- framework-driven compat mode (ksim_oracle_fw_*) ----------------------
+    def fw_prefilter(self, pods, index: int) -> dict:
+        self._sync()
+        self._ran = True
+        from ksim import abi
+        buf = abi.EvalBuffers(self.cluster.n_nodes, self.profile.n_score)
+        self._fw = (pods, index)
+        ps = pods.pod_set()
+        if lib().ksim_oracle_fw_filter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)) != 0:
+            raise RuntimeError("oracle fw_filter failed")
+        return buf.result()
+
+    def fw_score(self, nodes) -> dict:
+        from ksim import abi
+        pods, index = self._fw
+        arr = np.ascontiguousarray(nodes, np.int32)
+        buf = abi.EvalBuffers(self.cluster.n_nodes, self.profile.n_score)
+        ps = pods.pod_set()
+        if lib().ksim_oracle_fw_score(self.h, ctypes.byref(ps), index, arr.ctypes.data_as(ctypes.c_void_p),
+                                      arr.size, ctypes.byref(buf.out)) != 0:
+            raise RuntimeError("oracle fw_score failed")
+        return buf.result()
+
+    def fw_normalize(self, slot: int, nodes, scores) -> np.ndarray:
+        nd = np.ascontiguousarray(nodes, np.int32)
+        sc = np.ascontiguousarray(scores, np.int64)
+        out = np.zeros(nd.size, np.int64)
+        if lib().ksim_oracle_fw_normalize(self.h, slot, nd.ctypes.data_as(ctypes.c_void_p),
+                                          sc.ctypes.data_as(ctypes.c_void_p), nd.size,
+                                          out.ctypes.data_as(ctypes.c_void_p)) != 0:
+            raise RuntimeError("oracle fw_normalize failed")
+        return out
+
+    def assume(self, pods, index: int, node: int, sign: int = 1):
+        """NodeInfo.AddPod (sign 1) / RemovePod (-1): Reserve / Unreserve."""
+        self._sync()
+        self._ran = True
+        ps = pods.pod_set()
+        if lib().ksim_oracle_assume(self.h, ctypes.byref(ps), index, node, sign) != 0:
+            raise RuntimeError("oracle assume failed")
+
+    def forget(self, pods, index: int, node: int):
+        self.assume(pods, index, node, -1)
 
     def preempt(self, pods, index: int, priority: int, bound) -> tuple:
         """DefaultPreemption PostFilter (ksim_oracle_preempt).  ``bound`` is a

@@ -1,0 +1,283 @@
+"""A mirror of upstream's scheduling framework driving the wrapped plugins
+(TEST INFRASTRUCTURE: it plays [upstream] k8s.io/kubernetes v1.26.2
+pkg/scheduler, which the Go host keeps; not product code).
+
+What it reproduces of schedule_one.go / framework/runtime / parallelize:
+
+  findNodesThatPassFilters   Parallelizer(16).Until over the scan set from
+                             nextStartNodeIndex, chunked as chunkSizeFor(n, 16),
+                             workers racing: every worker takes chunks in order,
+                             checks ctx.Done() before each piece, and a piece
+                             may be in flight while another worker cancels, so
+                             several feasible nodes past the K-th can be
+                             evaluated (recorded, then dropped);
+                             nextStartNodeIndex += feasible + failed;
+  PreFilterResult            its node set in Go map order (shuffled);
+  prioritizeNodes            PreScore / Score / NormalizeScore over the feasible
+                             list in completion order, weights (0 -> 1);
+  selectHost                 reservoir sampling, rand.Intn(cnt) == 0 replaces,
+                             over a seeded random.Random (or TB, the engine's
+                             deterministic rule, for the parallelism-1 check);
+  Reserve / Unreserve        the framework's node;
+  PostFilter                 DefaultPreemption over NodeToStatusMap.
+
+The wrapper recording (simulator/scheduler/plugin/wrappedplugin.go) goes into
+a ksim.resultstore.Store as the Go wrapper does, per plugin call.  The random
+interleaving is drawn from ``seed`` only and from the plugins' answers, so two
+runs with plugin sets that answer alike make identical choices.
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import List, Optional
+
+from ksim import abi
+from ksim.fwplugins import ERROR, EnginePlugins, Status
+from ksim.profile import SchedulerProfile, num_feasible_nodes_to_find, original_name
+from ksim.resultstore import PASSED_FILTER_MESSAGE, SUCCESS_MESSAGE, Store
+from ksim.wrapped import HAS_NORMALIZE
+
+
+def chunk_size_for(n: int, parallelism: int) -> int:
+    """parallelize.chunkSizeFor (v1.26)."""
+    s = int(math.sqrt(n))
+    r = n // parallelism + 1
+    if s > r:
+        s = r
+    return max(s, 1)
+
+
+class Framework:
+    def __init__(self, plugins: EnginePlugins, prof: SchedulerProfile, store: Store, seed: int = 0,
+                 parallelism: int = 16, tie: str = "reservoir", tb_seed: int = 0):
+        self.pl = plugins
+        self.prof = prof
+        self.store = store
+        self.rng = random.Random(seed)
+        self.parallelism = parallelism
+        self.tie = tie
+        self.tb_seed = tb_seed
+        self.next_start = 0
+        self.pod_seq = 0
+        self.names = plugins.cluster.node_names
+        self.weights = {p.name: (p.weight or 1) for p in prof.score_plugins()}
+        self.log: List[dict] = []
+
+    # ---- findNodesThatPassFilters (racing Parallelizer) ------------------------
+    def _race(self, nodes: List[int], k: int, ns: str, name: str):
+        n = len(nodes)
+        feasible: List[int] = []
+        status_map = {}
+        evaluated: List[int] = []
+        state = {"length": 0, "cancel": False, "error": None}
+        chunk = chunk_size_for(n, self.parallelism)
+        chunks = list(range((n + chunk - 1) // chunk))
+        workers = [{"chunk": None, "p": None, "end": None, "flight": None, "done": False}
+                   for _ in range(min(self.parallelism, len(chunks)))]
+        slots = [None] * k
+
+        def check_node(i: int):
+            node = nodes[(self.next_start + i) % n]
+            evaluated.append(node)
+            st, ran = self.pl.run_filter_plugins(node)
+            for pl, s in ran:                     # wrappedPlugin.Filter records each call
+                self.store.add_filter_result(ns, name, self.names[node], pl,
+                                             PASSED_FILTER_MESSAGE if s.is_success() else s.message)
+            if st.code == ERROR:
+                if state["error"] is None:
+                    state["error"] = st
+                state["cancel"] = True
+                return
+            if st.is_success():
+                state["length"] += 1
+                if state["length"] > k:
+                    state["cancel"] = True
+                    state["length"] -= 1
+                else:
+                    slots[state["length"] - 1] = node
+            else:
+                status_map[node] = st
+
+        while True:
+            live = [w for w in workers if not w["done"]]
+            if not live:
+                break
+            w = self.rng.choice(live)
+            if w["flight"] is not None:           # finish the piece that passed the ctx check
+                p, w["flight"] = w["flight"], None
+                check_node(p)
+                continue
+            if w["p"] is None or w["p"] >= w["end"]:
+                if not chunks:
+                    w["done"] = True
+                    continue
+                c = chunks.pop(0)
+                w["p"], w["end"] = c * chunk, min(n, (c + 1) * chunk)
+            if state["cancel"]:                   # select { case <-stop: return }
+                w["done"] = True
+                continue
+            w["flight"] = w["p"]
+            w["p"] += 1
+        feasible = slots[:state["length"]]
+        return feasible, status_map, evaluated, state["error"]
+
+    # ---- selectHost -----------------------------------------------------------
+    def _select(self, lst: List[int], totals: List[int], seq: int) -> int:
+        if self.tie == "tb":
+            from oracle.objref import tb_key
+            best = max(range(len(lst)), key=lambda j: tb_key(totals[j], self.tb_seed, seq, lst[j]))
+            return lst[best]
+        best, sel, cnt = totals[0], lst[0], 1
+        for node, t in zip(lst[1:], totals[1:]):
+            if t > best:
+                best, sel, cnt = t, node, 1
+            elif t == best:
+                cnt += 1
+                if self.rng.randrange(cnt) == 0:
+                    sel = node
+        return sel
+
+    # ---- scheduleOne ----------------------------------------------------------
+    def schedule_one(self, pods, index: int, priority: int = 0, bound=None) -> dict:
+        ns, name = pods.names[index]
+        rec = {"pod": index, "chosen": -1, "status": abi.STATUS_UNSCHEDULABLE, "nominated": -1}
+        self.log.append(rec)
+        st, names = self.pl.pre_filter(pods, index)
+        conflict = names is not None and len(names) == 0
+        for p in self.prof.plugins["preFilter"].enabled:
+            plugin = original_name(p.name)
+            if plugin == "NodeAffinity" and names is not None:
+                self.store.add_pre_filter_result(ns, name, plugin, st.message if conflict else SUCCESS_MESSAGE,
+                                                 None if conflict else list(names))
+                if conflict:
+                    break
+            else:
+                self.store.add_pre_filter_result(ns, name, plugin, SUCCESS_MESSAGE, None)
+        seq = self.pod_seq                        # the tie-break sequence of this cycle
+        self.pod_seq += 1
+        if st.code == ERROR:
+            rec["status"], rec["chosen"] = abi.STATUS_ERROR, abi.CHOSEN_ERROR
+            return rec
+        if conflict:
+            for p in self.prof.plugins["postFilter"].enabled:
+                self.store.add_post_filter_result(ns, name, "", original_name(p.name), list(self.names))
+            return rec
+        pos = self.pl.pos
+        if names is None:
+            nodes = list(range(len(self.names)))
+        else:
+            nodes = sorted(pos[x] for x in names)
+            if self.tie != "tb":
+                self.rng.shuffle(nodes)           # Go map iteration order of PreFilterResult.NodeNames
+        k = num_feasible_nodes_to_find(len(nodes), self.prof.percentage_of_nodes_to_score)
+        feasible, status_map, evaluated, err = self._race(nodes, k, ns, name)
+        rec["evaluated"] = evaluated
+        processed = len(feasible) + len(status_map)
+        self.next_start = (self.next_start + processed) % len(nodes)
+        rec["next_start"] = self.next_start
+        rec["feasible"] = list(feasible)
+        rec["failed"] = list(status_map)
+        if err is not None:
+            rec["status"], rec["chosen"] = abi.STATUS_ERROR, abi.CHOSEN_ERROR
+            return rec
+        if not feasible:
+            for p in self.prof.plugins["postFilter"].enabled:
+                nom = -1
+                if original_name(p.name) == "DefaultPreemption" and bound is not None:
+                    pst, nom = self.pl.post_filter(priority, bound)
+                rec["nominated"] = nom
+                self.store.add_post_filter_result(ns, name, self.names[nom] if nom >= 0 else "",
+                                                  original_name(p.name), [self.names[x] for x in status_map])
+            return rec
+        if len(feasible) == 1:
+            chosen = feasible[0]
+        else:
+            splugins = self.prof.score_plugins()
+            if not splugins:
+                totals = [1] * len(feasible)
+            else:
+                for p in self.prof.plugins["preScore"].enabled:
+                    self.store.add_pre_score_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+                pst = self.pl.pre_score(feasible)
+                if pst.code == ERROR:
+                    rec["status"], rec["chosen"] = abi.STATUS_ERROR, abi.CHOSEN_ERROR
+                    return rec
+                totals = [0] * len(feasible)
+                for p in splugins:
+                    raws = [self.pl.score(p.name, x) for x in feasible]
+                    for x, v in zip(feasible, raws):
+                        self.store.add_score_result(ns, name, self.names[x], p.name, v)
+                    vals = raws
+                    if p.name in HAS_NORMALIZE:
+                        vals = self.pl.normalize_score(p.name, feasible, raws)
+                        for x, v in zip(feasible, vals):
+                            self.store.add_normalized_score_result(ns, name, self.names[x], p.name, v)
+                    for j, v in enumerate(vals):
+                        totals[j] += v * self.weights[p.name]
+            chosen = self._select(feasible, totals, seq)
+            rec["totals"] = dict(zip(feasible, totals))
+        # assume (the engine's reserve hook, unrecorded), then the wrapped Reserve plugins
+        self.pl.reserve(chosen)
+        for p in self.prof.plugins["reserve"].enabled:
+            self.store.add_selected_node(ns, name, self.names[chosen])
+            self.store.add_reserve_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+        for p in self.prof.plugins["preBind"].enabled:
+            self.store.add_pre_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+        for p in self.prof.plugins["bind"].enabled:
+            self.store.add_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+        rec["chosen"] = chosen
+        rec["status"] = abi.STATUS_SCHEDULED
+        return rec
+
+
+class OracleBackend:
+    """The C oracle's framework-mode calls under the engine's method names
+    (ksim.fwplugins.EnginePlugins' backend protocol)."""
+
+    def __init__(self, oracle, bound=None):
+        self.o = oracle
+        self.bound = bound
+
+    def fw_prefilter(self, pods, index):
+        return self.o.fw_prefilter(pods, index)
+
+    def fw_score(self, nodes):
+        return self.o.fw_score(nodes)
+
+    def fw_normalize(self, slot, nodes, scores):
+        return self.o.fw_normalize(slot, nodes, scores)
+
+    def assume(self, pods, index, node):
+        self.o.assume(pods, index, node, 1)
+
+    def forget(self, pods, index, node):
+        self.o.assume(pods, index, node, -1)
+
+    def preempt(self, pods, index, priority, bound=None):
+        return self.o.preempt(pods, index, priority, bound if bound is not None else self.bound)
+
+
+class EngineBackend:
+    """ksim.engine.Engine with the bound-pod table argument the oracle takes."""
+
+    def __init__(self, engine):
+        self.e = engine
+        self._bound = None
+
+    def __getattr__(self, k):
+        return getattr(self.e, k)
+
+    def preempt(self, pods, index, priority, bound=None):
+        if bound is not None and bound is not self._bound:
+            self.e.set_bound_pods(bound)
+            self._bound = bound
+        return self.e.preempt(pods, index, priority)
+
+
+def annotations(store: Store, pods, index: int) -> dict:
+    """Every annotation AddStoredResultToPod would write for the pod."""
+    ns, name = pods.names[index]
+    out = {}
+    store.add_stored_result_to_pod(ns, name, out)
+    return out

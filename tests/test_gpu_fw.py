@@ -1,0 +1,167 @@
+"""Framework-driven compat mode on the GPU (ksim_fw_*): the engine answers the
+wrapped plugins under the FRAMEWORK's own choices, as the simulator runs it
+(parallelism 16, percentageOfNodesToScore 0: simulator/scheduler/
+scheduler.go:149,153,231-241).  The framework mirror (tests/fwmirror.py) races
+16 workers over the scan set, breaks ties by reservoir sampling and hands
+Reserve its own node; the same mirror over the C oracle's answers, with the
+same seed, must make the same choices and record the same annotations, and
+both snapshots must end equal."""
+import numpy as np
+import pytest
+
+from ksim import abi, gen, profile
+from ksim.encode import encode_cluster, encode_pods
+from ksim.engine import Engine
+from ksim.fwplugins import EnginePlugins
+from ksim.model import Container, Pod
+from ksim.preemption import bound_table
+from ksim.resultstore import Store
+from oracle.oracle import Oracle
+
+from fwmirror import EngineBackend, Framework, OracleBackend, annotations
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(kind):
+    if kind == "config1":
+        cluster, pods = gen.config1(n_nodes=300, n_pods=300)
+        return cluster, pods, None, None
+    if kind == "prefilter":
+        nodes, pods_o = gen.prefilter_objects(n_nodes=300, n_pods=240)
+        cluster, _ = encode_cluster(nodes, [])
+        return cluster, encode_pods(cluster, pods_o), None, None
+    if kind == "config3":
+        nodes, bound, incoming = gen.config3_objects(n_nodes=400, pods_per_node=4, n_incoming=200)
+        cluster, _ = encode_cluster(nodes, bound)
+        return cluster, encode_pods(cluster, incoming), None, None
+    if kind == "preempt":
+        # crowded config-1 nodes with bound pods of mixed priorities: many
+        # cycles find no node and run DefaultPreemption's PostFilter
+        rng = np.random.default_rng(11)
+        nodes, _ = gen.config1_objects(n_nodes=160, n_pods=1)
+        bound, start = [], {}
+        for ni, n in enumerate(nodes):
+            for k in range(6):
+                nm = f"b{ni}-{k}"
+                bound.append(Pod(nm, node_name=n.name, priority=int(rng.choice([0, 10, 100, 1000])),
+                                 containers=[Container({"cpu": f"{int(rng.integers(2, 12)) * 100}m",
+                                                        "memory": f"{int(rng.integers(1, 6))}Gi"})]))
+                start[nm] = int(rng.integers(0, 50))
+        cluster, _ = encode_cluster(nodes, bound)
+        table = bound_table(cluster, bound, start)
+        pods_o = [Pod(f"p{i}", priority=int(rng.choice([0, 5, 50, 500, 5000])),
+                      containers=[Container({"cpu": f"{int(rng.integers(10, 300)) * 100}m",
+                                             "memory": f"{int(rng.integers(2, 40))}Gi"})]) for i in range(120)]
+        return cluster, encode_pods(cluster, pods_o), table, [p.priority for p in pods_o]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["config1", "prefilter", "config3", "preempt"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_framework_driven_cycles(kind, seed):
+    cluster, pods, table, prio = _cases(kind)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    w = profile.default_score_weights()
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    se, so = Store(w), Store(w)
+    fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, se, seed=seed)
+    fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, so, seed=seed)
+    raced = ties = nominated = 0
+    for i in range(pods.n_pods):
+        p = prio[i] if prio else 0
+        re = fe.schedule_one(pods, i, p, table)
+        ro = fo.schedule_one(pods, i, p, table)
+        for k in ("chosen", "status", "nominated", "feasible", "failed", "evaluated", "next_start", "totals"):
+            assert re.get(k) == ro.get(k), f"pod {i} {k}: engine {re.get(k)} oracle {ro.get(k)}"
+        assert annotations(se, pods, i) == annotations(so, pods, i), f"pod {i} annotations"
+        if "evaluated" in re:
+            raced += len(re["evaluated"]) > len(re["feasible"]) + len(re["failed"])
+        if "totals" in re:
+            t = list(re["totals"].values())
+            ties += t.count(max(t)) > 1
+        nominated += re["nominated"] >= 0
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    if kind != "preempt":
+        assert raced > 0, "no cycle evaluated a feasible node past the K-th"
+    else:
+        assert nominated > 0
+
+
+def test_fw_api_lists_and_normalize():
+    """ksim_fw_prefilter answers every node; ksim_fw_score over arbitrary
+    feasible sublists (any order) and ksim_fw_normalize over lists that are
+    not the scored list equal the oracle's."""
+    nodes, bound, incoming = gen.config3_objects(n_nodes=300, pods_per_node=3, n_incoming=40)
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, incoming)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    ora = Oracle(cluster, prof)
+    rng = np.random.default_rng(5)
+    S = prof.n_score
+    for i in range(pods.n_pods):
+        fe, fo = eng.fw_prefilter(pods, i), ora.fw_prefilter(pods, i)
+        np.testing.assert_array_equal(fe["fail_plugin"], fo["fail_plugin"])
+        np.testing.assert_array_equal(fe["fail_detail"], fo["fail_detail"])
+        assert fe["n_feasible"] == fo["n_feasible"] and fe["k_to_find"] == fo["k_to_find"]
+        assert not (fe["fail_plugin"] == abi.NOT_EVALUATED).any()
+        feas = np.nonzero(fe["fail_plugin"] == abi.PASSED)[0]
+        if feas.size < 2:
+            continue
+        lst = rng.permutation(feas)[:int(rng.integers(2, feas.size + 1))]
+        se, so = eng.fw_score(lst), ora.fw_score(lst)
+        for k in ("raw", "norm", "total", "scored"):
+            np.testing.assert_array_equal(se[k], so[k], err_msg=f"pod {i} {k}")
+        for slot in range(S):
+            sub = rng.permutation(lst)[:int(rng.integers(1, lst.size + 1))]
+            vals = rng.integers(-5, 300, sub.size)
+            np.testing.assert_array_equal(eng.fw_normalize(slot, sub, vals), ora.fw_normalize(slot, sub, vals),
+                                          err_msg=f"pod {i} slot {slot}")
+        node = int(lst[0])
+        eng.assume(pods, i, node)
+        ora.assume(pods, i, node)
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+
+
+def test_fw_rejects_bad_lists_and_abandons_cleanly():
+    """A list with an infeasible or repeated node is refused; a framework
+    cycle left without PreScore (one feasible node) does not leak its
+    PreFilter domain sums into the next deterministic cycle."""
+    nodes, bound, incoming = gen.config3_objects(n_nodes=200, pods_per_node=3, n_incoming=30)
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, incoming)
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=0))
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    ora = Oracle(cluster, prof)
+    f = eng.fw_prefilter(pods, 0)
+    bad = np.nonzero(f["fail_plugin"] != abi.PASSED)[0]
+    good = np.nonzero(f["fail_plugin"] == abi.PASSED)[0]
+    from ksim.engine import KsimError
+    if bad.size:
+        with pytest.raises(KsimError):
+            eng.fw_score([int(good[0]), int(bad[0])])
+    with pytest.raises(KsimError):
+        eng.fw_score([int(good[0]), int(good[0])])
+    # abandoned framework cycles, then deterministic cycles: equal to the oracle's
+    for i in range(1, 10):
+        eng.fw_prefilter(pods, i)
+    ora.set_pod_seq(0)
+    for i in range(10, pods.n_pods):
+        e, o = eng.eval_pod(pods, i), ora.cycle(pods, i)
+        assert e["chosen"] == o["chosen"], i
+        np.testing.assert_array_equal(e["norm"], o["norm"])

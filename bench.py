@@ -347,7 +347,7 @@ def main():
             # C4: every vector's placements, gathered to rank 0 in global order
             local_rows = sweep.order_engine_results([r for _, r in res], len(profs))
             SWEEP["placements"] = sweep.gather_placements(local_rows, rank, world, args.sweep, dist,
-                                                          "cuda" if dist is not None else None)
+                                                          "cuda" if dist is not None else None, n_pods=pods.n_pods)
             parts = [p for p, _ in res if p is not None]
             agg = parts[0]
             for st in parts[1:]:

@@ -9,6 +9,24 @@ namespace ksim {
 constexpr int kHashBits = kBatchPods * kTopT <= 2048 ? 12 : kBatchPods * kTopT <= 4096 ? 13 : 14;
 constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
+
+// KSIM_CHAIN_DELAY builds (the race regression test, tests/test_gpu_chain_race.py):
+// stretch the round boundary the per-parity flags protect.  The last wave
+// sleeps before it reads the round's flag, so the fastest wave (thread 0's,
+// which resets the flag slot) is a whole round ahead when it does; the
+// pre-76f29c9 single flag reset at the top of a round would then be read as
+// "every pod exact" by the sleeping wave.  s_sleep is a scalar ALU wait.
+#ifdef KSIM_CHAIN_DELAY
+#define CHAIN_DELAY(wave_sel)                                                      \
+  do {                                                                             \
+    if ((int)(threadIdx.x >> 6) == (wave_sel)) {                                   \
+      __builtin_amdgcn_s_sleep(127);                                               \
+      __builtin_amdgcn_s_sleep(127);                                               \
+    }                                                                              \
+  } while (0)
+#else
+#define CHAIN_DELAY(wave_sel) do {} while (0)
+#endif
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
 
 struct ChainLds {
@@ -86,6 +104,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
     for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
     if (a >= 0) atomicMin(&s_hold[ra], i);
     __syncthreads();
+    CHAIN_DELAY(1);                            // a middle wave late after the first barrier
     if (i == 0) L.first[par ^ 1] = kBatchPods;
     // every entry's holder at once, then the first one not held by an earlier pod
     int32_t held[kTopT];
@@ -100,6 +119,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
     if (na != a) atomicMin(&L.first[par], i);
     a = na;
     __syncthreads();
+    CHAIN_DELAY((int)(blockDim.x >> 6) - 1);   // the last wave reads the flag late
     first = L.first[par];
     if (first == kBatchPods) break;            // a fixpoint: every pod exact
   }

@@ -110,7 +110,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     if (s_aw && committed > 0) {
       const int2 w = s_aw[committed - 1];
       st->next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
-      st->evals += s_evals;
+      if (c.count_whole) st->evals += s_evals;
     } else {
       st->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);   // the nodes this handle evaluated
     }

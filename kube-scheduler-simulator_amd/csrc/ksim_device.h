@@ -34,6 +34,10 @@ struct DevCluster {
   // of them, except on replicated handles (ksim_set_eval_range), which hold
   // every node and evaluate one range of them
   int32_t eval_lo, eval_hi;
+  // 0 on a replica that is not its group's first (rank 0): the runs every
+  // replica executes whole (per-pod cycles, ADAPT batches) are counted in the
+  // evaluation statistics once, by the first replica
+  int32_t count_whole, _pad_cw;
   const int64_t* alloc_cpu;
   const int64_t* alloc_mem;
   const int64_t* alloc_eph;

@@ -152,6 +152,7 @@ struct ksim_handle {
   // binding every placement: one exchange per batch (the records' all-gather)
   bool replicated = false;
   int32_t eval_lo = 0, eval_hi = 0;
+  bool rep_primary = true;              // replicated: this replica counts the whole-run evaluations
   int32_t rank = 0, world = 1;
   ncclComm_t comm = nullptr;
 
@@ -426,6 +427,7 @@ LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen) {
   a.c = h->dc;
   a.c.eval_lo = 0;                       // every node (replicated shard batches narrow it, shard_batch)
   a.c.eval_hi = a.c.n;
+  a.c.count_whole = (!h->replicated || h->rep_primary) ? 1 : 0;
   a.P = P;
   a.prof = h->prof;
   a.bp = h->bp;
@@ -1186,6 +1188,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   if (h->shard_base < 0 || h->shard_base + n > n_total || n_total > KSIM_MAX_NODES)
     return set_err(h, KSIM_E_INVALID, "shard range outside the cluster (ksim_set_shard)");
   DevCluster c{};
+  c.count_whole = 1;
   c.base = h->shard_base;
   c.n_total = n_total;
   c.n_classes = t->n_classes;
@@ -1372,7 +1375,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
 // Loaded pods, the bound-pod table and captured graphs are dropped (node
 // positions changed).
 int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v, const int32_t* old_pos) {
-  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
+  // (a replica keeps its flag when the delta is refused; the new snapshot
+  // below clears it: ksim_set_eval_range again)
   if (!h || !t || !v) return KSIM_E_INVALID;
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_upsert_nodes before ksim_set_cluster");
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_upsert_nodes on a shard handle");
@@ -2297,6 +2301,10 @@ int ksim_comm_init(ksim_handle* h, int32_t rank, int32_t world, const uint8_t* i
   }
   h->rank = rank;
   h->world = world;
+  if (h->rep_primary != (rank == 0)) {
+    drop_graphs(h);                        // captured with the other counting flag
+    h->rep_primary = rank == 0;
+  }
   return KSIM_OK;
 }
 
@@ -2317,6 +2325,11 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
       if (h->dc.n != h0->dc.n || h->eval_lo != expect)
         return set_err(h0, KSIM_E_INVALID, "eval ranges must tile the cluster in order");
       expect = h->eval_hi;
+      if (h->rep_primary != (h == h0)) {       // the first replica counts whole-run evaluations
+        (void)hipStreamSynchronize(h->stream);
+        drop_graphs(h);
+        h->rep_primary = h == h0;
+      }
       continue;
     }
     if (h->dc.n_total != h0->dc.n_total || h->dc.base != expect)

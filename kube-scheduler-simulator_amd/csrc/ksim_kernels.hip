@@ -956,7 +956,7 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   // a pod PreFilter rejected scans nothing and leaves it
   const int32_t ns = NS > 0 ? (int32_t)(((int64_t)S.next_start + (cut < NS ? cut : NS)) % NS) : S.next_start;
   S.next_start = ns;
-  S.evals += evaluated;
+  if (c.count_whole) S.evals += evaluated;
   if (chosen >= 0) S.scheduled += 1;
   else S.unschedulable += 1;
   if (chosen_out) chosen_out[pi] = chosen >= 0 ? c.base + chosen : error ? KSIM_CHOSEN_ERROR : -1;

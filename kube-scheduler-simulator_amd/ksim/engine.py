@@ -40,61 +40,76 @@ class KsimError(RuntimeError):
         self.code = code
 
 
+_VARIANTS = {}
+
+
+def lib_variant(tag: str):
+    """An A/B or instrumented flavor of the library (same ABI), loaded next to
+    the product build."""
+    if tag not in _VARIANTS:
+        _VARIANTS[tag] = _load(os.path.join(_HERE, f"libksim_engine_{tag}.so"))
+    return _VARIANTS[tag]
+
+
 def lib():
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C kube-scheduler-simulator_amd/csrc` "
-                               "(or __graft_entry__.build()); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
-        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
-        L.ksim_abi_version.restype = ctypes.c_int
-        L.ksim_abi_sizeof.restype = ctypes.c_size_t
-        L.ksim_abi_sizeof.argtypes = [ctypes.c_int]
-        L.ksim_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
-        L.ksim_destroy.argtypes = [vp]
-        L.ksim_destroy.restype = None
-        L.ksim_last_error.argtypes = [vp]
-        L.ksim_last_error.restype = ctypes.c_char_p
-        L.ksim_set_profile.argtypes = [vp, vp]
-        L.ksim_set_cluster.argtypes = [vp, vp, vp]
-        L.ksim_upsert_nodes.argtypes = [vp, vp, vp, vp]
-        L.ksim_remove_node.argtypes = [vp, i32]
-        L.ksim_get_node_state.argtypes = [vp] * 7
-        L.ksim_get_class_count.argtypes = [vp, vp]
-        L.ksim_get_nb_alloc.argtypes = [vp, vp]
-        L.ksim_get_next_start.argtypes = [vp, vp]
-        L.ksim_set_next_start.argtypes = [vp, i32]
-        L.ksim_set_pod_seq.argtypes = [vp, i64]
-        L.ksim_eval_pod.argtypes = [vp, vp, i32, vp]
-        L.ksim_eval_pod_filter.argtypes = [vp, vp, i32, vp]
-        L.ksim_set_bound_pods.argtypes = [vp, vp]
-        L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
-        L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
-        L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
-        L.ksim_set_eval_range.argtypes = [vp, i32, i32]
-        L.ksim_fw_prefilter.argtypes = [vp, vp, i32, vp]
-        L.ksim_fw_score.argtypes = [vp, vp, i32, vp]
-        L.ksim_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
-        L.ksim_assume.argtypes = [vp, vp, i32, i32]
-        L.ksim_forget.argtypes = [vp, vp, i32, i32]
-        L.ksim_load_pods.argtypes = [vp, vp]
-        L.ksim_schedule_loaded.argtypes = [vp, i32, i32, vp, vp]
-        L.ksim_schedule_batch.argtypes = [vp, vp, vp, vp]
-        L.ksim_reset_cluster.argtypes = [vp]
-        L.ksim_time_kernels.argtypes = [vp, i32, i32, vp, vp, i32]
-        L.ksim_kernel_name.argtypes = [i32]
-        L.ksim_emit_cycle_json.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp]
-        L.ksim_time_eval.argtypes = [vp, i32, i32, vp, vp]
-        L.ksim_kernel_name.restype = ctypes.c_char_p
-        L.ksim_get_diag.argtypes = [vp, vp, i32]
-        L.ksim_batch_geometry.argtypes = [vp, i32]
-        L.ksim_set_shard.argtypes = [vp, i32, i32]
-        L.ksim_comm_unique_id.argtypes = [vp]
-        L.ksim_comm_init.argtypes = [vp, i32, i32, vp]
-        L.ksim_group_schedule_loaded.argtypes = [vp, i32, i32, i32, vp, vp]
-        _LIB = L
+        _LIB = _load(LIB_PATH)
     return _LIB
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: build it with `make -C kube-scheduler-simulator_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(path)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    L.ksim_abi_version.restype = ctypes.c_int
+    L.ksim_abi_sizeof.restype = ctypes.c_size_t
+    L.ksim_abi_sizeof.argtypes = [ctypes.c_int]
+    L.ksim_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.ksim_destroy.argtypes = [vp]
+    L.ksim_destroy.restype = None
+    L.ksim_last_error.argtypes = [vp]
+    L.ksim_last_error.restype = ctypes.c_char_p
+    L.ksim_set_profile.argtypes = [vp, vp]
+    L.ksim_set_cluster.argtypes = [vp, vp, vp]
+    L.ksim_upsert_nodes.argtypes = [vp, vp, vp, vp]
+    L.ksim_remove_node.argtypes = [vp, i32]
+    L.ksim_get_node_state.argtypes = [vp] * 7
+    L.ksim_get_class_count.argtypes = [vp, vp]
+    L.ksim_get_nb_alloc.argtypes = [vp, vp]
+    L.ksim_get_next_start.argtypes = [vp, vp]
+    L.ksim_set_next_start.argtypes = [vp, i32]
+    L.ksim_set_pod_seq.argtypes = [vp, i64]
+    L.ksim_eval_pod.argtypes = [vp, vp, i32, vp]
+    L.ksim_eval_pod_filter.argtypes = [vp, vp, i32, vp]
+    L.ksim_set_bound_pods.argtypes = [vp, vp]
+    L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
+    L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
+    L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
+    L.ksim_set_eval_range.argtypes = [vp, i32, i32]
+    L.ksim_fw_prefilter.argtypes = [vp, vp, i32, vp]
+    L.ksim_fw_score.argtypes = [vp, vp, i32, vp]
+    L.ksim_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
+    L.ksim_assume.argtypes = [vp, vp, i32, i32]
+    L.ksim_forget.argtypes = [vp, vp, i32, i32]
+    L.ksim_load_pods.argtypes = [vp, vp]
+    L.ksim_schedule_loaded.argtypes = [vp, i32, i32, vp, vp]
+    L.ksim_schedule_batch.argtypes = [vp, vp, vp, vp]
+    L.ksim_reset_cluster.argtypes = [vp]
+    L.ksim_time_kernels.argtypes = [vp, i32, i32, vp, vp, i32]
+    L.ksim_kernel_name.argtypes = [i32]
+    L.ksim_emit_cycle_json.argtypes = [vp, vp, i64, vp, i64, vp, i64, vp]
+    L.ksim_time_eval.argtypes = [vp, i32, i32, vp, vp]
+    L.ksim_kernel_name.restype = ctypes.c_char_p
+    L.ksim_get_diag.argtypes = [vp, vp, i32]
+    L.ksim_batch_geometry.argtypes = [vp, i32]
+    L.ksim_set_shard.argtypes = [vp, i32, i32]
+    L.ksim_comm_unique_id.argtypes = [vp]
+    L.ksim_comm_init.argtypes = [vp, i32, i32, vp]
+    L.ksim_group_schedule_loaded.argtypes = [vp, i32, i32, i32, vp, vp]
+    return L
 
 
 def batch_geometry() -> dict:
@@ -122,19 +137,24 @@ def group_schedule_loaded(engines, first: int, count: int):
     arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
     chosen = np.zeros(count, np.int32)
     st = abi.BatchStats()
-    rc = lib().ksim_group_schedule_loaded(arr, len(engines), first, count,
-                                          chosen.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
+    L = engines[0].L
+    rc = L.ksim_group_schedule_loaded(arr, len(engines), first, count,
+                                      chosen.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st))
     if rc != 0:
-        raise KsimError(rc, lib().ksim_last_error(engines[0].h).decode())
+        raise KsimError(rc, L.ksim_last_error(engines[0].h).decode())
     return chosen, st
 
 
 class Engine:
     """One engine handle on one GPU (one scheduler profile, one snapshot)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, variant: Optional[str] = None):
+        # variant: an instrumented / experimental build of the same ABI
+        # (csrc/Makefile "flavor": libksim_engine_<variant>.so), e.g. the
+        # chain-delay build of the race regression test
+        self.L = lib() if variant is None else lib_variant(variant)
         h = ctypes.c_void_p()
-        rc = lib().ksim_create(device, ctypes.byref(h))
+        rc = self.L.ksim_create(device, ctypes.byref(h))
         if rc != 0:
             raise KsimError(rc, f"ksim_create(device={device}) failed (no GPU / HIP runtime?)")
         self.h = h
@@ -146,34 +166,36 @@ class Engine:
 
     def _chk(self, rc: int):
         if rc != 0:
-            raise KsimError(rc, lib().ksim_last_error(self.h).decode())
+            raise KsimError(rc, self.L.ksim_last_error(self.h).decode())
 
     def close(self):
-        if getattr(self, "h", None) and _LIB is not None:
-            _LIB.ksim_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "L", None) is not None:
+            self.L.ksim_destroy(self.h)
         self.h = None
 
     __del__ = close
 
     def set_shard(self, node_base: int, n_total: int):
         """This handle holds global node positions [node_base, node_base + n) of n_total."""
-        self._chk(lib().ksim_set_shard(self.h, node_base, n_total))
+        self._chk(self.L.ksim_set_shard(self.h, node_base, n_total))
+        self._split = True
 
     def set_eval_range(self, lo: int, hi: int):
         """Replicated sharding: this handle (whole cluster) evaluates nodes [lo, hi)."""
-        self._chk(lib().ksim_set_eval_range(self.h, lo, hi))
+        self._chk(self.L.ksim_set_eval_range(self.h, lo, hi))
+        self._split = True
 
     def comm_init(self, rank: int, world: int, uid: bytes):
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
-        self._chk(lib().ksim_comm_init(self.h, rank, world, buf))
+        self._chk(self.L.ksim_comm_init(self.h, rank, world, buf))
 
     def set_profile(self, prof: abi.Profile):
-        self._chk(lib().ksim_set_profile(self.h, ctypes.byref(prof)))
+        self._chk(self.L.ksim_set_profile(self.h, ctypes.byref(prof)))
         self.n_score = prof.n_score
 
     def set_cluster(self, cluster):
         nt, vo = cluster.node_table(), cluster.vocab()
-        self._chk(lib().ksim_set_cluster(self.h, ctypes.byref(nt), ctypes.byref(vo)))
+        self._chk(self.L.ksim_set_cluster(self.h, ctypes.byref(nt), ctypes.byref(vo)))
         self._track(cluster, nt)
         self._ran = False
 
@@ -190,7 +212,7 @@ class Engine:
         op = np.ascontiguousarray(old_pos, np.int32)
         if op.size != cluster.n_nodes:
             raise ValueError("old_pos must have one entry per node of the new snapshot")
-        self._chk(lib().ksim_upsert_nodes(self.h, ctypes.byref(nt), ctypes.byref(vo),
+        self._chk(self.L.ksim_upsert_nodes(self.h, ctypes.byref(nt), ctypes.byref(vo),
                                           op.ctypes.data_as(ctypes.c_void_p)))
         self._track(cluster, nt)
         self._keep = []
@@ -198,7 +220,7 @@ class Engine:
     def remove_node(self, pos: int):
         """RemoveNode of the node at ``pos`` (ksim_remove_node); the host
         snapshot object is no longer the engine's (positions moved)."""
-        self._chk(lib().ksim_remove_node(self.h, pos))
+        self._chk(self.L.ksim_remove_node(self.h, pos))
         self.n_nodes -= 1
         self.cluster = None
         self._keep = []
@@ -210,6 +232,11 @@ class Engine:
         c = getattr(self, "cluster", None)
         if c is None or (c.n_label_cols, int(c.class_count.shape[0])) == self._layout:
             return
+        if getattr(self, "_split", False):
+            # a shard or a replica must not turn into a whole-snapshot handle
+            # behind its group's back: encode every pod before sharding
+            raise RuntimeError("pods encoded after the cluster was sharded / replicated added label columns or "
+                               "count classes: encode every pod before shard() / set_cluster")
         if int(c.class_count.shape[0]) != self._layout[1] and self._ran:
             raise RuntimeError("count classes were registered after cycles ran on this engine: "
                                "encode every pod before scheduling, or re-send the snapshot (upsert_nodes)")
@@ -218,13 +245,13 @@ class Engine:
     def class_count(self) -> np.ndarray:
         """Count classes [n_classes][n_nodes] as the device holds them now."""
         out = np.zeros((self.n_classes, self.n_nodes), np.int32)
-        self._chk(lib().ksim_get_class_count(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        self._chk(self.L.ksim_get_class_count(self.h, out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
     def nb_alloc(self) -> np.ndarray:
         """NetworkBandwidth allocated amount per node (milli-units), as the device holds it."""
         out = np.zeros(self.n_nodes, np.int64)
-        self._chk(lib().ksim_get_nb_alloc(self.h, out.ctypes.data_as(ctypes.c_void_p)))
+        self._chk(self.L.ksim_get_nb_alloc(self.h, out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
     def eval_pod(self, pods, index: int) -> dict:
@@ -232,7 +259,7 @@ class Engine:
         self._ran = True
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
         ps = pods.pod_set()
-        self._chk(lib().ksim_eval_pod(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        self._chk(self.L.ksim_eval_pod(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
         return buf.result()
 
     def eval_pod_extenders(self, pods, index: int, extender) -> dict:
@@ -243,12 +270,12 @@ class Engine:
         self._ran = True
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
         ps = pods.pod_set()
-        self._chk(lib().ksim_eval_pod_filter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        self._chk(self.L.ksim_eval_pod_filter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
         ef, es = extender(buf.result())
         ef = None if ef is None else np.ascontiguousarray(ef, np.uint8)
         es = None if es is None else np.ascontiguousarray(es, np.int64)
         buf2 = abi.EvalBuffers(self.n_nodes, self.n_score)
-        self._chk(lib().ksim_eval_pod_finish(self.h, None if ef is None else ef.ctypes.data_as(ctypes.c_void_p),
+        self._chk(self.L.ksim_eval_pod_finish(self.h, None if ef is None else ef.ctypes.data_as(ctypes.c_void_p),
                                              None if es is None else es.ctypes.data_as(ctypes.c_void_p),
                                              ctypes.byref(buf2.out)))
         return buf2.result()
@@ -261,14 +288,14 @@ class Engine:
         self._ran = True
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
         ps = pods.pod_set()
-        self._chk(lib().ksim_fw_prefilter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
+        self._chk(self.L.ksim_fw_prefilter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
         return buf.result()
 
     def fw_score(self, nodes) -> dict:
         """PreScore / Score / NormalizeScore over exactly the framework's feasible list."""
         arr = np.ascontiguousarray(nodes, np.int32)
         buf = abi.EvalBuffers(self.n_nodes, self.n_score)
-        self._chk(lib().ksim_fw_score(self.h, arr.ctypes.data_as(ctypes.c_void_p), arr.size,
+        self._chk(self.L.ksim_fw_score(self.h, arr.ctypes.data_as(ctypes.c_void_p), arr.size,
                                       ctypes.byref(buf.out)))
         return buf.result()
 
@@ -279,7 +306,7 @@ class Engine:
         if nd.size != sc.size:
             raise ValueError("one score per node")
         out = np.zeros(nd.size, np.int64)
-        self._chk(lib().ksim_fw_normalize(self.h, slot, nd.ctypes.data_as(ctypes.c_void_p),
+        self._chk(self.L.ksim_fw_normalize(self.h, slot, nd.ctypes.data_as(ctypes.c_void_p),
                                           sc.ctypes.data_as(ctypes.c_void_p), nd.size,
                                           out.ctypes.data_as(ctypes.c_void_p)))
         return out
@@ -287,7 +314,7 @@ class Engine:
     def set_bound_pods(self, bound):
         """The bound-pod table DefaultPreemption may evict (ksim.abi.BoundPods)."""
         self._bound_n = bound.n
-        self._chk(lib().ksim_set_bound_pods(self.h, ctypes.byref(bound.c)))
+        self._chk(self.L.ksim_set_bound_pods(self.h, ctypes.byref(bound.c)))
 
     def preempt(self, pods, index: int, priority: int) -> tuple:
         """DefaultPreemption PostFilter dry run: (nominated node or -1, victim
@@ -296,7 +323,7 @@ class Engine:
         self._ran = True
         out = abi.PreemptOut(max(getattr(self, "_bound_n", 1), 1))
         ps = pods.pod_set()
-        self._chk(lib().ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
+        self._chk(self.L.ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
         return out.result()
 
     def match_terms(self, mp: abi.MatchProblem, n_words: int, counts: Optional[np.ndarray]) -> np.ndarray:
@@ -304,7 +331,7 @@ class Engine:
         ([n_classes][n_nodes] int32, or None) receives the class counts."""
         bits = np.zeros((max(mp.n_sigs, 1), max(n_words, 1)), np.uint32)
         cp = None if counts is None else counts.ctypes.data_as(ctypes.c_void_p)
-        self._chk(lib().ksim_match_terms(self.h, ctypes.byref(mp), bits.ctypes.data_as(ctypes.c_void_p), cp))
+        self._chk(self.L.ksim_match_terms(self.h, ctypes.byref(mp), bits.ctypes.data_as(ctypes.c_void_p), cp))
         return bits[:mp.n_sigs, :n_words]
 
     def last_match_ms(self) -> float:
@@ -315,25 +342,25 @@ class Engine:
         self._sync()
         self._ran = True
         ps = pods.pod_set()
-        self._chk(lib().ksim_assume(self.h, ctypes.byref(ps), index, node))
+        self._chk(self.L.ksim_assume(self.h, ctypes.byref(ps), index, node))
 
     def forget(self, pods, index: int, node: int):
         self._sync()
         self._ran = True
         ps = pods.pod_set()
-        self._chk(lib().ksim_forget(self.h, ctypes.byref(ps), index, node))
+        self._chk(self.L.ksim_forget(self.h, ctypes.byref(ps), index, node))
 
     def load_pods(self, pods):
         self._sync()
         ps = pods.pod_set()
-        self._chk(lib().ksim_load_pods(self.h, ctypes.byref(ps)))
+        self._chk(self.L.ksim_load_pods(self.h, ctypes.byref(ps)))
         self._keep = [pods]
 
     def schedule_loaded(self, first: int, count: int, want_chosen: bool = True):
         chosen = np.zeros(count, np.int32) if want_chosen else None
         st = abi.BatchStats()
         self._ran = True
-        self._chk(lib().ksim_schedule_loaded(
+        self._chk(self.L.ksim_schedule_loaded(
             self.h, first, count, chosen.ctypes.data_as(ctypes.c_void_p) if chosen is not None else None,
             ctypes.byref(st)))
         return chosen, st
@@ -348,29 +375,29 @@ class Engine:
         out["num_pods"] = np.zeros(n, np.int32)
         a = [out[k].ctypes.data_as(ctypes.c_void_p) for k in
              ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")]
-        self._chk(lib().ksim_get_node_state(self.h, *a))
+        self._chk(self.L.ksim_get_node_state(self.h, *a))
         return out
 
     @property
     def next_start(self) -> int:
         v = ctypes.c_int32()
-        self._chk(lib().ksim_get_next_start(self.h, ctypes.byref(v)))
+        self._chk(self.L.ksim_get_next_start(self.h, ctypes.byref(v)))
         return v.value
 
     def set_next_start(self, s: int):
-        self._chk(lib().ksim_set_next_start(self.h, s))
+        self._chk(self.L.ksim_set_next_start(self.h, s))
 
     def set_pod_seq(self, s: int):
-        self._chk(lib().ksim_set_pod_seq(self.h, s))
+        self._chk(self.L.ksim_set_pod_seq(self.h, s))
 
     def reset_cluster(self):
         """Restore the uploaded snapshot's dynamic node state (device-side copy)."""
-        self._chk(lib().ksim_reset_cluster(self.h))
+        self._chk(self.L.ksim_reset_cluster(self.h))
 
     def diag(self) -> dict:
         """Batch-path diagnostics of the last schedule_loaded call."""
         out = np.zeros(21, np.int64)
-        n = lib().ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 21)
+        n = self.L.ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 21)
         if n < 0:
             self._chk(n)
         d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2]),
@@ -384,8 +411,8 @@ class Engine:
         """(kernel name, mean ms) of the evaluation kernel launched back to back (ksim_time_eval)."""
         ms = ctypes.c_double()
         k = ctypes.c_int32()
-        self._chk(lib().ksim_time_eval(self.h, first, reps, ctypes.byref(ms), ctypes.byref(k)))
-        return lib().ksim_kernel_name(k.value).decode(), ms.value
+        self._chk(self.L.ksim_time_eval(self.h, first, reps, ctypes.byref(ms), ctypes.byref(k)))
+        return self.L.ksim_kernel_name(k.value).decode(), ms.value
 
     def time_kernels(self, first: int, count: int) -> dict:
         """Schedule loaded pods [first, first+count) with HIP events between the
@@ -393,11 +420,11 @@ class Engine:
         for every kernel that ran."""
         out = np.zeros(32, np.float64)
         cnt = np.zeros(32, np.int64)
-        n = lib().ksim_time_kernels(self.h, first, count, out.ctypes.data_as(ctypes.c_void_p),
+        n = self.L.ksim_time_kernels(self.h, first, count, out.ctypes.data_as(ctypes.c_void_p),
                                     cnt.ctypes.data_as(ctypes.c_void_p), 32)
         if n < 0:
             self._chk(n)
-        return {lib().ksim_kernel_name(k).decode(): (float(out[k]), int(cnt[k]))
+        return {self.L.ksim_kernel_name(k).decode(): (float(out[k]), int(cnt[k]))
                 for k in range(n) if cnt[k] > 0}
 
 

@@ -25,13 +25,18 @@ def rank_vectors(n_vectors: int, rank: int, world: int) -> List[int]:
 
 
 def gather_placements(local: np.ndarray, rank: int, world: int, n_vectors: int, dist=None,
-                      device: Optional[str] = None) -> Optional[np.ndarray]:
+                      device: Optional[str] = None, n_pods: Optional[int] = None) -> Optional[np.ndarray]:
     """All ranks' [local vectors][pods] placement rows -> the [n_vectors][pods]
     matrix in global vector order on rank 0 (None elsewhere).  ``dist``: the
     torch.distributed module of an initialized process group (RCCL on GPU
-    tensors, gloo on CPU); None for one process."""
+    tensors, gloo on CPU); None for one process.  ``n_pods``: the queue length,
+    which every rank must send alike (a rank with no vectors has no rows to read
+    it from); taken from ``local`` when omitted."""
     local = np.ascontiguousarray(local, np.int32)
-    n_pods = local.shape[1] if local.ndim == 2 else 0
+    if n_pods is None:
+        n_pods = local.shape[1] if local.ndim == 2 and local.shape[0] else 0
+    if local.size == 0:
+        local = np.zeros((0, n_pods), np.int32)
     if dist is None or world == 1:
         out = np.full((n_vectors, n_pods), -3, np.int32)
         out[rank_vectors(n_vectors, 0, 1)] = local

@@ -85,10 +85,13 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
 
 
 def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, ns: str, name: str,
-                 res: Dict, prefilter_names: Optional[List[str]] = None) -> None:
+                 res: Dict, prefilter_names: Optional[List[str]] = None, nominated: int = -1) -> None:
     """Feed ``store`` with one compat-mode cycle result (engine or oracle).
     ``prefilter_names``: the pod's NodeAffinity PreFilterResult.NodeNames
-    (EncodedPods.prefilter_names; None = all nodes, [] = conflicting terms)."""
+    (EncodedPods.prefilter_names; None = all nodes, [] = conflicting terms).
+    ``nominated``: DefaultPreemption's nominated node of an unschedulable cycle
+    (ksim_preempt; -1 none), which wrappedPlugin.PostFilter records as
+    "preemption victim" (wrappedplugin.go:529-538, store.go:437-452)."""
     names = cluster.node_names
     conflict = prefilter_names is not None and len(prefilter_names) == 0
     for p in prof.plugins["preFilter"].enabled:
@@ -136,7 +139,8 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
     if res["status"] == abi.STATUS_UNSCHEDULABLE:
         failed = [names[i] for i in range(cluster.n_nodes) if fp[i] not in (abi.PASSED, abi.NOT_EVALUATED)]
         for p in prof.plugins["postFilter"].enabled:
-            store.add_post_filter_result(ns, name, "", original_name(p.name), failed)
+            nom = names[nominated] if nominated >= 0 and original_name(p.name) == "DefaultPreemption" else ""
+            store.add_post_filter_result(ns, name, nom, original_name(p.name), failed)
         return
     if res["n_feasible"] > 1:
         for p in prof.plugins["preScore"].enabled:
@@ -158,6 +162,29 @@ def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, 
         store.add_pre_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
     for p in prof.plugins["bind"].enabled:
         store.add_bind_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
+
+
+def compat_cycle(backend, store: Store, cluster: EncodedCluster, prof: SchedulerProfile, pods, index: int,
+                 priority: int = 0, bound=None) -> Dict:
+    """One deterministic compat cycle as the wrapped plugins see it: the cycle
+    (ksim_eval_pod), then for an unschedulable pod DefaultPreemption's
+    PostFilter dry run (ksim_preempt over the bound-pod table set with
+    set_bound_pods) when the profile enables it, recorded into ``store``.
+    ``backend`` is an Engine (or the oracle, whose preempt takes ``bound``)."""
+    res = backend.eval_pod(pods, index) if hasattr(backend, "eval_pod") else backend.cycle(pods, index)
+    nominated = -1
+    post = [original_name(p.name) for p in prof.plugins["postFilter"].enabled]
+    if res["status"] == abi.STATUS_UNSCHEDULABLE and "DefaultPreemption" in post:
+        names = pods.prefilter_names[index] if pods.prefilter_names else None
+        if not (names is not None and len(names) == 0):
+            out = backend.preempt(pods, index, priority) if bound is None else \
+                backend.preempt(pods, index, priority, bound)
+            nominated = int(out[0])
+    res["nominated"] = nominated
+    ns, name = pods.names[index]
+    record_cycle(store, cluster, prof, ns, name, res,
+                 pods.prefilter_names[index] if pods.prefilter_names else None, nominated)
+    return res
 
 
 def emit_cycle_annotations(cluster: EncodedCluster, prof: SchedulerProfile, res: Dict,

@@ -165,3 +165,28 @@ def test_fw_rejects_bad_lists_and_abandons_cleanly():
         e, o = eng.eval_pod(pods, i), ora.cycle(pods, i)
         assert e["chosen"] == o["chosen"], i
         np.testing.assert_array_equal(e["norm"], o["norm"])
+
+
+def test_compat_cycle_postfilter_nominated():
+    """Deterministic compat cycles with DefaultPreemption's PostFilter: the
+    engine's nominated node (ksim_preempt) and the recorded annotations equal
+    the oracle's."""
+    from ksim.wrapped import compat_cycle
+    cluster, pods, table, prio = _cases("preempt")
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    w = profile.default_score_weights()
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    eng.set_bound_pods(table)
+    ora = Oracle(cluster.copy_state(), prof)
+    se, so = Store(w), Store(w)
+    nominated = 0
+    for i in range(pods.n_pods):
+        re = compat_cycle(eng, se, cluster, sp, pods, i, prio[i])
+        ro = compat_cycle(ora, so, cluster, sp, pods, i, prio[i], table)
+        assert re["chosen"] == ro["chosen"] and re["nominated"] == ro["nominated"], i
+        assert annotations(se, pods, i) == annotations(so, pods, i), i
+        nominated += re["nominated"] >= 0
+    assert nominated > 0

@@ -52,3 +52,40 @@ def test_preempt_oracle_vs_objref(seed):
         assert [bound[v].name for v in victims] == rvictims, f"pod {i}"
         nominated += node >= 0
     assert 0 < nominated < len(pods)
+
+
+def test_postfilter_records_nominated_node():
+    """wrappedPlugin.PostFilter records the nominated node of DefaultPreemption
+    as "preemption victim" and "" otherwise (wrappedplugin.go:529-538,
+    store.go:437-452): compat_cycle feeds ksim_preempt's pick into the store."""
+    import json
+    from ksim.resultstore import POSTFILTER_RESULT, POST_FILTER_NOMINATED_MESSAGE, Store
+    from ksim.wrapped import compat_cycle
+    nodes, bound, start, order = crowded(seed=4)
+    cluster, _ = encode_cluster(nodes, bound)
+    table = bound_table(cluster, bound, start)
+    rng = np.random.default_rng(104)
+    pods = [Pod(f"p{i}", priority=int(rng.choice([0, 5, 50, 500, 5000])),
+                containers=[Container({"cpu": f"{int(rng.integers(10, 400)) * 100}m",
+                                       "memory": f"{int(rng.integers(4, 40))}Gi"})]) for i in range(30)]
+    enc = encode_pods(cluster, pods)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    ora = Oracle(cluster, profile.compile_profile(sp))
+    ref = Oracle(cluster.copy_state(), profile.compile_profile(sp))
+    store = Store(profile.default_score_weights())
+    seen = 0
+    for i, pod in enumerate(pods):
+        res = compat_cycle(ora, store, cluster, sp, enc, i, pod.priority, table)
+        ann = {}
+        store.add_stored_result_to_pod(*enc.names[i], ann)
+        if res["status"] != 1:
+            ref.cycle(enc, i)
+            continue
+        want, _, _, _ = ref.preempt(enc, i, pod.priority, table)
+        ref.cycle(enc, i)
+        assert res["nominated"] == want
+        post = json.loads(ann[POSTFILTER_RESULT])
+        marked = [n for n, v in post.items() if v.get("DefaultPreemption") == POST_FILTER_NOMINATED_MESSAGE]
+        assert marked == ([cluster.node_names[want]] if want >= 0 else [])
+        seen += want >= 0
+    assert seen > 0

@@ -32,7 +32,7 @@ def _worker(rank, world, port, n_vectors, n_pods, q):
         J = 3                                            # engines per rank
         results = [[_rows(mine[k], n_pods) for k in range(j, len(mine), J)] for j in range(J)]
         rows = sweep.order_engine_results(results, len(mine))
-        out = sweep.gather_placements(rows, rank, world, n_vectors, dist)
+        out = sweep.gather_placements(rows, rank, world, n_vectors, dist, n_pods=n_pods)
         q.put((rank, None if out is None else out.tolist()))
     finally:
         dist.destroy_process_group()
@@ -44,7 +44,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,n_vectors", [(2, 9), (3, 10)])
+@pytest.mark.parametrize("world,n_vectors", [(2, 9), (3, 10), (3, 2)])
 def test_gather_placements_gloo(world, n_vectors):
     n_pods = 17
     ctx = mp.get_context("spawn")

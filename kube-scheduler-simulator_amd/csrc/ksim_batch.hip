@@ -118,6 +118,8 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
   }
 }
 
+__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g);
+
 // ---- k_batch_top: evaluation and the pod's top-T in one launch -------------------
 // One block per pod of the batch (kTopThreads threads, kTopWaves waves: two per
 // SIMD when every CU holds one block), the nodes strided over its lanes.  Each
@@ -131,7 +133,10 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
 // every S0-feasible node is in the pod's list.  This replaces k_batch_eval's
 // per-tile lists and the k_batch_merge launch.
 #ifndef KSIM_TOP_STEP
-#define KSIM_TOP_STEP 2
+#define KSIM_TOP_STEP 1
+#endif
+#ifndef KSIM_TOP_THRESH
+#define KSIM_TOP_THRESH 1   // the threshold top-T (0: the round-by-round extraction and block merge, for A/B)
 #endif
 constexpr int kTopStep = KSIM_TOP_STEP;   // nodes per lane per step of the FAST loop
 
@@ -163,6 +168,10 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
   int32_t nfeas = 0;
   if constexpr (FAST) {
+    // the loop-invariant key inputs in registers (SGPRs): the profile's batch
+    // program and the pod's request fields, loaded once
+    const FastProg bq = fast_prog(bp);
+    const ksim_pod pf = fast_pod_fields(p);
     // kTopStep nodes per step as independent chains (every row loaded up front)
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
@@ -180,7 +189,9 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
 #pragma unroll
       for (int u = 0; u < kTopStep; u++) {
         const int32_t nu = node + u * kTopThreads;
-        const uint64_t k = nu < c.eval_hi ? dyn_key_fast(bp, p, r[u], ic[u], im[u], hseed, c.base + nu) : 0;
+        // computed for every slot (a slot past the range keys a valid node) and masked
+        const uint64_t k0 = dyn_key_fast(bq, pf, r[u], ic[u], im[u], hseed, c.base + (nu < c.eval_hi ? nu : node));
+        const uint64_t k = nu < c.eval_hi ? k0 : 0;
         nfeas += k != 0;
         a[3] = umax64(a[3], k);
         cswap_desc(a[2], a[3]);
@@ -189,19 +200,106 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
       }
     }
   }
+  if constexpr (!FAST) {                      // the generic loop is not compiled into FAST kernels
 #pragma unroll 1
-  for (int32_t node = c.eval_lo + threadIdx.x; node < (FAST ? 0 : c.eval_hi); node += kTopThreads) {
-    uint64_t kk = 0;
-    {
-      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+      uint64_t kk = 0;
+      {
+        const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+      }
+      nfeas += kk != 0;
+      a[3] = umax64(a[3], kk);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
     }
-    nfeas += kk != 0;
-    a[3] = umax64(a[3], kk);
-    cswap_desc(a[2], a[3]);
-    cswap_desc(a[1], a[2]);
-    cswap_desc(a[0], a[1]);
   }
+#if KSIM_TOP_THRESH
+  // ---- the pod's top-T by threshold (default) ------------------------------
+  // Provability: a lane that had more feasible nodes than it kept hides keys
+  // below its last kept key, so every key >= thr (the largest such key over
+  // the block; 0 when no lane overflowed) is in the exact order.  Pruning:
+  // the T-th largest of the waves' maxima, L, is <= the T-th largest key, so
+  // the pod's top-T lies among the kept keys >= cut = max(thr, L).  Those
+  // candidates (a prefix of each lane's sorted list) go to LDS by prefix
+  // sums, and one wave ranks them: no serial extraction rounds.  A block
+  // with more than 64 candidates (a long L tie region cannot happen: keys
+  // are unique) takes the round-by-round extraction below.
+  {
+    __shared__ uint64_t s_wmax[kTopWaves], s_wthr[kTopWaves];
+    __shared__ int32_t s_wc[kTopWaves], s_wf[kTopWaves];
+    __shared__ uint64_t s_cand[64];
+    const uint64_t u = nfeas > kTileCand ? a[kTileCand - 1] : 0;
+    const uint64_t wthr = wave_max_u64_dpp(u);
+    const uint64_t wmax = wave_max_u64_dpp(a[0]);
+    int32_t fsum = nfeas;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) fsum += __shfl_xor(fsum, m, 64);
+    if (lane == 0) {
+      s_wmax[wv] = wmax;
+      s_wthr[wv] = wthr;
+      s_wf[wv] = fsum;
+    }
+    __syncthreads();
+    uint64_t thr = 0, mine_w = lane < kTopWaves ? s_wmax[lane] : 0;
+    int32_t total = 0, rank = 0;
+#pragma unroll
+    for (int w = 0; w < kTopWaves; w++) {
+      const uint64_t o = s_wmax[w];               // LDS broadcast
+      thr = umax64(thr, s_wthr[w]);
+      total += s_wf[w];
+      rank += o > mine_w;
+    }
+    const uint64_t at = __ballot(lane < kTopWaves && mine_w != 0 && rank == kTopT - 1);
+    const uint64_t L = at ? readlane_u64(mine_w, __builtin_ctzll(at)) : 0;
+    const uint64_t cut = umax64(umax64(thr, L), 1);   // keys are nonzero
+    int32_t cl = 0;
+#pragma unroll
+    for (int q = 0; q < kTileCand; q++) cl += a[q] >= cut;   // lists are sorted: a prefix
+    int32_t pre = cl;                              // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(pre, d, 64);
+      if (lane >= d) pre += y;
+    }
+    if (lane == 63) s_wc[wv] = pre;
+    __syncthreads();
+    int32_t off = 0, C = 0;
+#pragma unroll
+    for (int w = 0; w < kTopWaves; w++) {
+      const int32_t x = s_wc[w];
+      off += w < wv ? x : 0;
+      C += x;
+    }
+    if (C <= 64) {                                 // block-uniform
+      const int32_t base_i = off + pre - cl;
+#pragma unroll
+      for (int q = 0; q < kTileCand; q++)
+        if (q < cl) s_cand[base_i + q] = a[q];
+      __syncthreads();
+      if (wv != 0) return;
+      const uint64_t c0 = lane < C ? s_cand[lane] : 0;
+      int32_t r = 0;
+      for (int j = 0; j < C; j++) r += s_cand[j] > c0;   // keys are unique: ranks are distinct
+      const int32_t n_out = C < kTopT ? C : kTopT;
+      if (lane < C && r < kTopT) topk[(size_t)j * kTopT + r] = c0;
+      if (lane >= n_out && lane < kTopT) topk[(size_t)j * kTopT + lane] = 0;
+      const int32_t cmp = (thr == 0 && total <= kTopT) ? 1 : 0;
+      if (lane == 0) {
+        topk_cnt[j] = n_out;
+        topk_complete[j] = cmp;
+      }
+      if (xsend) {                               // sharded: this shard's record for the all-gather
+        uint64_t* x = xsend + (size_t)j * kXRec;
+        if (lane < C && r < kTopT) x[r] = c0;
+        if (lane >= n_out && lane < kTopT) x[lane] = 0;
+        if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)n_out | ((uint64_t)cmp << 32);
+      }
+      return;
+    }
+  }
+#endif
   // the wave's provable top-T prefix (lane t keeps key t)
   uint64_t mine = 0;
   int32_t cnt = 0, complete = 0, popped = 0;

@@ -1026,9 +1026,19 @@ struct RawScores {
 // ([slot][n]); returns the weighted sum of the slots without NormalizeScore.
 // store_plain: also store the raw score of those slots (compat mode).
 struct BatchProg;
-__device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+// The FAST key's profile inputs as plain scalars, read once per kernel from the
+// device copy of the BatchProg (a captured graph outlives a weight change):
+// wave-uniform values the compiler keeps in SGPRs, so the key's conditions
+// on them are scalar branches, never per-lane control flow.
+struct FastProg {
+  int32_t fit, w_fit, w_ba, w_eq, no_score;
+  int64_t fw_cpu, fw_mem;
+  double iw_cpu, iw_mem, iw_sum;
+};
+__device__ __forceinline__ FastProg fast_prog(const BatchProg& bp);
+__device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m);
-__device__ __forceinline__ int32_t fast_balanced_allocation(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+__device__ __forceinline__ int32_t fast_balanced_allocation(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                             double inv_c, double inv_m);
 
 // fast (non-null): BatchProg::fast_w on a kClusterNarrow cluster, so the
@@ -1053,9 +1063,9 @@ __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const Dev
 #define KSIM_PUT(pl, dst, expr) \
   if (plan_slot(sp, pl) >= 0) { dst = (expr); put(pl, dst); }
   int64_t v;
-  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fast ? (int64_t)fast_least_allocated(*fast, p, r, inv_c, inv_m)
+  KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fast ? (int64_t)fast_least_allocated(fast_prog(*fast), p, r, inv_c, inv_m)
                                                 : fit_least_allocated_score(r, prof, p, c.n_scalar));
-  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(*fast, p, r, inv_c, inv_m)
+  KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(fast_prog(*fast), p, r, inv_c, inv_m)
                                                 : balanced_allocation_score(r, prof, p, c.n_scalar));
   KSIM_PUT(KSIM_PL_TAINT_TOLERATION, rv.taint, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
   KSIM_PUT(KSIM_PL_NODE_AFFINITY, rv.aff, p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0);
@@ -1489,59 +1499,80 @@ __device__ __forceinline__ double u52_to_f64(int64_t x) {
 // leastResourceScorer over {cpu, memory} (BatchProg::fast_w, kClusterNarrow).
 // (alloc - requested) * 100 is an integer below 2^53, so the double product of
 // the converted difference and 100 is exact, as the int64 product converted is.
-__device__ __forceinline__ int32_t fast_least_allocated(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+// Branch-free: every quotient is computed and the plugin's conditions select
+// (a quotient of a zero or overdrawn capacity is garbage that is never
+// selected; v_cvt_i32_f64 does not trap).  The batch kernels keep their lanes
+// convergent this way: no exec-mask branches, no per-branch SALU work.
+__device__ __forceinline__ FastProg fast_prog(const BatchProg& bp) {
+  FastProg f;
+  f.fit = bp.has_fit_filter;
+  f.w_fit = (int32_t)bp.w_fit;
+  f.w_ba = (int32_t)bp.w_ba;
+  f.w_eq = bp.fit_w_eq;
+  f.no_score = bp.no_score;
+  f.fw_cpu = bp.fit_w_cpu;
+  f.fw_mem = bp.fit_w_mem;
+  f.iw_cpu = bp.inv_w[0];
+  f.iw_mem = bp.inv_w[1];
+  f.iw_sum = bp.inv_w[2];
+  return f;
+}
+
+__device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m) {
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
-  const int64_t rc = r.nz_cpu + p.nz_cpu, rm = r.nz_mem + p.nz_mem;
+  const int64_t dc = r.alloc_cpu - (r.nz_cpu + p.nz_cpu), dm = r.alloc_mem - (r.nz_mem + p.nz_mem);
   const double ac = u52_to_f64(r.alloc_cpu), am = u52_to_f64(r.alloc_mem);
-  const int32_t sc = (!hc || rc > r.alloc_cpu) ? 0
-                     : (int32_t)div_rn(u52_to_f64(r.alloc_cpu - rc) * (double)kMaxNodeScore, ac, inv_c);
-  const int32_t sm = (!hm || rm > r.alloc_mem) ? 0
-                     : (int32_t)div_rn(u52_to_f64(r.alloc_mem - rm) * (double)kMaxNodeScore, am, inv_m);
-  if (bp.fit_w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
-  const int64_t wc = hc ? bp.fit_w_cpu : 0, wm = hm ? bp.fit_w_mem : 0;
-  const double inv = (hc && hm) ? bp.inv_w[2] : hc ? bp.inv_w[0] : bp.inv_w[1];
-  return (hc || hm) ? (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv) : 0;
+  const int32_t qc = (int32_t)div_rn(u52_to_f64(dc) * (double)kMaxNodeScore, ac, inv_c);
+  const int32_t qm = (int32_t)div_rn(u52_to_f64(dm) * (double)kMaxNodeScore, am, inv_m);
+  const int32_t sc = (hc && dc >= 0) ? qc : 0;   // requested > capacity scores 0
+  const int32_t sm = (hm && dm >= 0) ? qm : 0;
+  if (q.w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
+  // selects of values (a select of the struct members' lvalues becomes an
+  // address select, and the struct a per-lane copy in LDS)
+  const int64_t fwc = q.fw_cpu, fwm = q.fw_mem;
+  const double iws = q.iw_sum, iwc = q.iw_cpu, iwm = q.iw_mem;
+  const int64_t wc = hc ? fwc : 0, wm = hm ? fwm : 0;
+  const double inv = (hc && hm) ? iws : hc ? iwc : iwm;
+  const int32_t v = (int32_t)div_rn((double)(sc * wc + sm * wm), (double)(wc + wm), inv);
+  return (hc || hm) ? v : 0;
 }
 
 // balancedResourceScorer over {cpu, memory}: the float64 quotients Go computes.
 // With a Fit filter in the profile it passed, so requested + request <=
 // allocatable < 2^46 and the short conversion is exact (without one the sums
-// are unbounded and take the general conversion).
-__device__ __forceinline__ int32_t fast_balanced_allocation(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
+// are unbounded and take the general conversion).  With one resource missing
+// the standard deviation is 0 (score 100), as with both present and equal.
+__device__ __forceinline__ int32_t fast_balanced_allocation(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                             double inv_c, double inv_m) {
-  const bool fit = bp.has_fit_filter != 0;
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
   const int64_t qc = r.req_cpu + p.req_cpu, qm = r.req_mem + p.req_mem;
-  double f0 = 0, f1 = 0;
-  if (hc) {
-    const double f = div_rn(fit ? u52_to_f64(qc) : (double)qc, u52_to_f64(r.alloc_cpu), inv_c);
-    f0 = f > 1 ? 1 : f;
-  }
-  if (hm) {
-    const double f = div_rn(fit ? u52_to_f64(qm) : (double)qm, u52_to_f64(r.alloc_mem), inv_m);
-    if (hc) f1 = f > 1 ? 1 : f;
-    else f0 = f > 1 ? 1 : f;
-  }
-  const double std = (hc && hm) ? fabs((f0 - f1) / 2) : 0.0;
-  return (int32_t)((1 - std) * (double)kMaxNodeScore);
+  const double fc = fmin(div_rn(q.fit ? u52_to_f64(qc) : (double)qc, u52_to_f64(r.alloc_cpu), inv_c), 1.0);
+  const double fm = fmin(div_rn(q.fit ? u52_to_f64(qm) : (double)qm, u52_to_f64(r.alloc_mem), inv_m), 1.0);
+  const int32_t b = (int32_t)((1 - fabs((fc - fm) / 2)) * (double)kMaxNodeScore);
+  return (hc && hm) ? b : kMaxNodeScore;
+}
+
+__device__ __forceinline__ uint64_t dyn_key_fast(const FastProg& q, const ksim_pod& p, const NodeRow& r,
+                                                 double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
+  // the Fit filter with non-short-circuit operators: one select, no branches
+  // (the request's zero test is uniform across the wave)
+  const bool any = (p.req_cpu | p.req_mem | p.req_eph) != 0;
+  const bool fits = (p.req_cpu <= r.alloc_cpu - r.req_cpu) & (p.req_mem <= r.alloc_mem - r.req_mem) &
+                    (p.req_eph <= r.alloc_eph - r.req_eph);
+  const bool ok = !q.fit | ((r.num_pods < r.alloc_pods) & (!any | fits));
+  int32_t tot = 0;
+  if (q.w_fit) tot += q.w_fit * fast_least_allocated(q, p, r, inv_c, inv_m);
+  if (q.w_ba) tot += q.w_ba * fast_balanced_allocation(q, p, r, inv_c, inv_m);
+  if (q.no_score) tot = 1;
+  const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
+  const uint64_t key = ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);
+  return ok ? key : 0;
 }
 
 __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
                                                  double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
-  if (bp.has_fit_filter) {
-    if (r.num_pods + 1 > r.alloc_pods) return 0;
-    if ((p.req_cpu != 0 || p.req_mem != 0 || p.req_eph != 0) &&
-        (p.req_cpu > r.alloc_cpu - r.req_cpu || p.req_mem > r.alloc_mem - r.req_mem ||
-         p.req_eph > r.alloc_eph - r.req_eph))
-      return 0;
-  }
-  int32_t tot = 0;
-  if (bp.w_fit) tot += (int32_t)bp.w_fit * fast_least_allocated(bp, p, r, inv_c, inv_m);
-  if (bp.w_ba) tot += (int32_t)bp.w_ba * fast_balanced_allocation(bp, p, r, inv_c, inv_m);
-  if (bp.no_score) tot = 1;
-  const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
-  return ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);
+  return dyn_key_fast(fast_prog(bp), p, r, inv_c, inv_m, hseed, gnode);
 }
 
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).

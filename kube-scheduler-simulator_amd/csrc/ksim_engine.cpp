@@ -2434,6 +2434,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
 const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerCycle) return kKernelNames[k];
   k -= kKernelsPerCycle;
+  // the default P100 batch runs the chain inside the pairs launch (the chain
+  // slot stays empty): name the slot after the kernel it times
+  if (k == 3 && chain_fused()) return "k_batch_chain_pairs";
   if (k >= 0 && k < kKernelsPerBatch) return kBatchKernelNames[k];
   k -= kKernelsPerBatch;
   if (k >= 0 && k < kKernelsPerAdapt) return kAdaptKernelNames[k];

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
                                                            const DevState* __restrict__ st,
                                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
                                                            int32_t* __restrict__ topk_complete,
-                                                           uint64_t* __restrict__ xsend) {
+                                                           uint64_t* __restrict__ xsend, int64_t* __restrict__ pnorm) {
   constexpr int kTopWaves = kTopThreads / 64;
   constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
   static_assert(kTopSlots <= 4 && kTileCand == 4, "k_batch_top geometry");
@@ -201,12 +201,49 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     }
   }
   if constexpr (!FAST) {                      // the generic loop is not compiled into FAST kernels
+    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
+    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
+    // nodes (P100: every feasible node is scored), the keys then carry the
+    // normalized scores (norm_part)
+    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+    NormRaw mx{0, 0};
+    if (normv) {
+      __shared__ uint64_t s_nmax[2][kTopWaves];
+      uint64_t xt = 0, xa = 0;                   // raw scores are >= 0
+#pragma unroll 1
+      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+        const NodeRow r = load_row(c, node);
+        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
+          const NormRaw v = norm_raw(c, P, p, r);
+          xt = umax64(xt, (uint64_t)v.tt);
+          xa = umax64(xa, (uint64_t)v.na);
+        }
+      }
+      xt = wave_max_u64_dpp(xt);
+      xa = wave_max_u64_dpp(xa);
+      if (lane == 0) {
+        s_nmax[0][wv] = xt;
+        s_nmax[1][wv] = xa;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kTopWaves; w++) {
+        xt = umax64(xt, s_nmax[0][w]);
+        xa = umax64(xa, s_nmax[1][w]);
+      }
+      mx = NormRaw{(int64_t)xt, (int64_t)xa};
+      if (threadIdx.x == 0) {
+        pnorm[2 * j] = mx.tt;
+        pnorm[2 * j + 1] = mx.na;
+      }
+    }
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
       uint64_t kk = 0;
       {
-        const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
+        const NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
         if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
       }
       nfeas += kk != 0;
       a[3] = umax64(a[3], kk);
@@ -372,6 +409,176 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     if (lane < kTopT) x[lane] = lane < n_out ? out : 0;
     if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)n_out | ((uint64_t)cmp << 32);
   }
+}
+
+// ---- k_batch_top_ns: node-split, pod-grouped evaluation (FAST runs) ------------
+// The whole node table is read once per POD by k_batch_top (256 x 440 KB of L1
+// traffic per launch at 5,000 nodes, re-fetched past every XCD's L2 each batch:
+// latency-bound).  Here block (g, c) keys NP pods (g*NP ..) over node chunk c
+// of NP: a lane loads a node row once and keys it for the block's NP pods, so
+// a batch reads each row B / NP times, a lane holds about N / (1024 NP) rows,
+// and chunk c's blocks (blockIdx % NP) sit on the XCDs c, c + NP, ... (the
+// dispatcher deals workgroups to the 8 XCDs round-robin), each XCD's L2
+// holding one chunk of the table.  Each block writes, per pod, the provable
+// top-T prefix of its chunk (the threshold top-T of k_batch_top, with every
+// wave's contribution capped at its own top-T); the chain merges a pod's
+// chunk lists (ksim_chain.h load_merged_list).
+template <int NP>
+__global__ __launch_bounds__(1024) void k_batch_top_ns(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
+                                                       const BatchProg* __restrict__ bp_p,
+                                                       const DevState* __restrict__ st, uint64_t* __restrict__ ptopk,
+                                                       int32_t* __restrict__ pmeta) {
+  constexpr int kW = 16;                        // waves per block
+  constexpr int kCap = kW * kTopT;              // candidates per pod (each wave at most its top-T)
+  static_assert(kCap <= 128 && kTileCand == 4, "k_batch_top_ns geometry");
+  __shared__ uint64_t s_wmax[NP][kW], s_wthr[NP][kW];
+  __shared__ int32_t s_wf[NP][kW], s_wc[NP][kW];
+  __shared__ uint64_t s_cand[NP][kCap];
+  const int chunk = blockIdx.x % NP, grp = blockIdx.x / NP;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t j0 = grp * NP;
+  if (j0 >= nb) return;                         // block-uniform
+  const int64_t seq0 = st->pod_seq;
+  const int32_t ne = c.eval_hi - c.eval_lo;
+  const int32_t lo = c.eval_lo + (int32_t)((int64_t)ne * chunk / NP);
+  const int32_t hi = c.eval_lo + (int32_t)((int64_t)ne * (chunk + 1) / NP);
+  const FastProg fp = fast_prog(*bp_p);
+  const uint64_t seed = prof_p->tiebreak_seed;
+  ksim_pod pf[NP];
+  uint64_t hseed[NP];
+  bool on[NP];
+#pragma unroll
+  for (int q = 0; q < NP; q++) {
+    on[q] = j0 + q < nb;
+    pf[q] = fast_pod_fields(P.pods[base + (on[q] ? j0 + q : j0)]);
+    hseed[q] = seed ^ ((uint64_t)(seq0 + j0 + q) << 20);
+  }
+  uint64_t a[NP][kTileCand];
+  int32_t nf[NP];
+#pragma unroll
+  for (int q = 0; q < NP; q++) {
+    nf[q] = 0;
+#pragma unroll
+    for (int e = 0; e < kTileCand; e++) a[q][e] = 0;
+  }
+#pragma unroll 1
+  for (int32_t node = lo + (int32_t)threadIdx.x; node < hi; node += 1024) {
+    const NodeRow r = load_res_row(c, node);
+    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+      const uint64_t k0 = dyn_key_fast(fp, pf[q], r, ic, im, hseed[q], c.base + node);
+      const uint64_t k = on[q] ? k0 : 0;
+      nf[q] += k != 0;
+      a[q][3] = umax64(a[q][3], k);
+      cswap_desc(a[q][2], a[q][3]);
+      cswap_desc(a[q][1], a[q][2]);
+      cswap_desc(a[q][0], a[q][1]);
+    }
+  }
+  // per pod: the waves' maxima, provability floors and feasible counts
+#pragma unroll
+  for (int q = 0; q < NP; q++) {
+    const uint64_t u = nf[q] > kTileCand ? a[q][kTileCand - 1] : 0;
+    const uint64_t wthr = wave_max_u64_dpp(u);
+    const uint64_t wmax = wave_max_u64_dpp(a[q][0]);
+    int32_t fsum = nf[q];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) fsum += __shfl_xor(fsum, m, 64);
+    if (lane == 0) {
+      s_wmax[q][wv] = wmax;
+      s_wthr[q][wv] = wthr;
+      s_wf[q][wv] = fsum;
+    }
+  }
+  __syncthreads();
+  // per pod: cut = max(floor, T-th largest wave maximum); the lanes' prefixes
+  // >= cut, each wave's count capped at T
+  int32_t cl[NP], pre[NP], cw[NP], total[NP];
+  uint64_t thr[NP], cut[NP];
+#pragma unroll
+  for (int q = 0; q < NP; q++) {
+    const uint64_t mine_w = lane < kW ? s_wmax[q][lane] : 0;
+    thr[q] = 0;
+    total[q] = 0;
+    int32_t rank = 0;
+#pragma unroll
+    for (int w = 0; w < kW; w++) {
+      thr[q] = umax64(thr[q], s_wthr[q][w]);
+      total[q] += s_wf[q][w];
+      rank += s_wmax[q][w] > mine_w;
+    }
+    const uint64_t at = __ballot(lane < kW && mine_w != 0 && rank == kTopT - 1);
+    const uint64_t L = at ? readlane_u64(mine_w, __builtin_ctzll(at)) : 0;
+    cut[q] = umax64(umax64(thr[q], L), 1);
+    cl[q] = 0;
+#pragma unroll
+    for (int e = 0; e < kTileCand; e++) cl[q] += a[q][e] >= cut[q];
+    int32_t x = cl[q];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    pre[q] = x - cl[q];
+    cw[q] = __shfl(x, 63, 64);
+    if (lane == 0) s_wc[q][wv] = cw[q] < kTopT ? cw[q] : kTopT;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NP; q++) {
+    int32_t off = 0;
+#pragma unroll
+    for (int w = 0; w < kW; w++) off += w < wv ? s_wc[q][w] : 0;
+    if (cw[q] <= kTopT) {                       // wave-uniform: every key >= cut of the wave
+#pragma unroll
+      for (int e = 0; e < kTileCand; e++)
+        if (e < cl[q]) s_cand[q][off + pre[q] + e] = a[q][e];
+    } else {                                    // only the wave's top-T can reach the pod's top-T
+      for (int t = 0; t < kTopT; t++) {
+        const uint64_t m = wave_max_u64_dpp(a[q][0]);
+        if (lane == 0) s_cand[q][off + t] = m;
+        if (a[q][0] == m) {
+          a[q][0] = a[q][1];
+          a[q][1] = a[q][2];
+          a[q][2] = a[q][3];
+          a[q][3] = 0;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (wv >= NP) return;
+  // wave q ranks pod q's candidates (distinct keys: distinct ranks)
+  const int q = wv;
+  const int32_t j = j0 + q;
+  if (j >= nb) return;
+  int32_t C = 0;
+  uint64_t tq = 0;
+  int32_t totq = 0;
+#pragma unroll
+  for (int w = 0; w < kW; w++) C += s_wc[q][w];
+#pragma unroll
+  for (int qq = 0; qq < NP; qq++)
+    if (qq == q) {
+      tq = thr[qq];
+      totq = total[qq];
+    }
+  const uint64_t c0 = lane < C ? s_cand[q][lane] : 0, c1 = 64 + lane < C ? s_cand[q][64 + lane] : 0;
+  int32_t r0 = 0, r1 = 0;
+  for (int x = 0; x < C; x++) {
+    const uint64_t v = s_cand[q][x];
+    r0 += v > c0;
+    r1 += v > c1;
+  }
+  uint64_t* out = ptopk + ((size_t)chunk * kBatchPods + j) * kTopT;
+  const int32_t n_out = C < kTopT ? C : kTopT;
+  if (lane < C && r0 < kTopT) out[r0] = c0;
+  if (64 + lane < C && r1 < kTopT) out[r1] = c1;
+  if (lane >= n_out && lane < kTopT) out[lane] = 0;
+  if (lane == 0) pmeta[chunk * kBatchPods + j] = n_out | (((tq == 0 && totq <= kTopT) ? 1 : 0) << 8);
 }
 
 // A tile list holds only its best kTileCand keys: once one is fully consumed
@@ -603,20 +810,29 @@ __device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
 
 // Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
 // FAST with pj / pk: pod j's and pod k's fields loaded by the caller.
+// Generic runs also flag pod j in pinv[j] when a node that held one of its
+// normalization maxima (kPodNormVaries) left its feasible set: its S0 keys
+// no longer hold, and the batch commits only the pods before it.
 template <bool FAST>
 __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                             const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
                                             int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax,
-                                            const ksim_pod* pj = nullptr, const ksim_pod* pk = nullptr) {
+                                            const ksim_pod* pj = nullptr, const ksim_pod* pk = nullptr,
+                                            const int64_t* __restrict__ pnorm = nullptr,
+                                            int32_t* __restrict__ pinv = nullptr, int32_t* s_winv = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
   const int32_t base = st->cursor;
   const int64_t seq0 = st->pod_seq;
   if (j >= nchain) {                                 // block-uniform
-    if (tid == 0) pmax[j] = 0;
+    if (tid == 0) {
+      pmax[j] = 0;
+      if (!FAST) pinv[j] = 0;
+    }
     return;
   }
   uint64_t v = 0;
+  bool inv = false;
   if (k < j) {
     const int32_t local = gk ? key_node(gk) - c.base : -1;
     if (local >= 0 && local < c.n) {
@@ -628,19 +844,37 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
                          prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
       } else {
         NodeRow r = load_row(c, local);
+        const int32_t bf = P.bflags[base + j];
+        const bool normv = (bf & kPodNormVaries) != 0;
+        const bool sp = (bf & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r);
+        const bool feas0 = normv && sp && dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base) != 0;   // at S0
         row_add_pod(r, P.pods[base + k], 1);
-        if ((P.bflags[base + j] & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r))
-          v = dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base);
+        if (sp) v = dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base);
+        if (normv && (v || feas0)) {
+          const NormRaw mx{pnorm[2 * j], pnorm[2 * j + 1]};
+          const NormRaw x = norm_raw(c, P, p, r);
+          if (v) v += (uint64_t)norm_part(bp, x, mx) << 44;
+          else inv = (mx.tt > 0 && x.tt == mx.tt) || (mx.na > 0 && x.na == mx.na);
+        }
       }
     }
   }
   v = wave_max_u64_dpp(v);
   if (lane == 0) s_wmax[wave] = v;
+  if (!FAST) {
+    const uint64_t b = __ballot(inv);
+    if (lane == 0) s_winv[wave] = b != 0;
+  }
   __syncthreads();
   if (tid == 0) {
     uint64_t m = 0;
-    for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
+    int32_t any = 0;
+    for (int w = 0; w < kBatchPods / 64; w++) {
+      m = umax64(m, s_wmax[w]);
+      if (!FAST) any |= s_winv[w];
+    }
     pmax[j] = m;
+    if (!FAST) pinv[j] = any;
   }
 }
 
@@ -655,20 +889,22 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
                                                             const DevState* __restrict__ st,
                                                             const uint64_t* __restrict__ gkey,
                                                             const int32_t* __restrict__ chain_end,
-                                                            uint64_t* __restrict__ pmax) {
+                                                            uint64_t* __restrict__ pmax, const int64_t* __restrict__ pnorm,
+                                                            int32_t* __restrict__ pinv) {
   __shared__ uint64_t s_wmax[kBatchPods / 64];
+  __shared__ int32_t s_winv[kBatchPods / 64];
   const uint64_t gk = gkey[threadIdx.x];             // in flight with the state loads
   const int32_t nchain = *chain_end;
   const int32_t nb = min(kBatchPods, st->end - st->cursor);
   if (nb <= 0) return;
-  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax);
+  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, nullptr, nullptr, pnorm, pinv, s_winv);
 }
 
 // The chain and the pair keys in one launch: every block of the pairs grid
 // runs the (deterministic) chain itself, thread k ending with pod k's guess in
 // a register, so the pairs need no chain launch and no gkey round trip.
 // Block 0 also stores the guesses and the prefix length for k_batch_commit.
-template <bool FAST>
+template <bool FAST, int NCHUNK = 0>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -678,9 +914,12 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
                                                                   const int32_t* __restrict__ topk_complete,
                                                                   uint64_t* __restrict__ gkey,
                                                                   int32_t* __restrict__ chain_end,
-                                                                  uint64_t* __restrict__ pmax) {
+                                                                  uint64_t* __restrict__ pmax,
+                                                                  const int64_t* __restrict__ pnorm,
+                                                                  int32_t* __restrict__ pinv) {
   __shared__ ChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
+  __shared__ int32_t s_winv[kBatchPods / 64];
   // FAST: pod j's and pod k's request fields in flight during the chain
   ksim_pod pj, pk;
   if constexpr (FAST) {
@@ -691,25 +930,29 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
   }
   uint64_t gk;
   int32_t nchain;
-  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
+  // NCHUNK > 0: topk / topk_cnt are the node-split top's chunk lists (k_batch_top_ns)
+  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
   if (blockIdx.x == 0) {
     const int32_t nb = min(kBatchPods, st->end - st->cursor);
     if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
     if (threadIdx.x == 0) *chain_end = nchain;
   }
-  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr, FAST ? &pk : nullptr);
+  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr, FAST ? &pk : nullptr,
+                    pnorm, pinv, s_winv);
 }
 
 __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ gkey,
                                                              const int32_t* __restrict__ chain_end,
                                                              const uint64_t* __restrict__ pmax,
-                                                             int32_t* __restrict__ chosen_out) {
+                                                             int32_t* __restrict__ chosen_out,
+                                                             const int32_t* __restrict__ pinv) {
   __shared__ int32_t s_istar, s_sched, s_unsched;
   const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
+  const int32_t inv = pinv ? pinv[threadIdx.x] : 0;
   const int32_t nchain = *chain_end;
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
-  batch_commit(c, P, st, g, m, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched);
+  batch_commit(c, P, st, g, m, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, pinv ? &inv : nullptr);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.
@@ -759,7 +1002,7 @@ static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t st
   }
   static const int threads = getenv("KSIM_TOP_THREADS") ? atoi(getenv("KSIM_TOP_THREADS")) : 1024;   // A/B
 #define TOP(F, T) k_batch_top<F, T><<<kBatchPods, T, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, \
-                                                                   a.s.topk_cnt, a.s.topk_complete, xsend)
+                                                                   a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm)
   if (threads == 512) {
     if (a.fast) TOP(true, 512);
     else TOP(false, 512);
@@ -771,23 +1014,68 @@ static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t st
   if (mid) (void)hipEventRecord(*mid, stream);
 }
 
+// Node chunks of the node-split top for this run (0 = k_batch_top, the
+// default).  KSIM_TOP_NS=2 / 4 selects it for FAST runs with the chain inside
+// the pairs launch (the chain merges the chunk lists).  Measured and not kept
+// (profiles/r03/ab_ns, config 2, same box): 4 chunks 10.37 ms per step, 2
+// chunks 8.15 ms, k_batch_top 7.80 ms -- the NP-pod register lists and the
+// per-pod reductions cost more than the shared row loads save, and the chain
+// pays the list merge.
+#ifndef KSIM_TOP_NS_DEFAULT
+#define KSIM_TOP_NS_DEFAULT 0   // the "ns4" flavor (tests/test_gpu_batch_ns.py) builds it with 4
+#endif
+int top_ns_chunks(const LaunchArgs& a) {
+  static const int force = getenv("KSIM_TOP_NS") ? atoi(getenv("KSIM_TOP_NS")) : KSIM_TOP_NS_DEFAULT;
+  if (!a.fast || !chain_fused() || chain_clock(a) || tile_eval()) return 0;
+  const int32_t ne = a.c.eval_hi - a.c.eval_lo;
+  return (force == 2 || force == 4) && ne >= 64 * force ? force : 0;
+}
+
+static void launch_top_ns(const LaunchArgs& a, int nch, hipStream_t stream) {
+  if (nch == 4)
+    k_batch_top_ns<4><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
+  else
+    k_batch_top_ns<2><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
+}
+
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[0], stream);
-  launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
+  const int nch = top_ns_chunks(a);
+  if (nch) {
+    launch_top_ns(a, nch, stream);
+    if (evs) (void)hipEventRecord(evs[1], stream);
+  } else {
+    launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
+  }
   if (evs) (void)hipEventRecord(evs[2], stream);
+  if (nch) {
+    if (evs) (void)hipEventRecord(evs[3], stream);
+#define CP(N) k_batch_chain_pairs<true, N><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
+                  a.s.ptopk, a.s.pmeta, nullptr, a.s.gkey, a.s.chain_end, a.s.pmax, \
+                  a.s.pnorm, a.s.pinv)
+    if (nch == 4) CP(4);
+    else CP(2);
+#undef CP
+    if (evs) (void)hipEventRecord(evs[4], stream);
+    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
+                                                 a.fast ? nullptr : a.s.pinv);
+    if (evs) (void)hipEventRecord(evs[5], stream);
+    return 0x19u;
+  }
   if (chain_fused() && !chain_clock(a)) {
     // the chain inside every pairs block (k_batch_chain_pairs), timed in the pairs slot
     if (evs) (void)hipEventRecord(evs[3], stream);
     if (a.fast)
       k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
                                                                        a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                       a.s.chain_end, a.s.pmax);
+                                                                       a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
     else
       k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
                                                                         a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                        a.s.chain_end, a.s.pmax);
+                                                                        a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
     if (evs) (void)hipEventRecord(evs[4], stream);
-    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
+                                                 a.fast ? nullptr : a.s.pinv);
     if (evs) (void)hipEventRecord(evs[5], stream);
     return tile_eval() ? 0x1bu : 0x19u;
   }
@@ -798,17 +1086,22 @@ uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) 
   // the pairs kernel fencing for a last-block election
   if (a.fast)
     k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
-                                                               a.s.pmax);
+                                                               a.s.pmax, a.s.pnorm, a.s.pinv);
   else
     k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
-                                                                a.s.chain_end, a.s.pmax);
+                                                                a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
+                                                 a.fast ? nullptr : a.s.pinv);
   if (evs) (void)hipEventRecord(evs[5], stream);
   return tile_eval() ? 0x1fu : 0x1du;   // k_batch_top leaves the merge slot empty
 }
 
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
+  if (const int nch = top_ns_chunks(a)) {
+    launch_top_ns(a, nch, stream);
+    return;
+  }
   if (tile_eval()) {
     const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
     const dim3 g1((n_tiles + 3) / 4, kBatchPods);
@@ -839,25 +1132,25 @@ void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) 
     if (a.fast)
       k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
                                                                        a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                       a.s.chain_end, a.s.pmax);
+                                                                       a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
     else
       k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
                                                                         a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                        a.s.chain_end, a.s.pmax);
+                                                                        a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
     return;
   }
   k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
                                               a.s.gkey, a.s.chain_end, chain_clock(a));
   if (a.fast)
     k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
-                                                               a.s.pmax);
+                                                               a.s.pmax, a.s.pnorm, a.s.pinv);
   else
     k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
-                                                                a.s.chain_end, a.s.pmax);
+                                                                a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
 }
 
 void launch_shard_commit(const LaunchArgs& a, hipStream_t stream) {
-  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen);
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen, nullptr);
 }
 
 void launch_group_max(const GroupPtrs& g, hipStream_t stream) { k_group_max<<<1, kBatchPods, 0, stream>>>(g); }

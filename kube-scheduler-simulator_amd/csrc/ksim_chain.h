@@ -3,6 +3,7 @@
 #pragma once
 #include "ksim_device.h"
 #include "ksim_internal.h"
+#include "ksim_wave.h"
 
 namespace ksim {
 
@@ -36,16 +37,86 @@ struct ChainLds {
   int32_t first[2], cut;                      // first: one slot per round parity (see the round loop)
 };
 
+// ---- partial top-T lists of a node-split evaluation (k_batch_top_ns) ----------
+// Chunk c of the nodes wrote, for pod j, its provable top-T prefix
+// ptopk[(c * kBatchPods + j) * kTopT ..] and pmeta[c * kBatchPods + j] = count
+// | complete << 8.  Merged as the sharded records are (k_batch_gmerge): a key is
+// in the pod's exact order if it is >= the last listed key of every incomplete
+// chunk list (every key a chunk did not list is below it); the merged list is
+// complete when every chunk's was and nothing was dropped.
+static_assert((kTopT & (kTopT - 1)) == 0, "bitonic list merge needs a power-of-two T");
+
+// top-T of two descending lists, descending, into a (bitonic half-cleaners)
+__device__ __forceinline__ void merge_top_desc(uint64_t (&a)[kTopT], const uint64_t (&b)[kTopT]) {
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) a[e] = umax64(a[e], b[kTopT - 1 - e]);
+#pragma unroll
+  for (int d = kTopT / 2; d >= 1; d >>= 1)
+#pragma unroll
+    for (int e = 0; e < kTopT; e++)
+      if ((e & d) == 0) cswap_desc(a[e], a[e + d]);
+}
+
+template <int NCHUNK>
+__device__ __forceinline__ void load_merged_list(int32_t j, const uint64_t* __restrict__ ptopk,
+                                                 const int32_t* __restrict__ pmeta, uint64_t (&lst)[kTopT],
+                                                 int32_t& cnt_out, int32_t& complete_out) {
+  uint64_t L[NCHUNK][kTopT];
+  int32_t meta[NCHUNK];
+#pragma unroll
+  for (int c = 0; c < NCHUNK; c++) {
+    meta[c] = pmeta[c * kBatchPods + j];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) L[c][e] = ptopk[((size_t)c * kBatchPods + j) * kTopT + e];
+  }
+  uint64_t thr = 0;
+  bool all_complete = true, blind = false;
+#pragma unroll
+  for (int c = 0; c < NCHUNK; c++) {
+    const int32_t n = meta[c] & 0xff;
+    const bool cmp = (meta[c] >> 8) & 1;
+    uint64_t last = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) {
+      if (e >= n) L[c][e] = 0;
+      if (e == n - 1) last = L[c][e];
+    }
+    if (!cmp) {
+      all_complete = false;
+      if (n == 0) blind = true;                  // nothing of this chunk is provable
+      thr = umax64(thr, last);
+    }
+  }
+  int32_t nvalid = 0;
+#pragma unroll
+  for (int c = 0; c < NCHUNK; c++)
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) {
+      if (L[c][e] < thr) L[c][e] = 0;
+      nvalid += L[c][e] != 0;
+    }
+#pragma unroll
+  for (int w = 1; w < NCHUNK; w <<= 1)
+#pragma unroll
+    for (int c = 0; c + w < NCHUNK; c += 2 * w) merge_top_desc(L[c], L[c + w]);
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) lst[e] = blind ? 0 : L[0][e];
+  cnt_out = blind ? 0 : (nvalid < kTopT ? nvalid : kTopT);
+  complete_out = (!blind && all_complete && nvalid <= kTopT) ? 1 : 0;
+}
+
 // The chain of one batch in one block of kBatchPods threads (thread i = pod
-// i).  Returns false when the batch is empty (block-uniform); else *gk = pod
+// i; pods from nb_cap on take no part).  Returns false when the batch is empty (block-uniform); else *gk = pod
 // i's guessed key (0: none, or i past the exact prefix) and *nchain = the
 // prefix length.  A pure function of the lists: every block that runs it gets
 // the same guesses.
+template <int NCHUNK = 0>
 __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restrict__ st,
                                             const uint64_t* __restrict__ topk,
                                             const int32_t* __restrict__ topk_cnt,
                                             const int32_t* __restrict__ topk_complete, uint64_t* gk,
-                                            int32_t* nchain_out, unsigned long long* __restrict__ dbg) {
+                                            int32_t* nchain_out, unsigned long long* __restrict__ dbg,
+                                            int32_t nb_cap = kBatchPods) {
   int32_t* const s_key = L.key;
   int32_t* const s_hold = L.hold;
   int32_t& s_cut = L.cut;
@@ -55,12 +126,19 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   // the pod's list, count and state in flight together (independent loads;
   // the buffers hold kBatchPods entries, so no bound check is needed yet)
   uint64_t lst[kTopT];
+  int cnt0, complete0;
+  if constexpr (NCHUNK > 0) {
+    // node-split evaluation: merge the pod's chunk lists (topk / topk_cnt hold
+    // them, see k_batch_top_ns)
+    load_merged_list<NCHUNK>(i, topk, topk_cnt, lst, cnt0, complete0);
+  } else {
 #pragma unroll
-  for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
-  const int cnt0 = topk_cnt[i];
-  const int complete0 = topk_complete[i];
+    for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
+    cnt0 = topk_cnt[i];
+    complete0 = topk_complete[i];
+  }
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t nb = min(nb_cap, st->end - base);   // nb_cap: the topology batch's pod count
   if (nb <= 0) return false;
   for (int x = i; x < kHashSlots; x += kBatchPods) {
     s_key[x] = -1;

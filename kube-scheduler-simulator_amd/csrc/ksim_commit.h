@@ -34,18 +34,29 @@ struct ResCols {
 // cut is known; the evaluated counts and nextStartNodeIndex follow the
 // committed pods' windows.  g_own / m_own: this thread's gkey / pmax entries,
 // loaded by the caller at kernel start (before the state load they do not
-// depend on).
+// depend on).  inv_own (P100 generic runs, topology batches): this thread's
+// pinv entry; the chain ends before the first flagged pod (pairs_block).
+// nb_cap: the topology batch's pod count.
 __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
                                              uint64_t g_own, uint64_t m_own, const uint64_t* __restrict__ pmax,
                                              int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
                                              int32_t* s_sched, int32_t* s_unsched,
-                                             const int2* s_aw = nullptr) {
+                                             const int2* s_aw = nullptr, const int32_t* inv_own = nullptr,
+                                             int32_t nb_cap = kBatchPods) {
   __shared__ int32_t s_evals;
   __shared__ uint64_t s_m[kBatchPods];
   __shared__ ResCols s_req[kBatchPods];
   const int tid = threadIdx.x;
+  if (inv_own) {                                   // block-uniform
+    if (tid == 0) *s_istar = nchain;
+    __syncthreads();
+    if (tid < nchain && *inv_own) atomicMin(s_istar, tid);
+    __syncthreads();
+    nchain = *s_istar;
+    __syncthreads();                               // every read before s_istar is reused below
+  }
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t nb = min(nb_cap, st->end - base);   // the batch's pods (statistics: cut or truncated)
   const int64_t seq0 = st->pod_seq;
   const uint64_t gj = tid < nchain ? g_own : 0;
   const uint64_t mj = tid < nchain ? m_own : 0;

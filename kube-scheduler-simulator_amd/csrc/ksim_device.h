@@ -155,7 +155,8 @@ struct WinState {
   int32_t nscan;                         // nodes the cycle scans (ScanSet.n): nextStartNodeIndex modulus
   double w[KSIM_MAX_USES];               // PTS soft: topologyNormalizingWeight per use
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
-  int32_t done, _pad;                    // k_select blocks finished (the last one binds; reset by it)
+  int32_t done;                          // k_select blocks finished (the last one binds; reset by it)
+  uint32_t tflags;                       // topology batch: the pod's kTopo* flags (k_tb_filter block 0)
 };
 
 // The nodes one cycle scans, in scan order: every node of
@@ -230,11 +231,24 @@ struct DevScratch {
   int64_t* part;         // [n] sum of weighted raw of slots without NormalizeScore
   uint64_t* cand;        // batch path: [B][n_tiles][kTileCand] per-tile best keys
   uint64_t* topk;        // batch path: [B][T] merged top keys, descending
+  uint64_t* ptopk;       // node-split batch top (k_batch_top_ns): [chunks][B][T] per-chunk lists
+  int32_t* pmeta;        // ... [chunks][B] count | complete << 8
   int32_t* topk_cnt;     // batch path: [B] valid merged keys
   int32_t* topk_complete;// batch path: [B] 1 if every S0-feasible node is in the list
   uint64_t* gkey;        // batch path: [B] key of each pod's greedy guess (0: none)
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
+  int64_t* pnorm;        // batch path: [B][2] kPodNormVaries pods' S0 maxima (TaintToleration, NodeAffinity raw)
+  // topology batch path (ksim_tbatch.hip), per pod j of the batch: [kTbPods][n] slices
+  uint8_t* tb_fail;      // filter result per node
+  uint8_t* tb_ign;       // PodTopologySpread IgnoredNodes
+  int64_t* tb_part;      // weighted raw scores of the slots without NormalizeScore
+  int64_t* tb_raw;       // [kTbPods][KSIM_MAX_SCORE][n] raw scores
+  int32_t* tb_stat;      // total - (w_fit LeastAllocated + w_ba BalancedAllocation) at S0; kStatNone / kStatOne
+  WinState* tb_win;      // [kTbPods] counters, extrema, flags
+  uint64_t* tb_clist;    // [kTbPods][kTbMaxBlocks][T] each node block's exact top-T keys
+  int32_t* tb_ccnt;      // [kTbPods][kTbMaxBlocks] their counts
+  int32_t* pinv;         // batch path: [B] 1 = a maximum holder of pod j left its feasible set (batch ends before j)
   unsigned long long* dbg;   // [16] diagnostic accumulators (ksim_get_diag), e.g. chain phase times
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
   uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records
@@ -308,6 +322,9 @@ __host__ __device__ __forceinline__ int32_t key_node(uint64_t key) {
 // compare as two u64 words; 0 is below every image of a real total > INT64_MIN.
 __host__ __device__ __forceinline__ uint64_t max_image(int64_t x) { return (uint64_t)x ^ (1ull << 63); }
 __host__ __device__ __forceinline__ int64_t from_max_image(uint64_t m) { return (int64_t)(m ^ (1ull << 63)); }
+// Min image: order-reversing, so an atomicMax over images takes the minimum.
+__host__ __device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
+__host__ __device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
 
 // NodeInfo aggregates of one node, in registers.
 struct NodeRow {
@@ -394,6 +411,42 @@ __device__ __forceinline__ int64_t div_trunc_pos(int64_t a, int64_t b) {
   if (a == INT64_MIN) return a / b;
   return -div_floor_nonneg(-a, b);
 }
+
+// ---- normalization ----------------------------------------------------------
+// Extrema a slot needs, merged over the kept feasible list:
+//   DefaultNormalizeScore: maxCount = max(0, max)          (helper/normalize_score.go)
+//   PodTopologySpread:     maxScore = max(0, max), minScore = min, IgnoredNodes excluded
+//   InterPodAffinity:      min / max, only when topologyScore is non-empty
+__device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int64_t gmax, int64_t gmin,
+                                                   bool ipa_nonempty) {
+  switch (kind) {
+    case kNormDefault: {
+      int64_t m = gmax > 0 ? gmax : 0;
+      return m == 0 ? v : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
+    }
+    case kNormDefaultReverse: {
+      int64_t m = gmax > 0 ? gmax : 0;
+      return m == 0 ? (int64_t)kMaxNodeScore
+                    : (int64_t)kMaxNodeScore - div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
+    }
+    case kNormPTS: {
+      int64_t mx = gmax > 0 ? gmax : 0;
+      return mx == 0 ? (int64_t)kMaxNodeScore
+                     : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)(mx + gmin - v)), mx);
+    }
+    case kNormIPA:
+    case kNormMinMax: {
+      if (kind == kNormIPA && !ipa_nonempty) return v;
+      const int64_t diff = gmax - gmin;
+      double f = 0;
+      if (diff > 0) f = (double)kMaxNodeScore * ((double)(v - gmin) / (double)diff);
+      return (int64_t)f;
+    }
+    default:
+      return v;
+  }
+}
+
 
 // floor(a / b) for 0 <= a <= 100 * b, b > 0 (a score-sized quotient): an f32
 // reciprocal estimate is within 100 * 2^-20 of a / b, so its truncation is
@@ -1299,6 +1352,7 @@ struct BatchProg {
   int32_t has_fit_filter;
   int32_t cpu_mem;                         // both scoring strategies are exactly {cpu, memory}
   int64_t w_fit, w_ba;                     // summed profile weights of the Fit / BA score slots
+  int64_t w_tt, w_na;                      // ... of the TaintToleration / NodeAffinity slots (norm_part)
   int64_t fit_w_cpu, fit_w_mem;            // cpu_mem: LeastAllocated resource weights
   int32_t fast_w;                          // cpu_mem with both LeastAllocated weights in [1, 2^31) (dyn_key_fast)
   int32_t no_score;                        // the profile has no score plugin: every total is 1
@@ -1313,6 +1367,9 @@ struct BatchProg {
 // DevPods.bflags (batch path, per pod)
 constexpr int32_t kBatchStaticTrivial = 1; // every static filter passes on every node (host-proven)
 constexpr int32_t kPodRegistersValues = 2; // has a ScheduleAnyway spread keyed by a non-hostname column
+constexpr int32_t kPodNormVaries = 4;      // batch path: TaintToleration / NodeAffinity vary over nodes (norm_part)
+constexpr int32_t kPodTopoBatch = 8;       // topology batch path (ksim_tbatch.hip)
+constexpr int kTlenShift = 8;              // bflags >> kTlenShift: pods from this one with no class conflict (tbatch)
 
 // Compact row for the batch repair's LDS staging: the NodeRow fields a
 // batchable pod can read (batchable pods request no scalar resources and the
@@ -1576,15 +1633,36 @@ __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim
 }
 
 // Key of a batchable pod on a row whose static filters passed (0 = infeasible).
+// Pods with scalar requests take the generic functions (their Fit filter
+// checks the scalar columns).
 __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
                                             const NodeRow& r, int n_scalar, int64_t seq, int32_t base) {
-  if (bp.cpu_mem) return dyn_key_cpu_mem(prof, bp, p, r, seq, base);
+  if (bp.cpu_mem && !(p.flags & KSIM_POD_HAS_SCALAR)) return dyn_key_cpu_mem(prof, bp, p, r, seq, base);
   if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
   int64_t tot = 0;
   if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);
   if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, n_scalar);
   if (prof.n_score == 0) tot = 1;
   return tb_key(tot, prof.tiebreak_seed, seq, base + r.node);
+}
+
+// kPodNormVaries pods (P100 batch path): the raw scores of the two normalized
+// plugins that can vary over nodes for a batchable pod.  Both depend on the
+// node's taints and labels only, never on what is bound there.
+struct NormRaw {
+  int64_t tt, na;   // countIntolerableTaintsPreferNoSchedule, preferred NodeAffinity weight sum
+};
+__device__ __forceinline__ NormRaw norm_raw(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                            const NodeRow& r) {
+  return NormRaw{count_intolerable_prefer(c, p, r), p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0};
+}
+// Their weighted NormalizeScore over the pod's S0 maxima (mx): added to the
+// batch key's total.  Exact while the maxima hold: a node's raw scores never
+// change with binds, and the maxima only change when a node holding one
+// leaves the pod's feasible set (pairs_block flags that pod, pinv).
+__device__ __forceinline__ int64_t norm_part(const BatchProg& bp, const NormRaw& v, const NormRaw& mx) {
+  return bp.w_tt * normalize_value(kNormDefaultReverse, v.tt, mx.tt, 0, false) +
+         bp.w_na * normalize_value(kNormDefault, v.na, mx.na, 0, false);
 }
 
 __device__ __forceinline__ void row_add_pod(NodeRow& r, const ksim_pod& p, int sign) {

@@ -120,6 +120,7 @@ struct ksim_handle {
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
+  std::vector<int32_t> tlen;            // per loaded pod: topology batch run length from it (tbatch_runs)
   std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
@@ -161,6 +162,7 @@ struct ksim_handle {
   hipGraphExec_t graph_cycle[16] = {};   // | persistent tables (8)
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
+  hipGraphExec_t graph_tbatch = nullptr;       // topology batches (ksim_tbatch.hip)
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
   // the global bitmap (allocated at the first such run)
   std::vector<DevBuf> ash_bufs;
@@ -247,8 +249,10 @@ void drop_graphs(ksim_handle* h) {
   drop_cycle_graphs(h);
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
+  if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
   h->graph_batch_fast = nullptr;
   h->graph_batch = nullptr;
+  h->graph_tbatch = nullptr;
 }
 
 bool plugin_supported(int id) { return id >= 0 && id < KSIM_PL_COUNT; }
@@ -354,7 +358,7 @@ bool is_sharded(const ksim_handle* h) { return h->comm != nullptr || h->shard_to
 bool run_fast(const ksim_handle* h, int32_t a, int32_t b) {
   if (!h->bp.cpu_mem || !h->bp.fast_w || !h->alloc_narrow) return false;
   for (int32_t i = a; i < b; i++)
-    if (!h->trivial[i]) return false;
+    if (!h->trivial[i] || h->batchable[i] == 2) return false;
   return true;
 }
 
@@ -369,35 +373,77 @@ bool profile_nb(const ksim_profile& p) {
 }
 
 // The batch keys carry a pod's total minus its constant normalized part in
-// 20 bits (tb_key): 100 * (w_fit + w_ba) must stay below kKeyTotalLimit, or
-// the pods take the per-pod path, whose (total, TB) pairs are exact for any
-// int64 total.  Pods that NodeAffinity's PreFilterResult restricts scan a node
-// list of their own: per-pod path.
-bool pod_batchable(const ksim_handle* h, const ksim_pod& p) {
+// 20 bits (tb_key): 100 * (w_fit + w_ba), plus w_tt + w_na for the pods
+// whose normalized scores vary, must stay below kKeyTotalLimit, or the pods
+// take the per-pod path, whose (total, TB) pairs are exact for any int64 total.  Pods that NodeAffinity's PreFilterResult
+// restricts scan a node list of their own: per-pod path.
+// Returns 0 (per-pod path), 1 (every batch path) or 2 (the unsharded P100
+// batch path only): pods whose TaintToleration / NodeAffinity scores vary
+// over nodes (kPodNormVaries: the keys carry them, normalized over the pod's
+// S0 maxima) and pods with scalar requests (the ADAPT repair's compact rows
+// carry no scalars).
+int pod_batchable(const ksim_handle* h, const ksim_pod& p, bool* norm_varies = nullptr) {
   const ksim_profile& prof = h->prof;
-  if (p.use_count > 0) return false;
-  if (p.flags & KSIM_POD_NODE_NAMES) return false;
-  if (p.vb_count > 0 || p.vz_count > 0) return false;   // volume groups: the per-pod filter chain
+  if (norm_varies) *norm_varies = false;
+  if (p.use_count > 0) return 0;
+  if (p.flags & KSIM_POD_NODE_NAMES) return 0;
+  if (p.vb_count > 0 || p.vz_count > 0) return 0;       // volume groups: the per-pod filter chain
   // NetworkBandwidth runs on the per-pod path (its error statuses end cycles),
   // and so do pods that add to a node's allocated bandwidth
-  if (profile_nb(prof) || p.nb_add != 0) return false;
-  if (p.flags & KSIM_POD_HAS_SCALAR) return false;     // the repair's compact rows carry no scalars
-  if ((int64_t)kMaxNodeScore * (h->bp.w_fit + h->bp.w_ba) >= kKeyTotalLimit) return false;
+  if (profile_nb(prof) || p.nb_add != 0) return 0;
+  const int64_t w_dyn = h->bp.w_fit + h->bp.w_ba;
+  if ((int64_t)kMaxNodeScore * w_dyn >= kKeyTotalLimit) return 0;
+  int cls = (p.flags & KSIM_POD_HAS_SCALAR) ? 2 : 1;
+  bool varies = false;
   for (int k = 0; k < prof.n_score; k++) {
     switch (norm_kind(prof.score[k])) {
-      case kNormDefaultReverse:
+      case kNormDefaultReverse:                         // varies when some PreferNoSchedule taint is not tolerated
         for (size_t t = 1; t < h->taint_effect.size(); t++)
           if (h->taint_effect[t] == KSIM_EFFECT_PREFER_NO_SCHEDULE && !((p.tol_prefer[t >> 6] >> (t & 63)) & 1ull))
-            return false;
-        break;                                          // every node 100
+            varies = true;
+        break;                                          // else every node 100
       case kNormDefault:
-        if (p.pref_term_count > 0) return false;        // else every node 0
+        if (p.pref_term_count > 0) varies = true;        // else every node 0
         break;
       default:                                          // PodTopologySpread 100, InterPodAffinity 0
         break;
     }
   }
-  return true;
+  if (varies && (int64_t)kMaxNodeScore * (w_dyn + h->bp.w_tt + h->bp.w_na) >= kKeyTotalLimit) return 0;
+  if (varies) cls = 2;
+  if (norm_varies) *norm_varies = varies;
+  return cls;
+}
+
+// Whether loaded pod i runs on this handle's batch path (see pod_batchable):
+// class 2 needs the unsharded P100 path over the whole node table.
+bool pod_on_batch(const ksim_handle* h, int32_t i) {
+  const uint8_t b = h->batchable[i];
+  if (b != 2 && b != 3) return b != 0;
+  return !adapt_mode(h) && !is_sharded(h) && !h->replicated;   // replicated: a split evaluation range
+}
+
+// Topology pods the topology batch path takes (class 3; ksim_tbatch.hip): the
+// per-pod path's fused no-window cycle would run them (at most one
+// ScheduleAnyway spread constraint, keyed by hostname or by no node's key;
+// hard spread keys of <= kFuseMinValues values) with every domain sum read
+// from a persistent table, no port / volume / bandwidth inputs and no
+// PreFilterResult node list, totals inside the batch key's 20 bits, and a
+// cluster of at most kTbMaxBlocks node blocks.  KSIM_NO_TBATCH=1: per-pod path (A/B).
+bool tbatch_admit(const ksim_handle* h, const ksim_pod& p, const PodPlan& pl, bool hard_small, bool soft_le1) {
+  static const bool off = getenv("KSIM_NO_TBATCH") != nullptr;
+  if (off || p.use_count <= 0) return false;
+  if (h->dc.n > kTbMaxBlocks * 256) return false;
+  if (p.flags & KSIM_POD_NODE_NAMES) return false;
+  if (p.vb_count > 0 || p.vz_count > 0 || profile_nb(h->prof) || p.nb_add != 0) return false;
+  const UseMasks& m = pl.m;
+  if (m.port || m.soft_val || !hard_small || !soft_le1) return false;
+  const bool pt = (pl.flags & kPlanPtab) != 0;
+  if ((m.dom & ~(pt ? m.ptab : 0u)) != 0) return false;     // a domain sum k_topo_prefilter would build
+  if ((m.aff | m.score) != 0 && !pt) return false;         // the InterPodAffinity flags come from the tables
+  int64_t wsum = 0;
+  for (int k = 0; k < h->prof.n_score; k++) wsum += h->prof.score_weight[k] == 0 ? 1 : h->prof.score_weight[k];
+  return (int64_t)kMaxNodeScore * wsum < kKeyTotalLimit;
 }
 
 // A framework-driven cycle left behind by another entry point: its PreFilter
@@ -485,6 +531,45 @@ int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fas
 }
 
 
+// A run of topology batch pods [a, b) (set_run done).  The host knows each
+// batch's pod count (the conflict-free run from its first pod, capped) and a
+// batch commits at most that many, so launching the batches the counts predict
+// never passes the end; a batch that commits fewer (a cut, an exhausted list,
+// pinv) leaves pods for the next round.
+int run_tbatch(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
+  int rc;
+  HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+  if (!h->graph_tbatch) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    hipGraph_t g = nullptr;
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < kGraphBatches; i++) launch_tbatch(la, h->stream);
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
+    e = hipGraphInstantiate(&h->graph_tbatch, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+      h->graph_tbatch = nullptr;
+      return hip_fail(h, e, "hipGraphInstantiate");
+    }
+    h->graph_captures++;
+  }
+  int32_t cursor = a;
+  while (cursor < b) {
+    int32_t nbat = 0;
+    for (int32_t i = cursor; i < b; nbat++) i += std::min(std::min(kTbPods, b - i), std::max(h->tlen[i], 1));
+    int32_t done = 0;
+    for (; done + kGraphBatches <= nbat; done += kGraphBatches) HIPCHK(h, hipGraphLaunch(h->graph_tbatch, h->stream));
+    for (; done < nbat; done++) launch_tbatch(la, h->stream);
+    HIPCHK(h, hipGetLastError());
+    DevState st;
+    if ((rc = read_state(h, st))) return rc;
+    if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "topology batch path made no progress");
+    cursor = st.cursor;
+  }
+  return KSIM_OK;
+}
+
 // Run pods [a, b) on one path (all of them share the path).
 int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   int rc;
@@ -508,6 +593,7 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
     HIPCHK(h, hipGetLastError());
     return KSIM_OK;
   }
+  if (topo) return run_tbatch(h, a, b, la);
   // the FAST evaluation kernel when every pod of the run is trivial with cpu/memory scoring
   la.fast = run_fast(h, a, b);
   hipGraphExec_t& gb = la.fast ? h->graph_batch_fast : h->graph_batch;
@@ -549,10 +635,10 @@ int for_each_run(ksim_handle* h, int32_t first, int32_t count, F&& fn, bool adap
   const int32_t end = first + count;
   while (i < end) {
     const bool batch_ok = !(adapt_mode(h) && is_sharded(h)) || adapt_sharded;
-    const bool b = batch_ok && h->batchable[i] != 0;
+    const bool b = batch_ok && pod_on_batch(h, i);
     const bool t = h->topo[i] != 0;
     int32_t j = i + 1;
-    while (j < end && (batch_ok && h->batchable[j] != 0) == b && h->topo[j] == h->topo[i]) j++;
+    while (j < end && (batch_ok && pod_on_batch(h, j)) == b && h->topo[j] == h->topo[i]) j++;
     int rc = fn(i, j, b, t);
     if (rc) return rc;
     i = j;
@@ -1092,6 +1178,8 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
     const int64_t w = p->score_weight[k] == 0 ? 1 : p->score_weight[k];
     if (p->score[k] == KSIM_PL_NODE_RESOURCES_FIT) bp.w_fit += w;
     if (p->score[k] == KSIM_PL_BALANCED_ALLOCATION) bp.w_ba += w;
+    if (p->score[k] == KSIM_PL_TAINT_TOLERATION) bp.w_tt += w;
+    if (p->score[k] == KSIM_PL_NODE_AFFINITY) bp.w_na += w;
   }
   plan_profile(*p, bp.rank_lo, bp.rank_hi, bp.slot, bp.slot_hi);
   HIPCHK(h, hipSetDevice(h->device));
@@ -1332,11 +1420,24 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.part, int64_t*, 8 * N);
   SCR(s.cand, uint64_t*, 8 * (size_t)kBatchPods * n_tiles * kTileCand);
   SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kTopT);
+  SCR(s.ptopk, uint64_t*, 8 * (size_t)kTopNsMaxChunks * kBatchPods * kTopT);
+  SCR(s.pmeta, int32_t*, 4 * (size_t)kTopNsMaxChunks * kBatchPods);
   SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.chain_end, int32_t*, 4);
   SCR(s.pmax, uint64_t*, 8 * 2 * (size_t)kBatchPods);   // [M | sharded ADAPT broken flags]
+  SCR(s.pnorm, int64_t*, 8 * 2 * (size_t)kBatchPods);
+  const size_t NT = N <= (size_t)kTbMaxBlocks * 256 ? N : 0;   // topology batches (tbatch_admit)
+  SCR(s.tb_fail, uint8_t*, (size_t)kTbPods * NT);
+  SCR(s.tb_ign, uint8_t*, (size_t)kTbPods * NT);
+  SCR(s.tb_part, int64_t*, 8 * (size_t)kTbPods * NT);
+  SCR(s.tb_raw, int64_t*, 8 * (size_t)kTbPods * KSIM_MAX_SCORE * NT);
+  SCR(s.tb_stat, int32_t*, 4 * (size_t)kTbPods * NT);
+  SCR(s.tb_win, WinState*, sizeof(WinState) * (size_t)kTbPods);
+  SCR(s.tb_clist, uint64_t*, 8 * (size_t)kTbPods * kTbMaxBlocks * kTopT);
+  SCR(s.tb_ccnt, int32_t*, 4 * (size_t)kTbPods * kTbMaxBlocks);
+  SCR(s.pinv, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
   SCR(s.dbg, unsigned long long*, 8 * 16);
   SCR(s.xsend, uint64_t*, 8 * (size_t)kBatchPods * kXRec);
@@ -2053,6 +2154,34 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   }
 }
 
+// Topology batch runs (class 3 pods, ksim_tbatch.hip): tlen[i] = the number
+// of consecutive class-3 pods from i (at most kTbPods) none of which reads a
+// count class an earlier one of them adds (its uses' classes against the
+// earlier pods' adds), so that a batch starting at i sees every class it
+// reads at its S0 value.  0 for the other pods.
+void tbatch_runs(const ksim_pod_set* ps, const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen) {
+  const int32_t n = ps->n_pods;
+  tlen.assign((size_t)std::max(n, 0), 0);
+  int32_t n_cls = 0;
+  for (int32_t k = 0; k < ps->n_adds; k++) n_cls = std::max(n_cls, ps->adds[k].cls + 1);
+  std::vector<int32_t> stamp((size_t)n_cls, -1);   // class -> the window start that added it
+  for (int32_t i = 0; i < n; i++) {
+    if (batchable[i] != 3) continue;
+    int32_t L = 0;
+    for (int32_t j = i; j < n && L < kTbPods && batchable[j] == 3; j++, L++) {
+      const ksim_pod& p = ps->pods[j];
+      bool clash = false;
+      for (int32_t u = 0; u < p.use_count && !clash; u++) {
+        const int32_t c = ps->uses[p.use_first + u].cls;
+        clash = c >= 0 && c < n_cls && stamp[c] == i;
+      }
+      if (clash) break;
+      for (int32_t a = 0; a < p.add_count; a++) stamp[ps->adds[p.add_first + a].cls] = i;
+    }
+    tlen[i] = std::max(L, 1);
+  }
+}
+
 int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   int rc = ensure_ready(h);
   if (rc) return rc;
@@ -2118,7 +2247,9 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->soft_le1.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
   for (int32_t i = 0; i < ps->n_pods; i++) {
-    batchable[i] = pod_batchable(h, ps->pods[i]) ? 1 : 0;
+    bool nv = false;
+    batchable[i] = (uint8_t)pod_batchable(h, ps->pods[i], &nv);
+    if (nv) bf[i] |= kPodNormVaries;
     h->topo[i] = ps->pods[i].use_count > 0 ? (R.pod[i] ? 2 : 1) : 0;
     // sharded-cycle exchange sizes, laid out as k_dom_pack / k_window_sh do
     bool soft = false;
@@ -2137,9 +2268,29 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     }
     h->soft_le1[i] = n_soft <= 1 ? 1 : 0;
     h->xreg_len[i] = soft ? xr : 0;
-    if (static_trivial(h, ps->pods[i])) bf[i] |= kBatchStaticTrivial;
+    // class-2 pods (pod_batchable) read full rows: taints, labels, scalar columns
+    if (static_trivial(h, ps->pods[i]) && batchable[i] != 2) bf[i] |= kBatchStaticTrivial;
     h->trivial[i] = (bf[i] & kBatchStaticTrivial) ? 1 : 0;
   }
+  std::vector<PodPlan> plans((size_t)ps->n_pods);
+  for (int32_t i = 0; i < ps->n_pods; i++) {
+    plans[i] = make_plan(h, ps->pods[i], uses.data() + std::max(ps->pods[i].use_first, 0));
+    if (R.pod[i]) {
+      plans[i].flags |= kPlanPtab;
+      plans[i].m.ptab = R.mask[i];
+    }
+    if (!R.padd_first.empty() && !getenv("KSIM_NO_TADDS")) {   // the table updates of its binds, listed
+      plans[i].flags |= kPlanTadds;
+      plans[i].tadd_first = R.padd_first[(size_t)i];
+      plans[i].tadd_count = R.padd_count[(size_t)i];
+    }
+    if (batchable[i] == 0 && tbatch_admit(h, ps->pods[i], plans[i], h->hard_small[i] != 0, h->soft_le1[i] != 0)) {
+      batchable[i] = 3;
+      bf[i] |= kPodTopoBatch;
+    }
+  }
+  tbatch_runs(ps, batchable, h->tlen);
+  for (int32_t i = 0; i < ps->n_pods; i++) bf[i] |= std::min(h->tlen[i], 255) << kTlenShift;
   DevPods P{};
   void* p = nullptr;
   if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return drop_queue(rc);
@@ -2154,23 +2305,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.bflags = (const int32_t*)p;
   if ((rc = put(uses.data(), sizeof(ksim_topo_use) * uses.size(), &p))) return drop_queue(rc);
   P.uses = (const ksim_topo_use*)p;
-  {
-    std::vector<PodPlan> plans((size_t)ps->n_pods);
-    for (int32_t i = 0; i < ps->n_pods; i++) {
-      plans[i] = make_plan(h, ps->pods[i], uses.data() + std::max(ps->pods[i].use_first, 0));
-      if (R.pod[i]) {
-        plans[i].flags |= kPlanPtab;
-        plans[i].m.ptab = R.mask[i];
-      }
-      if (!R.padd_first.empty() && !getenv("KSIM_NO_TADDS")) {   // the table updates of its binds, listed
-        plans[i].flags |= kPlanTadds;
-        plans[i].tadd_first = R.padd_first[(size_t)i];
-        plans[i].tadd_count = R.padd_count[(size_t)i];
-      }
-    }
-    if ((rc = put(plans.data(), sizeof(PodPlan) * plans.size(), &p))) return drop_queue(rc);
-    P.plans = (const PodPlan*)p;
-  }
+  if ((rc = put(plans.data(), sizeof(PodPlan) * plans.size(), &p))) return drop_queue(rc);
+  P.plans = (const PodPlan*)p;
   if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)ps->n_adds, &p))) return drop_queue(rc);
   P.adds = (const ksim_class_add*)p;
   if ((rc = put(R.ent.data(), sizeof(int4) * R.ent.size(), &p))) return drop_queue(rc);
@@ -2222,7 +2358,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   if (is_sharded(h)) {
-    for (int32_t i = first; i < first + count; i++) perpod += h->batchable[i] ? 0 : 1;
+    for (int32_t i = first; i < first + count; i++) perpod += pod_on_batch(h, i) ? 0 : 1;
     rc = shard_schedule({h}, first, count);
   } else {
     rc = for_each_run(h, first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
@@ -2402,7 +2538,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   if (rc) return rc;
   if (!avg_ms || reps < 1 || !h->dp.pods || first < 0 || first >= h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "bad ksim_time_eval arguments");
-  const bool batch = h->batchable[first] && !is_sharded(h);
+  const bool batch = pod_on_batch(h, first) && !is_sharded(h);
+  if (batch && h->batchable[first] == 3)
+    return set_err(h, KSIM_E_UNSUPPORTED, "topology batch evaluations span two kernels");
   if (batch && adapt_mode(h)) return set_err(h, KSIM_E_UNSUPPORTED, "ADAPT batch evaluations span two kernels");
   HIPCHK(h, hipSetDevice(h->device));
   const int32_t end = batch ? std::min(h->dp.n_pods, first + kBatchPods) : first + 1;
@@ -2440,13 +2578,15 @@ const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerBatch) return kBatchKernelNames[k];
   k -= kKernelsPerBatch;
   if (k >= 0 && k < kKernelsPerAdapt) return kAdaptKernelNames[k];
+  k -= kKernelsPerAdapt;
+  if (k >= 0 && k < kKernelsPerTbatch) return kTbatchKernelNames[k];
   return nullptr;
 }
 
 int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms, int64_t* launches, int32_t cap) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt;
+  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch;
   if (!avg_ms || cap < kKinds) return set_err(h, KSIM_E_INVALID, "avg_ms too small");
   if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
@@ -2458,6 +2598,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     int r;
     if ((r = set_run(h, lo, hi))) return r;
     const bool adapt = batch && adapt_mode(h);
+    const bool tb = batch && topo;                 // topology batch runs (class 3)
     // the same kernel variants the run itself would launch
     a.fast = batch && run_fast(h, lo, hi);
     a.fuse_min = !batch && topo;
@@ -2465,17 +2606,26 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     a.fuse_ext = !batch;
     for (int32_t i = lo; i < hi && a.fuse_ext; i++) a.fuse_ext = h->soft_le1[i] != 0;
     a.ptab = !batch && h->topo[lo] == 2;
-    const int per = adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
-    const int base = adapt ? kKernelsPerCycle + kKernelsPerBatch : batch ? kKernelsPerCycle : 0;
+    const int per = tb ? kKernelsPerTbatch : adapt ? kKernelsPerAdapt : batch ? kKernelsPerBatch : kKernelsPerCycle;
+    const int base = tb      ? kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt
+                     : adapt ? kKernelsPerCycle + kKernelsPerBatch
+                     : batch ? kKernelsPerCycle : 0;
+    if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
     int32_t cursor = lo;
     uint32_t launched = (1u << per) - 1;         // batch paths launch every kernel of a batch
     while (cursor < hi) {
-      const int32_t iters = batch ? std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods) : std::min(512, hi - cursor);
+      int32_t iters = batch ? std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods) : std::min(512, hi - cursor);
+      if (tb) {                                  // the batches the host's run lengths predict (run_tbatch)
+        iters = 0;
+        for (int32_t i = cursor; i < hi && iters < 64; iters++) i += std::min(std::min(kTbPods, hi - i), std::max(h->tlen[i], 1));
+      }
       std::vector<hipEvent_t> evs((size_t)iters * (per + 1));
       for (auto& e : evs) HIPCHK(h, hipEventCreate(&e));
       if (batch) HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
       for (int32_t i = 0; i < iters; i++) {
-        if (adapt)
+        if (tb)
+          launched = launch_tbatch(a, h->stream, &evs[(size_t)i * (per + 1)]);
+        else if (adapt)
           launched = launch_batch_adapt(a, h->stream, &evs[(size_t)i * (per + 1)]);
         else if (batch)
           launched = launch_batch(a, h->stream, &evs[(size_t)i * (per + 1)]);

@@ -20,6 +20,7 @@ static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch 
 constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
 constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
 constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
+constexpr int kTopNsMaxChunks = 4;   // node chunks of the node-split batch top (k_batch_top_ns)
 constexpr int kXRec = kTopT + 1;   // sharded exchange record per pod: T keys + (count | complete << 32)
 constexpr int kMaxShards = 8;      // shards of one simulation (one per GPU of a node)
 constexpr int kGmergeSlots = (kTopT * kMaxShards + 63) / 64;   // list entries per lane in k_batch_gmerge
@@ -55,6 +56,14 @@ constexpr int kKernelsPerBatch = 5;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
 constexpr int kKernelsPerAdapt = 6;
 extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
+// Topology batch path (ksim_tbatch.hip): at most kTbPods pods per batch (the
+// host's class-conflict-free runs, bflags >> kTlenShift), clusters of at most
+// kTbMaxBlocks node blocks of 256.
+constexpr int kTbPods = 32;
+constexpr int kTbMaxBlocks = 64;
+constexpr int kKernelsPerTbatch = 5;
+extern const char* const kTbatchKernelNames[kKernelsPerTbatch];
+uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).
 // evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.

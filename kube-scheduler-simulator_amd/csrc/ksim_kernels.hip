@@ -21,17 +21,11 @@
 #include "ksim_device.h"
 #include "ksim_internal.h"
 #include "ksim_wave.h"
+#include "ksim_cycle.h"
 
 namespace ksim {
 
 // ---- wave64 / block reductions ------------------------------------------------
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  lo = (uint32_t)__shfl_xor((int)lo, m, 64);
-  hi = (uint32_t)__shfl_xor((int)hi, m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
@@ -46,15 +40,6 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   for (int m = 32; m >= 1; m >>= 1) {
     int64_t o = (int64_t)shfl_xor_u64((uint64_t)v, m);
     v = o > v ? o : v;
-  }
-  return v;
-}
-
-__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    int64_t o = (int64_t)shfl_xor_u64((uint64_t)v, m);
-    v = o < v ? o : v;
   }
   return v;
 }
@@ -145,41 +130,6 @@ __device__ int32_t block_sum_i32_nw(int32_t v, int32_t* sh) {
 #pragma unroll
   for (int i = 0; i < NW; i++) r += sh[i];
   return r;
-}
-
-// ---- normalization ----------------------------------------------------------
-// Extrema a slot needs, merged over the kept feasible list:
-//   DefaultNormalizeScore: maxCount = max(0, max)          (helper/normalize_score.go)
-//   PodTopologySpread:     maxScore = max(0, max), minScore = min, IgnoredNodes excluded
-//   InterPodAffinity:      min / max, only when topologyScore is non-empty
-__device__ __forceinline__ int64_t normalize_value(int32_t kind, int64_t v, int64_t gmax, int64_t gmin,
-                                                   bool ipa_nonempty) {
-  switch (kind) {
-    case kNormDefault: {
-      int64_t m = gmax > 0 ? gmax : 0;
-      return m == 0 ? v : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
-    }
-    case kNormDefaultReverse: {
-      int64_t m = gmax > 0 ? gmax : 0;
-      return m == 0 ? (int64_t)kMaxNodeScore
-                    : (int64_t)kMaxNodeScore - div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v), m);
-    }
-    case kNormPTS: {
-      int64_t mx = gmax > 0 ? gmax : 0;
-      return mx == 0 ? (int64_t)kMaxNodeScore
-                     : div_trunc_pos((int64_t)((uint64_t)kMaxNodeScore * (uint64_t)(mx + gmin - v)), mx);
-    }
-    case kNormIPA:
-    case kNormMinMax: {
-      if (kind == kNormIPA && !ipa_nonempty) return v;
-      const int64_t diff = gmax - gmin;
-      double f = 0;
-      if (diff > 0) f = (double)kMaxNodeScore * ((double)(v - gmin) / (double)diff);
-      return (int64_t)f;
-    }
-    default:
-      return v;
-  }
 }
 
 // ==== A. per-pod path ===========================================================
@@ -344,11 +294,9 @@ __global__ __launch_bounds__(256) void k_topo_min(DevCluster c, DevPods P, ksim_
 // function of one count (round(count * w + maxSkew - 1), w > 0 known only
 // after the pass), so its slots hold the count extrema and k_select maps them.
 
-// Order-preserving u64 images of an int64 so extrema are atomicMax on u64:
-// max image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both.
-// (max_image / from_max_image: ksim_device.h)
-__device__ __forceinline__ uint64_t min_image(int64_t x) { return ~((uint64_t)x ^ (1ull << 63)); }
-__device__ __forceinline__ int64_t from_min_image(uint64_t m) { return (int64_t)(~m ^ (1ull << 63)); }
+// Extrema are atomicMax over order-preserving u64 images of an int64 (max
+// image x ^ 2^63, min image ~(x ^ 2^63); 0 is the identity of both:
+// ksim_device.h).
 
 // Wave max of (img, lo) pairs in lexicographic order (selectHost over full
 // int64 totals): the max image first, then the max lo among the lanes holding it.
@@ -362,52 +310,6 @@ __device__ __forceinline__ void best2_merge(uint64_t& img, uint64_t& lo, uint64_
     img = img2;
     lo = lo2;
   }
-}
-
-// Per-slot extrema images of this block's values -> one atomicMax per slot.
-// zmask: slots whose raw score is 0 on every node for this pod; their extrema
-// are (0, 0) whenever some node is feasible (and unread otherwise), so block 0
-// stores them without a reduction.
-// s_cnt (optional): per wave {feasible, ignored} counts, added to the window
-// counters once per block after the barrier (one atomic per block, not per wave).
-__device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState* win, const uint64_t (&ix)[KSIM_MAX_SCORE],
-                                              const uint64_t (&in)[KSIM_MAX_SCORE], uint64_t (*s_red)[2 * KSIM_MAX_SCORE],
-                                              uint32_t zmask = 0, const int32_t (*s_cnt)[2] = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int S = prof.n_score;
-#pragma unroll
-  for (int k = 0; k < KSIM_MAX_SCORE; k++) {
-    if (k >= S) break;
-    if (norm_kind(prof.score[k]) == kNormNone || ((zmask >> k) & 1u)) continue;
-    const uint64_t a = wave_max_u64_dpp(ix[k]), b = wave_max_u64_dpp(in[k]);
-    if (lane == 0) {
-      s_red[wv][2 * k] = a;
-      s_red[wv][2 * k + 1] = b;
-    }
-  }
-  __syncthreads();
-  if (tid < 2 * KSIM_MAX_SCORE && tid < 2 * S && norm_kind(prof.score[tid >> 1]) != kNormNone) {
-    uint64_t m = 0;
-    if ((zmask >> (tid >> 1)) & 1u) {
-      m = blockIdx.x == 0 ? ((tid & 1) ? ~(1ull << 63) : (1ull << 63)) : 0ull;   // min_image(0) / max_image(0)
-    } else {
-#pragma unroll
-      for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][tid]);
-    }
-    if (m) atomicMax(reinterpret_cast<unsigned long long*>(&win->ext[tid]), (unsigned long long)m);
-  }
-  if (s_cnt && (tid == 64 || tid == 65)) {
-    const int q = tid - 64;
-    const int32_t v = s_cnt[0][q] + s_cnt[1][q] + s_cnt[2][q] + s_cnt[3][q];
-    if (v) atomicAdd(q ? &win->nign : &win->nfeas, v);
-  }
-}
-
-// scoreForCount with a single constraint (k_extrema's sum from 0, unfused)
-__device__ __forceinline__ int64_t soft_score(int64_t cnt, double w, int32_t max_skew) {
-  double score = 0;
-  score = score + ((double)cnt * w + (double)(max_skew - 1));
-  return (int64_t)round(score);
 }
 
 // KSIM_FS_CLOCKS builds: per-block phase times of k_filter_score (thread 0,
@@ -459,43 +361,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   if (p.use_count) load_topo_row(c, U, p.use_count, m, s, P0.ptab, xr, t);
   const bool pt = (pp.flags & kPlanPtab) != 0;    // block-uniform: persistent tables
   if ((fuse_min && m.hard) || (pt && (m.aff | m.score))) {
-    if (threadIdx.x < 64 && fuse_min) {            // the critical paths, one wave
-      for (uint32_t b = m.hard; b; b &= b - 1) {
-        const int i = __builtin_ctz(b);
-        const ksim_topo_use u = load_use(U, i);
-        int64_t mn = 2147483647;
-        if (u.col != KSIM_COL_NONE) {
-          const int32_t V = c.col_nvals[u.col];
-          const int64_t* d = pt ? P0.ptab + u._pad : s.dom + (size_t)i * c.vmax;
-          for (int32_t v = threadIdx.x; v < V; v += 64) {
-            const int64_t x = d[v];
-            if ((x >> kDomMarkShift) != 0) mn = min(mn, x & kDomCountMask);
-          }
-        }
-        mn = wave_min_i64(mn);
-        if (threadIdx.x == 0) s_min[i] = mn;
-      }
-    } else if (threadIdx.x >= 64 && threadIdx.x < 128 && pt) {
-      // len(affinityCounts) > 0 / len(topologyScore) > 0 from the tables
-      // (k_topo_prefilter's flags): some node with the key and a count
-      uint32_t f = 0;
-      for (uint32_t b = m.aff | m.score; b; b &= b - 1) {
-        const int i = __builtin_ctz(b);
-        const ksim_topo_use u = load_use(U, i);
-        if (u.col == KSIM_COL_NONE || u.cls < 0) continue;
-        const bool total = (m.node_count >> i) & 1u;   // a kPtabTotal table
-        const int32_t V = total ? 1 : c.col_nvals[u.col];
-        const int64_t* d = P0.ptab + u._pad;
-        bool nz = false;
-        for (int32_t v = (int32_t)threadIdx.x - 64 + (total ? 0 : 1); v < V; v += 64) nz = nz || d[v] != 0;
-        if (__ballot(nz))
-          f |= (((m.aff >> i) & 1u) ? kTopoAffinityNonEmpty : 0u) | (((m.score >> i) & 1u) ? kTopoScoreNonEmpty : 0u);
-      }
-      if (threadIdx.x == 64) {
-        s_tf = f;
-        if (blockIdx.x == 0) st->topo_flags = f;    // k_select's normalization reads it
-      }
-    }
+    // k_select's normalization reads the flags from the state
+    topo_block_setup(c, P0, s, U, m, pt, fuse_min != 0, s_min, &s_tf, &st->topo_flags);
     __syncthreads();
     if (fuse_min && m.hard) s.min_match = s_min;   // pts_filter reads the block's copy
   }
@@ -907,12 +774,32 @@ __global__ __launch_bounds__(256) void k_extrema(DevCluster c, DevPods P, ksim_p
 // the window state from the filter pass's counters, as k_extrema<true> does,
 // and block 0 publishes it for k_bind; PodTopologySpread's raw scores and
 // extrema come from the soft use's counts.
+// The window scalars bind_cycle reads (see its ws argument).
+struct WinScalars {
+  int32_t nscan, nf, cut, evaluated, k, error;
+};
+
 // selectHost over k_select's per-block records (one wave): the winning TB lo
 // word (0: no kept node).
+// KSIM_SEL_SC1=1 builds: k_select's blocks store their records write-through
+// (sc1) and drain them before a relaxed ticket add; the last block reads them
+// with sc1 loads, which miss its L1, so no agent fence is paid on either side
+// (cdna_hip_programming.md §6 Guideline 16, the sc1 form).  Measured and not
+// kept (profiles/r03/ab_sel, config 3, same box): 27.8 us per pod against
+// 26.7 us for the default acq_rel ticket (release + acquire in every block).
+#ifndef KSIM_SEL_SC1
+#define KSIM_SEL_SC1 0
+#endif
 __device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32_t n_blocks) {
   const int lane = threadIdx.x & 63;
   uint64_t img = 0, lo = 0;
+#if KSIM_SEL_SC1
+  for (int32_t b = lane; b < n_blocks; b += 64)
+    best2_merge(img, lo, __hip_atomic_load(&s.bbest[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(&s.bbest[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#else
   for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
+#endif
   wave_best2(img, lo);
   return lo;
 }
@@ -924,7 +811,7 @@ __device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32
 // k_topo_prefilter clears the registration rows).
 __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P, DevState* __restrict__ st,
                                            const DevScratch& s, int32_t* __restrict__ chosen_out, int32_t pi,
-                                           bool nowin, const PodPlan& pp) {
+                                           bool nowin, const PodPlan& pp, const WinScalars* ws = nullptr) {
   WinState* win = s.win;
   // the pod's persistent-table updates, loaded ahead of the selection they do not depend on
   const int lane = threadIdx.x & 63;
@@ -935,10 +822,13 @@ __device__ __forceinline__ void bind_cycle(const DevCluster& c, const DevPods& P
   if (lane < P.pods[pi].add_count) add0 = P.adds[P.pods[pi].add_first + lane];
   // the window scalars and the scheduler state do not depend on the choice
   // either (the row stores below could alias them for the compiler: load first)
-  const int32_t NS = win->nscan, nf = win->nf, cut = win->cut, evaluated = win->evaluated, k = win->k;
+  // (ws: the launch's own block 0 writes them -- k_select fuse_ext -- and the
+  // caller passes the values it derived itself instead of reading them back)
+  const int32_t NS = ws ? ws->nscan : win->nscan, nf = ws ? ws->nf : win->nf, cut = ws ? ws->cut : win->cut,
+                evaluated = ws ? ws->evaluated : win->evaluated, k = ws ? ws->k : win->k;
   DevState S = *st;                                // one read, one write back: no load-store chain
   const uint64_t best = reduce_block_best(s, (c.n + 255) / 256);   // every lane
-  const int32_t error = win->error;
+  const int32_t error = ws ? ws->error : win->error;
   const int32_t chosen = best && !error ? key_node(best) : -1;   // unsharded: base == 0
   const ksim_pod p = P.pods[pi];
   if (chosen >= 0) {
@@ -1152,23 +1042,46 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     uint64_t bi = s_best[0], bl = s_best[1];
 #pragma unroll
     for (int w = 1; w < 4; w++) best2_merge(bi, bl, s_best[2 * w], s_best[2 * w + 1]);
-    s.bbest[2 * blockIdx.x] = bi;
-    s.bbest[2 * blockIdx.x + 1] = bl;
+#if KSIM_SEL_SC1
+    if (bind_mode) {
+      __hip_atomic_store(&s.bbest[2 * blockIdx.x], bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&s.bbest[2 * blockIdx.x + 1], bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else
+#endif
+    {
+      s.bbest[2 * blockIdx.x] = bi;
+      s.bbest[2 * blockIdx.x + 1] = bl;
+    }
   }
   SEL_CLK(3);
   if (bind_mode) {
-    // the last block: its acquire sees every block's record (and block 0's
-    // window fields) released by their own increments
     __shared__ int32_t s_last;
     if (tid == 0) {
+#if KSIM_SEL_SC1
+      // the record is the only byte the last block reads from this launch's
+      // other blocks (fuse_ext's window scalars it derives itself, below):
+      // drain its write-through store, then take a ticket
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int32_t done = __hip_atomic_fetch_add(&win->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      // the last block: its acquire sees every block's record (and block 0's
+      // window fields) released by their own increments
       const int32_t done = __hip_atomic_fetch_add(&win->done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       s_last = done == (int32_t)gridDim.x - 1;
     }
     __syncthreads();
     SEL_CLK(4);
     if (s_last && tid < 64) {
-      if (tid == 0) win->done = 0;
-      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp);
+      if (tid == 0) __hip_atomic_store(&win->done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the record loads below the ticket
+      WinScalars ws{};
+      if (fuse_ext) {                              // the values block 0 stored, derived as it did
+        ws.nscan = ws.cut = ws.evaluated = ws.k = ss.n;
+        ws.nf = nf;
+        ws.error = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? kCycleErrorPrefilter : 0;
+      }
+      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp, fuse_ext && KSIM_SEL_SC1 ? &ws : nullptr);
 #ifdef KSIM_SEL_CLOCKS
       if (tid == 0) {
         atomicAdd(&s.dbg[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - sel_t));

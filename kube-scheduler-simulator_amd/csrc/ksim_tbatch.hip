@@ -1,0 +1,407 @@
+// ksim_tbatch.hip — the topology batch path (gfx950): pods with
+// PodTopologySpread / InterPodAffinity uses, scheduled up to kTbPods at a time
+// against the batch-start snapshot S0 (SURVEY §7 hard part 3; config 3).
+//
+// A pod's topology inputs are count classes (§5): the domain sums it reads
+// come from the persistent tables of the classes its uses name, and a bind
+// changes only the classes in the bound pod's adds.  The host cuts the queue
+// into runs in which no pod reads a class an earlier pod of the run adds
+// (DevPods.bflags >> kTlenShift, ksim_engine.cpp tbatch_runs).  Inside such a
+// run every pod's filter verdicts, raw scores, normalization extrema and
+// PodTopologySpread weights on every node are those of S0, except on the
+// nodes earlier pods of the batch bound, and there only NodeResourcesFit and
+// the two resource scores move.  So the P100 batch machinery applies: each
+// pod's exact S0 top-T, the greedy chain, the pair keys of every pod on the
+// earlier pods' nodes, and the commit up to the first pod whose choice
+// differs.  One more way a pod's S0 keys can fail: a node that was feasible
+// at S0 stops fitting after an earlier bind, which changes the feasible set
+// the normalization and the spread weights were taken over; such a pod ends
+// the batch before it (pinv), and the next batch starts from it.
+//
+//   k_tb_filter      grid (node blocks, pods): RunFilterPlugins and the raw
+//                    scores of pod j on every node (k_filter_score's plan
+//                    chains), feasible / ignored counts and NormalizeScore
+//                    extrema per pod (block_extrema), the critical paths and
+//                    InterPodAffinity flags from the persistent tables
+//   k_tb_select      grid (node blocks, pods): normalized weighted totals (as
+//                    k_select), TB keys, each block's exact top-T per pod, and
+//                    per node stat = total - (Fit + BalancedAllocation) part
+//   k_tb_merge       one wave per pod: the pod's exact top-T from its blocks'
+//   k_tb_chain_pairs the chain (ksim_chain.h), then pod j on each earlier
+//                    guess: stat + the resource part after that bind, or pinv
+//   k_tb_commit      batch_commit (class adds and persistent tables in the
+//                    binds), then the window state re-zeroed for the next batch
+#include "ksim_device.h"
+#include "ksim_internal.h"
+#include "ksim_wave.h"
+#include "ksim_cycle.h"
+#include "ksim_commit.h"
+#include "ksim_chain.h"
+
+namespace ksim {
+
+constexpr int32_t kStatNone = INT32_MIN;       // tb_stat: not feasible at S0
+constexpr int32_t kStatOne = INT32_MIN + 1;    // tb_stat: the pod's only feasible node (chosen unscored)
+
+// The batch's pod count: the conflict-free run from the cursor, capped.
+__device__ __forceinline__ int32_t tb_count(const DevState* __restrict__ st, const DevPods& P) {
+  const int32_t base = st->cursor;
+  if (base >= st->end) return 0;
+  const int32_t tlen = P.bflags[base] >> kTlenShift;
+  return min(min(kTbPods, st->end - base), max(tlen, 1));
+}
+
+// Pod j's slices of the topology batch scratch.
+struct TbSlice {
+  uint8_t* fail;
+  uint8_t* ign;
+  int64_t* part;
+  int64_t* raw;
+  int32_t* stat;
+  WinState* win;
+};
+__device__ __forceinline__ TbSlice tb_slice(const DevScratch& s, int32_t j, int32_t n) {
+  const size_t N = (size_t)n;
+  return TbSlice{s.tb_fail + j * N, s.tb_ign + j * N, s.tb_part + j * N, s.tb_raw + (size_t)j * KSIM_MAX_SCORE * N,
+                 s.tb_stat + j * N, s.tb_win + j};
+}
+
+__global__ __launch_bounds__(256) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
+                                                   const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
+                                                   DevScratch s) {
+  __shared__ int64_t s_min[KSIM_MAX_USES];
+  __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
+  __shared__ int32_t s_cnt[4][2];
+  __shared__ uint32_t s_tf;
+  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t xr = node < c.n ? node : c.n - 1;
+  // the node's row does not depend on the pod: its loads go out first
+  const NodeRow r = load_row(c, xr);
+  const double inv_c = c.inv_cpu[xr], inv_m = c.inv_mem[xr];
+  const int32_t j = blockIdx.y;
+  if (j >= tb_count(st, P0)) return;                // block-uniform
+  const ksim_profile& prof = *prof_p;
+  const int32_t pi = st->cursor + j;
+  const DevPods& P = P0;
+  const ksim_pod& p = P0.pods[pi];
+  const PodPlan pp = P0.plans[pi];
+  const UseMasks& m = pp.m;
+  const ksim_topo_use* U = P.uses + p.use_first;
+  const TbSlice q = tb_slice(s, j, c.n);
+  TopoRow t;
+  load_topo_row(c, U, p.use_count, m, s, P0.ptab, xr, t);
+  const bool pt = (pp.flags & kPlanPtab) != 0;      // the host admits only table-read pods (tbatch_admit)
+  if (m.hard || (pt && (m.aff | m.score))) {
+    topo_block_setup(c, P0, s, U, m, pt, true, s_min, &s_tf, &q.win->tflags);
+    __syncthreads();
+  }
+  const uint32_t tf = pt && (m.aff | m.score) ? s_tf : 0u;
+  bool feasible = false, ign = false;
+  RawScores rv{};
+  int64_t soft_cnt = 0;
+  const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;   // the pod's one ScheduleAnyway use
+  if (node < c.n) {
+    uint32_t det;
+    const uint8_t res = run_filter_plan(c, P, FilterPlan{bp->rank_lo, bp->rank_hi, pp.filter_en}, s_min, tf, p, r,
+                                        U, m, t, det);
+    q.fail[node] = res;
+    feasible = res == KSIM_PASSED;
+    if (feasible) {
+#pragma unroll
+      for (int i = 0; i < KSIM_MAX_USES; i++) {
+        if (((m.soft >> i) & 1u) && t.v[i] == 0) ign = true;
+        if (i == soft) soft_cnt = t.x[i];
+      }
+      q.ign[node] = ign;
+      const BatchProg* fast = (bp->fast_w && (c.cflags & kClusterNarrow)) ? bp : nullptr;
+      // store_plain: the Fit / BalancedAllocation raw scores stay for k_tb_select's stat
+      q.part[node] = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, q.raw, true, rv,
+                                    soft_cnt, fast, inv_c, inv_m);
+    }
+  }
+  // feasible / ignored counts and the NormalizeScore extrema (k_filter_score's fuse_ext tail)
+  const int lane = threadIdx.x & 63;
+  const uint64_t fm = __ballot(feasible), im = __ballot(feasible && ign);
+  if (lane == 0) {
+    s_cnt[threadIdx.x >> 6][0] = (int32_t)__popcll(fm);
+    s_cnt[threadIdx.x >> 6][1] = (int32_t)__popcll(im);
+  }
+  uint64_t ix[KSIM_MAX_SCORE], in[KSIM_MAX_SCORE];
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+    ix[k] = in[k] = 0;
+    if (k >= prof.n_score || !feasible) continue;
+    const int pl = (int)prof_score(prof, k);
+    if (norm_kind(pl) == kNormNone) continue;
+    int64_t v = 0;
+    bool counted = true;
+    if (pl == KSIM_PL_POD_TOPOLOGY_SPREAD) {
+      counted = soft < 0 || !ign;                  // IgnoredNodes: not in min / max
+      v = soft < 0 ? 0 : soft_cnt;
+    } else {
+      v = rv.of(pl);
+    }
+    if (counted) {
+      ix[k] = max_image(v);
+      in[k] = min_image(v);
+    }
+  }
+  uint32_t zmask = 0;                              // slots constant 0 for this pod
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+    if (k >= prof.n_score) continue;
+    const int pl = (int)prof_score(prof, k);
+    const bool z = (pl == KSIM_PL_TAINT_TOLERATION && !(c.cflags & kClusterPreferTaints)) ||
+                   (pl == KSIM_PL_NODE_AFFINITY && p.pref_term_count == 0) ||
+                   (pl == KSIM_PL_INTER_POD_AFFINITY && m.score == 0) ||
+                   (pl == KSIM_PL_POD_TOPOLOGY_SPREAD && soft < 0);
+    if (z) zmask |= 1u << k;
+  }
+  block_extrema(prof, q.win, ix, in, s_red, zmask, s_cnt);
+}
+
+// Each block's exact top-T keys of pod j over its 256 nodes: every wave
+// extracts its own top-T (kTopT rounds of DPP max), wave 0 ranks the 4 T
+// candidates (keys are unique: ranks are distinct).
+__device__ __forceinline__ void block_top_t(uint64_t key, uint64_t* s_cand, uint64_t* out, int32_t* out_cnt) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t a = key;
+#pragma unroll 1
+  for (int e = 0; e < kTopT; e++) {
+    const uint64_t mx = wave_max_u64_dpp(a);
+    if (lane == 0) s_cand[wv * kTopT + e] = mx;
+    if (a == mx) a = 0;                            // 0 stays 0: an exhausted wave lists zeros
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  constexpr int kC = 4 * kTopT;
+  static_assert(kC <= 64, "block_top_t geometry");
+  const uint64_t c0 = lane < kC ? s_cand[lane] : 0;
+  int32_t rank = 0;
+#pragma unroll
+  for (int x = 0; x < kC; x++) rank += s_cand[x] > c0;
+  const int32_t n = __popcll(__ballot(c0 != 0));
+  if (c0 != 0 && rank < kTopT) out[rank] = c0;
+  if (lane >= n && lane < kTopT) out[lane] = 0;
+  if (lane == 0) *out_cnt = n < kTopT ? n : kTopT;
+}
+
+__global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
+                                                   const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
+                                                   DevScratch s) {
+  __shared__ uint64_t s_cand[4 * kTopT];
+  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t j = blockIdx.y;
+  if (j >= tb_count(st, P0)) return;                // block-uniform
+  const ksim_profile& prof = *prof_p;
+  const int32_t N = c.n;
+  const int S = prof.n_score;
+  const int32_t pi = st->cursor + j;
+  const ksim_pod& p = P0.pods[pi];
+  const UseMasks m = P0.plans[pi].m;
+  const ksim_topo_use* U = P0.uses + p.use_first;
+  const TbSlice q = tb_slice(s, j, N);
+  const WinState* win = q.win;
+  const int32_t nf = win->nfeas;
+  const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
+  const bool has_soft = nf > 1 && soft >= 0;
+  double w_soft = 0;
+  int32_t ms = 0;
+  if (has_soft) {                                  // topologyNormalizingWeight (hostname keys only: tbatch_admit)
+    const ksim_topo_use u = load_use(U, soft);
+    w_soft = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - win->nign : 0];
+    ms = u.arg;
+  }
+  const bool ipa_nonempty = (win->tflags & kTopoScoreNonEmpty) != 0;
+  const ScorePlan sp{bp->slot, bp->slot_hi};
+  const int k_fit = plan_slot(sp, KSIM_PL_NODE_RESOURCES_FIT), k_ba = plan_slot(sp, KSIM_PL_BALANCED_ALLOCATION);
+  const uint64_t seed = prof.tiebreak_seed;
+  const int64_t seq = st->pod_seq + j;
+  uint64_t key = 0;
+  if (node < N) {
+    int32_t stat = kStatNone;
+    if (q.fail[node] == KSIM_PASSED) {
+      if (nf > 1) {
+        const bool ign = has_soft && q.ign[node];
+        int64_t tot = S == 0 ? 1 : q.part[node];
+        for (int k = 0; k < S; k++) {
+          const int32_t kind = norm_kind(prof_score(prof, k));
+          if (kind == kNormNone) continue;
+          int64_t gmax = from_max_image(win->ext[2 * k]), gmin = from_min_image(win->ext[2 * k + 1]);
+          int64_t raw;
+          if (kind == kNormPTS) {
+            raw = 0;
+            if (has_soft) {                        // counts -> scores (a non-decreasing map)
+              if (!ign) raw = soft_score(q.raw[(size_t)k * N + node], w_soft, ms);
+              if (win->ext[2 * k]) gmax = soft_score(gmax, w_soft, ms);
+              if (win->ext[2 * k + 1]) gmin = soft_score(gmin, w_soft, ms);
+            }
+          } else {
+            raw = q.raw[(size_t)k * N + node];
+          }
+          const int64_t nv = (kind == kNormPTS && ign) ? 0 : normalize_value(kind, raw, gmax, gmin, ipa_nonempty);
+          tot += nv * prof_weight(prof, k);
+        }
+        int64_t dyn0 = 0;                          // the part a bind on this node moves
+        if (k_fit >= 0) dyn0 += bp->w_fit * q.raw[(size_t)k_fit * N + node];
+        if (k_ba >= 0) dyn0 += bp->w_ba * q.raw[(size_t)k_ba * N + node];
+        stat = (int32_t)(tot - dyn0);
+        key = tb_key(tot, seed, seq, c.base + node);
+      } else {                                     // one feasible node: schedulePod takes it unscored
+        stat = kStatOne;
+        key = tb_key(0, seed, seq, c.base + node);
+      }
+    }
+    q.stat[node] = stat;
+  }
+  const size_t cl = (size_t)j * kTbMaxBlocks + blockIdx.x;
+  block_top_t(key, s_cand, s.tb_clist + cl * kTopT, s.tb_ccnt + cl);
+}
+
+// Pod j's exact top-T from its blocks' exact lists (the pod's top-T lies in
+// the union of the blocks' top-T): one wave, lane b holds block b's list.
+__global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const DevState* __restrict__ st,
+                                                 DevScratch s) {
+  const int lane = threadIdx.x;
+  const int32_t j = blockIdx.x;
+  if (j >= tb_count(st, P)) return;
+  const int32_t nblk = (c.n + 255) / 256;
+  uint64_t L[kTopT];
+  int32_t cnt = 0;
+  const size_t cl = (size_t)j * kTbMaxBlocks + lane;
+  if (lane < nblk) {
+    cnt = s.tb_ccnt[cl];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) L[e] = s.tb_clist[cl * kTopT + e];
+  }
+#pragma unroll
+  for (int e = 0; e < kTopT; e++)
+    if (e >= cnt) L[e] = 0;
+  uint64_t mine = 0;
+  int32_t n = 0;
+#pragma unroll 1
+  for (int e = 0; e < kTopT; e++) {
+    const uint64_t mx = wave_max_u64_dpp(L[0]);
+    if (mx == 0) break;
+    if (lane == e) mine = mx;
+    n = e + 1;
+    if (L[0] == mx) {                              // pop the head (a register shift)
+#pragma unroll
+      for (int x = 0; x + 1 < kTopT; x++) L[x] = L[x + 1];
+      L[kTopT - 1] = 0;
+    }
+  }
+  if (lane < kTopT) s.topk[(size_t)j * kTopT + lane] = lane < n ? mine : 0;
+  if (lane == 0) {
+    s.topk_cnt[j] = n;
+    s.topk_complete[j] = s.tb_win[j].nfeas <= kTopT ? 1 : 0;   // every feasible node listed
+  }
+}
+
+// Block j: the chain, then pod j's keys on the guesses of pods k < j after
+// those binds (the S0 stat plus the resource part on the updated row), or
+// pinv[j] when a guess that was feasible for pod j at S0 no longer fits.
+__global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, DevPods P,
+                                                               const ksim_profile* __restrict__ prof_p,
+                                                               const BatchProg* __restrict__ bp_p,
+                                                               const DevState* __restrict__ st, DevScratch s) {
+  __shared__ ChainLds L;
+  __shared__ uint64_t s_wmax[kBatchPods / 64];
+  __shared__ int32_t s_winv[kBatchPods / 64];
+  const int32_t nbt = tb_count(st, P);
+  uint64_t gk;
+  int32_t nchain;
+  if (!chain_block(L, st, s.topk, s.topk_cnt, s.topk_complete, &gk, &nchain, nullptr, nbt)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = blockIdx.x, k = tid;
+  if (j == 0) {
+    if (tid < nbt) s.gkey[tid] = gk;
+    if (tid == 0) *s.chain_end = nchain;
+  }
+  if (j >= nchain) {                               // block-uniform
+    if (tid == 0) {
+      s.pmax[j] = 0;
+      s.pinv[j] = 0;
+    }
+    return;
+  }
+  const ksim_profile& prof = *prof_p;
+  const BatchProg& bp = *bp_p;
+  const int32_t base = st->cursor;
+  const int64_t seq0 = st->pod_seq;
+  uint64_t v = 0;
+  bool inv = false;
+  const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
+  if (local >= 0 && local < c.n) {
+    const int32_t sv = s.tb_stat[(size_t)j * c.n + local];
+    if (sv != kStatNone) {
+      const ksim_pod& p = P.pods[base + j];
+      NodeRow r = load_row(c, local);
+      row_add_pod(r, P.pods[base + k], 1);
+      if (bp.has_fit_filter && fits_request(r, p, c.n_scalar)) {
+        inv = true;
+      } else {
+        int64_t tot = 0;
+        if (sv != kStatOne) {
+          tot = sv;
+          if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, c.n_scalar);
+          if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, c.n_scalar);
+        }
+        v = tb_key(tot, prof.tiebreak_seed, seq0 + j, c.base + local);
+      }
+    }
+  }
+  v = wave_max_u64_dpp(v);
+  const uint64_t b = __ballot(inv);
+  if (lane == 0) {
+    s_wmax[wave] = v;
+    s_winv[wave] = b != 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t mx = 0;
+    int32_t any = 0;
+    for (int w = 0; w < kBatchPods / 64; w++) {
+      mx = umax64(mx, s_wmax[w]);
+      any |= s_winv[w];
+    }
+    s.pmax[j] = mx;
+    s.pinv[j] = any;
+  }
+}
+
+__global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
+                                                          DevScratch s, int32_t* __restrict__ chosen_out) {
+  __shared__ int32_t s_istar, s_sched, s_unsched;
+  const int tid = threadIdx.x;
+  const uint64_t g = s.gkey[tid], m = s.pmax[tid];   // in flight with the state loads
+  const int32_t inv = tid < kTbPods ? s.pinv[tid] : 0;
+  const int32_t nchain = *s.chain_end;
+  const int32_t nbt = tb_count(st, P);
+  if (nbt <= 0) return;
+  batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt);
+  // the next batch's counters and extrema start from zero
+  for (int x = tid; x < kTbPods * (int)(sizeof(WinState) / 4); x += blockDim.x)
+    reinterpret_cast<int32_t*>(s.tb_win)[x] = 0;
+}
+
+const char* const kTbatchKernelNames[kKernelsPerTbatch] = {"k_tb_filter", "k_tb_select", "k_tb_merge",
+                                                           "k_tb_chain_pairs", "k_tb_commit"};
+
+uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
+  const dim3 grid((a.c.n + 255) / 256, kTbPods);
+  if (evs) (void)hipEventRecord(evs[0], stream);
+  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[2], stream);
+  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[3], stream);
+  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  if (evs) (void)hipEventRecord(evs[4], stream);
+  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+  if (evs) (void)hipEventRecord(evs[5], stream);
+  return (1u << kKernelsPerTbatch) - 1;
+}
+
+}  // namespace ksim

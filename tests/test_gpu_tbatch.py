@@ -1,0 +1,121 @@
+"""The topology batch path (ksim_tbatch.hip; class-3 pods of pod_batchable /
+tbatch_admit in ksim_engine.cpp) against the one-by-one oracle: pods with
+PodTopologySpread and InterPodAffinity uses read from the persistent domain
+tables, scheduled up to kTbPods at a time over runs in which no pod reads a
+count class an earlier pod of the run adds.  Placements, evaluation counts,
+node rows and count classes must equal the oracle's (config 3 shapes:
+/root/reference/simulator/scheduler/scheduler.go runs the upstream
+scheduler's per-pod cycle; the restatement is oracle/ksim_oracle.c)."""
+import numpy as np
+import pytest
+
+from ksim import gen, profile
+from ksim.encode import encode_cluster, encode_pods
+from ksim.engine import Engine
+from ksim.model import Container, LabelSelector, Pod
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cluster, pods, weights=None):
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    if weights:
+        sp = sp.with_weights(weights)
+    prof = profile.compile_profile(sp)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert eng.next_start == ora.next_start
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    return eng, st
+
+
+@pytest.mark.parametrize("n_nodes,per_node,n_inc,zone_every", [(300, 4, 800, 50), (1000, 10, 2500, 1000),
+                                                               (257, 3, 700, 7)])
+def test_config3_shapes(n_nodes, per_node, n_inc, zone_every):
+    """Config 3's objects: zone DoNotSchedule + hostname ScheduleAnyway spread
+    on the pod's app, preferred anti-affinity to it, existing pods' required
+    anti-affinity (hostname, and zone-wide for tier=critical) and preferred
+    affinity terms.  Every pod on the topology batch path."""
+    cluster, pods = gen.config3(n_nodes=n_nodes, pods_per_node=per_node, n_incoming=n_inc, seed=n_nodes,
+                                zone_anti_every=zone_every)
+    eng, st = _run(cluster, pods)
+    assert st.perpod_cycles == 0 and st.batches > 0
+    assert st.batches < pods.n_pods                  # batches of several pods
+
+
+def test_nodes_fill_up():
+    """Small nodes: guesses stop fitting for later pods of a batch (pinv ends
+    the batch before them) and pods become unschedulable."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=120, pods_per_node=2, n_incoming=1500, seed=5)
+    for n in nodes:
+        n.allocatable = {"cpu": "2", "memory": "4Gi", "pods": "110"}
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    assert st.perpod_cycles == 0 and st.unschedulable > 0 and st.truncations > 0
+
+
+def test_one_app_serializes():
+    """Every pod spreads over the same selector: each pod reads the class the
+    previous one adds, so every batch holds one pod; still exact."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=200, pods_per_node=3, n_incoming=200, seed=9)
+    for p in inc:
+        p.labels["app"] = "a7"
+        for c in p.topology_spread:
+            c.label_selector = LabelSelector({"app": "a7"})
+        for w in p.pod_anti_affinity_preferred:
+            w.term.label_selector = LabelSelector({"app": "a7"})
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    assert st.batches == 200
+
+
+def test_mixed_with_plain_pods():
+    """Spread pods (topology batches) interleaved with plain pods carrying the
+    same app labels (P100 batches whose binds add to the spread selectors'
+    classes): the runs alternate and hand the snapshot on."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=500, pods_per_node=4, n_incoming=900, seed=17)
+    plain = [Pod(f"plain-{k}", labels={"app": f"a{k % 64}", "tier": "web"},
+                 containers=[Container({"cpu": "300m", "memory": "512Mi"})]) for k in range(900)]
+    queue = []
+    for k in range(900):
+        queue.append(inc[k])
+        if k % 3 == 0:
+            queue.extend(plain[k:k + 3])
+    cluster, _ = encode_cluster(nodes, bound)
+    _run(cluster, encode_pods(cluster, queue))
+
+
+def test_weights_and_soft_only():
+    """Score weights from a config-5 style vector, and pods with only a
+    ScheduleAnyway hostname spread (no hard constraint)."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=400, pods_per_node=5, n_incoming=900, seed=21)
+    for k, p in enumerate(inc):
+        if k % 2:
+            p.topology_spread = [c for c in p.topology_spread if c.when_unsatisfiable == "ScheduleAnyway"]
+    cluster, _ = encode_cluster(nodes, bound)
+    w = {"NodeResourcesFit": 3, "NodeResourcesBalancedAllocation": 7, "PodTopologySpread": 5,
+         "InterPodAffinity": 9, "TaintToleration": 1, "NodeAffinity": 2}
+    _run(cluster, encode_pods(cluster, inc), weights=w)
+
+
+def test_kernel_timing_names():
+    """ksim_time_kernels times the topology batch kernels under their names."""
+    cluster, pods = gen.config3(n_nodes=300, pods_per_node=4, n_incoming=300, seed=3)
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=100))
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    eng.load_pods(pods)
+    kt = eng.time_kernels(0, pods.n_pods)
+    for k in ("k_tb_filter", "k_tb_select", "k_tb_merge", "k_tb_chain_pairs", "k_tb_commit"):
+        assert k in kt and kt[k][1] > 0, (k, kt)

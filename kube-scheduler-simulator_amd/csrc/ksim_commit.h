@@ -42,7 +42,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
                                              int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
                                              int32_t* s_sched, int32_t* s_unsched,
                                              const int2* s_aw = nullptr, const int32_t* inv_own = nullptr,
-                                             int32_t nb_cap = kBatchPods) {
+                                             int32_t nb_cap = kBatchPods, int32_t* s_node = nullptr) {
   __shared__ int32_t s_evals;
   __shared__ uint64_t s_m[kBatchPods];
   __shared__ ResCols s_req[kBatchPods];
@@ -85,6 +85,10 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   const int32_t istar = *s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
   const int32_t inode = istar < nchain ? key_node(s_m[istar]) : -1;
+  // s_node (topology batches): each committed pod's local node (-1: none,
+  // -2: not committed); the caller applies the class adds in parallel
+  if (s_node && tid < nb_cap) s_node[tid] = tid >= committed ? -2 : tid == istar ? inode - c.base
+                                                             : gj ? key_node(gj) - c.base : -1;
   if (tid < committed) {
     const int32_t node = tid == istar ? inode : (gj ? key_node(gj) : -1);     // global position
     if (chosen_out) chosen_out[base + tid] = node;
@@ -99,10 +103,12 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
         row.pods += q.pods;
       };
       add(s_req[tid]);
-      assume_pod_rest(c, P, P.pods[base + tid], glocal, 1);
+      if (!s_node) assume_pod_rest(c, P, P.pods[base + tid], glocal, 1);
+      else assume_pod_cols(c, P.pods[base + tid], glocal);
       if (node == inode) {
         add(s_req[istar]);
-        assume_pod_rest(c, P, P.pods[base + istar], glocal, 1);
+        if (!s_node) assume_pod_rest(c, P, P.pods[base + istar], glocal, 1);
+        else assume_pod_cols(c, P.pods[base + istar], glocal);
       }
       c.req_cpu[glocal] = row.cpu;
       c.req_mem[glocal] = row.mem;

@@ -1698,6 +1698,13 @@ __device__ __forceinline__ void assume_pod_rest(const DevCluster& c, const DevPo
   if (p.nb_add) c.nb_alloc[node] += sign * p.nb_add;
 }
 
+// assume_pod_rest without the class adds (a topology batch commit applies
+// those for all its pods at once): scalar resources, bandwidth.
+__device__ __forceinline__ void assume_pod_cols(const DevCluster& c, const ksim_pod& p, int32_t node) {
+  for (int k = 0; k < c.n_scalar; k++) c.req_scalar[(size_t)k * c.n + node] += p.scalar_req[k];
+  if (p.nb_add) c.nb_alloc[node] += p.nb_add;
+}
+
 // Returnless 64-bit atomic add (two's complement: wraps as the plain add does).
 __device__ __forceinline__ void atomic_add_i64(int64_t* x, int64_t v) {
   atomicAdd(reinterpret_cast<unsigned long long*>(x), (unsigned long long)v);

@@ -29,8 +29,9 @@
 //   k_tb_merge       one wave per pod: the pod's exact top-T from its blocks'
 //   k_tb_chain_pairs the chain (ksim_chain.h), then pod j on each earlier
 //                    guess: stat + the resource part after that bind, or pinv
-//   k_tb_commit      batch_commit (class adds and persistent tables in the
-//                    binds), then the window state re-zeroed for the next batch
+//   k_tb_commit      batch_commit, the committed pods' count-class adds and
+//                    persistent-table updates as parallel atomics, and the
+//                    window state re-zeroed for the next batch
 #include "ksim_device.h"
 #include "ksim_internal.h"
 #include "ksim_wave.h"
@@ -370,16 +371,43 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   }
 }
 
+// batch_commit, then the committed pods' count-class adds and persistent
+// table updates as parallel atomics (one (pod, add) / (pod, table) pair per
+// thread; a pod and the pod i* that binds on its node may share entries).
+constexpr int kTbAddSlots = 8;                     // adds / table updates per pod and pass
 __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
                                                           DevScratch s, int32_t* __restrict__ chosen_out) {
   __shared__ int32_t s_istar, s_sched, s_unsched;
+  __shared__ int32_t s_node[kTbPods];
   const int tid = threadIdx.x;
   const uint64_t g = s.gkey[tid], m = s.pmax[tid];   // in flight with the state loads
   const int32_t inv = tid < kTbPods ? s.pinv[tid] : 0;
   const int32_t nchain = *s.chain_end;
+  const int32_t base = st->cursor;
   const int32_t nbt = tb_count(st, P);
   if (nbt <= 0) return;
-  batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt);
+  batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt,
+               s_node);
+  __syncthreads();
+  const int q = tid / kTbAddSlots, e = tid % kTbAddSlots;
+  for (int qq = q; qq < nbt; qq += kBatchPods / kTbAddSlots) {
+    const int32_t node = s_node[qq];
+    if (node < 0) continue;
+    const ksim_pod& p = P.pods[base + qq];
+    const PodPlan& pl = P.plans[base + qq];
+    for (int a = e; a < p.add_count; a += kTbAddSlots) {
+      const ksim_class_add x = P.adds[p.add_first + a];
+      atomicAdd(&c.cnt[(size_t)x.cls * c.n + node], x.count);
+      if (!(pl.flags & kPlanTadds)) ptab_add(c, P, x.cls, node, (int64_t)x.count);
+    }
+    if (pl.flags & kPlanTadds)
+      for (int a = e; a < pl.tadd_count; a += kTbAddSlots) {
+        const int4 t = P.ptab_padd[pl.tadd_first + a];
+        const uint32_t v = c.labels[(size_t)t.y * c.n + node];
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(P.ptab + t.x + (t.z == kPtabTotal ? 0u : v)),
+                         (unsigned long long)(int64_t)t.w);
+      }
+  }
   // the next batch's counters and extrema start from zero
   for (int x = tid; x < kTbPods * (int)(sizeof(WinState) / 4); x += blockDim.x)
     reinterpret_cast<int32_t*>(s.tb_win)[x] = 0;

@@ -18,11 +18,14 @@ module turns one such document into what the engine runs:
   (plugins.go:103-179), every non-profile field reset to the default, so
   percentageOfNodesToScore is 0 (ADAPT) whatever the document says.
 
-PVs and PVCs feed VolumeBinding and VolumeZone for claims bound to a PV
-(ksim.volumes: PV node affinity, PV topology labels).  Pods with volumes the
-engine does not model (inline disks, CSI inline, ephemeral, unbound or missing
-claims, ReadWriteOncePod, PVs counted against node volume limits) are reported
-in ``unsupported`` and left out of the queue.
+PVs, PVCs and StorageClasses feed VolumeBinding, VolumeZone and
+VolumeRestrictions (ksim.volumes): the PV controller's binding of Immediate
+claims at load, bound claims by PV node affinity / topology labels, unbound
+WaitForFirstConsumer claims by static matching or dynamic provisioning, and
+ReadWriteOncePod claims in use; ``schedule_queue`` runs a queue whose pods take
+PVs as they bind.  Pods with volumes the engine does not model (inline disks,
+CSI inline, ephemeral, PVs counted against node volume limits) are reported in
+``unsupported`` and left out of the queue.
 """
 from __future__ import annotations
 
@@ -32,7 +35,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import profile as prof_mod
-from .model import Node, Pod, node_from_dict, pod_from_dict, pv_from_dict, pvc_from_dict
+from .model import Node, Pod, node_from_dict, pod_from_dict, pv_from_dict, pvc_from_dict, storage_class_from_dict
 from .volumes import VolumeIndex, VolumeUnsupported
 from .netbw import NetworkBandwidthArgs
 
@@ -134,7 +137,9 @@ def load(doc: dict) -> Snapshot:
     if len(names) != len(nodes):
         raise ValueError("duplicate node names")
     volumes = VolumeIndex.from_nodes(nodes, [pv_from_dict(d) for d in doc.get("pvs") or []],
-                                     [pvc_from_dict(d) for d in doc.get("pvcs") or []])
+                                     [pvc_from_dict(d) for d in doc.get("pvcs") or []],
+                                     [storage_class_from_dict(d) for d in doc.get("storageClasses") or []])
+    volumes.run_pv_controller()               # the simulator's PV controller binds Immediate claims
     bound, pending, unsupported = [], [], []
     keyed = []
     for idx, d in enumerate(doc.get("pods") or []):
@@ -159,10 +164,47 @@ def load(doc: dict) -> Snapshot:
         keyed.append((-pod.priority, ts, idx, pod))
     keyed.sort(key=lambda t: t[:3])           # PrioritySort, then queue arrival
     pending = [t[3] for t in keyed]
+    volumes.add_users(bound)                  # ReadWriteOncePod claims already in use
     return Snapshot(nodes, bound, pending, namespaces, profiles_from_config(doc.get("schedulerConfig")),
                     unsupported, volumes,
                     {k: len(doc.get(k) or []) for k in ("pods", "nodes", "pvs", "pvcs", "storageClasses",
                                                          "priorityClasses", "namespaces")})
+
+
+def schedule_queue(backend, cluster, pending: Sequence[Pod], volumes: Optional[VolumeIndex] = None,
+                   nodes: Optional[Sequence[Node]] = None) -> List[Optional[str]]:
+    """Schedule ``pending`` in queue order on ``backend`` (a ksim.engine.Engine
+    or the oracle: ``schedule_batch`` / ``schedule`` and ``eval_pod`` / ``cycle``)
+    whose cluster is ``cluster``; returns each pod's node name (None: not
+    scheduled).  Stretches of pods whose volume verdicts cannot change run as
+    one loaded queue (the batch paths); a pod with unbound WaitForFirstConsumer
+    or ReadWriteOncePod claims is encoded at its turn, under the bindings the
+    earlier pods made, runs one cycle, and its volumes are assumed on the chosen
+    node (VolumeBinding Reserve / PreBind)."""
+    from .encode import encode_pods
+    labels = {n.name: n.labels for n in (nodes if nodes is not None else (volumes.nodes if volumes else []) or [])}
+    out: List[Optional[str]] = []
+    n = len(pending)
+    i = 0
+    while i < n:
+        j = i
+        while j < n and not (volumes is not None and volumes.stateful(pending[j])):
+            j += 1
+        if j > i:
+            enc = encode_pods(cluster, pending[i:j], volumes=volumes)
+            run = backend.schedule_batch(enc) if hasattr(backend, "schedule_batch") else backend.schedule(enc)
+            out.extend(cluster.node_names[c] if c >= 0 else None for c in run[0])
+        if j < n:
+            pod = pending[j]
+            enc = encode_pods(cluster, [pod], volumes=volumes)
+            r = backend.eval_pod(enc, 0) if hasattr(backend, "eval_pod") else backend.cycle(enc, 0)
+            node = cluster.node_names[r["chosen"]] if r["chosen"] >= 0 else None
+            if node is not None:
+                volumes.assume(pod, labels[node])
+            out.append(node)
+            j += 1
+        i = j
+    return out
 
 
 def encode(snap: Snapshot, profile_index: int = 0):

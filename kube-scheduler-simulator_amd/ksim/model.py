@@ -255,12 +255,18 @@ class Pod:
 
 @dataclass
 class PersistentVolume:
-    """v1.PersistentVolume fields VolumeBinding / VolumeZone read for a bound claim."""
+    """v1.PersistentVolume fields VolumeBinding / VolumeZone read (bound claims,
+    and the static binding of unbound WaitForFirstConsumer claims)."""
     name: str
     labels: Dict[str, str] = field(default_factory=dict)
     node_affinity: Optional[List[NodeSelectorTerm]] = None   # spec.nodeAffinity.required.nodeSelectorTerms
     source: str = ""                                        # the spec key of its volume source (csi, local, ...)
     access_modes: List[str] = field(default_factory=list)
+    capacity: int = 0                                       # spec.capacity.storage (bytes)
+    storage_class: str = ""                                 # spec.storageClassName
+    claim_ref: Optional[Tuple[str, str]] = None             # spec.claimRef (namespace, name)
+    volume_mode: str = "Filesystem"                         # spec.volumeMode (nil: Filesystem)
+    deleting: bool = False                                  # metadata.deletionTimestamp set
 
 
 @dataclass
@@ -269,6 +275,20 @@ class PersistentVolumeClaim:
     namespace: str = "default"
     volume_name: str = ""                                    # spec.volumeName ("" = unbound)
     access_modes: List[str] = field(default_factory=list)
+    storage_class: Optional[str] = None                      # spec.storageClassName (None: unset)
+    request: int = 0                                         # spec.resources.requests.storage (bytes)
+    selector: Optional[LabelSelector] = None                 # spec.selector
+    volume_mode: str = "Filesystem"                          # spec.volumeMode (nil: Filesystem)
+
+
+@dataclass
+class StorageClass:
+    """storage.k8s.io/v1 StorageClass fields the volume binder reads."""
+    name: str
+    provisioner: str = ""
+    volume_binding_mode: str = "Immediate"                   # or WaitForFirstConsumer
+    # allowedTopologies: terms OR-ed, each a list of (key, values) requirements AND-ed
+    allowed_topologies: List[List[Tuple[str, List[str]]]] = field(default_factory=list)
 
 
 # ---- v1 dict parsing --------------------------------------------------------
@@ -286,18 +306,39 @@ _PV_SOURCES = ("csi", "local", "hostPath", "nfs", "awsElasticBlockStore", "gcePe
 def pv_from_dict(d: dict) -> PersistentVolume:
     md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
     req = ((spec.get("nodeAffinity") or {}).get("required"))
+    ref = spec.get("claimRef") or None
+    cap = (spec.get("capacity") or {}).get("storage")
     return PersistentVolume(
         name=md.get("name", ""), labels=dict(md.get("labels") or {}),
         node_affinity=None if req is None else [_term(t) for t in (req.get("nodeSelectorTerms") or [])],
         source=next((k for k in _PV_SOURCES if k in spec), ""),
-        access_modes=list(spec.get("accessModes") or []))
+        access_modes=list(spec.get("accessModes") or []),
+        capacity=quantity_value(cap) if cap is not None else 0,
+        storage_class=spec.get("storageClassName", "") or "",
+        claim_ref=None if not ref else (ref.get("namespace", "") or "", ref.get("name", "") or ""),
+        volume_mode=spec.get("volumeMode") or "Filesystem",
+        deleting=bool(md.get("deletionTimestamp")))
 
 
 def pvc_from_dict(d: dict) -> PersistentVolumeClaim:
     md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
+    req = ((spec.get("resources") or {}).get("requests") or {}).get("storage")
     return PersistentVolumeClaim(name=md.get("name", ""), namespace=md.get("namespace", "default") or "default",
                                  volume_name=spec.get("volumeName", "") or "",
-                                 access_modes=list(spec.get("accessModes") or []))
+                                 access_modes=list(spec.get("accessModes") or []),
+                                 storage_class=spec.get("storageClassName"),
+                                 request=quantity_value(req) if req is not None else 0,
+                                 selector=_selector(spec.get("selector")),
+                                 volume_mode=spec.get("volumeMode") or "Filesystem")
+
+
+def storage_class_from_dict(d: dict) -> StorageClass:
+    md = d.get("metadata", {}) or {}
+    topo = []
+    for t in d.get("allowedTopologies") or []:
+        topo.append([(e.get("key", ""), list(e.get("values") or [])) for e in (t.get("matchLabelExpressions") or [])])
+    return StorageClass(name=md.get("name", ""), provisioner=d.get("provisioner", "") or "",
+                        volume_binding_mode=d.get("volumeBindingMode") or "Immediate", allowed_topologies=topo)
 
 def _req(d) -> Requirement:
     return Requirement(d["key"], d["operator"], list(d.get("values") or []))

@@ -17,7 +17,8 @@ import math
 from typing import Dict, List, Optional, Tuple
 
 from ksim.encode import node_tree_order, pod_nonzero_requests, pod_requests, zone_key
-from ksim.model import LabelSelector, Node, Pod, PodAffinityTerm, Taint, parse_quantity, selector_matches
+from ksim.model import (LabelSelector, Node, PersistentVolume, Pod, PodAffinityTerm, Taint, parse_quantity,
+                        selector_matches)
 
 MAX_NODE_SCORE = 100
 LABEL_HOSTNAME = "kubernetes.io/hostname"
@@ -134,7 +135,7 @@ class ObjScheduler:
     def __init__(self, nodes: List[Node], bound: List[Pod] = (), namespaces: Optional[Dict[str, Dict]] = None,
                  pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
                  hard_pod_affinity_weight: int = 1, network_bandwidth=None, nb_filter: bool = True,
-                 nb_score: bool = True, pvs=(), pvcs=()):
+                 nb_score: bool = True, pvs=(), pvcs=(), storage_classes=()):
         order = node_tree_order([zone_key(n.labels) for n in nodes])
         self.nodes = [NodeInfo(nodes[i]) for i in order]
         # cache.addNodeImageStates, nodes in the order they were added: name -> [size, {node names}]
@@ -168,9 +169,18 @@ class ObjScheduler:
                 self.score_order.append("NetworkBandwidth")
         self.seed = seed
         self.hard_w = hard_pod_affinity_weight
-        # the snapshot's PersistentVolumes and PersistentVolumeClaims (VolumeBinding / VolumeZone)
-        self.pvs = {pv.name: pv for pv in pvs}
-        self.pvcs = {(c.namespace, c.name): c for c in pvcs}
+        # the snapshot's PersistentVolumes, PersistentVolumeClaims and StorageClasses
+        # (VolumeBinding / VolumeZone / VolumeRestrictions); copies, bound as the run goes
+        import copy
+        self.pvs = {pv.name: copy.deepcopy(pv) for pv in pvs}
+        self.pvcs = {(c.namespace, c.name): copy.deepcopy(c) for c in pvcs}
+        self.classes = {c.name: c for c in storage_classes}
+        self.claim_users: Dict[Tuple[str, str], int] = {}
+        for p in bound:
+            for claim in p.pvc_claims:
+                self.claim_users[(p.namespace, claim)] = self.claim_users.get((p.namespace, claim), 0) + 1
+        self.provisioned = 0
+        self._pv_controller()
         self.next_start = 0
         self.seq = 0
 
@@ -222,7 +232,123 @@ class ObjScheduler:
                        "topology.kubernetes.io/zone", "topology.kubernetes.io/region")
 
     def _bound_pvs(self, pod: Pod):
-        return [self.pvs[self.pvcs[(pod.namespace, c)].volume_name] for c in pod.pvc_claims]
+        out = []
+        for c in pod.pvc_claims:
+            pvc = self.pvcs[(pod.namespace, c)]
+            if pvc.volume_name:
+                out.append(self.pvs[pvc.volume_name])
+        return out
+
+    # ---- unbound claims: the PV controller and the volume binder (v1.26) -----------
+    def _find_matching_volume(self, pvc, labels: Optional[Dict[str, str]], excluded, delay: bool):
+        """pv/util FindMatchingVolume over the PVs in name order (upstream: the
+        cache's order); labels None: the PV controller's call (node nil)."""
+        key = (pvc.namespace, pvc.name)
+        best = None
+        for name in sorted(self.pvs):
+            pv = self.pvs[name]
+            if name in excluded:
+                continue
+            if pv.claim_ref is not None and pv.claim_ref != key:
+                continue
+            if pv.capacity < pvc.request or pv.volume_mode != pvc.volume_mode or pv.deleting:
+                continue
+            if labels is None and not set(pvc.access_modes) <= set(pv.access_modes):
+                continue                              # the controller's index by access modes
+            aff = labels is None or self._pv_affinity(pv, labels)
+            if pv.claim_ref == key:
+                return pv if aff else None
+            if labels is None and delay:
+                continue
+            if pvc.selector is not None and not selector_matches(pvc.selector, pv.labels):
+                continue
+            if pv.storage_class != (pvc.storage_class or "") or not aff:
+                continue
+            if labels is not None and not set(pvc.access_modes) <= set(pv.access_modes):
+                continue
+            if best is None or pv.capacity < best.capacity:
+                best = pv
+        return best
+
+    def _pv_affinity(self, pv, labels: Dict[str, str]) -> bool:
+        if pv.node_affinity is None:
+            return True
+        labels_only = Node(name="", labels=labels)
+        return any(self._term_match(t, labels_only) for t in pv.node_affinity)
+
+    def _delay(self, pvc) -> Optional[bool]:
+        cls = pvc.storage_class or ""
+        if not cls:
+            return False
+        sc = self.classes.get(cls)
+        return None if sc is None else sc.volume_binding_mode == "WaitForFirstConsumer"
+
+    def _pv_controller(self) -> None:
+        for pvc in self.pvcs.values():               # syncClaim of a claim naming its PV
+            pv = self.pvs.get(pvc.volume_name) if pvc.volume_name else None
+            if pv is not None and pv.claim_ref is None:
+                pv.claim_ref = (pvc.namespace, pvc.name)
+        for pvc in self.pvcs.values():
+            if pvc.volume_name or self._delay(pvc) is not False:
+                continue
+            pv = self._find_matching_volume(pvc, None, set(), False)
+            if pv is not None:
+                pv.claim_ref, pvc.volume_name = (pvc.namespace, pvc.name), pv.name
+
+    def volume_prefilter(self, pod: Pod) -> Optional[str]:
+        """VolumeRestrictions (ReadWriteOncePod) and VolumeBinding PreFilter."""
+        immediate = False
+        for claim in pod.pvc_claims:
+            pvc = self.pvcs.get((pod.namespace, claim))
+            if pvc is None:
+                return f'persistentvolumeclaim "{claim}" not found'
+            if "ReadWriteOncePod" in pvc.access_modes and self.claim_users.get((pod.namespace, claim), 0):
+                return "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"
+            if not pvc.volume_name:
+                d = self._delay(pvc)
+                if d is None:
+                    return f'storageclass.storage.k8s.io "{pvc.storage_class}" not found'
+                immediate = immediate or not d
+        return "pod has unbound immediate PersistentVolumeClaims" if immediate else None
+
+    def find_pod_volumes(self, pod: Pod, node: Node):
+        """binder.go FindPodVolumes for the unbound WaitForFirstConsumer claims:
+        (static [(pvc, pv)], to provision [pvc]) or None (ErrReasonBindConflict)."""
+        delay = [self.pvcs[(pod.namespace, c)] for c in pod.pvc_claims if not self.pvcs[(pod.namespace, c)].volume_name]
+        delay.sort(key=lambda c: c.request)
+        chosen, static, provision = set(), [], []
+        for pvc in delay:
+            pv = self._find_matching_volume(pvc, node.labels, chosen, True)
+            if pv is None:
+                provision.append(pvc)
+            else:
+                chosen.add(pv.name)
+                static.append((pvc, pv))
+        for pvc in provision:                          # checkVolumeProvisions
+            sc = self.classes[pvc.storage_class or ""]
+            if sc.provisioner == "kubernetes.io/no-provisioner":
+                return None
+            if sc.allowed_topologies and not any(
+                    term and all(vals and node.labels.get(k) in vals for k, vals in term)
+                    for term in sc.allowed_topologies):
+                return None
+        return static, provision
+
+    def assume_volumes(self, pod: Pod, node: Node) -> None:
+        got = self.find_pod_volumes(pod, node)
+        if got is not None:
+            static, provision = got
+            for pvc, pv in static:
+                pv.claim_ref, pvc.volume_name = (pvc.namespace, pvc.name), pv.name
+            for pvc in provision:
+                self.provisioned += 1
+                pv = PersistentVolume(name=f"pvc-provisioned-{self.provisioned}", capacity=pvc.request,
+                                      storage_class=pvc.storage_class or "", access_modes=list(pvc.access_modes),
+                                      volume_mode=pvc.volume_mode, claim_ref=(pvc.namespace, pvc.name))
+                self.pvs[pv.name] = pv
+                pvc.volume_name = pv.name
+        for claim in pod.pvc_claims:
+            self.claim_users[(pod.namespace, claim)] = self.claim_users.get((pod.namespace, claim), 0) + 1
 
     def volume_binding_ok(self, pod: Pod, node: Node) -> bool:
         """binder.go checkBoundClaims: volumeutil.CheckNodeAffinity(pv, node.Labels)
@@ -739,6 +865,8 @@ class ObjScheduler:
             elif pl == "VolumeBinding":
                 if pod.pvc_claims and not self.volume_binding_ok(pod, node):
                     msg = "node(s) had volume node affinity conflict"
+                elif pod.pvc_claims and self.find_pod_volumes(pod, node) is None:
+                    msg = "node(s) didn't find available persistent volumes to bind"
             elif pl == "VolumeZone":
                 if pod.pvc_claims and not self.volume_zone_ok(pod, node):
                     msg = "node(s) had no available volume zone"
@@ -768,6 +896,10 @@ class ObjScheduler:
         models the scheduler's extenders (findNodesThatPassExtenders, prioritizeNodes)."""
         seq = self.seq
         self.seq += 1
+        vmsg = self.volume_prefilter(pod) if pod.pvc_claims else None
+        if vmsg is not None:                               # UnschedulableAndUnresolvable at PreFilter
+            return {"filter": {}, "n_feasible": 0, "raw": {}, "norm": {}, "total": {}, "error": None,
+                    "chosen": None, "prefilter": vmsg}
         pts = self.pts_prefilter(pod)
         ipa = self.ipa_prefilter(pod)
         filt: Dict[str, Tuple[Optional[str], Optional[str]]] = {}
@@ -863,5 +995,7 @@ class ObjScheduler:
             best = max(range(len(feasible)), key=lambda j: tb_key(totals[j], self.seed, seq, index[names[j]]))
             chosen = feasible[best]
         chosen.add_pod(pod)
+        if pod.pvc_claims:
+            self.assume_volumes(pod, chosen.node)
         res["chosen"] = chosen.node.name
         return res

@@ -117,7 +117,9 @@ def test_volume_documents_schedule_like_objref():
     """A document whose PVs (the UI's pv.yaml template) carry node affinity and
     zone labels: pods with claims bound to them are scheduled with
     VolumeBinding / VolumeZone, and placements equal the object-level
-    restatement on the same PV / PVC objects; an unbound claim is reported."""
+    restatement on the same PV / PVC objects.  A claim that does not exist and
+    an unbound Immediate claim the PV controller finds no PV for reject their
+    pods at PreFilter (unschedulable, not unsupported)."""
     doc = _template_cluster(n_nodes=30, n_pods=60, bound_every=1000)
     pv_t, pvc_t, pod_t = _doc("template_pv.json"), _doc("template_pvc.json"), _doc("template_pod.json")
     pvs, pvcs = [], []
@@ -145,9 +147,11 @@ def test_volume_documents_schedule_like_objref():
         doc["pods"].append(p)
     doc["pvs"], doc["pvcs"] = pvs, pvcs
     snap = ingest.load(doc)
-    assert [u[1] for u in snap.unsupported] == ["with-pvc", "vol-7"]   # pvc1 is not in this document
+    assert snap.unsupported == []
     cluster, enc, _ = ingest.encode(snap)
-    assert (enc.pods["vb_count"] > 0).sum() == 10 and (enc.pods["vz_count"] > 0).sum() == 20
+    # claim-1's PV has node affinity (10 pods); with-pvc (pvc1 is not in this
+    # document) and vol-7 (claim-unbound) carry a group no node matches
+    assert (enc.pods["vb_count"] > 0).sum() == 12 and (enc.pods["vz_count"] > 0).sum() == 20
     sp = copy.deepcopy(snap.profiles[0][1])
     sp.percentage_of_nodes_to_score = 100
     prof = profile.compile_profile(sp, cluster.scalar_names)
@@ -155,9 +159,14 @@ def test_volume_documents_schedule_like_objref():
     ref = ObjScheduler(snap.nodes, snap.bound, namespaces=snap.namespaces, pct=100, seed=sp.tiebreak_seed,
                        pvs=snap.volumes.pvs.values(), pvcs=snap.volumes.pvcs.values())
     names = cluster.node_names
+    rejected = []
     for i, pod in enumerate(snap.pending):
-        got = ref.cycle(pod)["chosen"]
+        r = ref.cycle(pod)
+        got = r["chosen"]
         assert (names[ochosen[i]] if ochosen[i] >= 0 else None) == got, f"pod {i} {pod.name}"
+        if "prefilter" in r:
+            rejected.append(pod.name)
+    assert sorted(rejected) == ["vol-7", "with-pvc"]
     placed = {pod.name: names[ochosen[i]] for i, pod in enumerate(snap.pending) if pod.pvc_claims and ochosen[i] >= 0}
     aff = [placed[f"vol-{i}"] for i in range(1, 40, 4) if f"vol-{i}" in placed]   # pv-1: node-3 / node-4 only
     assert len(aff) >= 2 and set(aff) <= {"node-3", "node-4"}

@@ -68,6 +68,8 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
         return n_nodes * (1 + 8 + 8 * n_norm)         # fail code + partial total + normalized raws
     if name in ("k_batch_top", "k_batch_eval"):
         return B_EVAL * n_nodes * B                   # B pods x N nodes evals per launch
+    if name == "k_batch_top_commit":                  # the evaluation + the previous batch's commit
+        return B_EVAL * n_nodes * B + 8 * B * 3
     if name == "k_batch_merge":
         return 8 * B * (tiles * geom["tile_cand"] + T)
     if name == "k_batch_chain":
@@ -96,7 +98,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 
 
 # the kernel that carries the pod x node evaluations on each path
-EVAL_KERNELS = ("k_batch_top", "k_batch_eval", "k_adapt_top", "k_tb_filter", "k_filter_score")
+EVAL_KERNELS = ("k_batch_top_commit", "k_batch_top", "k_batch_eval", "k_adapt_top", "k_tb_filter", "k_filter_score")
 
 
 def _profile_entry(fname: str, kernel: str, nodes: int):

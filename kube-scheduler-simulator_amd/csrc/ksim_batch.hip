@@ -141,117 +141,18 @@ __device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g);
 constexpr int kTopStep = KSIM_TOP_STEP;   // nodes per lane per step of the FAST loop
 
 
-template <bool FAST, int kTopThreads>
-__global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
-                                                           const ksim_profile* __restrict__ prof_p,
-                                                           const BatchProg* __restrict__ bp_p,
-                                                           const DevState* __restrict__ st,
-                                                           uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
-                                                           int32_t* __restrict__ topk_complete,
-                                                           uint64_t* __restrict__ xsend, int64_t* __restrict__ pnorm) {
+// The pod's top-T from the lanes' kept keys (a[]: the lane's best kTileCand
+// keys, descending; nfeas: the lane's feasible nodes), written to topk[j] (and
+// the sharded record xsend[j]).  Every thread of the block calls it.
+template <int kTopThreads>
+__device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfeas, int32_t j,
+                                           uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                           int32_t* __restrict__ topk_complete, uint64_t* __restrict__ xsend) {
   constexpr int kTopWaves = kTopThreads / 64;
   constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
-  static_assert(kTopSlots <= 4 && kTileCand == 4, "k_batch_top geometry");
-  const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
-  const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_list[kTopWaves][kTopT];
   __shared__ int32_t s_cnt[kTopWaves], s_complete[kTopWaves];
-  const int32_t base = st->cursor;
-  const int32_t j = blockIdx.x;
-  const int32_t pi = base + j;
-  if (pi >= min(st->end, base + kBatchPods)) return;        // block-uniform
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const ksim_pod& p = P.pods[pi];
-  const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
-  const int64_t seq = st->pod_seq + j;
-  const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
-  uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
-  int32_t nfeas = 0;
-  if constexpr (FAST) {
-    // the loop-invariant key inputs in registers (SGPRs): the profile's batch
-    // program and the pod's request fields, loaded once
-    const FastProg bq = fast_prog(bp);
-    const ksim_pod pf = fast_pod_fields(p);
-    // kTopStep nodes per step as independent chains (every row loaded up front)
-#pragma unroll 1
-    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
-      NodeRow r[kTopStep];
-      double ic[kTopStep], im[kTopStep];
-#pragma unroll
-      for (int u = 0; u < kTopStep; u++) {
-        const int32_t nu = node + u * kTopThreads;
-        const int32_t x = nu < c.eval_hi ? nu : node;
-        r[u] = load_res_row(c, x);
-        ic[u] = c.inv_cpu[x];
-        im[u] = c.inv_mem[x];
-      }
-      __builtin_amdgcn_sched_barrier(0);      // every row in flight before the first key
-#pragma unroll
-      for (int u = 0; u < kTopStep; u++) {
-        const int32_t nu = node + u * kTopThreads;
-        // computed for every slot (a slot past the range keys a valid node) and masked
-        const uint64_t k0 = dyn_key_fast(bq, pf, r[u], ic[u], im[u], hseed, c.base + (nu < c.eval_hi ? nu : node));
-        const uint64_t k = nu < c.eval_hi ? k0 : 0;
-        nfeas += k != 0;
-        a[3] = umax64(a[3], k);
-        cswap_desc(a[2], a[3]);
-        cswap_desc(a[1], a[2]);
-        cswap_desc(a[0], a[1]);
-      }
-    }
-  }
-  if constexpr (!FAST) {                      // the generic loop is not compiled into FAST kernels
-    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
-    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
-    // nodes (P100: every feasible node is scored), the keys then carry the
-    // normalized scores (norm_part)
-    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
-    NormRaw mx{0, 0};
-    if (normv) {
-      __shared__ uint64_t s_nmax[2][kTopWaves];
-      uint64_t xt = 0, xa = 0;                   // raw scores are >= 0
-#pragma unroll 1
-      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
-        const NodeRow r = load_row(c, node);
-        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
-          const NormRaw v = norm_raw(c, P, p, r);
-          xt = umax64(xt, (uint64_t)v.tt);
-          xa = umax64(xa, (uint64_t)v.na);
-        }
-      }
-      xt = wave_max_u64_dpp(xt);
-      xa = wave_max_u64_dpp(xa);
-      if (lane == 0) {
-        s_nmax[0][wv] = xt;
-        s_nmax[1][wv] = xa;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < kTopWaves; w++) {
-        xt = umax64(xt, s_nmax[0][w]);
-        xa = umax64(xa, s_nmax[1][w]);
-      }
-      mx = NormRaw{(int64_t)xt, (int64_t)xa};
-      if (threadIdx.x == 0) {
-        pnorm[2 * j] = mx.tt;
-        pnorm[2 * j + 1] = mx.na;
-      }
-    }
-#pragma unroll 1
-    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
-      uint64_t kk = 0;
-      {
-        const NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
-        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
-        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
-      }
-      nfeas += kk != 0;
-      a[3] = umax64(a[3], kk);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
-    }
-  }
 #if KSIM_TOP_THRESH
   // ---- the pod's top-T by threshold (default) ------------------------------
   // Provability: a lane that had more feasible nodes than it kept hides keys
@@ -409,6 +310,118 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     if (lane < kTopT) x[lane] = lane < n_out ? out : 0;
     if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)n_out | ((uint64_t)cmp << 32);
   }
+}
+
+template <bool FAST, int kTopThreads>
+__global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
+                                                           const ksim_profile* __restrict__ prof_p,
+                                                           const BatchProg* __restrict__ bp_p,
+                                                           const DevState* __restrict__ st,
+                                                           uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                                           int32_t* __restrict__ topk_complete,
+                                                           uint64_t* __restrict__ xsend, int64_t* __restrict__ pnorm) {
+  constexpr int kTopWaves = kTopThreads / 64;
+  constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
+  static_assert(kTopSlots <= 4 && kTileCand == 4, "k_batch_top geometry");
+  const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
+  const BatchProg& bp = *bp_p;
+  const int32_t base = st->cursor;
+  const int32_t j = blockIdx.x;
+  const int32_t pi = base + j;
+  if (pi >= min(st->end, base + kBatchPods)) return;        // block-uniform
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const ksim_pod& p = P.pods[pi];
+  const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
+  const int64_t seq = st->pod_seq + j;
+  const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
+  uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
+  int32_t nfeas = 0;
+  if constexpr (FAST) {
+    // the loop-invariant key inputs in registers (SGPRs): the profile's batch
+    // program and the pod's request fields, loaded once
+    const FastProg bq = fast_prog(bp);
+    const ksim_pod pf = fast_pod_fields(p);
+    // kTopStep nodes per step as independent chains (every row loaded up front)
+#pragma unroll 1
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
+      NodeRow r[kTopStep];
+      double ic[kTopStep], im[kTopStep];
+#pragma unroll
+      for (int u = 0; u < kTopStep; u++) {
+        const int32_t nu = node + u * kTopThreads;
+        const int32_t x = nu < c.eval_hi ? nu : node;
+        r[u] = load_res_row(c, x);
+        ic[u] = c.inv_cpu[x];
+        im[u] = c.inv_mem[x];
+      }
+      __builtin_amdgcn_sched_barrier(0);      // every row in flight before the first key
+#pragma unroll
+      for (int u = 0; u < kTopStep; u++) {
+        const int32_t nu = node + u * kTopThreads;
+        // computed for every slot (a slot past the range keys a valid node) and masked
+        const uint64_t k0 = dyn_key_fast(bq, pf, r[u], ic[u], im[u], hseed, c.base + (nu < c.eval_hi ? nu : node));
+        const uint64_t k = nu < c.eval_hi ? k0 : 0;
+        nfeas += k != 0;
+        a[3] = umax64(a[3], k);
+        cswap_desc(a[2], a[3]);
+        cswap_desc(a[1], a[2]);
+        cswap_desc(a[0], a[1]);
+      }
+    }
+  }
+  if constexpr (!FAST) {                      // the generic loop is not compiled into FAST kernels
+    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
+    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
+    // nodes (P100: every feasible node is scored), the keys then carry the
+    // normalized scores (norm_part)
+    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+    NormRaw mx{0, 0};
+    if (normv) {
+      __shared__ uint64_t s_nmax[2][kTopWaves];
+      uint64_t xt = 0, xa = 0;                   // raw scores are >= 0
+#pragma unroll 1
+      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+        const NodeRow r = load_row(c, node);
+        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
+          const NormRaw v = norm_raw(c, P, p, r);
+          xt = umax64(xt, (uint64_t)v.tt);
+          xa = umax64(xa, (uint64_t)v.na);
+        }
+      }
+      xt = wave_max_u64_dpp(xt);
+      xa = wave_max_u64_dpp(xa);
+      if (lane == 0) {
+        s_nmax[0][wv] = xt;
+        s_nmax[1][wv] = xa;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kTopWaves; w++) {
+        xt = umax64(xt, s_nmax[0][w]);
+        xa = umax64(xa, s_nmax[1][w]);
+      }
+      mx = NormRaw{(int64_t)xt, (int64_t)xa};
+      if (threadIdx.x == 0) {
+        pnorm[2 * j] = mx.tt;
+        pnorm[2 * j + 1] = mx.na;
+      }
+    }
+#pragma unroll 1
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+      uint64_t kk = 0;
+      {
+        const NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
+        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
+      }
+      nfeas += kk != 0;
+      a[3] = umax64(a[3], kk);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+    }
+  }
+  top_finish<kTopThreads>(a, nfeas, j, topk, topk_cnt, topk_complete, xsend);
 }
 
 // ---- k_batch_top_ns: node-split, pod-grouped evaluation (FAST runs) ------------
@@ -904,7 +917,9 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
 // runs the (deterministic) chain itself, thread k ending with pod k's guess in
 // a register, so the pairs need no chain launch and no gkey round trip.
 // Block 0 also stores the guesses and the prefix length for k_batch_commit.
-template <bool FAST, int NCHUNK = 0>
+// LAZY (deferred-commit batches): a batch with no pods marks its ring slot
+// empty (chain_end = -1), so the next launch commits nothing for it.
+template <bool FAST, int NCHUNK = 0, bool LAZY = false>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -931,7 +946,10 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
   uint64_t gk;
   int32_t nchain;
   // NCHUNK > 0: topk / topk_cnt are the node-split top's chunk lists (k_batch_top_ns)
-  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
+  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) {
+    if (LAZY && blockIdx.x == 0 && threadIdx.x == 0) *chain_end = -1;
+    return;
+  }
   if (blockIdx.x == 0) {
     const int32_t nb = min(kBatchPods, st->end - st->cursor);
     if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
@@ -953,6 +971,286 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPo
   const int32_t nchain = *chain_end;
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
   batch_commit(c, P, st, g, m, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, pinv ? &inv : nullptr);
+}
+
+// ---- deferred commit: batch i-1's commit inside batch i's evaluation launch -----
+// (ksim_internal.h "deferred-commit FAST batches").  Every block recomputes
+// batch i-1's cut from its ring slot (the first pod whose pair maximum beats
+// its guess, as batch_commit), so every block knows cursor_i and the nodes
+// batch i-1 bound with the requests it bound there: an LDS overlay (a node
+// bitmap, and a node -> entry hash for the nodes it marks).  A block keys its
+// pod of batch i against X[p ^ 1] + overlay = S_i.  Block b also writes pod
+// b's placement and S_i into X[p] at guess b of batches i-1 and i-2 (X[p] held
+// S_{i-2}; a guess that was not bound keeps its value, so the superset is
+// harmless); block 0 writes the state after the commit to st[p].  FLUSH: no
+// evaluation, and slot i is marked empty.
+// KSIM_LAZY_WARM (default 1): rows batch i-1 and i-2 did not touch are read
+// from X[p], which batch i's chain + pairs read next (0: every row from
+// X[p ^ 1], for A/B builds)
+#ifndef KSIM_LAZY_WARM
+#define KSIM_LAZY_WARM 1
+#endif
+constexpr int kLazyHash = 1 << kLazyHashBits;
+constexpr int kLazyBitWords = kLazyMaxNodes / 32;
+static_assert(kLazyHash >= 4 * kBatchPods && kBatchPods <= 1024, "overlay hash / block geometry");
+
+__device__ __forceinline__ uint32_t lazy_hash(int32_t node) {
+  return ((uint32_t)node * 2654435761u) >> (32 - kLazyHashBits);
+}
+
+template <bool FLUSH>
+__global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
+                                                           const ksim_profile* __restrict__ prof_p,
+                                                           const BatchProg* __restrict__ bp_p, LazyStep L,
+                                                           uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
+                                                           int32_t* __restrict__ topk_complete,
+                                                           int32_t* __restrict__ chosen_out) {
+  constexpr int kThreads = 1024;
+  __shared__ ResCols s_rq[kBatchPods];          // batch i-1's pod requests, then each bound node's delta
+  __shared__ int32_t s_hkey[kLazyHash];         // overlay hash: local node or -1
+  __shared__ int16_t s_hval[kLazyHash];         // ... its entry
+  __shared__ uint32_t s_bits[kLazyBitWords];    // nodes batch i-1 bound
+  __shared__ int32_t s_istar, s_inode, s_sched, s_unsched;
+  const int tid = threadIdx.x;
+  const int32_t b = blockIdx.x;
+  // batch i-1's slot, batch i-2's guess b and the state batch i-1 started from
+  // (independent loads)
+  const int32_t e1 = *L.e1, e2 = *L.e2;
+  uint64_t g1 = 0, m1 = 0, g2 = 0;
+  if (tid < kBatchPods) {
+    g1 = L.g1[tid];
+    m1 = L.m1[tid];
+  }
+#if KSIM_LAZY_WARM
+  if (tid < kBatchPods) g2 = L.g2[tid];
+#else
+  if (tid == b) g2 = L.g2[b];
+#endif
+  const int32_t cur0 = L.st_in->cursor, end = L.st_in->end;
+  const int64_t seq0 = L.st_in->pod_seq;
+  const int nwords = (c.n + 31) >> 5;
+  for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
+  for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
+  const int32_t nchain = e1 > 0 ? e1 : 0;      // -1: no batch i-1 (run start, a flush, past the end)
+  if (tid == 0) {
+    s_istar = nchain;
+    s_inode = -1;
+    s_sched = 0;
+    s_unsched = 0;
+  }
+  __syncthreads();
+  if (tid < nchain && m1 > g1) atomicMin(&s_istar, tid);   // keys are unique per node: never equal unless 0
+  __syncthreads();
+  const int32_t istar = s_istar;
+  const int32_t committed = istar < nchain ? istar + 1 : nchain;
+  if (tid == istar && istar < nchain) s_inode = key_node(m1) - c.base;
+  ResCols rq{0, 0, 0, 0, 0, 0};
+  if (tid < committed) {
+    const ksim_pod& q = P.pods[cur0 + tid];
+    rq = ResCols{q.req_cpu, q.req_mem, q.req_eph, q.nz_cpu, q.nz_mem, 1};
+    s_rq[tid] = rq;
+  }
+  // this block's pod of batch i, in flight with the overlay build
+  const int32_t base = cur0 + committed;
+  const int32_t pi = base + b;
+  const bool live = !FLUSH && pi < min(end, base + kBatchPods);   // block-uniform
+  ksim_pod pf;
+  if (live) pf = fast_pod_fields(P.pods[pi]);
+  __syncthreads();
+  const int32_t inode = s_inode;
+  // entry tid < i*: its guessed node takes pod tid, and pod i* when i* chose it
+  const int32_t gnode = (tid < istar && g1) ? key_node(g1) - c.base : -1;
+  if (gnode >= 0) {
+    ResCols d = rq;
+    if (gnode == inode) {
+      const ResCols x = s_rq[istar];              // never overwritten: only entries < i* are
+      d.cpu += x.cpu;
+      d.mem += x.mem;
+      d.eph += x.eph;
+      d.nzc += x.nzc;
+      d.nzm += x.nzm;
+      d.pods += 1;
+    }
+    s_rq[tid] = d;
+    atomicOr(&s_bits[gnode >> 5], 1u << (gnode & 31));
+    uint32_t h = lazy_hash(gnode);
+    while (atomicCAS(&s_hkey[h], -1, gnode) != -1) h = (h + 1) & (kLazyHash - 1);   // guessed nodes are distinct
+    s_hval[h] = (int16_t)tid;
+  }
+#if KSIM_LAZY_WARM
+  // the bitmap marks every node where X[p] (S_{i-2}) and X[p ^ 1] (S_{i-1})
+  // may differ or batch i-1 bound: the guesses of batches i-2 and i-1.  Those
+  // rows are read from X[p ^ 1] (+ the delta); every other row from X[p],
+  // which then sits in each XCD's L2 for batch i's chain + pairs
+  if (tid < e2 && g2) {
+    const int32_t n2 = key_node(g2) - c.base;
+    atomicOr(&s_bits[n2 >> 5], 1u << (n2 & 31));
+  }
+  if (tid < nchain && g1) {
+    const int32_t n1 = key_node(g1) - c.base;
+    atomicOr(&s_bits[n1 >> 5], 1u << (n1 & 31));
+  }
+#endif
+  // batch i-1's placements and statistics (k_batch_commit's bookkeeping)
+  const int32_t pnode = tid == istar ? inode + c.base : (g1 ? key_node(g1) : -1);
+  if (tid == b && tid < committed && chosen_out) chosen_out[cur0 + b] = pnode;
+  if (b == 0 && tid < committed) atomicAdd(pnode >= 0 ? &s_sched : &s_unsched, 1);
+  // this block's two rows to materialize, loaded ahead of the node loop
+  int32_t mn0 = -1, mn1 = -1;
+  ResCols mr0{0, 0, 0, 0, 0, 0}, mr1{0, 0, 0, 0, 0, 0};
+  if (tid == b) {
+    if (b < nchain && g1) mn0 = key_node(g1) - c.base;
+    if (b < e2 && g2) mn1 = key_node(g2) - c.base;   // thread b holds g2[b]
+    if (mn0 >= 0) mr0 = ResCols{c.req_cpu[mn0], c.req_mem[mn0], c.req_eph[mn0], c.nz_cpu[mn0], c.nz_mem[mn0], c.num_pods[mn0]};
+    if (mn1 >= 0) mr1 = ResCols{c.req_cpu[mn1], c.req_mem[mn1], c.req_eph[mn1], c.nz_cpu[mn1], c.nz_mem[mn1], c.num_pods[mn1]};
+  }
+  __syncthreads();
+  if (b == 0 && tid < (int)(sizeof(DevState) / 8)) {   // st[p] = st[p ^ 1], then the commit's updates
+    static_assert(sizeof(DevState) % 8 == 0, "DevState copy by words");
+    reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
+  }
+  __syncthreads();
+  if (b == 0 && tid == 0) {
+    DevState* s = L.st_out;
+    if (e1 > 0) {
+      const int32_t nb = min(kBatchPods, end - cur0);
+      s->cursor = base;
+      s->pod_seq = seq0 + committed;
+      s->scheduled += s_sched;
+      s->unschedulable += s_unsched;
+      s->batches += 1;
+      if (committed < nb) {
+        if (istar < nchain) s->cuts += 1;
+        else s->truncations += 1;
+      }
+      s->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);
+    }
+    if (FLUSH) *L.e_self = -1;
+  }
+  // the overlay delta of a node (zero when batch i-1 did not bind it)
+  // the node's delta in the hash (zero when batch i-1 did not bind it)
+  auto hash_delta = [&](int32_t node) -> ResCols {
+    ResCols d{0, 0, 0, 0, 0, 0};
+    uint32_t h = lazy_hash(node);
+    for (int32_t k; (k = s_hkey[h]) != -1; h = (h + 1) & (kLazyHash - 1))
+      if (k == node) {
+        d = s_rq[s_hval[h]];
+        break;
+      }
+    return d;
+  };
+  auto delta = [&](int32_t node) -> ResCols {
+    ResCols d{0, 0, 0, 0, 0, 0};
+    if ((s_bits[node >> 5] >> (node & 31)) & 1u) d = hash_delta(node);
+    return d;
+  };
+  auto materialize = [&]() {
+    if (tid != b) return;
+    if (mn0 >= 0) {
+      const ResCols d = delta(mn0);
+      L.w.req_cpu[mn0] = mr0.cpu + d.cpu;
+      L.w.req_mem[mn0] = mr0.mem + d.mem;
+      L.w.req_eph[mn0] = mr0.eph + d.eph;
+      L.w.nz_cpu[mn0] = mr0.nzc + d.nzc;
+      L.w.nz_mem[mn0] = mr0.nzm + d.nzm;
+      L.w.num_pods[mn0] = mr0.pods + d.pods;
+    }
+    if (mn1 >= 0) {
+      const ResCols d = delta(mn1);
+      L.w.req_cpu[mn1] = mr1.cpu + d.cpu;
+      L.w.req_mem[mn1] = mr1.mem + d.mem;
+      L.w.req_eph[mn1] = mr1.eph + d.eph;
+      L.w.nz_cpu[mn1] = mr1.nzc + d.nzc;
+      L.w.nz_mem[mn1] = mr1.nzm + d.nzm;
+      L.w.num_pods[mn1] = mr1.pods + d.pods;
+    }
+  };
+  if (!live) {
+    materialize();
+    return;
+  }
+  // pod b of batch i against S_i (k_batch_top's FAST loop with the overlay)
+  const FastProg bq = fast_prog(*bp_p);
+  const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
+  uint64_t a[kTileCand] = {0, 0, 0, 0};
+  int32_t nfeas = 0;
+#pragma unroll 1
+  for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
+#if KSIM_LAZY_WARM
+    NodeRow r;
+    r.node = node;
+    r.flags = 0;
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCALAR; k++) r.alloc_sc[k] = r.req_sc[k] = 0;
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++) r.taints[k] = 0;
+    r.alloc_cpu = c.alloc_cpu[node];
+    r.alloc_mem = c.alloc_mem[node];
+    r.alloc_eph = c.alloc_eph[node];
+    r.alloc_pods = c.alloc_pods[node];
+    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
+    const bool dirty = (s_bits[node >> 5] >> (node & 31)) & 1u;
+    // dirty: X[p ^ 1] (+ delta); else X[p] (the same values)
+    const int64_t* q_rc = dirty ? c.req_cpu : L.w.req_cpu;
+    const int64_t* q_rm = dirty ? c.req_mem : L.w.req_mem;
+    const int64_t* q_re = dirty ? c.req_eph : L.w.req_eph;
+    const int64_t* q_nc = dirty ? c.nz_cpu : L.w.nz_cpu;
+    const int64_t* q_nm = dirty ? c.nz_mem : L.w.nz_mem;
+    const int32_t* q_np = dirty ? c.num_pods : L.w.num_pods;
+    r.req_cpu = q_rc[node];
+    r.req_mem = q_rm[node];
+    r.req_eph = q_re[node];
+    r.nz_cpu = q_nc[node];
+    r.nz_mem = q_nm[node];
+    r.num_pods = q_np[node];
+    const ResCols d = dirty ? hash_delta(node) : ResCols{0, 0, 0, 0, 0, 0};
+#else
+    NodeRow r = load_res_row(c, node);
+    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
+    const ResCols d = delta(node);
+#endif
+    r.req_cpu += d.cpu;
+    r.req_mem += d.mem;
+    r.req_eph += d.eph;
+    r.nz_cpu += d.nzc;
+    r.nz_mem += d.nzm;
+    r.num_pods += d.pods;
+    const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+    nfeas += k != 0;
+    a[3] = umax64(a[3], k);
+    cswap_desc(a[2], a[3]);
+    cswap_desc(a[1], a[2]);
+    cswap_desc(a[0], a[1]);
+  }
+  materialize();
+  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, nullptr);
+}
+
+const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_batch_chain_pairs"};
+
+uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
+  const LaunchArgs& a = z.a;
+  if (evs) (void)hipEventRecord(evs[0], stream);
+  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
+                                                             a.s.topk_complete, a.chosen);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
+                                                                            a.s.topk_cnt, a.s.topk_complete, z.gkey,
+                                                                            z.cend, z.pmax, a.s.pnorm, a.s.pinv);
+  if (evs) (void)hipEventRecord(evs[2], stream);
+  return 0x3u;
+}
+
+void launch_lazy_top(const LazyBatch& z, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
+                                                             a.s.topk_complete, a.chosen);
+}
+
+void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
+                                                            a.s.topk_complete, a.chosen);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.
@@ -1029,6 +1327,15 @@ int top_ns_chunks(const LaunchArgs& a) {
   if (!a.fast || !chain_fused() || chain_clock(a) || tile_eval()) return 0;
   const int32_t ne = a.c.eval_hi - a.c.eval_lo;
   return (force == 2 || force == 4) && ne >= 64 * force ? force : 0;
+}
+
+// Any A/B switch of the three-launch batch forms (tile lists, the separate
+// chain launch, chain clocks, the node-split top, the top's block size): those
+// runs keep the three-launch form, so the switch still selects what it names.
+bool batch_ab_forms() {
+  static const bool on = tile_eval() || !chain_fused() || getenv("KSIM_CHAIN_CLOCKS") || getenv("KSIM_TOP_NS") ||
+                         getenv("KSIM_TOP_THREADS") || KSIM_TOP_NS_DEFAULT != 0;
+  return on;
 }
 
 static void launch_top_ns(const LaunchArgs& a, int nch, hipStream_t stream) {

@@ -10,6 +10,12 @@ namespace ksim {
 constexpr int kHashBits = kBatchPods * kTopT <= 2048 ? 12 : kBatchPods * kTopT <= 4096 ? 13 : 14;
 constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
+// KSIM_CHAIN_BALLOT (default 1): a round's "first changed pod" flag takes one
+// LDS atomicMin per wave (ballot, first set lane) instead of one per changed
+// pod, which all hit the same word (0: per pod, for A/B builds)
+#ifndef KSIM_CHAIN_BALLOT
+#define KSIM_CHAIN_BALLOT 1
+#endif
 
 // KSIM_CHAIN_DELAY builds (the race regression test, tests/test_gpu_chain_race.py):
 // stretch the round boundary the per-parity flags protect.  The last wave
@@ -194,7 +200,14 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
       if (e < cnt && held[e] >= i) na = e;
     __syncthreads();
     if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
+#if KSIM_CHAIN_BALLOT
+    {                                                   // the wave's first changed pod: one LDS atomic per wave
+      const uint64_t chg = __ballot(na != a);
+      if (chg && (threadIdx.x & 63) == 0) atomicMin(&L.first[par], (int)(threadIdx.x & ~63u) + __builtin_ctzll(chg));
+    }
+#else
     if (na != a) atomicMin(&L.first[par], i);
+#endif
     a = na;
     __syncthreads();
     CHAIN_DELAY((int)(blockDim.x >> 6) - 1);   // the last wave reads the flag late

@@ -118,6 +118,7 @@ struct ksim_handle {
   std::vector<uint8_t> topo;            // per loaded pod: 0 no topology uses, 1 uses (k_topo_prefilter), 2 uses
                                         // read from persistent tables (kPlanPtab)
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
+  std::vector<uint8_t> noadd;           // per loaded pod: no count-class adds (deferred-commit batches)
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
   std::vector<int32_t> tlen;            // per loaded pod: topology batch run length from it (tbatch_runs)
@@ -163,6 +164,16 @@ struct ksim_handle {
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
   hipGraphExec_t graph_tbatch = nullptr;       // topology batches (ksim_tbatch.hip)
+  // deferred-commit FAST batches (ksim_internal.h): the second snapshot buffer
+  // X[1] and state st[1], the ring of chain + pairs outputs, kGraphBatches
+  // batches as one graph (starting at a batch index divisible by kLazySlots)
+  std::vector<DevBuf> lazy_bufs;
+  int32_t lazy_n = -1;
+  DynCols lazy_x1{};
+  DevState* lazy_st1 = nullptr;
+  uint64_t *lazy_g = nullptr, *lazy_m = nullptr;   // [kLazySlots][kBatchPods]
+  int32_t* lazy_e = nullptr;                        // [kLazySlots] prefix length, -1 = empty slot
+  hipGraphExec_t graph_lazy = nullptr;
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
   // the global bitmap (allocated at the first such run)
   std::vector<DevBuf> ash_bufs;
@@ -250,9 +261,11 @@ void drop_graphs(ksim_handle* h) {
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
+  if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
   h->graph_batch_fast = nullptr;
   h->graph_batch = nullptr;
   h->graph_tbatch = nullptr;
+  h->graph_lazy = nullptr;
 }
 
 bool plugin_supported(int id) { return id >= 0 && id < KSIM_PL_COUNT; }
@@ -570,6 +583,179 @@ int run_tbatch(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   return KSIM_OK;
 }
 
+// ---- deferred-commit FAST batches (ksim_internal.h, ksim_batch.hip) ----------
+// KSIM_NO_LAZY=1: the three-launch batches (A/B runs, parity of both forms).
+bool lazy_enabled() {
+  static const bool off = getenv("KSIM_NO_LAZY") != nullptr;
+  return !off;
+}
+
+// A FAST run [a, b) on an unsharded handle whose pods add to no count class
+// (the overlay carries the resource columns only), on a cluster the overlay's
+// LDS node bitmap covers.
+bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b) {
+  if (!lazy_enabled() || batch_ab_forms() || is_sharded(h) || h->replicated || adapt_mode(h)) return false;
+  if (h->dc.base != 0 || h->dc.n > kLazyMaxNodes || h->dc.n <= 0) return false;
+  for (int32_t i = a; i < b; i++)
+    if (!h->noadd[i]) return false;
+  return true;
+}
+
+int alloc_lazy(ksim_handle* h) {
+  if (h->lazy_n == h->dc.n) return KSIM_OK;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
+  h->graph_lazy = nullptr;
+  free_bufs(h->lazy_bufs);
+  h->lazy_n = -1;
+  const size_t n = (size_t)h->dc.n;
+  int rc;
+  void* p = nullptr;
+  int64_t** cols[5] = {&h->lazy_x1.req_cpu, &h->lazy_x1.req_mem, &h->lazy_x1.req_eph, &h->lazy_x1.nz_cpu,
+                       &h->lazy_x1.nz_mem};
+  for (auto* c : cols) {
+    if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * n, &p))) return rc;
+    *c = (int64_t*)p;
+  }
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * n, &p))) return rc;
+  h->lazy_x1.num_pods = (int32_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, sizeof(DevState), &p))) return rc;
+  h->lazy_st1 = (DevState*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
+  h->lazy_g = (uint64_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
+  h->lazy_m = (uint64_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * (size_t)kLazySlots, &p))) return rc;
+  h->lazy_e = (int32_t*)p;
+  h->lazy_n = h->dc.n;
+  return KSIM_OK;
+}
+
+DynCols dyn_cols(const DevCluster& c) {
+  return DynCols{c.req_cpu, c.req_mem, c.req_eph, c.nz_cpu, c.nz_mem, c.num_pods};
+}
+
+DevCluster with_cols(DevCluster c, const DynCols& d) {
+  c.req_cpu = d.req_cpu;
+  c.req_mem = d.req_mem;
+  c.req_eph = d.req_eph;
+  c.nz_cpu = d.nz_cpu;
+  c.nz_mem = d.nz_mem;
+  c.num_pods = d.num_pods;
+  return c;
+}
+
+// The launch arguments of deferred-commit batch i of a run.
+LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
+  const int p = (int)(i & 1), q = (int)(i & 3), q1 = (int)((i + 3) & 3), q2 = (int)((i + 2) & 3);
+  const DynCols x[2] = {dyn_cols(h->dc), h->lazy_x1};
+  DevState* st[2] = {h->st, h->lazy_st1};
+  LazyBatch z;
+  z.a = la;
+  z.a.c = with_cols(la.c, x[p ^ 1]);
+  z.cw = with_cols(la.c, x[p]);
+  z.step.w = x[p];
+  z.step.st_in = st[p ^ 1];
+  z.step.st_out = st[p];
+  z.step.g1 = h->lazy_g + (size_t)q1 * kBatchPods;
+  z.step.m1 = h->lazy_m + (size_t)q1 * kBatchPods;
+  z.step.e1 = h->lazy_e + q1;
+  z.step.g2 = h->lazy_g + (size_t)q2 * kBatchPods;
+  z.step.e2 = h->lazy_e + q2;
+  z.step.e_self = h->lazy_e + q;
+  z.st = st[p];
+  z.gkey = h->lazy_g + (size_t)q * kBatchPods;
+  z.pmax = h->lazy_m + (size_t)q * kBatchPods;
+  z.cend = h->lazy_e + q;
+  return z;
+}
+
+// Start of a deferred-commit run (set_run done): X[1] = X[0], st[1] = st[0],
+// every ring slot empty.
+int lazy_begin(ksim_handle* h) {
+  int rc;
+  if ((rc = alloc_lazy(h))) return rc;
+  const size_t n = (size_t)h->dc.n;
+  const DynCols x0 = dyn_cols(h->dc), x1 = h->lazy_x1;
+  HIPCHK(h, hipMemcpyAsync(x1.req_cpu, x0.req_cpu, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x1.req_mem, x0.req_mem, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x1.req_eph, x0.req_eph, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x1.nz_cpu, x0.nz_cpu, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x1.nz_mem, x0.nz_mem, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x1.num_pods, x0.num_pods, 4 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->lazy_st1, h->st, sizeof(DevState), hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->lazy_e, 0xff, 4 * kLazySlots, h->stream));
+  return KSIM_OK;
+}
+
+// After the flush of batch index f: the snapshot and state are in X[f & 1],
+// st[f & 1]; bring them to the handle's own buffers.
+int lazy_end(ksim_handle* h, int64_t f) {
+  if ((f & 1) == 0) return KSIM_OK;
+  const size_t n = (size_t)h->dc.n;
+  const DynCols x0 = dyn_cols(h->dc), x1 = h->lazy_x1;
+  HIPCHK(h, hipMemcpyAsync(x0.req_cpu, x1.req_cpu, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x0.req_mem, x1.req_mem, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x0.req_eph, x1.req_eph, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x0.nz_cpu, x1.nz_cpu, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x0.nz_mem, x1.nz_mem, 8 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(x0.num_pods, x1.num_pods, 4 * n, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->st, h->lazy_st1, sizeof(DevState), hipMemcpyDeviceToDevice, h->stream));
+  return KSIM_OK;
+}
+
+int read_state_at(ksim_handle* h, const DevState* src, DevState& st) {
+  HIPCHK(h, hipMemcpyAsync(&st, src, sizeof(st), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return KSIM_OK;
+}
+
+// A FAST run of pods [a, b) as deferred-commit batches (lazy_ok; set_run done).
+// Batch i commits batch i - 1; each stretch of launches ends with a flush, whose
+// state tells the host where the run stands.  A batch commits 1..kBatchPods
+// pods, so ceil(left / kBatchPods) batches never start past the end.
+int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
+  int rc;
+  if ((rc = lazy_begin(h))) return rc;
+  if (!h->graph_lazy) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    hipGraph_t g = nullptr;
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < kGraphBatches; i++) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
+    e = hipGraphInstantiate(&h->graph_lazy, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+      h->graph_lazy = nullptr;
+      return hip_fail(h, e, "hipGraphInstantiate");
+    }
+    h->graph_captures++;
+  }
+  static_assert(kGraphBatches % kLazySlots == 0, "lazy graphs keep the ring phase");
+  int64_t i = 0;
+  int32_t cursor = a;
+  while (cursor < b) {
+    int32_t nb = (b - cursor + kBatchPods - 1) / kBatchPods;
+    const int32_t align = (int32_t)((kLazySlots - (i & 3)) & 3);
+    if (nb >= align + kGraphBatches) {
+      for (int32_t r = 0; r < align; r++, i++, nb--) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
+      for (int32_t r = 0; r < nb / kGraphBatches; r++, i += kGraphBatches)
+        HIPCHK(h, hipGraphLaunch(h->graph_lazy, h->stream));
+    } else {
+      for (int32_t r = 0; r < nb; r++, i++) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
+    }
+    launch_lazy_flush(lazy_batch(h, la, i), h->stream);
+    HIPCHK(h, hipGetLastError());
+    DevState st;
+    if ((rc = read_state_at(h, (i & 1) ? h->lazy_st1 : h->st, st))) return rc;
+    if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "deferred-commit batch path made no progress");
+    cursor = st.cursor;
+    i++;
+  }
+  return lazy_end(h, i - 1);
+}
+
 // Run pods [a, b) on one path (all of them share the path).
 int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   int rc;
@@ -596,6 +782,7 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   if (topo) return run_tbatch(h, a, b, la);
   // the FAST evaluation kernel when every pod of the run is trivial with cpu/memory scoring
   la.fast = run_fast(h, a, b);
+  if (la.fast && lazy_ok(h, a, b)) return run_lazy(h, a, b, la);
   hipGraphExec_t& gb = la.fast ? h->graph_batch_fast : h->graph_batch;
   if (!gb && (rc = capture(h, true, false, &gb, la.fast))) return rc;
   // every batch commits between 1 and kBatchPods pods: a graph of
@@ -1120,6 +1307,7 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
   free_bufs(h->ash_bufs);
+  free_bufs(h->lazy_bufs);
   free_bufs(h->pod_bufs);
   free_bufs(h->pod1_bufs);
   free_bufs(h->pre_bufs);
@@ -1255,6 +1443,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
   free_bufs(h->ash_bufs);
+  free_bufs(h->lazy_bufs);
+  h->lazy_n = -1;
   h->ash_send = h->ash_recv = h->ash_gmask = nullptr;
   h->ash_world = h->ash_w = 0;
   free_bufs(h->pod_bufs);
@@ -2243,6 +2433,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->topo.assign((size_t)ps->n_pods, 0);
   h->xdom_len.assign((size_t)ps->n_pods, 0);
   h->trivial.assign((size_t)ps->n_pods, 0);
+  h->noadd.assign((size_t)ps->n_pods, 0);
   h->hard_small.assign((size_t)ps->n_pods, 1);
   h->soft_le1.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
@@ -2271,6 +2462,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     // class-2 pods (pod_batchable) read full rows: taints, labels, scalar columns
     if (static_trivial(h, ps->pods[i]) && batchable[i] != 2) bf[i] |= kBatchStaticTrivial;
     h->trivial[i] = (bf[i] & kBatchStaticTrivial) ? 1 : 0;
+    h->noadd[i] = ps->pods[i].add_count == 0 ? 1 : 0;
   }
   std::vector<PodPlan> plans((size_t)ps->n_pods);
   for (int32_t i = 0; i < ps->n_pods; i++) {
@@ -2550,6 +2742,27 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   a.fuse_min = !batch && h->topo[first] && h->hard_small[first];
   a.fuse_ext = !batch && h->soft_le1[first];
   a.ptab = !batch && h->topo[first] == 2;
+  if (batch && a.fast && lazy_ok(h, first, end)) {
+    // the deferred-commit evaluation launch as the run issues it: batch 0 of
+    // the run (both launches), then batch 1's k_batch_top_commit repeated
+    // (idempotent: it reads X[0], st[0] and slot 0, and writes X[1], st[1],
+    // the lists and batch 0's placements); the handle's own buffers keep
+    // their contents
+    if ((rc = lazy_begin(h))) return rc;
+    launch_batch_lazy(lazy_batch(h, a, 0), h->stream);
+    const LazyBatch z = lazy_batch(h, a, 1);
+    launch_lazy_top(z, h->stream);
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    for (int32_t i = 0; i < reps; i++) launch_lazy_top(z, h->stream);
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    HIPCHK(h, hipEventSynchronize(h->ev1));
+    HIPCHK(h, hipGetLastError());
+    float ms = 0;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    *avg_ms = ms / reps;
+    if (kernel) *kernel = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch;
+    return KSIM_OK;
+  }
   auto launch = [&] {
     if (batch) launch_batch_eval_only(a, h->stream);
     else launch_filter_only(a, h->stream);
@@ -2580,13 +2793,15 @@ const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerAdapt) return kAdaptKernelNames[k];
   k -= kKernelsPerAdapt;
   if (k >= 0 && k < kKernelsPerTbatch) return kTbatchKernelNames[k];
+  k -= kKernelsPerTbatch;
+  if (k >= 0 && k < kKernelsPerLazy) return kLazyKernelNames[k];
   return nullptr;
 }
 
 int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms, int64_t* launches, int32_t cap) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch;
+  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch + kKernelsPerLazy;
   if (!avg_ms || cap < kKinds) return set_err(h, KSIM_E_INVALID, "avg_ms too small");
   if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
@@ -2611,6 +2826,41 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
                      : adapt ? kKernelsPerCycle + kKernelsPerBatch
                      : batch ? kKernelsPerCycle : 0;
     if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+    if (batch && !adapt && !tb && a.fast && lazy_ok(h, lo, hi)) {
+      // deferred-commit batches: two launches each, a flush (untimed) before
+      // every state read
+      const int lbase = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch;
+      HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
+      if ((r = lazy_begin(h))) return r;
+      int64_t i = 0;
+      int32_t cursor = lo, done_batches = 0;
+      while (cursor < hi) {
+        const int32_t iters = std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods);
+        std::vector<hipEvent_t> evs((size_t)iters * (kKernelsPerLazy + 1));
+        for (auto& e : evs) HIPCHK(h, hipEventCreate(&e));
+        for (int32_t t = 0; t < iters; t++, i++)
+          launch_batch_lazy(lazy_batch(h, a, i), h->stream, &evs[(size_t)t * (kKernelsPerLazy + 1)]);
+        launch_lazy_flush(lazy_batch(h, a, i), h->stream);
+        HIPCHK(h, hipGetLastError());
+        DevState st;
+        if ((r = read_state_at(h, (i & 1) ? h->lazy_st1 : h->st, st))) return r;
+        const int32_t did = std::min<int32_t>(iters, st.batches - done_batches);
+        done_batches = st.batches;
+        for (int32_t t = 0; t < did; t++)
+          for (int k = 0; k < kKernelsPerLazy; k++) {
+            float ms = 0;
+            const size_t e0 = (size_t)t * (kKernelsPerLazy + 1);
+            HIPCHK(h, hipEventElapsedTime(&ms, evs[e0 + k], evs[e0 + k + 1]));
+            sum[lbase + k] += ms;
+            n[lbase + k] += 1;
+          }
+        for (auto& e : evs) (void)hipEventDestroy(e);
+        if (st.cursor <= cursor) return set_err(h, KSIM_E_DEVICE, "no progress while timing");
+        cursor = st.cursor;
+        i++;
+      }
+      return lazy_end(h, i - 1);
+    }
     int32_t cursor = lo;
     uint32_t launched = (1u << per) - 1;         // batch paths launch every kernel of a batch
     while (cursor < hi) {

@@ -75,9 +75,51 @@ uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 // Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
 bool chain_fused();   // KSIM_CHAIN_SEPARATE unset: the chain runs inside the pairs launch
+bool batch_ab_forms();   // an A/B switch of the three-launch batch forms is set (no deferred commit)
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
 uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+
+// ---- deferred-commit FAST batches (ksim_batch.hip k_batch_top_commit) ---------
+// Batch i's commit runs inside batch i+1's evaluation launch: two launches per
+// batch instead of three.  The dynamic node columns are double-buffered: batch
+// i evaluates the snapshot X[p ^ 1] (p = i & 1) that batch i-1 evaluated, plus
+// batch i-1's binds as an overlay, and writes S_i into X[p] for the nodes batch
+// i-1 or i-2 bound (X[p] held S_{i-2}); its chain + pairs then read X[p].  The
+// chain + pairs outputs (guess keys, pair maxima, prefix length) live in a
+// ring of kLazySlots slots, slot i & 3.  X[0] and st[0] are the handle's own.
+constexpr int kLazySlots = 4;
+constexpr int kLazyMaxNodes = 1 << 17;   // the overlay's LDS node bitmap (16 KB)
+constexpr int kLazyHashBits = 10;        // overlay hash: node -> entry, >= 4 x kBatchPods slots
+struct DynCols {
+  int64_t *req_cpu, *req_mem, *req_eph, *nz_cpu, *nz_mem;
+  int32_t* num_pods;
+};
+struct LazyStep {
+  DynCols w;                                       // X[p]: receives S_i
+  const DevState* st_in;                           // st[p ^ 1]: the state batch i-1 started from
+  DevState* st_out;                                // st[p]: after batch i-1's commit
+  const uint64_t* g1; const uint64_t* m1; const int32_t* e1;   // batch i-1's slot: guesses, pair maxima, prefix
+  const uint64_t* g2; const int32_t* e2;                       // batch i-2's slot: guesses, prefix
+  int32_t* e_self;                                 // batch i's slot (a flush marks it empty: -1)
+};
+struct LazyBatch {
+  LaunchArgs a;        // a.c: static columns + X[p ^ 1]
+  DevCluster cw;       // static columns + X[p]
+  LazyStep step;
+  DevState* st;        // st[p]
+  uint64_t* gkey;      // batch i's slot
+  uint64_t* pmax;
+  int32_t* cend;
+};
+constexpr int kKernelsPerLazy = 2;
+extern const char* const kLazyKernelNames[kKernelsPerLazy];
+// batch i: k_batch_top_commit (commit of i-1, evaluation of i), then the
+// chain + pairs of i.  A flush is the first launch alone with no evaluation:
+// it commits batch i-1 and leaves slot i empty.
+uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr);
+void launch_lazy_flush(const LazyBatch& z, hipStream_t stream);
+void launch_lazy_top(const LazyBatch& z, hipStream_t stream);   // the first launch alone (ksim_time_eval)
 void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // Compat cycle around the host's extender round trip (ksim_eval_pod_filter / _finish):
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.

@@ -1,6 +1,8 @@
 """The engine's A/B switches keep the pre-fusion launch forms alive
 (KSIM_CHAIN_SEPARATE: the chain as its own one-block launch ahead of the
-pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch).  They
+pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch;
+KSIM_NO_LAZY: the three-launch P100 batch, commit as its own launch, instead
+of the deferred commit).  They
 are read once per process, so each runs in one child process that schedules
 P100 and ADAPT batches and checks them against the oracle (the default forms
 run in every other GPU test)."""
@@ -36,7 +38,7 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE"])
+@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE", "KSIM_NO_LAZY"])
 def test_separate_launch_forms_vs_oracle(switch):
     env = dict(os.environ)
     env[switch] = "1"

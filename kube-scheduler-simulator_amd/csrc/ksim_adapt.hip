@@ -216,7 +216,10 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
     int64_t before = 0;
     for (int w = 0; w < wv; w++) before += sh[w];
     const int32_t ns = (int32_t)(((int64_t)s0 + before + x - proc) % n);
-    if (j < nb && ns != s) atomicMin(&s_first, j);
+    {                                                // the wave's first changed pod: one LDS atomic per wave
+      const uint64_t chg = __ballot(j < nb && ns != s);
+      if (chg && lane == 0) atomicMin(&s_first, (j & ~63) + __builtin_ctzll(chg));
+    }
     __syncthreads();
     const int32_t f = s_first;
     __syncthreads();                                 // sh / s_first are rewritten next round
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   s_aw[threadIdx.x] = aw;
   if (threadIdx.x == 0) s_fb = nchain0;
   __syncthreads();
-  if ((int32_t)threadIdx.x < nchain0 && brk) atomicMin(&s_fb, (int32_t)threadIdx.x);
+  block_first_min(&s_fb, (int32_t)threadIdx.x < nchain0 && brk);
   __syncthreads();
   batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw);
 }

@@ -988,7 +988,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPo
 // from X[p], which batch i's chain + pairs read next (0: every row from
 // X[p ^ 1], for A/B builds)
 #ifndef KSIM_LAZY_WARM
-#define KSIM_LAZY_WARM 1
+#define KSIM_LAZY_WARM 0
 #endif
 constexpr int kLazyHash = 1 << kLazyHashBits;
 constexpr int kLazyBitWords = kLazyMaxNodes / 32;
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     s_unsched = 0;
   }
   __syncthreads();
-  if (tid < nchain && m1 > g1) atomicMin(&s_istar, tid);   // keys are unique per node: never equal unless 0
+  block_first_min(&s_istar, tid < nchain && m1 > g1);   // keys are unique per node: never equal unless 0
   __syncthreads();
   const int32_t istar = s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
@@ -1111,19 +1111,21 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   }
   __syncthreads();
   if (b == 0 && tid == 0) {
+    // every new value from st[p ^ 1]: st[p] is never read back here (a
+    // uniform load of it would go through the scalar cache, which does not
+    // see the vector stores of the copy above)
+    const DevState* si = L.st_in;
     DevState* s = L.st_out;
     if (e1 > 0) {
       const int32_t nb = min(kBatchPods, end - cur0);
       s->cursor = base;
       s->pod_seq = seq0 + committed;
-      s->scheduled += s_sched;
-      s->unschedulable += s_unsched;
-      s->batches += 1;
-      if (committed < nb) {
-        if (istar < nchain) s->cuts += 1;
-        else s->truncations += 1;
-      }
-      s->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);
+      s->scheduled = si->scheduled + s_sched;
+      s->unschedulable = si->unschedulable + s_unsched;
+      s->batches = si->batches + 1;
+      s->cuts = si->cuts + (committed < nb && istar < nchain ? 1 : 0);
+      s->truncations = si->truncations + (committed < nb && istar >= nchain ? 1 : 0);
+      s->evals = si->evals + (int64_t)committed * (c.eval_hi - c.eval_lo);
     }
     if (FLUSH) *L.e_self = -1;
   }

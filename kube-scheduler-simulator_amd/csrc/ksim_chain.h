@@ -217,7 +217,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
   if (i == 0) s_cut = first < nb ? first : nb;
   __syncthreads();
-  if (i < first && i < nb && a < 0 && incomplete) atomicMin(&s_cut, i);
+  block_first_min(&s_cut, i < first && i < nb && a < 0 && incomplete);
   __syncthreads();
   const int32_t nchain = s_cut;
   const uint64_t t2 = __builtin_amdgcn_s_memrealtime();

@@ -4,6 +4,7 @@
 
 #include "ksim_device.h"
 #include "ksim_internal.h"
+#include "ksim_wave.h"
 
 namespace ksim {
 
@@ -50,7 +51,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   if (inv_own) {                                   // block-uniform
     if (tid == 0) *s_istar = nchain;
     __syncthreads();
-    if (tid < nchain && *inv_own) atomicMin(s_istar, tid);
+    block_first_min(s_istar, tid < nchain && *inv_own);
     __syncthreads();
     nchain = *s_istar;
     __syncthreads();                               // every read before s_istar is reused below
@@ -80,7 +81,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     s_evals = 0;
   }
   __syncthreads();
-  if (tid < nchain && mj > gj) atomicMin(s_istar, tid);   // keys are unique per node: never equal unless 0
+  block_first_min(s_istar, tid < nchain && mj > gj);   // keys are unique per node: never equal unless 0
   __syncthreads();
   const int32_t istar = *s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;

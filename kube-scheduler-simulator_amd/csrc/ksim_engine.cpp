@@ -2735,7 +2735,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
     return set_err(h, KSIM_E_UNSUPPORTED, "topology batch evaluations span two kernels");
   if (batch && adapt_mode(h)) return set_err(h, KSIM_E_UNSUPPORTED, "ADAPT batch evaluations span two kernels");
   HIPCHK(h, hipSetDevice(h->device));
-  const int32_t end = batch ? std::min(h->dp.n_pods, first + kBatchPods) : first + 1;
+  // two batches' pods: the deferred-commit timing below keys batch 1 (a full
+  // batch whatever batch 0 commits)
+  const int32_t end = batch ? std::min(h->dp.n_pods, first + 2 * kBatchPods) : first + 1;
   if ((rc = set_run(h, first, end))) return rc;
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = batch && run_fast(h, first, end);

@@ -91,4 +91,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+
+// *s = min(*s, the block's first thread with pred) for one-dimensional blocks:
+// one LDS atomicMin per wave (its first set lane) instead of one per thread,
+// which would all hit the same word.
+__device__ __forceinline__ void block_first_min(int32_t* s, bool pred) {
+  const uint64_t m = __ballot(pred);
+  if (m && (threadIdx.x & 63) == 0) atomicMin(s, (int32_t)(threadIdx.x & ~63u) + __builtin_ctzll(m));
+}
+
 }  // namespace ksim

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
 // CHAIN: every block runs the chain itself from the top-T lists (as
 // k_batch_chain_pairs on the P100 path); block 0 stores gkey / chain_end for
 // the commit.  Otherwise the guesses come from k_batch_chain.
-template <bool SH, bool CHAIN>
+template <bool SH, bool CHAIN, bool LAZY = false>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P,
                                                             const ksim_profile* __restrict__ prof_p,
                                                             const BatchProg* __restrict__ bp_p,
@@ -468,7 +468,10 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
-  if (nb <= 0) return;
+  if (nb <= 0) {
+    if (LAZY && blockIdx.x == 0 && tid == 0) *chain_end = -1;   // deferred commit: an empty slot
+    return;
+  }
   const int j = blockIdx.x, k = tid;
   int32_t nchain;
   uint64_t gk;
@@ -540,6 +543,205 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw);
 }
 
+// ---- deferred commit (ksim_internal.h): batch i-1's commit inside batch i's mask launch ----
+// Every block recomputes batch i-1's cut from its ring slot (first broken
+// window, then the first pod whose pair maximum beats its guess, as
+// k_adapt_commit / batch_commit) and so knows cursor_i.  A block holds 256
+// nodes, one per thread: the thread loads its row from X[p ^ 1], adds what
+// batch i-1 bound there (the entries whose guess lies in the block, with their
+// requests, in LDS), keys its node for the block's pods of batch i (the S_i
+// feasibility bitmaps) and, in the blocks of the first pod group, writes the
+// row to X[p] (every row: X[p] needs no older binds replayed).  Block b (flat
+// index) writes placement b of batch i-1; block 0 writes the state after the
+// commit to st[p].  FLUSH: the commit alone (rows written, no bitmaps).
+// Trivial cpu/memory pods only (FAST runs).
+template <bool FLUSH>
+__global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
+                                                           LazyStep L, const int32_t* __restrict__ b1,
+                                                           const int32_t* __restrict__ w1, uint64_t* __restrict__ amask,
+                                                           int32_t n_words, int32_t mp, int32_t* __restrict__ chosen_out) {
+  static_assert(kBatchPods % 256 == 0, "k_adapt_mask_commit walks the batch in 256-pod chunks");
+  constexpr int kChunks = kBatchPods / 256;
+  __shared__ int32_t s_fb, s_istar, s_inode, s_sched, s_unsched, s_evals;
+  __shared__ int16_t s_dn[256];                    // entry bound on this block's node tid, -1: none
+  __shared__ ResCols s_rq[kBatchPods];             // those entries' deltas
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int32_t nblocks = gridDim.x * gridDim.y, bl = blockIdx.y * gridDim.x + blockIdx.x;
+  const int32_t nbase = blockIdx.x * 256;          // this block's first node (4 words of 64)
+  const int32_t e1 = *L.e1;
+  uint64_t g[kChunks], m[kChunks];
+  int32_t brk[kChunks];
+#pragma unroll
+  for (int q = 0; q < kChunks; q++) {
+    g[q] = L.g1[q * 256 + tid];
+    m[q] = L.m1[q * 256 + tid];
+    brk[q] = b1[q * 256 + tid];
+  }
+  const int32_t cur0 = L.st_in->cursor, end = L.st_in->end;
+  const int64_t seq0 = L.st_in->pod_seq;
+  const int32_t nchain0 = e1 > 0 ? e1 : 0;         // -1: no batch i-1
+  s_dn[tid] = -1;
+  if (tid == 0) {
+    s_fb = nchain0;
+    s_inode = -1;
+    s_sched = 0;
+    s_unsched = 0;
+    s_evals = 0;
+  }
+  __syncthreads();
+  // the chain ends before the first broken window
+#pragma unroll
+  for (int q = 0; q < kChunks; q++) {
+    const uint64_t mm = __ballot(q * 256 + tid < nchain0 && brk[q]);
+    if (mm && lane == 0) atomicMin(&s_fb, q * 256 + (tid & ~63) + __builtin_ctzll(mm));
+  }
+  __syncthreads();
+  const int32_t nchain = s_fb;
+  if (tid == 0) s_istar = nchain;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kChunks; q++) {
+    const uint64_t mm = __ballot(q * 256 + tid < nchain && m[q] > g[q]);   // keys are unique per node
+    if (mm && lane == 0) atomicMin(&s_istar, q * 256 + (tid & ~63) + __builtin_ctzll(mm));
+  }
+  __syncthreads();
+  const int32_t istar = s_istar;
+  const int32_t committed = istar < nchain ? istar + 1 : nchain;
+#pragma unroll
+  for (int q = 0; q < kChunks; q++)
+    if (q * 256 + tid == istar && istar < nchain) s_inode = key_node(m[q]) - c.base;
+  __syncthreads();
+  const int32_t inode = s_inode;
+  // the entries whose guessed node is in this block: pod t's requests (and pod
+  // i*'s when i* took the same node)
+#pragma unroll
+  for (int q = 0; q < kChunks; q++) {
+    const int32_t t = q * 256 + tid;
+    const int32_t gn = (t < istar && g[q]) ? key_node(g[q]) - c.base : -1;
+    if (gn >= nbase && gn < nbase + 256) {
+      const ksim_pod& pt = P.pods[cur0 + t];
+      ResCols d{pt.req_cpu, pt.req_mem, pt.req_eph, pt.nz_cpu, pt.nz_mem, 1};
+      if (gn == inode) {
+        const ksim_pod& pi = P.pods[cur0 + istar];
+        d.cpu += pi.req_cpu;
+        d.mem += pi.req_mem;
+        d.eph += pi.req_eph;
+        d.nzc += pi.nz_cpu;
+        d.nzm += pi.nz_mem;
+        d.pods += 1;
+      }
+      s_rq[t] = d;
+      s_dn[gn - nbase] = (int16_t)t;
+    }
+  }
+  // batch i-1's statistics and the state after its commit (block 0)
+  if (bl == 0) {
+#pragma unroll
+    for (int q = 0; q < kChunks; q++) {
+      const int32_t t = q * 256 + tid;
+      if (t < committed) {
+        const int32_t pn = t == istar ? inode + c.base : (g[q] ? key_node(g[q]) : -1);
+        atomicAdd(pn >= 0 ? &s_sched : &s_unsched, 1);
+        const int2 w = reinterpret_cast<const int2*>(w1)[t];
+        atomicAdd(&s_evals, (int32_t)window_local(c, w.x, w.y >= 0 ? (int64_t)w.y + 1 : c.n_total));
+      }
+    }
+    if (tid < (int)(sizeof(DevState) / 8))
+      reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
+  }
+  // placements of batch i-1, one per block
+  if (tid == 0)
+    for (int32_t k = bl; k < committed; k += nblocks) {
+      const uint64_t gk = L.g1[k];
+      if (chosen_out) chosen_out[cur0 + k] = k == istar ? inode + c.base : (gk ? key_node(gk) : -1);
+    }
+  __syncthreads();
+  if (bl == 0 && tid == 0) {
+    // new values from st[p ^ 1] only (see k_batch_top_commit)
+    const DevState* si = L.st_in;
+    DevState* so = L.st_out;
+    if (e1 > 0) {
+      const int32_t nb = min(kBatchPods, end - cur0);
+      so->cursor = cur0 + committed;
+      so->pod_seq = seq0 + committed;
+      so->scheduled = si->scheduled + s_sched;
+      so->unschedulable = si->unschedulable + s_unsched;
+      so->batches = si->batches + 1;
+      so->cuts = si->cuts + (committed < nb && istar < nchain ? 1 : 0);
+      so->truncations = si->truncations + (committed < nb && istar >= nchain ? 1 : 0);
+      if (committed > 0) {
+        const int2 w = reinterpret_cast<const int2*>(w1)[committed - 1];
+        so->next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
+        if (c.count_whole) so->evals = si->evals + s_evals;
+      }
+    }
+    if (FLUSH) *L.e_self = -1;
+  }
+  // this thread's node: S_i row = X[p ^ 1] + delta; written to X[p] by the
+  // first pod group's blocks
+  const int32_t node = nbase + tid;
+  const bool on = node < c.n;
+  const int32_t x = on ? node : 0;
+  const int32_t e = s_dn[tid];
+  ResCols d{0, 0, 0, 0, 0, 0};
+  if (on && e >= 0) d = s_rq[e];
+  const int64_t rc = c.req_cpu[x] + d.cpu, rm = c.req_mem[x] + d.mem, re = c.req_eph[x] + d.eph;
+  const int32_t np = c.num_pods[x] + d.pods;
+  if (on && blockIdx.y == 0) {
+    L.w.req_cpu[x] = rc;
+    L.w.req_mem[x] = rm;
+    L.w.req_eph[x] = re;
+    L.w.nz_cpu[x] = c.nz_cpu[x] + d.nzc;
+    L.w.nz_mem[x] = c.nz_mem[x] + d.nzm;
+    L.w.num_pods[x] = np;
+  }
+  if (FLUSH) return;
+  // the S_i feasibility bitmaps of pods [j0, j1) of batch i (k_adapt_mask_ns's trivial path)
+  const int32_t base = cur0 + committed;
+  const int32_t nb = min(kBatchPods, end - base);
+  const int32_t j0 = blockIdx.y * mp;
+  if (j0 >= nb) return;                              // block-uniform
+  const int32_t w = blockIdx.x * 4 + (tid >> 6);
+  if (w >= n_words) return;                          // wave-uniform
+  const int32_t j1 = min(j0 + mp, nb);
+  int64_t qc = 0, qm = 0, qe = 0;
+  uint32_t qf = 0;
+  if (lane < j1 - j0) {
+    const ksim_pod& q = P.pods[base + j0 + lane];
+    qc = q.req_cpu;
+    qm = q.req_mem;
+    qe = q.req_eph;
+    qf = q.flags;
+  }
+  const BatchProg& bp = *bp_p;
+  const bool fit = bp.has_fit_filter != 0;
+  bool room = true;
+  int64_t fc = 0, fm = 0, fe = 0;
+  if (fit) {
+    room = np + 1 <= c.alloc_pods[x];
+    fc = c.alloc_cpu[x] - rc;
+    fm = c.alloc_mem[x] - rm;
+    fe = c.alloc_eph[x] - re;
+  }
+  uint64_t word = 0;                               // lane l: pod j0 + l's ballot
+#pragma unroll 1
+  for (int32_t j = j0; j < j1; j++) {
+    const int l = j - j0;
+    const int64_t c0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qc >> 32), l) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)qc, l));
+    const int64_t m0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qm >> 32), l) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)qm, l));
+    const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qe >> 32), l) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)qe, l));
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)qf, l);
+    const bool none = c0 == 0 && m0 == 0 && e0 == 0 && !(f0 & KSIM_POD_HAS_SCALAR);
+    const bool ok = !fit || (room && (none || (c0 <= fc && m0 <= fm && e0 <= fe)));
+    const uint64_t mk = __ballot(on && ok);
+    word = lane == l ? mk : word;
+  }
+  if (lane < j1 - j0) amask[(size_t)(j0 + lane) * n_words + w] = word;
+}
+
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",
                                                          "k_batch_chain", "k_adapt_pairs", "k_adapt_commit"};
 
@@ -595,6 +797,49 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   if (win_fused) mask &= ~0x2u;                   // likewise the window slot
   return mask;
 }
+
+const char* const kLazyAdaptKernelNames[kKernelsPerLazyAdapt] = {"k_adapt_mask_commit", "k_adapt_window",
+                                                                 "k_adapt_top", "k_adapt_pairs"};
+
+static void launch_adapt_mask_commit(const LazyBatch& z, bool flush, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  const int32_t n_words = (a.c.n + 63) / 64;
+  const int32_t mp = mask_pods(n_words);
+  const dim3 grid((n_words + 3) / 4, (kBatchPods + mp - 1) / mp);
+  if (flush)
+    k_adapt_mask_commit<true><<<grid, 256, 0, stream>>>(a.c, a.P, a.dbp, z.step, z.b1, z.w1, a.s.amask, n_words, mp,
+                                                        a.chosen);
+  else
+    k_adapt_mask_commit<false><<<grid, 256, 0, stream>>>(a.c, a.P, a.dbp, z.step, z.b1, z.w1, a.s.amask, n_words, mp,
+                                                         a.chosen);
+}
+
+uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
+  const LaunchArgs& a = z.a;
+  const int32_t n_words = (a.c.n + 63) / 64;
+  const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, a.c.n);
+  if (evs) (void)hipEventRecord(evs[0], stream);
+  launch_adapt_mask_commit(z, false, stream);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  const bool win_fused = window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
+  if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
+  if (evs) (void)hipEventRecord(evs[2], stream);
+  // every later launch reads X[p] (z.cw) and st[p]
+#define TOP(NT, W) k_adapt_top<false, true, NT, W><<<kBatchPods, NT, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, \
+    a.s.amask, n_words, z.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr)
+  if (k >= kTopWideK) TOP(1024, false);
+  else if (win_fused) TOP(256, true);
+  else TOP(256, false);
+#undef TOP
+  if (evs) (void)hipEventRecord(evs[3], stream);
+  k_adapt_pairs<false, true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+      z.cw, a.P, a.dprof, a.dbp, z.st, a.s.amask, n_words, z.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey,
+      z.cend, z.pmax, z.abroken);
+  if (evs) (void)hipEventRecord(evs[4], stream);
+  return win_fused ? 0xdu : 0xfu;
+}
+
+void launch_adapt_lazy_flush(const LazyBatch& z, hipStream_t stream) { launch_adapt_mask_commit(z, true, stream); }
 
 // ---- node-sharded ADAPT batch -----------------------------------
 // Shards hold 64-aligned node ranges (adapt_shard_chunk), so shard r's bitmap

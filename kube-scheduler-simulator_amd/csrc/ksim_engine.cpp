@@ -173,7 +173,9 @@ struct ksim_handle {
   DevState* lazy_st1 = nullptr;
   uint64_t *lazy_g = nullptr, *lazy_m = nullptr;   // [kLazySlots][kBatchPods]
   int32_t* lazy_e = nullptr;                        // [kLazySlots] prefix length, -1 = empty slot
+  int32_t *lazy_ab = nullptr, *lazy_aw = nullptr;   // ADAPT: [kLazySlots][kBatchPods] broken flags, [..][2 B] windows
   hipGraphExec_t graph_lazy = nullptr;
+  hipGraphExec_t graph_lazy_adapt = nullptr;
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
   // the global bitmap (allocated at the first such run)
   std::vector<DevBuf> ash_bufs;
@@ -262,6 +264,8 @@ void drop_graphs(ksim_handle* h) {
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
+  if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
+  h->graph_lazy_adapt = nullptr;
   h->graph_batch_fast = nullptr;
   h->graph_batch = nullptr;
   h->graph_tbatch = nullptr;
@@ -594,7 +598,7 @@ bool lazy_enabled() {
 // (the overlay carries the resource columns only), on a cluster the overlay's
 // LDS node bitmap covers.
 bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b) {
-  if (!lazy_enabled() || batch_ab_forms() || is_sharded(h) || h->replicated || adapt_mode(h)) return false;
+  if (!lazy_enabled() || batch_ab_forms() || is_sharded(h) || h->replicated) return false;
   if (h->dc.base != 0 || h->dc.n > kLazyMaxNodes || h->dc.n <= 0) return false;
   for (int32_t i = a; i < b; i++)
     if (!h->noadd[i]) return false;
@@ -605,7 +609,8 @@ int alloc_lazy(ksim_handle* h) {
   if (h->lazy_n == h->dc.n) return KSIM_OK;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
-  h->graph_lazy = nullptr;
+  if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
+  h->graph_lazy = h->graph_lazy_adapt = nullptr;
   free_bufs(h->lazy_bufs);
   h->lazy_n = -1;
   const size_t n = (size_t)h->dc.n;
@@ -627,6 +632,10 @@ int alloc_lazy(ksim_handle* h) {
   h->lazy_m = (uint64_t*)p;
   if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * (size_t)kLazySlots, &p))) return rc;
   h->lazy_e = (int32_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
+  h->lazy_ab = (int32_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
+  h->lazy_aw = (int32_t*)p;
   h->lazy_n = h->dc.n;
   return KSIM_OK;
 }
@@ -667,6 +676,10 @@ LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
   z.gkey = h->lazy_g + (size_t)q * kBatchPods;
   z.pmax = h->lazy_m + (size_t)q * kBatchPods;
   z.cend = h->lazy_e + q;
+  z.b1 = h->lazy_ab + (size_t)q1 * kBatchPods;
+  z.w1 = h->lazy_aw + (size_t)q1 * 2 * kBatchPods;
+  z.abroken = h->lazy_ab + (size_t)q * kBatchPods;
+  z.awin = h->lazy_aw + (size_t)q * 2 * kBatchPods;
   return z;
 }
 
@@ -714,20 +727,30 @@ int read_state_at(ksim_handle* h, const DevState* src, DevState& st) {
 // Batch i commits batch i - 1; each stretch of launches ends with a flush, whose
 // state tells the host where the run stands.  A batch commits 1..kBatchPods
 // pods, so ceil(left / kBatchPods) batches never start past the end.
+uint32_t lazy_launch(const ksim_handle* h, const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr) {
+  return adapt_mode(h) ? launch_batch_adapt_lazy(z, stream, evs) : launch_batch_lazy(z, stream, evs);
+}
+
+void lazy_flush(const ksim_handle* h, const LazyBatch& z, hipStream_t stream) {
+  if (adapt_mode(h)) launch_adapt_lazy_flush(z, stream);
+  else launch_lazy_flush(z, stream);
+}
+
 int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   int rc;
   if ((rc = lazy_begin(h))) return rc;
-  if (!h->graph_lazy) {
+  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt : h->graph_lazy;
+  if (!graph) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     hipGraph_t g = nullptr;
     HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < kGraphBatches; i++) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
+    for (int i = 0; i < kGraphBatches; i++) lazy_launch(h, lazy_batch(h, la, i), h->stream);
     hipError_t e = hipStreamEndCapture(h->stream, &g);
     if (e != hipSuccess) return hip_fail(h, e, "hipStreamEndCapture");
-    e = hipGraphInstantiate(&h->graph_lazy, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) {
-      h->graph_lazy = nullptr;
+      graph = nullptr;
       return hip_fail(h, e, "hipGraphInstantiate");
     }
     h->graph_captures++;
@@ -739,13 +762,12 @@ int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
     int32_t nb = (b - cursor + kBatchPods - 1) / kBatchPods;
     const int32_t align = (int32_t)((kLazySlots - (i & 3)) & 3);
     if (nb >= align + kGraphBatches) {
-      for (int32_t r = 0; r < align; r++, i++, nb--) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
-      for (int32_t r = 0; r < nb / kGraphBatches; r++, i += kGraphBatches)
-        HIPCHK(h, hipGraphLaunch(h->graph_lazy, h->stream));
+      for (int32_t r = 0; r < align; r++, i++, nb--) lazy_launch(h, lazy_batch(h, la, i), h->stream);
+      for (int32_t r = 0; r < nb / kGraphBatches; r++, i += kGraphBatches) HIPCHK(h, hipGraphLaunch(graph, h->stream));
     } else {
-      for (int32_t r = 0; r < nb; r++, i++) launch_batch_lazy(lazy_batch(h, la, i), h->stream);
+      for (int32_t r = 0; r < nb; r++, i++) lazy_launch(h, lazy_batch(h, la, i), h->stream);
     }
-    launch_lazy_flush(lazy_batch(h, la, i), h->stream);
+    lazy_flush(h, lazy_batch(h, la, i), h->stream);
     HIPCHK(h, hipGetLastError());
     DevState st;
     if ((rc = read_state_at(h, (i & 1) ? h->lazy_st1 : h->st, st))) return rc;
@@ -2797,13 +2819,16 @@ const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerTbatch) return kTbatchKernelNames[k];
   k -= kKernelsPerTbatch;
   if (k >= 0 && k < kKernelsPerLazy) return kLazyKernelNames[k];
+  k -= kKernelsPerLazy;
+  if (k >= 0 && k < kKernelsPerLazyAdapt) return kLazyAdaptKernelNames[k];
   return nullptr;
 }
 
 int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_ms, int64_t* launches, int32_t cap) {
   int rc = ensure_ready(h);
   if (rc) return rc;
-  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch + kKernelsPerLazy;
+  constexpr int kKinds = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch + kKernelsPerLazy +
+                         kKernelsPerLazyAdapt;
   if (!avg_ms || cap < kKinds) return set_err(h, KSIM_E_INVALID, "avg_ms too small");
   if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
@@ -2828,30 +2853,34 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
                      : adapt ? kKernelsPerCycle + kKernelsPerBatch
                      : batch ? kKernelsPerCycle : 0;
     if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
-    if (batch && !adapt && !tb && a.fast && lazy_ok(h, lo, hi)) {
-      // deferred-commit batches: two launches each, a flush (untimed) before
-      // every state read
-      const int lbase = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch;
+    if (batch && !tb && a.fast && lazy_ok(h, lo, hi)) {
+      // deferred-commit batches: two (P100) or three to four (ADAPT) launches
+      // each, a flush (untimed) before every state read
+      const int lper = adapt ? kKernelsPerLazyAdapt : kKernelsPerLazy;
+      const int lbase = kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt + kKernelsPerTbatch +
+                        (adapt ? kKernelsPerLazy : 0);
       HIPCHK(h, hipMemsetAsync(&h->st->batches, 0, 4, h->stream));
       if ((r = lazy_begin(h))) return r;
       int64_t i = 0;
       int32_t cursor = lo, done_batches = 0;
       while (cursor < hi) {
         const int32_t iters = std::min(64, (hi - cursor + kBatchPods - 1) / kBatchPods);
-        std::vector<hipEvent_t> evs((size_t)iters * (kKernelsPerLazy + 1));
+        std::vector<hipEvent_t> evs((size_t)iters * (lper + 1));
         for (auto& e : evs) HIPCHK(h, hipEventCreate(&e));
+        uint32_t launched = 0;
         for (int32_t t = 0; t < iters; t++, i++)
-          launch_batch_lazy(lazy_batch(h, a, i), h->stream, &evs[(size_t)t * (kKernelsPerLazy + 1)]);
-        launch_lazy_flush(lazy_batch(h, a, i), h->stream);
+          launched = lazy_launch(h, lazy_batch(h, a, i), h->stream, &evs[(size_t)t * (lper + 1)]);
+        lazy_flush(h, lazy_batch(h, a, i), h->stream);
         HIPCHK(h, hipGetLastError());
         DevState st;
         if ((r = read_state_at(h, (i & 1) ? h->lazy_st1 : h->st, st))) return r;
         const int32_t did = std::min<int32_t>(iters, st.batches - done_batches);
         done_batches = st.batches;
         for (int32_t t = 0; t < did; t++)
-          for (int k = 0; k < kKernelsPerLazy; k++) {
+          for (int k = 0; k < lper; k++) {
+            if (!((launched >> k) & 1u)) continue;   // an empty event pair (the window fused into the top)
             float ms = 0;
-            const size_t e0 = (size_t)t * (kKernelsPerLazy + 1);
+            const size_t e0 = (size_t)t * (lper + 1);
             HIPCHK(h, hipEventElapsedTime(&ms, evs[e0 + k], evs[e0 + k + 1]));
             sum[lbase + k] += ms;
             n[lbase + k] += 1;

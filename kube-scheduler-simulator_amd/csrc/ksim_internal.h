@@ -111,9 +111,22 @@ struct LazyBatch {
   uint64_t* gkey;      // batch i's slot
   uint64_t* pmax;
   int32_t* cend;
+  // ADAPT: batch i-1's broken-window flags and windows, batch i's slot of them
+  const int32_t* b1;
+  const int32_t* w1;
+  int32_t* abroken;
+  int32_t* awin;
 };
 constexpr int kKernelsPerLazy = 2;
 extern const char* const kLazyKernelNames[kKernelsPerLazy];
+// ADAPT (ksim_adapt.hip): k_adapt_mask_commit (commit of i-1, the S_i bitmaps
+// of i, every row written to X[p]), the window scan when not fused into the
+// top, the top, the chain + pairs.  X[p] is written whole, so only batch i-1's
+// slot is read.
+constexpr int kKernelsPerLazyAdapt = 4;
+extern const char* const kLazyAdaptKernelNames[kKernelsPerLazyAdapt];
+uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr);
+void launch_adapt_lazy_flush(const LazyBatch& z, hipStream_t stream);
 // batch i: k_batch_top_commit (commit of i-1, evaluation of i), then the
 // chain + pairs of i.  A flush is the first launch alone with no evaluation:
 // it commits batch i-1 and leaves slot i empty.

@@ -362,8 +362,9 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       const bool v2 = off + NT < kend;
       if (!v2) n2 = n1;
       const uint64_t w1 = mask[n1 >> 6], w2 = mask[n2 >> 6];
-      const NodeRow r1 = load_res_row(c, n1), r2 = load_res_row(c, n2);
-      const double c1 = c.inv_cpu[n1], m1 = c.inv_mem[n1], c2 = c.inv_cpu[n2], m2 = c.inv_mem[n2];
+      const NodeRow r1 = load_res_row_off(c, n1), r2 = load_res_row_off(c, n2);
+      const double c1 = ld_off(c.inv_cpu, (uint32_t)n1 << 3), m1 = ld_off(c.inv_mem, (uint32_t)n1 << 3);
+      const double c2 = ld_off(c.inv_cpu, (uint32_t)n2 << 3), m2 = ld_off(c.inv_mem, (uint32_t)n2 << 3);
       __builtin_amdgcn_sched_barrier(0);
       if ((w1 >> (n1 & 63)) & 1ull) {
         kept++;

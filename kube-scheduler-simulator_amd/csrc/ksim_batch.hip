@@ -350,9 +350,9 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
       for (int u = 0; u < kTopStep; u++) {
         const int32_t nu = node + u * kTopThreads;
         const int32_t x = nu < c.eval_hi ? nu : node;
-        r[u] = load_res_row(c, x);
-        ic[u] = c.inv_cpu[x];
-        im[u] = c.inv_mem[x];
+        r[u] = load_res_row_off(c, x);
+        ic[u] = ld_off(c.inv_cpu, (uint32_t)x << 3);
+        im[u] = ld_off(c.inv_mem, (uint32_t)x << 3);
       }
       __builtin_amdgcn_sched_barrier(0);      // every row in flight before the first key
 #pragma unroll
@@ -984,11 +984,10 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPo
 // S_{i-2}; a guess that was not bound keeps its value, so the superset is
 // harmless); block 0 writes the state after the commit to st[p].  FLUSH: no
 // evaluation, and slot i is marked empty.
-// KSIM_LAZY_WARM (default 1): rows batch i-1 and i-2 did not touch are read
-// from X[p], which batch i's chain + pairs read next (0: every row from
-// X[p ^ 1], for A/B builds)
-#ifndef KSIM_LAZY_WARM
-#define KSIM_LAZY_WARM 0
+// KSIM_TOP_OFF32 (default 1): the node loop's row loads by 32-bit byte
+// offsets (0: 64-bit addresses per column, for A/B builds)
+#ifndef KSIM_TOP_OFF32
+#define KSIM_TOP_OFF32 1
 #endif
 constexpr int kLazyHash = 1 << kLazyHashBits;
 constexpr int kLazyBitWords = kLazyMaxNodes / 32;
@@ -1021,11 +1020,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     g1 = L.g1[tid];
     m1 = L.m1[tid];
   }
-#if KSIM_LAZY_WARM
-  if (tid < kBatchPods) g2 = L.g2[tid];
-#else
   if (tid == b) g2 = L.g2[b];
-#endif
   const int32_t cur0 = L.st_in->cursor, end = L.st_in->end;
   const int64_t seq0 = L.st_in->pod_seq;
   const int nwords = (c.n + 31) >> 5;
@@ -1077,20 +1072,6 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     while (atomicCAS(&s_hkey[h], -1, gnode) != -1) h = (h + 1) & (kLazyHash - 1);   // guessed nodes are distinct
     s_hval[h] = (int16_t)tid;
   }
-#if KSIM_LAZY_WARM
-  // the bitmap marks every node where X[p] (S_{i-2}) and X[p ^ 1] (S_{i-1})
-  // may differ or batch i-1 bound: the guesses of batches i-2 and i-1.  Those
-  // rows are read from X[p ^ 1] (+ the delta); every other row from X[p],
-  // which then sits in each XCD's L2 for batch i's chain + pairs
-  if (tid < e2 && g2) {
-    const int32_t n2 = key_node(g2) - c.base;
-    atomicOr(&s_bits[n2 >> 5], 1u << (n2 & 31));
-  }
-  if (tid < nchain && g1) {
-    const int32_t n1 = key_node(g1) - c.base;
-    atomicOr(&s_bits[n1 >> 5], 1u << (n1 & 31));
-  }
-#endif
   // batch i-1's placements and statistics (k_batch_commit's bookkeeping)
   const int32_t pnode = tid == istar ? inode + c.base : (g1 ? key_node(g1) : -1);
   if (tid == b && tid < committed && chosen_out) chosen_out[cur0 + b] = pnode;
@@ -1130,20 +1111,14 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     if (FLUSH) *L.e_self = -1;
   }
   // the overlay delta of a node (zero when batch i-1 did not bind it)
-  // the node's delta in the hash (zero when batch i-1 did not bind it)
-  auto hash_delta = [&](int32_t node) -> ResCols {
-    ResCols d{0, 0, 0, 0, 0, 0};
-    uint32_t h = lazy_hash(node);
-    for (int32_t k; (k = s_hkey[h]) != -1; h = (h + 1) & (kLazyHash - 1))
-      if (k == node) {
-        d = s_rq[s_hval[h]];
-        break;
-      }
-    return d;
-  };
   auto delta = [&](int32_t node) -> ResCols {
     ResCols d{0, 0, 0, 0, 0, 0};
-    if ((s_bits[node >> 5] >> (node & 31)) & 1u) d = hash_delta(node);
+    const uint32_t bw = s_bits[node >> 5], bit = 1u << (node & 31);
+    if (bw & bit) {
+      uint32_t h = lazy_hash(node);
+      while (s_hkey[h] != node) h = (h + 1) & (kLazyHash - 1);   // present: the bit says so
+      d = s_rq[s_hval[h]];
+    }
     return d;
   };
   auto materialize = [&]() {
@@ -1178,39 +1153,14 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   int32_t nfeas = 0;
 #pragma unroll 1
   for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
-#if KSIM_LAZY_WARM
-    NodeRow r;
-    r.node = node;
-    r.flags = 0;
-#pragma unroll
-    for (int k = 0; k < KSIM_MAX_SCALAR; k++) r.alloc_sc[k] = r.req_sc[k] = 0;
-#pragma unroll
-    for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++) r.taints[k] = 0;
-    r.alloc_cpu = c.alloc_cpu[node];
-    r.alloc_mem = c.alloc_mem[node];
-    r.alloc_eph = c.alloc_eph[node];
-    r.alloc_pods = c.alloc_pods[node];
-    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
-    const bool dirty = (s_bits[node >> 5] >> (node & 31)) & 1u;
-    // dirty: X[p ^ 1] (+ delta); else X[p] (the same values)
-    const int64_t* q_rc = dirty ? c.req_cpu : L.w.req_cpu;
-    const int64_t* q_rm = dirty ? c.req_mem : L.w.req_mem;
-    const int64_t* q_re = dirty ? c.req_eph : L.w.req_eph;
-    const int64_t* q_nc = dirty ? c.nz_cpu : L.w.nz_cpu;
-    const int64_t* q_nm = dirty ? c.nz_mem : L.w.nz_mem;
-    const int32_t* q_np = dirty ? c.num_pods : L.w.num_pods;
-    r.req_cpu = q_rc[node];
-    r.req_mem = q_rm[node];
-    r.req_eph = q_re[node];
-    r.nz_cpu = q_nc[node];
-    r.nz_mem = q_nm[node];
-    r.num_pods = q_np[node];
-    const ResCols d = dirty ? hash_delta(node) : ResCols{0, 0, 0, 0, 0, 0};
+#if KSIM_TOP_OFF32
+    NodeRow r = load_res_row_off(c, node);
+    const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
 #else
     NodeRow r = load_res_row(c, node);
     const double ic = c.inv_cpu[node], im = c.inv_mem[node];
-    const ResCols d = delta(node);
 #endif
+    const ResCols d = delta(node);
     r.req_cpu += d.cpu;
     r.req_mem += d.mem;
     r.req_eph += d.eph;

@@ -365,6 +365,35 @@ __device__ __forceinline__ NodeRow load_res_row(const DevCluster& c, int32_t nod
   return r;
 }
 
+// load_res_row by 32-bit byte offsets from the column bases (one shift per
+// element size instead of a 64-bit address per column: the loads take the
+// scalar-base + vector-offset form)
+template <typename T>
+__device__ __forceinline__ T ld_off(const T* base, uint32_t off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+}
+__device__ __forceinline__ NodeRow load_res_row_off(const DevCluster& c, int32_t node) {
+  const uint32_t o8 = (uint32_t)node << 3, o4 = (uint32_t)node << 2;
+  NodeRow r;
+  r.node = node;
+  r.alloc_cpu = ld_off(c.alloc_cpu, o8);
+  r.alloc_mem = ld_off(c.alloc_mem, o8);
+  r.alloc_eph = ld_off(c.alloc_eph, o8);
+  r.req_cpu = ld_off((const int64_t*)c.req_cpu, o8);
+  r.req_mem = ld_off((const int64_t*)c.req_mem, o8);
+  r.req_eph = ld_off((const int64_t*)c.req_eph, o8);
+  r.nz_cpu = ld_off((const int64_t*)c.nz_cpu, o8);
+  r.nz_mem = ld_off((const int64_t*)c.nz_mem, o8);
+  r.alloc_pods = ld_off(c.alloc_pods, o4);
+  r.num_pods = ld_off((const int32_t*)c.num_pods, o4);
+  r.flags = 0;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) r.alloc_sc[k] = r.req_sc[k] = 0;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_NODE_TAINTS / 2; k++) r.taints[k] = 0;
+  return r;
+}
+
 __device__ __forceinline__ NodeRow load_row(const DevCluster& c, int32_t node) {
   NodeRow r;
   r.node = node;

@@ -528,6 +528,18 @@ def main():
                 "valu_insts_per_launch": ve["valu_insts_per_launch"],
                 "salu_insts_per_launch": ve.get("salu_insts_per_launch"),
                 "valu_insts_per_eval_lane": ve.get("valu_insts_per_eval_lane"), "source": ve.get("source")}
+        act, wcyc, waves = (ve.get("valu_active_quad_cycles_per_launch"), ve.get("wave_quad_cycles_per_launch"),
+                            ve.get("waves_per_launch"))
+        if act and wcyc and waves:
+            # SQ_ACTIVE_INST_VALU per SIMD over the mean wave lifetime (SQ_WAVE_CYCLES / SQ_WAVES): the
+            # share of the launch its SIMDs spend issuing VALU work (1,024 SIMDs, every one holding waves
+            # of the launch for its whole duration; a 64-bit or f64 op holds the SIMD longer than the
+            # 2-cycle issue slot the "frac" above prices every instruction at)
+            valu["busy_frac_pmc"] = (act / 1024.0) / (wcyc / waves)
+            valu["wait_mem_frac_pmc"] = ve.get("wait_any_quad_cycles_per_launch", 0) / wcyc
+            valu["wait_issue_frac_pmc"] = ve.get("wait_inst_any_quad_cycles_per_launch", 0) / wcyc
+            if ve.get("valu_mix_per_launch"):
+                valu["mix_per_launch"] = ve["valu_mix_per_launch"]
 
     seeds = {1: "0x4B53494D0001", 2: "0x4B53494D0002", 3: "0x4B53494D0003", 4: "0x4B53494D0004", 5: "0x4B53494D0002/0005"}
     result = {

@@ -917,6 +917,17 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPod
 // runs the (deterministic) chain itself, thread k ending with pod k's guess in
 // a register, so the pairs need no chain launch and no gkey round trip.
 // Block 0 also stores the guesses and the prefix length for k_batch_commit.
+#ifdef KSIM_CP_CLOCKS
+__device__ unsigned long long g_cp_dbg[8];
+unsigned long long* cp_clock_buffer() {
+  void* p = nullptr;
+  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_cp_dbg));
+  return (unsigned long long*)p;
+}
+#else
+unsigned long long* cp_clock_buffer() { return nullptr; }
+#endif
+
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
 template <bool FAST, int NCHUNK = 0, bool LAZY = false>
@@ -945,8 +956,17 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
   }
   uint64_t gk;
   int32_t nchain;
+#ifdef KSIM_CP_CLOCKS
+  // phase clocks of block 0 (KSIM_CP_CLOCKS builds, tools/cp_clocks.py): the
+  // chain's setup / rounds / epilogue (dbg 0-2, launches 3, rounds 4), the
+  // whole block (dbg 5)
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+  unsigned long long* dbgc = blockIdx.x == 0 ? g_cp_dbg : nullptr;
+#else
+  unsigned long long* dbgc = nullptr;
+#endif
   // NCHUNK > 0: topk / topk_cnt are the node-split top's chunk lists (k_batch_top_ns)
-  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) {
+  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc)) {
     if (LAZY && blockIdx.x == 0 && threadIdx.x == 0) *chain_end = -1;
     return;
   }
@@ -957,6 +977,9 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
   }
   pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr, FAST ? &pk : nullptr,
                     pnorm, pinv, s_winv);
+#ifdef KSIM_CP_CLOCKS
+  if (dbgc && threadIdx.x == 0) atomicAdd(&dbgc[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_in));
+#endif
 }
 
 __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
@@ -1003,7 +1026,8 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
                                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
                                                            int32_t* __restrict__ topk_complete,
-                                                           int32_t* __restrict__ chosen_out) {
+                                                           int32_t* __restrict__ chosen_out,
+                                                           uint64_t* __restrict__ xsend) {
   constexpr int kThreads = 1024;
   __shared__ ResCols s_rq[kBatchPods];          // batch i-1's pod requests, then each bound node's delta
   __shared__ int32_t s_hkey[kLazyHash];         // overlay hash: local node or -1
@@ -1175,7 +1199,8 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     cswap_desc(a[0], a[1]);
   }
   materialize();
-  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, nullptr);
+  // xsend (replicated handles): this replica's record of its node range, for the all-gather
+  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
 }
 
 const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_batch_chain_pairs"};
@@ -1184,7 +1209,7 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
   const LaunchArgs& a = z.a;
   if (evs) (void)hipEventRecord(evs[0], stream);
   k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, a.chosen);
+                                                             a.s.topk_complete, a.chosen, nullptr);
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
                                                                             a.s.topk_cnt, a.s.topk_complete, z.gkey,
@@ -1196,13 +1221,31 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
 void launch_lazy_top(const LazyBatch& z, hipStream_t stream) {
   const LaunchArgs& a = z.a;
   k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, a.chosen);
+                                                             a.s.topk_complete, a.chosen, nullptr);
+}
+
+// Replicated handles (ksim_set_eval_range): the first launch keys the replica's
+// node range and writes its record; after the records' all-gather, the global
+// merge and the chain + pairs on X[p].
+void launch_lazy_top_rep(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
+                                                             a.s.topk_complete, a.chosen, xsend);
+}
+
+void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
+                                                     a.s.topk_complete);
+  k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
+                                                                            a.s.topk_cnt, a.s.topk_complete, z.gkey,
+                                                                            z.cend, z.pmax, a.s.pnorm, a.s.pinv);
 }
 
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
   const LaunchArgs& a = z.a;
   k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                            a.s.topk_complete, a.chosen);
+                                                            a.s.topk_complete, a.chosen, nullptr);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.

@@ -598,7 +598,10 @@ bool lazy_enabled() {
 // (the overlay carries the resource columns only), on a cluster the overlay's
 // LDS node bitmap covers.
 bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b) {
-  if (!lazy_enabled() || batch_ab_forms() || is_sharded(h) || h->replicated) return false;
+  if (!lazy_enabled() || batch_ab_forms()) return false;
+  // ADAPT runs whole on a replica (no exchange); replicated P100 batches take
+  // shard_run_lazy (lazy_rep_ok)
+  if (adapt_mode(h) ? (is_sharded(h) && !h->replicated) : (is_sharded(h) || h->replicated)) return false;
   if (h->dc.base != 0 || h->dc.n > kLazyMaxNodes || h->dc.n <= 0) return false;
   for (int32_t i = a; i < b; i++)
     if (!h->noadd[i]) return false;
@@ -909,6 +912,113 @@ int shard_batch(const std::vector<ksim_handle*>& hs, hipStream_t stream, bool fa
 
 hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast, bool adapt);
 
+// ---- replicated deferred-commit batches (ksim_internal.h) -----------------------
+// Replicated handles of a FAST P100 run: batch i is k_batch_top_commit over the
+// replica's node range (the commit of batch i-1 included, every replica binds
+// every placement), the records' all-gather, the global merge and the chain +
+// pairs: one exchange and three launches per batch instead of four.
+bool lazy_rep_ok(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b, bool fast) {
+  if (!fast || !lazy_enabled() || batch_ab_forms()) return false;
+  for (auto* h : hs) {
+    if (!h->replicated || h->dc.base != 0 || h->dc.n > kLazyMaxNodes || h->dc.n <= 0) return false;
+    for (int32_t i = a; i < b; i++)
+      if (!h->noadd[i]) return false;
+  }
+  return true;
+}
+
+int shard_batch_lazy(const std::vector<ksim_handle*>& hs, hipStream_t stream, int64_t i) {
+  const int R = (int)hs.size();
+  ksim_handle* h0 = hs[0];
+  const size_t rec = (size_t)kBatchPods * kXRec;
+  for (auto* h : hs) launch_lazy_top_rep(lazy_batch(h, shard_args(h, true), i), h->sc.xsend, stream);
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(h0->sc.xsend, h0->sc.xrecv, rec, ncclUint64, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+  } else {
+    for (int src = 0; src < R; src++)
+      for (int dst = 0; dst < R; dst++)
+        HIPCHK(h0, hipMemcpyAsync(hs[dst]->sc.xrecv + (size_t)src * rec, hs[src]->sc.xsend, 8 * rec,
+                                  hipMemcpyDeviceToDevice, stream));
+  }
+  const int32_t world = h0->comm ? h0->world : R;
+  for (auto* h : hs) launch_lazy_chain_rep(lazy_batch(h, shard_args(h, true), i), world, stream);
+  HIPCHK(h0, hipGetLastError());
+  return KSIM_OK;
+}
+
+hipGraphExec_t shard_lazy_graph(const std::vector<ksim_handle*>& hs) {
+  ksim_handle* h0 = hs[0];
+  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  std::vector<std::pair<const ksim_handle*, int64_t>> sig;
+  for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
+  if (sig != h0->sg_sig) {
+    for (auto& kv : h0->sg_graphs) (void)hipGraphExecDestroy(kv.second);
+    h0->sg_graphs.clear();
+    h0->sg_sig = sig;
+  }
+  const auto key = std::make_tuple(true, (int64_t)-3, (int64_t)-1);
+  auto it = h0->sg_graphs.find(key);
+  if (it != h0->sg_graphs.end()) return it->second;
+  hipStream_t stream = h0->stream;
+  if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  bool ok = hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  for (int i = 0; ok && i < kGraphBatches; i++) ok = shard_batch_lazy(hs, stream, i) == KSIM_OK;
+  const hipError_t e = hipStreamEndCapture(stream, &g);
+  ok = ok && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess;
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  if (!ok) {
+    h0->sg_off = true;
+    h0->err.clear();
+    return nullptr;
+  }
+  h0->graph_captures++;
+  h0->sg_graphs.emplace(key, ge);
+  return ge;
+}
+
+// set_run done on every handle.  As run_lazy, on the group's stream.
+int shard_run_lazy(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
+  ksim_handle* h0 = hs[0];
+  hipStream_t stream = h0->stream;
+  int rc;
+  for (auto* h : hs) {
+    if ((rc = lazy_begin(h))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_lazy_graph(hs) : nullptr;
+  int64_t i = 0;
+  int32_t cursor = a;
+  while (cursor < b) {
+    int32_t nb = (b - cursor + kBatchPods - 1) / kBatchPods;
+    const int32_t align = (int32_t)((kLazySlots - (i & 3)) & 3);
+    if (g && nb >= align + kGraphBatches) {
+      for (int32_t r = 0; r < align; r++, i++, nb--)
+        if ((rc = shard_batch_lazy(hs, stream, i))) return rc;
+      for (int32_t r = 0; r < nb / kGraphBatches; r++, i += kGraphBatches) HIPCHK(h0, hipGraphLaunch(g, stream));
+    } else {
+      for (int32_t r = 0; r < nb; r++, i++)
+        if ((rc = shard_batch_lazy(hs, stream, i))) return rc;
+    }
+    for (auto* h : hs) launch_lazy_flush(lazy_batch(h, shard_args(h, true), i), stream);
+    HIPCHK(h0, hipGetLastError());
+    DevState st;
+    HIPCHK(h0, hipMemcpyAsync(&st, (i & 1) ? h0->lazy_st1 : h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));
+    HIPCHK(h0, hipStreamSynchronize(stream));
+    if (st.cursor <= cursor) return set_err(h0, KSIM_E_DEVICE, "replicated deferred-commit batches made no progress");
+    cursor = st.cursor;
+    i++;
+  }
+  for (auto* h : hs) {
+    if ((rc = lazy_end(h, i - 1))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  return KSIM_OK;
+}
+
 // Pods [a, b) on the sharded batch path (every pod must be batchable).  No
 // batch is ever issued past the run's end (each commits 1..kBatchPods pods):
 // whole graphs of kGraphBatches batches while at least kBatchPods *
@@ -923,6 +1033,7 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
     if ((rc = set_run(h, a, b))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  if (lazy_rep_ok(hs, a, b, fast)) return shard_run_lazy(hs, a, b);
   const hipGraphExec_t g = b - a >= kBatchPods * kGraphBatches ? shard_batch_graph(hs, fast, false) : nullptr;
   int32_t cursor = a;
   while (cursor < b) {
@@ -2950,6 +3061,8 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   if (rc) return rc;
   int64_t v[3 + 16 + 2] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
+  if (unsigned long long* cp = cp_clock_buffer())   // KSIM_CP_CLOCKS builds: the chain + pairs phase clocks
+    HIPCHK(h, hcopy(h, v + 3, cp, 8 * 8, hipMemcpyDeviceToHost));
   v[19] = h->graph_captures;
   v[20] = h->match_ns;
   const int32_t m = n < 21 ? n : 21;

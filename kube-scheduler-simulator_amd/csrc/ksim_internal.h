@@ -76,6 +76,7 @@ uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool
 // Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
 bool chain_fused();   // KSIM_CHAIN_SEPARATE unset: the chain runs inside the pairs launch
 bool batch_ab_forms();   // an A/B switch of the three-launch batch forms is set (no deferred commit)
+unsigned long long* cp_clock_buffer();   // KSIM_CP_CLOCKS builds: chain + pairs phase clocks (else null)
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
 uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
@@ -133,6 +134,10 @@ void launch_adapt_lazy_flush(const LazyBatch& z, hipStream_t stream);
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream);
 void launch_lazy_top(const LazyBatch& z, hipStream_t stream);   // the first launch alone (ksim_time_eval)
+// replicated handles: the first launch with the replica's record (xsend), then,
+// after the records' all-gather into a.s.xrecv, the global merge + chain + pairs
+void launch_lazy_top_rep(const LazyBatch& z, uint64_t* xsend, hipStream_t stream);
+void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream);
 void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // Compat cycle around the host's extender round trip (ksim_eval_pod_filter / _finish):
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.

@@ -1534,7 +1534,6 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
 }
 
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v) {
-  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
   if (!h || !t || !v) return KSIM_E_INVALID;
   HIPCHK(h, hipSetDevice(h->device));
   const int32_t n = t->n_nodes;
@@ -1572,6 +1571,9 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   if (v->n_topo_log < 0 || (v->n_topo_log > 0 && !v->topo_log))
     return set_err(h, KSIM_E_INVALID, "bad topo_log");
   (void)hipStreamSynchronize(h->stream);
+  // the inputs are valid: the old snapshot goes, and with it the evaluation
+  // range (a replica calls ksim_set_eval_range again)
+  h->replicated = false;
   drop_graphs(h);
   free_bufs(h->cluster_bufs);
   free_bufs(h->scratch_bufs);
@@ -1883,11 +1885,11 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
 // table handed to ksim_upsert_nodes is the current snapshot without it, so the
 // replay keeps every other node's state.
 int ksim_remove_node(ksim_handle* h, int32_t pos) {
-  if (h) h->replicated = false;                 // a new snapshot: ksim_set_eval_range again
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_remove_node on a shard handle");
   const int32_t n0 = h->dc.n;
   if (pos < 0 || pos >= n0) return set_err(h, KSIM_E_INVALID, "node position out of range");
+  h->replicated = false;                        // a new snapshot: ksim_set_eval_range again
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const DevCluster& c = h->dc;

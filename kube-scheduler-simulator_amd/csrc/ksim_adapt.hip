@@ -478,7 +478,9 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   uint64_t gk;
   if constexpr (CHAIN) {
     __shared__ ChainLds L;
-    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr)) return;
+    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr, kBatchPods,
+                     KSIM_CHAIN_DIRECT ? c.n_total : 0))
+      return;
     if (j == 0) {
       if (k < nb) gkey[k] = gk;
       if (k == 0) *chain_end = nchain;

@@ -966,7 +966,8 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
   unsigned long long* dbgc = nullptr;
 #endif
   // NCHUNK > 0: topk / topk_cnt are the node-split top's chunk lists (k_batch_top_ns)
-  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc)) {
+  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc, kBatchPods,
+                           KSIM_CHAIN_DIRECT ? c.n_total : 0)) {
     if (LAZY && blockIdx.x == 0 && threadIdx.x == 0) *chain_end = -1;
     return;
   }

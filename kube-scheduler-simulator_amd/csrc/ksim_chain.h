@@ -36,9 +36,18 @@ constexpr int kChainRounds = 64;               // exact prefix kept if not conve
 #endif
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
 
+// Clusters of at most kChainDirect nodes index the holders by node id (no hash
+// probes while the lists are registered).  KSIM_CHAIN_DIRECT (default 1) lets
+// the chain + pairs launches use it (0: the hash everywhere, for A/B builds):
+// config 2 7.03 -> 6.80 ms per step (profiles/r03/ab_chaindirect)
+#ifndef KSIM_CHAIN_DIRECT
+#define KSIM_CHAIN_DIRECT 1
+#endif
+constexpr int kChainDirect = 8192;
+constexpr int kChainHoldSlots = kHashSlots > kChainDirect ? kHashSlots : kChainDirect;
 struct ChainLds {
-  int32_t key[kHashSlots];                     // node id in the slot, -1 = empty
-  int32_t hold[kHashSlots];                    // lowest pod index holding the slot this round
+  int32_t key[kHashSlots];                     // node id in the slot, -1 = empty (hash mode)
+  int32_t hold[kChainHoldSlots];               // lowest pod index holding the slot this round
   int16_t rep[kBatchPods][kTopT];              // slot of each list entry
   int32_t first[2], cut;                      // first: one slot per round parity (see the round loop)
 };
@@ -122,7 +131,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
                                             const int32_t* __restrict__ topk_cnt,
                                             const int32_t* __restrict__ topk_complete, uint64_t* gk,
                                             int32_t* nchain_out, unsigned long long* __restrict__ dbg,
-                                            int32_t nb_cap = kBatchPods) {
+                                            int32_t nb_cap = kBatchPods, int32_t direct_n = 0) {
   int32_t* const s_key = L.key;
   int32_t* const s_hold = L.hold;
   int32_t& s_cut = L.cut;
@@ -146,34 +155,41 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   const int32_t base = st->cursor;
   const int32_t nb = min(nb_cap, st->end - base);   // nb_cap: the topology batch's pod count
   if (nb <= 0) return false;
-  for (int x = i; x < kHashSlots; x += kBatchPods) {
-    s_key[x] = -1;
-    s_hold[x] = kBatchPods;
-  }
-  if (i < 2) L.first[i] = kBatchPods;
   const int cnt = i < nb ? cnt0 : 0;
   const bool incomplete = i < nb && !complete0;
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < kTopT; e++) {
-    int16_t slot = -1;
-    if (e < cnt) {
-      const int32_t node = key_node(lst[e]);
-      uint32_t h = ((uint32_t)node * 2654435761u) >> (32 - kHashBits);
-      while (true) {
-        const int32_t prev = atomicCAS(&s_key[h], -1, node);
-        if (prev == -1 || prev == node) break;
-        h = (h + 1) & (kHashSlots - 1);
-      }
-      slot = (int16_t)h;
-    }
-    L.rep[i][e] = slot;
-  }
-  __syncthreads();
+  if (i < 2) L.first[i] = kBatchPods;
   // this pod's slots in registers (selects below, never a dynamic index)
   int32_t rep[kTopT];
+  if (direct_n > 0 && direct_n <= kChainDirect) {   // block-uniform: the slot is the node id
+    for (int x = i; x < direct_n; x += kBatchPods) s_hold[x] = kBatchPods;
 #pragma unroll
-  for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
+    for (int e = 0; e < kTopT; e++) rep[e] = e < cnt ? key_node(lst[e]) : -1;
+    __syncthreads();
+  } else {
+    for (int x = i; x < kHashSlots; x += kBatchPods) {
+      s_key[x] = -1;
+      s_hold[x] = kBatchPods;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) {
+      int16_t slot = -1;
+      if (e < cnt) {
+        const int32_t node = key_node(lst[e]);
+        uint32_t h = ((uint32_t)node * 2654435761u) >> (32 - kHashBits);
+        while (true) {
+          const int32_t prev = atomicCAS(&s_key[h], -1, node);
+          if (prev == -1 || prev == node) break;
+          h = (h + 1) & (kHashSlots - 1);
+        }
+        slot = (int16_t)h;
+      }
+      L.rep[i][e] = slot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
+  }
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
   int first = kBatchPods, rounds = 0;

@@ -312,6 +312,96 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   }
 }
 
+// The generic (non-FAST) keys of pod j = pi - cursor over the block's nodes:
+// static filters, the resource key, and for kPodNormVaries pods the
+// normalized TaintToleration / NodeAffinity parts.  ov(row) adds whatever the
+// caller knows the snapshot lacks (the deferred commit's overlay); k_batch_top
+// passes a no-op.
+template <int kTopThreads, typename Ov>
+__device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
+                                             const BatchProg& bp, const ksim_pod& p, int32_t pi, int32_t j,
+                                             int64_t seq, bool trivial, int64_t* __restrict__ pnorm,
+                                             uint64_t (&a)[kTileCand], int32_t& nfeas, Ov&& ov) {
+  constexpr int kTopWaves = kTopThreads / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
+    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
+    // nodes (P100: every feasible node is scored), the keys then carry the
+    // normalized scores (norm_part)
+    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+    NormRaw mx{0, 0};
+    if (normv) {
+      // the maxima and how many S0-feasible nodes hold each: the batch keeps
+      // pod j until every holder of a maximum has left its feasible set
+      // (pairs_block), not at the first one
+      __shared__ uint64_t s_nmax[2][kTopWaves];
+      __shared__ int32_t s_ncnt[2][kTopWaves];
+      uint64_t lt = 0, la = 0;                   // this lane's maxima (raw scores are >= 0) ...
+      int32_t ct = 0, ca = 0;                    // ... and its nodes holding them
+#pragma unroll 1
+      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+        NodeRow r = load_row(c, node);
+        ov(r);
+        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
+          const NormRaw v = norm_raw(c, P, p, r);
+          ct = (uint64_t)v.tt > lt ? 1 : ct + ((uint64_t)v.tt == lt ? 1 : 0);
+          lt = umax64(lt, (uint64_t)v.tt);
+          ca = (uint64_t)v.na > la ? 1 : ca + ((uint64_t)v.na == la ? 1 : 0);
+          la = umax64(la, (uint64_t)v.na);
+        }
+      }
+      uint64_t xt = wave_max_u64_dpp(lt), xa = wave_max_u64_dpp(la);
+      if (lane == 0) {
+        s_nmax[0][wv] = xt;
+        s_nmax[1][wv] = xa;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kTopWaves; w++) {
+        xt = umax64(xt, s_nmax[0][w]);
+        xa = umax64(xa, s_nmax[1][w]);
+      }
+      int32_t nt = lt == xt ? ct : 0, na = la == xa ? ca : 0;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        nt += __shfl_xor(nt, d, 64);
+        na += __shfl_xor(na, d, 64);
+      }
+      if (lane == 0) {
+        s_ncnt[0][wv] = nt;
+        s_ncnt[1][wv] = na;
+      }
+      __syncthreads();
+      mx = NormRaw{(int64_t)xt, (int64_t)xa};
+      if (threadIdx.x == 0) {
+        int32_t tt = 0, ta = 0;
+        for (int w = 0; w < kTopWaves; w++) {
+          tt += s_ncnt[0][w];
+          ta += s_ncnt[1][w];
+        }
+        pnorm[4 * j] = mx.tt;
+        pnorm[4 * j + 1] = mx.na;
+        pnorm[4 * j + 2] = tt;
+        pnorm[4 * j + 3] = ta;
+      }
+    }
+#pragma unroll 1
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+      uint64_t kk = 0;
+      {
+        NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
+        ov(r);
+        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
+      }
+      nfeas += kk != 0;
+      a[3] = umax64(a[3], kk);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+    }
+  }
+
 template <bool FAST, int kTopThreads>
 __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
@@ -329,7 +419,6 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   const int32_t j = blockIdx.x;
   const int32_t pi = base + j;
   if (pi >= min(st->end, base + kBatchPods)) return;        // block-uniform
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const ksim_pod& p = P.pods[pi];
   const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
   const int64_t seq = st->pod_seq + j;
@@ -369,58 +458,8 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
       }
     }
   }
-  if constexpr (!FAST) {                      // the generic loop is not compiled into FAST kernels
-    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
-    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
-    // nodes (P100: every feasible node is scored), the keys then carry the
-    // normalized scores (norm_part)
-    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
-    NormRaw mx{0, 0};
-    if (normv) {
-      __shared__ uint64_t s_nmax[2][kTopWaves];
-      uint64_t xt = 0, xa = 0;                   // raw scores are >= 0
-#pragma unroll 1
-      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
-        const NodeRow r = load_row(c, node);
-        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
-          const NormRaw v = norm_raw(c, P, p, r);
-          xt = umax64(xt, (uint64_t)v.tt);
-          xa = umax64(xa, (uint64_t)v.na);
-        }
-      }
-      xt = wave_max_u64_dpp(xt);
-      xa = wave_max_u64_dpp(xa);
-      if (lane == 0) {
-        s_nmax[0][wv] = xt;
-        s_nmax[1][wv] = xa;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < kTopWaves; w++) {
-        xt = umax64(xt, s_nmax[0][w]);
-        xa = umax64(xa, s_nmax[1][w]);
-      }
-      mx = NormRaw{(int64_t)xt, (int64_t)xa};
-      if (threadIdx.x == 0) {
-        pnorm[2 * j] = mx.tt;
-        pnorm[2 * j + 1] = mx.na;
-      }
-    }
-#pragma unroll 1
-    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
-      uint64_t kk = 0;
-      {
-        const NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
-        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
-        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
-      }
-      nfeas += kk != 0;
-      a[3] = umax64(a[3], kk);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
-    }
-  }
+  if constexpr (!FAST)                        // the generic loop is not compiled into FAST kernels
+    generic_keys<kTopThreads>(c, P, prof, bp, p, pi, j, seq, trivial, pnorm, a, nfeas, [](NodeRow&) {});
   top_finish<kTopThreads>(a, nfeas, j, topk, topk_cnt, topk_complete, xsend);
 }
 
@@ -823,9 +862,10 @@ __device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
 
 // Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
 // FAST with pj / pk: pod j's and pod k's fields loaded by the caller.
-// Generic runs also flag pod j in pinv[j] when a node that held one of its
-// normalization maxima (kPodNormVaries) left its feasible set: its S0 keys
-// no longer hold, and the batch commits only the pods before it.
+// Generic runs also flag pod j in pinv[j] when every S0-feasible node that
+// held one of its normalization maxima (kPodNormVaries) has left its feasible
+// set: the maximum, and so its S0 keys, no longer hold, and the batch commits
+// only the pods before it.
 template <bool FAST>
 __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                             const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
@@ -845,7 +885,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
     return;
   }
   uint64_t v = 0;
-  bool inv = false;
+  bool lost_t = false, lost_a = false;               // guess k held a maximum of pod j and left its feasible set
   if (k < j) {
     const int32_t local = gk ? key_node(gk) - c.base : -1;
     if (local >= 0 && local < c.n) {
@@ -864,30 +904,39 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
         row_add_pod(r, P.pods[base + k], 1);
         if (sp) v = dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base);
         if (normv && (v || feas0)) {
-          const NormRaw mx{pnorm[2 * j], pnorm[2 * j + 1]};
+          const NormRaw mx{pnorm[4 * j], pnorm[4 * j + 1]};
           const NormRaw x = norm_raw(c, P, p, r);
-          if (v) v += (uint64_t)norm_part(bp, x, mx) << 44;
-          else inv = (mx.tt > 0 && x.tt == mx.tt) || (mx.na > 0 && x.na == mx.na);
+          if (v) {
+            v += (uint64_t)norm_part(bp, x, mx) << 44;
+          } else {
+            lost_t = mx.tt > 0 && x.tt == mx.tt;
+            lost_a = mx.na > 0 && x.na == mx.na;
+          }
         }
       }
     }
   }
   v = wave_max_u64_dpp(v);
   if (lane == 0) s_wmax[wave] = v;
-  if (!FAST) {
-    const uint64_t b = __ballot(inv);
-    if (lane == 0) s_winv[wave] = b != 0;
+  if (!FAST) {                                       // holders lost per wave: TaintToleration | NodeAffinity << 16
+    const int32_t nt = __popcll(__ballot(lost_t)), na = __popcll(__ballot(lost_a));
+    if (lane == 0) s_winv[wave] = nt | (na << 16);
   }
   __syncthreads();
   if (tid == 0) {
     uint64_t m = 0;
-    int32_t any = 0;
+    int32_t lt = 0, la = 0;
     for (int w = 0; w < kBatchPods / 64; w++) {
       m = umax64(m, s_wmax[w]);
-      if (!FAST) any |= s_winv[w];
+      if (!FAST) {
+        lt += s_winv[w] & 0xffff;
+        la += s_winv[w] >> 16;
+      }
     }
     pmax[j] = m;
-    if (!FAST) pinv[j] = any;
+    // a maximum of pod j changes only once every S0-feasible node holding it
+    // has left its feasible set (binds only shrink it; the raw scores are static)
+    if (!FAST) pinv[j] = (lt > 0 && lt >= pnorm[4 * j + 2]) || (la > 0 && la >= pnorm[4 * j + 3]);
   }
 }
 
@@ -1021,15 +1070,23 @@ __device__ __forceinline__ uint32_t lazy_hash(int32_t node) {
   return ((uint32_t)node * 2654435761u) >> (32 - kLazyHashBits);
 }
 
-template <bool FLUSH>
-__global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
+// FAST = false: generic pods (static filters, per-node normalized scores; no
+// scalar requests, no class adds), the keys of generic_keys with the overlay;
+// batch i-1's chain also ends before its first pinv pod (batch_commit).
+// (512 threads: the generic loop's registers)
+constexpr int lazy_threads(bool fast) { return fast ? 1024 : 512; }
+
+template <bool FLUSH, bool FAST = true>
+__global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
                                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
                                                            int32_t* __restrict__ topk_complete,
                                                            int32_t* __restrict__ chosen_out,
-                                                           uint64_t* __restrict__ xsend) {
-  constexpr int kThreads = 1024;
+                                                           uint64_t* __restrict__ xsend,
+                                                           int64_t* __restrict__ pnorm = nullptr) {
+  constexpr int kThreads = lazy_threads(FAST);
+  static_assert(kThreads >= kBatchPods, "one thread per batch entry");
   __shared__ ResCols s_rq[kBatchPods];          // batch i-1's pod requests, then each bound node's delta
   __shared__ int32_t s_hkey[kLazyHash];         // overlay hash: local node or -1
   __shared__ int16_t s_hval[kLazyHash];         // ... its entry
@@ -1051,7 +1108,16 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   const int nwords = (c.n + 31) >> 5;
   for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
   for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
-  const int32_t nchain = e1 > 0 ? e1 : 0;      // -1: no batch i-1 (run start, a flush, past the end)
+  int32_t nchain = e1 > 0 ? e1 : 0;            // -1: no batch i-1 (run start, a flush, past the end)
+  if constexpr (!FAST) {                       // the chain ends before the first pinv pod
+    const int32_t inv = tid < nchain ? L.inv1[tid] : 0;
+    if (tid == 0) s_istar = nchain;
+    __syncthreads();
+    block_first_min(&s_istar, tid < nchain && inv);
+    __syncthreads();
+    nchain = s_istar;
+    __syncthreads();                           // every read of s_istar before it is reset below
+  }
   if (tid == 0) {
     s_istar = nchain;
     s_inode = -1;
@@ -1075,7 +1141,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   const int32_t pi = base + b;
   const bool live = !FLUSH && pi < min(end, base + kBatchPods);   // block-uniform
   ksim_pod pf;
-  if (live) pf = fast_pod_fields(P.pods[pi]);
+  if (FAST && live) pf = fast_pod_fields(P.pods[pi]);
   __syncthreads();
   const int32_t inode = s_inode;
   // entry tid < i*: its guessed node takes pod tid, and pod i* when i* chose it
@@ -1171,11 +1237,26 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     materialize();
     return;
   }
-  // pod b of batch i against S_i (k_batch_top's FAST loop with the overlay)
-  const FastProg bq = fast_prog(*bp_p);
-  const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
+  // pod b of batch i against S_i (k_batch_top's loops with the overlay)
   uint64_t a[kTileCand] = {0, 0, 0, 0};
   int32_t nfeas = 0;
+  if constexpr (!FAST) {
+    generic_keys<kThreads>(c, P, *prof_p, *bp_p, P.pods[pi], pi, b, seq0 + committed + b,
+                           (P.bflags[pi] & kBatchStaticTrivial) != 0, pnorm, a, nfeas, [&](NodeRow& r) {
+                             const ResCols d = delta(r.node);
+                             r.req_cpu += d.cpu;
+                             r.req_mem += d.mem;
+                             r.req_eph += d.eph;
+                             r.nz_cpu += d.nzc;
+                             r.nz_mem += d.nzm;
+                             r.num_pods += d.pods;
+                           });
+    materialize();
+    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
+    return;
+  }
+  const FastProg bq = fast_prog(*bp_p);
+  const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
 #pragma unroll 1
   for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
 #if KSIM_TOP_OFF32
@@ -1209,12 +1290,22 @@ const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
   const LaunchArgs& a = z.a;
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, a.chosen, nullptr);
+  if (a.fast)
+    k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                               a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
+  else
+    k_batch_top_commit<false, false><<<kBatchPods, lazy_threads(false), 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                      a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                      nullptr, a.s.pnorm);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
-                                                                            a.s.topk_cnt, a.s.topk_complete, z.gkey,
-                                                                            z.cend, z.pmax, a.s.pnorm, a.s.pinv);
+  if (a.fast)
+    k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
+        a.s.pinv);
+  else
+    k_batch_chain_pairs<false, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
+        z.inv);
   if (evs) (void)hipEventRecord(evs[2], stream);
   return 0x3u;
 }
@@ -1245,8 +1336,13 @@ void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream
 
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
   const LaunchArgs& a = z.a;
-  k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                            a.s.topk_complete, a.chosen, nullptr);
+  if (a.fast)
+    k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                              a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
+  else
+    k_batch_top_commit<true, false><<<kBatchPods, lazy_threads(false), 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                     a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                     nullptr, a.s.pnorm);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.

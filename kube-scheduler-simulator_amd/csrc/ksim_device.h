@@ -238,7 +238,8 @@ struct DevScratch {
   uint64_t* gkey;        // batch path: [B] key of each pod's greedy guess (0: none)
   int32_t* chain_end;    // batch path: pods covered by the chain (an exhausted list cuts it)
   uint64_t* pmax;        // batch path: [B] best key of pod j over the guesses of pods k < j
-  int64_t* pnorm;        // batch path: [B][2] kPodNormVaries pods' S0 maxima (TaintToleration, NodeAffinity raw)
+  int64_t* pnorm;        // batch path: [B][4] kPodNormVaries pods' S0 maxima (TaintToleration, NodeAffinity raw)
+                         // and the S0-feasible nodes holding each
   // topology batch path (ksim_tbatch.hip), per pod j of the batch: [kTbPods][n] slices
   uint8_t* tb_fail;      // filter result per node
   uint8_t* tb_ign;       // PodTopologySpread IgnoredNodes

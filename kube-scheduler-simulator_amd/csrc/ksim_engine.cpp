@@ -119,6 +119,7 @@ struct ksim_handle {
                                         // read from persistent tables (kPlanPtab)
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<uint8_t> noadd;           // per loaded pod: no count-class adds (deferred-commit batches)
+  std::vector<uint8_t> noscalar;        // ... and no scalar requests (generic deferred-commit batches)
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
   std::vector<int32_t> tlen;            // per loaded pod: topology batch run length from it (tbatch_runs)
@@ -173,8 +174,10 @@ struct ksim_handle {
   DevState* lazy_st1 = nullptr;
   uint64_t *lazy_g = nullptr, *lazy_m = nullptr;   // [kLazySlots][kBatchPods]
   int32_t* lazy_e = nullptr;                        // [kLazySlots] prefix length, -1 = empty slot
+  int32_t* lazy_inv = nullptr;          // generic P100: [kLazySlots][kBatchPods] pinv flags
   int32_t *lazy_ab = nullptr, *lazy_aw = nullptr;   // ADAPT: [kLazySlots][kBatchPods] broken flags, [..][2 B] windows
   hipGraphExec_t graph_lazy = nullptr;
+  hipGraphExec_t graph_lazy_gen = nullptr;
   hipGraphExec_t graph_lazy_adapt = nullptr;
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
   // the global bitmap (allocated at the first such run)
@@ -264,8 +267,9 @@ void drop_graphs(ksim_handle* h) {
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
+  if (h->graph_lazy_gen) (void)hipGraphExecDestroy(h->graph_lazy_gen);
   if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
-  h->graph_lazy_adapt = nullptr;
+  h->graph_lazy_adapt = h->graph_lazy_gen = nullptr;
   h->graph_batch_fast = nullptr;
   h->graph_batch = nullptr;
   h->graph_tbatch = nullptr;
@@ -594,11 +598,26 @@ bool lazy_enabled() {
   return !off;
 }
 
+// KSIM_LAZY_GEN=1: generic runs take the deferred commit too (opt-in: on
+// config 1 scaled it measured 46.8 against 35.3 ms per step for the three
+// launches, profiles/r03/ab_lazy_gen; the generic key loop with the overlay
+// holds 205 VGPRs at 512 threads)
+bool lazy_gen_enabled() {
+  static const bool on = getenv("KSIM_LAZY_GEN") != nullptr;
+  return on;
+}
+
 // A FAST run [a, b) on an unsharded handle whose pods add to no count class
 // (the overlay carries the resource columns only), on a cluster the overlay's
-// LDS node bitmap covers.
-bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b) {
+// LDS node bitmap covers.  Generic runs (fast false): unsharded P100 handles,
+// pods without scalar requests (k_batch_top_commit<.., false>).
+bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b, bool fast) {
   if (!lazy_enabled() || batch_ab_forms()) return false;
+  if (!fast) {
+    if (!lazy_gen_enabled() || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
+    for (int32_t i = a; i < b; i++)
+      if (!h->noscalar[i]) return false;
+  }
   // ADAPT runs whole on a replica (no exchange); replicated P100 batches take
   // shard_run_lazy (lazy_rep_ok)
   if (adapt_mode(h) ? (is_sharded(h) && !h->replicated) : (is_sharded(h) || h->replicated)) return false;
@@ -613,7 +632,8 @@ int alloc_lazy(ksim_handle* h) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
   if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
-  h->graph_lazy = h->graph_lazy_adapt = nullptr;
+  if (h->graph_lazy_gen) (void)hipGraphExecDestroy(h->graph_lazy_gen);
+  h->graph_lazy = h->graph_lazy_adapt = h->graph_lazy_gen = nullptr;
   free_bufs(h->lazy_bufs);
   h->lazy_n = -1;
   const size_t n = (size_t)h->dc.n;
@@ -639,6 +659,8 @@ int alloc_lazy(ksim_handle* h) {
   h->lazy_ab = (int32_t*)p;
   if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
   h->lazy_aw = (int32_t*)p;
+  if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
+  h->lazy_inv = (int32_t*)p;
   h->lazy_n = h->dc.n;
   return KSIM_OK;
 }
@@ -675,6 +697,7 @@ LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
   z.step.g2 = h->lazy_g + (size_t)q2 * kBatchPods;
   z.step.e2 = h->lazy_e + q2;
   z.step.e_self = h->lazy_e + q;
+  z.step.inv1 = h->lazy_inv + (size_t)q1 * kBatchPods;
   z.st = st[p];
   z.gkey = h->lazy_g + (size_t)q * kBatchPods;
   z.pmax = h->lazy_m + (size_t)q * kBatchPods;
@@ -683,6 +706,7 @@ LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
   z.w1 = h->lazy_aw + (size_t)q1 * 2 * kBatchPods;
   z.abroken = h->lazy_ab + (size_t)q * kBatchPods;
   z.awin = h->lazy_aw + (size_t)q * 2 * kBatchPods;
+  z.inv = h->lazy_inv + (size_t)q * kBatchPods;
   return z;
 }
 
@@ -726,7 +750,7 @@ int read_state_at(ksim_handle* h, const DevState* src, DevState& st) {
   return KSIM_OK;
 }
 
-// A FAST run of pods [a, b) as deferred-commit batches (lazy_ok; set_run done).
+// A run of pods [a, b) as deferred-commit batches (lazy_ok; set_run done).
 // Batch i commits batch i - 1; each stretch of launches ends with a flush, whose
 // state tells the host where the run stands.  A batch commits 1..kBatchPods
 // pods, so ceil(left / kBatchPods) batches never start past the end.
@@ -742,7 +766,7 @@ void lazy_flush(const ksim_handle* h, const LazyBatch& z, hipStream_t stream) {
 int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   int rc;
   if ((rc = lazy_begin(h))) return rc;
-  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt : h->graph_lazy;
+  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt : la.fast ? h->graph_lazy : h->graph_lazy_gen;
   if (!graph) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     hipGraph_t g = nullptr;
@@ -807,7 +831,7 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
   if (topo) return run_tbatch(h, a, b, la);
   // the FAST evaluation kernel when every pod of the run is trivial with cpu/memory scoring
   la.fast = run_fast(h, a, b);
-  if (la.fast && lazy_ok(h, a, b)) return run_lazy(h, a, b, la);
+  if (lazy_ok(h, a, b, la.fast)) return run_lazy(h, a, b, la);
   hipGraphExec_t& gb = la.fast ? h->graph_batch_fast : h->graph_batch;
   if (!gb && (rc = capture(h, true, false, &gb, la.fast))) return rc;
   // every batch commits between 1 and kBatchPods pods: a graph of
@@ -1752,7 +1776,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.chain_end, int32_t*, 4);
   SCR(s.pmax, uint64_t*, 8 * 2 * (size_t)kBatchPods);   // [M | sharded ADAPT broken flags]
-  SCR(s.pnorm, int64_t*, 8 * 2 * (size_t)kBatchPods);
+  SCR(s.pnorm, int64_t*, 8 * 4 * (size_t)kBatchPods);
   const size_t NT = N <= (size_t)kTbMaxBlocks * 256 ? N : 0;   // topology batches (tbatch_admit)
   SCR(s.tb_fail, uint8_t*, (size_t)kTbPods * NT);
   SCR(s.tb_ign, uint8_t*, (size_t)kTbPods * NT);
@@ -2569,6 +2593,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   h->xdom_len.assign((size_t)ps->n_pods, 0);
   h->trivial.assign((size_t)ps->n_pods, 0);
   h->noadd.assign((size_t)ps->n_pods, 0);
+  h->noscalar.assign((size_t)ps->n_pods, 0);
   h->hard_small.assign((size_t)ps->n_pods, 1);
   h->soft_le1.assign((size_t)ps->n_pods, 1);
   h->xreg_len.assign((size_t)ps->n_pods, 0);
@@ -2598,6 +2623,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     if (static_trivial(h, ps->pods[i]) && batchable[i] != 2) bf[i] |= kBatchStaticTrivial;
     h->trivial[i] = (bf[i] & kBatchStaticTrivial) ? 1 : 0;
     h->noadd[i] = ps->pods[i].add_count == 0 ? 1 : 0;
+    h->noscalar[i] = (ps->pods[i].flags & KSIM_POD_HAS_SCALAR) == 0 ? 1 : 0;
   }
   std::vector<PodPlan> plans((size_t)ps->n_pods);
   for (int32_t i = 0; i < ps->n_pods; i++) {
@@ -2879,7 +2905,7 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
   a.fuse_min = !batch && h->topo[first] && h->hard_small[first];
   a.fuse_ext = !batch && h->soft_le1[first];
   a.ptab = !batch && h->topo[first] == 2;
-  if (batch && a.fast && lazy_ok(h, first, end)) {
+  if (batch && a.fast && lazy_ok(h, first, end, true)) {
     // the deferred-commit evaluation launch as the run issues it: batch 0 of
     // the run (both launches), then batch 1's k_batch_top_commit repeated
     // (idempotent: it reads X[0], st[0] and slot 0, and writes X[1], st[1],
@@ -2966,7 +2992,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
                      : adapt ? kKernelsPerCycle + kKernelsPerBatch
                      : batch ? kKernelsPerCycle : 0;
     if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
-    if (batch && !tb && a.fast && lazy_ok(h, lo, hi)) {
+    if (batch && !tb && a.fast && lazy_ok(h, lo, hi, true)) {
       // deferred-commit batches: two (P100) or three to four (ADAPT) launches
       // each, a flush (untimed) before every state read
       const int lper = adapt ? kKernelsPerLazyAdapt : kKernelsPerLazy;

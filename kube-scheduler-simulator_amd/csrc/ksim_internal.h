@@ -103,6 +103,7 @@ struct LazyStep {
   const uint64_t* g1; const uint64_t* m1; const int32_t* e1;   // batch i-1's slot: guesses, pair maxima, prefix
   const uint64_t* g2; const int32_t* e2;                       // batch i-2's slot: guesses, prefix
   int32_t* e_self;                                 // batch i's slot (a flush marks it empty: -1)
+  const int32_t* inv1;                             // generic runs: batch i-1's pinv flags (kPodNormVaries)
 };
 struct LazyBatch {
   LaunchArgs a;        // a.c: static columns + X[p ^ 1]
@@ -117,6 +118,7 @@ struct LazyBatch {
   const int32_t* w1;
   int32_t* abroken;
   int32_t* awin;
+  int32_t* inv;        // generic P100 runs: batch i's pinv flags
 };
 constexpr int kKernelsPerLazy = 2;
 extern const char* const kLazyKernelNames[kKernelsPerLazy];

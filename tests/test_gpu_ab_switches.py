@@ -2,7 +2,8 @@
 (KSIM_CHAIN_SEPARATE: the chain as its own one-block launch ahead of the
 pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch;
 KSIM_NO_LAZY: the three-launch P100 batch, commit as its own launch, instead
-of the deferred commit).  They
+of the deferred commit; KSIM_LAZY_GEN: the deferred commit for generic pods
+too -- config 1's taints, tolerations and node affinity).  They
 are read once per process, so each runs in one child process that schedules
 P100 and ADAPT batches and checks them against the oracle (the default forms
 run in every other GPU test)."""
@@ -34,11 +35,25 @@ for pct, n_nodes, n_pods in ((100, 2000, 3000), (0, 2000, 3000), (0, 300, 300 * 
     assert st.evals == ost.evals and eng.next_start == ora.next_start
     assert st.batches > 0
     eng.close()
+from ksim.encode import encode_cluster, encode_pods
+nodes, objs = gen.config1_objects(n_nodes=1200, n_pods=4000)
+cluster, _ = encode_cluster(nodes)
+pods = encode_pods(cluster, objs)
+prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=100))
+eng = Engine(0)
+eng.set_profile(prof)
+eng.set_cluster(cluster)
+chosen, st = eng.schedule_batch(pods)
+ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+np.testing.assert_array_equal(chosen, ochosen)
+assert st.evals == ost.evals and st.perpod_cycles == 0 and st.batches > 0
+eng.close()
 print("ok")
 '''
 
 
-@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE", "KSIM_NO_LAZY"])
+@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE", "KSIM_NO_LAZY",
+                                    "KSIM_LAZY_GEN"])
 def test_separate_launch_forms_vs_oracle(switch):
     env = dict(os.environ)
     env[switch] = "1"

@@ -118,8 +118,6 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
   }
 }
 
-__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g);
-
 // ---- k_batch_top: evaluation and the pod's top-T in one launch -------------------
 // One block per pod of the batch (kTopThreads threads, kTopWaves waves: two per
 // SIMD when every CU holds one block), the nodes strided over its lanes.  Each
@@ -312,6 +310,80 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   }
 }
 
+// The request fields the FAST pair key reads (pod j's and the bound pod k's),
+// as a local ksim_pod: a caller can load them before it knows the guesses.
+__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
+  ksim_pod p;
+  p.req_cpu = g.req_cpu;
+  p.req_mem = g.req_mem;
+  p.req_eph = g.req_eph;
+  p.nz_cpu = g.nz_cpu;
+  p.nz_mem = g.nz_mem;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) p.scalar_req[k] = 0;   // trivial pods: no scalar requests
+  return p;
+}
+
+// A lane's DefaultNormalizeScore maxima of a kPodNormVaries pod's raw
+// TaintToleration / NodeAffinity scores over its S0-feasible nodes, and how
+// many of its nodes hold each (raw scores are >= 0).
+struct NormAcc {
+  uint64_t lt = 0, la = 0;
+  int32_t ct = 0, ca = 0;
+  __device__ __forceinline__ void take(const NormRaw& v) {
+    ct = (uint64_t)v.tt > lt ? 1 : ct + ((uint64_t)v.tt == lt ? 1 : 0);
+    lt = umax64(lt, (uint64_t)v.tt);
+    ca = (uint64_t)v.na > la ? 1 : ca + ((uint64_t)v.na == la ? 1 : 0);
+    la = umax64(la, (uint64_t)v.na);
+  }
+};
+
+// The block's maxima (returned to every thread) and their holder counts:
+// thread 0 writes pnorm[4 j .. 4 j + 3] (the batch keeps pod j until every
+// holder of a maximum has left its feasible set, pairs_block).
+template <int kTopThreads>
+__device__ __forceinline__ NormRaw norm_maxima(const NormAcc& n, int64_t* __restrict__ pnorm, int32_t j) {
+  constexpr int kTopWaves = kTopThreads / 64;
+  __shared__ uint64_t s_nmax[2][kTopWaves];
+  __shared__ int32_t s_ncnt[2][kTopWaves];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t xt = wave_max_u64_dpp(n.lt), xa = wave_max_u64_dpp(n.la);
+  if (lane == 0) {
+    s_nmax[0][wv] = xt;
+    s_nmax[1][wv] = xa;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kTopWaves; w++) {
+    xt = umax64(xt, s_nmax[0][w]);
+    xa = umax64(xa, s_nmax[1][w]);
+  }
+  int32_t nt = n.lt == xt ? n.ct : 0, na = n.la == xa ? n.ca : 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    nt += __shfl_xor(nt, d, 64);
+    na += __shfl_xor(na, d, 64);
+  }
+  if (lane == 0) {
+    s_ncnt[0][wv] = nt;
+    s_ncnt[1][wv] = na;
+  }
+  __syncthreads();
+  const NormRaw mx{(int64_t)xt, (int64_t)xa};
+  if (threadIdx.x == 0) {
+    int32_t tt = 0, ta = 0;
+    for (int w = 0; w < kTopWaves; w++) {
+      tt += s_ncnt[0][w];
+      ta += s_ncnt[1][w];
+    }
+    pnorm[4 * j] = mx.tt;
+    pnorm[4 * j + 1] = mx.na;
+    pnorm[4 * j + 2] = tt;
+    pnorm[4 * j + 3] = ta;
+  }
+  return mx;
+}
+
 // The generic (non-FAST) keys of pod j = pi - cursor over the block's nodes:
 // static filters, the resource key, and for kPodNormVaries pods the
 // normalized TaintToleration / NodeAffinity parts.  ov(row) adds whatever the
@@ -322,87 +394,131 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
                                              const BatchProg& bp, const ksim_pod& p, int32_t pi, int32_t j,
                                              int64_t seq, bool trivial, int64_t* __restrict__ pnorm,
                                              uint64_t (&a)[kTileCand], int32_t& nfeas, Ov&& ov) {
-  constexpr int kTopWaves = kTopThreads / 64;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
-    // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
-    // nodes (P100: every feasible node is scored), the keys then carry the
-    // normalized scores (norm_part)
-    const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
-    NormRaw mx{0, 0};
-    if (normv) {
-      // the maxima and how many S0-feasible nodes hold each: the batch keeps
-      // pod j until every holder of a maximum has left its feasible set
-      // (pairs_block), not at the first one
-      __shared__ uint64_t s_nmax[2][kTopWaves];
-      __shared__ int32_t s_ncnt[2][kTopWaves];
-      uint64_t lt = 0, la = 0;                   // this lane's maxima (raw scores are >= 0) ...
-      int32_t ct = 0, ca = 0;                    // ... and its nodes holding them
+  // kPodNormVaries: a first pass takes DefaultNormalizeScore's maxima of the
+  // pod's TaintToleration / NodeAffinity raw scores over its S0-feasible
+  // nodes (P100: every feasible node is scored), the keys then carry the
+  // normalized scores (norm_part)
+  const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+  // a static class (DevPods::stab): the static verdict and raw scores are one
+  // word per node, the row is the resource columns, and on a run_fast cluster
+  // the key takes the FAST arithmetic (block-uniform)
+  const int32_t scls = P.stab ? P.sclass[pi] : -1;
+  const uint64_t* srow = scls >= 0 ? P.stab + (size_t)scls * c.n : nullptr;
+  const bool fk = srow && P.stab_fast;
+  const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
+  auto tkey = [&](const NodeRow& r) -> uint64_t {   // table classes: the key of a row that passed
+    if (fk) {
+      const FastProg bq = fast_prog(bp);
+      const uint32_t o8 = (uint32_t)r.node << 3;
+      return dyn_key_fast(bq, fast_pod_fields(p), r, ld_off(c.inv_cpu, o8), ld_off(c.inv_mem, o8), hseed,
+                          c.base + r.node);
+    }
+    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+  };
+  NormRaw mx{0, 0};
+  if (normv) {
+    NormAcc acc;
+    if (srow) {
+#pragma unroll 1
+      for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+        NodeRow r = load_res_row(c, node);
+        ov(r);
+        const uint64_t w = srow[node];
+        if (stab_pass(w) && tkey(r)) acc.take(stab_raw(w, P, p));
+      }
+    } else {
 #pragma unroll 1
       for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
         NodeRow r = load_row(c, node);
         ov(r);
-        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base)) {
-          const NormRaw v = norm_raw(c, P, p, r);
-          ct = (uint64_t)v.tt > lt ? 1 : ct + ((uint64_t)v.tt == lt ? 1 : 0);
-          lt = umax64(lt, (uint64_t)v.tt);
-          ca = (uint64_t)v.na > la ? 1 : ca + ((uint64_t)v.na == la ? 1 : 0);
-          la = umax64(la, (uint64_t)v.na);
-        }
-      }
-      uint64_t xt = wave_max_u64_dpp(lt), xa = wave_max_u64_dpp(la);
-      if (lane == 0) {
-        s_nmax[0][wv] = xt;
-        s_nmax[1][wv] = xa;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < kTopWaves; w++) {
-        xt = umax64(xt, s_nmax[0][w]);
-        xa = umax64(xa, s_nmax[1][w]);
-      }
-      int32_t nt = lt == xt ? ct : 0, na = la == xa ? ca : 0;
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        nt += __shfl_xor(nt, d, 64);
-        na += __shfl_xor(na, d, 64);
-      }
-      if (lane == 0) {
-        s_ncnt[0][wv] = nt;
-        s_ncnt[1][wv] = na;
-      }
-      __syncthreads();
-      mx = NormRaw{(int64_t)xt, (int64_t)xa};
-      if (threadIdx.x == 0) {
-        int32_t tt = 0, ta = 0;
-        for (int w = 0; w < kTopWaves; w++) {
-          tt += s_ncnt[0][w];
-          ta += s_ncnt[1][w];
-        }
-        pnorm[4 * j] = mx.tt;
-        pnorm[4 * j + 1] = mx.na;
-        pnorm[4 * j + 2] = tt;
-        pnorm[4 * j + 3] = ta;
+        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base))
+          acc.take(norm_raw(c, P, p, r));
       }
     }
+    mx = norm_maxima<kTopThreads>(acc, pnorm, j);
+  }
+  auto insert = [&](uint64_t kk) {
+    nfeas += kk != 0;
+    a[3] = umax64(a[3], kk);
+    cswap_desc(a[2], a[3]);
+    cswap_desc(a[1], a[2]);
+    cswap_desc(a[0], a[1]);
+  };
+  if (srow) {
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
-      uint64_t kk = 0;
-      {
-        NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
-        ov(r);
-        if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
-        if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
-      }
-      nfeas += kk != 0;
-      a[3] = umax64(a[3], kk);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
+      NodeRow r = load_res_row(c, node);
+      ov(r);
+      const uint64_t w = srow[node];
+      uint64_t kk = stab_pass(w) ? tkey(r) : 0;
+      if (normv && kk) kk += (uint64_t)norm_part(bp, stab_raw(w, P, p), mx) << 44;
+      insert(kk);
     }
+    return;
   }
+#pragma unroll 1
+  for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+    uint64_t kk = 0;
+    {
+      NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
+      ov(r);
+      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+      if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
+    }
+    insert(kk);
+  }
+}
 
-template <bool FAST, int kTopThreads>
+// The FAST keys of a static class's pod (STAB runs: every pod of the run has
+// a class, the cluster meets run_fast's conditions): the FAST key, masked by
+// the class's static verdict, plus for kPodNormVaries pods the normalized
+// part (norm_part_fast) over the maxima of a first pass.  ov(row): as for
+// generic_keys.
+template <int kTopThreads, typename Ov>
+__device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPods& P, const BatchProg& bp,
+                                               const FastProg& bq, const ksim_pod& pf, int32_t pi, int32_t j,
+                                               uint64_t hseed, int64_t* __restrict__ pnorm, uint64_t (&a)[kTileCand],
+                                               int32_t& nfeas, Ov&& ov) {
+  const uint64_t* srow = P.stab + (size_t)P.sclass[pi] * c.n;
+  const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+  const ksim_pod& pp = P.pods[pi];                           // its preferred terms (stab_raw)
+  auto key = [&](int32_t node, uint64_t& w) -> uint64_t {
+    const uint32_t o8 = (uint32_t)node << 3;
+    NodeRow r = load_res_row_off(c, node);
+    const double ic = ld_off(c.inv_cpu, o8), im = ld_off(c.inv_mem, o8);
+    w = ld_off(srow, o8);
+    ov(r);
+    const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+    return stab_pass(w) ? k : 0;
+  };
+  NormRaw mx{0, 0};
+  double y_tt = 0, y_na = 0;
+  if (normv) {
+    NormAcc acc;
+#pragma unroll 1
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+      uint64_t w;
+      if (key(node, w)) acc.take(stab_raw(w, P, pp));
+    }
+    mx = norm_maxima<kTopThreads>(acc, pnorm, j);
+    y_tt = recip_or_zero(mx.tt);
+    y_na = recip_or_zero(mx.na);
+  }
+#pragma unroll 1
+  for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+    uint64_t w;
+    uint64_t k = key(node, w);
+    if (normv && k) k += (uint64_t)norm_part_fast(bp, stab_raw(w, P, pp), mx, y_tt, y_na) << 44;
+    nfeas += k != 0;
+    a[3] = umax64(a[3], k);
+    cswap_desc(a[2], a[3]);
+    cswap_desc(a[1], a[2]);
+    cswap_desc(a[0], a[1]);
+  }
+}
+
+// STAB (FAST only): a static-class run (stab_fast_keys).
+template <bool FAST, int kTopThreads, bool STAB = false>
 __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p,
@@ -430,6 +546,9 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     // program and the pod's request fields, loaded once
     const FastProg bq = fast_prog(bp);
     const ksim_pod pf = fast_pod_fields(p);
+    if constexpr (STAB) {
+      stab_fast_keys<kTopThreads>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, nfeas, [](NodeRow&) {});
+    } else {
     // kTopStep nodes per step as independent chains (every row loaded up front)
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
@@ -456,6 +575,7 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
         cswap_desc(a[1], a[2]);
         cswap_desc(a[0], a[1]);
       }
+    }
     }
   }
   if constexpr (!FAST)                        // the generic loop is not compiled into FAST kernels
@@ -846,27 +966,13 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __re
   if (threadIdx.x == 0) *chain_end = nchain;
 }
 
-// The request fields the FAST pair key reads (pod j's and the bound pod k's),
-// as a local ksim_pod: a caller can load them before it knows the guesses.
-__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
-  ksim_pod p;
-  p.req_cpu = g.req_cpu;
-  p.req_mem = g.req_mem;
-  p.req_eph = g.req_eph;
-  p.nz_cpu = g.nz_cpu;
-  p.nz_mem = g.nz_mem;
-#pragma unroll
-  for (int k = 0; k < KSIM_MAX_SCALAR; k++) p.scalar_req[k] = 0;   // trivial pods: no scalar requests
-  return p;
-}
-
 // Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
 // FAST with pj / pk: pod j's and pod k's fields loaded by the caller.
 // Generic runs also flag pod j in pinv[j] when every S0-feasible node that
 // held one of its normalization maxima (kPodNormVaries) has left its feasible
 // set: the maximum, and so its S0 keys, no longer hold, and the batch commits
 // only the pods before it.
-template <bool FAST>
+template <bool FAST, bool STAB = false>
 __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                             const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
                                             int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax,
@@ -877,10 +983,11 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
   const int j = blockIdx.x, k = tid;
   const int32_t base = st->cursor;
   const int64_t seq0 = st->pod_seq;
+  constexpr bool kInv = !FAST || STAB;               // pinv flags (kPodNormVaries pods)
   if (j >= nchain) {                                 // block-uniform
     if (tid == 0) {
       pmax[j] = 0;
-      if (!FAST) pinv[j] = 0;
+      if (kInv) pinv[j] = 0;
     }
     return;
   }
@@ -890,22 +997,50 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
     const int32_t local = gk ? key_node(gk) - c.base : -1;
     if (local >= 0 && local < c.n) {
       const ksim_pod& p = P.pods[base + j];
-      if constexpr (FAST) {
+      if constexpr (FAST && STAB) {
+        const int32_t bf = P.bflags[base + j];
+        const bool normv = (bf & kPodNormVaries) != 0;
+        const uint64_t w = P.stab[(size_t)P.sclass[base + j] * c.n + local];
+        const double ic = c.inv_cpu[local], im = c.inv_mem[local];
+        const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20);
+        NodeRow r = load_res_row(c, local);
+        const bool feas0 = normv && stab_pass(w) && dyn_key_fast(bp, *pj, r, ic, im, hseed, c.base + local) != 0;
+        row_add_pod(r, *pk, 1);
+        v = stab_pass(w) ? dyn_key_fast(bp, *pj, r, ic, im, hseed, c.base + local) : 0;
+        if (normv && (v || feas0)) {
+          const NormRaw mx{pnorm[4 * j], pnorm[4 * j + 1]};
+          if (v) {
+            v += (uint64_t)norm_part_fast(bp, stab_raw(w, P, p), mx, recip_or_zero(mx.tt), recip_or_zero(mx.na)) << 44;
+          } else {
+            const NormRaw x = stab_raw(w, P, p);
+            lost_t = mx.tt > 0 && x.tt == mx.tt;
+            lost_a = mx.na > 0 && x.na == mx.na;
+          }
+        }
+      } else if constexpr (FAST) {
         NodeRow r = load_res_row(c, local);
         row_add_pod(r, pk ? *pk : P.pods[base + k], 1);
         v = dyn_key_fast(bp, pj ? *pj : p, r, c.inv_cpu[local], c.inv_mem[local],
                          prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
       } else {
-        NodeRow r = load_row(c, local);
         const int32_t bf = P.bflags[base + j];
         const bool normv = (bf & kPodNormVaries) != 0;
-        const bool sp = (bf & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r);
-        const bool feas0 = normv && sp && dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base) != 0;   // at S0
+        const int32_t scls = P.stab ? P.sclass[base + j] : -1;   // block-uniform (generic_keys)
+        const uint64_t w = scls >= 0 ? P.stab[(size_t)scls * c.n + local] : 0;
+        NodeRow r = scls >= 0 ? load_res_row(c, local) : load_row(c, local);
+        auto key = [&](const NodeRow& x) -> uint64_t {
+          if (scls >= 0 && P.stab_fast)
+            return dyn_key_fast(bp, fast_pod_fields(p), x, c.inv_cpu[local], c.inv_mem[local],
+                                prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
+          return dyn_key(prof, bp, p, x, c.n_scalar, seq0 + j, c.base);
+        };
+        const bool sp = scls >= 0 ? stab_pass(w) : ((bf & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r));
+        const bool feas0 = normv && sp && key(r) != 0;   // at S0
         row_add_pod(r, P.pods[base + k], 1);
-        if (sp) v = dyn_key(prof, bp, p, r, c.n_scalar, seq0 + j, c.base);
+        if (sp) v = key(r);
         if (normv && (v || feas0)) {
           const NormRaw mx{pnorm[4 * j], pnorm[4 * j + 1]};
-          const NormRaw x = norm_raw(c, P, p, r);
+          const NormRaw x = scls >= 0 ? stab_raw(w, P, p) : norm_raw(c, P, p, r);
           if (v) {
             v += (uint64_t)norm_part(bp, x, mx) << 44;
           } else {
@@ -918,7 +1053,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
   }
   v = wave_max_u64_dpp(v);
   if (lane == 0) s_wmax[wave] = v;
-  if (!FAST) {                                       // holders lost per wave: TaintToleration | NodeAffinity << 16
+  if (kInv) {                                        // holders lost per wave: TaintToleration | NodeAffinity << 16
     const int32_t nt = __popcll(__ballot(lost_t)), na = __popcll(__ballot(lost_a));
     if (lane == 0) s_winv[wave] = nt | (na << 16);
   }
@@ -928,7 +1063,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
     int32_t lt = 0, la = 0;
     for (int w = 0; w < kBatchPods / 64; w++) {
       m = umax64(m, s_wmax[w]);
-      if (!FAST) {
+      if (kInv) {
         lt += s_winv[w] & 0xffff;
         la += s_winv[w] >> 16;
       }
@@ -936,7 +1071,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
     pmax[j] = m;
     // a maximum of pod j changes only once every S0-feasible node holding it
     // has left its feasible set (binds only shrink it; the raw scores are static)
-    if (!FAST) pinv[j] = (lt > 0 && lt >= pnorm[4 * j + 2]) || (la > 0 && la >= pnorm[4 * j + 3]);
+    if (kInv) pinv[j] = (lt > 0 && lt >= pnorm[4 * j + 2]) || (la > 0 && la >= pnorm[4 * j + 3]);
   }
 }
 
@@ -979,7 +1114,7 @@ unsigned long long* cp_clock_buffer() { return nullptr; }
 
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
-template <bool FAST, int NCHUNK = 0, bool LAZY = false>
+template <bool FAST, int NCHUNK = 0, bool LAZY = false, bool STAB = false>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -1025,8 +1160,8 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
     if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
     if (threadIdx.x == 0) *chain_end = nchain;
   }
-  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr, FAST ? &pk : nullptr,
-                    pnorm, pinv, s_winv);
+  pairs_block<FAST, STAB>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr,
+                          FAST ? &pk : nullptr, pnorm, pinv, s_winv);
 #ifdef KSIM_CP_CLOCKS
   if (dbgc && threadIdx.x == 0) atomicAdd(&dbgc[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_in));
 #endif
@@ -1044,6 +1179,26 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_commit(DevCluster c, DevPo
   const int32_t nchain = *chain_end;
   if (min(kBatchPods, st->end - st->cursor) <= 0) return;
   batch_commit(c, P, st, g, m, pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, pinv ? &inv : nullptr);
+}
+
+// ---- static classes (DevPods::stab) ------------------------------------------
+// Row cls of the table: the static verdict and raw normalized scores of the
+// class's representative pod rep[cls] on every node of the snapshot (grid
+// x: nodes, y: classes).  Pure functions of the pod's static fields and the
+// node's flags, taints and labels: built once per (pods, cluster, profile).
+__global__ __launch_bounds__(256) void k_static_table(DevCluster c, DevPods P, const BatchProg* __restrict__ bp_p,
+                                                      const int32_t* __restrict__ rep, uint64_t* __restrict__ stab) {
+  const int32_t node = blockIdx.x * 256 + threadIdx.x;
+  if (node >= c.n) return;
+  const ksim_pod& p = P.pods[rep[blockIdx.y]];
+  const NodeRow r = load_row(c, node);
+  const bool pass = static_filters_pass(c, P, *bp_p, p, r);
+  stab[(size_t)blockIdx.y * c.n + node] = stab_word(pass, count_intolerable_prefer(c, p, r), pref_term_mask(c, P, p, node));
+}
+
+void launch_static_table(const LaunchArgs& a, const int32_t* rep, int32_t n_cls, uint64_t* stab, hipStream_t stream) {
+  if (n_cls <= 0 || a.c.n <= 0) return;
+  k_static_table<<<dim3((a.c.n + 255) / 256, n_cls), 256, 0, stream>>>(a.c, a.P, a.dbp, rep, stab);
 }
 
 // ---- deferred commit: batch i-1's commit inside batch i's evaluation launch -----
@@ -1076,7 +1231,9 @@ __device__ __forceinline__ uint32_t lazy_hash(int32_t node) {
 // (512 threads: the generic loop's registers)
 constexpr int lazy_threads(bool fast) { return fast ? 1024 : 512; }
 
-template <bool FLUSH, bool FAST = true>
+// STAB (FAST only): a static-class run (stab_fast_keys with the overlay; the
+// chain of batch i-1 also ends before its first pinv pod).
+template <bool FLUSH, bool FAST = true, bool STAB = false>
 __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
@@ -1109,7 +1266,7 @@ __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevClus
   for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
   for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
   int32_t nchain = e1 > 0 ? e1 : 0;            // -1: no batch i-1 (run start, a flush, past the end)
-  if constexpr (!FAST) {                       // the chain ends before the first pinv pod
+  if constexpr (!FAST || STAB) {               // the chain ends before the first pinv pod
     const int32_t inv = tid < nchain ? L.inv1[tid] : 0;
     if (tid == 0) s_istar = nchain;
     __syncthreads();
@@ -1257,6 +1414,20 @@ __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevClus
   }
   const FastProg bq = fast_prog(*bp_p);
   const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
+  if constexpr (STAB) {
+    stab_fast_keys<kThreads>(c, P, *bp_p, bq, pf, pi, b, hseed, pnorm, a, nfeas, [&](NodeRow& r) {
+      const ResCols d = delta(r.node);
+      r.req_cpu += d.cpu;
+      r.req_mem += d.mem;
+      r.req_eph += d.eph;
+      r.nz_cpu += d.nzc;
+      r.nz_mem += d.nzm;
+      r.num_pods += d.pods;
+    });
+    materialize();
+    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
+    return;
+  }
 #pragma unroll 1
   for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
 #if KSIM_TOP_OFF32
@@ -1290,7 +1461,11 @@ const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
   const LaunchArgs& a = z.a;
   if (evs) (void)hipEventRecord(evs[0], stream);
-  if (a.fast)
+  if (a.stab)
+    k_batch_top_commit<false, true, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                           a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                           nullptr, a.s.pnorm);
+  else if (a.fast)
     k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
                                                                a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
   else
@@ -1298,7 +1473,11 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
                                                                       a.s.topk_cnt, a.s.topk_complete, a.chosen,
                                                                       nullptr, a.s.pnorm);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  if (a.fast)
+  if (a.stab)
+    k_batch_chain_pairs<true, 0, true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
+        z.inv);
+  else if (a.fast)
     k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(
         z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
         a.s.pinv);
@@ -1336,7 +1515,11 @@ void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream
 
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
   const LaunchArgs& a = z.a;
-  if (a.fast)
+  if (a.stab)
+    k_batch_top_commit<true, true, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                          a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                          nullptr, a.s.pnorm);
+  else if (a.fast)
     k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
                                                               a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
   else
@@ -1430,15 +1613,35 @@ bool batch_ab_forms() {
   return on;
 }
 
-static void launch_top_ns(const LaunchArgs& a, int nch, hipStream_t stream) {
-  if (nch == 4)
-    k_batch_top_ns<4><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
-  else
-    k_batch_top_ns<2><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
+// (a template, so a -DKSIM_TOP_T=16 build, whose candidates overflow the
+// node-split geometry, compiles without it)
+template <int T>
+static void launch_top_ns_t(const LaunchArgs& a, int nch, hipStream_t stream) {
+  if constexpr (16 * T <= 128) {
+    if (nch == 4)
+      k_batch_top_ns<4><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
+    else
+      k_batch_top_ns<2><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
+  }
 }
+static void launch_top_ns(const LaunchArgs& a, int nch, hipStream_t stream) { launch_top_ns_t<kTopT>(a, nch, stream); }
 
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[0], stream);
+  if (a.stab) {   // static-class runs: the default forms only (the host checks batch_ab_forms)
+    k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                    a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm);
+    if (evs) (void)hipEventRecord(evs[1], stream);
+    if (evs) (void)hipEventRecord(evs[2], stream);
+    if (evs) (void)hipEventRecord(evs[3], stream);
+    k_batch_chain_pairs<true, 0, false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey, a.s.chain_end, a.s.pmax,
+        a.s.pnorm, a.s.pinv);
+    if (evs) (void)hipEventRecord(evs[4], stream);
+    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen, a.s.pinv);
+    if (evs) (void)hipEventRecord(evs[5], stream);
+    return 0x19u;
+  }
   const int nch = top_ns_chunks(a);
   if (nch) {
     launch_top_ns(a, nch, stream);
@@ -1497,6 +1700,11 @@ uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) 
 }
 
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
+  if (a.stab) {
+    k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                    a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm);
+    return;
+  }
   if (const int nch = top_ns_chunks(a)) {
     launch_top_ns(a, nch, stream);
     return;

@@ -104,7 +104,27 @@ struct DevPods {
   const int4* ptab_padd;         // per pod (PodPlan.tadd_*): {first entry, column, kind, count} of
                                  // every table its adds change, so a bind skips the class lookup
   int32_t n_pods, n_exprs, n_terms, n_uses, n_adds, n_nn, n_ptab, _pad;
+  // Static classes (P100 batch keys of non-trivial and kPodNormVaries pods):
+  // pods whose static-filter and normalized-score inputs are identical share a
+  // class; stab[cls][node] holds the class's static verdict on the node and
+  // its two raw normalized scores (stab_word).  Null: no table (the keys
+  // evaluate every static plugin per node).  stab_fast: the handle meets
+  // run_fast's cluster conditions, so the keys take the FAST arithmetic.
+  const int32_t* sclass = nullptr;   // [n_pods] class or -1
+  const uint64_t* stab = nullptr;    // [n_classes][c.n]
+  int32_t stab_fast = 0, _pad2 = 0;
 };
+
+// A static-table word: bit 63 every static filter passes; bits 32..62
+// countIntolerableTaintsPreferNoSchedule; bit k < 32: the pod's preferred
+// node-affinity term k (weight != 0) matches the node.  The weights stay
+// with the pod (a class is the terms' expressions, so pods that differ only
+// in weights share it); stab_raw sums them.  The host admits a class only
+// with at most 32 preferred terms, all weights >= 0.
+__host__ __device__ __forceinline__ uint64_t stab_word(bool pass, int64_t tt, uint32_t match) {
+  return (pass ? (1ull << 63) : 0ull) | ((uint64_t)(tt & 0x7fffffff) << 32) | (uint64_t)match;
+}
+__host__ __device__ __forceinline__ bool stab_pass(uint64_t w) { return (w >> 63) != 0; }
 
 // Persistent table kinds (DevPods.ptab_ent .z)
 constexpr int32_t kPtabPlain = 0;    // sum[v] = class count over the nodes with value v
@@ -1682,6 +1702,25 @@ __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const Batc
 struct NormRaw {
   int64_t tt, na;   // countIntolerableTaintsPreferNoSchedule, preferred NodeAffinity weight sum
 };
+// The raw normalized scores of pod p from a static-table word of its class
+// (DevPods::stab): the taint count, and the weights of the matching terms
+// (preferred_node_affinity_score; the term count and weights are uniform).
+__device__ __forceinline__ NormRaw stab_raw(uint64_t w, const DevPods& P, const ksim_pod& p) {
+  int64_t na = 0;
+  for (int k = 0; k < p.pref_term_count; k++)
+    na += ((w >> k) & 1ull) ? (int64_t)P.terms[p.pref_term_first + k].weight : 0;
+  return NormRaw{(int64_t)((w >> 32) & 0x7fffffffull), na};
+}
+// The static-table word's match bits of pod p's preferred terms on a node.
+__device__ __forceinline__ uint32_t pref_term_mask(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                   int32_t node) {
+  uint32_t m = 0;
+  for (int k = 0; k < p.pref_term_count && k < 32; k++) {
+    const ksim_term& t = P.terms[p.pref_term_first + k];
+    if (t.weight != 0 && term_matches(c, P, t, node)) m |= 1u << k;
+  }
+  return m;
+}
 __device__ __forceinline__ NormRaw norm_raw(const DevCluster& c, const DevPods& P, const ksim_pod& p,
                                             const NodeRow& r) {
   return NormRaw{count_intolerable_prefer(c, p, r), p.pref_term_count ? preferred_node_affinity_score(c, P, p, r.node) : 0};
@@ -1694,6 +1733,23 @@ __device__ __forceinline__ int64_t norm_part(const BatchProg& bp, const NormRaw&
   return bp.w_tt * normalize_value(kNormDefaultReverse, v.tt, mx.tt, 0, false) +
          bp.w_na * normalize_value(kNormDefault, v.na, mx.na, 0, false);
 }
+
+// norm_part of a static-table word for the FAST keys of a static class
+// (at most 32 terms of weights in [0, 2^31), so both raw scores lie in
+// [0, 2^36)): each quotient 100 v / m through div_rn with y = RN(1 / m).
+// n = 100 v < 2^43 and 0 < m < 2^36, so the truncated correctly rounded
+// quotient is the integer quotient (as for the FAST key's quotients: a
+// non-integer quotient lies at least 1 / m below the next integer, the
+// rounding error of one below 128 is at most 2^-45).  y_tt / y_na: the caller's RN(1 / mx.tt), RN(1 / mx.na).
+__device__ __forceinline__ int64_t norm_part_fast(const BatchProg& bp, const NormRaw& v, const NormRaw& mx,
+                                                  double y_tt, double y_na) {
+  const int64_t qt = (int64_t)div_rn((double)(kMaxNodeScore * v.tt), (double)mx.tt, y_tt);
+  const int64_t qa = (int64_t)div_rn((double)(kMaxNodeScore * v.na), (double)mx.na, y_na);
+  const int64_t nt = mx.tt > 0 ? (int64_t)kMaxNodeScore - qt : (int64_t)kMaxNodeScore;
+  const int64_t na = mx.na > 0 ? qa : v.na;
+  return bp.w_tt * nt + bp.w_na * na;
+}
+__device__ __forceinline__ double recip_or_zero(int64_t m) { return m > 0 ? 1.0 / (double)m : 0.0; }
 
 __device__ __forceinline__ void row_add_pod(NodeRow& r, const ksim_pod& p, int sign) {
   r.req_cpu += sign * p.req_cpu;

@@ -18,6 +18,7 @@
 #include <map>
 #include <string>
 #include <tuple>
+#include <unordered_map>
 #include <type_traits>
 #include <vector>
 
@@ -120,6 +121,16 @@ struct ksim_handle {
   std::vector<uint8_t> trivial;         // per loaded pod: kBatchStaticTrivial
   std::vector<uint8_t> noadd;           // per loaded pod: no count-class adds (deferred-commit batches)
   std::vector<uint8_t> noscalar;        // ... and no scalar requests (generic deferred-commit batches)
+  // static classes (DevPods::stab, ensure_stab): per loaded pod its class or
+  // -1 (d_sclass), each class's representative pod (d_srep); the table is
+  // rebuilt after any change of pods, cluster or profile (stab_dirty)
+  int32_t* d_sclass = nullptr;
+  int32_t* d_srep = nullptr;
+  int32_t stab_ncls = 0;
+  bool stab_dirty = true, stab_ready = false;
+  std::vector<DevBuf> stab_bufs;
+  size_t stab_bytes = 0;
+  std::vector<int32_t> sclass;          // host copy of d_sclass
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
   std::vector<int32_t> tlen;            // per loaded pod: topology batch run length from it (tbatch_runs)
@@ -164,6 +175,8 @@ struct ksim_handle {
   hipGraphExec_t graph_cycle[16] = {};   // | persistent tables (8)
   hipGraphExec_t graph_batch = nullptr;
   hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
+  hipGraphExec_t graph_batch_stab = nullptr;   // static-class runs (LaunchArgs::stab)
+  hipGraphExec_t graph_lazy_stab = nullptr;
   hipGraphExec_t graph_tbatch = nullptr;       // topology batches (ksim_tbatch.hip)
   // deferred-commit FAST batches (ksim_internal.h): the second snapshot buffer
   // X[1] and state st[1], the ring of chain + pairs outputs, kGraphBatches
@@ -265,6 +278,9 @@ void drop_graphs(ksim_handle* h) {
   drop_cycle_graphs(h);
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
+  if (h->graph_batch_stab) (void)hipGraphExecDestroy(h->graph_batch_stab);
+  if (h->graph_lazy_stab) (void)hipGraphExecDestroy(h->graph_lazy_stab);
+  h->graph_batch_stab = h->graph_lazy_stab = nullptr;
   if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
   if (h->graph_lazy_gen) (void)hipGraphExecDestroy(h->graph_lazy_gen);
@@ -383,9 +399,117 @@ bool run_fast(const ksim_handle* h, int32_t a, int32_t b) {
   return true;
 }
 
+// ---- static classes (DevPods::stab) -------------------------------------------
+constexpr int32_t kStabMaxClasses = 4096;
+constexpr size_t kStabMaxEntries = (size_t)1 << 26;   // 512 MB of table
+
+// The static inputs of a batch pod's keys, as bytes: what static_filters_pass
+// (NodeUnschedulable, NodeName, TaintToleration, NodeAffinity) and norm_raw
+// read of the pod, the selector and affinity expressions expanded, the
+// preferred terms without their weights (two pods with equal signatures have
+// equal verdicts, taint counts and preferred-term matches on every node;
+// stab_word).  False past 32 preferred terms or for a negative weight.
+bool stab_signature(const ksim_pod_set* ps, const ksim_pod& q, std::string& s) {
+  s.clear();
+  auto put = [&](const void* p, size_t n) { s.append((const char*)p, n); };
+  auto put_expr = [&](int32_t e) {
+    const ksim_label_expr& x = ps->exprs[e];
+    put(&x.num, sizeof x.num);
+    put(&x.col, sizeof x.col);
+    put(&x.op, sizeof x.op);
+    put(&x.nvals, sizeof x.nvals);
+    put(x.vals, sizeof(uint32_t) * std::min<int>(x.nvals, KSIM_EXPR_VALS));
+  };
+  auto put_term = [&](int32_t t, bool preferred) {
+    const ksim_term& x = ps->terms[t];
+    if (preferred) s.push_back(x.weight != 0 ? 1 : 0);   // a zero weight never counts
+    put(&x.n_expr, sizeof x.n_expr);
+    for (int32_t k = 0; k < x.n_expr; k++) put_expr(x.first_expr + k);
+  };
+  const uint32_t fl = q.flags & (KSIM_POD_TOLERATES_UNSCHEDULABLE | KSIM_POD_HAS_REQUIRED_AFFINITY);
+  put(&fl, sizeof fl);
+  put(&q.node_name, sizeof q.node_name);
+  put(q.tol_filter, sizeof q.tol_filter);
+  put(q.tol_prefer, sizeof q.tol_prefer);
+  put(&q.sel_count, sizeof q.sel_count);
+  for (int32_t k = 0; k < q.sel_count; k++) put_expr(q.sel_first + k);
+  put(&q.req_term_count, sizeof q.req_term_count);
+  for (int32_t k = 0; k < q.req_term_count; k++) put_term(q.req_term_first + k, false);
+  if (q.pref_term_count > 32) return false;
+  put(&q.pref_term_count, sizeof q.pref_term_count);
+  for (int32_t k = 0; k < q.pref_term_count; k++) {
+    put_term(q.pref_term_first + k, true);
+    if (ps->terms[q.pref_term_first + k].weight < 0) return false;   // raw scores >= 0 (norm_part_fast)
+  }
+  return true;
+}
+
+// KSIM_NO_STAB=1: no table (the keys evaluate the static plugins per node; A/B runs).
+bool stab_enabled() {
+  static const bool off = getenv("KSIM_NO_STAB") != nullptr;
+  return !off;
+}
+
+LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen);
+
+// The static table of the loaded queue's classes on the current snapshot and
+// profile, rebuilt in place when stale (in stream order: a graph captured with
+// the table replays on the new contents, so a weight sweep keeps its graphs);
+// graphs that may hold the table's old address, or a table that no longer
+// exists, drop.
+int ensure_stab(ksim_handle* h) {
+  if (!h->stab_dirty) return KSIM_OK;
+  h->stab_dirty = false;
+  const bool was_ready = h->stab_ready;
+  h->stab_ready = false;
+  const size_t entries = (size_t)h->stab_ncls * (size_t)std::max(h->dc.n, 0);
+  if (!stab_enabled() || !h->dp.pods || entries == 0 || entries > kStabMaxEntries) {
+    if (was_ready) {
+      HIPCHK(h, hipStreamSynchronize(h->stream));
+      drop_graphs(h);
+    }
+    return KSIM_OK;
+  }
+  if (h->stab_bytes < 8 * entries) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    drop_graphs(h);
+    free_bufs(h->stab_bufs);
+    h->stab_bytes = 0;
+    void* p = nullptr;
+    int rc;
+    if ((rc = upload(h, h->stab_bufs, nullptr, 8 * entries, &p))) return rc;
+    h->stab_bytes = 8 * entries;
+  } else if (!was_ready) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    drop_graphs(h);                              // captured without the table
+  }
+  launch_static_table(make_args(h, h->dp, nullptr), h->d_srep, h->stab_ncls, (uint64_t*)h->stab_bufs[0].p, h->stream);
+  HIPCHK(h, hipGetLastError());
+  h->stab_ready = true;
+  return KSIM_OK;
+}
+
 // ADAPT: the profile keeps fewer than all nodes (K < N over the whole cluster).
 bool adapt_mode(const ksim_handle* h) {
   return num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->dc.n_total) < h->dc.n_total;
+}
+
+// The STAB batch kernels (LaunchArgs::stab): every pod of the P100 run in a
+// static class, run_fast's cluster conditions, an unsharded handle and the
+// default launch forms.
+bool run_stab(const ksim_handle* h, int32_t a, int32_t b) {
+  if (!h->stab_ready || h->stab_dirty || batch_ab_forms() || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
+  if (!h->bp.cpu_mem || !h->bp.fast_w || !h->alloc_narrow) return false;
+  for (int32_t i = a; i < b; i++)
+    if (h->sclass[(size_t)i] < 0) return false;
+  return true;
+}
+
+// The key kernels of a batch run: FAST, FAST with the static table, or generic.
+void pick_keys(const ksim_handle* h, int32_t a, int32_t b, LaunchArgs& la) {
+  la.fast = run_fast(h, a, b);
+  la.stab = !la.fast && run_stab(h, a, b);
+  la.fast = la.fast || la.stab;
 }
 
 // NetworkBandwidth in the profile (Filter or Score)
@@ -496,6 +620,11 @@ LaunchArgs make_args(ksim_handle* h, const DevPods& P, int32_t* chosen) {
   a.c.eval_hi = a.c.n;
   a.c.count_whole = (!h->replicated || h->rep_primary) ? 1 : 0;
   a.P = P;
+  if (h->stab_ready && !h->stab_dirty && P.pods == h->dp.pods) {   // the loaded queue's static classes
+    a.P.sclass = h->d_sclass;
+    a.P.stab = (const uint64_t*)h->stab_bufs[0].p;
+    a.P.stab_fast = (h->bp.cpu_mem && h->bp.fast_w && h->alloc_narrow) ? 1 : 0;
+  }
   a.prof = h->prof;
   a.bp = h->bp;
   a.dprof = h->d_prof;
@@ -524,10 +653,11 @@ int read_state(ksim_handle* h, DevState& st) {
 }
 
 int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fast = false, bool fuse_min = false,
-            bool fuse_ext = false, bool ptab = false) {
+            bool fuse_ext = false, bool ptab = false, bool stab = false) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
   a.fast = fast;
+  a.stab = stab;
   a.fuse_min = fuse_min;
   a.fuse_ext = fuse_ext;
   a.ptab = ptab;
@@ -611,8 +741,13 @@ bool lazy_gen_enabled() {
 // (the overlay carries the resource columns only), on a cluster the overlay's
 // LDS node bitmap covers.  Generic runs (fast false): unsharded P100 handles,
 // pods without scalar requests (k_batch_top_commit<.., false>).
-bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b, bool fast) {
-  if (!lazy_enabled() || batch_ab_forms()) return false;
+// Static-class runs (stab) only with KSIM_LAZY_STAB=1: config 1 scaled measured
+// 13.3 against 12.7 ms per step for the three launches (profiles/r03/ab_stab;
+// the overlay lookups of the maxima pass and the key pass cost more than the
+// separate commit launch).
+bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b, bool fast, bool stab = false) {
+  static const bool lazy_stab = getenv("KSIM_LAZY_STAB") != nullptr;
+  if (!lazy_enabled() || batch_ab_forms() || (stab && !lazy_stab)) return false;
   if (!fast) {
     if (!lazy_gen_enabled() || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
     for (int32_t i = a; i < b; i++)
@@ -766,7 +901,10 @@ void lazy_flush(const ksim_handle* h, const LazyBatch& z, hipStream_t stream) {
 int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   int rc;
   if ((rc = lazy_begin(h))) return rc;
-  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt : la.fast ? h->graph_lazy : h->graph_lazy_gen;
+  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt
+                          : la.stab     ? h->graph_lazy_stab
+                          : la.fast     ? h->graph_lazy
+                                        : h->graph_lazy_gen;
   if (!graph) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     hipGraph_t g = nullptr;
@@ -829,11 +967,12 @@ int run_range(ksim_handle* h, int32_t a, int32_t b, bool batch, bool topo) {
     return KSIM_OK;
   }
   if (topo) return run_tbatch(h, a, b, la);
-  // the FAST evaluation kernel when every pod of the run is trivial with cpu/memory scoring
-  la.fast = run_fast(h, a, b);
-  if (lazy_ok(h, a, b, la.fast)) return run_lazy(h, a, b, la);
-  hipGraphExec_t& gb = la.fast ? h->graph_batch_fast : h->graph_batch;
-  if (!gb && (rc = capture(h, true, false, &gb, la.fast))) return rc;
+  // the FAST evaluation kernel when every pod of the run is trivial with
+  // cpu/memory scoring, or is in a static class (STAB)
+  pick_keys(h, a, b, la);
+  if (lazy_ok(h, a, b, la.fast, la.stab)) return run_lazy(h, a, b, la);
+  hipGraphExec_t& gb = la.stab ? h->graph_batch_stab : la.fast ? h->graph_batch_fast : h->graph_batch;
+  if (!gb && (rc = capture(h, true, false, &gb, la.fast, false, false, false, la.stab))) return rc;
   // every batch commits between 1 and kBatchPods pods: a graph of
   // kGraphBatches batches never overshoots while left >= kBatchPods * kGraphBatches,
   // and ceil(left / kBatchPods) single batches never overshoot either
@@ -1465,6 +1604,7 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->scratch_bufs);
   free_bufs(h->ash_bufs);
   free_bufs(h->lazy_bufs);
+  free_bufs(h->stab_bufs);
   free_bufs(h->pod_bufs);
   free_bufs(h->pod1_bufs);
   free_bufs(h->pre_bufs);
@@ -1482,6 +1622,7 @@ const char* ksim_last_error(const ksim_handle* h) { return h ? h->err.c_str() : 
 
 int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   if (!h || !p) return KSIM_E_INVALID;
+  h->stab_dirty = true;                     // DevPods::stab: the static filter list may change
   if (p->n_filter < 0 || p->n_filter > KSIM_MAX_FILTER || p->n_score < 0 || p->n_score > KSIM_MAX_SCORE)
     return set_err(h, KSIM_E_INVALID, "plugin count out of range");
   for (int i = 0; i < p->n_filter; i++) {
@@ -1559,6 +1700,7 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
 
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v) {
   if (!h || !t || !v) return KSIM_E_INVALID;
+  h->stab_dirty = true;
   HIPCHK(h, hipSetDevice(h->device));
   const int32_t n = t->n_nodes;
   if (n < 0 || n > KSIM_MAX_NODES) return set_err(h, KSIM_E_INVALID, "n_nodes out of range");
@@ -1828,6 +1970,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
   // (a replica keeps its flag when the delta is refused; the new snapshot
   // below clears it: ksim_set_eval_range again)
   if (!h || !t || !v) return KSIM_E_INVALID;
+  h->stab_dirty = true;
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_upsert_nodes before ksim_set_cluster");
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_upsert_nodes on a shard handle");
   HIPCHK(h, hipSetDevice(h->device));
@@ -1910,6 +2053,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
 // replay keeps every other node's state.
 int ksim_remove_node(ksim_handle* h, int32_t pos) {
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
+  h->stab_dirty = true;
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_remove_node on a shard handle");
   const int32_t n0 = h->dc.n;
   if (pos < 0 || pos >= n0) return set_err(h, KSIM_E_INVALID, "node position out of range");
@@ -2566,7 +2710,8 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
                                      4 * np1,
                                      sizeof(ksim_topo_use) * (size_t)ps->n_uses,
                                      sizeof(PodPlan) * (size_t)ps->n_pods,
-                                     sizeof(ksim_class_add) * (size_t)ps->n_adds};
+                                     sizeof(ksim_class_add) * (size_t)ps->n_adds,
+                                     4 * np1, 4 * np1};
   const bool reuse = h->d_chosen && h->pod_buf_bytes == bytes;
   auto drop_queue = [&](int code) {
     drop_graphs(h);
@@ -2625,6 +2770,27 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     h->noadd[i] = ps->pods[i].add_count == 0 ? 1 : 0;
     h->noscalar[i] = (ps->pods[i].flags & KSIM_POD_HAS_SCALAR) == 0 ? 1 : 0;
   }
+  // static classes (DevPods::stab): the batch pods without scalar requests
+  // (trivial ones too, so a run mixing them with static-plugin pods takes
+  // the STAB kernels)
+  std::vector<int32_t> scls(np1, -1), srep(np1, 0);
+  int32_t ncls = 0;
+  {
+    std::unordered_map<std::string, int32_t> ids;
+    std::string sig;
+    for (int32_t i = 0; i < ps->n_pods; i++) {
+      const ksim_pod& q = ps->pods[i];
+      if (batchable[i] != 1 && batchable[i] != 2) continue;
+      if ((q.flags & KSIM_POD_HAS_SCALAR) || !stab_signature(ps, q, sig)) continue;
+      auto it = ids.find(sig);
+      if (it == ids.end()) {
+        if (ncls >= kStabMaxClasses) continue;
+        it = ids.emplace(sig, ncls).first;
+        srep[(size_t)ncls++] = i;
+      }
+      scls[(size_t)i] = it->second;
+    }
+  }
   std::vector<PodPlan> plans((size_t)ps->n_pods);
   for (int32_t i = 0; i < ps->n_pods; i++) {
     plans[i] = make_plan(h, ps->pods[i], uses.data() + std::max(ps->pods[i].use_first, 0));
@@ -2662,6 +2828,13 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
   P.plans = (const PodPlan*)p;
   if ((rc = put(ps->adds, sizeof(ksim_class_add) * (size_t)ps->n_adds, &p))) return drop_queue(rc);
   P.adds = (const ksim_class_add*)p;
+  if ((rc = put(scls.data(), 4 * np1, &p))) return drop_queue(rc);
+  h->d_sclass = (int32_t*)p;
+  if ((rc = put(srep.data(), 4 * np1, &p))) return drop_queue(rc);
+  h->d_srep = (int32_t*)p;
+  h->stab_ncls = ncls;
+  h->sclass.assign(scls.begin(), scls.begin() + ps->n_pods);
+  h->stab_dirty = true;
   if ((rc = put(R.ent.data(), sizeof(int4) * R.ent.size(), &p))) return drop_queue(rc);
   P.ptab_ent = (const int4*)p;
   if ((rc = put(R.cfirst.data(), 4 * R.cfirst.size(), &p))) return drop_queue(rc);
@@ -2707,6 +2880,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
   if (!h->dp.pods && count > 0) return set_err(h, KSIM_E_INVALID, "no pods loaded");
   if (first < 0 || count < 0 || first + count > h->dp.n_pods) return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
   HIPCHK(h, hipSetDevice(h->device));
+  if ((rc = ensure_stab(h))) return rc;
   if ((rc = reset_counters(h, h->stream))) return rc;
   int64_t perpod = 0;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -2743,6 +2917,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
 
 int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total) {
   if (!h) return KSIM_E_INVALID;
+  h->stab_dirty = true;
   if (node_base < 0 || n_total < 0 || n_total > KSIM_MAX_NODES || node_base > n_total)
     return set_err(h, KSIM_E_INVALID, "bad shard range");
   if (h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_set_shard must precede ksim_set_cluster");
@@ -2830,7 +3005,7 @@ int ksim_group_schedule_loaded(ksim_handle** hs, int32_t n, int32_t first, int32
   HIPCHK(h0, hipSetDevice(h0->device));
   int rc;
   for (auto* h : v)
-    if ((rc = reset_counters(h, h->stream))) return rc;
+    if ((rc = ensure_stab(h)) || (rc = reset_counters(h, h->stream))) return rc;
   HIPCHK(h0, hipEventRecord(h0->ev0, h0->stream));
   if (count && (rc = shard_schedule(v, first, count))) return rc;
   HIPCHK(h0, hipEventRecord(h0->ev1, h0->stream));
@@ -2865,6 +3040,7 @@ int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* ps, int32_t* chosen,
 
 int ksim_reset_cluster(ksim_handle* h) {
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
+  h->stab_dirty = true;
   HIPCHK(h, hipSetDevice(h->device));
   const size_t N = (size_t)h->dc.n;
   const DevCluster& c = h->dc;
@@ -2896,16 +3072,17 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
     return set_err(h, KSIM_E_UNSUPPORTED, "topology batch evaluations span two kernels");
   if (batch && adapt_mode(h)) return set_err(h, KSIM_E_UNSUPPORTED, "ADAPT batch evaluations span two kernels");
   HIPCHK(h, hipSetDevice(h->device));
+  if ((rc = ensure_stab(h))) return rc;
   // two batches' pods: the deferred-commit timing below keys batch 1 (a full
   // batch whatever batch 0 commits)
   const int32_t end = batch ? std::min(h->dp.n_pods, first + 2 * kBatchPods) : first + 1;
   if ((rc = set_run(h, first, end))) return rc;
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
-  a.fast = batch && run_fast(h, first, end);
+  if (batch) pick_keys(h, first, end, a);
   a.fuse_min = !batch && h->topo[first] && h->hard_small[first];
   a.fuse_ext = !batch && h->soft_le1[first];
   a.ptab = !batch && h->topo[first] == 2;
-  if (batch && a.fast && lazy_ok(h, first, end, true)) {
+  if (batch && a.fast && lazy_ok(h, first, end, true, a.stab)) {
     // the deferred-commit evaluation launch as the run issues it: batch 0 of
     // the run (both launches), then batch 1's k_batch_top_commit repeated
     // (idempotent: it reads X[0], st[0] and slot 0, and writes X[1], st[1],
@@ -2972,6 +3149,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
   if (!h->dp.pods || first < 0 || count <= 0 || first + count > h->dp.n_pods)
     return set_err(h, KSIM_E_INVALID, "range out of loaded pods");
   HIPCHK(h, hipSetDevice(h->device));
+  if ((rc = ensure_stab(h))) return rc;
   double sum[kKinds] = {0};
   int64_t n[kKinds] = {0};
   LaunchArgs a = make_args(h, h->dp, h->d_chosen);
@@ -2981,7 +3159,8 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     const bool adapt = batch && adapt_mode(h);
     const bool tb = batch && topo;                 // topology batch runs (class 3)
     // the same kernel variants the run itself would launch
-    a.fast = batch && run_fast(h, lo, hi);
+    a.fast = a.stab = false;
+    if (batch) pick_keys(h, lo, hi, a);
     a.fuse_min = !batch && topo;
     for (int32_t i = lo; i < hi && a.fuse_min; i++) a.fuse_min = h->hard_small[i] != 0;
     a.fuse_ext = !batch;
@@ -2992,7 +3171,7 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
                      : adapt ? kKernelsPerCycle + kKernelsPerBatch
                      : batch ? kKernelsPerCycle : 0;
     if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
-    if (batch && !tb && a.fast && lazy_ok(h, lo, hi, true)) {
+    if (batch && !tb && a.fast && lazy_ok(h, lo, hi, true, a.stab)) {
       // deferred-commit batches: two (P100) or three to four (ADAPT) launches
       // each, a flush (untimed) before every state read
       const int lper = adapt ? kKernelsPerLazyAdapt : kKernelsPerLazy;

@@ -44,6 +44,7 @@ struct LaunchArgs {
   const ksim_profile* dprof = nullptr;   // device copies of prof / bp (the batch kernels read these)
   const BatchProg* dbp = nullptr;
   bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
+  bool stab = false; // ... or (with fast) every pod in a static class (DevPods::stab; the STAB kernels)
   bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
   bool fuse_ext = false;  // per-pod runs: every pod has <= 1 ScheduleAnyway spread constraint (K = N: no k_extrema)
   bool ptab = false;      // per-pod topology runs: every pod carries kPlanPtab (no k_topo_prefilter)
@@ -133,6 +134,8 @@ void launch_adapt_lazy_flush(const LazyBatch& z, hipStream_t stream);
 // batch i: k_batch_top_commit (commit of i-1, evaluation of i), then the
 // chain + pairs of i.  A flush is the first launch alone with no evaluation:
 // it commits batch i-1 and leaves slot i empty.
+// DevPods::stab rows of classes [0, n_cls) (ksim_batch.hip k_static_table)
+void launch_static_table(const LaunchArgs& a, const int32_t* rep, int32_t n_cls, uint64_t* stab, hipStream_t stream);
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream);
 void launch_lazy_top(const LazyBatch& z, hipStream_t stream);   // the first launch alone (ksim_time_eval)

@@ -3,7 +3,9 @@
 pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch;
 KSIM_NO_LAZY: the three-launch P100 batch, commit as its own launch, instead
 of the deferred commit; KSIM_LAZY_GEN: the deferred commit for generic pods
-too -- config 1's taints, tolerations and node affinity).  They
+too -- config 1's taints, tolerations and node affinity; KSIM_NO_STAB: those
+pods' keys without the static-class table, every static plugin per node;
+KSIM_LAZY_STAB: the deferred commit for the static-class runs).  They
 are read once per process, so each runs in one child process that schedules
 P100 and ADAPT batches and checks them against the oracle (the default forms
 run in every other GPU test)."""
@@ -53,7 +55,7 @@ print("ok")
 
 
 @pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE", "KSIM_NO_LAZY",
-                                    "KSIM_LAZY_GEN"])
+                                    "KSIM_LAZY_GEN", "KSIM_NO_STAB", "KSIM_LAZY_STAB"])
 def test_separate_launch_forms_vs_oracle(switch):
     env = dict(os.environ)
     env[switch] = "1"

@@ -101,15 +101,18 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 EVAL_KERNELS = ("k_batch_top_commit", "k_batch_top", "k_batch_eval", "k_adapt_top", "k_tb_filter", "k_filter_score")
 
 
-def _profile_entry(fname: str, kernel: str, nodes: int):
-    """The committed PMC measurement (profiles/<fname>) of a kernel at a size."""
+def _profile_entry(fname: str, kernel: str, nodes: int, config: int):
+    """The committed PMC measurement (profiles/<fname>) of a kernel at a size,
+    on this bench config (config 1 and 2 run the same kernels on 5,000 nodes
+    with different pods)."""
     path = os.path.join(ROOT, "profiles", fname)
     try:
         tj = json.load(open(path))
     except (OSError, ValueError):
         return None
     for entry in (tj if isinstance(tj, list) else [tj]):
-        if isinstance(entry, dict) and entry.get("kernel") == kernel and entry.get("nodes") == nodes:
+        if (isinstance(entry, dict) and entry.get("kernel") == kernel and entry.get("nodes") == nodes
+                and entry.get("config") == config):
             return entry
     return None
 
@@ -518,9 +521,9 @@ def main():
     # PMC measurements committed under profiles/ (by kernel and size): HBM
     # bytes per launch (traffic.json) and vector instructions per launch
     # (valu.json), priced with this run's launch time
-    te = _profile_entry("traffic.json", dominant, knodes)
+    te = _profile_entry("traffic.json", dominant, knodes, cfg)
     traffic = te.get("hbm_bytes_per_launch") if te else None
-    ve = _profile_entry("valu.json", dominant, knodes)
+    ve = _profile_entry("valu.json", dominant, knodes, cfg)
     valu = None
     if ve and ve.get("valu_insts_per_launch"):
         g = ve["valu_insts_per_launch"] / (avg_ms * 1e-3) / 1e9

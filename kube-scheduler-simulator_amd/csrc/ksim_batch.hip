@@ -491,6 +491,12 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
     const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
     return stab_pass(w) ? k : 0;
   };
+  // kPodNormVaries: the first pass keeps each node's key (without the
+  // normalized part) in LDS when the range fits, so the second pass only adds
+  // that part (each slot is written and read by the same thread: no barrier)
+  constexpr int32_t kKeep = 8192;
+  __shared__ uint64_t s_keep[kKeep];
+  const bool keep = normv && c.eval_hi - c.eval_lo <= kKeep;   // block-uniform
   NormRaw mx{0, 0};
   double y_tt = 0, y_na = 0;
   if (normv) {
@@ -498,7 +504,9 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
       uint64_t w;
-      if (key(node, w)) acc.take(stab_raw(w, P, pp));
+      const uint64_t k = key(node, w);
+      if (keep) s_keep[node - c.eval_lo] = k;
+      if (k) acc.take(stab_raw(w, P, pp));
     }
     mx = norm_maxima<kTopThreads>(acc, pnorm, j);
     y_tt = recip_or_zero(mx.tt);
@@ -507,7 +515,13 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
 #pragma unroll 1
   for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
     uint64_t w;
-    uint64_t k = key(node, w);
+    uint64_t k;
+    if (keep) {
+      k = s_keep[node - c.eval_lo];
+      w = ld_off(srow, (uint32_t)node << 3);
+    } else {
+      k = key(node, w);
+    }
     if (normv && k) k += (uint64_t)norm_part_fast(bp, stab_raw(w, P, pp), mx, y_tt, y_na) << 44;
     nfeas += k != 0;
     a[3] = umax64(a[3], k);

@@ -279,7 +279,8 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
                                                    int32_t* __restrict__ aexact, uint64_t* __restrict__ topk,
                                                    int32_t* __restrict__ topk_cnt,
                                                    int32_t* __restrict__ topk_complete,
-                                                   uint64_t* __restrict__ xsend) {
+                                                   uint64_t* __restrict__ xsend,
+                                                   int64_t* __restrict__ pnorm = nullptr) {
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   constexpr int W = NT / 64;
@@ -380,13 +381,69 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       }
     }
   } else {
+    // kPodNormVaries (unsharded, pnorm given): DefaultNormalizeScore's maxima
+    // over the pod's scored list -- the kept nodes of its window -- then keys
+    // that carry the normalized part (norm_part).  The list stays the S0 list
+    // while the window is not broken (k_adapt_pairs flags every kept node
+    // that stops fitting for these pods), so the maxima hold for the batch.
+    const bool normv = pnorm && (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
+    // a static class (DevPods::stab): the raw scores from the class row, and on
+    // a run_fast cluster the FAST key arithmetic (block-uniform)
+    const int32_t scls = P.stab ? P.sclass[pi] : -1;
+    const uint64_t* srow = scls >= 0 ? P.stab + (size_t)scls * c.n : nullptr;
+    const bool fk = srow && P.stab_fast;
+    auto raw = [&](int32_t node) -> NormRaw {
+      return srow ? stab_raw(srow[node], P, p) : norm_raw(c, P, p, load_row(c, node));
+    };
+    auto gkey = [&](int32_t node) -> uint64_t {
+      if (fk) {
+        const NodeRow r = load_res_row_off(c, node);
+        const uint32_t o8 = (uint32_t)node << 3;
+        return dyn_key_fast(bp, fast_pod_fields(p), r, ld_off(c.inv_cpu, o8), ld_off(c.inv_mem, o8), hseed,
+                            c.base + node);
+      }
+      return node_key(node);
+    };
+    NormRaw mx{0, 0};
+    if (normv) {
+      __shared__ uint64_t s_nmx[2][W];
+      uint64_t lt = 0, la = 0;
+#pragma unroll 1
+      for (int32_t off = tid; off < kend; off += NT) {
+        int32_t node = s + off;
+        if (node >= n) node -= n;
+        if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
+        const NormRaw v = raw(node);
+        lt = umax64(lt, (uint64_t)v.tt);
+        la = umax64(la, (uint64_t)v.na);
+      }
+      lt = wave_max_u64_dpp(lt);
+      la = wave_max_u64_dpp(la);
+      if (lane == 0) {
+        s_nmx[0][wv] = lt;
+        s_nmx[1][wv] = la;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        lt = umax64(lt, s_nmx[0][w]);
+        la = umax64(la, s_nmx[1][w]);
+      }
+      mx = NormRaw{(int64_t)lt, (int64_t)la};
+      if (tid == 0) {
+        pnorm[4 * j] = mx.tt;
+        pnorm[4 * j + 1] = mx.na;
+      }
+    }
 #pragma unroll 1
     for (int32_t off = tid; off < kend; off += NT) {
       int32_t node = s + off;
       if (node >= n) node -= n;
       if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
       kept++;
-      a[kTopT - 1] = umax64(a[kTopT - 1], node_key(node));
+      uint64_t k = gkey(node);
+      if (normv && k) k += (uint64_t)norm_part(bp, raw(node), mx) << 44;
+      a[kTopT - 1] = umax64(a[kTopT - 1], k);
 #pragma unroll
       for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
     }
@@ -462,7 +519,8 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
                                                             uint64_t* __restrict__ gkey,
                                                             int32_t* __restrict__ chain_end,
                                                             uint64_t* __restrict__ pmax,
-                                                            int32_t* __restrict__ abroken) {
+                                                            int32_t* __restrict__ abroken,
+                                                            const int64_t* __restrict__ pnorm = nullptr) {
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
@@ -505,8 +563,13 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         const ksim_pod& p = P.pods[base + j];
         const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
         const bool was = (amask[(size_t)j * n_words + (g >> 6)] >> (g & 63)) & 1ull;
-        if (cut >= 0 && was && !now) brk = true;
+        // kPodNormVaries (k_adapt_top's maxima): a kept node that stops
+        // fitting changes the scored list even when every node is processed
+        const bool normv = pnorm && (P.bflags[base + j] & kPodNormVaries) != 0;
+        if ((cut >= 0 || normv) && was && !now) brk = true;
         if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base);
+        if (normv && v)
+          v += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), NormRaw{pnorm[4 * j], pnorm[4 * j + 1]}) << 44;
       }
     }
   }
@@ -767,7 +830,7 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
-    a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr)
+    a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
   if (k >= kTopWideK) {
     if (a.fast) TOP(true, 1024, false);
     else TOP(false, 1024, false);
@@ -784,13 +847,13 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
     if (evs) (void)hipEventRecord(evs[4], stream);
     k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
         a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-        a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken);
+        a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken, a.s.pnorm);
   } else {
     launch_chain(a, stream);
     if (evs) (void)hipEventRecord(evs[4], stream);
     k_adapt_pairs<false, false><<<kBatchPods, kBatchPods, 0, stream>>>(
         a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, nullptr, nullptr, nullptr, a.s.gkey,
-        a.s.chain_end, a.s.pmax, a.s.abroken);
+        a.s.chain_end, a.s.pmax, a.s.abroken, a.s.pnorm);
   }
   if (evs) (void)hipEventRecord(evs[5], stream);
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,

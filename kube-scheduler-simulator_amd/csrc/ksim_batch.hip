@@ -310,20 +310,6 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   }
 }
 
-// The request fields the FAST pair key reads (pod j's and the bound pod k's),
-// as a local ksim_pod: a caller can load them before it knows the guesses.
-__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
-  ksim_pod p;
-  p.req_cpu = g.req_cpu;
-  p.req_mem = g.req_mem;
-  p.req_eph = g.req_eph;
-  p.nz_cpu = g.nz_cpu;
-  p.nz_mem = g.nz_mem;
-#pragma unroll
-  for (int k = 0; k < KSIM_MAX_SCALAR; k++) p.scalar_req[k] = 0;   // trivial pods: no scalar requests
-  return p;
-}
-
 // A lane's DefaultNormalizeScore maxima of a kPodNormVaries pod's raw
 // TaintToleration / NodeAffinity scores over its S0-feasible nodes, and how
 // many of its nodes hold each (raw scores are >= 0).

@@ -1677,6 +1677,20 @@ __device__ __forceinline__ uint64_t dyn_key_fast(const FastProg& q, const ksim_p
   return ok ? key : 0;
 }
 
+// The request fields the FAST pair key reads (pod j's and the bound pod k's),
+// as a local ksim_pod: a caller can load them before it knows the guesses.
+__device__ __forceinline__ ksim_pod fast_pod_fields(const ksim_pod& g) {
+  ksim_pod p;
+  p.req_cpu = g.req_cpu;
+  p.req_mem = g.req_mem;
+  p.req_eph = g.req_eph;
+  p.nz_cpu = g.nz_cpu;
+  p.nz_mem = g.nz_mem;
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCALAR; k++) p.scalar_req[k] = 0;   // trivial pods: no scalar requests
+  return p;
+}
+
 __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim_pod& p, const NodeRow& r,
                                                  double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
   return dyn_key_fast(fast_prog(bp), p, r, inv_c, inv_m, hseed, gnode);

@@ -562,10 +562,16 @@ int pod_batchable(const ksim_handle* h, const ksim_pod& p, bool* norm_varies = n
 
 // Whether loaded pod i runs on this handle's batch path (see pod_batchable):
 // class 2 needs the unsharded P100 path over the whole node table.
+// Class 2 under ADAPT: pods whose normalized scores vary (k_adapt_top's
+// maxima over the window's kept nodes), without scalar requests, on an
+// unsharded handle (KSIM_NO_ADAPT_NORM=1: the per-pod path, A/B).
 bool pod_on_batch(const ksim_handle* h, int32_t i) {
+  static const bool adapt_norm = getenv("KSIM_NO_ADAPT_NORM") == nullptr;
   const uint8_t b = h->batchable[i];
   if (b != 2 && b != 3) return b != 0;
-  return !adapt_mode(h) && !is_sharded(h) && !h->replicated;   // replicated: a split evaluation range
+  if (is_sharded(h) || h->replicated) return false;   // replicated: a split evaluation range
+  if (!adapt_mode(h)) return true;
+  return b == 2 && adapt_norm && h->noscalar[(size_t)i];
 }
 
 // Topology pods the topology batch path takes (class 3; ksim_tbatch.hip): the

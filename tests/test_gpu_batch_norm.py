@@ -49,14 +49,18 @@ def test_config1_distribution_batched(n_nodes, n_pods):
     assert st.perpod_cycles == 0 and st.batches > 0
 
 
-def test_config1_distribution_adapt_stays_per_pod():
-    """ADAPT (K < N): the varying-normalization pods keep the per-pod path
+@pytest.mark.parametrize("n_nodes,n_pods", [(400, 1500), (1200, 4000), (3000, 6000)])
+def test_config1_distribution_adapt_batched(n_nodes, n_pods):
+    """ADAPT (K < N), the simulator's own mode: the varying-normalization pods
     (on config 1's distribution nearly every pod varies: 20 % of the nodes
-    carry a PreferNoSchedule taint, 30 % of the pods prefer node labels)."""
-    nodes, pods = gen.config1_objects(n_nodes=400, n_pods=1500)
+    carry a PreferNoSchedule taint, 30 % of the pods prefer node labels) take
+    the ADAPT batch path, their keys normalized over the window's kept nodes
+    (ksim_adapt.hip k_adapt_top), a kept node that stops fitting ending the
+    batch (k_adapt_pairs)."""
+    nodes, pods = gen.config1_objects(n_nodes=n_nodes, n_pods=n_pods)
     cluster, _ = encode_cluster(nodes)
     st = _run(cluster, encode_pods(cluster, pods), pct=0)
-    assert st.perpod_cycles > 0
+    assert st.perpod_cycles == 0 and st.batches > 0
 
 
 def _holder_cluster(n_nodes, n_small, big_weight):

@@ -114,11 +114,18 @@ def test_adapt_batch_config2_and_pct():
 
 def test_adapt_batch_mixed_runs():
     """Config-1 objects on 400 nodes (K = 100 < N): batch and per-pod runs
-    interleave and hand nextStartNodeIndex to each other."""
+    interleave and hand nextStartNodeIndex to each other (every fifth pod
+    carries a ScheduleAnyway zone spread constraint: the per-pod path)."""
     from ksim.encode import encode_cluster, encode_pods
+    from ksim.model import LabelSelector, TopologySpreadConstraint
     nodes, pods = gen.config1_objects(n_nodes=400, n_pods=2000)
     for n in nodes:
         n.taints = [t for t in n.taints if t.effect != "PreferNoSchedule"]
+    for k, p in enumerate(pods):
+        p.labels = {"app": f"a{k % 3}"}
+        if k % 5 == 4:
+            p.topology_spread = [TopologySpreadConstraint(1, "topology.kubernetes.io/zone", "ScheduleAnyway",
+                                                          LabelSelector({"app": p.labels["app"]}))]
     cluster, _ = encode_cluster(nodes)
     st = _batch_vs_oracle(cluster, encode_pods(cluster, pods), pct=0)
     assert st.perpod_cycles > 0 and st.batches > 0

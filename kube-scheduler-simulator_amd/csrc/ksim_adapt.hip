@@ -181,6 +181,34 @@ __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_
   return -1;
 }
 
+// find_cut from per-pod prefix counts (pc[w] = set bits in words [0, w),
+// pc[nw] = all of them; k_adapt_window<true>): the rank of the K-th set bit
+// from s, a binary search for its word in LDS, one word load.  The same
+// result as find_cut; a round costs a few LDS reads instead of a scan of the
+// bitmap, which is what a batch of pods whose windows converge slowly (a
+// heterogeneous queue: config 1's taints and affinities) pays every round.
+constexpr int32_t kWinPcWords = 127;                 // (nw + 1) uint16 per pod: 64 KB per block
+__device__ __forceinline__ int32_t find_cut_pc(const uint64_t* __restrict__ mask, const uint16_t* pc, int32_t nw,
+                                               int32_t s, int32_t n, int32_t k) {
+  const int32_t total = pc[nw];
+  if (total <= k) return -1;
+  const int32_t ws = s >> 6;
+  const int32_t before = pc[ws] + __popcll(mask[ws] & ((1ull << (s & 63)) - 1));
+  int32_t t = before + k;                            // the global rank of the cut's bit
+  const bool wrap = t >= total;
+  if (wrap) t -= total;
+  int32_t lo = 0, hi = nw - 1;                       // the last word with pc[w] <= t
+  while (lo < hi) {
+    const int32_t mid = (lo + hi + 1) >> 1;
+    if (pc[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  uint64_t x = mask[lo];
+  for (int32_t q = pc[lo]; q < t; q++) x &= x - 1;
+  const int32_t pos = (lo << 6) + __builtin_ctzll(x);
+  return wrap ? pos + n - s : pos - s;
+}
+
 constexpr int kWindowRounds = 48;
 constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length   // exact prefix kept if not converged by then
 
@@ -188,20 +216,35 @@ constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod fr
 // j): *s_out = pod j's scan start, *cut_out = its cut offset (-1: no cut),
 // *exact_out = pods with exact windows.  false: the batch is empty
 // (block-uniform).  A pure function of the bitmaps and the state.
+// PC: the prefix-count cut search (n_words <= kWinPcWords).
+template <bool PC = false>
 __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
                                              int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
                                              int32_t* cut_out, int32_t* exact_out) {
   __shared__ int64_t sh[kBatchPods / 64];
   __shared__ int32_t s_first;
+  __shared__ uint16_t s_pc[PC ? kBatchPods * (kWinPcWords + 1) : 1];
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return false;
+  uint16_t* const pcj = s_pc + (PC ? j * (kWinPcWords + 1) : 0);   // this pod's counts (its thread only)
+  if (PC && j < nb) {
+    const uint64_t* m = amask + (size_t)j * n_words;
+    int32_t acc = 0;
+#pragma unroll 8
+    for (int32_t w = 0; w < n_words; w++) {
+      pcj[w] = (uint16_t)acc;
+      acc += __popcll(m[w]);
+    }
+    pcj[n_words] = (uint16_t)acc;
+  }
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
   for (int round = 0; round < kWindowRounds; round++) {
-    cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
+    if constexpr (PC) cut = j < nb ? find_cut_pc(amask + (size_t)j * n_words, pcj, n_words, s, n, k) : -1;
+    else cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
     const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
     // exclusive prefix sum of the processed counts
     int64_t x = proc;
@@ -238,12 +281,13 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
 
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
+template <bool PC = false>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ amask, int32_t n_words,
                                                              int32_t n, int32_t k, int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ aexact) {
   int32_t s, cut, exact;
-  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact)) return;
+  if (!window_block<PC>(st, amask, n_words, n, k, &s, &cut, &exact)) return;
   const int j = threadIdx.x;
   if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
@@ -826,8 +870,15 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   k_adapt_mask_ns<<<dim3((n_words + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st,
                                                                                           a.s.amask, n_words, mp);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  const bool win_fused = window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
-  if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  // generic runs on small clusters: the prefix-count windows as their own
+  // launch (KSIM_WIN_NO_PC=1: the fused scan, A/B)
+  static const bool no_pc = getenv("KSIM_WIN_NO_PC") != nullptr;
+  const bool win_pc = !a.fast && !no_pc && n_words <= kWinPcWords;
+  const bool win_fused = !win_pc && window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
+  if (win_pc)
+    k_adapt_window<true><<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  else if (!win_fused)
+    k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)

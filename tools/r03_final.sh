@@ -13,9 +13,10 @@ tail -c 300 "$OUT/bench_default.json"; echo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- \
   python3 -u bench.py --no-cpu > "$OUT/bench_rocprof.json" 2> "$OUT/bench_rocprof.err" || exit $?
 find "$OUT/stats" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats_config2.csv" \;
-for c in ${CONFIGS:-1 3 4a 5 2a}; do
+for c in ${CONFIGS:-1 1a 3 4a 5 2a}; do
   case $c in
     1) args="--config 1 --steps 3 --warmup 1" ;;
+    1a) args="--config 1 --mode adapt --steps 2 --warmup 1" ;;
     3) args="--config 3 --steps 3 --warmup 1" ;;
     4a) args="--config 4 --mode adapt --steps 2 --warmup 1" ;;
     5) args="--config 5 --steps 1 --warmup 1" ;;

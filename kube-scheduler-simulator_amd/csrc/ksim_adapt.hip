@@ -210,6 +210,19 @@ __device__ __forceinline__ int32_t find_cut_pc(const uint64_t* __restrict__ mask
 }
 
 constexpr int kWindowRounds = 48;
+// PC windows, A/B builds: at most KSIM_WIN_PC_ROUNDS relaxation rounds, then
+// thread 0 extends the exact prefix pod by pod (the first inexact pod's start
+// is exact: every earlier processed count is) for up to KSIM_WIN_SEQ pods.
+// Off by default: on config 1 under ADAPT the batches end at broken windows
+// near where the relaxation's prefix ends, so 64 more exact windows cut 775
+// batches to 687 while the window launch grew from 162 to 246 us (184 -> 222
+// ms per step; 256 after 8 rounds: 259 ms; profiles/r03/ab_winseq)
+#ifndef KSIM_WIN_SEQ
+#define KSIM_WIN_SEQ 0
+#endif
+#ifndef KSIM_WIN_PC_ROUNDS
+#define KSIM_WIN_PC_ROUNDS 48
+#endif
 constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length   // exact prefix kept if not converged by then
 
 // The windows of one batch in one block of kBatchPods threads (thread j = pod
@@ -242,7 +255,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
-  for (int round = 0; round < kWindowRounds; round++) {
+  for (int round = 0; round < (PC ? KSIM_WIN_PC_ROUNDS : kWindowRounds); round++) {
     if constexpr (PC) cut = j < nb ? find_cut_pc(amask + (size_t)j * n_words, pcj, n_words, s, n, k) : -1;
     else cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
     const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
@@ -272,6 +285,32 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
     }
     exact = f;                                       // pods < f: start and cut exact
     if (j >= f) s = ns;                              // pods <= f now hold exact starts
+  }
+  if constexpr (PC && KSIM_WIN_SEQ > 0) {
+    if (exact < nb) {                                // block-uniform
+      __shared__ int32_t s_ws[kBatchPods], s_wc[kBatchPods];
+      __shared__ int32_t s_end;
+      if (j == exact) s_ws[j] = s;                   // its exact start
+      __syncthreads();
+      if (j == 0) {
+        int32_t x = exact, sx = s_ws[exact];
+        const int32_t lim = min(nb, exact + KSIM_WIN_SEQ);
+        for (; x < lim; x++) {
+          const int32_t cx = find_cut_pc(amask + (size_t)x * n_words, s_pc + x * (kWinPcWords + 1), n_words, sx, n, k);
+          s_ws[x] = sx;
+          s_wc[x] = cx;
+          sx = (int32_t)(((int64_t)sx + (cx >= 0 ? cx : n)) % n);
+        }
+        s_end = x;
+      }
+      __syncthreads();
+      const int32_t e = s_end;
+      if (j >= exact && j < e) {
+        s = s_ws[j];
+        cut = s_wc[j];
+      }
+      exact = e;
+    }
   }
   *s_out = s;
   *cut_out = cut;

@@ -921,7 +921,10 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
-  if (k >= kTopWideK) {
+  // PC windows (generic runs): 1,024 threads per pod as for long windows
+  // (KSIM_ADAPT_TOP_NARROW=1: 256, A/B)
+  static const bool narrow = getenv("KSIM_ADAPT_TOP_NARROW") != nullptr;
+  if (k >= kTopWideK || (win_pc && !narrow)) {
     if (a.fast) TOP(true, 1024, false);
     else TOP(false, 1024, false);
   } else if (win_fused) {

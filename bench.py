@@ -59,22 +59,17 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
     the node rows an evaluation kernel must read once per pod it evaluates;
     the small bookkeeping kernels are priced by the keys they move."""
     B, T = geom["pods_per_batch"], geom["top_t"]
-    tiles = (n_nodes + geom["tile_nodes"] - 1) // geom["tile_nodes"]
     if name == "k_filter_score":
         return B_EVAL * n_nodes                       # one node row per pod x node eval
     if name == "k_extrema":
         return n_nodes * (1 + 8 * n_norm)             # fail code + normalized raws
     if name == "k_select":
         return n_nodes * (1 + 8 + 8 * n_norm)         # fail code + partial total + normalized raws
-    if name in ("k_batch_top", "k_batch_eval"):
+    if name == "k_batch_top":
         return B_EVAL * n_nodes * B                   # B pods x N nodes evals per launch
     if name == "k_batch_top_commit":                  # the evaluation + the previous batch's commit
         return B_EVAL * n_nodes * B + 8 * B * 3
-    if name == "k_batch_merge":
-        return 8 * B * (tiles * geom["tile_cand"] + T)
-    if name == "k_batch_chain":
-        return 8 * B * T * 2
-    if name in ("k_batch_pairs", "k_batch_chain_pairs"):  # the fused form runs the chain inside this launch
+    if name == "k_batch_chain_pairs":                 # the chain runs inside every pairs block
         return B * (B - 1) // 2 * B_EVAL + 8 * B * T * 2   # one bound-row re-eval per pod pair + the lists
     if name.startswith("k_tb_"):                      # topology batches: Bt pods per launch on average
         bt = geom.get("tb_pods_per_batch", 1.0)
@@ -98,7 +93,7 @@ def kernel_alg_bytes(name: str, n_nodes: int, n_norm: int, geom: dict) -> int:
 
 
 # the kernel that carries the pod x node evaluations on each path
-EVAL_KERNELS = ("k_batch_top_commit", "k_batch_top", "k_batch_eval", "k_adapt_top", "k_tb_filter", "k_filter_score")
+EVAL_KERNELS = ("k_batch_top_commit", "k_batch_top", "k_adapt_top", "k_tb_filter", "k_filter_score")
 
 
 def _profile_entry(fname: str, kernel: str, nodes: int, config: int):

@@ -4,7 +4,7 @@
 // scans nodes in nodeTree order from nextStartNodeIndex and keeps the first K =
 // numFeasibleNodesToFind(N) feasible ones; the scan start of pod i+1 is pod i's
 // start plus the nodes pod i processed.  For a batch of B
-// batchable pods (same class of pods as ksim_batch.hip) six launches give the
+// batchable pods (same class of pods as ksim_batch.hip) five launches give the
 // placements of the pod-by-pod cycle, bit-exact:
 //
 //   k_adapt_mask    grid (64-node words, pods): the S0 feasibility bitmap of
@@ -18,8 +18,8 @@
 //                   round extends the exact prefix; a fixpoint is exact.
 //   k_adapt_top     one block per pod: TB keys of the kept nodes (the first K
 //                   feasible of its window), the pod's exact top-T.
-//   k_batch_chain   the greedy chain of ksim_batch.hip on those lists.
-//   k_adapt_pairs   block j, thread k < j: pod j on pod k's guessed node once pod
+//   k_adapt_pairs   every block runs the greedy chain of ksim_batch.hip on those
+//                   lists; then block j, thread k < j: pod j on pod k's guessed node once pod
 //                   k is bound there, if the node lies in pod j's window: the key
 //                   (M_j = max) and whether a node feasible under S0 became
 //                   infeasible at or before the cut ("broken": pod j's window, and
@@ -142,11 +142,8 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
 // Eight word segments per step: their loads do not depend on the counts, so
 // they go out together (one memory round trip per 512 nodes scanned instead of
 // one per 64).
-#ifndef KSIM_WIN_AHEAD
-#define KSIM_WIN_AHEAD 8
-#endif
 __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_t n, int32_t k) {
-  constexpr int kAhead = KSIM_WIN_AHEAD;             // bitmap words per step (their loads are independent)
+  constexpr int kAhead = 8;                          // bitmap words per step (their loads are independent)
   int32_t need = k, off = 0, pos = s;
   while (off < n) {
     uint64_t bits[kAhead];
@@ -210,20 +207,7 @@ __device__ __forceinline__ int32_t find_cut_pc(const uint64_t* __restrict__ mask
 }
 
 constexpr int kWindowRounds = 48;
-// PC windows, A/B builds: at most KSIM_WIN_PC_ROUNDS relaxation rounds, then
-// thread 0 extends the exact prefix pod by pod (the first inexact pod's start
-// is exact: every earlier processed count is) for up to KSIM_WIN_SEQ pods.
-// Off by default: on config 1 under ADAPT the batches end at broken windows
-// near where the relaxation's prefix ends, so 64 more exact windows cut 775
-// batches to 687 while the window launch grew from 162 to 246 us (184 -> 222
-// ms per step; 256 after 8 rounds: 259 ms; profiles/r03/ab_winseq)
-#ifndef KSIM_WIN_SEQ
-#define KSIM_WIN_SEQ 0
-#endif
-#ifndef KSIM_WIN_PC_ROUNDS
-#define KSIM_WIN_PC_ROUNDS 48
-#endif
-constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length   // exact prefix kept if not converged by then
+constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length
 
 // The windows of one batch in one block of kBatchPods threads (thread j = pod
 // j): *s_out = pod j's scan start, *cut_out = its cut offset (-1: no cut),
@@ -255,7 +239,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
-  for (int round = 0; round < (PC ? KSIM_WIN_PC_ROUNDS : kWindowRounds); round++) {
+  for (int round = 0; round < kWindowRounds; round++) {
     if constexpr (PC) cut = j < nb ? find_cut_pc(amask + (size_t)j * n_words, pcj, n_words, s, n, k) : -1;
     else cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
     const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
@@ -285,32 +269,6 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
     }
     exact = f;                                       // pods < f: start and cut exact
     if (j >= f) s = ns;                              // pods <= f now hold exact starts
-  }
-  if constexpr (PC && KSIM_WIN_SEQ > 0) {
-    if (exact < nb) {                                // block-uniform
-      __shared__ int32_t s_ws[kBatchPods], s_wc[kBatchPods];
-      __shared__ int32_t s_end;
-      if (j == exact) s_ws[j] = s;                   // its exact start
-      __syncthreads();
-      if (j == 0) {
-        int32_t x = exact, sx = s_ws[exact];
-        const int32_t lim = min(nb, exact + KSIM_WIN_SEQ);
-        for (; x < lim; x++) {
-          const int32_t cx = find_cut_pc(amask + (size_t)x * n_words, s_pc + x * (kWinPcWords + 1), n_words, sx, n, k);
-          s_ws[x] = sx;
-          s_wc[x] = cx;
-          sx = (int32_t)(((int64_t)sx + (cx >= 0 ? cx : n)) % n);
-        }
-        s_end = x;
-      }
-      __syncthreads();
-      const int32_t e = s_end;
-      if (j >= exact && j < e) {
-        s = s_ws[j];
-        cut = s_wc[j];
-      }
-      exact = e;
-    }
   }
   *s_out = s;
   *cut_out = cut;
@@ -586,10 +544,10 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
 
 // SH: windows and bitmaps are global; a shard scores only the guesses on its
 // own nodes; pmax[kBatchPods + j] carries the broken flag (all-reduced with M).
-// CHAIN: every block runs the chain itself from the top-T lists (as
+// Every block runs the chain itself from the top-T lists (as
 // k_batch_chain_pairs on the P100 path); block 0 stores gkey / chain_end for
-// the commit.  Otherwise the guesses come from k_batch_chain.
-template <bool SH, bool CHAIN, bool LAZY = false>
+// the commit.
+template <bool SH, bool LAZY = false>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPods P,
                                                             const ksim_profile* __restrict__ prof_p,
                                                             const BatchProg* __restrict__ bp_p,
@@ -617,18 +575,13 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   const int j = blockIdx.x, k = tid;
   int32_t nchain;
   uint64_t gk;
-  if constexpr (CHAIN) {
+  {
     __shared__ ChainLds L;
-    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr, kBatchPods,
-                     KSIM_CHAIN_DIRECT ? c.n_total : 0))
-      return;
+    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr, kBatchPods, c.n_total)) return;
     if (j == 0) {
       if (k < nb) gkey[k] = gk;
       if (k == 0) *chain_end = nchain;
     }
-  } else {
-    nchain = *chain_end;
-    gk = gkey[k];
   }
   uint64_t v = 0;
   bool brk = false;
@@ -892,14 +845,7 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
 }
 
 const char* const kAdaptKernelNames[kKernelsPerAdapt] = {"k_adapt_mask", "k_adapt_window", "k_adapt_top",
-                                                         "k_batch_chain", "k_adapt_pairs", "k_adapt_commit"};
-
-// A/B switch (read once per process): KSIM_WINDOW_SEPARATE=1 launches the
-// window scan as its own one-block kernel at every cluster size.
-static bool window_fused() {
-  static const bool separate = getenv("KSIM_WINDOW_SEPARATE") != nullptr;
-  return !separate;
-}
+                                                         "k_adapt_pairs", "k_adapt_commit"};
 
 uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const int32_t n_words = (a.c.n + 63) / 64;
@@ -909,11 +855,9 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   k_adapt_mask_ns<<<dim3((n_words + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st,
                                                                                           a.s.amask, n_words, mp);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  // generic runs on small clusters: the prefix-count windows as their own
-  // launch (KSIM_WIN_NO_PC=1: the fused scan, A/B)
-  static const bool no_pc = getenv("KSIM_WIN_NO_PC") != nullptr;
-  const bool win_pc = !a.fast && !no_pc && n_words <= kWinPcWords;
-  const bool win_fused = !win_pc && window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
+  // generic runs on small clusters: the prefix-count windows as their own launch
+  const bool win_pc = !a.fast && n_words <= kWinPcWords;
+  const bool win_fused = !win_pc && k < kTopWideK && n_words <= kWinFusedWords;
   if (win_pc)
     k_adapt_window<true><<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   else if (!win_fused)
@@ -922,9 +866,7 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
   // PC windows (generic runs): 1,024 threads per pod as for long windows
-  // (KSIM_ADAPT_TOP_NARROW=1: 256, A/B)
-  static const bool narrow = getenv("KSIM_ADAPT_TOP_NARROW") != nullptr;
-  if (k >= kTopWideK || (win_pc && !narrow)) {
+  if (k >= kTopWideK || win_pc) {
     if (a.fast) TOP(true, 1024, false);
     else TOP(false, 1024, false);
   } else if (win_fused) {
@@ -936,25 +878,14 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   }
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
-  if (chain_fused()) {                               // the chain inside the pairs launch, timed in its slot
-    if (evs) (void)hipEventRecord(evs[4], stream);
-    k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-        a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-        a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken, a.s.pnorm);
-  } else {
-    launch_chain(a, stream);
-    if (evs) (void)hipEventRecord(evs[4], stream);
-    k_adapt_pairs<false, false><<<kBatchPods, kBatchPods, 0, stream>>>(
-        a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, nullptr, nullptr, nullptr, a.s.gkey,
-        a.s.chain_end, a.s.pmax, a.s.abroken, a.s.pnorm);
-  }
-  if (evs) (void)hipEventRecord(evs[5], stream);
+  k_adapt_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(
+      a.c, a.P, a.dprof, a.dbp, a.st, a.s.amask, n_words, a.s.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
+      a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken, a.s.pnorm);
+  if (evs) (void)hipEventRecord(evs[4], stream);
   k_adapt_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.s.abroken,
                                                a.s.awin, a.chosen);
-  if (evs) (void)hipEventRecord(evs[6], stream);
-  uint32_t mask = chain_fused() ? 0x37u : 0x3fu;   // fused: the chain slot is an empty event pair
-  if (win_fused) mask &= ~0x2u;                   // likewise the window slot
-  return mask;
+  if (evs) (void)hipEventRecord(evs[5], stream);
+  return win_fused ? 0x1du : 0x1fu;                 // fused: the window slot is an empty event pair
 }
 
 const char* const kLazyAdaptKernelNames[kKernelsPerLazyAdapt] = {"k_adapt_mask_commit", "k_adapt_window",
@@ -980,7 +911,7 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   if (evs) (void)hipEventRecord(evs[0], stream);
   launch_adapt_mask_commit(z, false, stream);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  const bool win_fused = window_fused() && k < kTopWideK && n_words <= kWinFusedWords;
+  const bool win_fused = k < kTopWideK && n_words <= kWinFusedWords;
   if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
   // every later launch reads X[p] (z.cw) and st[p]
@@ -991,7 +922,7 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   else TOP(256, false);
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
-  k_adapt_pairs<false, true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+  k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
       z.cw, a.P, a.dprof, a.dbp, z.st, a.s.amask, n_words, z.awin, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey,
       z.cend, z.pmax, z.abroken);
   if (evs) (void)hipEventRecord(evs[4], stream);
@@ -1048,17 +979,9 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
 void launch_adapt_sh_pairs(const LaunchArgs& a, const uint64_t* gmask, int32_t world, hipStream_t stream) {
   const int32_t nw = (a.c.n_total + 63) / 64;
   k_batch_gmerge_launch(a, world, stream);
-  if (chain_fused()) {
-    k_adapt_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw,
-                                                                     a.s.awin, a.s.topk, a.s.topk_cnt,
-                                                                     a.s.topk_complete, a.s.gkey, a.s.chain_end,
-                                                                     a.s.pmax, nullptr);
-  } else {
-    launch_chain(a, stream);
-    k_adapt_pairs<true, false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw,
-                                                                      a.s.awin, nullptr, nullptr, nullptr, a.s.gkey,
-                                                                      a.s.chain_end, a.s.pmax, nullptr);
-  }
+  k_adapt_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, nw, a.s.awin,
+                                                              a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                                              a.s.chain_end, a.s.pmax, nullptr);
 }
 
 void launch_adapt_sh_commit(const LaunchArgs& a, hipStream_t stream) {

@@ -1,23 +1,23 @@
 // ksim_batch.hip — the speculative batch path of the scheduling cycle (gfx950).
 //
 // For B = kBatchPods consecutive pods of the queue that are "batchable" (P100,
-// every normalized score constant over nodes, no scalar requests; see
-// pod_batchable in ksim_engine.cpp), placements equal running the cycle pod by
-// pod (bit-exact with the oracle), in five launches per batch:
+// see pod_batchable in ksim_engine.cpp), placements equal running the cycle
+// pod by pod (bit-exact with the oracle).  A batch is
 //
-//   k_batch_eval   grid (node tiles, pods): every pod x node pair against the
-//                  batch-start snapshot S0 — static filters, Fit filter,
-//                  LeastAllocated, BalancedAllocation, TB key.  A wave tile is
-//                  64 lanes x 4 nodes; each lane sorts its 4 keys and 4 rounds
-//                  of DPP wave-max keep the tile's 4 best keys.
-//   k_batch_merge  one wave per pod: merge the sorted tile lists into the
-//                  pod's top-T under S0 (a prefix that is provably exact).
-//   k_batch_chain  one block: the greedy chain — pod i guesses the first entry
-//                  of its list not guessed by an earlier pod of the batch —
-//                  by parallel relaxation (see the kernel), keeping its exact prefix.
-//   k_batch_pairs  block j, thread k < j: key of pod j on pod k's guess after
-//                  pod k is bound there; the block max M_j.
-//   k_batch_commit one block: validates the chain and commits.
+//   k_batch_top          one block per pod: every pod x node pair against the
+//                        batch-start snapshot S0 (static filters, Fit filter,
+//                        LeastAllocated, BalancedAllocation, TB key) and the
+//                        pod's provably exact top-T under S0;
+//   k_batch_chain_pairs  one block per pod, every block running the greedy
+//                        chain (pod i guesses the first entry of its list not
+//                        guessed by an earlier pod of the batch; parallel
+//                        relaxation, ksim_chain.h), then block j, thread k < j:
+//                        key of pod j on pod k's guess after pod k is bound
+//                        there; the block max M_j;
+//   k_batch_commit       one block: validates the chain and commits
+//
+// or, on FAST runs of an unsharded handle, the deferred-commit form
+// (k_batch_top_commit: batch i-1's commit inside batch i's top launch).
 //
 // Exactness: pods 0..i-1 took their guesses (distinct nodes), so before pod i
 // only those nodes differ from S0.  Pod i's guess is the best node still at
@@ -34,90 +34,6 @@
 
 namespace ksim {
 
-// FAST: every pod of the run is trivial (host-proven static filters) and the
-// scoring strategies are {cpu, memory}: the loop reads the resource columns
-// and runs the cpu/memory key only (no static-filter or generic code, which
-// keeps the kernel small and its registers few).
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
-                                                    const BatchProg* __restrict__ bp_p,
-                                                    const DevState* __restrict__ st, uint64_t* __restrict__ cand,
-                                                    int32_t n_tiles) {
-  const ksim_profile& prof = *prof_p;   // device copies (ksim_set_profile): graphs outlive a weight change
-  const BatchProg& bp = *bp_p;
-  const int32_t base = st->cursor;
-  const int32_t end = min(st->end, base + kBatchPods);
-  const int32_t j = blockIdx.y;                      // one pod of the batch per grid row
-  const int32_t pi = base + j;
-  if (pi >= end) return;
-  const int lane = threadIdx.x & 63;
-  const int32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (tile >= n_tiles) return;                       // wave-uniform
-  const ksim_pod& p = P.pods[pi];
-  const bool trivial = (P.bflags[pi] & kBatchStaticTrivial) != 0;   // block-uniform
-  const int64_t seq = st->pod_seq + j;
-  // The lane's kNodesPerLane keys, kept sorted (descending) by insertion; the
-  // node loop is not unrolled so the kernel stays small (instruction cache).
-  uint64_t a[kTileCand] = {0, 0, 0, 0};
-  static_assert(kTileCand == 4, "insertion below is for 4 keys");
-  if constexpr (FAST) {
-    // the lane's kNodesPerLane keys as independent chains (every row load
-    // issued up front), then sorted in
-    const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
-    uint64_t kk[kNodesPerLane];
-    NodeRow rows[kNodesPerLane];
-    double ic[kNodesPerLane], im[kNodesPerLane];
-#pragma unroll
-    for (int k = 0; k < kNodesPerLane; k++) {
-      const int32_t node = tile * kTileNodes + k * 64 + lane;
-      const int32_t x = node < c.n ? node : c.n - 1;
-      rows[k] = load_res_row(c, x);
-      ic[k] = c.inv_cpu[x];
-      im[k] = c.inv_mem[x];
-    }
-    __builtin_amdgcn_sched_barrier(0);        // every row load in flight before the first key
-#pragma unroll
-    for (int k = 0; k < kNodesPerLane; k++) {
-      const int32_t node = tile * kTileNodes + k * 64 + lane;
-      kk[k] = node < c.n ? dyn_key_fast(bp, p, rows[k], ic[k], im[k], hseed, c.base + node) : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kNodesPerLane; k++) {
-      a[3] = umax64(a[3], kk[k]);
-      cswap_desc(a[2], a[3]);
-      cswap_desc(a[1], a[2]);
-      cswap_desc(a[0], a[1]);
-    }
-  }
-#pragma unroll 1
-  for (int k = 0; k < (FAST ? 0 : kNodesPerLane); k++) {
-    const int32_t node = tile * kTileNodes + k * 64 + lane;
-    uint64_t kk = 0;
-    if (node < c.n) {
-      // trivial: the static filters pass everywhere and the pod requests no
-      // scalar resources, so only the resource columns are read
-      const NodeRow r = trivial ? load_res_row(c, node) : load_row(c, node);
-      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
-    }
-    a[3] = umax64(a[3], kk);
-    cswap_desc(a[2], a[3]);
-    cswap_desc(a[1], a[2]);
-    cswap_desc(a[0], a[1]);
-  }
-  uint64_t* out = cand + ((size_t)j * n_tiles + tile) * kTileCand;
-#pragma unroll
-  for (int t = 0; t < kTileCand; t++) {
-    const uint64_t m = wave_max_u64_dpp(a[0]);
-    if (lane == 0) out[t] = m;
-    if (m != 0 && a[0] == m) {
-      a[0] = a[1];
-      a[1] = a[2];
-      a[2] = a[3];
-      a[3] = 0;
-    }
-  }
-}
-
 // ---- k_batch_top: evaluation and the pod's top-T in one launch -------------------
 // One block per pod of the batch (kTopThreads threads, kTopWaves waves: two per
 // SIMD when every CU holds one block), the nodes strided over its lanes.  Each
@@ -128,16 +44,7 @@ __global__ __launch_bounds__(256) void k_batch_eval(DevCluster c, DevPods P, con
 // the next key of its wave cannot be proven, so the wave's prefix ends there
 // (complete = 0); the block merge keeps the keys >= the last listed key of every
 // incomplete wave (every key a wave did not list is below it).  complete = 1:
-// every S0-feasible node is in the pod's list.  This replaces k_batch_eval's
-// per-tile lists and the k_batch_merge launch.
-#ifndef KSIM_TOP_STEP
-#define KSIM_TOP_STEP 1
-#endif
-#ifndef KSIM_TOP_THRESH
-#define KSIM_TOP_THRESH 1   // the threshold top-T (0: the round-by-round extraction and block merge, for A/B)
-#endif
-constexpr int kTopStep = KSIM_TOP_STEP;   // nodes per lane per step of the FAST loop
-
+// every S0-feasible node is in the pod's list.
 
 // The pod's top-T from the lanes' kept keys (a[]: the lane's best kTileCand
 // keys, descending; nfeas: the lane's feasible nodes), written to topk[j] (and
@@ -151,8 +58,7 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   __shared__ uint64_t s_list[kTopWaves][kTopT];
   __shared__ int32_t s_cnt[kTopWaves], s_complete[kTopWaves];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#if KSIM_TOP_THRESH
-  // ---- the pod's top-T by threshold (default) ------------------------------
+  // ---- the pod's top-T by threshold ----------------------------------------
   // Provability: a lane that had more feasible nodes than it kept hides keys
   // below its last kept key, so every key >= thr (the largest such key over
   // the block; 0 when no lane overflowed) is in the exact order.  Pruning:
@@ -235,7 +141,6 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
       return;
     }
   }
-#endif
   // the wave's provable top-T prefix (lane t keeps key t)
   uint64_t mine = 0;
   int32_t cnt = 0, complete = 0, popped = 0;
@@ -549,334 +454,23 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     if constexpr (STAB) {
       stab_fast_keys<kTopThreads>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, nfeas, [](NodeRow&) {});
     } else {
-    // kTopStep nodes per step as independent chains (every row loaded up front)
 #pragma unroll 1
-    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopStep * kTopThreads) {
-      NodeRow r[kTopStep];
-      double ic[kTopStep], im[kTopStep];
-#pragma unroll
-      for (int u = 0; u < kTopStep; u++) {
-        const int32_t nu = node + u * kTopThreads;
-        const int32_t x = nu < c.eval_hi ? nu : node;
-        r[u] = load_res_row_off(c, x);
-        ic[u] = ld_off(c.inv_cpu, (uint32_t)x << 3);
-        im[u] = ld_off(c.inv_mem, (uint32_t)x << 3);
-      }
-      __builtin_amdgcn_sched_barrier(0);      // every row in flight before the first key
-#pragma unroll
-      for (int u = 0; u < kTopStep; u++) {
-        const int32_t nu = node + u * kTopThreads;
-        // computed for every slot (a slot past the range keys a valid node) and masked
-        const uint64_t k0 = dyn_key_fast(bq, pf, r[u], ic[u], im[u], hseed, c.base + (nu < c.eval_hi ? nu : node));
-        const uint64_t k = nu < c.eval_hi ? k0 : 0;
-        nfeas += k != 0;
-        a[3] = umax64(a[3], k);
-        cswap_desc(a[2], a[3]);
-        cswap_desc(a[1], a[2]);
-        cswap_desc(a[0], a[1]);
-      }
+    for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
+      const NodeRow r = load_res_row_off(c, node);
+      const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
+      __builtin_amdgcn_sched_barrier(0);      // the row in flight before the key
+      const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+      nfeas += k != 0;
+      a[3] = umax64(a[3], k);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
     }
     }
   }
   if constexpr (!FAST)                        // the generic loop is not compiled into FAST kernels
     generic_keys<kTopThreads>(c, P, prof, bp, p, pi, j, seq, trivial, pnorm, a, nfeas, [](NodeRow&) {});
   top_finish<kTopThreads>(a, nfeas, j, topk, topk_cnt, topk_complete, xsend);
-}
-
-// ---- k_batch_top_ns: node-split, pod-grouped evaluation (FAST runs) ------------
-// The whole node table is read once per POD by k_batch_top (256 x 440 KB of L1
-// traffic per launch at 5,000 nodes, re-fetched past every XCD's L2 each batch:
-// latency-bound).  Here block (g, c) keys NP pods (g*NP ..) over node chunk c
-// of NP: a lane loads a node row once and keys it for the block's NP pods, so
-// a batch reads each row B / NP times, a lane holds about N / (1024 NP) rows,
-// and chunk c's blocks (blockIdx % NP) sit on the XCDs c, c + NP, ... (the
-// dispatcher deals workgroups to the 8 XCDs round-robin), each XCD's L2
-// holding one chunk of the table.  Each block writes, per pod, the provable
-// top-T prefix of its chunk (the threshold top-T of k_batch_top, with every
-// wave's contribution capped at its own top-T); the chain merges a pod's
-// chunk lists (ksim_chain.h load_merged_list).
-template <int NP>
-__global__ __launch_bounds__(1024) void k_batch_top_ns(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
-                                                       const BatchProg* __restrict__ bp_p,
-                                                       const DevState* __restrict__ st, uint64_t* __restrict__ ptopk,
-                                                       int32_t* __restrict__ pmeta) {
-  constexpr int kW = 16;                        // waves per block
-  constexpr int kCap = kW * kTopT;              // candidates per pod (each wave at most its top-T)
-  static_assert(kCap <= 128 && kTileCand == 4, "k_batch_top_ns geometry");
-  __shared__ uint64_t s_wmax[NP][kW], s_wthr[NP][kW];
-  __shared__ int32_t s_wf[NP][kW], s_wc[NP][kW];
-  __shared__ uint64_t s_cand[NP][kCap];
-  const int chunk = blockIdx.x % NP, grp = blockIdx.x / NP;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
-  const int32_t j0 = grp * NP;
-  if (j0 >= nb) return;                         // block-uniform
-  const int64_t seq0 = st->pod_seq;
-  const int32_t ne = c.eval_hi - c.eval_lo;
-  const int32_t lo = c.eval_lo + (int32_t)((int64_t)ne * chunk / NP);
-  const int32_t hi = c.eval_lo + (int32_t)((int64_t)ne * (chunk + 1) / NP);
-  const FastProg fp = fast_prog(*bp_p);
-  const uint64_t seed = prof_p->tiebreak_seed;
-  ksim_pod pf[NP];
-  uint64_t hseed[NP];
-  bool on[NP];
-#pragma unroll
-  for (int q = 0; q < NP; q++) {
-    on[q] = j0 + q < nb;
-    pf[q] = fast_pod_fields(P.pods[base + (on[q] ? j0 + q : j0)]);
-    hseed[q] = seed ^ ((uint64_t)(seq0 + j0 + q) << 20);
-  }
-  uint64_t a[NP][kTileCand];
-  int32_t nf[NP];
-#pragma unroll
-  for (int q = 0; q < NP; q++) {
-    nf[q] = 0;
-#pragma unroll
-    for (int e = 0; e < kTileCand; e++) a[q][e] = 0;
-  }
-#pragma unroll 1
-  for (int32_t node = lo + (int32_t)threadIdx.x; node < hi; node += 1024) {
-    const NodeRow r = load_res_row(c, node);
-    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
-#pragma unroll
-    for (int q = 0; q < NP; q++) {
-      const uint64_t k0 = dyn_key_fast(fp, pf[q], r, ic, im, hseed[q], c.base + node);
-      const uint64_t k = on[q] ? k0 : 0;
-      nf[q] += k != 0;
-      a[q][3] = umax64(a[q][3], k);
-      cswap_desc(a[q][2], a[q][3]);
-      cswap_desc(a[q][1], a[q][2]);
-      cswap_desc(a[q][0], a[q][1]);
-    }
-  }
-  // per pod: the waves' maxima, provability floors and feasible counts
-#pragma unroll
-  for (int q = 0; q < NP; q++) {
-    const uint64_t u = nf[q] > kTileCand ? a[q][kTileCand - 1] : 0;
-    const uint64_t wthr = wave_max_u64_dpp(u);
-    const uint64_t wmax = wave_max_u64_dpp(a[q][0]);
-    int32_t fsum = nf[q];
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) fsum += __shfl_xor(fsum, m, 64);
-    if (lane == 0) {
-      s_wmax[q][wv] = wmax;
-      s_wthr[q][wv] = wthr;
-      s_wf[q][wv] = fsum;
-    }
-  }
-  __syncthreads();
-  // per pod: cut = max(floor, T-th largest wave maximum); the lanes' prefixes
-  // >= cut, each wave's count capped at T
-  int32_t cl[NP], pre[NP], cw[NP], total[NP];
-  uint64_t thr[NP], cut[NP];
-#pragma unroll
-  for (int q = 0; q < NP; q++) {
-    const uint64_t mine_w = lane < kW ? s_wmax[q][lane] : 0;
-    thr[q] = 0;
-    total[q] = 0;
-    int32_t rank = 0;
-#pragma unroll
-    for (int w = 0; w < kW; w++) {
-      thr[q] = umax64(thr[q], s_wthr[q][w]);
-      total[q] += s_wf[q][w];
-      rank += s_wmax[q][w] > mine_w;
-    }
-    const uint64_t at = __ballot(lane < kW && mine_w != 0 && rank == kTopT - 1);
-    const uint64_t L = at ? readlane_u64(mine_w, __builtin_ctzll(at)) : 0;
-    cut[q] = umax64(umax64(thr[q], L), 1);
-    cl[q] = 0;
-#pragma unroll
-    for (int e = 0; e < kTileCand; e++) cl[q] += a[q][e] >= cut[q];
-    int32_t x = cl[q];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t y = __shfl_up(x, d, 64);
-      if (lane >= d) x += y;
-    }
-    pre[q] = x - cl[q];
-    cw[q] = __shfl(x, 63, 64);
-    if (lane == 0) s_wc[q][wv] = cw[q] < kTopT ? cw[q] : kTopT;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NP; q++) {
-    int32_t off = 0;
-#pragma unroll
-    for (int w = 0; w < kW; w++) off += w < wv ? s_wc[q][w] : 0;
-    if (cw[q] <= kTopT) {                       // wave-uniform: every key >= cut of the wave
-#pragma unroll
-      for (int e = 0; e < kTileCand; e++)
-        if (e < cl[q]) s_cand[q][off + pre[q] + e] = a[q][e];
-    } else {                                    // only the wave's top-T can reach the pod's top-T
-      for (int t = 0; t < kTopT; t++) {
-        const uint64_t m = wave_max_u64_dpp(a[q][0]);
-        if (lane == 0) s_cand[q][off + t] = m;
-        if (a[q][0] == m) {
-          a[q][0] = a[q][1];
-          a[q][1] = a[q][2];
-          a[q][2] = a[q][3];
-          a[q][3] = 0;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (wv >= NP) return;
-  // wave q ranks pod q's candidates (distinct keys: distinct ranks)
-  const int q = wv;
-  const int32_t j = j0 + q;
-  if (j >= nb) return;
-  int32_t C = 0;
-  uint64_t tq = 0;
-  int32_t totq = 0;
-#pragma unroll
-  for (int w = 0; w < kW; w++) C += s_wc[q][w];
-#pragma unroll
-  for (int qq = 0; qq < NP; qq++)
-    if (qq == q) {
-      tq = thr[qq];
-      totq = total[qq];
-    }
-  const uint64_t c0 = lane < C ? s_cand[q][lane] : 0, c1 = 64 + lane < C ? s_cand[q][64 + lane] : 0;
-  int32_t r0 = 0, r1 = 0;
-  for (int x = 0; x < C; x++) {
-    const uint64_t v = s_cand[q][x];
-    r0 += v > c0;
-    r1 += v > c1;
-  }
-  uint64_t* out = ptopk + ((size_t)chunk * kBatchPods + j) * kTopT;
-  const int32_t n_out = C < kTopT ? C : kTopT;
-  if (lane < C && r0 < kTopT) out[r0] = c0;
-  if (64 + lane < C && r1 < kTopT) out[r1] = c1;
-  if (lane >= n_out && lane < kTopT) out[lane] = 0;
-  if (lane == 0) pmeta[chunk * kBatchPods + j] = n_out | (((tq == 0 && totq <= kTopT) ? 1 : 0) << 8);
-}
-
-// A tile list holds only its best kTileCand keys: once one is fully consumed
-// the merge can no longer prove the next key, so the prefix ends there
-// (complete = 0).  complete = 1: every S0-feasible node is listed.
-__global__ __launch_bounds__(256) void k_batch_merge(const DevState* __restrict__ st,
-                                                     const uint64_t* __restrict__ cand, int32_t n_tiles,
-                                                     uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
-                                                     int32_t* __restrict__ topk_complete,
-                                                     uint64_t* __restrict__ xsend) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t s_m[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int32_t j = blockIdx.x * 4 + w;               // < kBatchPods: the grid is kBatchPods / 4 blocks
-  const int32_t per = n_tiles * kTileCand;
-  uint64_t* lst = s_m + (size_t)w * (per + (n_tiles + 7) / 8);
-  uint8_t* head = reinterpret_cast<uint8_t*>(lst + per);
-  const uint64_t* src = cand + (size_t)j * per;
-  for (int x = lane; x < per; x += 64) lst[x] = src[x];   // issued before the state load it does not need
-  for (int l = lane; l < n_tiles; l += 64) head[l] = 0;
-  const int32_t base = st->cursor;
-  if (base + j >= min(st->end, base + kBatchPods)) return;   // wave-uniform; no block barrier below
-  wave_lds_sync();
-  uint64_t mine = 0;                                 // lane t keeps merged key t
-  int32_t cnt = 0, complete = 0;
-  for (int t = 0; t < kTopT; t++) {
-    uint64_t best = 0;
-    int32_t bl = -1;
-    for (int l = lane; l < n_tiles; l += 64) {
-      const int h = head[l];
-      const uint64_t v = h < kTileCand ? lst[l * kTileCand + h] : 0;
-      if (v > best) { best = v; bl = l; }
-    }
-    const uint64_t m = wave_max_u64_dpp(best);
-    if (m == 0) { complete = 1; break; }
-    if (lane == t) mine = m;
-    cnt = t + 1;
-    bool stop = false;
-    if (best == m) {
-      const int h = ++head[bl];
-      stop = h == kTileCand;
-    }
-    if (__ballot(stop)) break;
-    wave_lds_sync();
-  }
-  if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
-  if (lane == 0) {
-    topk_cnt[j] = cnt;
-    topk_complete[j] = complete;
-  }
-  if (xsend) {                                       // sharded: this shard's record for the all-gather
-    uint64_t* x = xsend + (size_t)j * kXRec;
-    if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
-    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)cnt | ((uint64_t)complete << 32);
-  }
-}
-
-// The same merge with the pod's tile lists in registers (n_tiles * kTileCand
-// <= 64 * NREG, e.g. 5,000 nodes: 80 keys, NREG = 2), one 64-lane block per
-// pod.  Key x = s * 64 + lane is entry x % kTileCand of tile x / kTileCand.
-// Tile lists are sorted and keys are distinct (the node is in the key), so
-// the max over all remaining keys is the max over the tile heads the LDS
-// version scans; consuming entry kTileCand - 1 of a tile ends the prefix.
-template <int NREG>
-__global__ __launch_bounds__(64) void k_batch_merge_reg(const DevState* __restrict__ st,
-                                                        const uint64_t* __restrict__ cand, int32_t n_tiles,
-                                                        uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
-                                                        int32_t* __restrict__ topk_complete,
-                                                        uint64_t* __restrict__ xsend) {
-  const int lane = threadIdx.x;
-  const int32_t j = blockIdx.x;
-  const int32_t per = n_tiles * kTileCand;
-  const uint64_t* src = cand + (size_t)j * per;
-  uint64_t v[NREG];
-#pragma unroll
-  for (int s = 0; s < NREG; s++) v[s] = s * 64 + lane < per ? src[s * 64 + lane] : 0;   // before the state load
-  const int32_t base = st->cursor;
-  if (base + j >= min(st->end, base + kBatchPods)) return;   // block-uniform
-  uint64_t mine = 0;
-  int32_t cnt = 0, complete = 0;
-  for (int t = 0; t < kTopT; t++) {
-    uint64_t best = v[0];
-#pragma unroll
-    for (int s = 1; s < NREG; s++) best = umax64(best, v[s]);
-    const uint64_t m = wave_max_u64_dpp(best);
-    if (m == 0) { complete = 1; break; }
-    if (lane == t) mine = m;
-    cnt = t + 1;
-    bool stop = false;
-    if (best == m) {
-#pragma unroll
-      for (int s = 0; s < NREG; s++)
-        if (v[s] == m) {
-          v[s] = 0;
-          stop = ((s * 64 + lane) % kTileCand) == kTileCand - 1;
-        }
-    }
-    if (__ballot(stop)) break;
-  }
-  if (lane < kTopT) topk[(size_t)j * kTopT + lane] = lane < cnt ? mine : 0;
-  if (lane == 0) {
-    topk_cnt[j] = cnt;
-    topk_complete[j] = complete;
-  }
-  if (xsend) {
-    uint64_t* x = xsend + (size_t)j * kXRec;
-    if (lane < kTopT) x[lane] = lane < cnt ? mine : 0;
-    if (lane == 0) x[kTopT] = (uint64_t)(uint32_t)cnt | ((uint64_t)complete << 32);
-  }
-}
-
-// Merge launcher: registers for small tile counts, LDS otherwise.
-static void launch_merge(const DevState* st, const uint64_t* cand, int32_t n_tiles, uint64_t* topk,
-                         int32_t* topk_cnt, int32_t* topk_complete, uint64_t* xsend, hipStream_t stream) {
-  const int32_t per = n_tiles * kTileCand;
-  static const bool force_lds = getenv("KSIM_MERGE_LDS") != nullptr;   // A/B switch
-  if (force_lds || per > 256) {
-    const size_t per_wave = (size_t)per * 8 + (size_t)((n_tiles + 7) / 8) * 8;
-    k_batch_merge<<<kBatchPods / 4, 256, 4 * per_wave, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete,
-                                                                 xsend);
-  } else if (per <= 64) {
-    k_batch_merge_reg<1><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
-  } else if (per <= 128) {
-    k_batch_merge_reg<2><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
-  } else {
-    k_batch_merge_reg<4><<<kBatchPods, 64, 0, stream>>>(st, cand, n_tiles, topk, topk_cnt, topk_complete, xsend);
-  }
 }
 
 // Sharded: merge the R shard records of pod j (all-gathered, [R][B][kXRec])
@@ -938,32 +532,6 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
     topk_cnt[j] = n;
     topk_complete[j] = (all_complete && nvalid <= kTopT) ? 1 : 0;
   }
-}
-
-// The greedy chain (pod i guesses the first entry of its list that no earlier
-// pod of the batch guessed), computed by parallel relaxation instead of 256
-// dependent steps: every pod holds a current guess; a round lets each pod
-// re-pick the first entry not held by an earlier pod under the previous
-// round's guesses.  Pod i's pick depends only on pods < i, so once pods
-// 0..q-1 are unchanged by a round they are exact (the serial chain's
-// result); the batch keeps that exact prefix.  Node ids are mapped to slots of
-// an LDS hash table, and "held by an earlier pod" is an LDS atomicMin of pod
-// indices per slot.  Rounds needed = the depth of the conflict chain.
-__global__ __launch_bounds__(kBatchPods) void k_batch_chain(const DevState* __restrict__ st,
-                                                            int32_t n_nodes /* global */,
-                                                            const uint64_t* __restrict__ topk,
-                                                            const int32_t* __restrict__ topk_cnt,
-                                                            const int32_t* __restrict__ topk_complete,
-                                                            uint64_t* __restrict__ gkey,
-                                                            int32_t* __restrict__ chain_end,
-                                                            unsigned long long* __restrict__ dbg) {
-  __shared__ ChainLds L;
-  uint64_t gk;
-  int32_t nchain;
-  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbg)) return;
-  const int32_t nb = min(kBatchPods, st->end - st->cursor);
-  if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
-  if (threadIdx.x == 0) *chain_end = nchain;
 }
 
 // Block j: pod j's pair keys on the guesses gk of threads k < j, max to pmax[j].
@@ -1075,28 +643,6 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
   }
 }
 
-// Block j (thread k < j): key of pod j on pod k's guessed node once pod k is
-// bound there; M_j = the block max.  Sharded, each shard scores the guesses
-// it owns and M is all-reduced (max) before k_batch_commit.  FAST: as in
-// k_batch_eval (trivial pods, cpu/memory scoring).
-template <bool FAST>
-__global__ __launch_bounds__(kBatchPods) void k_batch_pairs(DevCluster c, DevPods P,
-                                                            const ksim_profile* __restrict__ prof_p,
-                                                            const BatchProg* __restrict__ bp_p,
-                                                            const DevState* __restrict__ st,
-                                                            const uint64_t* __restrict__ gkey,
-                                                            const int32_t* __restrict__ chain_end,
-                                                            uint64_t* __restrict__ pmax, const int64_t* __restrict__ pnorm,
-                                                            int32_t* __restrict__ pinv) {
-  __shared__ uint64_t s_wmax[kBatchPods / 64];
-  __shared__ int32_t s_winv[kBatchPods / 64];
-  const uint64_t gk = gkey[threadIdx.x];             // in flight with the state loads
-  const int32_t nchain = *chain_end;
-  const int32_t nb = min(kBatchPods, st->end - st->cursor);
-  if (nb <= 0) return;
-  pairs_block<FAST>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, nullptr, nullptr, pnorm, pinv, s_winv);
-}
-
 // The chain and the pair keys in one launch: every block of the pairs grid
 // runs the (deterministic) chain itself, thread k ending with pod k's guess in
 // a register, so the pairs need no chain launch and no gkey round trip.
@@ -1114,7 +660,7 @@ unsigned long long* cp_clock_buffer() { return nullptr; }
 
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
-template <bool FAST, int NCHUNK = 0, bool LAZY = false, bool STAB = false>
+template <bool FAST, bool LAZY = false, bool STAB = false>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -1149,9 +695,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
 #else
   unsigned long long* dbgc = nullptr;
 #endif
-  // NCHUNK > 0: topk / topk_cnt are the node-split top's chunk lists (k_batch_top_ns)
-  if (!chain_block<NCHUNK>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc, kBatchPods,
-                           KSIM_CHAIN_DIRECT ? c.n_total : 0)) {
+  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc, kBatchPods, c.n_total)) {
     if (LAZY && blockIdx.x == 0 && threadIdx.x == 0) *chain_end = -1;
     return;
   }
@@ -1212,11 +756,6 @@ void launch_static_table(const LaunchArgs& a, const int32_t* rep, int32_t n_cls,
 // S_{i-2}; a guess that was not bound keeps its value, so the superset is
 // harmless); block 0 writes the state after the commit to st[p].  FLUSH: no
 // evaluation, and slot i is marked empty.
-// KSIM_TOP_OFF32 (default 1): the node loop's row loads by 32-bit byte
-// offsets (0: 64-bit addresses per column, for A/B builds)
-#ifndef KSIM_TOP_OFF32
-#define KSIM_TOP_OFF32 1
-#endif
 constexpr int kLazyHash = 1 << kLazyHashBits;
 constexpr int kLazyBitWords = kLazyMaxNodes / 32;
 static_assert(kLazyHash >= 4 * kBatchPods && kBatchPods <= 1024, "overlay hash / block geometry");
@@ -1225,24 +764,15 @@ __device__ __forceinline__ uint32_t lazy_hash(int32_t node) {
   return ((uint32_t)node * 2654435761u) >> (32 - kLazyHashBits);
 }
 
-// FAST = false: generic pods (static filters, per-node normalized scores; no
-// scalar requests, no class adds), the keys of generic_keys with the overlay;
-// batch i-1's chain also ends before its first pinv pod (batch_commit).
-// (512 threads: the generic loop's registers)
-constexpr int lazy_threads(bool fast) { return fast ? 1024 : 512; }
-
-// STAB (FAST only): a static-class run (stab_fast_keys with the overlay; the
-// chain of batch i-1 also ends before its first pinv pod).
-template <bool FLUSH, bool FAST = true, bool STAB = false>
-__global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevCluster c, DevPods P,
+template <bool FLUSH>
+__global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
                                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
                                                            int32_t* __restrict__ topk_complete,
                                                            int32_t* __restrict__ chosen_out,
-                                                           uint64_t* __restrict__ xsend,
-                                                           int64_t* __restrict__ pnorm = nullptr) {
-  constexpr int kThreads = lazy_threads(FAST);
+                                                           uint64_t* __restrict__ xsend) {
+  constexpr int kThreads = 1024;
   static_assert(kThreads >= kBatchPods, "one thread per batch entry");
   __shared__ ResCols s_rq[kBatchPods];          // batch i-1's pod requests, then each bound node's delta
   __shared__ int32_t s_hkey[kLazyHash];         // overlay hash: local node or -1
@@ -1265,16 +795,7 @@ __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevClus
   const int nwords = (c.n + 31) >> 5;
   for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
   for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
-  int32_t nchain = e1 > 0 ? e1 : 0;            // -1: no batch i-1 (run start, a flush, past the end)
-  if constexpr (!FAST || STAB) {               // the chain ends before the first pinv pod
-    const int32_t inv = tid < nchain ? L.inv1[tid] : 0;
-    if (tid == 0) s_istar = nchain;
-    __syncthreads();
-    block_first_min(&s_istar, tid < nchain && inv);
-    __syncthreads();
-    nchain = s_istar;
-    __syncthreads();                           // every read of s_istar before it is reset below
-  }
+  const int32_t nchain = e1 > 0 ? e1 : 0;      // -1: no batch i-1 (run start, a flush, past the end)
   if (tid == 0) {
     s_istar = nchain;
     s_inode = -1;
@@ -1298,7 +819,7 @@ __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevClus
   const int32_t pi = base + b;
   const bool live = !FLUSH && pi < min(end, base + kBatchPods);   // block-uniform
   ksim_pod pf;
-  if (FAST && live) pf = fast_pod_fields(P.pods[pi]);
+  if (live) pf = fast_pod_fields(P.pods[pi]);
   __syncthreads();
   const int32_t inode = s_inode;
   // entry tid < i*: its guessed node takes pod tid, and pod i* when i* chose it
@@ -1397,46 +918,12 @@ __global__ __launch_bounds__(lazy_threads(FAST)) void k_batch_top_commit(DevClus
   // pod b of batch i against S_i (k_batch_top's loops with the overlay)
   uint64_t a[kTileCand] = {0, 0, 0, 0};
   int32_t nfeas = 0;
-  if constexpr (!FAST) {
-    generic_keys<kThreads>(c, P, *prof_p, *bp_p, P.pods[pi], pi, b, seq0 + committed + b,
-                           (P.bflags[pi] & kBatchStaticTrivial) != 0, pnorm, a, nfeas, [&](NodeRow& r) {
-                             const ResCols d = delta(r.node);
-                             r.req_cpu += d.cpu;
-                             r.req_mem += d.mem;
-                             r.req_eph += d.eph;
-                             r.nz_cpu += d.nzc;
-                             r.nz_mem += d.nzm;
-                             r.num_pods += d.pods;
-                           });
-    materialize();
-    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
-    return;
-  }
   const FastProg bq = fast_prog(*bp_p);
   const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
-  if constexpr (STAB) {
-    stab_fast_keys<kThreads>(c, P, *bp_p, bq, pf, pi, b, hseed, pnorm, a, nfeas, [&](NodeRow& r) {
-      const ResCols d = delta(r.node);
-      r.req_cpu += d.cpu;
-      r.req_mem += d.mem;
-      r.req_eph += d.eph;
-      r.nz_cpu += d.nzc;
-      r.nz_mem += d.nzm;
-      r.num_pods += d.pods;
-    });
-    materialize();
-    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
-    return;
-  }
 #pragma unroll 1
   for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
-#if KSIM_TOP_OFF32
     NodeRow r = load_res_row_off(c, node);
     const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
-#else
-    NodeRow r = load_res_row(c, node);
-    const double ic = c.inv_cpu[node], im = c.inv_mem[node];
-#endif
     const ResCols d = delta(node);
     r.req_cpu += d.cpu;
     r.req_mem += d.mem;
@@ -1461,30 +948,12 @@ const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
   const LaunchArgs& a = z.a;
   if (evs) (void)hipEventRecord(evs[0], stream);
-  if (a.stab)
-    k_batch_top_commit<false, true, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                           a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                           nullptr, a.s.pnorm);
-  else if (a.fast)
-    k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                               a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
-  else
-    k_batch_top_commit<false, false><<<kBatchPods, lazy_threads(false), 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                      a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                      nullptr, a.s.pnorm);
+  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                             a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  if (a.stab)
-    k_batch_chain_pairs<true, 0, true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
-        z.inv);
-  else if (a.fast)
-    k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
-        a.s.pinv);
-  else
-    k_batch_chain_pairs<false, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
-        z.inv);
+  k_batch_chain_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+      z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
+      a.s.pinv);
   if (evs) (void)hipEventRecord(evs[2], stream);
   return 0x3u;
 }
@@ -1508,24 +977,15 @@ void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream
   const LaunchArgs& a = z.a;
   k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
                                                      a.s.topk_complete);
-  k_batch_chain_pairs<true, 0, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
+  k_batch_chain_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk,
                                                                             a.s.topk_cnt, a.s.topk_complete, z.gkey,
                                                                             z.cend, z.pmax, a.s.pnorm, a.s.pinv);
 }
 
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
   const LaunchArgs& a = z.a;
-  if (a.stab)
-    k_batch_top_commit<true, true, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                          a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                          nullptr, a.s.pnorm);
-  else if (a.fast)
-    k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                              a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
-  else
-    k_batch_top_commit<true, false><<<kBatchPods, lazy_threads(false), 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                     a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                     nullptr, a.s.pnorm);
+  k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                            a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
 }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.
@@ -1536,195 +996,50 @@ __global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {
   for (int r = 0; r < g.n; r++) g.p[r][j] = m;
 }
 
-// k_batch_chain's phase clocks (diag "dbg" words 0-4) only when asked for
-// (KSIM_CHAIN_CLOCKS): the five device atomics sit at the end of every chain.
-static unsigned long long* chain_clock(const LaunchArgs& a) {
-  static const bool on = getenv("KSIM_CHAIN_CLOCKS") != nullptr;
-  return on ? a.s.dbg : nullptr;
-}
-
-const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch_merge", "k_batch_chain",
-                                                         "k_batch_pairs", "k_batch_commit"};
-
-// A/B switch (read once per process): the round-1 two-launch form, per-tile
-// lists (k_batch_eval) merged by k_batch_merge.
-static bool tile_eval() {
-  static const bool on = getenv("KSIM_BATCH_TILES") != nullptr;
-  return on;
-}
-
-// A/B switch (read once per process): KSIM_CHAIN_SEPARATE=1 launches the chain
-// as its own one-block kernel ahead of the pairs (the round-2 form).
-bool chain_fused() {
-  static const bool separate = getenv("KSIM_CHAIN_SEPARATE") != nullptr;
-  return !separate;
-}
+const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch_chain_pairs", "k_batch_commit"};
 
 // Evaluation and per-pod top-T (xsend: the sharded record, else null).
-static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream, hipEvent_t* mid = nullptr) {
-  if (tile_eval() && a.c.eval_lo == 0 && a.c.eval_hi == a.c.n) {   // the tile form evaluates every node
-    const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
-    const dim3 g1((n_tiles + 3) / 4, kBatchPods);
-    if (a.fast)
-      k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-    else
-      k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-    if (mid) (void)hipEventRecord(*mid, stream);
-    launch_merge(a.st, a.s.cand, n_tiles, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, stream);
-    return;
-  }
-  static const int threads = getenv("KSIM_TOP_THREADS") ? atoi(getenv("KSIM_TOP_THREADS")) : 1024;   // A/B
-#define TOP(F, T) k_batch_top<F, T><<<kBatchPods, T, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, \
-                                                                   a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm)
-  if (threads == 512) {
-    if (a.fast) TOP(true, 512);
-    else TOP(false, 512);
-  } else {
-    if (a.fast) TOP(true, 1024);
-    else TOP(false, 1024);
-  }
-#undef TOP
-  if (mid) (void)hipEventRecord(*mid, stream);
+static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream) {
+  if (a.stab)   // static-class runs (unsharded handles only: run_stab)
+    k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                    a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
+  else if (a.fast)
+    k_batch_top<true, 1024><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
+                                                              a.s.topk_complete, xsend, a.s.pnorm);
+  else
+    k_batch_top<false, 1024><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
+                                                               a.s.topk_complete, xsend, a.s.pnorm);
 }
 
-// Node chunks of the node-split top for this run (0 = k_batch_top, the
-// default).  KSIM_TOP_NS=2 / 4 selects it for FAST runs with the chain inside
-// the pairs launch (the chain merges the chunk lists).  Measured and not kept
-// (profiles/r03/ab_ns, config 2, same box): 4 chunks 10.37 ms per step, 2
-// chunks 8.15 ms, k_batch_top 7.80 ms -- the NP-pod register lists and the
-// per-pod reductions cost more than the shared row loads save, and the chain
-// pays the list merge.
-#ifndef KSIM_TOP_NS_DEFAULT
-#define KSIM_TOP_NS_DEFAULT 0   // the "ns4" flavor (tests/test_gpu_batch_ns.py) builds it with 4
-#endif
-int top_ns_chunks(const LaunchArgs& a) {
-  static const int force = getenv("KSIM_TOP_NS") ? atoi(getenv("KSIM_TOP_NS")) : KSIM_TOP_NS_DEFAULT;
-  if (!a.fast || !chain_fused() || chain_clock(a) || tile_eval()) return 0;
-  const int32_t ne = a.c.eval_hi - a.c.eval_lo;
-  return (force == 2 || force == 4) && ne >= 64 * force ? force : 0;
+// The chain inside every pairs block (k_batch_chain_pairs).
+static void launch_chain_pairs(const LaunchArgs& a, hipStream_t stream) {
+  if (a.stab)
+    k_batch_chain_pairs<true, false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey, a.s.chain_end, a.s.pmax,
+        a.s.pnorm, a.s.pinv);
+  else if (a.fast)
+    k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                     a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                                                     a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
+  else
+    k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
+                                                                      a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
+                                                                      a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
 }
-
-// Any A/B switch of the three-launch batch forms (tile lists, the separate
-// chain launch, chain clocks, the node-split top, the top's block size): those
-// runs keep the three-launch form, so the switch still selects what it names.
-bool batch_ab_forms() {
-  static const bool on = tile_eval() || !chain_fused() || getenv("KSIM_CHAIN_CLOCKS") || getenv("KSIM_TOP_NS") ||
-                         getenv("KSIM_TOP_THREADS") || KSIM_TOP_NS_DEFAULT != 0;
-  return on;
-}
-
-// (a template, so a -DKSIM_TOP_T=16 build, whose candidates overflow the
-// node-split geometry, compiles without it)
-template <int T>
-static void launch_top_ns_t(const LaunchArgs& a, int nch, hipStream_t stream) {
-  if constexpr (16 * T <= 128) {
-    if (nch == 4)
-      k_batch_top_ns<4><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
-    else
-      k_batch_top_ns<2><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.ptopk, a.s.pmeta);
-  }
-}
-static void launch_top_ns(const LaunchArgs& a, int nch, hipStream_t stream) { launch_top_ns_t<kTopT>(a, nch, stream); }
 
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   if (evs) (void)hipEventRecord(evs[0], stream);
-  if (a.stab) {   // static-class runs: the default forms only (the host checks batch_ab_forms)
-    k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                    a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm);
-    if (evs) (void)hipEventRecord(evs[1], stream);
-    if (evs) (void)hipEventRecord(evs[2], stream);
-    if (evs) (void)hipEventRecord(evs[3], stream);
-    k_batch_chain_pairs<true, 0, false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey, a.s.chain_end, a.s.pmax,
-        a.s.pnorm, a.s.pinv);
-    if (evs) (void)hipEventRecord(evs[4], stream);
-    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen, a.s.pinv);
-    if (evs) (void)hipEventRecord(evs[5], stream);
-    return 0x19u;
-  }
-  const int nch = top_ns_chunks(a);
-  if (nch) {
-    launch_top_ns(a, nch, stream);
-    if (evs) (void)hipEventRecord(evs[1], stream);
-  } else {
-    launch_eval_top(a, nullptr, stream, evs ? &evs[1] : nullptr);
-  }
-  if (evs) (void)hipEventRecord(evs[2], stream);
-  if (nch) {
-    if (evs) (void)hipEventRecord(evs[3], stream);
-#define CP(N) k_batch_chain_pairs<true, N><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
-                  a.s.ptopk, a.s.pmeta, nullptr, a.s.gkey, a.s.chain_end, a.s.pmax, \
-                  a.s.pnorm, a.s.pinv)
-    if (nch == 4) CP(4);
-    else CP(2);
-#undef CP
-    if (evs) (void)hipEventRecord(evs[4], stream);
-    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
-                                                 a.fast ? nullptr : a.s.pinv);
-    if (evs) (void)hipEventRecord(evs[5], stream);
-    return 0x19u;
-  }
-  if (chain_fused() && !chain_clock(a)) {
-    // the chain inside every pairs block (k_batch_chain_pairs), timed in the pairs slot
-    if (evs) (void)hipEventRecord(evs[3], stream);
-    if (a.fast)
-      k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                       a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                       a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
-    else
-      k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                        a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                        a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
-    if (evs) (void)hipEventRecord(evs[4], stream);
-    k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
-                                                 a.fast ? nullptr : a.s.pinv);
-    if (evs) (void)hipEventRecord(evs[5], stream);
-    return tile_eval() ? 0x1bu : 0x19u;
-  }
-  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, chain_clock(a));
-  if (evs) (void)hipEventRecord(evs[3], stream);
-  // pair keys, then a separate one-block commit: cheaper than every block of
-  // the pairs kernel fencing for a last-block election
-  if (a.fast)
-    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
-                                                               a.s.pmax, a.s.pnorm, a.s.pinv);
-  else
-    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
-                                                                a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
-  if (evs) (void)hipEventRecord(evs[4], stream);
-  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
-                                                 a.fast ? nullptr : a.s.pinv);
-  if (evs) (void)hipEventRecord(evs[5], stream);
-  return tile_eval() ? 0x1fu : 0x1du;   // k_batch_top leaves the merge slot empty
-}
-
-void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) {
-  if (a.stab) {
-    k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                    a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm);
-    return;
-  }
-  if (const int nch = top_ns_chunks(a)) {
-    launch_top_ns(a, nch, stream);
-    return;
-  }
-  if (tile_eval()) {
-    const int32_t n_tiles = (a.c.n + kTileNodes - 1) / kTileNodes;
-    const dim3 g1((n_tiles + 3) / 4, kBatchPods);
-    if (a.fast)
-      k_batch_eval<true><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-    else
-      k_batch_eval<false><<<g1, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.cand, n_tiles);
-    return;
-  }
   launch_eval_top(a, nullptr, stream);
+  if (evs) (void)hipEventRecord(evs[1], stream);
+  launch_chain_pairs(a, stream);
+  if (evs) (void)hipEventRecord(evs[2], stream);
+  k_batch_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s.gkey, a.s.chain_end, a.s.pmax, a.chosen,
+                                               (a.fast && !a.stab) ? nullptr : a.s.pinv);
+  if (evs) (void)hipEventRecord(evs[3], stream);
+  return 0x7u;
 }
 
-void launch_chain(const LaunchArgs& a, hipStream_t stream) {
-  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, chain_clock(a));
-}
+void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream) { launch_eval_top(a, nullptr, stream); }
 
 void launch_shard_eval(const LaunchArgs& a, hipStream_t stream) { launch_eval_top(a, a.s.xsend, stream); }
 
@@ -1733,27 +1048,8 @@ void k_batch_gmerge_launch(const LaunchArgs& a, int32_t world, hipStream_t strea
                                                      a.s.topk_complete);
 }
 void launch_shard_chain(const LaunchArgs& a, int32_t world, hipStream_t stream) {
-  k_batch_gmerge<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.xrecv, world, a.s.topk, a.s.topk_cnt,
-                                                     a.s.topk_complete);
-  if (chain_fused() && !chain_clock(a)) {
-    if (a.fast)
-      k_batch_chain_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                       a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                       a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
-    else
-      k_batch_chain_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
-                                                                        a.s.topk_cnt, a.s.topk_complete, a.s.gkey,
-                                                                        a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
-    return;
-  }
-  k_batch_chain<<<1, kBatchPods, 0, stream>>>(a.st, a.c.n_total, a.s.topk, a.s.topk_cnt, a.s.topk_complete,
-                                              a.s.gkey, a.s.chain_end, chain_clock(a));
-  if (a.fast)
-    k_batch_pairs<true><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey, a.s.chain_end,
-                                                               a.s.pmax, a.s.pnorm, a.s.pinv);
-  else
-    k_batch_pairs<false><<<kBatchPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.gkey,
-                                                                a.s.chain_end, a.s.pmax, a.s.pnorm, a.s.pinv);
+  k_batch_gmerge_launch(a, world, stream);
+  launch_chain_pairs(a, stream);
 }
 
 void launch_shard_commit(const LaunchArgs& a, hipStream_t stream) {

@@ -1,5 +1,5 @@
-// ksim_chain.h — the batch paths' greedy chain (k_batch_chain, and inside the
-// fused chain + pairs launches of the P100 and ADAPT batches).
+// ksim_chain.h — the batch paths' greedy chain, run inside the chain + pairs
+// launches of the P100, ADAPT and topology batches.
 #pragma once
 #include "ksim_device.h"
 #include "ksim_internal.h"
@@ -10,12 +10,6 @@ namespace ksim {
 constexpr int kHashBits = kBatchPods * kTopT <= 2048 ? 12 : kBatchPods * kTopT <= 4096 ? 13 : 14;
 constexpr int kHashSlots = 1 << kHashBits;     // >= 2 x the list entries (linear probing)
 constexpr int kChainRounds = 64;               // exact prefix kept if not converged by then
-// KSIM_CHAIN_BALLOT (default 1): a round's "first changed pod" flag takes one
-// LDS atomicMin per wave (ballot, first set lane) instead of one per changed
-// pod, which all hit the same word (0: per pod, for A/B builds)
-#ifndef KSIM_CHAIN_BALLOT
-#define KSIM_CHAIN_BALLOT 1
-#endif
 
 // KSIM_CHAIN_DELAY builds (the race regression test, tests/test_gpu_chain_race.py):
 // stretch the round boundary the per-parity flags protect.  The last wave
@@ -37,12 +31,8 @@ constexpr int kChainRounds = 64;               // exact prefix kept if not conve
 static_assert(kBatchPods * kTopT * 2 <= kHashSlots, "chain hash table too small");
 
 // Clusters of at most kChainDirect nodes index the holders by node id (no hash
-// probes while the lists are registered).  KSIM_CHAIN_DIRECT (default 1) lets
-// the chain + pairs launches use it (0: the hash everywhere, for A/B builds):
-// config 2 7.03 -> 6.80 ms per step (profiles/r03/ab_chaindirect)
-#ifndef KSIM_CHAIN_DIRECT
-#define KSIM_CHAIN_DIRECT 1
-#endif
+// probes while the lists are registered): config 2 7.03 -> 6.80 ms per step
+// (profiles/r03/ab_chaindirect)
 constexpr int kChainDirect = 8192;
 constexpr int kChainHoldSlots = kHashSlots > kChainDirect ? kHashSlots : kChainDirect;
 struct ChainLds {
@@ -52,80 +42,11 @@ struct ChainLds {
   int32_t first[2], cut;                      // first: one slot per round parity (see the round loop)
 };
 
-// ---- partial top-T lists of a node-split evaluation (k_batch_top_ns) ----------
-// Chunk c of the nodes wrote, for pod j, its provable top-T prefix
-// ptopk[(c * kBatchPods + j) * kTopT ..] and pmeta[c * kBatchPods + j] = count
-// | complete << 8.  Merged as the sharded records are (k_batch_gmerge): a key is
-// in the pod's exact order if it is >= the last listed key of every incomplete
-// chunk list (every key a chunk did not list is below it); the merged list is
-// complete when every chunk's was and nothing was dropped.
-static_assert((kTopT & (kTopT - 1)) == 0, "bitonic list merge needs a power-of-two T");
-
-// top-T of two descending lists, descending, into a (bitonic half-cleaners)
-__device__ __forceinline__ void merge_top_desc(uint64_t (&a)[kTopT], const uint64_t (&b)[kTopT]) {
-#pragma unroll
-  for (int e = 0; e < kTopT; e++) a[e] = umax64(a[e], b[kTopT - 1 - e]);
-#pragma unroll
-  for (int d = kTopT / 2; d >= 1; d >>= 1)
-#pragma unroll
-    for (int e = 0; e < kTopT; e++)
-      if ((e & d) == 0) cswap_desc(a[e], a[e + d]);
-}
-
-template <int NCHUNK>
-__device__ __forceinline__ void load_merged_list(int32_t j, const uint64_t* __restrict__ ptopk,
-                                                 const int32_t* __restrict__ pmeta, uint64_t (&lst)[kTopT],
-                                                 int32_t& cnt_out, int32_t& complete_out) {
-  uint64_t L[NCHUNK][kTopT];
-  int32_t meta[NCHUNK];
-#pragma unroll
-  for (int c = 0; c < NCHUNK; c++) {
-    meta[c] = pmeta[c * kBatchPods + j];
-#pragma unroll
-    for (int e = 0; e < kTopT; e++) L[c][e] = ptopk[((size_t)c * kBatchPods + j) * kTopT + e];
-  }
-  uint64_t thr = 0;
-  bool all_complete = true, blind = false;
-#pragma unroll
-  for (int c = 0; c < NCHUNK; c++) {
-    const int32_t n = meta[c] & 0xff;
-    const bool cmp = (meta[c] >> 8) & 1;
-    uint64_t last = 0;
-#pragma unroll
-    for (int e = 0; e < kTopT; e++) {
-      if (e >= n) L[c][e] = 0;
-      if (e == n - 1) last = L[c][e];
-    }
-    if (!cmp) {
-      all_complete = false;
-      if (n == 0) blind = true;                  // nothing of this chunk is provable
-      thr = umax64(thr, last);
-    }
-  }
-  int32_t nvalid = 0;
-#pragma unroll
-  for (int c = 0; c < NCHUNK; c++)
-#pragma unroll
-    for (int e = 0; e < kTopT; e++) {
-      if (L[c][e] < thr) L[c][e] = 0;
-      nvalid += L[c][e] != 0;
-    }
-#pragma unroll
-  for (int w = 1; w < NCHUNK; w <<= 1)
-#pragma unroll
-    for (int c = 0; c + w < NCHUNK; c += 2 * w) merge_top_desc(L[c], L[c + w]);
-#pragma unroll
-  for (int e = 0; e < kTopT; e++) lst[e] = blind ? 0 : L[0][e];
-  cnt_out = blind ? 0 : (nvalid < kTopT ? nvalid : kTopT);
-  complete_out = (!blind && all_complete && nvalid <= kTopT) ? 1 : 0;
-}
-
 // The chain of one batch in one block of kBatchPods threads (thread i = pod
 // i; pods from nb_cap on take no part).  Returns false when the batch is empty (block-uniform); else *gk = pod
 // i's guessed key (0: none, or i past the exact prefix) and *nchain = the
 // prefix length.  A pure function of the lists: every block that runs it gets
 // the same guesses.
-template <int NCHUNK = 0>
 __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restrict__ st,
                                             const uint64_t* __restrict__ topk,
                                             const int32_t* __restrict__ topk_cnt,
@@ -142,16 +63,10 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   // the buffers hold kBatchPods entries, so no bound check is needed yet)
   uint64_t lst[kTopT];
   int cnt0, complete0;
-  if constexpr (NCHUNK > 0) {
-    // node-split evaluation: merge the pod's chunk lists (topk / topk_cnt hold
-    // them, see k_batch_top_ns)
-    load_merged_list<NCHUNK>(i, topk, topk_cnt, lst, cnt0, complete0);
-  } else {
 #pragma unroll
-    for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
-    cnt0 = topk_cnt[i];
-    complete0 = topk_complete[i];
-  }
+  for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
+  cnt0 = topk_cnt[i];
+  complete0 = topk_complete[i];
   const int32_t base = st->cursor;
   const int32_t nb = min(nb_cap, st->end - base);   // nb_cap: the topology batch's pod count
   if (nb <= 0) return false;
@@ -216,14 +131,10 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
       if (e < cnt && held[e] >= i) na = e;
     __syncthreads();
     if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
-#if KSIM_CHAIN_BALLOT
     {                                                   // the wave's first changed pod: one LDS atomic per wave
       const uint64_t chg = __ballot(na != a);
       if (chg && (threadIdx.x & 63) == 0) atomicMin(&L.first[par], (int)(threadIdx.x & ~63u) + __builtin_ctzll(chg));
     }
-#else
-    if (na != a) atomicMin(&L.first[par], i);
-#endif
     a = na;
     __syncthreads();
     CHAIN_DELAY((int)(blockDim.x >> 6) - 1);   // the last wave reads the flag late

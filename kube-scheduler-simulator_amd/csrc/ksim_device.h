@@ -249,10 +249,7 @@ struct DevScratch {
   uint32_t* detail;      // [n]
   int64_t* raw;          // [KSIM_MAX_SCORE][n] raw scores (normalized slots; all in compat)
   int64_t* part;         // [n] sum of weighted raw of slots without NormalizeScore
-  uint64_t* cand;        // batch path: [B][n_tiles][kTileCand] per-tile best keys
   uint64_t* topk;        // batch path: [B][T] merged top keys, descending
-  uint64_t* ptopk;       // node-split batch top (k_batch_top_ns): [chunks][B][T] per-chunk lists
-  int32_t* pmeta;        // ... [chunks][B] count | complete << 8
   int32_t* topk_cnt;     // batch path: [B] valid merged keys
   int32_t* topk_complete;// batch path: [B] 1 if every S0-feasible node is in the list
   uint64_t* gkey;        // batch path: [B] key of each pod's greedy guess (0: none)
@@ -1581,7 +1578,7 @@ __device__ __forceinline__ double div_rn(double n, double d, double y) {
   return __builtin_fma(e, y, q0);
 }
 
-// The FAST key (k_batch_top<true>, k_batch_pairs<true>): trivial pods (every
+// The FAST key (k_batch_top<true>, k_batch_chain_pairs<true>): trivial pods (every
 // static filter host-proven to pass), {cpu, memory} strategies with
 // LeastAllocated weights in [1, 2^31) (BatchProg::fast_w), allocatable cpu and
 // memory in [0, 2^46) on every node (checked at ksim_set_cluster).  Then each

@@ -174,9 +174,8 @@ struct ksim_handle {
   // filter pass (2) | NormalizeScore extrema in the filter pass (4)
   hipGraphExec_t graph_cycle[16] = {};   // | persistent tables (8)
   hipGraphExec_t graph_batch = nullptr;
-  hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_eval<true> runs
+  hipGraphExec_t graph_batch_fast = nullptr;   // k_batch_top<true> runs
   hipGraphExec_t graph_batch_stab = nullptr;   // static-class runs (LaunchArgs::stab)
-  hipGraphExec_t graph_lazy_stab = nullptr;
   hipGraphExec_t graph_tbatch = nullptr;       // topology batches (ksim_tbatch.hip)
   // deferred-commit FAST batches (ksim_internal.h): the second snapshot buffer
   // X[1] and state st[1], the ring of chain + pairs outputs, kGraphBatches
@@ -187,10 +186,8 @@ struct ksim_handle {
   DevState* lazy_st1 = nullptr;
   uint64_t *lazy_g = nullptr, *lazy_m = nullptr;   // [kLazySlots][kBatchPods]
   int32_t* lazy_e = nullptr;                        // [kLazySlots] prefix length, -1 = empty slot
-  int32_t* lazy_inv = nullptr;          // generic P100: [kLazySlots][kBatchPods] pinv flags
   int32_t *lazy_ab = nullptr, *lazy_aw = nullptr;   // ADAPT: [kLazySlots][kBatchPods] broken flags, [..][2 B] windows
   hipGraphExec_t graph_lazy = nullptr;
-  hipGraphExec_t graph_lazy_gen = nullptr;
   hipGraphExec_t graph_lazy_adapt = nullptr;
   // node-sharded ADAPT batch: this shard's bitmaps, the all-gathered ones and
   // the global bitmap (allocated at the first such run)
@@ -279,13 +276,11 @@ void drop_graphs(ksim_handle* h) {
   if (h->graph_batch) (void)hipGraphExecDestroy(h->graph_batch);
   if (h->graph_batch_fast) (void)hipGraphExecDestroy(h->graph_batch_fast);
   if (h->graph_batch_stab) (void)hipGraphExecDestroy(h->graph_batch_stab);
-  if (h->graph_lazy_stab) (void)hipGraphExecDestroy(h->graph_lazy_stab);
-  h->graph_batch_stab = h->graph_lazy_stab = nullptr;
+  h->graph_batch_stab = nullptr;
   if (h->graph_tbatch) (void)hipGraphExecDestroy(h->graph_tbatch);
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
-  if (h->graph_lazy_gen) (void)hipGraphExecDestroy(h->graph_lazy_gen);
   if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
-  h->graph_lazy_adapt = h->graph_lazy_gen = nullptr;
+  h->graph_lazy_adapt = nullptr;
   h->graph_batch_fast = nullptr;
   h->graph_batch = nullptr;
   h->graph_tbatch = nullptr;
@@ -498,7 +493,7 @@ bool adapt_mode(const ksim_handle* h) {
 // static class, run_fast's cluster conditions, an unsharded handle and the
 // default launch forms.
 bool run_stab(const ksim_handle* h, int32_t a, int32_t b) {
-  if (!h->stab_ready || h->stab_dirty || batch_ab_forms() || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
+  if (!h->stab_ready || h->stab_dirty || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
   if (!h->bp.cpu_mem || !h->bp.fast_w || !h->alloc_narrow) return false;
   for (int32_t i = a; i < b; i++)
     if (h->sclass[(size_t)i] < 0) return false;
@@ -734,31 +729,16 @@ bool lazy_enabled() {
   return !off;
 }
 
-// KSIM_LAZY_GEN=1: generic runs take the deferred commit too (opt-in: on
-// config 1 scaled it measured 46.8 against 35.3 ms per step for the three
-// launches, profiles/r03/ab_lazy_gen; the generic key loop with the overlay
-// holds 205 VGPRs at 512 threads)
-bool lazy_gen_enabled() {
-  static const bool on = getenv("KSIM_LAZY_GEN") != nullptr;
-  return on;
-}
-
-// A FAST run [a, b) on an unsharded handle whose pods add to no count class
-// (the overlay carries the resource columns only), on a cluster the overlay's
-// LDS node bitmap covers.  Generic runs (fast false): unsharded P100 handles,
-// pods without scalar requests (k_batch_top_commit<.., false>).
-// Static-class runs (stab) only with KSIM_LAZY_STAB=1: config 1 scaled measured
-// 13.3 against 12.7 ms per step for the three launches (profiles/r03/ab_stab;
-// the overlay lookups of the maxima pass and the key pass cost more than the
-// separate commit launch).
+// A FAST run [a, b) whose pods add to no count class (the overlay carries the
+// resource columns only), on a cluster the overlay's LDS node bitmap covers.
+// Generic runs and static-class runs keep the three launches: the deferred
+// commit measured slower for both (config 1 scaled, profiles/r03/ab_lazy_gen:
+// 46.8 against 35.3 ms per step for generic keys, whose loop with the overlay
+// held 205 VGPRs; profiles/r03/ab_stab: 13.3 against 12.7 ms for the
+// static-class keys, whose overlay lookups in both passes cost more than the
+// commit launch).
 bool lazy_ok(const ksim_handle* h, int32_t a, int32_t b, bool fast, bool stab = false) {
-  static const bool lazy_stab = getenv("KSIM_LAZY_STAB") != nullptr;
-  if (!lazy_enabled() || batch_ab_forms() || (stab && !lazy_stab)) return false;
-  if (!fast) {
-    if (!lazy_gen_enabled() || adapt_mode(h) || is_sharded(h) || h->replicated) return false;
-    for (int32_t i = a; i < b; i++)
-      if (!h->noscalar[i]) return false;
-  }
+  if (!lazy_enabled() || !fast || stab) return false;
   // ADAPT runs whole on a replica (no exchange); replicated P100 batches take
   // shard_run_lazy (lazy_rep_ok)
   if (adapt_mode(h) ? (is_sharded(h) && !h->replicated) : (is_sharded(h) || h->replicated)) return false;
@@ -773,8 +753,7 @@ int alloc_lazy(ksim_handle* h) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->graph_lazy) (void)hipGraphExecDestroy(h->graph_lazy);
   if (h->graph_lazy_adapt) (void)hipGraphExecDestroy(h->graph_lazy_adapt);
-  if (h->graph_lazy_gen) (void)hipGraphExecDestroy(h->graph_lazy_gen);
-  h->graph_lazy = h->graph_lazy_adapt = h->graph_lazy_gen = nullptr;
+  h->graph_lazy = h->graph_lazy_adapt = nullptr;
   free_bufs(h->lazy_bufs);
   h->lazy_n = -1;
   const size_t n = (size_t)h->dc.n;
@@ -800,8 +779,6 @@ int alloc_lazy(ksim_handle* h) {
   h->lazy_ab = (int32_t*)p;
   if ((rc = upload(h, h->lazy_bufs, nullptr, 8 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
   h->lazy_aw = (int32_t*)p;
-  if ((rc = upload(h, h->lazy_bufs, nullptr, 4 * (size_t)kLazySlots * kBatchPods, &p))) return rc;
-  h->lazy_inv = (int32_t*)p;
   h->lazy_n = h->dc.n;
   return KSIM_OK;
 }
@@ -838,7 +815,6 @@ LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
   z.step.g2 = h->lazy_g + (size_t)q2 * kBatchPods;
   z.step.e2 = h->lazy_e + q2;
   z.step.e_self = h->lazy_e + q;
-  z.step.inv1 = h->lazy_inv + (size_t)q1 * kBatchPods;
   z.st = st[p];
   z.gkey = h->lazy_g + (size_t)q * kBatchPods;
   z.pmax = h->lazy_m + (size_t)q * kBatchPods;
@@ -847,7 +823,6 @@ LazyBatch lazy_batch(const ksim_handle* h, const LaunchArgs& la, int64_t i) {
   z.w1 = h->lazy_aw + (size_t)q1 * 2 * kBatchPods;
   z.abroken = h->lazy_ab + (size_t)q * kBatchPods;
   z.awin = h->lazy_aw + (size_t)q * 2 * kBatchPods;
-  z.inv = h->lazy_inv + (size_t)q * kBatchPods;
   return z;
 }
 
@@ -907,10 +882,7 @@ void lazy_flush(const ksim_handle* h, const LazyBatch& z, hipStream_t stream) {
 int run_lazy(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   int rc;
   if ((rc = lazy_begin(h))) return rc;
-  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt
-                          : la.stab     ? h->graph_lazy_stab
-                          : la.fast     ? h->graph_lazy
-                                        : h->graph_lazy_gen;
+  hipGraphExec_t& graph = adapt_mode(h) ? h->graph_lazy_adapt : h->graph_lazy;
   if (!graph) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     hipGraph_t g = nullptr;
@@ -1087,7 +1059,7 @@ hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast,
 // every placement), the records' all-gather, the global merge and the chain +
 // pairs: one exchange and three launches per batch instead of four.
 bool lazy_rep_ok(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b, bool fast) {
-  if (!fast || !lazy_enabled() || batch_ab_forms()) return false;
+  if (!fast || !lazy_enabled()) return false;
   for (auto* h : hs) {
     if (!h->replicated || h->dc.base != 0 || h->dc.n > kLazyMaxNodes || h->dc.n <= 0) return false;
     for (int32_t i = a; i < b; i++)
@@ -1895,7 +1867,6 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
 
   DevScratch s{};
   DevEvalOut o{};
-  const size_t n_tiles = (N + kTileNodes - 1) / kTileNodes;
   void* p = nullptr;
 #define SCR(dst, type, bytes)                                                         \
   do {                                                                                \
@@ -1915,10 +1886,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
-  SCR(s.cand, uint64_t*, 8 * (size_t)kBatchPods * n_tiles * kTileCand);
   SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kTopT);
-  SCR(s.ptopk, uint64_t*, 8 * (size_t)kTopNsMaxChunks * kBatchPods * kTopT);
-  SCR(s.pmeta, int32_t*, 4 * (size_t)kTopNsMaxChunks * kBatchPods);
   SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
@@ -2804,7 +2772,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
       plans[i].flags |= kPlanPtab;
       plans[i].m.ptab = R.mask[i];
     }
-    if (!R.padd_first.empty() && !getenv("KSIM_NO_TADDS")) {   // the table updates of its binds, listed
+    if (!R.padd_first.empty()) {   // the table updates of its binds, listed
       plans[i].flags |= kPlanTadds;
       plans[i].tadd_first = R.padd_first[(size_t)i];
       plans[i].tadd_count = R.padd_count[(size_t)i];
@@ -3131,9 +3099,6 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
 const char* ksim_kernel_name(int32_t k) {
   if (k >= 0 && k < kKernelsPerCycle) return kKernelNames[k];
   k -= kKernelsPerCycle;
-  // the default P100 batch runs the chain inside the pairs launch (the chain
-  // slot stays empty): name the slot after the kernel it times
-  if (k == 3 && chain_fused()) return "k_batch_chain_pairs";
   if (k >= 0 && k < kKernelsPerBatch) return kBatchKernelNames[k];
   k -= kKernelsPerBatch;
   if (k >= 0 && k < kKernelsPerAdapt) return kAdaptKernelNames[k];
@@ -3285,7 +3250,7 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
 
 extern "C" int ksim_batch_geometry(int32_t* out, int32_t n) {
   if (!out || n < 0) return KSIM_E_INVALID;
-  const int32_t v[4] = {kBatchPods, kTopT, kTileNodes, kTileCand};
+  const int32_t v[4] = {kBatchPods, kTopT, kTopThreads, kTileCand};
   const int32_t m = n < 4 ? n : 4;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;

@@ -17,10 +17,8 @@ namespace ksim {
 constexpr int kBatchPods = KSIM_BATCH_PODS;   // B: pods per speculative batch
 constexpr int kTopT = KSIM_TOP_T;             // T: candidate keys kept per pod
 static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch geometry");
-constexpr int kNodesPerLane = 4;   // nodes per lane in k_batch_eval
-constexpr int kTileNodes = 64 * kNodesPerLane;   // nodes per wave tile
-constexpr int kTileCand = 4;       // best keys a wave tile keeps per pod
-constexpr int kTopNsMaxChunks = 4;   // node chunks of the node-split batch top (k_batch_top_ns)
+constexpr int kTopThreads = 1024;  // threads per pod of the batch top
+constexpr int kTileCand = 4;       // best keys each lane of the batch top keeps per pod
 constexpr int kXRec = kTopT + 1;   // sharded exchange record per pod: T keys + (count | complete << 32)
 constexpr int kMaxShards = 8;      // shards of one simulation (one per GPU of a node)
 constexpr int kGmergeSlots = (kTopT * kMaxShards + 63) / 64;   // list entries per lane in k_batch_gmerge
@@ -43,7 +41,7 @@ struct LaunchArgs {
   int32_t* chosen;   // [n_pods] device, may be null
   const ksim_profile* dprof = nullptr;   // device copies of prof / bp (the batch kernels read these)
   const BatchProg* dbp = nullptr;
-  bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_eval<true>)
+  bool fast = false; // batch runs: every pod trivial and cpu/memory scoring (k_batch_top<true>)
   bool stab = false; // ... or (with fast) every pod in a static class (DevPods::stab; the STAB kernels)
   bool fuse_min = false;  // per-pod topology runs: every hard spread key has <= 256 values
   bool fuse_ext = false;  // per-pod runs: every pod has <= 1 ScheduleAnyway spread constraint (K = N: no k_extrema)
@@ -53,9 +51,9 @@ struct LaunchArgs {
 constexpr int kKernelsPerCycle = 7;
 constexpr int kFuseMinValues = 256;   // k_filter_score computes the PTS critical paths itself up to this many values
 extern const char* const kKernelNames[kKernelsPerCycle];
-constexpr int kKernelsPerBatch = 5;
+constexpr int kKernelsPerBatch = 3;
 extern const char* const kBatchKernelNames[kKernelsPerBatch];
-constexpr int kKernelsPerAdapt = 6;
+constexpr int kKernelsPerAdapt = 5;
 extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 // Topology batch path (ksim_tbatch.hip): at most kTbPods pods per batch (the
 // host's class-conflict-free runs, bflags >> kTlenShift), clusters of at most
@@ -75,8 +73,6 @@ uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs 
 uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 // Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
-bool chain_fused();   // KSIM_CHAIN_SEPARATE unset: the chain runs inside the pairs launch
-bool batch_ab_forms();   // an A/B switch of the three-launch batch forms is set (no deferred commit)
 unsigned long long* cp_clock_buffer();   // KSIM_CP_CLOCKS builds: chain + pairs phase clocks (else null)
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.
@@ -104,7 +100,6 @@ struct LazyStep {
   const uint64_t* g1; const uint64_t* m1; const int32_t* e1;   // batch i-1's slot: guesses, pair maxima, prefix
   const uint64_t* g2; const int32_t* e2;                       // batch i-2's slot: guesses, prefix
   int32_t* e_self;                                 // batch i's slot (a flush marks it empty: -1)
-  const int32_t* inv1;                             // generic runs: batch i-1's pinv flags (kPodNormVaries)
 };
 struct LazyBatch {
   LaunchArgs a;        // a.c: static columns + X[p ^ 1]
@@ -119,7 +114,6 @@ struct LazyBatch {
   const int32_t* w1;
   int32_t* abroken;
   int32_t* awin;
-  int32_t* inv;        // generic P100 runs: batch i's pinv flags
 };
 constexpr int kKernelsPerLazy = 2;
 extern const char* const kLazyKernelNames[kKernelsPerLazy];
@@ -143,7 +137,6 @@ void launch_lazy_top(const LazyBatch& z, hipStream_t stream);   // the first lau
 // after the records' all-gather into a.s.xrecv, the global merge + chain + pairs
 void launch_lazy_top_rep(const LazyBatch& z, uint64_t* xsend, hipStream_t stream);
 void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream);
-void launch_chain(const LaunchArgs& a, hipStream_t stream);
 // Compat cycle around the host's extender round trip (ksim_eval_pod_filter / _finish):
 // the filter pass + window, then (a.s.ext_fail / ext_score set) the rest.
 void launch_cycle_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
@@ -176,7 +169,7 @@ void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_inde
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream);
 void launch_filter_only(const LaunchArgs& a, hipStream_t stream);
 // Sharded batch (node shards; the caller exchanges between the phases):
-//   launch_shard_eval    eval + merge; writes this shard's records to s.xsend
+//   launch_shard_eval    batch top; writes this shard's records to s.xsend
 //   (all-gather s.xsend -> s.xrecv [world][kBatchPods][kXRec])
 //   launch_shard_chain   global merge + chain + pair keys of owned guesses -> s.pmax
 //   (all-reduce max s.pmax)

@@ -781,25 +781,10 @@ struct WinScalars {
 
 // selectHost over k_select's per-block records (one wave): the winning TB lo
 // word (0: no kept node).
-// KSIM_SEL_SC1=1 builds: k_select's blocks store their records write-through
-// (sc1) and drain them before a relaxed ticket add; the last block reads them
-// with sc1 loads, which miss its L1, so no agent fence is paid on either side
-// (cdna_hip_programming.md §6 Guideline 16, the sc1 form).  Measured and not
-// kept (profiles/r03/ab_sel, config 3, same box): 27.8 us per pod against
-// 26.7 us for the default acq_rel ticket (release + acquire in every block).
-#ifndef KSIM_SEL_SC1
-#define KSIM_SEL_SC1 0
-#endif
 __device__ __forceinline__ uint64_t reduce_block_best(const DevScratch& s, int32_t n_blocks) {
   const int lane = threadIdx.x & 63;
   uint64_t img = 0, lo = 0;
-#if KSIM_SEL_SC1
-  for (int32_t b = lane; b < n_blocks; b += 64)
-    best2_merge(img, lo, __hip_atomic_load(&s.bbest[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                __hip_atomic_load(&s.bbest[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-#else
   for (int32_t b = lane; b < n_blocks; b += 64) best2_merge(img, lo, s.bbest[2 * b], s.bbest[2 * b + 1]);
-#endif
   wave_best2(img, lo);
   return lo;
 }
@@ -1042,12 +1027,6 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     uint64_t bi = s_best[0], bl = s_best[1];
 #pragma unroll
     for (int w = 1; w < 4; w++) best2_merge(bi, bl, s_best[2 * w], s_best[2 * w + 1]);
-#if KSIM_SEL_SC1
-    if (bind_mode) {
-      __hip_atomic_store(&s.bbest[2 * blockIdx.x], bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&s.bbest[2 * blockIdx.x + 1], bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else
-#endif
     {
       s.bbest[2 * blockIdx.x] = bi;
       s.bbest[2 * blockIdx.x + 1] = bl;
@@ -1057,17 +1036,9 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
   if (bind_mode) {
     __shared__ int32_t s_last;
     if (tid == 0) {
-#if KSIM_SEL_SC1
-      // the record is the only byte the last block reads from this launch's
-      // other blocks (fuse_ext's window scalars it derives itself, below):
-      // drain its write-through store, then take a ticket
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int32_t done = __hip_atomic_fetch_add(&win->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
       // the last block: its acquire sees every block's record (and block 0's
       // window fields) released by their own increments
       const int32_t done = __hip_atomic_fetch_add(&win->done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-#endif
       s_last = done == (int32_t)gridDim.x - 1;
     }
     __syncthreads();
@@ -1075,13 +1046,7 @@ __global__ __launch_bounds__(256) void k_select(DevCluster c, DevPods P0, ksim_p
     if (s_last && tid < 64) {
       if (tid == 0) __hip_atomic_store(&win->done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the record loads below the ticket
-      WinScalars ws{};
-      if (fuse_ext) {                              // the values block 0 stored, derived as it did
-        ws.nscan = ws.cut = ws.evaluated = ws.k = ss.n;
-        ws.nf = nf;
-        ws.error = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? kCycleErrorPrefilter : 0;
-      }
-      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp, fuse_ext && KSIM_SEL_SC1 ? &ws : nullptr);
+      bind_cycle(c, P, st, s, chosen_out, pi, bind_mode == 2, pp, nullptr);
 #ifdef KSIM_SEL_CLOCKS
       if (tid == 0) {
         atomicAdd(&s.dbg[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - sel_t));

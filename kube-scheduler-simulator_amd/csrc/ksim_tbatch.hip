@@ -312,8 +312,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const int32_t nbt = tb_count(st, P);
   uint64_t gk;
   int32_t nchain;
-  if (!chain_block(L, st, s.topk, s.topk_cnt, s.topk_complete, &gk, &nchain, nullptr, nbt,
-                   KSIM_CHAIN_DIRECT ? c.n_total : 0))
+  if (!chain_block(L, st, s.topk, s.topk_cnt, s.topk_complete, &gk, &nchain, nullptr, nbt, c.n_total))
     return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;

@@ -116,8 +116,8 @@ def batch_geometry() -> dict:
     """Batch-path geometry compiled into libksim_engine.so (no GPU needed)."""
     out = np.zeros(4, np.int32)
     lib().ksim_batch_geometry(out.ctypes.data_as(ctypes.c_void_p), 4)
-    return {"pods_per_batch": int(out[0]), "top_t": int(out[1]), "tile_nodes": int(out[2]),
-            "tile_cand": int(out[3])}
+    return {"pods_per_batch": int(out[0]), "top_t": int(out[1]), "top_threads": int(out[2]),
+            "lane_cand": int(out[3])}
 
 
 COMM_ID_BYTES = 128

@@ -46,7 +46,7 @@ def test_struct_sizes_match(which):
 def test_batch_geometry():
     g = engine.batch_geometry()
     assert g["pods_per_batch"] % 64 == 0 and 0 < g["top_t"] <= 64
-    assert g["tile_nodes"] % 64 == 0 and g["tile_cand"] > 0
+    assert g["top_threads"] % 64 == 0 and g["lane_cand"] > 0
 
 
 def test_create_without_gpu_fails_loudly():

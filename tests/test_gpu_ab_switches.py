@@ -1,14 +1,10 @@
-"""The engine's A/B switches keep the pre-fusion launch forms alive
-(KSIM_CHAIN_SEPARATE: the chain as its own one-block launch ahead of the
-pairs; KSIM_WINDOW_SEPARATE: the ADAPT window scan as its own launch;
-KSIM_NO_LAZY: the three-launch P100 batch, commit as its own launch, instead
-of the deferred commit; KSIM_LAZY_GEN: the deferred commit for generic pods
-too -- config 1's taints, tolerations and node affinity; KSIM_NO_STAB: those
-pods' keys without the static-class table, every static plugin per node;
-KSIM_LAZY_STAB: the deferred commit for the static-class runs).  They
-are read once per process, so each runs in one child process that schedules
-P100 and ADAPT batches and checks them against the oracle (the default forms
-run in every other GPU test)."""
+"""The engine's remaining A/B switches select other production forms of the
+same runs (KSIM_NO_LAZY: the three-launch P100 / ADAPT batches, commit as its
+own launch, instead of the deferred commit; KSIM_NO_STAB: the static plugins
+evaluated per node instead of the static-class table).  They are read once
+per process, so each runs in one child process that schedules P100 and ADAPT
+batches and checks them against the oracle (the default forms run in every
+other GPU test)."""
 import os
 import subprocess
 import sys
@@ -54,8 +50,7 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("switch", ["KSIM_CHAIN_SEPARATE", "KSIM_WINDOW_SEPARATE", "KSIM_NO_LAZY",
-                                    "KSIM_LAZY_GEN", "KSIM_NO_STAB", "KSIM_LAZY_STAB"])
+@pytest.mark.parametrize("switch", ["KSIM_NO_LAZY", "KSIM_NO_STAB"])
 def test_separate_launch_forms_vs_oracle(switch):
     env = dict(os.environ)
     env[switch] = "1"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Config 3 A/B on one box, each variant REPS times interleaved.  A variant is a
 # KSIM_LIB_VARIANT flavor, or ENV=1 to run the default library with that
-# environment variable set.  Usage: REPS=2 bash tools/ab_c3.sh head KSIM_NO_TADDS=1
+# environment variable set.  Usage: REPS=2 bash tools/ab_c3.sh head KSIM_NO_PTAB=1
 set -o pipefail
 mkdir -p gpurun_out/abc3
 for r in $(seq 1 ${REPS:-1}); do

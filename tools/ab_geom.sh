@@ -5,9 +5,9 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/${TAG:-geom}
 mkdir -p "$OUT"
 for v in ${VARIANTS:-base b512t8 b256t16 b512t16 base}; do
-  unset KSIM_LIB_VARIANT KSIM_BATCH_TILES
+  unset KSIM_LIB_VARIANT
   [ $v != base ] && export KSIM_LIB_VARIANT=$v
-  [ -n "$TILES" ] && export KSIM_BATCH_TILES=1
+  [ -n "$TILES" ] && export=1
   timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 3 --no-cpu ${BENCH_ARGS} > "$OUT/bench_$v.json" 2> "$OUT/bench_$v.err" || exit $?
   python3 -c "
 import json

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=$PWD/gpurun_out/${TAG:-run}/sq
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-KRE=${KRE:-k_batch_eval}
+KRE=${KRE:-k_batch_top_commit}
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY \
     --kernel-include-regex "$KRE" -d "$OUT/p1" -o run --output-format csv \
     -- python3 bench.py --steps 1 --warmup 0 --no-cpu ${BENCH_ARGS} > "$OUT/p1.log" 2>&1 || exit $?

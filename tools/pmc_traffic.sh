@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=$PWD/gpurun_out/${TAG:-run}/pmc
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-KRE=${KRE:-k_batch_eval}
+KRE=${KRE:-k_batch_top_commit}
 i=0
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 7
+#define KSIM_ABI_VERSION 8
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -42,6 +42,7 @@ extern "C" {
 #define KSIM_MAX_FILTER       16
 #define KSIM_MAX_SCORE        8
 #define KSIM_MAX_RES          4          /* resources in a scoring strategy */
+#define KSIM_MAX_SHAPE        16         /* RequestedToCapacityRatio shape points */
 #define KSIM_MAX_USES         16         /* topology uses per pod (PTS constraints + IPA terms) */
 #define KSIM_MAX_CLASSES      4096       /* count classes (see ksim_topo_use) */
 #define KSIM_COL_NONE         0xFFFF     /* topology key carried by no node */
@@ -114,6 +115,15 @@ enum ksim_plugin {
 /* ... and a listed name is not a node of the snapshot: NodeInfos().Get fails
  * and the cycle fails with framework.Error before any Filter call. */
 #define KSIM_POD_NODE_NAMES_UNKNOWN     64u
+/* NodeAffinityArgs.addedAffinity.requiredDuringSchedulingIgnoredDuringExecution
+ * (the profile's scheduler-enforced node selector) applies: terms
+ * [added_term_first, +added_term_count) of the pod set, OR-ed.  NodeAffinity's
+ * Filter checks them before the pod's own selector and terms and fails with
+ * fail_detail KSIM_NA_ENFORCED (nodeaffinity.go errReasonEnforced).  The
+ * added PREFERRED terms are scored exactly like the pod's own preferred terms,
+ * so the host appends them to pref_term_* instead.  PodTopologySpread's
+ * nodeAffinityPolicy reads the pod's own affinity only (GetRequiredNodeAffinity). */
+#define KSIM_POD_ADDED_AFFINITY        128u
 
 /* pod nb_flags (NetworkBandwidth request annotations) */
 #define KSIM_POD_NB_INGRESS_BAD 1u   /* the ingress request annotation does not parse */
@@ -121,6 +131,15 @@ enum ksim_plugin {
 
 /* pod topo_flags */
 #define KSIM_POD_IPA_SELF_AFFINITY 1u  /* podMatchesAllAffinityTerms(required affinity terms, pod) */
+/* The pod's PodTopologySpread constraints are the system defaults
+ * (PodTopologySpreadArgs defaultingType System, the pod has no constraints of
+ * its own and a Service / ReplicaSet / ReplicationController / StatefulSet
+ * selects it: buildDefaultConstraints with helper.DefaultSelector).  PreScore
+ * then runs with requireAllTopologies = false (podtopologyspread.PreScore): no
+ * IgnoredNodes, and a node lacking a key registers and counts toward the pair
+ * (key, "") -- value id 0 of the use's column -- while Score credits only the
+ * keys the node has. */
+#define KSIM_POD_PTS_SYSTEM_DEFAULT 2u
 
 /* node-selector requirement operators (k8s NodeSelectorOperator + matchFields) */
 #define KSIM_OP_IN            0
@@ -152,6 +171,9 @@ enum ksim_plugin {
 #define KSIM_IPA_AFFINITY        1u   /* ErrReasonAffinityRulesNotMatch (UnschedulableAndUnresolvable) */
 #define KSIM_IPA_ANTI_AFFINITY   2u   /* ErrReasonAntiAffinityRulesNotMatch */
 #define KSIM_IPA_EXISTING_ANTI   3u   /* ErrReasonExistingAntiAffinityRulesNotMatch */
+/* NodeAffinity failure detail: 0 = the pod's selector / required terms
+ * (ErrReasonPod), KSIM_NA_ENFORCED = the profile's addedAffinity (errReasonEnforced) */
+#define KSIM_NA_ENFORCED         1u
 
 /* per-pod cycle status */
 #define KSIM_STATUS_SCHEDULED      0
@@ -261,6 +283,8 @@ typedef struct ksim_pod {
                                                 to the *-bandwidth annotation */
   int64_t  nb_add;                           /* added to the node's allocated amount once bound
                                                 (request annotations only, unparsable ones skipped) */
+  int32_t  added_term_first, added_term_count;/* NodeAffinityArgs.addedAffinity required terms
+                                                (KSIM_POD_ADDED_AFFINITY) */
 } ksim_pod;
 
 /* Volume groups.  A pod's PersistentVolumeClaims bound to PersistentVolumes
@@ -338,8 +362,16 @@ typedef struct ksim_pod_set {
   const int32_t* nn;                /* PreFilterResult node positions (see KSIM_POD_NODE_NAMES) */
 } ksim_pod_set;
 
+/* NodeResourcesFit ScoringStrategy types (NodeResourcesFitArgs.scoringStrategy.type) */
+#define KSIM_FIT_LEAST_ALLOCATED              0   /* least_allocated.go leastResourceScorer */
+#define KSIM_FIT_MOST_ALLOCATED               1   /* most_allocated.go mostResourceScorer */
+#define KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO  2   /* requested_to_capacity_ratio.go (broken-linear shape) */
+
 /* Profile: the converted KubeSchedulerProfile (simulator/scheduler/scheduler.go:199-249,
- * plugins.go:185-220) restricted to what the cycle needs. */
+ * plugins.go:185-220) restricted to what the cycle needs, with the plugin args
+ * NewPluginConfig merges over the defaults (plugins.go:103-179).  An arg the
+ * engine does not implement is refused by the host compile (ksim/profile.py),
+ * never dropped. */
 typedef struct ksim_profile {
   int32_t n_filter;
   int32_t n_score;
@@ -347,7 +379,7 @@ typedef struct ksim_profile {
   uint8_t score[KSIM_MAX_SCORE];       /* ksim_plugin ids, profile Score order */
   int32_t score_weight[KSIM_MAX_SCORE];/* profile weights; 0 is treated as 1 (framework) */
   int32_t percentage_of_nodes_to_score;/* 0 = adaptive (simulator default), 100 = all */
-  /* NodeResourcesFit ScoringStrategy (LeastAllocated) */
+  /* NodeResourcesFit ScoringStrategy: resources and weights (weight 0 defaulted to 1) */
   int32_t fit_n_res;
   int32_t fit_res[KSIM_MAX_RES];       /* KSIM_RES_* */
   int64_t fit_res_weight[KSIM_MAX_RES];
@@ -356,8 +388,18 @@ typedef struct ksim_profile {
   int32_t ba_res[KSIM_MAX_RES];
   int64_t ba_res_weight[KSIM_MAX_RES];
   int32_t hard_pod_affinity_weight;    /* InterPodAffinityArgs (default 1) */
-  int32_t _pad;
+  uint32_t fit_ignored_scalar;         /* NodeResourcesFitArgs ignoredResources / ignoredResourceGroups:
+                                          bit k = Fit's Filter skips scalar column k (extended resources
+                                          only; the scores and the binds still count it) */
   uint64_t tiebreak_seed;              /* selectHost fixed-seed tie-break TB(seed) */
+  /* ABI 8: the rest of NodeResourcesFitArgs.scoringStrategy and DefaultPreemptionArgs */
+  int32_t fit_strategy;                /* KSIM_FIT_* */
+  int32_t fit_n_shape;                 /* RequestedToCapacityRatio: shape points (1..KSIM_MAX_SHAPE) */
+  int32_t fit_shape_util[KSIM_MAX_SHAPE];  /* utilization, strictly increasing in [0, 100] */
+  int32_t fit_shape_score[KSIM_MAX_SHAPE]; /* score already scaled to [0, 100]
+                                              (x MaxNodeScore / MaxCustomPriorityScore = x 10) */
+  int32_t preempt_min_pct;             /* DefaultPreemptionArgs.minCandidateNodesPercentage (default 10) */
+  int32_t preempt_min_abs;             /* ... minCandidateNodesAbsolute (default 100) */
 } ksim_profile;
 
 /* Full per-node outputs of one scheduling cycle (compat mode: what the

@@ -27,7 +27,7 @@ import (
 )
 
 // ABIVersion is the header version this binding was written against.
-const ABIVersion = 7
+const ABIVersion = 8
 
 // Engine owns one device handle (one GPU, or one node shard of a cluster).
 type Engine struct{ h *C.ksim_handle }

@@ -45,7 +45,7 @@ namespace ksim {
 __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPods& P, const BatchProg& bp,
                                                const ksim_pod& p, const NodeRow& r, bool trivial) {
   if (!trivial && !static_filters_pass(c, P, bp, p, r)) return false;
-  return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar);
+  return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar, c.fit_ignore);
 }
 
 // The S0 feasibility bitmaps, node-stationary: a block of 256 threads holds
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
   auto node_key = [&](int32_t local) -> uint64_t {
     const NodeRow r = load_res_row(c, local);       // scores read the resource columns only
     if constexpr (FAST) return dyn_key_fast(bp, p, r, c.inv_cpu[local], c.inv_mem[local], hseed, c.base + local);
-    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base, c.fit_ignore);
   };
   const uint64_t* mask = amask + (size_t)j * n_words;
   uint64_t a[kTopT];
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         // fitting changes the scored list even when every node is processed
         const bool normv = pnorm && (P.bflags[base + j] & kPodNormVaries) != 0;
         if ((cut >= 0 || normv) && was && !now) brk = true;
-        if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base);
+        if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base, c.fit_ignore);
         if (normv && v)
           v += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), NormRaw{pnorm[4 * j], pnorm[4 * j + 1]}) << 44;
       }

@@ -304,7 +304,7 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
       return dyn_key_fast(bq, fast_pod_fields(p), r, ld_off(c.inv_cpu, o8), ld_off(c.inv_mem, o8), hseed,
                           c.base + r.node);
     }
-    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+    return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base, c.fit_ignore);
   };
   NormRaw mx{0, 0};
   if (normv) {
@@ -322,7 +322,7 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
       for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
         NodeRow r = load_row(c, node);
         ov(r);
-        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base))
+        if (static_filters_pass(c, P, bp, p, r) && dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base, c.fit_ignore))
           acc.take(norm_raw(c, P, p, r));
       }
     }
@@ -353,7 +353,7 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
     {
       NodeRow r = trivial && !normv ? load_res_row(c, node) : load_row(c, node);
       ov(r);
-      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base);
+      if (trivial || static_filters_pass(c, P, bp, p, r)) kk = dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base, c.fit_ignore);
       if (normv && kk) kk += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), mx) << 44;
     }
     insert(kk);
@@ -600,7 +600,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
           if (scls >= 0 && P.stab_fast)
             return dyn_key_fast(bp, fast_pod_fields(p), x, c.inv_cpu[local], c.inv_mem[local],
                                 prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
-          return dyn_key(prof, bp, p, x, c.n_scalar, seq0 + j, c.base);
+          return dyn_key(prof, bp, p, x, c.n_scalar, seq0 + j, c.base, c.fit_ignore);
         };
         const bool sp = scls >= 0 ? stab_pass(w) : ((bf & kBatchStaticTrivial) || static_filters_pass(c, P, bp, p, r));
         const bool feas0 = normv && sp && key(r) != 0;   // at S0

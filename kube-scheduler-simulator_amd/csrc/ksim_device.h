@@ -37,7 +37,10 @@ struct DevCluster {
   // 0 on a replica that is not its group's first (rank 0): the runs every
   // replica executes whole (per-pod cycles, ADAPT batches) are counted in the
   // evaluation statistics once, by the first replica
-  int32_t count_whole, _pad_cw;
+  int32_t count_whole;
+  // NodeResourcesFitArgs ignoredResources / ignoredResourceGroups (ksim_profile
+  // fit_ignored_scalar): bit k = Fit's Filter skips scalar column k
+  uint32_t fit_ignore;
   const int64_t* alloc_cpu;
   const int64_t* alloc_mem;
   const int64_t* alloc_eph;
@@ -574,6 +577,24 @@ __device__ __forceinline__ bool required_node_affinity_match(const DevCluster& c
   return true;
 }
 
+// nodeaffinity.NodeAffinity.Filter: the profile's scheduler-enforced
+// addedAffinity first (errReasonEnforced, detail KSIM_NA_ENFORCED), then the
+// pod's selector and required terms (ErrReasonPod, detail 0).  Returns true
+// when the node passes.
+__device__ __forceinline__ bool node_affinity_filter(const DevCluster& c, const DevPods& P, const ksim_pod& p,
+                                                     int32_t node, uint32_t& detail) {
+  if (p.flags & KSIM_POD_ADDED_AFFINITY) {
+    bool any = false;
+    for (int i = 0; i < p.added_term_count && !any; i++) any = term_matches(c, P, P.terms[p.added_term_first + i], node);
+    if (!any) {
+      detail = KSIM_NA_ENFORCED;
+      return false;
+    }
+  }
+  detail = 0;
+  return required_node_affinity_match(c, P, p, node);
+}
+
 // VolumeBinding / VolumeZone (ksim_engine.h "Volume groups"): terms
 // [first, first + count) of the pod set in groups (ksim_term.weight = group
 // index, non-decreasing); true iff every group has a matching term.
@@ -631,8 +652,9 @@ __device__ __forceinline__ int64_t count_intolerable_prefer(const DevCluster& c,
   return n;
 }
 
-// noderesources fitsRequest -> reason bits
-__device__ __forceinline__ uint32_t fits_request(const NodeRow& r, const ksim_pod& p, int n_scalar) {
+// noderesources fitsRequest -> reason bits.  ignore: scalar columns the
+// profile's ignoredResources / ignoredResourceGroups name (extended resources).
+__device__ __forceinline__ uint32_t fits_request(const NodeRow& r, const ksim_pod& p, int n_scalar, uint32_t ignore) {
   uint32_t bits = 0;
   if (r.num_pods + 1 > r.alloc_pods) bits |= KSIM_FIT_TOO_MANY_PODS;
   if (p.req_cpu == 0 && p.req_mem == 0 && p.req_eph == 0 && !(p.flags & KSIM_POD_HAS_SCALAR)) return bits;
@@ -643,7 +665,7 @@ __device__ __forceinline__ uint32_t fits_request(const NodeRow& r, const ksim_po
   for (int k = 0; k < KSIM_MAX_SCALAR; k++) {
     if (k >= n_scalar) break;
     const int64_t q = p.scalar_req[k];
-    if (q != 0 && q > r.alloc_sc[k] - r.req_sc[k]) bits |= (KSIM_FIT_SCALAR0 << k);
+    if (q != 0 && !((ignore >> k) & 1u) && q > r.alloc_sc[k] - r.req_sc[k]) bits |= (KSIM_FIT_SCALAR0 << k);
   }
   return bits;
 }
@@ -692,18 +714,73 @@ __device__ __forceinline__ int64_t least_requested_q100(int64_t requested, int64
   return div_q100((capacity - requested) * kMaxNodeScore, capacity);
 }
 
-__device__ __forceinline__ int64_t fit_least_allocated_score(const NodeRow& r, const ksim_profile& prof, const ksim_pod& p,
-                                                    int n_scalar) {
+// most_allocated.go mostRequestedScore: requested clamped to capacity, Go
+// int64 arithmetic (the product wraps as leastRequestedScore's does).
+__device__ __forceinline__ int64_t most_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  const int64_t prod = (int64_t)((uint64_t)requested * (uint64_t)kMaxNodeScore);
+  if (capacity < 0 || prod < 0) return prod / capacity;
+  return div_floor_nonneg(prod, capacity);
+}
+
+// helper.BuildBrokenLinearFunction over the profile's RequestedToCapacityRatio
+// shape (scores already x 10): the first point whose utilization is >= p, the
+// segment before it interpolated in Go int64 (truncating) arithmetic.
+// Constant indices only, so the shape stays in scalar registers.
+__device__ __forceinline__ int64_t broken_linear(const ksim_profile& prof, int64_t p) {
+  int64_t res = 0, pu = 0, ps = 0;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < KSIM_MAX_SHAPE; i++) {
+    if (i < prof.fit_n_shape && !done) {
+      const int64_t u = prof.fit_shape_util[i], sc = prof.fit_shape_score[i];
+      if (p <= u) {
+        res = i == 0 ? sc : ps + (sc - ps) * (p - pu) / (u - pu);
+        done = true;
+      }
+      pu = u;
+      ps = sc;
+    }
+  }
+  return done ? res : ps;
+}
+
+// requested_to_capacity_ratio.go resourceScoringFunction
+__device__ __forceinline__ int64_t rtcr_resource_score(const ksim_profile& prof, int64_t requested, int64_t capacity) {
+  if (capacity == 0 || requested > capacity) return broken_linear(prof, 100);   // maxUtilization
+  const int64_t prod = (int64_t)((uint64_t)requested * 100u);
+  return broken_linear(prof, prod / capacity);
+}
+
+// NodeResourcesFit Score: resourceAllocationScorer.score with the profile's
+// ScoringStrategy (useRequested = false: the non-zero requests).  Resources a
+// node has no allocatable of (or an extended resource the pod does not
+// request) are left out of the map, hence of the weight sum.
+__device__ __forceinline__ int64_t fit_score(const NodeRow& r, const ksim_profile& prof, const ksim_pod& p,
+                                             int n_scalar) {
   int64_t node_score = 0, weight_sum = 0;
+  const int strat = prof.fit_strategy;
 #pragma unroll
   for (int i = 0; i < KSIM_MAX_RES; i++) {      // constant indices only (no exit): prof stays in registers
     int64_t a = 0, q = 0;
     if (i < prof.fit_n_res) calc_alloc_req(r, p, prof.fit_res[i], false, n_scalar, a, q);
     if (a == 0) continue;
-    node_score += least_requested_score(q, a) * prof.fit_res_weight[i];
-    weight_sum += prof.fit_res_weight[i];
+    const int64_t w = prof.fit_res_weight[i];
+    if (strat == KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO) {
+      const int64_t rs = rtcr_resource_score(prof, q, a);
+      if (rs > 0) {                             // only positive resource scores count
+        node_score += rs * w;
+        weight_sum += w;
+      }
+      continue;
+    }
+    node_score += (strat == KSIM_FIT_MOST_ALLOCATED ? most_requested_score(q, a) : least_requested_score(q, a)) * w;
+    weight_sum += w;
   }
   if (weight_sum == 0) return 0;
+  if (strat == KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO)   // math.Round(float64(nodeScore) / float64(weightSum))
+    return (int64_t)round((double)node_score / (double)weight_sum);
   if (node_score < 0 || weight_sum < 0) return node_score / weight_sum;
   return div_floor_nonneg(node_score, weight_sum);
 }
@@ -926,9 +1003,11 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (tid) { detail = tid; return (uint8_t)f; }
         break;
       }
-      case KSIM_PL_NODE_AFFINITY:
-        if (!required_node_affinity_match(c, P, p, node)) return (uint8_t)f;
+      case KSIM_PL_NODE_AFFINITY: {
+        uint32_t why;
+        if (!node_affinity_filter(c, P, p, node, why)) { detail = why; return (uint8_t)f; }
         break;
+      }
       case KSIM_PL_VOLUME_BINDING:
         if (p.vb_count && !volume_groups_match(c, P, p.vb_first, p.vb_count, node)) return (uint8_t)f;
         break;
@@ -936,7 +1015,7 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (p.vz_count && !volume_groups_match(c, P, p.vz_first, p.vz_count, node)) return (uint8_t)f;
         break;
       case KSIM_PL_NODE_RESOURCES_FIT: {
-        uint32_t bits = fits_request(r, p, c.n_scalar);
+        uint32_t bits = fits_request(r, p, c.n_scalar, c.fit_ignore);
         if (bits) { detail = bits; return (uint8_t)f; }
         break;
       }
@@ -973,7 +1052,7 @@ __device__ __forceinline__ int64_t score_plugin_raw(const DevCluster& c, const D
                                            const ksim_pod& p, int plugin, const NodeRow& r,
                                            const ksim_topo_use* U, const UseMasks& m, const TopoRow& t) {
   switch (plugin) {
-    case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(r, prof, p, c.n_scalar);
+    case KSIM_PL_NODE_RESOURCES_FIT: return fit_score(r, prof, p, c.n_scalar);
     case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(r, prof, p, c.n_scalar);
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer(c, p, r);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(c, P, p, r.node);
@@ -1015,7 +1094,9 @@ inline uint32_t plan_filter_en(const ksim_profile& prof, const ksim_pod& p, cons
         break;
       case KSIM_PL_NODE_NAME: on = p.node_name != -1; break;
       case KSIM_PL_TAINT_TOLERATION: on = hard_taints; break;
-      case KSIM_PL_NODE_AFFINITY: on = p.sel_count > 0 || (p.flags & KSIM_POD_HAS_REQUIRED_AFFINITY); break;
+      case KSIM_PL_NODE_AFFINITY:
+        on = p.sel_count > 0 || (p.flags & (KSIM_POD_HAS_REQUIRED_AFFINITY | KSIM_POD_ADDED_AFFINITY));
+        break;
       case KSIM_PL_NODE_PORTS: on = m.port != 0; break;
       case KSIM_PL_NODE_RESOURCES_FIT: on = true; break;
       case KSIM_PL_POD_TOPOLOGY_SPREAD: on = m.hard != 0; break;
@@ -1072,14 +1153,17 @@ __device__ __forceinline__ uint8_t run_filter_plan(const DevCluster& c, const De
     const uint32_t tid = find_matching_untolerated_taint(c, p, r);
     take(KSIM_PL_TAINT_TOLERATION, tid != 0, tid, false);
   }
-  if (fp.en & (1u << KSIM_PL_NODE_AFFINITY))
-    take(KSIM_PL_NODE_AFFINITY, !required_node_affinity_match(c, P, p, node), 0, false);
+  if (fp.en & (1u << KSIM_PL_NODE_AFFINITY)) {
+    uint32_t why;
+    const bool ok = node_affinity_filter(c, P, p, node, why);
+    take(KSIM_PL_NODE_AFFINITY, !ok, why, false);
+  }
   if (fp.en & (1u << KSIM_PL_VOLUME_BINDING))
     take(KSIM_PL_VOLUME_BINDING, !volume_groups_match(c, P, p.vb_first, p.vb_count, node), 0, false);
   if (fp.en & (1u << KSIM_PL_VOLUME_ZONE))
     take(KSIM_PL_VOLUME_ZONE, !volume_groups_match(c, P, p.vz_first, p.vz_count, node), 0, false);
   if (fp.en & (1u << KSIM_PL_NODE_RESOURCES_FIT)) {
-    const uint32_t bits = fits_request(r, p, c.n_scalar);
+    const uint32_t bits = fits_request(r, p, c.n_scalar, c.fit_ignore);
     take(KSIM_PL_NODE_RESOURCES_FIT, bits != 0, bits, false);
   }
   if (fp.en & (1u << KSIM_PL_NODE_PORTS)) take(KSIM_PL_NODE_PORTS, node_port_conflict(m, t), 0, false);
@@ -1164,7 +1248,7 @@ __device__ __forceinline__ int64_t run_score_plan(const DevCluster& c, const Dev
   if (plan_slot(sp, pl) >= 0) { dst = (expr); put(pl, dst); }
   int64_t v;
   KSIM_PUT(KSIM_PL_NODE_RESOURCES_FIT, v, fast ? (int64_t)fast_least_allocated(fast_prog(*fast), p, r, inv_c, inv_m)
-                                                : fit_least_allocated_score(r, prof, p, c.n_scalar));
+                                                : fit_score(r, prof, p, c.n_scalar));
   KSIM_PUT(KSIM_PL_BALANCED_ALLOCATION, v, fast ? (int64_t)fast_balanced_allocation(fast_prog(*fast), p, r, inv_c, inv_m)
                                                 : balanced_allocation_score(r, prof, p, c.n_scalar));
   KSIM_PUT(KSIM_PL_TAINT_TOLERATION, rv.taint, (c.cflags & kClusterPreferTaints) ? count_intolerable_prefer(c, p, r) : 0);
@@ -1502,9 +1586,11 @@ __device__ __forceinline__ bool static_filters_pass(const DevCluster& c, const D
       case KSIM_PL_TAINT_TOLERATION:
         if (find_matching_untolerated_taint(c, p, r)) return false;
         break;
-      case KSIM_PL_NODE_AFFINITY:
-        if (!required_node_affinity_match(c, P, p, r.node)) return false;
+      case KSIM_PL_NODE_AFFINITY: {
+        uint32_t why;
+        if (!node_affinity_filter(c, P, p, r.node, why)) return false;
         break;
+      }
       default:
         break;
     }
@@ -1697,11 +1783,12 @@ __device__ __forceinline__ uint64_t dyn_key_fast(const BatchProg& bp, const ksim
 // Pods with scalar requests take the generic functions (their Fit filter
 // checks the scalar columns).
 __device__ __forceinline__ uint64_t dyn_key(const ksim_profile& prof, const BatchProg& bp, const ksim_pod& p,
-                                            const NodeRow& r, int n_scalar, int64_t seq, int32_t base) {
+                                            const NodeRow& r, int n_scalar, int64_t seq, int32_t base,
+                                            uint32_t ignore) {
   if (bp.cpu_mem && !(p.flags & KSIM_POD_HAS_SCALAR)) return dyn_key_cpu_mem(prof, bp, p, r, seq, base);
-  if (bp.has_fit_filter && fits_request(r, p, n_scalar)) return 0;
+  if (bp.has_fit_filter && fits_request(r, p, n_scalar, ignore)) return 0;
   int64_t tot = 0;
-  if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, n_scalar);
+  if (bp.w_fit) tot += bp.w_fit * fit_score(r, prof, p, n_scalar);
   if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, n_scalar);
   if (prof.n_score == 0) tot = 1;
   return tb_key(tot, prof.tiebreak_seed, seq, base + r.node);

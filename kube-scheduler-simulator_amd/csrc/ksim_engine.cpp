@@ -319,6 +319,8 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
     if (!check_expr(p.sel_first + k)) return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad nodeSelector expr");
   if (!check_terms(p.req_term_first, p.req_term_count) || !check_terms(p.pref_term_first, p.pref_term_count))
     return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad affinity term range");
+  if ((p.flags & KSIM_POD_ADDED_AFFINITY) && (p.added_term_count <= 0 || !check_terms(p.added_term_first, p.added_term_count)))
+    return set_err(h, KSIM_E_INVALID, "pod " + std::to_string(i) + ": bad addedAffinity term range");
   const std::string who = "pod " + std::to_string(i) + ": ";
   for (const auto& vl : {std::make_pair(p.vb_first, p.vb_count), std::make_pair(p.vz_first, p.vz_count)}) {
     if (vl.second == 0) continue;
@@ -376,7 +378,8 @@ int validate_pod(ksim_handle* h, const ksim_pod_set* ps, int32_t i) {
 // NoSchedule/NoExecute taint in the cluster tolerated, no unschedulable node
 // (or tolerated).  The batch kernels then skip the static filters.
 bool static_trivial(const ksim_handle* h, const ksim_pod& p) {
-  if (p.node_name != -1 || p.sel_count > 0 || (p.flags & KSIM_POD_HAS_REQUIRED_AFFINITY)) return false;
+  if (p.node_name != -1 || p.sel_count > 0 || (p.flags & (KSIM_POD_HAS_REQUIRED_AFFINITY | KSIM_POD_ADDED_AFFINITY)))
+    return false;
   if (h->any_unschedulable && !(p.flags & KSIM_POD_TOLERATES_UNSCHEDULABLE)) return false;
   for (uint16_t id : h->hard_taints)
     if (!((p.tol_filter[id >> 6] >> (id & 63)) & 1ull)) return false;
@@ -421,8 +424,13 @@ bool stab_signature(const ksim_pod_set* ps, const ksim_pod& q, std::string& s) {
     put(&x.n_expr, sizeof x.n_expr);
     for (int32_t k = 0; k < x.n_expr; k++) put_expr(x.first_expr + k);
   };
-  const uint32_t fl = q.flags & (KSIM_POD_TOLERATES_UNSCHEDULABLE | KSIM_POD_HAS_REQUIRED_AFFINITY);
+  const uint32_t fl = q.flags & (KSIM_POD_TOLERATES_UNSCHEDULABLE | KSIM_POD_HAS_REQUIRED_AFFINITY |
+                                 KSIM_POD_ADDED_AFFINITY);
   put(&fl, sizeof fl);
+  if (q.flags & KSIM_POD_ADDED_AFFINITY) {
+    put(&q.added_term_count, sizeof q.added_term_count);
+    for (int32_t k = 0; k < q.added_term_count; k++) put_term(q.added_term_first + k, false);
+  }
   put(&q.node_name, sizeof q.node_name);
   put(q.tol_filter, sizeof q.tol_filter);
   put(q.tol_prefer, sizeof q.tol_prefer);
@@ -1616,10 +1624,32 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   }
   if (p->fit_n_res < 0 || p->fit_n_res > KSIM_MAX_RES || p->ba_n_res < 0 || p->ba_n_res > KSIM_MAX_RES)
     return set_err(h, KSIM_E_INVALID, "scoring resources out of range");
+  // NodeResourcesFitArgs / DefaultPreemptionArgs as validation.ValidateNodeResourcesFitArgs /
+  // ValidateDefaultPreemptionArgs accept them (the plugin constructors refuse anything else)
+  if (p->fit_strategy < KSIM_FIT_LEAST_ALLOCATED || p->fit_strategy > KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO)
+    return set_err(h, KSIM_E_INVALID, "unknown NodeResourcesFit scoring strategy");
+  if (p->fit_strategy == KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO) {
+    if (p->fit_n_shape < 1 || p->fit_n_shape > KSIM_MAX_SHAPE)
+      return set_err(h, KSIM_E_INVALID, "RequestedToCapacityRatio shape: 1..16 points");
+    for (int i = 0; i < p->fit_n_shape; i++) {
+      if (p->fit_shape_util[i] < 0 || p->fit_shape_util[i] > 100 || (i > 0 && p->fit_shape_util[i] <= p->fit_shape_util[i - 1]))
+        return set_err(h, KSIM_E_INVALID, "RequestedToCapacityRatio shape: utilization strictly increasing in [0, 100]");
+      if (p->fit_shape_score[i] < 0 || p->fit_shape_score[i] > 100 || p->fit_shape_score[i] % 10 != 0)
+        return set_err(h, KSIM_E_INVALID, "RequestedToCapacityRatio shape: score x 10 in [0, 100]");
+    }
+  }
+  if (p->fit_ignored_scalar >> KSIM_MAX_SCALAR) return set_err(h, KSIM_E_INVALID, "fit_ignored_scalar past the scalar columns");
+  if (p->preempt_min_pct < 0 || p->preempt_min_pct > 100 || p->preempt_min_abs < 0 ||
+      (p->preempt_min_pct == 0 && p->preempt_min_abs == 0))
+    return set_err(h, KSIM_E_INVALID, "DefaultPreemptionArgs: minCandidateNodesPercentage in [0, 100], "
+                                      "minCandidateNodesAbsolute >= 0, not both 0");
   // the profile compiled for batchable pods (see BatchProg in ksim_device.h)
   BatchProg bp{};
-  bp.cpu_mem = p->fit_n_res == 2 && p->fit_res[0] == KSIM_RES_CPU && p->fit_res[1] == KSIM_RES_MEMORY &&
-               p->ba_n_res == 2 && p->ba_res[0] == KSIM_RES_CPU && p->ba_res[1] == KSIM_RES_MEMORY;
+  // the FAST / cpu-memory keys implement LeastAllocated; the other strategies
+  // take the generic keys (fit_score)
+  bp.cpu_mem = p->fit_strategy == KSIM_FIT_LEAST_ALLOCATED && p->fit_n_res == 2 && p->fit_res[0] == KSIM_RES_CPU &&
+               p->fit_res[1] == KSIM_RES_MEMORY && p->ba_n_res == 2 && p->ba_res[0] == KSIM_RES_CPU &&
+               p->ba_res[1] == KSIM_RES_MEMORY;
   bp.fit_w_cpu = p->fit_res_weight[0];
   bp.fit_w_mem = p->fit_res_weight[1];
   bp.fast_w = bp.cpu_mem && bp.fit_w_cpu >= 1 && bp.fit_w_cpu < (1ll << 31) && bp.fit_w_mem >= 1 &&
@@ -1650,8 +1680,10 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
   // window size K is captured by value (from percentageOfNodesToScore)
+  // and the Fit filter's ignored scalar columns (DevCluster::fit_ignore)
   const bool keep_batch_graphs = h->has_profile &&
-                                 h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score;
+                                 h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score &&
+                                 h->dc.fit_ignore == p->fit_ignored_scalar;
   // batchability depends on the profile: a loaded queue must be reloaded (its
   // buffers stay allocated for ksim_load_pods to reuse)
   h->dp = DevPods{};
@@ -1668,6 +1700,7 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   }
   h->prof = *p;
   h->bp = bp;
+  h->dc.fit_ignore = p->fit_ignored_scalar;
   h->has_profile = true;
   if (keep_batch_graphs)
     drop_cycle_graphs(h);
@@ -1823,6 +1856,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   }
 #undef UP
   h->col_nvals = col_nvals;
+  c.fit_ignore = h->has_profile ? h->prof.fit_ignored_scalar : 0u;
   h->dc = c;
   h->taint_effect.assign(v->taint_effect, v->taint_effect + v->n_taints);
   {
@@ -2211,6 +2245,7 @@ static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std
   };
   copy_terms(pod.req_term_first, pod.req_term_count);
   copy_terms(pod.pref_term_first, pod.pref_term_count);
+  copy_terms(pod.added_term_first, pod.added_term_count);
   copy_terms(pod.vb_first, pod.vb_count);
   copy_terms(pod.vz_first, pod.vz_count);
 }

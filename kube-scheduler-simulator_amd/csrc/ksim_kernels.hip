@@ -185,6 +185,8 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P,
         cnt[i] = class_count(c, u.cls, node);
       }
     }
+    // requireAllTopologies is false for system-defaulted constraints (PreScore)
+    const bool sysdef = (p.topo_flags & KSIM_POD_PTS_SYSTEM_DEFAULT) != 0;
     bool all_hard = true, all_soft = true;         // nodeLabelsMatchSpreadConstraints per kind
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_USES; i++) {
@@ -200,13 +202,14 @@ __global__ __launch_bounds__(256) void k_topo_prefilter(DevCluster c, DevPods P,
 #pragma unroll
     for (int i = 0; i < KSIM_MAX_USES; i++) {
       const uint32_t v = val[i];
-      if (!((m.dom >> i) & 1u) || v == 0) continue;   // no table, or the node has no pair for this key
+      // no table, or the node has no pair for this key (system defaults: the pair (key, ""))
+      if (!((m.dom >> i) & 1u) || (v == 0 && !(sysdef && ((m.soft_val >> i) & 1u)))) continue;
       const bool incl = (!((m.honor_aff >> i) & 1u) || aff_ok) && (!((m.honor_taints >> i) & 1u) || taint_ok);
       int64_t add = cnt[i];
       if ((m.hard >> i) & 1u)                      // TpPairToMatchNum[pair] += count (+ presence mark)
         add = all_hard && incl ? add + (1ll << kDomMarkShift) : 0;
       else if ((m.soft_val >> i) & 1u)             // TopologyPairToPodCounts
-        add = all_soft && incl ? add : 0;
+        add = (all_soft || sysdef) && incl ? add : 0;
       if (add == 0) continue;
       if ((lds >> i) & 1u)
         atomicAdd(&s_dom[i][v], (unsigned long long)add);
@@ -402,9 +405,11 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     feasible = res == KSIM_PASSED;
     if (feasible) {
       // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
+      // (none for system-defaulted constraints: requireAllTopologies false)
+      const bool sysdef = (p.topo_flags & KSIM_POD_PTS_SYSTEM_DEFAULT) != 0;
 #pragma unroll
       for (int i = 0; i < KSIM_MAX_USES; i++) {
-        if (((m.soft >> i) & 1u) && t.v[i] == 0) ign = true;
+        if (((m.soft >> i) & 1u) && t.v[i] == 0 && !sysdef) ign = true;
         if (i == soft) soft_cnt = t.x[i];          // soft_count: the node's own count or the domain sum
       }
       s.ign[node] = ign;

@@ -45,14 +45,14 @@ __global__ __launch_bounds__(256) void k_preempt_nodes(DevCluster c, DevPods P, 
     while (j0 < b && pre.prio[j0] >= prio) j0++;       // lower priorities: the suffix [j0, b)
     NodeRow r = load_row(c, node);
     for (int32_t j = j0; j < b; j++) row_add_req(r, pre.req + (size_t)j * KSIM_PREEMPT_REQ, -1, c.n_scalar);
-    if (fits_request(r, p, c.n_scalar) == 0) {
+    if (fits_request(r, p, c.n_scalar, c.fit_ignore) == 0) {
       out.cand = 1;
       int32_t nv = 0, high = 0;
       int64_t sum = 0, early = INT64_MAX;
       for (int32_t j = j0; j < b; j++) {                 // reprievePod, most important first
         const int64_t* q = pre.req + (size_t)j * KSIM_PREEMPT_REQ;
         row_add_req(r, q, 1, c.n_scalar);
-        const bool victim = fits_request(r, p, c.n_scalar) != 0;
+        const bool victim = fits_request(r, p, c.n_scalar, c.fit_ignore) != 0;
         pre.vflag[j] = victim;
         if (victim) {
           row_add_req(r, q, -1, c.n_scalar);
@@ -86,7 +86,9 @@ __device__ __forceinline__ bool better(const PreemptNode& a, int32_t na, const P
 
 constexpr int kPickThreads = 1024;
 
-__global__ __launch_bounds__(kPickThreads) void k_preempt_pick(DevCluster c, DevPreempt pre) {
+// min_pct / min_abs: DefaultPreemptionArgs (calculateNumCandidates)
+__global__ __launch_bounds__(kPickThreads) void k_preempt_pick(DevCluster c, DevPreempt pre, int32_t min_pct,
+                                                               int32_t min_abs) {
   __shared__ int32_t sh[kPickThreads / 64];
   __shared__ PreemptNode s_best[kPickThreads];
   __shared__ int32_t s_node[kPickThreads];
@@ -133,8 +135,8 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(DevCluster c, Dev
     cexcl = base + y - ncand;
     total_cand = tot;
   }
-  int32_t want = total_pot * 10 / 100;
-  if (want < 100) want = 100;
+  int32_t want = total_pot * min_pct / 100;
+  if (want < min_abs) want = min_abs;
   if (want > total_pot) want = total_pot;
   PreemptNode best{};
   int32_t best_node = -1, rank = cexcl;
@@ -170,7 +172,7 @@ void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_inde
   const int blocks = (a.c.n + 255) / 256;
   launch_filter_only(a, stream);                         // the filter statuses of every node
   k_preempt_nodes<<<blocks, 256, 0, stream>>>(a.c, a.P, a.st, a.s, pre, fit_index, prio);
-  k_preempt_pick<<<1, kPickThreads, 0, stream>>>(a.c, pre);
+  k_preempt_pick<<<1, kPickThreads, 0, stream>>>(a.c, pre, a.prof.preempt_min_pct, a.prof.preempt_min_abs);
 }
 
 }  // namespace ksim

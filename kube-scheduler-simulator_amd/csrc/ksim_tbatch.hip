@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void k_tb_filter(DevCluster c, DevPods P0, con
     if (feasible) {
 #pragma unroll
       for (int i = 0; i < KSIM_MAX_USES; i++) {
-        if (((m.soft >> i) & 1u) && t.v[i] == 0) ign = true;
+        if (((m.soft >> i) & 1u) && t.v[i] == 0 && !(p.topo_flags & KSIM_POD_PTS_SYSTEM_DEFAULT)) ign = true;
         if (i == soft) soft_cnt = t.x[i];
       }
       q.ign[node] = ign;
@@ -340,13 +340,13 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
       const ksim_pod& p = P.pods[base + j];
       NodeRow r = load_row(c, local);
       row_add_pod(r, P.pods[base + k], 1);
-      if (bp.has_fit_filter && fits_request(r, p, c.n_scalar)) {
+      if (bp.has_fit_filter && fits_request(r, p, c.n_scalar, c.fit_ignore)) {
         inv = true;
       } else {
         int64_t tot = 0;
         if (sv != kStatOne) {
           tot = sv;
-          if (bp.w_fit) tot += bp.w_fit * fit_least_allocated_score(r, prof, p, c.n_scalar);
+          if (bp.w_fit) tot += bp.w_fit * fit_score(r, prof, p, c.n_scalar);
           if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, c.n_scalar);
         }
         v = tb_key(tot, prof.tiebreak_seed, seq0 + j, c.base + local);

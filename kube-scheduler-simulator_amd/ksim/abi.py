@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -21,6 +21,7 @@ EXPR_VALS = 6
 MAX_FILTER = 16
 MAX_SCORE = 8
 MAX_RES = 4
+MAX_SHAPE = 16
 MAX_USES = 16
 MAX_CLASSES = 4096
 COL_NONE = 0xFFFF
@@ -89,6 +90,7 @@ POD_HAS_HOST_PORTS = 8
 POD_HAS_VOLUMES = 16
 POD_NODE_NAMES = 32            # NodeAffinity PreFilterResult restricts the scan (nn_first, nn_count)
 POD_NODE_NAMES_UNKNOWN = 64    # ... and names a node the snapshot lacks: the cycle errors
+POD_ADDED_AFFINITY = 128       # NodeAffinityArgs.addedAffinity required terms (added_term_first, added_term_count)
 
 # pod nb_flags
 POD_NB_INGRESS_BAD = 1
@@ -96,6 +98,7 @@ POD_NB_EGRESS_BAD = 2
 
 # pod topo_flags
 POD_IPA_SELF_AFFINITY = 1
+POD_PTS_SYSTEM_DEFAULT = 2     # system-defaulted spread constraints: PreScore's requireAllTopologies = false
 
 # topology uses (ksim_topo_use.kind)
 USE_PTS_HARD = 0
@@ -118,6 +121,14 @@ PTS_SKEW = 2
 IPA_AFFINITY = 1
 IPA_ANTI_AFFINITY = 2
 IPA_EXISTING_ANTI = 3
+NA_ENFORCED = 1                # NodeAffinity failed the scheduler-enforced addedAffinity
+
+# NodeResourcesFit scoring strategies
+FIT_LEAST_ALLOCATED = 0
+FIT_MOST_ALLOCATED = 1
+FIT_REQUESTED_TO_CAPACITY_RATIO = 2
+FIT_STRATEGY_ID = {"LeastAllocated": FIT_LEAST_ALLOCATED, "MostAllocated": FIT_MOST_ALLOCATED,
+                   "RequestedToCapacityRatio": FIT_REQUESTED_TO_CAPACITY_RATIO}
 
 OP_IN = 0
 OP_NOT_IN = 1
@@ -171,7 +182,8 @@ POD_DTYPE = np.dtype(
      ("use_first", "<i4"), ("use_count", "<i4"), ("add_first", "<i4"), ("add_count", "<i4"),
      ("topo_flags", "<u4"), ("nb_flags", "<u4"), ("nn_first", "<i4"), ("nn_count", "<i4"),
      ("vb_first", "<i4"), ("vb_count", "<i4"), ("vz_first", "<i4"), ("vz_count", "<i4"),
-     ("nb_req", "<i8"), ("nb_add", "<i8")], align=True)
+     ("nb_req", "<i8"), ("nb_add", "<i8"), ("added_term_first", "<i4"), ("added_term_count", "<i4")],
+    align=True)
 TOPO_USE_DTYPE = np.dtype(
     [("cls", "<i4"), ("arg", "<i4"), ("col", "<u2"), ("kind", "u1"), ("flags", "u1"), ("_pad", "<i4")],
     align=True)
@@ -234,8 +246,11 @@ class Profile(ctypes.Structure):
         ("fit_res_weight", ctypes.c_int64 * MAX_RES),
         ("ba_n_res", ctypes.c_int32), ("ba_res", ctypes.c_int32 * MAX_RES),
         ("ba_res_weight", ctypes.c_int64 * MAX_RES),
-        ("hard_pod_affinity_weight", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("hard_pod_affinity_weight", ctypes.c_int32), ("fit_ignored_scalar", ctypes.c_uint32),
         ("tiebreak_seed", ctypes.c_uint64),
+        ("fit_strategy", ctypes.c_int32), ("fit_n_shape", ctypes.c_int32),
+        ("fit_shape_util", ctypes.c_int32 * MAX_SHAPE), ("fit_shape_score", ctypes.c_int32 * MAX_SHAPE),
+        ("preempt_min_pct", ctypes.c_int32), ("preempt_min_abs", ctypes.c_int32),
     ]
 
 

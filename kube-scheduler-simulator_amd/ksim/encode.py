@@ -552,20 +552,36 @@ def _tol_bits(tolerations: Sequence[Toleration], vocab: Sequence[Taint]) -> np.n
     return w
 
 
-def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None) -> EncodedPods:
+def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None, added_affinity=None,
+                spread=None) -> EncodedPods:
     """Compile pods against the cluster vocabulary (the per-pod PreFilter /
     PreScore precomputation of Fit, TaintToleration and NodeAffinity).
     ``volumes``: a ksim.volumes.VolumeIndex for pods with PersistentVolumeClaims
     (VolumeBinding / VolumeZone groups); without one such pods are flagged
-    KSIM_POD_HAS_VOLUMES (the engine refuses them)."""
+    KSIM_POD_HAS_VOLUMES (the engine refuses them).
+    ``added_affinity``: the profile's NodeAffinityArgs (ksim.profile): its
+    required terms become every pod's KSIM_POD_ADDED_AFFINITY terms (one shared
+    term range), its preferred terms are appended to every pod's own
+    (nodeaffinity.Score adds both sums).
+    ``spread``: a ksim.topology.SpreadDefaults (the profile's PodTopologySpread
+    default constraints and the Services / controllers that select pods)."""
     b = _PodBuilder(cluster)
+    added_first = added_count = 0
+    added_pref = []
+    if added_affinity is not None:
+        if added_affinity.required is not None:
+            added_first = len(b.terms)
+            for t in added_affinity.required:
+                b.term(t)
+            added_count = len(b.terms) - added_first
+        added_pref = [pt for pt in added_affinity.preferred if pt.weight]
     arr = np.zeros(len(pods), abi.POD_DTYPE)
     names = []
     topo = cluster.topo
     topo.deferred = topo.matcher is not None
     try:
         for p in pods:                        # pass 1: every class exists before any adds
-            register_pod_classes(topo, p)
+            register_pod_classes(topo, p, spread)
     except TopologyError as e:
         raise EncodeError(str(e)) from e
     if topo.deferred:                         # the new classes' counts, the pods' matches (device)
@@ -621,7 +637,12 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None) -> E
             if pt.weight == 0:
                 continue
             b.term(pt.term, pt.weight)
+        for pt in added_pref:                 # pl.addedPrefSchedTerms.Score(node)
+            b.term(pt.term, pt.weight)
         rec["pref_term_count"] = len(b.terms) - rec["pref_term_first"]
+        if added_count:
+            flags |= abi.POD_ADDED_AFFINITY
+            rec["added_term_first"], rec["added_term_count"] = added_first, added_count
         if p.has_volumes:
             flags |= abi.POD_HAS_VOLUMES
         elif p.pvc_claims:
@@ -651,7 +672,7 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None) -> E
             nn.extend(known)
         rec["flags"] = flags
         try:
-            u, tflags = pod_uses(topo, cluster, p)
+            u, tflags = pod_uses(topo, cluster, p, spread)
         except TopologyError as e:
             raise EncodeError(str(e)) from e
         rec["use_first"], rec["use_count"] = len(uses), len(u)

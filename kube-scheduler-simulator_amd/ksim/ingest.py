@@ -35,7 +35,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import profile as prof_mod
-from .model import Node, Pod, node_from_dict, pod_from_dict, pv_from_dict, pvc_from_dict, storage_class_from_dict
+from .model import (Controller, Node, Pod, Service, controller_from_dict, node_from_dict, pod_from_dict, pv_from_dict,
+                    pvc_from_dict, service_from_dict, storage_class_from_dict)
 from .volumes import VolumeIndex, VolumeUnsupported
 from .netbw import NetworkBandwidthArgs
 
@@ -50,6 +51,12 @@ class Snapshot:
     unsupported: List[Tuple[str, str, str]] = field(default_factory=list)   # (namespace, name, why)
     volumes: Optional[VolumeIndex] = None    # the document's PVs / PVCs (VolumeBinding, VolumeZone)
     counts: Dict[str, int] = field(default_factory=dict)
+    # Services and controllers that select pods (PodTopologySpread default
+    # constraints, helper.DefaultSelector).  Not part of the reference's
+    # export document: a host fills them from its listers (optional keys
+    # "services", "replicationControllers", "replicaSets", "statefulSets").
+    services: List[Service] = field(default_factory=list)
+    controllers: List[Controller] = field(default_factory=list)
 
 
 # ---- priority (admission: priority from PriorityClass) -------------------------------
@@ -89,32 +96,139 @@ _EXT_JSON = {"queueSort": "queueSort", "preFilter": "preFilter", "filter": "filt
              "preBind": "preBind", "bind": "bind", "postBind": "postBind"}
 
 
+class UnsupportedArgs(ValueError):
+    """A pluginConfig argument the engine does not implement (refused, never dropped)."""
+
+
+def _check_keys(plugin: str, args: dict, known: Sequence[str]) -> None:
+    for k in args:
+        if k not in known and k not in ("kind", "apiVersion"):
+            raise UnsupportedArgs(f"{plugin} args: {k!r} not supported by the engine")
+
+
+def _fit_args(args: dict, cur: prof_mod.FitArgs) -> prof_mod.FitArgs:
+    """NodeResourcesFitArgs decoded over the current (default) object: a field
+    the document sets replaces it, a nested object is merged field by field
+    (json.Unmarshal into the typed default, plugins.go:131-136)."""
+    _check_keys("NodeResourcesFit", args, ("ignoredResources", "ignoredResourceGroups", "scoringStrategy"))
+    fit = prof_mod.FitArgs(cur.strategy, list(cur.resources), None if cur.shape is None else list(cur.shape),
+                           list(cur.ignored_resources), list(cur.ignored_resource_groups))
+    if "ignoredResources" in args:
+        fit.ignored_resources = [str(x) for x in args["ignoredResources"] or []]
+    if "ignoredResourceGroups" in args:
+        fit.ignored_resource_groups = [str(x) for x in args["ignoredResourceGroups"] or []]
+    if "scoringStrategy" in args:
+        ss = args["scoringStrategy"]
+        if ss is None:                                  # nil: SetDefaults_NodeResourcesFitArgs
+            return prof_mod.FitArgs(ignored_resources=fit.ignored_resources,
+                                    ignored_resource_groups=fit.ignored_resource_groups)
+        _check_keys("NodeResourcesFit scoringStrategy", ss, ("type", "resources", "requestedToCapacityRatio"))
+        if ss.get("type"):
+            fit.strategy = str(ss["type"])
+        if "resources" in ss:
+            fit.resources = [(r["name"], int(r.get("weight") or 1)) for r in ss["resources"] or []]
+            if not fit.resources:                       # empty: the default set (SetDefaults)
+                fit.resources = [("cpu", 1), ("memory", 1)]
+        if ss.get("requestedToCapacityRatio") is not None:
+            rt = ss["requestedToCapacityRatio"]
+            _check_keys("requestedToCapacityRatio", rt, ("shape",))
+            fit.shape = [(int(x.get("utilization") or 0), int(x.get("score") or 0)) for x in rt.get("shape") or []]
+    return fit
+
+
+def _node_affinity_args(args: dict) -> prof_mod.NodeAffinityArgs:
+    from .model import _term, PreferredTerm
+    _check_keys("NodeAffinity", args, ("addedAffinity",))
+    aa = args.get("addedAffinity") or {}
+    _check_keys("NodeAffinity addedAffinity", aa, ("requiredDuringSchedulingIgnoredDuringExecution",
+                                                   "preferredDuringSchedulingIgnoredDuringExecution"))
+    out = prof_mod.NodeAffinityArgs()
+    req = aa.get("requiredDuringSchedulingIgnoredDuringExecution")
+    if req is not None:
+        terms = [_term(t) for t in req.get("nodeSelectorTerms") or []]
+        if not terms:                                   # ValidateNodeAffinityArgs -> ValidateNodeSelector
+            raise ValueError("NodeAffinityArgs.addedAffinity: must have at least one node selector term")
+        out.required = terms
+    for pt in aa.get("preferredDuringSchedulingIgnoredDuringExecution") or []:
+        w = int(pt.get("weight") or 0)
+        if not 1 <= w <= 100:                           # ValidatePreferredSchedulingTerms
+            raise ValueError("NodeAffinityArgs.addedAffinity: preferred term weight must be in the range 1-100")
+        out.preferred.append(PreferredTerm(w, _term(pt.get("preference") or {})))
+    return out
+
+
+def _spread_args(args: dict, cur: prof_mod.PodTopologySpreadArgs) -> prof_mod.PodTopologySpreadArgs:
+    from .model import _spread
+    _check_keys("PodTopologySpread", args, ("defaultConstraints", "defaultingType"))
+    out = prof_mod.PodTopologySpreadArgs(cur.defaulting_type, list(cur.default_constraints))
+    if args.get("defaultingType"):
+        out.defaulting_type = str(args["defaultingType"])
+    if "defaultConstraints" in args:
+        out.default_constraints = []
+        for d in args["defaultConstraints"] or []:
+            _check_keys("PodTopologySpread defaultConstraints", d, ("maxSkew", "topologyKey", "whenUnsatisfiable",
+                                                                     "labelSelector", "minDomains",
+                                                                     "nodeAffinityPolicy", "nodeTaintsPolicy",
+                                                                     "matchLabelKeys"))
+            if d.get("matchLabelKeys"):
+                raise UnsupportedArgs("PodTopologySpread defaultConstraints: matchLabelKeys not supported")
+            out.default_constraints.append(_spread(d))
+    prof_mod.validate_spread_args(out)
+    return out
+
+
+def _preemption_args(args: dict, cur: prof_mod.PreemptionArgs) -> prof_mod.PreemptionArgs:
+    _check_keys("DefaultPreemption", args, ("minCandidateNodesPercentage", "minCandidateNodesAbsolute"))
+    out = prof_mod.PreemptionArgs(cur.min_candidate_nodes_percentage, cur.min_candidate_nodes_absolute)
+    if args.get("minCandidateNodesPercentage") is not None:
+        out.min_candidate_nodes_percentage = int(args["minCandidateNodesPercentage"])
+    if args.get("minCandidateNodesAbsolute") is not None:
+        out.min_candidate_nodes_absolute = int(args["minCandidateNodesAbsolute"])
+    return out
+
+
 def profile_from_config(p: dict) -> prof_mod.SchedulerProfile:
-    """One v1beta2 KubeSchedulerProfile -> the converted SchedulerProfile."""
+    """One v1beta2 KubeSchedulerProfile -> the converted SchedulerProfile.
+    NewPluginConfig (plugins.go:103-179): each in-tree plugin's args are the
+    default object with the document's fields decoded over it.  Every arg is
+    implemented or refused (UnsupportedArgs), none is dropped."""
     plugins = {}
     for key, ext in _EXT_JSON.items():
         if key in (p.get("plugins") or {}):
             plugins[ext] = _plugin_set(p["plugins"][key])
     sp = prof_mod.SchedulerProfile(plugins=prof_mod.convert_for_simulator(plugins))
-    # NewPluginConfig: user args override the defaults (Object over Raw: JSON carries the object)
     for pc in p.get("pluginConfig") or []:
         name, args = pc.get("name", ""), pc.get("args") or {}
         if name == "NodeResourcesFit":
-            ss = args.get("scoringStrategy") or {}
-            if ss.get("type", "LeastAllocated") != "LeastAllocated":
-                raise ValueError(f"NodeResourcesFit scoringStrategy {ss.get('type')} not supported by the engine")
-            if ss.get("resources"):
-                sp.fit = prof_mod.FitArgs("LeastAllocated", [(r["name"], int(r.get("weight") or 1))
-                                                             for r in ss["resources"]])
+            sp.fit = _fit_args(args, sp.fit)
         elif name == "NodeResourcesBalancedAllocation":
+            _check_keys(name, args, ("resources",))
             if args.get("resources"):
                 sp.balanced = prof_mod.BalancedAllocationArgs([(r["name"], int(r.get("weight") or 1))
                                                                for r in args["resources"]])
         elif name == "InterPodAffinity":
+            _check_keys(name, args, ("hardPodAffinityWeight", "ignorePreferredTermsOfExistingPods"))
+            if args.get("ignorePreferredTermsOfExistingPods"):
+                raise UnsupportedArgs("InterPodAffinity args: ignorePreferredTermsOfExistingPods not supported")
             if args.get("hardPodAffinityWeight") is not None:
                 sp.hard_pod_affinity_weight = int(args["hardPodAffinityWeight"])
+                if not 0 <= sp.hard_pod_affinity_weight <= 100:   # ValidateInterPodAffinityArgs
+                    raise ValueError("InterPodAffinityArgs.hardPodAffinityWeight not in valid range [0, 100]")
+        elif name == "NodeAffinity":
+            sp.node_affinity = _node_affinity_args(args)
+        elif name == "PodTopologySpread":
+            sp.spread = _spread_args(args, sp.spread)
+        elif name == "DefaultPreemption":
+            sp.preemption = _preemption_args(args, sp.preemption)
+        elif name == "VolumeBinding":
+            # bindTimeoutSeconds bounds PreBind's wait (no placement effect);
+            # shape scores capacity only behind the VolumeCapacityPriority gate (off)
+            _check_keys(name, args, ("bindTimeoutSeconds", "shape"))
         elif name == "NetworkBandwidth":
             sp.network_bandwidth = NetworkBandwidthArgs.from_config(args)
+        elif name in prof_mod.SUPPORTED_FILTER or name in prof_mod.SUPPORTED_SCORE:
+            if args and set(args) - {"kind", "apiVersion"}:
+                raise UnsupportedArgs(f"{name} takes no args the engine knows: {sorted(args)}")
     sp.percentage_of_nodes_to_score = 0      # non-profile fields are reset to the defaults
     return sp
 
@@ -165,14 +279,22 @@ def load(doc: dict) -> Snapshot:
     keyed.sort(key=lambda t: t[:3])           # PrioritySort, then queue arrival
     pending = [t[3] for t in keyed]
     volumes.add_users(bound)                  # ReadWriteOncePod claims already in use
+    services = [service_from_dict(d) for d in doc.get("services") or []]
+    controllers = [controller_from_dict(kind, d) for key, kind in
+                   (("replicationControllers", "ReplicationController"), ("replicaSets", "ReplicaSet"),
+                    ("statefulSets", "StatefulSet")) for d in doc.get(key) or []]
     return Snapshot(nodes, bound, pending, namespaces, profiles_from_config(doc.get("schedulerConfig")),
                     unsupported, volumes,
                     {k: len(doc.get(k) or []) for k in ("pods", "nodes", "pvs", "pvcs", "storageClasses",
-                                                         "priorityClasses", "namespaces")})
+                                                         "priorityClasses", "namespaces", "services",
+                                                         "replicaSets")},
+                    services, controllers)
 
 
 def schedule_queue(backend, cluster, pending: Sequence[Pod], volumes: Optional[VolumeIndex] = None,
-                   nodes: Optional[Sequence[Node]] = None) -> List[Optional[str]]:
+                   nodes: Optional[Sequence[Node]] = None,
+                   profile: Optional[prof_mod.SchedulerProfile] = None,
+                   snap: Optional[Snapshot] = None) -> List[Optional[str]]:
     """Schedule ``pending`` in queue order on ``backend`` (a ksim.engine.Engine
     or the oracle: ``schedule_batch`` / ``schedule`` and ``eval_pod`` / ``cycle``)
     whose cluster is ``cluster``; returns each pod's node name (None: not
@@ -191,12 +313,12 @@ def schedule_queue(backend, cluster, pending: Sequence[Pod], volumes: Optional[V
         while j < n and not (volumes is not None and volumes.stateful(pending[j])):
             j += 1
         if j > i:
-            enc = encode_pods(cluster, pending[i:j], volumes=volumes)
+            enc = encode_pods(cluster, pending[i:j], volumes=volumes, **_pod_args(profile, snap))
             run = backend.schedule_batch(enc) if hasattr(backend, "schedule_batch") else backend.schedule(enc)
             out.extend(cluster.node_names[c] if c >= 0 else None for c in run[0])
         if j < n:
             pod = pending[j]
-            enc = encode_pods(cluster, [pod], volumes=volumes)
+            enc = encode_pods(cluster, [pod], volumes=volumes, **_pod_args(profile, snap))
             r = backend.eval_pod(enc, 0) if hasattr(backend, "eval_pod") else backend.cycle(enc, 0)
             node = cluster.node_names[r["chosen"]] if r["chosen"] >= 0 else None
             if node is not None:
@@ -207,12 +329,22 @@ def schedule_queue(backend, cluster, pending: Sequence[Pod], volumes: Optional[V
     return out
 
 
+def _pod_args(profile: Optional[prof_mod.SchedulerProfile], snap: Optional[Snapshot] = None) -> dict:
+    """The profile-dependent part of the pod compile (encode_pods keywords):
+    NodeAffinity's addedAffinity, PodTopologySpread's default constraints."""
+    if profile is None:
+        return {}
+    from .topology import SpreadDefaults
+    return {"added_affinity": profile.node_affinity,
+            "spread": SpreadDefaults(profile.spread, snap.services if snap else (), snap.controllers if snap else ())}
+
+
 def encode(snap: Snapshot, profile_index: int = 0):
     """(EncodedCluster, EncodedPods of the pending queue, compiled profile)."""
     from .encode import encode_cluster, encode_pods
     sp = snap.profiles[profile_index][1]
     cluster, _ = encode_cluster(snap.nodes, snap.bound, namespaces=snap.namespaces, nb_args=sp.network_bandwidth)
-    pods = encode_pods(cluster, snap.pending, volumes=snap.volumes)
+    pods = encode_pods(cluster, snap.pending, volumes=snap.volumes, **_pod_args(sp, snap))
     return cluster, pods, prof_mod.compile_profile(sp, cluster.scalar_names)
 
 

@@ -246,6 +246,8 @@ class Pod:
     pod_anti_affinity_required: List[PodAffinityTerm] = field(default_factory=list)
     pod_anti_affinity_preferred: List[WeightedPodAffinityTerm] = field(default_factory=list)
     annotations: Dict[str, str] = field(default_factory=dict)
+    # metav1.GetControllerOf: (apiVersion, kind, name) of the ownerReference with controller: true
+    owner: Optional[Tuple[str, str, str]] = None
 
     def has_pod_affinity(self) -> bool:
         """PodInfo: pods with any (anti)affinity term (NodeInfo.PodsWithAffinity)."""
@@ -426,4 +428,41 @@ def pod_from_dict(d: dict) -> Pod:
         pod_anti_affinity_preferred=[_weighted(t) for t in
                                      (paa.get("preferredDuringSchedulingIgnoredDuringExecution") or [])],
         annotations={k: str(v) for k, v in (md.get("annotations") or {}).items()},
+        owner=next(((o.get("apiVersion", ""), o.get("kind", ""), o.get("name", ""))
+                    for o in (md.get("ownerReferences") or []) if o.get("controller")), None),
     )
+
+
+@dataclass
+class Service:
+    """v1.Service as helper.GetPodServices reads it: a nil selector matches no pod."""
+    name: str
+    namespace: str = "default"
+    selector: Optional[Dict[str, str]] = None
+
+
+@dataclass
+class Controller:
+    """A ReplicationController (selector: a label map, nil = none) or a
+    ReplicaSet / StatefulSet (selector: a LabelSelector, nil = Nothing), as
+    helper.DefaultSelector reads them; kind is the object's Kind."""
+    kind: str
+    name: str
+    namespace: str = "default"
+    selector: object = None
+
+
+def service_from_dict(d: dict) -> Service:
+    md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
+    sel = spec.get("selector")
+    return Service(md.get("name", ""), md.get("namespace", "default"), None if sel is None else dict(sel))
+
+
+def controller_from_dict(kind: str, d: dict) -> Controller:
+    md, spec = d.get("metadata", {}) or {}, d.get("spec", {}) or {}
+    sel = spec.get("selector")
+    if kind == "ReplicationController":
+        sel = None if sel is None else dict(sel)
+    else:
+        sel = _selector(sel)
+    return Controller(kind, md.get("name", ""), md.get("namespace", "default"), sel)

@@ -29,13 +29,14 @@ A pod's "uses" (ksim_topo_use) list which class / key / role it needs; its
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import abi
-from .model import LabelSelector, Pod, PodAffinityTerm
+from .model import Controller, LabelSelector, Pod, PodAffinityTerm, Requirement, Service, TopologySpreadConstraint
 
 LABEL_HOSTNAME = "kubernetes.io/hostname"
 
@@ -393,6 +394,70 @@ class TopologyIndex:
         return np.stack(self.counts).astype(np.int32)
 
 
+# ---- PodTopologySpread default constraints ---------------------------------------
+class SpreadDefaults:
+    """podtopologyspread.buildDefaultConstraints with helper.DefaultSelector
+    (v1.26): a pod with no topologySpreadConstraints of its own takes the
+    profile's default constraints (PodTopologySpreadArgs: System = hostname
+    maxSkew 3 and zone maxSkew 5, both ScheduleAnyway; List = the args'
+    defaultConstraints), with the selector merged from the Services that
+    select it and its controlling ReplicationController / ReplicaSet /
+    StatefulSet; none when that selector is empty.  The simulator runs the
+    Deployment and ReplicaSet controllers
+    (/root/reference/simulator/controller/controller.go:79-80), so every
+    Deployment pod is ReplicaSet-owned."""
+
+    def __init__(self, args, services: Sequence[Service] = (), controllers: Sequence[Controller] = ()):
+        self.args = args
+        self.system = args.defaulting_type == "System"
+        self.defaults = args.constraints()
+        self.services: Dict[str, List[Service]] = {}
+        for s in services:
+            self.services.setdefault(s.namespace, []).append(s)
+        self.controllers = {(c.kind, c.namespace, c.name): c for c in controllers}
+
+    def default_selector(self, pod: Pod) -> Optional[LabelSelector]:
+        """helper.DefaultSelector; None when the selector is Empty()."""
+        label_set: Dict[str, str] = {}
+        for svc in self.services.get(pod.namespace, []):          # GetPodServices
+            if svc.selector is None:                               # nil selectors match nothing
+                continue
+            if all(pod.labels.get(k) == v for k, v in svc.selector.items()):
+                label_set.update(svc.selector)                     # labels.Merge
+        extra: List[Requirement] = []
+        if pod.owner is not None:
+            api, kind, name = pod.owner
+            if (api, kind) == ("v1", "ReplicationController"):
+                rc = self.controllers.get(("ReplicationController", pod.namespace, name))
+                if rc is not None and rc.selector:
+                    label_set.update(rc.selector)
+            elif (api, kind) in (("apps/v1", "ReplicaSet"), ("apps/v1", "StatefulSet")):
+                obj = self.controllers.get((kind, pod.namespace, name))
+                sel = obj.selector if obj is not None else None
+                if sel is not None:                                # nil: labels.Nothing(), no requirements
+                    _validate_selector(sel)
+                    extra += [Requirement(k, "In", [v]) for k, v in sorted(sel.match_labels.items())]
+                    extra += list(sel.match_expressions)
+        if not label_set and not extra:
+            return None
+        return LabelSelector(dict(label_set), extra)
+
+    def constraints(self, pod: Pod) -> Tuple[List[TopologySpreadConstraint], bool]:
+        """(the pod's spread constraints, whether they are system defaults)."""
+        if pod.topology_spread:
+            return list(pod.topology_spread), False
+        if not self.defaults:
+            return [], False
+        sel = self.default_selector(pod)
+        if sel is None:
+            return [], False
+        return [dataclasses.replace(c, label_selector=sel) for c in self.defaults], self.system
+
+
+def pod_spread(spread: Optional[SpreadDefaults], pod: Pod) -> Tuple[List[TopologySpreadConstraint], bool]:
+    return spread.constraints(pod) if spread is not None else (list(pod.topology_spread), False)
+
+
 # ---- per-pod compilation -------------------------------------------------------
 DEFAULT_BIND_ALL_HOST_IP = "0.0.0.0"
 _MB = 1024 * 1024
@@ -424,12 +489,12 @@ def _col(cluster, key: str) -> int:
     return abi.COL_NONE if c < 0 else c
 
 
-def register_pod_classes(topo: TopologyIndex, pod: Pod) -> None:
+def register_pod_classes(topo: TopologyIndex, pod: Pod, spread: Optional[SpreadDefaults] = None) -> None:
     """Pass 1: every class the pod will use or carry exists before any pod's
     adds are computed (so a later queue pod's selector counts earlier ones)."""
     topo.note_namespace(pod.namespace)
     topo.carried_terms(pod)
-    for c in pod.topology_spread:
+    for c in pod_spread(spread, pod)[0]:
         _validate_selector(c.label_selector)
         if c.label_selector is not None and not c.label_selector.empty():
             topo.selector_class(Matcher(frozenset([pod.namespace]), False, topo._sel_key(c.label_selector)))
@@ -447,13 +512,16 @@ def _use(kind, cls, col, arg=0, flags=0):
     return (cls, arg, col, kind, flags)
 
 
-def pod_uses(topo: TopologyIndex, cluster, pod: Pod) -> Tuple[List[tuple], int]:
+def pod_uses(topo: TopologyIndex, cluster, pod: Pod, spread: Optional[SpreadDefaults] = None) -> Tuple[List[tuple], int]:
     """Pass 2: the pod's uses (ksim_topo_use rows) and topo flags."""
     uses: List[tuple] = []
     flags = 0
     # --- PodTopologySpread: filterTopologySpreadConstraints (hard, then soft) ---
     seen = {"DoNotSchedule": set(), "ScheduleAnyway": set()}
-    for c in pod.topology_spread:
+    cons, sysdef = pod_spread(spread, pod)
+    if sysdef and cons:
+        flags |= abi.POD_PTS_SYSTEM_DEFAULT
+    for c in cons:
         if c.when_unsatisfiable not in seen:
             raise TopologyError(f"whenUnsatisfiable {c.when_unsatisfiable} not supported")
         if c.topology_key in seen[c.when_unsatisfiable]:

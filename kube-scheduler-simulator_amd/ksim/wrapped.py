@@ -31,6 +31,7 @@ HAS_NORMALIZE = {"TaintToleration", "NodeAffinity", "PodTopologySpread", "InterP
 ERR_UNSCHEDULABLE = "node(s) were unschedulable"                        # nodeunschedulable
 ERR_NODE_NAME = "node(s) didn't match the requested node name"          # nodename
 ERR_NODE_AFFINITY = "node(s) didn't match Pod's node affinity/selector"  # nodeaffinity ErrReasonPod
+ERR_NODE_AFFINITY_ENFORCED = "node(s) didn't match scheduler-enforced node affinity"   # errReasonEnforced
 ERR_NODE_PORTS = "node(s) didn't have free ports for the requested pod ports"     # nodeports.ErrReason
 ERR_PTS = "node(s) didn't match pod topology spread constraints"        # podtopologyspread ErrReasonConstraintsNotMatch
 ERR_PTS_LABEL = ERR_PTS + " (missing required label)"                   # ErrReasonNodeLabelNotMatch
@@ -54,7 +55,7 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
         t = cluster.taint_vocab[detail]
         return f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
     if plugin == "NodeAffinity":
-        return ERR_NODE_AFFINITY
+        return ERR_NODE_AFFINITY_ENFORCED if detail == abi.NA_ENFORCED else ERR_NODE_AFFINITY
     if plugin == "NodePorts":
         return ERR_NODE_PORTS
     if plugin == "NodeResourcesFit":

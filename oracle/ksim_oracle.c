@@ -358,6 +358,24 @@ static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set
   return 1;
 }
 
+/* nodeaffinity.NodeAffinity.Filter (v1.26): the profile's addedAffinity
+ * (NodeAffinityArgs, addedNodeSelector.Match) first -> errReasonEnforced,
+ * then the pod's RequiredNodeAffinity -> ErrReasonPod.  Returns 1 on pass. */
+static int node_affinity_filter(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p, int32_t node,
+                                uint32_t* detail) {
+  *detail = 0;
+  if (p->flags & KSIM_POD_ADDED_AFFINITY) {
+    int any = 0;
+    for (int i = 0; i < p->added_term_count && !any; i++)
+      any = term_matches(o, ps, &ps->terms[p->added_term_first + i], node);
+    if (!any) {
+      *detail = KSIM_NA_ENFORCED;
+      return 0;
+    }
+  }
+  return required_node_affinity_match(o, ps, p, node);
+}
+
 /* PreferredSchedulingTerms.Score — [upstream] nodeaffinity.Score */
 static int64_t preferred_node_affinity_score(const ksim_oracle* o, const ksim_pod_set* ps,
                                              const ksim_pod* p, int32_t node) {
@@ -417,6 +435,8 @@ static uint32_t fits_request(const ksim_oracle* o, const ksim_pod* p, int32_t no
   for (int k = 0; k < o->n_scalar; k++) {
     int64_t q = p->scalar_req[k];
     if (q == 0) continue;
+    /* NodeResourcesFitArgs ignoredResources / ignoredResourceGroups (extended resources) */
+    if ((o->prof.fit_ignored_scalar >> k) & 1u) continue;
     size_t ix = (size_t)k * o->n + node;
     if (q > o->alloc_scalar[ix] - o->req_scalar[ix]) r |= (KSIM_FIT_SCALAR0 << k);
   }
@@ -467,17 +487,68 @@ int64_t ksim_oracle_least_requested_score(int64_t requested, int64_t capacity) {
   return prod / capacity;
 }
 
-/* leastResourceScorer over resourceAllocationScorer.score — a23 */
-static int64_t fit_least_allocated_score(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+/* mostRequestedScore — [upstream] noderesources/most_allocated.go */
+int64_t ksim_oracle_most_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;   /* pods with no requests get minimum values */
+  const int64_t prod = (int64_t)((uint64_t)requested * (uint64_t)MAX_NODE_SCORE);
+  return prod / capacity;
+}
+
+/* helper.BuildBrokenLinearFunction (scores already x MaxNodeScore / MaxCustomPriorityScore) */
+int64_t ksim_oracle_broken_linear(const ksim_profile* prof, int64_t p) {
+  for (int i = 0; i < prof->fit_n_shape; i++) {
+    if (p <= prof->fit_shape_util[i]) {
+      if (i == 0) return prof->fit_shape_score[0];
+      const int64_t s0 = prof->fit_shape_score[i - 1], s1 = prof->fit_shape_score[i];
+      const int64_t u0 = prof->fit_shape_util[i - 1], u1 = prof->fit_shape_util[i];
+      return s0 + (s1 - s0) * (p - u0) / (u1 - u0);
+    }
+  }
+  return prof->fit_shape_score[prof->fit_n_shape - 1];
+}
+
+/* requested_to_capacity_ratio.go buildRequestedToCapacityRatioScorerFunction's
+ * resourceScoringFunction (maxUtilization = 100) */
+static int64_t rtcr_resource_score(const ksim_profile* prof, int64_t requested, int64_t capacity) {
+  if (capacity == 0 || requested > capacity) return ksim_oracle_broken_linear(prof, 100);
+  const int64_t prod = (int64_t)((uint64_t)requested * 100u);
+  return ksim_oracle_broken_linear(prof, prod / capacity);
+}
+
+/* NodeResourcesFit.Score: resourceAllocationScorer.score with the profile's
+ * ScoringStrategy (leastResourceScorer / mostResourceScorer /
+ * requestedToCapacityRatioScorer) — a23 */
+static int64_t fit_score(const ksim_oracle* o, const ksim_pod* p, int32_t node) {
+  const ksim_profile* prof = &o->prof;
   int64_t node_score = 0, weight_sum = 0;
-  for (int i = 0; i < o->prof.fit_n_res; i++) {
+  for (int i = 0; i < prof->fit_n_res; i++) {
     int64_t a, r;
-    calc_alloc_req(o, p, node, o->prof.fit_res[i], 0, &a, &r);
-    if (a == 0) continue;
-    node_score += ksim_oracle_least_requested_score(r, a) * o->prof.fit_res_weight[i];
-    weight_sum += o->prof.fit_res_weight[i];
+    calc_alloc_req(o, p, node, prof->fit_res[i], 0, &a, &r);
+    if (a == 0) continue;                      /* only non-zero allocatable enters the map */
+    const int64_t w = prof->fit_res_weight[i];
+    switch (prof->fit_strategy) {
+      case KSIM_FIT_MOST_ALLOCATED:
+        node_score += ksim_oracle_most_requested_score(r, a) * w;
+        weight_sum += w;
+        break;
+      case KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO: {
+        const int64_t rs = rtcr_resource_score(prof, r, a);
+        if (rs > 0) {
+          node_score += rs * w;
+          weight_sum += w;
+        }
+        break;
+      }
+      default:
+        node_score += ksim_oracle_least_requested_score(r, a) * w;
+        weight_sum += w;
+        break;
+    }
   }
   if (weight_sum == 0) return 0;
+  if (prof->fit_strategy == KSIM_FIT_REQUESTED_TO_CAPACITY_RATIO)
+    return (int64_t)round((double)node_score / (double)weight_sum);   /* math.Round: half away from zero */
   return node_score / weight_sum;
 }
 
@@ -693,11 +764,13 @@ static void topo_prescore(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod
       memset(dom_of(o, i), 0, 8 * (size_t)o->vmax);
       memset(present_of(o, i), 0, (size_t)o->vmax);
     }
+  /* requireAllTopologies = len(pod constraints) > 0 || !systemDefaulted */
+  const int require_all = !(p->topo_flags & KSIM_POD_PTS_SYSTEM_DEFAULT);
   if (t->has_soft) {
     int32_t size[KSIM_MAX_USES] = {0};
     for (int32_t j = 0; j < nf; j++) {
       int32_t node = flist[j];
-      o->ignored[node] = !node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node);
+      o->ignored[node] = require_all && !node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node);
       if (o->ignored[node]) { n_ignored++; continue; }
       for (int i = 0; i < t->n; i++) {
         const ksim_topo_use* u = t->u[i];
@@ -713,7 +786,7 @@ static void topo_prescore(ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod
       t->weight[i] = o->topo_log[sz];                 /* topologyNormalizingWeight(sz) = log(sz + 2) */
     }
     for (int32_t node = 0; node < o->n; node++) {     /* processAllNode */
-      if (!node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node)) continue;
+      if (require_all && !node_has_all_keys(o, t, KSIM_USE_PTS_SOFT, node)) continue;
       for (int i = 0; i < t->n; i++) {
         const ksim_topo_use* u = t->u[i];
         if (u->kind != KSIM_USE_PTS_SOFT || (u->flags & KSIM_USEF_HOSTNAME)) continue;
@@ -833,9 +906,11 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
         if (tid) { *detail = tid; return (uint8_t)f; }
         break;
       }
-      case KSIM_PL_NODE_AFFINITY:
-        if (!required_node_affinity_match(o, ps, p, node)) return (uint8_t)f;
+      case KSIM_PL_NODE_AFFINITY: {
+        uint32_t why;
+        if (!node_affinity_filter(o, ps, p, node, &why)) { *detail = why; return (uint8_t)f; }
         break;
+      }
       case KSIM_PL_VOLUME_BINDING:       /* bound claims: PV node affinity */
         if (!volume_groups_match(o, ps, p->vb_first, p->vb_count, node)) return (uint8_t)f;
         break;
@@ -876,7 +951,7 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
 static int64_t score_plugin_raw(const ksim_oracle* o, const ksim_pod_set* ps, const ksim_pod* p,
                                 const topo_ctx* t, int plugin, int32_t node) {
   switch (plugin) {
-    case KSIM_PL_NODE_RESOURCES_FIT: return fit_least_allocated_score(o, p, node);
+    case KSIM_PL_NODE_RESOURCES_FIT: return fit_score(o, p, node);
     case KSIM_PL_BALANCED_ALLOCATION: return balanced_allocation_score(o, p, node);
     case KSIM_PL_TAINT_TOLERATION: return count_intolerable_prefer_no_schedule(o, p, node);
     case KSIM_PL_NODE_AFFINITY: return preferred_node_affinity_score(o, ps, p, node);
@@ -1430,8 +1505,8 @@ int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int3
     uint32_t det;
     if (fit >= 0 && run_filter_plugins(o, ps, p, &tc, node, &det) == (uint8_t)fit) potential[np++] = node;
   }
-  int32_t want = np * 10 / 100;                         /* GetOffsetAndNumCandidates */
-  if (want < 100) want = 100;
+  int32_t want = np * o->prof.preempt_min_pct / 100;    /* GetOffsetAndNumCandidates / calculateNumCandidates */
+  if (want < o->prof.preempt_min_abs) want = o->prof.preempt_min_abs;
   if (want > np) want = np;
   victim_rec* buf = (victim_rec*)malloc(sizeof(victim_rec) * (size_t)(b->n > 0 ? b->n : 1));
   int32_t* vic = (int32_t*)malloc(sizeof(int32_t) * (size_t)(b->n > 0 ? b->n : 1));

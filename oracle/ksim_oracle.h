@@ -70,6 +70,8 @@ void ksim_oracle_set_pod_seq(ksim_oracle* o, int64_t seq);
 int32_t ksim_oracle_num_feasible_nodes_to_find(int32_t percentage, int32_t num_all_nodes);
 int64_t ksim_oracle_least_requested_score(int64_t requested, int64_t capacity);
 int64_t ksim_oracle_balanced_score(int32_t n, const int64_t* requested, const int64_t* allocatable);
+int64_t ksim_oracle_most_requested_score(int64_t requested, int64_t capacity);
+int64_t ksim_oracle_broken_linear(const ksim_profile* prof, int64_t p);
 void    ksim_oracle_default_normalize(int64_t max_priority, int reverse, int32_t n, int64_t* scores);
 uint64_t ksim_oracle_tb_key(int64_t total, uint64_t seed, int64_t pod_seq, int32_t node);
 uint64_t ksim_oracle_tb_lo(uint64_t seed, int64_t pod_seq, int32_t node);

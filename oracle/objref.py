@@ -135,7 +135,12 @@ class ObjScheduler:
     def __init__(self, nodes: List[Node], bound: List[Pod] = (), namespaces: Optional[Dict[str, Dict]] = None,
                  pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
                  hard_pod_affinity_weight: int = 1, network_bandwidth=None, nb_filter: bool = True,
-                 nb_score: bool = True, pvs=(), pvcs=(), storage_classes=()):
+                 nb_score: bool = True, pvs=(), pvcs=(), storage_classes=(), fit=None, node_affinity=None,
+                 preemption=None, spread=None, services=(), controllers=()):
+        """fit / node_affinity / preemption / spread: ksim.profile FitArgs,
+        NodeAffinityArgs, PreemptionArgs, PodTopologySpreadArgs (the plugin args of
+        the profile; None = the defaults).  services / controllers: the
+        ksim.model Service / Controller objects helper.DefaultSelector reads."""
         order = node_tree_order([zone_key(n.labels) for n in nodes])
         self.nodes = [NodeInfo(nodes[i]) for i in order]
         # cache.addNodeImageStates, nodes in the order they were added: name -> [size, {node names}]
@@ -169,6 +174,20 @@ class ObjScheduler:
                 self.score_order.append("NetworkBandwidth")
         self.seed = seed
         self.hard_w = hard_pod_affinity_weight
+        from ksim.profile import FitArgs, NodeAffinityArgs, PreemptionArgs, is_extended_resource_name
+        self.fit = fit or FitArgs()
+        rw: Dict[str, int] = {}
+        for r, w in self.fit.resources:            # resourcesToWeightMap
+            rw.pop(r, None)
+            rw[r] = w
+        self.fit_weights = rw
+        self.is_extended = is_extended_resource_name
+        self.added = node_affinity or NodeAffinityArgs()
+        self.preemption = preemption or PreemptionArgs()
+        from ksim.profile import PodTopologySpreadArgs
+        self.spread = spread or PodTopologySpreadArgs()
+        self.services = list(services)
+        self.controllers = list(controllers)
         # the snapshot's PersistentVolumes, PersistentVolumeClaims and StorageClasses
         # (VolumeBinding / VolumeZone / VolumeRestrictions); copies, bound as the run goes
         import copy
@@ -218,6 +237,14 @@ class ObjScheduler:
             if (node.name in r.values) != (r.operator == "In"):
                 return False
         return True
+
+    def node_affinity_filter(self, pod: Pod, node: Node) -> Optional[str]:
+        """nodeaffinity.Filter: addedNodeSelector first (errReasonEnforced), then the pod's."""
+        if self.added.required is not None and not any(self._term_match(t, node) for t in self.added.required):
+            return "node(s) didn't match scheduler-enforced node affinity"
+        if not self.required_node_affinity(pod, node):
+            return "node(s) didn't match Pod's node affinity/selector"
+        return None
 
     def required_node_affinity(self, pod: Pod, node: Node) -> bool:
         for k, v in pod.node_selector.items():
@@ -384,12 +411,47 @@ class ObjScheduler:
         return None
 
     # ---- PodTopologySpread (filtering.go / scoring.go) ---------------------------
+    def _default_selector(self, pod: Pod) -> Optional[LabelSelector]:
+        """helper.DefaultSelector: the Services selecting the pod (merged label
+        maps), then its controller's selector (an RC's map merged in, a
+        ReplicaSet's / StatefulSet's requirements added); None when Empty()."""
+        merged: Dict[str, str] = {}
+        for svc in self.services:
+            if svc.namespace != pod.namespace or svc.selector is None:
+                continue
+            if LabelSelector(dict(svc.selector)).matches(pod.labels):
+                merged.update(svc.selector)
+        reqs = []
+        if pod.owner is not None:
+            api, kind, name = pod.owner
+            gvk = {("v1", "ReplicationController"), ("apps/v1", "ReplicaSet"), ("apps/v1", "StatefulSet")}
+            if (api, kind) in gvk:
+                for ctl in self.controllers:
+                    if ctl.kind == kind and ctl.namespace == pod.namespace and ctl.name == name:
+                        if kind == "ReplicationController":
+                            merged.update(ctl.selector or {})
+                        elif ctl.selector is not None:
+                            from ksim.model import Requirement
+                            reqs += [Requirement(k, "In", [v]) for k, v in ctl.selector.match_labels.items()]
+                            reqs += list(ctl.selector.match_expressions)
+                        break
+        if not merged and not reqs:
+            return None
+        return LabelSelector(merged, reqs)
+
+    def _pod_constraints(self, pod: Pod):
+        """(constraints, system-defaulted): the pod's own, else buildDefaultConstraints."""
+        if pod.topology_spread:
+            return list(pod.topology_spread), False
+        import dataclasses
+        sel = self._default_selector(pod)
+        cons = self.spread.constraints()
+        if sel is None or not cons:
+            return [], False
+        return [dataclasses.replace(c, label_selector=sel) for c in cons], self.spread.defaulting_type == "System"
+
     def _constraints(self, pod: Pod, when: str):
-        out = []
-        for c in pod.topology_spread:
-            if c.when_unsatisfiable == when:
-                out.append(c)
-        return out
+        return [c for c in self._pod_constraints(pod)[0] if c.when_unsatisfiable == when]
 
     @staticmethod
     def _count_match(ni: NodeInfo, sel: Optional[LabelSelector], ns: str) -> int:
@@ -437,6 +499,8 @@ class ObjScheduler:
 
     def pts_prescore(self, pod: Pod, filtered: List[NodeInfo]):
         cons = self._constraints(pod, "ScheduleAnyway")
+        # requireAllTopologies = len(pod.Spec.TopologySpreadConstraints) > 0 || !systemDefaulted
+        require_all = bool(pod.topology_spread) or self.spread.defaulting_type != "System"
         ignored = set()
         pair_counts: Dict[Tuple[str, str], int] = {}
         weights = []
@@ -445,13 +509,13 @@ class ObjScheduler:
         topo_size = [0] * len(cons)
         for ni in filtered:
             node = ni.node
-            if not all(c.topology_key in node.labels for c in cons):
+            if require_all and not all(c.topology_key in node.labels for c in cons):
                 ignored.add(node.name)
                 continue
             for i, c in enumerate(cons):
                 if c.topology_key == LABEL_HOSTNAME:
                     continue
-                pair = (c.topology_key, node.labels[c.topology_key])
+                pair = (c.topology_key, node.labels.get(c.topology_key, ""))
                 if pair not in pair_counts:
                     pair_counts[pair] = 0
                     topo_size[i] += 1
@@ -462,12 +526,12 @@ class ObjScheduler:
             weights.append(math.log(float(sz + 2)))
         for ni in self.nodes:
             node = ni.node
-            if not all(c.topology_key in node.labels for c in cons):
+            if require_all and not all(c.topology_key in node.labels for c in cons):
                 continue
             for c in cons:
                 if not self._inclusion(c, pod, node):
                     continue
-                pair = (c.topology_key, node.labels[c.topology_key])
+                pair = (c.topology_key, node.labels.get(c.topology_key, ""))
                 if pair not in pair_counts:
                     continue
                 pair_counts[pair] += self._count_match(ni, c.label_selector, pod.namespace)
@@ -682,29 +746,84 @@ class ObjScheduler:
         return [int(float(MAX_NODE_SCORE) * (float(s - mn) / float(d))) if d > 0 else 0 for s in scores]
 
     # ---- resources -------------------------------------------------------------------
-    @staticmethod
-    def fit_filter(pod: Pod, ni: NodeInfo) -> Optional[str]:
+    def fit_filter(self, pod: Pod, ni: NodeInfo, scalar_order=None) -> Optional[str]:
+        """fitsRequest; scalar reasons follow ``scalar_order`` (Go appends them in
+        map order; the C restatement in column order)."""
         req = pod_requests(pod)
         reasons = []
         if len(ni.pods) + 1 > ni.alloc.get("pods", 0):
             reasons.append("Too many pods")
-        if any(v for v in req.values()) or any(k not in ("cpu", "memory", "ephemeral-storage") for k in req):
-            for r in ("cpu", "memory", "ephemeral-storage"):
+        native = ("cpu", "memory", "ephemeral-storage")
+        if any(v for v in req.values()) or any(k not in native for k in req):
+            for r in native:
                 if req.get(r, 0) > ni.alloc.get(r, 0) - ni.requested.get(r, 0):
+                    reasons.append(f"Insufficient {r}")
+            scal = [k for k in req if k not in native]
+            if scalar_order is not None:
+                scal.sort(key=lambda k: scalar_order.index(k) if k in scalar_order else len(scalar_order))
+            for r in scal:
+                q = req[r]
+                if q == 0:
+                    continue
+                if self.is_extended(r) and (r in self.fit.ignored_resources or
+                                            r.split("/")[0] in self.fit.ignored_resource_groups):
+                    continue                       # ignoredResources / ignoredResourceGroups
+                if q > ni.alloc.get(r, 0) - ni.requested.get(r, 0):
                     reasons.append(f"Insufficient {r}")
         return ", ".join(reasons) if reasons else None
 
-    @staticmethod
-    def least_allocated(pod: Pod, ni: NodeInfo) -> int:
-        ncpu, nmem = pod_nonzero_requests(pod)
+    def _alloc_req(self, pod: Pod, ni: NodeInfo, r: str, use_requested: bool):
+        """calculateResourceAllocatableRequest (+ calculatePodResourceRequest)."""
+        req = pod_requests(pod)
+        if r in ("cpu", "memory") and not use_requested:
+            ncpu, nmem = pod_nonzero_requests(pod)
+            pr = ncpu if r == "cpu" else nmem
+            have = ni.nz_cpu if r == "cpu" else ni.nz_mem
+            return ni.alloc.get(r, 0), have + pr
+        pr = req.get(r, 0)
+        if r in ("cpu", "memory", "ephemeral-storage"):
+            return ni.alloc.get(r, 0), ni.requested.get(r, 0) + pr
+        if pr == 0:                                # an extended resource the pod does not request
+            return 0, 0
+        if r in ni.alloc:
+            return ni.alloc[r], ni.requested.get(r, 0) + pr
+        return 0, 0
+
+    def _broken_linear(self, p: int) -> int:
+        shape = [(u, sc * 10) for u, sc in self.fit.shape]
+        for i, (u, sc) in enumerate(shape):
+            if p <= u:
+                if i == 0:
+                    return sc
+                pu, ps = shape[i - 1]
+                return ps + go_div((sc - ps) * (p - pu), u - pu)
+        return shape[-1][1]
+
+    def least_allocated(self, pod: Pod, ni: NodeInfo) -> int:
+        """NodeResourcesFit.Score under the profile's scoring strategy (the name
+        keeps the default's)."""
         score = wsum = 0
-        for alloc, req in ((ni.alloc["cpu"], ni.nz_cpu + ncpu), (ni.alloc["memory"], ni.nz_mem + nmem)):
+        strat = self.fit.strategy
+        for r, w in self.fit_weights.items():
+            alloc, req = self._alloc_req(pod, ni, r, False)
             if alloc == 0:
                 continue
-            s = 0 if req > alloc else go_div(go_i64((alloc - req) * MAX_NODE_SCORE), alloc)
-            score += s
-            wsum += 1
-        return go_div(score, wsum) if wsum else 0
+            if strat == "MostAllocated":
+                s = go_div(go_i64(min(req, alloc) * MAX_NODE_SCORE), alloc)
+            elif strat == "RequestedToCapacityRatio":
+                s = self._broken_linear(100 if req > alloc else go_div(go_i64(req * 100), alloc))
+                if s <= 0:
+                    continue
+            else:
+                s = 0 if req > alloc else go_div(go_i64((alloc - req) * MAX_NODE_SCORE), alloc)
+            score += s * w
+            wsum += w
+        if not wsum:
+            return 0
+        if strat == "RequestedToCapacityRatio":
+            x = float(score) / float(wsum)
+            return int(math.floor(x + 0.5)) if x >= 0 else -int(math.floor(-x + 0.5))   # math.Round
+        return go_div(score, wsum)
 
     @staticmethod
     def balanced(pod: Pod, ni: NodeInfo) -> int:
@@ -734,7 +853,9 @@ class ObjScheduler:
         MoreImportantPod ties).  Returns (nominated node name or None, victim names)."""
         pts, ipa = self.pts_prefilter(pod), self.ipa_prefilter(pod)
         potential = [ni for ni in self.nodes if self.filter_node(pod, ni, pts, ipa)[0] == "NodeResourcesFit"]
-        want = min(max(len(potential) * 10 // 100, 100), len(potential))
+        pa = self.preemption
+        want = min(max(len(potential) * pa.min_candidate_nodes_percentage // 100, pa.min_candidate_nodes_absolute),
+                   len(potential))
         want_req = pod_requests(pod)
         nothing = not any(want_req.values())
 
@@ -851,13 +972,12 @@ class ObjScheduler:
                 if t is not None:
                     msg = f"node(s) had untolerated taint {{{t.key}: {t.value}}}"
             elif pl == "NodeAffinity":
-                if not self.required_node_affinity(pod, node):
-                    msg = "node(s) didn't match Pod's node affinity/selector"
+                msg = self.node_affinity_filter(pod, node)
             elif pl == "NodePorts":
                 if not self.fits_ports(pod, ni):
                     msg = "node(s) didn't have free ports for the requested pod ports"
             elif pl == "NodeResourcesFit":
-                msg = self.fit_filter(pod, ni)
+                msg = self.fit_filter(pod, ni, getattr(self, "scalar_order", None))
             elif pl == "PodTopologySpread":
                 msg = self.pts_filter(pod, pts, node)
             elif pl == "InterPodAffinity":
@@ -970,7 +1090,8 @@ class ObjScheduler:
                     raw = [self.least_allocated(pod, ni) for ni in feasible]
                     norm = raw
                 elif pl == "NodeAffinity":
-                    raw = [sum(t.weight for t in pod.preferred_terms if t.weight and self._term_match(t.term, ni.node))
+                    raw = [sum(t.weight for t in list(pod.preferred_terms) + list(self.added.preferred)
+                               if t.weight and self._term_match(t.term, ni.node))
                            for ni in feasible]
                     norm = self.default_normalize(raw, False)
                 elif pl == "PodTopologySpread":

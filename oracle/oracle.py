@@ -47,6 +47,10 @@ def lib():
         L.ksim_oracle_least_requested_score.restype = i64
         L.ksim_oracle_balanced_score.argtypes = [i32, vp, vp]
         L.ksim_oracle_balanced_score.restype = i64
+        L.ksim_oracle_most_requested_score.argtypes = [i64, i64]
+        L.ksim_oracle_most_requested_score.restype = i64
+        L.ksim_oracle_broken_linear.argtypes = [vp, i64]
+        L.ksim_oracle_broken_linear.restype = i64
         L.ksim_oracle_default_normalize.argtypes = [i64, ctypes.c_int, i32, vp]
         L.ksim_oracle_tb_key.argtypes = [i64, ctypes.c_uint64, i64, i32]
         L.ksim_oracle_tb_key.restype = ctypes.c_uint64

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 8
+#define KSIM_ABI_VERSION 9
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -174,6 +174,9 @@ enum ksim_plugin {
 /* NodeAffinity failure detail: 0 = the pod's selector / required terms
  * (ErrReasonPod), KSIM_NA_ENFORCED = the profile's addedAffinity (errReasonEnforced) */
 #define KSIM_NA_ENFORCED         1u
+/* VolumeBinding failure detail: the reasons FindPodVolumes gives the node */
+#define KSIM_VB_NODE_CONFLICT    1u   /* a bound PV's node affinity (ErrReasonNodeConflict) */
+#define KSIM_VB_BIND_CONFLICT    2u   /* an unbound claim: no PV, no provisioning (ErrReasonBindConflict) */
 
 /* per-pod cycle status */
 #define KSIM_STATUS_SCHEDULED      0
@@ -298,10 +301,20 @@ typedef struct ksim_pod {
  *                  failure-domain keys): the terms {key In LabelZonesToSet(v)}
  *                  and {every topology key DoesNotExist} (a node without any
  *                  topology label passes).
+ *   VolumeBinding, unbound WaitForFirstConsumer claims (binder.go
+ *                  FindPodVolumes): groups of node-name / label terms the host
+ *                  derives from the matching PVs and the class's provisioning,
+ *                  their group index or-ed with KSIM_VB_UNBOUND_GROUP, after
+ *                  the bound-PV groups.
  * Terms of a list are consecutive ksim_term entries of the pod set; a term's
  * `weight` is its group index (0, 0, 1, 2, 2, ... non-decreasing).  The filter
- * passes iff every group has a matching term.  Failure reasons: "node(s) had
- * volume node affinity conflict" / "node(s) had no available volume zone". */
+ * passes iff every group has a matching term.  VolumeBinding's failure detail
+ * is KSIM_VB_NODE_CONFLICT if a bound-PV group failed, | KSIM_VB_BIND_CONFLICT
+ * if an unbound-claim group failed ("node(s) had volume node affinity
+ * conflict", "node(s) didn't find available persistent volumes to bind",
+ * joined in that order); VolumeZone's is 0 ("node(s) had no available volume
+ * zone"). */
+#define KSIM_VB_UNBOUND_GROUP    (1 << 30)
 
 /* Count classes.  The host evaluates every label selector / affinity term
  * against pod namespaces and labels once (that string work does not depend
@@ -578,6 +591,29 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_inde
 int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out* out);
 int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, const int64_t* scores, int32_t n,
                       int64_t* out);
+/* Nominated pods (ABI 8).  After a preemption the framework keeps the
+ * preemptor nominated to a node (PostFilter's result, handleSchedulingFailure
+ * -> SchedulingQueue.AddNominatedPod) and later cycles run
+ * RunFilterPluginsWithNominatedPods (framework/runtime/framework.go): on a node
+ * with nominated pods of equal or higher priority, Filter first runs on a
+ * clone of the NodeInfo with those pods added and a clone of the cycle state
+ * after the PreFilterExtensions' AddPod (addNominatedPods), then -- if that
+ * passed -- on the plain NodeInfo; the wrapper records both passes.
+ *   ksim_fw_filter_nominated  the first pass, for the cycle in flight
+ *                             (ksim_fw_prefilter): group k is node nodes[k]
+ *                             with pods [first[k], first[k] + count[k]) of
+ *                             `nominated` added.  fail_plugin[k] /
+ *                             fail_detail[k] are the filter outcome there
+ *                             (KSIM_PASSED or the failing plugin's filter
+ *                             index).  The second pass is ksim_fw_prefilter's
+ *                             answer for the node; the framework (the host)
+ *                             combines them.  The cycle's own PreFilter state
+ *                             is unchanged afterwards.  Replaces the
+ *                             original plugins' AddPod (PreFilterExtensions)
+ *                             and Filter behind wrappedplugin.go:491-516. */
+int ksim_fw_filter_nominated(ksim_handle* h, const ksim_pod_set* nominated, int32_t n_nodes, const int32_t* nodes,
+                             const int32_t* first, const int32_t* count, uint8_t* fail_plugin,
+                             uint32_t* fail_detail);
 
 /* Batch mode: upload a pod set once (device-resident), then schedule a range
  * of it in queue order; chosen[i] = node position or -1.  The whole-cycle
@@ -693,7 +729,9 @@ int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b);
  *                    return UnschedulableAndUnresolvable);
  *   dry run          SelectVictimsOnNode on each, in nodeTree order from
  *                    offset 0 (upstream draws a random offset), keeping the
- *                    first numCandidates = max(10 % of them, 100) candidates;
+ *                    first numCandidates = max(minCandidateNodesPercentage %
+ *                    of them, minCandidateNodesAbsolute) candidates (the
+ *                    profile's DefaultPreemptionArgs; 10 % and 100 default);
  *   selection        pickOneNodeForPreemption: lowest highest-victim
  *                    priority, lowest sum of (priority + 2^31), fewest
  *                    victims, latest earliest start among the highest-
@@ -701,6 +739,18 @@ int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b);
  * The pod must carry no topology / port / image uses (KSIM_E_UNSUPPORTED). */
 int ksim_preempt(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
                  ksim_preempt_out* out);
+/* ksim_preempt with the PodNominator's pods (replaces the same PostFilter;
+ * upstream SelectVictimsOnNode filters through RunFilterPluginsWithNominatedPods,
+ * framework.go:764-800 v1.26).  Group k = the pods [first[k], first[k] +
+ * count[k]) of `nominated`, nominated on node nodes[k] with priority >=
+ * `priority`, the preemptor excluded (the caller selects them, as for
+ * ksim_fw_filter_nominated; nodes distinct).  A grouped node's status is the
+ * two-pass one (pass 1 with the group's pods added; pass 2 as is only if pass
+ * 1 passed) and its dry run keeps the group's requests and pod count on the
+ * node.  n_groups = 0 is ksim_preempt. */
+int ksim_preempt_nominated(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
+                           const ksim_pod_set* nominated, int32_t n_groups, const int32_t* nodes,
+                           const int32_t* first, const int32_t* count, ksim_preempt_out* out);
 
 /* ---- selector / affinity-term matching -------------------- */
 /* The pod-matching half of PodTopologySpread's and InterPodAffinity's

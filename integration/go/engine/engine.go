@@ -23,14 +23,30 @@ import "C"
 
 import (
 	"fmt"
+	"sync"
 	"unsafe"
 )
 
 // ABIVersion is the header version this binding was written against.
-const ABIVersion = 8
+const ABIVersion = 9
 
 // Engine owns one device handle (one GPU, or one node shard of a cluster).
-type Engine struct{ h *C.ksim_handle }
+// A handle is not reentrant: the framework's 16 Filter goroutines (nominated
+// first passes), the binding goroutine (Unreserve) and the next scheduling
+// cycle reach it concurrently, so every call holds mu.
+type Engine struct {
+	h  *C.ksim_handle
+	mu sync.Mutex
+}
+
+// locked runs one C call under the handle's mutex.
+func (e *Engine) locked(f func() C.int) error {
+	e.mu.Lock()
+	rc := f()
+	err := e.err(rc)
+	e.mu.Unlock()
+	return err
+}
 
 // New opens the engine on a HIP device; it fails when no GPU is present (the
 // engine has no CPU fallback).
@@ -57,13 +73,15 @@ func (e *Engine) err(rc C.int) error {
 
 // SetProfile installs the converted KubeSchedulerProfile
 // (convertConfigurationForSimulator, simulator/scheduler/scheduler.go:199-249).
-func (e *Engine) SetProfile(p *C.ksim_profile) error { return e.err(C.ksim_set_profile(e.h, p)) }
+func (e *Engine) SetProfile(p *C.ksim_profile) error {
+	return e.locked(func() C.int { return C.ksim_set_profile(e.h, p) })
+}
 
 // SetCluster uploads the whole snapshot in nodeTree order (resets
 // nextStartNodeIndex).  t's column pointers point into Go memory pinned for
 // the call only.
 func (e *Engine) SetCluster(t *C.ksim_node_table, v *C.ksim_vocab) error {
-	return e.err(C.ksim_set_cluster(e.h, t, v))
+	return e.locked(func() C.int { return C.ksim_set_cluster(e.h, t, v) })
 }
 
 // UpsertNodes applies node informer events (AddNode / UpdateNode / RemoveNode)
@@ -74,16 +92,18 @@ func (e *Engine) UpsertNodes(t *C.ksim_node_table, v *C.ksim_vocab, oldPos []int
 	if len(oldPos) > 0 {
 		p = (*C.int32_t)(unsafe.Pointer(&oldPos[0]))
 	}
-	return e.err(C.ksim_upsert_nodes(e.h, t, v, p))
+	return e.locked(func() C.int { return C.ksim_upsert_nodes(e.h, t, v, p) })
 }
 
 // RemoveNode removes the node at position pos (later nodes move down by one).
-func (e *Engine) RemoveNode(pos int) error { return e.err(C.ksim_remove_node(e.h, C.int32_t(pos))) }
+func (e *Engine) RemoveNode(pos int) error {
+	return e.locked(func() C.int { return C.ksim_remove_node(e.h, C.int32_t(pos)) })
+}
 
 // SetEvalRange makes this handle a replica (whole snapshot) that evaluates
 // nodes [lo, hi) in the batch top-T; the ranks' ranges tile the cluster.
 func (e *Engine) SetEvalRange(lo, hi int) error {
-	return e.err(C.ksim_set_eval_range(e.h, C.int32_t(lo), C.int32_t(hi)))
+	return e.locked(func() C.int { return C.ksim_set_eval_range(e.h, C.int32_t(lo), C.int32_t(hi)) })
 }
 
 // MatchTerms answers every (signature, matcher) pair of the count classes'
@@ -97,20 +117,20 @@ func (e *Engine) MatchTerms(mp *C.ksim_match_problem, bits []uint32, counts []in
 	if len(counts) > 0 {
 		cp = (*C.int32_t)(unsafe.Pointer(&counts[0]))
 	}
-	return e.err(C.ksim_match_terms(e.h, mp, (*C.uint32_t)(unsafe.Pointer(&bits[0])), cp))
+	return e.locked(func() C.int { return C.ksim_match_terms(e.h, mp, (*C.uint32_t)(unsafe.Pointer(&bits[0])), cp) })
 }
 
 // EvalPod runs one full cycle for pod idx of ps (PreFilter .. bind) and fills
 // the per-node outputs the wrapped plugins record (out's slices are Go-owned:
 // n_nodes entries, n_score x n_nodes for the score matrices).
 func (e *Engine) EvalPod(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
-	return e.err(C.ksim_eval_pod(e.h, ps, C.int32_t(idx), out))
+	return e.locked(func() C.int { return C.ksim_eval_pod(e.h, ps, C.int32_t(idx), out) })
 }
 
 // EvalPodFilter / EvalPodFinish split a cycle around the host's extender
 // round trip (findNodesThatPassExtenders, the extender part of prioritizeNodes).
 func (e *Engine) EvalPodFilter(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
-	return e.err(C.ksim_eval_pod_filter(e.h, ps, C.int32_t(idx), out))
+	return e.locked(func() C.int { return C.ksim_eval_pod_filter(e.h, ps, C.int32_t(idx), out) })
 }
 
 func (e *Engine) EvalPodFinish(extFail []uint8, extScore []int64, out *C.ksim_eval_out) error {
@@ -122,7 +142,7 @@ func (e *Engine) EvalPodFinish(extFail []uint8, extScore []int64, out *C.ksim_ev
 	if len(extScore) > 0 {
 		s = (*C.int64_t)(unsafe.Pointer(&extScore[0]))
 	}
-	return e.err(C.ksim_eval_pod_finish(e.h, f, s, out))
+	return e.locked(func() C.int { return C.ksim_eval_pod_finish(e.h, f, s, out) })
 }
 
 // Framework-driven compat mode (plugins.go uses these through cgo directly):
@@ -130,7 +150,7 @@ func (e *Engine) EvalPodFinish(extFail []uint8, extScore []int64, out *C.ksim_ev
 // runs PreScore / Score / NormalizeScore over the framework's list,
 // FwNormalize normalizes one score slot over an explicit list.
 func (e *Engine) FwPreFilter(ps *C.ksim_pod_set, idx int, out *C.ksim_eval_out) error {
-	return e.err(C.ksim_fw_prefilter(e.h, ps, C.int32_t(idx), out))
+	return e.locked(func() C.int { return C.ksim_fw_prefilter(e.h, ps, C.int32_t(idx), out) })
 }
 
 func (e *Engine) FwScore(nodes []int32, out *C.ksim_eval_out) error {
@@ -138,36 +158,72 @@ func (e *Engine) FwScore(nodes []int32, out *C.ksim_eval_out) error {
 	if len(nodes) > 0 {
 		p = (*C.int32_t)(unsafe.Pointer(&nodes[0]))
 	}
-	return e.err(C.ksim_fw_score(e.h, p, C.int32_t(len(nodes)), out))
+	return e.locked(func() C.int { return C.ksim_fw_score(e.h, p, C.int32_t(len(nodes)), out) })
 }
 
 func (e *Engine) FwNormalize(slot int, nodes []int32, scores, out []int64) error {
 	if len(nodes) == 0 {
 		return nil
 	}
-	return e.err(C.ksim_fw_normalize(e.h, C.int32_t(slot), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
-		(*C.int64_t)(unsafe.Pointer(&scores[0])), C.int32_t(len(nodes)), (*C.int64_t)(unsafe.Pointer(&out[0]))))
+	return e.locked(func() C.int {
+		return C.ksim_fw_normalize(e.h, C.int32_t(slot), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
+			(*C.int64_t)(unsafe.Pointer(&scores[0])), C.int32_t(len(nodes)), (*C.int64_t)(unsafe.Pointer(&out[0])))
+	})
 }
 
 // SetBoundPods / Preempt: DefaultPreemption's dry run over the bound pods.
-func (e *Engine) SetBoundPods(b *C.ksim_bound_pods) error { return e.err(C.ksim_set_bound_pods(e.h, b)) }
+func (e *Engine) SetBoundPods(b *C.ksim_bound_pods) error {
+	return e.locked(func() C.int { return C.ksim_set_bound_pods(e.h, b) })
+}
 
 func (e *Engine) Preempt(ps *C.ksim_pod_set, idx int, priority int32, out *C.ksim_preempt_out) error {
-	return e.err(C.ksim_preempt(e.h, ps, C.int32_t(idx), C.int32_t(priority), out))
+	return e.locked(func() C.int { return C.ksim_preempt(e.h, ps, C.int32_t(idx), C.int32_t(priority), out) })
+}
+
+// PreemptNominated: the dry run with the PodNominator's pods; group k is
+// nominated[first[k] : first[k]+count[k]] on node position nodes[k].
+func (e *Engine) PreemptNominated(ps *C.ksim_pod_set, idx int, priority int32, nominated *C.ksim_pod_set,
+	nodes, first, count []int32, out *C.ksim_preempt_out) error {
+	var n, f, c *C.int32_t
+	if len(nodes) > 0 {
+		n = (*C.int32_t)(unsafe.Pointer(&nodes[0]))
+		f = (*C.int32_t)(unsafe.Pointer(&first[0]))
+		c = (*C.int32_t)(unsafe.Pointer(&count[0]))
+	}
+	return e.locked(func() C.int {
+		return C.ksim_preempt_nominated(e.h, ps, C.int32_t(idx), C.int32_t(priority), nominated,
+			C.int32_t(len(nodes)), n, f, c, out)
+	})
+}
+
+// FwFilterNominated: RunFilterPluginsWithNominatedPods' first pass of the
+// cycle in flight on the grouped nodes (plugins.go calls it per node).
+func (e *Engine) FwFilterNominated(nominated *C.ksim_pod_set, nodes, first, count []int32, fail []uint8,
+	detail []uint32) error {
+	if len(nodes) == 0 {
+		return nil
+	}
+	return e.locked(func() C.int {
+		return C.ksim_fw_filter_nominated(e.h, nominated, C.int32_t(len(nodes)), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
+			(*C.int32_t)(unsafe.Pointer(&first[0])), (*C.int32_t)(unsafe.Pointer(&count[0])),
+			(*C.uint8_t)(unsafe.Pointer(&fail[0])), (*C.uint32_t)(unsafe.Pointer(&detail[0])))
+	})
 }
 
 // Assume / Forget: NodeInfo.AddPod / RemovePod of a bound pod (informer pod
 // events, Unreserve), count classes included.
 func (e *Engine) Assume(ps *C.ksim_pod_set, idx, node int) error {
-	return e.err(C.ksim_assume(e.h, ps, C.int32_t(idx), C.int32_t(node)))
+	return e.locked(func() C.int { return C.ksim_assume(e.h, ps, C.int32_t(idx), C.int32_t(node)) })
 }
 
 func (e *Engine) Forget(ps *C.ksim_pod_set, idx, node int) error {
-	return e.err(C.ksim_forget(e.h, ps, C.int32_t(idx), C.int32_t(node)))
+	return e.locked(func() C.int { return C.ksim_forget(e.h, ps, C.int32_t(idx), C.int32_t(node)) })
 }
 
 // LoadPods uploads a pending queue in PrioritySort order for ScheduleLoaded.
-func (e *Engine) LoadPods(ps *C.ksim_pod_set) error { return e.err(C.ksim_load_pods(e.h, ps)) }
+func (e *Engine) LoadPods(ps *C.ksim_pod_set) error {
+	return e.locked(func() C.int { return C.ksim_load_pods(e.h, ps) })
+}
 
 // ScheduleLoaded schedules loaded pods [first, first+count) on the device
 // (batch, ADAPT batch or per-pod cycles; placements identical to cycle by
@@ -178,18 +234,20 @@ func (e *Engine) ScheduleLoaded(first, count int, chosen []int32) (C.ksim_batch_
 	if len(chosen) > 0 {
 		p = (*C.int32_t)(unsafe.Pointer(&chosen[0]))
 	}
-	rc := C.ksim_schedule_loaded(e.h, C.int32_t(first), C.int32_t(count), p, &st)
-	return st, e.err(rc)
+	err := e.locked(func() C.int { return C.ksim_schedule_loaded(e.h, C.int32_t(first), C.int32_t(count), p, &st) })
+	return st, err
 }
 
 // ResetCluster restores the snapshot of the last SetCluster / UpsertNodes.
-func (e *Engine) ResetCluster() error { return e.err(C.ksim_reset_cluster(e.h)) }
+func (e *Engine) ResetCluster() error {
+	return e.locked(func() C.int { return C.ksim_reset_cluster(e.h) })
+}
 
 // NextStart is the scheduler's nextStartNodeIndex.
 func (e *Engine) NextStart() (int, error) {
 	var v C.int32_t
-	rc := C.ksim_get_next_start(e.h, &v)
-	return int(v), e.err(rc)
+	err := e.locked(func() C.int { return C.ksim_get_next_start(e.h, &v) })
+	return int(v), err
 }
 
 // Multi-GPU: one process per GPU.  SetShard (before SetCluster) gives this
@@ -197,7 +255,7 @@ func (e *Engine) NextStart() (int, error) {
 // the communicator id with CommUniqueID, the ranks share it over any side
 // channel, and each calls CommInit.
 func (e *Engine) SetShard(base, nTotal int) error {
-	return e.err(C.ksim_set_shard(e.h, C.int32_t(base), C.int32_t(nTotal)))
+	return e.locked(func() C.int { return C.ksim_set_shard(e.h, C.int32_t(base), C.int32_t(nTotal)) })
 }
 
 func CommUniqueID() ([C.KSIM_COMM_ID_BYTES]byte, error) {
@@ -209,5 +267,5 @@ func CommUniqueID() ([C.KSIM_COMM_ID_BYTES]byte, error) {
 }
 
 func (e *Engine) CommInit(rank, world int, id [C.KSIM_COMM_ID_BYTES]byte) error {
-	return e.err(C.ksim_comm_init(e.h, C.int32_t(rank), C.int32_t(world), (*C.uint8_t)(unsafe.Pointer(&id[0]))))
+	return e.locked(func() C.int { return C.ksim_comm_init(e.h, C.int32_t(rank), C.int32_t(world), (*C.uint8_t)(unsafe.Pointer(&id[0]))) })
 }

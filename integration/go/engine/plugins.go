@@ -35,8 +35,21 @@
 //	                ksim_assume on the framework's node; Unreserve ksim_forget.
 //	                This is the scheduler cache's AssumePod for the engine's
 //	                device-resident snapshot.
-//	PostFilter      DefaultPreemption: ksim_preempt's dry run picks the node
-//	                and victims; victims are deleted as prepareCandidate does.
+//	PostFilter      DefaultPreemption: PodEligibleToPreemptOthers on the host,
+//	                then ksim_preempt_nominated's dry run (the PodNominator's
+//	                pods of priority >= the preemptor stay on each candidate)
+//	                picks the node and victims; prepareCandidate's side effects
+//	                (DisruptionTarget condition, delete, lower-priority
+//	                nominations cleared) on the host.
+//	AddPod          PreFilterExtensions on the CycleState clone that
+//	                RunFilterPluginsWithNominatedPods builds: the clone carries
+//	                the nominated pods, and Filter on it answers from
+//	                ksim_fw_filter_nominated (pass 1), once per node and cycle.
+//
+// Concurrency: the framework's 16 Filter goroutines, the binding goroutine
+// (Unreserve) and the next scheduling cycle reach the handle concurrently;
+// every engine call holds Engine.mu, and a cycle's first engine pass is made
+// once under Profile.mu.
 //
 // A pod the engine refuses (KSIM_E_UNSUPPORTED: e.g. unbound PVCs) is answered
 // by the original plugin for the whole cycle: the engine has no CPU fallback,
@@ -61,9 +74,14 @@ import (
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
-	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/util/sets"
+	utilfeature "k8s.io/apiserver/pkg/util/feature"
+	corev1helpers "k8s.io/component-helpers/scheduling/corev1"
+	"k8s.io/klog/v2"
+	apipod "k8s.io/kubernetes/pkg/api/v1/pod"
+	"k8s.io/kubernetes/pkg/features"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
+	schedutil "k8s.io/kubernetes/pkg/scheduler/util"
 )
 
 // Encoder is the host side of the snapshot: NodeInfo -> SoA node table in
@@ -84,8 +102,14 @@ type Encoder interface {
 	FilterMessage(plugin string, detail uint32, node string, pod *v1.Pod) string
 	// PreFilterNodeNames is NodeAffinity's PreFilterResult.NodeNames (nil: all).
 	PreFilterNodeNames(pod *v1.Pod) sets.String
-	// Priority and victims bookkeeping for DefaultPreemption.
+	// Priority and victims bookkeeping for DefaultPreemption: the bound-pod
+	// table row index -> pod (the table follows the snapshot, SetBoundPods).
 	BoundPod(index int) *v1.Pod
+	// Pods encodes a list of pods into a set the caller owns (C memory) until
+	// release: the nominated pods of a first pass / dry run, and the copy of
+	// the cycle's pod KsimAssume keeps for Unreserve, which may run on the
+	// binding goroutine after the next cycle re-used Pod's buffers.
+	Pods(pods []*v1.Pod) (ps *C.ksim_pod_set, release func(), err error)
 }
 
 // Profile is the engine-side view of one framework profile.
@@ -94,6 +118,7 @@ type Profile struct {
 	Enc         Encoder
 	FilterOrder []string // the profile's Filter plugins in order (original names)
 	ScoreOrder  []string // the profile's Score plugins in order
+	mu          sync.Mutex
 }
 
 var (
@@ -129,9 +154,34 @@ type cycle struct {
 	scored   bool
 	raw      []int64 // [score slot][node]
 	nNodes   int
+	// added: the nominated pods addNominatedPods put on this clone of the
+	// CycleState (PreFilterExtensions.AddPod); empty on the cycle's own state
+	added []*v1.Pod
+	sh    *cycleShared
 }
 
-func (c *cycle) Clone() framework.StateData { return c }
+// cycleShared is what every clone of one cycle's state shares.
+type cycleShared struct {
+	mu      sync.Mutex
+	nom     map[int]nomAnswer // node position -> pass-1 answer
+	owned   *C.ksim_pod_set   // KsimAssume's copy of the pod (Unreserve)
+	release func()
+	assumed bool // ksim_assume succeeded and was not undone
+	node    int
+}
+
+type nomAnswer struct {
+	fail   uint8
+	detail uint32
+}
+
+// Clone: RunFilterPluginsWithNominatedPods clones the state before AddPod, so
+// the added list is per clone; the engine's answers are shared.
+func (c *cycle) Clone() framework.StateData {
+	d := *c
+	d.added = append([]*v1.Pod(nil), c.added...)
+	return &d
+}
 
 func readCycle(state *framework.CycleState) *cycle {
 	d, err := state.Read(cycleKey)
@@ -141,8 +191,15 @@ func readCycle(state *framework.CycleState) *cycle {
 	return d.(*cycle)
 }
 
-// ensureFilter runs the engine's PreFilter + Filter pass once per cycle.
+// ensureFilter runs the engine's PreFilter + Filter pass once per cycle.  A
+// profile without an engine-backed PreFilter reaches it first from the 16
+// Filter goroutines, hence Profile.mu around the check and the pass.
 func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f framework.Handle) (*cycle, error) {
+	if c := readCycle(state); c != nil {
+		return c, nil
+	}
+	p.mu.Lock()
+	defer p.mu.Unlock()
 	if c := readCycle(state); c != nil {
 		return c, nil
 	}
@@ -150,7 +207,7 @@ func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f frame
 		return nil, err
 	}
 	ps, err := p.Enc.Pod(pod)
-	c := &cycle{nNodes: len(p.Enc.NodeNames())}
+	c := &cycle{nNodes: len(p.Enc.NodeNames()), sh: &cycleShared{nom: map[int]nomAnswer{}}}
 	if err != nil {
 		c.refused = true
 		state.Write(cycleKey, c)
@@ -164,7 +221,9 @@ func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f frame
 	var out C.ksim_eval_out
 	out.fail_plugin = (*C.uint8_t)(unsafe.Pointer(&c.fail[0]))
 	out.fail_detail = (*C.uint32_t)(unsafe.Pointer(&c.detail[0]))
+	p.Engine.mu.Lock()
 	rc := C.ksim_fw_prefilter(p.Engine.h, ps, 0, &out)
+	p.Engine.mu.Unlock()
 	if rc == C.KSIM_E_UNSUPPORTED {
 		c.refused = true
 	} else if err := p.Engine.err(rc); err != nil {
@@ -173,6 +232,33 @@ func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f frame
 	c.status = int32(out.status)
 	state.Write(cycleKey, c)
 	return c, nil
+}
+
+// nominatedAnswer: pass 1 of RunFilterPluginsWithNominatedPods on node pos,
+// the clone's added pods on the node (ksim_fw_filter_nominated), once per
+// node and cycle (the 15 Filter plugins of the clone all read it).
+func (p *Profile) nominatedAnswer(c *cycle, pos int) (nomAnswer, error) {
+	c.sh.mu.Lock()
+	defer c.sh.mu.Unlock()
+	if a, ok := c.sh.nom[pos]; ok {
+		return a, nil
+	}
+	nps, release, err := p.Enc.Pods(c.added)
+	if err != nil {
+		return nomAnswer{}, err
+	}
+	defer release()
+	node, first, count := C.int32_t(pos), C.int32_t(0), C.int32_t(len(c.added))
+	var fp C.uint8_t
+	var fd C.uint32_t
+	if err := p.Engine.locked(func() C.int {
+		return C.ksim_fw_filter_nominated(p.Engine.h, nps, 1, &node, &first, &count, &fp, &fd)
+	}); err != nil {
+		return nomAnswer{}, err
+	}
+	a := nomAnswer{fail: uint8(fp), detail: uint32(fd)}
+	c.sh.nom[pos] = a
+	return a, nil
 }
 
 // Backed returns the engine-backed plugin for an in-tree / out-of-tree plugin
@@ -231,11 +317,17 @@ func (p *filterOnly) Filter(ctx context.Context, state *framework.CycleState, po
 		return framework.AsStatus(fmt.Errorf("node %s not in the engine snapshot", nodeInfo.Node().Name))
 	}
 	k := index(pr.FilterOrder, p.name)
-	r := int(c.fail[pos])
+	r, d := int(c.fail[pos]), c.detail[pos]
+	if len(c.added) > 0 { // the clone carrying the node's nominated pods (pass 1)
+		a, err := pr.nominatedAnswer(c, pos)
+		if err != nil {
+			return framework.AsStatus(err)
+		}
+		r, d = int(a.fail), a.detail
+	}
 	if r == C.KSIM_PASSED || r != k {
 		return nil
 	}
-	d := c.detail[pos]
 	return framework.NewStatus(filterCode(p.name, d), pr.Enc.FilterMessage(p.name, d, nodeInfo.Node().Name, pod))
 }
 
@@ -285,7 +377,48 @@ func (p *preFilterFilterScore) PreFilter(ctx context.Context, state *framework.C
 	return nil, nil
 }
 
-func (p *preFilterFilterScore) PreFilterExtensions() framework.PreFilterExtensions { return nil }
+// PreFilterExtensions: AddPod / RemovePod record the nominated pods on the
+// CycleState clone (every engine-backed PreFilter plugin gets the call; the
+// pod is added once).  Refused cycles forward to the original's extensions.
+func (p *preFilterFilterScore) PreFilterExtensions() framework.PreFilterExtensions { return p }
+
+func (p *preFilterFilterScore) AddPod(ctx context.Context, state *framework.CycleState, podToSchedule *v1.Pod,
+	podInfoToAdd *framework.PodInfo, nodeInfo *framework.NodeInfo) *framework.Status {
+	c := readCycle(state)
+	if c == nil || c.refused {
+		if ext := p.orig.(framework.PreFilterPlugin).PreFilterExtensions(); ext != nil {
+			return ext.AddPod(ctx, state, podToSchedule, podInfoToAdd, nodeInfo)
+		}
+		return nil
+	}
+	for _, q := range c.added {
+		if q.UID == podInfoToAdd.Pod.UID {
+			return nil
+		}
+	}
+	c.added = append(c.added, podInfoToAdd.Pod)
+	return nil
+}
+
+func (p *preFilterFilterScore) RemovePod(ctx context.Context, state *framework.CycleState, podToSchedule *v1.Pod,
+	podInfoToRemove *framework.PodInfo, nodeInfo *framework.NodeInfo) *framework.Status {
+	c := readCycle(state)
+	if c == nil || c.refused {
+		if ext := p.orig.(framework.PreFilterPlugin).PreFilterExtensions(); ext != nil {
+			return ext.RemovePod(ctx, state, podToSchedule, podInfoToRemove, nodeInfo)
+		}
+		return nil
+	}
+	for i, q := range c.added {
+		if q.UID == podInfoToRemove.Pod.UID {
+			c.added = append(c.added[:i], c.added[i+1:]...)
+			return nil
+		}
+	}
+	// removing a bound pod from the clone happens only in the original
+	// DefaultPreemption's dry run, which the engine-backed PostFilter replaces
+	return framework.AsStatus(fmt.Errorf("RemovePod of a bound pod on an engine-backed cycle"))
+}
 
 func (p *preFilterFilterScore) Score(ctx context.Context, state *framework.CycleState, pod *v1.Pod,
 	nodeName string) (int64, *framework.Status) {
@@ -324,7 +457,9 @@ func (p *fullPlugin) PreScore(ctx context.Context, state *framework.CycleState, 
 	if len(list) > 0 {
 		lp = (*C.int32_t)(unsafe.Pointer(&list[0]))
 	}
-	if err := pr.Engine.err(C.ksim_fw_score(pr.Engine.h, lp, C.int32_t(len(list)), &out)); err != nil {
+	if err := pr.Engine.locked(func() C.int {
+		return C.ksim_fw_score(pr.Engine.h, lp, C.int32_t(len(list)), &out)
+	}); err != nil {
 		return framework.AsStatus(err)
 	}
 	c.scored = true
@@ -356,9 +491,10 @@ func (p *fullPlugin) NormalizeScore(ctx context.Context, state *framework.CycleS
 	}
 	out := make([]int64, n)
 	slot := index(pr.ScoreOrder, p.name)
-	rc := C.ksim_fw_normalize(pr.Engine.h, C.int32_t(slot), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
-		(*C.int64_t)(unsafe.Pointer(&vals[0])), C.int32_t(n), (*C.int64_t)(unsafe.Pointer(&out[0])))
-	if err := pr.Engine.err(rc); err != nil {
+	if err := pr.Engine.locked(func() C.int {
+		return C.ksim_fw_normalize(pr.Engine.h, C.int32_t(slot), (*C.int32_t)(unsafe.Pointer(&nodes[0])),
+			(*C.int64_t)(unsafe.Pointer(&vals[0])), C.int32_t(n), (*C.int64_t)(unsafe.Pointer(&out[0])))
+	}); err != nil {
 		return framework.AsStatus(err)
 	}
 	for i := range scores {
@@ -394,10 +530,14 @@ func score(b *base, ctx context.Context, state *framework.CycleState, pod *v1.Po
 }
 
 // ---- KsimAssume: the engine snapshot's AssumePod ----------------------------------
-// An unwrapped Reserve plugin the host appends to every profile's Reserve set
+// An unwrapped Reserve + PostBind plugin the host appends to every profile
 // (after ConvertForSimulator, so the wrapped set and its annotations are
 // unchanged).  Reserve records nothing; it assumes the pod on the framework's
-// node (selectHost's pick, ties included) in the device snapshot.
+// node (selectHost's pick, ties included) in the device snapshot, from a copy
+// of the pod's encoding the cycle owns.  Unreserve -- from a later Reserve
+// plugin's failure, Permit, PreBind or Bind, possibly on the binding goroutine
+// after the next cycle started -- forgets it only if this Reserve assumed it
+// (upstream cache.ForgetPod is likewise a no-op for a pod never assumed).
 type KsimAssume struct{ f framework.Handle }
 
 func NewKsimAssume(_ interface{}, f framework.Handle) (framework.Plugin, error) {
@@ -417,7 +557,18 @@ func (p *KsimAssume) Reserve(ctx context.Context, state *framework.CycleState, p
 	if !ok {
 		return framework.AsStatus(fmt.Errorf("node %s not in the engine snapshot", nodeName))
 	}
-	return framework.AsStatus(pr.Engine.err(C.ksim_assume(pr.Engine.h, c.ps, 0, C.int32_t(pos))))
+	owned, release, err := pr.Enc.Pods([]*v1.Pod{pod})
+	if err != nil {
+		return framework.AsStatus(err)
+	}
+	if err := pr.Engine.locked(func() C.int { return C.ksim_assume(pr.Engine.h, owned, 0, C.int32_t(pos)) }); err != nil {
+		release()
+		return framework.AsStatus(err)
+	}
+	c.sh.mu.Lock()
+	c.sh.owned, c.sh.release, c.sh.assumed, c.sh.node = owned, release, true, pos
+	c.sh.mu.Unlock()
+	return nil
 }
 
 func (p *KsimAssume) Unreserve(ctx context.Context, state *framework.CycleState, pod *v1.Pod, nodeName string) {
@@ -426,14 +577,36 @@ func (p *KsimAssume) Unreserve(ctx context.Context, state *framework.CycleState,
 		return
 	}
 	pr := profileOf(p.f)
-	if pos, ok := pr.Enc.Position(nodeName); ok {
-		_ = C.ksim_forget(pr.Engine.h, c.ps, 0, C.int32_t(pos))
+	c.sh.mu.Lock()
+	defer c.sh.mu.Unlock()
+	if !c.sh.assumed {
+		return
+	}
+	_ = pr.Engine.locked(func() C.int { return C.ksim_forget(pr.Engine.h, c.sh.owned, 0, C.int32_t(c.sh.node)) })
+	c.sh.assumed = false
+	c.sh.release()
+	c.sh.owned, c.sh.release = nil, nil
+}
+
+// PostBind: the pod is bound; the snapshot keeps it, the copy is released.
+func (p *KsimAssume) PostBind(ctx context.Context, state *framework.CycleState, pod *v1.Pod, nodeName string) {
+	c := readCycle(state)
+	if c == nil || c.refused {
+		return
+	}
+	c.sh.mu.Lock()
+	defer c.sh.mu.Unlock()
+	if c.sh.release != nil {
+		c.sh.release()
+		c.sh.owned, c.sh.release = nil, nil
 	}
 }
 
 // ---- DefaultPreemption --------------------------------------------------------------
 type postFilter struct{ *base }
 
+// PostFilter restates DefaultPreemption.PostFilter / Evaluator.Preempt (v1.26
+// default_preemption.go, preemption.go) around the engine's dry run.
 func (p *postFilter) PostFilter(ctx context.Context, state *framework.CycleState, pod *v1.Pod,
 	m framework.NodeToStatusMap) (*framework.PostFilterResult, *framework.Status) {
 	c := readCycle(state)
@@ -441,15 +614,62 @@ func (p *postFilter) PostFilter(ctx context.Context, state *framework.CycleState
 		return p.orig.(framework.PostFilterPlugin).PostFilter(ctx, state, pod, m)
 	}
 	pr := p.prof()
+	// 0) the latest version of the pod (its nominatedNodeName)
+	if latest, err := p.f.SharedInformerFactory().Core().V1().Pods().Lister().Pods(pod.Namespace).Get(pod.Name); err == nil {
+		pod = latest
+	} else {
+		return nil, framework.AsStatus(err)
+	}
+	prio := corev1helpers.PodPriority(pod)
+	// 1) PodEligibleToPreemptOthers
+	if pod.Spec.PreemptionPolicy != nil && *pod.Spec.PreemptionPolicy == v1.PreemptNever {
+		return nil, framework.NewStatus(framework.Unschedulable, "preemption: not eligible due to preemptionPolicy=Never.")
+	}
+	if nom := pod.Status.NominatedNodeName; nom != "" && m[nom].Code() != framework.UnschedulableAndUnresolvable {
+		if ni, err := p.f.SnapshotSharedLister().NodeInfos().Get(nom); err == nil {
+			for _, q := range ni.Pods {
+				if q.Pod.DeletionTimestamp != nil && corev1helpers.PodPriority(q.Pod) < prio {
+					return nil, framework.NewStatus(framework.Unschedulable,
+						"preemption: not eligible due to a terminating pod on the nominated node.")
+				}
+			}
+		}
+	}
+	// 2) the dry run, with the PodNominator's pods of priority >= the pod's
+	// (SelectVictimsOnNode filters through RunFilterPluginsWithNominatedPods)
+	var noms []*v1.Pod
+	var gnodes, first, count []C.int32_t
+	for pos, name := range pr.Enc.NodeNames() {
+		k := 0
+		for _, q := range p.f.NominatedPodsForNode(name) {
+			if q.Pod.UID != pod.UID && corev1helpers.PodPriority(q.Pod) >= prio {
+				noms = append(noms, q.Pod)
+				k++
+			}
+		}
+		if k > 0 {
+			gnodes = append(gnodes, C.int32_t(pos))
+			first = append(first, C.int32_t(len(noms)-k))
+			count = append(count, C.int32_t(k))
+		}
+	}
+	var nps *C.ksim_pod_set
+	var gn, gf, gc *C.int32_t
+	if len(noms) > 0 {
+		set, release, err := pr.Enc.Pods(noms)
+		if err != nil {
+			return nil, framework.AsStatus(err)
+		}
+		defer release()
+		nps, gn, gf, gc = set, &gnodes[0], &first[0], &count[0]
+	}
 	victims := make([]int32, 1024)
 	var out C.ksim_preempt_out
 	out.victims = (*C.int32_t)(unsafe.Pointer(&victims[0]))
 	out.victims_cap = C.int32_t(len(victims))
-	prio := int32(0)
-	if pod.Spec.Priority != nil {
-		prio = *pod.Spec.Priority
-	}
-	rc := C.ksim_preempt(pr.Engine.h, c.ps, 0, C.int32_t(prio), &out)
+	pr.Engine.mu.Lock()
+	rc := C.ksim_preempt_nominated(pr.Engine.h, c.ps, 0, C.int32_t(prio), nps, C.int32_t(len(gnodes)), gn, gf, gc, &out)
+	pr.Engine.mu.Unlock()
 	if rc == C.KSIM_E_UNSUPPORTED {
 		return p.orig.(framework.PostFilterPlugin).PostFilter(ctx, state, pod, m)
 	}
@@ -457,18 +677,51 @@ func (p *postFilter) PostFilter(ctx context.Context, state *framework.CycleState
 		return nil, framework.AsStatus(err)
 	}
 	if out.nominated < 0 {
-		return nil, framework.NewStatus(framework.Unschedulable, "preemption: no candidate node")
+		// no candidate: ModeOverride "" clears the pod's nomination
+		return framework.NewPostFilterResultWithNominatedNode(""),
+			framework.NewStatus(framework.Unschedulable, "preemption: no candidate node")
 	}
-	// prepareCandidate: delete the victims (PodDisruptionBudgets are out of
-	// the engine's scope, DESIGN.md §8)
+	// 5) prepareCandidate (PodDisruptionBudgets are out of the engine's scope,
+	// DESIGN.md §8): reject waiting victims, else patch the DisruptionTarget
+	// condition (PodDisruptionConditions, beta in v1.26; upstream builds the
+	// new status from the preemptor's own status, restated as is) and delete
+	// with the default grace period; then clear the nominations of
+	// lower-priority pods nominated on the node.
 	cs := p.f.ClientSet()
 	for i := 0; i < int(out.n_victims) && i < len(victims); i++ {
 		v := pr.Enc.BoundPod(int(victims[i]))
-		if err := cs.CoreV1().Pods(v.Namespace).Delete(ctx, v.Name, metav1.DeleteOptions{}); err != nil {
+		if wp := p.f.GetWaitingPod(v.UID); wp != nil {
+			wp.Reject("DefaultPreemption", "preempted")
+			continue
+		}
+		if utilfeature.DefaultFeatureGate.Enabled(features.PodDisruptionConditions) {
+			cond := &v1.PodCondition{Type: v1.DisruptionTarget, Status: v1.ConditionTrue,
+				Reason:  v1.PodReasonPreemptionByScheduler,
+				Message: fmt.Sprintf("%s: preempting to accommodate a higher priority pod", pod.Spec.SchedulerName)}
+			st := pod.Status.DeepCopy()
+			if apipod.UpdatePodCondition(st, cond) {
+				if err := schedutil.PatchPodStatus(ctx, cs, v, st); err != nil {
+					return nil, framework.AsStatus(err)
+				}
+			}
+		}
+		if err := schedutil.DeletePod(ctx, cs, v); err != nil {
 			return nil, framework.AsStatus(err)
 		}
+		p.f.EventRecorder().Eventf(v, pod, v1.EventTypeNormal, "Preempted", "Preempting",
+			"Preempted by a pod on node %v", pr.Enc.NodeNames()[int(out.nominated)])
 	}
 	name := pr.Enc.NodeNames()[int(out.nominated)]
-	return &framework.PostFilterResult{NominatingInfo: &framework.NominatingInfo{
-		NominatedNodeName: name, NominatingMode: framework.ModeOverride}}, nil
+	var lower []*v1.Pod
+	for _, q := range p.f.NominatedPodsForNode(name) {
+		if corev1helpers.PodPriority(q.Pod) < prio {
+			lower = append(lower, q.Pod)
+		}
+	}
+	if len(lower) > 0 {
+		if err := schedutil.ClearNominatedNodeName(ctx, cs, lower...); err != nil {
+			klog.ErrorS(err, "Cannot clear 'NominatedNodeName' field")
+		}
+	}
+	return framework.NewPostFilterResultWithNominatedNode(name), framework.NewStatus(framework.Success)
 }

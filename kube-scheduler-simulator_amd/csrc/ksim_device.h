@@ -614,6 +614,26 @@ __device__ __forceinline__ bool volume_groups_match(const DevCluster& c, const D
   return ok;
 }
 
+// VolumeBinding: the reasons of the failing groups (KSIM_VB_NODE_CONFLICT for
+// a bound-PV group, KSIM_VB_BIND_CONFLICT for an unbound-claim group); 0 = pass.
+__device__ __forceinline__ uint32_t volume_binding_fails(const DevCluster& c, const DevPods& P, int32_t first,
+                                                         int32_t count, int32_t node) {
+  int32_t group = -1;
+  bool ok = true;
+  uint32_t why = 0;
+  for (int i = 0; i < count; i++) {
+    const ksim_term& t = P.terms[first + i];
+    if (t.weight != group) {
+      if (!ok) why |= (group & KSIM_VB_UNBOUND_GROUP) ? KSIM_VB_BIND_CONFLICT : KSIM_VB_NODE_CONFLICT;
+      group = t.weight;
+      ok = false;
+    }
+    if (!ok && term_matches(c, P, t, node)) ok = true;
+  }
+  if (!ok) why |= (group & KSIM_VB_UNBOUND_GROUP) ? KSIM_VB_BIND_CONFLICT : KSIM_VB_NODE_CONFLICT;
+  return why;
+}
+
 // nodeaffinity PreferredSchedulingTerms.Score
 __device__ __forceinline__ int64_t preferred_node_affinity_score(const DevCluster& c, const DevPods& P,
                                                         const ksim_pod& p, int32_t node) {
@@ -1008,9 +1028,11 @@ __device__ __forceinline__ uint8_t run_filter_plugins(const DevCluster& c, const
         if (!node_affinity_filter(c, P, p, node, why)) { detail = why; return (uint8_t)f; }
         break;
       }
-      case KSIM_PL_VOLUME_BINDING:
-        if (p.vb_count && !volume_groups_match(c, P, p.vb_first, p.vb_count, node)) return (uint8_t)f;
+      case KSIM_PL_VOLUME_BINDING: {
+        const uint32_t why = p.vb_count ? volume_binding_fails(c, P, p.vb_first, p.vb_count, node) : 0u;
+        if (why) { detail = why; return (uint8_t)f; }
         break;
+      }
       case KSIM_PL_VOLUME_ZONE:
         if (p.vz_count && !volume_groups_match(c, P, p.vz_first, p.vz_count, node)) return (uint8_t)f;
         break;
@@ -1159,7 +1181,10 @@ __device__ __forceinline__ uint8_t run_filter_plan(const DevCluster& c, const De
     take(KSIM_PL_NODE_AFFINITY, !ok, why, false);
   }
   if (fp.en & (1u << KSIM_PL_VOLUME_BINDING))
-    take(KSIM_PL_VOLUME_BINDING, !volume_groups_match(c, P, p.vb_first, p.vb_count, node), 0, false);
+  {
+    const uint32_t why = volume_binding_fails(c, P, p.vb_first, p.vb_count, node);
+    take(KSIM_PL_VOLUME_BINDING, why != 0, why, false);
+  }
   if (fp.en & (1u << KSIM_PL_VOLUME_ZONE))
     take(KSIM_PL_VOLUME_ZONE, !volume_groups_match(c, P, p.vz_first, p.vz_count, node), 0, false);
   if (fp.en & (1u << KSIM_PL_NODE_RESOURCES_FIT)) {

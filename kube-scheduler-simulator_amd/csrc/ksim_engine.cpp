@@ -139,8 +139,10 @@ struct ksim_handle {
 
   // compat-mode single pod
   std::vector<DevBuf> pod1_bufs;
+  std::vector<DevBuf> nom_bufs;         // a nominated pod (ksim_fw_filter_nominated)
   // DefaultPreemption: bound pods per node in importance order
   std::vector<DevBuf> pre_bufs;
+  std::vector<DevBuf> pre_nom_bufs;     // ksim_preempt_nominated's group requests
   DevPreempt pre{};
   std::vector<int32_t> pre_index;       // CSR position -> bound-pod table index
   int32_t pre_n = 0;
@@ -152,7 +154,7 @@ struct ksim_handle {
   // framework-driven compat cycle (ksim_fw_prefilter -> ksim_fw_score ->
   // ksim_fw_normalize): the pod in h->pod1, its filter pass on the host for
   // list validation, the scan-set size
-  bool fw_pending = false, fw_scored = false, fw_dom_dirty = false;
+  bool fw_pending = false, fw_scored = false, fw_dom_dirty = false, fw_topo = false;
   int32_t fw_ns = 0;
   std::vector<uint8_t> fw_fail;
   int32_t* fw_nodes = nullptr;     // device [n]
@@ -1594,6 +1596,8 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->pod_bufs);
   free_bufs(h->pod1_bufs);
   free_bufs(h->pre_bufs);
+  free_bufs(h->pre_nom_bufs);
+  free_bufs(h->nom_bufs);
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   if (h->st) (void)hipFree(h->st);
   if (h->d_prof) (void)hipFree(h->d_prof);
@@ -1768,6 +1772,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   // node positions of the old snapshot: the bound-pod table and a pending
   // extender round trip do not carry over
   free_bufs(h->pre_bufs);
+  free_bufs(h->pre_nom_bufs);
   h->pre = DevPreempt{};
   h->pre_index.clear();
   h->pre_n = 0;
@@ -2251,7 +2256,8 @@ static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std
 }
 
 // Upload one pod (re-based) as a device pod set of its own.
-static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P) {
+static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P,
+                         std::vector<DevBuf>& bufs) {
   ksim_pod pod;
   std::vector<ksim_label_expr> ex;
   std::vector<ksim_term> tm;
@@ -2261,30 +2267,30 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   single_pod_set(ps, pod_index, pod, ex, tm, us, ad, nn);
   mark_unique(h, us.data(), us.size());
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  free_bufs(h->pod1_bufs);
+  free_bufs(bufs);
   P = DevPods{};
   void* p = nullptr;
   int rc;
-  if ((rc = upload(h, h->pod1_bufs, &pod, sizeof(pod), &p))) return rc;
+  if ((rc = upload(h, bufs, &pod, sizeof(pod), &p))) return rc;
   P.pods = (const ksim_pod*)p;
-  if ((rc = upload(h, h->pod1_bufs, ex.data(), ex.size() * sizeof(ksim_label_expr), &p))) return rc;
+  if ((rc = upload(h, bufs, ex.data(), ex.size() * sizeof(ksim_label_expr), &p))) return rc;
   P.exprs = (const ksim_label_expr*)p;
-  if ((rc = upload(h, h->pod1_bufs, tm.data(), tm.size() * sizeof(ksim_term), &p))) return rc;
+  if ((rc = upload(h, bufs, tm.data(), tm.size() * sizeof(ksim_term), &p))) return rc;
   P.terms = (const ksim_term*)p;
-  if ((rc = upload(h, h->pod1_bufs, nn.data(), 4 * nn.size(), &p))) return rc;
+  if ((rc = upload(h, bufs, nn.data(), 4 * nn.size(), &p))) return rc;
   P.nn = (const int32_t*)p;
   P.n_nn = (int32_t)nn.size();
   int32_t bflag[4] = {0, 0, 0, 0};
   for (const auto& u : us)
     if (use_registers_values(u)) bflag[0] |= kPodRegistersValues;
-  if ((rc = upload(h, h->pod1_bufs, bflag, sizeof(bflag), &p))) return rc;
+  if ((rc = upload(h, bufs, bflag, sizeof(bflag), &p))) return rc;
   P.bflags = (const int32_t*)p;
   const PodPlan plan = make_plan(h, pod, us.data());
-  if ((rc = upload(h, h->pod1_bufs, &plan, sizeof(plan), &p))) return rc;
+  if ((rc = upload(h, bufs, &plan, sizeof(plan), &p))) return rc;
   P.plans = (const PodPlan*)p;
-  if ((rc = upload(h, h->pod1_bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
+  if ((rc = upload(h, bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
   P.uses = (const ksim_topo_use*)p;
-  if ((rc = upload(h, h->pod1_bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
+  if ((rc = upload(h, bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
   P.adds = (const ksim_class_add*)p;
   P.n_pods = 1;
   P.n_exprs = (int32_t)ex.size();
@@ -2298,6 +2304,10 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   P.n_uses = (int32_t)us.size();
   P.n_adds = (int32_t)ad.size();
   return KSIM_OK;
+}
+
+static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P) {
+  return upload_single(h, ps, pod_index, P, h->pod1_bufs);
 }
 
 // Copy one compat cycle's per-node outputs and scalars to the caller.
@@ -2439,6 +2449,7 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, p.use_count > 0);
   HIPCHK(h, hipGetLastError());
   h->fw_dom_dirty = p.use_count > 0;
+  h->fw_topo = p.use_count > 0;
   const size_t N = (size_t)h->dc.n;
   h->fw_fail.resize(N);
   HIPCHK(h, hcopy(h, h->fw_fail.data(), h->sc.fail, N, hipMemcpyDeviceToHost));
@@ -2463,6 +2474,70 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   out->next_start = next;
   h->fw_ns = ns;
   h->fw_pending = !unknown;
+  return KSIM_OK;
+}
+
+// The cycle's filter pass again, on the current dynamic state: the PreFilter
+// domain sums start from zero, the topology flags too (ksim_fw_prefilter).
+static int fw_filter_pass(ksim_handle* h) {
+  if (h->fw_topo && h->sc.dom)
+    HIPCHK(h, hipMemsetAsync(h->sc.dom, 0, 8 * (size_t)KSIM_MAX_USES * h->dc.vmax, h->stream));
+  int rc;
+  if ((rc = set_run(h, 0, 1))) return rc;
+  HIPCHK(h, hipMemsetAsync(&h->st->topo_flags, 0, sizeof(uint32_t), h->stream));
+  launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, h->fw_topo);
+  HIPCHK(h, hipGetLastError());
+  return KSIM_OK;
+}
+
+// RunFilterPluginsWithNominatedPods' first pass: for each listed node, the
+// cycle's pod against that node with its nominated pods added (addNominatedPods:
+// NodeInfo.AddPodInfo and the PreFilterExtensions' AddPod of PodTopologySpread
+// and InterPodAffinity, which for +1 updates equal a PreFilter over the state
+// with the pods bound there).  Each node's pods are assumed, the filter pass
+// re-run, the node's verdict read, the pods forgotten; a last pass restores the
+// cycle's own PreFilter state for ksim_fw_score.
+int ksim_fw_filter_nominated(ksim_handle* h, const ksim_pod_set* nps, int32_t n_nodes, const int32_t* nodes,
+                             const int32_t* first, const int32_t* count, uint8_t* fail_plugin,
+                             uint32_t* fail_detail) {
+  int rc = ensure_ready(h, true);
+  if (rc) return rc;
+  if (!h->fw_pending) return set_err(h, KSIM_E_INVALID, "ksim_fw_filter_nominated without ksim_fw_prefilter");
+  if (n_nodes < 0 || (n_nodes > 0 && (!nodes || !first || !count || !nps || !nps->pods || !fail_plugin)))
+    return set_err(h, KSIM_E_INVALID, "bad nominated-node groups");
+  for (int32_t k = 0; k < n_nodes; k++) {
+    if (nodes[k] < 0 || nodes[k] >= h->dc.n) return set_err(h, KSIM_E_INVALID, "nominated node out of range");
+    if (count[k] < 0 || first[k] < 0 || first[k] + count[k] > nps->n_pods)
+      return set_err(h, KSIM_E_INVALID, "nominated pod range out of the pod set");
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++)
+      if ((rc = validate_pod(h, nps, j))) return rc;
+  }
+  if (n_nodes == 0) return KSIM_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  auto bind_all = [&](int32_t k, int sign) -> int {
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
+      DevPods P;
+      int r;
+      if ((r = upload_single(h, nps, j, P, h->nom_bufs))) return r;
+      launch_assume(h->dc, P, 0, nodes[k], sign, h->stream);
+      HIPCHK(h, hipGetLastError());
+    }
+    return KSIM_OK;
+  };
+  for (int32_t k = 0; k < n_nodes; k++) {
+    if ((rc = bind_all(k, 1))) return rc;
+    if ((rc = fw_filter_pass(h))) return rc;
+    uint8_t f = 0;
+    uint32_t d = 0;
+    HIPCHK(h, hcopy(h, &f, h->sc.fail + nodes[k], 1, hipMemcpyDeviceToHost));
+    HIPCHK(h, hcopy(h, &d, h->sc.detail + nodes[k], 4, hipMemcpyDeviceToHost));
+    if (fail_is_error(f)) f &= (uint8_t)~kFailError;
+    fail_plugin[k] = f;
+    if (fail_detail) fail_detail[k] = d;
+    if ((rc = bind_all(k, -1))) return rc;
+  }
+  if ((rc = fw_filter_pass(h))) return rc;                 // the cycle's own PreFilter state again
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return KSIM_OK;
 }
 
@@ -3339,6 +3414,10 @@ extern "C" int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b) {
   d.res = (PreemptNode*)p;
   if ((rc = upload(h, h->pre_bufs, nullptr, 16, &p))) return rc;
   d.pick = (int32_t*)p;
+  if ((rc = upload(h, h->pre_bufs, nullptr, 4 * (size_t)std::max(N, 1), &p))) return rc;
+  d.nslot = (int32_t*)p;
+  HIPCHK(h, hipMemsetAsync(d.nslot, 0xff, 4 * (size_t)std::max(N, 1), h->stream));   // -1: no group
+  d.nreq = nullptr;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->pre = d;
   h->pre_index = ix;
@@ -3348,10 +3427,30 @@ extern "C" int ksim_set_bound_pods(ksim_handle* h, const ksim_bound_pods* b) {
 
 extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t priority,
                             ksim_preempt_out* out) {
+  return ksim_preempt_nominated(h, ps, pod_index, priority, nullptr, 0, nullptr, nullptr, nullptr, out);
+}
+
+extern "C" int ksim_preempt_nominated(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t priority,
+                                      const ksim_pod_set* nps, int32_t n_groups, const int32_t* gnodes,
+                                      const int32_t* first, const int32_t* count, ksim_preempt_out* out) {
   int rc = ensure_ready(h);
   if (rc) return rc;
   if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
     return set_err(h, KSIM_E_INVALID, "bad pod set / index");
+  if (n_groups < 0 || (n_groups > 0 && (!nps || !nps->pods || !gnodes || !first || !count)))
+    return set_err(h, KSIM_E_INVALID, "bad nominated-node groups");
+  {
+    std::vector<uint8_t> seen((size_t)std::max(h->dc.n, 1), 0);
+    for (int32_t k = 0; k < n_groups; k++) {
+      if (gnodes[k] < 0 || gnodes[k] >= h->dc.n || seen[gnodes[k]])
+        return set_err(h, KSIM_E_INVALID, "nominated node out of range or repeated");
+      seen[gnodes[k]] = 1;
+      if (count[k] < 0 || first[k] < 0 || first[k] + count[k] > nps->n_pods)
+        return set_err(h, KSIM_E_INVALID, "nominated pod range out of the pod set");
+      for (int32_t j = first[k]; j < first[k] + count[k]; j++)
+        if ((rc = validate_pod(h, nps, j))) return rc;
+    }
+  }
   if (!h->pre.off) return set_err(h, KSIM_E_INVALID, "ksim_set_bound_pods first");
   if (is_sharded(h)) return set_err(h, KSIM_E_UNSUPPORTED, "preemption runs on unsharded handles");
   if (prof_has_filter(h->prof, KSIM_PL_NETWORK_BANDWIDTH))
@@ -3368,8 +3467,60 @@ extern "C" int ksim_preempt(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_
   DevPods P;
   if ((rc = upload_single(h, ps, pod_index, P))) return rc;
   if ((rc = set_run(h, 0, 1))) return rc;
-  launch_preempt(make_args(h, P, nullptr), h->pre, fit, priority, h->stream);
+  const LaunchArgs a = make_args(h, P, nullptr);
+  DevPreempt pre = h->pre;
+  std::vector<uint8_t> gfail((size_t)std::max(n_groups, 1), KSIM_PASSED);
+  std::vector<int64_t> nreq((size_t)std::max(n_groups, 1) * (KSIM_PREEMPT_REQ + 1), 0);
+  auto bind_group = [&](int32_t k, int sign) -> int {
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
+      DevPods Q;
+      int r;
+      if ((r = upload_single(h, nps, j, Q, h->nom_bufs))) return r;
+      launch_assume(h->dc, Q, 0, gnodes[k], sign, h->stream);
+      HIPCHK(h, hipGetLastError());
+    }
+    return KSIM_OK;
+  };
+  for (int32_t k = 0; k < n_groups; k++) {                // pass 1 of each grouped node
+    if ((rc = bind_group(k, 1))) return rc;
+    launch_filter_only(a, h->stream);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hcopy(h, &gfail[k], h->sc.fail + gnodes[k], 1, hipMemcpyDeviceToHost));
+    if ((rc = bind_group(k, -1))) return rc;
+    int64_t* q = nreq.data() + (size_t)k * (KSIM_PREEMPT_REQ + 1);
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
+      const ksim_pod& x = nps->pods[j];
+      q[0] += x.req_cpu;
+      q[1] += x.req_mem;
+      q[2] += x.req_eph;
+      for (int c = 0; c < KSIM_MAX_SCALAR; c++) q[3 + c] += x.scalar_req[c];
+    }
+    q[KSIM_PREEMPT_REQ] = count[k];
+  }
+  launch_filter_only(a, h->stream);                        // every node as is
   HIPCHK(h, hipGetLastError());
+  if (n_groups > 0) {
+    free_bufs(h->pre_nom_bufs);
+    void* p = nullptr;
+    if ((rc = upload(h, h->pre_nom_bufs, nreq.data(), 8 * nreq.size(), &p))) return rc;
+    pre.nreq = (const int64_t*)p;
+    for (int32_t k = 0; k < n_groups; k++) {
+      // a grouped node's status: pass 1's unless it passed (then pass 2's, as is)
+      if (gfail[k] != KSIM_PASSED) {
+        gfail[k] &= (uint8_t)~kFailError;
+        HIPCHK(h, hipMemcpyAsync(h->sc.fail + gnodes[k], &gfail[k], 1, hipMemcpyHostToDevice, h->stream));
+      }
+      HIPCHK(h, hipMemcpyAsync(pre.nslot + gnodes[k], &k, 4, hipMemcpyHostToDevice, h->stream));
+      HIPCHK(h, hipStreamSynchronize(h->stream));        // k and gfail[k] are host stack / vector slots
+    }
+  }
+  launch_preempt(a, pre, fit, priority, h->stream, false);
+  HIPCHK(h, hipGetLastError());
+  if (n_groups > 0) {
+    static const int32_t kNoGroup = -1;
+    for (int32_t k = 0; k < n_groups; k++)
+      HIPCHK(h, hipMemcpyAsync(pre.nslot + gnodes[k], &kNoGroup, 4, hipMemcpyHostToDevice, h->stream));
+  }
   int32_t pick[4];
   HIPCHK(h, hipMemcpyAsync(pick, h->pre.pick, sizeof(pick), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));

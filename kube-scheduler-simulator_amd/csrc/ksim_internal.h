@@ -162,8 +162,12 @@ struct DevPreempt {
   uint8_t* vflag;                      // [n_bound] victim of its node's dry run
   PreemptNode* res;                    // [n]
   int32_t* pick;                       // [4] nominated, victims, potential, candidates
+  int32_t* nslot;                      // [n] nominated group of the node, -1: none
+  const int64_t* nreq;                 // [groups][KSIM_PREEMPT_REQ + 1] requests, pod count
 };
-void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_index, int32_t prio, hipStream_t stream);
+// filter = false: s.fail already holds the statuses (ksim_preempt_nominated)
+void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_index, int32_t prio, hipStream_t stream,
+                    bool filter = true);
 
 // The evaluation kernels alone (ksim_time_eval).
 void launch_batch_eval_only(const LaunchArgs& a, hipStream_t stream);

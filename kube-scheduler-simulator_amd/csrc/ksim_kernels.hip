@@ -1299,7 +1299,8 @@ __global__ __launch_bounds__(256) void k_wfinal_sh(DevCluster c, DevPods P, cons
     } else if (u.col != KSIM_COL_NONE) {
       const int32_t V = c.col_nvals[u.col];
       int32_t cnt = 0;
-      for (int32_t v = threadIdx.x; v < V; v += blockDim.x) cnt += v != 0 && s.xreg[off + v] > 0;
+      // value 0 registers only for system-defaulted constraints: the pair (key, "")
+      for (int32_t v = threadIdx.x; v < V; v += blockDim.x) cnt += s.xreg[off + v] > 0;
       size = block_sum_i32_nw<4>(cnt, sh32);
       off += V;
     }

@@ -43,7 +43,13 @@ __global__ __launch_bounds__(256) void k_preempt_nodes(DevCluster c, DevPods P, 
     const int32_t a = pre.off[node], b = pre.off[node + 1];
     int32_t j0 = a;
     while (j0 < b && pre.prio[j0] >= prio) j0++;       // lower priorities: the suffix [j0, b)
+    for (int32_t j = a; j < j0; j++) pre.vflag[j] = 0;   // no stale flags from an earlier preemptor
     NodeRow r = load_row(c, node);
+    if (pre.nslot && pre.nslot[node] >= 0) {              // the nominated pods stay (pass 1)
+      const int64_t* q = pre.nreq + (size_t)pre.nslot[node] * (KSIM_PREEMPT_REQ + 1);
+      row_add_req(r, q, 1, c.n_scalar);
+      r.num_pods += (int32_t)q[KSIM_PREEMPT_REQ] - 1;
+    }
     for (int32_t j = j0; j < b; j++) row_add_req(r, pre.req + (size_t)j * KSIM_PREEMPT_REQ, -1, c.n_scalar);
     if (fits_request(r, p, c.n_scalar, c.fit_ignore) == 0) {
       out.cand = 1;
@@ -168,9 +174,9 @@ __global__ __launch_bounds__(kPickThreads) void k_preempt_pick(DevCluster c, Dev
 }
 
 void launch_preempt(const LaunchArgs& a, const DevPreempt& pre, int32_t fit_index, int32_t prio,
-                    hipStream_t stream) {
+                    hipStream_t stream, bool filter) {
   const int blocks = (a.c.n + 255) / 256;
-  launch_filter_only(a, stream);                         // the filter statuses of every node
+  if (filter) launch_filter_only(a, stream);             // the filter statuses of every node
   k_preempt_nodes<<<blocks, 256, 0, stream>>>(a.c, a.P, a.st, a.s, pre, fit_index, prio);
   k_preempt_pick<<<1, kPickThreads, 0, stream>>>(a.c, pre, a.prof.preempt_min_pct, a.prof.preempt_min_abs);
 }

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -122,6 +122,9 @@ IPA_AFFINITY = 1
 IPA_ANTI_AFFINITY = 2
 IPA_EXISTING_ANTI = 3
 NA_ENFORCED = 1                # NodeAffinity failed the scheduler-enforced addedAffinity
+VB_NODE_CONFLICT = 1           # VolumeBinding detail: a bound PV's node affinity
+VB_BIND_CONFLICT = 2           # VolumeBinding detail: an unbound claim found no PV / provisioning
+VB_UNBOUND_GROUP = 1 << 30     # group-index flag of an unbound-claim VolumeBinding group
 
 # NodeResourcesFit scoring strategies
 FIT_LEAST_ALLOCATED = 0

@@ -285,6 +285,12 @@ class EncodedPods:
     # per pod: NodeAffinity's PreFilterResult.NodeNames (sorted names, as the
     # wrapper records them) or None (all nodes); [] = conflicting terms
     prefilter_names: List[Optional[List[str]]] = field(default_factory=list)
+    # per pod: a PreFilter rejection (plugin, message) the hosts record instead
+    # of Filter (VolumeBinding's UnschedulableAndUnresolvable); [] = none at all
+    prefilter_reject: List[Optional[Tuple[str, str]]] = field(default_factory=list)
+
+    def rejection(self, index: int) -> Optional[Tuple[str, str]]:
+        return self.prefilter_reject[index] if self.prefilter_reject else None
 
     @property
     def n_pods(self) -> int:
@@ -309,7 +315,15 @@ class EncodedPods:
     def subset(self, first: int, count: int) -> "EncodedPods":
         return EncodedPods(self.pods[first:first + count].copy(), self.exprs, self.terms,
                            self.names[first:first + count], self.uses, self.adds, self.nn,
-                           self.prefilter_names[first:first + count])
+                           self.prefilter_names[first:first + count], self.prefilter_reject[first:first + count])
+
+    def subset_indices(self, idx) -> "EncodedPods":
+        """The pods at ``idx`` (any order, repeats allowed) sharing this set's tables."""
+        idx = [int(i) for i in idx]
+        return EncodedPods(self.pods[idx].copy(), self.exprs, self.terms, [self.names[i] for i in idx],
+                           self.uses, self.adds, self.nn,
+                           [self.prefilter_names[i] for i in idx] if self.prefilter_names else self.prefilter_names,
+                           [self.prefilter_reject[i] for i in idx] if self.prefilter_reject else [])
 
 
 # ---- cluster encoder --------------------------------------------------------
@@ -590,6 +604,7 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None, adde
     adds: List[Tuple[int, int]] = []
     nn: List[int] = []
     pf_names: List[Optional[List[str]]] = []
+    pf_reject: Dict[int, Tuple[str, str]] = {}
     for i, p in enumerate(pods):
         r = pod_requests(p)
         nz = pod_nonzero_requests(p)
@@ -655,12 +670,17 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None, adde
             if groups is None:
                 flags |= abi.POD_HAS_VOLUMES
             else:
-                for key, terms_of in (("vb", groups[0]), ("vz", groups[1])):
+                vb, vz, n_bound = groups
+                for key, terms_of, nb in (("vb", vb, n_bound), ("vz", vz, len(vz))):
                     rec[f"{key}_first"] = len(b.terms)
                     for g, ts in enumerate(terms_of):
+                        gid = g if g < nb else g | abi.VB_UNBOUND_GROUP   # unbound-claim group
                         for t in ts:
-                            b.term(t, g)
+                            b.term(t, gid)
                     rec[f"{key}_count"] = len(b.terms) - rec[f"{key}_first"]
+                msg = volumes.prefilter_rejection(p)
+                if msg is not None:                   # VolumeBinding PreFilter: no Filter runs
+                    pf_reject[i] = ("VolumeBinding", msg)
         pf = prefilter_node_names(p)
         pf_names.append(pf)
         if pf is not None:                    # findNodesThatFitPod scans only these nodes
@@ -699,4 +719,5 @@ def encode_pods(cluster: EncodedCluster, pods: Sequence[Pod], volumes=None, adde
         aarr["cls"] = [x[0] for x in adds]
         aarr["count"] = [x[1] for x in adds]
     cluster.refresh_classes()
-    return EncodedPods(arr, exprs, terms, names, uarr, aarr, np.array(nn, np.int32), pf_names)
+    return EncodedPods(arr, exprs, terms, names, uarr, aarr, np.array(nn, np.int32), pf_names,
+                       [pf_reject.get(i) for i in range(len(pods))] if pf_reject else [])

@@ -31,7 +31,20 @@ EXPORTS = [
     "ksim_emit_cycle_json", "ksim_eval_pod_filter", "ksim_eval_pod_finish",
     "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
     "ksim_match_terms", "ksim_set_eval_range", "ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize",
+    "ksim_fw_filter_nominated", "ksim_preempt_nominated",
 ]
+
+
+def _nominated_groups(groups):
+    """(node, [pod indices]) groups -> the C arrays: the pods of group k are
+    entries [first[k], first[k] + count[k]) of the pod set re-ordered by ``order``."""
+    nodes, first, count, order = [], [], [], []
+    for node, idx in groups:
+        nodes.append(int(node))
+        first.append(len(order))
+        count.append(len(idx))
+        order.extend(int(i) for i in idx)
+    return (np.array(nodes, np.int32), np.array(first, np.int32), np.array(count, np.int32), order)
 
 
 class KsimError(RuntimeError):
@@ -86,11 +99,13 @@ def _load(path):
     L.ksim_eval_pod_filter.argtypes = [vp, vp, i32, vp]
     L.ksim_set_bound_pods.argtypes = [vp, vp]
     L.ksim_preempt.argtypes = [vp, vp, i32, i32, vp]
+    L.ksim_preempt_nominated.argtypes = [vp, vp, i32, i32, vp, i32, vp, vp, vp, vp]
     L.ksim_eval_pod_finish.argtypes = [vp, vp, vp, vp]
     L.ksim_match_terms.argtypes = [vp, vp, vp, vp]
     L.ksim_set_eval_range.argtypes = [vp, i32, i32]
     L.ksim_fw_prefilter.argtypes = [vp, vp, i32, vp]
     L.ksim_fw_score.argtypes = [vp, vp, i32, vp]
+    L.ksim_fw_filter_nominated.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
     L.ksim_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
     L.ksim_assume.argtypes = [vp, vp, i32, i32]
     L.ksim_forget.argtypes = [vp, vp, i32, i32]
@@ -291,6 +306,21 @@ class Engine:
         self._chk(self.L.ksim_fw_prefilter(self.h, ctypes.byref(ps), index, ctypes.byref(buf.out)))
         return buf.result()
 
+    def fw_filter_nominated(self, nominated, groups):
+        """RunFilterPluginsWithNominatedPods' first pass for the cycle in flight:
+        ``groups`` = [(node, [pod indices of ``nominated``]), ...].  Returns
+        (fail_plugin, fail_detail) arrays, one entry per group."""
+        nodes, first, count, order = _nominated_groups(groups)
+        fp = np.zeros(len(nodes), np.uint8)
+        fd = np.zeros(len(nodes), np.uint32)
+        sub = nominated.subset_indices(order)      # kept alive: the pod set points into it
+        ps = sub.pod_set()
+        self._chk(self.L.ksim_fw_filter_nominated(self.h, ctypes.byref(ps), len(nodes),
+                                                  *(a.ctypes.data_as(ctypes.c_void_p) for a in (nodes, first, count)),
+                                                  fp.ctypes.data_as(ctypes.c_void_p),
+                                                  fd.ctypes.data_as(ctypes.c_void_p)))
+        return fp, fd
+
     def fw_score(self, nodes) -> dict:
         """PreScore / Score / NormalizeScore over exactly the framework's feasible list."""
         arr = np.ascontiguousarray(nodes, np.int32)
@@ -316,14 +346,25 @@ class Engine:
         self._bound_n = bound.n
         self._chk(self.L.ksim_set_bound_pods(self.h, ctypes.byref(bound.c)))
 
-    def preempt(self, pods, index: int, priority: int) -> tuple:
+    def preempt(self, pods, index: int, priority: int, groups=None) -> tuple:
         """DefaultPreemption PostFilter dry run: (nominated node or -1, victim
-        indices into the bound-pod table, potential nodes, candidates)."""
+        indices into the bound-pod table, potential nodes, candidates).
+        ``groups`` = [(node, [indices of ``pods``]), ...]: the PodNominator's
+        pods of priority >= ``priority`` per node (ksim_preempt_nominated)."""
         self._sync()
         self._ran = True
         out = abi.PreemptOut(max(getattr(self, "_bound_n", 1), 1))
         ps = pods.pod_set()
-        self._chk(self.L.ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
+        if not groups:
+            self._chk(self.L.ksim_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(out.c)))
+            return out.result()
+        nodes, first, count, order = _nominated_groups(groups)
+        sub = pods.subset_indices(order)      # kept alive: the pod set points into it
+        nps = sub.pod_set()
+        self._chk(self.L.ksim_preempt_nominated(self.h, ctypes.byref(ps), index, priority, ctypes.byref(nps),
+                                                len(nodes), *(a.ctypes.data_as(ctypes.c_void_p)
+                                                              for a in (nodes, first, count)),
+                                                ctypes.byref(out.c)))
         return out.result()
 
     def match_terms(self, mp: abi.MatchProblem, n_words: int, counts: Optional[np.ndarray]) -> np.ndarray:

@@ -30,6 +30,12 @@ compat mode"):
   PostFilter      DefaultPreemption's dry run, ksim_preempt: the nominated node
                   (:518-538, Store.AddPostFilterResult store.go:437-452).
 
+Nominated pods (RunFilterPluginsWithNominatedPods, framework.go v1.26): the
+framework hands Filter a NodeInfo / CycleState clone carrying the node's
+nominated pods of priority >= the pod's (PreFilterExtensions.AddPod); the
+plugins answer that first pass from ksim_fw_filter_nominated, one call per
+cycle over every such node, and the dry run from ksim_preempt_nominated.
+
 One cycle is in flight at a time (upstream scheduleOne is serial); the wrapped
 plugins of a profile share one ``EnginePlugins``.
 """
@@ -95,41 +101,61 @@ class EnginePlugins:
         self._score: Optional[Dict] = None
 
     # ---- PreFilter / Filter ---------------------------------------------------
-    def pre_filter(self, pods, index: int) -> Tuple[Status, Optional[List[str]]]:
+    def pre_filter(self, pods, index: int, nominated: Optional[Dict[int, List[int]]] = None
+                   ) -> Tuple[Status, Optional[List[str]]]:
         """The engine's PreFilter pass; returns NodeAffinity's status and
-        PreFilterResult.NodeNames (None = all nodes)."""
+        PreFilterResult.NodeNames (None = all nodes).  ``nominated``: {node:
+        [indices of ``pods``]}, the nominated pods addNominatedPods would add
+        for this pod (priority >= its own, itself excluded)."""
         self._pods, self._idx = pods, index
         self._score = None
+        self._groups = [(n, list(v)) for n, v in (nominated or {}).items() if v]
+        self._nom: Dict[int, Tuple[int, int]] = {}
         names = pods.prefilter_names[index] if pods.prefilter_names else None
+        rej = pods.rejection(index)
+        if rej is not None:                       # the original VolumeBinding's PreFilter answers
+            self._filter = None
+            return Status(UNSCHEDULABLE_AND_UNRESOLVABLE, rej[1], rej[0]), names
         if names is not None and len(names) == 0:
             self._filter = None
             return Status(UNSCHEDULABLE_AND_UNRESOLVABLE, ERR_NODE_AFFINITY_CONFLICT, "NodeAffinity"), []
         self._filter = self.b.fw_prefilter(pods, index)
         if self._filter["status"] == abi.STATUS_ERROR:
             return Status(ERROR, "node in PreFilterResult not found", "NodeAffinity"), names
+        if self._groups:
+            fp, fd = self.b.fw_filter_nominated(pods, self._groups)
+            self._nom = {n: (int(fp[k]), int(fd[k])) for k, (n, _) in enumerate(self._groups)}
         return Status(), names
 
-    def filter(self, plugin: str, node: int) -> Status:
-        """wrappedPlugin.Filter's original-plugin call for ``plugin`` on ``node``."""
+    def has_nominated(self, node: int) -> bool:
+        """addNominatedPods added pods for ``node`` (the first pass runs)."""
+        return node in self._nom
+
+    def filter(self, plugin: str, node: int, nominated: bool = False) -> Status:
+        """wrappedPlugin.Filter's original-plugin call for ``plugin`` on ``node``
+        (``nominated``: on the clone carrying the node's nominated pods)."""
         k = self.forder.index(plugin)
-        r = int(self._filter["fail_plugin"][node])
+        if nominated:
+            r, d = self._nom[node]
+        else:
+            r = int(self._filter["fail_plugin"][node])
+            d = int(self._filter["fail_detail"][node])
         if r == abi.NOT_EVALUATED:
             raise RuntimeError(f"Filter on node {node} outside the pod's scan set")
         if r == abi.PASSED or r != k:
             if r != abi.PASSED and r < k:
                 raise RuntimeError(f"{plugin} called on node {node} after {self.forder[r]} failed")
             return Status()
-        d = int(self._filter["fail_detail"][node])
         ns, name = self._pods.names[self._idx]
         msg = filter_message(self.cluster, plugin, d, self.cluster.node_names[node], name)
         return Status(filter_code(plugin, d), msg, plugin)
 
-    def run_filter_plugins(self, node: int) -> Tuple[Status, List[Tuple[str, Status]]]:
+    def run_filter_plugins(self, node: int, nominated: bool = False) -> Tuple[Status, List[Tuple[str, Status]]]:
         """framework.RunFilterPlugins: the plugins in order up to the first
         non-success; returns the cycle status and each (plugin, status) run."""
         ran = []
         for pl in self.forder:
-            st = self.filter(pl, node)
+            st = self.filter(pl, node, nominated)
             ran.append((pl, st))
             if not st.is_success():
                 return st, ran
@@ -151,18 +177,40 @@ class EnginePlugins:
 
     # ---- Reserve / Unreserve / PostFilter -------------------------------------
     def reserve(self, node: int) -> Status:
+        """KsimAssume.Reserve: assume the cycle's pod on the framework's node;
+        the pod set and index are kept for Unreserve (the Go adapter keeps an
+        owned copy of the encoding: Unreserve may run after the next cycle)."""
+        self._assumed = (self._pods, self._idx, node)
         self.b.assume(self._pods, self._idx, node)
         return Status()
 
     def unreserve(self, node: int) -> None:
-        self.b.forget(self._pods, self._idx, node)
+        """KsimAssume.Unreserve: forget only what Reserve assumed (a Reserve
+        plugin failing before KsimAssume ran leaves nothing to undo)."""
+        a = getattr(self, "_assumed", None)
+        if a is None:
+            return
+        self._assumed = None
+        self.b.forget(a[0], a[1], a[2])
 
-    def post_filter(self, priority: int, bound=None) -> Tuple[Status, int]:
-        """DefaultPreemption.PostFilter: (status, nominated node or -1)."""
+    def post_filter(self, priority: int, bound=None, nominated_node: int = -1, nominated_status=None,
+                    terminating_lower=None) -> Tuple[Status, int, List[int], bool]:
+        """DefaultPreemption.PostFilter (default_preemption.go v1.26):
+        PodEligibleToPreemptOthers, then the dry run over this cycle's
+        nominated groups.  Returns (status, nominated node or -1, victim
+        indices of the bound-pod table, override): override False is a nil
+        result (ModeNoop, the pod keeps its nomination), True with node -1 is
+        NominatedNodeName "" (ModeOverride clears it).  ``terminating_lower(node,
+        priority)``: a Terminating pod of lower priority is on the node."""
+        if nominated_node >= 0 and (nominated_status is None or
+                                    nominated_status.code != UNSCHEDULABLE_AND_UNRESOLVABLE):
+            if terminating_lower is not None and terminating_lower(nominated_node, priority):
+                return (Status(UNSCHEDULABLE, "preemption: not eligible due to a terminating pod on the "
+                                              "nominated node."), -1, [], False)
         if bound is None:
-            node, _victims = self.b.preempt(self._pods, self._idx, priority)[:2]
+            node, victims = self.b.preempt(self._pods, self._idx, priority, groups=self._groups)[:2]
         else:
-            node, _victims = self.b.preempt(self._pods, self._idx, priority, bound)[:2]
+            node, victims = self.b.preempt(self._pods, self._idx, priority, bound, groups=self._groups)[:2]
         if node < 0:
-            return Status(UNSCHEDULABLE, "preemption: 0/... nodes are available"), -1
-        return Status(), int(node)
+            return Status(UNSCHEDULABLE, "preemption: no candidate node"), -1, [], True
+        return Status(), int(node), list(victims), True

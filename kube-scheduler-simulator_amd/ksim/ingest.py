@@ -322,7 +322,7 @@ def schedule_queue(backend, cluster, pending: Sequence[Pod], volumes: Optional[V
             r = backend.eval_pod(enc, 0) if hasattr(backend, "eval_pod") else backend.cycle(enc, 0)
             node = cluster.node_names[r["chosen"]] if r["chosen"] >= 0 else None
             if node is not None:
-                volumes.assume(pod, labels[node])
+                volumes.assume(pod, labels[node], node)   # False: waiting in PreBind for a provisioner
             out.append(node)
             j += 1
         i = j

@@ -281,6 +281,7 @@ class PersistentVolumeClaim:
     request: int = 0                                         # spec.resources.requests.storage (bytes)
     selector: Optional[LabelSelector] = None                 # spec.selector
     volume_mode: str = "Filesystem"                          # spec.volumeMode (nil: Filesystem)
+    selected_node: str = ""                                  # annotation volume.kubernetes.io/selected-node
 
 
 @dataclass
@@ -331,7 +332,9 @@ def pvc_from_dict(d: dict) -> PersistentVolumeClaim:
                                  storage_class=spec.get("storageClassName"),
                                  request=quantity_value(req) if req is not None else 0,
                                  selector=_selector(spec.get("selector")),
-                                 volume_mode=spec.get("volumeMode") or "Filesystem")
+                                 volume_mode=spec.get("volumeMode") or "Filesystem",
+                                 selected_node=(md.get("annotations") or {}).get("volume.kubernetes.io/selected-node",
+                                                                                 "") or "")
 
 
 def storage_class_from_dict(d: dict) -> StorageClass:

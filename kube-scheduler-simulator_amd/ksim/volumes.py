@@ -27,27 +27,47 @@ Every per-node verdict is a set of groups of NodeSelectorTerms (ksim_engine.h
                  whose value parses (LabelZonesToSet): {key In zones} or {no
                  topology label on the node}; unbound WaitForFirstConsumer
                  claims are skipped.
-  PreFilter rejections (a missing claim or class, an unbound Immediate claim,
-  a ReadWriteOncePod claim another pod uses): one group that no node matches.
+  A claim whose provisioning already started (annotation
+  volume.kubernetes.io/selected-node) admits that node only, if its class can
+  provision there.
+The bound-PV groups come first; the unbound-claim groups carry
+abi.VB_UNBOUND_GROUP in their group index, so the engine's failure detail says
+which reasons the node gets (ErrReasonNodeConflict, ErrReasonBindConflict, or
+both, in FindPodVolumes' order).
+
+PreFilter rejections (VolumeBinding PreFilter, UnschedulableAndUnresolvable: a
+missing claim, an unbound Immediate claim -- a claim whose class does not
+exist is Immediate, IsDelayBindingMode treats NotFound as not delayed):
+``prefilter_rejection`` gives the message the hosts record as VolumeBinding's
+PreFilter status (no Filter runs, nextStartNodeIndex unchanged); the engine
+gets one group no node matches, which leaves nextStartNodeIndex where it was
+(every node is processed) and the pod unschedulable.
 
 The verdicts depend on which PVs earlier pods took, so a pod with unbound
-WaitForFirstConsumer or ReadWriteOncePod claims is encoded at its turn
-(``stateful``; ksim.ingest.schedule_snapshot) and ``assume`` records its
-bindings (AssumePodVolumes) once the cycle chose a node.  Dynamic provisioning
-is taken as the provisioner doing its job (the PVC is bound to a new PV of the
-claim's size, without node affinity: the provisioner's topology is not
-modelled); the simulator itself runs no provisioner, so there such a pod would
-wait in PreBind.
+WaitForFirstConsumer claims is encoded at its turn (``stateful``;
+ksim.ingest.schedule_queue) and ``assume`` records its bindings
+(AssumePodVolumes) once the cycle chose a node.  Dynamic provisioning: the
+simulator's PV controller runs without provisioning plugins
+(/root/reference/simulator/controller/pvcontroller.go, VolumeConfig{}) and no
+external provisioner runs, so a pod whose claims need provisioning is assumed
+on the node, its claims get the selected-node annotation, and it waits in
+PreBind (``waiting``; it never binds: its bindTimeoutSeconds run out after the
+simulation).  ``provisioning=True`` models a working provisioner instead (the
+PVC is bound to a new PV of the claim's size, without node affinity).
 
 Still unsupported (VolumeUnsupported: the pod is reported and not scheduled,
 never mis-scheduled): PVs counted against node volume limits (EBS / GCE PD /
 Azure disk / Cinder by their in-tree limit plugins; CSI volumes by
-NodeVolumeLimits when a node publishes attachable-volumes-* limits).
+NodeVolumeLimits when a node publishes attachable-volumes-* limits);
+ReadWriteOncePod claims (the ReadWriteOncePod feature gate is alpha and off in
+v1.26: the API server refuses the access mode and VolumeRestrictions skips
+the check; the reference sets no feature gates).
 """
 from __future__ import annotations
 
 from typing import Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
+from . import abi
 from .model import (NodeSelectorTerm, PersistentVolume, PersistentVolumeClaim, Pod, Requirement, StorageClass,
                     selector_matches)
 
@@ -60,7 +80,6 @@ MSG_VOLUME_BINDING = "node(s) had volume node affinity conflict"    # volumebind
 MSG_BIND_CONFLICT = "node(s) didn't find available persistent volumes to bind"   # ErrReasonBindConflict
 MSG_VOLUME_ZONE = "node(s) had no available volume zone"            # volumezone ErrReasonConflict
 MSG_UNBOUND_IMMEDIATE = "pod has unbound immediate PersistentVolumeClaims"
-MSG_RWOP = "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"
 
 _NEVER = NodeSelectorTerm([], [Requirement("", "__false__", [])])   # a term no node matches
 _ALWAYS = NodeSelectorTerm([], [Requirement("", "__true__", [])])
@@ -122,6 +141,22 @@ def pv_node_affinity_ok(pv: PersistentVolume, labels: Dict[str, str]) -> bool:
     return False
 
 
+def binding_message(detail: int) -> str:
+    """VolumeBinding Filter's Status.Message(): its reasons joined (FindPodVolumes order)."""
+    out = []
+    if detail & abi.VB_NODE_CONFLICT or not detail:
+        out.append(MSG_VOLUME_BINDING)
+    if detail & abi.VB_BIND_CONFLICT:
+        out.append(MSG_BIND_CONFLICT)
+    return ", ".join(out)
+
+
+def can_provision(sc: Optional[StorageClass]) -> bool:
+    """checkVolumeProvisions: a class with no provisioner ("" or
+    kubernetes.io/no-provisioner) cannot provision."""
+    return sc is not None and sc.provisioner not in ("", NO_PROVISIONER)
+
+
 def topology_ok(sc: StorageClass, labels: Dict[str, str]) -> bool:
     """v1helper.MatchTopologySelectorTerms over allowedTopologies."""
     if not sc.allowed_topologies:
@@ -139,7 +174,7 @@ class VolumeIndex:
     pvcs / storageClasses) and the bindings the run has made so far."""
 
     def __init__(self, pvs: Iterable[PersistentVolume] = (), pvcs: Iterable[PersistentVolumeClaim] = (),
-                 csi_limits: bool = False, classes: Iterable[StorageClass] = ()):
+                 csi_limits: bool = False, classes: Iterable[StorageClass] = (), provisioning: bool = False):
         self.pvs: Dict[str, PersistentVolume] = {pv.name: pv for pv in pvs}
         self.pvcs: Dict[Tuple[str, str], PersistentVolumeClaim] = {(c.namespace, c.name): c for c in pvcs}
         self.classes: Dict[str, StorageClass] = {c.name: c for c in classes}
@@ -147,11 +182,13 @@ class VolumeIndex:
         self.users: Dict[Tuple[str, str], int] = {}   # claim -> pods on nodes using it (RWOP)
         self.provisioned = 0
         self.nodes: Optional[list] = None     # the cluster's nodes (the exact group of competing claims)
+        self.provisioning = provisioning      # a provisioner acts on selected-node claims (none in the simulator)
+        self.waiting: Dict[Tuple[str, str], str] = {}   # pods waiting in PreBind for provisioning -> node
 
     @staticmethod
-    def from_nodes(nodes, pvs=(), pvcs=(), classes=()) -> "VolumeIndex":
+    def from_nodes(nodes, pvs=(), pvcs=(), classes=(), provisioning: bool = False) -> "VolumeIndex":
         lim = any(k.startswith("attachable-volumes-") for n in nodes for k in n.allocatable)
-        v = VolumeIndex(pvs, pvcs, lim, classes)
+        v = VolumeIndex(pvs, pvcs, lim, classes, provisioning)
         v.nodes = list(nodes)
         return v
 
@@ -160,11 +197,10 @@ class VolumeIndex:
         return pvc.storage_class or ""
 
     def delay_binding(self, pvc: PersistentVolumeClaim) -> bool:
-        """IsDelayBindingMode (class "" or Immediate: False); a missing class raises KeyError."""
-        name = self._class_of(pvc)
-        if not name:
-            return False
-        return self.classes[name].volume_binding_mode == "WaitForFirstConsumer"
+        """IsDelayBindingMode: class "", a class that does not exist (NotFound is
+        not an error there) or Immediate: False."""
+        sc = self.classes.get(self._class_of(pvc))
+        return sc is not None and sc.volume_binding_mode == "WaitForFirstConsumer"
 
     def candidates(self, pvc: PersistentVolumeClaim, exclude: Set[str] = frozenset()) -> List[PersistentVolume]:
         """The PVs FindMatchingVolume may pick for pvc, node affinity not
@@ -206,9 +242,9 @@ class VolumeIndex:
 
     def run_pv_controller(self) -> int:
         """The PV controller's sync of every unbound Immediate claim (class ""
-        or volumeBindingMode Immediate): bind it to the smallest matching
-        available PV (findBestMatchForClaim, no node); claims pre-bound by a PV's
-        claimRef first.  Claims of a missing class or with no match stay
+        or volumeBindingMode Immediate, or a class that does not exist): bind it
+        to the smallest matching available PV (findBestMatchForClaim, no node);
+        claims pre-bound by a PV's claimRef first.  Claims with no match stay
         unbound.  Returns the number of bindings."""
         n = 0
         for pvc in self.pvcs.values():            # a claim naming its PV: the PV is bound to it
@@ -216,12 +252,7 @@ class VolumeIndex:
             if pv is not None and pv.claim_ref is None:
                 pv.claim_ref = (pvc.namespace, pvc.name)
         for pvc in self.pvcs.values():
-            if pvc.volume_name:
-                continue
-            try:
-                if self.delay_binding(pvc):
-                    continue
-            except KeyError:
+            if pvc.volume_name or self.delay_binding(pvc):
                 continue
             # the controller's volume index holds only PVs with the claim's access modes
             c = [pv for pv in self.candidates(pvc) if set(pvc.access_modes) <= set(pv.access_modes)]
@@ -246,8 +277,8 @@ class VolumeIndex:
             pvc = self.pvcs.get((pod.namespace, claim))
             if pvc is None:
                 return f'persistentvolumeclaim "{claim}" not found'
-            if "ReadWriteOncePod" in pvc.access_modes and self.users.get((pod.namespace, claim), 0) > 0:
-                return MSG_RWOP
+            if "ReadWriteOncePod" in pvc.access_modes:
+                raise VolumeUnsupported("ReadWriteOncePod: feature gate off in v1.26")
             if pvc.volume_name:
                 pv = self.pvs.get(pvc.volume_name)
                 if pv is None:
@@ -257,36 +288,32 @@ class VolumeIndex:
                                             f"node limits")
                 bound.append(pv)
                 continue
-            try:
-                delayed = self.delay_binding(pvc)
-            except KeyError:
-                return f'storageclass.storage.k8s.io "{self._class_of(pvc)}" not found'
-            if not delayed:
+            if not self.delay_binding(pvc):
                 return MSG_UNBOUND_IMMEDIATE
             delay.append(pvc)
         return bound, delay
+
+    def prefilter_rejection(self, pod: Pod) -> Optional[str]:
+        """VolumeBinding PreFilter's UnschedulableAndUnresolvable message, or None."""
+        if not pod.pvc_claims:
+            return None
+        got = self._claims(pod)
+        return got if isinstance(got, str) else None
 
     def stateful(self, pod: Pod) -> bool:
         """The pod's verdicts depend on the bindings earlier pods make."""
         for claim in pod.pvc_claims:
             pvc = self.pvcs.get((pod.namespace, claim))
-            if pvc is None:
-                continue
-            if "ReadWriteOncePod" in pvc.access_modes:
+            if pvc is not None and not pvc.volume_name and self.delay_binding(pvc):
                 return True
-            if not pvc.volume_name:
-                try:
-                    if self.delay_binding(pvc):
-                        return True
-                except KeyError:
-                    pass
         return False
 
     def _delay_sorted(self, delay: List[PersistentVolumeClaim]) -> List[PersistentVolumeClaim]:
         return sorted(delay, key=lambda c: c.request)     # byPVCSize (stable here)
 
-    def match_on_node(self, pod: Pod, labels: Dict[str, str]):
-        """FindPodVolumes for the unbound delay-binding claims on one node:
+    def match_on_node(self, pod: Pod, labels: Dict[str, str], name: Optional[str] = None):
+        """FindPodVolumes for the unbound delay-binding claims on one node
+        (``name``: the node's name, for claims with a selected node):
         ([(pvc, pv)] static bindings, [pvc] to provision) or None (the node
         fails: no PV and no provisioning)."""
         got = self._claims(pod)
@@ -295,7 +322,12 @@ class VolumeIndex:
         _, delay = got
         chosen: Set[str] = set()
         static, provision = [], []
-        for pvc in self._delay_sorted(delay):
+        for pvc in delay:                                 # AnnSelectedNode: that node only, to provision
+            if pvc.selected_node:
+                if name is not None and pvc.selected_node != name:
+                    return None
+                provision.append(pvc)
+        for pvc in self._delay_sorted([c for c in delay if not c.selected_node]):
             pv = self._pick(pvc, labels, chosen)
             if pv is not None:
                 chosen.add(pv.name)
@@ -303,19 +335,20 @@ class VolumeIndex:
             else:
                 provision.append(pvc)
         for pvc in provision:                             # checkVolumeProvisions
-            sc = self.classes[self._class_of(pvc)]
-            if sc.provisioner == NO_PROVISIONER or not topology_ok(sc, labels):
+            sc = self.classes.get(self._class_of(pvc))
+            if not can_provision(sc) or not topology_ok(sc, labels):
                 return None
         return static, provision
 
     def groups(self, pod: Pod, nodes: Optional[Sequence] = None) -> Tuple[List[List[NodeSelectorTerm]],
-                                                                           List[List[NodeSelectorTerm]]]:
-        """(VolumeBinding groups, VolumeZone groups) of the pod under the
-        current bindings.  ``nodes`` (objects with name / labels): needed only
-        for the exact group of competing claims."""
+                                                                           List[List[NodeSelectorTerm]], int]:
+        """(VolumeBinding groups, VolumeZone groups, how many of the VolumeBinding
+        groups are bound-PV groups -- the rest are unbound-claim groups) of the
+        pod under the current bindings.  ``nodes`` (objects with name /
+        labels): needed only for the exact group of competing claims."""
         got = self._claims(pod)
         if isinstance(got, str):
-            return [[_NEVER]], []                         # a PreFilter rejection: no node passes
+            return [[_NEVER]], [], 1                      # a PreFilter rejection: no node passes
         bound, delay = got
         vb: List[List[NodeSelectorTerm]] = []
         vz: List[List[NodeSelectorTerm]] = []
@@ -330,6 +363,15 @@ class VolumeIndex:
                 if zones is None:
                     continue                            # getPVbyPod skips a label it cannot parse
                 vz.append([NodeSelectorTerm([Requirement(k, "In", zones)], []), absent])
+        n_bound = len(vb)
+        for pvc in [c for c in delay if c.selected_node]:  # provisioning started on one node
+            sc = self.classes.get(self._class_of(pvc))
+            known = nodes if nodes is not None else self.nodes
+            ok = can_provision(sc) and (known is None or any(
+                n.name == pvc.selected_node and topology_ok(sc, n.labels) for n in known))
+            vb.append([NodeSelectorTerm([], [Requirement("metadata.name", "In", [pvc.selected_node])])] if ok
+                      else [_NEVER])
+        delay = [c for c in delay if not c.selected_node]
         if delay:
             cands = [self.candidates(pvc) for pvc in delay]
             names = [{pv.name for pv in c} for c in cands]
@@ -338,7 +380,7 @@ class VolumeIndex:
                 nodes = nodes if nodes is not None else self.nodes
                 if nodes is None:
                     raise VolumeUnsupported("claims competing for one PV need the node list")
-                ok = [n.name for n in nodes if self.match_on_node(pod, n.labels) is not None]
+                ok = [n.name for n in nodes if self.match_on_node(pod, n.labels, n.name) is not None]
                 vb.append([NodeSelectorTerm([], [Requirement("metadata.name", "In", [nm])]) for nm in ok] or [_NEVER])
             else:
                 for pvc, cs in zip(delay, cands):
@@ -350,7 +392,7 @@ class VolumeIndex:
                             break
                         group.extend(_labels_only_term(t) for t in pv.node_affinity)
                     sc = self.classes[self._class_of(pvc)]
-                    if not always and sc.provisioner != NO_PROVISIONER:
+                    if not always and can_provision(sc):
                         if not sc.allowed_topologies:
                             always = True
                         else:
@@ -359,26 +401,35 @@ class VolumeIndex:
                                     group.append(NodeSelectorTerm([Requirement(k, "In", list(v)) for k, v in term], []))
                     if not always:
                         vb.append(group or [_NEVER])
-        return vb, vz
+        return vb, vz, n_bound
 
-    def assume(self, pod: Pod, labels: Dict[str, str]) -> None:
-        """AssumePodVolumes on the chosen node (then PreBind): static matches
-        bind their PV; claims to provision get a new PV of their size on the
-        node's topology; the pod's claims count as in use."""
-        m = self.match_on_node(pod, labels)
+    def assume(self, pod: Pod, labels: Dict[str, str], name: Optional[str] = None) -> bool:
+        """AssumePodVolumes on the chosen node ``name`` (then PreBind): static
+        matches bind their PV.  Claims to provision get the selected-node
+        annotation and the pod waits in PreBind (``waiting``; returns False:
+        not bound) -- or, with ``provisioning``, a new PV of their size.  The
+        pod's claims count as in use."""
+        m = self.match_on_node(pod, labels, name)
+        bound = True
         if m is not None:
             static, provision = m
             for pvc, pv in static:
                 self.bind(pvc, pv)
             for pvc in provision:
+                if not self.provisioning:
+                    pvc.selected_node = name or pvc.selected_node
+                    self.waiting[(pod.namespace, pod.name)] = name or ""
+                    bound = False
+                    continue
                 self.provisioned += 1
-                name = f"pvc-provisioned-{self.provisioned}"
+                pv_name = f"pvc-provisioned-{self.provisioned}"
                 # the provisioner's topology is unknown here: the new PV carries no node affinity
-                pv = PersistentVolume(name=name, capacity=pvc.request, storage_class=self._class_of(pvc),
+                pv = PersistentVolume(name=pv_name, capacity=pvc.request, storage_class=self._class_of(pvc),
                                       access_modes=list(pvc.access_modes), volume_mode=pvc.volume_mode)
-                self.pvs[name] = pv
+                self.pvs[pv_name] = pv
                 self.bind(pvc, pv)
         self.add_users([pod])
+        return bound
 
 
 def _labels_only_term(t: NodeSelectorTerm) -> NodeSelectorTerm:

@@ -17,7 +17,7 @@ Keys are the ORIGINAL plugin names (wrappedplugin.go:374,406,447,479,510).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from . import abi
 from .encode import EncodedCluster
@@ -77,8 +77,8 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
     if plugin == "InterPodAffinity":
         return ERR_IPA[detail]
     if plugin == "VolumeBinding":
-        from .volumes import MSG_VOLUME_BINDING
-        return MSG_VOLUME_BINDING
+        from .volumes import binding_message
+        return binding_message(detail)
     if plugin == "VolumeZone":
         from .volumes import MSG_VOLUME_ZONE
         return MSG_VOLUME_ZONE
@@ -86,26 +86,35 @@ def filter_message(cluster: EncodedCluster, plugin: str, detail: int, node: str 
 
 
 def record_cycle(store: Store, cluster: EncodedCluster, prof: SchedulerProfile, ns: str, name: str,
-                 res: Dict, prefilter_names: Optional[List[str]] = None, nominated: int = -1) -> None:
+                 res: Dict, prefilter_names: Optional[List[str]] = None, nominated: int = -1,
+                 rejection: Optional[Tuple[str, str]] = None) -> None:
     """Feed ``store`` with one compat-mode cycle result (engine or oracle).
     ``prefilter_names``: the pod's NodeAffinity PreFilterResult.NodeNames
     (EncodedPods.prefilter_names; None = all nodes, [] = conflicting terms).
     ``nominated``: DefaultPreemption's nominated node of an unschedulable cycle
     (ksim_preempt; -1 none), which wrappedPlugin.PostFilter records as
-    "preemption victim" (wrappedplugin.go:529-538, store.go:437-452)."""
+    "preemption victim" (wrappedplugin.go:529-538, store.go:437-452).
+    ``rejection``: (plugin, message) of a PreFilter that rejects the pod
+    (EncodedPods.rejection: VolumeBinding's UnschedulableAndUnresolvable)."""
     names = cluster.node_names
     conflict = prefilter_names is not None and len(prefilter_names) == 0
+    stopped = False
     for p in prof.plugins["preFilter"].enabled:
         plugin = original_name(p.name)
+        if rejection is not None and plugin == rejection[0]:
+            store.add_pre_filter_result(ns, name, plugin, rejection[1], None)
+            stopped = True
+            break                              # RunPreFilterPlugins stops at a failing plugin
         if plugin == "NodeAffinity" and prefilter_names is not None:
             # wrappedPlugin.PreFilter records the status and result.NodeNames.List()
             store.add_pre_filter_result(ns, name, plugin, ERR_NODE_AFFINITY_CONFLICT if conflict else SUCCESS_MESSAGE,
                                         None if conflict else list(prefilter_names))
             if conflict:
-                break                          # RunPreFilterPlugins stops at a failing plugin
+                stopped = True
+                break
         else:
             store.add_pre_filter_result(ns, name, plugin, SUCCESS_MESSAGE, None)
-    if conflict:
+    if stopped:
         # findNodesThatFitPod: every node gets the PreFilter status; no Filter runs
         for p in prof.plugins["postFilter"].enabled:
             store.add_post_filter_result(ns, name, "", original_name(p.name), list(names))
@@ -175,7 +184,7 @@ def compat_cycle(backend, store: Store, cluster: EncodedCluster, prof: Scheduler
     res = backend.eval_pod(pods, index) if hasattr(backend, "eval_pod") else backend.cycle(pods, index)
     nominated = -1
     post = [original_name(p.name) for p in prof.plugins["postFilter"].enabled]
-    if res["status"] == abi.STATUS_UNSCHEDULABLE and "DefaultPreemption" in post:
+    if res["status"] == abi.STATUS_UNSCHEDULABLE and "DefaultPreemption" in post and pods.rejection(index) is None:
         names = pods.prefilter_names[index] if pods.prefilter_names else None
         if not (names is not None and len(names) == 0):
             out = backend.preempt(pods, index, priority) if bound is None else \
@@ -184,7 +193,7 @@ def compat_cycle(backend, store: Store, cluster: EncodedCluster, prof: Scheduler
     res["nominated"] = nominated
     ns, name = pods.names[index]
     record_cycle(store, cluster, prof, ns, name, res,
-                 pods.prefilter_names[index] if pods.prefilter_names else None, nominated)
+                 pods.prefilter_names[index] if pods.prefilter_names else None, nominated, pods.rejection(index))
     return res
 
 

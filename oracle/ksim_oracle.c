@@ -344,6 +344,23 @@ static int volume_groups_match(const ksim_oracle* o, const ksim_pod_set* ps, int
   return ok;
 }
 
+/* VolumeBinding: KSIM_VB_NODE_CONFLICT if a bound-PV group fails,
+ * KSIM_VB_BIND_CONFLICT if an unbound-claim group (group index with
+ * KSIM_VB_UNBOUND_GROUP) fails -- FindPodVolumes' reasons; 0 = pass. */
+static uint32_t volume_binding_fails(const ksim_oracle* o, const ksim_pod_set* ps, int32_t first, int32_t count,
+                                     int32_t node) {
+  uint32_t why = 0;
+  int32_t i = 0;
+  while (i < count) {
+    const int32_t g = ps->terms[first + i].weight;
+    int ok = 0;
+    for (; i < count && ps->terms[first + i].weight == g; i++)
+      if (!ok && term_matches(o, ps, &ps->terms[first + i], node)) ok = 1;
+    if (!ok) why |= (g & KSIM_VB_UNBOUND_GROUP) ? KSIM_VB_BIND_CONFLICT : KSIM_VB_NODE_CONFLICT;
+  }
+  return why;
+}
+
 /* RequiredNodeAffinity.Match: nodeSelector (labels.SelectorFromSet) AND
  * (OR of required terms) — [upstream] nodeaffinity.Filter, §8(a) a26 */
 static int required_node_affinity_match(const ksim_oracle* o, const ksim_pod_set* ps,
@@ -911,9 +928,11 @@ static uint8_t run_filter_plugins(const ksim_oracle* o, const ksim_pod_set* ps, 
         if (!node_affinity_filter(o, ps, p, node, &why)) { *detail = why; return (uint8_t)f; }
         break;
       }
-      case KSIM_PL_VOLUME_BINDING:       /* bound claims: PV node affinity */
-        if (!volume_groups_match(o, ps, p->vb_first, p->vb_count, node)) return (uint8_t)f;
+      case KSIM_PL_VOLUME_BINDING: {     /* bound claims' PV node affinity, unbound claims' matches */
+        uint32_t r = volume_binding_fails(o, ps, p->vb_first, p->vb_count, node);
+        if (r) { *detail = r; return (uint8_t)f; }
         break;
+      }
       case KSIM_PL_VOLUME_ZONE:          /* bound claims: PV topology labels */
         if (!volume_groups_match(o, ps, p->vz_first, p->vz_count, node)) return (uint8_t)f;
         break;
@@ -1214,6 +1233,36 @@ int ksim_oracle_fw_filter(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, ks
   return KSIM_OK;
 }
 
+/* RunFilterPluginsWithNominatedPods' first pass (addNominatedPods): for each
+ * group, the nominated pods added to the node (NodeInfo.AddPodInfo; the
+ * PreFilterExtensions' AddPod of PodTopologySpread / InterPodAffinity, which
+ * for +1 updates equal the PreFilter state over the snapshot with them bound),
+ * the node's Filter, the pods removed again; the cycle's PreFilter state is
+ * recomputed at the end. */
+int ksim_oracle_fw_filter_nominated(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, const ksim_pod_set* nps,
+                                    int32_t n_nodes, const int32_t* nodes, const int32_t* first, const int32_t* count,
+                                    uint8_t* fail_plugin, uint32_t* fail_detail) {
+  if (!o || !o->fw_active || !ps || pi < 0 || pi >= ps->n_pods || n_nodes < 0) return KSIM_E_INVALID;
+  if (n_nodes == 0) return KSIM_OK;
+  if (!nps || !nodes || !first || !count || !fail_plugin) return KSIM_E_INVALID;
+  const ksim_pod* p = &ps->pods[pi];
+  for (int32_t k = 0; k < n_nodes; k++) {
+    if (nodes[k] < 0 || nodes[k] >= o->n || first[k] < 0 || count[k] < 0 || first[k] + count[k] > nps->n_pods)
+      return KSIM_E_INVALID;
+  }
+  topo_ctx tc;
+  for (int32_t k = 0; k < n_nodes; k++) {
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) assume_pod(o, nps, &nps->pods[j], nodes[k], 1);
+    topo_prefilter(o, ps, p, &tc);
+    uint32_t det;
+    fail_plugin[k] = run_filter_plugins(o, ps, p, &tc, nodes[k], &det);
+    if (fail_detail) fail_detail[k] = det;
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) assume_pod(o, nps, &nps->pods[j], nodes[k], -1);
+  }
+  topo_prefilter(o, ps, p, o->fw_tc);            /* the cycle's own PreFilter state */
+  return KSIM_OK;
+}
+
 /* PreScore + Score + NormalizeScore + weights over exactly `nodes` (the
  * framework's feasible list, any order).  No selectHost, no bind. */
 int ksim_oracle_fw_score(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, const int32_t* nodes, int32_t n,
@@ -1457,7 +1506,7 @@ static int fits_adjusted(const ksim_oracle* o, const ksim_pod* p, int32_t node, 
 
 /* SelectVictimsOnNode: 1 + victims written to vout (importance order), or 0 */
 static int32_t select_victims(const ksim_oracle* o, const ksim_pod* p, int32_t prio, const ksim_bound_pods* b,
-                              int32_t node, victim_rec* buf, int32_t* vout) {
+                              int32_t node, const int64_t* nom, victim_rec* buf, int32_t* vout) {
   int32_t m = 0;
   for (int32_t i = 0; i < b->n; i++)
     if (b->node[i] == node && b->priority[i] < prio) {
@@ -1467,10 +1516,11 @@ static int32_t select_victims(const ksim_oracle* o, const ksim_pod* p, int32_t p
       m++;
     }
   qsort(buf, (size_t)m, sizeof(victim_rec), victim_cmp);
-  int64_t delta[KSIM_PREEMPT_REQ] = {0};
+  int64_t delta[KSIM_PREEMPT_REQ];
+  for (int k = 0; k < KSIM_PREEMPT_REQ; k++) delta[k] = nom[k];
   for (int32_t j = 0; j < m; j++)
     for (int k = 0; k < KSIM_PREEMPT_REQ; k++) delta[k] -= b->req[(size_t)buf[j].idx * KSIM_PREEMPT_REQ + k];
-  int64_t dpods = -m;
+  int64_t dpods = nom[KSIM_PREEMPT_REQ] - m;
   if (!fits_adjusted(o, p, node, delta, dpods)) return 0;
   int32_t nv = 0;
   for (int32_t j = 0; j < m; j++) {                      /* reprievePod, most important first */
@@ -1488,7 +1538,22 @@ static int32_t select_victims(const ksim_oracle* o, const ksim_pod* p, int32_t p
 
 int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32_t prio, const ksim_bound_pods* b,
                         ksim_preempt_out* out) {
-  if (!o || !ps || !b || !out || pi < 0 || pi >= ps->n_pods) return KSIM_E_INVALID;
+  return ksim_oracle_preempt_nominated(o, ps, pi, prio, b, NULL, 0, NULL, NULL, NULL, out);
+}
+
+/* With the PodNominator's pods (ksim_engine.h ksim_preempt_nominated): a
+ * grouped node's status is RunFilterPluginsWithNominatedPods' (pass 1 with the
+ * group's pods assumed; pass 2 as is only when pass 1 passed), and
+ * SelectVictimsOnNode keeps the group's requests on the node. */
+int ksim_oracle_preempt_nominated(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32_t prio,
+                                  const ksim_bound_pods* b, const ksim_pod_set* nps, int32_t n_groups,
+                                  const int32_t* gnodes, const int32_t* first, const int32_t* count,
+                                  ksim_preempt_out* out) {
+  if (!o || !ps || !b || !out || pi < 0 || pi >= ps->n_pods || n_groups < 0) return KSIM_E_INVALID;
+  if (n_groups > 0 && (!nps || !gnodes || !first || !count)) return KSIM_E_INVALID;
+  for (int32_t k = 0; k < n_groups; k++)
+    if (gnodes[k] < 0 || gnodes[k] >= o->n || first[k] < 0 || count[k] < 0 || first[k] + count[k] > nps->n_pods)
+      return KSIM_E_INVALID;
   const ksim_pod* p = &ps->pods[pi];
   if (p->use_count > 0) return KSIM_E_UNSUPPORTED;
   const int32_t N = o->n;
@@ -1497,13 +1562,26 @@ int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int3
     if (o->prof.filter[f] == KSIM_PL_NETWORK_BANDWIDTH) return KSIM_E_UNSUPPORTED;
   for (int f = 0; f < o->prof.n_filter; f++)
     if (o->prof.filter[f] == KSIM_PL_NODE_RESOURCES_FIT) fit = f;
+  int32_t* group = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
+  uint8_t* gfail = (uint8_t*)malloc((size_t)(n_groups > 0 ? n_groups : 1));
+  for (int32_t node = 0; node < N; node++) group[node] = -1;
   topo_ctx tc;
+  for (int32_t k = 0; k < n_groups; k++) {               /* pass 1 of each grouped node */
+    group[gnodes[k]] = k;
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) assume_pod(o, nps, &nps->pods[j], gnodes[k], 1);
+    topo_prefilter(o, ps, p, &tc);
+    uint32_t det;
+    gfail[k] = run_filter_plugins(o, ps, p, &tc, gnodes[k], &det);
+    for (int32_t j = first[k]; j < first[k] + count[k]; j++) assume_pod(o, nps, &nps->pods[j], gnodes[k], -1);
+  }
   topo_prefilter(o, ps, p, &tc);
   int32_t* potential = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N > 0 ? N : 1));
   int32_t np = 0;
   for (int32_t node = 0; node < N; node++) {            /* nodesWherePreemptionMightHelp */
     uint32_t det;
-    if (fit >= 0 && run_filter_plugins(o, ps, p, &tc, node, &det) == (uint8_t)fit) potential[np++] = node;
+    uint8_t f = run_filter_plugins(o, ps, p, &tc, node, &det);
+    if (group[node] >= 0 && gfail[group[node]] != KSIM_PASSED) f = gfail[group[node]];
+    if (fit >= 0 && f == (uint8_t)fit) potential[np++] = node;
   }
   int32_t want = np * o->prof.preempt_min_pct / 100;    /* GetOffsetAndNumCandidates / calculateNumCandidates */
   if (want < o->prof.preempt_min_abs) want = o->prof.preempt_min_abs;
@@ -1516,7 +1594,19 @@ int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int3
   int64_t best_sum = 0, best_start = 0;
   for (int32_t i = 0; i < np && ncand < want; i++) {
     const int32_t node = potential[i];
-    const int32_t r = select_victims(o, p, prio, b, node, buf, vic);
+    int64_t nom[KSIM_PREEMPT_REQ + 1] = {0};            /* the group's requests and pod count */
+    if (group[node] >= 0) {
+      const int32_t k = group[node];
+      for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
+        const ksim_pod* q = &nps->pods[j];
+        nom[0] += q->req_cpu;
+        nom[1] += q->req_mem;
+        nom[2] += q->req_eph;
+        for (int s2 = 0; s2 < KSIM_MAX_SCALAR; s2++) nom[3 + s2] += q->scalar_req[s2];
+      }
+      nom[KSIM_PREEMPT_REQ] = count[k];
+    }
+    const int32_t r = select_victims(o, p, prio, b, node, nom, buf, vic);
     if (r == 0) continue;
     ncand++;
     const int32_t nv = r - 1;
@@ -1544,6 +1634,6 @@ int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int3
   out->n_candidates = ncand;
   if (out->victims)
     for (int32_t j = 0; j < out->n_victims && j < out->victims_cap; j++) out->victims[j] = best_v[j];
-  free(potential); free(buf); free(vic); free(best_v);
+  free(potential); free(buf); free(vic); free(best_v); free(group); free(gfail);
   return KSIM_OK;
 }

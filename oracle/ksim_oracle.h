@@ -38,6 +38,11 @@ int ksim_oracle_cycle(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_inde
                       ksim_eval_out* out);
 int ksim_oracle_preempt(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, int32_t priority,
                         const ksim_bound_pods* b, ksim_preempt_out* out);
+/* ksim_engine.h ksim_preempt_nominated. */
+int ksim_oracle_preempt_nominated(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32_t prio,
+                                  const ksim_bound_pods* b, const ksim_pod_set* nps, int32_t n_groups,
+                                  const int32_t* nodes, const int32_t* first, const int32_t* count,
+                                  ksim_preempt_out* out);
 int ksim_oracle_cycle_ext(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, const uint8_t* ext_fail,
                           const int64_t* ext_score, ksim_eval_out* out);
 
@@ -56,6 +61,10 @@ int ksim_oracle_fw_score(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_i
                          int32_t n, ksim_eval_out* out);
 int ksim_oracle_fw_normalize(ksim_oracle* o, int32_t slot, const int32_t* nodes, const int64_t* scores, int32_t n,
                              int64_t* out);
+/* ksim_engine.h ksim_fw_filter_nominated for the framework cycle of pod pi of ps. */
+int ksim_oracle_fw_filter_nominated(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, const ksim_pod_set* nps,
+                                    int32_t n_nodes, const int32_t* nodes, const int32_t* first, const int32_t* count,
+                                    uint8_t* fail_plugin, uint32_t* fail_detail);
 int ksim_oracle_assume(ksim_oracle* o, const ksim_pod_set* pods, int32_t pod_index, int32_t node, int sign);
 int ksim_oracle_get_node_state(const ksim_oracle* o, int64_t* req_cpu, int64_t* req_mem,
                                int64_t* req_eph, int64_t* nz_cpu, int64_t* nz_mem,

@@ -128,6 +128,15 @@ class NodeInfo:
         self.nz_mem += m
         self.pods.append(PodInfo(pod))
 
+    def save(self):
+        return (dict(self.requested), self.nz_cpu, self.nz_mem, len(self.pods),
+                {k: set(v) for k, v in self.used_ports.items()})
+
+    def restore(self, saved) -> None:
+        """Undo add_pod calls made after save() (addNominatedPods works on a clone)."""
+        self.requested, self.nz_cpu, self.nz_mem, n, self.used_ports = saved
+        del self.pods[n:]
+
 
 class ObjScheduler:
     """One simulated scheduler (sequential semantics, TB tie-break)."""
@@ -136,7 +145,7 @@ class ObjScheduler:
                  pct: int = 0, weights: Optional[Dict[str, int]] = None, seed: int = 0x4B53494D,
                  hard_pod_affinity_weight: int = 1, network_bandwidth=None, nb_filter: bool = True,
                  nb_score: bool = True, pvs=(), pvcs=(), storage_classes=(), fit=None, node_affinity=None,
-                 preemption=None, spread=None, services=(), controllers=()):
+                 preemption=None, spread=None, services=(), controllers=(), provisioning: bool = False):
         """fit / node_affinity / preemption / spread: ksim.profile FitArgs,
         NodeAffinityArgs, PreemptionArgs, PodTopologySpreadArgs (the plugin args of
         the profile; None = the defaults).  services / controllers: the
@@ -199,6 +208,7 @@ class ObjScheduler:
             for claim in p.pvc_claims:
                 self.claim_users[(p.namespace, claim)] = self.claim_users.get((p.namespace, claim), 0) + 1
         self.provisioned = 0
+        self.provisioning = provisioning             # a provisioner acts (the simulator runs none)
         self._pv_controller()
         self.next_start = 0
         self.seq = 0
@@ -303,12 +313,11 @@ class ObjScheduler:
         labels_only = Node(name="", labels=labels)
         return any(self._term_match(t, labels_only) for t in pv.node_affinity)
 
-    def _delay(self, pvc) -> Optional[bool]:
-        cls = pvc.storage_class or ""
-        if not cls:
-            return False
-        sc = self.classes.get(cls)
-        return None if sc is None else sc.volume_binding_mode == "WaitForFirstConsumer"
+    def _delay(self, pvc) -> bool:
+        """IsDelayBindingMode: a class that does not exist is NotFound, not an
+        error, so such a claim is Immediate."""
+        sc = self.classes.get(pvc.storage_class or "")
+        return sc is not None and sc.volume_binding_mode == "WaitForFirstConsumer"
 
     def _pv_controller(self) -> None:
         for pvc in self.pvcs.values():               # syncClaim of a claim naming its PV
@@ -316,34 +325,35 @@ class ObjScheduler:
             if pv is not None and pv.claim_ref is None:
                 pv.claim_ref = (pvc.namespace, pvc.name)
         for pvc in self.pvcs.values():
-            if pvc.volume_name or self._delay(pvc) is not False:
+            if pvc.volume_name or self._delay(pvc):
                 continue
             pv = self._find_matching_volume(pvc, None, set(), False)
             if pv is not None:
                 pv.claim_ref, pvc.volume_name = (pvc.namespace, pvc.name), pv.name
 
     def volume_prefilter(self, pod: Pod) -> Optional[str]:
-        """VolumeRestrictions (ReadWriteOncePod) and VolumeBinding PreFilter."""
+        """VolumeBinding PreFilter (VolumeRestrictions' ReadWriteOncePod check is
+        behind a feature gate that is off in v1.26)."""
         immediate = False
         for claim in pod.pvc_claims:
             pvc = self.pvcs.get((pod.namespace, claim))
             if pvc is None:
                 return f'persistentvolumeclaim "{claim}" not found'
-            if "ReadWriteOncePod" in pvc.access_modes and self.claim_users.get((pod.namespace, claim), 0):
-                return "node has pod using PersistentVolumeClaim with the same name and ReadWriteOncePod access mode"
             if not pvc.volume_name:
-                d = self._delay(pvc)
-                if d is None:
-                    return f'storageclass.storage.k8s.io "{pvc.storage_class}" not found'
-                immediate = immediate or not d
+                immediate = immediate or not self._delay(pvc)
         return "pod has unbound immediate PersistentVolumeClaims" if immediate else None
 
     def find_pod_volumes(self, pod: Pod, node: Node):
         """binder.go FindPodVolumes for the unbound WaitForFirstConsumer claims:
         (static [(pvc, pv)], to provision [pvc]) or None (ErrReasonBindConflict)."""
         delay = [self.pvcs[(pod.namespace, c)] for c in pod.pvc_claims if not self.pvcs[(pod.namespace, c)].volume_name]
-        delay.sort(key=lambda c: c.request)
         chosen, static, provision = set(), [], []
+        for pvc in delay:                              # AnnSelectedNode: provisioning started there
+            if pvc.selected_node:
+                if pvc.selected_node != node.name:
+                    return None
+                provision.append(pvc)
+        delay = sorted((c for c in delay if not c.selected_node), key=lambda c: c.request)
         for pvc in delay:
             pv = self._find_matching_volume(pvc, node.labels, chosen, True)
             if pv is None:
@@ -353,7 +363,7 @@ class ObjScheduler:
                 static.append((pvc, pv))
         for pvc in provision:                          # checkVolumeProvisions
             sc = self.classes[pvc.storage_class or ""]
-            if sc.provisioner == "kubernetes.io/no-provisioner":
+            if sc.provisioner in ("", "kubernetes.io/no-provisioner"):
                 return None
             if sc.allowed_topologies and not any(
                     term and all(vals and node.labels.get(k) in vals for k, vals in term)
@@ -368,6 +378,9 @@ class ObjScheduler:
             for pvc, pv in static:
                 pv.claim_ref, pvc.volume_name = (pvc.namespace, pvc.name), pv.name
             for pvc in provision:
+                if not self.provisioning:              # no provisioner: the claim waits on its node
+                    pvc.selected_node = node.name
+                    continue
                 self.provisioned += 1
                 pv = PersistentVolume(name=f"pvc-provisioned-{self.provisioned}", capacity=pvc.request,
                                       storage_class=pvc.storage_class or "", access_modes=list(pvc.access_modes),
@@ -847,12 +860,18 @@ class ObjScheduler:
         return [MAX_NODE_SCORE - s for s in out] if reverse else out
 
     # ---- DefaultPreemption (preemption.go / default_preemption.go) -------------------
-    def preempt(self, pod: Pod, priority: int, start_time: Dict[str, int], order: Dict[str, int]):
+    def preempt(self, pod: Pod, priority: int, start_time: Dict[str, int], order: Dict[str, int],
+                nominated=None):
         """PostFilter for an unschedulable pod, deterministic (offset 0, candidates
         in nodeTree order).  start_time / order: per bound pod name (order breaks
-        MoreImportantPod ties).  Returns (nominated node name or None, victim names)."""
+        MoreImportantPod ties).  ``nominated``: the PodNominator as in cycle();
+        SelectVictimsOnNode's filter runs RunFilterPluginsWithNominatedPods, so
+        the nominated pods of priority >= the pod's stay on the node (pass 1;
+        pass 2 without them passes whenever pass 1 does for Fit).  Returns
+        (nominated node name or None, victim names)."""
         pts, ipa = self.pts_prefilter(pod), self.ipa_prefilter(pod)
-        potential = [ni for ni in self.nodes if self.filter_node(pod, ni, pts, ipa)[0] == "NodeResourcesFit"]
+        potential = [ni for ni in self.nodes
+                     if self.filter_with_nominated(pod, ni, pts, ipa, nominated)[0] == "NodeResourcesFit"]
         pa = self.preemption
         want = min(max(len(potential) * pa.min_candidate_nodes_percentage // 100, pa.min_candidate_nodes_absolute),
                    len(potential))
@@ -872,6 +891,10 @@ class ObjScheduler:
             lower.sort(key=lambda q: (-q.priority, start_time[q.name], order[q.name]))   # MoreImportantPod
             req = dict(ni.requested)
             n = len(ni.pods) - len(lower)
+            for q in self._nominated_for(pod, ni, nominated):
+                for k, v in pod_requests(q).items():
+                    req[k] = req.get(k, 0) + v
+                n += 1
             for q in lower:
                 for k, v in pod_requests(q).items():
                     req[k] = req.get(k, 0) - v
@@ -982,17 +1005,42 @@ class ObjScheduler:
                 msg = self.pts_filter(pod, pts, node)
             elif pl == "InterPodAffinity":
                 msg = self.ipa_filter(ipa, node)
-            elif pl == "VolumeBinding":
-                if pod.pvc_claims and not self.volume_binding_ok(pod, node):
-                    msg = "node(s) had volume node affinity conflict"
-                elif pod.pvc_claims and self.find_pod_volumes(pod, node) is None:
-                    msg = "node(s) didn't find available persistent volumes to bind"
+            elif pl == "VolumeBinding" and pod.pvc_claims:   # FindPodVolumes' reasons, in its order
+                reasons = []
+                if not self.volume_binding_ok(pod, node):
+                    reasons.append("node(s) had volume node affinity conflict")
+                if self.find_pod_volumes(pod, node) is None:
+                    reasons.append("node(s) didn't find available persistent volumes to bind")
+                msg = ", ".join(reasons) or None
             elif pl == "VolumeZone":
                 if pod.pvc_claims and not self.volume_zone_ok(pod, node):
                     msg = "node(s) had no available volume zone"
             if msg:
                 return pl, msg
         return None, None
+
+    @staticmethod
+    def _nominated_for(pod: Pod, ni: NodeInfo, nominated) -> List[Pod]:
+        """addNominatedPods' pods: the node's nominated pods of priority >= the
+        pod's, the pod itself excluded (framework/runtime/framework.go v1.26)."""
+        if not nominated:
+            return []
+        return [q for q in nominated.get(ni.node.name, ()) if q.priority >= pod.priority and q.name != pod.name]
+
+    def filter_with_nominated(self, pod: Pod, ni: NodeInfo, pts, ipa, nominated):
+        """RunFilterPluginsWithNominatedPods: with nominated pods, pass 1 runs on
+        a clone carrying them (PreFilterExtensions.AddPod: the PTS / IPA counts
+        recomputed over the clone); only if it passes, pass 2 on the node as is."""
+        add = self._nominated_for(pod, ni, nominated)
+        if add:
+            saved = ni.save()
+            for q in add:
+                ni.add_pod(q)
+            pl, msg = self.filter_node(pod, ni, self.pts_prefilter(pod), self.ipa_prefilter(pod))
+            ni.restore(saved)
+            if pl is not None:
+                return pl, msg
+        return self.filter_node(pod, ni, pts, ipa)
 
     @staticmethod
     def node_affinity_prefilter(pod: Pod) -> Optional[set]:
@@ -1011,9 +1059,11 @@ class ObjScheduler:
             out = set(term) if out is None else out | term
         return out
 
-    def cycle(self, pod: Pod, extender=None) -> dict:
+    def cycle(self, pod: Pod, extender=None, nominated=None, nominated_node: Optional[str] = None) -> dict:
         """``extender(kept node names) -> (filtered-out names, {name: combined weighted score})``
-        models the scheduler's extenders (findNodesThatPassExtenders, prioritizeNodes)."""
+        models the scheduler's extenders (findNodesThatPassExtenders, prioritizeNodes).
+        ``nominated``: the PodNominator, {node name: [pods nominated there]};
+        ``nominated_node``: the pod's own status.nominatedNodeName."""
         seq = self.seq
         self.seq += 1
         vmsg = self.volume_prefilter(pod) if pod.pvc_claims else None
@@ -1036,14 +1086,30 @@ class ObjScheduler:
                 return {"filter": filt, "n_feasible": 0, "raw": {}, "norm": {}, "total": {},
                         "error": None, "chosen": None}
             scan = [ni for ni in self.nodes if ni.node.name in names_pf]
+        failed = set()
+        if nominated_node is not None and nominated_node in self.by_name:
+            # evaluateNominatedNode (schedule_one.go v1.26): the nominated node
+            # first, whatever the PreFilterResult; if it passes it is the only
+            # feasible node (no scoring, nextStartNodeIndex untouched); if it
+            # fails its status stays in the diagnosis and counts as processed
+            ni = self.by_name[nominated_node]
+            pl, msg = self.filter_with_nominated(pod, ni, pts, ipa, nominated)
+            filt[nominated_node] = (pl[:-1] if pl and pl.endswith("!") else pl, msg)
+            if pl is None:
+                ni.add_pod(pod)
+                if pod.pvc_claims:
+                    self.assume_volumes(pod, ni.node)
+                return {"filter": filt, "n_feasible": 1, "raw": {}, "norm": {}, "total": {}, "error": None,
+                        "chosen": nominated_node, "nominated_pass": True}
+            if not pl.endswith("!"):
+                failed.add(nominated_node)
         N = len(scan)
         K = num_feasible_nodes_to_find(self.pct, N)
         feasible: List[NodeInfo] = []
-        failed = 0
         error = None
         for i in range(N):
             ni = scan[(self.next_start + i) % N]
-            pl, msg = self.filter_node(pod, ni, pts, ipa)
+            pl, msg = self.filter_with_nominated(pod, ni, pts, ipa, nominated)
             if pl is not None and pl.endswith("!"):        # checkNode: the error ends the scan
                 filt[ni.node.name] = (pl[:-1], msg)
                 error = "filter"
@@ -1054,8 +1120,9 @@ class ObjScheduler:
                     break
                 feasible.append(ni)
             else:
-                failed += 1
-        self.next_start = (self.next_start + len(feasible) + failed) % N
+                failed.add(ni.node.name)
+        # processedNodes = feasible + len(diagnosis.NodeToStatusMap)
+        self.next_start = (self.next_start + len(feasible) + len(failed)) % N
         ext_scores: Dict[str, int] = {}
         if extender is not None:
             out, ext_scores = extender([ni.node.name for ni in feasible])

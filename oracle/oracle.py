@@ -29,9 +29,11 @@ def lib():
         L.ksim_oracle_cycle.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_cycle_ext.argtypes = [vp, vp, i32, vp, vp, vp]
         L.ksim_oracle_preempt.argtypes = [vp, vp, i32, i32, vp, vp]
+        L.ksim_oracle_preempt_nominated.argtypes = [vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp]
         L.ksim_oracle_fw_filter.argtypes = [vp, vp, i32, vp]
         L.ksim_oracle_fw_score.argtypes = [vp, vp, i32, vp, i32, vp]
         L.ksim_oracle_fw_normalize.argtypes = [vp, i32, vp, vp, i32, vp]
+        L.ksim_oracle_fw_filter_nominated.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, vp, vp]
         L.ksim_oracle_assume.argtypes = [vp, vp, i32, i32, ctypes.c_int]
         L.ksim_oracle_schedule.argtypes = [vp, vp, i32, i32, vp, ctypes.c_int, vp]
         L.ksim_oracle_get_node_state.argtypes = [vp] * 7
@@ -144,6 +146,23 @@ class Oracle:
             raise RuntimeError("oracle fw_score failed")
         return buf.result()
 
+    def fw_filter_nominated(self, nominated, groups):
+        """ksim_oracle_fw_filter_nominated (see ksim.engine.Engine.fw_filter_nominated)."""
+        from ksim.engine import _nominated_groups
+        pods, index = self._fw
+        nodes, first, count, order = _nominated_groups(groups)
+        fp = np.zeros(len(nodes), np.uint8)
+        fd = np.zeros(len(nodes), np.uint32)
+        ps = pods.pod_set()
+        sub = nominated.subset_indices(order)      # kept alive: the pod set points into it
+        nps = sub.pod_set()
+        if lib().ksim_oracle_fw_filter_nominated(self.h, ctypes.byref(ps), index, ctypes.byref(nps), len(nodes),
+                                                 *(a.ctypes.data_as(ctypes.c_void_p) for a in (nodes, first, count)),
+                                                 fp.ctypes.data_as(ctypes.c_void_p),
+                                                 fd.ctypes.data_as(ctypes.c_void_p)) != 0:
+            raise RuntimeError("oracle fw_filter_nominated failed")
+        return fp, fd
+
     def fw_normalize(self, slot: int, nodes, scores) -> np.ndarray:
         nd = np.ascontiguousarray(nodes, np.int32)
         sc = np.ascontiguousarray(scores, np.int64)
@@ -165,16 +184,27 @@ class Oracle:
     def forget(self, pods, index: int, node: int):
         self.assume(pods, index, node, -1)
 
-    def preempt(self, pods, index: int, priority: int, bound) -> tuple:
-        """DefaultPreemption PostFilter (ksim_oracle_preempt).  ``bound`` is a
-        ksim.abi.BoundPods.  Returns (nominated node position or -1, victim indices)."""
+    def preempt(self, pods, index: int, priority: int, bound, groups=None) -> tuple:
+        """DefaultPreemption PostFilter (ksim_oracle_preempt / _nominated).  ``bound``
+        is a ksim.abi.BoundPods; ``groups`` as ksim.engine.Engine.preempt.  Returns
+        (nominated node position or -1, victim indices, potential, candidates)."""
         self._sync()
         self._ran = True
         from ksim import abi
+        from ksim.engine import _nominated_groups
         out = abi.PreemptOut(max(bound.n, 1))
         ps = pods.pod_set()
-        rc = lib().ksim_oracle_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(bound.c),
-                                       ctypes.byref(out.c))
+        if groups:
+            nodes, first, count, order = _nominated_groups(groups)
+            sub = pods.subset_indices(order)      # kept alive: the pod set points into it
+            nps = sub.pod_set()
+            rc = lib().ksim_oracle_preempt_nominated(self.h, ctypes.byref(ps), index, priority, ctypes.byref(bound.c),
+                                                     ctypes.byref(nps), len(nodes),
+                                                     *(a.ctypes.data_as(ctypes.c_void_p) for a in (nodes, first, count)),
+                                                     ctypes.byref(out.c))
+        else:
+            rc = lib().ksim_oracle_preempt(self.h, ctypes.byref(ps), index, priority, ctypes.byref(bound.c),
+                                           ctypes.byref(out.c))
         if rc != 0:
             raise RuntimeError(f"oracle preempt failed: {rc}")
         return out.result()

@@ -20,6 +20,19 @@ What it reproduces of schedule_one.go / framework/runtime / parallelize:
                              deterministic rule, for the parallelism-1 check);
   Reserve / Unreserve        the framework's node;
   PostFilter                 DefaultPreemption over NodeToStatusMap.
+  PodNominator               nominated pods (queue.AddNominatedPod after a
+                             PostFilter nomination; deleted when the pod is
+                             assumed, cleared by ModeOverride "" and by
+                             prepareCandidate for lower-priority pods nominated
+                             on the chosen node); RunFilterPluginsWithNominated
+                             Pods' two passes (each recorded, the second's
+                             calls overwriting the first's in the store);
+                             evaluateNominatedNode before the scan;
+                             PodEligibleToPreemptOthers (a terminating
+                             lower-priority pod on the nominated node blocks).
+  victims                    deleted with the default grace period: with no
+                             kubelet in the simulator they stay Terminating,
+                             bound and counted (``terminating``).
 
 The wrapper recording (simulator/scheduler/plugin/wrappedplugin.go) goes into
 a ksim.resultstore.Store as the Go wrapper does, per plugin call.  The random
@@ -30,7 +43,7 @@ from __future__ import annotations
 
 import math
 import random
-from typing import List, Optional
+from typing import Dict, List, Optional, Set
 
 from ksim import abi
 from ksim.fwplugins import ERROR, EnginePlugins, Status
@@ -63,12 +76,44 @@ class Framework:
         self.names = plugins.cluster.node_names
         self.weights = {p.name: (p.weight or 1) for p in prof.score_plugins()}
         self.log: List[dict] = []
+        self.nominator: Dict[int, int] = {}      # pod index -> nominated node (insertion order)
+        self.nom_prio: Dict[int, int] = {}
+        self.terminating: Set[int] = set()       # bound-table indices deleted by preemption
+
+    # ---- PodNominator ---------------------------------------------------------
+    def nominate(self, index: int, node: int, priority: int) -> None:
+        self.nominator.pop(index, None)
+        self.nominator[index] = node
+        self.nom_prio[index] = priority
+
+    def _nominated_view(self, index: int, priority: int) -> Dict[int, List[int]]:
+        """addNominatedPods' choice per node: priority >= the pod's, itself excluded."""
+        out: Dict[int, List[int]] = {}
+        for j, node in self.nominator.items():
+            if j != index and self.nom_prio[j] >= priority:
+                out.setdefault(node, []).append(j)
+        return out
+
+    def _filter_node(self, node: int, ns: str, name: str) -> Status:
+        """RunFilterPluginsWithNominatedPods, each pass's plugin calls recorded."""
+        def record(ran):
+            for pl, s in ran:                     # wrappedPlugin.Filter records each call
+                self.store.add_filter_result(ns, name, self.names[node], pl,
+                                             PASSED_FILTER_MESSAGE if s.is_success() else s.message)
+        if self.pl.has_nominated(node):
+            st, ran = self.pl.run_filter_plugins(node, nominated=True)
+            record(ran)
+            if not st.is_success():
+                return st
+        st, ran = self.pl.run_filter_plugins(node)
+        record(ran)
+        return st
 
     # ---- findNodesThatPassFilters (racing Parallelizer) ------------------------
-    def _race(self, nodes: List[int], k: int, ns: str, name: str):
+    def _race(self, nodes: List[int], k: int, ns: str, name: str, status_map: Optional[dict] = None):
         n = len(nodes)
         feasible: List[int] = []
-        status_map = {}
+        status_map = {} if status_map is None else status_map
         evaluated: List[int] = []
         state = {"length": 0, "cancel": False, "error": None}
         chunk = chunk_size_for(n, self.parallelism)
@@ -80,10 +125,7 @@ class Framework:
         def check_node(i: int):
             node = nodes[(self.next_start + i) % n]
             evaluated.append(node)
-            st, ran = self.pl.run_filter_plugins(node)
-            for pl, s in ran:                     # wrappedPlugin.Filter records each call
-                self.store.add_filter_result(ns, name, self.names[node], pl,
-                                             PASSED_FILTER_MESSAGE if s.is_success() else s.message)
+            st = self._filter_node(node, ns, name)
             if st.code == ERROR:
                 if state["error"] is None:
                     state["error"] = st
@@ -143,15 +185,15 @@ class Framework:
         ns, name = pods.names[index]
         rec = {"pod": index, "chosen": -1, "status": abi.STATUS_UNSCHEDULABLE, "nominated": -1}
         self.log.append(rec)
-        st, names = self.pl.pre_filter(pods, index)
-        conflict = names is not None and len(names) == 0
+        st, names = self.pl.pre_filter(pods, index, self._nominated_view(index, priority))
+        conflict = not st.is_success() and st.code != ERROR   # RunPreFilterPlugins stops at st.failed_plugin
         for p in self.prof.plugins["preFilter"].enabled:
             plugin = original_name(p.name)
+            if conflict and plugin == st.failed_plugin:
+                self.store.add_pre_filter_result(ns, name, plugin, st.message, None)
+                break
             if plugin == "NodeAffinity" and names is not None:
-                self.store.add_pre_filter_result(ns, name, plugin, st.message if conflict else SUCCESS_MESSAGE,
-                                                 None if conflict else list(names))
-                if conflict:
-                    break
+                self.store.add_pre_filter_result(ns, name, plugin, SUCCESS_MESSAGE, list(names))
             else:
                 self.store.add_pre_filter_result(ns, name, plugin, SUCCESS_MESSAGE, None)
         seq = self.pod_seq                        # the tie-break sequence of this cycle
@@ -170,22 +212,39 @@ class Framework:
             nodes = sorted(pos[x] for x in names)
             if self.tie != "tb":
                 self.rng.shuffle(nodes)           # Go map iteration order of PreFilterResult.NodeNames
-        k = num_feasible_nodes_to_find(len(nodes), self.prof.percentage_of_nodes_to_score)
-        feasible, status_map, evaluated, err = self._race(nodes, k, ns, name)
-        rec["evaluated"] = evaluated
-        processed = len(feasible) + len(status_map)
-        self.next_start = (self.next_start + processed) % len(nodes)
-        rec["next_start"] = self.next_start
-        rec["feasible"] = list(feasible)
-        rec["failed"] = list(status_map)
-        if err is not None:
-            rec["status"], rec["chosen"] = abi.STATUS_ERROR, abi.CHOSEN_ERROR
-            return rec
+        status_map = {}
+        mine = self.nominator.get(index)
+        feasible = []
+        if mine is not None:
+            # evaluateNominatedNode: the pod's nominated node first, whatever the
+            # PreFilterResult; passing, it is the only feasible node (no scoring,
+            # nextStartNodeIndex untouched); failing, its status stays in the
+            # diagnosis (and counts in processedNodes)
+            nst = self._filter_node(mine, ns, name)
+            rec["nominated_eval"] = mine
+            if nst.is_success():
+                feasible = [mine]
+                rec["evaluated"], rec["feasible"], rec["failed"] = [mine], [mine], []
+                rec["next_start"] = self.next_start
+            elif nst.code != ERROR:
+                status_map[mine] = nst
+        if not feasible:
+            k = num_feasible_nodes_to_find(len(nodes), self.prof.percentage_of_nodes_to_score)
+            feasible, status_map, evaluated, err = self._race(nodes, k, ns, name, status_map)
+            rec["evaluated"] = evaluated
+            processed = len(feasible) + len(status_map)
+            self.next_start = (self.next_start + processed) % len(nodes)
+            rec["next_start"] = self.next_start
+            rec["feasible"] = list(feasible)
+            rec["failed"] = list(status_map)
+            if err is not None:
+                rec["status"], rec["chosen"] = abi.STATUS_ERROR, abi.CHOSEN_ERROR
+                return rec
         if not feasible:
             for p in self.prof.plugins["postFilter"].enabled:
                 nom = -1
                 if original_name(p.name) == "DefaultPreemption" and bound is not None:
-                    pst, nom = self.pl.post_filter(priority, bound)
+                    nom = self._post_filter(index, priority, bound, status_map, rec)
                 rec["nominated"] = nom
                 self.store.add_post_filter_result(ns, name, self.names[nom] if nom >= 0 else "",
                                                   original_name(p.name), [self.names[x] for x in status_map])
@@ -217,8 +276,10 @@ class Framework:
                         totals[j] += v * self.weights[p.name]
             chosen = self._select(feasible, totals, seq)
             rec["totals"] = dict(zip(feasible, totals))
-        # assume (the engine's reserve hook, unrecorded), then the wrapped Reserve plugins
+        # assume (the engine's reserve hook, unrecorded), then the wrapped Reserve
+        # plugins; the assumed pod leaves the nominator (DeleteNominatedPodIfExists)
         self.pl.reserve(chosen)
+        self.nominator.pop(index, None)
         for p in self.prof.plugins["reserve"].enabled:
             self.store.add_selected_node(ns, name, self.names[chosen])
             self.store.add_reserve_result(ns, name, original_name(p.name), SUCCESS_MESSAGE)
@@ -229,6 +290,31 @@ class Framework:
         rec["chosen"] = chosen
         rec["status"] = abi.STATUS_SCHEDULED
         return rec
+
+
+    def _post_filter(self, index: int, priority: int, bound, status_map: dict, rec: dict) -> int:
+        """DefaultPreemption.PostFilter with the queue's handling of its
+        NominatingInfo; returns the node the wrapper records (-1: none)."""
+        mine = self.nominator.get(index, -1)
+
+        def terminating_lower(node, prio):        # the snapshot's DeletionTimestamp'd pods
+            return any(int(bound.node[j]) == node and int(bound.priority[j]) < prio for j in self.terminating)
+        pst, nom, victims, override = self.pl.post_filter(priority, bound, mine, status_map.get(mine),
+                                                          terminating_lower)
+        if not override:                          # nil result: ModeNoop, the nomination stays
+            rec["eligible"] = False
+            return -1
+        rec["victims"] = victims
+        if nom < 0:
+            self.nominator.pop(index, None)       # ModeOverride "": the nomination is cleared
+            return -1
+        # prepareCandidate: the victims are deleted (Terminating from now on) and
+        # lower-priority pods nominated on the node lose their nomination
+        self.terminating.update(victims)
+        for j in [j for j, n in self.nominator.items() if n == nom and self.nom_prio[j] < priority]:
+            del self.nominator[j]
+        self.nominate(index, nom, priority)
+        return nom
 
 
 class OracleBackend:
@@ -254,8 +340,11 @@ class OracleBackend:
     def forget(self, pods, index, node):
         self.o.assume(pods, index, node, -1)
 
-    def preempt(self, pods, index, priority, bound=None):
-        return self.o.preempt(pods, index, priority, bound if bound is not None else self.bound)
+    def fw_filter_nominated(self, pods, groups):
+        return self.o.fw_filter_nominated(pods, groups)
+
+    def preempt(self, pods, index, priority, bound=None, groups=None):
+        return self.o.preempt(pods, index, priority, bound if bound is not None else self.bound, groups)
 
 
 class EngineBackend:
@@ -268,11 +357,11 @@ class EngineBackend:
     def __getattr__(self, k):
         return getattr(self.e, k)
 
-    def preempt(self, pods, index, priority, bound=None):
+    def preempt(self, pods, index, priority, bound=None, groups=None):
         if bound is not None and bound is not self._bound:
             self.e.set_bound_pods(bound)
             self._bound = bound
-        return self.e.preempt(pods, index, priority)
+        return self.e.preempt(pods, index, priority, groups)
 
 
 def annotations(store: Store, pods, index: int) -> dict:

@@ -39,5 +39,5 @@ def test_framework_entry_points_bound():
     """The framework-driven calls the engine-backed plugins need are bound."""
     src = "\n".join(_go_sources().values())
     for fn in ("ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize", "ksim_assume", "ksim_forget",
-               "ksim_preempt"):
+               "ksim_preempt", "ksim_preempt_nominated", "ksim_fw_filter_nominated"):
         assert f"C.{fn}(" in src, fn

@@ -190,3 +190,111 @@ def test_compat_cycle_postfilter_nominated():
         assert annotations(se, pods, i) == annotations(so, pods, i), i
         nominated += re["nominated"] >= 0
     assert nominated > 0
+
+
+def _nominated_run(fe, fo, pods, prio, table_for, steps, where):
+    """One schedule_one per step on both mirrors; the outcomes, annotations and
+    nominators must agree.  ``table_for(step)`` returns the bound-pod table."""
+    stats = {"nominated": 0, "two_pass": 0, "nominated_eval": 0, "ineligible": 0}
+    for step, i in enumerate(steps):
+        table = table_for(step)
+        re = fe.schedule_one(pods, i, prio[i], table)
+        ro = fo.schedule_one(pods, i, prio[i], table)
+        for k in ("chosen", "status", "nominated", "feasible", "failed", "evaluated", "next_start", "totals",
+                  "victims", "eligible", "nominated_eval"):
+            assert re.get(k) == ro.get(k), f"{where} step {step} pod {i} {k}: engine {re.get(k)} oracle {ro.get(k)}"
+        assert annotations(fe.store, pods, i) == annotations(fo.store, pods, i), f"{where} pod {i} annotations"
+        assert fe.nominator == fo.nominator and fe.terminating == fo.terminating, f"{where} step {step}"
+        stats["nominated"] += re["nominated"] >= 0
+        stats["ineligible"] += re.get("eligible") is False
+        stats["nominated_eval"] += "nominated_eval" in re
+        stats["two_pass"] += any(fe.pl.has_nominated(x) for x in re.get("evaluated", []))
+    return stats
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_framework_nominated_preemption_chains(seed):
+    """The racing mirror with the PodNominator over the engine and over the
+    oracle: preemptors nominated (ksim_preempt_nominated keeps the nominated
+    pods of priority >= the preemptor on each candidate), victims Terminating,
+    the nominated pods re-queued (evaluateNominatedNode, then refused while
+    their victims terminate), every other pod filtered with its two passes
+    (ksim_fw_filter_nominated).  The bound-pod table grows with each bind."""
+    import dataclasses
+    from test_preemption import crowded
+    nodes, bound, start, _ = crowded(n_nodes=400, seed=seed + 20)
+    cluster, _ = encode_cluster(nodes, bound)
+    rng = np.random.default_rng(seed)
+    pods_o = [Pod(f"p{i}", priority=int(rng.choice([0, 5, 50, 500, 5000])),
+                  containers=[Container({"cpu": f"{int(rng.integers(5, 300)) * 100}m",
+                                         "memory": f"{int(rng.integers(2, 30))}Gi"})]) for i in range(160)]
+    pods = encode_pods(cluster, pods_o)
+    prio = [p.priority for p in pods_o]
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    w = profile.default_score_weights()
+    fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, Store(w), seed=seed)
+    fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, Store(w), seed=seed)
+    placed = list(bound)
+    tables = [bound_table(cluster, placed, start)]
+    retries = []
+    # the queue, step by step so the table grows with each bind; preemptors
+    # come back three pods later
+    stats = {"nominated": 0, "two_pass": 0, "nominated_eval": 0, "ineligible": 0}
+    queue, step = list(range(len(pods_o))), 0
+    while queue and step < 400:
+        i = queue.pop(0)
+        s = _nominated_run(fe, fo, pods, prio, lambda _: tables[-1], [i], f"seed {seed}")
+        for k in stats:
+            stats[k] += s[k]
+        last = fe.log[-1]
+        if last["status"] == abi.STATUS_SCHEDULED:
+            placed.append(dataclasses.replace(pods_o[i], node_name=cluster.node_names[last["chosen"]]))
+            start[pods_o[i].name] = 100 + step
+            tables.append(bound_table(cluster, placed, start))
+        elif last["nominated"] >= 0:
+            retries.append(i)
+        if len(retries) >= 3 or (not queue and retries):
+            queue.extend(retries)
+            retries = []
+        step += 1
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    assert stats["nominated"] > 5 and stats["two_pass"] > 5 and stats["nominated_eval"] > 5, stats
+
+
+def test_framework_seeded_nominations_topology():
+    """Nominations seeded on spreading / anti-affine config-3 pods: the first
+    pass's PodTopologySpread / InterPodAffinity state carries the nominated
+    pods (assume, re-run, forget on the device), then the seeded pods try
+    their nominated node first."""
+    nodes, bound, incoming = gen.config3_objects(n_nodes=500, pods_per_node=4, n_incoming=400)
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, incoming)
+    prio = [p.priority for p in incoming]
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    w = profile.default_score_weights()
+    fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, Store(w), seed=3)
+    fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, Store(w), seed=3)
+    rng = np.random.default_rng(9)
+    seeded = list(range(60))
+    for j in seeded:
+        node = int(rng.integers(0, 40)) * 3
+        fe.nominate(j, node, prio[j])
+        fo.nominate(j, node, prio[j])
+    stats = _nominated_run(fe, fo, pods, prio, lambda _: None, list(range(60, len(incoming))) + seeded, "config3")
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+    assert stats["two_pass"] > 50 and stats["nominated_eval"] > 10, stats

@@ -1,8 +1,11 @@
 """Unbound PersistentVolumeClaims: the PV controller's binding of Immediate
-claims, VolumeBinding's static matching and dynamic provisioning of
-WaitForFirstConsumer claims (FindPodVolumes, AssumePodVolumes), PreFilter
-rejections (missing claim or class, unbound Immediate claim) and
-VolumeRestrictions' ReadWriteOncePod (ksim/volumes.py; SURVEY §8(f) 1,
+claims (a claim of a class that does not exist is Immediate), VolumeBinding's
+static matching and dynamic provisioning of WaitForFirstConsumer claims
+(FindPodVolumes, AssumePodVolumes: with no provisioner in the simulator the
+pod waits in PreBind and its claims keep the selected node; ``provisioning``
+models one), PreFilter rejections (missing claim, unbound Immediate claim)
+recorded as VolumeBinding's PreFilter status, and the Filter reasons
+(node affinity conflict, bind conflict, both) (ksim/volumes.py; SURVEY §8(f) 1,
 /root/reference/simulator/export/export.go:47-49,59-61 carries pvs / pvcs /
 storageClasses).
 
@@ -38,7 +41,8 @@ def binding_scenario(seed=0, n_nodes=40, n_pods=150):
                StorageClass("zonal", "csi.example.com", "WaitForFirstConsumer",
                             [[(ZONE, ["z0", "z1"])], []]),
                StorageClass("fast", "csi.example.com", "WaitForFirstConsumer"),
-               StorageClass("imm", "kubernetes.io/no-provisioner", "Immediate")]
+               StorageClass("imm", "kubernetes.io/no-provisioner", "Immediate"),
+               StorageClass("blank", "", "WaitForFirstConsumer")]
     pvs, pvcs = [], []
     for k in range(60):                                  # local PVs: one host each, mixed sizes
         host = f"n{int(rng.integers(0, n_nodes)):03d}"
@@ -76,11 +80,15 @@ def binding_scenario(seed=0, n_nodes=40, n_pods=150):
         if j == 30:
             pvcs.append(PersistentVolumeClaim(name="c-noclass", storage_class="gone"))
             claims.append("c-noclass")
-        if j in (40, 41, 60):                           # one ReadWriteOncePod claim, then its second user
+        if j in (40, 41, 60):                           # one provisioned claim, then its later users
             if j == 40:
-                pvcs.append(PersistentVolumeClaim(name="c-rwop", storage_class="fast", request=GI,
-                                                  access_modes=["ReadWriteOncePod"]))
-            claims.append("c-rwop")
+                pvcs.append(PersistentVolumeClaim(name="c-prov", storage_class="fast", request=GI,
+                                                  access_modes=["ReadWriteOnce"]))
+            claims.append("c-prov")
+        if j == 70:                                     # a class with an empty provisioner cannot provision
+            pvcs.append(PersistentVolumeClaim(name="c-noprov", storage_class="blank", request=100 * GI,
+                                              access_modes=["ReadWriteOnce"]))
+            claims.append("c-noprov")
         if j in (50, 51):                               # the same local claim twice: the second finds it bound
             if j == 50:
                 pvcs.append(PersistentVolumeClaim(name="c-shared", storage_class="local", request=GI,
@@ -91,12 +99,13 @@ def binding_scenario(seed=0, n_nodes=40, n_pods=150):
     return nodes, pods, pvs, pvcs, classes
 
 
-def _objref(nodes, pvs, pvcs, classes, pct, seed):
-    return ObjScheduler(nodes, [], pct=pct, seed=seed, pvs=pvs, pvcs=pvcs, storage_classes=classes)
+def _objref(nodes, pvs, pvcs, classes, pct, seed, provisioning=False):
+    return ObjScheduler(nodes, [], pct=pct, seed=seed, pvs=pvs, pvcs=pvcs, storage_classes=classes,
+                        provisioning=provisioning)
 
 
-def run_queue(backend_factory, nodes, pods, pvs, pvcs, classes, pct=100):
-    vol = VolumeIndex.from_nodes(nodes, copy.deepcopy(pvs), copy.deepcopy(pvcs), classes)
+def run_queue(backend_factory, nodes, pods, pvs, pvcs, classes, pct=100, provisioning=False):
+    vol = VolumeIndex.from_nodes(nodes, copy.deepcopy(pvs), copy.deepcopy(pvcs), classes, provisioning)
     vol.run_pv_controller()
     cluster, _ = encode_cluster(nodes)
     sp = profile.SchedulerProfile(percentage_of_nodes_to_score=pct)
@@ -106,11 +115,11 @@ def run_queue(backend_factory, nodes, pods, pvs, pvcs, classes, pct=100):
     return got, vol, backend, sp
 
 
-@pytest.mark.parametrize("seed,pct", [(0, 100), (1, 0), (2, 100)])
-def test_binding_queue_vs_objref(seed, pct):
+@pytest.mark.parametrize("seed,pct,prov", [(0, 100, False), (1, 0, False), (2, 100, True), (3, 0, True)])
+def test_binding_queue_vs_objref(seed, pct, prov):
     nodes, pods, pvs, pvcs, classes = binding_scenario(seed)
-    got, vol, _, sp = run_queue(lambda c, p: Oracle(c, p), nodes, pods, pvs, pvcs, classes, pct)
-    ref = _objref(nodes, pvs, pvcs, classes, pct, sp.tiebreak_seed)
+    got, vol, _, sp = run_queue(lambda c, p: Oracle(c, p), nodes, pods, pvs, pvcs, classes, pct, prov)
+    ref = _objref(nodes, pvs, pvcs, classes, pct, sp.tiebreak_seed, prov)
     want, rejected = [], 0
     for pod in pods:
         r = ref.cycle(pod)
@@ -118,11 +127,77 @@ def test_binding_queue_vs_objref(seed, pct):
         rejected += "prefilter" in r
     assert got == want
     # every path ran: static binds, provisioning, PreFilter rejections, unschedulable pods
-    assert rejected >= 3 and vol.provisioned > 0 and None in got
+    assert rejected >= 2 and None in got
+    assert (vol.provisioned > 0) == prov and (len(vol.waiting) > 0) == (not prov)
     bound_static = sum(1 for pv in vol.pvs.values() if pv.claim_ref and not pv.name.startswith("pvc-provisioned"))
     assert bound_static > 10
-    # the same bindings on both sides
+    # the same bindings (and provisioning nodes) on both sides
     assert {n: pv.claim_ref for n, pv in vol.pvs.items()} == {n: pv.claim_ref for n, pv in ref.pvs.items()}
+    assert {k: c.selected_node for k, c in vol.pvcs.items()} == {k: c.selected_node for k, c in ref.pvcs.items()}
+    if not prov:                          # the later users of the claim waiting on a node follow it
+        users = [got[j] for j in (40, 41, 60)]
+        assert users[0] is not None and all(u in (users[0], None) for u in users)
+
+
+def test_missing_class_claims_are_immediate():
+    """IsDelayBindingMode: a class that does not exist is not delay binding, so
+    the PV controller binds the claim like an Immediate one (a PV naming the
+    same class), or the pod is rejected at PreFilter while it stays unbound."""
+    vol = VolumeIndex([PersistentVolume("g", capacity=GI, storage_class="gone", access_modes=["ReadWriteOnce"])],
+                      [PersistentVolumeClaim("a", storage_class="gone", request=GI, access_modes=["ReadWriteOnce"]),
+                       PersistentVolumeClaim("b", storage_class="gone", request=GI, access_modes=["ReadWriteOnce"])])
+    assert vol.run_pv_controller() == 1
+    assert vol.pvcs[("default", "a")].volume_name == "g"
+    assert vol.prefilter_rejection(Pod("p", pvc_claims=["a"])) is None
+    assert vol.prefilter_rejection(Pod("q", pvc_claims=["b"])) == "pod has unbound immediate PersistentVolumeClaims"
+
+
+def test_prefilter_rejections_and_reasons_recorded():
+    """Compat annotations: a missing claim / unbound Immediate claim is
+    VolumeBinding's PreFilter status (no Filter entries, every node in
+    PostFilter); a node failing both a bound PV's affinity and an unbound
+    claim's matching gets both reasons, joined in FindPodVolumes' order."""
+    from ksim.encode import encode_pods
+    from ksim.resultstore import Store
+    from ksim.wrapped import compat_cycle
+    nodes = [Node(name=f"n{i}", labels={HOST: f"n{i}", ZONE: f"z{i % 2}"},
+                  allocatable={"cpu": "8", "memory": "8Gi", "pods": "10"}) for i in range(4)]
+    aff = lambda key, vals: [NodeSelectorTerm([Requirement(key, "In", vals)])]
+    pvs = [PersistentVolume("zpv", capacity=GI, storage_class="local", access_modes=["ReadWriteOnce"],
+                            node_affinity=aff(ZONE, ["z0"])),
+           PersistentVolume("hpv", capacity=GI, storage_class="local", access_modes=["ReadWriteOnce"],
+                            node_affinity=aff(HOST, ["n0", "n1"]))]
+    pvcs = [PersistentVolumeClaim("bound", storage_class="local", volume_name="zpv", access_modes=["ReadWriteOnce"]),
+            PersistentVolumeClaim("wffc", storage_class="local", request=GI, access_modes=["ReadWriteOnce"]),
+            PersistentVolumeClaim("imm", request=GI, access_modes=["ReadWriteOnce"])]
+    classes = [StorageClass("local", "kubernetes.io/no-provisioner", "WaitForFirstConsumer")]
+    vol = VolumeIndex.from_nodes(nodes, pvs, pvcs, classes)
+    vol.run_pv_controller()
+    pods = [Pod("both", pvc_claims=["bound", "wffc"]), Pod("gone", pvc_claims=["nope"]),
+            Pod("immediate", pvc_claims=["imm"])]
+    cluster, _ = encode_cluster(nodes)
+    enc = encode_pods(cluster, pods, volumes=vol)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=100)
+    ora = Oracle(cluster, profile.compile_profile(sp))
+    st = Store(profile.default_score_weights())
+    got = [compat_cycle(ora, st, cluster, sp, enc, i)["chosen"] for i in range(3)]
+    assert got[1] < 0 and got[2] < 0
+    ref = _objref(nodes, pvs, pvcs, classes, 100, sp.tiebreak_seed)
+    r = ref.cycle(pods[0])
+    assert cluster.node_names[got[0]] == r["chosen"] == "n0"
+    res = st.results["default/both"]
+    msgs = {n: res.filter[n]["VolumeBinding"] for n in ("n1", "n2", "n3")}
+    assert msgs == {n: r["filter"][n][1] for n in msgs}
+    assert msgs["n3"] == "node(s) had volume node affinity conflict, node(s) didn't find available persistent " \
+                         "volumes to bind"
+    assert msgs["n2"] == "node(s) didn't find available persistent volumes to bind"
+    assert msgs["n1"] == "node(s) had volume node affinity conflict"
+    for name, msg in (("gone", 'persistentvolumeclaim "nope" not found'),
+                      ("immediate", "pod has unbound immediate PersistentVolumeClaims")):
+        res = st.results["default/" + name]
+        assert res.pre_filter_status["VolumeBinding"] == msg and not res.filter
+        assert "NodeAffinity" not in res.pre_filter_status      # RunPreFilterPlugins stopped
+        assert set(res.post_filter) == {n.name for n in nodes}
 
 
 def test_pv_controller_binds_immediate_claims():
@@ -157,7 +232,7 @@ def test_competing_claims_get_an_exact_group():
     classes = [StorageClass("local", "kubernetes.io/no-provisioner", "WaitForFirstConsumer")]
     vol = VolumeIndex.from_nodes(nodes, pvs, pvcs, classes)
     pod = Pod("p", containers=[Container({"cpu": "1"})], pvc_claims=["a", "b"])
-    vb, _ = vol.groups(pod)
+    vb, _, _ = vol.groups(pod)
     assert len(vb) == 1 and [t.match_fields[0].values[0] for t in vb[0]] == ["n1"]
     got, vol2, _, sp = run_queue(lambda c, p: Oracle(c, p), nodes, [pod], pvs, pvcs, classes)
     ref = _objref(nodes, pvs, pvcs, classes, 100, sp.tiebreak_seed)

@@ -114,9 +114,10 @@ def test_volume_filters_vs_objref(pct):
 
 
 def test_unsupported_claims_are_flagged():
-    """Volumes counted against node limits are flagged (not scheduled); a
-    missing claim and an unbound Immediate claim reject the pod at PreFilter (a
-    group no node matches); an unused ReadWriteOncePod claim schedules."""
+    """Volumes counted against node limits and ReadWriteOncePod claims (feature
+    gate off in v1.26) are flagged (not scheduled); a missing claim and an
+    unbound Immediate claim reject the pod at PreFilter (recorded as
+    VolumeBinding's PreFilter status; the engine gets a group no node matches)."""
     nodes, _, pvs, pvcs = volume_scenario()
     pvs = pvs + [PersistentVolume(name="pv-ebs", source="awsElasticBlockStore")]
     pvcs = pvcs + [PersistentVolumeClaim(name="c-ebs", volume_name="pv-ebs"),
@@ -127,8 +128,11 @@ def test_unsupported_claims_are_flagged():
     cluster, _ = encode_cluster(nodes)
     enc = encode_pods(cluster, pods, volumes=VolumeIndex.from_nodes(nodes, pvs, pvcs))
     flags = enc.pods["flags"] & abi.POD_HAS_VOLUMES
-    assert list(flags != 0) == [True, False, False, False, False]
+    assert list(flags != 0) == [True, False, True, False, False]
     assert list(enc.pods["vb_count"] > 0) == [False, True, False, True, False]
+    assert [enc.rejection(i) for i in range(5)] == [
+        None, ("VolumeBinding", "pod has unbound immediate PersistentVolumeClaims"), None,
+        ("VolumeBinding", 'persistentvolumeclaim "c-missing" not found'), None]
     # CSI volumes count against attachable-volumes-* node limits when a node publishes one
     nodes2 = nodes + [Node(name="lim", allocatable={"cpu": "1", "attachable-volumes-csi-x": "10"})]
     enc2 = encode_pods(encode_cluster(nodes2)[0], [Pod(name="c", pvc_claims=["c-pv-lr1"])],

@@ -178,34 +178,6 @@ __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_
   return -1;
 }
 
-// find_cut from per-pod prefix counts (pc[w] = set bits in words [0, w),
-// pc[nw] = all of them; k_adapt_window<true>): the rank of the K-th set bit
-// from s, a binary search for its word in LDS, one word load.  The same
-// result as find_cut; a round costs a few LDS reads instead of a scan of the
-// bitmap, which is what a batch of pods whose windows converge slowly (a
-// heterogeneous queue: config 1's taints and affinities) pays every round.
-constexpr int32_t kWinPcWords = 127;                 // (nw + 1) uint16 per pod: 64 KB per block
-__device__ __forceinline__ int32_t find_cut_pc(const uint64_t* __restrict__ mask, const uint16_t* pc, int32_t nw,
-                                               int32_t s, int32_t n, int32_t k) {
-  const int32_t total = pc[nw];
-  if (total <= k) return -1;
-  const int32_t ws = s >> 6;
-  const int32_t before = pc[ws] + __popcll(mask[ws] & ((1ull << (s & 63)) - 1));
-  int32_t t = before + k;                            // the global rank of the cut's bit
-  const bool wrap = t >= total;
-  if (wrap) t -= total;
-  int32_t lo = 0, hi = nw - 1;                       // the last word with pc[w] <= t
-  while (lo < hi) {
-    const int32_t mid = (lo + hi + 1) >> 1;
-    if (pc[mid] <= t) lo = mid;
-    else hi = mid - 1;
-  }
-  uint64_t x = mask[lo];
-  for (int32_t q = pc[lo]; q < t; q++) x &= x - 1;
-  const int32_t pos = (lo << 6) + __builtin_ctzll(x);
-  return wrap ? pos + n - s : pos - s;
-}
-
 constexpr int kWindowRounds = 48;
 constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length
 
@@ -213,35 +185,20 @@ constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod fr
 // j): *s_out = pod j's scan start, *cut_out = its cut offset (-1: no cut),
 // *exact_out = pods with exact windows.  false: the batch is empty
 // (block-uniform).  A pure function of the bitmaps and the state.
-// PC: the prefix-count cut search (n_words <= kWinPcWords).
-template <bool PC = false>
 __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
                                              int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
                                              int32_t* cut_out, int32_t* exact_out) {
   __shared__ int64_t sh[kBatchPods / 64];
   __shared__ int32_t s_first;
-  __shared__ uint16_t s_pc[PC ? kBatchPods * (kWinPcWords + 1) : 1];
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
   const int32_t base = st->cursor;
   const int32_t nb = min(kBatchPods, st->end - base);
   if (nb <= 0) return false;
-  uint16_t* const pcj = s_pc + (PC ? j * (kWinPcWords + 1) : 0);   // this pod's counts (its thread only)
-  if (PC && j < nb) {
-    const uint64_t* m = amask + (size_t)j * n_words;
-    int32_t acc = 0;
-#pragma unroll 8
-    for (int32_t w = 0; w < n_words; w++) {
-      pcj[w] = (uint16_t)acc;
-      acc += __popcll(m[w]);
-    }
-    pcj[n_words] = (uint16_t)acc;
-  }
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
   for (int round = 0; round < kWindowRounds; round++) {
-    if constexpr (PC) cut = j < nb ? find_cut_pc(amask + (size_t)j * n_words, pcj, n_words, s, n, k) : -1;
-    else cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
+    cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
     const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
     // exclusive prefix sum of the processed counts
     int64_t x = proc;
@@ -278,19 +235,186 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
 
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
-template <bool PC = false>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ amask, int32_t n_words,
                                                              int32_t n, int32_t k, int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ aexact) {
   int32_t s, cut, exact;
-  if (!window_block<PC>(st, amask, n_words, n, k, &s, &cut, &exact)) return;
+  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact)) return;
   const int j = threadIdx.x;
   if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
     awin[2 * j + 1] = cut;
   }
   if (j == 0) *aexact = exact;
+}
+
+// The exact windows in one ordered walk, no relaxation (clusters up to
+// kWinSeqWords bitmap words; generic runs, whose windows converge slowly under
+// relaxation: a heterogeneous queue's feasible sets are sparse and uneven, so
+// one pod's start error moves every later pod's).  Pod j's scan stops at its
+// (K+1)-th feasible node and pod j+1's scan starts there, so the starts are
+// the walk s_{j+1} = cut node of pod j from s_j.  The bitmaps were written by
+// every XCD and this block runs on one, so each global load costs a trip to
+// the MALL: the 16 waves stage a slice of the pods' bitmaps and their prefix
+// counts (pc[w] = set bits in words [0, w)) in LDS, then wave 0 walks the
+// slice from LDS alone, its loads kAhead pods early.  Per pod the walk is
+// register work: the counts and words sit two per lane, the start's rank is a
+// readlane, the cut's word a ballot over the counts, the cut's bit a ballot
+// over the word's per-bit ranks.
+constexpr int32_t kWinSeqWords = 128;
+constexpr int kWinSeqThreads = 1024;
+
+// One pod of the walk (wave-wide; s, n, k, the result and *cut uniform): the
+// pod's bitmap words w and w + 64 and their prefix counts in lane w's a / pa
+// and b / pb, tot = its feasible nodes.  Returns the next pod's start.
+__device__ __forceinline__ int32_t walk_step(uint64_t a, uint64_t b, int32_t pa, int32_t pb, int32_t tot, bool ina,
+                                             bool inb, int lane, int32_t s, int32_t n, int32_t k, int32_t& cut) {
+  constexpr int32_t kNone = 0x7fffffff;                // a count no rank reaches (lanes past the words)
+  a = ina ? a : 0ull;
+  b = inb ? b : 0ull;
+  pa = ina ? pa : kNone;
+  pb = inb ? pb : kNone;
+  const int32_t total = __builtin_amdgcn_readfirstlane(tot);
+  if (total <= k) {                                    // at most K feasible: all N processed, same start
+    cut = -1;
+    return s;
+  }
+  s = __builtin_amdgcn_readfirstlane(s);               // every value below is scalar
+  const int32_t ws = s >> 6, sb = s & 63;
+  const bool whi = ws >= 64;                           // uniform: the word's half (a selects, no branch)
+  const int32_t pw = __builtin_amdgcn_readlane(whi ? pb : pa, ws & 63);
+  const uint64_t mw = readlane_u64(whi ? b : a, ws & 63);
+  int32_t t = __builtin_amdgcn_readfirstlane(pw + (int32_t)__popcll(mw & ((1ull << sb) - 1)) + k);   // the cut's rank
+  const bool wrap = t >= total;
+  if (wrap) t -= total;
+  const uint64_t ba = __ballot(pa <= t), bb = __ballot(pb <= t);    // pc[0] = 0: ba != 0
+  const int32_t lo = bb ? 127 - (int32_t)__builtin_clzll(bb) : 63 - (int32_t)__builtin_clzll(ba);
+  const bool lhi = lo >= 64;
+  const uint64_t x = readlane_u64(lhi ? b : a, lo & 63);
+  const int32_t r = __builtin_amdgcn_readfirstlane(t - __builtin_amdgcn_readlane(lhi ? pb : pa, lo & 63));
+  // the r-th (0-based) set bit of x: lane l tests bit l and the count of bits 0..l
+  const uint64_t upto = x & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+  const uint64_t hit = __ballot(((x >> lane) & 1ull) && (int32_t)__popcll(upto) == r + 1);
+  const int32_t pos = lo * 64 + (int32_t)__builtin_ctzll(hit);
+  cut = wrap ? pos + n - s : pos - s;
+  return pos;
+}
+#if defined(KSIM_WIN_CLOCKS) && !defined(KSIM_CP_CLOCKS)
+// phase clocks (KSIM_WIN_CLOCKS builds, ksim_get_diag dbg): staging, walk, launches, kernel, pods
+__device__ unsigned long long g_win_dbg[8];
+unsigned long long* cp_clock_buffer() {
+  void* p = nullptr;
+  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_win_dbg));
+  return (unsigned long long*)p;
+}
+#define WIN_CLK(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#define WIN_ADD(slot_, val_) do { if (threadIdx.x == 0) atomicAdd(&g_win_dbg[slot_], (unsigned long long)(val_)); } while (0)
+#else
+#define WIN_CLK(v) do {} while (0)
+#define WIN_ADD(slot_, val_) do {} while (0)
+#endif
+constexpr int32_t kWinSeqLdsWords = 11776;             // staged bitmap words (92 KB) per slice
+
+__global__ __launch_bounds__(kWinSeqThreads) void k_adapt_window_seq(const DevState* __restrict__ st,
+                                                                     const uint64_t* __restrict__ amask,
+                                                                     int32_t n_words, int32_t n, int32_t k,
+                                                                     int32_t* __restrict__ awin,
+                                                                     int32_t* __restrict__ aexact) {
+  __shared__ uint16_t s_pc[kBatchPods][kWinSeqWords + 2];   // [w < n_words] counts, [n_words] the total
+  __shared__ uint64_t s_mk[kWinSeqLdsWords];                // the slice's bitmaps, pod-major
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t base = st->cursor;
+  const int32_t nb = min(kBatchPods, st->end - base);
+  if (nb <= 0) return;                                 // block-uniform
+  const bool ina = lane < n_words, inb = lane + 64 < n_words;
+  const int32_t la = min(lane, n_words - 1), lb = min(lane + 64, n_words - 1);
+  const int32_t slice = min(nb, kWinSeqLdsWords / n_words);
+  struct Ops {
+    uint64_t a, b;
+    int32_t pa, pb, tot;
+  };
+  int32_t s = __builtin_amdgcn_readfirstlane(st->next_start);
+  int32_t my_s = 0, my_cut = -1;                       // lane l: pod (j & ~63) + l's window, stored per 64 pods
+  WIN_CLK(t_start);
+  for (int32_t j_lo = 0; j_lo < nb; j_lo += slice) {
+    const int32_t j_hi = min(nb, j_lo + slice);
+    if (j_lo > 0) __syncthreads();                     // the walk of the previous slice is done
+    WIN_CLK(t_stage);
+    {                                                  // the slice's bitmaps, one coalesced copy
+      const int32_t words = (j_hi - j_lo) * n_words;
+      const uint64_t* src = amask + (size_t)j_lo * n_words;
+      constexpr int kCopy = 4;                         // loads in flight per thread
+      for (int32_t x0 = tid; x0 < words; x0 += kCopy * kWinSeqThreads) {
+        uint64_t v[kCopy];
+#pragma unroll
+        for (int u = 0; u < kCopy; u++) v[u] = src[min(x0 + u * kWinSeqThreads, words - 1)];
+#pragma unroll
+        for (int u = 0; u < kCopy; u++)
+          if (x0 + u * kWinSeqThreads < words) s_mk[x0 + u * kWinSeqThreads] = v[u];
+      }
+    }
+    __syncthreads();
+    if (tid < j_hi - j_lo) {                           // thread t: pod j_lo + t's prefix counts
+      const uint64_t* d = s_mk + (size_t)tid * n_words;
+      uint16_t* pc = s_pc[j_lo + tid];
+      int32_t acc = 0;
+#pragma unroll 8
+      for (int32_t w = 0; w < n_words; w++) {
+        pc[w] = (uint16_t)acc;
+        acc += __popcll(d[w]);
+      }
+      pc[n_words] = (uint16_t)acc;
+    }
+    __syncthreads();
+    WIN_CLK(t_walk);
+    WIN_ADD(0, t_walk - t_stage);
+    if (wv != 0) continue;                             // wave 0 walks the slice
+    auto load = [&](int32_t jj) {
+      jj = min(jj, j_hi - 1);
+      const uint64_t* d = s_mk + (size_t)(jj - j_lo) * n_words;
+      return Ops{d[la], d[lb], (int32_t)s_pc[jj][la], (int32_t)s_pc[jj][lb], (int32_t)s_pc[jj][n_words]};
+    };
+    auto step = [&](const Ops& cur, int32_t j) {
+      int32_t cut;
+      const int32_t next = walk_step(cur.a, cur.b, cur.pa, cur.pb, cur.tot, ina, inb, lane, s, n, k, cut);
+      if (lane == (j & 63)) {
+        my_s = s;
+        my_cut = cut;
+      }
+      if ((j & 63) == 63 || j == nb - 1) {             // uniform: this group of 64 pods is done
+        const int32_t g = j & ~63;
+        if (lane <= j - g) {
+          awin[2 * (g + lane)] = my_s;
+          awin[2 * (g + lane) + 1] = my_cut;
+        }
+      }
+      s = __builtin_amdgcn_readfirstlane(next);
+    };
+    // four register sets in rotation, each refilled kAhead pods ahead
+    Ops o0 = load(j_lo), o1 = load(j_lo + 1), o2 = load(j_lo + 2), o3 = load(j_lo + 3);
+    int32_t j = j_lo;
+    for (; j + 3 < j_hi; j += 4) {
+      step(o0, j);
+      o0 = load(j + 4);
+      step(o1, j + 1);
+      o1 = load(j + 5);
+      step(o2, j + 2);
+      o2 = load(j + 6);
+      step(o3, j + 3);
+      o3 = load(j + 7);
+    }
+    if (j < j_hi) step(o0, j++);
+    if (j < j_hi) step(o1, j++);
+    if (j < j_hi) step(o2, j++);
+    WIN_CLK(t_done);
+    WIN_ADD(1, t_done - t_walk);
+  }
+  if (tid == 0) *aexact = nb;
+  WIN_CLK(t_end);
+  WIN_ADD(2, 1);
+  WIN_ADD(3, t_end - t_start);
+  WIN_ADD(4, nb);
 }
 
 // Clusters up to this many bitmap words run the window scan inside k_adapt_top
@@ -855,18 +979,18 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   k_adapt_mask_ns<<<dim3((n_words + 3) / 4, (kBatchPods + mp - 1) / mp), 256, 0, stream>>>(a.c, a.P, a.dbp, a.st,
                                                                                           a.s.amask, n_words, mp);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  // generic runs on small clusters: the prefix-count windows as their own launch
-  const bool win_pc = !a.fast && n_words <= kWinPcWords;
-  const bool win_fused = !win_pc && k < kTopWideK && n_words <= kWinFusedWords;
-  if (win_pc)
-    k_adapt_window<true><<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  // generic runs on small clusters: the exact ordered walk as its own launch
+  const bool win_seq = !a.fast && n_words <= kWinSeqWords;
+  const bool win_fused = !win_seq && k < kTopWideK && n_words <= kWinFusedWords;
+  if (win_seq)
+    k_adapt_window_seq<<<1, kWinSeqThreads, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   else if (!win_fused)
     k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
-  // PC windows (generic runs): 1,024 threads per pod as for long windows
-  if (k >= kTopWideK || win_pc) {
+  // ordered-walk windows (generic runs): 1,024 threads per pod as for long windows
+  if (k >= kTopWideK || win_seq) {
     if (a.fast) TOP(true, 1024, false);
     else TOP(false, 1024, false);
   } else if (win_fused) {

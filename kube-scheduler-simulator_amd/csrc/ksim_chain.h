@@ -37,7 +37,7 @@ constexpr int kChainDirect = 8192;
 constexpr int kChainHoldSlots = kHashSlots > kChainDirect ? kHashSlots : kChainDirect;
 struct ChainLds {
   int32_t key[kHashSlots];                     // node id in the slot, -1 = empty (hash mode)
-  int32_t hold[kChainHoldSlots];               // lowest pod index holding the slot this round
+  int32_t hold[2][kChainHoldSlots];            // per round parity: lowest pod index holding the slot
   int16_t rep[kBatchPods][kTopT];              // slot of each list entry
   int32_t first[2], cut;                      // first: one slot per round parity (see the round loop)
 };
@@ -54,7 +54,6 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
                                             int32_t* nchain_out, unsigned long long* __restrict__ dbg,
                                             int32_t nb_cap = kBatchPods, int32_t direct_n = 0) {
   int32_t* const s_key = L.key;
-  int32_t* const s_hold = L.hold;
   int32_t& s_cut = L.cut;
   // phase clock (100 MHz realtime): dbg[0] setup, dbg[1] rounds, dbg[2] epilogue, dbg[3] launches, dbg[4] rounds run
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -76,15 +75,10 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   // this pod's slots in registers (selects below, never a dynamic index)
   int32_t rep[kTopT];
   if (direct_n > 0 && direct_n <= kChainDirect) {   // block-uniform: the slot is the node id
-    for (int x = i; x < direct_n; x += kBatchPods) s_hold[x] = kBatchPods;
 #pragma unroll
     for (int e = 0; e < kTopT; e++) rep[e] = e < cnt ? key_node(lst[e]) : -1;
-    __syncthreads();
   } else {
-    for (int x = i; x < kHashSlots; x += kBatchPods) {
-      s_key[x] = -1;
-      s_hold[x] = kBatchPods;
-    }
+    for (int x = i; x < kHashSlots; x += kBatchPods) s_key[x] = -1;
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < kTopT; e++) {
@@ -105,36 +99,44 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
 #pragma unroll
     for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
   }
+  // only the slots the lists name are ever read: each pod clears its own (a
+  // slot shared by several lists is cleared by each, to the same value)
+#pragma unroll
+  for (int e = 0; e < kTopT; e++)
+    if (e < cnt) L.hold[0][rep[e]] = L.hold[1][rep[e]] = kBatchPods;
+  __syncthreads();
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
+  int32_t pra = -1;                            // the slot this pod registered last round
   int first = kBatchPods, rounds = 0;
   for (; rounds < kChainRounds; rounds++) {
-    // round r reports in first[r & 1].  The other slot was read at the end of
-    // round r - 1, by every thread before the first barrier below, so it is
-    // reset after that barrier (resetting the current slot at the top of the
-    // round raced with slower waves still reading the previous round's flag).
+    // Round r registers in hold[r & 1] and reports in first[r & 1], with two
+    // barriers.  The other parity's table and flag were last read in round
+    // r - 1, by every thread before this round's first barrier, so they are
+    // reset after it, for round r + 1 (resetting the current flag at the top
+    // of the round raced with slower waves still reading the previous round's).
     const int par = rounds & 1;
     int32_t ra = 0;
 #pragma unroll
     for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
-    if (a >= 0) atomicMin(&s_hold[ra], i);
+    if (a >= 0) atomicMin(&L.hold[par][ra], i);
     __syncthreads();
     CHAIN_DELAY(1);                            // a middle wave late after the first barrier
+    if (pra >= 0) L.hold[par ^ 1][pra] = kBatchPods;
     if (i == 0) L.first[par ^ 1] = kBatchPods;
     // every entry's holder at once, then the first one not held by an earlier pod
     int32_t held[kTopT];
 #pragma unroll
-    for (int e = 0; e < kTopT; e++) held[e] = e < cnt ? s_hold[rep[e]] : 0;
+    for (int e = 0; e < kTopT; e++) held[e] = e < cnt ? L.hold[par][rep[e]] : 0;
     int na = -1;
 #pragma unroll
     for (int e = kTopT - 1; e >= 0; e--)
       if (e < cnt && held[e] >= i) na = e;
-    __syncthreads();
-    if (a >= 0) s_hold[ra] = kBatchPods;                // reset for the next round
-    {                                                   // the wave's first changed pod: one LDS atomic per wave
+    {                                          // the wave's first changed pod: one LDS atomic per wave
       const uint64_t chg = __ballot(na != a);
       if (chg && (threadIdx.x & 63) == 0) atomicMin(&L.first[par], (int)(threadIdx.x & ~63u) + __builtin_ctzll(chg));
     }
+    pra = a >= 0 ? ra : -1;
     a = na;
     __syncthreads();
     CHAIN_DELAY((int)(blockDim.x >> 6) - 1);   // the last wave reads the flag late

@@ -54,10 +54,23 @@ def _cases(kind):
                       containers=[Container({"cpu": f"{int(rng.integers(10, 300)) * 100}m",
                                              "memory": f"{int(rng.integers(2, 40))}Gi"})]) for i in range(120)]
         return cluster, encode_pods(cluster, pods_o), table, [p.priority for p in pods_o]
+    if kind == "replicaset":
+        # ReplicaSet / Service / StatefulSet-owned pods under the System default
+        # spreading (requireAllTopologies = false) on nodes missing zone or
+        # hostname labels
+        from ksim.topology import SpreadDefaults
+        from test_spread_defaults import WORKLOADS, mixed_nodes, workload_pods
+        nodes = mixed_nodes(300, seed=4)
+        bound = workload_pods(600, seed=12, bound_nodes=[n.name for n in nodes])
+        cluster, _ = encode_cluster(nodes, bound)
+        pods = encode_pods(cluster, workload_pods(300, seed=13),
+                           spread=SpreadDefaults(profile.PodTopologySpreadArgs(), *WORKLOADS))
+        assert (pods.pods["topo_flags"] & abi.POD_PTS_SYSTEM_DEFAULT).any()
+        return cluster, pods, None, None
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["config1", "prefilter", "config3", "preempt"])
+@pytest.mark.parametrize("kind", ["config1", "prefilter", "config3", "preempt", "replicaset"])
 @pytest.mark.parametrize("seed", [1, 2])
 def test_framework_driven_cycles(kind, seed):
     cluster, pods, table, prio = _cases(kind)

@@ -273,7 +273,7 @@ def build(cfg: int, args, rank: int, world: int):
     raise SystemExit(f"unknown config {cfg}")
 
 
-def kernel_table(kt, kt_pods, n_pods, ms_per_step, knodes, n_norm, geom, sharded) -> dict:
+def kernel_table(kt, kt_pods, n_pods, ms_per_step, knodes, n_norm, geom, sharded, concurrent=False) -> dict:
     """Per-kernel times that add up to the step.  ksim_time_kernels brackets
     every launch with HIP events on the engine's stream, run eagerly, which
     adds a few microseconds per launch that the graph-replayed step does not
@@ -282,15 +282,21 @@ def kernel_table(kt, kt_pods, n_pods, ms_per_step, knodes, n_norm, geom, sharded
     times), so sum(avg_ms x launches) reconciles with ms_per_step (exactly for
     unsharded runs, whose step is device time; the rocprof summaries under
     profiles/ give the unscaled kernel durations).  ``share`` is the fraction
-    of the step."""
+    of the step.  ``concurrent`` (config 5: many weight vectors per step on
+    concurrent streams): the table is one vector's run, event times as
+    measured (a step holds no single vector's device time to reconcile to)."""
     total = sum(v[0] * v[1] for v in kt.values())
     target = ms_per_step * kt_pods / max(n_pods, 1)
-    scale = target / total if total > 0 and not sharded else 1.0
+    scale = target / total if total > 0 and not sharded and not concurrent else 1.0
     out = {}
     for k, (ms, n) in kt.items():
         a = ms * scale
         out[k] = {"avg_ms": a, "avg_ms_events": ms, "launches": n, "share": (ms * n / total) if total else None,
                   "alg_GBps": kernel_alg_bytes(k, knodes, n_norm, geom) / (a * 1e-3) / 1e9}
+    if concurrent:
+        out["_reconciled"] = {"per": "one weight vector, its own run (event times)", "timed_pods": kt_pods,
+                              "sum_ms": sum(v["avg_ms"] * v["launches"] for k, v in out.items())}
+        return out
     out["_reconciled"] = {"sum_ms_for_timed_pods": sum(v["avg_ms"] * v["launches"] for k, v in out.items()),
                           "timed_pods": kt_pods, "step_ms_scaled_to_timed_pods": target, "event_scale": scale}
     return out
@@ -302,9 +308,14 @@ def roofline_entry(dominant, achieved, traffic, alg, avg_ms, timing, knodes, by_
     sweep an L2-resident node table (PMC HBM traffic far below the 112 B per
     evaluation), so their algorithmic-HBM fraction can exceed 1 and bounds
     nothing; that figure is kept under "hbm", the PMC bytes under "traffic"."""
-    hbm = {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-           "alg_bytes_per_launch": alg,
-           "note": "algorithmic bytes = 112 B per pod x node evaluation (SURVEY 8(d))"}
+    # the HBM side of a VALU-bound kernel: the PMC bytes it moves per launch
+    # over its launch time; the algorithmic rate (112 B per evaluation, from
+    # L2 / MALL mostly) is no HBM utilisation and carries no fraction
+    hbm = {"achieved": (traffic / (avg_ms * 1e-3) / 1e9) if traffic else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": (traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+           "source": "PMC traffic (profiles/traffic.json) over this run's launch time",
+           "alg_bytes_per_launch": alg, "alg_rate_GBps": achieved,
+           "note": "algorithmic bytes = 112 B per pod x node evaluation (SURVEY 8(d)), served from L2 / MALL"}
     common = {"kernel": dominant, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
               "avg_launch_ms": avg_ms, "timing": timing, "kernel_nodes": knodes, "dominant_by_time": by_time}
     if valu is None:
@@ -317,13 +328,128 @@ def roofline_entry(dominant, achieved, traffic, alg, avg_ms, timing, knodes, by_
                      "run's launch time")}
 
 
+def bench_fw(args, out):
+    """--mode fw: the drop-in's per-pod cost.  The framework-driven calls the
+    Go adapter makes for one scheduling cycle (integration/go/engine/plugins.go):
+    ksim_fw_prefilter (Filter of every node, F x N answers copied back),
+    the framework's feasible list (here the sequential worker's first K in
+    scan order from nextStartNodeIndex), ksim_fw_score over it (S x N raw
+    scores copied back), ksim_fw_normalize per NormalizeScore plugin, the
+    max total, ksim_assume; output buffers reused as the adapter would.
+    Config 1's distribution at 100 nodes (the reference's own config 1) and
+    5,000 nodes; the oracle's ksim_oracle_fw_* calls beside it on the same
+    sequence (CPU, one thread).  One JSON line; host (Python ctypes) overhead
+    included in ``us_per_cycle``, the C calls alone in ``us_in_calls``."""
+    import ctypes
+    import time
+    import numpy as np
+    from ksim import abi, engine, gen, profile
+    from ksim.wrapped import HAS_NORMALIZE
+    from oracle.oracle import Oracle, lib as olib
+    rows = []
+    for n_nodes, n_pods in ((100, 1000), (5000, 3000)):
+        cluster, pods = gen.config1(n_nodes=n_nodes, n_pods=n_pods)
+        sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+        prof = profile.compile_profile(sp)
+        snames = [p.name for p in sp.score_plugins()]
+        nslots = [k for k, nm in enumerate(snames) if nm in HAS_NORMALIZE]
+        N = cluster.n_nodes
+        K = profile.num_feasible_nodes_to_find(N, 0)
+        ps = pods.pod_set()
+
+        def run(kind, count):
+            if kind == "engine":
+                e = engine.Engine(0)
+                e.set_profile(prof)
+                e.set_cluster(cluster.copy_state())
+                L, h = e.L, e.h
+                pre = lambda i, out: L.ksim_fw_prefilter(h, ctypes.byref(ps), i, ctypes.byref(out))
+                score = lambda arr, out: L.ksim_fw_score(h, arr.ctypes.data_as(ctypes.c_void_p), arr.size,
+                                                         ctypes.byref(out))
+                norm = lambda k, arr, sc, o: L.ksim_fw_normalize(h, k, arr.ctypes.data_as(ctypes.c_void_p),
+                                                                 sc.ctypes.data_as(ctypes.c_void_p), arr.size,
+                                                                 o.ctypes.data_as(ctypes.c_void_p))
+                assume = lambda i, node: L.ksim_assume(h, ctypes.byref(ps), i, node)
+            else:
+                e = Oracle(cluster.copy_state(), prof)
+                O, h = olib(), e.h
+                pre = lambda i, out: O.ksim_oracle_fw_filter(h, ctypes.byref(ps), i, ctypes.byref(out))
+                score = lambda arr, out: O.ksim_oracle_fw_score(h, ctypes.byref(ps), cur[0],
+                                                               arr.ctypes.data_as(ctypes.c_void_p), arr.size,
+                                                               ctypes.byref(out))
+                norm = lambda k, arr, sc, o: O.ksim_oracle_fw_normalize(h, k, arr.ctypes.data_as(ctypes.c_void_p),
+                                                                        sc.ctypes.data_as(ctypes.c_void_p),
+                                                                        arr.size, o.ctypes.data_as(ctypes.c_void_p))
+                assume = lambda i, node: O.ksim_oracle_assume(h, ctypes.byref(ps), i, node, 1)
+            cur = [0]
+            fb, sb = abi.EvalBuffers(N, prof.n_score), abi.EvalBuffers(N, prof.n_score)
+            nout = np.zeros(N, np.int64)
+            ns, in_calls, bound = 0, 0.0, 0
+            split = {"prefilter": 0.0, "score": 0.0, "normalize": 0.0, "assume": 0.0}
+            t0 = time.perf_counter()
+            for i in range(count):
+                cur[0] = i
+                c0 = time.perf_counter()
+                rc = pre(i, fb.out)
+                split["prefilter"] += time.perf_counter() - c0
+                in_calls += time.perf_counter() - c0
+                if rc != 0:
+                    raise RuntimeError(f"{kind} fw_prefilter rc {rc}")
+                order = np.roll(np.arange(N, dtype=np.int32), -ns)
+                feas = order[fb.fail_plugin[order] == abi.PASSED]
+                lst = np.ascontiguousarray(feas[:K])
+                proc = int(np.nonzero(order == feas[K])[0][0]) if feas.size > K else N
+                ns = (ns + proc) % N
+                if lst.size == 0:
+                    continue
+                node = int(lst[0])
+                if lst.size > 1:
+                    c0 = time.perf_counter()
+                    rc = score(lst, sb.out)
+                    c1 = time.perf_counter()
+                    for k in nslots:
+                        rc |= norm(k, lst, np.ascontiguousarray(sb.raw[k][lst]), nout)
+                    c2 = time.perf_counter()
+                    split["score"] += c1 - c0
+                    split["normalize"] += c2 - c1
+                    in_calls += c2 - c0
+                    if rc != 0:
+                        raise RuntimeError(f"{kind} fw_score / normalize rc {rc}")
+                    node = int(lst[int(np.argmax(sb.total[lst]))])
+                c0 = time.perf_counter()
+                assume(i, node)
+                split["assume"] += time.perf_counter() - c0
+                in_calls += time.perf_counter() - c0
+                bound += 1
+            dt = time.perf_counter() - t0
+            return {"us_per_cycle": dt / count * 1e6, "us_in_calls": in_calls / count * 1e6, "cycles": count,
+                    "bound": bound, "us_per_call": {k: v / count * 1e6 for k, v in split.items()}}
+
+        run("engine", min(200, n_pods))                      # warm-up (graphs, first launches)
+        e_r = run("engine", n_pods)
+        o_r = run("oracle", min(n_pods, 1000 if n_nodes <= 100 else 300))
+        rows.append({"nodes": n_nodes, "engine": e_r, "oracle_cpu_1thread": o_r,
+                     "engine_vs_oracle_in_calls": o_r["us_in_calls"] / e_r["us_in_calls"]})
+    line = {"metric": "framework_driven_cycle_us", "value": rows[-1]["engine"]["us_per_cycle"],
+            "unit": "us per pod cycle (5000 nodes)", "higher_is_better": False, "n_gpus": 1,
+            "config": {"workload": "config-1 distribution, framework-driven compat cycle (drop-in)",
+                       "parallelism": "single GPU"},
+            "rows": rows,
+            "note": "per cycle: fw_prefilter + fw_score + fw_normalize per NormalizeScore plugin + assume, "
+                    "with the F x N / S x N copies back to host memory; Python ctypes glue included in "
+                    "us_per_cycle"}
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--mode", choices=["p100", "adapt"], default="p100")
+    ap.add_argument("--mode", choices=["p100", "adapt", "fw"], default="p100",
+                    help="fw: the drop-in's framework-driven per-pod cycle (bench_fw)")
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=50000)
     ap.add_argument("--nodes-per-gpu", type=int, default=5000)
@@ -370,6 +496,9 @@ def main():
     from ksim import engine, gen, profile, shard
 
     engine.lib()
+    if args.mode == "fw":
+        bench_fw(args, out)
+        return
     cfg = args.config
     cluster, pods, sp, desc, sharded, scaling = build(cfg, args, rank, world)
     prof = profile.compile_profile(sp)
@@ -498,14 +627,17 @@ def main():
     kt_pods = min(pods.n_pods, 50000 if cfg != 3 else 2000)
     kt = keng.time_kernels(0, kt_pods)
     by_time = max(kt, key=lambda k: kt[k][0] * kt[k][1])      # largest share of device time
-    dominant = next((k for k in EVAL_KERNELS if k in kt), by_time)
+    dominant = by_time                                        # the roofline prices the by-time dominant kernel
     n_norm = sum(1 for p in sp.score_plugins()
                  if p.name in ("TaintToleration", "NodeAffinity", "PodTopologySpread", "InterPodAffinity"))
     alg = kernel_alg_bytes(dominant, knodes, n_norm, geom)
     # the evaluation kernel's mean duration: HIP events around back-to-back
     # launches on the engine's stream (no event records between launches,
     # which add 2-4 us each in the per-kernel table above)
-    avg_ms, timing = kt[dominant][0], "per-kernel HIP events inside the run"
+    ktab = kernel_table(kt, kt_pods, pods.n_pods, elapsed / args.steps * 1e3, knodes, n_norm, geom, sharded,
+                        concurrent=cfg == 5)
+    avg_ms, timing = ktab[dominant]["avg_ms"], ("per-kernel HIP events inside the run, reconciled with the "
+                                                "graph-replayed step (kernels table)")
     try:
         name, ms = keng.time_eval(0, 200)
         if name == dominant:
@@ -528,7 +660,8 @@ def main():
                 "valu_insts_per_eval_lane": ve.get("valu_insts_per_eval_lane"), "source": ve.get("source")}
         act, wcyc, waves = (ve.get("valu_active_quad_cycles_per_launch"), ve.get("wave_quad_cycles_per_launch"),
                             ve.get("waves_per_launch"))
-        if act and wcyc and waves:
+        fills = ve.get("waves_per_launch", 0) >= 256 * 4     # at least one wave per SIMD of the chip
+        if act and wcyc and waves and fills:
             # SQ_ACTIVE_INST_VALU per SIMD over the mean wave lifetime (SQ_WAVE_CYCLES / SQ_WAVES): the
             # share of the launch its SIMDs spend issuing VALU work (1,024 SIMDs, every one holding waves
             # of the launch for its whole duration; a 64-bit or f64 op holds the SIMD longer than the
@@ -557,8 +690,7 @@ def main():
                    "parallelism": (f"node-sharded over {world} GPUs (RCCL)" if sharded else
                                    f"{world} independent replicas" if world > 1 else "single GPU")},
         "pods_per_s": cycles / elapsed,
-        "kernels": kernel_table(kt, kt_pods, pods.n_pods, elapsed / args.steps * 1e3, knodes, n_norm, geom,
-                                sharded),
+        "kernels": ktab,
         "batch_stats": {"batches": st.batches, "truncations": st.truncations,
                         "perpod_cycles": st.perpod_cycles},
         "roofline": roofline_entry(dominant, achieved, traffic, alg, avg_ms, timing, knodes, by_time, valu),

@@ -69,6 +69,14 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// A device buffer reused across calls, grown (never shrunk) on demand: the
+// per-call uploads of the framework-driven calls (one pod, its terms and uses)
+// without a hipMalloc / hipFree pair per call.
+struct DevArena {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
 }  // namespace
 
 struct ksim_handle {
@@ -138,8 +146,12 @@ struct ksim_handle {
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
   // compat-mode single pod
-  std::vector<DevBuf> pod1_bufs;
-  std::vector<DevBuf> nom_bufs;         // a nominated pod (ksim_fw_filter_nominated)
+  DevArena pod1_arena;                  // the single-pod uploads (upload_single)
+  DevArena nom_arena;                   // a nominated pod (ksim_fw_filter_nominated)
+  void* pin = nullptr;                  // pinned host staging for the per-call uploads
+  size_t pin_cap = 0;
+  void* pout = nullptr;                 // pinned host staging for the per-call results
+  size_t pout_cap = 0;
   // DefaultPreemption: bound pods per node in importance order
   std::vector<DevBuf> pre_bufs;
   std::vector<DevBuf> pre_nom_bufs;     // ksim_preempt_nominated's group requests
@@ -157,9 +169,14 @@ struct ksim_handle {
   bool fw_pending = false, fw_scored = false, fw_dom_dirty = false, fw_topo = false;
   int32_t fw_ns = 0;
   std::vector<uint8_t> fw_fail;
+  // ksim_fw_score's list and answers, host side: a NormalizeScore over that
+  // list with the raw scores it returned is answered from here
+  std::vector<int32_t> fw_list;
+  std::vector<int64_t> fw_raw, fw_norm;         // [slot][list position]
   int32_t* fw_nodes = nullptr;     // device [n]
   int64_t* fw_vals = nullptr;      // device [n]
   int64_t* fw_out = nullptr;       // device [n]
+  int64_t* fw_comp = nullptr;      // device: ksim_fw_score's answers for the listed nodes (k_fw_gather)
 
   // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
   int32_t shard_base = 0, shard_total = 0;
@@ -609,6 +626,8 @@ int fw_abandon(ksim_handle* h) {
   if (h->fw_dom_dirty && h->sc.dom)
     HIPCHK(h, hipMemsetAsync(h->sc.dom, 0, 8 * (size_t)KSIM_MAX_USES * h->dc.vmax, h->stream));
   h->fw_dom_dirty = h->fw_pending = h->fw_scored = false;
+  h->fw_list.clear();
+  h->fw_raw.clear();
   return KSIM_OK;
 }
 
@@ -1594,10 +1613,12 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->lazy_bufs);
   free_bufs(h->stab_bufs);
   free_bufs(h->pod_bufs);
-  free_bufs(h->pod1_bufs);
+  if (h->pod1_arena.p) (void)hipFree(h->pod1_arena.p);
+  if (h->nom_arena.p) (void)hipFree(h->nom_arena.p);
+  if (h->pin) (void)hipHostFree(h->pin);
+  if (h->pout) (void)hipHostFree(h->pout);
   free_bufs(h->pre_bufs);
   free_bufs(h->pre_nom_bufs);
-  free_bufs(h->nom_bufs);
   if (h->d_chosen) (void)hipFree(h->d_chosen);
   if (h->st) (void)hipFree(h->st);
   if (h->d_prof) (void)hipFree(h->d_prof);
@@ -1922,6 +1943,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(h->fw_nodes, int32_t*, 4 * N);
   SCR(h->fw_vals, int64_t*, 8 * N);
   SCR(h->fw_out, int64_t*, 8 * N);
+  SCR(h->fw_comp, int64_t*, (16 * (size_t)KSIM_MAX_SCORE + 9) * N);
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
@@ -2255,9 +2277,51 @@ static void single_pod_set(const ksim_pod_set* ps, int32_t i, ksim_pod& pod, std
   copy_terms(pod.vz_first, pod.vz_count);
 }
 
-// Upload one pod (re-based) as a device pod set of its own.
-static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P,
-                         std::vector<DevBuf>& bufs) {
+static int arena_reserve(ksim_handle* h, DevArena& a, size_t bytes) {
+  if (bytes <= a.cap) return KSIM_OK;
+  if (a.p) (void)hipFree(a.p);
+  a.p = nullptr;
+  a.cap = 0;
+  const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
+  const hipError_t e = hipMalloc(&a.p, cap);
+  if (e != hipSuccess) return hip_fail(h, e, "hipMalloc (arena)");
+  a.cap = cap;
+  return KSIM_OK;
+}
+
+// The handle's pinned staging (the stream must be idle: a copy from it may be
+// in flight otherwise).
+static int pin_reserve(ksim_handle* h, size_t bytes) {
+  if (bytes <= h->pin_cap) return KSIM_OK;
+  if (h->pin) (void)hipHostFree(h->pin);
+  if (h->pout) (void)hipHostFree(h->pout);
+  h->pin = nullptr;
+  h->pin_cap = 0;
+  const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
+  const hipError_t e = hipHostMalloc(&h->pin, cap, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (staging)");
+  h->pin_cap = cap;
+  return KSIM_OK;
+}
+
+// The results' pinned staging (callers sync before reading it).
+static int pout_reserve(ksim_handle* h, size_t bytes) {
+  if (bytes <= h->pout_cap) return KSIM_OK;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (h->pout) (void)hipHostFree(h->pout);
+  h->pout = nullptr;
+  h->pout_cap = 0;
+  const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
+  const hipError_t e = hipHostMalloc(&h->pout, cap, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (results)");
+  h->pout_cap = cap;
+  return KSIM_OK;
+}
+
+// Upload one pod (re-based) as a device pod set of its own: every piece packed
+// into the pinned staging, one copy into the arena (valid until the arena's
+// next upload).
+static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P, DevArena& arena) {
   ksim_pod pod;
   std::vector<ksim_label_expr> ex;
   std::vector<ksim_term> tm;
@@ -2266,32 +2330,45 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   std::vector<int32_t> nn;
   single_pod_set(ps, pod_index, pod, ex, tm, us, ad, nn);
   mark_unique(h, us.data(), us.size());
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  free_bufs(bufs);
-  P = DevPods{};
-  void* p = nullptr;
-  int rc;
-  if ((rc = upload(h, bufs, &pod, sizeof(pod), &p))) return rc;
-  P.pods = (const ksim_pod*)p;
-  if ((rc = upload(h, bufs, ex.data(), ex.size() * sizeof(ksim_label_expr), &p))) return rc;
-  P.exprs = (const ksim_label_expr*)p;
-  if ((rc = upload(h, bufs, tm.data(), tm.size() * sizeof(ksim_term), &p))) return rc;
-  P.terms = (const ksim_term*)p;
-  if ((rc = upload(h, bufs, nn.data(), 4 * nn.size(), &p))) return rc;
-  P.nn = (const int32_t*)p;
-  P.n_nn = (int32_t)nn.size();
   int32_t bflag[4] = {0, 0, 0, 0};
   for (const auto& u : us)
     if (use_registers_values(u)) bflag[0] |= kPodRegistersValues;
-  if ((rc = upload(h, bufs, bflag, sizeof(bflag), &p))) return rc;
-  P.bflags = (const int32_t*)p;
   const PodPlan plan = make_plan(h, pod, us.data());
-  if ((rc = upload(h, bufs, &plan, sizeof(plan), &p))) return rc;
-  P.plans = (const PodPlan*)p;
-  if ((rc = upload(h, bufs, us.data(), us.size() * sizeof(ksim_topo_use), &p))) return rc;
-  P.uses = (const ksim_topo_use*)p;
-  if ((rc = upload(h, bufs, ad.data(), ad.size() * sizeof(ksim_class_add), &p))) return rc;
-  P.adds = (const ksim_class_add*)p;
+  struct Piece {
+    const void* src;
+    size_t bytes;
+    size_t off;
+  };
+  Piece pc[8] = {{&pod, sizeof(pod), 0},
+                 {ex.data(), ex.size() * sizeof(ksim_label_expr), 0},
+                 {tm.data(), tm.size() * sizeof(ksim_term), 0},
+                 {nn.data(), 4 * nn.size(), 0},
+                 {bflag, sizeof(bflag), 0},
+                 {&plan, sizeof(plan), 0},
+                 {us.data(), us.size() * sizeof(ksim_topo_use), 0},
+                 {ad.data(), ad.size() * sizeof(ksim_class_add), 0}};
+  size_t total = 0;
+  for (auto& x : pc) {
+    x.off = total;
+    total += (std::max<size_t>(x.bytes, 16) + 63) & ~(size_t)63;
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));     // the staging and the arena are free again
+  int rc;
+  if ((rc = pin_reserve(h, total)) || (rc = arena_reserve(h, arena, total))) return rc;
+  for (auto& x : pc)
+    if (x.bytes) std::memcpy((char*)h->pin + x.off, x.src, x.bytes);
+  HIPCHK(h, hipMemcpyAsync(arena.p, h->pin, total, hipMemcpyHostToDevice, h->stream));
+  char* d = (char*)arena.p;
+  P = DevPods{};
+  P.pods = (const ksim_pod*)(d + pc[0].off);
+  P.exprs = (const ksim_label_expr*)(d + pc[1].off);
+  P.terms = (const ksim_term*)(d + pc[2].off);
+  P.nn = (const int32_t*)(d + pc[3].off);
+  P.n_nn = (int32_t)nn.size();
+  P.bflags = (const int32_t*)(d + pc[4].off);
+  P.plans = (const PodPlan*)(d + pc[5].off);
+  P.uses = (const ksim_topo_use*)(d + pc[6].off);
+  P.adds = (const ksim_class_add*)(d + pc[7].off);
   P.n_pods = 1;
   P.n_exprs = (int32_t)ex.size();
   P.n_terms = (int32_t)tm.size();
@@ -2307,7 +2384,7 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
 }
 
 static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P) {
-  return upload_single(h, ps, pod_index, P, h->pod1_bufs);
+  return upload_single(h, ps, pod_index, P, h->pod1_arena);
 }
 
 // Copy one compat cycle's per-node outputs and scalars to the caller.
@@ -2440,6 +2517,8 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   if ((rc = validate_pod(h, ps, pod_index))) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   h->ext_pending = false;
+  h->fw_list.clear();                // a new cycle: no normalization answered from the last one
+  h->fw_raw.clear();
   if ((rc = upload_single(h, ps, pod_index, h->pod1))) return rc;
   if ((rc = set_run(h, 0, 1))) return rc;
   // the two topology flags are OR-ed by the PreFilter pass and reset by a bind,
@@ -2452,8 +2531,18 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   h->fw_topo = p.use_count > 0;
   const size_t N = (size_t)h->dc.n;
   h->fw_fail.resize(N);
-  HIPCHK(h, hcopy(h, h->fw_fail.data(), h->sc.fail, N, hipMemcpyDeviceToHost));
-  if (out->fail_detail) HIPCHK(h, hcopy(h, out->fail_detail, h->sc.detail, 4 * N, hipMemcpyDeviceToHost));
+  // the results into pinned staging, one synchronization: next_start, the
+  // filter codes, the details
+  const size_t o_fail = 64, o_det = 64 + ((N + 63) & ~(size_t)63);
+  if ((rc = pout_reserve(h, o_det + 4 * N))) return rc;
+  char* po = (char*)h->pout;
+  HIPCHK(h, hipMemcpyAsync(po, &h->st->next_start, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(po + o_fail, h->sc.fail, N, hipMemcpyDeviceToHost, h->stream));
+  if (out->fail_detail)
+    HIPCHK(h, hipMemcpyAsync(po + o_det, h->sc.detail, 4 * N, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::memcpy(h->fw_fail.data(), po + o_fail, N);
+  if (out->fail_detail) std::memcpy(out->fail_detail, po + o_det, 4 * N);
   int32_t ns = h->dc.n;
   if (p.flags & KSIM_POD_NODE_NAMES) ns = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 0 : p.nn_count;
   int32_t nf = 0;
@@ -2463,7 +2552,7 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
     strip_fail_errors(out->fail_plugin, N);
   }
   int32_t next = 0;
-  HIPCHK(h, hcopy(h, &next, &h->st->next_start, sizeof(next), hipMemcpyDeviceToHost));
+  std::memcpy(&next, po, sizeof(next));
   const bool unknown = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) != 0;
   out->chosen = unknown ? KSIM_CHOSEN_ERROR : -1;
   out->status = unknown ? KSIM_STATUS_ERROR : 0;
@@ -2518,7 +2607,7 @@ int ksim_fw_filter_nominated(ksim_handle* h, const ksim_pod_set* nps, int32_t n_
     for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
       DevPods P;
       int r;
-      if ((r = upload_single(h, nps, j, P, h->nom_bufs))) return r;
+      if ((r = upload_single(h, nps, j, P, h->nom_arena))) return r;
       launch_assume(h->dc, P, 0, nodes[k], sign, h->stream);
       HIPCHK(h, hipGetLastError());
     }
@@ -2547,35 +2636,74 @@ int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out
   if (!out || n < 0 || (n > 0 && !nodes)) return set_err(h, KSIM_E_INVALID, "bad node list");
   if (!h->fw_pending) return set_err(h, KSIM_E_INVALID, "ksim_fw_score without ksim_fw_prefilter");
   const size_t N = (size_t)h->dc.n;
-  // the list: feasible nodes of the filter pass, each once
-  std::vector<uint8_t> out_of_list(N, 1);
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));    // the upload staging is free again
+  const size_t o_list = (64 + N + 63) & ~(size_t)63;
+  if ((rc = pin_reserve(h, o_list + 4 * (size_t)n))) return rc;
+  // the list: feasible nodes of the filter pass, each once (the mask in staging)
+  uint8_t* out_of_list = (uint8_t*)h->pin + 64;
+  std::memset(out_of_list, 1, N);
   for (int32_t j = 0; j < n; j++) {
     const int32_t x = nodes[j];
     if (x < 0 || (size_t)x >= N || h->fw_fail[x] != KSIM_PASSED || !out_of_list[x])
       return set_err(h, KSIM_E_INVALID, "node list: not a feasible node of the filter pass, or repeated");
     out_of_list[x] = 0;
   }
-  HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(h->ext_fail, out_of_list.data(), N, hipMemcpyHostToDevice, h->stream));
+  std::memcpy((char*)h->pin + o_list, nodes, 4 * (size_t)n);
   // the window of the filter pass covers the whole scan set (k_window's
   // extender branch keeps it and drops the unlisted nodes)
-  const int32_t cut = h->fw_ns;
-  HIPCHK(h, hipMemcpyAsync(&h->sc.win->cut, &cut, sizeof(cut), hipMemcpyHostToDevice, h->stream));
+  std::memcpy(h->pin, &h->fw_ns, sizeof(int32_t));
+  HIPCHK(h, hipMemcpyAsync(h->ext_fail, out_of_list, N, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(&h->sc.win->cut, h->pin, sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+  if (n) HIPCHK(h, hipMemcpyAsync(h->fw_nodes, (char*)h->pin + o_list, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
   LaunchArgs a = make_args(h, h->pod1, nullptr);
   a.s.ext_fail = h->ext_fail;
   a.s.ext_score = nullptr;
   launch_fw_score(a, h->stream);
+  const int S = h->prof.n_score;
+  if (n) launch_fw_gather(h->eo, h->fw_nodes, n, (int32_t)N, S, h->fw_comp, h->stream);
   HIPCHK(h, hipGetLastError());
   h->fw_pending = false;
   h->fw_dom_dirty = false;                 // k_select re-zeroed the domain sums
   h->fw_scored = true;
-  const int S = h->prof.n_score;
-  if (out->scored) HIPCHK(h, hcopy(h, out->scored, h->eo.scored, N, hipMemcpyDeviceToHost));
-  if (out->raw && S) HIPCHK(h, hcopy(h, out->raw, h->eo.raw, 8 * N * S, hipMemcpyDeviceToHost));
-  if (out->norm && S) HIPCHK(h, hcopy(h, out->norm, h->eo.norm, 8 * N * S, hipMemcpyDeviceToHost));
-  if (out->total) HIPCHK(h, hcopy(h, out->total, h->eo.total, 8 * N, hipMemcpyDeviceToHost));
+  // the listed nodes' answers into pinned staging, one synchronization; the
+  // unlisted nodes' answers are 0
+  const size_t o_comp = (sizeof(WinState) + 63) & ~(size_t)63, nb = (16 * (size_t)S + 9) * n;
+  if ((rc = pout_reserve(h, o_comp + nb))) return rc;
+  char* po = (char*)h->pout;
+  HIPCHK(h, hipMemcpyAsync(po, h->sc.win, sizeof(WinState), hipMemcpyDeviceToHost, h->stream));
+  if (n) HIPCHK(h, hipMemcpyAsync(po + o_comp, h->fw_comp, nb, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const int64_t* craw = (const int64_t*)(po + o_comp);
+  const int64_t* cnorm = craw + (size_t)S * n;
+  const int64_t* ctot = cnorm + (size_t)S * n;
+  const uint8_t* csc = (const uint8_t*)(ctot + n);
+  if (out->scored) {
+    std::memset(out->scored, 0, N);
+    for (int32_t j = 0; j < n; j++) out->scored[nodes[j]] = csc[j];
+  }
+  for (int k = 0; k < S; k++) {
+    if (out->raw) {
+      int64_t* r = out->raw + (size_t)k * N;
+      std::memset(r, 0, 8 * N);
+      for (int32_t j = 0; j < n; j++) r[nodes[j]] = craw[(size_t)k * n + j];
+    }
+    if (out->norm) {
+      int64_t* r = out->norm + (size_t)k * N;
+      std::memset(r, 0, 8 * N);
+      for (int32_t j = 0; j < n; j++) r[nodes[j]] = cnorm[(size_t)k * n + j];
+    }
+  }
+  if (out->total) {
+    std::memset(out->total, 0, 8 * N);
+    for (int32_t j = 0; j < n; j++) out->total[nodes[j]] = ctot[j];
+  }
+  // kept for ksim_fw_normalize over the same list
+  h->fw_list.assign(nodes, nodes + n);
+  h->fw_raw.assign(craw, craw + (size_t)S * n);
+  h->fw_norm.assign(cnorm, cnorm + (size_t)S * n);
   WinState w;
-  HIPCHK(h, hcopy(h, &w, h->sc.win, sizeof(w), hipMemcpyDeviceToHost));
+  std::memcpy(&w, po, sizeof(w));
   if (out->fail_plugin) {                  // the filter pass, unchanged
     std::memcpy(out->fail_plugin, h->fw_fail.data(), N);
     strip_fail_errors(out->fail_plugin, N);
@@ -2602,12 +2730,30 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
   for (int32_t j = 0; j < n; j++)
     if (nodes[j] < 0 || (size_t)nodes[j] >= N) return set_err(h, KSIM_E_INVALID, "bad node in score list");
   if (n == 0) return KSIM_OK;
+  // the framework's NormalizeScore hands over exactly ksim_fw_score's list
+  // and the raw scores it returned: that normalization is already computed
+  if ((size_t)n == h->fw_list.size() && h->fw_raw.size() == (size_t)h->prof.n_score * n) {
+    const int64_t* raw = h->fw_raw.data() + (size_t)score_slot * n;
+    bool same = std::equal(nodes, nodes + n, h->fw_list.begin());
+    for (int32_t j = 0; same && j < n; j++) same = scores[j] == raw[j];
+    if (same) {
+      std::memcpy(out, h->fw_norm.data() + (size_t)score_slot * n, 8 * (size_t)n);
+      return KSIM_OK;
+    }
+  }
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemcpyAsync(h->fw_nodes, nodes, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->fw_vals, scores, 8 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));    // the staging is free again
+  const size_t o_vals = (4 * (size_t)n + 63) & ~(size_t)63;
+  if ((rc = pin_reserve(h, o_vals + 8 * (size_t)n)) || (rc = pout_reserve(h, 8 * (size_t)n))) return rc;
+  std::memcpy(h->pin, nodes, 4 * (size_t)n);
+  std::memcpy((char*)h->pin + o_vals, scores, 8 * (size_t)n);
+  HIPCHK(h, hipMemcpyAsync(h->fw_nodes, h->pin, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->fw_vals, (char*)h->pin + o_vals, 8 * (size_t)n, hipMemcpyHostToDevice, h->stream));
   launch_fw_normalize(make_args(h, h->pod1, nullptr), score_slot, h->fw_nodes, h->fw_vals, n, h->fw_out, h->stream);
   HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hcopy(h, out, h->fw_out, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpyAsync(h->pout, h->fw_out, 8 * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::memcpy(out, h->pout, 8 * (size_t)n);
   return KSIM_OK;
 }
 
@@ -3475,7 +3621,7 @@ extern "C" int ksim_preempt_nominated(ksim_handle* h, const ksim_pod_set* ps, in
     for (int32_t j = first[k]; j < first[k] + count[k]; j++) {
       DevPods Q;
       int r;
-      if ((r = upload_single(h, nps, j, Q, h->nom_bufs))) return r;
+      if ((r = upload_single(h, nps, j, Q, h->nom_arena))) return r;
       launch_assume(h->dc, Q, 0, gnodes[k], sign, h->stream);
       HIPCHK(h, hipGetLastError());
     }

@@ -146,6 +146,8 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
 // 1 for unlisted nodes), no bind; NormalizeScore of one slot over an explicit list.
 void launch_fw_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
 void launch_fw_score(const LaunchArgs& a, hipStream_t stream);
+void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,
+                      hipStream_t stream);
 void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,
                          int64_t* out, hipStream_t stream);
 // DefaultPreemption dry run (ksim_preempt.hip): the bound pods per node in

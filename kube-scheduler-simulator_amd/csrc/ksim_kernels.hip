@@ -1512,6 +1512,27 @@ void launch_fw_score(const LaunchArgs& a, hipStream_t stream) {
   k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 0, nullptr);
 }
 
+// ksim_fw_score's answers for the listed nodes only: comp = [raw S x n][norm
+// S x n][total n] (list order), then the scored flags (n bytes); the host
+// copies n entries back instead of N (every unlisted node's answers are 0)
+__global__ __launch_bounds__(256) void k_fw_gather(DevEvalOut o, const int32_t* __restrict__ nodes, int32_t n,
+                                                   int32_t N, int32_t S, int64_t* __restrict__ comp) {
+  const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t x = nodes[j];
+  for (int32_t k = 0; k < S; k++) {
+    comp[(size_t)k * n + j] = o.raw[(size_t)k * N + x];
+    comp[(size_t)(S + k) * n + j] = o.norm[(size_t)k * N + x];
+  }
+  comp[(size_t)2 * S * n + j] = o.total[x];
+  reinterpret_cast<uint8_t*>(comp + (size_t)(2 * S + 1) * n)[j] = o.scored[x];
+}
+
+void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,
+                      hipStream_t stream) {
+  k_fw_gather<<<(n + 255) / 256, 256, 0, stream>>>(o, nodes, n, N, S, comp);
+}
+
 void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,
                          int64_t* out, hipStream_t stream) {
   k_fw_normalize<<<1, kFinalThreads, 0, stream>>>(a.prof, slot, a.st, a.s, nodes, vals, n, out);

@@ -141,6 +141,15 @@ def test_fw_api_lists_and_normalize():
             vals = rng.integers(-5, 300, sub.size)
             np.testing.assert_array_equal(eng.fw_normalize(slot, sub, vals), ora.fw_normalize(slot, sub, vals),
                                           err_msg=f"pod {i} slot {slot}")
+            # the scored list with its raw scores (answered from fw_score's
+            # normalization), then with one score changed (the device path)
+            raw = se["raw"][slot][lst]
+            np.testing.assert_array_equal(eng.fw_normalize(slot, lst, raw), se["norm"][slot][lst])
+            np.testing.assert_array_equal(eng.fw_normalize(slot, lst, raw), ora.fw_normalize(slot, lst, raw))
+            bent = raw.copy()
+            bent[-1] += 7
+            np.testing.assert_array_equal(eng.fw_normalize(slot, lst, bent), ora.fw_normalize(slot, lst, bent),
+                                          err_msg=f"pod {i} slot {slot} bent")
         node = int(lst[0])
         eng.assume(pods, i, node)
         ora.assume(pods, i, node)

@@ -180,6 +180,7 @@ struct WinState {
   uint64_t ext[kExtWords];               // per score slot: max image, min image (atomicMax); cut
   int32_t done;                          // k_select blocks finished (the last one binds; reset by it)
   uint32_t tflags;                       // topology batch: the pod's kTopo* flags (k_tb_filter block 0)
+  int32_t hold[2 * KSIM_MAX_SCORE];      // topology batch: nodes holding each slot's max / min (k_tb_select)
 };
 
 // The nodes one cycle scans, in scan order: every node of
@@ -269,6 +270,8 @@ struct DevScratch {
   WinState* tb_win;      // [kTbPods] counters, extrema, flags
   uint64_t* tb_clist;    // [kTbPods][kTbMaxBlocks][T] each node block's exact top-T keys
   int32_t* tb_ccnt;      // [kTbPods][kTbMaxBlocks] their counts
+  uint8_t* tb_xrecv;     // replicated topology batches: [world][kTbPods] WinState (the filter's counters)
+  uint64_t* tb_pp;       // replicated topology batches: [2][kTbPods] pair maxima, pinv (all-reduced max)
   int32_t* pinv;         // batch path: [B] 1 = a maximum holder of pod j left its feasible set (batch ends before j)
   unsigned long long* dbg;   // [16] diagnostic accumulators (ksim_get_diag), e.g. chain phase times
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records

@@ -591,7 +591,8 @@ bool pod_on_batch(const ksim_handle* h, int32_t i) {
   static const bool adapt_norm = getenv("KSIM_NO_ADAPT_NORM") == nullptr;
   const uint8_t b = h->batchable[i];
   if (b != 2 && b != 3) return b != 0;
-  if (is_sharded(h) || h->replicated) return false;   // replicated: a split evaluation range
+  if (h->replicated) return b == 3 && !adapt_mode(h);   // class 3: replicated topology batches (shard_run_tbatch)
+  if (is_sharded(h)) return false;
   if (!adapt_mode(h)) return true;
   return b == 2 && adapt_norm && h->noscalar[(size_t)i];
 }
@@ -1227,6 +1228,75 @@ int shard_run(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
   return KSIM_OK;
 }
 
+// ---- replicated topology batches (ksim_tbatch.hip launch_tb_rep_*) -------------
+template <typename F>
+int x_allreduce(const std::vector<ksim_handle*>& hs, F&& ptr, int64_t count, bool op_max, hipStream_t stream);
+
+// All-gather of `bytes` per handle: src(h) -> dst(h) + rank * bytes.
+template <typename S, typename D>
+int x_allgather_bytes(const std::vector<ksim_handle*>& hs, S&& src, D&& dst, size_t bytes, hipStream_t stream) {
+  ksim_handle* h0 = hs[0];
+  if (h0->comm) {
+    const ncclResult_t r = rccl().all_gather(src(h0), dst(h0), bytes, ncclUint8, h0->comm, stream);
+    if (r != ncclSuccess) return set_err(h0, KSIM_E_RCCL, std::string("ncclAllGather: ") + rccl().error_string(r));
+    return KSIM_OK;
+  }
+  for (size_t a = 0; a < hs.size(); a++)
+    for (size_t b = 0; b < hs.size(); b++)
+      HIPCHK(h0, hipMemcpyAsync((char*)dst(hs[b]) + a * bytes, src(hs[a]), bytes, hipMemcpyDeviceToDevice, stream));
+  return KSIM_OK;
+}
+
+// One topology batch on every replica of a group: each evaluates its node
+// range; three exchanges (the filter's per-pod counters and extrema, the
+// per-pod top-T records with the extremum holder counts, the pair maxima and
+// pinv); every replica commits every placement.
+int shard_tbatch(const std::vector<ksim_handle*>& hs, hipStream_t stream) {
+  ksim_handle* h0 = hs[0];
+  const int32_t world = h0->comm ? h0->world : (int32_t)hs.size();
+  int rc;
+  for (auto* h : hs) launch_tb_rep_filter(shard_args(h, false), stream);
+  if ((rc = x_allgather_bytes(hs, [](ksim_handle* h) { return (void*)h->sc.tb_win; },
+                              [](ksim_handle* h) { return (void*)h->sc.tb_xrecv; }, sizeof(WinState) * kTbPods, stream)))
+    return rc;
+  for (auto* h : hs) launch_tb_rep_select(shard_args(h, false), world, stream);
+  if ((rc = x_allgather_bytes(hs, [](ksim_handle* h) { return (void*)h->sc.xsend; },
+                              [](ksim_handle* h) { return (void*)h->sc.xrecv; }, 8 * (size_t)kTbPods * kTbXRec,
+                              stream)))
+    return rc;
+  for (auto* h : hs) launch_tb_rep_pairs(shard_args(h, false), world, stream);
+  if ((rc = x_allreduce(hs, [](ksim_handle* h) { return h->sc.tb_pp; }, 2 * kTbPods, true, stream))) return rc;
+  for (auto* h : hs) launch_tb_rep_commit(shard_args(h, false), stream);
+  HIPCHK(h0, hipGetLastError());
+  return KSIM_OK;
+}
+
+// Topology batch pods [a, b) on the replicas of a group (as run_tbatch: the
+// batches the run lengths predict, then the state).
+int shard_run_tbatch(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) {
+  ksim_handle* h0 = hs[0];
+  hipStream_t stream = h0->stream;
+  int rc;
+  for (auto* h : hs) {
+    if ((rc = set_run(h, a, b))) return rc;
+    HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  int32_t cursor = a;
+  while (cursor < b) {
+    int32_t nbat = 0;
+    for (int32_t i = cursor; i < b; nbat++) i += std::min(std::min(kTbPods, b - i), std::max(h0->tlen[i], 1));
+    for (int32_t i = 0; i < nbat; i++)
+      if ((rc = shard_tbatch(hs, stream))) return rc;
+    DevState st;
+    HIPCHK(h0, hipMemcpyAsync(&st, h0->st, sizeof(st), hipMemcpyDeviceToHost, stream));
+    HIPCHK(h0, hipStreamSynchronize(stream));
+    if (st.cursor <= cursor) return set_err(h0, KSIM_E_DEVICE, "replicated topology batches made no progress");
+    cursor = st.cursor;
+  }
+  return KSIM_OK;
+}
+
 // ---- node-sharded per-pod cycle (C1 extrema, C2 argmax, C3 window) ----
 // Element-wise all-reduce of a per-handle device buffer of `count` 8-byte words:
 // sum (int64) or max (uint64).  RCCL across processes, a group kernel in-process.
@@ -1529,7 +1599,7 @@ int shard_schedule(const std::vector<ksim_handle*>& hs, int32_t first, int32_t c
     // whole on every replica (the same cycles, so the replicas stay equal)
     const bool adapt = adapt_mode(hs[0]);
     return for_each_run(hs[0], first, count, [&](int32_t a, int32_t b, bool batch, bool topo) {
-      if (batch && !adapt) return shard_run(hs, a, b);
+      if (batch && !adapt) return topo ? shard_run_tbatch(hs, a, b) : shard_run(hs, a, b);
       for (auto* h : hs) {
         int rc = run_range(h, a, b, batch, topo);
         if (rc) return rc;
@@ -1963,6 +2033,8 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.tb_win, WinState*, sizeof(WinState) * (size_t)kTbPods);
   SCR(s.tb_clist, uint64_t*, 8 * (size_t)kTbPods * kTbMaxBlocks * kTopT);
   SCR(s.tb_ccnt, int32_t*, 4 * (size_t)kTbPods * kTbMaxBlocks);
+  SCR(s.tb_xrecv, uint8_t*, sizeof(WinState) * (size_t)kMaxShards * kTbPods);
+  SCR(s.tb_pp, uint64_t*, 8 * 2 * (size_t)kTbPods);
   SCR(s.pinv, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.dom, int64_t*, 8 * (size_t)KSIM_MAX_USES * vmax);
   SCR(s.dbg, unsigned long long*, 8 * 16);
@@ -2804,7 +2876,8 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   R = PtabRegistry{};
   R.pod.assign((size_t)ps->n_pods, 0);
   R.mask.assign((size_t)ps->n_pods, 0);
-  if (is_sharded(h) || getenv("KSIM_NO_PTAB")) return;   // A/B switch: per-cycle PreFilter sums
+  // replicas (RCCL ones included) hold every node: their tables are whole
+  if ((is_sharded(h) && !h->replicated) || getenv("KSIM_NO_PTAB")) return;   // A/B switch: per-cycle PreFilter sums
   std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> index;
   for (int32_t i = 0; i < ps->n_pods; i++) {
     const ksim_pod& p = ps->pods[i];
@@ -2877,12 +2950,26 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   }
 }
 
+// A use of a topology batch pod that may read a class an earlier pod of its
+// run adds (ksim_tbatch.hip k_tb_chain_pairs): node-local (the guessed node's
+// own count, re-keyed there), or a PodTopologySpread DoNotSchedule constraint
+// read from a persistent table, among the pod's first kTbHardDom, on a key of
+// at most kTbDomValues values (its per-domain verdicts re-checked).
+static bool tbatch_conflict_ok(const ksim_handle* h, const ksim_topo_use* U, int32_t i) {
+  const ksim_topo_use& u = U[i];
+  if (use_node_count(u)) return u.kind != KSIM_USE_PTS_HARD && u.kind != KSIM_USE_NODE_PORT && u.kind != KSIM_USE_IMAGE;
+  if (u.kind != KSIM_USE_PTS_HARD || u.col == KSIM_COL_NONE || h->col_nvals[u.col] > kTbDomValues) return false;
+  int32_t ord = 0;
+  for (int32_t x = 0; x < i; x++) ord += U[x].kind == KSIM_USE_PTS_HARD;
+  return ord < kTbHardDom;
+}
+
 // Topology batch runs (class 3 pods, ksim_tbatch.hip): tlen[i] = the number
 // of consecutive class-3 pods from i (at most kTbPods) none of which reads a
-// count class an earlier one of them adds (its uses' classes against the
-// earlier pods' adds), so that a batch starting at i sees every class it
-// reads at its S0 value.  0 for the other pods.
-void tbatch_runs(const ksim_pod_set* ps, const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen) {
+// count class an earlier one of them adds through a use tbatch_conflict_ok
+// refuses.  0 for the other pods.  uses: the queue's device use copies.
+void tbatch_runs(const ksim_handle* h, const ksim_pod_set* ps, const std::vector<ksim_topo_use>& uses,
+                 const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen) {
   const int32_t n = ps->n_pods;
   tlen.assign((size_t)std::max(n, 0), 0);
   int32_t n_cls = 0;
@@ -2893,10 +2980,11 @@ void tbatch_runs(const ksim_pod_set* ps, const std::vector<uint8_t>& batchable, 
     int32_t L = 0;
     for (int32_t j = i; j < n && L < kTbPods && batchable[j] == 3; j++, L++) {
       const ksim_pod& p = ps->pods[j];
+      const ksim_topo_use* U = uses.data() + p.use_first;
       bool clash = false;
       for (int32_t u = 0; u < p.use_count && !clash; u++) {
-        const int32_t c = ps->uses[p.use_first + u].cls;
-        clash = c >= 0 && c < n_cls && stamp[c] == i;
+        const int32_t c = U[u].cls;
+        clash = c >= 0 && c < n_cls && stamp[c] == i && !tbatch_conflict_ok(h, U, u);
       }
       if (clash) break;
       for (int32_t a = 0; a < p.add_count; a++) stamp[ps->adds[p.add_first + a].cls] = i;
@@ -3038,7 +3126,7 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
       bf[i] |= kPodTopoBatch;
     }
   }
-  tbatch_runs(ps, batchable, h->tlen);
+  tbatch_runs(h, ps, uses, batchable, h->tlen);
   for (int32_t i = 0; i < ps->n_pods; i++) bf[i] |= std::min(h->tlen[i], 255) << kTlenShift;
   DevPods P{};
   void* p = nullptr;

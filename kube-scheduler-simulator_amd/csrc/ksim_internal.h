@@ -56,13 +56,35 @@ extern const char* const kBatchKernelNames[kKernelsPerBatch];
 constexpr int kKernelsPerAdapt = 5;
 extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 // Topology batch path (ksim_tbatch.hip): at most kTbPods pods per batch (the
-// host's class-conflict-free runs, bflags >> kTlenShift), clusters of at most
-// kTbMaxBlocks node blocks of 256.
-constexpr int kTbPods = 32;
+// host's runs, bflags >> kTlenShift), clusters of at most kTbMaxBlocks node
+// blocks of 256.  A run may cross a class an earlier pod of it adds when every
+// such use is node-local (the pairs step re-keys the guessed node) or a
+// PodTopologySpread DoNotSchedule constraint among the pod's first kTbHardDom
+// ones whose key has at most kTbDomValues values (the pairs step re-checks its
+// per-domain verdicts); tbatch_conflict_ok.
+constexpr int kTbPods = 64;
 constexpr int kTbMaxBlocks = 64;
+constexpr int kTbHardDom = 4;
+constexpr int kTbDomValues = 64;
 constexpr int kKernelsPerTbatch = 5;
 extern const char* const kTbatchKernelNames[kKernelsPerTbatch];
 uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
+// Replicated topology batches (every replica holds the whole snapshot and
+// evaluates its node range [c.eval_lo, c.eval_hi)); the caller exchanges
+// between the phases:
+//   launch_tb_rep_filter   filter + raw scores + per-pod counters / extrema
+//                          (all-gather s.tb_win -> s.tb_xrecv [world][kTbPods])
+//   launch_tb_rep_select   merged counters, totals + keys, holders, the
+//                          replica's per-pod top-T record
+//                          (all-gather s.xsend -> s.xrecv [world][kTbPods][kTbXRec])
+//   launch_tb_rep_pairs    global top-T, chain, pair keys of the guesses this
+//                          replica evaluated (all-reduce max s.tb_pp)
+//   launch_tb_rep_commit   commit on every replica (every bind, every class add)
+constexpr int kTbXRec = kTopT + 1 + KSIM_MAX_SCORE;   // T keys, count, holder counts (2 x int32 per slot)
+void launch_tb_rep_filter(const LaunchArgs& a, hipStream_t stream);
+void launch_tb_rep_select(const LaunchArgs& a, int32_t world, hipStream_t stream);
+void launch_tb_rep_pairs(const LaunchArgs& a, int32_t world, hipStream_t stream);
+void launch_tb_rep_commit(const LaunchArgs& a, hipStream_t stream);
 
 // One scheduling cycle for the pod at st->cursor (no-op once cursor >= end).
 // evs (nullable, kKernelsPerCycle + 1 events) are recorded around each kernel.

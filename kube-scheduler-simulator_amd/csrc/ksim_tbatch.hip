@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256) void k_tb_filter(DevCluster c, DevPods P0, con
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
   __shared__ int32_t s_cnt[4][2];
   __shared__ uint32_t s_tf;
-  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t xr = node < c.n ? node : c.n - 1;
+  const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;   // replicas: their range
+  const int32_t xr = node < c.eval_hi ? node : c.eval_hi - 1;
   // the node's row does not depend on the pod: its loads go out first
   const NodeRow r = load_row(c, xr);
   const double inv_c = c.inv_cpu[xr], inv_m = c.inv_mem[xr];
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_tb_filter(DevCluster c, DevPods P0, con
   RawScores rv{};
   int64_t soft_cnt = 0;
   const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;   // the pod's one ScheduleAnyway use
-  if (node < c.n) {
+  if (node < c.eval_hi) {
     uint32_t det;
     const uint8_t res = run_filter_plan(c, P, FilterPlan{bp->rank_lo, bp->rank_hi, pp.filter_en}, s_min, tf, p, r,
                                         U, m, t, det);
@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
                                                    DevScratch s) {
   __shared__ uint64_t s_cand[4 * kTopT];
-  const int32_t node = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int32_t s_hold[4][4];
+  const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t j = blockIdx.y;
   if (j >= tb_count(st, P0)) return;                // block-uniform
   const ksim_profile& prof = *prof_p;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
   const UseMasks m = P0.plans[pi].m;
   const ksim_topo_use* U = P0.uses + p.use_first;
   const TbSlice q = tb_slice(s, j, N);
-  const WinState* win = q.win;
+  WinState* win = q.win;
   const int32_t nf = win->nfeas;
   const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
   const bool has_soft = nf > 1 && soft >= 0;
@@ -219,7 +220,8 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
   const uint64_t seed = prof.tiebreak_seed;
   const int64_t seq = st->pod_seq + j;
   uint64_t key = 0;
-  if (node < N) {
+  uint32_t hf = 0;                                 // holds PTS max, PTS min, IPA max, IPA min
+  if (node < c.eval_hi) {
     int32_t stat = kStatNone;
     if (q.fail[node] == KSIM_PASSED) {
       if (nf > 1) {
@@ -229,6 +231,13 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
           const int32_t kind = norm_kind(prof_score(prof, k));
           if (kind == kNormNone) continue;
           int64_t gmax = from_max_image(win->ext[2 * k]), gmin = from_min_image(win->ext[2 * k + 1]);
+          if (kind == kNormIPA) {                  // the holders of the extrema (k_tb_chain_pairs)
+            const int64_t x = q.raw[(size_t)k * N + node];
+            hf |= (x == gmax ? 4u : 0u) | (x == gmin ? 8u : 0u);
+          } else if (kind == kNormPTS && has_soft && !ign) {
+            const int64_t x = q.raw[(size_t)k * N + node];
+            hf |= (x == gmax ? 1u : 0u) | (x == gmin ? 2u : 0u);
+          }
           int64_t raw;
           if (kind == kNormPTS) {
             raw = 0;
@@ -255,18 +264,39 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
     }
     q.stat[node] = stat;
   }
-  const size_t cl = (size_t)j * kTbMaxBlocks + blockIdx.x;
-  block_top_t(key, s_cand, s.tb_clist + cl * kTopT, s.tb_ccnt + cl);
+  // holder counts: one popcount per wave, one atomic per block and counter
+  // (after block_top_t's barrier)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+    const int32_t n = (int32_t)__popcll(__ballot((hf >> h) & 1u));
+    if (lane == 0) s_hold[wv][h] = n;
+  }
+  block_top_t(key, s_cand, s.tb_clist + ((size_t)j * kTbMaxBlocks + blockIdx.x) * kTopT,
+              s.tb_ccnt + (size_t)j * kTbMaxBlocks + blockIdx.x);
+  if (threadIdx.x < 4) {
+    int kp = -1, ki = -1;                          // the profile's slots (block-uniform)
+    for (int k = 0; k < S; k++) {
+      const int32_t kind = norm_kind(prof_score(prof, k));
+      if (kind == kNormPTS) kp = k;
+      if (kind == kNormIPA) ki = k;
+    }
+    const int h = threadIdx.x, k = h < 2 ? kp : ki;
+    const int32_t n = s_hold[0][h] + s_hold[1][h] + s_hold[2][h] + s_hold[3][h];
+    if (k >= 0 && n) atomicAdd(&win->hold[2 * k + (h & 1)], n);
+  }
 }
 
 // Pod j's exact top-T from its blocks' exact lists (the pod's top-T lies in
 // the union of the blocks' top-T): one wave, lane b holds block b's list.
+// xsend (replicas): the record [kTbPods][kTbXRec] of this replica's range
+// (keys, count, holder counts) instead of the pod's lists.
 __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const DevState* __restrict__ st,
-                                                 DevScratch s) {
+                                                 DevScratch s, uint64_t* __restrict__ xsend) {
   const int lane = threadIdx.x;
   const int32_t j = blockIdx.x;
   if (j >= tb_count(st, P)) return;
-  const int32_t nblk = (c.n + 255) / 256;
+  const int32_t nblk = (c.eval_hi - c.eval_lo + 255) / 256;
   uint64_t L[kTopT];
   int32_t cnt = 0;
   const size_t cl = (size_t)j * kTbMaxBlocks + lane;
@@ -292,6 +322,15 @@ __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const 
       L[kTopT - 1] = 0;
     }
   }
+  if (xsend) {
+    uint64_t* r = xsend + (size_t)j * kTbXRec;
+    if (lane < kTopT) r[lane] = lane < n ? mine : 0;
+    if (lane == 0) r[kTopT] = (uint64_t)n;
+    if (lane < KSIM_MAX_SCORE)
+      r[kTopT + 1 + lane] = (uint64_t)(uint32_t)s.tb_win[j].hold[2 * lane] |
+                            ((uint64_t)(uint32_t)s.tb_win[j].hold[2 * lane + 1] << 32);
+    return;
+  }
   if (lane < kTopT) s.topk[(size_t)j * kTopT + lane] = lane < n ? mine : 0;
   if (lane == 0) {
     s.topk_cnt[j] = n;
@@ -299,16 +338,103 @@ __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const 
   }
 }
 
+// Replicas: pod j's counters and extrema over every replica's range (thread j).
+__global__ __launch_bounds__(kTbPods) void k_tb_wmerge(DevScratch s, int32_t world) {
+  const int32_t j = threadIdx.x;
+  const WinState* w = reinterpret_cast<const WinState*>(s.tb_xrecv);
+  WinState& o = s.tb_win[j];
+  int32_t nf = 0, ni = 0;
+  uint32_t tf = 0;
+  uint64_t ext[2 * KSIM_MAX_SCORE];
+#pragma unroll
+  for (int x = 0; x < 2 * KSIM_MAX_SCORE; x++) ext[x] = 0;
+  for (int32_t r = 0; r < world; r++) {
+    const WinState& x = w[(size_t)r * kTbPods + j];
+    nf += x.nfeas;
+    ni += x.nign;
+    tf |= x.tflags;                                // the same tables on every replica
+#pragma unroll
+    for (int e = 0; e < 2 * KSIM_MAX_SCORE; e++) ext[e] = umax64(ext[e], x.ext[e]);
+  }
+  o.nfeas = nf;
+  o.nign = ni;
+  o.tflags = tf;
+#pragma unroll
+  for (int e = 0; e < 2 * KSIM_MAX_SCORE; e++) o.ext[e] = ext[e];
+}
+
+// Replicas: pod j's exact global top-T from the replicas' exact range lists
+// (one wave; lane l holds list entry l % T of replica l / T), and its holder
+// counts summed.
+__global__ __launch_bounds__(64) void k_tb_gmerge(DevPods P, const DevState* __restrict__ st, DevScratch s,
+                                                  int32_t world) {
+  static_assert(kTopT * kMaxShards <= 64, "k_tb_gmerge: one list entry per lane");
+  const int lane = threadIdx.x;
+  const int32_t j = blockIdx.x;
+  if (j >= tb_count(st, P)) return;
+  const int32_t r = lane / kTopT, e = lane % kTopT;
+  uint64_t key = 0;
+  if (r < world) {
+    const uint64_t* rec = s.xrecv + ((size_t)r * kTbPods + j) * kTbXRec;
+    if ((uint64_t)e < rec[kTopT]) key = rec[e];
+  }
+  int32_t rank = 0;                                // keys are unique (node-specific) or 0
+  for (int x = 0; x < 64; x++) {
+    const uint64_t o = __shfl(key, x, 64);
+    rank += o > key;
+  }
+  const int32_t n = __popcll(__ballot(key != 0));
+  if (key != 0 && rank < kTopT) s.topk[(size_t)j * kTopT + rank] = key;
+  if (lane >= n && lane < kTopT) s.topk[(size_t)j * kTopT + lane] = 0;
+  if (lane == 0) {
+    s.topk_cnt[j] = n < kTopT ? n : kTopT;
+    s.topk_complete[j] = s.tb_win[j].nfeas <= kTopT ? 1 : 0;
+  }
+  if (lane < KSIM_MAX_SCORE) {
+    uint32_t hmax = 0, hmin = 0;
+    for (int32_t q = 0; q < world; q++) {
+      const uint64_t h = s.xrecv[((size_t)q * kTbPods + j) * kTbXRec + kTopT + 1 + lane];
+      hmax += (uint32_t)h;
+      hmin += (uint32_t)(h >> 32);
+    }
+    s.tb_win[j].hold[2 * lane] = (int32_t)hmax;
+    s.tb_win[j].hold[2 * lane + 1] = (int32_t)hmin;
+  }
+}
+
+// A local change of one normalized raw score (PodTopologySpread counts,
+// InterPodAffinity scores) on a node pod j keeps S0's extrema when the new
+// value stays inside [gmin, gmax] and, if the node held an extremum, more nodes
+// held it than the batch moves (at most j: one guessed node per earlier pod).
+__device__ __forceinline__ bool tb_keeps_extrema(int64_t x0, int64_t x1, int64_t gmax, int64_t gmin, int32_t hmax,
+                                                 int32_t hmin, int32_t j) {
+  if (x1 > gmax || x1 < gmin) return false;
+  if (x1 != x0 && x0 == gmax && hmax <= j) return false;
+  if (x1 != x0 && x0 == gmin && hmin <= j) return false;
+  return true;
+}
+
 // Block j: the chain, then pod j's keys on the guesses of pods k < j after
-// those binds (the S0 stat plus the resource part on the updated row), or
-// pinv[j] when a guess that was feasible for pod j at S0 no longer fits.
+// those binds (thread k: pod k's guess), or pinv[j] when pod j's S0 lists no
+// longer describe it.  Pod k's bind moves pod j's inputs only on its guessed
+// node g (the resources; the classes pod k adds, through pod j's node-local
+// uses) and, for pod j's PodTopologySpread DoNotSchedule constraints on small
+// keys, in g's domain.  The key on g is the S0 stat with the resource part
+// and the changed PodTopologySpread / InterPodAffinity raw scores recomputed
+// against S0's extrema; pinv when a change would move an extremum, the
+// feasible set (a node's verdict, a domain's verdict) or an emptiness flag.
+// pp (replicas): pair maxima and pinv into pp[j] / pp[kTbPods + j], keyed
+// only on the guesses in this replica's range (the all-reduce max combines).
 __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, DevPods P,
                                                                const ksim_profile* __restrict__ prof_p,
                                                                const BatchProg* __restrict__ bp_p,
-                                                               const DevState* __restrict__ st, DevScratch s) {
+                                                               const DevState* __restrict__ st, DevScratch s,
+                                                               uint64_t* __restrict__ pp) {
   __shared__ ChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   __shared__ int32_t s_winv[kBatchPods / 64];
+  __shared__ int32_t s_dd[kTbHardDom][kTbDomValues];   // pod j's DoNotSchedule count deltas per domain
+  __shared__ int32_t s_ddany;
   const int32_t nbt = tb_count(st, P);
   uint64_t gk;
   int32_t nchain;
@@ -322,35 +448,120 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   }
   if (j >= nchain) {                               // block-uniform
     if (tid == 0) {
-      s.pmax[j] = 0;
-      s.pinv[j] = 0;
+      if (pp) {
+        pp[j] = 0;
+        pp[kTbPods + j] = 0;
+      } else {
+        s.pmax[j] = 0;
+        s.pinv[j] = 0;
+      }
     }
     return;
   }
+  for (int x = tid; x < kTbHardDom * kTbDomValues; x += kBatchPods) (&s_dd[0][0])[x] = 0;
+  if (tid == 0) s_ddany = 0;
+  __syncthreads();
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
   const int64_t seq0 = st->pod_seq;
+  const int32_t N = c.n;
+  const ksim_pod& p = P.pods[base + j];
+  const UseMasks m = P.plans[base + j].m;
+  const ksim_topo_use* U = P.uses + p.use_first;
+  const int nu = p.use_count;
+  const WinState* win = s.tb_win + j;
+  const uint32_t tf = win->tflags;
+  const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
   uint64_t v = 0;
   bool inv = false;
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
-  if (local >= 0 && local < c.n) {
-    const int32_t sv = s.tb_stat[(size_t)j * c.n + local];
-    if (sv != kStatNone) {
-      const ksim_pod& p = P.pods[base + j];
+  if (local >= 0 && local < N) {
+    const bool own = local >= c.eval_lo && local < c.eval_hi;   // S0 values of g live on its replica
+    // what pod k's adds change for pod j on g = local
+    const ksim_pod& pk = P.pods[base + k];
+    int64_t d_soft = 0, d_ipa = 0;
+    bool hit_anti = false, hit_aff = false, hit_score = false;
+    for (int i = 0; i < nu; i++) {
+      const ksim_topo_use u = load_use(U, i);
+      if (u.cls < 0) continue;
+      int32_t d = 0;
+      for (int a = 0; a < pk.add_count; a++) {
+        const ksim_class_add x = P.adds[pk.add_first + a];
+        if (x.cls == u.cls) d += x.count;
+      }
+      if (d == 0) continue;
+      const uint32_t b = 1u << i;
+      if ((m.node_count & b) && !(m.hard & b)) {   // g's own count
+        if (use_value(c, u, local) == 0) continue;   // the use ignores a node without its key
+        if ((m.anti | m.exist) & b) hit_anti = true;
+        if (m.aff & b) hit_aff = true;
+        if (m.score & b) {
+          hit_score = true;
+          d_ipa += ipa_coef(prof, u) * d;
+        }
+        if (i == soft) d_soft += d;
+      } else if ((m.hard & b) && !(m.node_count & b)) {   // g's domain
+        const int ord = __popc(m.hard & (b - 1u));
+        const uint32_t dv = use_value(c, u, local);
+        if (ord < kTbHardDom && dv < (uint32_t)kTbDomValues) {
+          atomicAdd(&s_dd[ord][dv], d);
+          s_ddany = 1;
+        } else {
+          inv = true;
+        }
+      } else {
+        inv = true;                                // a domain-keyed InterPodAffinity use (tbatch_conflict_ok)
+      }
+    }
+    if (hit_aff && !(tf & kTopoAffinityNonEmpty)) inv = true;   // len(affinityCounts) would change
+    if (hit_score && !(tf & kTopoScoreNonEmpty)) inv = true;    // len(topologyScore) would change
+    const int32_t sv = own ? s.tb_stat[(size_t)j * N + local] : kStatNone;
+    if (!own) {
+    } else if (sv != kStatNone) {
       NodeRow r = load_row(c, local);
-      row_add_pod(r, P.pods[base + k], 1);
-      if (bp.has_fit_filter && fits_request(r, p, c.n_scalar, c.fit_ignore)) {
-        inv = true;
+      row_add_pod(r, pk, 1);
+      if (hit_anti || (bp.has_fit_filter && fits_request(r, p, c.n_scalar, c.fit_ignore))) {
+        inv = true;                                // a node of the S0 feasible set stops passing
       } else {
         int64_t tot = 0;
         if (sv != kStatOne) {
           tot = sv;
+          if (d_soft || d_ipa) {                   // the changed topology scores, S0's extrema
+            const bool ipa_ne = (tf & kTopoScoreNonEmpty) != 0;
+            const int32_t nf = win->nfeas;
+            for (int kk = 0; kk < prof.n_score; kk++) {
+              const int32_t kind = norm_kind(prof_score(prof, kk));
+              const bool pts = kind == kNormPTS && d_soft != 0 && soft >= 0 && !s.tb_ign[(size_t)j * N + local];
+              const bool ipa = kind == kNormIPA && d_ipa != 0;
+              if (!pts && !ipa) continue;
+              const int64_t x0 = s.tb_raw[((size_t)j * KSIM_MAX_SCORE + kk) * N + local];
+              const int64_t x1 = x0 + (pts ? d_soft : d_ipa);
+              int64_t gmax = from_max_image(win->ext[2 * kk]), gmin = from_min_image(win->ext[2 * kk + 1]);
+              if (!tb_keeps_extrema(x0, x1, gmax, gmin, win->hold[2 * kk], win->hold[2 * kk + 1], j)) {
+                inv = true;
+                break;
+              }
+              int64_t r0 = x0, r1 = x1;
+              if (pts) {                           // counts -> scores (topologyNormalizingWeight, hostname)
+                const ksim_topo_use u = load_use(U, soft);
+                const double w = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - win->nign : 0];
+                r0 = soft_score(x0, w, u.arg);
+                r1 = soft_score(x1, w, u.arg);
+                gmax = soft_score(gmax, w, u.arg);
+                gmin = soft_score(gmin, w, u.arg);
+              }
+              tot += prof_weight(prof, kk) *
+                     (normalize_value(kind, r1, gmax, gmin, ipa_ne) - normalize_value(kind, r0, gmax, gmin, ipa_ne));
+            }
+          }
           if (bp.w_fit) tot += bp.w_fit * fit_score(r, prof, p, c.n_scalar);
           if (bp.w_ba) tot += bp.w_ba * balanced_allocation_score(r, prof, p, c.n_scalar);
         }
-        v = tb_key(tot, prof.tiebreak_seed, seq0 + j, c.base + local);
+        if (!inv) v = tb_key(tot, prof.tiebreak_seed, seq0 + j, c.base + local);
       }
+    } else if (hit_aff) {
+      inv = true;                                  // required affinity may now pass on g
     }
   }
   v = wave_max_u64_dpp(v);
@@ -360,15 +571,44 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     s_winv[wave] = b != 0;
   }
   __syncthreads();
-  if (tid == 0) {
-    uint64_t mx = 0;
-    int32_t any = 0;
-    for (int w = 0; w < kBatchPods / 64; w++) {
-      mx = umax64(mx, s_wmax[w]);
-      any |= s_winv[w];
+  if (wave == 0) {
+    bool dinv = false;
+    if (s_ddany) {                                 // block-uniform: the domains' verdicts, before and after
+      for (int i = 0, ord = 0; i < nu && ord < kTbHardDom; i++) {
+        if (!((m.hard >> i) & 1u)) continue;
+        const int o = ord++;
+        if ((m.node_count >> i) & 1u) continue;
+        const ksim_topo_use u = load_use(U, i);
+        if (u.col == KSIM_COL_NONE) continue;
+        const int32_t V = c.col_nvals[u.col];
+        if (V > kTbDomValues) {                    // unchecked domains (tbatch_conflict_ok refuses these)
+          dinv = true;
+          break;
+        }
+        const int64_t self = (m.self_match >> i) & 1u;
+        const int64_t x = lane < V && lane < kTbDomValues ? P.ptab[u._pad + lane] : 0;
+        const bool present = (x >> kDomMarkShift) != 0;
+        const int64_t c0 = x & kDomCountMask, c1 = c0 + (lane < kTbDomValues ? s_dd[o][lane] : 0);
+        const int64_t min0 = wave_min_i64(present ? c0 : INT64_MAX), min1 = wave_min_i64(present ? c1 : INT64_MAX);
+        const bool ok0 = c0 + self - min0 <= (int64_t)u.arg, ok1 = c1 + self - min1 <= (int64_t)u.arg;
+        if (__ballot(present && lane != 0 && ok0 != ok1)) dinv = true;
+      }
     }
-    s.pmax[j] = mx;
-    s.pinv[j] = any;
+    if (tid == 0) {
+      uint64_t mx = 0;
+      int32_t any = dinv;
+      for (int w = 0; w < kBatchPods / 64; w++) {
+        mx = umax64(mx, s_wmax[w]);
+        any |= s_winv[w];
+      }
+      if (pp) {
+        pp[j] = mx;
+        pp[kTbPods + j] = (uint64_t)any;
+      } else {
+        s.pmax[j] = mx;
+        s.pinv[j] = any;
+      }
+    }
   }
 }
 
@@ -377,12 +617,14 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
 // thread; a pod and the pod i* that binds on its node may share entries).
 constexpr int kTbAddSlots = 8;                     // adds / table updates per pod and pass
 __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
-                                                          DevScratch s, int32_t* __restrict__ chosen_out) {
+                                                          DevScratch s, int32_t* __restrict__ chosen_out,
+                                                          const uint64_t* __restrict__ pp) {
   __shared__ int32_t s_istar, s_sched, s_unsched;
   __shared__ int32_t s_node[kTbPods];
   const int tid = threadIdx.x;
-  const uint64_t g = s.gkey[tid], m = s.pmax[tid];   // in flight with the state loads
-  const int32_t inv = tid < kTbPods ? s.pinv[tid] : 0;
+  const uint64_t g = s.gkey[tid];                  // in flight with the state loads
+  const uint64_t m = pp ? (tid < kTbPods ? pp[tid] : 0) : s.pmax[tid];
+  const int32_t inv = tid < kTbPods ? (pp ? (int32_t)(pp[kTbPods + tid] != 0) : s.pinv[tid]) : 0;
   const int32_t nchain = *s.chain_end;
   const int32_t base = st->cursor;
   const int32_t nbt = tb_count(st, P);
@@ -424,13 +666,34 @@ uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs)
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s);
+  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s, nullptr);
   if (evs) (void)hipEventRecord(evs[3], stream);
-  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, nullptr);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen);
+  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, nullptr);
   if (evs) (void)hipEventRecord(evs[5], stream);
   return (1u << kKernelsPerTbatch) - 1;
+}
+
+void launch_tb_rep_filter(const LaunchArgs& a, hipStream_t stream) {
+  const dim3 grid((a.c.eval_hi - a.c.eval_lo + 255) / 256, kTbPods);
+  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+}
+
+void launch_tb_rep_select(const LaunchArgs& a, int32_t world, hipStream_t stream) {
+  const dim3 grid((a.c.eval_hi - a.c.eval_lo + 255) / 256, kTbPods);
+  k_tb_wmerge<<<1, kTbPods, 0, stream>>>(a.s, world);
+  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.s.xsend);
+}
+
+void launch_tb_rep_pairs(const LaunchArgs& a, int32_t world, hipStream_t stream) {
+  k_tb_gmerge<<<kTbPods, 64, 0, stream>>>(a.P, a.st, a.s, world);
+  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, a.s.tb_pp);
+}
+
+void launch_tb_rep_commit(const LaunchArgs& a, hipStream_t stream) {
+  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, a.s.tb_pp);
 }
 
 }  // namespace ksim

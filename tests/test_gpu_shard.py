@@ -287,3 +287,57 @@ def test_rccl_world1_replicated():
     ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and e.diag()["graph_captures"] >= 1
+
+
+@pytest.mark.parametrize("n_nodes,world,n_apps", [(900, 2, 64), (1031, 3, 6), (2000, 8, 64)])
+def test_group_replicated_config3(n_nodes, world, n_apps):
+    """Replicated topology batches (config 3): each replica filters / scores
+    its node range; the per-pod counters and extrema, the top-T records with
+    the extremum holders, and the pair maxima are exchanged; every replica
+    commits every placement and every class add, ending with the oracle's
+    node state and class counts."""
+    from ksim.encode import encode_cluster, encode_pods
+    from ksim.model import LabelSelector
+    nodes, bound, inc = gen.config3_objects(n_nodes=n_nodes, pods_per_node=4, n_incoming=1500, seed=world,
+                                            zone_anti_every=50)
+    rng = np.random.default_rng(world)
+    for p in inc:
+        app = f"a{int(rng.integers(0, n_apps))}"
+        p.labels["app"] = app
+        for c in p.topology_spread:
+            c.label_selector = LabelSelector({"app": app})
+        for w in p.pod_anti_affinity_preferred:
+            w.term.label_selector = LabelSelector({"app": app})
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, inc)
+    prof = _prof()
+    engines = _replicas(cluster, pods, prof, world)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.scheduled == ost.scheduled and st.perpod_cycles == 0 and st.batches < pods.n_pods
+    os_ = ora.node_state()
+    for e in engines:
+        es = e.node_state()
+        for k in es:
+            np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+        np.testing.assert_array_equal(e.class_count(), ora.class_count())
+
+
+def test_rccl_world1_replicated_config3():
+    from ksim.encode import encode_cluster, encode_pods
+    nodes, bound, inc = gen.config3_objects(n_nodes=700, pods_per_node=4, n_incoming=1200, seed=13)
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, inc)
+    prof = _prof()
+    e = Engine(0)
+    e.set_profile(prof)
+    e.set_cluster(cluster)
+    e.set_eval_range(0, cluster.n_nodes)
+    e.comm_init(0, 1, engine.comm_unique_id())
+    e.load_pods(pods)
+    chosen, st = e.schedule_loaded(0, pods.n_pods)
+    ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.perpod_cycles == 0 and st.batches < pods.n_pods

@@ -1,8 +1,9 @@
 """The topology batch path (ksim_tbatch.hip; class-3 pods of pod_batchable /
 tbatch_admit in ksim_engine.cpp) against the one-by-one oracle: pods with
 PodTopologySpread and InterPodAffinity uses read from the persistent domain
-tables, scheduled up to kTbPods at a time over runs in which no pod reads a
-count class an earlier pod of the run adds.  Placements, evaluation counts,
+tables, scheduled up to kTbPods at a time over runs that cross a class an
+earlier pod of the run adds only through uses the pairs step repairs
+(tbatch_conflict_ok).  Placements, evaluation counts,
 node rows and count classes must equal the oracle's (config 3 shapes:
 /root/reference/simulator/scheduler/scheduler.go runs the upstream
 scheduler's per-pod cycle; the restatement is oracle/ksim_oracle.c)."""
@@ -64,9 +65,11 @@ def test_nodes_fill_up():
     assert st.perpod_cycles == 0 and st.unschedulable > 0 and st.truncations > 0
 
 
-def test_one_app_serializes():
-    """Every pod spreads over the same selector: each pod reads the class the
-    previous one adds, so every batch holds one pod; still exact."""
+def test_one_app_crosses_classes():
+    """Every pod spreads over the same selector: each pod reads the classes the
+    earlier ones add (the zone DoNotSchedule counts, the hostname counts); the
+    runs cross them and the pairs step cuts where a zone's verdict flips or an
+    extremum moves; still exact."""
     nodes, bound, inc = gen.config3_objects(n_nodes=200, pods_per_node=3, n_incoming=200, seed=9)
     for p in inc:
         p.labels["app"] = "a7"
@@ -76,7 +79,55 @@ def test_one_app_serializes():
             w.term.label_selector = LabelSelector({"app": "a7"})
     cluster, _ = encode_cluster(nodes, bound)
     eng, st = _run(cluster, encode_pods(cluster, inc))
-    assert st.batches == 200
+    assert st.perpod_cycles == 0 and st.batches <= 200
+
+
+def _few_apps(inc, n_apps, rng):
+    """Incoming pods relabelled to n_apps apps (selectors follow): most pods of
+    a batch read classes earlier ones add."""
+    for p in inc:
+        app = f"a{int(rng.integers(0, n_apps))}"
+        p.labels["app"] = app
+        for c in p.topology_spread:
+            c.label_selector = LabelSelector({"app": app})
+        for w in p.pod_anti_affinity_preferred:
+            w.term.label_selector = LabelSelector({"app": app})
+    return inc
+
+
+@pytest.mark.parametrize("n_apps,per_node", [(2, 4), (6, 4), (6, 0)])
+def test_cross_class_runs(n_apps, per_node):
+    """Runs that cross class conflicts (tbatch_conflict_ok): pods of few apps
+    re-key the guessed nodes (hostname spread counts, preferred anti-affinity
+    scores, the holders of the extrema) and re-check the zone verdicts.  With
+    no existing pods the InterPodAffinity topologyScore starts empty (the
+    emptiness flag flips)."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=600, pods_per_node=per_node, n_incoming=1500, seed=31 + n_apps)
+    inc = _few_apps(inc, n_apps, np.random.default_rng(n_apps))
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    # few apps over 3 zones even out quickly: many zone verdicts flip (pinv)
+    print(f"apps {n_apps}: {len(inc)} pods in {st.batches} batches, {st.truncations} truncated")
+    assert st.perpod_cycles == 0 and st.batches < len(inc)
+
+
+def test_cross_class_required_terms():
+    """Required anti-affinity (hostname, against the pod's own app) on some
+    pods and required affinity (hostname, to an app) on others: a guessed node
+    stops passing for a later pod of the app (pinv) or may start passing."""
+    from ksim.model import PodAffinityTerm
+    nodes, bound, inc = gen.config3_objects(n_nodes=400, pods_per_node=3, n_incoming=1200, seed=41)
+    rng = np.random.default_rng(41)
+    inc = _few_apps(inc, 5, rng)
+    for k, p in enumerate(inc):
+        if k % 4 == 1:
+            p.pod_anti_affinity_required = [PodAffinityTerm("kubernetes.io/hostname",
+                                                            LabelSelector({"app": p.labels["app"]}))]
+        elif k % 9 == 2:
+            p.pod_affinity_required = [PodAffinityTerm("kubernetes.io/hostname",
+                                                       LabelSelector({"app": f"a{int(rng.integers(0, 5))}"}))]
+    cluster, _ = encode_cluster(nodes, bound)
+    _run(cluster, encode_pods(cluster, inc))
 
 
 def test_mixed_with_plain_pods():

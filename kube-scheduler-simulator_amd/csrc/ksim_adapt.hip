@@ -249,172 +249,112 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
   if (j == 0) *aexact = exact;
 }
 
-// The exact windows in one ordered walk, no relaxation (clusters up to
-// kWinSeqWords bitmap words; generic runs, whose windows converge slowly under
-// relaxation: a heterogeneous queue's feasible sets are sparse and uneven, so
-// one pod's start error moves every later pod's).  Pod j's scan stops at its
-// (K+1)-th feasible node and pod j+1's scan starts there, so the starts are
-// the walk s_{j+1} = cut node of pod j from s_j.  The bitmaps were written by
-// every XCD and this block runs on one, so each global load costs a trip to
-// the MALL: the 16 waves stage a slice of the pods' bitmaps and their prefix
-// counts (pc[w] = set bits in words [0, w)) in LDS, then wave 0 walks the
-// slice from LDS alone, its loads kAhead pods early.  Per pod the walk is
-// register work: the counts and words sit two per lane, the start's rank is a
-// readlane, the cut's word a ballot over the counts, the cut's bit a ballot
-// over the word's per-bit ranks.
+// Clusters of at most kWinSeqWords bitmap words take the exact windows of
+// generic runs by doubling (below): a heterogeneous queue's feasible sets are
+// sparse and uneven, so one pod's start error moves every later pod's and the
+// relaxation converges slowly.  Pod j's scan stops at its (K+1)-th feasible
+// node and pod j+1's scan starts there: s_{j+1} = F_j(s_j).  (Round 4 first
+// walked this recurrence on one wave, 0.27 us per pod; profiles/r04/next1.)
 constexpr int32_t kWinSeqWords = 128;
-constexpr int kWinSeqThreads = 1024;
 
-// One pod of the walk (wave-wide; s, n, k, the result and *cut uniform): the
-// pod's bitmap words w and w + 64 and their prefix counts in lane w's a / pa
-// and b / pb, tot = its feasible nodes.  Returns the next pod's start.
-__device__ __forceinline__ int32_t walk_step(uint64_t a, uint64_t b, int32_t pa, int32_t pb, int32_t tot, bool ina,
-                                             bool inb, int lane, int32_t s, int32_t n, int32_t k, int32_t& cut) {
-  constexpr int32_t kNone = 0x7fffffff;                // a count no rank reaches (lanes past the words)
-  a = ina ? a : 0ull;
-  b = inb ? b : 0ull;
-  pa = ina ? pa : kNone;
-  pb = inb ? pb : kNone;
-  const int32_t total = __builtin_amdgcn_readfirstlane(tot);
-  if (total <= k) {                                    // at most K feasible: all N processed, same start
-    cut = -1;
-    return s;
+// The same windows by pointer doubling (clusters of at most kWinSeqWords
+// bitmap words; the walk's function made parallel).  Pod j's step is a map
+// F_j: start -> next start over the n starts (the (K+1)-th feasible node
+// from the start, the start itself when at most K are feasible).  k_win_build
+// tabulates every F_j (one block per pod: its ranks and the positions of its
+// feasible nodes in LDS).  Four radix-4 rounds compose the prefixes,
+// Q_j = F_j o ... o F_max(0, j-4^r+1) after round r, so pod j starts at
+// Q_{j-1}(s_0) (k_win_final).  Six launches of independent table lookups in
+// place of the walk's 256 dependent steps on one wave.
+__global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ st,
+                                                   const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
+                                                   int32_t k, uint16_t* __restrict__ tab0, int32_t* __restrict__ wtot) {
+  __shared__ uint64_t s_w[kWinSeqWords];
+  __shared__ int32_t s_pc[kWinSeqWords];
+  __shared__ int32_t s_tot0;
+  __shared__ uint16_t s_sel[kWinSeqWords * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int32_t j = blockIdx.x;
+  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // block-uniform
+  const uint64_t* m = amask + (size_t)j * n_words;
+  if (tid < kWinSeqWords) {                        // the words' prefix counts, two waves
+    const uint64_t w = tid < n_words ? m[tid] : 0ull;
+    s_w[tid] = w;
+    const int32_t c = (int32_t)__popcll(w);
+    int32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    s_pc[tid] = x - c;
+    if (tid == 63) s_tot0 = x;
   }
-  s = __builtin_amdgcn_readfirstlane(s);               // every value below is scalar
-  const int32_t ws = s >> 6, sb = s & 63;
-  const bool whi = ws >= 64;                           // uniform: the word's half (a selects, no branch)
-  const int32_t pw = __builtin_amdgcn_readlane(whi ? pb : pa, ws & 63);
-  const uint64_t mw = readlane_u64(whi ? b : a, ws & 63);
-  int32_t t = __builtin_amdgcn_readfirstlane(pw + (int32_t)__popcll(mw & ((1ull << sb) - 1)) + k);   // the cut's rank
-  const bool wrap = t >= total;
-  if (wrap) t -= total;
-  const uint64_t ba = __ballot(pa <= t), bb = __ballot(pb <= t);    // pc[0] = 0: ba != 0
-  const int32_t lo = bb ? 127 - (int32_t)__builtin_clzll(bb) : 63 - (int32_t)__builtin_clzll(ba);
-  const bool lhi = lo >= 64;
-  const uint64_t x = readlane_u64(lhi ? b : a, lo & 63);
-  const int32_t r = __builtin_amdgcn_readfirstlane(t - __builtin_amdgcn_readlane(lhi ? pb : pa, lo & 63));
-  // the r-th (0-based) set bit of x: lane l tests bit l and the count of bits 0..l
-  const uint64_t upto = x & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-  const uint64_t hit = __ballot(((x >> lane) & 1ull) && (int32_t)__popcll(upto) == r + 1);
-  const int32_t pos = lo * 64 + (int32_t)__builtin_ctzll(hit);
-  cut = wrap ? pos + n - s : pos - s;
-  return pos;
+  __syncthreads();
+  if (tid >= 64 && tid < kWinSeqWords) s_pc[tid] += s_tot0;
+  __syncthreads();
+  const int32_t total = s_pc[n_words - 1] + (int32_t)__popcll(s_w[n_words - 1]);
+  for (int32_t x = tid; x < n; x += 256) {         // the positions of the feasible nodes by rank
+    const uint64_t w = s_w[x >> 6];
+    const int b = x & 63;
+    if ((w >> b) & 1ull) s_sel[s_pc[x >> 6] + (int32_t)__popcll(w & ((1ull << b) - 1ull))] = (uint16_t)x;
+  }
+  __syncthreads();
+  uint16_t* out = tab0 + (size_t)j * n;
+  for (int32_t x = tid; x < n; x += 256) {
+    const uint64_t w = s_w[x >> 6];
+    int32_t t = s_pc[x >> 6] + (int32_t)__popcll(w & ((1ull << (x & 63)) - 1ull)) + k;   // the cut's rank
+    if (t >= total) t -= total;
+    out[x] = total > k ? s_sel[t] : (uint16_t)x;
+  }
+  if (tid == 0) wtot[j] = total;
 }
-#if defined(KSIM_WIN_CLOCKS) && !defined(KSIM_CP_CLOCKS)
-// phase clocks (KSIM_WIN_CLOCKS builds, ksim_get_diag dbg): staging, walk, launches, kernel, pods
-__device__ unsigned long long g_win_dbg[8];
-unsigned long long* cp_clock_buffer() {
-  void* p = nullptr;
-  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_win_dbg));
-  return (unsigned long long*)p;
-}
-#define WIN_CLK(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
-#define WIN_ADD(slot_, val_) do { if (threadIdx.x == 0) atomicAdd(&g_win_dbg[slot_], (unsigned long long)(val_)); } while (0)
-#else
-#define WIN_CLK(v) do {} while (0)
-#define WIN_ADD(slot_, val_) do {} while (0)
-#endif
-constexpr int32_t kWinSeqLdsWords = 11776;             // staged bitmap words (92 KB) per slice
 
-__global__ __launch_bounds__(kWinSeqThreads) void k_adapt_window_seq(const DevState* __restrict__ st,
-                                                                     const uint64_t* __restrict__ amask,
-                                                                     int32_t n_words, int32_t n, int32_t k,
-                                                                     int32_t* __restrict__ awin,
-                                                                     int32_t* __restrict__ aexact) {
-  __shared__ uint16_t s_pc[kBatchPods][kWinSeqWords + 2];   // [w < n_words] counts, [n_words] the total
-  __shared__ uint64_t s_mk[kWinSeqLdsWords];                // the slice's bitmaps, pod-major
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
-  if (nb <= 0) return;                                 // block-uniform
-  const bool ina = lane < n_words, inb = lane + 64 < n_words;
-  const int32_t la = min(lane, n_words - 1), lb = min(lane + 64, n_words - 1);
-  const int32_t slice = min(nb, kWinSeqLdsWords / n_words);
-  struct Ops {
-    uint64_t a, b;
-    int32_t pa, pb, tot;
-  };
-  int32_t s = __builtin_amdgcn_readfirstlane(st->next_start);
-  int32_t my_s = 0, my_cut = -1;                       // lane l: pod (j & ~63) + l's window, stored per 64 pods
-  WIN_CLK(t_start);
-  for (int32_t j_lo = 0; j_lo < nb; j_lo += slice) {
-    const int32_t j_hi = min(nb, j_lo + slice);
-    if (j_lo > 0) __syncthreads();                     // the walk of the previous slice is done
-    WIN_CLK(t_stage);
-    {                                                  // the slice's bitmaps, one coalesced copy
-      const int32_t words = (j_hi - j_lo) * n_words;
-      const uint64_t* src = amask + (size_t)j_lo * n_words;
-      constexpr int kCopy = 4;                         // loads in flight per thread
-      for (int32_t x0 = tid; x0 < words; x0 += kCopy * kWinSeqThreads) {
-        uint64_t v[kCopy];
-#pragma unroll
-        for (int u = 0; u < kCopy; u++) v[u] = src[min(x0 + u * kWinSeqThreads, words - 1)];
-#pragma unroll
-        for (int u = 0; u < kCopy; u++)
-          if (x0 + u * kWinSeqThreads < words) s_mk[x0 + u * kWinSeqThreads] = v[u];
-      }
-    }
-    __syncthreads();
-    if (tid < j_hi - j_lo) {                           // thread t: pod j_lo + t's prefix counts
-      const uint64_t* d = s_mk + (size_t)tid * n_words;
-      uint16_t* pc = s_pc[j_lo + tid];
-      int32_t acc = 0;
-#pragma unroll 8
-      for (int32_t w = 0; w < n_words; w++) {
-        pc[w] = (uint16_t)acc;
-        acc += __popcll(d[w]);
-      }
-      pc[n_words] = (uint16_t)acc;
-    }
-    __syncthreads();
-    WIN_CLK(t_walk);
-    WIN_ADD(0, t_walk - t_stage);
-    if (wv != 0) continue;                             // wave 0 walks the slice
-    auto load = [&](int32_t jj) {
-      jj = min(jj, j_hi - 1);
-      const uint64_t* d = s_mk + (size_t)(jj - j_lo) * n_words;
-      return Ops{d[la], d[lb], (int32_t)s_pc[jj][la], (int32_t)s_pc[jj][lb], (int32_t)s_pc[jj][n_words]};
-    };
-    auto step = [&](const Ops& cur, int32_t j) {
-      int32_t cut;
-      const int32_t next = walk_step(cur.a, cur.b, cur.pa, cur.pb, cur.tot, ina, inb, lane, s, n, k, cut);
-      if (lane == (j & 63)) {
-        my_s = s;
-        my_cut = cut;
-      }
-      if ((j & 63) == 63 || j == nb - 1) {             // uniform: this group of 64 pods is done
-        const int32_t g = j & ~63;
-        if (lane <= j - g) {
-          awin[2 * (g + lane)] = my_s;
-          awin[2 * (g + lane) + 1] = my_cut;
-        }
-      }
-      s = __builtin_amdgcn_readfirstlane(next);
-    };
-    // four register sets in rotation, each refilled kAhead pods ahead
-    Ops o0 = load(j_lo), o1 = load(j_lo + 1), o2 = load(j_lo + 2), o3 = load(j_lo + 3);
-    int32_t j = j_lo;
-    for (; j + 3 < j_hi; j += 4) {
-      step(o0, j);
-      o0 = load(j + 4);
-      step(o1, j + 1);
-      o1 = load(j + 5);
-      step(o2, j + 2);
-      o2 = load(j + 6);
-      step(o3, j + 3);
-      o3 = load(j + 7);
-    }
-    if (j < j_hi) step(o0, j++);
-    if (j < j_hi) step(o1, j++);
-    if (j < j_hi) step(o2, j++);
-    WIN_CLK(t_done);
-    WIN_ADD(1, t_done - t_walk);
+// Round with stride d: Q'_j = Q_j o Q_{j-d} o Q_{j-2d} o Q_{j-3d} (terms with
+// a negative index left out).
+__global__ __launch_bounds__(256) void k_win_round(const DevState* __restrict__ st, int32_t n, int32_t d,
+                                                   const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
+  const int32_t j = blockIdx.y;
+  const int32_t x = blockIdx.x * 256 + threadIdx.x;
+  if (j >= min(kBatchPods, st->end - st->cursor) || x >= n) return;
+  int32_t v = x;
+  if (j - 3 * d >= 0) v = src[(size_t)(j - 3 * d) * n + v];
+  if (j - 2 * d >= 0) v = src[(size_t)(j - 2 * d) * n + v];
+  if (j - d >= 0) v = src[(size_t)(j - d) * n + v];
+  dst[(size_t)j * n + x] = src[(size_t)j * n + v];
+}
+
+__global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __restrict__ st,
+                                                          const uint16_t* __restrict__ tab0,
+                                                          const uint16_t* __restrict__ q,
+                                                          const int32_t* __restrict__ wtot, int32_t n, int32_t k,
+                                                          int32_t* __restrict__ awin, int32_t* __restrict__ aexact) {
+  const int32_t j = threadIdx.x;
+  const int32_t nb = min(kBatchPods, st->end - st->cursor);
+  if (nb <= 0) return;
+  if (j < nb) {
+    const int32_t s0 = st->next_start;
+    const int32_t s = j == 0 ? s0 : (int32_t)q[(size_t)(j - 1) * n + s0];
+    const int32_t nx = tab0[(size_t)j * n + s];
+    awin[2 * j] = s;
+    awin[2 * j + 1] = wtot[j] <= k ? -1 : (nx > s ? nx - s : nx + n - s);
   }
-  if (tid == 0) *aexact = nb;
-  WIN_CLK(t_end);
-  WIN_ADD(2, 1);
-  WIN_ADD(3, t_end - t_start);
-  WIN_ADD(4, nb);
+  if (j == 0) *aexact = nb;
+}
+
+static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, hipStream_t stream) {
+  const int32_t n = a.c.n;
+  uint16_t* t0 = a.s.wtab;
+  uint16_t* t1 = t0 + (size_t)kBatchPods * n;
+  uint16_t* t2 = t1 + (size_t)kBatchPods * n;
+  k_win_build<<<kBatchPods, 256, 0, stream>>>(a.st, a.s.amask, n_words, n, k, t0, a.s.wtot);
+  const dim3 grid((n + 255) / 256, kBatchPods);
+  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 1, t0, t1);
+  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 4, t1, t2);
+  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 16, t2, t1);
+  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 64, t1, t2);
+  static_assert(kBatchPods <= 256, "four radix-4 rounds cover 256 pods");
+  k_win_final<<<1, kBatchPods, 0, stream>>>(a.st, t0, t2, a.s.wtot, n, k, a.s.awin, a.s.aexact);
 }
 
 // Clusters up to this many bitmap words run the window scan inside k_adapt_top
@@ -983,7 +923,7 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   const bool win_seq = !a.fast && n_words <= kWinSeqWords;
   const bool win_fused = !win_seq && k < kTopWideK && n_words <= kWinFusedWords;
   if (win_seq)
-    k_adapt_window_seq<<<1, kWinSeqThreads, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+    launch_window_dbl(a, n_words, k, stream);
   else if (!win_fused)
     k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);

@@ -654,7 +654,7 @@ unsigned long long* cp_clock_buffer() {
   (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_cp_dbg));
   return (unsigned long long*)p;
 }
-#elif !defined(KSIM_WIN_CLOCKS)
+#else
 unsigned long long* cp_clock_buffer() { return nullptr; }
 #endif
 

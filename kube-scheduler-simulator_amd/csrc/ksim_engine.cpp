@@ -2045,6 +2045,11 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.amask, uint64_t*, 8 * (size_t)kBatchPods * ((N + 63) / 64));
   SCR(s.awin, int32_t*, 4 * 2 * (size_t)kBatchPods);
   SCR(s.aexact, int32_t*, 4);
+  {                                      // the doubling window's tables (clusters of <= 128 bitmap words)
+    const size_t NW = (N + 63) / 64 <= 128 ? N : 0;
+    SCR(s.wtab, uint16_t*, 2 * 3 * (size_t)kBatchPods * std::max<size_t>(NW, 1));
+    SCR(s.wtot, int32_t*, 4 * (size_t)kBatchPods);
+  }
   SCR(s.abroken, int32_t*, 4 * (size_t)kBatchPods);
   SCR(s.xreg, int64_t*, 8 * (1 + (size_t)KSIM_MAX_USES * vmax));
   SCR(o.scored, uint8_t*, N);
@@ -2975,16 +2980,18 @@ void tbatch_runs(const ksim_handle* h, const ksim_pod_set* ps, const std::vector
   int32_t n_cls = 0;
   for (int32_t k = 0; k < ps->n_adds; k++) n_cls = std::max(n_cls, ps->adds[k].cls + 1);
   std::vector<int32_t> stamp((size_t)n_cls, -1);   // class -> the window start that added it
+  static const int32_t cap = getenv("KSIM_TB_CAP") ? std::max(1, std::min(kTbPods, atoi(getenv("KSIM_TB_CAP")))) : kTbPods;
+  static const bool nocross = getenv("KSIM_TB_NOCROSS") != nullptr;
   for (int32_t i = 0; i < n; i++) {
     if (batchable[i] != 3) continue;
     int32_t L = 0;
-    for (int32_t j = i; j < n && L < kTbPods && batchable[j] == 3; j++, L++) {
+    for (int32_t j = i; j < n && L < cap && batchable[j] == 3; j++, L++) {
       const ksim_pod& p = ps->pods[j];
       const ksim_topo_use* U = uses.data() + p.use_first;
       bool clash = false;
       for (int32_t u = 0; u < p.use_count && !clash; u++) {
         const int32_t c = U[u].cls;
-        clash = c >= 0 && c < n_cls && stamp[c] == i && !tbatch_conflict_ok(h, U, u);
+        clash = c >= 0 && c < n_cls && stamp[c] == i && (nocross || !tbatch_conflict_ok(h, U, u));
       }
       if (clash) break;
       for (int32_t a = 0; a < p.add_count; a++) stamp[ps->adds[p.add_first + a].cls] = i;

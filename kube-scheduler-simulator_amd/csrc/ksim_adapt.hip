@@ -262,10 +262,11 @@ constexpr int32_t kWinSeqWords = 128;
 // F_j: start -> next start over the n starts (the (K+1)-th feasible node
 // from the start, the start itself when at most K are feasible).  k_win_build
 // tabulates every F_j (one block per pod: its ranks and the positions of its
-// feasible nodes in LDS).  Four radix-4 rounds compose the prefixes,
-// Q_j = F_j o ... o F_max(0, j-4^r+1) after round r, so pod j starts at
-// Q_{j-1}(s_0) (k_win_final).  Six launches of independent table lookups in
-// place of the walk's 256 dependent steps on one wave.
+// feasible nodes in LDS).  Radix-4 rounds compose the prefixes,
+// Q_j = F_j o ... o F_max(0, j-4^r+1) after round r; three over whole tables
+// (strides 1, 4, 16), the fourth (stride 64) only at s_0 inside k_win_final,
+// where pod j starts at Q_{j-1}(s_0).  Five launches of independent table
+// lookups in place of the walk's 256 dependent steps on one wave.
 __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
                                                    int32_t k, uint16_t* __restrict__ tab0, int32_t* __restrict__ wtot) {
@@ -333,8 +334,14 @@ __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __rest
   const int32_t nb = min(kBatchPods, st->end - st->cursor);
   if (nb <= 0) return;
   if (j < nb) {
-    const int32_t s0 = st->next_start;
-    const int32_t s = j == 0 ? s0 : (int32_t)q[(size_t)(j - 1) * n + s0];
+    // the last radix-4 round (stride 64) at s_0 alone: Q_{j-1} composed from
+    // the 64-pod prefixes in q
+    const int32_t s0 = st->next_start, i = j - 1;
+    int32_t s = s0;
+    if (i - 192 >= 0) s = q[(size_t)(i - 192) * n + s];
+    if (i - 128 >= 0) s = q[(size_t)(i - 128) * n + s];
+    if (i - 64 >= 0) s = q[(size_t)(i - 64) * n + s];
+    if (i >= 0) s = q[(size_t)i * n + s];
     const int32_t nx = tab0[(size_t)j * n + s];
     awin[2 * j] = s;
     awin[2 * j + 1] = wtot[j] <= k ? -1 : (nx > s ? nx - s : nx + n - s);
@@ -352,9 +359,8 @@ static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, h
   k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 1, t0, t1);
   k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 4, t1, t2);
   k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 16, t2, t1);
-  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 64, t1, t2);
   static_assert(kBatchPods <= 256, "four radix-4 rounds cover 256 pods");
-  k_win_final<<<1, kBatchPods, 0, stream>>>(a.st, t0, t2, a.s.wtot, n, k, a.s.awin, a.s.aexact);
+  k_win_final<<<1, kBatchPods, 0, stream>>>(a.st, t0, t1, a.s.wtot, n, k, a.s.awin, a.s.aexact);
 }
 
 // Clusters up to this many bitmap words run the window scan inside k_adapt_top

@@ -1530,7 +1530,8 @@ constexpr int32_t kBatchStaticTrivial = 1; // every static filter passes on ever
 constexpr int32_t kPodRegistersValues = 2; // has a ScheduleAnyway spread keyed by a non-hostname column
 constexpr int32_t kPodNormVaries = 4;      // batch path: TaintToleration / NodeAffinity vary over nodes (norm_part)
 constexpr int32_t kPodTopoBatch = 8;       // topology batch path (ksim_tbatch.hip)
-constexpr int kTlenShift = 8;              // bflags >> kTlenShift: pods from this one with no class conflict (tbatch)
+constexpr int32_t kPodTbCross = 16;       // topology batch run from this pod crosses a class conflict (node-local)
+constexpr int kTlenShift = 8;              // bflags >> kTlenShift: topology batch run length from this pod
 
 // Compact row for the batch repair's LDS staging: the NodeRow fields a
 // batchable pod can read (batchable pods request no scalar resources and the

@@ -2956,47 +2956,51 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
 }
 
 // A use of a topology batch pod that may read a class an earlier pod of its
-// run adds (ksim_tbatch.hip k_tb_chain_pairs): node-local (the guessed node's
-// own count, re-keyed there), or a PodTopologySpread DoNotSchedule constraint
-// read from a persistent table, among the pod's first kTbHardDom, on a key of
-// at most kTbDomValues values (its per-domain verdicts re-checked).
-static bool tbatch_conflict_ok(const ksim_handle* h, const ksim_topo_use* U, int32_t i) {
-  const ksim_topo_use& u = U[i];
-  if (use_node_count(u)) return u.kind != KSIM_USE_PTS_HARD && u.kind != KSIM_USE_NODE_PORT && u.kind != KSIM_USE_IMAGE;
-  if (u.kind != KSIM_USE_PTS_HARD || u.col == KSIM_COL_NONE || h->col_nvals[u.col] > kTbDomValues) return false;
-  int32_t ord = 0;
-  for (int32_t x = 0; x < i; x++) ord += U[x].kind == KSIM_USE_PTS_HARD;
-  return ord < kTbHardDom;
+// run adds (ksim_tbatch.hip k_tb_chain_pairs): a node-local one (the guessed
+// node's own count, re-keyed there).  A domain-keyed use ends the run: pod
+// k's bind moves a whole domain for pod j.  Re-checking DoNotSchedule domain
+// verdicts per batch was built and measured on config 3 (profiles/r04/tbcap):
+// once an app's zones are level, nearly every bind of the app flips a zone's
+// verdict, so the crossing pods were cut (pinv) after their evaluation was
+// paid for (61.6 ms per step without crossing, 68.6-81.4 ms with).
+static bool tbatch_conflict_ok(const ksim_topo_use& u) {
+  return use_node_count(u) && u.kind != KSIM_USE_PTS_HARD && u.kind != KSIM_USE_NODE_PORT &&
+         u.kind != KSIM_USE_IMAGE;
 }
 
 // Topology batch runs (class 3 pods, ksim_tbatch.hip): tlen[i] = the number
 // of consecutive class-3 pods from i (at most kTbPods) none of which reads a
 // count class an earlier one of them adds through a use tbatch_conflict_ok
-// refuses.  0 for the other pods.  uses: the queue's device use copies.
-void tbatch_runs(const ksim_handle* h, const ksim_pod_set* ps, const std::vector<ksim_topo_use>& uses,
-                 const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen) {
+// refuses; cross[i]: the run crosses a conflict.  0 for the other pods.
+// uses: the queue's device use copies.
+void tbatch_runs(const ksim_pod_set* ps, const std::vector<ksim_topo_use>& uses,
+                 const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen, std::vector<uint8_t>& cross) {
   const int32_t n = ps->n_pods;
   tlen.assign((size_t)std::max(n, 0), 0);
+  cross.assign((size_t)std::max(n, 0), 0);
   int32_t n_cls = 0;
   for (int32_t k = 0; k < ps->n_adds; k++) n_cls = std::max(n_cls, ps->adds[k].cls + 1);
   std::vector<int32_t> stamp((size_t)n_cls, -1);   // class -> the window start that added it
-  static const int32_t cap = getenv("KSIM_TB_CAP") ? std::max(1, std::min(kTbPods, atoi(getenv("KSIM_TB_CAP")))) : kTbPods;
-  static const bool nocross = getenv("KSIM_TB_NOCROSS") != nullptr;
   for (int32_t i = 0; i < n; i++) {
     if (batchable[i] != 3) continue;
     int32_t L = 0;
-    for (int32_t j = i; j < n && L < cap && batchable[j] == 3; j++, L++) {
+    bool crossed = false;
+    for (int32_t j = i; j < n && L < kTbPods && batchable[j] == 3; j++, L++) {
       const ksim_pod& p = ps->pods[j];
       const ksim_topo_use* U = uses.data() + p.use_first;
-      bool clash = false;
+      bool clash = false, hit = false;
       for (int32_t u = 0; u < p.use_count && !clash; u++) {
         const int32_t c = U[u].cls;
-        clash = c >= 0 && c < n_cls && stamp[c] == i && (nocross || !tbatch_conflict_ok(h, U, u));
+        if (c < 0 || c >= n_cls || stamp[c] != i) continue;
+        hit = true;
+        clash = !tbatch_conflict_ok(U[u]);
       }
       if (clash) break;
+      crossed = crossed || hit;
       for (int32_t a = 0; a < p.add_count; a++) stamp[ps->adds[p.add_first + a].cls] = i;
     }
     tlen[i] = std::max(L, 1);
+    cross[i] = crossed;
   }
 }
 
@@ -3133,8 +3137,10 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
       bf[i] |= kPodTopoBatch;
     }
   }
-  tbatch_runs(h, ps, uses, batchable, h->tlen);
-  for (int32_t i = 0; i < ps->n_pods; i++) bf[i] |= std::min(h->tlen[i], 255) << kTlenShift;
+  std::vector<uint8_t> tcross;
+  tbatch_runs(ps, uses, batchable, h->tlen, tcross);
+  for (int32_t i = 0; i < ps->n_pods; i++)
+    bf[i] |= (std::min(h->tlen[i], 255) << kTlenShift) | (tcross[(size_t)i] ? kPodTbCross : 0);
   DevPods P{};
   void* p = nullptr;
   if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return drop_queue(rc);

@@ -58,14 +58,10 @@ extern const char* const kAdaptKernelNames[kKernelsPerAdapt];
 // Topology batch path (ksim_tbatch.hip): at most kTbPods pods per batch (the
 // host's runs, bflags >> kTlenShift), clusters of at most kTbMaxBlocks node
 // blocks of 256.  A run may cross a class an earlier pod of it adds when every
-// such use is node-local (the pairs step re-keys the guessed node) or a
-// PodTopologySpread DoNotSchedule constraint among the pod's first kTbHardDom
-// ones whose key has at most kTbDomValues values (the pairs step re-checks its
-// per-domain verdicts); tbatch_conflict_ok.
-constexpr int kTbPods = 64;
+// use that reads it is node-local (tbatch_conflict_ok; the pairs step re-keys
+// the guessed node; the run's first pod carries kPodTbCross).
+constexpr int kTbPods = 32;
 constexpr int kTbMaxBlocks = 64;
-constexpr int kTbHardDom = 4;
-constexpr int kTbDomValues = 64;
 constexpr int kKernelsPerTbatch = 5;
 extern const char* const kTbatchKernelNames[kKernelsPerTbatch];
 uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);

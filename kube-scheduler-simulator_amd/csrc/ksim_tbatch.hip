@@ -264,17 +264,20 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
     }
     q.stat[node] = stat;
   }
-  // holder counts: one popcount per wave, one atomic per block and counter
-  // (after block_top_t's barrier)
+  // holder counts (runs that cross a class conflict): one popcount per wave,
+  // one atomic per block and counter (after block_top_t's barrier)
+  const bool cross = (P0.bflags[st->cursor] & kPodTbCross) != 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (cross) {
 #pragma unroll
-  for (int h = 0; h < 4; h++) {
-    const int32_t n = (int32_t)__popcll(__ballot((hf >> h) & 1u));
-    if (lane == 0) s_hold[wv][h] = n;
+    for (int h = 0; h < 4; h++) {
+      const int32_t n = (int32_t)__popcll(__ballot((hf >> h) & 1u));
+      if (lane == 0) s_hold[wv][h] = n;
+    }
   }
   block_top_t(key, s_cand, s.tb_clist + ((size_t)j * kTbMaxBlocks + blockIdx.x) * kTopT,
               s.tb_ccnt + (size_t)j * kTbMaxBlocks + blockIdx.x);
-  if (threadIdx.x < 4) {
+  if (cross && threadIdx.x < 4) {
     int kp = -1, ki = -1;                          // the profile's slots (block-uniform)
     for (int k = 0; k < S; k++) {
       const int32_t kind = norm_kind(prof_score(prof, k));
@@ -417,12 +420,12 @@ __device__ __forceinline__ bool tb_keeps_extrema(int64_t x0, int64_t x1, int64_t
 // Block j: the chain, then pod j's keys on the guesses of pods k < j after
 // those binds (thread k: pod k's guess), or pinv[j] when pod j's S0 lists no
 // longer describe it.  Pod k's bind moves pod j's inputs only on its guessed
-// node g (the resources; the classes pod k adds, through pod j's node-local
-// uses) and, for pod j's PodTopologySpread DoNotSchedule constraints on small
-// keys, in g's domain.  The key on g is the S0 stat with the resource part
-// and the changed PodTopologySpread / InterPodAffinity raw scores recomputed
-// against S0's extrema; pinv when a change would move an extremum, the
-// feasible set (a node's verdict, a domain's verdict) or an emptiness flag.
+// node g: the resources and, in a run that crosses a class conflict
+// (kPodTbCross), the classes pod k adds through pod j's node-local uses.  The
+// key on g is the S0 stat with the resource part and the changed
+// PodTopologySpread / InterPodAffinity raw scores recomputed against S0's
+// extrema; pinv when a change would move an extremum, the feasible set (a
+// node's verdict) or an emptiness flag.
 // pp (replicas): pair maxima and pinv into pp[j] / pp[kTbPods + j], keyed
 // only on the guesses in this replica's range (the all-reduce max combines).
 __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, DevPods P,
@@ -433,8 +436,6 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   __shared__ ChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   __shared__ int32_t s_winv[kBatchPods / 64];
-  __shared__ int32_t s_dd[kTbHardDom][kTbDomValues];   // pod j's DoNotSchedule count deltas per domain
-  __shared__ int32_t s_ddany;
   const int32_t nbt = tb_count(st, P);
   uint64_t gk;
   int32_t nchain;
@@ -458,9 +459,6 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     }
     return;
   }
-  for (int x = tid; x < kTbHardDom * kTbDomValues; x += kBatchPods) (&s_dd[0][0])[x] = 0;
-  if (tid == 0) s_ddany = 0;
-  __syncthreads();
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
@@ -473,6 +471,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const WinState* win = s.tb_win + j;
   const uint32_t tf = win->tflags;
   const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
+  const bool cross = (P.bflags[base] & kPodTbCross) != 0;
   uint64_t v = 0;
   bool inv = false;
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
@@ -482,7 +481,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     const ksim_pod& pk = P.pods[base + k];
     int64_t d_soft = 0, d_ipa = 0;
     bool hit_anti = false, hit_aff = false, hit_score = false;
-    for (int i = 0; i < nu; i++) {
+    for (int i = 0; cross && i < nu; i++) {
       const ksim_topo_use u = load_use(U, i);
       if (u.cls < 0) continue;
       int32_t d = 0;
@@ -501,17 +500,8 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
           d_ipa += ipa_coef(prof, u) * d;
         }
         if (i == soft) d_soft += d;
-      } else if ((m.hard & b) && !(m.node_count & b)) {   // g's domain
-        const int ord = __popc(m.hard & (b - 1u));
-        const uint32_t dv = use_value(c, u, local);
-        if (ord < kTbHardDom && dv < (uint32_t)kTbDomValues) {
-          atomicAdd(&s_dd[ord][dv], d);
-          s_ddany = 1;
-        } else {
-          inv = true;
-        }
       } else {
-        inv = true;                                // a domain-keyed InterPodAffinity use (tbatch_conflict_ok)
+        inv = true;                                // a domain-keyed use (the host ends runs there)
       }
     }
     if (hit_aff && !(tf & kTopoAffinityNonEmpty)) inv = true;   // len(affinityCounts) would change
@@ -572,31 +562,9 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   }
   __syncthreads();
   if (wave == 0) {
-    bool dinv = false;
-    if (s_ddany) {                                 // block-uniform: the domains' verdicts, before and after
-      for (int i = 0, ord = 0; i < nu && ord < kTbHardDom; i++) {
-        if (!((m.hard >> i) & 1u)) continue;
-        const int o = ord++;
-        if ((m.node_count >> i) & 1u) continue;
-        const ksim_topo_use u = load_use(U, i);
-        if (u.col == KSIM_COL_NONE) continue;
-        const int32_t V = c.col_nvals[u.col];
-        if (V > kTbDomValues) {                    // unchecked domains (tbatch_conflict_ok refuses these)
-          dinv = true;
-          break;
-        }
-        const int64_t self = (m.self_match >> i) & 1u;
-        const int64_t x = lane < V && lane < kTbDomValues ? P.ptab[u._pad + lane] : 0;
-        const bool present = (x >> kDomMarkShift) != 0;
-        const int64_t c0 = x & kDomCountMask, c1 = c0 + (lane < kTbDomValues ? s_dd[o][lane] : 0);
-        const int64_t min0 = wave_min_i64(present ? c0 : INT64_MAX), min1 = wave_min_i64(present ? c1 : INT64_MAX);
-        const bool ok0 = c0 + self - min0 <= (int64_t)u.arg, ok1 = c1 + self - min1 <= (int64_t)u.arg;
-        if (__ballot(present && lane != 0 && ok0 != ok1)) dinv = true;
-      }
-    }
     if (tid == 0) {
       uint64_t mx = 0;
-      int32_t any = dinv;
+      int32_t any = 0;
       for (int w = 0; w < kBatchPods / 64; w++) {
         mx = umax64(mx, s_wmax[w]);
         any |= s_winv[w];

@@ -2,8 +2,8 @@
 tbatch_admit in ksim_engine.cpp) against the one-by-one oracle: pods with
 PodTopologySpread and InterPodAffinity uses read from the persistent domain
 tables, scheduled up to kTbPods at a time over runs that cross a class an
-earlier pod of the run adds only through uses the pairs step repairs
-(tbatch_conflict_ok).  Placements, evaluation counts,
+earlier pod of the run adds only through node-local uses the pairs step
+re-keys (tbatch_conflict_ok).  Placements, evaluation counts,
 node rows and count classes must equal the oracle's (config 3 shapes:
 /root/reference/simulator/scheduler/scheduler.go runs the upstream
 scheduler's per-pod cycle; the restatement is oracle/ksim_oracle.c)."""
@@ -65,11 +65,10 @@ def test_nodes_fill_up():
     assert st.perpod_cycles == 0 and st.unschedulable > 0 and st.truncations > 0
 
 
-def test_one_app_crosses_classes():
-    """Every pod spreads over the same selector: each pod reads the classes the
-    earlier ones add (the zone DoNotSchedule counts, the hostname counts); the
-    runs cross them and the pairs step cuts where a zone's verdict flips or an
-    extremum moves; still exact."""
+def test_one_app_serializes():
+    """Every pod spreads over the same selector: each pod reads the zone
+    DoNotSchedule counts the previous one adds (a domain-keyed use), so every
+    batch holds one pod; still exact."""
     nodes, bound, inc = gen.config3_objects(n_nodes=200, pods_per_node=3, n_incoming=200, seed=9)
     for p in inc:
         p.labels["app"] = "a7"
@@ -79,15 +78,19 @@ def test_one_app_crosses_classes():
             w.term.label_selector = LabelSelector({"app": "a7"})
     cluster, _ = encode_cluster(nodes, bound)
     eng, st = _run(cluster, encode_pods(cluster, inc))
-    assert st.perpod_cycles == 0 and st.batches <= 200
+    assert st.perpod_cycles == 0 and st.batches == 200
 
 
-def _few_apps(inc, n_apps, rng):
+def _few_apps(inc, n_apps, rng, zone=True):
     """Incoming pods relabelled to n_apps apps (selectors follow): most pods of
-    a batch read classes earlier ones add."""
+    a batch read classes earlier ones add.  zone=False drops the zone
+    DoNotSchedule constraint (a domain-keyed use ends a run; the hostname
+    spread and the preferred anti-affinity are node-local and runs cross them)."""
     for p in inc:
         app = f"a{int(rng.integers(0, n_apps))}"
         p.labels["app"] = app
+        if not zone:
+            p.topology_spread = [c for c in p.topology_spread if c.when_unsatisfiable == "ScheduleAnyway"]
         for c in p.topology_spread:
             c.label_selector = LabelSelector({"app": app})
         for w in p.pod_anti_affinity_preferred:
@@ -95,15 +98,15 @@ def _few_apps(inc, n_apps, rng):
     return inc
 
 
-@pytest.mark.parametrize("n_apps,per_node", [(2, 4), (6, 4), (6, 0)])
-def test_cross_class_runs(n_apps, per_node):
+@pytest.mark.parametrize("n_apps,per_node,zone", [(2, 4, False), (6, 4, False), (6, 0, False), (6, 4, True)])
+def test_cross_class_runs(n_apps, per_node, zone):
     """Runs that cross class conflicts (tbatch_conflict_ok): pods of few apps
     re-key the guessed nodes (hostname spread counts, preferred anti-affinity
-    scores, the holders of the extrema) and re-check the zone verdicts.  With
-    no existing pods the InterPodAffinity topologyScore starts empty (the
-    emptiness flag flips)."""
+    scores, the holders of the extrema).  With no existing pods the
+    InterPodAffinity topologyScore starts empty (the emptiness flag flips).
+    With the zone DoNotSchedule constraint runs end at the conflicts."""
     nodes, bound, inc = gen.config3_objects(n_nodes=600, pods_per_node=per_node, n_incoming=1500, seed=31 + n_apps)
-    inc = _few_apps(inc, n_apps, np.random.default_rng(n_apps))
+    inc = _few_apps(inc, n_apps, np.random.default_rng(n_apps), zone=zone)
     cluster, _ = encode_cluster(nodes, bound)
     eng, st = _run(cluster, encode_pods(cluster, inc))
     # few apps over 3 zones even out quickly: many zone verdicts flip (pinv)
@@ -118,7 +121,7 @@ def test_cross_class_required_terms():
     from ksim.model import PodAffinityTerm
     nodes, bound, inc = gen.config3_objects(n_nodes=400, pods_per_node=3, n_incoming=1200, seed=41)
     rng = np.random.default_rng(41)
-    inc = _few_apps(inc, 5, rng)
+    inc = _few_apps(inc, 5, rng, zone=False)
     for k, p in enumerate(inc):
         if k % 4 == 1:
             p.pod_anti_affinity_required = [PodAffinityTerm("kubernetes.io/hostname",

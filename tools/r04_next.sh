@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: topology batches across classes, replicated topology batches, the
 # doubling ADAPT window: their GPU tests, then config 3, config 1 scaled under
-# ADAPT (doubling / ordered walk) and the drop-in cycle.  Output under
+# ADAPT (doubling) and the drop-in cycle.  Output under
 # gpurun_out/${TAG:-r04next}.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -27,8 +27,6 @@ timeout -k 10 400 python3 -u bench.py --config 3 --steps 3 --warmup 1 > "$OUT/be
 summ "$OUT/bench_config3.json"
 timeout -k 10 300 python3 -u bench.py --config 1 --mode adapt --steps 2 --warmup 1 --no-cpu > "$OUT/c1a_dbl.json" 2> "$OUT/c1a_dbl.err" || exit $?
 summ "$OUT/c1a_dbl.json"
-KSIM_WIN_WALK=1 timeout -k 10 300 python3 -u bench.py --config 1 --mode adapt --steps 2 --warmup 1 --no-cpu > "$OUT/c1a_walk.json" 2> "$OUT/c1a_walk.err" || exit $?
-summ "$OUT/c1a_walk.json"
 [ -n "$NOFW" ] && exit 0
 timeout -k 10 300 python3 -u bench.py --mode fw > "$OUT/fw.json" 2> "$OUT/fw.err" || exit $?
 python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); [print(r['nodes'], round(r['engine']['us_per_cycle'],1), {k: round(v,1) for k,v in r['engine']['us_per_call'].items()}, round(r['oracle_cpu_1thread']['us_per_cycle'],1)) for r in d['rows']]" "$OUT/fw.json"

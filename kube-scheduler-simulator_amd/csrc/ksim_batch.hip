@@ -1006,9 +1006,9 @@ static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t st
   else if (a.fast)
     k_batch_top<true, 1024><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
                                                               a.s.topk_complete, xsend, a.s.pnorm);
-  else
-    k_batch_top<false, 1024><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
-                                                               a.s.topk_complete, xsend, a.s.pnorm);
+  else   // generic keys: 512 threads, so the full plugin chain's registers fit without spilling
+    k_batch_top<false, 512><<<kBatchPods, 512, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
+                                                             a.s.topk_complete, xsend, a.s.pnorm);
 }
 
 // The chain inside every pairs block (k_batch_chain_pairs).

@@ -67,7 +67,9 @@ __device__ __forceinline__ TbSlice tb_slice(const DevScratch& s, int32_t j, int3
                  s.tb_stat + j * N, s.tb_win + j};
 }
 
-__global__ __launch_bounds__(256) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
+// Three waves per SIMD (152 VGPRs, no spills) instead of the two its 176
+// VGPRs allowed: the kernel waits on its table and row loads most of the time.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
                                                    DevScratch s) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
@@ -465,23 +467,29 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const int64_t seq0 = st->pod_seq;
   const int32_t N = c.n;
   const ksim_pod& p = P.pods[base + j];
-  const UseMasks m = P.plans[base + j].m;
-  const ksim_topo_use* U = P.uses + p.use_first;
-  const int nu = p.use_count;
-  const WinState* win = s.tb_win + j;
-  const uint32_t tf = win->tflags;
-  const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
   const bool cross = (P.bflags[base] & kPodTbCross) != 0;
   uint64_t v = 0;
   bool inv = false;
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
   if (local >= 0 && local < N) {
     const bool own = local >= c.eval_lo && local < c.eval_hi;   // S0 values of g live on its replica
-    // what pod k's adds change for pod j on g = local
+    // what pod k's adds change for pod j on g = local (runs that cross only)
     const ksim_pod& pk = P.pods[base + k];
     int64_t d_soft = 0, d_ipa = 0;
     bool hit_anti = false, hit_aff = false, hit_score = false;
-    for (int i = 0; cross && i < nu; i++) {
+    UseMasks m{};
+    const ksim_topo_use* U = nullptr;
+    const WinState* win = s.tb_win + j;
+    uint32_t tf = 0;
+    int soft = -1, nu = 0;
+    if (cross) {
+      m = P.plans[base + j].m;
+      U = P.uses + p.use_first;
+      nu = p.use_count;
+      tf = win->tflags;
+      soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
+    }
+    for (int i = 0; i < nu; i++) {
       const ksim_topo_use u = load_use(U, i);
       if (u.cls < 0) continue;
       int32_t d = 0;

@@ -20,7 +20,11 @@ SRC, KEEP = sys.argv[1], sys.argv[2]
 # config label -> (bench config, nodes)
 CFG = {"c1": (1, 5000), "c1a": (1, 5000), "c2": (2, 5000), "c3": (3, 10000), "c4a": (4, 100000), "c5": (5, 5000)}
 # kernel symbol -> the bench kernel table's slot name
-NAME = {"k_adapt_window_seq": "k_adapt_window", "k_adapt_mask_ns": "k_adapt_mask"}
+NAME = {"k_adapt_mask_ns": "k_adapt_mask"}
+# kernels launched together in one slot (the doubling ADAPT window): per batch,
+# the sum over the group's dispatches; the anchor runs once per batch
+GROUP = {"k_win_build": "k_adapt_window", "k_win_round": "k_adapt_window", "k_win_final": "k_adapt_window"}
+ANCHOR = {"k_adapt_window": "k_win_final"}
 
 
 def kname(raw):
@@ -51,9 +55,16 @@ for f in glob.glob(os.path.join(SRC, "*", "**", "*counter_collection.csv"), recu
         d = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per[(label, kname(r["Kernel_Name"]), r["Counter_Name"], d)] += float(r["Counter_Value"])
 acc = collections.defaultdict(list)
+gsum, gcnt = collections.defaultdict(float), collections.defaultdict(int)
 for (label, k, c, _), v in per.items():
+    if k in GROUP:
+        slot = GROUP[k]
+        gsum[(label, slot, c)] += v
+        gcnt[(label, slot, c)] += k == ANCHOR[slot]
+        continue
     acc[(label, k, c)].append(v)
 mean = {key: statistics.mean(v) for key, v in acc.items()}
+mean.update({key: v / gcnt[key] for key, v in gsum.items() if gcnt[key]})
 valu, traffic = [], []
 src = f"<KEEP>/summary.txt (tools/r04_pmc.sh + tools/pmc_entries.py: rocprofv3 --pmc, one pass per counter group, " \
       "kernel trace only; counters summed over XCD/SE instances per dispatch, averaged over dispatches; " \

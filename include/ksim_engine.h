@@ -571,7 +571,8 @@ int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int
  *                      PodTopologySpread's IgnoredNodes, pair registration and
  *                      topologyNormalizingWeight over the list, raw / norm /
  *                      total / scored for the listed nodes (the same layout as
- *                      ksim_eval_out).  No selectHost, no bind: chosen = -1
+ *                      ksim_eval_out; the entries of unlisted nodes are left
+ *                      as the caller had them).  No selectHost, no bind: chosen = -1
  *                      (KSIM_CHOSEN_ERROR with status KSIM_STATUS_ERROR when a
  *                      listed node's NetworkBandwidth Score fails).
  *                      Replaces PreScore / Score (wrappedplugin.go:427-454,
@@ -584,7 +585,10 @@ int ksim_forget(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, int
  *                      emptiness).  out[j] = normalized score of entry j;
  *                      plugins without NormalizeScore copy the scores.
  *   Reserve / Unreserve with the framework's node: ksim_assume / ksim_forget
- *                      (wrappedplugin.go:583-584, 617).
+ *                      (wrappedplugin.go:583-584, 617); they return once the
+ *                      update is queued on the handle's stream (every later
+ *                      call on the handle sees it; a device error shows at the
+ *                      next call that synchronizes).
  * Any other cycle or snapshot call on the handle ends a framework cycle in
  * flight.  Unsharded handles only. */
 int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* pods, int32_t pod_index, ksim_eval_out* out);

@@ -148,9 +148,13 @@ struct ksim_handle {
   // compat-mode single pod
   DevArena pod1_arena;                  // the single-pod uploads (upload_single)
   DevArena nom_arena;                   // a nominated pod (ksim_fw_filter_nominated)
-  void* pin = nullptr;                  // pinned host staging for the per-call uploads
+  // pinned, coherent host staging for the per-call uploads / results, and the
+  // device's addresses of it (copy kernels read / write it directly)
+  void* pin = nullptr;
+  void* pin_d = nullptr;
   size_t pin_cap = 0;
-  void* pout = nullptr;                 // pinned host staging for the per-call results
+  void* pout = nullptr;
+  void* pout_d = nullptr;
   size_t pout_cap = 0;
   // DefaultPreemption: bound pods per node in importance order
   std::vector<DevBuf> pre_bufs;
@@ -176,7 +180,6 @@ struct ksim_handle {
   int32_t* fw_nodes = nullptr;     // device [n]
   int64_t* fw_vals = nullptr;      // device [n]
   int64_t* fw_out = nullptr;       // device [n]
-  int64_t* fw_comp = nullptr;      // device: ksim_fw_score's answers for the listed nodes (k_fw_gather)
 
   // node sharding: this handle holds [shard_base, shard_base + n) of shard_total
   int32_t shard_base = 0, shard_total = 0;
@@ -2013,7 +2016,6 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(h->fw_nodes, int32_t*, 4 * N);
   SCR(h->fw_vals, int64_t*, 8 * N);
   SCR(h->fw_out, int64_t*, 8 * N);
-  SCR(h->fw_comp, int64_t*, (16 * (size_t)KSIM_MAX_SCORE + 9) * N);
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
@@ -2371,26 +2373,45 @@ static int arena_reserve(ksim_handle* h, DevArena& a, size_t bytes) {
 static int pin_reserve(ksim_handle* h, size_t bytes) {
   if (bytes <= h->pin_cap) return KSIM_OK;
   if (h->pin) (void)hipHostFree(h->pin);
-  if (h->pout) (void)hipHostFree(h->pout);
-  h->pin = nullptr;
+  h->pin = h->pin_d = nullptr;
   h->pin_cap = 0;
   const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
-  const hipError_t e = hipHostMalloc(&h->pin, cap, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(&h->pin, cap, hipHostMallocCoherent | hipHostMallocMapped);
   if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (staging)");
+  if ((e = hipHostGetDevicePointer(&h->pin_d, h->pin, 0)) != hipSuccess) return hip_fail(h, e, "hipHostGetDevicePointer");
   h->pin_cap = cap;
   return KSIM_OK;
 }
+
+// Copies to / from the pinned staging by one kernel (launch_copy_list).
+struct Copies {
+  CopyList l{};
+  int n = 0;
+  void add(const void* src, void* dst, size_t bytes) {
+    if (!bytes) return;
+    l.src[n] = (const uint8_t*)src;
+    l.dst[n] = (uint8_t*)dst;
+    l.n[n] = (uint32_t)bytes;
+    n++;
+  }
+  int run(ksim_handle* h) {
+    if (n) launch_copy_list(l, n, h->stream);
+    HIPCHK(h, hipGetLastError());
+    return KSIM_OK;
+  }
+};
 
 // The results' pinned staging (callers sync before reading it).
 static int pout_reserve(ksim_handle* h, size_t bytes) {
   if (bytes <= h->pout_cap) return KSIM_OK;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->pout) (void)hipHostFree(h->pout);
-  h->pout = nullptr;
+  h->pout = h->pout_d = nullptr;
   h->pout_cap = 0;
   const size_t cap = std::max<size_t>(bytes * 2, 1 << 16);
-  const hipError_t e = hipHostMalloc(&h->pout, cap, hipHostMallocDefault);
+  hipError_t e = hipHostMalloc(&h->pout, cap, hipHostMallocCoherent | hipHostMallocMapped);
   if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (results)");
+  if ((e = hipHostGetDevicePointer(&h->pout_d, h->pout, 0)) != hipSuccess) return hip_fail(h, e, "hipHostGetDevicePointer");
   h->pout_cap = cap;
   return KSIM_OK;
 }
@@ -2434,7 +2455,9 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   if ((rc = pin_reserve(h, total)) || (rc = arena_reserve(h, arena, total))) return rc;
   for (auto& x : pc)
     if (x.bytes) std::memcpy((char*)h->pin + x.off, x.src, x.bytes);
-  HIPCHK(h, hipMemcpyAsync(arena.p, h->pin, total, hipMemcpyHostToDevice, h->stream));
+  Copies cp;
+  cp.add(h->pin_d, arena.p, total);
+  if ((rc = cp.run(h))) return rc;
   char* d = (char*)arena.p;
   P = DevPods{};
   P.pods = (const ksim_pod*)(d + pc[0].off);
@@ -2597,10 +2620,9 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   h->fw_list.clear();                // a new cycle: no normalization answered from the last one
   h->fw_raw.clear();
   if ((rc = upload_single(h, ps, pod_index, h->pod1))) return rc;
-  if ((rc = set_run(h, 0, 1))) return rc;
-  // the two topology flags are OR-ed by the PreFilter pass and reset by a bind,
-  // which a framework cycle does not run
-  HIPCHK(h, hipMemsetAsync(&h->st->topo_flags, 0, sizeof(uint32_t), h->stream));
+  // the run header, the window state and the two topology flags (OR-ed by the
+  // PreFilter pass and reset by a bind, which a framework cycle does not run)
+  launch_fw_begin(h->st, h->sc.win, 0, 1, h->stream);
   const ksim_pod& p = ps->pods[pod_index];
   launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, p.use_count > 0);
   HIPCHK(h, hipGetLastError());
@@ -2613,10 +2635,12 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   const size_t o_fail = 64, o_det = 64 + ((N + 63) & ~(size_t)63);
   if ((rc = pout_reserve(h, o_det + 4 * N))) return rc;
   char* po = (char*)h->pout;
-  HIPCHK(h, hipMemcpyAsync(po, &h->st->next_start, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipMemcpyAsync(po + o_fail, h->sc.fail, N, hipMemcpyDeviceToHost, h->stream));
-  if (out->fail_detail)
-    HIPCHK(h, hipMemcpyAsync(po + o_det, h->sc.detail, 4 * N, hipMemcpyDeviceToHost, h->stream));
+  char* pd = (char*)h->pout_d;
+  Copies cp;
+  cp.add(&h->st->next_start, pd, sizeof(int32_t));
+  cp.add(h->sc.fail, pd + o_fail, N);
+  if (out->fail_detail) cp.add(h->sc.detail, pd + o_det, 4 * N);
+  if ((rc = cp.run(h))) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   std::memcpy(h->fw_fail.data(), po + o_fail, N);
   if (out->fail_detail) std::memcpy(out->fail_detail, po + o_det, 4 * N);
@@ -2648,9 +2672,7 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
 static int fw_filter_pass(ksim_handle* h) {
   if (h->fw_topo && h->sc.dom)
     HIPCHK(h, hipMemsetAsync(h->sc.dom, 0, 8 * (size_t)KSIM_MAX_USES * h->dc.vmax, h->stream));
-  int rc;
-  if ((rc = set_run(h, 0, 1))) return rc;
-  HIPCHK(h, hipMemsetAsync(&h->st->topo_flags, 0, sizeof(uint32_t), h->stream));
+  launch_fw_begin(h->st, h->sc.win, 0, 1, h->stream);
   launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, h->fw_topo);
   HIPCHK(h, hipGetLastError());
   return KSIM_OK;
@@ -2730,51 +2752,49 @@ int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out
   // the window of the filter pass covers the whole scan set (k_window's
   // extender branch keeps it and drops the unlisted nodes)
   std::memcpy(h->pin, &h->fw_ns, sizeof(int32_t));
-  HIPCHK(h, hipMemcpyAsync(h->ext_fail, out_of_list, N, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(&h->sc.win->cut, h->pin, sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
-  if (n) HIPCHK(h, hipMemcpyAsync(h->fw_nodes, (char*)h->pin + o_list, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  {
+    Copies cp;
+    cp.add((char*)h->pin_d + 64, h->ext_fail, N);
+    cp.add(h->pin_d, &h->sc.win->cut, sizeof(int32_t));
+    cp.add((char*)h->pin_d + o_list, h->fw_nodes, 4 * (size_t)n);
+    if ((rc = cp.run(h))) return rc;
+  }
   LaunchArgs a = make_args(h, h->pod1, nullptr);
   a.s.ext_fail = h->ext_fail;
   a.s.ext_score = nullptr;
   launch_fw_score(a, h->stream);
   const int S = h->prof.n_score;
-  if (n) launch_fw_gather(h->eo, h->fw_nodes, n, (int32_t)N, S, h->fw_comp, h->stream);
+  // the listed nodes' answers and the window state gathered straight into
+  // the pinned staging, one synchronization; the caller's entries of
+  // unlisted nodes are left as they are (ksim_engine.h)
+  const size_t o_comp = (sizeof(WinState) + 63) & ~(size_t)63, nb = (16 * (size_t)S + 9) * n;
+  if ((rc = pout_reserve(h, o_comp + nb))) return rc;
+  char* po = (char*)h->pout;
+  launch_fw_gather(h->eo, h->fw_nodes, n, (int32_t)N, S, (int64_t*)((char*)h->pout_d + o_comp), h->sc.win,
+                   h->pout_d, h->stream);
   HIPCHK(h, hipGetLastError());
   h->fw_pending = false;
   h->fw_dom_dirty = false;                 // k_select re-zeroed the domain sums
   h->fw_scored = true;
-  // the listed nodes' answers into pinned staging, one synchronization; the
-  // unlisted nodes' answers are 0
-  const size_t o_comp = (sizeof(WinState) + 63) & ~(size_t)63, nb = (16 * (size_t)S + 9) * n;
-  if ((rc = pout_reserve(h, o_comp + nb))) return rc;
-  char* po = (char*)h->pout;
-  HIPCHK(h, hipMemcpyAsync(po, h->sc.win, sizeof(WinState), hipMemcpyDeviceToHost, h->stream));
-  if (n) HIPCHK(h, hipMemcpyAsync(po + o_comp, h->fw_comp, nb, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const int64_t* craw = (const int64_t*)(po + o_comp);
   const int64_t* cnorm = craw + (size_t)S * n;
   const int64_t* ctot = cnorm + (size_t)S * n;
   const uint8_t* csc = (const uint8_t*)(ctot + n);
-  if (out->scored) {
-    std::memset(out->scored, 0, N);
+  if (out->scored)
     for (int32_t j = 0; j < n; j++) out->scored[nodes[j]] = csc[j];
-  }
   for (int k = 0; k < S; k++) {
     if (out->raw) {
       int64_t* r = out->raw + (size_t)k * N;
-      std::memset(r, 0, 8 * N);
       for (int32_t j = 0; j < n; j++) r[nodes[j]] = craw[(size_t)k * n + j];
     }
     if (out->norm) {
       int64_t* r = out->norm + (size_t)k * N;
-      std::memset(r, 0, 8 * N);
       for (int32_t j = 0; j < n; j++) r[nodes[j]] = cnorm[(size_t)k * n + j];
     }
   }
-  if (out->total) {
-    std::memset(out->total, 0, 8 * N);
+  if (out->total)
     for (int32_t j = 0; j < n; j++) out->total[nodes[j]] = ctot[j];
-  }
   // kept for ksim_fw_normalize over the same list
   h->fw_list.assign(nodes, nodes + n);
   h->fw_raw.assign(craw, craw + (size_t)S * n);
@@ -2791,7 +2811,8 @@ int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out
   out->k_to_find = num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->fw_ns);
   out->chosen = w.error ? KSIM_CHOSEN_ERROR : -1;
   out->status = w.error ? KSIM_STATUS_ERROR : 0;
-  if (out->scored && w.nf <= 1) std::memset(out->scored, 0, N);
+  if (out->scored && w.nf <= 1)
+    for (int32_t j = 0; j < n; j++) out->scored[nodes[j]] = 0;
   return KSIM_OK;
 }
 
@@ -2824,11 +2845,19 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
   if ((rc = pin_reserve(h, o_vals + 8 * (size_t)n)) || (rc = pout_reserve(h, 8 * (size_t)n))) return rc;
   std::memcpy(h->pin, nodes, 4 * (size_t)n);
   std::memcpy((char*)h->pin + o_vals, scores, 8 * (size_t)n);
-  HIPCHK(h, hipMemcpyAsync(h->fw_nodes, h->pin, 4 * (size_t)n, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->fw_vals, (char*)h->pin + o_vals, 8 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+  {
+    Copies cp;
+    cp.add(h->pin_d, h->fw_nodes, 4 * (size_t)n);
+    cp.add((char*)h->pin_d + o_vals, h->fw_vals, 8 * (size_t)n);
+    if ((rc = cp.run(h))) return rc;
+  }
   launch_fw_normalize(make_args(h, h->pod1, nullptr), score_slot, h->fw_nodes, h->fw_vals, n, h->fw_out, h->stream);
   HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemcpyAsync(h->pout, h->fw_out, 8 * (size_t)n, hipMemcpyDeviceToHost, h->stream));
+  {
+    Copies cp;
+    cp.add(h->fw_out, h->pout_d, 8 * (size_t)n);
+    if ((rc = cp.run(h))) return rc;
+  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   std::memcpy(out, h->pout, 8 * (size_t)n);
   return KSIM_OK;
@@ -2845,7 +2874,8 @@ static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   if ((rc = upload_single(h, ps, pod_index, P))) return rc;
   launch_assume(h->dc, P, 0, node, sign, h->stream);
   HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  // no synchronization: every later call is ordered after it on the stream,
+  // and the next upload waits for the staging (upload_single)
   return KSIM_OK;
 }
 

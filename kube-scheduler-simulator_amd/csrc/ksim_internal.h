@@ -164,8 +164,16 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
 // 1 for unlisted nodes), no bind; NormalizeScore of one slot over an explicit list.
 void launch_fw_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
 void launch_fw_score(const LaunchArgs& a, hipStream_t stream);
+constexpr int kCopyPieces = 4;
+struct CopyList {
+  const uint8_t* src[kCopyPieces];
+  uint8_t* dst[kCopyPieces];
+  uint32_t n[kCopyPieces];
+};
+void launch_copy_list(const CopyList& l, int count, hipStream_t stream);
 void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,
-                      hipStream_t stream);
+                      const WinState* win, void* win_out, hipStream_t stream);
+void launch_fw_begin(DevState* st, WinState* win, int32_t first, int32_t end, hipStream_t stream);
 void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,
                          int64_t* out, hipStream_t stream);
 // DefaultPreemption dry run (ksim_preempt.hip): the bound pods per node in

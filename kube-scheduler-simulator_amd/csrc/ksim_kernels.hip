@@ -1512,11 +1512,39 @@ void launch_fw_score(const LaunchArgs& a, hipStream_t stream) {
   k_select<true><<<blocks, 256, 0, stream>>>(a.c, a.P, a.prof, a.st, a.s, a.o, 0, 0, nullptr);
 }
 
+// Small copies to or from the handle's coherent pinned staging (its device
+// address) as one kernel launch: the per-call uploads and result copies of
+// the framework-driven calls, where a DMA copy per piece costs more than the
+// bytes (up to kCopyPieces pieces; 16-byte accesses when a piece is at least
+// 16 bytes, its addresses then 16-byte aligned; byte accesses for the tail).
+__global__ __launch_bounds__(256) void k_copy_list(CopyList l) {
+  const int q = blockIdx.y;
+  const uint8_t* src = l.src[q];
+  uint8_t* dst = l.dst[q];
+  const uint32_t n = l.n[q], n16 = n >> 4;
+  for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < n16; x += gridDim.x * 256)
+    reinterpret_cast<uint4*>(dst)[x] = reinterpret_cast<const uint4*>(src)[x];
+  if (blockIdx.x == 0 && threadIdx.x < (n & 15u)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+}
+
+void launch_copy_list(const CopyList& l, int count, hipStream_t stream) {
+  uint32_t mx = 0;
+  for (int q = 0; q < count; q++) mx = l.n[q] > mx ? l.n[q] : mx;
+  const uint32_t blocks = ((mx >> 4) + 255) / 256;
+  k_copy_list<<<dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks, count), 256, 0, stream>>>(l);
+}
+
 // ksim_fw_score's answers for the listed nodes only: comp = [raw S x n][norm
 // S x n][total n] (list order), then the scored flags (n bytes); the host
 // copies n entries back instead of N (every unlisted node's answers are 0)
+// win_out (nullable): the cycle's WinState copied there too (block 0); comp
+// and win_out may be the pinned staging's device address.
 __global__ __launch_bounds__(256) void k_fw_gather(DevEvalOut o, const int32_t* __restrict__ nodes, int32_t n,
-                                                   int32_t N, int32_t S, int64_t* __restrict__ comp) {
+                                                   int32_t N, int32_t S, int64_t* __restrict__ comp,
+                                                   const WinState* __restrict__ win, uint32_t* __restrict__ win_out) {
+  if (win_out && blockIdx.x == 0)
+    for (int x = threadIdx.x; x < (int)(sizeof(WinState) / 4); x += blockDim.x)
+      win_out[x] = reinterpret_cast<const uint32_t*>(win)[x];
   const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const int32_t x = nodes[j];
@@ -1529,8 +1557,25 @@ __global__ __launch_bounds__(256) void k_fw_gather(DevEvalOut o, const int32_t* 
 }
 
 void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,
-                      hipStream_t stream) {
-  k_fw_gather<<<(n + 255) / 256, 256, 0, stream>>>(o, nodes, n, N, S, comp);
+                      const WinState* win, void* win_out, hipStream_t stream) {
+  k_fw_gather<<<n > 0 ? (n + 255) / 256 : 1, 256, 0, stream>>>(o, nodes, n, N, S, comp, win, (uint32_t*)win_out);
+}
+
+// A framework-driven filter pass's start: the run header, the topology flags
+// and the window state, in one launch (set_run's copy and two memsets).
+__global__ __launch_bounds__(256) void k_fw_begin(DevState* __restrict__ st, WinState* __restrict__ win,
+                                                  int32_t first, int32_t end) {
+  for (int x = threadIdx.x; x < (int)(sizeof(WinState) / 4); x += blockDim.x)
+    reinterpret_cast<uint32_t*>(win)[x] = 0;
+  if (threadIdx.x == 0) {
+    st->cursor = first;
+    st->end = end;
+    st->topo_flags = 0;
+  }
+}
+
+void launch_fw_begin(DevState* st, WinState* win, int32_t first, int32_t end, hipStream_t stream) {
+  k_fw_begin<<<1, 256, 0, stream>>>(st, win, first, end);
 }
 
 void launch_fw_normalize(const LaunchArgs& a, int32_t slot, const int32_t* nodes, const int64_t* vals, int32_t n,

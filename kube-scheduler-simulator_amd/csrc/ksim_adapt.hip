@@ -262,11 +262,12 @@ constexpr int32_t kWinSeqWords = 128;
 // F_j: start -> next start over the n starts (the (K+1)-th feasible node
 // from the start, the start itself when at most K are feasible).  k_win_build
 // tabulates every F_j (one block per pod: its ranks and the positions of its
-// feasible nodes in LDS).  Radix-4 rounds compose the prefixes,
-// Q_j = F_j o ... o F_max(0, j-4^r+1) after round r; three over whole tables
-// (strides 1, 4, 16), the fourth (stride 64) only at s_0 inside k_win_final,
-// where pod j starts at Q_{j-1}(s_0).  Five launches of independent table
-// lookups in place of the walk's 256 dependent steps on one wave.
+// feasible nodes in LDS).  One radix-16 round over whole tables composes
+// Q_j = F_j o ... o F_max(0, j-15); k_win_final composes the 16-pod prefixes
+// at s_0 alone (stride 16), so pod j starts at (F_{j-1} o ... o F_0)(s_0).
+// Three launches of independent table lookups in place of the walk's 256
+// dependent steps on one wave (radix 4 over four rounds, 31.4 us per batch,
+// and radix 8, 30.3 us, measured against radix 16's 30.1: profiles/r04/radix).
 __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
                                                    int32_t k, uint16_t* __restrict__ tab0, int32_t* __restrict__ wtot) {
@@ -313,18 +314,21 @@ __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ 
 
 // Round with stride d: Q'_j = Q_j o Q_{j-d} o Q_{j-2d} o Q_{j-3d} (terms with
 // a negative index left out).
+template <int R>
 __global__ __launch_bounds__(256) void k_win_round(const DevState* __restrict__ st, int32_t n, int32_t d,
                                                    const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
   const int32_t j = blockIdx.y;
   const int32_t x = blockIdx.x * 256 + threadIdx.x;
   if (j >= min(kBatchPods, st->end - st->cursor) || x >= n) return;
   int32_t v = x;
-  if (j - 3 * d >= 0) v = src[(size_t)(j - 3 * d) * n + v];
-  if (j - 2 * d >= 0) v = src[(size_t)(j - 2 * d) * n + v];
-  if (j - d >= 0) v = src[(size_t)(j - d) * n + v];
+#pragma unroll
+  for (int t = R - 1; t >= 1; t--)
+    if (j - t * d >= 0) v = src[(size_t)(j - t * d) * n + v];
   dst[(size_t)j * n + x] = src[(size_t)j * n + v];
 }
 
+// D: the span of the prefixes in q (the last round, stride D, at s_0 alone).
+template <int D>
 __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __restrict__ st,
                                                           const uint16_t* __restrict__ tab0,
                                                           const uint16_t* __restrict__ q,
@@ -334,14 +338,11 @@ __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __rest
   const int32_t nb = min(kBatchPods, st->end - st->cursor);
   if (nb <= 0) return;
   if (j < nb) {
-    // the last radix-4 round (stride 64) at s_0 alone: Q_{j-1} composed from
-    // the 64-pod prefixes in q
     const int32_t s0 = st->next_start, i = j - 1;
     int32_t s = s0;
-    if (i - 192 >= 0) s = q[(size_t)(i - 192) * n + s];
-    if (i - 128 >= 0) s = q[(size_t)(i - 128) * n + s];
-    if (i - 64 >= 0) s = q[(size_t)(i - 64) * n + s];
-    if (i >= 0) s = q[(size_t)i * n + s];
+#pragma unroll
+    for (int t = kBatchPods / D - 1; t >= 0; t--)
+      if (i - t * D >= 0) s = q[(size_t)(i - t * D) * n + s];
     const int32_t nx = tab0[(size_t)j * n + s];
     awin[2 * j] = s;
     awin[2 * j + 1] = wtot[j] <= k ? -1 : (nx > s ? nx - s : nx + n - s);
@@ -353,14 +354,11 @@ static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, h
   const int32_t n = a.c.n;
   uint16_t* t0 = a.s.wtab;
   uint16_t* t1 = t0 + (size_t)kBatchPods * n;
-  uint16_t* t2 = t1 + (size_t)kBatchPods * n;
   k_win_build<<<kBatchPods, 256, 0, stream>>>(a.st, a.s.amask, n_words, n, k, t0, a.s.wtot);
   const dim3 grid((n + 255) / 256, kBatchPods);
-  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 1, t0, t1);
-  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 4, t1, t2);
-  k_win_round<<<grid, 256, 0, stream>>>(a.st, n, 16, t2, t1);
-  static_assert(kBatchPods <= 256, "four radix-4 rounds cover 256 pods");
-  k_win_final<<<1, kBatchPods, 0, stream>>>(a.st, t0, t1, a.s.wtot, n, k, a.s.awin, a.s.aexact);
+  static_assert(kBatchPods == 256, "a radix-16 round and the stride-16 final cover 256 pods");
+  k_win_round<16><<<grid, 256, 0, stream>>>(a.st, n, 1, t0, t1);
+  k_win_final<16><<<1, kBatchPods, 0, stream>>>(a.st, t0, t1, a.s.wtot, n, k, a.s.awin, a.s.aexact);
 }
 
 // Clusters up to this many bitmap words run the window scan inside k_adapt_top

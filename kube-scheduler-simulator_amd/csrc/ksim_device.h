@@ -244,7 +244,7 @@ struct DevScratch {
   uint64_t* amask;       // ADAPT batch: S0 feasibility bitmaps [kBatchPods][ceil(n / 64)]
   int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
   int32_t* aexact;       // ADAPT batch: pods whose windows are exact
-  uint16_t* wtab;        // ADAPT windows by doubling (n <= 8192): [3][kBatchPods][n] start -> next-start tables
+  uint16_t* wtab;        // ADAPT windows by doubling (n <= 8192): [2][kBatchPods][n] start -> next-start tables
   int32_t* wtot;         // ADAPT windows by doubling: [kBatchPods] feasible nodes per pod
   int32_t* abroken;      // ADAPT batch: a bound node flipped feasibility inside the pod's window
   const uint8_t* ext_fail;   // extender pass only (else null): nodes an extender filtered out

@@ -20,6 +20,7 @@ for c in ${CONFIGS:-c1 c1a c3 c4a c5}; do
     c1) args="--config 1" ;;
     c1a) args="--config 1 --mode adapt" ;;
     c2) args="" ;;
+    c2a) args="--mode adapt" ;;
     c3) args="--config 3" ;;
     c4a) args="--config 4 --mode adapt --pods4 100000" ;;
     c5) args="--config 5 --sweep 16" ;;

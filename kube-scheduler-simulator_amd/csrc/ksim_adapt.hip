@@ -262,12 +262,14 @@ constexpr int32_t kWinSeqWords = 128;
 // F_j: start -> next start over the n starts (the (K+1)-th feasible node
 // from the start, the start itself when at most K are feasible).  k_win_build
 // tabulates every F_j (one block per pod: its ranks and the positions of its
-// feasible nodes in LDS).  One radix-16 round over whole tables composes
-// Q_j = F_j o ... o F_max(0, j-15); k_win_final composes the 16-pod prefixes
-// at s_0 alone (stride 16), so pod j starts at (F_{j-1} o ... o F_0)(s_0).
-// Three launches of independent table lookups in place of the walk's 256
-// dependent steps on one wave (radix 4 over four rounds, 31.4 us per batch,
-// and radix 8, 30.3 us, measured against radix 16's 30.1: profiles/r04/radix).
+// feasible nodes in LDS).  Two radix-8 rounds compose the prefixes
+// (Q_j = F_j o ... o F_max(0, j-7), then strides of 8), each block staging
+// the 8 source rows its pod reads in LDS; k_win_final composes the 64-pod
+// prefixes at s_0 alone (stride 64), so pod j starts at
+// (F_{j-1} o ... o F_0)(s_0).  Four launches of table lookups in place of the
+// walk's 256 dependent steps on one wave (profiles/r04/winlds: 23.9 us per
+// batch; radix 16 over global gathers 30.1 us, radix 4 31.4 us, radix 8
+// 30.3 us in profiles/r04/radix).
 __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
                                                    int32_t k, uint16_t* __restrict__ tab0, int32_t* __restrict__ wtot) {
@@ -314,19 +316,6 @@ __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ 
 
 // Round with stride d: Q'_j = Q_j o Q_{j-d} o Q_{j-2d} o Q_{j-3d} (terms with
 // a negative index left out).
-template <int R>
-__global__ __launch_bounds__(256) void k_win_round(const DevState* __restrict__ st, int32_t n, int32_t d,
-                                                   const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
-  const int32_t j = blockIdx.y;
-  const int32_t x = blockIdx.x * 256 + threadIdx.x;
-  if (j >= min(kBatchPods, st->end - st->cursor) || x >= n) return;
-  int32_t v = x;
-#pragma unroll
-  for (int t = R - 1; t >= 1; t--)
-    if (j - t * d >= 0) v = src[(size_t)(j - t * d) * n + v];
-  dst[(size_t)j * n + x] = src[(size_t)j * n + v];
-}
-
 // D: the span of the prefixes in q (the last round, stride D, at s_0 alone).
 template <int D>
 __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __restrict__ st,
@@ -350,15 +339,49 @@ __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __rest
   if (j == 0) *aexact = nb;
 }
 
+// A radix-R round with the R source rows a pod reads staged in LDS (one block
+// per pod, rows of at most kWinSeqWords * 64 entries): R - 1 dependent LDS
+// lookups per start instead of global gathers.
+template <int R>
+__global__ __launch_bounds__(1024) void k_win_round_lds(const DevState* __restrict__ st, int32_t n, int32_t d,
+                                                        const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
+  __shared__ uint16_t s_rows[R][kWinSeqWords * 64];
+  const int32_t j = blockIdx.x;
+  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // block-uniform
+  const int32_t words = (n + 7) >> 3;                  // 16-byte pieces per row (the row starts 16-byte aligned)
+#pragma unroll
+  for (int t = 0; t < R; t++) {
+    const int32_t row = j - t * d;
+    if (row < 0) continue;                              // block-uniform
+    const uint16_t* in = src + (size_t)row * n;
+    if ((n & 7) == 0) {
+      for (int32_t x = threadIdx.x; x < words; x += 1024)
+        reinterpret_cast<uint4*>(s_rows[t])[x] = reinterpret_cast<const uint4*>(in)[x];
+    } else {
+      for (int32_t x = threadIdx.x; x < n; x += 1024) s_rows[t][x] = in[x];
+    }
+  }
+  __syncthreads();
+  uint16_t* out = dst + (size_t)j * n;
+  for (int32_t x = threadIdx.x; x < n; x += 1024) {
+    int32_t v = x;
+#pragma unroll
+    for (int t = R - 1; t >= 1; t--)
+      if (j - t * d >= 0) v = s_rows[t][v];
+    out[x] = s_rows[0][v];
+  }
+}
+
 static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, hipStream_t stream) {
   const int32_t n = a.c.n;
   uint16_t* t0 = a.s.wtab;
   uint16_t* t1 = t0 + (size_t)kBatchPods * n;
   k_win_build<<<kBatchPods, 256, 0, stream>>>(a.st, a.s.amask, n_words, n, k, t0, a.s.wtot);
-  const dim3 grid((n + 255) / 256, kBatchPods);
-  static_assert(kBatchPods == 256, "a radix-16 round and the stride-16 final cover 256 pods");
-  k_win_round<16><<<grid, 256, 0, stream>>>(a.st, n, 1, t0, t1);
-  k_win_final<16><<<1, kBatchPods, 0, stream>>>(a.st, t0, t1, a.s.wtot, n, k, a.s.awin, a.s.aexact);
+  static_assert(kBatchPods == 256, "two radix-8 rounds and the stride-64 final cover 256 pods");
+  uint16_t* t2 = t1 + (size_t)kBatchPods * n;
+  k_win_round_lds<8><<<kBatchPods, 1024, 0, stream>>>(a.st, n, 1, t0, t1);
+  k_win_round_lds<8><<<kBatchPods, 1024, 0, stream>>>(a.st, n, 8, t1, t2);
+  k_win_final<64><<<1, kBatchPods, 0, stream>>>(a.st, t0, t2, a.s.wtot, n, k, a.s.awin, a.s.aexact);
 }
 
 // Clusters up to this many bitmap words run the window scan inside k_adapt_top

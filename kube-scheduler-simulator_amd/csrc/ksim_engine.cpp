@@ -2049,7 +2049,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.aexact, int32_t*, 4);
   {                                      // the doubling window's tables (clusters of <= 128 bitmap words)
     const size_t NW = (N + 63) / 64 <= 128 ? N : 0;
-    SCR(s.wtab, uint16_t*, 2 * 2 * (size_t)kBatchPods * std::max<size_t>(NW, 1));
+    SCR(s.wtab, uint16_t*, 2 * 3 * (size_t)kBatchPods * std::max<size_t>(NW, 1));
     SCR(s.wtot, int32_t*, 4 * (size_t)kBatchPods);
   }
   SCR(s.abroken, int32_t*, 4 * (size_t)kBatchPods);

@@ -267,10 +267,11 @@ constexpr int32_t kWinSeqWords = 128;
 // the 8 source rows its pod reads in LDS; k_win_final composes the 64-pod
 // prefixes at s_0 alone (stride 64), so pod j starts at
 // (F_{j-1} o ... o F_0)(s_0).  Four launches of table lookups in place of the
-// walk's 256 dependent steps on one wave (profiles/r04/winlds: 23.9 us per
+// walk's 256 dependent steps on one wave (profiles/r04/winb: 21.0 us per
 // batch; radix 16 over global gathers 30.1 us, radix 4 31.4 us, radix 8
 // 30.3 us in profiles/r04/radix).
-__global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ st,
+constexpr int kWinBuildThreads = 1024;
+__global__ __launch_bounds__(kWinBuildThreads) void k_win_build(const DevState* __restrict__ st,
                                                    const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
                                                    int32_t k, uint16_t* __restrict__ tab0, int32_t* __restrict__ wtot) {
   __shared__ uint64_t s_w[kWinSeqWords];
@@ -298,14 +299,14 @@ __global__ __launch_bounds__(256) void k_win_build(const DevState* __restrict__ 
   if (tid >= 64 && tid < kWinSeqWords) s_pc[tid] += s_tot0;
   __syncthreads();
   const int32_t total = s_pc[n_words - 1] + (int32_t)__popcll(s_w[n_words - 1]);
-  for (int32_t x = tid; x < n; x += 256) {         // the positions of the feasible nodes by rank
+  for (int32_t x = tid; x < n; x += kWinBuildThreads) {         // the positions of the feasible nodes by rank
     const uint64_t w = s_w[x >> 6];
     const int b = x & 63;
     if ((w >> b) & 1ull) s_sel[s_pc[x >> 6] + (int32_t)__popcll(w & ((1ull << b) - 1ull))] = (uint16_t)x;
   }
   __syncthreads();
   uint16_t* out = tab0 + (size_t)j * n;
-  for (int32_t x = tid; x < n; x += 256) {
+  for (int32_t x = tid; x < n; x += kWinBuildThreads) {
     const uint64_t w = s_w[x >> 6];
     int32_t t = s_pc[x >> 6] + (int32_t)__popcll(w & ((1ull << (x & 63)) - 1ull)) + k;   // the cut's rank
     if (t >= total) t -= total;
@@ -376,7 +377,7 @@ static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, h
   const int32_t n = a.c.n;
   uint16_t* t0 = a.s.wtab;
   uint16_t* t1 = t0 + (size_t)kBatchPods * n;
-  k_win_build<<<kBatchPods, 256, 0, stream>>>(a.st, a.s.amask, n_words, n, k, t0, a.s.wtot);
+  k_win_build<<<kBatchPods, kWinBuildThreads, 0, stream>>>(a.st, a.s.amask, n_words, n, k, t0, a.s.wtot);
   static_assert(kBatchPods == 256, "two radix-8 rounds and the stride-64 final cover 256 pods");
   uint16_t* t2 = t1 + (size_t)kBatchPods * n;
   k_win_round_lds<8><<<kBatchPods, 1024, 0, stream>>>(a.st, n, 1, t0, t1);

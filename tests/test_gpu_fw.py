@@ -158,6 +158,40 @@ def test_fw_api_lists_and_normalize():
         np.testing.assert_array_equal(es[k], os_[k])
 
 
+def test_fw_staging_grows_with_the_cluster():
+    """The pinned staging of the framework-driven calls grows past its first
+    allocation (20,000 nodes: the score call's list mask alone exceeds it):
+    the results' staging must survive the upload staging's reallocation, and
+    every answer still equals the oracle's."""
+    cluster, pods = gen.config2(n_nodes=20000, n_pods=40, seed=3)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    ora = Oracle(cluster, prof)
+    rng = np.random.default_rng(11)
+    for i in range(pods.n_pods):
+        fe, fo = eng.fw_prefilter(pods, i), ora.fw_prefilter(pods, i)
+        np.testing.assert_array_equal(fe["fail_plugin"], fo["fail_plugin"])
+        feas = np.nonzero(fe["fail_plugin"] == abi.PASSED)[0]
+        lst = rng.permutation(feas)[:int(rng.integers(2, feas.size + 1))] if feas.size > 1 else feas
+        if lst.size < 2:
+            continue
+        se, so = eng.fw_score(lst), ora.fw_score(lst)
+        for k in ("raw", "norm", "total", "scored"):
+            np.testing.assert_array_equal(se[k], so[k], err_msg=f"pod {i} {k}")
+        for slot in range(prof.n_score):
+            vals = rng.integers(-5, 300, lst.size)
+            np.testing.assert_array_equal(eng.fw_normalize(slot, lst, vals), ora.fw_normalize(slot, lst, vals))
+        node = int(lst[0])
+        eng.assume(pods, i, node)
+        ora.assume(pods, i, node)
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k])
+
+
 def test_fw_rejects_bad_lists_and_abandons_cleanly():
     """A list with an infeasible or repeated node is refused; a framework
     cycle left without PreScore (one feasible node) does not leak its

@@ -179,6 +179,20 @@ __device__ int32_t find_cut(const uint64_t* __restrict__ mask, int32_t s, int32_
 }
 
 constexpr int kWindowRounds = 48;
+__device__ __forceinline__ int select_bit(uint64_t v, int32_t need) {   // position of set bit #need (0-based)
+  int pos = 0;
+#pragma unroll
+  for (int wd = 32; wd >= 1; wd >>= 1) {
+    const int32_t c = __popcll(v & ((1ull << wd) - 1));
+    if (need >= c) {
+      need -= c;
+      v >>= wd;
+      pos += wd;
+    }
+  }
+  return pos;
+}
+
 constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod from this window length
 
 // The windows of one batch in one block of kBatchPods threads (thread j = pod
@@ -187,7 +201,8 @@ constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod fr
 // (block-uniform).  A pure function of the bitmaps and the state.
 __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
                                              int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
-                                             int32_t* cut_out, int32_t* exact_out) {
+                                             int32_t* cut_out, int32_t* exact_out,
+                                             const int32_t* __restrict__ cut0 = nullptr) {
   __shared__ int64_t sh[kBatchPods / 64];
   __shared__ int32_t s_first;
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
@@ -198,7 +213,8 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
   int32_t cut = -1, exact = 0;
   for (int round = 0; round < kWindowRounds; round++) {
-    cut = j < nb ? find_cut(amask + (size_t)j * n_words, s, n, k) : -1;
+    // cut0: the first round's cuts, from k_adapt_cut0 (a wave per pod)
+    cut = j < nb ? (round == 0 && cut0 ? cut0[2 * j + 1] : find_cut(amask + (size_t)j * n_words, s, n, k)) : -1;
     const int64_t proc = j < nb ? (cut >= 0 ? cut : n) : 0;
     // exclusive prefix sum of the processed counts
     int64_t x = proc;
@@ -233,14 +249,78 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   return true;
 }
 
+// The relaxation's first round over the whole chip: pod j's cut from its
+// first guess s_j = s_0 + j K (mod N), one wave per pod, 128 bitmap words per
+// step (each lane two, popcounts, a wave scan, the bit by halving), into
+// awin[2j + 1].  window_block's walk is one thread per pod from one block,
+// ~80 dependent words per pod at K = 5,000 (13.8 us per batch, config 4,
+// where the first round is the fixpoint in every batch: profiles/r04/windbg);
+// this launch takes the walk off the single block.
+__global__ __launch_bounds__(256) void k_adapt_cut0(const DevState* __restrict__ st,
+                                                    const uint64_t* __restrict__ amask, int32_t n_words, int32_t n,
+                                                    int32_t k, int32_t* __restrict__ awin) {
+  const int lane = threadIdx.x & 63;
+  const int32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // wave-uniform
+  const int32_t s = (int32_t)(((int64_t)st->next_start + (int64_t)j * k) % n);
+  const uint64_t* m = amask + (size_t)j * n_words;
+  const int32_t ws = s >> 6;
+  const uint64_t below = (1ull << (s & 63)) - 1;
+  int32_t need = k, cut = -1;
+  // virtual word v = 0 .. n_words: word (ws + v) mod n_words; v = 0 keeps the
+  // bits from s on, v = n_words (ws again) the bits below s
+  for (int32_t v0 = 0; v0 <= n_words; v0 += 128) {
+    uint64_t b[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int32_t v = v0 + 2 * lane + h;
+      int32_t w = ws + v;
+      if (w >= n_words) w -= n_words;
+      b[h] = v <= n_words ? m[w] : 0ull;
+      if (v == 0) b[h] &= ~below;
+      if (v == n_words) b[h] &= below;
+    }
+    const int32_t c0 = __popcll(b[0]), c = c0 + __popcll(b[1]);
+    int32_t x = c;                                   // inclusive scan over the lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    const uint64_t hit = __ballot(x > need);
+    if (hit) {
+      const int L = __builtin_ctzll(hit);
+      if (lane == L) {
+        int32_t r = need - (x - c);                  // set bit #r of the lane's two words
+        const int h = r < c0 ? 0 : 1;
+        if (h) r -= c0;
+        const int32_t v = v0 + 2 * lane + h;
+        int32_t w = ws + v;
+        if (w >= n_words) w -= n_words;
+        const int32_t node = w * 64 + select_bit(b[h], r);
+        cut = node >= s ? node - s : node + n - s;
+      }
+      cut = __shfl(cut, L, 64);
+      break;
+    }
+    need -= __shfl(x, 63, 64);
+  }
+  if (lane == 0) {
+    awin[2 * j] = s;
+    awin[2 * j + 1] = cut;
+  }
+}
+
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
+// CUT0: the first round's cuts are in awin (k_adapt_cut0).
+template <bool CUT0>
 __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ amask, int32_t n_words,
                                                              int32_t n, int32_t k, int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ aexact) {
   int32_t s, cut, exact;
-  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact)) return;
+  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, CUT0 ? awin : nullptr)) return;
   const int j = threadIdx.x;
   if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
@@ -953,7 +1033,7 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   if (win_seq)
     launch_window_dbl(a, n_words, k, stream);
   else if (!win_fused)
-    k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+    k_adapt_window<false><<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
@@ -1004,7 +1084,10 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   launch_adapt_mask_commit(z, false, stream);
   if (evs) (void)hipEventRecord(evs[1], stream);
   const bool win_fused = k < kTopWideK && n_words <= kWinFusedWords;
-  if (!win_fused) k_adapt_window<<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
+  if (!win_fused) {
+    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin);
+    k_adapt_window<true><<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
+  }
   if (evs) (void)hipEventRecord(evs[2], stream);
   // every later launch reads X[p] (z.cw) and st[p]
 #define TOP(NT, W) k_adapt_top<false, true, NT, W><<<kBatchPods, NT, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, \
@@ -1055,7 +1138,7 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
   const int32_t N = a.c.n_total, nw = (N + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
   k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
-  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
+  k_adapt_window<false><<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
 #define TOP(F, NT) k_adapt_top<true, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, \
     nw, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend)
   if (k >= kTopWideK) {

@@ -53,7 +53,7 @@ def test_config1_batch(pct):
     eng.set_cluster(cluster)
     chosen, st = eng.schedule_batch(pods)
     ora = Oracle(cluster, prof)
-    ochosen, ost = ora.schedule(pods)
+    ochosen, ost = ora.schedule(pods) if nthreads is None else ora.schedule(pods, nthreads=nthreads)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.scheduled == ost.scheduled
     assert eng.next_start == ora.next_start
@@ -77,7 +77,7 @@ def test_config2_slice_batch(pct):
         np.testing.assert_array_equal(es[k], os_[k])
 
 
-def _batch_vs_oracle(cluster, pods, pct=100, seed=0x4B53494D):
+def _batch_vs_oracle(cluster, pods, pct=100, seed=0x4B53494D, nthreads=None):
     prof = _prof(pct, seed)
     eng = Engine(0)
     eng.set_profile(prof)
@@ -110,6 +110,21 @@ def test_adapt_batch_config2_and_pct():
     _batch_vs_oracle(cluster, pods, pct=0)
     cluster, pods = gen.config2(n_nodes=3000, n_pods=4000, seed=77)
     _batch_vs_oracle(cluster, pods, pct=30)
+
+
+@pytest.mark.parametrize("pct,n_pods", [(0, 45000), (30, 20000)])
+def test_adapt_batch_group_counts(pct, n_pods):
+    """Lazy ADAPT windows by group counts (k_adapt_window_gc: more than 256
+    bitmap words, 1024-node groups ragged at the end): 17,000 nodes, pods at
+    16x config 2's requests fill them, so the feasibility bitmaps turn sparse,
+    the windows wrap and ~2,000 pods find no node; K = 850 (pct 0) and
+    K = 5,100 (pct 30, the wide top)."""
+    cluster, _ = gen.config2(n_nodes=17000, n_pods=1)
+    pods = gen.bare_pods(n_pods, seed=41)
+    for col in ("req_cpu", "req_mem", "nz_cpu", "nz_mem"):
+        pods.pods[col] *= 16
+    st = _batch_vs_oracle(cluster, pods, pct=pct, nthreads=16)
+    assert st.perpod_cycles == 0 and st.batches > 0
 
 
 def test_adapt_batch_mixed_runs():

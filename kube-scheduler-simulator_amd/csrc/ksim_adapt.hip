@@ -15,8 +15,9 @@
 //                   every pod find its cut (the K-th feasible node from s_i) in
 //                   its bitmap, re-derive the starts as the prefix sum of the
 //                   processed counts, repeat.  Pod 0's start is exact and each
-//                   round extends the exact prefix; a fixpoint is exact.
-//   k_adapt_top     one block per pod: TB keys of the kept nodes (the first K
+//                   round extends the exact prefix; a fixpoint is exact.  The
+//                   first round's cuts come from k_adapt_cut0 (a wave per pod).
+//   k_adapt_top    one block per pod: TB keys of the kept nodes (the first K
 //                   feasible of its window), the pod's exact top-T.
 //   k_adapt_pairs   every block runs the greedy chain of ksim_batch.hip on those
 //                   lists; then block j, thread k < j: pod j on pod k's guessed node once pod
@@ -313,14 +314,13 @@ __global__ __launch_bounds__(256) void k_adapt_cut0(const DevState* __restrict__
 
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
-// CUT0: the first round's cuts are in awin (k_adapt_cut0).
-template <bool CUT0>
+// The first round's cuts are in awin (k_adapt_cut0).
 __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ amask, int32_t n_words,
                                                              int32_t n, int32_t k, int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ aexact) {
   int32_t s, cut, exact;
-  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, CUT0 ? awin : nullptr)) return;
+  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, awin)) return;
   const int j = threadIdx.x;
   if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
@@ -1032,8 +1032,10 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   const bool win_fused = !win_seq && k < kTopWideK && n_words <= kWinFusedWords;
   if (win_seq)
     launch_window_dbl(a, n_words, k, stream);
-  else if (!win_fused)
-    k_adapt_window<false><<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  else if (!win_fused) {
+    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin);
+    k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+  }
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
     a.s.amask, n_words, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, a.s.pnorm)
@@ -1086,7 +1088,7 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   const bool win_fused = k < kTopWideK && n_words <= kWinFusedWords;
   if (!win_fused) {
     k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin);
-    k_adapt_window<true><<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
+    k_adapt_window<<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
   }
   if (evs) (void)hipEventRecord(evs[2], stream);
   // every later launch reads X[p] (z.cw) and st[p]
@@ -1138,7 +1140,8 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
   const int32_t N = a.c.n_total, nw = (N + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
   k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
-  k_adapt_window<false><<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
+  k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin);
+  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
 #define TOP(F, NT) k_adapt_top<true, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, \
     nw, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend)
   if (k >= kTopWideK) {

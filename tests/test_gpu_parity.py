@@ -53,7 +53,7 @@ def test_config1_batch(pct):
     eng.set_cluster(cluster)
     chosen, st = eng.schedule_batch(pods)
     ora = Oracle(cluster, prof)
-    ochosen, ost = ora.schedule(pods) if nthreads is None else ora.schedule(pods, nthreads=nthreads)
+    ochosen, ost = ora.schedule(pods)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.scheduled == ost.scheduled
     assert eng.next_start == ora.next_start
@@ -84,7 +84,7 @@ def _batch_vs_oracle(cluster, pods, pct=100, seed=0x4B53494D, nthreads=None):
     eng.set_cluster(cluster)
     chosen, st = eng.schedule_batch(pods)
     ora = Oracle(cluster, prof)
-    ochosen, ost = ora.schedule(pods)
+    ochosen, ost = ora.schedule(pods) if nthreads is None else ora.schedule(pods, nthreads=nthreads)
     np.testing.assert_array_equal(chosen, ochosen)
     assert st.evals == ost.evals and st.scheduled == ost.scheduled
     assert eng.next_start == ora.next_start

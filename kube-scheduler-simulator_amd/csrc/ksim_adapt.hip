@@ -978,40 +978,37 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
   const int32_t w = blockIdx.x * 4 + (tid >> 6);
   if (w >= n_words) return;                          // wave-uniform
   const int32_t j1 = min(j0 + mp, nb);
-  int64_t qc = 0, qm = 0, qe = 0;
-  uint32_t qf = 0;
-  if (lane < j1 - j0) {
-    const ksim_pod& q = P.pods[base + j0 + lane];
-    qc = q.req_cpu;
-    qm = q.req_mem;
-    qe = q.req_eph;
-    qf = q.flags;
-  }
   const BatchProg& bp = *bp_p;
   const bool fit = bp.has_fit_filter != 0;
-  bool room = true;
-  int64_t fc = 0, fm = 0, fe = 0;
-  if (fit) {
-    room = np + 1 <= c.alloc_pods[x];
-    fc = c.alloc_cpu[x] - rc;
-    fm = c.alloc_mem[x] - rm;
-    fe = c.alloc_eph[x] - re;
-  }
   uint64_t word = 0;                               // lane l: pod j0 + l's ballot
-#pragma unroll 1
-  for (int32_t j = j0; j < j1; j++) {
-    const int l = j - j0;
-    const int64_t c0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qc >> 32), l) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)qc, l));
-    const int64_t m0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qm >> 32), l) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)qm, l));
-    const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qe >> 32), l) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)qe, l));
-    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)qf, l);
-    const bool none = c0 == 0 && m0 == 0 && e0 == 0 && !(f0 & KSIM_POD_HAS_SCALAR);
-    const bool ok = !fit || (room && (none || (c0 <= fc && m0 <= fm && e0 <= fe)));
-    const uint64_t mk = __ballot(on && ok);
-    word = lane == l ? mk : word;
+  if (!fit) {                                      // every pod: the nodes that exist
+    const uint64_t mk = __ballot(on);
+    word = lane < j1 - j0 ? mk : 0ull;
+  } else {
+    // lane l's pod requests staged in the wave's own LDS rows (a wave reads
+    // its own writes in order: no barrier), read back at a uniform address,
+    // so each pod costs three 64-bit compares and one LDS row of ballots; a pod
+    // with no requests (and no scalar ones) compares as INT64_MIN: it fits
+    // wherever a pod slot is free
+    __shared__ int64_t s_pq[4][64][4];
+    const int wv = tid >> 6;
+    if (lane < j1 - j0) {
+      const ksim_pod& q = P.pods[base + j0 + lane];
+      const bool none = q.req_cpu == 0 && q.req_mem == 0 && q.req_eph == 0 && !(q.flags & KSIM_POD_HAS_SCALAR);
+      s_pq[wv][lane][0] = none ? INT64_MIN : q.req_cpu;
+      s_pq[wv][lane][1] = none ? INT64_MIN : q.req_mem;
+      s_pq[wv][lane][2] = none ? INT64_MIN : q.req_eph;
+    }
+    const uint64_t room = __ballot(on && np + 1 <= c.alloc_pods[x]);
+    const int64_t fc = c.alloc_cpu[x] - rc, fm = c.alloc_mem[x] - rm, fe = c.alloc_eph[x] - re;
+    __shared__ uint64_t s_mk[4][64];
+#pragma unroll 4
+    for (int32_t l = 0; l < j1 - j0; l++) {
+      const int64_t c0 = s_pq[wv][l][0], m0 = s_pq[wv][l][1], e0 = s_pq[wv][l][2];
+      const uint64_t mk = room & __ballot(c0 <= fc) & __ballot(m0 <= fm) & __ballot(e0 <= fe);
+      if (lane == 0) s_mk[wv][l] = mk;
+    }
+    word = lane < j1 - j0 ? s_mk[wv][lane] : 0ull;
   }
   if (lane < j1 - j0) amask[(size_t)(j0 + lane) * n_words + w] = word;
 }

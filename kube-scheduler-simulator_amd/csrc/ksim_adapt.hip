@@ -76,48 +76,41 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
   const bool on = node < c.n;
   const int32_t x = on ? node : 0;
   const int32_t j1 = min(j0 + mp, nb);
-  // The group's request fields, one pod per lane (mp <= 64), read back per pod
-  // by readlane: no scalar memory round trip inside the pod loop.  Trivial
-  // pods only (every static filter host-proven to pass; batchable pods
-  // request no scalar resources).
-  int64_t qc = 0, qm = 0, qe = 0;
-  uint32_t qf = 0;
+  // The group's request fields, one pod per lane (mp <= 64), staged in the
+  // wave's own LDS rows and read back per pod at a uniform address (as in
+  // k_adapt_mask_commit).  Trivial pods only (every static filter host-proven
+  // to pass; batchable pods request no scalar resources).
+  __shared__ int64_t s_pq[4][64][4];
+  __shared__ uint64_t s_mk[4][64];
+  const int wv = threadIdx.x >> 6;
   bool nontriv = false;
   if (lane < j1 - j0) {
     const ksim_pod& q = P.pods[base + j0 + lane];
-    qc = q.req_cpu;
-    qm = q.req_mem;
-    qe = q.req_eph;
-    qf = q.flags;
+    // fits_request: a pod requesting nothing (and no scalar resources) needs
+    // only a pod slot: its requests compare as INT64_MIN
+    const bool none = q.req_cpu == 0 && q.req_mem == 0 && q.req_eph == 0 && !(q.flags & KSIM_POD_HAS_SCALAR);
+    s_pq[wv][lane][0] = none ? INT64_MIN : q.req_cpu;
+    s_pq[wv][lane][1] = none ? INT64_MIN : q.req_mem;
+    s_pq[wv][lane][2] = none ? INT64_MIN : q.req_eph;
     nontriv = !(P.bflags[base + j0 + lane] & kBatchStaticTrivial);
   }
   if (__ballot(nontriv) == 0) {                    // wave-uniform
     // only the Fit filter's columns (the table is re-read once per pod group)
-    const bool fit = bp.has_fit_filter != 0;
-    bool room = true;
-    int64_t fc = 0, fm = 0, fe = 0;
-    if (fit) {
-      room = c.num_pods[x] + 1 <= c.alloc_pods[x];
-      fc = c.alloc_cpu[x] - c.req_cpu[x];
-      fm = c.alloc_mem[x] - c.req_mem[x];
-      fe = c.alloc_eph[x] - c.req_eph[x];
-    }
-    uint64_t word = 0;                             // lane l: pod j0 + l's ballot
-#pragma unroll 1
-    for (int32_t j = j0; j < j1; j++) {
-      const int l = j - j0;
-      const int64_t c0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qc >> 32), l) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)qc, l));
-      const int64_t m0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qm >> 32), l) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)qm, l));
-      const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(qe >> 32), l) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)qe, l));
-      const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)qf, l);
-      // fits_request: the pod count, then the requests unless the pod requests nothing
-      const bool none = c0 == 0 && m0 == 0 && e0 == 0 && !(f0 & KSIM_POD_HAS_SCALAR);
-      const bool ok = !fit || (room && (none || (c0 <= fc && m0 <= fm && e0 <= fe)));
-      const uint64_t m = __ballot(on && ok);
-      word = lane == l ? m : word;
+    uint64_t word;                                 // lane l: pod j0 + l's ballot
+    if (bp.has_fit_filter == 0) {
+      const uint64_t mk = __ballot(on);
+      word = lane < j1 - j0 ? mk : 0ull;
+    } else {
+      const uint64_t room = __ballot(on && c.num_pods[x] + 1 <= c.alloc_pods[x]);
+      const int64_t fc = c.alloc_cpu[x] - c.req_cpu[x];
+      const int64_t fm = c.alloc_mem[x] - c.req_mem[x];
+      const int64_t fe = c.alloc_eph[x] - c.req_eph[x];
+      for (int32_t l = 0; l < j1 - j0; l++) {
+        const int64_t c0 = s_pq[wv][l][0], m0 = s_pq[wv][l][1], e0 = s_pq[wv][l][2];
+        const uint64_t mk = room & __ballot(c0 <= fc) & __ballot(m0 <= fm) & __ballot(e0 <= fe);
+        if (lane == 0) s_mk[wv][l] = mk;
+      }
+      word = lane < j1 - j0 ? s_mk[wv][lane] : 0ull;
     }
     if (lane < j1 - j0) amask[(size_t)(j0 + lane) * n_words + w] = word;   // one store instruction per wave
     return;

@@ -193,11 +193,14 @@ constexpr int32_t kTopWideK = 4096;  // k_adapt_top with 1024 threads per pod fr
 // j): *s_out = pod j's scan start, *cut_out = its cut offset (-1: no cut),
 // *exact_out = pods with exact windows.  false: the batch is empty
 // (block-uniform).  A pure function of the bitmaps and the state.
+// NT threads (>= kBatchPods): thread j < nb is pod j, the others only join the barriers
+template <int NT = kBatchPods>
 __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
                                              int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
                                              int32_t* cut_out, int32_t* exact_out,
                                              const int32_t* __restrict__ cut0 = nullptr) {
-  __shared__ int64_t sh[kBatchPods / 64];
+  static_assert(NT >= kBatchPods && NT % 64 == 0, "a thread per pod");
+  __shared__ int64_t sh[NT / 64];
   __shared__ int32_t s_first;
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
   const int32_t base = st->cursor;
@@ -246,7 +249,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
 // The relaxation's first round over the whole chip: pod j's cut from its
 // first guess s_j = s_0 + j K (mod N), one wave per pod, 128 bitmap words per
 // step (each lane two, popcounts, a wave scan, the bit by halving), into
-// awin[2j + 1].  window_block's walk is one thread per pod from one block,
+// acut[2j + 1].  window_block's walk is one thread per pod from one block,
 // ~80 dependent words per pod at K = 5,000 (13.8 us per batch, config 4,
 // where the first round is the fixpoint in every batch: profiles/r04/windbg);
 // this launch takes the walk off the single block.
@@ -307,13 +310,14 @@ __global__ __launch_bounds__(256) void k_adapt_cut0(const DevState* __restrict__
 
 // awin[2j] = scan start of pod j, awin[2j+1] = cut offset (-1: no cut, every
 // feasible node kept and all N processed); *aexact = pods with exact windows.
-// The first round's cuts are in awin (k_adapt_cut0).
+// The first round's cuts are in acut (k_adapt_cut0).
 __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __restrict__ st,
                                                              const uint64_t* __restrict__ amask, int32_t n_words,
-                                                             int32_t n, int32_t k, int32_t* __restrict__ awin,
+                                                             int32_t n, int32_t k, const int32_t* __restrict__ acut,
+                                                             int32_t* __restrict__ awin,
                                                              int32_t* __restrict__ aexact) {
   int32_t s, cut, exact;
-  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, awin)) return;
+  if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, acut)) return;
   const int j = threadIdx.x;
   if (j < min(kBatchPods, st->end - st->cursor)) {
     awin[2 * j] = s;
@@ -476,7 +480,7 @@ constexpr int32_t kWinFusedWords = 256;
 // WIN (NT = kBatchPods, unsharded): every block runs the window scan itself
 // (window_block, thread i = pod i) instead of reading k_adapt_window's
 // output; block 0 stores awin / aexact for the pairs and the commit.
-template <bool SH, bool FAST, int NT, bool WIN = false>
+template <bool SH, bool FAST, int NT, int WIN = 0>
 __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
@@ -486,7 +490,8 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
                                                    int32_t* __restrict__ topk_cnt,
                                                    int32_t* __restrict__ topk_complete,
                                                    uint64_t* __restrict__ xsend,
-                                                   int64_t* __restrict__ pnorm = nullptr) {
+                                                   int64_t* __restrict__ pnorm = nullptr,
+                                                   const int32_t* __restrict__ acut = nullptr) {
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
   constexpr int W = NT / 64;
@@ -498,12 +503,15 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
   const int32_t base = st->cursor;
   if (j >= min(kBatchPods, st->end - base)) return;   // block-uniform
   int32_t win_s = 0, win_cut = -1, exact;
-  if constexpr (WIN) {
-    static_assert(!SH && NT == kBatchPods, "fused window: unsharded, one thread per pod");
+  if constexpr (WIN != 0) {
+    // WIN 1: the whole relaxation in every block; WIN 2: from k_adapt_cut0's
+    // first round (acut), so a batch at its fixpoint costs every block one
+    // prefix sum over the batch's cuts
+    static_assert(!SH && (WIN == 2 || NT == kBatchPods), "fused window: unsharded, one thread per pod");
     __shared__ int2 s_win;
     int32_t ws, wc;
     const int32_t kk = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, c.n);
-    window_block(st, amask, n_words, c.n, kk, &ws, &wc, &exact);   // the batch is not empty (above)
+    window_block<NT>(st, amask, n_words, c.n, kk, &ws, &wc, &exact, WIN == 2 ? acut : nullptr);   // batch not empty (above)
     if (tid == j) s_win = make_int2(ws, wc);
     if (j == 0) {
       if (tid < min(kBatchPods, st->end - base)) {
@@ -1023,8 +1031,8 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   if (win_seq)
     launch_window_dbl(a, n_words, k, stream);
   else if (!win_fused) {
-    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin);
-    k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.awin, a.s.aexact);
+    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.acut);
+    k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, a.s.amask, n_words, a.c.n, k, a.s.acut, a.s.awin, a.s.aexact);
   }
   if (evs) (void)hipEventRecord(evs[2], stream);
 #define TOP(F, NT, W) k_adapt_top<false, F, NT, W><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, \
@@ -1052,7 +1060,7 @@ uint32_t launch_batch_adapt(const LaunchArgs& a, hipStream_t stream, hipEvent_t*
   return win_fused ? 0x1du : 0x1fu;                 // fused: the window slot is an empty event pair
 }
 
-const char* const kLazyAdaptKernelNames[kKernelsPerLazyAdapt] = {"k_adapt_mask_commit", "k_adapt_window",
+const char* const kLazyAdaptKernelNames[kKernelsPerLazyAdapt] = {"k_adapt_mask_commit", "k_adapt_cut0",
                                                                  "k_adapt_top", "k_adapt_pairs"};
 
 static void launch_adapt_mask_commit(const LazyBatch& z, bool flush, hipStream_t stream) {
@@ -1077,16 +1085,16 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   if (evs) (void)hipEventRecord(evs[1], stream);
   const bool win_fused = k < kTopWideK && n_words <= kWinFusedWords;
   if (!win_fused) {
-    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin);
-    k_adapt_window<<<1, kBatchPods, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, z.awin, a.s.aexact);
+    // the fixpoint check inside the top (every block): no single-block launch
+    k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(z.st, a.s.amask, n_words, a.c.n, k, a.s.acut);
   }
   if (evs) (void)hipEventRecord(evs[2], stream);
   // every later launch reads X[p] (z.cw) and st[p]
 #define TOP(NT, W) k_adapt_top<false, true, NT, W><<<kBatchPods, NT, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, \
-    a.s.amask, n_words, z.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr)
-  if (k >= kTopWideK) TOP(1024, false);
-  else if (win_fused) TOP(256, true);
-  else TOP(256, false);
+    a.s.amask, n_words, z.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, nullptr, a.s.acut)
+  if (k >= kTopWideK) TOP(1024, 2);
+  else if (win_fused) TOP(256, 1);
+  else TOP(256, 2);
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
   k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
@@ -1130,8 +1138,8 @@ void launch_adapt_sh_window(const LaunchArgs& a, const uint64_t* recv, int32_t W
   const int32_t N = a.c.n_total, nw = (N + 63) / 64;
   const int32_t k = num_feasible_nodes_to_find(a.prof.percentage_of_nodes_to_score, N);
   k_adapt_unpack<<<dim3((nw + 255) / 256, kBatchPods), 256, 0, stream>>>(a.st, recv, W, nw, gmask);
-  k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin);
-  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.awin, a.s.aexact);
+  k_adapt_cut0<<<kBatchPods / 4, 256, 0, stream>>>(a.st, gmask, nw, N, k, a.s.acut);
+  k_adapt_window<<<1, kBatchPods, 0, stream>>>(a.st, gmask, nw, N, k, a.s.acut, a.s.awin, a.s.aexact);
 #define TOP(F, NT) k_adapt_top<true, F, NT><<<kBatchPods, NT, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, gmask, \
     nw, a.s.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.xsend)
   if (k >= kTopWideK) {

@@ -244,6 +244,7 @@ struct DevScratch {
   uint64_t* amask;       // ADAPT batch: S0 feasibility bitmaps [kBatchPods][ceil(n / 64)]
   int32_t* awin;         // ADAPT batch: per pod {scan start, cut offset or -1}
   int32_t* aexact;       // ADAPT batch: pods whose windows are exact
+  int32_t* acut;         // ADAPT batch: k_adapt_cut0's first-round {start, cut} per pod
   uint16_t* wtab;        // ADAPT windows by doubling (n <= 8192): [2][kBatchPods][n] start -> next-start tables
   int32_t* wtot;         // ADAPT windows by doubling: [kBatchPods] feasible nodes per pod
   int32_t* abroken;      // ADAPT batch: a bound node flipped feasibility inside the pod's window

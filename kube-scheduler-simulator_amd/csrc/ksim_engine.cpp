@@ -2047,6 +2047,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.amask, uint64_t*, 8 * (size_t)kBatchPods * ((N + 63) / 64));
   SCR(s.awin, int32_t*, 4 * 2 * (size_t)kBatchPods);
   SCR(s.aexact, int32_t*, 4);
+  SCR(s.acut, int32_t*, 4 * 2 * (size_t)kBatchPods);
   {                                      // the doubling window's tables (clusters of <= 128 bitmap words)
     const size_t NW = (N + 63) / 64 <= 128 ? N : 0;
     SCR(s.wtab, uint16_t*, 2 * 3 * (size_t)kBatchPods * std::max<size_t>(NW, 1));

@@ -114,8 +114,8 @@ def test_adapt_batch_config2_and_pct():
 
 @pytest.mark.parametrize("pct,n_pods", [(0, 45000), (30, 20000)])
 def test_adapt_batch_group_counts(pct, n_pods):
-    """Lazy ADAPT windows by group counts (k_adapt_window_gc: more than 256
-    bitmap words, 1024-node groups ragged at the end): 17,000 nodes, pods at
+    """Lazy ADAPT windows on more than 256 bitmap words (k_adapt_cut0, then
+    the relaxation inside k_adapt_top from those cuts): 17,000 nodes, pods at
     16x config 2's requests fill them, so the feasibility bitmaps turn sparse,
     the windows wrap and ~2,000 pods find no node; K = 850 (pct 0) and
     K = 5,100 (pct 30, the wide top)."""

@@ -55,9 +55,12 @@ __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPod
 // every node row once per pod: B x the node table from L2 / MALL per batch,
 // ~190 us at 100k nodes; here a row is read once per mp pods.)  mp shrinks on
 // small clusters so the grid still fills the chip (mask_pods).
+// (profiles/r04/maskdiv: with the LDS-staged pod loop, 1,280 in place of
+// 2,560 blocks at 5,000 nodes: k_adapt_mask_commit 8.9 -> 7.9 us; at 100,000
+// nodes the 2,048-block grid stays best, 15.8 against 16.6 us)
 __host__ __device__ inline int32_t mask_pods(int32_t n_words) {
   const int32_t wb = (n_words + 3) / 4;            // 4 words (waves) per block
-  const int32_t mp = wb / 8;                       // about 2,048 blocks over B pods
+  const int32_t mp = wb / (n_words <= 256 ? 4 : 8);   // about 2,048 blocks over B pods (1,024 small)
   return mp < 1 ? 1 : mp > 64 ? 64 : mp;
 }
 

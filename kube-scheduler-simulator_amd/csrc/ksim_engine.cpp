@@ -148,6 +148,22 @@ struct ksim_handle {
   // compat-mode single pod
   DevArena pod1_arena;                  // the single-pod uploads (upload_single)
   DevArena nom_arena;                   // a nominated pod (ksim_fw_filter_nominated)
+  DevArena asm_arena;                   // ksim_assume / ksim_forget uploads (never the cycle's pod1)
+  // Reserve / Unreserve calls that arrive while a framework cycle sits between
+  // its PreFilter and Score (the binding goroutine's Unreserve):
+  // upstream's running cycle keeps its snapshot, so the engine applies them
+  // once that cycle has scored (flush_deferred_binds), in call order
+  struct DeferredBind {
+    ksim_pod pod;
+    std::vector<ksim_label_expr> ex;
+    std::vector<ksim_term> tm;
+    std::vector<ksim_topo_use> us;
+    std::vector<ksim_class_add> ad;
+    std::vector<int32_t> nn;
+    int32_t node;
+    int sign;
+  };
+  std::vector<DeferredBind> deferred_binds;
   // pinned, coherent host staging for the per-call uploads / results, and the
   // device's addresses of it (copy kernels read / write it directly)
   void* pin = nullptr;
@@ -635,6 +651,10 @@ int fw_abandon(ksim_handle* h) {
   return KSIM_OK;
 }
 
+}  // namespace
+static int flush_deferred_binds(ksim_handle* h);
+namespace {
+
 int ensure_ready(ksim_handle* h, bool fw = false) {
   if (!h) return KSIM_E_INVALID;
   if (!fw && (h->fw_pending || h->fw_scored || h->fw_dom_dirty)) {
@@ -644,6 +664,7 @@ int ensure_ready(ksim_handle* h, bool fw = false) {
   if (!h->has_profile) return set_err(h, KSIM_E_INVALID, "profile not set");
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   if (h->dc.n <= 0) return set_err(h, KSIM_E_INVALID, "no nodes available");
+  if (!h->fw_pending && !h->deferred_binds.empty()) return flush_deferred_binds(h);
   return KSIM_OK;
 }
 
@@ -1688,6 +1709,7 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->pod_bufs);
   if (h->pod1_arena.p) (void)hipFree(h->pod1_arena.p);
   if (h->nom_arena.p) (void)hipFree(h->nom_arena.p);
+  if (h->asm_arena.p) (void)hipFree(h->asm_arena.p);
   if (h->pin) (void)hipHostFree(h->pin);
   if (h->pout) (void)hipHostFree(h->pout);
   free_bufs(h->pre_bufs);
@@ -1872,6 +1894,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   h->pre_n = 0;
   h->ext_pending = false;
   h->fw_pending = h->fw_scored = h->fw_dom_dirty = false;   // fresh scratch below
+  h->deferred_binds.clear();           // Reserve / Unreserve queued against the old node positions
 
   const int32_t n_total = h->shard_total ? h->shard_total : n;
   if (h->shard_base < 0 || h->shard_base + n > n_total || n_total > KSIM_MAX_NODES)
@@ -2864,20 +2887,62 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
   return KSIM_OK;
 }
 
-static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
-  int rc = ensure_ready(h);
-  if (rc) return rc;
-  if (!ps || !ps->pods || pod_index < 0 || pod_index >= ps->n_pods || node < 0 || node >= h->dc.n)
-    return set_err(h, KSIM_E_INVALID, "bad pod / node");
-  if ((rc = validate_pod(h, ps, pod_index))) return rc;
-  HIPCHK(h, hipSetDevice(h->device));
+// Reserve / Unreserve (wrappedplugin.go:583-584, 617).  They never abandon a
+// framework cycle in flight and never touch its pod upload (their own arena):
+// between that cycle's PreFilter and Score they are queued and applied once it
+// has scored (ensure_ready), as upstream's cycle keeps the snapshot it started
+// from while the cache takes the binding goroutine's ForgetPod.
+static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
   DevPods P;
-  if ((rc = upload_single(h, ps, pod_index, P))) return rc;
+  int rc;
+  if ((rc = upload_single(h, ps, pod_index, P, h->asm_arena))) return rc;
   launch_assume(h->dc, P, 0, node, sign, h->stream);
   HIPCHK(h, hipGetLastError());
   // no synchronization: every later call is ordered after it on the stream,
   // and the next upload waits for the staging (upload_single)
   return KSIM_OK;
+}
+
+static int flush_deferred_binds(ksim_handle* h) {
+  std::vector<ksim_handle::DeferredBind> q;
+  q.swap(h->deferred_binds);
+  HIPCHK(h, hipSetDevice(h->device));
+  for (auto& d : q) {
+    ksim_pod_set v{};
+    v.n_pods = 1;
+    v.pods = &d.pod;
+    v.n_exprs = (int32_t)d.ex.size();
+    v.exprs = d.ex.data();
+    v.n_terms = (int32_t)d.tm.size();
+    v.terms = d.tm.data();
+    v.n_uses = (int32_t)d.us.size();
+    v.uses = d.us.data();
+    v.n_adds = (int32_t)d.ad.size();
+    v.adds = d.ad.data();
+    v.n_nn = (int32_t)d.nn.size();
+    v.nn = d.nn.data();
+    const int rc = apply_bind(h, &v, 0, d.node, d.sign);
+    if (rc) return rc;
+  }
+  return KSIM_OK;
+}
+
+static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
+  int rc = ensure_ready(h, true);
+  if (rc) return rc;
+  if (!ps || !ps->pods || pod_index < 0 || pod_index >= ps->n_pods || node < 0 || node >= h->dc.n)
+    return set_err(h, KSIM_E_INVALID, "bad pod / node");
+  if ((rc = validate_pod(h, ps, pod_index))) return rc;
+  if (h->fw_pending) {                     // a cycle between PreFilter and Score: queued
+    ksim_handle::DeferredBind d;
+    single_pod_set(ps, pod_index, d.pod, d.ex, d.tm, d.us, d.ad, d.nn);
+    d.node = node;
+    d.sign = sign;
+    h->deferred_binds.push_back(std::move(d));
+    return KSIM_OK;
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  return apply_bind(h, ps, pod_index, node, sign);
 }
 
 int ksim_assume(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node) {

@@ -354,3 +354,43 @@ def test_framework_seeded_nominations_topology():
         np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
     np.testing.assert_array_equal(eng.class_count(), ora.class_count())
     assert stats["two_pass"] > 50 and stats["nominated_eval"] > 10, stats
+
+
+def test_forget_during_framework_cycle():
+    """Unreserve from the binding goroutine while the next cycle sits between
+    PreFilter and Score: the engine queues the ksim_forget, the
+    cycle's Score still sees the snapshot it started from, and the forget
+    lands once the cycle has scored.  The oracle runs the same calls with the
+    forget after the cycle's Reserve; every answer and the final node state,
+    class counts included, must agree."""
+    nodes, bound, incoming = gen.config3_objects(n_nodes=300, pods_per_node=3, n_incoming=120)
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, incoming)
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=0))
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    placed = []
+    for i in range(pods.n_pods):
+        e, o = eng.fw_prefilter(pods, i), ora.fw_prefilter(pods, i)
+        np.testing.assert_array_equal(e["fail_plugin"], o["fail_plugin"], err_msg=f"prefilter {i}")
+        forget = placed.pop(0) if (i % 3 == 2 and placed) else None
+        if forget is not None:                 # engine: inside the cycle; oracle: after it
+            eng.forget(pods, *forget)
+        feas = np.flatnonzero(e["fail_plugin"] == abi.PASSED).astype(np.int32)
+        if feas.size == 0:
+            continue
+        es, os_ = eng.fw_score(feas), ora.fw_score(feas)
+        for k in ("raw", "norm", "total"):
+            np.testing.assert_array_equal(es[k][..., feas], os_[k][..., feas], err_msg=f"score {k} {i}")
+        node = int(feas[np.argmax(es["total"][feas])])
+        eng.assume(pods, i, node)
+        ora.assume(pods, i, node)
+        if forget is not None:
+            ora.forget(pods, *forget)
+        placed.append((i, node))
+    es, os_ = eng.node_state(), ora.node_state()
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())

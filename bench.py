@@ -201,6 +201,54 @@ class TimedMatcher:
         return r
 
 
+def host_compile(args, nodes, bound, incoming):
+    """The snapshot and queue compile (once per snapshot / queue, outside the
+    timed region; it replaces upstream's per-pod PreFilter / PreScore scans of
+    the existing pods).  Default: the native encoder (csrc/ksim_encode.cpp,
+    ksim_encode_nodes / ksim_encode_pods); the ksim.model objects are first
+    laid out as its flat ksim_k8s_pool, the step a Go host does with its v1
+    objects (pool_build_s, Python here).  --python-encode: the Python compile
+    (ksim/encode.py) with the count classes matched on the device."""
+    if not args.python_encode:
+        from ksim.nativeenc import NativeEncoder
+        enc = NativeEncoder()
+        cluster, _ = enc.encode_cluster(nodes, bound)
+        pods = enc.encode_pods(cluster, incoming)
+        sec = enc.seconds
+        HOST_COMPILE.update({
+            "encoder": "native (ksim_encode_nodes / ksim_encode_pods)",
+            "native_s": sec["native_s"] + sec["pods_native_s"],
+            "native_encode_nodes_s": sec["native_s"], "native_encode_pods_s": sec["pods_native_s"],
+            "pool_build_s": sec["pool_s"] + sec["pods_pool_s"],
+            "existing_pods": len(bound), "incoming_pods": len(incoming),
+            "note": "count-class compile, once per snapshot / queue, not in the timed region; pool_build_s lays "
+                    "the Python objects out as the encoder's flat input (a Go host builds it from v1 objects)"})
+        return cluster, pods
+    from ksim.encode import encode_cluster, encode_pods
+    matcher = None
+    if not args.host_match and bound:
+        # selector / term matching of the count classes on the device
+        # (ksim_match_terms, int8 MFMA contraction, SURVEY K8)
+        from ksim.engine import Engine
+        from ksim.termmatch import DeviceMatcher
+        matcher = TimedMatcher(DeviceMatcher(Engine(int(os.environ.get("LOCAL_RANK", "0")))))
+    t0 = time.perf_counter()
+    cluster, _ = encode_cluster(nodes, bound, matcher=matcher)
+    t1 = time.perf_counter()
+    pods = encode_pods(cluster, incoming)
+    t2 = time.perf_counter()
+    HOST_COMPILE.update({"encoder": "python (ksim/encode.py)", "encode_cluster_s": t1 - t0, "encode_pods_s": t2 - t1,
+                         "existing_pods": len(bound), "incoming_pods": len(incoming),
+                         "term_matching": "host (Python)" if matcher is None else "device (ksim_match_terms)",
+                         "note": "count-class compile (ksim/encode.py + ksim/topology.py), once per "
+                                 "snapshot/queue, not in the timed region"})
+    if matcher is not None:
+        HOST_COMPILE["match_calls_s"] = matcher.seconds
+        HOST_COMPILE["match_device_ms"] = matcher.device_ms
+        matcher.inner.engine.close()
+    return cluster, pods
+
+
 def build(cfg: int, args, rank: int, world: int):
     """(cluster, pods, profile, description, sharded, scaling) for one rank."""
     from ksim import gen, profile
@@ -217,13 +265,8 @@ def build(cfg: int, args, rank: int, world: int):
         # config 1's object distribution (taints incl. PreferNoSchedule,
         # tolerations, required / preferred node affinity) scaled to config 2's
         # size: the batch path with per-node normalized scores
-        from ksim.encode import encode_cluster, encode_pods
         nodes, pobjs = gen.config1_objects(n_nodes=args.nodes, n_pods=args.pods)
-        t0 = time.perf_counter()
-        cluster, _ = encode_cluster(nodes)
-        pods = encode_pods(cluster, pobjs)
-        HOST_COMPILE.update({"encode_s": time.perf_counter() - t0,
-                             "note": "object encode, once per snapshot/queue, not in the timed region"})
+        cluster, pods = host_compile(args, nodes, [], pobjs)
         desc = (f"config1-scaled: default profile, config-1 distribution on {cluster.n_nodes} nodes x "
                 f"{pods.n_pods} pods, {args.mode.upper()}")
         return cluster, pods, sp, desc, False, "strong"
@@ -233,32 +276,8 @@ def build(cfg: int, args, rank: int, world: int):
                f"node-sharded over {world} GPU(s)"
         return cluster, pods, sp, desc, world > 1, "strong"
     if cfg == 3:
-        from ksim.encode import encode_cluster, encode_pods
         nodes, bound, incoming = gen.config3_objects(n_nodes=args.nodes3, n_incoming=args.pods3)
-        matcher = None
-        if not args.host_match:
-            # selector / term matching of the count classes on the device
-            # (ksim_match_terms, int8 MFMA contraction)
-            from ksim.engine import Engine
-            from ksim.termmatch import DeviceMatcher
-            matcher = TimedMatcher(DeviceMatcher(Engine(int(os.environ.get("LOCAL_RANK", "0")))))
-        t0 = time.perf_counter()
-        cluster, _ = encode_cluster(nodes, bound, matcher=matcher)
-        t1 = time.perf_counter()
-        pods = encode_pods(cluster, incoming)
-        t2 = time.perf_counter()
-        # The count-class compile replaces upstream's per-pod PreFilter/PreScore
-        # scans over existing pods (done once here, outside the timed region).
-        HOST_COMPILE.update({"encode_cluster_s": t1 - t0, "encode_pods_s": t2 - t1,
-                             "existing_pods": len(bound), "incoming_pods": len(incoming),
-                             "term_matching": "host (Python)" if matcher is None else
-                             "device (ksim_match_terms)",
-                             "note": "count-class compile (ksim/encode.py + ksim/topology.py), once per "
-                                     "snapshot/queue, not in the timed region"})
-        if matcher is not None:
-            HOST_COMPILE["match_calls_s"] = matcher.seconds
-            HOST_COMPILE["match_device_ms"] = matcher.device_ms
-            matcher.inner.engine.close()
+        cluster, pods = host_compile(args, nodes, bound, incoming)
         desc = (f"config3: default profile, {cluster.n_nodes} nodes / 3 zones, "
                 f"{int(cluster.num_pods.sum())} existing pods with anti-affinity terms, {pods.n_pods} incoming "
                 f"pods with spread constraints + preferred anti-affinity, {args.mode.upper()}")
@@ -466,6 +485,8 @@ def main():
     ap.add_argument("--shard-mode", choices=["replicated", "nodes"], default="replicated",
                     help="config 2 over N > 1 GPUs: replicated snapshot with the evaluation split by node range "
                          "(one collective per batch), or node shards (two)")
+    ap.add_argument("--python-encode", action="store_true",
+                    help="compile configs 1 / 3 with the Python encoder (ksim/encode.py) instead of the native one")
     ap.add_argument("--host-match", action="store_true",
                     help="config 3: match the count classes' selectors on the host instead of ksim_match_terms")
     ap.add_argument("--no-adapt", action="store_true", help="skip the secondary ADAPT measurement (config 2)")

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 9
+#define KSIM_ABI_VERSION 10
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -824,6 +824,232 @@ typedef struct ksim_emit_input {
  * code only: no device, no handle. */
 int ksim_emit_cycle_json(const ksim_emit_input* in, char* filter_json, int64_t filter_cap, char* score_json,
                          int64_t score_cap, char* final_json, int64_t final_cap, int64_t* lens);
+
+/* ---- native snapshot encoder (ABI 10; SURVEY §2.3 "Host snapshot encoder") ----
+ * Replaces the host compile a simulator host runs before the engine sees a
+ * snapshot: v1.Node / v1.Pod objects -> ksim_node_table / ksim_vocab (nodeTree
+ * order, NodeInfo aggregates of the bound pods, taint and label vocabularies)
+ * and the pending queue -> ksim_pod_set (request sums, toleration bitsets,
+ * compiled node-selector terms, PodTopologySpread / InterPodAffinity count
+ * classes, NodePorts / ImageLocality classes, NetworkBandwidth quantities).
+ * It is the restatement of ksim/encode.py + ksim/topology.py in C++ and its
+ * outputs are byte-equal to theirs (tests/test_native_encode.py).  Host code
+ * only: no device, no engine handle.
+ *
+ * The reference hands the plugins these objects through the scheduler cache
+ * (simulator/scheduler/plugin/plugins.go:75-87 builds the plugins the engine
+ * replaces; integration/go/engine/plugins.go implements its Encoder over this
+ * API).  Input objects live in one flat pool: every string is an id into one
+ * string table, every list a (first, count) range into a typed array of the
+ * pool.  A Go caller builds the pool from v1 objects with no Go pointer inside
+ * C memory (cgo rule): one byte blob, offsets and arrays of plain structs.
+ * Where nil and empty differ in Kubernetes (label selectors, nodeAffinity
+ * required terms) first = -1 (or id -1) is nil. */
+typedef struct ksim_k8s_kv {              /* map entry: labels, annotations, resource lists */
+  int32_t key, value;                     /* string ids; resource lists carry Quantity strings */
+} ksim_k8s_kv;
+
+typedef struct ksim_k8s_taint {
+  int32_t key, value, effect;             /* string ids */
+} ksim_k8s_taint;
+
+typedef struct ksim_k8s_toleration {
+  int32_t key, op, value, effect;         /* string ids; op "" = Equal */
+} ksim_k8s_toleration;
+
+typedef struct ksim_k8s_requirement {     /* NodeSelectorRequirement / LabelSelectorRequirement */
+  int32_t key, op;                        /* string ids */
+  int32_t values_first, values_count;     /* range of ksim_k8s_pool.str_list */
+} ksim_k8s_requirement;
+
+typedef struct ksim_k8s_selector_term {   /* NodeSelectorTerm */
+  int32_t exprs_first, exprs_count;       /* matchExpressions: ksim_k8s_pool.reqs */
+  int32_t fields_first, fields_count;     /* matchFields: ksim_k8s_pool.reqs */
+} ksim_k8s_selector_term;
+
+typedef struct ksim_k8s_preferred_term {  /* PreferredSchedulingTerm */
+  int32_t weight, term;                   /* term: index into ksim_k8s_pool.terms */
+} ksim_k8s_preferred_term;
+
+typedef struct ksim_k8s_label_selector {  /* metav1.LabelSelector */
+  int32_t labels_first, labels_count;     /* matchLabels: ksim_k8s_pool.kv */
+  int32_t exprs_first, exprs_count;       /* matchExpressions: ksim_k8s_pool.reqs */
+} ksim_k8s_label_selector;
+
+typedef struct ksim_k8s_pod_term {        /* PodAffinityTerm (weight: WeightedPodAffinityTerm) */
+  int32_t topology_key;                   /* string id */
+  int32_t selector;                       /* ksim_k8s_pool.selectors index, -1 = nil */
+  int32_t ns_first, ns_count;             /* namespaces: ksim_k8s_pool.str_list */
+  int32_t ns_selector;                    /* namespaceSelector, -1 = nil */
+  int32_t weight;
+} ksim_k8s_pod_term;
+
+typedef struct ksim_k8s_spread {          /* TopologySpreadConstraint */
+  int32_t max_skew;
+  int32_t topology_key, when_unsatisfiable;   /* string ids */
+  int32_t selector;                       /* -1 = nil */
+  int32_t node_affinity_policy;           /* string id, -1 = nil (Honor) */
+  int32_t node_taints_policy;             /* string id, -1 = nil (Ignore) */
+} ksim_k8s_spread;
+
+typedef struct ksim_k8s_port {            /* ContainerPort: hostPort 0 = none */
+  int32_t host_port, protocol, host_ip;   /* protocol / host_ip: string ids ("" = TCP / 0.0.0.0) */
+} ksim_k8s_port;
+
+typedef struct ksim_k8s_container {
+  int32_t requests_first, requests_count; /* resources.requests: ksim_k8s_pool.kv */
+  int32_t ports_first, ports_count;
+  int32_t image;                          /* string id */
+} ksim_k8s_container;
+
+typedef struct ksim_k8s_image {           /* node status.images entry */
+  int32_t names_first, names_count;       /* ksim_k8s_pool.str_list */
+  int64_t size_bytes;
+} ksim_k8s_image;
+
+typedef struct ksim_k8s_volume_group {    /* one VolumeBinding / VolumeZone group (see "volume groups") */
+  int32_t terms_first, terms_count;       /* ksim_k8s_pool.terms; match_fields ops "__true__" /
+                                             "__false__" are decided by the host's binder */
+} ksim_k8s_volume_group;
+
+typedef struct ksim_k8s_node {
+  int32_t name, unschedulable;
+  int32_t labels_first, labels_count;
+  int32_t taints_first, taints_count;
+  int32_t alloc_first, alloc_count;       /* status.allocatable: kv of Quantity strings */
+  int32_t annotations_first, annotations_count;
+  int32_t images_first, images_count;
+} ksim_k8s_node;
+
+#define KSIM_K8S_VOLUMES_NONE   0         /* no persistentVolumeClaim volume */
+#define KSIM_K8S_VOLUMES_REFUSE 1         /* a volume the engine does not model (KSIM_POD_HAS_VOLUMES) */
+#define KSIM_K8S_VOLUMES_GROUPS 2         /* claims compiled by the host's binder into groups */
+
+typedef struct ksim_k8s_pod {
+  int32_t name, namespace_;
+  int32_t labels_first, labels_count;
+  int32_t annotations_first, annotations_count;
+  int32_t containers_first, containers_count;
+  int32_t init_first, init_count;         /* initContainers */
+  int32_t overhead_first, overhead_count; /* kv */
+  int32_t selector_first, selector_count; /* spec.nodeSelector: kv */
+  int32_t required_first, required_count; /* nodeAffinity required terms; first = -1: nil */
+  int32_t preferred_first, preferred_count;
+  int32_t tolerations_first, tolerations_count;
+  int32_t spread_first, spread_count;
+  int32_t aff_req_first, aff_req_count;   /* podAffinity required: ksim_k8s_pool.pod_terms */
+  int32_t aff_pref_first, aff_pref_count; /* podAffinity preferred (weighted) */
+  int32_t anti_req_first, anti_req_count; /* podAntiAffinity required */
+  int32_t anti_pref_first, anti_pref_count;
+  int32_t node_name;                      /* string id ("" = unbound) */
+  int32_t owner_api_version, owner_kind, owner_name;   /* controller ownerReference; -1 = none */
+  int32_t volumes;                        /* KSIM_K8S_VOLUMES_* */
+  int32_t vb_first, vb_count, vb_bound;   /* VolumeBinding groups; the first vb_bound are bound PVs */
+  int32_t vz_first, vz_count;             /* VolumeZone groups */
+  int32_t _pad;
+} ksim_k8s_pod;
+
+typedef struct ksim_k8s_namespace {
+  int32_t name, labels_first, labels_count, _pad;
+} ksim_k8s_namespace;
+
+typedef struct ksim_k8s_service {         /* v1.Service: spec.selector (first = -1: nil) */
+  int32_t namespace_, selector_first, selector_count, _pad;
+} ksim_k8s_service;
+
+typedef struct ksim_k8s_controller {      /* ReplicationController / ReplicaSet / StatefulSet */
+  int32_t kind, namespace_, name;         /* string ids */
+  int32_t rc_selector_first, rc_selector_count;   /* ReplicationController spec.selector (kv, -1: nil) */
+  int32_t selector;                       /* ReplicaSet / StatefulSet spec.selector (-1: nil) */
+} ksim_k8s_controller;
+
+typedef struct ksim_k8s_pool {
+  const char* strings;                    /* string i = strings[str_off[i] .. str_off[i+1]) */
+  const int64_t* str_off;                 /* [n_strings + 1] */
+  int64_t n_strings;
+  const int32_t* str_list;   int64_t n_str_list;   /* string-id lists */
+  const ksim_k8s_kv* kv;     int64_t n_kv;
+  const ksim_k8s_taint* taints;           int64_t n_taints;
+  const ksim_k8s_toleration* tolerations; int64_t n_tolerations;
+  const ksim_k8s_requirement* reqs;       int64_t n_reqs;
+  const ksim_k8s_selector_term* terms;    int64_t n_terms;
+  const ksim_k8s_preferred_term* preferred; int64_t n_preferred;
+  const ksim_k8s_label_selector* selectors; int64_t n_selectors;
+  const ksim_k8s_pod_term* pod_terms;     int64_t n_pod_terms;
+  const ksim_k8s_spread* spread;          int64_t n_spread;
+  const ksim_k8s_port* ports;             int64_t n_ports;
+  const ksim_k8s_container* containers;   int64_t n_containers;
+  const ksim_k8s_image* images;           int64_t n_images;
+  const ksim_k8s_volume_group* volume_groups; int64_t n_volume_groups;
+  const ksim_k8s_node* nodes;             int64_t n_nodes;
+  const ksim_k8s_pod* pods;               int64_t n_pods;
+  const ksim_k8s_namespace* namespaces;   int64_t n_namespaces;
+  const ksim_k8s_service* services;       int64_t n_services;
+  const ksim_k8s_controller* controllers; int64_t n_controllers;
+} ksim_k8s_pool;
+
+typedef struct ksim_encode_nodes_opts {
+  /* NetworkBandwidthArgs annotation names (string ids of the pool; -1 = the
+     plugin's default, networkbandwidth/plugin.go:200-204) */
+  int32_t nb_node_limit, nb_ingress_request, nb_egress_request;
+  int32_t keep_previous;                  /* 1: the previous snapshot's scalar columns first and its
+                                             count classes registered first, with their ids (the
+                                             scheduler cache after node deltas, ksim/ingest.py NodeCache) */
+  int32_t extra_scalar_first, extra_scalar_count;  /* str_list: scalar columns no node offers yet */
+} ksim_encode_nodes_opts;
+
+#define KSIM_SPREAD_DEFAULTS_NONE   0     /* no profile defaults: only the pods' own constraints */
+#define KSIM_SPREAD_DEFAULTS_SYSTEM 1     /* PodTopologySpreadArgs defaultingType System */
+#define KSIM_SPREAD_DEFAULTS_LIST   2     /* defaultingType List: spread_first/count */
+
+typedef struct ksim_encode_pods_opts {
+  /* NodeAffinityArgs.addedAffinity: required terms (first = -1: nil) and preferred terms */
+  int32_t added_required_first, added_required_count;
+  int32_t added_preferred_first, added_preferred_count;
+  /* PodTopologySpreadArgs: the defaults a pod without constraints takes, with
+     the selector helper.DefaultSelector builds from the pool's services and
+     controllers */
+  int32_t spread_defaults;                /* KSIM_SPREAD_DEFAULTS_* */
+  int32_t spread_first, spread_count;     /* List defaults (ksim_k8s_pool.spread) */
+  int32_t _pad;
+} ksim_encode_pods_opts;
+
+typedef struct ksim_encoder ksim_encoder;
+
+typedef struct ksim_encoder_info {
+  int32_t n_nodes, n_scalar, n_label_cols, n_taints;
+  int32_t n_classes, n_pods, n_exprs, n_terms;
+  int32_t n_uses, n_adds, n_nn, _pad;
+} ksim_encoder_info;
+
+int  ksim_encoder_create(ksim_encoder** out);
+void ksim_encoder_destroy(ksim_encoder* e);
+const char* ksim_encoder_last_error(const ksim_encoder* e);
+/* A snapshot: pool.nodes (any order; encoded in nodeTree order) and pool.pods,
+ * the pods already bound (spec.nodeName; a pod naming no node of the pool is
+ * skipped), pool.namespaces for namespaceSelector terms.  Replaces the
+ * encoder's snapshot; label columns start empty. */
+int ksim_encode_nodes(ksim_encoder* e, const ksim_k8s_pool* pool, const ksim_encode_nodes_opts* opts);
+/* The queue pool.pods against the current snapshot: label columns and count
+ * classes the pods reference are added to the snapshot (the node table's
+ * labels / class_count change), the pod set is replaced. */
+int ksim_encode_pods(ksim_encoder* e, const ksim_k8s_pool* pool, const ksim_encode_pods_opts* opts);
+/* Views of the encoder's buffers, valid until its next encode call. */
+int ksim_encoder_cluster(const ksim_encoder* e, ksim_node_table* nodes, ksim_vocab* vocab);
+int ksim_encoder_pods(const ksim_encoder* e, ksim_pod_set* pods);
+int ksim_encoder_get_info(const ksim_encoder* e, ksim_encoder_info* out);
+/* order[position] = index into the snapshot pool's nodes */
+int ksim_encoder_node_order(const ksim_encoder* e, int32_t* order);
+/* Host metadata (strings never cross to the device): what = KSIM_ENC_STR_*,
+ * i / j as listed; NULL when out of range.  Valid until the next encode call. */
+#define KSIM_ENC_STR_LABEL_KEY    0       /* i: label column */
+#define KSIM_ENC_STR_LABEL_VALUE  1       /* i: label column, j: value id */
+#define KSIM_ENC_STR_SCALAR       2       /* i: scalar column */
+#define KSIM_ENC_STR_TAINT_KEY    3       /* i: taint vocabulary id (>= 1) */
+#define KSIM_ENC_STR_TAINT_VALUE  4
+#define KSIM_ENC_STR_TAINT_EFFECT 5
+#define KSIM_ENC_STR_NODE_NAME    6       /* i: node position */
+const char* ksim_encoder_string(const ksim_encoder* e, int32_t what, int32_t i, int32_t j);
 
 #ifdef __cplusplus
 }

@@ -55,10 +55,11 @@
 // by the original plugin for the whole cycle: the engine has no CPU fallback,
 // the reference plugins are the answer outside its scope.
 //
-// NOT BUILT HERE (no Go toolchain in the build container).  The node / pod
-// encoders (Encoder) are the Go counterparts of ksim/encode.py and
-// ksim/topology.py; ksim/fwplugins.py is the Python mirror of this file and
-// tests/test_gpu_fw.py drives it under a racing-framework mirror.
+// NOT BUILT HERE (no Go toolchain in the build container).  The Encoder is
+// NativeEncoder (encoder.go) over the engine's native snapshot encoder
+// (ksim_encode_nodes / ksim_encode_pods, byte-equal to ksim/encode.py);
+// ksim/fwplugins.py is the Python mirror of this file and tests/test_gpu_fw.py
+// drives it under a racing-framework mirror.
 package engine
 
 /*
@@ -87,12 +88,16 @@ import (
 // Encoder is the host side of the snapshot: NodeInfo -> SoA node table in
 // nodeTree order, Pod -> ksim_pod_set (requests, tolerations, selector terms,
 // topology uses / adds, PreFilterResult.NodeNames), as ksim/encode.py does.
+// NativeEncoder (encoder.go) implements it over ksim_encode_nodes / _pods.
 type Encoder interface {
 	// Snapshot brings the engine's device snapshot up to the framework's
 	// (UpdateSnapshot: node informer deltas through Engine.UpsertNodes).
 	Snapshot(e *Engine, f framework.Handle) error
 	// Pod encodes one pod; the returned set stays valid until the next call.
 	Pod(pod *v1.Pod) (*C.ksim_pod_set, error)
+	// Resync re-sends the node table when Pod added label columns or count
+	// classes (keys / selectors no earlier pod referenced).
+	Resync(e *Engine) error
 	// NodeNames are the node names in nodeTree order (engine positions).
 	NodeNames() []string
 	// Position of a node name in the engine's snapshot.
@@ -207,6 +212,9 @@ func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f frame
 		return nil, err
 	}
 	ps, err := p.Enc.Pod(pod)
+	if err == nil {
+		err = p.Enc.Resync(p.Engine)
+	}
 	c := &cycle{nNodes: len(p.Enc.NodeNames()), sh: &cycleShared{nom: map[int]nomAnswer{}}}
 	if err != nil {
 		c.refused = true
@@ -221,12 +229,15 @@ func (p *Profile) ensureFilter(state *framework.CycleState, pod *v1.Pod, f frame
 	var out C.ksim_eval_out
 	out.fail_plugin = (*C.uint8_t)(unsafe.Pointer(&c.fail[0]))
 	out.fail_detail = (*C.uint32_t)(unsafe.Pointer(&c.detail[0]))
+	// the error text is read under the handle's mutex (another goroutine's
+	// call may set the handle's last error right after this one)
 	p.Engine.mu.Lock()
 	rc := C.ksim_fw_prefilter(p.Engine.h, ps, 0, &out)
+	err = p.Engine.err(rc)
 	p.Engine.mu.Unlock()
 	if rc == C.KSIM_E_UNSUPPORTED {
 		c.refused = true
-	} else if err := p.Engine.err(rc); err != nil {
+	} else if err != nil {
 		return nil, err
 	}
 	c.status = int32(out.status)
@@ -669,12 +680,13 @@ func (p *postFilter) PostFilter(ctx context.Context, state *framework.CycleState
 	out.victims_cap = C.int32_t(len(victims))
 	pr.Engine.mu.Lock()
 	rc := C.ksim_preempt_nominated(pr.Engine.h, c.ps, 0, C.int32_t(prio), nps, C.int32_t(len(gnodes)), gn, gf, gc, &out)
+	perr := pr.Engine.err(rc) // under the mutex: the handle's last error is this call's
 	pr.Engine.mu.Unlock()
 	if rc == C.KSIM_E_UNSUPPORTED {
 		return p.orig.(framework.PostFilterPlugin).PostFilter(ctx, state, pod, m)
 	}
-	if err := pr.Engine.err(rc); err != nil {
-		return nil, framework.AsStatus(err)
+	if perr != nil {
+		return nil, framework.AsStatus(perr)
 	}
 	if out.nominated < 0 {
 		// no candidate: ModeOverride "" clears the pod's nomination

@@ -1669,6 +1669,28 @@ size_t ksim_abi_sizeof(int which) {
     case 9: return sizeof(ksim_topo_use);
     case 10: return sizeof(ksim_class_add);
     case 11: return sizeof(ksim_match_problem);
+    case 12: return sizeof(ksim_k8s_kv);
+    case 13: return sizeof(ksim_k8s_taint);
+    case 14: return sizeof(ksim_k8s_toleration);
+    case 15: return sizeof(ksim_k8s_requirement);
+    case 16: return sizeof(ksim_k8s_selector_term);
+    case 17: return sizeof(ksim_k8s_preferred_term);
+    case 18: return sizeof(ksim_k8s_label_selector);
+    case 19: return sizeof(ksim_k8s_pod_term);
+    case 20: return sizeof(ksim_k8s_spread);
+    case 21: return sizeof(ksim_k8s_port);
+    case 22: return sizeof(ksim_k8s_container);
+    case 23: return sizeof(ksim_k8s_image);
+    case 24: return sizeof(ksim_k8s_volume_group);
+    case 25: return sizeof(ksim_k8s_node);
+    case 26: return sizeof(ksim_k8s_pod);
+    case 27: return sizeof(ksim_k8s_namespace);
+    case 28: return sizeof(ksim_k8s_service);
+    case 29: return sizeof(ksim_k8s_controller);
+    case 30: return sizeof(ksim_k8s_pool);
+    case 31: return sizeof(ksim_encode_nodes_opts);
+    case 32: return sizeof(ksim_encode_pods_opts);
+    case 33: return sizeof(ksim_encoder_info);
     default: return 0;
   }
 }

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -293,8 +293,91 @@ class MatchProblem(ctypes.Structure):
     ]
 
 
+# ---- native snapshot encoder input pool (ksim_k8s_*; ksim/nativeenc.py) ------
+def _i32s(*names):
+    return np.dtype([(n, "<i4") for n in names], align=True)
+
+
+K8S_KV_DTYPE = _i32s("key", "value")
+K8S_TAINT_DTYPE = _i32s("key", "value", "effect")
+K8S_TOLERATION_DTYPE = _i32s("key", "op", "value", "effect")
+K8S_REQ_DTYPE = _i32s("key", "op", "values_first", "values_count")
+K8S_TERM_DTYPE = _i32s("exprs_first", "exprs_count", "fields_first", "fields_count")
+K8S_PREF_DTYPE = _i32s("weight", "term")
+K8S_SELECTOR_DTYPE = _i32s("labels_first", "labels_count", "exprs_first", "exprs_count")
+K8S_POD_TERM_DTYPE = _i32s("topology_key", "selector", "ns_first", "ns_count", "ns_selector", "weight")
+K8S_SPREAD_DTYPE = _i32s("max_skew", "topology_key", "when_unsatisfiable", "selector", "node_affinity_policy",
+                         "node_taints_policy")
+K8S_PORT_DTYPE = _i32s("host_port", "protocol", "host_ip")
+K8S_CONTAINER_DTYPE = _i32s("requests_first", "requests_count", "ports_first", "ports_count", "image")
+K8S_IMAGE_DTYPE = np.dtype([("names_first", "<i4"), ("names_count", "<i4"), ("size_bytes", "<i8")], align=True)
+K8S_GROUP_DTYPE = _i32s("terms_first", "terms_count")
+K8S_NODE_DTYPE = _i32s("name", "unschedulable", "labels_first", "labels_count", "taints_first", "taints_count",
+                       "alloc_first", "alloc_count", "annotations_first", "annotations_count", "images_first",
+                       "images_count")
+K8S_POD_DTYPE = _i32s("name", "namespace", "labels_first", "labels_count", "annotations_first",
+                      "annotations_count", "containers_first", "containers_count", "init_first", "init_count",
+                      "overhead_first", "overhead_count", "selector_first", "selector_count", "required_first",
+                      "required_count", "preferred_first", "preferred_count", "tolerations_first",
+                      "tolerations_count", "spread_first", "spread_count", "aff_req_first", "aff_req_count",
+                      "aff_pref_first", "aff_pref_count", "anti_req_first", "anti_req_count", "anti_pref_first",
+                      "anti_pref_count", "node_name", "owner_api_version", "owner_kind", "owner_name", "volumes",
+                      "vb_first", "vb_count", "vb_bound", "vz_first", "vz_count", "_pad")
+K8S_NAMESPACE_DTYPE = _i32s("name", "labels_first", "labels_count", "_pad")
+K8S_SERVICE_DTYPE = _i32s("namespace", "selector_first", "selector_count", "_pad")
+K8S_CONTROLLER_DTYPE = _i32s("kind", "namespace", "name", "rc_selector_first", "rc_selector_count", "selector")
+K8S_VOLUMES_NONE = 0
+K8S_VOLUMES_REFUSE = 1
+K8S_VOLUMES_GROUPS = 2
+SPREAD_DEFAULTS_NONE = 0
+SPREAD_DEFAULTS_SYSTEM = 1
+SPREAD_DEFAULTS_LIST = 2
+ENC_STR_LABEL_KEY = 0
+ENC_STR_LABEL_VALUE = 1
+ENC_STR_SCALAR = 2
+ENC_STR_TAINT_KEY = 3
+ENC_STR_TAINT_VALUE = 4
+ENC_STR_TAINT_EFFECT = 5
+ENC_STR_NODE_NAME = 6
+
+# ksim_k8s_pool: (field, element dtype or None for raw pointers) in C order
+POOL_ARRAYS = [("str_list", np.dtype("<i4")), ("kv", K8S_KV_DTYPE), ("taints", K8S_TAINT_DTYPE),
+               ("tolerations", K8S_TOLERATION_DTYPE), ("reqs", K8S_REQ_DTYPE), ("terms", K8S_TERM_DTYPE),
+               ("preferred", K8S_PREF_DTYPE), ("selectors", K8S_SELECTOR_DTYPE), ("pod_terms", K8S_POD_TERM_DTYPE),
+               ("spread", K8S_SPREAD_DTYPE), ("ports", K8S_PORT_DTYPE), ("containers", K8S_CONTAINER_DTYPE),
+               ("images", K8S_IMAGE_DTYPE), ("volume_groups", K8S_GROUP_DTYPE), ("nodes", K8S_NODE_DTYPE),
+               ("pods", K8S_POD_DTYPE), ("namespaces", K8S_NAMESPACE_DTYPE), ("services", K8S_SERVICE_DTYPE),
+               ("controllers", K8S_CONTROLLER_DTYPE)]
+
+
+class K8sPool(ctypes.Structure):
+    _fields_ = ([("strings", ctypes.c_void_p), ("str_off", ctypes.c_void_p), ("n_strings", ctypes.c_int64)] +
+                [f for name, _ in POOL_ARRAYS for f in ((name, ctypes.c_void_p), ("n_" + name, ctypes.c_int64))])
+
+
+class EncodeNodesOpts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("nb_node_limit", "nb_ingress_request", "nb_egress_request",
+                                              "keep_previous", "extra_scalar_first", "extra_scalar_count")]
+
+
+class EncodePodsOpts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("added_required_first", "added_required_count",
+                                              "added_preferred_first", "added_preferred_count", "spread_defaults",
+                                              "spread_first", "spread_count", "_pad")]
+
+
+class EncoderInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("n_nodes", "n_scalar", "n_label_cols", "n_taints", "n_classes",
+                                              "n_pods", "n_exprs", "n_terms", "n_uses", "n_adds", "n_nn", "_pad")]
+
+
 STRUCT_ORDER = [NodeTable, Vocab, LABEL_EXPR_DTYPE, TERM_DTYPE, POD_DTYPE, PodSet, Profile,
-                EvalOut, BatchStats, TOPO_USE_DTYPE, CLASS_ADD_DTYPE, MatchProblem]
+                EvalOut, BatchStats, TOPO_USE_DTYPE, CLASS_ADD_DTYPE, MatchProblem,
+                K8S_KV_DTYPE, K8S_TAINT_DTYPE, K8S_TOLERATION_DTYPE, K8S_REQ_DTYPE, K8S_TERM_DTYPE,
+                K8S_PREF_DTYPE, K8S_SELECTOR_DTYPE, K8S_POD_TERM_DTYPE, K8S_SPREAD_DTYPE, K8S_PORT_DTYPE,
+                K8S_CONTAINER_DTYPE, K8S_IMAGE_DTYPE, K8S_GROUP_DTYPE, K8S_NODE_DTYPE, K8S_POD_DTYPE,
+                K8S_NAMESPACE_DTYPE, K8S_SERVICE_DTYPE, K8S_CONTROLLER_DTYPE, K8sPool, EncodeNodesOpts,
+                EncodePodsOpts, EncoderInfo]
 
 
 def struct_size(s) -> int:

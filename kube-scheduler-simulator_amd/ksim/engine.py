@@ -32,6 +32,9 @@ EXPORTS = [
     "ksim_set_bound_pods", "ksim_preempt", "ksim_upsert_nodes", "ksim_remove_node",
     "ksim_match_terms", "ksim_set_eval_range", "ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize",
     "ksim_fw_filter_nominated", "ksim_preempt_nominated",
+    "ksim_encoder_create", "ksim_encoder_destroy", "ksim_encoder_last_error", "ksim_encode_nodes",
+    "ksim_encode_pods", "ksim_encoder_cluster", "ksim_encoder_pods", "ksim_encoder_get_info",
+    "ksim_encoder_node_order", "ksim_encoder_string",
 ]
 
 
@@ -124,6 +127,20 @@ def _load(path):
     L.ksim_comm_unique_id.argtypes = [vp]
     L.ksim_comm_init.argtypes = [vp, i32, i32, vp]
     L.ksim_group_schedule_loaded.argtypes = [vp, i32, i32, i32, vp, vp]
+    # the native snapshot encoder (host code: callable without a GPU)
+    L.ksim_encoder_create.argtypes = [ctypes.POINTER(vp)]
+    L.ksim_encoder_destroy.argtypes = [vp]
+    L.ksim_encoder_destroy.restype = None
+    L.ksim_encoder_last_error.argtypes = [vp]
+    L.ksim_encoder_last_error.restype = ctypes.c_char_p
+    L.ksim_encode_nodes.argtypes = [vp, vp, vp]
+    L.ksim_encode_pods.argtypes = [vp, vp, vp]
+    L.ksim_encoder_cluster.argtypes = [vp, vp, vp]
+    L.ksim_encoder_pods.argtypes = [vp, vp]
+    L.ksim_encoder_get_info.argtypes = [vp, vp]
+    L.ksim_encoder_node_order.argtypes = [vp, vp]
+    L.ksim_encoder_string.argtypes = [vp, i32, i32, i32]
+    L.ksim_encoder_string.restype = ctypes.c_char_p
     return L
 
 

@@ -207,6 +207,16 @@ def config3_objects(n_nodes: int = 10000, pods_per_node: int = 10, n_incoming: i
             name=f"node-{i:06d}",
             labels={"kubernetes.io/hostname": f"node-{i:06d}", "topology.kubernetes.io/zone": f"z{i % 3}"},
             allocatable={"cpu": str(cores), "memory": f"{mem}Gi", "pods": "110"}))
+    # pods of one workload share their spec's objects (selectors, terms,
+    # containers), as the pods of a ReplicaSet do: built once per distinct value
+    shared: dict = {}
+
+    def one(key, make):
+        x = shared.get(key)
+        if x is None:
+            x = shared[key] = make()
+        return x
+
     bound = []
     j = 0
     for i in range(n_nodes):
@@ -215,17 +225,18 @@ def config3_objects(n_nodes: int = 10000, pods_per_node: int = 10, n_incoming: i
             cpu = 100 * (1 + r.below(5))
             mem = 256 * (1 + r.below(8))
             p = Pod(name=f"existing-{j:07d}", labels={"app": app, "tier": "web"},
-                    containers=[Container({"cpu": f"{cpu}m", "memory": f"{mem}Mi"})],
+                    containers=[one(("c", cpu, mem), lambda: Container({"cpu": f"{cpu}m", "memory": f"{mem}Mi"}))],
                     node_name=nodes[i].name)
             target = f"a{r.below(N_APPS)}"
             if zone_anti_every and j % zone_anti_every == zone_anti_every - 1:
-                p.pod_anti_affinity_required = [PodAffinityTerm(
-                    "topology.kubernetes.io/zone", LabelSelector({"app": target, "tier": "critical"}))]
+                p.pod_anti_affinity_required = [one(("za", target), lambda: PodAffinityTerm(
+                    "topology.kubernetes.io/zone", LabelSelector({"app": target, "tier": "critical"})))]
             else:
-                p.pod_anti_affinity_required = [PodAffinityTerm(
-                    "kubernetes.io/hostname", LabelSelector({"app": target}))]
-            p.pod_affinity_preferred = [WeightedPodAffinityTerm(1 + r.below(100), PodAffinityTerm(
-                "topology.kubernetes.io/zone", LabelSelector({"app": f"a{r.below(N_APPS)}"})))]
+                p.pod_anti_affinity_required = [one(("ha", target), lambda: PodAffinityTerm(
+                    "kubernetes.io/hostname", LabelSelector({"app": target})))]
+            w, pref = 1 + r.below(100), f"a{r.below(N_APPS)}"
+            p.pod_affinity_preferred = [one(("pa", w, pref), lambda: WeightedPodAffinityTerm(w, PodAffinityTerm(
+                "topology.kubernetes.io/zone", LabelSelector({"app": pref}))))]
             bound.append(p)
             j += 1
     incoming = []

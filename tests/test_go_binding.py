@@ -41,3 +41,17 @@ def test_framework_entry_points_bound():
     for fn in ("ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize", "ksim_assume", "ksim_forget",
                "ksim_preempt", "ksim_preempt_nominated", "ksim_fw_filter_nominated"):
         assert f"C.{fn}(" in src, fn
+
+
+def test_native_encoder_implements_encoder():
+    """integration/go/engine/encoder.go NativeEncoder has every method of the
+    Encoder interface the engine-backed plugins call (plugins.go), and drives
+    the native snapshot encoder of the header."""
+    src = _go_sources()
+    iface = re.search(r"type Encoder interface \{(.*?)\n\}", src["plugins.go"], re.S).group(1)
+    methods = set(re.findall(r"^\t([A-Z]\w*)\(", iface, re.M))
+    impl = set(re.findall(r"^func \(n \*NativeEncoder\) ([A-Z]\w*)\(", src["encoder.go"], re.M))
+    assert methods and methods <= impl, methods - impl
+    for fn in ("ksim_encoder_create", "ksim_encode_nodes", "ksim_encode_pods", "ksim_encoder_cluster",
+               "ksim_encoder_pods", "ksim_encoder_node_order", "ksim_encoder_string"):
+        assert f"C.{fn}(" in src["encoder.go"], fn

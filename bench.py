@@ -348,33 +348,54 @@ def roofline_entry(dominant, achieved, traffic, alg, avg_ms, timing, knodes, by_
 
 
 def bench_fw(args, out):
-    """--mode fw: the drop-in's per-pod cost.  The framework-driven calls the
-    Go adapter makes for one scheduling cycle (integration/go/engine/plugins.go):
-    ksim_fw_prefilter (Filter of every node, F x N answers copied back),
-    the framework's feasible list (here the sequential worker's first K in
-    scan order from nextStartNodeIndex), ksim_fw_score over it (S x N raw
-    scores copied back), ksim_fw_normalize per NormalizeScore plugin, the
-    max total, ksim_assume; output buffers reused as the adapter would.
-    Config 1's distribution at 100 nodes (the reference's own config 1) and
-    5,000 nodes; the oracle's ksim_oracle_fw_* calls beside it on the same
-    sequence (CPU, one thread).  One JSON line; host (Python ctypes) overhead
-    included in ``us_per_cycle``, the C calls alone in ``us_in_calls``."""
+    """--mode fw: the drop-in's per-pod cost.  The calls the Go adapter makes
+    for one scheduling cycle (integration/go/engine/plugins.go, encoder.go):
+    ksim_encode_pods (the pod compiled against the snapshot by the native
+    encoder), ksim_fw_prefilter (Filter of every node, F x N answers and the
+    raw scores copied back), the framework's feasible list (here the
+    sequential worker's first K in scan order from nextStartNodeIndex),
+    ksim_fw_score over it (answered on the host when no PreScore depends on
+    the list), ksim_fw_normalize per NormalizeScore plugin, the max total,
+    ksim_assume; output buffers reused as the adapter would.  Config 1's
+    distribution at 100 nodes (the reference's own config 1) and 5,000 nodes;
+    the oracle's ksim_oracle_fw_* calls beside it on the same sequence (CPU,
+    one thread; pods pre-compiled).  The Python objects are laid out as the
+    encoder's flat pool before the loop (a Go host builds it from its v1 pod:
+    ``pool_build_us``, Python here, is reported, not counted).  One JSON line;
+    Python ctypes glue included in ``us_per_cycle``, the C calls alone in
+    ``us_in_calls``."""
     import ctypes
     import time
     import numpy as np
     from ksim import abi, engine, gen, profile
+    from ksim.nativeenc import NativeEncoder, Pool
     from ksim.wrapped import HAS_NORMALIZE
     from oracle.oracle import Oracle, lib as olib
     rows = []
     for n_nodes, n_pods in ((100, 1000), (5000, 3000)):
-        cluster, pods = gen.config1(n_nodes=n_nodes, n_pods=n_pods)
+        nodes, pobjs = gen.config1_objects(n_nodes=n_nodes, n_pods=n_pods)
+        enc = NativeEncoder()
+        cluster, _ = enc.encode_cluster(nodes)
+        pods = enc.encode_pods(cluster, pobjs)      # every label column / class of the queue exists
         sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
         prof = profile.compile_profile(sp)
         snames = [p.name for p in sp.score_plugins()]
         nslots = [k for k, nm in enumerate(snames) if nm in HAS_NORMALIZE]
         N = cluster.n_nodes
         K = profile.num_feasible_nodes_to_find(N, 0)
-        ps = pods.pod_set()
+        ps_all = pods.pod_set()
+        # one flat pool per pod (the Go host's marshalling of its v1 pod)
+        t0 = time.perf_counter()
+        pools = []
+        for p in pobjs:
+            pl = Pool()
+            pl.pod(p)
+            pl.build()
+            pools.append(pl)
+        pool_us = (time.perf_counter() - t0) / n_pods * 1e6
+        opts = abi.EncodePodsOpts()
+        opts.added_required_first = -1
+        EL = engine.lib()
 
         def run(kind, count):
             if kind == "engine":
@@ -382,38 +403,48 @@ def bench_fw(args, out):
                 e.set_profile(prof)
                 e.set_cluster(cluster.copy_state())
                 L, h = e.L, e.h
-                pre = lambda i, out: L.ksim_fw_prefilter(h, ctypes.byref(ps), i, ctypes.byref(out))
+                pset = abi.PodSet()
+
+                def encode(i):
+                    rc = EL.ksim_encode_pods(enc.h, ctypes.byref(pools[i].c), ctypes.byref(opts))
+                    return rc or EL.ksim_encoder_pods(enc.h, ctypes.byref(pset))
+                pre = lambda i, out: L.ksim_fw_prefilter(h, ctypes.byref(pset), 0, ctypes.byref(out))
                 score = lambda arr, out: L.ksim_fw_score(h, arr.ctypes.data_as(ctypes.c_void_p), arr.size,
                                                          ctypes.byref(out))
                 norm = lambda k, arr, sc, o: L.ksim_fw_normalize(h, k, arr.ctypes.data_as(ctypes.c_void_p),
                                                                  sc.ctypes.data_as(ctypes.c_void_p), arr.size,
                                                                  o.ctypes.data_as(ctypes.c_void_p))
-                assume = lambda i, node: L.ksim_assume(h, ctypes.byref(ps), i, node)
+                assume = lambda i, node: L.ksim_assume(h, ctypes.byref(pset), 0, node)
             else:
                 e = Oracle(cluster.copy_state(), prof)
                 O, h = olib(), e.h
-                pre = lambda i, out: O.ksim_oracle_fw_filter(h, ctypes.byref(ps), i, ctypes.byref(out))
-                score = lambda arr, out: O.ksim_oracle_fw_score(h, ctypes.byref(ps), cur[0],
+                encode = lambda i: 0
+                pre = lambda i, out: O.ksim_oracle_fw_filter(h, ctypes.byref(ps_all), i, ctypes.byref(out))
+                score = lambda arr, out: O.ksim_oracle_fw_score(h, ctypes.byref(ps_all), cur[0],
                                                                arr.ctypes.data_as(ctypes.c_void_p), arr.size,
                                                                ctypes.byref(out))
                 norm = lambda k, arr, sc, o: O.ksim_oracle_fw_normalize(h, k, arr.ctypes.data_as(ctypes.c_void_p),
                                                                         sc.ctypes.data_as(ctypes.c_void_p),
                                                                         arr.size, o.ctypes.data_as(ctypes.c_void_p))
-                assume = lambda i, node: O.ksim_oracle_assume(h, ctypes.byref(ps), i, node, 1)
+                assume = lambda i, node: O.ksim_oracle_assume(h, ctypes.byref(ps_all), i, node, 1)
             cur = [0]
             fb, sb = abi.EvalBuffers(N, prof.n_score), abi.EvalBuffers(N, prof.n_score)
             nout = np.zeros(N, np.int64)
             ns, in_calls, bound = 0, 0.0, 0
-            split = {"prefilter": 0.0, "score": 0.0, "normalize": 0.0, "assume": 0.0}
+            split = {"encode": 0.0, "prefilter": 0.0, "score": 0.0, "normalize": 0.0, "assume": 0.0}
             t0 = time.perf_counter()
             for i in range(count):
                 cur[0] = i
                 c0 = time.perf_counter()
-                rc = pre(i, fb.out)
-                split["prefilter"] += time.perf_counter() - c0
-                in_calls += time.perf_counter() - c0
+                rc = encode(i)
+                c1 = time.perf_counter()
+                rc = rc or pre(i, fb.out)
+                c2 = time.perf_counter()
+                split["encode"] += c1 - c0
+                split["prefilter"] += c2 - c1
+                in_calls += c2 - c0
                 if rc != 0:
-                    raise RuntimeError(f"{kind} fw_prefilter rc {rc}")
+                    raise RuntimeError(f"{kind} encode / fw_prefilter rc {rc}")
                 order = np.roll(np.arange(N, dtype=np.int32), -ns)
                 feas = order[fb.fail_plugin[order] == abi.PASSED]
                 lst = np.ascontiguousarray(feas[:K])
@@ -447,16 +478,16 @@ def bench_fw(args, out):
         run("engine", min(200, n_pods))                      # warm-up (graphs, first launches)
         e_r = run("engine", n_pods)
         o_r = run("oracle", min(n_pods, 1000 if n_nodes <= 100 else 300))
-        rows.append({"nodes": n_nodes, "engine": e_r, "oracle_cpu_1thread": o_r,
+        rows.append({"nodes": n_nodes, "engine": e_r, "oracle_cpu_1thread": o_r, "pool_build_us": pool_us,
                      "engine_vs_oracle_in_calls": o_r["us_in_calls"] / e_r["us_in_calls"]})
     line = {"metric": "framework_driven_cycle_us", "value": rows[-1]["engine"]["us_per_cycle"],
             "unit": "us per pod cycle (5000 nodes)", "higher_is_better": False, "n_gpus": 1,
             "config": {"workload": "config-1 distribution, framework-driven compat cycle (drop-in)",
                        "parallelism": "single GPU"},
             "rows": rows,
-            "note": "per cycle: fw_prefilter + fw_score + fw_normalize per NormalizeScore plugin + assume, "
-                    "with the F x N / S x N copies back to host memory; Python ctypes glue included in "
-                    "us_per_cycle"}
+            "note": "per cycle: ksim_encode_pods (native) + fw_prefilter + fw_score + fw_normalize per "
+                    "NormalizeScore plugin + assume, with the copies back to host memory; Python ctypes glue "
+                    "included in us_per_cycle; the oracle's calls take pre-compiled pods"}
     out.write(json.dumps(line) + "\n")
     out.flush()
 

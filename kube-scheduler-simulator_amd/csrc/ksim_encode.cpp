@@ -1342,10 +1342,13 @@ uint8_t effect_id(const string& e) {
   return KSIM_EFFECT_NONE;
 }
 
-void materialize_classes(ksim_encoder* e) {
+// class_count [C][N] from the classes' rows.  A queue compile only appends
+// classes (a pending pod's adds never change a count), so only the new rows
+// are copied (from = the classes materialized before).
+void materialize_classes(ksim_encoder* e, size_t from = 0) {
   Cluster& c = e->c;
   c.class_count.resize((size_t)e->topo.classes.size() * c.n);
-  for (size_t k = 0; k < e->topo.classes.size(); k++)
+  for (size_t k = from; k < e->topo.classes.size(); k++)
     std::copy(e->topo.classes[k].counts.begin(), e->topo.classes[k].counts.end(),
               c.class_count.begin() + k * (size_t)c.n);
 }
@@ -1949,6 +1952,7 @@ void encode_pods(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_p
   for (int64_t i = 0; i < pool.n_pods; i++) {
     pods.push_back(read_pod(rd, pool.pods[i], t, e->req_memo, e->qs, false));
   }
+  const size_t classes_before = t.classes.size();
   for (const auto& p : pods) register_pod_classes(t, p, sd);   // pass 1
   vector<Taint> unsched_vocab{Taint{}, Taint{kTaintUnschedulable, "", "NoSchedule"}};
   e->pods.resize(pods.size());
@@ -2079,7 +2083,7 @@ void encode_pods(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_p
       }
     }
   }
-  materialize_classes(e);
+  materialize_classes(e, classes_before);
 }
 
 template <class F>

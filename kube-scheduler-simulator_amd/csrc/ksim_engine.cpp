@@ -193,6 +193,18 @@ struct ksim_handle {
   // list with the raw scores it returned is answered from here
   std::vector<int32_t> fw_list;
   std::vector<int64_t> fw_raw, fw_norm;         // [slot][list position]
+  // host-answered Score (fw_host): ksim_fw_prefilter also copies every node's
+  // raw scores, the weighted sum of the plugins without NormalizeScore and the
+  // topology flags into pinned memory, and ksim_fw_score normalizes over the
+  // framework's list on the host (no second device round trip) when no
+  // PreScore of the pod depends on that list
+  bool fw_host = false;
+  std::vector<uint8_t> fw_seen;    // list validation (all zero between calls)
+  std::vector<int64_t> fw_tot;
+  void* fwh = nullptr;             // pinned: [S][n] raw, [n] part
+  void* fwh_d = nullptr;
+  size_t fwh_cap = 0;
+  uint32_t fw_tflags = 0;
   int32_t* fw_nodes = nullptr;     // device [n]
   int64_t* fw_vals = nullptr;      // device [n]
   int64_t* fw_out = nullptr;       // device [n]
@@ -653,6 +665,7 @@ int fw_abandon(ksim_handle* h) {
 
 }  // namespace
 static int flush_deferred_binds(ksim_handle* h);
+static int flush_idle(ksim_handle* h);
 namespace {
 
 int ensure_ready(ksim_handle* h, bool fw = false) {
@@ -1732,6 +1745,7 @@ void ksim_destroy(ksim_handle* h) {
   if (h->pod1_arena.p) (void)hipFree(h->pod1_arena.p);
   if (h->nom_arena.p) (void)hipFree(h->nom_arena.p);
   if (h->asm_arena.p) (void)hipFree(h->asm_arena.p);
+  if (h->fwh) (void)hipHostFree(h->fwh);
   if (h->pin) (void)hipHostFree(h->pin);
   if (h->pout) (void)hipHostFree(h->pout);
   free_bufs(h->pre_bufs);
@@ -2300,6 +2314,7 @@ int ksim_remove_node(ksim_handle* h, int32_t pos) {
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
                         int64_t* nz_mem, int32_t* num_pods) {
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
+  if (int rc = flush_idle(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   const size_t N = (size_t)h->dc.n;
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2314,6 +2329,7 @@ int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int6
 
 int ksim_get_nb_alloc(ksim_handle* h, int64_t* out) {
   if (!h || !h->has_cluster || !out) return set_err(h, KSIM_E_INVALID, "cluster not set / null out");
+  if (int rc = flush_idle(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hcopy(h, out, h->dc.nb_alloc, 8 * (size_t)h->dc.n, hipMemcpyDeviceToHost));
@@ -2322,6 +2338,7 @@ int ksim_get_nb_alloc(ksim_handle* h, int64_t* out) {
 
 int ksim_get_class_count(ksim_handle* h, int32_t* out) {
   if (!h || !h->has_cluster || !out) return set_err(h, KSIM_E_INVALID, "cluster not set / null out");
+  if (int rc = flush_idle(h)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (h->dc.n_classes)
@@ -2676,16 +2693,43 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   h->fw_topo = p.use_count > 0;
   const size_t N = (size_t)h->dc.n;
   h->fw_fail.resize(N);
+  // Score on the host (ksim_fw_score) unless a PreScore reads the framework's
+  // list: PodTopologySpread's ScheduleAnyway constraints (IgnoredNodes, pair
+  // counts over the list); NetworkBandwidth's Score may fail the cycle
+  const int S = h->prof.n_score;
+  bool host = S > 0 && !profile_nb(h->prof) && !(p.flags & KSIM_POD_NODE_NAMES_UNKNOWN);
+  for (int32_t u = 0; host && u < p.use_count; u++)
+    if (ps->uses[p.use_first + u].kind == KSIM_USE_PTS_SOFT) host = false;
+  h->fw_host = host;
+  if (host) {
+    const size_t need = ((8 * (size_t)S * N + 63) & ~(size_t)63) + 8 * N;
+    if (need > h->fwh_cap) {
+      HIPCHK(h, hipStreamSynchronize(h->stream));
+      if (h->fwh) (void)hipHostFree(h->fwh);
+      h->fwh = h->fwh_d = nullptr;
+      h->fwh_cap = 0;
+      hipError_t e = hipHostMalloc(&h->fwh, need, hipHostMallocCoherent | hipHostMallocMapped);
+      if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (fw scores)");
+      if ((e = hipHostGetDevicePointer(&h->fwh_d, h->fwh, 0)) != hipSuccess)
+        return hip_fail(h, e, "hipHostGetDevicePointer");
+      h->fwh_cap = need;
+    }
+  }
   // the results into pinned staging, one synchronization: next_start, the
-  // filter codes, the details
+  // topology flags, the filter codes, the details (and the raw scores)
   const size_t o_fail = 64, o_det = 64 + ((N + 63) & ~(size_t)63);
   if ((rc = pout_reserve(h, o_det + 4 * N))) return rc;
   char* po = (char*)h->pout;
   char* pd = (char*)h->pout_d;
   Copies cp;
   cp.add(&h->st->next_start, pd, sizeof(int32_t));
+  cp.add(&h->st->topo_flags, pd + 4, sizeof(uint32_t));
   cp.add(h->sc.fail, pd + o_fail, N);
   if (out->fail_detail) cp.add(h->sc.detail, pd + o_det, 4 * N);
+  if (host) {
+    cp.add(h->sc.raw, h->fwh_d, 8 * (size_t)S * N);
+    cp.add(h->sc.part, (char*)h->fwh_d + ((8 * (size_t)S * N + 63) & ~(size_t)63), 8 * N);
+  }
   if ((rc = cp.run(h))) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   std::memcpy(h->fw_fail.data(), po + o_fail, N);
@@ -2700,6 +2744,7 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   }
   int32_t next = 0;
   std::memcpy(&next, po, sizeof(next));
+  std::memcpy(&h->fw_tflags, po + 4, sizeof(uint32_t));
   const bool unknown = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) != 0;
   out->chosen = unknown ? KSIM_CHOSEN_ERROR : -1;
   out->status = unknown ? KSIM_STATUS_ERROR : 0;
@@ -2775,11 +2820,121 @@ int ksim_fw_filter_nominated(ksim_handle* h, const ksim_pod_set* nps, int32_t n_
   return KSIM_OK;
 }
 
+// NormalizeScore of one value on the host (ksim_device.h normalize_value, the
+// same integer and float64 expressions; -ffp-contract=off holds for this file)
+static int64_t host_normalize(int32_t kind, int64_t v, int64_t gmax, int64_t gmin, bool ipa_nonempty) {
+  switch (kind) {
+    case kNormDefault: {
+      const int64_t m = gmax > 0 ? gmax : 0;
+      return m == 0 ? v : (int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v) / m;
+    }
+    case kNormDefaultReverse: {
+      const int64_t m = gmax > 0 ? gmax : 0;
+      return m == 0 ? (int64_t)kMaxNodeScore : (int64_t)kMaxNodeScore - (int64_t)((uint64_t)kMaxNodeScore * (uint64_t)v) / m;
+    }
+    case kNormPTS: {
+      const int64_t mx = gmax > 0 ? gmax : 0;
+      return mx == 0 ? (int64_t)kMaxNodeScore : (int64_t)((uint64_t)kMaxNodeScore * (uint64_t)(mx + gmin - v)) / mx;
+    }
+    case kNormIPA:
+    case kNormMinMax: {
+      if (kind == kNormIPA && !ipa_nonempty) return v;
+      const int64_t diff = gmax - gmin;
+      double f = 0;
+      if (diff > 0) f = (double)kMaxNodeScore * ((double)(v - gmin) / (double)diff);
+      return (int64_t)f;
+    }
+    default:
+      return v;
+  }
+}
+
+// ksim_fw_score answered on the host (fw_host): PreScore / Score were the
+// filter pass's (no list-dependent PreScore), NormalizeScore, the weights and
+// the totals over the framework's list, as k_window / k_extrema / k_select
+// compute them (k_select: one listed node is not scored).
+static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out* out) {
+  const size_t N = (size_t)h->dc.n;
+  const int S = h->prof.n_score;
+  std::vector<uint8_t>& seen = h->fw_seen;
+  if (seen.size() != N) seen.assign(N, 0);
+  for (int32_t j = 0; j < n; j++) {
+    const int32_t x = nodes[j];
+    if (x < 0 || (size_t)x >= N || h->fw_fail[x] != KSIM_PASSED || seen[x]) {
+      for (int32_t q = 0; q < j; q++) seen[nodes[q]] = 0;
+      return set_err(h, KSIM_E_INVALID, "node list: not a feasible node of the filter pass, or repeated");
+    }
+    seen[x] = 1;
+  }
+  for (int32_t j = 0; j < n; j++) seen[nodes[j]] = 0;
+  const int64_t* raw = (const int64_t*)h->fwh;
+  const int64_t* part = (const int64_t*)((const char*)h->fwh + ((8 * (size_t)S * N + 63) & ~(size_t)63));
+  const bool scored = n > 1;
+  const bool ipa_nonempty = (h->fw_tflags & kTopoScoreNonEmpty) != 0;
+  h->fw_list.assign(nodes, nodes + n);
+  h->fw_raw.assign((size_t)S * n, 0);
+  h->fw_norm.assign((size_t)S * n, 0);
+  std::vector<int64_t>& tot = h->fw_tot;
+  tot.assign(n, 0);
+  if (scored) {
+    for (int32_t j = 0; j < n; j++) tot[j] = part[nodes[j]];
+    for (int k = 0; k < S; k++) {
+      int64_t* r = h->fw_raw.data() + (size_t)k * n;
+      int64_t* nv = h->fw_norm.data() + (size_t)k * n;
+      const int64_t* src = raw + (size_t)k * N;
+      for (int32_t j = 0; j < n; j++) r[j] = src[nodes[j]];
+      const int32_t kind = norm_kind(h->prof.score[k]);
+      if (kind == kNormNone) {
+        std::memcpy(nv, r, 8 * (size_t)n);
+        continue;
+      }
+      int64_t gmax = INT64_MIN, gmin = INT64_MAX;
+      for (int32_t j = 0; j < n; j++) {
+        gmax = std::max(gmax, r[j]);
+        gmin = std::min(gmin, r[j]);
+      }
+      const int64_t w = h->prof.score_weight[k] == 0 ? 1 : h->prof.score_weight[k];
+      for (int32_t j = 0; j < n; j++) {
+        nv[j] = host_normalize(kind, r[j], gmax, gmin, ipa_nonempty);
+        tot[j] += nv[j] * w;
+      }
+    }
+  }
+  if (out->scored)
+    for (int32_t j = 0; j < n; j++) out->scored[nodes[j]] = scored ? 1 : 0;
+  for (int k = 0; k < S; k++) {
+    if (out->raw) {
+      int64_t* r = out->raw + (size_t)k * N;
+      for (int32_t j = 0; j < n; j++) r[nodes[j]] = h->fw_raw[(size_t)k * n + j];
+    }
+    if (out->norm) {
+      int64_t* r = out->norm + (size_t)k * N;
+      for (int32_t j = 0; j < n; j++) r[nodes[j]] = h->fw_norm[(size_t)k * n + j];
+    }
+  }
+  if (out->total)
+    for (int32_t j = 0; j < n; j++) out->total[nodes[j]] = tot[j];
+  if (out->fail_plugin) {                  // the filter pass, unchanged
+    std::memcpy(out->fail_plugin, h->fw_fail.data(), N);
+    strip_fail_errors(out->fail_plugin, N);
+  }
+  out->n_feasible = n;
+  out->n_evaluated = h->fw_ns;
+  out->n_processed = 0;
+  out->k_to_find = num_feasible_nodes_to_find(h->prof.percentage_of_nodes_to_score, h->fw_ns);
+  out->chosen = -1;
+  out->status = 0;
+  h->fw_pending = false;                   // the domain sums stay for fw_abandon (no k_select ran)
+  h->fw_scored = true;
+  return KSIM_OK;
+}
+
 int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out* out) {
   int rc = ensure_ready(h, true);
   if (rc) return rc;
   if (!out || n < 0 || (n > 0 && !nodes)) return set_err(h, KSIM_E_INVALID, "bad node list");
   if (!h->fw_pending) return set_err(h, KSIM_E_INVALID, "ksim_fw_score without ksim_fw_prefilter");
+  if (h->fw_host) return fw_score_host(h, nodes, n, out);
   const size_t N = (size_t)h->dc.n;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));    // the upload staging is free again
@@ -2909,11 +3064,14 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
   return KSIM_OK;
 }
 
-// Reserve / Unreserve (wrappedplugin.go:583-584, 617).  They never abandon a
-// framework cycle in flight and never touch its pod upload (their own arena):
-// between that cycle's PreFilter and Score they are queued and applied once it
-// has scored (ensure_ready), as upstream's cycle keeps the snapshot it started
-// from while the cache takes the binding goroutine's ForgetPod.
+// Reserve / Unreserve (wrappedplugin.go:583-584, 617), uploaded through their
+// own arena (never the cycle's pod).  Unreserve never abandons a framework
+// cycle in flight: between that cycle's PreFilter and Score it is queued and
+// applied once the cycle has scored (ensure_ready), as upstream's cycle keeps
+// the snapshot it started from while the cache takes the binding goroutine's
+// ForgetPod.  Reserve is the end of a cycle (after Score, or with one
+// feasible node, which the framework does not score): it closes the cycle,
+// applies what was queued, then assumes.
 static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
   DevPods P;
   int rc;
@@ -2923,6 +3081,12 @@ static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   // no synchronization: every later call is ordered after it on the stream,
   // and the next upload waits for the staging (upload_single)
   return KSIM_OK;
+}
+
+// the queued Unreserves, when no framework cycle sits between PreFilter and
+// Score (the state getters read the cache's view)
+static int flush_idle(ksim_handle* h) {
+  return (!h->fw_pending && !h->deferred_binds.empty()) ? flush_deferred_binds(h) : KSIM_OK;
 }
 
 static int flush_deferred_binds(ksim_handle* h) {
@@ -2950,12 +3114,12 @@ static int flush_deferred_binds(ksim_handle* h) {
 }
 
 static int assume_common(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
-  int rc = ensure_ready(h, true);
+  int rc = ensure_ready(h, sign < 0);
   if (rc) return rc;
   if (!ps || !ps->pods || pod_index < 0 || pod_index >= ps->n_pods || node < 0 || node >= h->dc.n)
     return set_err(h, KSIM_E_INVALID, "bad pod / node");
   if ((rc = validate_pod(h, ps, pod_index))) return rc;
-  if (h->fw_pending) {                     // a cycle between PreFilter and Score: queued
+  if (h->fw_pending) {                     // Unreserve, a cycle between PreFilter and Score: queued
     ksim_handle::DeferredBind d;
     single_pod_set(ps, pod_index, d.pod, d.ex, d.tm, d.us, d.ad, d.nn);
     d.node = node;

@@ -164,7 +164,7 @@ void launch_cycle_finish(const LaunchArgs& a, hipStream_t stream);
 // 1 for unlisted nodes), no bind; NormalizeScore of one slot over an explicit list.
 void launch_fw_filter(const LaunchArgs& a, hipStream_t stream, bool topo);
 void launch_fw_score(const LaunchArgs& a, hipStream_t stream);
-constexpr int kCopyPieces = 4;
+constexpr int kCopyPieces = 8;
 struct CopyList {
   const uint8_t* src[kCopyPieces];
   uint8_t* dst[kCopyPieces];

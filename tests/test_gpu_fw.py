@@ -35,6 +35,14 @@ def _cases(kind):
         nodes, bound, incoming = gen.config3_objects(n_nodes=400, pods_per_node=4, n_incoming=200)
         cluster, _ = encode_cluster(nodes, bound)
         return cluster, encode_pods(cluster, incoming), None, None
+    if kind == "ipa":
+        # InterPodAffinity only (no spread constraints): ksim_fw_score is
+        # answered on the host from the filter pass's raw scores
+        nodes, bound, incoming = gen.config3_objects(n_nodes=400, pods_per_node=4, n_incoming=200)
+        for p in incoming:
+            p.topology_spread = []
+        cluster, _ = encode_cluster(nodes, bound)
+        return cluster, encode_pods(cluster, incoming), None, None
     if kind == "preempt":
         # crowded config-1 nodes with bound pods of mixed priorities: many
         # cycles find no node and run DefaultPreemption's PostFilter
@@ -70,7 +78,7 @@ def _cases(kind):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["config1", "prefilter", "config3", "preempt", "replicaset"])
+@pytest.mark.parametrize("kind", ["config1", "prefilter", "config3", "ipa", "preempt", "replicaset"])
 @pytest.mark.parametrize("seed", [1, 2])
 def test_framework_driven_cycles(kind, seed):
     cluster, pods, table, prio = _cases(kind)

@@ -690,8 +690,10 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
  * ticks: [3] chain prologue, [4] chain loop, [5] chain epilogue, [6] chain
  * launches); out[19] hipGraphs captured since ksim_create (a weight sweep that
  * keeps its graphs across ksim_set_profile captures none); out[20] device
- * time of the last ksim_match_terms in ns (HIP events).  Returns the number
- * of values written (<= n). */
+ * time of the last ksim_match_terms in ns (HIP events); out[21..24] framework-
+ * driven calls since ksim_create: ksim_fw_score answered on the host / on the
+ * device, ksim_fw_normalize answered from ksim_fw_score's list / on the device.
+ * Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),
  * out[1] candidate keys kept per pod (T), out[2] nodes per wave tile,

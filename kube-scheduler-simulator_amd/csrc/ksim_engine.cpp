@@ -199,6 +199,7 @@ struct ksim_handle {
   // framework's list on the host (no second device round trip) when no
   // PreScore of the pod depends on that list
   bool fw_host = false;
+  int64_t fw_counts[4] = {0, 0, 0, 0};   // Score on the host / device, NormalizeScore cached / device
   std::vector<uint8_t> fw_seen;    // list validation (all zero between calls)
   std::vector<int64_t> fw_tot;
   void* fwh = nullptr;             // pinned: [S][n] raw, [n] part
@@ -497,9 +498,9 @@ bool stab_signature(const ksim_pod_set* ps, const ksim_pod& q, std::string& s) {
   return true;
 }
 
-// KSIM_NO_STAB=1: no table (the keys evaluate the static plugins per node; A/B runs).
+// The "ab" flavor: no table (the keys evaluate the static plugins per node).
 bool stab_enabled() {
-  static const bool off = getenv("KSIM_NO_STAB") != nullptr;
+  constexpr bool off = kAbForms;
   return !off;
 }
 
@@ -617,9 +618,9 @@ int pod_batchable(const ksim_handle* h, const ksim_pod& p, bool* norm_varies = n
 // class 2 needs the unsharded P100 path over the whole node table.
 // Class 2 under ADAPT: pods whose normalized scores vary (k_adapt_top's
 // maxima over the window's kept nodes), without scalar requests, on an
-// unsharded handle (KSIM_NO_ADAPT_NORM=1: the per-pod path, A/B).
+// unsharded handle (the "ab" flavor: the per-pod path).
 bool pod_on_batch(const ksim_handle* h, int32_t i) {
-  static const bool adapt_norm = getenv("KSIM_NO_ADAPT_NORM") == nullptr;
+  constexpr bool adapt_norm = !kAbForms;
   const uint8_t b = h->batchable[i];
   if (b != 2 && b != 3) return b != 0;
   if (h->replicated) return b == 3 && !adapt_mode(h);   // class 3: replicated topology batches (shard_run_tbatch)
@@ -634,9 +635,9 @@ bool pod_on_batch(const ksim_handle* h, int32_t i) {
 // hard spread keys of <= kFuseMinValues values) with every domain sum read
 // from a persistent table, no port / volume / bandwidth inputs and no
 // PreFilterResult node list, totals inside the batch key's 20 bits, and a
-// cluster of at most kTbMaxBlocks node blocks.  KSIM_NO_TBATCH=1: per-pod path (A/B).
+// cluster of at most kTbMaxBlocks node blocks.  The "ab" flavor: per-pod path.
 bool tbatch_admit(const ksim_handle* h, const ksim_pod& p, const PodPlan& pl, bool hard_small, bool soft_le1) {
-  static const bool off = getenv("KSIM_NO_TBATCH") != nullptr;
+  constexpr bool off = kAbForms;
   if (off || p.use_count <= 0) return false;
   if (h->dc.n > kTbMaxBlocks * 256) return false;
   if (p.flags & KSIM_POD_NODE_NAMES) return false;
@@ -790,9 +791,9 @@ int run_tbatch(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
 }
 
 // ---- deferred-commit FAST batches (ksim_internal.h, ksim_batch.hip) ----------
-// KSIM_NO_LAZY=1: the three-launch batches (A/B runs, parity of both forms).
+// The "ab" flavor: the three-launch batches (parity of both forms).
 bool lazy_enabled() {
-  static const bool off = getenv("KSIM_NO_LAZY") != nullptr;
+  constexpr bool off = kAbForms;
   return !off;
 }
 
@@ -1157,7 +1158,7 @@ int shard_batch_lazy(const std::vector<ksim_handle*>& hs, hipStream_t stream, in
 
 hipGraphExec_t shard_lazy_graph(const std::vector<ksim_handle*>& hs) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  if (h0->sg_off || kAbForms) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {
@@ -1409,7 +1410,7 @@ int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t st
 // capture is off or fails (the caller runs the cycles eagerly).
 hipGraphExec_t shard_graph(const std::vector<ksim_handle*>& hs, bool topo, int64_t xdom, int64_t xreg) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  if (h0->sg_off || kAbForms) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {                     // another group, or some handle dropped its graphs
@@ -1447,7 +1448,7 @@ int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream, b
 
 hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast, bool adapt) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || getenv("KSIM_NO_SHARD_GRAPH")) return nullptr;
+  if (h0->sg_off || kAbForms) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {
@@ -2934,6 +2935,7 @@ int ksim_fw_score(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_eval_out
   if (rc) return rc;
   if (!out || n < 0 || (n > 0 && !nodes)) return set_err(h, KSIM_E_INVALID, "bad node list");
   if (!h->fw_pending) return set_err(h, KSIM_E_INVALID, "ksim_fw_score without ksim_fw_prefilter");
+  h->fw_counts[h->fw_host ? 0 : 1]++;
   if (h->fw_host) return fw_score_host(h, nodes, n, out);
   const size_t N = (size_t)h->dc.n;
   HIPCHK(h, hipSetDevice(h->device));
@@ -3036,10 +3038,12 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
     bool same = std::equal(nodes, nodes + n, h->fw_list.begin());
     for (int32_t j = 0; same && j < n; j++) same = scores[j] == raw[j];
     if (same) {
+      h->fw_counts[2]++;
       std::memcpy(out, h->fw_norm.data() + (size_t)score_slot * n, 8 * (size_t)n);
       return KSIM_OK;
     }
   }
+  h->fw_counts[3]++;
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));    // the staging is free again
   const size_t o_vals = (4 * (size_t)n + 63) & ~(size_t)63;
@@ -3164,7 +3168,7 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   R.pod.assign((size_t)ps->n_pods, 0);
   R.mask.assign((size_t)ps->n_pods, 0);
   // replicas (RCCL ones included) hold every node: their tables are whole
-  if ((is_sharded(h) && !h->replicated) || getenv("KSIM_NO_PTAB")) return;   // A/B switch: per-cycle PreFilter sums
+  if ((is_sharded(h) && !h->replicated) || kAbForms) return;   // A/B form: per-cycle PreFilter sums
   std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> index;
   for (int32_t i = 0; i < ps->n_pods; i++) {
     const ksim_pod& p = ps->pods[i];
@@ -3876,13 +3880,14 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  int64_t v[3 + 16 + 2] = {st.batches, st.truncations, st.cuts};
+  int64_t v[3 + 16 + 2 + 4] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   if (unsigned long long* cp = cp_clock_buffer())   // KSIM_CP_CLOCKS builds: the chain + pairs phase clocks
     HIPCHK(h, hcopy(h, v + 3, cp, 8 * 8, hipMemcpyDeviceToHost));
   v[19] = h->graph_captures;
   v[20] = h->match_ns;
-  const int32_t m = n < 21 ? n : 21;
+  for (int k = 0; k < 4; k++) v[21 + k] = h->fw_counts[k];
+  const int32_t m = n < 25 ? n : 25;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }

@@ -6,6 +6,18 @@
 
 namespace ksim {
 
+// A/B forms of the same runs, chosen at compile time (csrc/Makefile "ab":
+// libksim_engine_ab.so, every alternative form on; tests/test_gpu_ab_switches.py
+// runs it against the oracle).  The product library has none of them.
+#ifdef KSIM_AB_FORMS
+constexpr bool kAbForms = true;   // per-node static plugins (no static-class table), ADAPT normalized-score
+                                  // pods per pod, topology pods per pod, three-launch batches, eager
+                                  // shard cycles, per-cycle PreFilter domain sums
+#else
+constexpr bool kAbForms = false;
+#endif
+
+
 // Batch path geometry.
 // Compile-time overridable for A/B builds (-DKSIM_BATCH_PODS=512 -DKSIM_TOP_T=16).
 #ifndef KSIM_BATCH_PODS

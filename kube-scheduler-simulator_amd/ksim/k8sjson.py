@@ -111,7 +111,14 @@ def pod_to_dict(p: Pod) -> dict:
         md["labels"] = dict(p.labels)
     if p.annotations:
         md["annotations"] = dict(p.annotations)
+    if p.owner is not None:
+        api, kind, name = p.owner
+        md["ownerReferences"] = [{"apiVersion": api, "kind": kind, "name": name, "uid": f"uid-{kind}-{name}",
+                                  "controller": True}]
     spec: Dict[str, object] = {"containers": [_container(c, f"c{i}") for i, c in enumerate(p.containers)]}
+    if p.pvc_claims:
+        spec["volumes"] = [{"name": f"v{i}", "persistentVolumeClaim": {"claimName": c}}
+                           for i, c in enumerate(p.pvc_claims)]
     if p.init_containers:
         spec["initContainers"] = [_container(c, f"i{i}") for i, c in enumerate(p.init_containers)]
     if p.overhead:

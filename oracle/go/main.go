@@ -24,6 +24,22 @@
 //     math/rand reservoir;
 //   - the chosen node's NodeInfo.AddPod (assume).
 //
+// Round 5 cases (tools/make_go_fixtures.py "optional inputs"):
+//   - profile.pluginConfig: the v1beta2 args decoded over the defaults,
+//     defaulted and converted (NewPluginConfig, plugins.go:103-179);
+//   - services / replicaSets / statefulSets / replicationControllers and pvs /
+//     pvcs: created in the fake clientset before the informers sync (the
+//     listers PodTopologySpread's DefaultSelector and VolumeBinding read);
+//   - nominatedPods / cycleInputs: the PodNominator of each cycle:
+//     RunFilterPluginsWithNominatedPods (pass 1 on a clone carrying the node's
+//     nominated pods of priority >= the pod's, PreFilterExtensions.AddPod, then
+//     pass 2) and evaluateNominatedNode (schedule_one.go v1.26);
+//   - preemption: after an unschedulable cycle, DefaultPreemption's dry run
+//     with the candidate search from offset 0 (the deterministic stand-in for
+//     GetOffsetAndNumCandidates' random offset): potential nodes are those whose
+//     status is Unschedulable, SelectVictimsOnNode per node, the first
+//     numCandidates candidates, pickOneNodeForPreemption restated below.
+//
 //	cd oracle/go && go run . ../../tests/golden/go/*.json.gz
 package main
 
@@ -32,9 +48,13 @@ import (
 	"context"
 	"encoding/json"
 	"fmt"
+	"math"
 	"os"
+	"sort"
 	"strings"
+	"time"
 
+	appsv1 "k8s.io/api/apps/v1"
 	v1 "k8s.io/api/core/v1"
 	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/runtime"
@@ -45,7 +65,9 @@ import (
 	"k8s.io/kubernetes/pkg/scheduler/apis/config/scheme"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 	"k8s.io/kubernetes/pkg/scheduler/framework/plugins"
+	"k8s.io/kubernetes/pkg/scheduler/framework/plugins/defaultpreemption"
 	frameworkruntime "k8s.io/kubernetes/pkg/scheduler/framework/runtime"
+	corev1helpers "k8s.io/component-helpers/scheduling/corev1"
 )
 
 // The simulator's default profile (scheduler_test.go:388-437).
@@ -72,7 +94,25 @@ type fixture struct {
 	Nodes                 []v1.Node                    `json:"nodes"`
 	BoundPods             []v1.Pod                     `json:"boundPods"`
 	Pods                  []v1.Pod                     `json:"pods"`
+	// round 5 (optional)
+	Profile                *configv1beta2.KubeSchedulerProfile `json:"profile"`
+	Services               []v1.Service                        `json:"services"`
+	ReplicaSets            []appsv1.ReplicaSet                 `json:"replicaSets"`
+	StatefulSets           []appsv1.StatefulSet                `json:"statefulSets"`
+	ReplicationControllers []v1.ReplicationController          `json:"replicationControllers"`
+	PVs                    []v1.PersistentVolume               `json:"pvs"`
+	PVCs                   []v1.PersistentVolumeClaim          `json:"pvcs"`
+	NominatedPods          []v1.Pod                            `json:"nominatedPods"`
+	CycleInputs            []struct {
+		Nominator         map[string][]string `json:"nominator"`
+		NominatedNodeName *string             `json:"nominatedNodeName"`
+	} `json:"cycleInputs"`
+	Preemption bool `json:"preemption"`
 }
+
+// assumedStart: status.startTime of queue pod i once assumed (seconds after
+// 2022-01-01T00:00:00Z; tools/make_go_fixtures.py ASSUMED_START)
+const assumedStart = 20000
 
 // One cycle in the schema of tests/golden/go (tools/make_go_fixtures.py).
 type cycle struct {
@@ -84,6 +124,12 @@ type cycle struct {
 	Score      map[string]map[string]int64 `json:"score"`
 	Normalized map[string]map[string]int64 `json:"normalized"`
 	Total      map[string]int64            `json:"total"`
+	PostFilter *postFilter                 `json:"postFilter,omitempty"`
+}
+
+type postFilter struct {
+	NominatedNode *string  `json:"nominatedNode"`
+	Victims       []string `json:"victims"`
 }
 
 // snapshot is the framework.SharedLister the plugins read: NodeInfos in
@@ -202,9 +248,13 @@ func tbLo(seed uint64, seq int64, node int) uint64 {
 }
 
 // defaultArgs: the v1beta2 defaults the simulator starts from
-// (NewPluginConfig, plugins.go:103-179), converted to the internal types.
-func defaultArgs(hardW int32) (map[string]runtime.Object, error) {
+// (NewPluginConfig, plugins.go:103-179), with the fixture profile's
+// pluginConfig decoded over them, converted to the internal types.
+func defaultArgs(hardW int32, prof *configv1beta2.KubeSchedulerProfile) (map[string]runtime.Object, error) {
 	versioned := &configv1beta2.KubeSchedulerConfiguration{}
+	if prof != nil {
+		versioned.Profiles = []configv1beta2.KubeSchedulerProfile{*prof.DeepCopy()}
+	}
 	scheme.Scheme.Default(versioned)
 	var internal config.KubeSchedulerConfiguration
 	if err := scheme.Scheme.Convert(versioned, &internal, nil); err != nil {
@@ -214,7 +264,7 @@ func defaultArgs(hardW int32) (map[string]runtime.Object, error) {
 	for _, pc := range internal.Profiles[0].PluginConfig {
 		args[pc.Name] = pc.Args
 	}
-	if a, ok := args["InterPodAffinity"].(*config.InterPodAffinityArgs); ok && hardW > 0 {
+	if a, ok := args["InterPodAffinity"].(*config.InterPodAffinityArgs); ok && hardW > 0 && prof == nil {
 		a.HardPodAffinityWeight = hardW
 	}
 	return args, nil
@@ -232,9 +282,43 @@ func run(f *fixture) ([]cycle, error) {
 			return nil, err
 		}
 	}
+	for i := range f.Services {
+		if _, err := client.CoreV1().Services(f.Services[i].Namespace).Create(ctx, &f.Services[i], metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
+	for i := range f.ReplicationControllers {
+		rc := &f.ReplicationControllers[i]
+		if _, err := client.CoreV1().ReplicationControllers(rc.Namespace).Create(ctx, rc, metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
+	for i := range f.ReplicaSets {
+		rs := &f.ReplicaSets[i]
+		if _, err := client.AppsV1().ReplicaSets(rs.Namespace).Create(ctx, rs, metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
+	for i := range f.StatefulSets {
+		ss := &f.StatefulSets[i]
+		if _, err := client.AppsV1().StatefulSets(ss.Namespace).Create(ctx, ss, metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
+	for i := range f.PVs {
+		if _, err := client.CoreV1().PersistentVolumes().Create(ctx, &f.PVs[i], metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
+	for i := range f.PVCs {
+		c := &f.PVCs[i]
+		if _, err := client.CoreV1().PersistentVolumeClaims(c.Namespace).Create(ctx, c, metav1.CreateOptions{}); err != nil {
+			return nil, err
+		}
+	}
 	informerFactory := informers.NewSharedInformerFactory(client, 0)
 	snap := newSnapshot(f)
-	args, err := defaultArgs(f.HardPodAffinityWeight)
+	args, err := defaultArgs(f.HardPodAffinityWeight, f.Profile)
 	if err != nil {
 		return nil, err
 	}
@@ -252,6 +336,9 @@ func run(f *fixture) ([]cycle, error) {
 	// (plugins.go:76: r(configuration, f)), with the framework as their Handle
 	pl := map[string]framework.Plugin{}
 	names := append(append(append([]string{}, filterOrder...), scoreOrder...), preFilterOrder...)
+	if f.Preemption {
+		names = append(names, "DefaultPreemption")
+	}
 	for _, name := range names {
 		if pl[name] != nil {
 			continue
@@ -268,6 +355,58 @@ func run(f *fixture) ([]cycle, error) {
 	index := map[string]int{}
 	for i, ni := range snap.list {
 		index[ni.Node().Name] = i
+	}
+	nominatedByName := map[string]*v1.Pod{}
+	for i := range f.NominatedPods {
+		nominatedByName[f.NominatedPods[i].Name] = &f.NominatedPods[i]
+	}
+	// RunFilterPlugins: the first failing plugin (name, status) or nil
+	runFilters := func(state *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) (string, *framework.Status) {
+		for _, name := range filterOrder {
+			if st := pl[name].(framework.FilterPlugin).Filter(ctx, state, pod, ni); !st.IsSuccess() {
+				return name, st
+			}
+		}
+		return "", nil
+	}
+	// RunFilterPluginsWithNominatedPods (framework/runtime/framework.go v1.26)
+	filterWithNominated := func(seq int, state *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) (string, *framework.Status) {
+		var add []*v1.Pod
+		if seq < len(f.CycleInputs) {
+			for _, n := range f.CycleInputs[seq].Nominator[ni.Node().Name] {
+				q := nominatedByName[n]
+				if q != nil && corev1helpers.PodPriority(q) >= corev1helpers.PodPriority(pod) && q.UID != pod.UID &&
+					q.Name != pod.Name {
+					add = append(add, q)
+				}
+			}
+		}
+		if len(add) > 0 {
+			stateOut := state.Clone()
+			niOut := ni.Clone()
+			for _, q := range add {
+				pi := framework.NewPodInfo(q)
+				niOut.AddPodInfo(pi)
+				for _, name := range preFilterOrder {
+					if p, ok := pl[name].(framework.PreFilterPlugin); ok && p.PreFilterExtensions() != nil {
+						if st := p.PreFilterExtensions().AddPod(ctx, stateOut, pod, pi, niOut); !st.IsSuccess() {
+							return name, st
+						}
+					}
+				}
+			}
+			if name, st := runFilters(stateOut, pod, niOut); st != nil {
+				return name, st
+			}
+		}
+		return runFilters(state, pod, ni)
+	}
+	startOf := map[string]time.Time{}
+	base := time.Date(2022, 1, 1, 0, 0, 0, 0, time.UTC)
+	for i := range f.BoundPods {
+		if st := f.BoundPods[i].Status.StartTime; st != nil {
+			startOf[f.BoundPods[i].Name] = st.Time
+		}
 	}
 	nextStart := 0
 	var out []cycle
@@ -304,37 +443,57 @@ func run(f *fixture) ([]cycle, error) {
 		if N == 0 {
 			return nil, fmt.Errorf("pod %s: empty PreFilterResult (not modelled)", pod.Name)
 		}
-		K := int(numFeasibleNodesToFind(f.Pct, int32(N)))
-		// findNodesThatPassFilters, parallelism 1
+		statuses := map[string]*framework.Status{}
+		var chosen *framework.NodeInfo
 		var feasible []*framework.NodeInfo
-		failed := 0
-		for i := 0; i < N; i++ {
-			ni := scan[(nextStart+i)%N]
-			var rec interface{} = "passed"
-			for _, name := range filterOrder {
-				st := pl[name].(framework.FilterPlugin).Filter(ctx, state, pod, ni)
-				if !st.IsSuccess() {
+		failed := map[string]bool{}
+		nominatedPass := false
+		// evaluateNominatedNode (schedule_one.go v1.26): the pod's nominated node
+		// first; passing, it is the only feasible node and nextStartNodeIndex
+		// stays; failing, its status stays in the diagnosis
+		if seq < len(f.CycleInputs) && f.CycleInputs[seq].NominatedNodeName != nil {
+			if ni, ok := snap.byName[*f.CycleInputs[seq].NominatedNodeName]; ok {
+				name, st := filterWithNominated(seq, state, pod, ni)
+				if st == nil {
+					c.Filter[ni.Node().Name] = "passed"
+					feasible, nominatedPass = []*framework.NodeInfo{ni}, true
+				} else {
+					if st.Code() == framework.Error {
+						return nil, fmt.Errorf("pod %s: Filter %s: %s", pod.Name, name, st.Message())
+					}
+					c.Filter[ni.Node().Name] = []interface{}{name, st.Message()}
+					statuses[ni.Node().Name] = st
+					failed[ni.Node().Name] = true
+				}
+			}
+		}
+		if !nominatedPass {
+			K := int(numFeasibleNodesToFind(f.Pct, int32(N)))
+			// findNodesThatPassFilters, parallelism 1
+			for i := 0; i < N; i++ {
+				ni := scan[(nextStart+i)%N]
+				var rec interface{} = "passed"
+				if name, st := filterWithNominated(seq, state, pod, ni); st != nil {
 					if st.Code() == framework.Error {
 						return nil, fmt.Errorf("pod %s: Filter %s on %s: %s", pod.Name, name, ni.Node().Name, st.Message())
 					}
 					rec = []interface{}{name, st.Message()}
-					break
+					statuses[ni.Node().Name] = st
+				}
+				c.Filter[ni.Node().Name] = rec
+				if rec == "passed" {
+					if len(feasible) == K {
+						break // the (K+1)-th feasible node: recorded, not kept
+					}
+					feasible = append(feasible, ni)
+				} else {
+					failed[ni.Node().Name] = true
 				}
 			}
-			c.Filter[ni.Node().Name] = rec
-			if rec == "passed" {
-				if len(feasible) == K {
-					break // the (K+1)-th feasible node: recorded, not kept
-				}
-				feasible = append(feasible, ni)
-			} else {
-				failed++
-			}
+			nextStart = (nextStart + len(feasible) + len(failed)) % N
 		}
-		nextStart = (nextStart + len(feasible) + failed) % N
 		c.NextStart = nextStart
 		c.NFeasible = len(feasible)
-		var chosen *framework.NodeInfo
 		switch {
 		case len(feasible) == 0:
 		case len(feasible) == 1:
@@ -397,11 +556,129 @@ func run(f *fixture) ([]cycle, error) {
 			name := chosen.Node().Name
 			c.Chosen = &name
 			pod.Spec.NodeName = name
+			if f.Preemption {
+				st := metav1.NewTime(base.Add(time.Duration(assumedStart+seq) * time.Second))
+				pod.Status.StartTime = &st
+				startOf[pod.Name] = st.Time
+			}
 			chosen.AddPod(pod) // assume
+		} else if f.Preemption {
+			pf, err := preempt(ctx, pl["DefaultPreemption"].(*defaultpreemption.DefaultPreemption), state, pod,
+				snap, statuses, args, startOf)
+			if err != nil {
+				return nil, fmt.Errorf("pod %s: preemption: %w", pod.Name, err)
+			}
+			c.PostFilter = pf
 		}
 		out = append(out, c)
 	}
 	return out, nil
+}
+
+// preempt: DefaultPreemption's dry run (preemption.Evaluator.findCandidates +
+// SelectCandidate, v1.26) with the candidate search from offset 0.  Potential
+// nodes: status Unschedulable (nodesWherePreemptionMightHelp drops
+// UnschedulableAndUnresolvable), in nodeTree order; SelectVictimsOnNode is
+// the plugin's own; pickOneNodeForPreemption is restated (unexported upstream).
+func preempt(ctx context.Context, dp *defaultpreemption.DefaultPreemption, state *framework.CycleState, pod *v1.Pod,
+	snap *snapshot, statuses map[string]*framework.Status, args map[string]runtime.Object,
+	startOf map[string]time.Time) (*postFilter, error) {
+	var potential []*framework.NodeInfo
+	for _, ni := range snap.list {
+		if st, ok := statuses[ni.Node().Name]; ok && st.Code() == framework.Unschedulable {
+			potential = append(potential, ni)
+		}
+	}
+	pa := args["DefaultPreemption"].(*config.DefaultPreemptionArgs)
+	// GetOffsetAndNumCandidates (default_preemption.go v1.26)
+	want := len(potential) * int(pa.MinCandidateNodesPercentage) / 100
+	if want < int(pa.MinCandidateNodesAbsolute) {
+		want = int(pa.MinCandidateNodesAbsolute)
+	}
+	if want > len(potential) {
+		want = len(potential)
+	}
+	type cand struct {
+		node    string
+		victims []*v1.Pod
+	}
+	var cands []cand
+	for _, ni := range potential {
+		if len(cands) >= want {
+			break
+		}
+		victims, _, st := dp.SelectVictimsOnNode(ctx, state.Clone(), pod, ni.Clone(), nil)
+		if st.IsSuccess() {
+			cands = append(cands, cand{ni.Node().Name, victims})
+		}
+	}
+	none := &postFilter{Victims: []string{}}
+	if len(cands) == 0 {
+		return none, nil
+	}
+	// pickOneNodeForPreemption (preemption.go v1.26): lowest highest-victim
+	// priority, lowest sum of (priority + MaxInt32 + 1), fewest victims, latest
+	// earliest start time of the highest-priority victims, first candidate
+	start := func(p *v1.Pod) time.Time { return startOf[p.Name] }
+	best := 0
+	key := func(c cand) (int32, int64, int, time.Time) {
+		if len(c.victims) == 0 {
+			return math.MinInt32, 0, 0, time.Time{}
+		}
+		hi := corev1helpers.PodPriority(c.victims[0])
+		var sum int64
+		earliest := start(c.victims[0])
+		for _, v := range c.victims {
+			pr := corev1helpers.PodPriority(v)
+			if pr > hi {
+				hi = pr
+			}
+			sum += int64(pr) + int64(math.MaxInt32) + 1
+		}
+		for _, v := range c.victims {
+			if corev1helpers.PodPriority(v) == hi && start(v).Before(earliest) {
+				earliest = start(v)
+			}
+		}
+		return hi, sum, len(c.victims), earliest
+	}
+	for i := 1; i < len(cands); i++ {
+		h0, s0, n0, t0 := key(cands[best])
+		h1, s1, n1, t1 := key(cands[i])
+		switch {
+		case h1 != h0:
+			if h1 < h0 {
+				best = i
+			}
+		case s1 != s0:
+			if s1 < s0 {
+				best = i
+			}
+		case n1 != n0:
+			if n1 < n0 {
+				best = i
+			}
+		case !t1.Equal(t0):
+			if t1.After(t0) {
+				best = i
+			}
+		}
+	}
+	// the victims in MoreImportantPod order (SelectVictimsOnNode's result order)
+	vs := cands[best].victims
+	sort.SliceStable(vs, func(a, b int) bool {
+		pa, pb := corev1helpers.PodPriority(vs[a]), corev1helpers.PodPriority(vs[b])
+		if pa != pb {
+			return pa > pb
+		}
+		return start(vs[a]).Before(start(vs[b]))
+	})
+	names := make([]string, len(vs))
+	for i, v := range vs {
+		names[i] = v.Name
+	}
+	node := cands[best].node
+	return &postFilter{NominatedNode: &node, Victims: names}, nil
 }
 
 func main() {

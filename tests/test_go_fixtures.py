@@ -13,6 +13,14 @@ object-level restatement records for it.  Here, on the CPU:
    the fixture), its cycles must equal the recorded ones.  That is the pin
    against the reference's plugins; without the file the case is skipped and
    parity stays "unpinned vs Go".
+
+Round 5 added cases for what rounds 3-4 built (tests/gofixture.py reads them):
+plugin args (MostAllocated with an extended resource and ignoredResources,
+RequestedToCapacityRatio, addedAffinity), PodTopologySpread System / List
+default constraints on workload-owned pods, nominated pods, DefaultPreemption's
+dry run and bound-PV volume filters.  Cycles with a PodNominator or a PostFilter
+replay on objref here; the C oracle's nominated / preemption calls are held to
+objref by tests/test_nominated.py and tests/test_preemption.py.
 """
 import glob
 import gzip
@@ -25,8 +33,9 @@ from ksim import abi, profile
 from ksim.encode import encode_cluster, encode_pods
 from ksim.model import node_from_dict, pod_from_dict
 from ksim.wrapped import filter_message
-from oracle.objref import ObjScheduler
 from oracle.oracle import Oracle
+
+import gofixture
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIXTURES = sorted(p for p in glob.glob(os.path.join(HERE, "golden", "go", "*.json.gz"))
@@ -55,32 +64,46 @@ def _cycle(pod_name, res, next_start):
 
 
 def test_fixtures_present():
-    assert len(FIXTURES) >= 4
+    assert len(FIXTURES) >= 13
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p).split(".")[0] for p in FIXTURES])
 def test_fixture_matches_objref(path):
     doc = _load(path)
     nodes, bound, pods = _objects(doc)
-    ref = ObjScheduler(nodes, bound, namespaces=doc["namespaces"], pct=doc["percentageOfNodesToScore"],
-                       seed=doc["tiebreakSeed"], hard_pod_affinity_weight=doc["hardPodAffinityWeight"])
+    ref = gofixture.objref(doc, nodes, bound)
     assert [ni.node.name for ni in ref.nodes] == [d["metadata"]["name"] for d in doc["nodes"]], "nodeTree order"
-    for p, exp in zip(pods, doc["expected"]):
-        got = json.loads(json.dumps(_cycle(p.name, ref.cycle(p), ref.next_start)))
+    nominated = gofixture.nominated_pods(doc)
+    start = {p.name: _seconds(d) for p, d in zip(bound, doc["boundPods"])} if doc.get("preemption") else {}
+    order = {p.name: k for k, p in enumerate(bound)}
+    for i, (p, exp) in enumerate(zip(pods, doc["expected"])):
+        kw = gofixture.cycle_kwargs(doc, i, nominated)
+        res = ref.cycle(p, **kw)
+        got = json.loads(json.dumps(_cycle(p.name, res, ref.next_start)))
+        if "postFilter" in exp:
+            node, victims = ref.preempt(p, p.priority, start, order, nominated=kw.get("nominated"))
+            got["postFilter"] = {"nominatedNode": node, "victims": victims}
+        elif doc.get("preemption") and res["chosen"] is not None:
+            start[p.name] = 20000 + i                 # tools/make_go_fixtures.py ASSUMED_START
+            order[p.name] = len(order)
         assert got == exp, f"{os.path.basename(path)}: pod {p.name}"
+
+
+def _seconds(d):
+    t = d["status"]["startTime"]                       # 2022-01-01THH:MM:SSZ
+    h, m, sec = (int(x) for x in t[11:19].split(":"))
+    return h * 3600 + m * 60 + sec
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p).split(".")[0] for p in FIXTURES])
 def test_fixture_matches_c_oracle(path):
     doc = _load(path)
-    nodes, bound, pods = _objects(doc)
-    cluster, _ = encode_cluster(nodes, bound, namespaces=doc["namespaces"])
-    enc = encode_pods(cluster, pods)
-    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=doc["percentageOfNodesToScore"],
-                                  tiebreak_seed=doc["tiebreakSeed"],
-                                  hard_pod_affinity_weight=doc["hardPodAffinityWeight"])
-    ora = Oracle(cluster, profile.compile_profile(sp))
+    if not gofixture.plain(doc):
+        pytest.skip("PodNominator / PostFilter cycles: objref replays them (test_fixture_matches_objref)")
+    cluster, enc, sp, prof = gofixture.encode(doc, encode_cluster, encode_pods)
+    ora = Oracle(cluster, prof)
     forder = sp.filter_order()
+    snames = [p.name for p in sp.score_plugins()]
     names = cluster.node_names
     for i, exp in enumerate(doc["expected"]):
         o = ora.cycle(enc, i)
@@ -97,7 +120,7 @@ def test_fixture_matches_c_oracle(path):
         assert o["n_feasible"] == exp["nFeasible"], where
         assert o["next_start"] == exp["nextStartNodeIndex"], where
         if exp["nFeasible"] > 1:
-            for k, pl in enumerate(SCORE_NAMES):
+            for k, pl in enumerate(snames):
                 for name, raw in exp["score"][pl].items():
                     pos = names.index(name)
                     assert o["raw"][k][pos] == raw, (where, pl, name)

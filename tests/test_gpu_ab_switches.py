@@ -1,10 +1,12 @@
-"""The engine's remaining A/B switches select other production forms of the
-same runs (KSIM_NO_LAZY: the three-launch P100 / ADAPT batches, commit as its
-own launch, instead of the deferred commit; KSIM_NO_STAB: the static plugins
-evaluated per node instead of the static-class table).  They are read once
-per process, so each runs in one child process that schedules P100 and ADAPT
-batches and checks them against the oracle (the default forms run in every
-other GPU test)."""
+"""The A/B forms of the same runs live in a flavor build, not behind runtime
+switches (csrc/Makefile "ab": libksim_engine_ab.so, KSIM_AB_FORMS): the
+three-launch P100 / ADAPT batches (commit as its own launch) instead of the
+deferred commit, the static plugins evaluated per node instead of the
+static-class table, ADAPT normalized-score and topology pods on the per-pod
+path, per-cycle PreFilter domain sums, eager shard cycles.  A child process
+loads that library (KSIM_LIB_VARIANT=ab), schedules P100 and ADAPT batches
+and checks them against the oracle (the product forms run in every other GPU
+test)."""
 import os
 import subprocess
 import sys
@@ -50,10 +52,11 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("switch", ["KSIM_NO_LAZY", "KSIM_NO_STAB"])
-def test_separate_launch_forms_vs_oracle(switch):
+def test_ab_forms_vs_oracle():
+    lib = os.path.join(ROOT, "kube-scheduler-simulator_amd", "ksim", "libksim_engine_ab.so")
+    assert os.path.exists(lib), "build the ab flavor: make -C kube-scheduler-simulator_amd/csrc ab"
     env = dict(os.environ)
-    env[switch] = "1"
+    env["KSIM_LIB_VARIANT"] = "ab"
     env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd"),
                                          env.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, cwd=ROOT, capture_output=True, text=True,

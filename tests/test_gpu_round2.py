@@ -315,18 +315,16 @@ def test_persistent_tables_under_assume_forget():
     (ksim_assume / ksim_forget of single uploads: the class-index update path)
     and snapshot resets: an engine reading the tables must place every later
     pod exactly as one that recomputes the domain sums per cycle
-    (k_topo_prefilter, KSIM_NO_PTAB), and both as the oracle before the binds."""
+    (k_topo_prefilter: the "ab" flavor), and both as the oracle before the binds."""
     cluster, pods = gen.config3(n_nodes=800, pods_per_node=6, n_incoming=900, seed=31, zone_anti_every=40)
     extra = pods.subset(800, 60)                     # same encoding: their adds name this cluster's classes
     prof = _prof(100)
     a = _engine(cluster, prof)
     a.load_pods(pods)
-    os.environ["KSIM_NO_PTAB"] = "1"
-    try:
-        b = _engine(cluster, prof)
-        b.load_pods(pods)
-    finally:
-        del os.environ["KSIM_NO_PTAB"]
+    b = Engine(0, variant="ab")
+    b.set_profile(prof)
+    b.set_cluster(cluster)
+    b.load_pods(pods)
     ca, _ = a.schedule_loaded(0, 300)
     cb, _ = b.schedule_loaded(0, 300)
     np.testing.assert_array_equal(ca, cb)
@@ -360,19 +358,14 @@ def test_go_fixtures_through_engine(path):
     """The recorded cycles of each fixture (which a Go run would pin) reproduced
     by the device: filter outcomes and messages, scores, totals, placement,
     nextStartNodeIndex."""
-    from ksim.model import node_from_dict, pod_from_dict
+    import gofixture
     from ksim.wrapped import filter_message
     with gzip.open(path, "rb") as f:
         doc = json.loads(f.read())
-    nodes = [node_from_dict(d) for d in doc["nodes"]]
-    bound = [pod_from_dict(d) for d in doc["boundPods"]]
-    pods = [pod_from_dict(d) for d in doc["pods"]]
-    cluster, _ = encode_cluster(nodes, bound, namespaces=doc["namespaces"])
-    enc = encode_pods(cluster, pods)
-    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=doc["percentageOfNodesToScore"],
-                                  tiebreak_seed=doc["tiebreakSeed"],
-                                  hard_pod_affinity_weight=doc["hardPodAffinityWeight"])
-    eng = _engine(cluster, profile.compile_profile(sp))
+    if not gofixture.plain(doc):
+        pytest.skip("PodNominator / PostFilter cycles (objref replays them on the CPU)")
+    cluster, enc, sp, prof = gofixture.encode(doc, encode_cluster, encode_pods)
+    eng = _engine(cluster, prof)
     forder, names = sp.filter_order(), cluster.node_names
     snames = [p.name for p in sp.score_plugins()]
     for i, exp in enumerate(doc["expected"]):

@@ -472,8 +472,14 @@ def bench_fw(args, out):
                 in_calls += time.perf_counter() - c0
                 bound += 1
             dt = time.perf_counter() - t0
-            return {"us_per_cycle": dt / count * 1e6, "us_in_calls": in_calls / count * 1e6, "cycles": count,
-                    "bound": bound, "us_per_call": {k: v / count * 1e6 for k, v in split.items()}}
+            r = {"us_per_cycle": dt / count * 1e6, "us_in_calls": in_calls / count * 1e6, "cycles": count,
+                 "bound": bound, "us_per_call": {k: v / count * 1e6 for k, v in split.items()}}
+            if kind == "engine":   # where fw_score / fw_normalize were answered (host or device)
+                d = e.diag()
+                r["answered"] = {k: d[k] for k in ("fw_score_host", "fw_score_device", "fw_normalize_cached",
+                                                   "fw_normalize_device")}
+                e.close()
+            return r
 
         run("engine", min(200, n_pods))                      # warm-up (graphs, first launches)
         e_r = run("engine", n_pods)

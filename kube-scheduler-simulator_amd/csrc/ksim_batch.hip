@@ -52,7 +52,8 @@ namespace ksim {
 template <int kTopThreads>
 __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfeas, int32_t j,
                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
-                                           int32_t* __restrict__ topk_complete, uint64_t* __restrict__ xsend) {
+                                           int32_t* __restrict__ topk_complete, uint64_t* __restrict__ xsend,
+                                           uint64_t* tclk = nullptr) {
   constexpr int kTopWaves = kTopThreads / 64;
   constexpr int kTopSlots = (kTopWaves * kTopT + 63) / 64;   // block-merge entries per lane
   __shared__ uint64_t s_list[kTopWaves][kTopT];
@@ -75,15 +76,16 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     const uint64_t u = nfeas > kTileCand ? a[kTileCand - 1] : 0;
     const uint64_t wthr = wave_max_u64_dpp(u);
     const uint64_t wmax = wave_max_u64_dpp(a[0]);
-    int32_t fsum = nfeas;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) fsum += __shfl_xor(fsum, m, 64);
+    const int32_t fsum = (int32_t)wave_sum_u32_dpp((uint32_t)nfeas);
     if (lane == 0) {
       s_wmax[wv] = wmax;
       s_wthr[wv] = wthr;
       s_wf[wv] = fsum;
     }
-    __syncthreads();
+    lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+    if (tclk && threadIdx.x == 0) tclk[0] = __builtin_amdgcn_s_memrealtime();
+#endif
     uint64_t thr = 0, mine_w = lane < kTopWaves ? s_wmax[lane] : 0;
     int32_t total = 0, rank = 0;
 #pragma unroll
@@ -99,14 +101,15 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     int32_t cl = 0;
 #pragma unroll
     for (int q = 0; q < kTileCand; q++) cl += a[q] >= cut;   // lists are sorted: a prefix
-    int32_t pre = cl;                              // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t y = __shfl_up(pre, d, 64);
-      if (lane >= d) pre += y;
-    }
-    if (lane == 63) s_wc[wv] = pre;
-    __syncthreads();
+    // inclusive wave scan of cl in [0, kTileCand]: by its bits' ballots
+    static_assert(kTileCand < 8, "three ballots cover the count");
+    const uint64_t c0b = __ballot(cl & 1), c1b = __ballot(cl & 2), c2b = __ballot(cl & 4);
+    const int32_t pre = (int32_t)(mask_below(c0b) + 2 * mask_below(c1b) + 4 * mask_below(c2b)) + cl;
+    if (lane == 0) s_wc[wv] = __popcll(c0b) + 2 * __popcll(c1b) + 4 * __popcll(c2b);
+    lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+    if (tclk && threadIdx.x == 0) tclk[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     int32_t off = 0, C = 0;
 #pragma unroll
     for (int w = 0; w < kTopWaves; w++) {
@@ -119,11 +122,15 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
 #pragma unroll
       for (int q = 0; q < kTileCand; q++)
         if (q < cl) s_cand[base_i + q] = a[q];
-      __syncthreads();
+      lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+      if (tclk && threadIdx.x == 0) tclk[2] = __builtin_amdgcn_s_memrealtime();
+      if (tclk && threadIdx.x == 0) tclk[3] = C;
+#endif
       if (wv != 0) return;
       const uint64_t c0 = lane < C ? s_cand[lane] : 0;
       int32_t r = 0;
-      for (int j = 0; j < C; j++) r += s_cand[j] > c0;   // keys are unique: ranks are distinct
+      for (int j = 0; j < C; j++) r += readlane_u64(c0, j) > c0;   // keys are unique: ranks are distinct
       const int32_t n_out = C < kTopT ? C : kTopT;
       if (lane < C && r < kTopT) topk[(size_t)j * kTopT + r] = c0;
       if (lane >= n_out && lane < kTopT) topk[(size_t)j * kTopT + lane] = 0;
@@ -164,7 +171,7 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     s_cnt[wv] = cnt;
     s_complete[wv] = complete;
   }
-  __syncthreads();
+  lds_barrier();
   if (wv != 0) return;
   // block merge: entry x = w * kTopT + e sits in lane x % 64, slot x / 64
   uint64_t key[kTopSlots], last = 0;
@@ -625,7 +632,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
     const int32_t nt = __popcll(__ballot(lost_t)), na = __popcll(__ballot(lost_a));
     if (lane == 0) s_winv[wave] = nt | (na << 16);
   }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     uint64_t m = 0;
     int32_t lt = 0, la = 0;
@@ -647,7 +654,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
 // runs the (deterministic) chain itself, thread k ending with pod k's guess in
 // a register, so the pairs need no chain launch and no gkey round trip.
 // Block 0 also stores the guesses and the prefix length for k_batch_commit.
-#ifdef KSIM_CP_CLOCKS
+#if defined(KSIM_CP_CLOCKS) || defined(KSIM_TC_CLOCKS)
 __device__ unsigned long long g_cp_dbg[8];
 unsigned long long* cp_clock_buffer() {
   void* p = nullptr;
@@ -759,12 +766,22 @@ void launch_static_table(const LaunchArgs& a, const int32_t* rep, int32_t n_cls,
 constexpr int kLazyHash = 1 << kLazyHashBits;
 constexpr int kLazyBitWords = kLazyMaxNodes / 32;
 static_assert(kLazyHash >= 4 * kBatchPods && kBatchPods <= 1024, "overlay hash / block geometry");
+// Clusters of at most kLazyDirect nodes index the overlay by node id (an int16
+// entry per node, 64 KB of LDS): one LDS read per node instead of the bitmap
+// test and the hash probe.
+constexpr int kLazyDirect = 1 << 15;
+static_assert(kBatchPods < 32767, "overlay entries are int16");
 
 __device__ __forceinline__ uint32_t lazy_hash(int32_t node) {
   return ((uint32_t)node * 2654435761u) >> (32 - kLazyHashBits);
 }
 
-template <bool FLUSH>
+// the request fields a FAST pod's key reads
+struct PodReq {
+  int64_t cpu, mem, eph, nzc, nzm;
+};
+
+template <bool FLUSH, bool DIRECT>
 __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
@@ -774,13 +791,23 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
                                                            uint64_t* __restrict__ xsend) {
   constexpr int kThreads = 1024;
   static_assert(kThreads >= kBatchPods, "one thread per batch entry");
-  __shared__ ResCols s_rq[kBatchPods];          // batch i-1's pod requests, then each bound node's delta
-  __shared__ int32_t s_hkey[kLazyHash];         // overlay hash: local node or -1
-  __shared__ int16_t s_hval[kLazyHash];         // ... its entry
-  __shared__ uint32_t s_bits[kLazyBitWords];    // nodes batch i-1 bound
+  // s_rq: batch i-1's pod requests, then each bound node's delta; entry
+  // kBatchPods stays zero (DIRECT: the entry of every node batch i-1 did not bind)
+  __shared__ ResCols s_rq[kBatchPods + 1];
+  __shared__ PodReq s_pc[kBatchPods + 1];      // pod cur0 + b + t: this block's pod of batch i is t = committed
+  __shared__ __attribute__((aligned(16))) int16_t s_ent[DIRECT ? kLazyDirect : 1];   // node -> entry
+  __shared__ int32_t s_hkey[DIRECT ? 1 : kLazyHash];   // overlay hash: local node or -1
+  __shared__ int16_t s_hval[DIRECT ? 1 : kLazyHash];   // ... its entry
+  __shared__ uint32_t s_bits[DIRECT ? 1 : kLazyBitWords];   // nodes batch i-1 bound
   __shared__ int32_t s_istar, s_inode, s_sched, s_unsched;
   const int tid = threadIdx.x;
   const int32_t b = blockIdx.x;
+#ifdef KSIM_TC_CLOCKS
+  // phase clocks of every block (KSIM_TC_CLOCKS builds, tools/tc_clocks.py),
+  // thread 0's view, summed (see the end of the kernel)
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_pro = 0, t_loop = 0, tclk[4] = {0, 0, 0, 0}, tp[3] = {0, 0, 0};
+#endif
   // batch i-1's slot, batch i-2's guess b and the state batch i-1 started from
   // (independent loads)
   const int32_t e1 = *L.e1, e2 = *L.e2;
@@ -792,35 +819,59 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   if (tid == b) g2 = L.g2[b];
   const int32_t cur0 = L.st_in->cursor, end = L.st_in->end;
   const int64_t seq0 = L.st_in->pod_seq;
-  const int nwords = (c.n + 31) >> 5;
-  for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
-  for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
+  // every pod record the commit may need, before the cut is known (they only
+  // depend on cur0): pod tid of batch i-1 (its request, kept if committed) and
+  // the candidates cur0 + b + t for this block's pod of batch i
+  ResCols rq{0, 0, 0, 0, 0, 0};
+  for (int x = tid; x < 2 * kBatchPods + 1; x += kThreads) {
+    const int32_t q = x < kBatchPods ? cur0 + x : cur0 + b + (x - kBatchPods);
+    if (q < end) {
+      const ksim_pod& y = P.pods[q];
+      if (x < kBatchPods) {
+        rq = ResCols{y.req_cpu, y.req_mem, y.req_eph, y.nz_cpu, y.nz_mem, 1};
+      } else {
+        s_pc[x - kBatchPods] = PodReq{y.req_cpu, y.req_mem, y.req_eph, y.nz_cpu, y.nz_mem};
+      }
+    }
+  }
+  if constexpr (DIRECT) {
+    // every local node's entry = kBatchPods (the zero entry), 4 per store
+    const uint64_t fill = 0x0001000100010001ull * (uint64_t)kBatchPods;
+    for (int x = tid; x < (c.n + 3) >> 2; x += kThreads) reinterpret_cast<uint64_t*>(s_ent)[x] = fill;
+  } else {
+    const int nwords = (c.n + 31) >> 5;
+    for (int x = tid; x < kLazyHash; x += kThreads) s_hkey[x] = -1;
+    for (int x = tid; x < nwords; x += kThreads) s_bits[x] = 0;
+  }
   const int32_t nchain = e1 > 0 ? e1 : 0;      // -1: no batch i-1 (run start, a flush, past the end)
   if (tid == 0) {
     s_istar = nchain;
     s_inode = -1;
     s_sched = 0;
     s_unsched = 0;
+    s_rq[kBatchPods] = ResCols{0, 0, 0, 0, 0, 0};
   }
-  __syncthreads();
+  lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+  tp[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   block_first_min(&s_istar, tid < nchain && m1 > g1);   // keys are unique per node: never equal unless 0
-  __syncthreads();
+  lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+  tp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int32_t istar = s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
   if (tid == istar && istar < nchain) s_inode = key_node(m1) - c.base;
-  ResCols rq{0, 0, 0, 0, 0, 0};
-  if (tid < committed) {
-    const ksim_pod& q = P.pods[cur0 + tid];
-    rq = ResCols{q.req_cpu, q.req_mem, q.req_eph, q.nz_cpu, q.nz_mem, 1};
-    s_rq[tid] = rq;
-  }
-  // this block's pod of batch i, in flight with the overlay build
+  if (tid < committed) s_rq[tid] = rq;
+  // this block's pod of batch i
   const int32_t base = cur0 + committed;
   const int32_t pi = base + b;
   const bool live = !FLUSH && pi < min(end, base + kBatchPods);   // block-uniform
-  ksim_pod pf;
-  if (live) pf = fast_pod_fields(P.pods[pi]);
-  __syncthreads();
+  lds_barrier();
+#ifdef KSIM_TC_CLOCKS
+  tp[2] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int32_t inode = s_inode;
   // entry tid < i*: its guessed node takes pod tid, and pod i* when i* chose it
   const int32_t gnode = (tid < istar && g1) ? key_node(g1) - c.base : -1;
@@ -836,10 +887,14 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
       d.pods += 1;
     }
     s_rq[tid] = d;
-    atomicOr(&s_bits[gnode >> 5], 1u << (gnode & 31));
-    uint32_t h = lazy_hash(gnode);
-    while (atomicCAS(&s_hkey[h], -1, gnode) != -1) h = (h + 1) & (kLazyHash - 1);   // guessed nodes are distinct
-    s_hval[h] = (int16_t)tid;
+    if constexpr (DIRECT) {
+      s_ent[gnode] = (int16_t)tid;                // guessed nodes are distinct
+    } else {
+      atomicOr(&s_bits[gnode >> 5], 1u << (gnode & 31));
+      uint32_t h = lazy_hash(gnode);
+      while (atomicCAS(&s_hkey[h], -1, gnode) != -1) h = (h + 1) & (kLazyHash - 1);   // guessed nodes are distinct
+      s_hval[h] = (int16_t)tid;
+    }
   }
   // batch i-1's placements and statistics (k_batch_commit's bookkeeping)
   const int32_t pnode = tid == istar ? inode + c.base : (g1 ? key_node(g1) : -1);
@@ -854,12 +909,14 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     if (mn0 >= 0) mr0 = ResCols{c.req_cpu[mn0], c.req_mem[mn0], c.req_eph[mn0], c.nz_cpu[mn0], c.nz_mem[mn0], c.num_pods[mn0]};
     if (mn1 >= 0) mr1 = ResCols{c.req_cpu[mn1], c.req_mem[mn1], c.req_eph[mn1], c.nz_cpu[mn1], c.nz_mem[mn1], c.num_pods[mn1]};
   }
-  __syncthreads();
-  if (b == 0 && tid < (int)(sizeof(DevState) / 8)) {   // st[p] = st[p ^ 1], then the commit's updates
-    static_assert(sizeof(DevState) % 8 == 0, "DevState copy by words");
-    reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
+  lds_barrier();
+  if (b == 0) {                                 // block-uniform
+    if (tid < (int)(sizeof(DevState) / 8)) {    // st[p] = st[p ^ 1], then the commit's updates
+      static_assert(sizeof(DevState) % 8 == 0, "DevState copy by words");
+      reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
+    }
+    __syncthreads();                            // the copy's stores land before thread 0's below
   }
-  __syncthreads();
   if (b == 0 && tid == 0) {
     // every new value from st[p ^ 1]: st[p] is never read back here (a
     // uniform load of it would go through the scalar cache, which does not
@@ -881,14 +938,18 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   }
   // the overlay delta of a node (zero when batch i-1 did not bind it)
   auto delta = [&](int32_t node) -> ResCols {
-    ResCols d{0, 0, 0, 0, 0, 0};
-    const uint32_t bw = s_bits[node >> 5], bit = 1u << (node & 31);
-    if (bw & bit) {
-      uint32_t h = lazy_hash(node);
-      while (s_hkey[h] != node) h = (h + 1) & (kLazyHash - 1);   // present: the bit says so
-      d = s_rq[s_hval[h]];
+    if constexpr (DIRECT) {
+      return s_rq[s_ent[node]];
+    } else {
+      ResCols d{0, 0, 0, 0, 0, 0};
+      const uint32_t bw = s_bits[node >> 5], bit = 1u << (node & 31);
+      if (bw & bit) {
+        uint32_t h = lazy_hash(node);
+        while (s_hkey[h] != node) h = (h + 1) & (kLazyHash - 1);   // present: the bit says so
+        d = s_rq[s_hval[h]];
+      }
+      return d;
     }
-    return d;
   };
   auto materialize = [&]() {
     if (tid != b) return;
@@ -916,12 +977,25 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     return;
   }
   // pod b of batch i against S_i (k_batch_top's loops with the overlay)
+  ksim_pod pf;
+  {
+    const PodReq x = s_pc[committed];
+    pf.req_cpu = x.cpu;
+    pf.req_mem = x.mem;
+    pf.req_eph = x.eph;
+    pf.nz_cpu = x.nzc;
+    pf.nz_mem = x.nzm;
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCALAR; k++) pf.scalar_req[k] = 0;   // FAST pods: no scalar requests
+  }
   uint64_t a[kTileCand] = {0, 0, 0, 0};
   int32_t nfeas = 0;
   const FastProg bq = fast_prog(*bp_p);
   const uint64_t hseed = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + committed + b) << 20);
-#pragma unroll 1
-  for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) {
+#ifdef KSIM_TC_CLOCKS
+  t_pro = __builtin_amdgcn_s_memrealtime();
+#endif
+  auto key_of = [&](int32_t node) -> uint64_t {
     NodeRow r = load_res_row_off(c, node);
     const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
     const ResCols d = delta(node);
@@ -931,16 +1005,66 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     r.nz_cpu += d.nzc;
     r.nz_mem += d.nzm;
     r.num_pods += d.pods;
-    const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+    return dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+  };
+  auto insert = [&](uint64_t k) {
     nfeas += k != 0;
     a[3] = umax64(a[3], k);
     cswap_desc(a[2], a[3]);
     cswap_desc(a[1], a[2]);
     cswap_desc(a[0], a[1]);
+  };
+  int32_t node = c.eval_lo + tid;
+#ifdef KSIM_TOP_UNROLL2
+  // two nodes per iteration: both rows in flight together
+#pragma unroll 1
+  for (; node + kThreads < c.eval_hi; node += 2 * kThreads) {
+    const uint64_t k0 = key_of(node), k1 = key_of(node + kThreads);
+    insert(k0);
+    insert(k1);
   }
+#endif
+#pragma unroll 1
+  for (; node < c.eval_hi; node += kThreads) insert(key_of(node));
+#ifdef KSIM_TC_CLOCKS
+  t_loop = __builtin_amdgcn_s_memrealtime();
+#endif
   materialize();
   // xsend (replicated handles): this replica's record of its node range, for the all-gather
+#ifdef KSIM_TC_CLOCKS
+  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend, tclk);
+  if (tid == 0) {
+    // dbg: 0 prologue, 1 thread 0's node loop, 2 wait for the block's slowest
+    // wave, 3 the finish after its first barrier, 4 prologue to the first
+    // barrier (loads, LDS init), 5 blocks, 6 the cut, 7 the overlay
+    const uint64_t t_out = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&g_cp_dbg[0], (unsigned long long)(t_pro - t_in));
+    atomicAdd(&g_cp_dbg[1], (unsigned long long)(t_loop - t_pro));
+    atomicAdd(&g_cp_dbg[2], (unsigned long long)(tclk[0] - t_loop));
+    atomicAdd(&g_cp_dbg[3], (unsigned long long)(t_out - tclk[0]));
+    atomicAdd(&g_cp_dbg[4], (unsigned long long)(tp[0] - t_in));
+    atomicAdd(&g_cp_dbg[5], 1ull);
+    atomicAdd(&g_cp_dbg[6], (unsigned long long)(tp[1] - tp[0]));
+    atomicAdd(&g_cp_dbg[7], (unsigned long long)(tp[2] - tp[1]));
+  }
+#else
   top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
+#endif
+}
+
+// the evaluation launch of a deferred-commit batch (DIRECT overlay when the
+// local node range fits kLazyDirect)
+template <bool FLUSH>
+static void launch_top_commit(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  if (a.c.n <= kLazyDirect)
+    k_batch_top_commit<FLUSH, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                      a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                      xsend);
+  else
+    k_batch_top_commit<FLUSH, false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
+                                                                       a.s.topk_cnt, a.s.topk_complete, a.chosen,
+                                                                       xsend);
 }
 
 const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_batch_chain_pairs"};
@@ -948,8 +1072,7 @@ const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs) {
   const LaunchArgs& a = z.a;
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                             a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
+  launch_top_commit<false>(z, nullptr, stream);
   if (evs) (void)hipEventRecord(evs[1], stream);
   k_batch_chain_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
       z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
@@ -958,19 +1081,13 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
   return 0x3u;
 }
 
-void launch_lazy_top(const LazyBatch& z, hipStream_t stream) {
-  const LaunchArgs& a = z.a;
-  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, a.chosen, nullptr);
-}
+void launch_lazy_top(const LazyBatch& z, hipStream_t stream) { launch_top_commit<false>(z, nullptr, stream); }
 
 // Replicated handles (ksim_set_eval_range): the first launch keys the replica's
 // node range and writes its record; after the records' all-gather, the global
 // merge and the chain + pairs on X[p].
 void launch_lazy_top_rep(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
-  const LaunchArgs& a = z.a;
-  k_batch_top_commit<false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt,
-                                                             a.s.topk_complete, a.chosen, xsend);
+  launch_top_commit<false>(z, xsend, stream);
 }
 
 void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream) {
@@ -982,11 +1099,7 @@ void launch_lazy_chain_rep(const LazyBatch& z, int32_t world, hipStream_t stream
                                                                             z.cend, z.pmax, a.s.pnorm, a.s.pinv);
 }
 
-void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) {
-  const LaunchArgs& a = z.a;
-  k_batch_top_commit<true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                            a.s.topk_cnt, a.s.topk_complete, a.chosen, nullptr);
-}
+void launch_lazy_flush(const LazyBatch& z, hipStream_t stream) { launch_top_commit<true>(z, nullptr, stream); }
 
 // In-process shard group: M = max over the group's pmax arrays, written back to each.
 __global__ __launch_bounds__(kBatchPods) void k_group_max(GroupPtrs g) {

@@ -79,7 +79,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
     for (int e = 0; e < kTopT; e++) rep[e] = e < cnt ? key_node(lst[e]) : -1;
   } else {
     for (int x = i; x < kHashSlots; x += kBatchPods) s_key[x] = -1;
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int e = 0; e < kTopT; e++) {
       int16_t slot = -1;
@@ -95,7 +95,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
       }
       L.rep[i][e] = slot;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int e = 0; e < kTopT; e++) rep[e] = L.rep[i][e];
   }
@@ -104,7 +104,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
 #pragma unroll
   for (int e = 0; e < kTopT; e++)
     if (e < cnt) L.hold[0][rep[e]] = L.hold[1][rep[e]] = kBatchPods;
-  __syncthreads();
+  lds_barrier();
   const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
   int a = cnt > 0 ? 0 : -1;                    // current guess (entry index) or -1
   int32_t pra = -1;                            // the slot this pod registered last round
@@ -120,7 +120,7 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
 #pragma unroll
     for (int e = 0; e < kTopT; e++) ra = e == a ? rep[e] : ra;
     if (a >= 0) atomicMin(&L.hold[par][ra], i);
-    __syncthreads();
+    lds_barrier();
     CHAIN_DELAY(1);                            // a middle wave late after the first barrier
     if (pra >= 0) L.hold[par ^ 1][pra] = kBatchPods;
     if (i == 0) L.first[par ^ 1] = kBatchPods;
@@ -138,16 +138,16 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
     }
     pra = a >= 0 ? ra : -1;
     a = na;
-    __syncthreads();
+    lds_barrier();
     CHAIN_DELAY((int)(blockDim.x >> 6) - 1);   // the last wave reads the flag late
     first = L.first[par];
     if (first == kBatchPods) break;            // a fixpoint: every pod exact
   }
   // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
   if (i == 0) s_cut = first < nb ? first : nb;
-  __syncthreads();
+  lds_barrier();
   block_first_min(&s_cut, i < first && i < nb && a < 0 && incomplete);
-  __syncthreads();
+  lds_barrier();
   const int32_t nchain = s_cut;
   const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
   uint64_t ga = 0;

@@ -58,6 +58,30 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_add_u32(uint32_t v) {
+  // old = 0 for disabled rows and lanes (the identity of the sum)
+  return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, true);
+}
+
+// Wave sum over u32 by the same DPP steps as wave_max_u32_dpp (pairs, quads,
+// rotations inside each 16-lane row, then rows 0+1 -> 1, 2+3 -> 3, 1 -> 2, 3;
+// the total in lane 63); all 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
+  v = dpp_add_u32<0xb1, 0xf>(v);
+  v = dpp_add_u32<0x4e, 0xf>(v);
+  v = dpp_add_u32<0x124, 0xf>(v);
+  v = dpp_add_u32<0x128, 0xf>(v);
+  v = dpp_add_u32<0x142, 0xa>(v);
+  v = dpp_add_u32<0x143, 0xc>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// The number of set bits of m in the lanes below this one.
+__device__ __forceinline__ uint32_t mask_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Wave max over u64 keys, high words first: one 32-bit reduction, and when a
 // single lane holds the maximal high word (the common case for tie-break keys,
 // whose high word carries hash bits) its low word by one readlane; otherwise a
@@ -91,6 +115,18 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+
+// A workgroup barrier for LDS hand-offs only: the fences are LDS-scoped, so
+// the barrier waits for the wave's LDS operations (lgkmcnt) and not for its
+// outstanding global loads and stores, as __syncthreads does (a load issued
+// early for use after the barrier stays in flight across it; a store does not
+// hold the barrier until it is acknowledged).  Not for hand-offs through
+// global memory.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // *s = min(*s, the block's first thread with pred) for one-dimensional blocks:
 // one LDS atomicMin per wave (its first set lane) instead of one per thread,

@@ -1014,18 +1014,8 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     cswap_desc(a[1], a[2]);
     cswap_desc(a[0], a[1]);
   };
-  int32_t node = c.eval_lo + tid;
-#ifdef KSIM_TOP_UNROLL2
-  // two nodes per iteration: both rows in flight together
 #pragma unroll 1
-  for (; node + kThreads < c.eval_hi; node += 2 * kThreads) {
-    const uint64_t k0 = key_of(node), k1 = key_of(node + kThreads);
-    insert(k0);
-    insert(k1);
-  }
-#endif
-#pragma unroll 1
-  for (; node < c.eval_hi; node += kThreads) insert(key_of(node));
+  for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) insert(key_of(node));
 #ifdef KSIM_TC_CLOCKS
   t_loop = __builtin_amdgcn_s_memrealtime();
 #endif

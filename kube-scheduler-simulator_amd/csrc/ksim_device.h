@@ -277,6 +277,15 @@ struct DevScratch {
   uint64_t* tb_pp;       // replicated topology batches: [2][kTbPods] pair maxima, pinv (all-reduced max)
   int32_t* pinv;         // batch path: [B] 1 = a maximum holder of pod j left its feasible set (batch ends before j)
   unsigned long long* dbg;   // [16] diagnostic accumulators (ksim_get_diag), e.g. chain phase times
+  // framework-driven filter pass (ksim_fw_prefilter), pods without topology
+  // uses: the answers written straight to the host's pinned staging (device
+  // addresses; else null): next_start and a too-wide flag, the codes, the
+  // details, each feasible node's raw scores [S][n] and weighted part as int32
+  int32_t* m_head;
+  uint8_t* m_fail;
+  uint32_t* m_detail;
+  int32_t* m_raw;
+  int32_t* m_part;
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
   uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records
   int64_t* dom;          // [KSIM_MAX_USES][vmax] topology-pair sums of the current pod (zero between pods)

@@ -169,6 +169,25 @@ struct ksim_handle {
   void* pin = nullptr;
   void* pin_d = nullptr;
   size_t pin_cap = 0;
+  // the last pod upload's copy out of the staging (upload_blob waits on it
+  // instead of the whole stream); the pod last uploaded into pod1_arena (its
+  // bytes and device address: a Reserve / Unreserve of the same pod binds
+  // from there, no upload)
+  hipEvent_t up_ev = nullptr;
+  bool up_pending = false;
+  std::vector<char> pod1_blob;
+  char* pod1_base = nullptr;
+  // the framework-driven filter passes alternate two arenas, so the Reserve of
+  // cycle i (binding from cycle i's arena) can wait, queued, and run inside
+  // cycle i+1's upload launch (pend_bind); any other call launches it first
+  DevArena fw_arena[2];
+  int fw_flip = 0;
+  struct PendBind {
+    bool on = false;
+    DevPods P{};
+    int32_t node = 0;
+    int sign = 0;
+  } pend_bind;
   void* pout = nullptr;
   void* pout_d = nullptr;
   size_t pout_cap = 0;
@@ -206,6 +225,8 @@ struct ksim_handle {
   void* fwh_d = nullptr;
   size_t fwh_cap = 0;
   uint32_t fw_tflags = 0;
+  size_t fw_oraw = 0, fw_opart = 0;  // fwh offsets of the raw scores and the weighted part
+  bool fw_raw32 = false;             // ... as int32 (the filter kernel's own copy) or int64 (a copy launch)
   int32_t* fw_nodes = nullptr;     // device [n]
   int64_t* fw_vals = nullptr;      // device [n]
   int64_t* fw_out = nullptr;       // device [n]
@@ -667,10 +688,23 @@ int fw_abandon(ksim_handle* h) {
 }  // namespace
 static int flush_deferred_binds(ksim_handle* h);
 static int flush_idle(ksim_handle* h);
+// The queued Reserve of the last framework cycle (pend_bind), launched now.
+static int flush_pend_bind(ksim_handle* h) {
+  if (!h || !h->pend_bind.on) return KSIM_OK;
+  h->pend_bind.on = false;
+  HIPCHK(h, hipSetDevice(h->device));
+  launch_assume(h->dc, h->pend_bind.P, 0, h->pend_bind.node, h->pend_bind.sign, h->stream);
+  HIPCHK(h, hipGetLastError());
+  return KSIM_OK;
+}
 namespace {
 
-int ensure_ready(ksim_handle* h, bool fw = false) {
+int ensure_ready(ksim_handle* h, bool fw = false, bool keep_pend = false) {
   if (!h) return KSIM_E_INVALID;
+  if (!keep_pend) {
+    const int rc = flush_pend_bind(h);
+    if (rc) return rc;
+  }
   if (!fw && (h->fw_pending || h->fw_scored || h->fw_dom_dirty)) {
     const int rc = fw_abandon(h);
     if (rc) return rc;
@@ -1746,6 +1780,8 @@ void ksim_destroy(ksim_handle* h) {
   if (h->pod1_arena.p) (void)hipFree(h->pod1_arena.p);
   if (h->nom_arena.p) (void)hipFree(h->nom_arena.p);
   if (h->asm_arena.p) (void)hipFree(h->asm_arena.p);
+  for (auto& a : h->fw_arena)
+    if (a.p) (void)hipFree(a.p);
   if (h->fwh) (void)hipHostFree(h->fwh);
   if (h->pin) (void)hipHostFree(h->pin);
   if (h->pout) (void)hipHostFree(h->pout);
@@ -1755,6 +1791,7 @@ void ksim_destroy(ksim_handle* h) {
   if (h->st) (void)hipFree(h->st);
   if (h->d_prof) (void)hipFree(h->d_prof);
   if (h->d_bp) (void)hipFree(h->d_bp);
+  if (h->up_ev) (void)hipEventDestroy(h->up_ev);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1764,6 +1801,7 @@ void ksim_destroy(ksim_handle* h) {
 const char* ksim_last_error(const ksim_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
 int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !p) return KSIM_E_INVALID;
   h->stab_dirty = true;                     // DevPods::stab: the static filter list may change
   if (p->n_filter < 0 || p->n_filter > KSIM_MAX_FILTER || p->n_score < 0 || p->n_score > KSIM_MAX_SCORE)
@@ -1867,6 +1905,7 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
 }
 
 int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !t || !v) return KSIM_E_INVALID;
   h->stab_dirty = true;
   HIPCHK(h, hipSetDevice(h->device));
@@ -2142,6 +2181,7 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
 // Loaded pods, the bound-pod table and captured graphs are dropped (node
 // positions changed).
 int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v, const int32_t* old_pos) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   // (a replica keeps its flag when the delta is refused; the new snapshot
   // below clears it: ksim_set_eval_range again)
   if (!h || !t || !v) return KSIM_E_INVALID;
@@ -2227,6 +2267,7 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
 // table handed to ksim_upsert_nodes is the current snapshot without it, so the
 // replay keeps every other node's state.
 int ksim_remove_node(ksim_handle* h, int32_t pos) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   h->stab_dirty = true;
   if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_remove_node on a shard handle");
@@ -2348,6 +2389,7 @@ int ksim_get_class_count(ksim_handle* h, int32_t* out) {
 }
 
 int ksim_get_next_start(ksim_handle* h, int32_t* next_start) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !next_start) return KSIM_E_INVALID;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hcopy(h, next_start, &h->st->next_start, 4, hipMemcpyDeviceToHost));
@@ -2355,6 +2397,7 @@ int ksim_get_next_start(ksim_handle* h, int32_t* next_start) {
 }
 
 int ksim_set_next_start(ksim_handle* h, int32_t next_start) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h) return KSIM_E_INVALID;
   if (h->has_cluster && (next_start < 0 || next_start >= std::max(h->dc.n, 1)))
     return set_err(h, KSIM_E_INVALID, "next_start out of range");
@@ -2364,6 +2407,7 @@ int ksim_set_next_start(ksim_handle* h, int32_t next_start) {
 }
 
 int ksim_set_pod_seq(ksim_handle* h, int64_t seq) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h) return KSIM_E_INVALID;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hcopy(h, &h->st->pod_seq, &seq, 8, hipMemcpyHostToDevice));
@@ -2451,6 +2495,7 @@ static int pin_reserve(ksim_handle* h, size_t bytes) {
 struct Copies {
   CopyList l{};
   int n = 0;
+  Copies() { l.anode = -1; }
   void add(const void* src, void* dst, size_t bytes) {
     if (!bytes) return;
     l.src[n] = (const uint8_t*)src;
@@ -2458,8 +2503,22 @@ struct Copies {
     l.n[n] = (uint32_t)bytes;
     n++;
   }
+  // a framework-driven filter pass's start in the same launch (launch_fw_begin)
+  void begin(DevState* st, WinState* win, int32_t first, int32_t end) {
+    l.bst = st;
+    l.bwin = win;
+    l.bfirst = first;
+    l.bend = end;
+  }
+  // a queued bind in the same launch
+  void bind(const DevCluster& c, const DevPods& P, int32_t node, int sign) {
+    l.ac = c;
+    l.aP = P;
+    l.anode = node;
+    l.asign = sign;
+  }
   int run(ksim_handle* h) {
-    if (n) launch_copy_list(l, n, h->stream);
+    if (n || l.bst || l.anode >= 0) launch_copy_list(l, n, h->stream);
     HIPCHK(h, hipGetLastError());
     return KSIM_OK;
   }
@@ -2480,10 +2539,15 @@ static int pout_reserve(ksim_handle* h, size_t bytes) {
   return KSIM_OK;
 }
 
-// Upload one pod (re-based) as a device pod set of its own: every piece packed
-// into the pinned staging, one copy into the arena (valid until the arena's
-// next upload).
-static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P, DevArena& arena) {
+// One pod (re-based) as a device pod set of its own, packed the way it is
+// uploaded: every piece at a 64-byte aligned offset of one blob.
+struct PodBlob {
+  std::vector<char> bytes;
+  size_t off[8];
+  int32_t n_nn, n_exprs, n_terms, n_uses, n_adds;
+};
+
+static void build_pod_blob(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, PodBlob& b) {
   ksim_pod pod;
   std::vector<ksim_label_expr> ex;
   std::vector<ksim_term> tm;
@@ -2499,52 +2563,97 @@ static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_ind
   struct Piece {
     const void* src;
     size_t bytes;
-    size_t off;
   };
-  Piece pc[8] = {{&pod, sizeof(pod), 0},
-                 {ex.data(), ex.size() * sizeof(ksim_label_expr), 0},
-                 {tm.data(), tm.size() * sizeof(ksim_term), 0},
-                 {nn.data(), 4 * nn.size(), 0},
-                 {bflag, sizeof(bflag), 0},
-                 {&plan, sizeof(plan), 0},
-                 {us.data(), us.size() * sizeof(ksim_topo_use), 0},
-                 {ad.data(), ad.size() * sizeof(ksim_class_add), 0}};
+  const Piece pc[8] = {{&pod, sizeof(pod)},
+                       {ex.data(), ex.size() * sizeof(ksim_label_expr)},
+                       {tm.data(), tm.size() * sizeof(ksim_term)},
+                       {nn.data(), 4 * nn.size()},
+                       {bflag, sizeof(bflag)},
+                       {&plan, sizeof(plan)},
+                       {us.data(), us.size() * sizeof(ksim_topo_use)},
+                       {ad.data(), ad.size() * sizeof(ksim_class_add)}};
   size_t total = 0;
-  for (auto& x : pc) {
-    x.off = total;
-    total += (std::max<size_t>(x.bytes, 16) + 63) & ~(size_t)63;
+  for (int q = 0; q < 8; q++) {
+    b.off[q] = total;
+    total += (std::max<size_t>(pc[q].bytes, 16) + 63) & ~(size_t)63;
   }
-  HIPCHK(h, hipStreamSynchronize(h->stream));     // the staging and the arena are free again
-  int rc;
-  if ((rc = pin_reserve(h, total)) || (rc = arena_reserve(h, arena, total))) return rc;
-  for (auto& x : pc)
-    if (x.bytes) std::memcpy((char*)h->pin + x.off, x.src, x.bytes);
-  Copies cp;
-  cp.add(h->pin_d, arena.p, total);
-  if ((rc = cp.run(h))) return rc;
-  char* d = (char*)arena.p;
-  P = DevPods{};
-  P.pods = (const ksim_pod*)(d + pc[0].off);
-  P.exprs = (const ksim_label_expr*)(d + pc[1].off);
-  P.terms = (const ksim_term*)(d + pc[2].off);
-  P.nn = (const int32_t*)(d + pc[3].off);
-  P.n_nn = (int32_t)nn.size();
-  P.bflags = (const int32_t*)(d + pc[4].off);
-  P.plans = (const PodPlan*)(d + pc[5].off);
-  P.uses = (const ksim_topo_use*)(d + pc[6].off);
-  P.adds = (const ksim_class_add*)(d + pc[7].off);
+  b.bytes.assign(total, 0);                // zero padding: blobs of one pod compare equal
+  for (int q = 0; q < 8; q++)
+    if (pc[q].bytes) std::memcpy(b.bytes.data() + b.off[q], pc[q].src, pc[q].bytes);
+  b.n_nn = (int32_t)nn.size();
+  b.n_exprs = (int32_t)ex.size();
+  b.n_terms = (int32_t)tm.size();
+  b.n_uses = (int32_t)us.size();
+  b.n_adds = (int32_t)ad.size();
+}
+
+// The device pod set of a blob uploaded at d.
+static DevPods blob_pods(const ksim_handle* h, const PodBlob& b, char* d) {
+  DevPods P{};
+  P.pods = (const ksim_pod*)(d + b.off[0]);
+  P.exprs = (const ksim_label_expr*)(d + b.off[1]);
+  P.terms = (const ksim_term*)(d + b.off[2]);
+  P.nn = (const int32_t*)(d + b.off[3]);
+  P.n_nn = b.n_nn;
+  P.bflags = (const int32_t*)(d + b.off[4]);
+  P.plans = (const PodPlan*)(d + b.off[5]);
+  P.uses = (const ksim_topo_use*)(d + b.off[6]);
+  P.adds = (const ksim_class_add*)(d + b.off[7]);
   P.n_pods = 1;
-  P.n_exprs = (int32_t)ex.size();
-  P.n_terms = (int32_t)tm.size();
+  P.n_exprs = b.n_exprs;
+  P.n_terms = b.n_terms;
   // this pod's binds keep the loaded queue's persistent tables (its plan reads
   // none of them: no kPlanPtab on single uploads)
   P.ptab = h->dp.ptab;
   P.ptab_ent = h->dp.ptab_ent;
   P.ptab_cfirst = h->dp.ptab_cfirst;
   P.ptab_cidx = h->dp.ptab_cidx;
-  P.n_uses = (int32_t)us.size();
-  P.n_adds = (int32_t)ad.size();
+  P.n_uses = b.n_uses;
+  P.n_adds = b.n_adds;
+  return P;
+}
+
+// The blob into the pinned staging and, by one copy kernel, into the arena
+// (valid until the arena's next upload).  The staging is reused once the last
+// upload's copy has run (its event), not after the whole stream drains; a
+// growing staging or arena drains the stream first.  begin_win: a
+// framework-driven filter pass's start in the same launch.
+static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPods& P,
+                       WinState* begin_win = nullptr, bool record = false) {
+  const size_t total = b.bytes.size();
+  if (total > h->pin_cap || total > arena.cap) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  } else if (h->up_pending) {
+    HIPCHK(h, hipEventSynchronize(h->up_ev));
+  }
+  h->up_pending = false;
+  int rc;
+  if ((rc = pin_reserve(h, total)) || (rc = arena_reserve(h, arena, total))) return rc;
+  std::memcpy(h->pin, b.bytes.data(), total);
+  Copies cp;
+  cp.add(h->pin_d, arena.p, total);
+  if (begin_win) cp.begin(h->st, begin_win, 0, 1);
+  if (record && h->pend_bind.on) {         // the last cycle's queued Reserve, ahead of this pass
+    cp.bind(h->dc, h->pend_bind.P, h->pend_bind.node, h->pend_bind.sign);
+    h->pend_bind.on = false;
+  }
+  if ((rc = cp.run(h))) return rc;
+  if (!h->up_ev) HIPCHK(h, hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming));
+  HIPCHK(h, hipEventRecord(h->up_ev, h->stream));
+  h->up_pending = true;
+  P = blob_pods(h, b, (char*)arena.p);
+  if (record || &arena == &h->pod1_arena) {   // what a Reserve of this pod binds from
+    h->pod1_blob = b.bytes;
+    h->pod1_base = (char*)arena.p;
+  }
   return KSIM_OK;
+}
+
+// Upload one pod (re-based) as a device pod set of its own.
+static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P, DevArena& arena) {
+  PodBlob b;
+  build_pod_blob(h, ps, pod_index, b);
+  return upload_blob(h, b, arena, P);
 }
 
 static int upload_single(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, DevPods& P) {
@@ -2673,7 +2782,13 @@ int ksim_eval_pod_finish(ksim_handle* h, const uint8_t* ext_fail, const int64_t*
 // (wrappedplugin.go:356-375, 491-516, 583-584).  These entry points answer the
 // engine-backed plugins under those choices.
 int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, ksim_eval_out* out) {
-  int rc = ensure_ready(h);        // abandons any framework cycle in flight
+  // a queued Reserve of the last cycle runs inside this pass's upload launch;
+  // with Unreserves queued behind it (deferred_binds) it is launched first
+  if (h && h->pend_bind.on && !h->deferred_binds.empty()) {
+    const int prc = flush_pend_bind(h);
+    if (prc) return prc;
+  }
+  int rc = ensure_ready(h, false, true);   // abandons any framework cycle in flight
   if (rc) return rc;
   if (!ps || !out || pod_index < 0 || pod_index >= ps->n_pods || !ps->pods)
     return set_err(h, KSIM_E_INVALID, "bad pod set / index");
@@ -2683,58 +2798,76 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   h->ext_pending = false;
   h->fw_list.clear();                // a new cycle: no normalization answered from the last one
   h->fw_raw.clear();
-  if ((rc = upload_single(h, ps, pod_index, h->pod1))) return rc;
-  // the run header, the window state and the two topology flags (OR-ed by the
-  // PreFilter pass and reset by a bind, which a framework cycle does not run)
-  launch_fw_begin(h->st, h->sc.win, 0, 1, h->stream);
   const ksim_pod& p = ps->pods[pod_index];
-  launch_fw_filter(make_args(h, h->pod1, nullptr), h->stream, p.use_count > 0);
-  HIPCHK(h, hipGetLastError());
-  h->fw_dom_dirty = p.use_count > 0;
-  h->fw_topo = p.use_count > 0;
   const size_t N = (size_t)h->dc.n;
-  h->fw_fail.resize(N);
+  const int S = h->prof.n_score;
   // Score on the host (ksim_fw_score) unless a PreScore reads the framework's
   // list: PodTopologySpread's ScheduleAnyway constraints (IgnoredNodes, pair
   // counts over the list); NetworkBandwidth's Score may fail the cycle
-  const int S = h->prof.n_score;
   bool host = S > 0 && !profile_nb(h->prof) && !(p.flags & KSIM_POD_NODE_NAMES_UNKNOWN);
   for (int32_t u = 0; host && u < p.use_count; u++)
     if (ps->uses[p.use_first + u].kind == KSIM_USE_PTS_SOFT) host = false;
   h->fw_host = host;
-  if (host) {
-    const size_t need = ((8 * (size_t)S * N + 63) & ~(size_t)63) + 8 * N;
-    if (need > h->fwh_cap) {
-      HIPCHK(h, hipStreamSynchronize(h->stream));
-      if (h->fwh) (void)hipHostFree(h->fwh);
-      h->fwh = h->fwh_d = nullptr;
-      h->fwh_cap = 0;
-      hipError_t e = hipHostMalloc(&h->fwh, need, hipHostMallocCoherent | hipHostMallocMapped);
-      if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (fw scores)");
-      if ((e = hipHostGetDevicePointer(&h->fwh_d, h->fwh, 0)) != hipSuccess)
-        return hip_fail(h, e, "hipHostGetDevicePointer");
-      h->fwh_cap = need;
+  // a pod without topology uses: the filter kernel writes its answers straight
+  // to the pinned staging (fwh), no copy launch; with uses, the topology flags
+  // are the PreFilter pass's, copied after it
+  const bool mirror = p.use_count == 0;
+  // fwh: [head 64][fail N][detail 4N][raw S x N][part N], 64-byte aligned pieces
+  const size_t o_fail = 64, o_det = o_fail + ((N + 63) & ~(size_t)63),
+               o_raw = o_det + ((4 * N + 63) & ~(size_t)63), o_part = o_raw + ((8 * (size_t)S * N + 63) & ~(size_t)63),
+               need = o_part + 8 * N;
+  if (need > h->fwh_cap) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->fwh) (void)hipHostFree(h->fwh);
+    h->fwh = h->fwh_d = nullptr;
+    h->fwh_cap = 0;
+    hipError_t e = hipHostMalloc(&h->fwh, need, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (fw answers)");
+    if ((e = hipHostGetDevicePointer(&h->fwh_d, h->fwh, 0)) != hipSuccess)
+      return hip_fail(h, e, "hipHostGetDevicePointer");
+    h->fwh_cap = need;
+  }
+  char* fo = (char*)h->fwh;
+  char* fd = (char*)h->fwh_d;
+  // the pod, and the run header / window state / topology flags reset, in one
+  // launch (upload_blob's begin job)
+  {
+    PodBlob b;
+    build_pod_blob(h, ps, pod_index, b);
+    h->fw_flip ^= 1;
+    if ((rc = upload_blob(h, b, h->fw_arena[h->fw_flip], h->pod1, h->sc.win, true))) return rc;
+  }
+  LaunchArgs a = make_args(h, h->pod1, nullptr);
+  if (mirror) {
+    a.s.m_head = (int32_t*)fd;
+    a.s.m_fail = (uint8_t*)(fd + o_fail);
+    a.s.m_detail = out->fail_detail ? (uint32_t*)(fd + o_det) : nullptr;
+    a.s.m_raw = host ? (int32_t*)(fd + o_raw) : nullptr;
+    a.s.m_part = host ? (int32_t*)(fd + o_part) : nullptr;
+    reinterpret_cast<int32_t*>(fo)[1] = 0;        // the kernel's too-wide flag
+  }
+  launch_fw_filter(a, h->stream, p.use_count > 0);
+  HIPCHK(h, hipGetLastError());
+  h->fw_dom_dirty = p.use_count > 0;
+  h->fw_topo = p.use_count > 0;
+  h->fw_fail.resize(N);
+  if (!mirror) {
+    // the results into the same staging, one copy launch: next_start, the
+    // topology flags, the filter codes, the details (and the raw scores)
+    Copies cp;
+    cp.add(&h->st->next_start, fd, sizeof(int32_t));
+    cp.add(&h->st->topo_flags, fd + 4, sizeof(uint32_t));
+    cp.add(h->sc.fail, fd + o_fail, N);
+    if (out->fail_detail) cp.add(h->sc.detail, fd + o_det, 4 * N);
+    if (host) {
+      cp.add(h->sc.raw, fd + o_raw, 8 * (size_t)S * N);
+      cp.add(h->sc.part, fd + o_part, 8 * N);
     }
+    if ((rc = cp.run(h))) return rc;
   }
-  // the results into pinned staging, one synchronization: next_start, the
-  // topology flags, the filter codes, the details (and the raw scores)
-  const size_t o_fail = 64, o_det = 64 + ((N + 63) & ~(size_t)63);
-  if ((rc = pout_reserve(h, o_det + 4 * N))) return rc;
-  char* po = (char*)h->pout;
-  char* pd = (char*)h->pout_d;
-  Copies cp;
-  cp.add(&h->st->next_start, pd, sizeof(int32_t));
-  cp.add(&h->st->topo_flags, pd + 4, sizeof(uint32_t));
-  cp.add(h->sc.fail, pd + o_fail, N);
-  if (out->fail_detail) cp.add(h->sc.detail, pd + o_det, 4 * N);
-  if (host) {
-    cp.add(h->sc.raw, h->fwh_d, 8 * (size_t)S * N);
-    cp.add(h->sc.part, (char*)h->fwh_d + ((8 * (size_t)S * N + 63) & ~(size_t)63), 8 * N);
-  }
-  if ((rc = cp.run(h))) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  std::memcpy(h->fw_fail.data(), po + o_fail, N);
-  if (out->fail_detail) std::memcpy(out->fail_detail, po + o_det, 4 * N);
+  std::memcpy(h->fw_fail.data(), fo + o_fail, N);
+  if (out->fail_detail) std::memcpy(out->fail_detail, fo + o_det, 4 * N);
   int32_t ns = h->dc.n;
   if (p.flags & KSIM_POD_NODE_NAMES) ns = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 0 : p.nn_count;
   int32_t nf = 0;
@@ -2744,8 +2877,14 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
     strip_fail_errors(out->fail_plugin, N);
   }
   int32_t next = 0;
-  std::memcpy(&next, po, sizeof(next));
-  std::memcpy(&h->fw_tflags, po + 4, sizeof(uint32_t));
+  std::memcpy(&next, fo, sizeof(next));
+  h->fw_tflags = 0;
+  if (!mirror) std::memcpy(&h->fw_tflags, fo + 4, sizeof(uint32_t));
+  h->fw_oraw = o_raw;
+  h->fw_opart = o_part;
+  h->fw_raw32 = mirror;
+  if (mirror && host && reinterpret_cast<const int32_t*>(fo)[1] != 0)
+    h->fw_host = false;                  // a raw score past int32: ksim_fw_score on the device
   const bool unknown = (p.flags & KSIM_POD_NODE_NAMES_UNKNOWN) != 0;
   out->chosen = unknown ? KSIM_CHOSEN_ERROR : -1;
   out->status = unknown ? KSIM_STATUS_ERROR : 0;
@@ -2868,8 +3007,15 @@ static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_e
     seen[x] = 1;
   }
   for (int32_t j = 0; j < n; j++) seen[nodes[j]] = 0;
-  const int64_t* raw = (const int64_t*)h->fwh;
-  const int64_t* part = (const int64_t*)((const char*)h->fwh + ((8 * (size_t)S * N + 63) & ~(size_t)63));
+  const char* rawb = (const char*)h->fwh + h->fw_oraw;
+  const char* partb = (const char*)h->fwh + h->fw_opart;
+  const bool w32 = h->fw_raw32;
+  auto raw_at = [&](size_t i) -> int64_t {
+    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(rawb)[i] : reinterpret_cast<const int64_t*>(rawb)[i];
+  };
+  auto part_at = [&](size_t i) -> int64_t {
+    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(partb)[i] : reinterpret_cast<const int64_t*>(partb)[i];
+  };
   const bool scored = n > 1;
   const bool ipa_nonempty = (h->fw_tflags & kTopoScoreNonEmpty) != 0;
   h->fw_list.assign(nodes, nodes + n);
@@ -2878,12 +3024,11 @@ static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_e
   std::vector<int64_t>& tot = h->fw_tot;
   tot.assign(n, 0);
   if (scored) {
-    for (int32_t j = 0; j < n; j++) tot[j] = part[nodes[j]];
+    for (int32_t j = 0; j < n; j++) tot[j] = part_at((size_t)nodes[j]);
     for (int k = 0; k < S; k++) {
       int64_t* r = h->fw_raw.data() + (size_t)k * n;
       int64_t* nv = h->fw_norm.data() + (size_t)k * n;
-      const int64_t* src = raw + (size_t)k * N;
-      for (int32_t j = 0; j < n; j++) r[j] = src[nodes[j]];
+      for (int32_t j = 0; j < n; j++) r[j] = raw_at((size_t)k * N + (size_t)nodes[j]);
       const int32_t kind = norm_kind(h->prof.score[k]);
       if (kind == kNormNone) {
         std::memcpy(nv, r, 8 * (size_t)n);
@@ -2895,9 +3040,20 @@ static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_e
         gmin = std::min(gmin, r[j]);
       }
       const int64_t w = h->prof.score_weight[k] == 0 ? 1 : h->prof.score_weight[k];
+      // a list's raw scores take few distinct values: each value's normalized
+      // score once (a 64-entry direct-mapped memo), not a division per node
+      int64_t mk[64], mv[64];
+      bool mset[64] = {};
       for (int32_t j = 0; j < n; j++) {
-        nv[j] = host_normalize(kind, r[j], gmax, gmin, ipa_nonempty);
-        tot[j] += nv[j] * w;
+        const int64_t v = r[j];
+        const uint32_t e = (uint32_t)((uint64_t)v * 0x9E3779B97F4A7C15ull >> 58);
+        if (!mset[e] || mk[e] != v) {
+          mset[e] = true;
+          mk[e] = v;
+          mv[e] = host_normalize(kind, v, gmax, gmin, ipa_nonempty);
+        }
+        nv[j] = mv[e];
+        tot[j] += mv[e] * w;
       }
     }
   }
@@ -3079,7 +3235,21 @@ int ksim_fw_normalize(ksim_handle* h, int32_t score_slot, const int32_t* nodes, 
 static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, int32_t node, int sign) {
   DevPods P;
   int rc;
-  if ((rc = upload_single(h, ps, pod_index, P, h->asm_arena))) return rc;
+  if ((rc = flush_pend_bind(h))) return rc;
+  PodBlob b;
+  build_pod_blob(h, ps, pod_index, b);
+  if (h->pod1_base && b.bytes == h->pod1_blob) {
+    // the pod the last filter pass uploaded (the framework's Reserve of the
+    // cycle's pod): bind from its arena copy, queued (pend_bind) until the
+    // next call: the next framework-driven pass runs it inside its upload
+    // launch (into the other arena), any other call launches it first
+    h->pend_bind.P = blob_pods(h, b, h->pod1_base);
+    h->pend_bind.node = node;
+    h->pend_bind.sign = sign;
+    h->pend_bind.on = true;
+    return KSIM_OK;
+  }
+  if ((rc = upload_blob(h, b, h->asm_arena, P))) return rc;
   launch_assume(h->dc, P, 0, node, sign, h->stream);
   HIPCHK(h, hipGetLastError());
   // no synchronization: every later call is ordered after it on the stream,
@@ -3090,6 +3260,8 @@ static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
 // the queued Unreserves, when no framework cycle sits between PreFilter and
 // Score (the state getters read the cache's view)
 static int flush_idle(ksim_handle* h) {
+  int rc = flush_pend_bind(h);
+  if (rc) return rc;
   return (!h->fw_pending && !h->deferred_binds.empty()) ? flush_deferred_binds(h) : KSIM_OK;
 }
 
@@ -3533,6 +3705,7 @@ int ksim_schedule_loaded(ksim_handle* h, int32_t first, int32_t count, int32_t* 
 }
 
 int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h) return KSIM_E_INVALID;
   h->stab_dirty = true;
   if (node_base < 0 || n_total < 0 || n_total > KSIM_MAX_NODES || node_base > n_total)
@@ -3544,6 +3717,7 @@ int ksim_set_shard(ksim_handle* h, int32_t node_base, int32_t n_total) {
 }
 
 int ksim_set_eval_range(ksim_handle* h, int32_t eval_lo, int32_t eval_hi) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h) return KSIM_E_INVALID;
   if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_set_eval_range needs the cluster (ksim_set_cluster)");
   if (h->shard_total != 0) return set_err(h, KSIM_E_INVALID, "a node-shard handle holds only its nodes: no eval range");
@@ -3566,6 +3740,7 @@ int ksim_comm_unique_id(uint8_t* id) {
 }
 
 int ksim_comm_init(ksim_handle* h, int32_t rank, int32_t world, const uint8_t* id) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !id) return KSIM_E_INVALID;
   if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
     return set_err(h, KSIM_E_INVALID, "world must be 1.." + std::to_string(kMaxShards));
@@ -3656,6 +3831,7 @@ int ksim_schedule_batch(ksim_handle* h, const ksim_pod_set* ps, int32_t* chosen,
 }
 
 int ksim_reset_cluster(ksim_handle* h) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");
   h->stab_dirty = true;
   HIPCHK(h, hipSetDevice(h->device));
@@ -4077,6 +4253,7 @@ extern "C" int ksim_preempt_nominated(ksim_handle* h, const ksim_pod_set* ps, in
 
 // ---- selector / affinity-term matching (ksim_match.hip) ------
 extern "C" int ksim_match_terms(ksim_handle* h, const ksim_match_problem* mp, uint32_t* match_bits, int32_t* counts) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !mp || !match_bits) return set_err(h, KSIM_E_INVALID, "null argument");
   const ksim_match_problem& q = *mp;
   if (q.n_sigs < 0 || q.n_feat < 0 || q.n_reqs < 0 || q.n_matchers < 0 || q.n_pods < 0 || q.n_nodes < 0 ||

@@ -181,6 +181,16 @@ struct CopyList {
   const uint8_t* src[kCopyPieces];
   uint8_t* dst[kCopyPieces];
   uint32_t n[kCopyPieces];
+  // optional (bst non-null): a framework-driven filter pass's start in the same
+  // launch (launch_fw_begin's work, by block (0, 0))
+  DevState* bst;
+  WinState* bwin;
+  int32_t bfirst, bend;
+  // optional (anode >= 0): a queued Reserve / Unreserve (assume_pod of pod 0 of
+  // aP on node anode, sign asign) in the same launch, by block (0, 0)
+  int32_t anode, asign;
+  DevCluster ac;
+  DevPods aP;
 };
 void launch_copy_list(const CopyList& l, int count, hipStream_t stream);
 void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,

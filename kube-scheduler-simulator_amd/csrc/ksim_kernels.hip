@@ -349,8 +349,11 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   const int32_t xr = node < c.n ? node : c.n - 1;
   const NodeRow r = load_row(c, xr);
   const double inv_c = c.inv_cpu[xr], inv_m = c.inv_mem[xr];
-  const int32_t pi = st->cursor;
-  if (pi >= st->end) return;
+  // a framework-driven pass mirrored to the host (m_head) runs pod 0 of its
+  // single-pod set (ksim_fw_prefilter's begin job): no state load first
+  const bool fwm = COMPAT && s.m_head != nullptr;
+  const int32_t pi = fwm ? 0 : st->cursor;
+  if (!fwm && pi >= st->end) return;
   // the pod record and its uses sit at a block-uniform address: scalar loads
   const DevPods& P = P0;
   const ksim_pod& p = P0.pods[pi];                // block-uniform address: scalar loads where used
@@ -377,9 +380,12 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
   bool scanned = true;
   if (p.flags & KSIM_POD_NODE_NAMES)              // block-uniform: NodeAffinity's PreFilterResult
     scanned = node < c.n && scan_pos(scan_set(c, P, p, st->next_start), c.base + node) >= 0;
+  if (fwm && blockIdx.x == 0 && threadIdx.x == 0) s.m_head[0] = st->next_start;
   if (node < c.n && !scanned) {                   // never handed to Filter
     s.fail[node] = KSIM_NOT_EVALUATED;
     if (COMPAT) s.detail[node] = 0;
+    if (COMPAT && s.m_fail) s.m_fail[node] = KSIM_NOT_EVALUATED;
+    if (COMPAT && s.m_detail) s.m_detail[node] = 0;
   } else if (node < c.n) {
     const uint32_t tf = !p.use_count ? 0u : pt ? ((m.aff | m.score) ? s_tf : 0u) : st->topo_flags;
 #ifdef KSIM_FS_CLOCKS
@@ -402,6 +408,8 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
     FS_CLK(3);
     s.fail[node] = res;
     if (COMPAT) s.detail[node] = det;
+    if (COMPAT && s.m_fail) s.m_fail[node] = res;
+    if (COMPAT && s.m_detail) s.m_detail[node] = det;
     feasible = res == KSIM_PASSED;
     if (feasible) {
       // PodTopologySpread IgnoredNodes candidates: feasible nodes missing a soft key
@@ -416,6 +424,19 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
       const BatchProg* fast = (bp->fast_w && (c.cflags & kClusterNarrow)) ? bp : nullptr;
       s.part[node] = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT, rv,
                                     soft_cnt, fast, inv_c, inv_m);
+      if (COMPAT && s.m_raw) {                     // the feasible node's answers in the host's staging too,
+        const size_t N = (size_t)c.n;                // as int32 (m_head[1] = 1: a value did not fit)
+        bool wide = false;
+        for (int k = 0; k < prof.n_score; k++) {
+          const int64_t v = s.raw[(size_t)k * N + node];
+          wide |= v != (int64_t)(int32_t)v;
+          s.m_raw[(size_t)k * N + node] = (int32_t)v;
+        }
+        const int64_t v = s.part[node];
+        wide |= v != (int64_t)(int32_t)v;
+        s.m_part[node] = (int32_t)v;
+        if (wide) s.m_head[1] = 1;
+      }
     }
   }
   FS_CLK(4);
@@ -1517,7 +1538,21 @@ void launch_fw_score(const LaunchArgs& a, hipStream_t stream) {
 // the framework-driven calls, where a DMA copy per piece costs more than the
 // bytes (up to kCopyPieces pieces; 16-byte accesses when a piece is at least
 // 16 bytes, its addresses then 16-byte aligned; byte accesses for the tail).
+__device__ __forceinline__ void fw_begin_block(DevState* __restrict__ st, WinState* __restrict__ win, int32_t first,
+                                               int32_t end) {
+  for (int x = threadIdx.x; x < (int)(sizeof(WinState) / 4); x += blockDim.x)
+    reinterpret_cast<uint32_t*>(win)[x] = 0;
+  if (threadIdx.x == 0) {
+    st->cursor = first;
+    st->end = end;
+    st->topo_flags = 0;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy_list(CopyList l) {
+  if (l.bst && blockIdx.x == 0 && blockIdx.y == 0) fw_begin_block(l.bst, l.bwin, l.bfirst, l.bend);
+  if (l.anode >= 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    assume_pod(l.ac, l.aP, l.aP.pods[0], l.anode, l.asign);
   const int q = blockIdx.y;
   const uint8_t* src = l.src[q];
   uint8_t* dst = l.dst[q];
@@ -1531,7 +1566,9 @@ void launch_copy_list(const CopyList& l, int count, hipStream_t stream) {
   uint32_t mx = 0;
   for (int q = 0; q < count; q++) mx = l.n[q] > mx ? l.n[q] : mx;
   const uint32_t blocks = ((mx >> 4) + 255) / 256;
-  k_copy_list<<<dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks, count), 256, 0, stream>>>(l);
+  CopyList x = l;
+  if (count == 0) x.n[0] = 0;                    // the begin job alone: one block, nothing to copy
+  k_copy_list<<<dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks, count > 0 ? count : 1), 256, 0, stream>>>(x);
 }
 
 // ksim_fw_score's answers for the listed nodes only: comp = [raw S x n][norm
@@ -1565,13 +1602,7 @@ void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int3
 // and the window state, in one launch (set_run's copy and two memsets).
 __global__ __launch_bounds__(256) void k_fw_begin(DevState* __restrict__ st, WinState* __restrict__ win,
                                                   int32_t first, int32_t end) {
-  for (int x = threadIdx.x; x < (int)(sizeof(WinState) / 4); x += blockDim.x)
-    reinterpret_cast<uint32_t*>(win)[x] = 0;
-  if (threadIdx.x == 0) {
-    st->cursor = first;
-    st->end = end;
-    st->topo_flags = 0;
-  }
+  fw_begin_block(st, win, first, end);
 }
 
 void launch_fw_begin(DevState* st, WinState* win, int32_t first, int32_t end, hipStream_t stream) {

@@ -116,6 +116,46 @@ def test_framework_driven_cycles(kind, seed):
         assert nominated > 0
 
 
+def test_queued_reserve_lands_before_every_other_call():
+    """The framework's Reserve of the cycle's pod is queued (ksim_assume binds
+    from the pod's upload) and runs inside the next ksim_fw_prefilter's upload
+    launch; any other call lands it first.  Cycles interleaved with state
+    reads, next-start writes and a cluster reset keep the node state equal to
+    the oracle's after every step."""
+    cluster, pods = gen.config1(n_nodes=200, n_pods=120)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    w = profile.default_score_weights()
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    se, so = Store(w), Store(w)
+    fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, se, seed=3)
+    fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, so, seed=3)
+
+    def same_state():
+        es, os_ = eng.node_state(), ora.node_state()
+        for k in es:
+            np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+
+    for i in range(pods.n_pods):
+        re, ro = fe.schedule_one(pods, i, 0, None), fo.schedule_one(pods, i, 0, None)
+        assert re.get("chosen") == ro.get("chosen"), i
+        if i % 7 == 3:
+            same_state()                        # a getter: the queued Reserve lands now
+        if i % 11 == 5:
+            eng.set_next_start(eng.next_start)
+        if i == 60:
+            same_state()
+            eng.reset_cluster()                 # the queued Reserve first, then the reset
+            ora = Oracle(cluster.copy_state(), prof)
+            fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, so, seed=3)
+            fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, se, seed=3)
+            same_state()
+    same_state()
+
+
 def test_fw_api_lists_and_normalize():
     """ksim_fw_prefilter answers every node; ksim_fw_score over arbitrary
     feasible sublists (any order) and ksim_fw_normalize over lists that are

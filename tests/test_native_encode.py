@@ -267,12 +267,20 @@ def test_template_cluster():
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "go", "*.json.gz"))),
                          ids=os.path.basename)
 def test_go_documents(path):
+    """The Go-harness fixtures with their plugin args, workloads, volumes and
+    scalar resources (tests/gofixture.py encode's inputs)."""
+    import gofixture
     with gzip.open(path, "rb") as f:
         doc = json.loads(f.read())
-    nodes = [node_from_dict(d) for d in doc["nodes"]]
-    bound = [pod_from_dict(d) for d in doc["boundPods"]]
-    pods = [pod_from_dict(d) for d in doc["pods"]]
-    both(nodes, bound, [pods], cluster_kw={"namespaces": doc["namespaces"]})
+    nodes, bound, pods = gofixture.objects(doc)
+    sp = gofixture.scheduler_profile(doc)
+    services, controllers = gofixture.workloads(doc)
+    _, _, vol = gofixture.volumes(doc, nodes)
+    scalar = sorted({k for p in pods for c in p.containers + p.init_containers for k in c.requests
+                     if k not in ("cpu", "memory", "ephemeral-storage", "pods")})
+    both(nodes, bound, [pods], cluster_kw={"namespaces": doc["namespaces"], "extra_scalar": scalar},
+         pods_kw={"volumes": vol, "added_affinity": sp.node_affinity,
+                  "spread": SpreadDefaults(sp.spread, services, controllers)})
 
 
 def test_node_deltas_keep_classes():

@@ -280,12 +280,12 @@ struct DevScratch {
   // framework-driven filter pass (ksim_fw_prefilter), pods without topology
   // uses: the answers written straight to the host's pinned staging (device
   // addresses; else null): next_start and a too-wide flag, the codes, the
-  // details, each feasible node's raw scores [S][n] and weighted part as int32
+  // details, each feasible node's row [n][S + 1] of its raw scores and
+  // weighted part as int32 (one cache line per node for the host's reads)
   int32_t* m_head;
   uint8_t* m_fail;
   uint32_t* m_detail;
   int32_t* m_raw;
-  int32_t* m_part;
   uint64_t* xsend;       // sharded: [kBatchPods][kXRec] this shard's candidate records
   uint64_t* xrecv;       // sharded: [world][kBatchPods][kXRec] all shards' records
   int64_t* dom;          // [KSIM_MAX_USES][vmax] topology-pair sums of the current pod (zero between pods)

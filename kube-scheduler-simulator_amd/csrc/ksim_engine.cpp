@@ -79,6 +79,14 @@ struct DevArena {
 
 }  // namespace
 
+// One pod (re-based) as a device pod set of its own, packed the way it is
+// uploaded: every piece at a 64-byte aligned offset of one blob.
+struct PodBlob {
+  std::vector<char> bytes;
+  size_t off[8];
+  int32_t n_nn, n_exprs, n_terms, n_uses, n_adds;
+};
+
 struct ksim_handle {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -177,6 +185,14 @@ struct ksim_handle {
   bool up_pending = false;
   std::vector<char> pod1_blob;
   char* pod1_base = nullptr;
+  // build_pod_blob's pieces and the framework-driven pass's blob, kept so the
+  // per-cycle calls reuse their capacity
+  std::vector<ksim_label_expr> bs_ex;
+  std::vector<ksim_term> bs_tm;
+  std::vector<ksim_topo_use> bs_us;
+  std::vector<ksim_class_add> bs_ad;
+  std::vector<int32_t> bs_nn;
+  PodBlob fw_blob;
   // the framework-driven filter passes alternate two arenas, so the Reserve of
   // cycle i (binding from cycle i's arena) can wait, queued, and run inside
   // cycle i+1's upload launch (pend_bind); any other call launches it first
@@ -2539,21 +2555,16 @@ static int pout_reserve(ksim_handle* h, size_t bytes) {
   return KSIM_OK;
 }
 
-// One pod (re-based) as a device pod set of its own, packed the way it is
-// uploaded: every piece at a 64-byte aligned offset of one blob.
-struct PodBlob {
-  std::vector<char> bytes;
-  size_t off[8];
-  int32_t n_nn, n_exprs, n_terms, n_uses, n_adds;
-};
-
 static void build_pod_blob(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index, PodBlob& b) {
   ksim_pod pod;
-  std::vector<ksim_label_expr> ex;
-  std::vector<ksim_term> tm;
-  std::vector<ksim_topo_use> us;
-  std::vector<ksim_class_add> ad;
-  std::vector<int32_t> nn;
+  std::vector<ksim_label_expr>& ex = h->bs_ex;
+  std::vector<ksim_term>& tm = h->bs_tm;
+  std::vector<ksim_topo_use>& us = h->bs_us;
+  std::vector<ksim_class_add>& ad = h->bs_ad;
+  std::vector<int32_t>& nn = h->bs_nn;
+  ex.clear();                              // single_pod_set appends
+  tm.clear();
+  nn.clear();
   single_pod_set(ps, pod_index, pod, ex, tm, us, ad, nn);
   mark_unique(h, us.data(), us.size());
   int32_t bflag[4] = {0, 0, 0, 0};
@@ -2577,7 +2588,7 @@ static void build_pod_blob(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_i
     b.off[q] = total;
     total += (std::max<size_t>(pc[q].bytes, 16) + 63) & ~(size_t)63;
   }
-  b.bytes.assign(total, 0);                // zero padding: blobs of one pod compare equal
+  b.bytes.assign(total, 0);                // zero padding: blobs of one pod compare equal (capacity reused)
   for (int q = 0; q < 8; q++)
     if (pc[q].bytes) std::memcpy(b.bytes.data() + b.off[q], pc[q].src, pc[q].bytes);
   b.n_nn = (int32_t)nn.size();
@@ -2619,7 +2630,7 @@ static DevPods blob_pods(const ksim_handle* h, const PodBlob& b, char* d) {
 // growing staging or arena drains the stream first.  begin_win: a
 // framework-driven filter pass's start in the same launch.
 static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPods& P,
-                       WinState* begin_win = nullptr, bool record = false) {
+                       WinState* begin_win = nullptr, bool record = false, bool synced = false) {
   const size_t total = b.bytes.size();
   if (total > h->pin_cap || total > arena.cap) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2638,9 +2649,11 @@ static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPod
     h->pend_bind.on = false;
   }
   if ((rc = cp.run(h))) return rc;
-  if (!h->up_ev) HIPCHK(h, hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming));
-  HIPCHK(h, hipEventRecord(h->up_ev, h->stream));
-  h->up_pending = true;
+  if (!synced) {                           // synced: the caller drains the stream before returning
+    if (!h->up_ev) HIPCHK(h, hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(h->up_ev, h->stream));
+    h->up_pending = true;
+  }
   P = blob_pods(h, b, (char*)arena.p);
   if (record || &arena == &h->pod1_arena) {   // what a Reserve of this pod binds from
     h->pod1_blob = b.bytes;
@@ -2831,19 +2844,15 @@ int ksim_fw_prefilter(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
   char* fd = (char*)h->fwh_d;
   // the pod, and the run header / window state / topology flags reset, in one
   // launch (upload_blob's begin job)
-  {
-    PodBlob b;
-    build_pod_blob(h, ps, pod_index, b);
-    h->fw_flip ^= 1;
-    if ((rc = upload_blob(h, b, h->fw_arena[h->fw_flip], h->pod1, h->sc.win, true))) return rc;
-  }
+  build_pod_blob(h, ps, pod_index, h->fw_blob);
+  h->fw_flip ^= 1;
+  if ((rc = upload_blob(h, h->fw_blob, h->fw_arena[h->fw_flip], h->pod1, h->sc.win, true, true))) return rc;
   LaunchArgs a = make_args(h, h->pod1, nullptr);
   if (mirror) {
     a.s.m_head = (int32_t*)fd;
     a.s.m_fail = (uint8_t*)(fd + o_fail);
     a.s.m_detail = out->fail_detail ? (uint32_t*)(fd + o_det) : nullptr;
     a.s.m_raw = host ? (int32_t*)(fd + o_raw) : nullptr;
-    a.s.m_part = host ? (int32_t*)(fd + o_part) : nullptr;
     reinterpret_cast<int32_t*>(fo)[1] = 0;        // the kernel's too-wide flag
   }
   launch_fw_filter(a, h->stream, p.use_count > 0);
@@ -3007,14 +3016,19 @@ static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_e
     seen[x] = 1;
   }
   for (int32_t j = 0; j < n; j++) seen[nodes[j]] = 0;
+  // the filter pass's answers: node-major int32 rows [n][S + 1] (the kernel's
+  // own copy), or slot-major int64 [S][n] and [n] (a copy launch)
   const char* rawb = (const char*)h->fwh + h->fw_oraw;
   const char* partb = (const char*)h->fwh + h->fw_opart;
   const bool w32 = h->fw_raw32;
-  auto raw_at = [&](size_t i) -> int64_t {
-    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(rawb)[i] : reinterpret_cast<const int64_t*>(rawb)[i];
+  const size_t W = (size_t)S + 1;
+  auto raw_at = [&](int k, size_t node) -> int64_t {
+    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(rawb)[node * W + (size_t)k]
+               : reinterpret_cast<const int64_t*>(rawb)[(size_t)k * N + node];
   };
-  auto part_at = [&](size_t i) -> int64_t {
-    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(partb)[i] : reinterpret_cast<const int64_t*>(partb)[i];
+  auto part_at = [&](size_t node) -> int64_t {
+    return w32 ? (int64_t)reinterpret_cast<const int32_t*>(rawb)[node * W + (size_t)S]
+               : reinterpret_cast<const int64_t*>(partb)[node];
   };
   const bool scored = n > 1;
   const bool ipa_nonempty = (h->fw_tflags & kTopoScoreNonEmpty) != 0;
@@ -3024,11 +3038,22 @@ static int fw_score_host(ksim_handle* h, const int32_t* nodes, int32_t n, ksim_e
   std::vector<int64_t>& tot = h->fw_tot;
   tot.assign(n, 0);
   if (scored) {
-    for (int32_t j = 0; j < n; j++) tot[j] = part_at((size_t)nodes[j]);
+    if (w32) {                             // one row (a cache line) per listed node
+      const int32_t* rows = reinterpret_cast<const int32_t*>(rawb);
+      int64_t* fr = h->fw_raw.data();
+      for (int32_t j = 0; j < n; j++) {
+        const int32_t* row = rows + (size_t)nodes[j] * W;
+        for (int k = 0; k < S; k++) fr[(size_t)k * n + j] = row[k];
+        tot[j] = row[S];
+      }
+    } else {
+      for (int32_t j = 0; j < n; j++) tot[j] = part_at((size_t)nodes[j]);
+      for (int k = 0; k < S; k++)
+        for (int32_t j = 0; j < n; j++) h->fw_raw[(size_t)k * n + j] = raw_at(k, (size_t)nodes[j]);
+    }
     for (int k = 0; k < S; k++) {
       int64_t* r = h->fw_raw.data() + (size_t)k * n;
       int64_t* nv = h->fw_norm.data() + (size_t)k * n;
-      for (int32_t j = 0; j < n; j++) r[j] = raw_at((size_t)k * N + (size_t)nodes[j]);
       const int32_t kind = norm_kind(h->prof.score[k]);
       if (kind == kNormNone) {
         std::memcpy(nv, r, 8 * (size_t)n);

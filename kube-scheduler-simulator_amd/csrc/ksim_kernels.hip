@@ -424,17 +424,19 @@ __global__ __launch_bounds__(256) void k_filter_score(DevCluster c, DevPods P0, 
       const BatchProg* fast = (bp->fast_w && (c.cflags & kClusterNarrow)) ? bp : nullptr;
       s.part[node] = run_score_plan(c, P, prof, ScorePlan{bp->slot, bp->slot_hi}, p, r, U, m, t, s.raw, COMPAT, rv,
                                     soft_cnt, fast, inv_c, inv_m);
-      if (COMPAT && s.m_raw) {                     // the feasible node's answers in the host's staging too,
-        const size_t N = (size_t)c.n;                // as int32 (m_head[1] = 1: a value did not fit)
+      if (COMPAT && s.m_raw) {                     // the feasible node's answers in the host's staging too:
+        const size_t N = (size_t)c.n;                // node-major rows of S raw scores + the part, int32
+        const int W = prof.n_score + 1;              // (m_head[1] = 1: a value did not fit)
+        int32_t* row = s.m_raw + (size_t)node * W;
         bool wide = false;
         for (int k = 0; k < prof.n_score; k++) {
           const int64_t v = s.raw[(size_t)k * N + node];
           wide |= v != (int64_t)(int32_t)v;
-          s.m_raw[(size_t)k * N + node] = (int32_t)v;
+          row[k] = (int32_t)v;
         }
         const int64_t v = s.part[node];
         wide |= v != (int64_t)(int32_t)v;
-        s.m_part[node] = (int32_t)v;
+        row[prof.n_score] = (int32_t)v;
         if (wide) s.m_head[1] = 1;
       }
     }

@@ -564,7 +564,7 @@ def main():
                     help="run the node-sharded RCCL path even at N = 1 (a one-rank communicator)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--shard-mode", choices=["replicated", "nodes"], default="replicated",
-                    help="config 2 over N > 1 GPUs: replicated snapshot with the evaluation split by node range "
+                    help="configs 2 / 4 (P100) over N > 1 GPUs: replicated snapshot with the evaluation split by node range "
                          "(one collective per batch), or node shards (two)")
     ap.add_argument("--python-encode", action="store_true",
                     help="compile configs 1 / 3 with the Python encoder (ksim/encode.py) instead of the native one")
@@ -610,7 +610,7 @@ def main():
 
     if sharded:
         uid = shard.broadcast_unique_id(dist, rank) if world > 1 else engine.comm_unique_id()
-        if cfg == 2 and args.shard_mode == "replicated":
+        if cfg in (2, 4) and args.mode == "p100" and args.shard_mode == "replicated":
             # every rank holds the whole snapshot, the batch top-T is split:
             # one all-gather per batch instead of an all-gather + all-reduce
             eng = shard.replicated_engine(cluster, prof, rank, world, local, uid)

@@ -623,34 +623,19 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
     };
     NormRaw mx{0, 0};
     if (normv) {
-      __shared__ uint64_t s_nmx[2][W];
-      uint64_t lt = 0, la = 0;
+      // the maxima over the kept nodes and how many kept nodes hold each
+      // (pnorm[4 j + 2..3]): a window that scans every node never shifts, so
+      // its pod stays exact until every holder of a maximum stops fitting
+      // (k_adapt_pairs), as on the P100 path
+      NormAcc acc;
 #pragma unroll 1
       for (int32_t off = tid; off < kend; off += NT) {
         int32_t node = s + off;
         if (node >= n) node -= n;
         if (!((mask[node >> 6] >> (node & 63)) & 1ull)) continue;
-        const NormRaw v = raw(node);
-        lt = umax64(lt, (uint64_t)v.tt);
-        la = umax64(la, (uint64_t)v.na);
+        acc.take(raw(node));
       }
-      lt = wave_max_u64_dpp(lt);
-      la = wave_max_u64_dpp(la);
-      if (lane == 0) {
-        s_nmx[0][wv] = lt;
-        s_nmx[1][wv] = la;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int w = 0; w < W; w++) {
-        lt = umax64(lt, s_nmx[0][w]);
-        la = umax64(la, s_nmx[1][w]);
-      }
-      mx = NormRaw{(int64_t)lt, (int64_t)la};
-      if (tid == 0) {
-        pnorm[4 * j] = mx.tt;
-        pnorm[4 * j + 1] = mx.na;
-      }
+      mx = norm_maxima<NT>(acc, pnorm, j);
     }
 #pragma unroll 1
     for (int32_t off = tid; off < kend; off += NT) {
@@ -761,6 +746,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   }
   uint64_t v = 0;
   bool brk = false;
+  bool lost_t = false, lost_a = false;           // guess k held a normalization maximum of pod j and stopped fitting
   if (j < nchain && k < j) {
     const int32_t node = gk ? key_node(gk) - c.base : -1;
     if (node >= 0 && node < c.n) {
@@ -775,16 +761,37 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         const ksim_pod& p = P.pods[base + j];
         const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
         const bool was = (amask[(size_t)j * n_words + (g >> 6)] >> (g & 63)) & 1ull;
-        // kPodNormVaries (k_adapt_top's maxima): a kept node that stops
-        // fitting changes the scored list even when every node is processed
+        // a window that stops before the ring's end shifts when a kept node
+        // stops fitting; one that scans every node keeps its span, and for
+        // kPodNormVaries pods (k_adapt_top's maxima) its scored list loses
+        // the node: the maxima change once every holder has left
         const bool normv = pnorm && (P.bflags[base + j] & kPodNormVaries) != 0;
-        if ((cut >= 0 || normv) && was && !now) brk = true;
+        if (was && !now) {
+          if (cut >= 0) {
+            brk = true;
+          } else if (normv) {
+            const NormRaw x = norm_raw(c, P, p, r);
+            lost_t = pnorm[4 * j] > 0 && x.tt == pnorm[4 * j];
+            lost_a = pnorm[4 * j + 1] > 0 && x.na == pnorm[4 * j + 1];
+          }
+        }
         if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base, c.fit_ignore);
         if (normv && v)
           v += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), NormRaw{pnorm[4 * j], pnorm[4 * j + 1]}) << 44;
       }
     }
   }
+  __shared__ int32_t s_lost[2];
+  if (tid < 2) s_lost[tid] = 0;
+  __syncthreads();
+  {
+    const int32_t nt = __popcll(__ballot(lost_t)), na = __popcll(__ballot(lost_a));
+    if (lane == 0 && nt) atomicAdd(&s_lost[0], nt);
+    if (lane == 0 && na) atomicAdd(&s_lost[1], na);
+  }
+  __syncthreads();
+  if (s_lost[0] > 0 && s_lost[0] >= pnorm[4 * j + 2]) brk = true;   // every holder of a maximum left
+  if (s_lost[1] > 0 && s_lost[1] >= pnorm[4 * j + 3]) brk = true;
   const bool any_brk = __syncthreads_or(brk);
   v = wave_max_u64_dpp(v);
   if (lane == 0) s_wmax[wave] = v;
@@ -797,6 +804,22 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
     else abroken[j] = j < nchain && any_brk ? 1 : 0;
   }
 }
+
+#ifdef KSIM_ADAPT_DBG
+// KSIM_ADAPT_DBG builds (tools/adapt_dbg.py): why ADAPT batches end short.
+// dbg 0 batches, 1 the chain ended before the batch (an exhausted incomplete
+// list), 2 a broken window before the chain's end, 3 sum of the chain's
+// length, 4 sum of the prefix before the first broken window, 5 cut by a pair
+// maximum, 6 sum of committed pods, 7 sum of the batch's pods
+__device__ unsigned long long g_adapt_dbg[8];
+unsigned long long* adapt_dbg_buffer() {
+  void* p = nullptr;
+  (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_adapt_dbg));
+  return (unsigned long long*)p;
+}
+#else
+unsigned long long* adapt_dbg_buffer() { return nullptr; }
+#endif
 
 // abroken null (sharded): the broken flags follow M in pmax[kBatchPods + j].
 __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
@@ -818,7 +841,25 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   __syncthreads();
   block_first_min(&s_fb, (int32_t)threadIdx.x < nchain0 && brk);
   __syncthreads();
+#ifdef KSIM_ADAPT_DBG
+  const int32_t nb_dbg = min(kBatchPods, st->end - st->cursor), fb_dbg = s_fb;
+  const int32_t cur_dbg = st->cursor;
+#endif
   batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw);
+#ifdef KSIM_ADAPT_DBG
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t committed = st->cursor - cur_dbg;
+    atomicAdd(&g_adapt_dbg[0], 1ull);
+    if (nchain0 < nb_dbg) atomicAdd(&g_adapt_dbg[1], 1ull);
+    if (fb_dbg < nchain0) atomicAdd(&g_adapt_dbg[2], 1ull);
+    atomicAdd(&g_adapt_dbg[3], (unsigned long long)nchain0);
+    atomicAdd(&g_adapt_dbg[4], (unsigned long long)fb_dbg);
+    if (committed < fb_dbg) atomicAdd(&g_adapt_dbg[5], 1ull);
+    atomicAdd(&g_adapt_dbg[6], (unsigned long long)committed);
+    atomicAdd(&g_adapt_dbg[7], (unsigned long long)nb_dbg);
+  }
+#endif
 }
 
 // ---- deferred commit (ksim_internal.h): batch i-1's commit inside batch i's mask launch ----

@@ -222,66 +222,6 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   }
 }
 
-// A lane's DefaultNormalizeScore maxima of a kPodNormVaries pod's raw
-// TaintToleration / NodeAffinity scores over its S0-feasible nodes, and how
-// many of its nodes hold each (raw scores are >= 0).
-struct NormAcc {
-  uint64_t lt = 0, la = 0;
-  int32_t ct = 0, ca = 0;
-  __device__ __forceinline__ void take(const NormRaw& v) {
-    ct = (uint64_t)v.tt > lt ? 1 : ct + ((uint64_t)v.tt == lt ? 1 : 0);
-    lt = umax64(lt, (uint64_t)v.tt);
-    ca = (uint64_t)v.na > la ? 1 : ca + ((uint64_t)v.na == la ? 1 : 0);
-    la = umax64(la, (uint64_t)v.na);
-  }
-};
-
-// The block's maxima (returned to every thread) and their holder counts:
-// thread 0 writes pnorm[4 j .. 4 j + 3] (the batch keeps pod j until every
-// holder of a maximum has left its feasible set, pairs_block).
-template <int kTopThreads>
-__device__ __forceinline__ NormRaw norm_maxima(const NormAcc& n, int64_t* __restrict__ pnorm, int32_t j) {
-  constexpr int kTopWaves = kTopThreads / 64;
-  __shared__ uint64_t s_nmax[2][kTopWaves];
-  __shared__ int32_t s_ncnt[2][kTopWaves];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t xt = wave_max_u64_dpp(n.lt), xa = wave_max_u64_dpp(n.la);
-  if (lane == 0) {
-    s_nmax[0][wv] = xt;
-    s_nmax[1][wv] = xa;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int w = 0; w < kTopWaves; w++) {
-    xt = umax64(xt, s_nmax[0][w]);
-    xa = umax64(xa, s_nmax[1][w]);
-  }
-  int32_t nt = n.lt == xt ? n.ct : 0, na = n.la == xa ? n.ca : 0;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    nt += __shfl_xor(nt, d, 64);
-    na += __shfl_xor(na, d, 64);
-  }
-  if (lane == 0) {
-    s_ncnt[0][wv] = nt;
-    s_ncnt[1][wv] = na;
-  }
-  __syncthreads();
-  const NormRaw mx{(int64_t)xt, (int64_t)xa};
-  if (threadIdx.x == 0) {
-    int32_t tt = 0, ta = 0;
-    for (int w = 0; w < kTopWaves; w++) {
-      tt += s_ncnt[0][w];
-      ta += s_ncnt[1][w];
-    }
-    pnorm[4 * j] = mx.tt;
-    pnorm[4 * j + 1] = mx.na;
-    pnorm[4 * j + 2] = tt;
-    pnorm[4 * j + 3] = ta;
-  }
-  return mx;
-}
-
 // The generic (non-FAST) keys of pod j = pi - cursor over the block's nodes:
 // static filters, the resource key, and for kPodNormVaries pods the
 // normalized TaintToleration / NodeAffinity parts.  ov(row) adds whatever the

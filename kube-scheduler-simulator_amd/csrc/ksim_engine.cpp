@@ -4085,6 +4085,8 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   if (unsigned long long* cp = cp_clock_buffer())   // KSIM_CP_CLOCKS builds: the chain + pairs phase clocks
     HIPCHK(h, hcopy(h, v + 3, cp, 8 * 8, hipMemcpyDeviceToHost));
+  if (unsigned long long* ad = adapt_dbg_buffer())  // KSIM_ADAPT_DBG builds: ADAPT batch ends
+    HIPCHK(h, hcopy(h, v + 3, ad, 8 * 8, hipMemcpyDeviceToHost));
   v[19] = h->graph_captures;
   v[20] = h->match_ns;
   for (int k = 0; k < 4; k++) v[21 + k] = h->fw_counts[k];

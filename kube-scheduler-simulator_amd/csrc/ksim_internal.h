@@ -103,6 +103,7 @@ void launch_tb_rep_commit(const LaunchArgs& a, hipStream_t stream);
 uint32_t launch_cycle(const LaunchArgs& a, hipStream_t stream, bool compat, bool topo, hipEvent_t* evs = nullptr);
 // One speculative batch of up to kBatchPods pods from st->cursor (>= 1 committed).
 // Returns the mask of kernel slots launched (bit k: kBatchKernelNames[k]).
+unsigned long long* adapt_dbg_buffer();  // KSIM_ADAPT_DBG builds: why ADAPT batches end short (else null)
 unsigned long long* cp_clock_buffer();   // KSIM_CP_CLOCKS builds: chain + pairs phase clocks (else null)
 uint32_t launch_batch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs = nullptr);
 // The same under ADAPT (K < N): windows by relaxation, see ksim_adapt.hip.

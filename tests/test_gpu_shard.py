@@ -263,6 +263,25 @@ def test_group_replicated(n_nodes, world):
             np.testing.assert_array_equal(es[k], os_[k])
 
 
+def test_group_replicated_config4():
+    """Config 4's cluster (100,000 nodes) over eight replicas, each keying its
+    12,500-node range (bench.py --gpus 8 --config 4's protocol): the oracle's
+    placements and every replica's node state."""
+    cluster, pods = gen.config4(n_nodes=100000, n_pods=2500)
+    prof = _prof()
+    engines = _replicas(cluster, pods, prof, 8)
+    chosen, st = group_schedule_loaded(engines, 0, pods.n_pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=8)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    os_ = ora.node_state()
+    for e in engines:
+        es = e.node_state()
+        for k in es:
+            np.testing.assert_array_equal(es[k], os_[k])
+
+
 def test_group_replicated_mixed_paths():
     """Pods the batch path cannot take (taints, node affinity: per-pod cycles)
     run whole on every replica between replicated batches."""

@@ -100,6 +100,14 @@ def test_replicated_protocol_gloo(world, n_nodes, n_pods, T, B):
     mp.spawn(_worker, args=(world, _free_port(), n_nodes, n_pods, 7, T, B, None, True), nprocs=world, join=True)
 
 
+def test_replicated_protocol_gloo_config4_world8():
+    """The eight-replica exchange bench.py --gpus 8 --config 4 runs (one
+    all-gather of the ranges' top-T records per batch), on config 4's
+    generator at a CPU-sized scale."""
+    from ksim import gen
+    mp.spawn(_worker, args=(8, _free_port(), 240, 400, gen.SEEDS[4], 4, 32, None, True), nprocs=8, join=True)
+
+
 def _worker_perpod(rank, world, port, n_nodes, n_pods, seed, pct):
     import sys
     root = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))

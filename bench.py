@@ -765,10 +765,15 @@ def main():
     valu = None
     if ve and ve.get("valu_insts_per_launch"):
         g = ve["valu_insts_per_launch"] / (avg_ms * 1e-3) / 1e9
+        per_eval = ve.get("valu_insts_per_eval_lane")
+        if per_eval is None and dominant in ("k_batch_top_commit", "k_batch_top", "k_adapt_top"):
+            # one block per pod of the batch, each over the evaluated node range
+            per_eval = ve["valu_insts_per_launch"] * 64 / (geom["pods_per_batch"] *
+                                                           (geom["adapt_k"] if dominant == "k_adapt_top" else knodes))
         valu = {"achieved": g, "peak": VALU_PEAK_G, "unit": "G wave-instructions/s", "frac": g / VALU_PEAK_G,
                 "valu_insts_per_launch": ve["valu_insts_per_launch"],
                 "salu_insts_per_launch": ve.get("salu_insts_per_launch"),
-                "valu_insts_per_eval_lane": ve.get("valu_insts_per_eval_lane"), "source": ve.get("source")}
+                "valu_insts_per_eval_lane": per_eval, "source": ve.get("source")}
         act, wcyc, waves = (ve.get("valu_active_quad_cycles_per_launch"), ve.get("wave_quad_cycles_per_launch"),
                             ve.get("waves_per_launch"))
         fills = ve.get("waves_per_launch", 0) >= 256 * 4     # at least one wave per SIMD of the chip

@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC, KEEP = sys.argv[1], sys.argv[2]
 # config label -> (bench config, nodes)
-CFG = {"c1": (1, 5000), "c1a": (1, 5000), "c2": (2, 5000), "c2a": (2, 5000), "c3": (3, 10000), "c4a": (4, 100000),
+CFG = {"c1": (1, 5000), "c1a": (1, 5000), "c2": (2, 5000), "c2a": (2, 5000), "c3": (3, 10000), "c4": (4, 100000), "c4a": (4, 100000),
        "c5": (5, 5000)}
 # kernel symbol -> the bench kernel table's slot name
 NAME = {"k_adapt_mask_ns": "k_adapt_mask"}

@@ -201,7 +201,8 @@ template <int NT = kBatchPods>
 __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, const uint64_t* __restrict__ amask,
                                              int32_t n_words, int32_t n, int32_t k, int32_t* s_out,
                                              int32_t* cut_out, int32_t* exact_out,
-                                             const int32_t* __restrict__ cut0 = nullptr) {
+                                             const int32_t* __restrict__ cut0 = nullptr,
+                                             int32_t stop_after = kBatchPods) {
   static_assert(NT >= kBatchPods && NT % 64 == 0, "a thread per pod");
   __shared__ int64_t sh[NT / 64];
   __shared__ int32_t s_first;
@@ -242,6 +243,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
     }
     exact = f;                                       // pods < f: start and cut exact
     if (j >= f) s = ns;                              // pods <= f now hold exact starts
+    if (f > stop_after) break;                       // the caller's pod is exact: enough
   }
   *s_out = s;
   *cut_out = cut;
@@ -514,7 +516,12 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
     __shared__ int2 s_win;
     int32_t ws, wc;
     const int32_t kk = num_feasible_nodes_to_find(prof.percentage_of_nodes_to_score, c.n);
-    window_block<NT>(st, amask, n_words, c.n, kk, &ws, &wc, &exact, WIN == 2 ? acut : nullptr);   // batch not empty (above)
+    // block 0 stores every window and the exact prefix: the whole relaxation;
+    // block j stops once pod j's window is exact (rounds past the first,
+    // a batch off its first-round fixpoint costs the later blocks
+    // only the rounds their own pod needs)
+    window_block<NT>(st, amask, n_words, c.n, kk, &ws, &wc, &exact, WIN == 2 ? acut : nullptr,
+                     j == 0 ? kBatchPods : j);   // batch not empty (above)
     if (tid == j) s_win = make_int2(ws, wc);
     if (j == 0) {
       if (tid < min(kBatchPods, st->end - base)) {

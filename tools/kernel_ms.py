@@ -11,12 +11,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles", "kernel_ms.json")
+# bench kernel-table slot -> the kernel symbol rocprofv3 reports
+SYMBOL = {"k_adapt_mask": "k_adapt_mask_ns"}
 
 
 def mean_ms(path, kernel):
     """Mean duration (ms) of the kernel whose name starts with ksim::<kernel>< or ( (template instances
     summed by count)."""
-    keys = (f"ksim::{kernel}<", f"ksim::{kernel}(")
+    sym = SYMBOL.get(kernel, kernel)
+    keys = (f"ksim::{sym}<", f"ksim::{sym}(")
     n = tot = 0
     if path.endswith(".db"):
         for name, cnt, s in sqlite3.connect(path).execute(

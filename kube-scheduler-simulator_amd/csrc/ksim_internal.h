@@ -32,7 +32,10 @@ static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch 
 constexpr int kTopThreads = 1024;  // threads per pod of the batch top
 constexpr int kTileCand = 4;       // best keys each lane of the batch top keeps per pod
 constexpr int kXRec = kTopT + 1;   // sharded exchange record per pod: T keys + (count | complete << 32)
-constexpr int kMaxShards = 8;      // shards of one simulation (one per GPU of a node)
+#ifndef KSIM_MAX_SHARDS
+#define KSIM_MAX_SHARDS 8
+#endif
+constexpr int kMaxShards = KSIM_MAX_SHARDS;   // shards of one simulation (one per GPU of a node)
 constexpr int kGmergeSlots = (kTopT * kMaxShards + 63) / 64;   // list entries per lane in k_batch_gmerge
 static_assert(kGmergeSlots <= 2, "gmerge geometry");
 

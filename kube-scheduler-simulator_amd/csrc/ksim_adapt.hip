@@ -972,8 +972,6 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
         atomicAdd(&s_evals, (int32_t)window_local(c, w.x, w.y >= 0 ? (int64_t)w.y + 1 : c.n_total));
       }
     }
-    if (tid < (int)(sizeof(DevState) / 8))
-      reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
   }
   // placements of batch i-1, one per block
   if (tid == 0)
@@ -983,24 +981,32 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
     }
   __syncthreads();
   if (bl == 0 && tid == 0) {
-    // new values from st[p ^ 1] only (see k_batch_top_commit)
-    const DevState* si = L.st_in;
-    DevState* so = L.st_out;
+    // st[p] = st[p ^ 1] with the commit's updates, written whole: its words
+    // loaded together, no store-then-reload chain (see k_batch_top_commit)
+    constexpr int kWords = (int)(sizeof(DevState) / 8);
+    uint64_t wd[kWords];
+#pragma unroll
+    for (int q = 0; q < kWords; q++) wd[q] = reinterpret_cast<const uint64_t*>(L.st_in)[q];
+    DevState ns;
+    __builtin_memcpy(&ns, wd, sizeof(ns));
     if (e1 > 0) {
       const int32_t nb = min(kBatchPods, end - cur0);
-      so->cursor = cur0 + committed;
-      so->pod_seq = seq0 + committed;
-      so->scheduled = si->scheduled + s_sched;
-      so->unschedulable = si->unschedulable + s_unsched;
-      so->batches = si->batches + 1;
-      so->cuts = si->cuts + (committed < nb && istar < nchain ? 1 : 0);
-      so->truncations = si->truncations + (committed < nb && istar >= nchain ? 1 : 0);
+      ns.cursor = cur0 + committed;
+      ns.pod_seq = seq0 + committed;
+      ns.scheduled += s_sched;
+      ns.unschedulable += s_unsched;
+      ns.batches += 1;
+      ns.cuts += (committed < nb && istar < nchain ? 1 : 0);
+      ns.truncations += (committed < nb && istar >= nchain ? 1 : 0);
       if (committed > 0) {
         const int2 w = reinterpret_cast<const int2*>(w1)[committed - 1];
-        so->next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
-        if (c.count_whole) so->evals = si->evals + s_evals;
+        ns.next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
+        if (c.count_whole) ns.evals += s_evals;
       }
     }
+    __builtin_memcpy(wd, &ns, sizeof(ns));
+#pragma unroll
+    for (int q = 0; q < kWords; q++) reinterpret_cast<uint64_t*>(L.st_out)[q] = wd[q];
     if (FLUSH) *L.e_self = -1;
   }
   // this thread's node: S_i row = X[p ^ 1] + delta; written to X[p] by the

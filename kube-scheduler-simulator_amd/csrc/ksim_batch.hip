@@ -850,32 +850,34 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     if (mn1 >= 0) mr1 = ResCols{c.req_cpu[mn1], c.req_mem[mn1], c.req_eph[mn1], c.nz_cpu[mn1], c.nz_mem[mn1], c.num_pods[mn1]};
   }
   lds_barrier();
-  if (b == 0) {                                 // block-uniform
-    if (tid < (int)(sizeof(DevState) / 8)) {    // st[p] = st[p ^ 1], then the commit's updates
-      static_assert(sizeof(DevState) % 8 == 0, "DevState copy by words");
-      reinterpret_cast<uint64_t*>(L.st_out)[tid] = reinterpret_cast<const uint64_t*>(L.st_in)[tid];
-    }
-    __syncthreads();                            // the copy's stores land before thread 0's below
-  }
-  if (b == 0 && tid == 0) {
-    // every new value from st[p ^ 1]: st[p] is never read back here (a
-    // uniform load of it would go through the scalar cache, which does not
-    // see the vector stores of the copy above)
-    const DevState* si = L.st_in;
-    DevState* s = L.st_out;
+  // st[p] = st[p ^ 1] with the commit's updates, written whole by one thread
+  // of block 0 off the critical path (a wave that is done before the top-T
+  // merge): its words loaded together, no store-then-reload chain
+  auto update_state = [&]() {
+    static_assert(sizeof(DevState) % 8 == 0, "DevState by words");
+    constexpr int kWords = (int)(sizeof(DevState) / 8);
+    uint64_t w[kWords];
+#pragma unroll
+    for (int q = 0; q < kWords; q++) w[q] = reinterpret_cast<const uint64_t*>(L.st_in)[q];
+    DevState ns;
+    __builtin_memcpy(&ns, w, sizeof(ns));
     if (e1 > 0) {
       const int32_t nb = min(kBatchPods, end - cur0);
-      s->cursor = base;
-      s->pod_seq = seq0 + committed;
-      s->scheduled = si->scheduled + s_sched;
-      s->unschedulable = si->unschedulable + s_unsched;
-      s->batches = si->batches + 1;
-      s->cuts = si->cuts + (committed < nb && istar < nchain ? 1 : 0);
-      s->truncations = si->truncations + (committed < nb && istar >= nchain ? 1 : 0);
-      s->evals = si->evals + (int64_t)committed * (c.eval_hi - c.eval_lo);
+      ns.cursor = base;
+      ns.pod_seq = seq0 + committed;
+      ns.scheduled += s_sched;
+      ns.unschedulable += s_unsched;
+      ns.batches += 1;
+      ns.cuts += (committed < nb && istar < nchain ? 1 : 0);
+      ns.truncations += (committed < nb && istar >= nchain ? 1 : 0);
+      ns.evals += (int64_t)committed * (c.eval_hi - c.eval_lo);
     }
+    __builtin_memcpy(w, &ns, sizeof(ns));
+#pragma unroll
+    for (int q = 0; q < kWords; q++) reinterpret_cast<uint64_t*>(L.st_out)[q] = w[q];
     if (FLUSH) *L.e_self = -1;
-  }
+  };
+  const bool st_writer = b == 0 && tid == kThreads - 64;   // the last wave's first lane
   // the overlay delta of a node (zero when batch i-1 did not bind it)
   auto delta = [&](int32_t node) -> ResCols {
     if constexpr (DIRECT) {
@@ -914,6 +916,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   };
   if (!live) {
     materialize();
+    if (st_writer) update_state();
     return;
   }
   // pod b of batch i against S_i (k_batch_top's loops with the overlay)
@@ -980,6 +983,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
 #else
   top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
 #endif
+  if (st_writer) update_state();              // waves past the first return from the merge early
 }
 
 // the evaluation launch of a deferred-commit batch (DIRECT overlay when the

@@ -59,6 +59,15 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   const int32_t base = st->cursor;
   const int32_t nb = min(nb_cap, st->end - base);   // the batch's pods (statistics: cut or truncated)
   const int64_t seq0 = st->pod_seq;
+  // thread 0 rewrites the state whole at the end: its words loaded now, in
+  // flight with the rest (no load round trip after the last barrier)
+  constexpr int kStWords = (int)(sizeof(DevState) / 8);
+  static_assert(sizeof(DevState) % 8 == 0, "DevState by words");
+  uint64_t stw[kStWords];
+  if (tid == 0) {
+#pragma unroll
+    for (int q = 0; q < kStWords; q++) stw[q] = reinterpret_cast<const uint64_t*>(st)[q];
+  }
   const uint64_t gj = tid < nchain ? g_own : 0;
   const uint64_t mj = tid < nchain ? m_own : 0;
   // ahead of the cut: the row of the node this pod guessed (it binds there if
@@ -125,22 +134,27 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   }
   __syncthreads();
   if (tid == 0) {
+    DevState ns;
+    __builtin_memcpy(&ns, stw, sizeof(ns));
     if (s_aw && committed > 0) {
       const int2 w = s_aw[committed - 1];
-      st->next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
-      if (c.count_whole) st->evals += s_evals;
+      ns.next_start = (int32_t)(((int64_t)w.x + (w.y >= 0 ? w.y : c.n_total)) % c.n_total);
+      if (c.count_whole) ns.evals += s_evals;
     } else {
-      st->evals += (int64_t)committed * (c.eval_hi - c.eval_lo);   // the nodes this handle evaluated
+      ns.evals += (int64_t)committed * (c.eval_hi - c.eval_lo);   // the nodes this handle evaluated
     }
-    st->cursor = base + committed;
-    st->pod_seq = seq0 + committed;
-    st->scheduled += *s_sched;
-    st->unschedulable += *s_unsched;
-    st->batches += 1;
+    ns.cursor = base + committed;
+    ns.pod_seq = seq0 + committed;
+    ns.scheduled += *s_sched;
+    ns.unschedulable += *s_unsched;
+    ns.batches += 1;
     if (committed < nb) {
-      if (istar < nchain) st->cuts += 1;
-      else st->truncations += 1;
+      if (istar < nchain) ns.cuts += 1;
+      else ns.truncations += 1;
     }
+    __builtin_memcpy(stw, &ns, sizeof(ns));
+#pragma unroll
+    for (int q = 0; q < kStWords; q++) reinterpret_cast<uint64_t*>(st)[q] = stw[q];
   }
 }
 

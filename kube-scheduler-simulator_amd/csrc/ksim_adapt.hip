@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
                                                        int32_t n_words, int32_t mp) {
   const BatchProg& bp = *bp_p;
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t nb = batch_pods(st);
   const int32_t j0 = blockIdx.y * mp;
   if (j0 >= nb) return;                              // block-uniform
   const int lane = threadIdx.x & 63;
@@ -208,7 +208,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   __shared__ int32_t s_first;
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t nb = batch_pods(st);
   if (nb <= 0) return false;
   const int32_t s0 = st->next_start;
   int32_t s = (int32_t)(((int64_t)s0 + (int64_t)j * k) % n);
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void k_adapt_cut0(const DevState* __restrict__
                                                     int32_t k, int32_t* __restrict__ awin) {
   const int lane = threadIdx.x & 63;
   const int32_t j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // wave-uniform
+  if (j >= batch_pods(st)) return;   // wave-uniform
   const int32_t s = (int32_t)(((int64_t)st->next_start + (int64_t)j * k) % n);
   const uint64_t* m = amask + (size_t)j * n_words;
   const int32_t ws = s >> 6;
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_window(const DevState* __r
   int32_t s, cut, exact;
   if (!window_block(st, amask, n_words, n, k, &s, &cut, &exact, acut)) return;
   const int j = threadIdx.x;
-  if (j < min(kBatchPods, st->end - st->cursor)) {
+  if (j < batch_pods(st)) {
     awin[2 * j] = s;
     awin[2 * j + 1] = cut;
   }
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kWinBuildThreads) void k_win_build(const DevState* 
   __shared__ uint16_t s_sel[kWinSeqWords * 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int32_t j = blockIdx.x;
-  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // block-uniform
+  if (j >= batch_pods(st)) return;   // block-uniform
   const uint64_t* m = amask + (size_t)j * n_words;
   if (tid < kWinSeqWords) {                        // the words' prefix counts, two waves
     const uint64_t w = tid < n_words ? m[tid] : 0ull;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBatchPods) void k_win_final(const DevState* __rest
                                                           const int32_t* __restrict__ wtot, int32_t n, int32_t k,
                                                           int32_t* __restrict__ awin, int32_t* __restrict__ aexact) {
   const int32_t j = threadIdx.x;
-  const int32_t nb = min(kBatchPods, st->end - st->cursor);
+  const int32_t nb = batch_pods(st);
   if (nb <= 0) return;
   if (j < nb) {
     const int32_t s0 = st->next_start, i = j - 1;
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(1024) void k_win_round_lds(const DevState* __restri
                                                         const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
   __shared__ uint16_t s_rows[R][kWinSeqWords * 64];
   const int32_t j = blockIdx.x;
-  if (j >= min(kBatchPods, st->end - st->cursor)) return;   // block-uniform
+  if (j >= batch_pods(st)) return;   // block-uniform
   const int32_t words = (n + 7) >> 3;                  // 16-byte pieces per row (the row starts 16-byte aligned)
 #pragma unroll
   for (int t = 0; t < R; t++) {
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t j = blockIdx.x;
   const int32_t base = st->cursor;
-  if (j >= min(kBatchPods, st->end - base)) return;   // block-uniform
+  if (j >= batch_pods(st)) return;   // block-uniform
   int32_t win_s = 0, win_cut = -1, exact;
   if constexpr (WIN != 0) {
     // WIN 1: the whole relaxation in every block; WIN 2: from k_adapt_cut0's
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
                      j == 0 ? kBatchPods : j);   // batch not empty (above)
     if (tid == j) s_win = make_int2(ws, wc);
     if (j == 0) {
-      if (tid < min(kBatchPods, st->end - base)) {
+      if (tid < batch_pods(st)) {
         awin[2 * tid] = ws;
         awin[2 * tid + 1] = wc;
       }
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int32_t base = st->cursor;
-  const int32_t nb = min(kBatchPods, st->end - base);
+  const int32_t nb = batch_pods(st);
   if (nb <= 0) {
     if (LAZY && blockIdx.x == 0 && tid == 0) *chain_end = -1;   // deferred commit: an empty slot
     return;
@@ -745,7 +745,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   uint64_t gk;
   {
     __shared__ ChainLds L;
-    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr, kBatchPods, c.n_total)) return;
+    if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, nullptr, batch_cap(st), c.n_total)) return;
     if (j == 0) {
       if (k < nb) gkey[k] = gk;
       if (k == 0) *chain_end = nchain;
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   const uint64_t g = gkey[threadIdx.x], m = pmax[threadIdx.x];   // in flight with the state loads
   const int32_t brk = abroken ? abroken[threadIdx.x] : (int32_t)pmax[kBatchPods + threadIdx.x];
   const int2 aw = reinterpret_cast<const int2*>(awin)[threadIdx.x];   // {scan start, cut}, likewise
-  if (min(kBatchPods, st->end - st->cursor) <= 0) return;
+  if (batch_pods(st) <= 0) return;
   const int32_t nchain0 = *chain_end;
   s_aw[threadIdx.x] = aw;
   if (threadIdx.x == 0) s_fb = nchain0;
@@ -849,10 +849,11 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   block_first_min(&s_fb, (int32_t)threadIdx.x < nchain0 && brk);
   __syncthreads();
 #ifdef KSIM_ADAPT_DBG
-  const int32_t nb_dbg = min(kBatchPods, st->end - st->cursor), fb_dbg = s_fb;
+  const int32_t nb_dbg = batch_pods(st), fb_dbg = s_fb;
   const int32_t cur_dbg = st->cursor;
 #endif
-  batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw);
+  batch_commit(c, P, st, g, m, pmax, s_fb, chosen_out, &s_istar, &s_sched, &s_unsched, s_aw, nullptr, batch_cap(st),
+               nullptr, !abroken ? false : true);
 #ifdef KSIM_ADAPT_DBG
   __syncthreads();
   if (threadIdx.x == 0) {

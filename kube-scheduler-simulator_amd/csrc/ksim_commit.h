@@ -8,6 +8,15 @@
 
 namespace ksim {
 
+// The batch's pod cap (DevState::bcap; kBatchPods when none) and its pods.
+__device__ __forceinline__ int32_t batch_cap(const DevState* __restrict__ st) {
+  const int32_t cap = st->bcap;
+  return cap > 0 && cap < kBatchPods ? cap : kBatchPods;
+}
+__device__ __forceinline__ int32_t batch_pods(const DevState* __restrict__ st) {
+  return min(batch_cap(st), st->end - st->cursor);
+}
+
 // Nodes of the circular scan window [s, s + len) of the cluster's n_total
 // nodes that lie on this snapshot ([base, base + n)): the evaluations a shard
 // ran for the window (all of them on an unsharded handle).
@@ -43,7 +52,8 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
                                              int32_t nchain, int32_t* __restrict__ chosen_out, int32_t* s_istar,
                                              int32_t* s_sched, int32_t* s_unsched,
                                              const int2* s_aw = nullptr, const int32_t* inv_own = nullptr,
-                                             int32_t nb_cap = kBatchPods, int32_t* s_node = nullptr) {
+                                             int32_t nb_cap = kBatchPods, int32_t* s_node = nullptr,
+                                             bool adapt_cap = false) {
   __shared__ int32_t s_evals;
   __shared__ uint64_t s_m[kBatchPods];
   __shared__ ResCols s_req[kBatchPods];
@@ -151,6 +161,14 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     if (committed < nb) {
       if (istar < nchain) ns.cuts += 1;
       else ns.truncations += 1;
+    }
+    if (adapt_cap) {
+      // generic ADAPT: the next batch evaluates about twice what this one
+      // committed (its mask and window launches scale with the pods), at
+      // least 32, the whole batch again once a batch commits every pod
+      const int32_t want = committed < nb ? 2 * committed : 2 * nb;
+      const int32_t cap = min(kBatchPods, max(32, (want + 31) & ~31));
+      ns.bcap = cap >= kBatchPods ? 0 : cap;
     }
     __builtin_memcpy(stw, &ns, sizeof(ns));
 #pragma unroll

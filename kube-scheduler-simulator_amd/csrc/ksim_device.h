@@ -152,7 +152,9 @@ struct DevState {
   int64_t cuts;
   // per-pod topology flags of the current cycle (kTopo*), reset by k_bind
   uint32_t topo_flags;
-  int32_t _pad;
+  // generic ADAPT batches: the next batch's pod cap (0: the full batch), set
+  // by k_adapt_commit from the last batch's committed pods, reset by set_run
+  int32_t bcap;
 };
 
 // DevState.topo_flags

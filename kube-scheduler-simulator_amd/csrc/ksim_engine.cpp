@@ -759,6 +759,8 @@ int set_run(ksim_handle* h, int32_t first, int32_t end) {
   h->run_hdr[0] = first;
   h->run_hdr[1] = end;
   HIPCHK(h, hipMemcpyAsync(h->st, h->run_hdr, sizeof(h->run_hdr), hipMemcpyHostToDevice, h->stream));
+  // a run starts with full batches (generic ADAPT batches cap the next one, DevState::bcap)
+  HIPCHK(h, hipMemsetAsync(&h->st->bcap, 0, sizeof(int32_t), h->stream));
   // per-cycle selection state starts from zero (the no-window cycle keeps it
   // zero between its own cycles; other paths leave extrema behind)
   HIPCHK(h, hipMemsetAsync(h->sc.win, 0, sizeof(WinState), h->stream));

@@ -207,7 +207,6 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
   __shared__ int64_t sh[NT / 64];
   __shared__ int32_t s_first;
   const int j = threadIdx.x, lane = j & 63, wv = j >> 6;
-  const int32_t base = st->cursor;
   const int32_t nb = batch_pods(st);
   if (nb <= 0) return false;
   const int32_t s0 = st->next_start;

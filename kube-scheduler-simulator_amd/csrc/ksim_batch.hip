@@ -46,11 +46,12 @@ namespace ksim {
 // incomplete wave (every key a wave did not list is below it).  complete = 1:
 // every S0-feasible node is in the pod's list.
 
-// The pod's top-T from the lanes' kept keys (a[]: the lane's best kTileCand
-// keys, descending; nfeas: the lane's feasible nodes), written to topk[j] (and
-// the sharded record xsend[j]).  Every thread of the block calls it.
-template <int kTopThreads>
-__device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfeas, int32_t j,
+// The pod's top-T from the lanes' kept keys (a[]: the lane's best N keys,
+// descending; nfeas: the lane's feasible nodes), written to topk[j] (and the
+// sharded record xsend[j]).  Every thread of the block calls it.  !SORTED: a[]
+// holds every key of the lane, in node order (nfeas <= N: nothing hidden).
+template <int kTopThreads, int N = kTileCand, bool SORTED = true>
+__device__ __forceinline__ void top_finish(uint64_t (&a)[N], int32_t nfeas, int32_t j,
                                            uint64_t* __restrict__ topk, int32_t* __restrict__ topk_cnt,
                                            int32_t* __restrict__ topk_complete, uint64_t* __restrict__ xsend,
                                            uint64_t* tclk = nullptr) {
@@ -73,9 +74,14 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     __shared__ uint64_t s_wmax[kTopWaves], s_wthr[kTopWaves];
     __shared__ int32_t s_wc[kTopWaves], s_wf[kTopWaves];
     __shared__ uint64_t s_cand[64];
-    const uint64_t u = nfeas > kTileCand ? a[kTileCand - 1] : 0;
+    uint64_t lmax = a[0];
+    if constexpr (!SORTED) {
+#pragma unroll
+      for (int q = 1; q < N; q++) lmax = umax64(lmax, a[q]);
+    }
+    const uint64_t u = SORTED && nfeas > N ? a[N - 1] : 0;
     const uint64_t wthr = wave_max_u64_dpp(u);
-    const uint64_t wmax = wave_max_u64_dpp(a[0]);
+    const uint64_t wmax = wave_max_u64_dpp(lmax);
     const int32_t fsum = (int32_t)wave_sum_u32_dpp((uint32_t)nfeas);
     if (lane == 0) {
       s_wmax[wv] = wmax;
@@ -100,12 +106,18 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     const uint64_t cut = umax64(umax64(thr, L), 1);   // keys are nonzero
     int32_t cl = 0;
 #pragma unroll
-    for (int q = 0; q < kTileCand; q++) cl += a[q] >= cut;   // lists are sorted: a prefix
-    // inclusive wave scan of cl in [0, kTileCand]: by its bits' ballots
-    static_assert(kTileCand < 8, "three ballots cover the count");
-    const uint64_t c0b = __ballot(cl & 1), c1b = __ballot(cl & 2), c2b = __ballot(cl & 4);
-    const int32_t pre = (int32_t)(mask_below(c0b) + 2 * mask_below(c1b) + 4 * mask_below(c2b)) + cl;
-    if (lane == 0) s_wc[wv] = __popcll(c0b) + 2 * __popcll(c1b) + 4 * __popcll(c2b);
+    for (int q = 0; q < N; q++) cl += a[q] >= cut;   // SORTED: a prefix
+    // inclusive wave scan of cl in [0, N]: by its bits' ballots
+    constexpr int kBits = N < 4 ? 2 : N < 8 ? 3 : 4;
+    static_assert(N < 16, "four ballots cover the count");
+    int32_t pre = cl, wsum = 0;
+#pragma unroll
+    for (int bit = 0; bit < kBits; bit++) {
+      const uint64_t cb = __ballot(cl & (1 << bit));
+      pre += (int32_t)mask_below(cb) << bit;
+      wsum += __popcll(cb) << bit;
+    }
+    if (lane == 0) s_wc[wv] = wsum;
     lds_barrier();
 #ifdef KSIM_TC_CLOCKS
     if (tclk && threadIdx.x == 0) tclk[1] = __builtin_amdgcn_s_memrealtime();
@@ -119,9 +131,16 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
     }
     if (C <= 64) {                                 // block-uniform
       const int32_t base_i = off + pre - cl;
+      if constexpr (SORTED) {
 #pragma unroll
-      for (int q = 0; q < kTileCand; q++)
-        if (q < cl) s_cand[base_i + q] = a[q];
+        for (int q = 0; q < N; q++)
+          if (q < cl) s_cand[base_i + q] = a[q];
+      } else {
+        int32_t w = base_i;
+#pragma unroll
+        for (int q = 0; q < N; q++)
+          if (a[q] >= cut) s_cand[w++] = a[q];
+      }
       lds_barrier();
 #ifdef KSIM_TC_CLOCKS
       if (tclk && threadIdx.x == 0) tclk[2] = __builtin_amdgcn_s_memrealtime();
@@ -152,17 +171,27 @@ __device__ __forceinline__ void top_finish(uint64_t (&a)[kTileCand], int32_t nfe
   uint64_t mine = 0;
   int32_t cnt = 0, complete = 0, popped = 0;
   for (int t = 0; t < kTopT; t++) {
-    const uint64_t m = wave_max_u64_hi(a[0]);
+    uint64_t lm = a[0];
+    if constexpr (!SORTED) {
+#pragma unroll
+      for (int q = 1; q < N; q++) lm = umax64(lm, a[q]);
+    }
+    const uint64_t m = wave_max_u64_hi(lm);
     if (m == 0) { complete = 1; break; }
     if (lane == t) mine = m;
     cnt = t + 1;
     bool stop = false;
-    if (a[0] == m) {                              // keys are unique (the node is in the key)
-      a[0] = a[1];
-      a[1] = a[2];
-      a[2] = a[3];
-      a[3] = 0;
-      stop = ++popped == kTileCand && nfeas > kTileCand;
+    if constexpr (SORTED) {
+      if (a[0] == m) {                            // keys are unique (the node is in the key)
+#pragma unroll
+        for (int q = 0; q + 1 < N; q++) a[q] = a[q + 1];
+        a[N - 1] = 0;
+        stop = ++popped == N && nfeas > N;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < N; q++)
+        if (a[q] == m) a[q] = 0;
     }
     if (__ballot(stop)) break;
   }
@@ -721,7 +750,11 @@ struct PodReq {
   int64_t cpu, mem, eph, nzc, nzm;
 };
 
-template <bool FLUSH, bool DIRECT>
+// DEF: the FAST key with the default profile's shape compiled in (fast_def).
+// KEEP: the local node range is at most kKeepPerLane * 1024 nodes, so every
+// lane keeps all of its keys (no insertion network; top_finish unsorted).
+constexpr int kKeepPerLane = 8;
+template <bool FLUSH, bool DIRECT, bool DEF = false, bool KEEP = false>
 __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
@@ -948,24 +981,41 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     r.nz_cpu += d.nzc;
     r.nz_mem += d.nzm;
     r.num_pods += d.pods;
-    return dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+    return dyn_key_fast_t<DEF>(bq, pf, r, ic, im, hseed, c.base + node);
   };
-  auto insert = [&](uint64_t k) {
-    nfeas += k != 0;
-    a[3] = umax64(a[3], k);
-    cswap_desc(a[2], a[3]);
-    cswap_desc(a[1], a[2]);
-    cswap_desc(a[0], a[1]);
-  };
+  uint64_t ak[kKeepPerLane];                   // KEEP: the lane's keys, node order
+  if constexpr (KEEP) {
+#pragma unroll
+    for (int q = 0; q < kKeepPerLane; q++) ak[q] = 0;
+#pragma unroll
+    for (int q = 0; q < kKeepPerLane; q++) {
+      if (c.eval_lo + q * kThreads >= c.eval_hi) break;   // block-uniform
+      const int32_t node = c.eval_lo + tid + q * kThreads;
+      const uint64_t k = node < c.eval_hi ? key_of(node) : 0;
+      nfeas += k != 0;
+      ak[q] = k;
+    }
+  } else {
+    auto insert = [&](uint64_t k) {
+      nfeas += k != 0;
+      a[3] = umax64(a[3], k);
+      cswap_desc(a[2], a[3]);
+      cswap_desc(a[1], a[2]);
+      cswap_desc(a[0], a[1]);
+    };
 #pragma unroll 1
-  for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) insert(key_of(node));
+    for (int32_t node = c.eval_lo + tid; node < c.eval_hi; node += kThreads) insert(key_of(node));
+  }
 #ifdef KSIM_TC_CLOCKS
   t_loop = __builtin_amdgcn_s_memrealtime();
 #endif
   materialize();
   // xsend (replicated handles): this replica's record of its node range, for the all-gather
 #ifdef KSIM_TC_CLOCKS
-  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend, tclk);
+  if constexpr (KEEP)
+    top_finish<kThreads, kKeepPerLane, false>(ak, nfeas, b, topk, topk_cnt, topk_complete, xsend, tclk);
+  else
+    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend, tclk);
   if (tid == 0) {
     // dbg: 0 prologue, 1 thread 0's node loop, 2 wait for the block's slowest
     // wave, 3 the finish after its first barrier, 4 prologue to the first
@@ -981,24 +1031,43 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     atomicAdd(&g_cp_dbg[7], (unsigned long long)(tp[2] - tp[1]));
   }
 #else
-  top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
+  if constexpr (KEEP)
+    top_finish<kThreads, kKeepPerLane, false>(ak, nfeas, b, topk, topk_cnt, topk_complete, xsend);
+  else
+    top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
 #endif
   if (st_writer) update_state();              // waves past the first return from the merge early
 }
 
 // the evaluation launch of a deferred-commit batch (DIRECT overlay when the
-// local node range fits kLazyDirect)
+// local node range fits kLazyDirect; DEF / KEEP as k_batch_top_commit says)
+template <bool FLUSH, bool DIRECT, bool DEF, bool KEEP>
+static void launch_tc(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
+  const LaunchArgs& a = z.a;
+  k_batch_top_commit<FLUSH, DIRECT, DEF, KEEP><<<kBatchPods, 1024, 0, stream>>>(
+      a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.chosen, xsend);
+}
 template <bool FLUSH>
 static void launch_top_commit(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
   const LaunchArgs& a = z.a;
-  if (a.c.n <= kLazyDirect)
-    k_batch_top_commit<FLUSH, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                      a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                      xsend);
-  else
-    k_batch_top_commit<FLUSH, false><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk,
-                                                                       a.s.topk_cnt, a.s.topk_complete, a.chosen,
-                                                                       xsend);
+  const bool direct = a.c.n <= kLazyDirect;
+  if constexpr (FLUSH) {
+    if (direct) launch_tc<FLUSH, true, false, false>(z, xsend, stream);
+    else launch_tc<FLUSH, false, false, false>(z, xsend, stream);
+  } else {
+    const bool def = fast_def(a.bp);
+    const bool keep = direct && a.c.eval_hi - a.c.eval_lo <= kKeepPerLane * 1024;
+    if (keep) {
+      if (def) launch_tc<FLUSH, true, true, true>(z, xsend, stream);
+      else launch_tc<FLUSH, true, false, true>(z, xsend, stream);
+    } else if (direct) {
+      if (def) launch_tc<FLUSH, true, true, false>(z, xsend, stream);
+      else launch_tc<FLUSH, true, false, false>(z, xsend, stream);
+    } else {
+      if (def) launch_tc<FLUSH, false, true, false>(z, xsend, stream);
+      else launch_tc<FLUSH, false, false, false>(z, xsend, stream);
+    }
+  }
 }
 
 const char* const kLazyKernelNames[kKernelsPerLazy] = {"k_batch_top_commit", "k_batch_chain_pairs"};

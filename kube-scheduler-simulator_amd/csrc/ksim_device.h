@@ -1262,8 +1262,11 @@ struct FastProg {
   double iw_cpu, iw_mem, iw_sum;
 };
 __device__ __forceinline__ FastProg fast_prog(const BatchProg& bp);
+// DEF: the default profile's shape, known at compile time (fast_def below)
+template <bool DEF = false>
 __device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m);
+template <bool DEF = false>
 __device__ __forceinline__ int32_t fast_balanced_allocation(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                             double inv_c, double inv_m);
 
@@ -1537,6 +1540,15 @@ struct BatchProg {
   uint32_t slot_hi, _pad2;
 };
 
+// The FAST key with the default profile's shape compiled in (dyn_key_fast_t<true>):
+// a Fit filter, equal LeastAllocated weights (fit_w_eq), a score plugin, and
+// Fit / BA score weights in [0, 2^14) (24-bit multiplies).  The launch picks
+// the kernel by it, so a profile change that flips it drops the batch graphs.
+__host__ __device__ inline bool fast_def(const BatchProg& bp) {
+  return bp.has_fit_filter && bp.fit_w_eq && !bp.no_score && bp.w_fit >= 0 && bp.w_fit < (1 << 14) &&
+         bp.w_ba >= 0 && bp.w_ba < (1 << 14);
+}
+
 // DevPods.bflags (batch path, per pod)
 constexpr int32_t kBatchStaticTrivial = 1; // every static filter passes on every node (host-proven)
 constexpr int32_t kPodRegistersValues = 2; // has a ScheduleAnyway spread keyed by a non-hostname column
@@ -1751,6 +1763,7 @@ __device__ __forceinline__ FastProg fast_prog(const BatchProg& bp) {
   return f;
 }
 
+template <bool DEF>
 __device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                         double inv_c, double inv_m) {
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
@@ -1760,7 +1773,7 @@ __device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const
   const int32_t qm = (int32_t)div_rn(u52_to_f64(dm) * (double)kMaxNodeScore, am, inv_m);
   const int32_t sc = (hc && dc >= 0) ? qc : 0;   // requested > capacity scores 0
   const int32_t sm = (hm && dm >= 0) ? qm : 0;
-  if (q.w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
+  if (DEF || q.w_eq) return (hc && hm) ? (sc + sm) >> 1 : hc ? sc : sm;   // (sc w + sm w) / (2 w)
   // selects of values (a select of the struct members' lvalues becomes an
   // address select, and the struct a per-lane copy in LDS)
   const int64_t fwc = q.fw_cpu, fwm = q.fw_mem;
@@ -1776,31 +1789,51 @@ __device__ __forceinline__ int32_t fast_least_allocated(const FastProg& q, const
 // allocatable < 2^46 and the short conversion is exact (without one the sums
 // are unbounded and take the general conversion).  With one resource missing
 // the standard deviation is 0 (score 100), as with both present and equal.
+template <bool DEF>
 __device__ __forceinline__ int32_t fast_balanced_allocation(const FastProg& q, const ksim_pod& p, const NodeRow& r,
                                                             double inv_c, double inv_m) {
   const bool hc = r.alloc_cpu != 0, hm = r.alloc_mem != 0;
   const int64_t qc = r.req_cpu + p.req_cpu, qm = r.req_mem + p.req_mem;
-  const double fc = fmin(div_rn(q.fit ? u52_to_f64(qc) : (double)qc, u52_to_f64(r.alloc_cpu), inv_c), 1.0);
-  const double fm = fmin(div_rn(q.fit ? u52_to_f64(qm) : (double)qm, u52_to_f64(r.alloc_mem), inv_m), 1.0);
+  const bool fit = DEF || q.fit;
+  const double fc = fmin(div_rn(fit ? u52_to_f64(qc) : (double)qc, u52_to_f64(r.alloc_cpu), inv_c), 1.0);
+  const double fm = fmin(div_rn(fit ? u52_to_f64(qm) : (double)qm, u52_to_f64(r.alloc_mem), inv_m), 1.0);
   const int32_t b = (int32_t)((1 - fabs((fc - fm) / 2)) * (double)kMaxNodeScore);
   return (hc && hm) ? b : kMaxNodeScore;
 }
 
-__device__ __forceinline__ uint64_t dyn_key_fast(const FastProg& q, const ksim_pod& p, const NodeRow& r,
-                                                 double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
+// DEF (fast_def(bp) on the host): a Fit filter, equal LeastAllocated weights,
+// at least one score plugin and both score weights below 2^14, so the key's
+// shape is compiled in: no uniform branches in the node loop, and the weights
+// scale the scores by 24-bit multiplies (w * 100 < 2^21) instead of 32-bit ones.
+template <bool DEF>
+__device__ __forceinline__ uint64_t dyn_key_fast_t(const FastProg& q, const ksim_pod& p, const NodeRow& r,
+                                                   double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
   // the Fit filter with non-short-circuit operators: one select, no branches
   // (the request's zero test is uniform across the wave)
   const bool any = (p.req_cpu | p.req_mem | p.req_eph) != 0;
   const bool fits = (p.req_cpu <= r.alloc_cpu - r.req_cpu) & (p.req_mem <= r.alloc_mem - r.req_mem) &
                     (p.req_eph <= r.alloc_eph - r.req_eph);
-  const bool ok = !q.fit | ((r.num_pods < r.alloc_pods) & (!any | fits));
+  const bool ok = !(DEF || q.fit) | ((r.num_pods < r.alloc_pods) & (!any | fits));
   int32_t tot = 0;
-  if (q.w_fit) tot += q.w_fit * fast_least_allocated(q, p, r, inv_c, inv_m);
-  if (q.w_ba) tot += q.w_ba * fast_balanced_allocation(q, p, r, inv_c, inv_m);
-  if (q.no_score) tot = 1;
+  if constexpr (DEF) {
+    // the masks change no value (weights < 2^14, scores in [0, 100]); they let
+    // the compiler prove both factors narrow and pick v_mul_u32_u24
+    const uint32_t la = (uint32_t)fast_least_allocated<true>(q, p, r, inv_c, inv_m) & 0xffffu;
+    const uint32_t ba = (uint32_t)fast_balanced_allocation<true>(q, p, r, inv_c, inv_m) & 0xffffu;
+    tot = (int32_t)(((uint32_t)q.w_fit & 0x3fffu) * la + ((uint32_t)q.w_ba & 0x3fffu) * ba);
+  } else {
+    if (q.w_fit) tot += q.w_fit * fast_least_allocated(q, p, r, inv_c, inv_m);
+    if (q.w_ba) tot += q.w_ba * fast_balanced_allocation(q, p, r, inv_c, inv_m);
+    if (q.no_score) tot = 1;
+  }
   const uint64_t h = splitmix64(hseed ^ (uint64_t)(uint32_t)gnode) >> 38;
   const uint64_t key = ((uint64_t)(uint32_t)tot << 44) | (h << 18) | (uint64_t)(KSIM_KEY_NODE_MASK - gnode);
   return ok ? key : 0;
+}
+
+__device__ __forceinline__ uint64_t dyn_key_fast(const FastProg& q, const ksim_pod& p, const NodeRow& r,
+                                                 double inv_c, double inv_m, uint64_t hseed, int32_t gnode) {
+  return dyn_key_fast_t<false>(q, p, r, inv_c, inv_m, hseed, gnode);
 }
 
 // The request fields the FAST pair key reads (pod j's and the bound pod k's),

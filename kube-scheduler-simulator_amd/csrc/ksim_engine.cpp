@@ -1893,10 +1893,11 @@ int ksim_set_profile(ksim_handle* h, const ksim_profile* p) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   // the batch graphs read the profile from d_prof / d_bp; only the ADAPT
   // window size K is captured by value (from percentageOfNodesToScore)
-  // and the Fit filter's ignored scalar columns (DevCluster::fit_ignore)
+  // and the Fit filter's ignored scalar columns (DevCluster::fit_ignore); the
+  // launch picks the evaluation kernel by the FAST key's shape (fast_def)
   const bool keep_batch_graphs = h->has_profile &&
                                  h->prof.percentage_of_nodes_to_score == p->percentage_of_nodes_to_score &&
-                                 h->dc.fit_ignore == p->fit_ignored_scalar;
+                                 h->dc.fit_ignore == p->fit_ignored_scalar && fast_def(h->bp) == fast_def(bp);
   // batchability depends on the profile: a loaded queue must be reloaded (its
   // buffers stay allocated for ksim_load_pods to reuse)
   h->dp = DevPods{};

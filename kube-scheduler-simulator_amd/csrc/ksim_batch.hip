@@ -636,7 +636,8 @@ unsigned long long* cp_clock_buffer() { return nullptr; }
 
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
-template <bool FAST, bool LAZY = false, bool STAB = false>
+// R: each pod's list is R slice records (the node-stationary evaluation)
+template <bool FAST, bool LAZY = false, bool STAB = false, int R = 1>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
 #else
   unsigned long long* dbgc = nullptr;
 #endif
-  if (!chain_block(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc, kBatchPods, c.n_total)) {
+  if (!chain_block<R>(L, st, topk, topk_cnt, topk_complete, &gk, &nchain, dbgc, kBatchPods, c.n_total)) {
     if (LAZY && blockIdx.x == 0 && threadIdx.x == 0) *chain_end = -1;
     return;
   }
@@ -753,8 +754,26 @@ struct PodReq {
 // DEF: the FAST key with the default profile's shape compiled in (fast_def).
 // KEEP: the local node range is at most kKeepPerLane * 1024 nodes, so every
 // lane keeps all of its keys (no insertion network; top_finish unsorted).
+// NS: node-stationary blocks on larger ranges: block b keys the kNsPods pods
+// kNsPods * (b / kNsSlices) + [0, kNsPods) over node slice b % kNsSlices, so
+// a node's row, its overlay delta and the addressing are paid once for
+// kNsPods keys; each block writes one list record per pod for its slice (rec
+// = pod * kNsSlices + slice: the slice's provable top-T), which
+// chain_block<kNsSlices> merges as it loads the pod's list.
 constexpr int kKeepPerLane = 8;
-template <bool FLUSH, bool DIRECT, bool DEF = false, bool KEEP = false>
+constexpr int kNsSlices = 4;
+constexpr int kNsPods = 4;
+static_assert(kNsSlices == kNsPods && kBatchPods % kNsPods == 0, "NS grid: kBatchPods blocks");
+static_assert(kNsSlices <= kMaxListRecords, "NS records: DevScratch::topk holds kMaxListRecords per pod");
+
+// a wave-uniform 64-bit value as such (SGPRs)
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+template <bool FLUSH, bool DIRECT, bool DEF = false, bool KEEP = false, bool NS = false>
 __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p, LazyStep L,
@@ -767,7 +786,8 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   // s_rq: batch i-1's pod requests, then each bound node's delta; entry
   // kBatchPods stays zero (DIRECT: the entry of every node batch i-1 did not bind)
   __shared__ ResCols s_rq[kBatchPods + 1];
-  __shared__ PodReq s_pc[kBatchPods + 1];      // pod cur0 + b + t: this block's pod of batch i is t = committed
+  // pod cur0 + pod0 + t: this block's (first) pod of batch i is t = committed
+  __shared__ PodReq s_pc[kBatchPods + (NS ? kNsPods : 1)];
   __shared__ __attribute__((aligned(16))) int16_t s_ent[DIRECT ? kLazyDirect : 1];   // node -> entry
   __shared__ int32_t s_hkey[DIRECT ? 1 : kLazyHash];   // overlay hash: local node or -1
   __shared__ int16_t s_hval[DIRECT ? 1 : kLazyHash];   // ... its entry
@@ -775,6 +795,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   __shared__ int32_t s_istar, s_inode, s_sched, s_unsched;
   const int tid = threadIdx.x;
   const int32_t b = blockIdx.x;
+  const int32_t pod0 = NS ? (b / kNsSlices) * kNsPods : b;   // the block's first pod (batch i offset)
 #ifdef KSIM_TC_CLOCKS
   // phase clocks of every block (KSIM_TC_CLOCKS builds, tools/tc_clocks.py),
   // thread 0's view, summed (see the end of the kernel)
@@ -794,10 +815,10 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   const int64_t seq0 = L.st_in->pod_seq;
   // every pod record the commit may need, before the cut is known (they only
   // depend on cur0): pod tid of batch i-1 (its request, kept if committed) and
-  // the candidates cur0 + b + t for this block's pod of batch i
+  // the candidates cur0 + pod0 + t for this block's pods of batch i
   ResCols rq{0, 0, 0, 0, 0, 0};
-  for (int x = tid; x < 2 * kBatchPods + 1; x += kThreads) {
-    const int32_t q = x < kBatchPods ? cur0 + x : cur0 + b + (x - kBatchPods);
+  for (int x = tid; x < 2 * kBatchPods + (NS ? kNsPods : 1); x += kThreads) {
+    const int32_t q = x < kBatchPods ? cur0 + x : cur0 + pod0 + (x - kBatchPods);
     if (q < end) {
       const ksim_pod& y = P.pods[q];
       if (x < kBatchPods) {
@@ -839,7 +860,7 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   if (tid < committed) s_rq[tid] = rq;
   // this block's pod of batch i
   const int32_t base = cur0 + committed;
-  const int32_t pi = base + b;
+  const int32_t pi = base + pod0;
   const bool live = !FLUSH && pi < min(end, base + kBatchPods);   // block-uniform
   lds_barrier();
 #ifdef KSIM_TC_CLOCKS
@@ -952,6 +973,86 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     if (st_writer) update_state();
     return;
   }
+  if constexpr (NS) {
+    // pods pod0 + [0, kNsPods) of batch i against S_i over node slice s
+    const int32_t s = b % kNsSlices;
+    const int32_t len = c.eval_hi - c.eval_lo, S = (len + kNsSlices - 1) / kNsSlices;
+    const int32_t slo = c.eval_lo + s * S, shi = min(c.eval_hi, slo + S);
+    const FastProg bq = fast_prog(*bp_p);
+    const int32_t cu = __builtin_amdgcn_readfirstlane(committed);
+    ksim_pod pf[kNsPods];
+    uint64_t hs[kNsPods];
+    bool pv[kNsPods];
+#pragma unroll
+    for (int p = 0; p < kNsPods; p++) {
+      const PodReq x = s_pc[cu + p];
+      pf[p].req_cpu = uni64(x.cpu);
+      pf[p].req_mem = uni64(x.mem);
+      pf[p].req_eph = uni64(x.eph);
+      pf[p].nz_cpu = uni64(x.nzc);
+      pf[p].nz_mem = uni64(x.nzm);
+#pragma unroll
+      for (int k = 0; k < KSIM_MAX_SCALAR; k++) pf[p].scalar_req[k] = 0;   // FAST pods: no scalar requests
+      hs[p] = prof_p->tiebreak_seed ^ ((uint64_t)(seq0 + cu + pod0 + p) << 20);
+      pv[p] = pi + p < end;                      // block-uniform
+    }
+    uint64_t ap[kNsPods][kTileCand];
+    int32_t nf[kNsPods];
+#pragma unroll
+    for (int p = 0; p < kNsPods; p++) {
+      nf[p] = 0;
+#pragma unroll
+      for (int q = 0; q < kTileCand; q++) ap[p][q] = 0;
+    }
+#ifdef KSIM_TC_CLOCKS
+    t_pro = __builtin_amdgcn_s_memrealtime();
+#endif
+#pragma unroll 1
+    for (int32_t node = slo + tid; node < shi; node += kThreads) {
+      NodeRow r = load_res_row_off(c, node);
+      const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
+      const ResCols d = delta(node);
+      r.req_cpu += d.cpu;
+      r.req_mem += d.mem;
+      r.req_eph += d.eph;
+      r.nz_cpu += d.nzc;
+      r.nz_mem += d.nzm;
+      r.num_pods += d.pods;
+#pragma unroll
+      for (int p = 0; p < kNsPods; p++) {
+        const uint64_t k = pv[p] ? dyn_key_fast_t<DEF>(bq, pf[p], r, ic, im, hs[p], c.base + node) : 0;
+        nf[p] += k != 0;
+        ap[p][3] = umax64(ap[p][3], k);
+        cswap_desc(ap[p][2], ap[p][3]);
+        cswap_desc(ap[p][1], ap[p][2]);
+        cswap_desc(ap[p][0], ap[p][1]);
+      }
+    }
+#ifdef KSIM_TC_CLOCKS
+    t_loop = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      atomicAdd(&g_cp_dbg[0], (unsigned long long)(t_pro - t_in));
+      atomicAdd(&g_cp_dbg[1], (unsigned long long)(t_loop - t_pro));
+      atomicAdd(&g_cp_dbg[4], (unsigned long long)(tp[0] - t_in));
+      atomicAdd(&g_cp_dbg[5], 1ull);
+      atomicAdd(&g_cp_dbg[6], (unsigned long long)(tp[1] - tp[0]));
+      atomicAdd(&g_cp_dbg[7], (unsigned long long)(tp[2] - tp[1]));
+    }
+#endif
+    materialize();
+    // the pods' slice records one after another (top_finish's LDS reused:
+    // a barrier between them, which waits for the previous merge's wave)
+#pragma unroll
+    for (int p = 0; p < kNsPods; p++) {
+      if (p) lds_barrier();
+      top_finish<kThreads>(ap[p], nf[p], (pod0 + p) * kNsSlices + s, topk, topk_cnt, topk_complete, nullptr);
+    }
+#ifdef KSIM_TC_CLOCKS
+    if (tid == 0) atomicAdd(&g_cp_dbg[3], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_loop));
+#endif
+    if (st_writer) update_state();
+    return;
+  } else {
   // pod b of batch i against S_i (k_batch_top's loops with the overlay)
   ksim_pod pf;
   {
@@ -1037,15 +1138,22 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
     top_finish<kThreads>(a, nfeas, b, topk, topk_cnt, topk_complete, xsend);
 #endif
   if (st_writer) update_state();              // waves past the first return from the merge early
+  }
 }
 
 // the evaluation launch of a deferred-commit batch (DIRECT overlay when the
 // local node range fits kLazyDirect; DEF / KEEP as k_batch_top_commit says)
-template <bool FLUSH, bool DIRECT, bool DEF, bool KEEP>
+template <bool FLUSH, bool DIRECT, bool DEF, bool KEEP, bool NS = false>
 static void launch_tc(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
   const LaunchArgs& a = z.a;
-  k_batch_top_commit<FLUSH, DIRECT, DEF, KEEP><<<kBatchPods, 1024, 0, stream>>>(
+  k_batch_top_commit<FLUSH, DIRECT, DEF, KEEP, NS><<<kBatchPods, 1024, 0, stream>>>(
       a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.chosen, xsend);
+}
+// the node-stationary form (its records are merged by chain_block<kNsSlices>):
+// unsharded launches of the default profile's shape past the KEEP range
+static bool ns_eval(const LaunchArgs& a, const uint64_t* xsend) {
+  const int32_t len = a.c.eval_hi - a.c.eval_lo;
+  return !xsend && fast_def(a.bp) && len > kKeepPerLane * 1024;
 }
 template <bool FLUSH>
 static void launch_top_commit(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
@@ -1057,7 +1165,10 @@ static void launch_top_commit(const LazyBatch& z, uint64_t* xsend, hipStream_t s
   } else {
     const bool def = fast_def(a.bp);
     const bool keep = direct && a.c.eval_hi - a.c.eval_lo <= kKeepPerLane * 1024;
-    if (keep) {
+    if (ns_eval(a, xsend)) {
+      if (direct) launch_tc<FLUSH, true, true, false, true>(z, xsend, stream);
+      else launch_tc<FLUSH, false, true, false, true>(z, xsend, stream);
+    } else if (keep) {
       if (def) launch_tc<FLUSH, true, true, true>(z, xsend, stream);
       else launch_tc<FLUSH, true, false, true>(z, xsend, stream);
     } else if (direct) {
@@ -1077,9 +1188,14 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
   if (evs) (void)hipEventRecord(evs[0], stream);
   launch_top_commit<false>(z, nullptr, stream);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  k_batch_chain_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
-      z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax, a.s.pnorm,
-      a.s.pinv);
+  if (ns_eval(a, nullptr))                     // the slice records merged as the chain loads them
+    k_batch_chain_pairs<true, true, false, kNsSlices><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax,
+        a.s.pnorm, a.s.pinv);
+  else
+    k_batch_chain_pairs<true, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax,
+        a.s.pnorm, a.s.pinv);
   if (evs) (void)hipEventRecord(evs[2], stream);
   return 0x3u;
 }

@@ -47,6 +47,26 @@ struct ChainLds {
 // i's guessed key (0: none, or i past the exact prefix) and *nchain = the
 // prefix length.  A pure function of the lists: every block that runs it gets
 // the same guesses.
+// The top T of two descending lists, descending, into x: the elementwise max
+// of x and y reversed is bitonic and holds the top T; a half-cleaner network
+// sorts it.
+__device__ __forceinline__ void merge_top(uint64_t (&x)[kTopT], const uint64_t (&y)[kTopT]) {
+  static_assert((kTopT & (kTopT - 1)) == 0, "bitonic merge: T a power of two");
+#pragma unroll
+  for (int e = 0; e < kTopT; e++) x[e] = umax64(x[e], y[kTopT - 1 - e]);
+#pragma unroll
+  for (int h = kTopT / 2; h >= 1; h >>= 1)
+#pragma unroll
+    for (int e = 0; e < kTopT; e++)
+      if ((e & h) == 0) cswap_desc(x[e], x[e + h]);
+}
+
+// R > 1: pod i's list is R records (i * R + r: a node slice's provable top-T,
+// count, complete), merged here.  A key is provable when it is >= the last
+// listed key of every incomplete record (a record hides only keys below its
+// last); the merged list is complete when every record is and nothing was
+// dropped.
+template <int R = 1>
 __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restrict__ st,
                                             const uint64_t* __restrict__ topk,
                                             const int32_t* __restrict__ topk_cnt,
@@ -62,10 +82,46 @@ __device__ __forceinline__ bool chain_block(ChainLds& L, const DevState* __restr
   // the buffers hold kBatchPods entries, so no bound check is needed yet)
   uint64_t lst[kTopT];
   int cnt0, complete0;
+  if constexpr (R == 1) {
 #pragma unroll
-  for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
-  cnt0 = topk_cnt[i];
-  complete0 = topk_complete[i];
+    for (int e = 0; e < kTopT; e++) lst[e] = topk[(size_t)i * kTopT + e];
+    cnt0 = topk_cnt[i];
+    complete0 = topk_complete[i];
+  } else {
+    uint64_t k[R][kTopT];
+    int32_t rc[R], rp[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+#pragma unroll
+      for (int e = 0; e < kTopT; e++) k[r][e] = topk[((size_t)i * R + r) * kTopT + e];
+      rc[r] = topk_cnt[i * R + r];
+      rp[r] = topk_complete[i * R + r];
+    }
+    uint64_t thr = 0;
+    int32_t all_c = 1, csum = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      uint64_t last = ~0ull;                     // an incomplete empty record proves nothing
+#pragma unroll
+      for (int e = 0; e < kTopT; e++) last = e == rc[r] - 1 ? k[r][e] : last;
+      if (!rp[r]) thr = umax64(thr, last);
+      all_c &= rp[r];
+      csum += rc[r];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int e = 0; e < kTopT; e++)
+        if (k[r][e] < thr) k[r][e] = 0;          // a sorted suffix: the records stay sorted
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) lst[e] = k[0][e];
+#pragma unroll
+    for (int r = 1; r < R; r++) merge_top(lst, k[r]);
+    cnt0 = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) cnt0 += lst[e] != 0;
+    complete0 = all_c && csum <= kTopT;
+  }
   const int32_t base = st->cursor;
   const int32_t nb = min(nb_cap, st->end - base);   // nb_cap: the topology batch's pod count
   if (nb <= 0) return false;

@@ -2137,9 +2137,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.detail, uint32_t*, 4 * N);
   SCR(s.raw, int64_t*, 8 * N * KSIM_MAX_SCORE);
   SCR(s.part, int64_t*, 8 * N);
-  SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kTopT);
-  SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods);
-  SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods);
+  // [B][kMaxListRecords] list records: the node-stationary evaluation writes one per node slice
+  SCR(s.topk, uint64_t*, 8 * (size_t)kBatchPods * kMaxListRecords * kTopT);
+  SCR(s.topk_cnt, int32_t*, 4 * (size_t)kBatchPods * kMaxListRecords);
+  SCR(s.topk_complete, int32_t*, 4 * (size_t)kBatchPods * kMaxListRecords);
   SCR(s.gkey, uint64_t*, 8 * (size_t)kBatchPods);
   SCR(s.chain_end, int32_t*, 4);
   SCR(s.pmax, uint64_t*, 8 * 2 * (size_t)kBatchPods);   // [M | sharded ADAPT broken flags]

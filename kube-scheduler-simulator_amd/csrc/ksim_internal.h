@@ -28,6 +28,7 @@ constexpr bool kAbForms = false;
 #endif
 constexpr int kBatchPods = KSIM_BATCH_PODS;   // B: pods per speculative batch
 constexpr int kTopT = KSIM_TOP_T;             // T: candidate keys kept per pod
+constexpr int kMaxListRecords = 4;            // list records per pod (ksim_batch.hip kNsSlices)
 static_assert(kBatchPods % 64 == 0 && kBatchPods <= 1024 && kTopT <= 64, "batch geometry");
 constexpr int kTopThreads = 1024;  // threads per pod of the batch top
 constexpr int kTileCand = 4;       // best keys each lane of the batch top keeps per pod

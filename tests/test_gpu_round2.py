@@ -225,6 +225,27 @@ def test_config3_full():
     _same_state(eng, ora)
 
 
+@pytest.mark.parametrize("n_nodes,n_pods", [(100000, 3000), (20000, 6000)])
+def test_node_stationary_p100(n_nodes, n_pods):
+    """P100 batches past 8,192 nodes on one handle: the node-stationary
+    evaluation (4 pods x a quarter of the nodes per block, the slice lists
+    merged by the chain) on config 4's cluster (hash overlay) and on a
+    20,000-node config-2 cluster (overlay indexed by node id)."""
+    if n_nodes == 100000:
+        cluster, pods = gen.config4(n_pods=n_pods)
+    else:
+        cluster, pods = gen.config2(n_nodes=n_nodes, n_pods=n_pods, seed=5)
+    prof = _prof(100)
+    eng = _engine(cluster, prof)
+    chosen, st = eng.schedule_batch(pods)
+    ora = Oracle(cluster, prof)
+    ochosen, ost = ora.schedule(pods, nthreads=16)
+    np.testing.assert_array_equal(chosen, ochosen)
+    assert st.evals == ost.evals and st.scheduled == ost.scheduled
+    assert st.perpod_cycles == 0 and st.batches > 0
+    _same_state(eng, ora)
+
+
 def test_config4_group8():
     """Config 4's cluster (100,000 nodes) as an in-process 8-shard group, the
     node-sharded exchange protocol on one device, for 20,000 pods."""

@@ -341,7 +341,7 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
 // the class's static verdict, plus for kPodNormVaries pods the normalized
 // part (norm_part_fast) over the maxima of a first pass.  ov(row): as for
 // generic_keys.
-template <int kTopThreads, typename Ov>
+template <int kTopThreads, bool DEF, typename Ov>
 __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPods& P, const BatchProg& bp,
                                                const FastProg& bq, const ksim_pod& pf, int32_t pi, int32_t j,
                                                uint64_t hseed, int64_t* __restrict__ pnorm, uint64_t (&a)[kTileCand],
@@ -355,7 +355,7 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
     const double ic = ld_off(c.inv_cpu, o8), im = ld_off(c.inv_mem, o8);
     w = ld_off(srow, o8);
     ov(r);
-    const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+    const uint64_t k = dyn_key_fast_t<DEF>(bq, pf, r, ic, im, hseed, c.base + node);
     return stab_pass(w) ? k : 0;
   };
   // kPodNormVaries: the first pass keeps each node's key (without the
@@ -398,8 +398,9 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
   }
 }
 
-// STAB (FAST only): a static-class run (stab_fast_keys).
-template <bool FAST, int kTopThreads, bool STAB = false>
+// STAB (FAST only): a static-class run (stab_fast_keys).  DEF (FAST only): the
+// default profile's key shape compiled in (fast_def).
+template <bool FAST, int kTopThreads, bool STAB = false, bool DEF = false>
 __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p,
@@ -428,14 +429,14 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
     const FastProg bq = fast_prog(bp);
     const ksim_pod pf = fast_pod_fields(p);
     if constexpr (STAB) {
-      stab_fast_keys<kTopThreads>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, nfeas, [](NodeRow&) {});
+      stab_fast_keys<kTopThreads, DEF>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, nfeas, [](NodeRow&) {});
     } else {
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
       const NodeRow r = load_res_row_off(c, node);
       const double ic = ld_off(c.inv_cpu, (uint32_t)node << 3), im = ld_off(c.inv_mem, (uint32_t)node << 3);
       __builtin_amdgcn_sched_barrier(0);      // the row in flight before the key
-      const uint64_t k = dyn_key_fast(bq, pf, r, ic, im, hseed, c.base + node);
+      const uint64_t k = dyn_key_fast_t<DEF>(bq, pf, r, ic, im, hseed, c.base + node);
       nfeas += k != 0;
       a[3] = umax64(a[3], k);
       cswap_desc(a[2], a[3]);
@@ -1232,9 +1233,16 @@ const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch
 
 // Evaluation and per-pod top-T (xsend: the sharded record, else null).
 static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream) {
-  if (a.stab)   // static-class runs (unsharded handles only: run_stab)
+  const bool def = fast_def(a.bp);
+  if (a.stab && def)   // static-class runs (unsharded handles only: run_stab)
+    k_batch_top<true, 1024, true, true><<<kBatchPods, 1024, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
+  else if (a.stab)
     k_batch_top<true, 1024, true><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk,
                                                                     a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
+  else if (a.fast && def)
+    k_batch_top<true, 1024, false, true><<<kBatchPods, 1024, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
   else if (a.fast)
     k_batch_top<true, 1024><<<kBatchPods, 1024, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt,
                                                               a.s.topk_complete, xsend, a.s.pnorm);

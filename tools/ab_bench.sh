@@ -1,7 +1,8 @@
 #!/bin/bash
-# GPU parity tests named by K, then config 4 P100 (bench.py --config 4) on the
+# GPU parity tests named by K, then bench.py $ARGS (default: config 4 P100) on the
 # default library and on KSIM_LIB_VARIANT=$1, alternating; output gpurun_out/$2
 set -o pipefail
+ARGS=${ARGS:---config 4 --steps 2 --warmup 1}
 cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/$2; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -11,8 +12,8 @@ if [ -n "$K" ]; then
   tail -2 $OUT/pytest.txt
 fi
 for r in 1 2; do
-  timeout -k 10 400 python3 -u bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $OUT/cur_$r.json 2>$OUT/cur_$r.err || exit 1
-  KSIM_LIB_VARIANT=$1 timeout -k 10 400 python3 -u bench.py --config 4 --steps 2 --warmup 1 --no-cpu > $OUT/$1_$r.json 2>$OUT/$1_$r.err || exit 1
+  timeout -k 10 400 python3 -u bench.py $ARGS --no-cpu > $OUT/cur_$r.json 2>$OUT/cur_$r.err || exit 1
+  KSIM_LIB_VARIANT=$1 timeout -k 10 400 python3 -u bench.py $ARGS --no-cpu > $OUT/$1_$r.json 2>$OUT/$1_$r.err || exit 1
 done
 python3 - $OUT <<'PY'
 import json, sys, glob

@@ -34,6 +34,11 @@
 
 namespace ksim {
 
+// KEEP forms: on node ranges of at most kKeepPerLane * threads nodes every lane
+// keeps all of its keys in registers (no insertion network; top_finish takes
+// them unsorted)
+constexpr int kKeepPerLane = 8;
+
 // ---- k_batch_top: evaluation and the pod's top-T in one launch -------------------
 // One block per pod of the batch (kTopThreads threads, kTopWaves waves: two per
 // SIMD when every CU holds one block), the nodes strided over its lanes.  Each
@@ -341,11 +346,13 @@ __device__ __forceinline__ void generic_keys(const DevCluster& c, const DevPods&
 // the class's static verdict, plus for kPodNormVaries pods the normalized
 // part (norm_part_fast) over the maxima of a first pass.  ov(row): as for
 // generic_keys.
-template <int kTopThreads, bool DEF, typename Ov>
+// KEEP: the range fits kKeepPerLane nodes per lane, every key stays in ak[]
+// (node order), and a[] is not used.
+template <int kTopThreads, bool DEF, bool KEEP, typename Ov>
 __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPods& P, const BatchProg& bp,
                                                const FastProg& bq, const ksim_pod& pf, int32_t pi, int32_t j,
                                                uint64_t hseed, int64_t* __restrict__ pnorm, uint64_t (&a)[kTileCand],
-                                               int32_t& nfeas, Ov&& ov) {
+                                               uint64_t (&ak)[kKeepPerLane], int32_t& nfeas, Ov&& ov) {
   const uint64_t* srow = P.stab + (size_t)P.sclass[pi] * c.n;
   const bool normv = (P.bflags[pi] & kPodNormVaries) != 0;   // block-uniform
   const ksim_pod& pp = P.pods[pi];                           // its preferred terms (stab_raw)
@@ -358,6 +365,39 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
     const uint64_t k = dyn_key_fast_t<DEF>(bq, pf, r, ic, im, hseed, c.base + node);
     return stab_pass(w) ? k : 0;
   };
+  if constexpr (KEEP) {
+    // the keys and static words in registers; for kPodNormVaries pods the
+    // maxima over them, then the normalized parts added in place
+    uint64_t wk[kKeepPerLane];
+    NormAcc acc;
+#pragma unroll
+    for (int q = 0; q < kKeepPerLane; q++) {
+      ak[q] = 0;
+      wk[q] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < kKeepPerLane; q++) {
+      if (c.eval_lo + q * kTopThreads >= c.eval_hi) break;   // block-uniform
+      const int32_t node = c.eval_lo + (int32_t)threadIdx.x + q * kTopThreads;
+      if (node < c.eval_hi) {
+        uint64_t w;
+        const uint64_t k = key(node, w);
+        ak[q] = k;
+        wk[q] = w;
+        if (normv && k) acc.take(stab_raw(w, P, pp));
+      }
+    }
+    if (normv) {                                 // block-uniform
+      const NormRaw mx = norm_maxima<kTopThreads>(acc, pnorm, j);
+      const double y_tt = recip_or_zero(mx.tt), y_na = recip_or_zero(mx.na);
+#pragma unroll
+      for (int q = 0; q < kKeepPerLane; q++)
+        if (ak[q]) ak[q] += (uint64_t)norm_part_fast(bp, stab_raw(wk[q], P, pp), mx, y_tt, y_na) << 44;
+    }
+#pragma unroll
+    for (int q = 0; q < kKeepPerLane; q++) nfeas += ak[q] != 0;
+    return;
+  }
   // kPodNormVaries: the first pass keeps each node's key (without the
   // normalized part) in LDS when the range fits, so the second pass only adds
   // that part (each slot is written and read by the same thread: no barrier)
@@ -399,8 +439,9 @@ __device__ __forceinline__ void stab_fast_keys(const DevCluster& c, const DevPod
 }
 
 // STAB (FAST only): a static-class run (stab_fast_keys).  DEF (FAST only): the
-// default profile's key shape compiled in (fast_def).
-template <bool FAST, int kTopThreads, bool STAB = false, bool DEF = false>
+// default profile's key shape compiled in (fast_def).  KEEP (STAB only): every
+// key of a lane kept (node ranges of at most kKeepPerLane * kTopThreads).
+template <bool FAST, int kTopThreads, bool STAB = false, bool DEF = false, bool KEEP = false>
 __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods P,
                                                            const ksim_profile* __restrict__ prof_p,
                                                            const BatchProg* __restrict__ bp_p,
@@ -422,14 +463,16 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   const int64_t seq = st->pod_seq + j;
   const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
   uint64_t a[kTileCand] = {0, 0, 0, 0};        // the lane's best keys, descending
+  uint64_t ak[kKeepPerLane];                    // KEEP: every key of the lane, node order
   int32_t nfeas = 0;
+  static_assert(!KEEP || STAB, "KEEP: static-class runs");
   if constexpr (FAST) {
     // the loop-invariant key inputs in registers (SGPRs): the profile's batch
     // program and the pod's request fields, loaded once
     const FastProg bq = fast_prog(bp);
     const ksim_pod pf = fast_pod_fields(p);
     if constexpr (STAB) {
-      stab_fast_keys<kTopThreads, DEF>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, nfeas, [](NodeRow&) {});
+      stab_fast_keys<kTopThreads, DEF, KEEP>(c, P, bp, bq, pf, pi, j, hseed, pnorm, a, ak, nfeas, [](NodeRow&) {});
     } else {
 #pragma unroll 1
     for (int32_t node = c.eval_lo + threadIdx.x; node < c.eval_hi; node += kTopThreads) {
@@ -447,7 +490,10 @@ __global__ __launch_bounds__(kTopThreads) void k_batch_top(DevCluster c, DevPods
   }
   if constexpr (!FAST)                        // the generic loop is not compiled into FAST kernels
     generic_keys<kTopThreads>(c, P, prof, bp, p, pi, j, seq, trivial, pnorm, a, nfeas, [](NodeRow&) {});
-  top_finish<kTopThreads>(a, nfeas, j, topk, topk_cnt, topk_complete, xsend);
+  if constexpr (KEEP)
+    top_finish<kTopThreads, kKeepPerLane, false>(ak, nfeas, j, topk, topk_cnt, topk_complete, xsend);
+  else
+    top_finish<kTopThreads>(a, nfeas, j, topk, topk_cnt, topk_complete, xsend);
 }
 
 // Sharded: merge the R shard records of pod j (all-gathered, [R][B][kXRec])
@@ -761,7 +807,6 @@ struct PodReq {
 // kNsPods keys; each block writes one list record per pod for its slice (rec
 // = pod * kNsSlices + slice: the slice's provable top-T), which
 // chain_block<kNsSlices> merges as it loads the pod's list.
-constexpr int kKeepPerLane = 8;
 constexpr int kNsSlices = 4;
 constexpr int kNsPods = 4;
 static_assert(kNsSlices == kNsPods && kBatchPods % kNsPods == 0, "NS grid: kBatchPods blocks");
@@ -1234,7 +1279,11 @@ const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch
 // Evaluation and per-pod top-T (xsend: the sharded record, else null).
 static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream) {
   const bool def = fast_def(a.bp);
-  if (a.stab && def)   // static-class runs (unsharded handles only: run_stab)
+  const bool keep = a.c.eval_hi - a.c.eval_lo <= kKeepPerLane * 1024;
+  if (a.stab && def && keep)
+    k_batch_top<true, 1024, true, true, true><<<kBatchPods, 1024, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
+  else if (a.stab && def)   // static-class runs (unsharded handles only: run_stab)
     k_batch_top<true, 1024, true, true><<<kBatchPods, 1024, 0, stream>>>(
         a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);
   else if (a.stab)

@@ -484,7 +484,8 @@ constexpr int32_t kWinFusedWords = 256;
 // WIN (NT = kBatchPods, unsharded): every block runs the window scan itself
 // (window_block, thread i = pod i) instead of reading k_adapt_window's
 // output; block 0 stores awin / aexact for the pairs and the commit.
-template <bool SH, bool FAST, int NT, int WIN = 0>
+// DEF (FAST only): the default profile's key shape compiled in (fast_def)
+template <bool SH, bool FAST, int NT, int WIN = 0, bool DEF = false>
 __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp_p,
                                                    const DevState* __restrict__ st,
@@ -552,7 +553,8 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
   const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)seq << 20);
   auto node_key = [&](int32_t local) -> uint64_t {
     const NodeRow r = load_res_row(c, local);       // scores read the resource columns only
-    if constexpr (FAST) return dyn_key_fast(bp, p, r, c.inv_cpu[local], c.inv_mem[local], hseed, c.base + local);
+    if constexpr (FAST)
+      return dyn_key_fast_t<DEF>(fast_prog(bp), p, r, c.inv_cpu[local], c.inv_mem[local], hseed, c.base + local);
     return dyn_key(prof, bp, p, r, c.n_scalar, seq, c.base, c.fit_ignore);
   };
   const uint64_t* mask = amask + (size_t)j * n_words;
@@ -592,13 +594,13 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       __builtin_amdgcn_sched_barrier(0);
       if ((w1 >> (n1 & 63)) & 1ull) {
         kept++;
-        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast(bp, p, r1, c1, m1, hseed, c.base + n1));
+        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast_t<DEF>(fast_prog(bp), p, r1, c1, m1, hseed, c.base + n1));
 #pragma unroll
         for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
       }
       if (v2 && ((w2 >> (n2 & 63)) & 1ull)) {
         kept++;
-        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast(bp, p, r2, c2, m2, hseed, c.base + n2));
+        a[kTopT - 1] = umax64(a[kTopT - 1], dyn_key_fast_t<DEF>(fast_prog(bp), p, r2, c2, m2, hseed, c.base + n2));
 #pragma unroll
         for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
       }
@@ -1147,11 +1149,19 @@ uint32_t launch_batch_adapt_lazy(const LazyBatch& z, hipStream_t stream, hipEven
   }
   if (evs) (void)hipEventRecord(evs[2], stream);
   // every later launch reads X[p] (z.cw) and st[p]
-#define TOP(NT, W) k_adapt_top<false, true, NT, W><<<kBatchPods, NT, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, z.st, \
-    a.s.amask, n_words, z.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, nullptr, a.s.acut)
-  if (k >= kTopWideK) TOP(1024, 2);
-  else if (win_fused) TOP(256, 1);
-  else TOP(256, 2);
+#define TOP(NT, W, D) k_adapt_top<false, true, NT, W, D><<<kBatchPods, NT, 0, stream>>>(z.cw, a.P, a.dprof, a.dbp, \
+    z.st, a.s.amask, n_words, z.awin, a.s.aexact, a.s.topk, a.s.topk_cnt, a.s.topk_complete, nullptr, nullptr, a.s.acut)
+  const bool def = fast_def(a.bp);
+  if (k >= kTopWideK) {
+    if (def) TOP(1024, 2, true);
+    else TOP(1024, 2, false);
+  } else if (win_fused) {
+    if (def) TOP(256, 1, true);
+    else TOP(256, 1, false);
+  } else {
+    if (def) TOP(256, 2, true);
+    else TOP(256, 2, false);
+  }
 #undef TOP
   if (evs) (void)hipEventRecord(evs[3], stream);
   k_adapt_pairs<false, true><<<kBatchPods, kBatchPods, 0, stream>>>(

@@ -563,7 +563,7 @@ __global__ __launch_bounds__(256) void k_batch_gmerge(const DevState* __restrict
 // held one of its normalization maxima (kPodNormVaries) has left its feasible
 // set: the maximum, and so its S0 keys, no longer hold, and the batch commits
 // only the pods before it.
-template <bool FAST, bool STAB = false>
+template <bool FAST, bool STAB = false, bool DEF = false>
 __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& P, const ksim_profile& prof,
                                             const BatchProg& bp, const DevState* __restrict__ st, uint64_t gk,
                                             int32_t nchain, uint64_t* s_wmax, uint64_t* __restrict__ pmax,
@@ -611,7 +611,7 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
       } else if constexpr (FAST) {
         NodeRow r = load_res_row(c, local);
         row_add_pod(r, pk ? *pk : P.pods[base + k], 1);
-        v = dyn_key_fast(bp, pj ? *pj : p, r, c.inv_cpu[local], c.inv_mem[local],
+        v = dyn_key_fast_t<DEF>(fast_prog(bp), pj ? *pj : p, r, c.inv_cpu[local], c.inv_mem[local],
                          prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20), c.base + local);
       } else {
         const int32_t bf = P.bflags[base + j];
@@ -683,8 +683,9 @@ unsigned long long* cp_clock_buffer() { return nullptr; }
 
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
-// R: each pod's list is R slice records (the node-stationary evaluation)
-template <bool FAST, bool LAZY = false, bool STAB = false, int R = 1>
+// R: each pod's list is R slice records (the node-stationary evaluation).
+// DEF (FAST P100 pairs): the default profile's key shape compiled in.
+template <bool FAST, bool LAZY = false, bool STAB = false, int R = 1, bool DEF = false>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
                                                                   const BatchProg* __restrict__ bp_p,
@@ -728,7 +729,7 @@ __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, 
     if ((int)threadIdx.x < nb) gkey[threadIdx.x] = gk;
     if (threadIdx.x == 0) *chain_end = nchain;
   }
-  pairs_block<FAST, STAB>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr,
+  pairs_block<FAST, STAB, DEF>(c, P, *prof_p, *bp_p, st, gk, nchain, s_wmax, pmax, FAST ? &pj : nullptr,
                           FAST ? &pk : nullptr, pnorm, pinv, s_winv);
 #ifdef KSIM_CP_CLOCKS
   if (dbgc && threadIdx.x == 0) atomicAdd(&dbgc[5], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t_in));
@@ -1235,7 +1236,11 @@ uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* e
   launch_top_commit<false>(z, nullptr, stream);
   if (evs) (void)hipEventRecord(evs[1], stream);
   if (ns_eval(a, nullptr))                     // the slice records merged as the chain loads them
-    k_batch_chain_pairs<true, true, false, kNsSlices><<<kBatchPods, kBatchPods, 0, stream>>>(
+    k_batch_chain_pairs<true, true, false, kNsSlices, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax,
+        a.s.pnorm, a.s.pinv);
+  else if (fast_def(a.bp))
+    k_batch_chain_pairs<true, true, false, 1, true><<<kBatchPods, kBatchPods, 0, stream>>>(
         z.cw, a.P, a.dprof, a.dbp, z.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, z.gkey, z.cend, z.pmax,
         a.s.pnorm, a.s.pinv);
   else

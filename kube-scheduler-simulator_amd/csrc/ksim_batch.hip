@@ -595,9 +595,10 @@ __device__ __forceinline__ void pairs_block(const DevCluster& c, const DevPods& 
         const double ic = c.inv_cpu[local], im = c.inv_mem[local];
         const uint64_t hseed = prof.tiebreak_seed ^ ((uint64_t)(seq0 + j) << 20);
         NodeRow r = load_res_row(c, local);
-        const bool feas0 = normv && stab_pass(w) && dyn_key_fast(bp, *pj, r, ic, im, hseed, c.base + local) != 0;
+        const bool feas0 =
+            normv && stab_pass(w) && dyn_key_fast_t<DEF>(fast_prog(bp), *pj, r, ic, im, hseed, c.base + local) != 0;
         row_add_pod(r, *pk, 1);
-        v = stab_pass(w) ? dyn_key_fast(bp, *pj, r, ic, im, hseed, c.base + local) : 0;
+        v = stab_pass(w) ? dyn_key_fast_t<DEF>(fast_prog(bp), *pj, r, ic, im, hseed, c.base + local) : 0;
         if (normv && (v || feas0)) {
           const NormRaw mx{pnorm[4 * j], pnorm[4 * j + 1]};
           if (v) {
@@ -684,7 +685,7 @@ unsigned long long* cp_clock_buffer() { return nullptr; }
 // LAZY (deferred-commit batches): a batch with no pods marks its ring slot
 // empty (chain_end = -1), so the next launch commits nothing for it.
 // R: each pod's list is R slice records (the node-stationary evaluation).
-// DEF (FAST P100 pairs): the default profile's key shape compiled in.
+// DEF (FAST pairs): the default profile's key shape compiled in.
 template <bool FAST, bool LAZY = false, bool STAB = false, int R = 1, bool DEF = false>
 __global__ __launch_bounds__(kBatchPods) void k_batch_chain_pairs(DevCluster c, DevPods P,
                                                                   const ksim_profile* __restrict__ prof_p,
@@ -1307,7 +1308,11 @@ static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t st
 
 // The chain inside every pairs block (k_batch_chain_pairs).
 static void launch_chain_pairs(const LaunchArgs& a, hipStream_t stream) {
-  if (a.stab)
+  if (a.stab && fast_def(a.bp))
+    k_batch_chain_pairs<true, false, true, 1, true><<<kBatchPods, kBatchPods, 0, stream>>>(
+        a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey, a.s.chain_end, a.s.pmax,
+        a.s.pnorm, a.s.pinv);
+  else if (a.stab)
     k_batch_chain_pairs<true, false, true><<<kBatchPods, kBatchPods, 0, stream>>>(
         a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.s.gkey, a.s.chain_end, a.s.pmax,
         a.s.pnorm, a.s.pinv);

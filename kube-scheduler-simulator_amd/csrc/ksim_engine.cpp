@@ -3866,18 +3866,21 @@ int ksim_reset_cluster(ksim_handle* h) {
   HIPCHK(h, hipSetDevice(h->device));
   const size_t N = (size_t)h->dc.n;
   const DevCluster& c = h->dc;
-  HIPCHK(h, hipMemcpyAsync(c.req_cpu, h->init.req_cpu, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.req_mem, h->init.req_mem, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.req_eph, h->init.req_eph, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  if (c.n_scalar)
-    HIPCHK(h, hipMemcpyAsync(c.req_scalar, h->init.req_scalar, 8 * N * c.n_scalar, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.nz_cpu, h->init.nz_cpu, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.nz_mem, h->init.nz_mem, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.num_pods, h->init.num_pods, 4 * N, hipMemcpyDeviceToDevice, h->stream));
-  if (c.n_classes)
-    HIPCHK(h, hipMemcpyAsync(c.cnt, h->init.cnt, 4 * N * c.n_classes, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(c.nb_alloc, h->init.nb_alloc, 8 * N, hipMemcpyDeviceToDevice, h->stream));
-  HIPCHK(h, hipMemsetAsync(h->st, 0, sizeof(DevState), h->stream));
+  // the dynamic columns from their snapshot copies and the run state zeroed,
+  // in one launch (every buffer is a hipMalloc allocation: 16-byte aligned)
+  ResetList L;
+  L.add(c.req_cpu, h->init.req_cpu, 8 * N);
+  L.add(c.req_mem, h->init.req_mem, 8 * N);
+  L.add(c.req_eph, h->init.req_eph, 8 * N);
+  if (c.n_scalar) L.add(c.req_scalar, h->init.req_scalar, 8 * N * c.n_scalar);
+  L.add(c.nz_cpu, h->init.nz_cpu, 8 * N);
+  L.add(c.nz_mem, h->init.nz_mem, 8 * N);
+  L.add(c.num_pods, h->init.num_pods, 4 * N);
+  if (c.n_classes) L.add(c.cnt, h->init.cnt, 4 * N * c.n_classes);
+  L.add(c.nb_alloc, h->init.nb_alloc, 8 * N);
+  static_assert(sizeof(DevState) % 4 == 0, "DevState by words");
+  L.add(h->st, nullptr, sizeof(DevState));
+  launch_reset_copy(L, h->stream);
   launch_ptab_init(h->dc, h->dp, h->stream);        // the queue's persistent tables follow the counts
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -264,6 +264,21 @@ void launch_group_reduce(const GroupPtrs& g, int64_t count, bool op_max, hipStre
 void launch_group_gather(const GroupPtrs& src, const GroupPtrs& dst, int32_t words, hipStream_t stream);
 // Persistent domain tables of a loaded queue (DevPods.ptab) from the class counts.
 void launch_ptab_init(const DevCluster& c, const DevPods& P, hipStream_t stream);
+// ksim_reset_cluster: copies (or zeroes, src null) of 16-byte-aligned buffers in one launch
+struct ResetList {
+  static constexpr int kMax = 12;
+  int n = 0;
+  uint32_t* dst[kMax];
+  const uint32_t* src[kMax];
+  size_t words[kMax];
+  void add(void* d, const void* s, size_t bytes) {
+    dst[n] = (uint32_t*)d;
+    src[n] = (const uint32_t*)s;
+    words[n] = bytes / 4;
+    n++;
+  }
+};
+void launch_reset_copy(const ResetList& L, hipStream_t stream);
 
 // Selector / term matching as an int8 contraction (ksim_match.hip, ksim_match_terms).
 constexpr int kMatchMaxReqs = 4096;     // requirement columns (LDS: 16 rows x 4096 bits)

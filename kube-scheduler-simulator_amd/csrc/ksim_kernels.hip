@@ -1121,6 +1121,32 @@ void launch_ptab_init(const DevCluster& c, const DevPods& P, hipStream_t stream)
   if (P.n_ptab > 0) k_ptab_init<<<P.n_ptab, 256, 0, stream>>>(c, P);
 }
 
+// ksim_reset_cluster's column copies and the state zeroing in one launch (one
+// dispatch instead of nine copy / fill dispatches): segment k copies words[k]
+// 32-bit words from src[k] to dst[k] (src null: zeroes), blocks strided over
+// every segment in 16-byte units, the tails by word.
+__global__ __launch_bounds__(256) void k_reset_copy(ResetList L) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int k = 0; k < L.n; k++) {
+    uint32_t* d = L.dst[k];
+    const uint32_t* sp = L.src[k];
+    const size_t n = L.words[k], n4 = n / 4;
+    for (size_t i = t0; i < n4; i += stride) {
+      const uint4 v = sp ? reinterpret_cast<const uint4*>(sp)[i] : make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(d)[i] = v;
+    }
+    for (size_t i = 4 * n4 + t0; i < n; i += stride) d[i] = sp ? sp[i] : 0u;
+  }
+}
+
+void launch_reset_copy(const ResetList& L, hipStream_t stream) {
+  size_t most = 0;
+  for (int k = 0; k < L.n; k++) most = L.words[k] > most ? L.words[k] : most;
+  const int blocks = (int)std::min<size_t>(1024, std::max<size_t>(1, (most / 4 + 255) / 256));
+  k_reset_copy<<<blocks, 256, 0, stream>>>(L);
+}
+
 __global__ void k_assume(DevCluster c, DevPods P, int32_t pod, int32_t node, int sign) {
   if (threadIdx.x == 0 && blockIdx.x == 0) assume_pod(c, P, P.pods[pod], node, sign);
 }

@@ -525,21 +525,162 @@ def bench_fw(args, out):
         e_r = run("engine", n_pods)
         c_r = run_c() if DRV is not None else None
         o_r = run("oracle", min(n_pods, 1000 if n_nodes <= 100 else 300))
-        rows.append({"nodes": n_nodes, "engine": e_r, "engine_c_driver": c_r, "oracle_cpu_1thread": o_r,
-                     "pool_build_us": pool_us,
-                     "engine_vs_oracle_in_calls": o_r["us_in_calls"] / e_r["us_in_calls"]})
-    best = rows[-1]["engine_c_driver"] or rows[-1]["engine"]
+        row = {"nodes": n_nodes, "engine": e_r, "engine_c_driver": c_r, "oracle_cpu_1thread": o_r,
+               "pool_build_us": pool_us, "engine_vs_oracle_in_calls": o_r["us_in_calls"] / e_r["us_in_calls"]}
+        if DRV is not None and n_nodes >= 5000:
+            ext, upd = _fw_delta_objects(nodes, pobjs, seed=5)
+            row["engine_c_driver_deltas"] = _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots,
+                                                           ext, upd)
+        rows.append(row)
+    if DRV is not None:
+        # config 3's cluster: 10,000 nodes in 3 zones, 100,000 bound pods with
+        # anti-affinity terms, spreading incoming pods; the snapshot encoded
+        # once, then deltas
+        n3 = min(args.nodes3, 10000)
+        nodes3, bound3, inc3 = gen.config3_objects(n_nodes=n3, pods_per_node=10, n_incoming=1500)
+        enc3 = NativeEncoder()
+        t0 = time.perf_counter()
+        cl3, _ = enc3.encode_cluster(nodes3, bound3)
+        full_s = time.perf_counter() - t0
+        enc3.encode_pods(cl3, inc3)
+        sp3 = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+        prof3 = profile.compile_profile(sp3)
+        pools3 = []
+        for p3 in inc3:
+            pl = Pool()
+            pl.pod(p3)
+            pl.build()
+            pools3.append(pl)
+        ext3, upd3 = _fw_delta_objects(nodes3, bound3, seed=6)
+        N3 = cl3.n_nodes
+        r3 = _fw_run_deltas(DRV, EL, enc3, cl3, prof3, pools3, opts, N3, profile.num_feasible_nodes_to_find(N3, 0),
+                            [k for k, p3 in enumerate(sp3.score_plugins()) if p3.name in HAS_NORMALIZE], ext3, upd3)
+        r3["full_encode_s"] = full_s
+        rows.append({"nodes": N3, "bound_pods": len(bound3), "workload": "config 3 (PTS + IPA)",
+                     "engine_c_driver_deltas": r3})
+    best = rows[1].get("engine_c_driver_deltas") or rows[1]["engine_c_driver"] or rows[1]["engine"]
     line = {"metric": "framework_driven_cycle_us", "value": best["us_per_cycle"],
-            "unit": "us per pod cycle (5000 nodes)", "higher_is_better": False, "n_gpus": 1,
+            "unit": "us per pod cycle (5000 nodes, deltas and pool build included)", "higher_is_better": False,
+            "n_gpus": 1,
             "config": {"workload": "config-1 distribution, framework-driven compat cycle (drop-in)",
                        "parallelism": "single GPU"},
             "rows": rows,
             "note": "per cycle: ksim_encode_pods (native) + fw_prefilter + fw_score + fw_normalize per "
                     "NormalizeScore plugin + assume, with the copies back to host memory; value: the C driver "
-                    "(tools/fwdrive.c, the calls a cgo host makes) when built, else the Python loop, whose "
-                    "us_per_cycle includes the ctypes glue; the oracle's calls take pre-compiled pods"}
+                    "(tools/fwdrive.c, the calls a cgo host makes) with the incremental snapshot's work "
+                    "(engine_c_driver_deltas: the pod's pool copied into a fresh allocation, the encoder bind "
+                    "after Reserve, an external bound-pod add every 4 cycles and its delete 8 adds later, a node "
+                    "update every 50 cycles) when built, else the Python loop, whose us_per_cycle includes the "
+                    "ctypes glue; the oracle's calls take pre-compiled pods"}
     out.write(json.dumps(line) + "\n")
     out.flush()
+
+
+def _fw_delta_objects(nodes, pods, seed):
+    """Informer events for bench_fw's incremental run: bound pods added on
+    random nodes (copies of ``pods``, renamed), node updates (allocatable cpu
+    changed, same zone)."""
+    import copy
+    import random
+    rng = random.Random(seed)
+    ext = []
+    for k in range(2000):
+        p = copy.copy(pods[rng.randrange(len(pods))])
+        p.name = f"ext-{k:06d}"
+        p.node_name = nodes[rng.randrange(len(nodes))].name
+        ext.append(p)
+    upd = []
+    for k in range(64):
+        n = copy.copy(nodes[rng.randrange(len(nodes))])
+        n.allocatable = dict(n.allocatable, cpu=str(rng.choice([8, 16, 24, 48])))
+        upd.append(n)
+    return ext, upd
+
+
+def _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots, ext, upd):
+    """tools/fwdrive.c fwdrive_run_deltas on a fresh engine over ``cluster``
+    (the encoder ``enc`` keeps the snapshot's membership)."""
+    import ctypes
+    from ksim import engine
+    from ksim.nativeenc import Pool
+
+    class Fns(ctypes.Structure):
+        _fields_ = [(nm, ctypes.c_void_p) for nm in ("encode_pods", "encoder_pods", "prefilter", "score",
+                                                      "normalize", "assume")]
+
+    class DFns(ctypes.Structure):
+        _fields_ = [(nm, ctypes.c_void_p) for nm in ("encoder_bind", "encoder_unbind", "encoder_update_nodes",
+                                                      "encoder_old_pos", "encoder_cluster", "encoder_info",
+                                                      "upsert_nodes", "forget")]
+
+    class Deltas(ctypes.Structure):
+        _fields_ = [("ext", ctypes.c_void_p), ("ext_ns", ctypes.c_void_p), ("ext_name", ctypes.c_void_p),
+                    ("ext_node", ctypes.c_void_p), ("n_ext", ctypes.c_int32), ("ext_every", ctypes.c_int32),
+                    ("lag", ctypes.c_int32), ("node_upd", ctypes.c_void_p), ("n_node_upd", ctypes.c_int32),
+                    ("node_every", ctypes.c_int32)]
+
+    class Res(ctypes.Structure):
+        _fields_ = [("sec", ctypes.c_double * 7), ("total", ctypes.c_double)] + \
+                   [(nm, ctypes.c_int64) for nm in ("bound", "cycles", "pod_adds", "pod_deletes", "node_updates",
+                                                     "resends")]
+
+    DRV.fwdrive_run_deltas.restype = ctypes.c_int
+    DRV.fwdrive_run_deltas.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                                               ctypes.c_void_p]
+    import numpy as np
+    pos = {n: i for i, n in enumerate(cluster.node_names)}
+    ext_pools, ext_ns, ext_name = [], [], []
+    for p in ext:
+        pl = Pool()
+        pl.pod(p)
+        pl.build()
+        ext_pools.append(pl)
+        ext_ns.append(p.namespace.encode())
+        ext_name.append(p.name.encode())
+    ext_node = np.array([pos[p.node_name] for p in ext], np.int32)
+    upd_pools = []
+    for n in upd:
+        pl = Pool()
+        pl.node(n)
+        pl.build()
+        upd_pools.append(pl)
+    e = engine.Engine(0)
+    e.set_profile(prof)
+    e.set_cluster(cluster.copy_state())
+    f = Fns(*[ctypes.cast(getattr(EL, nm), ctypes.c_void_p).value for nm in
+              ("ksim_encode_pods", "ksim_encoder_pods", "ksim_fw_prefilter", "ksim_fw_score", "ksim_fw_normalize",
+               "ksim_assume")])
+    g = DFns(*[ctypes.cast(getattr(EL, nm), ctypes.c_void_p).value for nm in
+               ("ksim_encoder_bind", "ksim_encoder_unbind", "ksim_encoder_update_nodes", "ksim_encoder_old_pos",
+                "ksim_encoder_cluster", "ksim_encoder_get_info", "ksim_upsert_nodes", "ksim_forget")])
+    a_ext = (ctypes.c_void_p * len(ext_pools))(*[ctypes.addressof(pl.c) for pl in ext_pools])
+    a_ns = (ctypes.c_char_p * len(ext_ns))(*ext_ns)
+    a_name = (ctypes.c_char_p * len(ext_name))(*ext_name)
+    a_upd = (ctypes.c_void_p * len(upd_pools))(*[ctypes.addressof(pl.c) for pl in upd_pools])
+    dl = Deltas(ctypes.cast(a_ext, ctypes.c_void_p), ctypes.cast(a_ns, ctypes.c_void_p),
+                ctypes.cast(a_name, ctypes.c_void_p), ext_node.ctypes.data, len(ext_pools), 4, 8,
+                ctypes.cast(a_upd, ctypes.c_void_p), len(upd_pools), 50)
+    n_pods = len(pools)
+    arr = (ctypes.c_void_p * n_pods)(*[ctypes.addressof(pl.c) for pl in pools])
+    ns = (ctypes.c_int32 * max(1, len(nslots)))(*nslots)
+    res = Res()
+    rc = DRV.fwdrive_run_deltas(ctypes.byref(f), ctypes.byref(g), e.h, enc.h, arr, n_pods, ctypes.byref(opts), N, K,
+                                ns, len(nslots), prof.n_score, ctypes.byref(dl), ctypes.byref(res))
+    if rc != 0:
+        err = EL.ksim_last_error(e.h).decode() + " / " + (EL.ksim_encoder_last_error(enc.h) or b"").decode()
+        raise RuntimeError(f"fwdrive_run_deltas rc {rc}: {err}")
+    d = e.diag()
+    e.close()
+    names = ("encode", "prefilter", "score", "normalize", "assume_bind", "deltas", "pool_build")
+    return {"us_per_cycle": res.total / n_pods * 1e6, "cycles": int(res.cycles), "bound": int(res.bound),
+            "us_per_call": {nm: res.sec[q] / n_pods * 1e6 for q, nm in enumerate(names)},
+            "events": {"pod_adds": int(res.pod_adds), "pod_deletes": int(res.pod_deletes),
+                       "node_updates": int(res.node_updates), "resends": int(res.resends)},
+            "full_encodes_after_first": 0,
+            "answered": {k: d[k] for k in ("fw_score_host", "fw_score_device", "fw_normalize_cached",
+                                           "fw_normalize_device")}}
 
 
 def main():

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 10
+#define KSIM_ABI_VERSION 11
 
 /* ---- limits ------------------------------------------------------------ */
 #define KSIM_KEY_NODE_MASK    ((1 << 18) - 1)  /* tie-break key: node field = mask - node (>= 1) */
@@ -1021,7 +1021,7 @@ typedef struct ksim_encoder ksim_encoder;
 typedef struct ksim_encoder_info {
   int32_t n_nodes, n_scalar, n_label_cols, n_taints;
   int32_t n_classes, n_pods, n_exprs, n_terms;
-  int32_t n_uses, n_adds, n_nn, _pad;
+  int32_t n_uses, n_adds, n_nn, n_members;   /* n_members: bound pods in the snapshot (ABI 11) */
 } ksim_encoder_info;
 
 int  ksim_encoder_create(ksim_encoder** out);
@@ -1052,6 +1052,55 @@ int ksim_encoder_node_order(const ksim_encoder* e, int32_t* order);
 #define KSIM_ENC_STR_TAINT_EFFECT 5
 #define KSIM_ENC_STR_NODE_NAME    6       /* i: node position */
 const char* ksim_encoder_string(const ksim_encoder* e, int32_t what, int32_t i, int32_t j);
+
+/* ---- snapshot deltas (ABI 11) ----------------------------------------------------
+ * The scheduler cache between two snapshots, without re-encoding the cluster:
+ * the simulator's scheduler runs off informers
+ * (simulator/scheduler/scheduler.go:160-167) and upstream's UpdateSnapshot
+ * copies only the NodeInfos whose generation moved.  The host diffs the
+ * framework's snapshot by NodeInfo generation (integration/go/engine/
+ * encoder.go NativeEncoder.Snapshot, ksim/fwsnapshot.py SnapshotSync) and
+ * feeds the changes here and to the engine:
+ *
+ *   a node added / updated / removed   ksim_encoder_update_nodes, then
+ *                                      ksim_encoder_cluster + ksim_encoder_old_pos
+ *                                      into ksim_upsert_nodes (the engine replays
+ *                                      its binds on the kept nodes);
+ *   a bound pod added (an informer     ksim_encode_pods of the pod, the table
+ *   event, or the framework's Reserve) re-sent if the compile added label
+ *                                      columns or count classes (ksim_upsert_nodes
+ *                                      with every node kept), ksim_assume,
+ *                                      ksim_encoder_bind;
+ *   a bound pod deleted / Unreserve    ksim_encode_pods of the pod (same re-send
+ *                                      rule), ksim_forget, ksim_encoder_unbind.
+ *
+ * The encoder keeps the snapshot's node rows and class rows as the engine last
+ * received them (the rows ksim_upsert_nodes replays onto) and the membership
+ * of every bound pod (its signature and host ports per node), so a count class
+ * a later pod registers counts every pod bound so far.  Re-send a grown table
+ * before the next ksim_assume / ksim_forget, so that a new class row reaches
+ * the engine before any bind it does not count.
+ *
+ * ksim_encoder_update_nodes: pool.nodes are added (new name) or updated
+ * (known name) nodes, removed[0..n_removed) string ids of the pool naming the
+ * nodes that leave (their bound pods leave the snapshot).  Nodes keep informer
+ * add order; an update that changes a node's zone re-adds it at the end
+ * (nodeTree.updateNode).  Scalar columns, taint ids, label columns and count
+ * class ids are kept; the pod set is cleared (its positions are stale).
+ * ksim_encoder_old_pos: old_pos[i] = the previous position of node i of the
+ * new snapshot, -1 for an added node (KSIM_E_INVALID before any delta).
+ * ksim_encoder_bind: pod `pod_index` of the current pod set (the last
+ * ksim_encode_pods) is bound at node position `node`, under its
+ * namespace / name; binding a pod already bound is KSIM_E_INVALID.
+ * ksim_encoder_unbind: the bound pod namespace/name leaves (its position in
+ * *node); KSIM_E_INVALID when it is not bound.
+ * ksim_encoder_bound_node: the pod's position, or -1 when not bound. */
+int ksim_encoder_update_nodes(ksim_encoder* e, const ksim_k8s_pool* pool, const int32_t* removed,
+                              int32_t n_removed);
+int ksim_encoder_old_pos(const ksim_encoder* e, int32_t* old_pos);
+int ksim_encoder_bind(ksim_encoder* e, int32_t pod_index, int32_t node);
+int ksim_encoder_unbind(ksim_encoder* e, const char* namespace_, const char* name, int32_t* node);
+int ksim_encoder_bound_node(const ksim_encoder* e, const char* namespace_, const char* name, int32_t* node);
 
 #ifdef __cplusplus
 }

@@ -7,11 +7,9 @@
 // does (tests/test_native_encode.py checks the C++ encoder byte for byte
 // against it).
 //
-// The framework's snapshot is the truth: Snapshot re-encodes it whenever it
-// holds nodes or pods the device snapshot does not (node informer events,
-// pods assumed by the original plugins for a pod the engine refused), and
-// re-sends it with ksim_set_cluster, nextStartNodeIndex carried over.  Pods the
-// engine itself assumed (KsimAssume) are already on the device.
+// The device snapshot is encoded whole once and then follows the informers'
+// events and the framework's Reserve / Unreserve as deltas (ABI 11, "snapshot
+// deltas"): NativeEncoder below; ksim/fwsnapshot.py is its Python mirror.
 //
 // NOT BUILT HERE (no Go toolchain in the build container).
 package engine
@@ -24,6 +22,7 @@ package engine
 import "C"
 
 import (
+	"errors"
 	"fmt"
 	"sort"
 	"strings"
@@ -31,10 +30,11 @@ import (
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/api/equality"
 	"k8s.io/apimachinery/pkg/api/resource"
 	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
-	"k8s.io/apimachinery/pkg/types"
 	"k8s.io/apimachinery/pkg/util/sets"
+	"k8s.io/client-go/tools/cache"
 	"k8s.io/kubernetes/pkg/scheduler/framework"
 )
 
@@ -440,14 +440,36 @@ func copyPodSet(ps *C.ksim_pod_set) (*C.ksim_pod_set, func()) {
 // ---- the Encoder ------------------------------------------------------------------
 
 // NativeEncoder implements Encoder (plugins.go) over ksim_encode_nodes /
-// ksim_encode_pods.  The host sets the profile's plugin args before the first
-// cycle (NewPluginConfig's merged args, plugins.go:103-179).
+// ksim_encode_pods and the encoder's snapshot deltas (ABI 11).  The host sets
+// the profile's plugin args before the first cycle (NewPluginConfig's merged
+// args, plugins.go:103-179) and registers Handlers() on the pod and node
+// informers (plugins.go Register does both).
+//
+// The snapshot is encoded whole once, at the first cycle.  From then on the
+// informers' events queue here and the next cycle start applies them
+// (Snapshot), as the scheduler cache applies them before UpdateSnapshot
+// (simulator/scheduler/scheduler.go:160-167 runs the scheduler off informers):
+//
+//	node added / updated / removed  ksim_encoder_update_nodes, then
+//	                                ksim_upsert_nodes (one per cycle start;
+//	                                the engine replays its binds on kept nodes)
+//	bound pod added                 ksim_encode_pods, the table re-sent if the
+//	                                compile grew it, ksim_assume, ksim_encoder_bind
+//	bound pod deleted               ksim_encode_pods, ksim_forget, ksim_encoder_unbind
+//	Reserve / Unreserve             Assume / Forget: the same, for the cycle's pod
+//
+// A pod the engine assumed and the informer then reports bound on the same
+// node is already in the snapshot (a no-op).  A full re-encode (of the host's
+// record of nodes and bound pods, ksim_set_cluster) happens again only when a
+// delta cannot be encoded (a vocabulary or class limit): Stats.FullEncodes.
 type NativeEncoder struct {
 	// NetworkBandwidthArgs annotation names ("" = the plugin's defaults)
 	NodeLimitAnnotation, IngressRequestAnnotation, EgressRequestAnnotation string
 	// NodeAffinityArgs.addedAffinity (nil: none)
 	AddedAffinity *v1.NodeAffinity
-	// PodTopologySpreadArgs: "System", "List" (with DefaultConstraints) or "" (none)
+	// PodTopologySpreadArgs.defaultingType: "" or "System" (upstream's default,
+	// SetDefaults_PodTopologySpreadArgs), "List" (with DefaultConstraints), or
+	// "None" (no default constraints at all: an explicit opt-out)
 	SpreadDefaulting   string
 	DefaultConstraints []v1.TopologySpreadConstraint
 	// Namespaces (namespaceSelector terms), Services and controllers
@@ -457,16 +479,134 @@ type NativeEncoder struct {
 	ReplicaSets     func() []metav1.Object
 	ControllerOf    func(obj metav1.Object) (kind string, rcSelector map[string]string, selector *metav1.LabelSelector)
 
-	mu        sync.Mutex
-	enc       *C.ksim_encoder
-	encoded   bool
-	names     []string
-	pos       map[string]int
-	known     map[types.UID]int // pods in the device snapshot -> node position
-	bound     []*v1.Pod         // the bound-pod table rows (DefaultPreemption), in snapshot order
+	Stats struct{ FullEncodes, NodeDeltas, PodAdds, PodDeletes, Resends int }
+
+	mu       sync.Mutex
+	enc      *C.ksim_encoder
+	encoded  bool
+	names    []string
+	pos      map[string]int
+	podCopy  func() // Pod's set (C memory), freed by the next Pod call
+	layout   [2]int32
+
+	// the host's record of the snapshot: nodes in informer add order, bound
+	// pods by namespace/name (with their node) in bind order
+	nodes     map[string]*v1.Node
+	nodeOrder []string
+	bound     map[string]boundPod
+	waiting   map[string]*v1.Pod // bound to a node the snapshot does not hold yet
+	boundRows []*v1.Pod          // the bound-pod table rows (DefaultPreemption)
 	boundBufs func()
-	podCopy   func() // Pod's set (C memory), freed by the next Pod call
-	layout    [2]int32
+	tableOld  bool
+
+	evMu   sync.Mutex
+	events []event
+}
+
+type boundPod struct {
+	pod  *v1.Pod
+	node string
+	seq  uint64 // bind order
+}
+
+type eventKind int
+
+const (
+	evNode eventKind = iota
+	evNodeGone
+	evPod
+	evPodGone
+)
+
+type event struct {
+	kind eventKind
+	node *v1.Node
+	name string
+	pod  *v1.Pod
+}
+
+func podKey(p *v1.Pod) string { return p.Namespace + "/" + p.Name }
+
+func (n *NativeEncoder) queue(ev ...event) {
+	n.evMu.Lock()
+	n.events = append(n.events, ev...)
+	n.evMu.Unlock()
+}
+
+// Handlers are the informer event handlers (pods, nodes) that feed the deltas.
+func (n *NativeEncoder) Handlers() (pods, nodes cache.ResourceEventHandlerFuncs) {
+	asPod := func(obj interface{}) *v1.Pod {
+		switch t := obj.(type) {
+		case *v1.Pod:
+			return t
+		case cache.DeletedFinalStateUnknown:
+			p, _ := t.Obj.(*v1.Pod)
+			return p
+		}
+		return nil
+	}
+	asNode := func(obj interface{}) *v1.Node {
+		switch t := obj.(type) {
+		case *v1.Node:
+			return t
+		case cache.DeletedFinalStateUnknown:
+			nd, _ := t.Obj.(*v1.Node)
+			return nd
+		}
+		return nil
+	}
+	pods = cache.ResourceEventHandlerFuncs{
+		AddFunc: func(obj interface{}) {
+			if p := asPod(obj); p != nil && p.Spec.NodeName != "" {
+				n.queue(event{kind: evPod, pod: p})
+			}
+		},
+		UpdateFunc: func(oldObj, newObj interface{}) {
+			o, p := asPod(oldObj), asPod(newObj)
+			if o == nil || p == nil {
+				return
+			}
+			if o.Spec.NodeName != "" && o.Spec.NodeName == p.Spec.NodeName && samePlacementInputs(o, p) {
+				return // status / metadata churn the plugins do not read
+			}
+			if o.Spec.NodeName != "" {
+				n.queue(event{kind: evPodGone, pod: o})
+			}
+			if p.Spec.NodeName != "" {
+				n.queue(event{kind: evPod, pod: p})
+			}
+		},
+		DeleteFunc: func(obj interface{}) {
+			if p := asPod(obj); p != nil {
+				n.queue(event{kind: evPodGone, pod: p})
+			}
+		},
+	}
+	nodes = cache.ResourceEventHandlerFuncs{
+		AddFunc: func(obj interface{}) {
+			if nd := asNode(obj); nd != nil {
+				n.queue(event{kind: evNode, node: nd})
+			}
+		},
+		UpdateFunc: func(_, newObj interface{}) {
+			if nd := asNode(newObj); nd != nil {
+				n.queue(event{kind: evNode, node: nd})
+			}
+		},
+		DeleteFunc: func(obj interface{}) {
+			if nd := asNode(obj); nd != nil {
+				n.queue(event{kind: evNodeGone, name: nd.Name})
+			}
+		},
+	}
+	return pods, nodes
+}
+
+// samePlacementInputs: what the encoder reads of a bound pod (labels, the
+// NetworkBandwidth annotations, the spec) did not change.
+func samePlacementInputs(a, b *v1.Pod) bool {
+	return equality.Semantic.DeepEqual(a.Labels, b.Labels) && equality.Semantic.DeepEqual(a.Annotations, b.Annotations) &&
+		equality.Semantic.DeepEqual(a.Spec, b.Spec)
 }
 
 func (n *NativeEncoder) ensure() error {
@@ -478,15 +618,19 @@ func (n *NativeEncoder) ensure() error {
 		return fmt.Errorf("ksim_encoder_create: %d", int(rc))
 	}
 	n.enc = e
-	n.known = map[types.UID]int{}
 	return nil
 }
+
+// encodeError marks a delta the encoder refused (a limit): the record is re-encoded whole.
+type encodeError struct{ err error }
+
+func (x *encodeError) Error() string { return x.err.Error() }
 
 func (n *NativeEncoder) errOf(rc C.int) error {
 	if rc == C.KSIM_OK {
 		return nil
 	}
-	return fmt.Errorf("ksim encoder %d: %s", int(rc), C.GoString(C.ksim_encoder_last_error(n.enc)))
+	return &encodeError{fmt.Errorf("ksim encoder %d: %s", int(rc), C.GoString(C.ksim_encoder_last_error(n.enc)))}
 }
 
 func (n *NativeEncoder) info() C.ksim_encoder_info {
@@ -495,54 +639,64 @@ func (n *NativeEncoder) info() C.ksim_encoder_info {
 	return in
 }
 
-// Snapshot re-encodes the framework's snapshot when it holds a node or a pod
-// the device snapshot lacks (or lacks one it holds), and re-sends it.
+// Snapshot brings the device snapshot up to the cluster at a cycle start: the
+// whole snapshot at the first cycle, the queued informer events afterwards.
 func (n *NativeEncoder) Snapshot(e *Engine, f framework.Handle) error {
 	n.mu.Lock()
 	defer n.mu.Unlock()
 	if err := n.ensure(); err != nil {
 		return err
 	}
-	infos, err := f.SnapshotSharedLister().NodeInfos().List()
-	if err != nil {
-		return err
-	}
-	same := n.encoded && len(infos) == len(n.names)
-	pods := 0
-	for i, ni := range infos {
-		if !same {
-			break
+	n.evMu.Lock()
+	ev := n.events
+	n.events = nil
+	n.evMu.Unlock()
+	if !n.encoded {
+		// the framework's snapshot is the record; events queued before it are
+		// in it already (an add of a pod the record holds is a no-op)
+		infos, err := f.SnapshotSharedLister().NodeInfos().List()
+		if err != nil {
+			return err
 		}
-		if ni.Node() == nil || n.pos[ni.Node().Name] != i {
-			same = false
-			break
-		}
-		for _, pi := range ni.Pods {
-			pods++
-			if p, ok := n.known[pi.Pod.UID]; !ok || p != i {
-				same = false
-				break
+		n.nodes, n.bound, n.waiting = map[string]*v1.Node{}, map[string]boundPod{}, map[string]*v1.Pod{}
+		n.nodeOrder = nil
+		var seq uint64
+		for _, ni := range infos {
+			if ni.Node() == nil {
+				continue
+			}
+			n.nodes[ni.Node().Name] = ni.Node()
+			n.nodeOrder = append(n.nodeOrder, ni.Node().Name)
+			for _, pi := range ni.Pods {
+				seq++
+				n.bound[podKey(pi.Pod)] = boundPod{pi.Pod, ni.Node().Name, seq}
 			}
 		}
+		return n.encodeRecord(e)
 	}
-	if same && pods == len(n.known) {
-		return nil
+	if err := n.apply(e, ev); err != nil {
+		var ee *encodeError
+		if errors.As(err, &ee) {
+			return n.encodeRecord(e)
+		}
+		return err
 	}
-	return n.encodeSnapshot(e, infos)
+	return nil
 }
 
-func (n *NativeEncoder) encodeSnapshot(e *Engine, infos []*framework.NodeInfo) error {
+// encodeRecord: the whole record, one ksim_encode_nodes and ksim_set_cluster.
+func (n *NativeEncoder) encodeRecord(e *Engine) error {
 	p := newPool()
-	var bound []*v1.Pod
-	for _, ni := range infos {
-		if ni.Node() == nil {
-			continue
+	for _, name := range n.nodeOrder {
+		p.node(n.nodes[name])
+	}
+	for _, b := range n.sortedBound() {
+		q := b.pod
+		if q.Spec.NodeName != b.node {
+			q = q.DeepCopy() // assumed by the engine: the framework's node
+			q.Spec.NodeName = b.node
 		}
-		p.node(ni.Node())
-		for _, pi := range ni.Pods {
-			p.pod(pi.Pod)
-			bound = append(bound, pi.Pod)
-		}
+		p.pod(q)
 	}
 	if n.Namespaces != nil {
 		for _, ns := range n.Namespaces() {
@@ -568,31 +722,9 @@ func (n *NativeEncoder) encodeSnapshot(e *Engine, infos []*framework.NodeInfo) e
 	if err := n.errOf(C.ksim_encode_nodes(n.enc, cp, &opts)); err != nil {
 		return err
 	}
-	in := n.info()
-	order := make([]int32, int(in.n_nodes))
-	if len(order) > 0 {
-		C.ksim_encoder_node_order(n.enc, (*C.int32_t)(unsafe.Pointer(&order[0])))
-	}
-	names := make([]string, len(order))
-	pos := make(map[string]int, len(order))
-	for i := range order {
-		names[i] = C.GoString(C.ksim_encoder_string(n.enc, C.KSIM_ENC_STR_NODE_NAME, C.int32_t(i), 0))
-		pos[names[i]] = i
-	}
-	n.names, n.pos, n.encoded = names, pos, true
-	n.known = map[types.UID]int{}
-	for _, b := range bound {
-		if q, ok := pos[b.Spec.NodeName]; ok {
-			n.known[b.UID] = q
-		}
-	}
-	n.bound = bound
-	return n.send(e, true)
-}
-
-// send re-sends the encoder's node table (nextStartNodeIndex carried over) and
-// the bound-pod table of DefaultPreemption.
-func (n *NativeEncoder) send(e *Engine, table bool) error {
+	n.readNames()
+	n.encoded = true
+	n.Stats.FullEncodes++
 	var t C.ksim_node_table
 	var v C.ksim_vocab
 	if err := n.errOf(C.ksim_encoder_cluster(n.enc, &t, &v)); err != nil {
@@ -605,17 +737,313 @@ func (n *NativeEncoder) send(e *Engine, table bool) error {
 	if len(n.names) > 0 {
 		_ = e.locked(func() C.int { return C.ksim_set_next_start(e.h, C.int32_t(ns%len(n.names))) })
 	}
-	in := n.info()
-	n.layout = [2]int32{int32(in.n_label_cols), int32(in.n_classes)}
-	if !table {
-		return nil
-	}
-	return n.sendBoundPods(e)
+	n.noteLayout()
+	n.tableOld = true
+	return nil
 }
 
-// sendBoundPods builds ksim_bound_pods (node, priority, start time, requests
-// as NodeInfo's Requested: ksim/preemption.py bound_table).
-func (n *NativeEncoder) sendBoundPods(e *Engine) error {
+func (n *NativeEncoder) sortedBound() []boundPod {
+	out := make([]boundPod, 0, len(n.bound))
+	for _, b := range n.bound {
+		out = append(out, b)
+	}
+	sort.Slice(out, func(i, j int) bool { return out[i].seq < out[j].seq })
+	return out
+}
+
+func (n *NativeEncoder) readNames() {
+	in := n.info()
+	names := make([]string, int(in.n_nodes))
+	pos := make(map[string]int, len(names))
+	for i := range names {
+		names[i] = C.GoString(C.ksim_encoder_string(n.enc, C.KSIM_ENC_STR_NODE_NAME, C.int32_t(i), 0))
+		pos[names[i]] = i
+	}
+	n.names, n.pos = names, pos
+}
+
+func (n *NativeEncoder) noteLayout() {
+	in := n.info()
+	n.layout = [2]int32{int32(in.n_label_cols), int32(in.n_classes)}
+}
+
+// apply: the node events in one update, then the pod events in order.
+func (n *NativeEncoder) apply(e *Engine, ev []event) error {
+	var upd []*v1.Node
+	var gone []string
+	seen := map[string]int{}
+	for _, x := range ev {
+		switch x.kind {
+		case evNode:
+			if i, ok := seen[x.node.Name]; ok {
+				upd[i] = x.node
+			} else {
+				seen[x.node.Name] = len(upd)
+				upd = append(upd, x.node)
+			}
+		case evNodeGone:
+			if i, ok := seen[x.name]; ok {
+				upd = append(upd[:i], upd[i+1:]...)
+				delete(seen, x.name)
+				for k, j := range seen {
+					if j > i {
+						seen[k] = j - 1
+					}
+				}
+			}
+			if _, ok := n.nodes[x.name]; ok {
+				gone = append(gone, x.name)
+			}
+		}
+	}
+	if len(upd) > 0 || len(gone) > 0 {
+		if err := n.applyNodes(e, upd, gone); err != nil {
+			return err
+		}
+	}
+	for _, x := range ev {
+		var err error
+		switch x.kind {
+		case evPod:
+			err = n.podAdded(e, x.pod)
+		case evPodGone:
+			err = n.podDeleted(e, x.pod)
+		}
+		if err != nil {
+			return err
+		}
+	}
+	for key, p := range n.waiting {
+		if _, ok := n.pos[p.Spec.NodeName]; ok {
+			delete(n.waiting, key)
+			if err := n.podAdded(e, p); err != nil {
+				return err
+			}
+		}
+	}
+	return nil
+}
+
+func (n *NativeEncoder) applyNodes(e *Engine, upd []*v1.Node, gone []string) error {
+	// the record first (nodeTree.updateNode re-adds a node whose zone moved)
+	for _, name := range gone {
+		delete(n.nodes, name)
+		for key, b := range n.bound {
+			if b.node == name {
+				delete(n.bound, key)
+			}
+		}
+	}
+	order := n.nodeOrder[:0:0]
+	for _, name := range n.nodeOrder {
+		if _, ok := n.nodes[name]; ok {
+			order = append(order, name)
+		}
+	}
+	for _, nd := range upd {
+		if old, ok := n.nodes[nd.Name]; ok && zoneKey(old) != zoneKey(nd) {
+			for i, x := range order {
+				if x == nd.Name {
+					order = append(order[:i], order[i+1:]...)
+					break
+				}
+			}
+			order = append(order, nd.Name)
+		} else if !ok {
+			order = append(order, nd.Name)
+		}
+		n.nodes[nd.Name] = nd
+	}
+	n.nodeOrder = order
+	p := newPool()
+	for _, nd := range upd {
+		p.node(nd)
+	}
+	removed := make([]C.int32_t, len(gone)+1)
+	for i, name := range gone {
+		removed[i] = p.s(name)
+	}
+	cp, free := p.build()
+	defer free()
+	if err := n.errOf(C.ksim_encoder_update_nodes(n.enc, cp, &removed[0], C.int32_t(len(gone)))); err != nil {
+		return err
+	}
+	n.readNames()
+	oldPos := make([]int32, len(n.names)+1)
+	if err := n.errOf(C.ksim_encoder_old_pos(n.enc, (*C.int32_t)(unsafe.Pointer(&oldPos[0])))); err != nil {
+		return err
+	}
+	var t C.ksim_node_table
+	var v C.ksim_vocab
+	if err := n.errOf(C.ksim_encoder_cluster(n.enc, &t, &v)); err != nil {
+		return err
+	}
+	if err := e.UpsertNodes(&t, &v, oldPos[:len(n.names)]); err != nil {
+		return err
+	}
+	n.noteLayout()
+	n.tableOld = true // the engine dropped the bound-pod table (positions moved)
+	n.Stats.NodeDeltas++
+	return nil
+}
+
+// zoneKey: utilnode.GetZoneKey (region and zone labels, GA then beta)
+func zoneKey(nd *v1.Node) string {
+	l := nd.Labels
+	zone, region := l[v1.LabelTopologyZone], l[v1.LabelTopologyRegion]
+	if zone == "" {
+		zone = l[v1.LabelFailureDomainBetaZone]
+	}
+	if region == "" {
+		region = l[v1.LabelFailureDomainBetaRegion]
+	}
+	if zone == "" && region == "" {
+		return ""
+	}
+	return region + ":\x00:" + zone
+}
+
+// resend: the compile added label columns or count classes; the table again
+// with every node kept (ksim_upsert_nodes replays the device's binds), before
+// any bind the new rows do not count.
+func (n *NativeEncoder) resend(e *Engine) error {
+	in := n.info()
+	if int32(in.n_label_cols) == n.layout[0] && int32(in.n_classes) == n.layout[1] {
+		return nil
+	}
+	var t C.ksim_node_table
+	var v C.ksim_vocab
+	if err := n.errOf(C.ksim_encoder_cluster(n.enc, &t, &v)); err != nil {
+		return err
+	}
+	keep := make([]int32, len(n.names)+1)
+	for i := range n.names {
+		keep[i] = int32(i)
+	}
+	if err := e.UpsertNodes(&t, &v, keep[:len(n.names)]); err != nil {
+		return err
+	}
+	n.noteLayout()
+	n.tableOld = true
+	n.Stats.Resends++
+	return nil
+}
+
+// podAdded: a bound pod enters the snapshot (informer Add / Update).
+func (n *NativeEncoder) podAdded(e *Engine, p *v1.Pod) error {
+	key := podKey(p)
+	if b, ok := n.bound[key]; ok {
+		if b.node == p.Spec.NodeName {
+			return nil // assumed by the engine's Reserve already
+		}
+		if err := n.podDeleted(e, b.pod); err != nil {
+			return err
+		}
+	}
+	pos, ok := n.pos[p.Spec.NodeName]
+	if !ok {
+		n.waiting[key] = p
+		return nil
+	}
+	if err := n.encodeQueue([]*v1.Pod{p}); err != nil {
+		return err
+	}
+	if err := n.resend(e); err != nil {
+		return err
+	}
+	if err := e.Assume(n.encodedSet(), 0, pos); err != nil {
+		return err
+	}
+	if err := n.errOf(C.ksim_encoder_bind(n.enc, 0, C.int32_t(pos))); err != nil {
+		return err
+	}
+	n.bind(key, p, p.Spec.NodeName)
+	n.Stats.PodAdds++
+	return nil
+}
+
+func (n *NativeEncoder) bind(key string, p *v1.Pod, node string) {
+	var seq uint64
+	for _, b := range n.bound {
+		if b.seq > seq {
+			seq = b.seq
+		}
+	}
+	n.bound[key] = boundPod{p, node, seq + 1}
+	n.tableOld = true
+}
+
+// podDeleted: a bound pod leaves the snapshot (informer Delete, Unreserve).
+// The pod is compiled again as it was bound: its adds include the classes
+// registered since its bind, which count it.
+func (n *NativeEncoder) podDeleted(e *Engine, p *v1.Pod) error {
+	key := podKey(p)
+	delete(n.waiting, key)
+	b, ok := n.bound[key]
+	if !ok {
+		return nil
+	}
+	if err := n.encodeQueue([]*v1.Pod{b.pod}); err != nil {
+		return err
+	}
+	if err := n.resend(e); err != nil {
+		return err
+	}
+	ns, name := C.CString(b.pod.Namespace), C.CString(b.pod.Name)
+	defer C.free(unsafe.Pointer(ns))
+	defer C.free(unsafe.Pointer(name))
+	var pos C.int32_t
+	if err := n.errOf(C.ksim_encoder_unbind(n.enc, ns, name, &pos)); err != nil {
+		return err
+	}
+	if err := e.Forget(n.encodedSet(), 0, int(pos)); err != nil {
+		return err
+	}
+	delete(n.bound, key)
+	n.tableOld = true
+	n.Stats.PodDeletes++
+	return nil
+}
+
+// Assume is KsimAssume.Reserve: the cycle's pod on the framework's node, on
+// the device and in the snapshot's membership.
+func (n *NativeEncoder) Assume(e *Engine, pod *v1.Pod, node int) error {
+	n.mu.Lock()
+	defer n.mu.Unlock()
+	if err := n.encodeQueue([]*v1.Pod{pod}); err != nil {
+		return err
+	}
+	if err := n.resend(e); err != nil {
+		return err
+	}
+	if err := e.Assume(n.encodedSet(), 0, node); err != nil {
+		return err
+	}
+	if err := n.errOf(C.ksim_encoder_bind(n.enc, 0, C.int32_t(node))); err != nil {
+		return err
+	}
+	n.bind(podKey(pod), pod, n.names[node])
+	return nil
+}
+
+// Forget is KsimAssume.Unreserve (possibly on the binding goroutine while the
+// next cycle runs: the engine queues it behind that cycle's PreFilter).
+func (n *NativeEncoder) Forget(e *Engine, pod *v1.Pod) error {
+	n.mu.Lock()
+	defer n.mu.Unlock()
+	return n.podDeleted(e, pod)
+}
+
+// BoundTable re-sends DefaultPreemption's bound-pod table when binds, deletes
+// or node deltas changed it since the last dry run (ksim_set_bound_pods:
+// node, priority, start time, requests as NodeInfo's Requested,
+// ksim/preemption.py bound_table).
+func (n *NativeEncoder) BoundTable(e *Engine) error {
+	n.mu.Lock()
+	defer n.mu.Unlock()
+	if !n.tableOld {
+		return nil
+	}
 	if n.boundBufs != nil {
 		n.boundBufs()
 		n.boundBufs = nil
@@ -625,7 +1053,15 @@ func (n *NativeEncoder) sendBoundPods(e *Engine) error {
 	for k := range scalars {
 		scalars[k] = C.GoString(C.ksim_encoder_string(n.enc, C.KSIM_ENC_STR_SCALAR, C.int32_t(k), 0))
 	}
-	rows := len(n.bound)
+	n.boundRows = n.boundRows[:0]
+	var nodes []int
+	for _, b := range n.sortedBound() {
+		if q, ok := n.pos[b.node]; ok {
+			n.boundRows = append(n.boundRows, b.pod)
+			nodes = append(nodes, q)
+		}
+	}
+	rows := len(n.boundRows)
 	node := (*[1 << 30]C.int32_t)(C.malloc(C.size_t(4*rows + 4)))[: rows+1 : rows+1]
 	prio := (*[1 << 30]C.int32_t)(C.malloc(C.size_t(4*rows + 4)))[: rows+1 : rows+1]
 	start := (*[1 << 30]C.int64_t)(C.malloc(C.size_t(8*rows + 8)))[: rows+1 : rows+1]
@@ -636,8 +1072,8 @@ func (n *NativeEncoder) sendBoundPods(e *Engine) error {
 		C.free(unsafe.Pointer(&start[0]))
 		C.free(unsafe.Pointer(&req[0]))
 	}
-	for i, b := range n.bound {
-		node[i] = C.int32_t(n.pos[b.Spec.NodeName])
+	for i, b := range n.boundRows {
+		node[i] = C.int32_t(nodes[i])
 		if b.Spec.Priority != nil {
 			prio[i] = C.int32_t(*b.Spec.Priority)
 		} else {
@@ -659,7 +1095,11 @@ func (n *NativeEncoder) sendBoundPods(e *Engine) error {
 		}
 	}
 	bp := C.ksim_bound_pods{n: C.int32_t(rows), node: &node[0], priority: &prio[0], start_time: &start[0], req: &req[0]}
-	return e.SetBoundPods(&bp)
+	if err := e.SetBoundPods(&bp); err != nil {
+		return err
+	}
+	n.tableOld = false
+	return nil
 }
 
 // podRequests: computePodResourceRequest (sum of containers, max of each init
@@ -704,13 +1144,16 @@ func (n *NativeEncoder) encodeQueue(pods []*v1.Pod) error {
 		opts.added_preferred_first, opts.added_preferred_count = p.preferredTerms(a.PreferredDuringSchedulingIgnoredDuringExecution)
 	}
 	switch n.SpreadDefaulting {
-	case "System":
+	case "", "System": // PodTopologySpreadArgs.defaultingType defaults to System
 		opts.spread_defaults = C.KSIM_SPREAD_DEFAULTS_SYSTEM
 	case "List":
 		if len(n.DefaultConstraints) > 0 {
 			opts.spread_defaults = C.KSIM_SPREAD_DEFAULTS_LIST
 			opts.spread_first, opts.spread_count = p.spreads(n.DefaultConstraints)
 		}
+	case "None":
+	default:
+		return fmt.Errorf("ksim: PodTopologySpread defaultingType %q not supported", n.SpreadDefaulting)
 	}
 	if opts.spread_defaults != C.KSIM_SPREAD_DEFAULTS_NONE {
 		if n.Services != nil {
@@ -787,14 +1230,12 @@ func (n *NativeEncoder) Pods(pods []*v1.Pod) (*C.ksim_pod_set, func(), error) {
 }
 
 // Resync re-sends the table after Pod grew the layout (call before the cycle's
-// ksim_fw_prefilter; plugins.go ensureFilter does).
+// ksim_fw_prefilter; plugins.go ensureFilter does): every node kept, the
+// device's binds replayed on the grown table.
 func (n *NativeEncoder) Resync(e *Engine) error {
 	n.mu.Lock()
 	defer n.mu.Unlock()
-	if !n.layoutGrew() {
-		return nil
-	}
-	return n.send(e, false)
+	return n.resend(e)
 }
 
 func (n *NativeEncoder) NodeNames() []string { return n.names }
@@ -804,7 +1245,7 @@ func (n *NativeEncoder) Position(name string) (int, bool) {
 	return p, ok
 }
 
-func (n *NativeEncoder) BoundPod(index int) *v1.Pod { return n.bound[index] }
+func (n *NativeEncoder) BoundPod(index int) *v1.Pod { return n.boundRows[index] }
 
 // PreFilterNodeNames: NodeAffinity's PreFilterResult.NodeNames (nil: all
 // nodes; empty: conflicting terms), ksim/encode.py prefilter_node_names.

@@ -28,7 +28,7 @@ import (
 )
 
 // ABIVersion is the header version this binding was written against.
-const ABIVersion = 10
+const ABIVersion = 11
 
 // Engine owns one device handle (one GPU, or one node shard of a cluster).
 // A handle is not reentrant: the framework's 16 Filter goroutines (nominated

@@ -77,6 +77,7 @@ import (
 	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/util/sets"
 	utilfeature "k8s.io/apiserver/pkg/util/feature"
+	"k8s.io/client-go/tools/cache"
 	corev1helpers "k8s.io/component-helpers/scheduling/corev1"
 	"k8s.io/klog/v2"
 	apipod "k8s.io/kubernetes/pkg/api/v1/pod"
@@ -90,8 +91,9 @@ import (
 // topology uses / adds, PreFilterResult.NodeNames), as ksim/encode.py does.
 // NativeEncoder (encoder.go) implements it over ksim_encode_nodes / _pods.
 type Encoder interface {
-	// Snapshot brings the engine's device snapshot up to the framework's
-	// (UpdateSnapshot: node informer deltas through Engine.UpsertNodes).
+	// Snapshot brings the engine's device snapshot up to the cluster at a
+	// cycle start (UpdateSnapshot): the whole snapshot once, then the queued
+	// informer events as deltas (Engine.UpsertNodes, ksim_assume / ksim_forget).
 	Snapshot(e *Engine, f framework.Handle) error
 	// Pod encodes one pod; the returned set stays valid until the next call.
 	Pod(pod *v1.Pod) (*C.ksim_pod_set, error)
@@ -111,10 +113,20 @@ type Encoder interface {
 	// table row index -> pod (the table follows the snapshot, SetBoundPods).
 	BoundPod(index int) *v1.Pod
 	// Pods encodes a list of pods into a set the caller owns (C memory) until
-	// release: the nominated pods of a first pass / dry run, and the copy of
-	// the cycle's pod KsimAssume keeps for Unreserve, which may run on the
-	// binding goroutine after the next cycle re-used Pod's buffers.
+	// release: the nominated pods of a first pass / dry run.
 	Pods(pods []*v1.Pod) (ps *C.ksim_pod_set, release func(), err error)
+	// Assume / Forget: the cycle's pod enters / leaves the device snapshot and
+	// the encoder's membership (KsimAssume's Reserve / Unreserve).
+	Assume(e *Engine, pod *v1.Pod, node int) error
+	Forget(e *Engine, pod *v1.Pod) error
+	// BoundTable re-sends DefaultPreemption's bound-pod table when it is stale.
+	BoundTable(e *Engine) error
+}
+
+// informerFed is an Encoder that follows the cluster through informer event
+// handlers (NativeEncoder.Handlers).
+type informerFed interface {
+	Handlers() (pods, nodes cache.ResourceEventHandlerFuncs)
 }
 
 // Profile is the engine-side view of one framework profile.
@@ -132,11 +144,18 @@ var (
 )
 
 // Register attaches an engine to the framework handle of one profile (the
-// host does this when it builds the scheduler, scheduler.go:141-155).
+// host does this when it builds the scheduler, scheduler.go:141-155) and
+// feeds the encoder the pod and node informers' events (the deltas the next
+// cycle start applies).
 func Register(f framework.Handle, p *Profile) {
 	profilesMu.Lock()
 	defer profilesMu.Unlock()
 	profiles[f] = p
+	if fed, ok := p.Enc.(informerFed); ok {
+		pods, nodes := fed.Handlers()
+		f.SharedInformerFactory().Core().V1().Pods().Informer().AddEventHandler(pods)
+		f.SharedInformerFactory().Core().V1().Nodes().Informer().AddEventHandler(nodes)
+	}
 }
 
 func profileOf(f framework.Handle) *Profile {
@@ -169,9 +188,7 @@ type cycle struct {
 type cycleShared struct {
 	mu      sync.Mutex
 	nom     map[int]nomAnswer // node position -> pass-1 answer
-	owned   *C.ksim_pod_set   // KsimAssume's copy of the pod (Unreserve)
-	release func()
-	assumed bool // ksim_assume succeeded and was not undone
+	assumed bool              // KsimAssume's Reserve succeeded and was not undone
 	node    int
 }
 
@@ -544,11 +561,13 @@ func score(b *base, ctx context.Context, state *framework.CycleState, pod *v1.Po
 // An unwrapped Reserve + PostBind plugin the host appends to every profile
 // (after ConvertForSimulator, so the wrapped set and its annotations are
 // unchanged).  Reserve records nothing; it assumes the pod on the framework's
-// node (selectHost's pick, ties included) in the device snapshot, from a copy
-// of the pod's encoding the cycle owns.  Unreserve -- from a later Reserve
-// plugin's failure, Permit, PreBind or Bind, possibly on the binding goroutine
-// after the next cycle started -- forgets it only if this Reserve assumed it
-// (upstream cache.ForgetPod is likewise a no-op for a pod never assumed).
+// node (selectHost's pick, ties included) in the device snapshot and in the
+// encoder's membership (Encoder.Assume), so the next cycle starts from it
+// without a re-encode; the informer's later report of the bound pod is a
+// no-op.  Unreserve -- from a later Reserve plugin's failure, Permit, PreBind
+// or Bind, possibly on the binding goroutine after the next cycle started --
+// forgets it only if this Reserve assumed it (upstream cache.ForgetPod is
+// likewise a no-op for a pod never assumed).
 type KsimAssume struct{ f framework.Handle }
 
 func NewKsimAssume(_ interface{}, f framework.Handle) (framework.Plugin, error) {
@@ -568,16 +587,11 @@ func (p *KsimAssume) Reserve(ctx context.Context, state *framework.CycleState, p
 	if !ok {
 		return framework.AsStatus(fmt.Errorf("node %s not in the engine snapshot", nodeName))
 	}
-	owned, release, err := pr.Enc.Pods([]*v1.Pod{pod})
-	if err != nil {
-		return framework.AsStatus(err)
-	}
-	if err := pr.Engine.locked(func() C.int { return C.ksim_assume(pr.Engine.h, owned, 0, C.int32_t(pos)) }); err != nil {
-		release()
+	if err := pr.Enc.Assume(pr.Engine, pod, pos); err != nil {
 		return framework.AsStatus(err)
 	}
 	c.sh.mu.Lock()
-	c.sh.owned, c.sh.release, c.sh.assumed, c.sh.node = owned, release, true, pos
+	c.sh.assumed, c.sh.node = true, pos
 	c.sh.mu.Unlock()
 	return nil
 }
@@ -593,25 +607,15 @@ func (p *KsimAssume) Unreserve(ctx context.Context, state *framework.CycleState,
 	if !c.sh.assumed {
 		return
 	}
-	_ = pr.Engine.locked(func() C.int { return C.ksim_forget(pr.Engine.h, c.sh.owned, 0, C.int32_t(c.sh.node)) })
+	if err := pr.Enc.Forget(pr.Engine, pod); err != nil {
+		klog.ErrorS(err, "ksim: Unreserve", "pod", klog.KObj(pod))
+	}
 	c.sh.assumed = false
-	c.sh.release()
-	c.sh.owned, c.sh.release = nil, nil
 }
 
-// PostBind: the pod is bound; the snapshot keeps it, the copy is released.
-func (p *KsimAssume) PostBind(ctx context.Context, state *framework.CycleState, pod *v1.Pod, nodeName string) {
-	c := readCycle(state)
-	if c == nil || c.refused {
-		return
-	}
-	c.sh.mu.Lock()
-	defer c.sh.mu.Unlock()
-	if c.sh.release != nil {
-		c.sh.release()
-		c.sh.owned, c.sh.release = nil, nil
-	}
-}
+// PostBind: the pod is bound; the snapshot keeps it (the informer's report of
+// the binding finds it assumed already).
+func (p *KsimAssume) PostBind(ctx context.Context, state *framework.CycleState, pod *v1.Pod, nodeName string) {}
 
 // ---- DefaultPreemption --------------------------------------------------------------
 type postFilter struct{ *base }
@@ -673,6 +677,9 @@ func (p *postFilter) PostFilter(ctx context.Context, state *framework.CycleState
 		}
 		defer release()
 		nps, gn, gf, gc = set, &gnodes[0], &first[0], &count[0]
+	}
+	if err := pr.Enc.BoundTable(pr.Engine); err != nil {
+		return nil, framework.AsStatus(err)
 	}
 	victims := make([]int32, 1024)
 	var out C.ksim_preempt_out

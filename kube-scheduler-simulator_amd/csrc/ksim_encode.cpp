@@ -26,6 +26,7 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -384,6 +385,7 @@ struct Spread {                 // TopologySpreadConstraint
 struct HostPort {
   string ip, proto;
   int32_t port;
+  bool operator==(const HostPort& o) const { return port == o.port && ip == o.ip && proto == o.proto; }
 };
 
 struct Container {
@@ -964,6 +966,16 @@ struct Topo {
     for (const auto& x : names) key += x + '\x1f';
     auto it = class_ids.find(key);
     if (it != class_ids.end()) return it->second;
+    Cls c;
+    c.kind = kImage;
+    c.names = names;
+    c.counts = image_counts(names);
+    return new_class(key, std::move(c));
+  }
+
+  // ImageLocality's per-node score of a container image list (scaledImageScore
+  // over the snapshot's image states)
+  vector<int32_t> image_counts(const vector<string>& names) const {
     vector<int64_t> total(n, 0);
     for (const auto& nm : names) {
       auto st = images.find(nm);
@@ -976,15 +988,12 @@ struct Topo {
         if (st->second.mask[i]) total[i] += add;
     }
     const int64_t max_t = kImageMaxContainer * (int64_t)names.size();
-    Cls c;
-    c.kind = kImage;
-    c.names = names;
-    c.counts.resize(n);
+    vector<int32_t> counts(n);
     for (int i = 0; i < n; i++) {
       const int64_t s = std::min(std::max(total[i], kImageMin), max_t);
-      c.counts[i] = (int32_t)((100 * (s - kImageMin)) / (max_t - kImageMin));
+      counts[i] = (int32_t)((100 * (s - kImageMin)) / (max_t - kImageMin));
     }
-    return new_class(key, std::move(c));
+    return counts;
   }
 
   int image_class(const Pod& p) {
@@ -1082,14 +1091,53 @@ struct Topo {
     for (int cid : sel_ids)
       if (class_matches(classes[cid], p.sig)) classes[cid].counts[pos] += 1;
     for (const auto& c : port_adds(p)) classes[c.first].counts[pos] += c.second;
+    vector<HostPort> ports;
     for (const auto& c : p.containers)
-      for (const auto& hp : c.ports) bound_ports.emplace_back(pos, hp);
-    auto it = bound_sigs.find(p.sig);
+      for (const auto& hp : c.ports) ports.push_back(hp);
+    add_member(p.sig, ports, pos);
+  }
+
+  // The snapshot's membership (ABI 11 deltas): which signatures and host
+  // ports sit on which node.  A class registered later counts its bound pods
+  // from it; the class rows of registered classes stay the snapshot's (the
+  // device adds the binds made since, ksim_upsert_nodes' replay).
+  void add_member(int sig, const vector<HostPort>& ports, int32_t pos) {
+    for (const auto& hp : ports) bound_ports.emplace_back(pos, hp);
+    auto it = bound_sigs.find(sig);
     if (it == bound_sigs.end()) {
-      bound_sig_order.push_back(p.sig);
-      bound_sigs[p.sig].push_back(pos);
+      bound_sig_order.push_back(sig);
+      bound_sigs[sig].push_back(pos);
     } else {
       it->second.push_back(pos);
+    }
+  }
+
+  void drop_member(int sig, const vector<HostPort>& ports, int32_t pos) {
+    for (const auto& hp : ports)
+      for (size_t i = 0; i < bound_ports.size(); i++)
+        if (bound_ports[i].first == pos && bound_ports[i].second == hp) {
+          bound_ports.erase(bound_ports.begin() + (long)i);
+          break;
+        }
+    auto it = bound_sigs.find(sig);
+    if (it == bound_sigs.end()) fail("encoder membership: signature not bound");
+    auto at = std::find(it->second.begin(), it->second.end(), pos);
+    if (at == it->second.end()) fail("encoder membership: pod not on its node");
+    it->second.erase(at);
+  }
+
+  // node positions moved (a node delta): new_of[old] = new position, -1 = the
+  // node left the snapshot with its pods
+  void remap_members(const vector<int32_t>& new_of) {
+    vector<std::pair<int, HostPort>> ports;
+    for (auto& bp : bound_ports)
+      if (new_of[bp.first] >= 0) ports.emplace_back(new_of[bp.first], std::move(bp.second));
+    bound_ports = std::move(ports);
+    for (auto& s : bound_sigs) {
+      vector<int32_t> v;
+      for (int32_t q : s.second)
+        if (new_of[q] >= 0) v.push_back(new_of[q]);
+      s.second = std::move(v);
     }
   }
 
@@ -1126,6 +1174,14 @@ struct Topo {
 };
 
 // ---- the encoder --------------------------------------------------------------------------
+// a pod bound in the snapshot (the scheduler cache's view): its node and
+// what the count classes registered after its bind read of it
+struct Member {
+  int32_t pos = -1;
+  int sig = -1;
+  vector<HostPort> ports;
+};
+
 struct Cluster {
   int32_t n = 0, n_scalar = 0;
   vector<int64_t> alloc_cpu, alloc_mem, alloc_eph, alloc_scalar, req_cpu, req_mem, req_eph, req_scalar, nz_cpu,
@@ -1157,6 +1213,15 @@ struct ksim_encoder {
   Quantities qs;
   std::unordered_map<string, ReqMemo> req_memo;   // per call: resource lists by pool content
   bool has_cluster = false;
+  // snapshot deltas (ABI 11): the nodes in informer add order, the bound pods
+  // by namespace / name, the current pod set's membership records (bind), the
+  // last node delta's old positions
+  vector<Node> nodes;
+  vector<string> extra_scalar;
+  std::unordered_map<string, Member> members;
+  std::unordered_set<string> dup_keys;      // bound twice in one snapshot: not unbindable
+  vector<std::pair<string, Member>> queue_members;
+  vector<int32_t> old_pos;
   // the pod set
   vector<ksim_pod> pods;
   vector<ksim_label_expr> exprs;
@@ -1243,16 +1308,15 @@ Pod read_pod(const Reader& rd, const ksim_k8s_pod& x, Topo& t, std::unordered_ma
 }
 
 // ---- label columns (encode.py EncodedCluster.label_col / value_id) -------------------------
-int label_col(ksim_encoder* e, const string& key) {
+int label_col(ksim_encoder* e, const string& key, bool force = false) {
   Cluster& c = e->c;
   for (size_t i = 0; i < c.label_keys.size(); i++)
     if (c.label_keys[i] == key) return (int)i;
-  bool any = false;
-  for (const auto& lb : c.node_labels)
-    if (lookup(lb, key)) {
-      any = true;
-      break;
-    }
+  bool any = force;
+  for (const auto& lb : c.node_labels) {
+    if (any) break;
+    if (lookup(lb, key)) any = true;
+  }
   if (!any) return -1;
   if ((int)c.label_keys.size() >= KSIM_MAX_LABEL_COLS)
     fail("more than " + std::to_string(KSIM_MAX_LABEL_COLS) + " referenced label keys");
@@ -1353,30 +1417,13 @@ void materialize_classes(ksim_encoder* e, size_t from = 0) {
               c.class_count.begin() + k * (size_t)c.n);
 }
 
-void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_nodes_opts& o) {
-  PoolView pv(pool);
-  Reader rd{pv};
-  Cluster prev = std::move(e->c);
-  Topo prev_topo = std::move(e->topo);
-  const bool keep = o.keep_previous && e->has_cluster;
-  e->has_cluster = false;
-  e->c = Cluster{};
-  e->topo = Topo{};
-  e->pods.clear();
-  e->exprs.clear();
-  e->terms.clear();
-  e->uses.clear();
-  e->adds.clear();
-  e->nn.clear();
-  Cluster& c = e->c;
-  e->req_memo.clear();
-  if (o.nb_node_limit >= 0) c.nb.node_limit = string(pv.str(o.nb_node_limit));
-  if (o.nb_egress_request >= 0) c.nb.egress = string(pv.str(o.nb_egress_request));
-  if (o.nb_ingress_request >= 0) c.nb.ingress = string(pv.str(o.nb_ingress_request));
-  if (pool.n_nodes < 0 || (pool.n_nodes > 0 && !pool.nodes)) fail("pool: bad node list");
-  vector<Node> nodes;
-  nodes.reserve(pool.n_nodes);
-  for (int64_t i = 0; i < pool.n_nodes; i++) nodes.push_back(rd.node(pool.nodes[i]));
+// The node half of a snapshot (encode.py encode_cluster up to the bound pods):
+// nodeTree order over `nodes` (informer add order), scalar columns (`prev`'s
+// first when given), the taint vocabulary (`prev`'s ids first when
+// keep_taints), the static columns, zeroed dynamic columns, names, labels,
+// positions.  c.nb must be set.
+void node_columns(Cluster& c, const vector<Node>& nodes, Quantities& qs, const Cluster* prev, bool keep_taints,
+                  const vector<string>& extra_scalar) {
   vector<string> zk;
   zk.reserve(nodes.size());
   for (const auto& nd : nodes) zk.push_back(zone_key(nd.labels));
@@ -1385,20 +1432,28 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
   if (N > KSIM_MAX_NODES) fail("too many nodes");
   c.n = N;
   // scalar resources: every non-native allocatable name
-  if (keep) c.scalar_names = prev.scalar_names;
+  if (prev) c.scalar_names = prev->scalar_names;
   for (int32_t pos = 0; pos < N; pos++)
     for (const auto& kv : nodes[c.order[pos]].alloc)
       if (!is_native_resource(kv.first) &&
           std::find(c.scalar_names.begin(), c.scalar_names.end(), kv.first) == c.scalar_names.end())
         c.scalar_names.push_back(kv.first);
-  for (const auto& s : pv.strs(o.extra_scalar_first, o.extra_scalar_count))
+  for (const auto& s : extra_scalar)
     if (std::find(c.scalar_names.begin(), c.scalar_names.end(), s) == c.scalar_names.end()) c.scalar_names.push_back(s);
   if ((int)c.scalar_names.size() > KSIM_MAX_SCALAR) fail("too many scalar resources");
   const int32_t S = (int32_t)c.scalar_names.size();
   c.n_scalar = S;
   // taints
-  c.taint_vocab.push_back(Taint{});
   std::unordered_map<string, int> tindex;
+  if (keep_taints && prev && !prev->taint_vocab.empty()) {
+    c.taint_vocab = prev->taint_vocab;
+    for (size_t t = 1; t < c.taint_vocab.size(); t++) {
+      const Taint& x = c.taint_vocab[t];
+      tindex.emplace(x.key + '\x1f' + x.value + '\x1f' + x.effect, (int)t);
+    }
+  } else {
+    c.taint_vocab.push_back(Taint{});
+  }
   c.taints.assign((size_t)KSIM_MAX_NODE_TAINTS * N, 0);
   for (int32_t pos = 0; pos < N; pos++) {
     const Node& nd = nodes[c.order[pos]];
@@ -1423,7 +1478,6 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
   c.taint_effect.push_back(0);
   for (size_t t = 1; t < c.taint_vocab.size(); t++) c.taint_effect.push_back(effect_id(c.taint_vocab[t].effect));
   // allocatable columns
-  Quantities& qs = e->qs;
   c.alloc_cpu.resize(N);
   c.alloc_mem.resize(N);
   c.alloc_eph.resize(N);
@@ -1465,9 +1519,13 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
     c.node_labels.push_back(nodes[c.order[pos]].labels);
   }
   for (int32_t pos = 0; pos < N; pos++) c.pos_of[c.node_names[pos]] = pos;
-  // count classes
-  Topo& t = e->topo;
-  t.n = N;
+  c.topo_log.resize((size_t)N + 1);
+  for (int32_t s = 0; s <= N; s++) c.topo_log[s] = std::log((double)(s + 2));
+}
+
+void read_namespaces(Topo& t, const PoolView& pv) {
+  const ksim_k8s_pool& pool = pv.p;
+  if (pool.n_namespaces < 0 || (pool.n_namespaces > 0 && !pool.namespaces)) fail("pool: bad namespace list");
   for (int64_t i = 0; i < pool.n_namespaces; i++) {
     const ksim_k8s_namespace& ns = pool.namespaces[i];
     const string name(pv.str(ns.name));
@@ -1480,6 +1538,59 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
       t.ns_labels[it->second].second = std::move(lb);
     }
   }
+}
+
+string member_key(string_view ns, string_view name) {
+  string k(ns);
+  k += '\x1f';
+  k += name;
+  return k;
+}
+
+vector<HostPort> host_ports(const Pod& p) {
+  vector<HostPort> out;
+  for (const auto& c : p.containers)
+    for (const auto& hp : c.ports) out.push_back(hp);
+  return out;
+}
+
+void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_nodes_opts& o) {
+  PoolView pv(pool);
+  Reader rd{pv};
+  Cluster prev = std::move(e->c);
+  Topo prev_topo = std::move(e->topo);
+  const bool keep = o.keep_previous && e->has_cluster;
+  e->has_cluster = false;
+  e->c = Cluster{};
+  e->topo = Topo{};
+  e->pods.clear();
+  e->exprs.clear();
+  e->terms.clear();
+  e->uses.clear();
+  e->adds.clear();
+  e->nn.clear();
+  e->members.clear();
+  e->dup_keys.clear();
+  e->queue_members.clear();
+  e->old_pos.clear();
+  Cluster& c = e->c;
+  e->req_memo.clear();
+  if (o.nb_node_limit >= 0) c.nb.node_limit = string(pv.str(o.nb_node_limit));
+  if (o.nb_egress_request >= 0) c.nb.egress = string(pv.str(o.nb_egress_request));
+  if (o.nb_ingress_request >= 0) c.nb.ingress = string(pv.str(o.nb_ingress_request));
+  if (pool.n_nodes < 0 || (pool.n_nodes > 0 && !pool.nodes)) fail("pool: bad node list");
+  vector<Node> nodes;
+  nodes.reserve(pool.n_nodes);
+  for (int64_t i = 0; i < pool.n_nodes; i++) nodes.push_back(rd.node(pool.nodes[i]));
+  e->extra_scalar = pv.strs(o.extra_scalar_first, o.extra_scalar_count);
+  Quantities& qs = e->qs;
+  node_columns(c, nodes, qs, keep ? &prev : nullptr, false, e->extra_scalar);
+  const int32_t N = c.n;
+  const int32_t S = c.n_scalar;
+  // count classes
+  Topo& t = e->topo;
+  t.n = N;
+  read_namespaces(t, pv);
   t.set_images(nodes, c.pos_of);
   if (keep) {                                // TopologyIndex.preregister
     t.selectors = prev_topo.selectors;
@@ -1579,6 +1690,10 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
     const Pod p = read_pod(rd, pool.pods[i], t, e->req_memo, qs, true);
     const int32_t pos = bpos[i];
     t.add_bound(p, pos, carried[i]);
+    const ksim_k8s_pod& x = pool.pods[i];
+    string key = member_key(pv.str(x.namespace_), pv.str(x.name));
+    auto [mi, fresh] = e->members.emplace(std::move(key), Member{pos, p.sig, host_ports(p)});
+    if (!fresh) e->dup_keys.insert(mi->first);
     const ReqMemo& rm = requests_of(e, p);
     const auto& r = rm.requests;
     const auto& nz = rm.nonzero;
@@ -1591,9 +1706,8 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
     c.num_pods[pos] += 1;
     if (!p.annotations.empty()) c.nb_alloc[pos] += nb_pod_allocated(p.annotations, c.nb);
   }
-  c.topo_log.resize((size_t)N + 1);
-  for (int32_t s = 0; s <= N; s++) c.topo_log[s] = std::log((double)(s + 2));
   materialize_classes(e);
+  e->nodes = std::move(nodes);
   e->has_cluster = true;
 }
 
@@ -1956,8 +2070,11 @@ void encode_pods(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_p
   for (const auto& p : pods) register_pod_classes(t, p, sd);   // pass 1
   vector<Taint> unsched_vocab{Taint{}, Taint{kTaintUnschedulable, "", "NoSchedule"}};
   e->pods.resize(pods.size());
+  e->queue_members.clear();
+  e->queue_members.reserve(pods.size());
   for (size_t i = 0; i < pods.size(); i++) {
     const Pod& p = pods[i];
+    e->queue_members.emplace_back(member_key(p.ns, p.name), Member{-1, p.sig, host_ports(p)});
     ksim_pod& rec = e->pods[i];
     rec = ksim_pod{};
     const ReqMemo& rm = requests_of(e, p);
@@ -2084,6 +2201,166 @@ void encode_pods(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_p
     }
   }
   materialize_classes(e, classes_before);
+}
+
+// ---- snapshot deltas (ABI 11) ---------------------------------------------------------------
+// Node informer deltas on the encoder's snapshot ([upstream] internal/cache
+// cache.go AddNode / UpdateNode / RemoveNode, node_tree.go): pool.nodes are
+// added (a new name) or updated (a known name) nodes, removed[] string ids of
+// the pool naming nodes that leave.  The node table is rebuilt over the nodes
+// in add order -- an update that changes the node's zone re-adds it at the end,
+// as nodeTree.updateNode does -- with the previous scalar columns, taint ids,
+// label columns and count classes kept.  A kept node's dynamic columns and
+// class rows stay the snapshot's (the device replays the binds made since on
+// them, ksim_upsert_nodes); an added node starts empty; a removed node's bound
+// pods leave the snapshot.  ImageLocality's rows are recomputed (they read
+// every node's images and the node count).
+void update_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const int32_t* removed, int32_t n_removed) {
+  if (!e->has_cluster) fail("ksim_encoder_update_nodes before ksim_encode_nodes");
+  if (n_removed < 0 || (n_removed > 0 && !removed)) fail("bad removed-node list");
+  PoolView pv(pool);
+  Reader rd{pv};
+  if (pool.n_nodes < 0 || (pool.n_nodes > 0 && !pool.nodes)) fail("pool: bad node list");
+  const size_t M = e->nodes.size();
+  std::unordered_map<string, size_t> at;     // name -> index in the add order
+  for (size_t i = 0; i < M; i++) at.emplace(e->nodes[i].name, i);
+  vector<char> gone(M, 0);
+  for (int32_t r = 0; r < n_removed; r++) {
+    auto it = at.find(string(pv.str(removed[r])));
+    if (it == at.end()) fail("remove of a node not in the snapshot: " + string(pv.str(removed[r])));
+    gone[it->second] = 1;
+  }
+  struct Entry {
+    Node node;
+    int32_t old;                               // position in the current snapshot, -1: new
+  };
+  vector<Entry> head, tail;                    // kept in place; re-added or added (delta order)
+  vector<std::pair<bool, Node>> upd(M);
+  std::unordered_set<string> seen;
+  for (int64_t i = 0; i < pool.n_nodes; i++) {
+    Node nd = rd.node(pool.nodes[i]);
+    if (!seen.insert(nd.name).second) fail("node " + nd.name + " twice in one delta");
+    auto it = at.find(nd.name);
+    if (it == at.end() || gone[it->second]) {  // added (a removed name added again starts empty)
+      tail.push_back(Entry{std::move(nd), -1});
+      continue;
+    }
+    const size_t k = it->second;
+    if (zone_key(e->nodes[k].labels) != zone_key(nd.labels)) {
+      tail.push_back(Entry{std::move(nd), e->c.pos_of.at(e->nodes[k].name)});
+      gone[k] = 2;                             // moved: out of its place, identity kept
+    } else {
+      upd[k] = {true, std::move(nd)};
+    }
+  }
+  for (size_t k = 0; k < M; k++) {
+    if (gone[k]) continue;
+    const int32_t old = e->c.pos_of.at(e->nodes[k].name);
+    head.push_back(Entry{upd[k].first ? std::move(upd[k].second) : std::move(e->nodes[k]), old});
+  }
+  for (auto& x : tail) head.push_back(std::move(x));
+  vector<Node> nodes;
+  vector<int32_t> entry_old;
+  nodes.reserve(head.size());
+  for (auto& x : head) {
+    entry_old.push_back(x.old);
+    nodes.push_back(std::move(x.node));
+  }
+  Cluster oc = std::move(e->c);
+  e->c = Cluster{};
+  Cluster& c = e->c;
+  c.nb = oc.nb;
+  node_columns(c, nodes, e->qs, &oc, true, e->extra_scalar);
+  const int32_t N = c.n, oN = oc.n;
+  vector<int32_t> old_pos(N), new_of(oN, -1);
+  for (int32_t p = 0; p < N; p++) {
+    old_pos[p] = entry_old[c.order[p]];
+    if (old_pos[p] >= 0) new_of[old_pos[p]] = p;
+  }
+  // the snapshot's dynamic columns on kept nodes
+  for (int32_t p = 0; p < N; p++) {
+    const int32_t o = old_pos[p];
+    if (o < 0) continue;
+    c.req_cpu[p] = oc.req_cpu[o];
+    c.req_mem[p] = oc.req_mem[o];
+    c.req_eph[p] = oc.req_eph[o];
+    c.nz_cpu[p] = oc.nz_cpu[o];
+    c.nz_mem[p] = oc.nz_mem[o];
+    c.num_pods[p] = oc.num_pods[o];
+    c.nb_alloc[p] = oc.nb_alloc[o];
+    for (int32_t k = 0; k < oc.n_scalar; k++) c.req_scalar[(size_t)k * N + p] = oc.req_scalar[(size_t)k * oN + o];
+  }
+  // the same label columns, in the same order (value ids renumbered over the new nodes)
+  for (const auto& key : oc.label_keys) label_col(e, key, true);
+  // count classes: membership moves with its nodes, rows too
+  Topo& t = e->topo;
+  t.n = N;
+  read_namespaces(t, pv);
+  for (auto it = e->members.begin(); it != e->members.end();) {
+    const int32_t np = new_of[it->second.pos];
+    if (np < 0) {
+      e->dup_keys.erase(it->first);
+      it = e->members.erase(it);
+    } else {
+      it->second.pos = np;
+      ++it;
+    }
+  }
+  t.remap_members(new_of);
+  t.images.clear();
+  t.set_images(nodes, c.pos_of);
+  for (auto& cls : t.classes) {
+    if (cls.kind == kImage) {
+      cls.counts = t.image_counts(cls.names);
+      continue;
+    }
+    vector<int32_t> row(N, 0);
+    for (int32_t p = 0; p < N; p++)
+      if (old_pos[p] >= 0) row[p] = cls.counts[old_pos[p]];
+    cls.counts = std::move(row);
+  }
+  materialize_classes(e);
+  e->nodes = std::move(nodes);
+  e->old_pos = std::move(old_pos);
+  // pod sets compiled against the old positions are gone
+  e->pods.clear();
+  e->exprs.clear();
+  e->terms.clear();
+  e->uses.clear();
+  e->adds.clear();
+  e->nn.clear();
+  e->queue_members.clear();
+}
+
+// Pod `pod_index` of the current pod set is bound at node position `node` in
+// the snapshot: the scheduler cache's AssumePod / an informer AddPod of a
+// bound pod.  Membership only: the device takes the pod's adds through
+// ksim_assume, and the count classes registered from now on count it.
+void bind_pod(ksim_encoder* e, int32_t pod_index, int32_t node) {
+  if (!e->has_cluster) fail("ksim_encoder_bind before ksim_encode_nodes");
+  if (pod_index < 0 || pod_index >= (int32_t)e->queue_members.size()) fail("bind: pod index out of the pod set");
+  if (node < 0 || node >= e->c.n) fail("bind: node position out of range");
+  const auto& q = e->queue_members[pod_index];
+  if (e->members.count(q.first)) fail("bind: the pod is already bound in the snapshot");
+  Member m = q.second;
+  m.pos = node;
+  e->topo.note_namespace(q.first.substr(0, q.first.find('\x1f')));
+  e->topo.add_member(m.sig, m.ports, node);
+  e->members.emplace(q.first, std::move(m));
+}
+
+// The bound pod namespace/name leaves the snapshot (ForgetPod / RemovePod).
+int32_t unbind_pod(ksim_encoder* e, const char* ns, const char* name) {
+  if (!e->has_cluster) fail("ksim_encoder_unbind before ksim_encode_nodes");
+  if (!ns || !name) fail("unbind: null name");
+  const string key = member_key(ns, name);
+  auto it = e->members.find(key);
+  if (it == e->members.end()) fail("unbind: " + string(ns) + "/" + name + " is not bound in the snapshot");
+  if (e->dup_keys.count(key)) fail("unbind: " + string(ns) + "/" + name + " is bound twice in the snapshot");
+  const int32_t pos = it->second.pos;
+  e->topo.drop_member(it->second.sig, it->second.ports, pos);
+  e->members.erase(it);
+  return pos;
 }
 
 template <class F>
@@ -2217,6 +2494,40 @@ int ksim_encoder_get_info(const ksim_encoder* e, ksim_encoder_info* out) {
   out->n_uses = (int32_t)e->uses.size();
   out->n_adds = (int32_t)e->adds.size();
   out->n_nn = (int32_t)e->nn.size();
+  out->n_members = (int32_t)e->members.size();
+  return KSIM_OK;
+}
+
+int ksim_encoder_update_nodes(ksim_encoder* e, const ksim_k8s_pool* pool, const int32_t* removed,
+                              int32_t n_removed) {
+  return guarded(e, [&] {
+    if (!pool) fail("pool is null");
+    update_nodes(e, *pool, removed, n_removed);
+  });
+}
+
+int ksim_encoder_old_pos(const ksim_encoder* e, int32_t* old_pos) {
+  if (!e || !e->has_cluster || (!old_pos && e->c.n > 0)) return KSIM_E_INVALID;
+  if ((int32_t)e->old_pos.size() != e->c.n) return KSIM_E_INVALID;   // no node delta since the snapshot
+  std::copy(e->old_pos.begin(), e->old_pos.end(), old_pos);
+  return KSIM_OK;
+}
+
+int ksim_encoder_bind(ksim_encoder* e, int32_t pod_index, int32_t node) {
+  return guarded(e, [&] { bind_pod(e, pod_index, node); });
+}
+
+int ksim_encoder_unbind(ksim_encoder* e, const char* namespace_, const char* name, int32_t* node) {
+  return guarded(e, [&] {
+    const int32_t pos = unbind_pod(e, namespace_, name);
+    if (node) *node = pos;
+  });
+}
+
+int ksim_encoder_bound_node(const ksim_encoder* e, const char* namespace_, const char* name, int32_t* node) {
+  if (!e || !e->has_cluster || !namespace_ || !name || !node) return KSIM_E_INVALID;
+  auto it = e->members.find(member_key(namespace_, name));
+  *node = it == e->members.end() ? -1 : it->second.pos;
   return KSIM_OK;
 }
 

@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 MAX_NODES = (1 << 18) - 1
 MAX_NODE_TAINTS = 8
@@ -368,7 +368,7 @@ class EncodePodsOpts(ctypes.Structure):
 
 class EncoderInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("n_nodes", "n_scalar", "n_label_cols", "n_taints", "n_classes",
-                                              "n_pods", "n_exprs", "n_terms", "n_uses", "n_adds", "n_nn", "_pad")]
+                                              "n_pods", "n_exprs", "n_terms", "n_uses", "n_adds", "n_nn", "n_members")]
 
 
 STRUCT_ORDER = [NodeTable, Vocab, LABEL_EXPR_DTYPE, TERM_DTYPE, POD_DTYPE, PodSet, Profile,

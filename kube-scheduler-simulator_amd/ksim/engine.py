@@ -34,7 +34,8 @@ EXPORTS = [
     "ksim_fw_filter_nominated", "ksim_preempt_nominated",
     "ksim_encoder_create", "ksim_encoder_destroy", "ksim_encoder_last_error", "ksim_encode_nodes",
     "ksim_encode_pods", "ksim_encoder_cluster", "ksim_encoder_pods", "ksim_encoder_get_info",
-    "ksim_encoder_node_order", "ksim_encoder_string",
+    "ksim_encoder_node_order", "ksim_encoder_string", "ksim_encoder_update_nodes", "ksim_encoder_old_pos",
+    "ksim_encoder_bind", "ksim_encoder_unbind", "ksim_encoder_bound_node",
 ]
 
 
@@ -141,6 +142,11 @@ def _load(path):
     L.ksim_encoder_node_order.argtypes = [vp, vp]
     L.ksim_encoder_string.argtypes = [vp, i32, i32, i32]
     L.ksim_encoder_string.restype = ctypes.c_char_p
+    L.ksim_encoder_update_nodes.argtypes = [vp, vp, vp, i32]
+    L.ksim_encoder_old_pos.argtypes = [vp, vp]
+    L.ksim_encoder_bind.argtypes = [vp, i32, i32]
+    L.ksim_encoder_unbind.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp]
+    L.ksim_encoder_bound_node.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp]
     return L
 
 

@@ -88,17 +88,33 @@ class EnginePlugins:
     binding (same method names) to get the reference answers under the same
     framework choices."""
 
-    def __init__(self, backend, cluster, prof: SchedulerProfile):
+    def __init__(self, backend, cluster, prof: SchedulerProfile, sync=None):
         self.b = backend
-        self.cluster = cluster
+        self.sync = sync
+        self._cluster = cluster if sync is None else None
         self.prof = prof
         self.forder = prof.filter_order()
         self.snames = [p.name for p in prof.score_plugins()]
-        self.pos = {n: i for i, n in enumerate(cluster.node_names)}
+        self._pos = {n: i for i, n in enumerate(cluster.node_names)} if sync is None else None
         self._pods = None
         self._idx = -1
         self._filter: Optional[Dict] = None
         self._score: Optional[Dict] = None
+
+    @property
+    def cluster(self):
+        """The snapshot the answers refer to (the SnapshotSync's current one)."""
+        return self._cluster if self.sync is None else self.sync.cluster
+
+    @property
+    def pos(self) -> Dict[str, int]:
+        return self._pos if self.sync is None else self.sync.pos
+
+    def begin(self, pod):
+        """Cycle start with an incremental snapshot (plugins.go ensureFilter:
+        Encoder.Snapshot, Pod, Resync): the queued informer events applied,
+        the pod compiled; returns its one-pod set for ``pre_filter``."""
+        return self.sync.cycle(pod)
 
     # ---- PreFilter / Filter ---------------------------------------------------
     def pre_filter(self, pods, index: int, nominated: Optional[Dict[int, List[int]]] = None
@@ -181,7 +197,10 @@ class EnginePlugins:
         the pod set and index are kept for Unreserve (the Go adapter keeps an
         owned copy of the encoding: Unreserve may run after the next cycle)."""
         self._assumed = (self._pods, self._idx, node)
-        self.b.assume(self._pods, self._idx, node)
+        if self.sync is not None:
+            self.sync.assume(node)                # the device, and the snapshot's membership
+        else:
+            self.b.assume(self._pods, self._idx, node)
         return Status()
 
     def unreserve(self, node: int) -> None:
@@ -191,7 +210,10 @@ class EnginePlugins:
         if a is None:
             return
         self._assumed = None
-        self.b.forget(a[0], a[1], a[2])
+        if self.sync is not None:
+            self.sync.forget()
+        else:
+            self.b.forget(a[0], a[1], a[2])
 
     def post_filter(self, priority: int, bound=None, nominated_node: int = -1, nominated_status=None,
                     terminating_lower=None) -> Tuple[Status, int, List[int], bool]:

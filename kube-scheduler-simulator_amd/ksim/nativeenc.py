@@ -354,6 +354,8 @@ class NativeEncoder:
         for name, labels in (namespaces or {}).items():
             pool.lists["namespaces"].extend((pool.s(name),) + pool.kv(labels) + (0,))
         nb_args = nb_args or netbw.NetworkBandwidthArgs()
+        self.nb_args = nb_args
+        self.namespaces = dict(namespaces or {})
         o = abi.EncodeNodesOpts()
         o.nb_node_limit = pool.s(nb_args.node_limit_annotation)
         o.nb_ingress_request = pool.s(nb_args.ingress_request_annotation)
@@ -364,29 +366,73 @@ class NativeEncoder:
         t1 = time.perf_counter()
         self._chk(self.L.ksim_encode_nodes(self.h, ctypes.byref(c), ctypes.byref(o)))
         t2 = time.perf_counter()
+        self.nodes = {n.name: n for n in nodes}
+        cl, order = self._new_cluster()
+        self.seconds = {"pool_s": t1 - t0, "native_s": t2 - t1}
+        return cl, order
+
+    def _new_cluster(self) -> Tuple[EncodedCluster, List[int]]:
+        """A fresh EncodedCluster over the encoder's snapshot (``self.nodes``
+        holds the node objects by name)."""
         info = self.info()
         N = info.n_nodes
         order = np.zeros(N, np.int32)
         self._chk(self.L.ksim_encoder_node_order(self.h, order.ctypes.data_as(ctypes.c_void_p)))
         order = [int(i) for i in order]
+        names = [self._str(abi.ENC_STR_NODE_NAME, i) for i in range(N)]
         taint_vocab = [None] + [Taint(self._str(abi.ENC_STR_TAINT_KEY, t), self._str(abi.ENC_STR_TAINT_VALUE, t),
                                       self._str(abi.ENC_STR_TAINT_EFFECT, t)) for t in range(1, info.n_taints)]
         cl = EncodedCluster(n_nodes=N, n_scalar=info.n_scalar, alloc_cpu=None, alloc_mem=None, alloc_eph=None,
                             alloc_pods=None, alloc_scalar=None, req_cpu=None, req_mem=None, req_eph=None,
                             req_scalar=None, nz_cpu=None, nz_mem=None, num_pods=None, flags=None, taints=None,
                             labels=None, taint_effect=None, label_col_offset=None, label_num=None,
-                            label_num_ok=None, topo=TopologyIndex(N, namespaces),
+                            label_num_ok=None, topo=TopologyIndex(N, self.namespaces),
                             class_count=np.zeros((0, N), np.int32), topo_log=np.zeros(0),
                             nb_limit=np.zeros(0, np.int64), nb_alloc=np.zeros(0, np.int64),
-                            node_names=[nodes[i].name for i in order],
+                            node_names=names,
                             taint_vocab=taint_vocab,
                             scalar_names=[self._str(abi.ENC_STR_SCALAR, k) for k in range(info.n_scalar)],
-                            nb_args=nb_args, node_labels=[dict(nodes[i].labels) for i in order])
+                            nb_args=self.nb_args, node_labels=[dict(self.nodes[n].labels) for n in names])
         cl.native = self
         self.cluster = cl
         self._refresh(cl, full=True)
-        self.seconds = {"pool_s": t1 - t0, "native_s": t2 - t1}
         return cl, order
+
+    # ---- snapshot deltas (ABI 11) ----------------------------------------------------
+    def update_nodes(self, nodes: Sequence[Node] = (), removed: Sequence[str] = ()) -> Tuple[EncodedCluster, np.ndarray]:
+        """ksim_encoder_update_nodes: ``nodes`` added or updated, ``removed``
+        names leave.  Returns the new snapshot (a new EncodedCluster) and
+        old_pos for ksim_upsert_nodes."""
+        pool = Pool()
+        for n in nodes:
+            pool.node(n)
+        rem = np.array([pool.s(x) for x in removed], np.int32)
+        c = pool.build()
+        self._chk(self.L.ksim_encoder_update_nodes(self.h, ctypes.byref(c), rem.ctypes.data_as(ctypes.c_void_p),
+                                                   int(rem.size)))
+        for x in removed:
+            self.nodes.pop(x, None)
+        for n in nodes:
+            self.nodes[n.name] = n
+        cl, _ = self._new_cluster()
+        old_pos = np.zeros(cl.n_nodes, np.int32)
+        self._chk(self.L.ksim_encoder_old_pos(self.h, old_pos.ctypes.data_as(ctypes.c_void_p)))
+        return cl, old_pos
+
+    def bind(self, index: int, node: int) -> None:
+        """ksim_encoder_bind: pod ``index`` of the last encode_pods is bound at ``node``."""
+        self._chk(self.L.ksim_encoder_bind(self.h, index, node))
+
+    def unbind(self, namespace: str, name: str) -> int:
+        """ksim_encoder_unbind: returns the position the pod was bound at."""
+        pos = ctypes.c_int32(-1)
+        self._chk(self.L.ksim_encoder_unbind(self.h, namespace.encode(), name.encode(), ctypes.byref(pos)))
+        return int(pos.value)
+
+    def bound_node(self, namespace: str, name: str) -> int:
+        pos = ctypes.c_int32(-1)
+        self._chk(self.L.ksim_encoder_bound_node(self.h, namespace.encode(), name.encode(), ctypes.byref(pos)))
+        return int(pos.value)
 
     def info(self) -> abi.EncoderInfo:
         info = abi.EncoderInfo()

@@ -73,12 +73,16 @@ class Framework:
         self.tb_seed = tb_seed
         self.next_start = 0
         self.pod_seq = 0
-        self.names = plugins.cluster.node_names
         self.weights = {p.name: (p.weight or 1) for p in prof.score_plugins()}
         self.log: List[dict] = []
         self.nominator: Dict[int, int] = {}      # pod index -> nominated node (insertion order)
         self.nom_prio: Dict[int, int] = {}
         self.terminating: Set[int] = set()       # bound-table indices deleted by preemption
+
+    @property
+    def names(self):
+        """The snapshot's node names (they move with node deltas)."""
+        return self.pl.cluster.node_names
 
     # ---- PodNominator ---------------------------------------------------------
     def nominate(self, index: int, node: int, priority: int) -> None:
@@ -324,6 +328,19 @@ class OracleBackend:
     def __init__(self, oracle, bound=None):
         self.o = oracle
         self.bound = bound
+
+    # the snapshot calls (ksim.fwsnapshot.SnapshotSync's backend protocol)
+    def set_cluster(self, cluster):
+        from oracle.oracle import Oracle
+        prof = self.o.profile
+        self.o.close()
+        self.o = Oracle(cluster, prof)
+
+    def upsert_nodes(self, cluster, old_pos):
+        self.o.upsert_nodes(cluster, old_pos)
+
+    def node_state(self):
+        return self.o.node_state()
 
     def fw_prefilter(self, pods, index):
         return self.o.fw_prefilter(pods, index)

@@ -53,5 +53,35 @@ def test_native_encoder_implements_encoder():
     impl = set(re.findall(r"^func \(n \*NativeEncoder\) ([A-Z]\w*)\(", src["encoder.go"], re.M))
     assert methods and methods <= impl, methods - impl
     for fn in ("ksim_encoder_create", "ksim_encode_nodes", "ksim_encode_pods", "ksim_encoder_cluster",
-               "ksim_encoder_pods", "ksim_encoder_node_order", "ksim_encoder_string"):
+               "ksim_encoder_pods", "ksim_encoder_string"):
         assert f"C.{fn}(" in src["encoder.go"], fn
+
+
+def test_native_encoder_applies_deltas():
+    """ABI 11: the Go encoder follows informer events with the encoder's delta
+    calls (ksim/fwsnapshot.py is its Python mirror, tests/test_fw_snapshot.py
+    and tests/test_gpu_fw_snapshot.py run that mirror): node events through
+    ksim_encoder_update_nodes + ksim_upsert_nodes, bound pods through
+    ksim_assume / ksim_forget + ksim_encoder_bind / _unbind, the framework's
+    Reserve / Unreserve through Encoder.Assume / Forget, and no per-cycle walk
+    of the NodeInfos' pods."""
+    src = _go_sources()
+    enc, plg = src["encoder.go"], src["plugins.go"]
+    for fn in ("ksim_encoder_update_nodes", "ksim_encoder_old_pos", "ksim_encoder_bind", "ksim_encoder_unbind"):
+        assert f"C.{fn}(" in enc, fn
+    assert "e.UpsertNodes(" in enc and "e.Assume(" in enc and "e.Forget(" in enc
+    assert "func (n *NativeEncoder) Handlers()" in enc
+    assert "fed.Handlers()" in plg and ".Informer().AddEventHandler(" in plg
+    assert "pr.Enc.Assume(" in plg and "pr.Enc.Forget(" in plg and "pr.Enc.BoundTable(" in plg
+    snap = re.search(r"func \(n \*NativeEncoder\) Snapshot\(.*?\n}\n", enc, re.S).group(0)
+    # the framework's NodeInfos are read once, at the first cycle (the whole snapshot)
+    assert snap.count("NodeInfos().List()") == 1 and "if !n.encoded" in snap
+
+
+def test_spread_defaulting_defaults_to_system():
+    """PodTopologySpreadArgs.defaultingType defaults to System upstream; the
+    Go encoder's zero value must mean the same, "None" opts out."""
+    enc = _go_sources()["encoder.go"]
+    m = re.search(r'case "", "System":[^\n]*\n\s*opts.spread_defaults = C.KSIM_SPREAD_DEFAULTS_SYSTEM', enc)
+    assert m, "empty SpreadDefaulting must select KSIM_SPREAD_DEFAULTS_SYSTEM"
+    assert 'case "None":' in enc

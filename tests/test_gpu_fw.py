@@ -156,6 +156,73 @@ def test_queued_reserve_lands_before_every_other_call():
     same_state()
 
 
+def test_reserve_after_unscored_cycle_lands_before_every_call():
+    """The round-5 r05b failure: a cycle with ONE feasible node is not scored
+    (the framework skips prioritizeNodes), so its Reserve arrives while the
+    cycle is still open and is queued (pend_bind) -- at r05b (eaa7358) into
+    deferred_binds, which ksim_get_node_state read past: the last cycle's bind
+    was missing from the state read after the run.  Each such Reserve is
+    followed here by a different call -- every state getter, a compat cycle
+    (ksim_eval_pod), a loaded-queue run (ksim_schedule_batch), a next-start
+    write -- and the engine must equal the oracle after it."""
+    nodes, bound, incoming = gen.config3_objects(n_nodes=240, pods_per_node=3, n_incoming=160)
+    rng = np.random.default_rng(4)
+    for k, p in enumerate(incoming):
+        if k % 2 == 0:                              # pinned to one node: one feasible node, no Score
+            p.node_selector = {"kubernetes.io/hostname": nodes[int(rng.integers(0, len(nodes)))].name}
+    extra = gen.config3_objects(n_nodes=240, pods_per_node=0, n_incoming=60, seed=77)[2]
+    for k, p in enumerate(extra):
+        p.name = f"other-{k:04d}"
+    cluster, _ = encode_cluster(nodes, bound)
+    pods = encode_pods(cluster, incoming)
+    others = encode_pods(cluster, extra)
+    sp = profile.SchedulerProfile(percentage_of_nodes_to_score=0)
+    prof = profile.compile_profile(sp)
+    w = profile.default_score_weights()
+    eng = Engine(0)
+    eng.set_profile(prof)
+    eng.set_cluster(cluster.copy_state())
+    ora = Oracle(cluster.copy_state(), prof)
+    fe = Framework(EnginePlugins(EngineBackend(eng), cluster, sp), sp, Store(w), seed=5)
+    fo = Framework(EnginePlugins(OracleBackend(ora), cluster, sp), sp, Store(w), seed=5)
+    unscored, j, b = 0, 0, 0
+    for i in range(pods.n_pods):
+        re, ro = fe.schedule_one(pods, i, 0, None), fo.schedule_one(pods, i, 0, None)
+        assert re.get("chosen") == ro.get("chosen"), i
+        if re.get("chosen", -1) < 0 or len(re.get("feasible", [])) != 1:
+            continue
+        unscored += 1                               # the Reserve is queued behind an unscored cycle
+        what = unscored % 6
+        if what == 0:
+            es, os_ = eng.node_state(), ora.node_state()
+            for k in es:
+                np.testing.assert_array_equal(es[k], os_[k], err_msg=f"{i} {k}")
+        elif what == 1:
+            np.testing.assert_array_equal(eng.class_count(), ora.class_count(), err_msg=str(i))
+        elif what == 2 and j < others.n_pods:
+            e1, o1 = eng.eval_pod(others, j), ora.cycle(others, j)
+            assert e1["chosen"] == o1["chosen"], (i, j)
+            for k in ("fail_plugin", "raw", "total"):
+                np.testing.assert_array_equal(e1[k], o1[k], err_msg=f"{i} {k}")
+            j += 1
+        elif what == 3 and b + 2 <= others.n_pods:
+            sub = others.subset(others.n_pods - 2 - b, 2)
+            ce, _ = eng.schedule_batch(sub)
+            co, _ = ora.schedule(sub)
+            np.testing.assert_array_equal(ce, co, err_msg=str(i))
+            b += 2
+        elif what == 4:
+            np.testing.assert_array_equal(eng.nb_alloc(), ora.nb_alloc(), err_msg=str(i))
+        else:
+            assert eng.next_start == ora.next_start, i
+            eng.set_next_start(eng.next_start)
+    assert unscored > 40
+    es, os_ = eng.node_state(), ora.node_state()      # the last Reserve lands before this read
+    for k in es:
+        np.testing.assert_array_equal(es[k], os_[k], err_msg=k)
+    np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+
+
 def test_fw_api_lists_and_normalize():
     """ksim_fw_prefilter answers every node; ksim_fw_score over arbitrary
     feasible sublists (any order) and ksim_fw_normalize over lists that are

@@ -138,16 +138,17 @@ def host_cpu() -> dict:
 
 
 def cpu_threads_sweep(arg: str) -> list:
-    """--cpu-threads: a comma list, "sweep" (16, 64 and every logical CPU),
-    or one count.  The sweep stops at 4x the cgroup CPU quota when one is set:
-    the GPU box grants 16 CPUs of its 256, and 256 OpenMP threads time-sliced
-    on them ran 100 cycles in 43.6 s against 4.7 s for 49,900 cycles at 16
-    (profiles/r03/reentry/bench_default.json threads_sweep)."""
+    """--cpu-threads: a comma list, "sweep" (1, 4, 16, 64 and every logical
+    CPU: the 1 -> 16 scaling is reported), or one count.  The sweep stops at
+    4x the cgroup CPU quota when one is set: the GPU box grants 16 CPUs of its
+    256, and 256 OpenMP threads time-sliced on them ran 100 cycles in 43.6 s
+    against 4.7 s for 49,900 cycles at 16 (profiles/r03/reentry/
+    bench_default.json threads_sweep)."""
     n = os.cpu_count() or 1
     if arg == "sweep":
         quota = host_cpu()["cgroup_cpu_quota"]
         cap = n if not quota else max(16, int(4 * quota))
-        return sorted({t for t in (16, 64, n) if t <= min(n, cap)} | {min(16, n)})
+        return sorted({t for t in (1, 4, 16, 64, n) if t <= min(n, cap)} | {min(16, n)})
     return [int(x) for x in arg.split(",")]
 
 
@@ -172,11 +173,14 @@ def cpu_baseline(cluster, pods, sp, seconds: float, threads, label: str) -> dict
                       "evals": int(st2.evals), "seconds": dt2})
         log(f"[rank 0] cpu baseline {t} threads: {st2.evals / dt2:.3e} evals/s ({n} cycles, {dt2:.1f} s)")
     best = max(sweep, key=lambda x: x["value"])
+    one = next((x for x in sweep if x["threads"] == 1), None)
+    scaling = {f"{x['threads']}_threads_vs_1": x["value"] / one["value"] for x in sweep} if one else None
     return {"value": best["value"], "unit": "pod x node evals/s", "cores": best["threads"], "kind": "port",
-            "pods_per_s": best["pods_per_s"], "host": host_cpu(), "threads_sweep": sweep,
+            "pods_per_s": best["pods_per_s"], "host": host_cpu(), "threads_sweep": sweep, "scaling": scaling,
             "sample": f"{label} pods 100..{100 + best['cycles']} ({best['cycles']} cycles, {best['evals']} evals) "
                       f"after 100 warm cycles from the empty cluster, same profile/mode, oracle/ksim_oracle.c "
-                      f"OpenMP; best of {[x['threads'] for x in sweep]} threads ({best['threads']}), "
+                      f"OpenMP (filter, scan, scores, NormalizeScore extrema, totals and selectHost split per "
+                      f"thread); best of {[x['threads'] for x in sweep]} threads ({best['threads']}), "
                       f"{best['seconds']:.1f} s"}
 
 

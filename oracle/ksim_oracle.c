@@ -27,7 +27,15 @@
 #define MIN_FEASIBLE_NODES_TO_FIND 100            /* schedule_one.go minFeasibleNodesToFind */
 #define MIN_FEASIBLE_NODES_PERCENTAGE_TO_FIND 5   /* schedule_one.go minFeasibleNodesPercentageToFind */
 
+#define ORACLE_MAX_THREADS 256
+
 struct ksim_oracle {
+  /* ksim_oracle_schedule's per-thread partials (one cache line apart) */
+  int32_t th_cnt[ORACLE_MAX_THREADS * 16], th_err[ORACLE_MAX_THREADS * 16], th_pre[ORACLE_MAX_THREADS * 16];
+  int32_t th_node[ORACLE_MAX_THREADS * 16], th_stop;
+  int64_t th_mn[ORACLE_MAX_THREADS * 8], th_mx[ORACLE_MAX_THREADS * 8];
+  uint64_t th_lo[ORACLE_MAX_THREADS * 8];
+  int64_t th_ext[ORACLE_MAX_THREADS * 2 * KSIM_MAX_SCORE];
   ksim_profile prof;
   int32_t n, n_scalar, n_label_cols;
   /* static node columns */
@@ -1029,6 +1037,31 @@ static void normalize_plugin(int plugin, const topo_ctx* t, const uint8_t* ign, 
   }
 }
 
+/* normalize_plugin's map of one score given the list's extrema (the timing
+ * path reduces the extrema across threads first) */
+static int64_t normalize_one(int plugin, uint8_t ign, int64_t mn, int64_t mx, int64_t v) {
+  switch (plugin) {
+    case KSIM_PL_TAINT_TOLERATION:
+    case KSIM_PL_NODE_AFFINITY: {         /* DefaultNormalizeScore: mx = maxCount */
+      const int reverse = plugin == KSIM_PL_TAINT_TOLERATION;
+      if (mx == 0) return reverse ? MAX_NODE_SCORE : v;
+      const int64_t x = MAX_NODE_SCORE * v / mx;
+      return reverse ? MAX_NODE_SCORE - x : x;
+    }
+    case KSIM_PL_POD_TOPOLOGY_SPREAD:
+      if (ign) return 0;
+      return (mx == 0) ? MAX_NODE_SCORE : MAX_NODE_SCORE * (mx + mn - v) / mx;
+    case KSIM_PL_INTER_POD_AFFINITY:
+    case KSIM_PL_NETWORK_BANDWIDTH: {
+      const int64_t diff = mx - mn;
+      double f = 0;
+      if (diff > 0) f = (double)MAX_NODE_SCORE * ((double)(v - mn) / (double)diff);
+      return (int64_t)f;
+    }
+  }
+  return v;
+}
+
 static int has_normalize(int plugin) {
   return plugin == KSIM_PL_TAINT_TOLERATION || plugin == KSIM_PL_NODE_AFFINITY ||
          plugin == KSIM_PL_POD_TOPOLOGY_SPREAD || plugin == KSIM_PL_INTER_POD_AFFINITY ||
@@ -1352,6 +1385,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
   const int32_t N = o->n;
   if (N == 0) return KSIM_E_INVALID;
   if (nthreads < 1) nthreads = 1;
+  if (nthreads > ORACLE_MAX_THREADS) nthreads = ORACLE_MAX_THREADS;
   const int S = o->prof.n_score;
   int64_t evals = 0, sched = 0, unsched = 0;
   uint8_t* feas = o->fail;   /* 1 = passed all filters */
@@ -1371,58 +1405,197 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
     topo_ctx tc;
     topo_prefilter(o, ps, p, &tc);
 
+    /* no PreScore state and no NetworkBandwidth score check: the list's scores,
+     * extrema and totals are made slice by slice, with four barriers a pod */
+    const int fused = tc.n == 0 && !has_score_plugin(o, KSIM_PL_NETWORK_BANDWIDTH);
 #pragma omp parallel num_threads(nthreads) if (nthreads > 1)
     {
-#pragma omp for schedule(static)
-      for (int32_t node = 0; node < N; node++) {
+      const int T = omp_get_num_threads(), tid = omp_get_thread_num();
+      /* findNodesThatPassFilters: each thread filters its slice of the scan
+       * from nextStartNodeIndex and counts its feasible nodes up to its first
+       * error; one thread places the stop (the (K+1)-th feasible node or the
+       * first error, both counted as evaluated); each thread then lists its
+       * feasible nodes before the stop at its prefix offset. */
+      const int32_t a = (int32_t)((int64_t)NS * tid / T), b = (int32_t)((int64_t)NS * (tid + 1) / T);
+      int32_t cnt = 0, err_at = NS;
+      for (int32_t i = a; i < b; i++) {
+        const int32_t node = scan_node_at(&ss, i);
         uint32_t det;
         const uint8_t r = run_filter_plugins(o, ps, p, &tc, node, &det);
-        feas[node] = r == KSIM_PASSED ? 1 : nb_error(o, r, det) ? 2 : 0;
+        const uint8_t f = r == KSIM_PASSED ? 1 : nb_error(o, r, det) ? 2 : 0;
+        feas[node] = f;
+        if (err_at == NS) {
+          if (f == 2) err_at = i;
+          else cnt += f;
+        }
       }
+      o->th_cnt[tid * 16] = cnt;
+      o->th_err[tid * 16] = err_at;
+#pragma omp barrier
 #pragma omp single
       {
-        for (int32_t i = 0; i < NS; i++) {
-          int32_t node = scan_node_at(&ss, i);
-          evaluated++;
-          if (feas[node] == 2) {
-            error = 1;
+        int32_t pre = 0, stop = NS, before = -1;
+        for (int t = 0; t < T; t++) {
+          const int32_t ta = (int32_t)((int64_t)NS * t / T), tb = (int32_t)((int64_t)NS * (t + 1) / T);
+          o->th_pre[t * 16] = pre;
+          if (pre + o->th_cnt[t * 16] > K) {            /* the (K+1)-th feasible node is in this slice */
+            int32_t c2 = pre;
+            for (int32_t i = ta; i < tb; i++)
+              if (feas[scan_node_at(&ss, i)] == 1 && ++c2 == K + 1) {
+                stop = i;
+                break;
+              }
+            before = K;
             break;
           }
-          if (feas[node]) {
-            if (nf == K) break;
-            o->flist[nf++] = node;
-          } else {
-            nfailed++;
+          pre += o->th_cnt[t * 16];
+          if (o->th_err[t * 16] < NS) {                 /* an error before it */
+            stop = o->th_err[t * 16];
+            error = 1;
+            before = pre;
+            break;
           }
         }
-        if (!error && nb_score_error(o, o->flist, nf)) error = 1;
+        nf = before < 0 ? pre : before;
+        evaluated = stop < NS ? stop + 1 : NS;
+        nfailed = (stop < NS ? stop : NS) - nf;
+        o->th_stop = stop;
       }
-      if (nf > 1 && !error) {
-#pragma omp single
-        topo_prescore(o, ps, p, o->flist, nf, &tc);
-#pragma omp for schedule(static)
-        for (int32_t j = 0; j < nf; j++)
-          for (int s = 0; s < S; s++)
-            raw[(size_t)s * N + j] = score_plugin_raw(o, ps, p, &tc, o->prof.score[s], o->flist[j]);
-#pragma omp single
-        {
-          for (int32_t j = 0; j < nf; j++) totals[j] = (S == 0) ? 1 : 0;
-          for (int32_t j = 0; j < nf; j++) ign_buf[j] = tc.has_soft ? o->ignored[o->flist[j]] : 0;
-          for (int s = 0; s < S; s++) {
-            int pl = o->prof.score[s];
-            int64_t* v = raw + (size_t)s * N;
-            if (has_normalize(pl)) normalize_plugin(pl, &tc, ign_buf, nf, v);
-            int64_t w = o->prof.score_weight[s] == 0 ? 1 : o->prof.score_weight[s];
-            for (int32_t j = 0; j < nf; j++) totals[j] += v[j] * w;
+      const int32_t w0 = o->th_pre[tid * 16];
+      int32_t w1 = w0;
+      {
+        const int32_t e = b < o->th_stop ? b : o->th_stop;
+        for (int32_t i = a; i < e; i++) {
+          const int32_t node = scan_node_at(&ss, i);
+          if (feas[node] == 1) o->flist[w1++] = node;
+        }
+      }
+      if (fused && nf > 1 && !error) {
+        /* prioritizeNodes over this thread's part of the list: raw scores and
+         * the per-plugin extrema NormalizeScore reads */
+        int64_t* mn = &o->th_ext[tid * 2 * KSIM_MAX_SCORE];
+        int64_t* mx = mn + KSIM_MAX_SCORE;
+        for (int s2 = 0; s2 < S; s2++) {
+          const int pl = o->prof.score[s2];
+          mn[s2] = INT64_MAX;
+          mx[s2] = (pl == KSIM_PL_INTER_POD_AFFINITY || pl == KSIM_PL_NETWORK_BANDWIDTH) ? INT64_MIN : 0;
+        }
+        for (int32_t j = w0; j < w1; j++)
+          for (int s2 = 0; s2 < S; s2++) {
+            const int64_t v = score_plugin_raw(o, ps, p, &tc, o->prof.score[s2], o->flist[j]);
+            raw[(size_t)s2 * N + j] = v;
+            if (v < mn[s2]) mn[s2] = v;
+            if (v > mx[s2]) mx[s2] = v;
           }
-          int64_t best_total = 0;
-          uint64_t best_lo = 0;
+#pragma omp barrier
+        int64_t gmn[KSIM_MAX_SCORE], gmx[KSIM_MAX_SCORE];
+        for (int s2 = 0; s2 < S; s2++) {
+          gmn[s2] = mn[s2];
+          gmx[s2] = mx[s2];
+          for (int t = 0; t < T; t++) {
+            const int64_t* tm = &o->th_ext[t * 2 * KSIM_MAX_SCORE];
+            if (tm[s2] < gmn[s2]) gmn[s2] = tm[s2];
+            if (tm[KSIM_MAX_SCORE + s2] > gmx[s2]) gmx[s2] = tm[KSIM_MAX_SCORE + s2];
+          }
+        }
+        /* NormalizeScore, the weighted totals and selectHost's best (TB) on this part */
+        int64_t bt = 0;
+        uint64_t bl = 0;
+        int32_t bn = -1;
+        for (int32_t j = w0; j < w1; j++) {
+          int64_t tot = S == 0 ? 1 : 0;
+          for (int s2 = 0; s2 < S; s2++) {
+            const int pl = o->prof.score[s2];
+            int64_t v = raw[(size_t)s2 * N + j];
+            if (has_normalize(pl) && !(pl == KSIM_PL_INTER_POD_AFFINITY && tc.topology_score_empty))
+              v = normalize_one(pl, 0, gmn[s2], gmx[s2], v);
+            tot += v * (o->prof.score_weight[s2] == 0 ? 1 : o->prof.score_weight[s2]);
+          }
+          const uint64_t lo = ksim_oracle_tb_lo(o->prof.tiebreak_seed, seq, o->flist[j]);
+          if (bn < 0 || tb_better(tot, lo, bt, bl)) {
+            bt = tot;
+            bl = lo;
+            bn = o->flist[j];
+          }
+        }
+        o->th_mn[tid * 8] = bt;
+        o->th_lo[tid * 8] = bl;
+        o->th_node[tid * 16] = bn;
+#pragma omp barrier
+#pragma omp single
+        for (int t = 0; t < T; t++) {
+          const int32_t n2 = o->th_node[t * 16];
+          if (n2 >= 0 && (chosen < 0 || tb_better(o->th_mn[t * 8], o->th_lo[t * 8], bt, bl))) {
+            bt = o->th_mn[t * 8];
+            bl = o->th_lo[t * 8];
+            chosen = n2;
+          }
+        }
+      } else {
+#pragma omp barrier
+#pragma omp single
+        if (!error && nb_score_error(o, o->flist, nf)) error = 1;
+        if (nf > 1 && !error) {
+#pragma omp single
+          topo_prescore(o, ps, p, o->flist, nf, &tc);
+#pragma omp for schedule(static)
           for (int32_t j = 0; j < nf; j++) {
+            totals[j] = (S == 0) ? 1 : 0;
+            ign_buf[j] = tc.has_soft ? o->ignored[o->flist[j]] : 0;
+            for (int s2 = 0; s2 < S; s2++)
+              raw[(size_t)s2 * N + j] = score_plugin_raw(o, ps, p, &tc, o->prof.score[s2], o->flist[j]);
+          }
+          /* NormalizeScore per plugin: per-thread extrema, combined, then the map */
+          for (int s2 = 0; s2 < S; s2++) {
+            const int pl = o->prof.score[s2];
+            if (!has_normalize(pl) || (pl == KSIM_PL_INTER_POD_AFFINITY && tc.topology_score_empty)) continue;
+            int64_t* v = raw + (size_t)s2 * N;
+            int64_t mn = INT64_MAX, mx = (pl == KSIM_PL_INTER_POD_AFFINITY || pl == KSIM_PL_NETWORK_BANDWIDTH)
+                                             ? INT64_MIN : 0;
+#pragma omp for schedule(static)
+            for (int32_t j = 0; j < nf; j++) {
+              if (pl == KSIM_PL_POD_TOPOLOGY_SPREAD && ign_buf[j]) continue;
+              if (v[j] < mn) mn = v[j];
+              if (v[j] > mx) mx = v[j];
+            }
+            o->th_mn[tid * 8] = mn;
+            o->th_mx[tid * 8] = mx;
+#pragma omp barrier
+            for (int t = 0; t < T; t++) {
+              if (o->th_mn[t * 8] < mn) mn = o->th_mn[t * 8];
+              if (o->th_mx[t * 8] > mx) mx = o->th_mx[t * 8];
+            }
+#pragma omp for schedule(static)
+            for (int32_t j = 0; j < nf; j++) v[j] = normalize_one(pl, ign_buf[j], mn, mx, v[j]);
+          }
+          /* the weighted totals and selectHost (TB): per thread, then combined */
+          int64_t bt = 0;
+          uint64_t bl = 0;
+          int32_t bn = -1;
+#pragma omp for schedule(static)
+          for (int32_t j = 0; j < nf; j++) {
+            for (int s2 = 0; s2 < S; s2++) {
+              const int64_t w = o->prof.score_weight[s2] == 0 ? 1 : o->prof.score_weight[s2];
+              totals[j] += raw[(size_t)s2 * N + j] * w;
+            }
             const uint64_t lo = ksim_oracle_tb_lo(o->prof.tiebreak_seed, seq, o->flist[j]);
-            if (chosen < 0 || tb_better(totals[j], lo, best_total, best_lo)) {
-              best_total = totals[j];
-              best_lo = lo;
-              chosen = o->flist[j];
+            if (bn < 0 || tb_better(totals[j], lo, bt, bl)) {
+              bt = totals[j];
+              bl = lo;
+              bn = o->flist[j];
+            }
+          }
+          o->th_mn[tid * 8] = bt;
+          o->th_lo[tid * 8] = bl;
+          o->th_node[tid * 16] = bn;
+#pragma omp barrier
+#pragma omp single
+          for (int t = 0; t < T; t++) {
+            const int32_t n2 = o->th_node[t * 16];
+            if (n2 >= 0 && (chosen < 0 || tb_better(o->th_mn[t * 8], o->th_lo[t * 8], bt, bl))) {
+              bt = o->th_mn[t * 8];
+              bl = o->th_lo[t * 8];
+              chosen = n2;
             }
           }
         }

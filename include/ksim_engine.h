@@ -692,7 +692,13 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
  * keeps its graphs across ksim_set_profile captures none); out[20] device
  * time of the last ksim_match_terms in ns (HIP events); out[21..24] framework-
  * driven calls since ksim_create: ksim_fw_score answered on the host / on the
- * device, ksim_fw_normalize answered from ksim_fw_score's list / on the device.
+ * device, ksim_fw_normalize answered from ksim_fw_score's list / on the device;
+ * out[25] the batch evaluation launches' instantiations launched or captured
+ * by this process (a bitmask: bits 0..9 k_batch_top_commit -- flush direct /
+ * overlay-indexed, node-stationary direct / indexed, KEEP default-shape /
+ * generic, direct default-shape / generic, indexed default-shape / generic --
+ * bits 16..21 k_batch_top -- static-class default-shape KEEP, static-class
+ * default-shape, static-class, FAST default-shape, FAST, generic keys).
  * Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),

@@ -27,6 +27,8 @@
 // An exhausted incomplete list also ends the batch; the next batch starts at
 // the first pod not committed.
 #include "ksim_device.h"
+#include <atomic>
+
 #include "ksim_internal.h"
 #include "ksim_wave.h"
 #include "ksim_commit.h"
@@ -1189,11 +1191,29 @@ __global__ __launch_bounds__(1024) void k_batch_top_commit(DevCluster c, DevPods
   }
 }
 
+// Which instantiations of the evaluation launches a process has launched (or
+// captured into a graph): bits 0..9 k_batch_top_commit (tc_variant), bits
+// 16..21 k_batch_top (launch_eval_top).  ksim_get_diag out[25]; the variant
+// tests assert every bit is reached.
+static std::atomic<uint64_t> g_variant_reach{0};
+uint64_t batch_variant_reach() { return g_variant_reach.load(std::memory_order_relaxed); }
+static void note_variant(int bit) { g_variant_reach.fetch_or(1ull << bit, std::memory_order_relaxed); }
+
+template <bool FLUSH, bool DIRECT, bool DEF, bool KEEP, bool NS>
+constexpr int tc_variant() {
+  if (FLUSH) return DIRECT ? 0 : 1;
+  if (NS) return DIRECT ? 2 : 3;
+  if (KEEP) return DEF ? 4 : 5;
+  if (DIRECT) return DEF ? 6 : 7;
+  return DEF ? 8 : 9;
+}
+
 // the evaluation launch of a deferred-commit batch (DIRECT overlay when the
 // local node range fits kLazyDirect; DEF / KEEP as k_batch_top_commit says)
 template <bool FLUSH, bool DIRECT, bool DEF, bool KEEP, bool NS = false>
 static void launch_tc(const LazyBatch& z, uint64_t* xsend, hipStream_t stream) {
   const LaunchArgs& a = z.a;
+  note_variant(tc_variant<FLUSH, DIRECT, DEF, KEEP, NS>());
   k_batch_top_commit<FLUSH, DIRECT, DEF, KEEP, NS><<<kBatchPods, 1024, 0, stream>>>(
       a.c, a.P, a.dprof, a.dbp, z.step, a.s.topk, a.s.topk_cnt, a.s.topk_complete, a.chosen, xsend);
 }
@@ -1286,6 +1306,7 @@ const char* const kBatchKernelNames[kKernelsPerBatch] = {"k_batch_top", "k_batch
 static void launch_eval_top(const LaunchArgs& a, uint64_t* xsend, hipStream_t stream) {
   const bool def = fast_def(a.bp);
   const bool keep = a.c.eval_hi - a.c.eval_lo <= kKeepPerLane * 1024;
+  note_variant(a.stab && def && keep ? 16 : a.stab && def ? 17 : a.stab ? 18 : a.fast && def ? 19 : a.fast ? 20 : 21);
   if (a.stab && def && keep)
     k_batch_top<true, 1024, true, true, true><<<kBatchPods, 1024, 0, stream>>>(
         a.c, a.P, a.dprof, a.dbp, a.st, a.s.topk, a.s.topk_cnt, a.s.topk_complete, xsend, a.s.pnorm);

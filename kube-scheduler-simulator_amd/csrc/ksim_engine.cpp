@@ -204,6 +204,7 @@ struct ksim_handle {
     int32_t node = 0;
     int sign = 0;
   } pend_bind;
+  int64_t pend_reuse = 0;                      // upload_blob found the queued Reserve's arena reused (flushed)
   void* pout = nullptr;
   void* pout_d = nullptr;
   size_t pout_cap = 0;
@@ -2636,6 +2637,13 @@ static DevPods blob_pods(const ksim_handle* h, const PodBlob& b, char* d) {
 static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPods& P,
                        WinState* begin_win = nullptr, bool record = false, bool synced = false) {
   const size_t total = b.bytes.size();
+  if (h->pend_bind.on && arena.p && (const char*)h->pend_bind.P.pods >= (const char*)arena.p &&
+      (const char*)h->pend_bind.P.pods < (const char*)arena.p + arena.cap) {
+    // the queued Reserve reads this arena (every caller alternates arenas, so
+    // this does not happen today): land it before the arena is grown or overwritten
+    h->pend_reuse++;
+    if (const int prc = flush_pend_bind(h)) return prc;
+  }
   if (total > h->pin_cap || total > arena.cap) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
   } else if (h->up_pending) {
@@ -3869,18 +3877,24 @@ int ksim_reset_cluster(ksim_handle* h) {
   // the dynamic columns from their snapshot copies and the run state zeroed,
   // in one launch (every buffer is a hipMalloc allocation: 16-byte aligned)
   ResetList L;
-  L.add(c.req_cpu, h->init.req_cpu, 8 * N);
-  L.add(c.req_mem, h->init.req_mem, 8 * N);
-  L.add(c.req_eph, h->init.req_eph, 8 * N);
-  if (c.n_scalar) L.add(c.req_scalar, h->init.req_scalar, 8 * N * c.n_scalar);
-  L.add(c.nz_cpu, h->init.nz_cpu, 8 * N);
-  L.add(c.nz_mem, h->init.nz_mem, 8 * N);
-  L.add(c.num_pods, h->init.num_pods, 4 * N);
-  if (c.n_classes) L.add(c.cnt, h->init.cnt, 4 * N * c.n_classes);
-  L.add(c.nb_alloc, h->init.nb_alloc, 8 * N);
+  hipError_t fe = hipSuccess;
+  auto put = [&](void* d, const void* s, size_t bytes) {   // an entry the launch cannot take: its own copy
+    if (L.add(d, s, bytes) || fe != hipSuccess) return;
+    fe = s ? hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, h->stream) : hipMemsetAsync(d, 0, bytes, h->stream);
+  };
+  put(c.req_cpu, h->init.req_cpu, 8 * N);
+  put(c.req_mem, h->init.req_mem, 8 * N);
+  put(c.req_eph, h->init.req_eph, 8 * N);
+  if (c.n_scalar) put(c.req_scalar, h->init.req_scalar, 8 * N * c.n_scalar);
+  put(c.nz_cpu, h->init.nz_cpu, 8 * N);
+  put(c.nz_mem, h->init.nz_mem, 8 * N);
+  put(c.num_pods, h->init.num_pods, 4 * N);
+  if (c.n_classes) put(c.cnt, h->init.cnt, 4 * N * c.n_classes);
+  put(c.nb_alloc, h->init.nb_alloc, 8 * N);
   static_assert(sizeof(DevState) % 4 == 0, "DevState by words");
-  L.add(h->st, nullptr, sizeof(DevState));
-  launch_reset_copy(L, h->stream);
+  put(h->st, nullptr, sizeof(DevState));
+  HIPCHK(h, fe);
+  if (L.n) launch_reset_copy(L, h->stream);
   launch_ptab_init(h->dc, h->dp, h->stream);        // the queue's persistent tables follow the counts
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -4088,7 +4102,7 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  int64_t v[3 + 16 + 2 + 4] = {st.batches, st.truncations, st.cuts};
+  int64_t v[3 + 16 + 2 + 4 + 1] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   if (unsigned long long* cp = cp_clock_buffer())   // KSIM_CP_CLOCKS builds: the chain + pairs phase clocks
     HIPCHK(h, hcopy(h, v + 3, cp, 8 * 8, hipMemcpyDeviceToHost));
@@ -4097,7 +4111,8 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   v[19] = h->graph_captures;
   v[20] = h->match_ns;
   for (int k = 0; k < 4; k++) v[21 + k] = h->fw_counts[k];
-  const int32_t m = n < 25 ? n : 25;
+  v[25] = (int64_t)batch_variant_reach();
+  const int32_t m = n < 26 ? n : 26;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }

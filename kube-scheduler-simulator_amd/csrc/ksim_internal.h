@@ -167,6 +167,8 @@ void launch_adapt_lazy_flush(const LazyBatch& z, hipStream_t stream);
 void launch_static_table(const LaunchArgs& a, const int32_t* rep, int32_t n_cls, uint64_t* stab, hipStream_t stream);
 uint32_t launch_batch_lazy(const LazyBatch& z, hipStream_t stream, hipEvent_t* evs = nullptr);
 void launch_lazy_flush(const LazyBatch& z, hipStream_t stream);
+// the evaluation-launch instantiations launched so far (ksim_get_diag out[25])
+uint64_t batch_variant_reach();
 void launch_lazy_top(const LazyBatch& z, hipStream_t stream);   // the first launch alone (ksim_time_eval)
 // replicated handles: the first launch with the replica's record (xsend), then,
 // after the records' all-gather into a.s.xrecv, the global merge + chain + pairs
@@ -271,11 +273,16 @@ struct ResetList {
   uint32_t* dst[kMax];
   const uint32_t* src[kMax];
   size_t words[kMax];
-  void add(void* d, const void* s, size_t bytes) {
+  // Takes the entry when k_reset_copy can (a slot left, whole words, both
+  // pointers 16-byte aligned: it moves uint4 words); false: the caller copies
+  // it itself.
+  [[nodiscard]] bool add(void* d, const void* s, size_t bytes) {
+    if (n >= kMax || bytes % 4 != 0 || ((uintptr_t)d & 15) != 0 || ((uintptr_t)s & 15) != 0) return false;
     dst[n] = (uint32_t*)d;
     src[n] = (const uint32_t*)s;
     words[n] = bytes / 4;
     n++;
+    return true;
   }
 };
 void launch_reset_copy(const ResetList& L, hipStream_t stream);

@@ -538,7 +538,7 @@ bool stab_signature(const ksim_pod_set* ps, const ksim_pod& q, std::string& s) {
 
 // The "ab" flavor: no table (the keys evaluate the static plugins per node).
 bool stab_enabled() {
-  constexpr bool off = kAbForms;
+  constexpr bool off = ab(kAbStab);
   return !off;
 }
 
@@ -658,7 +658,7 @@ int pod_batchable(const ksim_handle* h, const ksim_pod& p, bool* norm_varies = n
 // maxima over the window's kept nodes), without scalar requests, on an
 // unsharded handle (the "ab" flavor: the per-pod path).
 bool pod_on_batch(const ksim_handle* h, int32_t i) {
-  constexpr bool adapt_norm = !kAbForms;
+  constexpr bool adapt_norm = !ab(kAbAdaptNorm);
   const uint8_t b = h->batchable[i];
   if (b != 2 && b != 3) return b != 0;
   if (h->replicated) return b == 3 && !adapt_mode(h);   // class 3: replicated topology batches (shard_run_tbatch)
@@ -675,7 +675,7 @@ bool pod_on_batch(const ksim_handle* h, int32_t i) {
 // PreFilterResult node list, totals inside the batch key's 20 bits, and a
 // cluster of at most kTbMaxBlocks node blocks.  The "ab" flavor: per-pod path.
 bool tbatch_admit(const ksim_handle* h, const ksim_pod& p, const PodPlan& pl, bool hard_small, bool soft_le1) {
-  constexpr bool off = kAbForms;
+  constexpr bool off = ab(kAbTbatch);
   if (off || p.use_count <= 0) return false;
   if (h->dc.n > kTbMaxBlocks * 256) return false;
   if (p.flags & KSIM_POD_NODE_NAMES) return false;
@@ -846,7 +846,7 @@ int run_tbatch(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
 // ---- deferred-commit FAST batches (ksim_internal.h, ksim_batch.hip) ----------
 // The "ab" flavor: the three-launch batches (parity of both forms).
 bool lazy_enabled() {
-  constexpr bool off = kAbForms;
+  constexpr bool off = ab(kAbLazy);
   return !off;
 }
 
@@ -1211,7 +1211,7 @@ int shard_batch_lazy(const std::vector<ksim_handle*>& hs, hipStream_t stream, in
 
 hipGraphExec_t shard_lazy_graph(const std::vector<ksim_handle*>& hs) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || kAbForms) return nullptr;
+  if (h0->sg_off || ab(kAbShardGraph)) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {
@@ -1463,7 +1463,7 @@ int shard_cycle(const std::vector<ksim_handle*>& hs, int32_t pod, hipStream_t st
 // capture is off or fails (the caller runs the cycles eagerly).
 hipGraphExec_t shard_graph(const std::vector<ksim_handle*>& hs, bool topo, int64_t xdom, int64_t xreg) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || kAbForms) return nullptr;
+  if (h0->sg_off || ab(kAbShardGraph)) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {                     // another group, or some handle dropped its graphs
@@ -1501,7 +1501,7 @@ int shard_batch_adapt(const std::vector<ksim_handle*>& hs, hipStream_t stream, b
 
 hipGraphExec_t shard_batch_graph(const std::vector<ksim_handle*>& hs, bool fast, bool adapt) {
   ksim_handle* h0 = hs[0];
-  if (h0->sg_off || kAbForms) return nullptr;
+  if (h0->sg_off || ab(kAbShardGraph)) return nullptr;
   std::vector<std::pair<const ksim_handle*, int64_t>> sig;
   for (auto* h : hs) sig.emplace_back(h, h->graph_gen);
   if (sig != h0->sg_sig) {
@@ -3377,7 +3377,7 @@ static void build_ptab(const ksim_handle* h, const ksim_pod_set* ps, std::vector
   R.pod.assign((size_t)ps->n_pods, 0);
   R.mask.assign((size_t)ps->n_pods, 0);
   // replicas (RCCL ones included) hold every node: their tables are whole
-  if ((is_sharded(h) && !h->replicated) || kAbForms) return;   // A/B form: per-cycle PreFilter sums
+  if ((is_sharded(h) && !h->replicated) || ab(kAbPtab)) return;   // A/B form: per-cycle PreFilter sums
   std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> index;
   for (int32_t i = 0; i < ps->n_pods; i++) {
     const ksim_pod& p = ps->pods[i];

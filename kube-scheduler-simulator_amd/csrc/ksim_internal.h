@@ -9,13 +9,21 @@ namespace ksim {
 // A/B forms of the same runs, chosen at compile time (csrc/Makefile "ab":
 // libksim_engine_ab.so, every alternative form on; tests/test_gpu_ab_switches.py
 // runs it against the oracle).  The product library has none of them.
+// KSIM_AB_FORMS is a bitmask of the alternative forms (csrc/Makefile "ab":
+// 63, every one on; "abforms": one form each, checked against the product's
+// other forms):
+constexpr unsigned kAbStab = 1;      // per-node static plugins (no static-class table)
+constexpr unsigned kAbLazy = 2;      // three-launch batches (commit as its own launch)
+constexpr unsigned kAbAdaptNorm = 4; // ADAPT normalized-score pods on the per-pod path
+constexpr unsigned kAbTbatch = 8;    // topology pods on the per-pod path
+constexpr unsigned kAbShardGraph = 16;   // eager shard cycles (no shard-group graphs)
+constexpr unsigned kAbPtab = 32;     // per-cycle PreFilter domain sums (no persistent tables)
 #ifdef KSIM_AB_FORMS
-constexpr bool kAbForms = true;   // per-node static plugins (no static-class table), ADAPT normalized-score
-                                  // pods per pod, topology pods per pod, three-launch batches, eager
-                                  // shard cycles, per-cycle PreFilter domain sums
+constexpr unsigned kAbMask = KSIM_AB_FORMS;
 #else
-constexpr bool kAbForms = false;
+constexpr unsigned kAbMask = 0;
 #endif
+constexpr bool ab(unsigned form) { return (kAbMask & form) != 0; }
 
 
 // Batch path geometry.

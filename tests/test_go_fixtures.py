@@ -1,5 +1,13 @@
 """Go-harness fixtures (golden vectors item 4; tests/golden/go/).
 
+WHAT THESE PIN: every recorded cycle in tests/golden/go/*.json.gz is an output
+of oracle/objref.py, the builder's own object-level restatement
+(tools/make_go_fixtures.py), not of the reference's Go plugins.  They are
+objref REGRESSION PINS: they hold the C oracle, the encoders and the engine to
+objref's answers.  No case counts as parity with upstream until
+oracle/go/main.go has written its <case>.go.json.gz (test_go_harness_output),
+which needs Go and the k8s.io/kubernetes v1.26.2 module, absent here.
+
 Each fixture is a scheduling run as Kubernetes v1 documents plus the cycles the
 object-level restatement records for it.  Here, on the CPU:
 

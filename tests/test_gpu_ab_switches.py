@@ -52,11 +52,15 @@ print("ok")
 '''
 
 
-def test_ab_forms_vs_oracle():
-    lib = os.path.join(ROOT, "kube-scheduler-simulator_amd", "ksim", "libksim_engine_ab.so")
-    assert os.path.exists(lib), "build the ab flavor: make -C kube-scheduler-simulator_amd/csrc ab"
+@pytest.mark.parametrize("flavor", ["ab", "ab1", "ab2"])
+def test_ab_forms_vs_oracle(flavor):
+    """ab: every alternative form at once; ab1: only the static-class table
+    off (deferred commit kept); ab2: only the three-launch batches (the table
+    kept) -- each form alone against the product's others."""
+    lib = os.path.join(ROOT, "kube-scheduler-simulator_amd", "ksim", f"libksim_engine_{flavor}.so")
+    assert os.path.exists(lib), "build the ab flavors: make -C kube-scheduler-simulator_amd/csrc ab abforms"
     env = dict(os.environ)
-    env["KSIM_LIB_VARIANT"] = "ab"
+    env["KSIM_LIB_VARIANT"] = flavor
     env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "kube-scheduler-simulator_amd"),
                                          env.get("PYTHONPATH", "")])
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, cwd=ROOT, capture_output=True, text=True,

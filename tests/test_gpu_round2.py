@@ -376,9 +376,10 @@ GO = sorted(p for p in __import__("glob").glob(os.path.join(os.path.dirname(__fi
 
 @pytest.mark.parametrize("path", GO, ids=[os.path.basename(p).split(".")[0] for p in GO])
 def test_go_fixtures_through_engine(path):
-    """The recorded cycles of each fixture (which a Go run would pin) reproduced
-    by the device: filter outcomes and messages, scores, totals, placement,
-    nextStartNodeIndex."""
+    """The recorded cycles of each fixture reproduced by the device: filter
+    outcomes and messages, scores, totals, placement, nextStartNodeIndex.  The
+    recorded cycles are oracle/objref.py's (objref regression pins, see
+    tests/test_go_fixtures.py), not the Go plugins'."""
     import gofixture
     from ksim.wrapped import filter_message
     with gzip.open(path, "rb") as f:

@@ -73,6 +73,16 @@ def test_config1_pods_at_keep_threshold(n_nodes, shape):
     _check(cluster, pods, profile.compile_profile(_sp(100, shape)), f"config1 {n_nodes} {shape}")
 
 
+@pytest.mark.parametrize("n_nodes", [3000, 8193])
+def test_generic_keys(n_nodes):
+    """A scoring strategy over ephemeral-storage as well as cpu and memory:
+    neither the FAST nor the static-class keys, the generic key (512 threads)."""
+    cluster, pods = gen.config1(n_nodes=n_nodes, n_pods=500)
+    sp = _sp(100, "default")
+    sp.fit = profile.FitArgs(resources=[("cpu", 1), ("memory", 1), ("ephemeral-storage", 1)])
+    _check(cluster, pods, profile.compile_profile(sp), f"generic keys {n_nodes}")
+
+
 def _shards(cluster, pods, prof, world, replicated):
     engines = []
     for base, cnt in partition(cluster.n_nodes, world):

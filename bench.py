@@ -615,7 +615,8 @@ def _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots, ext, 
     class DFns(ctypes.Structure):
         _fields_ = [(nm, ctypes.c_void_p) for nm in ("encoder_bind", "encoder_unbind", "encoder_update_nodes",
                                                       "encoder_old_pos", "encoder_cluster", "encoder_info",
-                                                      "upsert_nodes", "forget")]
+                                                      "upsert_nodes", "forget", "encoder_changed_rows",
+                                                      "update_node_rows")]
 
     class Deltas(ctypes.Structure):
         _fields_ = [("ext", ctypes.c_void_p), ("ext_ns", ctypes.c_void_p), ("ext_name", ctypes.c_void_p),
@@ -626,7 +627,7 @@ def _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots, ext, 
     class Res(ctypes.Structure):
         _fields_ = [("sec", ctypes.c_double * 7), ("total", ctypes.c_double)] + \
                    [(nm, ctypes.c_int64) for nm in ("bound", "cycles", "pod_adds", "pod_deletes", "node_updates",
-                                                     "resends")]
+                                                     "resends", "node_rows_in_place")]
 
     DRV.fwdrive_run_deltas.restype = ctypes.c_int
     DRV.fwdrive_run_deltas.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
@@ -658,7 +659,8 @@ def _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots, ext, 
                "ksim_assume")])
     g = DFns(*[ctypes.cast(getattr(EL, nm), ctypes.c_void_p).value for nm in
                ("ksim_encoder_bind", "ksim_encoder_unbind", "ksim_encoder_update_nodes", "ksim_encoder_old_pos",
-                "ksim_encoder_cluster", "ksim_encoder_get_info", "ksim_upsert_nodes", "ksim_forget")])
+                "ksim_encoder_cluster", "ksim_encoder_get_info", "ksim_upsert_nodes", "ksim_forget",
+                "ksim_encoder_changed_rows", "ksim_update_node_rows")])
     a_ext = (ctypes.c_void_p * len(ext_pools))(*[ctypes.addressof(pl.c) for pl in ext_pools])
     a_ns = (ctypes.c_char_p * len(ext_ns))(*ext_ns)
     a_name = (ctypes.c_char_p * len(ext_name))(*ext_name)
@@ -681,7 +683,8 @@ def _fw_run_deltas(DRV, EL, enc, cluster, prof, pools, opts, N, K, nslots, ext, 
     return {"us_per_cycle": res.total / n_pods * 1e6, "cycles": int(res.cycles), "bound": int(res.bound),
             "us_per_call": {nm: res.sec[q] / n_pods * 1e6 for q, nm in enumerate(names)},
             "events": {"pod_adds": int(res.pod_adds), "pod_deletes": int(res.pod_deletes),
-                       "node_updates": int(res.node_updates), "resends": int(res.resends)},
+                       "node_updates": int(res.node_updates), "node_rows_in_place": int(res.node_rows_in_place),
+                       "resends": int(res.resends)},
             "full_encodes_after_first": 0,
             "answered": {k: d[k] for k in ("fw_score_host", "fw_score_device", "fw_normalize_cached",
                                            "fw_normalize_device")}}

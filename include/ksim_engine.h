@@ -489,6 +489,18 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* nodes, const ksim_v
 /* RemoveNode of the node at position `pos` (later nodes move down by one),
  * from the device-resident snapshot alone. */
 int ksim_remove_node(ksim_handle* h, int32_t pos);
+/* UpdateNode in place (ABI 11): the static columns of the nodes at positions
+ * rows[0..n_rows) -- allocatable (and its reciprocals), scalar allocatable,
+ * flags, taints, label value ids, the NetworkBandwidth limit -- taken from
+ * `nodes` at those positions.  `nodes` / `vocab` must have the handle's node
+ * count, scalar columns, label columns and count classes and the same taint
+ * and label-value vocabulary sizes; anything else is KSIM_E_INVALID (send the
+ * table with ksim_upsert_nodes).  Dynamic columns, count classes and
+ * nextStartNodeIndex are kept; loaded pods are dropped (their filter plans
+ * read the cluster's taint and unschedulable facts).  The encoder's
+ * ksim_encoder_changed_rows names the rows when a delta moved no node. */
+int ksim_update_node_rows(ksim_handle* h, const ksim_node_table* nodes, const ksim_vocab* vocab, const int32_t* rows,
+                          int32_t n_rows);
 /* Read back the dynamic node state (Requested/NonZeroRequested/len(Pods)). NULL skips a field. */
 int ksim_get_node_state(ksim_handle* h, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph,
                         int64_t* nz_cpu, int64_t* nz_mem, int32_t* num_pods);
@@ -1095,6 +1107,8 @@ const char* ksim_encoder_string(const ksim_encoder* e, int32_t what, int32_t i, 
  * class ids are kept; the pod set is cleared (its positions are stale).
  * ksim_encoder_old_pos: old_pos[i] = the previous position of node i of the
  * new snapshot, -1 for an added node (KSIM_E_INVALID before any delta).
+ * Updates that move no node and add no vocabulary are applied in place
+ * (ksim_encoder_changed_rows, then ksim_update_node_rows on the engine).
  * ksim_encoder_bind: pod `pod_index` of the current pod set (the last
  * ksim_encode_pods) is bound at node position `node`, under its
  * namespace / name; binding a pod already bound is KSIM_E_INVALID.
@@ -1104,6 +1118,13 @@ const char* ksim_encoder_string(const ksim_encoder* e, int32_t what, int32_t i, 
 int ksim_encoder_update_nodes(ksim_encoder* e, const ksim_k8s_pool* pool, const int32_t* removed,
                               int32_t n_removed);
 int ksim_encoder_old_pos(const ksim_encoder* e, int32_t* old_pos);
+/* The last ksim_encoder_update_nodes, when it only updated nodes in place
+ * (no node added, removed or moved to another zone; no new scalar column,
+ * taint or label value; images unchanged): the number of updated positions,
+ * written to rows[0..min(count, cap)); the table then differs from the
+ * previous one only in those rows' static columns (ksim_update_node_rows).
+ * -1 when the delta needs ksim_upsert_nodes with ksim_encoder_old_pos. */
+int ksim_encoder_changed_rows(const ksim_encoder* e, int32_t* rows, int32_t cap);
 int ksim_encoder_bind(ksim_encoder* e, int32_t pod_index, int32_t node);
 int ksim_encoder_unbind(ksim_encoder* e, const char* namespace_, const char* name, int32_t* node);
 int ksim_encoder_bound_node(const ksim_encoder* e, const char* namespace_, const char* name, int32_t* node);

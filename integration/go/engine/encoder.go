@@ -869,13 +869,19 @@ func (n *NativeEncoder) applyNodes(e *Engine, upd []*v1.Node, gone []string) err
 		return err
 	}
 	n.readNames()
-	oldPos := make([]int32, len(n.names)+1)
-	if err := n.errOf(C.ksim_encoder_old_pos(n.enc, (*C.int32_t)(unsafe.Pointer(&oldPos[0])))); err != nil {
-		return err
-	}
 	var t C.ksim_node_table
 	var v C.ksim_vocab
 	if err := n.errOf(C.ksim_encoder_cluster(n.enc, &t, &v)); err != nil {
+		return err
+	}
+	n.Stats.NodeDeltas++
+	// in place (no node moved, no new vocabulary): the updated rows only
+	rows := make([]int32, len(upd)+1)
+	if k := int(C.ksim_encoder_changed_rows(n.enc, (*C.int32_t)(unsafe.Pointer(&rows[0])), C.int32_t(len(rows)))); k >= 0 {
+		return e.UpdateNodeRows(&t, &v, rows[:k])
+	}
+	oldPos := make([]int32, len(n.names)+1)
+	if err := n.errOf(C.ksim_encoder_old_pos(n.enc, (*C.int32_t)(unsafe.Pointer(&oldPos[0])))); err != nil {
 		return err
 	}
 	if err := e.UpsertNodes(&t, &v, oldPos[:len(n.names)]); err != nil {
@@ -883,7 +889,6 @@ func (n *NativeEncoder) applyNodes(e *Engine, upd []*v1.Node, gone []string) err
 	}
 	n.noteLayout()
 	n.tableOld = true // the engine dropped the bound-pod table (positions moved)
-	n.Stats.NodeDeltas++
 	return nil
 }
 

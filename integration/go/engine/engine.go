@@ -95,6 +95,17 @@ func (e *Engine) UpsertNodes(t *C.ksim_node_table, v *C.ksim_vocab, oldPos []int
 	return e.locked(func() C.int { return C.ksim_upsert_nodes(e.h, t, v, p) })
 }
 
+// UpdateNodeRows applies an in-place UpdateNode (ABI 11): the static columns
+// of rows from t, whose layout and vocabulary are the handle's (the encoder's
+// ksim_encoder_changed_rows says when a delta qualifies).
+func (e *Engine) UpdateNodeRows(t *C.ksim_node_table, v *C.ksim_vocab, rows []int32) error {
+	var p *C.int32_t
+	if len(rows) > 0 {
+		p = (*C.int32_t)(unsafe.Pointer(&rows[0]))
+	}
+	return e.locked(func() C.int { return C.ksim_update_node_rows(e.h, t, v, p, C.int32_t(len(rows))) })
+}
+
 // RemoveNode removes the node at position pos (later nodes move down by one).
 func (e *Engine) RemoveNode(pos int) error {
 	return e.locked(func() C.int { return C.ksim_remove_node(e.h, C.int32_t(pos)) })

@@ -1222,6 +1222,8 @@ struct ksim_encoder {
   std::unordered_set<string> dup_keys;      // bound twice in one snapshot: not unbindable
   vector<std::pair<string, Member>> queue_members;
   vector<int32_t> old_pos;
+  bool in_place = false;                    // the last node delta only updated rows (ksim_encoder_changed_rows)
+  vector<int32_t> changed;
   // the pod set
   vector<ksim_pod> pods;
   vector<ksim_label_expr> exprs;
@@ -1573,6 +1575,7 @@ void encode_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_
   e->dup_keys.clear();
   e->queue_members.clear();
   e->old_pos.clear();
+  e->in_place = false;
   Cluster& c = e->c;
   e->req_memo.clear();
   if (o.nb_node_limit >= 0) c.nb.node_limit = string(pv.str(o.nb_node_limit));
@@ -2215,12 +2218,98 @@ void encode_pods(ksim_encoder* e, const ksim_k8s_pool& pool, const ksim_encode_p
 // them, ksim_upsert_nodes); an added node starts empty; a removed node's bound
 // pods leave the snapshot.  ImageLocality's rows are recomputed (they read
 // every node's images and the node count).
+// Node updates that move no node and need no new vocabulary (same zone, same
+// images, scalar resources, taints and label values the snapshot already
+// has): the rows' static columns in place.  False (nothing changed) otherwise.
+bool update_rows_in_place(ksim_encoder* e, const vector<Node>& upd) {
+  Cluster& c = e->c;
+  std::unordered_map<string, size_t> at;
+  for (size_t i = 0; i < e->nodes.size(); i++) at.emplace(e->nodes[i].name, i);
+  std::unordered_map<string, int> tid;
+  for (size_t t = 1; t < c.taint_vocab.size(); t++) {
+    const Taint& x = c.taint_vocab[t];
+    tid.emplace(x.key + '\x1f' + x.value + '\x1f' + x.effect, (int)t);
+  }
+  std::unordered_set<string> seen;
+  for (const Node& nd : upd) {
+    auto it = at.find(nd.name);
+    if (it == at.end() || !seen.insert(nd.name).second) return false;
+    const Node& old = e->nodes[it->second];
+    if (zone_key(old.labels) != zone_key(nd.labels) || old.images != nd.images) return false;
+    if ((int)nd.taints.size() > KSIM_MAX_NODE_TAINTS) return false;
+    for (const auto& kv : nd.alloc)
+      if (!is_native_resource(kv.first) &&
+          std::find(c.scalar_names.begin(), c.scalar_names.end(), kv.first) == c.scalar_names.end())
+        return false;
+    for (const Taint& x : nd.taints)
+      if (!tid.count(x.key + '\x1f' + x.value + '\x1f' + x.effect)) return false;
+    for (size_t k = 0; k < c.label_keys.size(); k++) {
+      const string* v = lookup(nd.labels, c.label_keys[k]);
+      if (v && !c.value_index[k].count(*v)) return false;
+    }
+  }
+  const int32_t N = c.n;
+  Quantities& qs = e->qs;
+  e->changed.clear();
+  for (const Node& nd : upd) {
+    const int32_t pos = c.pos_of.at(nd.name);
+    c.alloc_cpu[pos] = qs.res(nd.alloc, "cpu");
+    c.alloc_mem[pos] = qs.res(nd.alloc, "memory");
+    c.alloc_eph[pos] = qs.res(nd.alloc, "ephemeral-storage");
+    const int64_t pods = qs.res(nd.alloc, "pods");
+    if (pods < INT32_MIN || pods > INT32_MAX) fail("node " + nd.name + ": allocatable pods out of the int32 range");
+    c.alloc_pods[pos] = (int32_t)pods;
+    for (int32_t k = 0; k < c.n_scalar; k++) c.alloc_scalar[(size_t)k * N + pos] = qs.res(nd.alloc, c.scalar_names[k]);
+    c.flags[pos] = nd.unschedulable ? KSIM_NODE_UNSCHEDULABLE : 0;
+    c.nb_limit[pos] = 0;
+    if (const string* lim = lookup(nd.annotations, c.nb.node_limit)) {
+      int64_t q;
+      if (netbw_milli(*lim, q)) {
+        c.flags[pos] |= KSIM_NODE_NB_LIMIT;
+        c.nb_limit[pos] = q;
+      } else {
+        c.flags[pos] |= KSIM_NODE_NB_LIMIT | KSIM_NODE_NB_LIMIT_BAD;
+      }
+    }
+    for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) c.taints[(size_t)k * N + pos] = 0;
+    for (size_t k = 0; k < nd.taints.size(); k++) {
+      const Taint& x = nd.taints[k];
+      c.taints[k * N + pos] = (uint16_t)tid.at(x.key + '\x1f' + x.value + '\x1f' + x.effect);
+    }
+    for (size_t k = 0; k < c.label_keys.size(); k++) {
+      const string* v = lookup(nd.labels, c.label_keys[k]);
+      c.labels[k * N + pos] = v ? (uint32_t)c.value_index[k].at(*v) : 0u;
+    }
+    c.node_labels[pos] = nd.labels;
+    e->nodes[at.at(nd.name)] = nd;
+    e->changed.push_back(pos);
+  }
+  e->old_pos.resize(N);
+  for (int32_t p = 0; p < N; p++) e->old_pos[p] = p;
+  e->in_place = true;
+  e->pods.clear();
+  e->exprs.clear();
+  e->terms.clear();
+  e->uses.clear();
+  e->adds.clear();
+  e->nn.clear();
+  e->queue_members.clear();
+  return true;
+}
+
 void update_nodes(ksim_encoder* e, const ksim_k8s_pool& pool, const int32_t* removed, int32_t n_removed) {
   if (!e->has_cluster) fail("ksim_encoder_update_nodes before ksim_encode_nodes");
   if (n_removed < 0 || (n_removed > 0 && !removed)) fail("bad removed-node list");
   PoolView pv(pool);
   Reader rd{pv};
   if (pool.n_nodes < 0 || (pool.n_nodes > 0 && !pool.nodes)) fail("pool: bad node list");
+  e->in_place = false;
+  if (n_removed == 0) {
+    vector<Node> upd;
+    for (int64_t i = 0; i < pool.n_nodes; i++) upd.push_back(rd.node(pool.nodes[i]));
+    read_namespaces(e->topo, pv);
+    if (update_rows_in_place(e, upd)) return;
+  }
   const size_t M = e->nodes.size();
   std::unordered_map<string, size_t> at;     // name -> index in the add order
   for (size_t i = 0; i < M; i++) at.emplace(e->nodes[i].name, i);
@@ -2511,6 +2600,14 @@ int ksim_encoder_old_pos(const ksim_encoder* e, int32_t* old_pos) {
   if ((int32_t)e->old_pos.size() != e->c.n) return KSIM_E_INVALID;   // no node delta since the snapshot
   std::copy(e->old_pos.begin(), e->old_pos.end(), old_pos);
   return KSIM_OK;
+}
+
+int ksim_encoder_changed_rows(const ksim_encoder* e, int32_t* rows, int32_t cap) {
+  if (!e || !e->has_cluster || cap < 0 || (cap > 0 && !rows)) return KSIM_E_INVALID;
+  if (!e->in_place) return -1;
+  const int32_t n = (int32_t)e->changed.size();
+  for (int32_t i = 0; i < n && i < cap; i++) rows[i] = e->changed[i];
+  return n;
 }
 
 int ksim_encoder_bind(ksim_encoder* e, int32_t pod_index, int32_t node) {

@@ -2287,6 +2287,122 @@ int ksim_upsert_nodes(ksim_handle* h, const ksim_node_table* t, const ksim_vocab
 // DeleteNode: the node at `pos` leaves; later positions move down by one.  The
 // table handed to ksim_upsert_nodes is the current snapshot without it, so the
 // replay keeps every other node's state.
+static int pin_reserve(ksim_handle* h, size_t bytes);
+
+// UpdateNode in place: the changed rows' static columns through one launch
+// from the pinned staging; the cluster facts the filter plans read (hard
+// taints, unschedulable nodes, narrow allocatable, unique / total label
+// columns) recomputed from the whole table on the host.
+int ksim_update_node_rows(ksim_handle* h, const ksim_node_table* t, const ksim_vocab* v, const int32_t* rows,
+                          int32_t n_rows) {
+  if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
+  if (!h || !t || !v || n_rows < 0 || (n_rows > 0 && !rows)) return KSIM_E_INVALID;
+  if (!h->has_cluster) return set_err(h, KSIM_E_INVALID, "ksim_update_node_rows before ksim_set_cluster");
+  if (h->shard_total || h->world > 1) return set_err(h, KSIM_E_UNSUPPORTED, "ksim_update_node_rows on a shard handle");
+  const DevCluster& c = h->dc;
+  const int32_t n = c.n;
+  if (t->n_nodes != n || t->n_scalar != c.n_scalar || t->n_label_cols != c.n_label_cols ||
+      t->n_classes != c.n_classes || v->n_taints != c.n_taints || v->n_label_values != c.n_label_values)
+    return set_err(h, KSIM_E_INVALID, "ksim_update_node_rows: the table's layout or vocabulary differs (ksim_upsert_nodes)");
+  if (n > 0 && (!t->alloc_cpu || !t->alloc_mem || !t->alloc_eph || !t->alloc_pods || !t->flags || !t->taints ||
+                (t->n_label_cols > 0 && !t->labels) || (t->n_scalar > 0 && !t->alloc_scalar)))
+    return set_err(h, KSIM_E_INVALID, "null node column");
+  for (int k = 0; k < c.n_label_cols; k++)
+    if (!v->label_col_offset || (k + 1 < c.n_label_cols ? v->label_col_offset[k + 1] : v->n_label_values) -
+                                        v->label_col_offset[k] != h->col_nvals[k])
+      return set_err(h, KSIM_E_INVALID, "ksim_update_node_rows: a label column's vocabulary changed (ksim_upsert_nodes)");
+  if (!v->taint_effect || !std::equal(h->taint_effect.begin(), h->taint_effect.end(), v->taint_effect))
+    return set_err(h, KSIM_E_INVALID, "ksim_update_node_rows: the taint vocabulary changed (ksim_upsert_nodes)");
+  const size_t N = (size_t)n;
+  std::vector<uint8_t> seen_row((size_t)n, 0);
+  for (int32_t q = 0; q < n_rows; q++) {
+    const int32_t r = rows[q];
+    if (r < 0 || r >= n || seen_row[r]++) return set_err(h, KSIM_E_INVALID, "rows: out of range or repeated");
+    for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++)
+      if (t->taints[(size_t)k * N + r] >= v->n_taints) return set_err(h, KSIM_E_INVALID, "taint id out of vocabulary");
+    for (int k = 0; k < c.n_label_cols; k++)
+      if (t->labels[(size_t)k * N + r] >= (uint32_t)h->col_nvals[k])
+        return set_err(h, KSIM_E_INVALID, "label value id out of its column's vocabulary");
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));     // the pinned staging is free
+  h->up_pending = false;
+  const int32_t words = 1 + 8 + KSIM_MAX_NODE_TAINTS + c.n_scalar + c.n_label_cols;
+  int rc;
+  if ((rc = pin_reserve(h, 8 * (size_t)words * (size_t)std::max(n_rows, 1)))) return rc;
+  int64_t* rec = (int64_t*)h->pin;
+  for (int32_t q = 0; q < n_rows; q++) {
+    const int32_t r = rows[q];
+    int64_t* w = rec + (size_t)q * words;
+    const double ic = t->alloc_cpu[r] ? 1.0 / (double)t->alloc_cpu[r] : 0.0;   // as ksim_set_cluster
+    const double im = t->alloc_mem[r] ? 1.0 / (double)t->alloc_mem[r] : 0.0;
+    w[0] = r;
+    w[1] = t->alloc_cpu[r];
+    w[2] = t->alloc_mem[r];
+    w[3] = t->alloc_eph[r];
+    w[4] = t->alloc_pods[r];
+    w[5] = t->flags[r];
+    w[6] = t->nb_limit ? t->nb_limit[r] : 0;
+    std::memcpy(&w[7], &ic, 8);
+    std::memcpy(&w[8], &im, 8);
+    for (int k = 0; k < KSIM_MAX_NODE_TAINTS; k++) w[9 + k] = t->taints[(size_t)k * N + r];
+    for (int k = 0; k < c.n_scalar; k++) w[9 + KSIM_MAX_NODE_TAINTS + k] = t->alloc_scalar[(size_t)k * N + r];
+    for (int k = 0; k < c.n_label_cols; k++)
+      w[9 + KSIM_MAX_NODE_TAINTS + c.n_scalar + k] = t->labels[(size_t)k * N + r];
+  }
+  launch_node_rows(c, (const int64_t*)h->pin_d, n_rows, words, h->stream);
+  HIPCHK(h, hipGetLastError());
+  // the cluster facts, from the whole table (as ksim_set_cluster)
+  {
+    std::vector<uint8_t> seen((size_t)v->n_taints, 0);
+    for (size_t i = 0; i < N * KSIM_MAX_NODE_TAINTS; i++) seen[t->taints[i]] = 1;
+    h->hard_taints.clear();
+    for (int id = 1; id < v->n_taints; id++)
+      if (seen[id] && (h->taint_effect[id] == KSIM_EFFECT_NO_SCHEDULE || h->taint_effect[id] == KSIM_EFFECT_NO_EXECUTE))
+        h->hard_taints.push_back((uint16_t)id);
+    h->any_unschedulable = false;
+    for (int32_t i = 0; i < n; i++) h->any_unschedulable = h->any_unschedulable || (t->flags[i] & KSIM_NODE_UNSCHEDULABLE);
+    uint32_t cf = h->any_unschedulable ? kClusterUnschedulable : 0u;
+    if (!h->hard_taints.empty()) cf |= kClusterHardTaints;
+    for (size_t i = 0; i < N * KSIM_MAX_NODE_TAINTS; i++)
+      if (t->taints[i] && h->taint_effect[t->taints[i]] == KSIM_EFFECT_PREFER_NO_SCHEDULE) cf |= kClusterPreferTaints;
+    h->alloc_narrow = true;
+    for (int32_t i = 0; i < n; i++)
+      h->alloc_narrow = h->alloc_narrow && t->alloc_cpu[i] >= 0 && t->alloc_cpu[i] < (1ll << 46) &&
+                        t->alloc_mem[i] >= 0 && t->alloc_mem[i] < (1ll << 46);
+    if (h->alloc_narrow) cf |= kClusterNarrow;
+    h->dc.cflags = cf;
+    std::vector<uint8_t> uniq((size_t)c.n_label_cols, 0);
+    std::vector<uint8_t> vs;
+    for (int k = 0; k < c.n_label_cols; k++) {
+      vs.assign((size_t)h->col_nvals[k], 0);
+      bool u = true;
+      for (int32_t i = 0; i < n && u; i++) {
+        const uint32_t x = t->labels[(size_t)k * N + i];
+        if (x && vs[x]++) u = false;
+      }
+      uniq[k] = u;
+      h->col_total[k] = 1;
+      for (int32_t i = 0; i < n && h->col_total[k]; i++)
+        if (!t->labels[(size_t)k * N + i]) h->col_total[k] = 0;
+    }
+    if (uniq != h->col_unique && c.n_label_cols > 0) {
+      HIPCHK(h, hcopy(h, const_cast<uint8_t*>(c.col_unique), uniq.data(), uniq.size(), hipMemcpyHostToDevice));
+      h->col_unique = uniq;
+    }
+  }
+  // what was compiled against the old rows: graphs, the static-class table, loaded pods
+  drop_graphs(h);
+  h->stab_dirty = true;
+  free_bufs(h->pod_bufs);
+  h->pod_buf_bytes.clear();
+  h->dp = DevPods{};
+  h->batchable.clear();
+  h->topo.clear();
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return KSIM_OK;
+}
+
 int ksim_remove_node(ksim_handle* h, int32_t pos) {
   if (const int prc = flush_pend_bind(h)) return prc;   // a queued Reserve lands first
   if (!h || !h->has_cluster) return set_err(h, KSIM_E_INVALID, "cluster not set");

@@ -208,6 +208,8 @@ struct CopyList {
   DevPods aP;
 };
 void launch_copy_list(const CopyList& l, int count, hipStream_t stream);
+// ksim_update_node_rows: packed static-column records of n rows (words int64 each)
+void launch_node_rows(const DevCluster& c, const int64_t* rec, int32_t n, int32_t words, hipStream_t stream);
 void launch_fw_gather(const DevEvalOut& o, const int32_t* nodes, int32_t n, int32_t N, int32_t S, int64_t* comp,
                       const WinState* win, void* win_out, hipStream_t stream);
 void launch_fw_begin(DevState* st, WinState* win, int32_t first, int32_t end, hipStream_t stream);

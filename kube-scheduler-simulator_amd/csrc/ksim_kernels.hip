@@ -1590,6 +1590,36 @@ __global__ __launch_bounds__(256) void k_copy_list(CopyList l) {
   if (blockIdx.x == 0 && threadIdx.x < (n & 15u)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
 }
 
+// ksim_update_node_rows: the static columns of updated nodes, one block per
+// row, from packed records in mapped pinned memory: [pos, alloc cpu / mem /
+// eph / pods, flags, nb_limit, inv_cpu, inv_mem, taints x8, alloc_scalar x S,
+// labels x L] as 64-bit words.
+__global__ __launch_bounds__(64) void k_node_rows(DevCluster c, const int64_t* __restrict__ rec, int32_t words) {
+  const int64_t* r = rec + (size_t)blockIdx.x * words;
+  const int32_t pos = (int32_t)r[0];
+  const size_t N = (size_t)c.n;
+  for (int32_t f = threadIdx.x; f < words - 1; f += 64) {
+    const int64_t x = r[1 + f];
+    if (f == 0) const_cast<int64_t*>(c.alloc_cpu)[pos] = x;
+    else if (f == 1) const_cast<int64_t*>(c.alloc_mem)[pos] = x;
+    else if (f == 2) const_cast<int64_t*>(c.alloc_eph)[pos] = x;
+    else if (f == 3) const_cast<int32_t*>(c.alloc_pods)[pos] = (int32_t)x;
+    else if (f == 4) const_cast<uint32_t*>(c.flags)[pos] = (uint32_t)x;
+    else if (f == 5) const_cast<int64_t*>(c.nb_limit)[pos] = x;
+    else if (f == 6) const_cast<int64_t*>(reinterpret_cast<const int64_t*>(c.inv_cpu))[pos] = x;
+    else if (f == 7) const_cast<int64_t*>(reinterpret_cast<const int64_t*>(c.inv_mem))[pos] = x;
+    else if (f < 8 + KSIM_MAX_NODE_TAINTS) const_cast<uint16_t*>(c.taints)[(size_t)(f - 8) * N + pos] = (uint16_t)x;
+    else if (f < 8 + KSIM_MAX_NODE_TAINTS + c.n_scalar)
+      const_cast<int64_t*>(c.alloc_scalar)[(size_t)(f - 8 - KSIM_MAX_NODE_TAINTS) * N + pos] = x;
+    else
+      const_cast<uint32_t*>(c.labels)[(size_t)(f - 8 - KSIM_MAX_NODE_TAINTS - c.n_scalar) * N + pos] = (uint32_t)x;
+  }
+}
+
+void launch_node_rows(const DevCluster& c, const int64_t* rec, int32_t n, int32_t words, hipStream_t stream) {
+  if (n > 0) k_node_rows<<<n, 64, 0, stream>>>(c, rec, words);
+}
+
 void launch_copy_list(const CopyList& l, int count, hipStream_t stream) {
   uint32_t mx = 0;
   for (int q = 0; q < count; q++) mx = l.n[q] > mx ? l.n[q] : mx;

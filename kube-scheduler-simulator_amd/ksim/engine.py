@@ -35,7 +35,8 @@ EXPORTS = [
     "ksim_encoder_create", "ksim_encoder_destroy", "ksim_encoder_last_error", "ksim_encode_nodes",
     "ksim_encode_pods", "ksim_encoder_cluster", "ksim_encoder_pods", "ksim_encoder_get_info",
     "ksim_encoder_node_order", "ksim_encoder_string", "ksim_encoder_update_nodes", "ksim_encoder_old_pos",
-    "ksim_encoder_bind", "ksim_encoder_unbind", "ksim_encoder_bound_node",
+    "ksim_encoder_bind", "ksim_encoder_unbind", "ksim_encoder_bound_node", "ksim_encoder_changed_rows",
+    "ksim_update_node_rows",
 ]
 
 
@@ -145,6 +146,8 @@ def _load(path):
     L.ksim_encoder_update_nodes.argtypes = [vp, vp, vp, i32]
     L.ksim_encoder_old_pos.argtypes = [vp, vp]
     L.ksim_encoder_bind.argtypes = [vp, i32, i32]
+    L.ksim_encoder_changed_rows.argtypes = [vp, vp, i32]
+    L.ksim_update_node_rows.argtypes = [vp, vp, vp, vp, i32]
     L.ksim_encoder_unbind.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp]
     L.ksim_encoder_bound_node.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, vp]
     return L
@@ -253,6 +256,17 @@ class Engine:
         self._chk(self.L.ksim_upsert_nodes(self.h, ctypes.byref(nt), ctypes.byref(vo),
                                           op.ctypes.data_as(ctypes.c_void_p)))
         self._track(cluster, nt)
+        self._keep = []
+
+    def update_node_rows(self, cluster, rows):
+        """UpdateNode in place (ksim_update_node_rows): the static columns of
+        ``rows`` from ``cluster`` (same layout and vocabulary as the handle's)."""
+        nt, vo = cluster.node_table(), cluster.vocab()
+        r = np.ascontiguousarray(rows, np.int32)
+        self._chk(self.L.ksim_update_node_rows(self.h, ctypes.byref(nt), ctypes.byref(vo),
+                                               r.ctypes.data_as(ctypes.c_void_p), int(r.size)))
+        self.cluster = cluster
+        self._layout = (cluster.n_label_cols, int(nt.n_classes))
         self._keep = []
 
     def remove_node(self, pos: int):

@@ -8,9 +8,11 @@ it, and each cycle starts from UpdateSnapshot, which copies only what changed.
 The engine's device-resident snapshot follows the same events through the
 encoder's delta calls (include/ksim_engine.h "snapshot deltas", ABI 11):
 
-  node added / updated / removed   ksim_encoder_update_nodes + ksim_upsert_nodes,
-                                   one per cycle start for all queued node events
-                                   (the engine replays its binds on kept nodes);
+  node added / updated / removed   ksim_encoder_update_nodes, then
+                                   ksim_update_node_rows when the delta moved no node
+                                   and added no vocabulary (ksim_encoder_changed_rows),
+                                   else ksim_upsert_nodes (the engine replays its binds
+                                   on kept nodes); one per cycle start;
   bound pod added                  ksim_encode_pods of the pod, the table re-sent
                                    when the compile grew it, ksim_assume,
                                    ksim_encoder_bind;
@@ -70,8 +72,8 @@ class SnapshotSync:
                 self.bound[(p.namespace, p.name)] = (p, p.node_name)
         self.waiting: Dict[Tuple[str, str], Pod] = {}             # bound to a node not yet added
         self.events: List[tuple] = []
-        self.stats = {"full_encodes": 0, "node_deltas": 0, "pod_adds": 0, "pod_deletes": 0, "resends": 0,
-                      "reserves": 0, "unreserves": 0}
+        self.stats = {"full_encodes": 0, "node_deltas": 0, "node_rows_in_place": 0, "pod_adds": 0,
+                      "pod_deletes": 0, "resends": 0, "reserves": 0, "unreserves": 0}
         self._encodes = 0
         self._cycle: Optional[Pod] = None
         self._cycle_set = None
@@ -196,8 +198,12 @@ class SnapshotSync:
 
     def _apply_nodes(self, ev) -> None:
         upserts, removed = self._record_nodes(ev)
-        cluster, old_pos = self.enc.update_nodes(upserts, removed)
-        self.b.upsert_nodes(cluster, old_pos)
+        cluster, old_pos, rows = self.enc.update_nodes(upserts, removed)
+        if rows is not None:                       # in place: the rows' static columns only
+            self.b.update_node_rows(cluster, rows)
+            self.stats["node_rows_in_place"] += 1
+        else:
+            self.b.upsert_nodes(cluster, old_pos)
         self._use(cluster)
         self.stats["node_deltas"] += 1
 

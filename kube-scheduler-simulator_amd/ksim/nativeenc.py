@@ -399,10 +399,12 @@ class NativeEncoder:
         return cl, order
 
     # ---- snapshot deltas (ABI 11) ----------------------------------------------------
-    def update_nodes(self, nodes: Sequence[Node] = (), removed: Sequence[str] = ()) -> Tuple[EncodedCluster, np.ndarray]:
+    def update_nodes(self, nodes: Sequence[Node] = (), removed: Sequence[str] = ()
+                     ) -> Tuple[EncodedCluster, np.ndarray, Optional[np.ndarray]]:
         """ksim_encoder_update_nodes: ``nodes`` added or updated, ``removed``
-        names leave.  Returns the new snapshot (a new EncodedCluster) and
-        old_pos for ksim_upsert_nodes."""
+        names leave.  Returns the new snapshot (a new EncodedCluster), old_pos
+        for ksim_upsert_nodes, and the updated rows when the delta was in place
+        (ksim_encoder_changed_rows: ksim_update_node_rows takes it), else None."""
         pool = Pool()
         for n in nodes:
             pool.node(n)
@@ -417,7 +419,9 @@ class NativeEncoder:
         cl, _ = self._new_cluster()
         old_pos = np.zeros(cl.n_nodes, np.int32)
         self._chk(self.L.ksim_encoder_old_pos(self.h, old_pos.ctypes.data_as(ctypes.c_void_p)))
-        return cl, old_pos
+        rows = np.zeros(max(len(nodes), 1), np.int32)
+        k = self.L.ksim_encoder_changed_rows(self.h, rows.ctypes.data_as(ctypes.c_void_p), rows.size)
+        return cl, old_pos, (rows[:k].copy() if k >= 0 else None)
 
     def bind(self, index: int, node: int) -> None:
         """ksim_encoder_bind: pod ``index`` of the last encode_pods is bound at ``node``."""

@@ -339,6 +339,12 @@ class OracleBackend:
     def upsert_nodes(self, cluster, old_pos):
         self.o.upsert_nodes(cluster, old_pos)
 
+    def update_node_rows(self, cluster, rows):
+        """The oracle has no row update: the table again, every node kept
+        (ksim_oracle_upsert_nodes, the same state)."""
+        import numpy as np
+        self.o.upsert_nodes(cluster, np.arange(cluster.n_nodes, dtype=np.int32))
+
     def node_state(self):
         return self.o.node_state()
 

@@ -36,6 +36,7 @@ def test_incremental_snapshot_matches_full_reencode(seed):
     assert st["full_encodes"] == 1, st              # the first snapshot only
     assert st["node_deltas"] > 5 and st["pod_adds"] > 10 and st["pod_deletes"] > 10, st
     assert st["reserves"] > 100, st
+    assert st["node_rows_in_place"] > 0 and st["node_rows_in_place"] < st["node_deltas"], st
 
 
 def test_encoder_membership_counts_new_classes():
@@ -89,7 +90,8 @@ def test_encoder_node_delta_positions_and_rows():
     new = Node(name="fresh", labels={"kubernetes.io/hostname": "fresh", "topology.kubernetes.io/zone": "z1"},
                allocatable={"cpu": "4", "memory": "8Gi", "pods": "10"})
     gone = nodes[7].name
-    cl2, old_pos = enc.update_nodes([moved, new], [gone])
+    cl2, old_pos, rows = enc.update_nodes([moved, new], [gone])
+    assert rows is None                             # nodes added, removed and moved: the whole table
     assert cl2.n_nodes == 12
     assert gone not in cl2.node_names and "fresh" in cl2.node_names
     for i, n in enumerate(cl2.node_names):
@@ -101,3 +103,43 @@ def test_encoder_node_delta_positions_and_rows():
     assert enc.info().n_members == members - 2      # the removed node's two pods
     # the moved node sits in its own zone: nodeTree order puts the new zone last among zones
     assert cl2.node_labels[cl2.node_names.index(nodes[4].name)]["topology.kubernetes.io/zone"] == "z9"
+
+
+def test_encoder_updates_rows_in_place():
+    """An update that moves no node and needs no new vocabulary changes only
+    the updated rows' static columns (ksim_encoder_changed_rows); a new label
+    value or taint takes the whole-table path."""
+    from ksim.model import Taint
+    nodes, bound, _ = objects(n_nodes=12, pods_per_node=2, n_incoming=0)
+    nodes[3].taints = [Taint("dedicated", "x", "NoSchedule")]
+    enc = NativeEncoder()
+    cl, _ = enc.encode_cluster(nodes, bound)
+    from ksim.model import LabelSelector, PodAffinityTerm
+    probe = Pod(name="probe", containers=[Container({"cpu": "1"})],
+                pod_anti_affinity_required=[PodAffinityTerm("kubernetes.io/hostname", LabelSelector({"app": "a1"}))])
+    enc.encode_pods(cl, [probe])                    # a hostname label column
+    cl = enc.cluster
+    before = {k: getattr(cl, k).copy() for k in ("alloc_cpu", "flags", "taints", "labels", "req_cpu", "num_pods")}
+    a = copy.copy(nodes[5])
+    a.allocatable = dict(a.allocatable, cpu="3")
+    a.unschedulable = True
+    a.taints = [Taint("dedicated", "x", "NoSchedule")]
+    cl2, old_pos, rows = enc.update_nodes([a], [])
+    assert rows is not None and list(old_pos) == list(range(cl2.n_nodes))
+    p = cl2.node_names.index(a.name)
+    assert list(rows) == [p]
+    assert cl2.alloc_cpu[p] == 3000 and cl2.flags[p] & abi.NODE_UNSCHEDULABLE and cl2.taints[0][p] != 0
+    for k, v in before.items():
+        got = getattr(cl2, k)
+        mask = np.ones(cl2.n_nodes, bool)
+        if k in ("alloc_cpu", "flags", "taints"):
+            mask[p] = False
+        np.testing.assert_array_equal(np.asarray(got)[..., mask], np.asarray(v)[..., mask], err_msg=k)
+    b = copy.copy(nodes[6])
+    b.labels = dict(b.labels, **{"kubernetes.io/hostname": "renamed-host"})   # a value the column lacks
+    _, _, rows2 = enc.update_nodes([b], [])
+    assert rows2 is None
+    c2 = copy.copy(nodes[7])
+    c2.taints = [Taint("fresh", "y", "NoExecute")]                             # a taint the vocabulary lacks
+    _, _, rows3 = enc.update_nodes([c2], [])
+    assert rows3 is None

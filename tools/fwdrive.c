@@ -149,6 +149,8 @@ typedef struct fwdrive_delta_fns {
   int (*encoder_info)(const ksim_encoder*, ksim_encoder_info*);
   int (*upsert_nodes)(ksim_handle*, const ksim_node_table*, const ksim_vocab*, const int32_t*);
   int (*forget)(ksim_handle*, const ksim_pod_set*, int32_t, int32_t);
+  int (*encoder_changed_rows)(const ksim_encoder*, int32_t*, int32_t);
+  int (*update_node_rows)(ksim_handle*, const ksim_node_table*, const ksim_vocab*, const int32_t*, int32_t);
 } fwdrive_delta_fns;
 
 typedef struct fwdrive_deltas {
@@ -165,7 +167,7 @@ typedef struct fwdrive_deltas {
 typedef struct fwdrive_delta_result {
   double sec[7];
   double total;
-  int64_t bound, cycles, pod_adds, pod_deletes, node_updates, resends;
+  int64_t bound, cycles, pod_adds, pod_deletes, node_updates, resends, node_rows_in_place;
 } fwdrive_delta_result;
 
 /* the host's pool.build (encoder.go): the flat pool into one fresh C allocation */
@@ -287,8 +289,15 @@ static int node_update(dstate* s, const ksim_k8s_pool* pool, int32_t* old_pos) {
   if ((rc = s->g->encoder_update_nodes(s->enc, pool, NULL, 0))) return rc;
   ksim_node_table t;
   ksim_vocab v;
-  if ((rc = s->g->encoder_cluster(s->enc, &t, &v)) || (rc = s->g->encoder_old_pos(s->enc, old_pos))) return rc;
-  if ((rc = s->g->upsert_nodes(s->h, &t, &v, old_pos))) return rc;
+  if ((rc = s->g->encoder_cluster(s->enc, &t, &v))) return rc;
+  int32_t rows[8];
+  const int k = s->g->encoder_changed_rows(s->enc, rows, 8);
+  if (k >= 0 && k <= 8) {                      /* in place: the updated rows only */
+    if ((rc = s->g->update_node_rows(s->h, &t, &v, rows, k))) return rc;
+    s->res->node_rows_in_place++;
+  } else {
+    if ((rc = s->g->encoder_old_pos(s->enc, old_pos)) || (rc = s->g->upsert_nodes(s->h, &t, &v, old_pos))) return rc;
+  }
   s->res->node_updates++;
   return 0;
 }

@@ -181,8 +181,19 @@ struct ksim_handle {
   // instead of the whole stream); the pod last uploaded into pod1_arena (its
   // bytes and device address: a Reserve / Unreserve of the same pod binds
   // from there, no upload)
-  hipEvent_t up_ev = nullptr;
-  bool up_pending = false;
+  // upload_blob's pinned staging ring: consecutive pod uploads (an informer's
+  // pod deltas, another pod's Reserve, the next cycle's pod) do not wait for
+  // each other's copies; a slot is reused once its copy has run (its event)
+  struct PinSlot {
+    void* p = nullptr;
+    void* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  };
+  static constexpr int kPinRing = 4;
+  PinSlot ring[kPinRing];
+  int ring_next = 0;
   std::vector<char> pod1_blob;
   char* pod1_base = nullptr;
   // build_pod_blob's pieces and the framework-driven pass's blob, kept so the
@@ -1810,7 +1821,10 @@ void ksim_destroy(ksim_handle* h) {
   if (h->st) (void)hipFree(h->st);
   if (h->d_prof) (void)hipFree(h->d_prof);
   if (h->d_bp) (void)hipFree(h->d_bp);
-  if (h->up_ev) (void)hipEventDestroy(h->up_ev);
+  for (auto& r : h->ring) {
+    if (r.p) (void)hipHostFree(r.p);
+    if (r.ev) (void)hipEventDestroy(r.ev);
+  }
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -2326,7 +2340,6 @@ int ksim_update_node_rows(ksim_handle* h, const ksim_node_table* t, const ksim_v
   }
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));     // the pinned staging is free
-  h->up_pending = false;
   const int32_t words = 1 + 8 + KSIM_MAX_NODE_TAINTS + c.n_scalar + c.n_label_cols;
   int rc;
   if ((rc = pin_reserve(h, 8 * (size_t)words * (size_t)std::max(n_rows, 1)))) return rc;
@@ -2760,17 +2773,30 @@ static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPod
     h->pend_reuse++;
     if (const int prc = flush_pend_bind(h)) return prc;
   }
-  if (total > h->pin_cap || total > arena.cap) {
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-  } else if (h->up_pending) {
-    HIPCHK(h, hipEventSynchronize(h->up_ev));
+  ksim_handle::PinSlot& sl = h->ring[h->ring_next];
+  h->ring_next = (h->ring_next + 1) % ksim_handle::kPinRing;
+  if (total > arena.cap) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));   // the arena is reallocated: nothing may read it
+    for (auto& r : h->ring) r.pending = false;
+  } else if (sl.pending) {
+    HIPCHK(h, hipEventSynchronize(sl.ev));         // this slot's last copy (four uploads ago)
   }
-  h->up_pending = false;
+  sl.pending = false;
   int rc;
-  if ((rc = pin_reserve(h, total)) || (rc = arena_reserve(h, arena, total))) return rc;
-  std::memcpy(h->pin, b.bytes.data(), total);
+  if (total > sl.cap) {
+    if (sl.p) (void)hipHostFree(sl.p);
+    sl.p = sl.d = nullptr;
+    sl.cap = 0;
+    const size_t cap = std::max<size_t>(total * 2, 1 << 14);
+    hipError_t e = hipHostMalloc(&sl.p, cap, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (upload ring)");
+    if ((e = hipHostGetDevicePointer(&sl.d, sl.p, 0)) != hipSuccess) return hip_fail(h, e, "hipHostGetDevicePointer");
+    sl.cap = cap;
+  }
+  if ((rc = arena_reserve(h, arena, total))) return rc;
+  std::memcpy(sl.p, b.bytes.data(), total);
   Copies cp;
-  cp.add(h->pin_d, arena.p, total);
+  cp.add(sl.d, arena.p, total);
   if (begin_win) cp.begin(h->st, begin_win, 0, 1);
   if (record && h->pend_bind.on) {         // the last cycle's queued Reserve, ahead of this pass
     cp.bind(h->dc, h->pend_bind.P, h->pend_bind.node, h->pend_bind.sign);
@@ -2778,9 +2804,9 @@ static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPod
   }
   if ((rc = cp.run(h))) return rc;
   if (!synced) {                           // synced: the caller drains the stream before returning
-    if (!h->up_ev) HIPCHK(h, hipEventCreateWithFlags(&h->up_ev, hipEventDisableTiming));
-    HIPCHK(h, hipEventRecord(h->up_ev, h->stream));
-    h->up_pending = true;
+    if (!sl.ev) HIPCHK(h, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(sl.ev, h->stream));
+    sl.pending = true;
   }
   P = blob_pods(h, b, (char*)arena.p);
   if (record || &arena == &h->pod1_arena) {   // what a Reserve of this pod binds from

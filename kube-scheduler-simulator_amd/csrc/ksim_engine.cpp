@@ -156,7 +156,6 @@ struct ksim_handle {
   // compat-mode single pod
   DevArena pod1_arena;                  // the single-pod uploads (upload_single)
   DevArena nom_arena;                   // a nominated pod (ksim_fw_filter_nominated)
-  DevArena asm_arena;                   // ksim_assume / ksim_forget uploads (never the cycle's pod1)
   // Reserve / Unreserve calls that arrive while a framework cycle sits between
   // its PreFilter and Score (the binding goroutine's Unreserve):
   // upstream's running cycle keeps its snapshot, so the engine applies them
@@ -1809,7 +1808,6 @@ void ksim_destroy(ksim_handle* h) {
   free_bufs(h->pod_bufs);
   if (h->pod1_arena.p) (void)hipFree(h->pod1_arena.p);
   if (h->nom_arena.p) (void)hipFree(h->nom_arena.p);
-  if (h->asm_arena.p) (void)hipFree(h->asm_arena.p);
   for (auto& a : h->fw_arena)
     if (a.p) (void)hipFree(a.p);
   if (h->fwh) (void)hipHostFree(h->fwh);
@@ -2763,6 +2761,27 @@ static DevPods blob_pods(const ksim_handle* h, const PodBlob& b, char* d) {
 // upload's copy has run (its event), not after the whole stream drains; a
 // growing staging or arena drains the stream first.  begin_win: a
 // framework-driven filter pass's start in the same launch.
+// The next slot of the upload ring, free (its last copy has run) and at least
+// `bytes` large.
+static int ring_slot(ksim_handle* h, size_t bytes, ksim_handle::PinSlot** out) {
+  ksim_handle::PinSlot& sl = h->ring[h->ring_next];
+  h->ring_next = (h->ring_next + 1) % ksim_handle::kPinRing;
+  if (sl.pending) HIPCHK(h, hipEventSynchronize(sl.ev));   // this slot's last reader (four uploads ago)
+  sl.pending = false;
+  if (bytes > sl.cap) {
+    if (sl.p) (void)hipHostFree(sl.p);
+    sl.p = sl.d = nullptr;
+    sl.cap = 0;
+    const size_t cap = std::max<size_t>(bytes * 2, 1 << 14);
+    hipError_t e = hipHostMalloc(&sl.p, cap, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (upload ring)");
+    if ((e = hipHostGetDevicePointer(&sl.d, sl.p, 0)) != hipSuccess) return hip_fail(h, e, "hipHostGetDevicePointer");
+    sl.cap = cap;
+  }
+  *out = &sl;
+  return KSIM_OK;
+}
+
 static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPods& P,
                        WinState* begin_win = nullptr, bool record = false, bool synced = false) {
   const size_t total = b.bytes.size();
@@ -2773,26 +2792,14 @@ static int upload_blob(ksim_handle* h, const PodBlob& b, DevArena& arena, DevPod
     h->pend_reuse++;
     if (const int prc = flush_pend_bind(h)) return prc;
   }
-  ksim_handle::PinSlot& sl = h->ring[h->ring_next];
-  h->ring_next = (h->ring_next + 1) % ksim_handle::kPinRing;
   if (total > arena.cap) {
     HIPCHK(h, hipStreamSynchronize(h->stream));   // the arena is reallocated: nothing may read it
     for (auto& r : h->ring) r.pending = false;
-  } else if (sl.pending) {
-    HIPCHK(h, hipEventSynchronize(sl.ev));         // this slot's last copy (four uploads ago)
   }
-  sl.pending = false;
+  ksim_handle::PinSlot* slp = nullptr;
   int rc;
-  if (total > sl.cap) {
-    if (sl.p) (void)hipHostFree(sl.p);
-    sl.p = sl.d = nullptr;
-    sl.cap = 0;
-    const size_t cap = std::max<size_t>(total * 2, 1 << 14);
-    hipError_t e = hipHostMalloc(&sl.p, cap, hipHostMallocCoherent | hipHostMallocMapped);
-    if (e != hipSuccess) return hip_fail(h, e, "hipHostMalloc (upload ring)");
-    if ((e = hipHostGetDevicePointer(&sl.d, sl.p, 0)) != hipSuccess) return hip_fail(h, e, "hipHostGetDevicePointer");
-    sl.cap = cap;
-  }
+  if ((rc = ring_slot(h, total, &slp))) return rc;
+  ksim_handle::PinSlot& sl = *slp;
   if ((rc = arena_reserve(h, arena, total))) return rc;
   std::memcpy(sl.p, b.bytes.data(), total);
   Copies cp;
@@ -3428,11 +3435,19 @@ static int apply_bind(ksim_handle* h, const ksim_pod_set* ps, int32_t pod_index,
     h->pend_bind.on = true;
     return KSIM_OK;
   }
-  if ((rc = upload_blob(h, b, h->asm_arena, P))) return rc;
+  // another pod's Reserve / Unreserve (an informer's pod delta, a forget): the
+  // bind reads the pod straight from a pinned ring slot (mapped host memory):
+  // one launch, no arena copy
+  ksim_handle::PinSlot* sl = nullptr;
+  if ((rc = ring_slot(h, b.bytes.size(), &sl))) return rc;
+  std::memcpy(sl->p, b.bytes.data(), b.bytes.size());
+  P = blob_pods(h, b, (char*)sl->d);
   launch_assume(h->dc, P, 0, node, sign, h->stream);
   HIPCHK(h, hipGetLastError());
-  // no synchronization: every later call is ordered after it on the stream,
-  // and the next upload waits for the staging (upload_single)
+  if (!sl->ev) HIPCHK(h, hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming));
+  HIPCHK(h, hipEventRecord(sl->ev, h->stream));
+  sl->pending = true;
+  // no synchronization: every later call is ordered after it on the stream
   return KSIM_OK;
 }
 

@@ -1379,6 +1379,13 @@ int ksim_oracle_assume(ksim_oracle* o, const ksim_pod_set* ps, int32_t pi, int32
 }
 
 /* ---- timing mode: same cycle, node loop fanned out (Parallelizer analogue) */
+/* One OpenMP region for the whole run (no fork / join per pod).  Per pod:
+ * every thread filters its slice of the scan and counts it; one thread places
+ * the stop; every thread lists its slice's feasible nodes at its offset and
+ * (no PreScore state, no NetworkBandwidth score check: `fused`) scores them,
+ * keeping per-plugin extrema; after a barrier, NormalizeScore, the totals and
+ * selectHost's best of its part; one thread combines the bests, binds, and
+ * sets up the next pod.  Four barriers a pod on the fused path. */
 int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, int32_t count,
                          int32_t* chosen_out, int nthreads, ksim_batch_stats* st) {
   if (!o || !ps || first < 0 || count < 0 || first + count > ps->n_pods) return KSIM_E_INVALID;
@@ -1392,30 +1399,34 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
   int64_t* raw = o->raw;     /* [S][N] */
   int64_t* totals = (int64_t*)malloc(8 * (size_t)N);
   uint8_t* ign_buf = (uint8_t*)malloc((size_t)N);
+  const int nb_score = has_score_plugin(o, KSIM_PL_NETWORK_BANDWIDTH);
+  /* the pod in flight (shared; written by one thread between barriers) */
+  const ksim_pod* p = NULL;
+  int64_t seq = 0;
+  scan_set ss;
+  int32_t NS = 0, K = 0, nf = 0, nfailed = 0, evaluated = 0, error = 0, chosen = -1, fused = 0;
+  topo_ctx tc;
+#define POD_SETUP(cc)                                                                                 \
+  do {                                                                                                \
+    p = &ps->pods[first + (cc)];                                                                      \
+    seq = o->pod_seq++;                                                                               \
+    ss = pod_scan_set(o, ps, p);                                                                      \
+    NS = ss.n;                                                                                        \
+    K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, NS);             \
+    nf = nfailed = evaluated = 0;                                                                     \
+    error = (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 1 : 0;                                         \
+    chosen = -1;                                                                                      \
+    topo_prefilter(o, ps, p, &tc);                                                                    \
+    fused = tc.n == 0 && !nb_score;                                                                   \
+  } while (0)
+  if (count > 0) POD_SETUP(0);
 
-  for (int32_t c = 0; c < count; c++) {
-    const int32_t pi = first + c;
-    const ksim_pod* p = &ps->pods[pi];
-    const int64_t seq = o->pod_seq++;
-    const scan_set ss = pod_scan_set(o, ps, p);
-    const int32_t NS = ss.n;
-    const int32_t K = ksim_oracle_num_feasible_nodes_to_find(o->prof.percentage_of_nodes_to_score, NS);
-    int32_t nf = 0, nfailed = 0, evaluated = 0, error = (p->flags & KSIM_POD_NODE_NAMES_UNKNOWN) ? 1 : 0;
-    int32_t chosen = -1;
-    topo_ctx tc;
-    topo_prefilter(o, ps, p, &tc);
-
-    /* no PreScore state and no NetworkBandwidth score check: the list's scores,
-     * extrema and totals are made slice by slice, with four barriers a pod */
-    const int fused = tc.n == 0 && !has_score_plugin(o, KSIM_PL_NETWORK_BANDWIDTH);
 #pragma omp parallel num_threads(nthreads) if (nthreads > 1)
-    {
-      const int T = omp_get_num_threads(), tid = omp_get_thread_num();
-      /* findNodesThatPassFilters: each thread filters its slice of the scan
-       * from nextStartNodeIndex and counts its feasible nodes up to its first
-       * error; one thread places the stop (the (K+1)-th feasible node or the
-       * first error, both counted as evaluated); each thread then lists its
-       * feasible nodes before the stop at its prefix offset. */
+  {
+    const int T = omp_get_num_threads(), tid = omp_get_thread_num();
+    for (int32_t c = 0; c < count; c++) {
+      /* findNodesThatPassFilters: this thread's slice of the scan from
+       * nextStartNodeIndex, its feasible nodes counted up to its first error */
       const int32_t a = (int32_t)((int64_t)NS * tid / T), b = (int32_t)((int64_t)NS * (tid + 1) / T);
       int32_t cnt = 0, err_at = NS;
       for (int32_t i = a; i < b; i++) {
@@ -1434,6 +1445,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
 #pragma omp barrier
 #pragma omp single
       {
+        /* the stop: the (K+1)-th feasible node or the first error, both evaluated */
         int32_t pre = 0, stop = NS, before = -1;
         for (int t = 0; t < T; t++) {
           const int32_t ta = (int32_t)((int64_t)NS * t / T), tb = (int32_t)((int64_t)NS * (t + 1) / T);
@@ -1470,6 +1482,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
           if (feas[node] == 1) o->flist[w1++] = node;
         }
       }
+      o->th_node[tid * 16] = -1;
       if (fused && nf > 1 && !error) {
         /* prioritizeNodes over this thread's part of the list: raw scores and
          * the per-plugin extrema NormalizeScore reads */
@@ -1521,16 +1534,6 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
         o->th_mn[tid * 8] = bt;
         o->th_lo[tid * 8] = bl;
         o->th_node[tid * 16] = bn;
-#pragma omp barrier
-#pragma omp single
-        for (int t = 0; t < T; t++) {
-          const int32_t n2 = o->th_node[t * 16];
-          if (n2 >= 0 && (chosen < 0 || tb_better(o->th_mn[t * 8], o->th_lo[t * 8], bt, bl))) {
-            bt = o->th_mn[t * 8];
-            bl = o->th_lo[t * 8];
-            chosen = n2;
-          }
-        }
       } else {
 #pragma omp barrier
 #pragma omp single
@@ -1568,7 +1571,7 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
 #pragma omp for schedule(static)
             for (int32_t j = 0; j < nf; j++) v[j] = normalize_one(pl, ign_buf[j], mn, mx, v[j]);
           }
-          /* the weighted totals and selectHost (TB): per thread, then combined */
+          /* the weighted totals and selectHost (TB): per thread */
           int64_t bt = 0;
           uint64_t bl = 0;
           int32_t bn = -1;
@@ -1588,8 +1591,15 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
           o->th_mn[tid * 8] = bt;
           o->th_lo[tid * 8] = bl;
           o->th_node[tid * 16] = bn;
+        }
+      }
 #pragma omp barrier
 #pragma omp single
+      {
+        /* selectHost over the threads' bests, the bind, the next pod */
+        if (nf > 1 && !error) {
+          int64_t bt = 0;
+          uint64_t bl = 0;
           for (int t = 0; t < T; t++) {
             const int32_t n2 = o->th_node[t * 16];
             if (n2 >= 0 && (chosen < 0 || tb_better(o->th_mn[t * 8], o->th_lo[t * 8], bt, bl))) {
@@ -1599,14 +1609,21 @@ int ksim_oracle_schedule(ksim_oracle* o, const ksim_pod_set* ps, int32_t first, 
             }
           }
         }
+        if (nf == 1 && !error) chosen = o->flist[0];
+        if (NS > 0) o->next_start = (int32_t)(((int64_t)o->next_start + nf + nfailed) % NS);
+        evals += evaluated;
+        if (chosen >= 0) {
+          assume_pod(o, ps, p, chosen, 1);
+          sched++;
+        } else {
+          unsched++;
+        }
+        if (chosen_out) chosen_out[c] = error ? KSIM_CHOSEN_ERROR : chosen;
+        if (c + 1 < count) POD_SETUP(c + 1);
       }
     }
-    if (nf == 1 && !error) chosen = o->flist[0];
-    if (NS > 0) o->next_start = (int32_t)(((int64_t)o->next_start + nf + nfailed) % NS);
-    evals += evaluated;
-    if (chosen >= 0) { assume_pod(o, ps, p, chosen, 1); sched++; } else { unsched++; }
-    if (chosen_out) chosen_out[c] = error ? KSIM_CHOSEN_ERROR : chosen;
   }
+#undef POD_SETUP
   free(totals);
   free(ign_buf);
   if (st) {

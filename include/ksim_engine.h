@@ -710,7 +710,9 @@ int ksim_time_eval(ksim_handle* h, int32_t first, int32_t reps, double* avg_ms, 
  * overlay-indexed, node-stationary direct / indexed, KEEP default-shape /
  * generic, direct default-shape / generic, indexed default-shape / generic --
  * bits 16..21 k_batch_top -- static-class default-shape KEEP, static-class
- * default-shape, static-class, FAST default-shape, FAST, generic keys).
+ * default-shape, static-class, FAST default-shape, FAST, generic keys);
+ * out[26] topology batch pods committed on a zone variant (their batch moved
+ * their DoNotSchedule domain verdicts; ksim_tbatch.hip TbVar), cumulative.
  * Returns the number of values written (<= n). */
 int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n);
 /* Batch-path geometry compiled into the library: out[0] pods per batch (B),

@@ -168,6 +168,30 @@ constexpr int64_t kDomCountMask = (1ll << kDomMarkShift) - 1;
 
 struct BRow;
 
+// Topology batch zone variants (ksim_tbatch.hip): a pod whose one
+// DoNotSchedule spread key has at most kVarDom domains is evaluated per
+// feasible-domain set its batch can reach.  An earlier pod of the batch that
+// adds to the constraint's count class (its adder) moves one domain's count by
+// where it lands; each landing domain (or none) gives a set of domains whose
+// skew passes, and each distinct set is a slot with its own normalization,
+// top-T list and pair keys.  The chain takes the slot its adder's guess names.
+constexpr int kVarDom = 4;
+constexpr int kVarSlots = kVarDom + 1;
+struct TbVar {
+  int32_t use;                     // the variant use (-1: the pod's plain S0 path)
+  int32_t adder;                   // batch index of the one earlier pod adding its class (-1: none, or several)
+  int32_t nslot;                   // slots (1 without an adder)
+  int32_t ndom;                    // domains of the key (value ids 1 .. ndom)
+  int32_t col;                     // the key column
+  uint32_t zmask;                  // score slots constant 0 for the pod (k_tb_filter)
+  int32_t slot_of[kVarSlots];      // slot by the adder's landing domain (0: it moves no count)
+  uint32_t mask[kVarSlots];        // feasible domains per slot (bit d - 1)
+};
+struct TbDom {                     // per (pod, domain): nodes passing every filter but the variant skew
+  int32_t nfeas, nign;
+  uint64_t ext[2 * KSIM_MAX_SCORE];
+};
+
 // Selection state of one per-pod cycle (k_window -> k_extrema -> k_select -> k_bind).
 // ext[kExtCut] (sharded cycles): 1 + the scan position of the cut node on the
 // shard that holds it, 0 elsewhere; all-reduced (max) together with the extrema.
@@ -273,6 +297,11 @@ struct DevScratch {
   int64_t* tb_raw;       // [kTbPods][KSIM_MAX_SCORE][n] raw scores
   int32_t* tb_stat;      // total - (w_fit LeastAllocated + w_ba BalancedAllocation) at S0; kStatNone / kStatOne
   WinState* tb_win;      // [kTbPods] counters, extrema, flags
+  TbVar* tb_var;         // [kTbPods] zone variants of the pod (k_tb_filter block 0)
+  TbDom* tb_dom;         // [kTbPods][kVarDom] variant pods: counters and extrema per domain of the variant key
+  int32_t* tb_vhold;     // [kTbPods][kVarSlots][2 * KSIM_MAX_SCORE] variant pods: extremum holders per slot
+  int32_t* tb_slot;      // [kTbPods] the slot the chain took per pod (k_tb_chain_pairs block 0)
+  unsigned long long* tb_vpods;   // [1] committed pods whose zone verdicts moved inside their batch (ksim_get_diag)
   uint64_t* tb_clist;    // [kTbPods][kTbMaxBlocks][T] each node block's exact top-T keys
   int32_t* tb_ccnt;      // [kTbPods][kTbMaxBlocks] their counts
   uint8_t* tb_xrecv;     // replicated topology batches: [world][kTbPods] WinState (the filter's counters)
@@ -998,6 +1027,13 @@ constexpr uint32_t kPlanPtab = 1u;
 // kPlanTadds: tadd_first / tadd_count list every persistent-table update of
 // the pod's binds (queue pods; single uploads go through the class index).
 constexpr uint32_t kPlanTadds = 2u;
+// (flags >> kPlanVuseShift) & 31: 1 + the pod's zone-variant use (topology
+// batches, TbVar: its first DoNotSchedule spread use read from a persistent
+// table whose key has at most kVarDom domains), 0: none
+constexpr int kPlanVuseShift = 8;
+// (flags >> kPlanVcolShift) - 1: the key column of the zone variants of the
+// topology batch run from this pod (-1: the run has none)
+constexpr int kPlanVcolShift = 16;
 
 // One node's inputs of every topology use of the cycle's pod, loaded up front:
 // one round of label loads, then one of domain-table / class-count loads, so
@@ -1555,7 +1591,9 @@ constexpr int32_t kPodRegistersValues = 2; // has a ScheduleAnyway spread keyed 
 constexpr int32_t kPodNormVaries = 4;      // batch path: TaintToleration / NodeAffinity vary over nodes (norm_part)
 constexpr int32_t kPodTopoBatch = 8;       // topology batch path (ksim_tbatch.hip)
 constexpr int32_t kPodTbCross = 16;       // topology batch run from this pod crosses a class conflict (node-local)
-constexpr int kTlenShift = 8;              // bflags >> kTlenShift: topology batch run length from this pod
+constexpr int kTlenShift = 8;              // (bflags >> kTlenShift) & kTlenMask: topology batch run length from this pod
+constexpr int kTlenPlainShift = 16;        // ... without zone variants (replicated topology batches)
+constexpr int32_t kTlenMask = 255;
 
 // Compact row for the batch repair's LDS staging: the NodeRow fields a
 // batchable pod can read (batchable pods request no scalar resources and the

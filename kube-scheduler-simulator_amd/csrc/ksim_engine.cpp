@@ -150,6 +150,7 @@ struct ksim_handle {
   std::vector<uint8_t> hard_small;      // per loaded pod: every hard spread key column has <= kFuseMinValues values
   std::vector<uint8_t> soft_le1;        // per loaded pod: at most one ScheduleAnyway spread constraint
   std::vector<int32_t> tlen;            // per loaded pod: topology batch run length from it (tbatch_runs)
+  std::vector<int32_t> tlen_plain;      // ... without zone variants (replicated topology batches)
   std::vector<int64_t> xdom_len;        // per loaded pod: sharded cycle, packed domain words
   std::vector<int64_t> xreg_len;        // per loaded pod: sharded cycle, registration words (0: no soft spread)
 
@@ -822,6 +823,8 @@ int capture(ksim_handle* h, bool batch, bool topo, hipGraphExec_t* out, bool fas
 int run_tbatch(ksim_handle* h, int32_t a, int32_t b, const LaunchArgs& la) {
   int rc;
   HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->sc.tb_dom, 0, sizeof(TbDom) * kTbPods * kVarDom, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->sc.tb_vhold, 0, 4 * (size_t)kTbPods * kVarSlots * 2 * KSIM_MAX_SCORE, h->stream));
   if (!h->graph_tbatch) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     hipGraph_t g = nullptr;
@@ -1386,7 +1389,7 @@ int shard_run_tbatch(const std::vector<ksim_handle*>& hs, int32_t a, int32_t b) 
   int32_t cursor = a;
   while (cursor < b) {
     int32_t nbat = 0;
-    for (int32_t i = cursor; i < b; nbat++) i += std::min(std::min(kTbPods, b - i), std::max(h0->tlen[i], 1));
+    for (int32_t i = cursor; i < b; nbat++) i += std::min(std::min(kTbPods, b - i), std::max(h0->tlen_plain[i], 1));
     for (int32_t i = 0; i < nbat; i++)
       if ((rc = shard_tbatch(hs, stream))) return rc;
     DevState st;
@@ -2163,10 +2166,15 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.tb_ign, uint8_t*, (size_t)kTbPods * NT);
   SCR(s.tb_part, int64_t*, 8 * (size_t)kTbPods * NT);
   SCR(s.tb_raw, int64_t*, 8 * (size_t)kTbPods * KSIM_MAX_SCORE * NT);
-  SCR(s.tb_stat, int32_t*, 4 * (size_t)kTbPods * NT);
+  SCR(s.tb_stat, int32_t*, 4 * (size_t)kTbPods * kVarSlots * NT);   // per zone-variant slot
   SCR(s.tb_win, WinState*, sizeof(WinState) * (size_t)kTbPods);
-  SCR(s.tb_clist, uint64_t*, 8 * (size_t)kTbPods * kTbMaxBlocks * kTopT);
-  SCR(s.tb_ccnt, int32_t*, 4 * (size_t)kTbPods * kTbMaxBlocks);
+  SCR(s.tb_var, TbVar*, sizeof(TbVar) * (size_t)kTbPods);
+  SCR(s.tb_dom, TbDom*, sizeof(TbDom) * (size_t)kTbPods * kVarDom);
+  SCR(s.tb_vhold, int32_t*, 4 * (size_t)kTbPods * kVarSlots * 2 * KSIM_MAX_SCORE);
+  SCR(s.tb_slot, int32_t*, 4 * (size_t)kTbPods);
+  SCR(s.tb_vpods, unsigned long long*, 8);
+  SCR(s.tb_clist, uint64_t*, 8 * (size_t)kTbPods * kVarSlots * kTbMaxBlocks * kTopT);
+  SCR(s.tb_ccnt, int32_t*, 4 * (size_t)kTbPods * kVarSlots * kTbMaxBlocks);
   SCR(s.tb_xrecv, uint8_t*, sizeof(WinState) * (size_t)kMaxShards * kTbPods);
   SCR(s.tb_pp, uint64_t*, 8 * 2 * (size_t)kTbPods);
   SCR(s.pinv, int32_t*, 4 * (size_t)kBatchPods);
@@ -3620,39 +3628,73 @@ static bool tbatch_conflict_ok(const ksim_topo_use& u) {
          u.kind != KSIM_USE_IMAGE;
 }
 
+// The zone-variant use of a topology batch pod (ksim_device.h TbVar), or -1:
+// its first DoNotSchedule spread use, read from a persistent table, keyed by a
+// column of at most kVarDom domains (value ids 1 .. col_nvals - 1).
+int32_t tbatch_vuse(const ksim_handle* h, const ksim_pod& p, const PodPlan& pl, const ksim_topo_use* U) {
+  if (!(pl.flags & kPlanPtab)) return -1;
+  for (int32_t i = 0; i < p.use_count && i < KSIM_MAX_USES; i++) {
+    const ksim_topo_use& u = U[i];
+    if (u.kind != KSIM_USE_PTS_HARD) continue;
+    if (!((pl.m.hard >> i) & 1u) || !((pl.m.ptab >> i) & 1u) || u.col == KSIM_COL_NONE || u.cls < 0) return -1;
+    if (u.col >= (1 << (32 - kPlanVcolShift)) - 1) return -1;
+    const int32_t nd = h->col_nvals[u.col] - 1;
+    return nd >= 1 && nd <= kVarDom ? i : -1;
+  }
+  return -1;
+}
+
 // Topology batch runs (class 3 pods, ksim_tbatch.hip): tlen[i] = the number
 // of consecutive class-3 pods from i (at most kTbPods) none of which reads a
 // count class an earlier one of them adds through a use tbatch_conflict_ok
 // refuses; cross[i]: the run crosses a conflict.  0 for the other pods.
+// variants: a pod may also read such a class through its zone-variant use
+// (tbatch_vuse) when exactly one earlier pod of the run adds the class and the
+// use's column is the run's variant column vcol[i] (the first such use's;
+// -1: none), so the chain names its slot by where that pod lands.
 // uses: the queue's device use copies.
 void tbatch_runs(const ksim_pod_set* ps, const std::vector<ksim_topo_use>& uses,
-                 const std::vector<uint8_t>& batchable, std::vector<int32_t>& tlen, std::vector<uint8_t>& cross) {
+                 const std::vector<uint8_t>& batchable, const std::vector<PodPlan>& plans, bool variants,
+                 std::vector<int32_t>& tlen, std::vector<uint8_t>& cross, std::vector<int32_t>& vcol) {
   const int32_t n = ps->n_pods;
   tlen.assign((size_t)std::max(n, 0), 0);
   cross.assign((size_t)std::max(n, 0), 0);
+  vcol.assign((size_t)std::max(n, 0), -1);
   int32_t n_cls = 0;
   for (int32_t k = 0; k < ps->n_adds; k++) n_cls = std::max(n_cls, ps->adds[k].cls + 1);
   std::vector<int32_t> stamp((size_t)n_cls, -1);   // class -> the window start that added it
+  std::vector<int32_t> nadd((size_t)n_cls, 0);     // ... and how many pods of that run add it
   for (int32_t i = 0; i < n; i++) {
     if (batchable[i] != 3) continue;
-    int32_t L = 0;
+    int32_t L = 0, vc = -1;
     bool crossed = false;
     for (int32_t j = i; j < n && L < kTbPods && batchable[j] == 3; j++, L++) {
       const ksim_pod& p = ps->pods[j];
       const ksim_topo_use* U = uses.data() + p.use_first;
+      const int32_t vu = variants ? (int32_t)((plans[(size_t)j].flags >> kPlanVuseShift) & 31u) - 1 : -1;
       bool clash = false, hit = false;
       for (int32_t u = 0; u < p.use_count && !clash; u++) {
         const int32_t c = U[u].cls;
         if (c < 0 || c >= n_cls || stamp[c] != i) continue;
         hit = true;
-        clash = !tbatch_conflict_ok(U[u]);
+        if (tbatch_conflict_ok(U[u])) continue;
+        clash = !(u == vu && nadd[c] == 1 && (vc < 0 || vc == U[u].col));
+        if (!clash) vc = U[u].col;
       }
       if (clash) break;
       crossed = crossed || hit;
-      for (int32_t a = 0; a < p.add_count; a++) stamp[ps->adds[p.add_first + a].cls] = i;
+      for (int32_t a = 0; a < p.add_count; a++) {
+        const int32_t c = ps->adds[p.add_first + a].cls;
+        if (stamp[c] != i) {
+          stamp[c] = i;
+          nadd[c] = 0;
+        }
+        nadd[c]++;   // per add entry: a pod listing the class twice counts as two adders
+      }
     }
     tlen[i] = std::max(L, 1);
     cross[i] = crossed;
+    vcol[i] = vc;
   }
 }
 
@@ -3787,12 +3829,20 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod_set* ps) {
     if (batchable[i] == 0 && tbatch_admit(h, ps->pods[i], plans[i], h->hard_small[i] != 0, h->soft_le1[i] != 0)) {
       batchable[i] = 3;
       bf[i] |= kPodTopoBatch;
+      const int32_t vu = tbatch_vuse(h, ps->pods[i], plans[i], uses.data() + std::max(ps->pods[i].use_first, 0));
+      if (vu >= 0) plans[i].flags |= (uint32_t)(vu + 1) << kPlanVuseShift;
     }
   }
-  std::vector<uint8_t> tcross;
-  tbatch_runs(ps, uses, batchable, h->tlen, tcross);
-  for (int32_t i = 0; i < ps->n_pods; i++)
-    bf[i] |= (std::min(h->tlen[i], 255) << kTlenShift) | (tcross[(size_t)i] ? kPodTbCross : 0);
+  std::vector<uint8_t> tcross, c2;
+  std::vector<int32_t> tvcol, v2;
+  tbatch_runs(ps, uses, batchable, plans, !ab(kAbTbVar), h->tlen, tcross, tvcol);
+  tbatch_runs(ps, uses, batchable, plans, false, h->tlen_plain, c2, v2);   // replicated handles
+  for (int32_t i = 0; i < ps->n_pods; i++) {
+    // a run crosses with variants when it does without (a prefix of it)
+    bf[i] |= (std::min(h->tlen[i], kTlenMask) << kTlenShift) | (std::min(h->tlen_plain[i], kTlenMask) << kTlenPlainShift) |
+             (tcross[(size_t)i] ? kPodTbCross : 0);
+    plans[i].flags |= (uint32_t)(tvcol[(size_t)i] + 1) << kPlanVcolShift;
+  }
   DevPods P{};
   void* p = nullptr;
   if ((rc = put(ps->pods, sizeof(ksim_pod) * ps->n_pods, &p))) return drop_queue(rc);
@@ -4163,7 +4213,11 @@ int ksim_time_kernels(ksim_handle* h, int32_t first, int32_t count, double* avg_
     const int base = tb      ? kKernelsPerCycle + kKernelsPerBatch + kKernelsPerAdapt
                      : adapt ? kKernelsPerCycle + kKernelsPerBatch
                      : batch ? kKernelsPerCycle : 0;
-    if (tb) HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+    if (tb) {
+      HIPCHK(h, hipMemsetAsync(h->sc.tb_win, 0, sizeof(WinState) * kTbPods, h->stream));
+      HIPCHK(h, hipMemsetAsync(h->sc.tb_dom, 0, sizeof(TbDom) * kTbPods * kVarDom, h->stream));
+      HIPCHK(h, hipMemsetAsync(h->sc.tb_vhold, 0, 4 * (size_t)kTbPods * kVarSlots * 2 * KSIM_MAX_SCORE, h->stream));
+    }
     if (batch && !tb && a.fast && lazy_ok(h, lo, hi, true, a.stab)) {
       // deferred-commit batches: two (P100) or three to four (ADAPT) launches
       // each, a flush (untimed) before every state read
@@ -4259,7 +4313,7 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   DevState st;
   int rc = read_state(h, st);
   if (rc) return rc;
-  int64_t v[3 + 16 + 2 + 4 + 1] = {st.batches, st.truncations, st.cuts};
+  int64_t v[3 + 16 + 2 + 4 + 2] = {st.batches, st.truncations, st.cuts};
   if (h->has_cluster) HIPCHK(h, hcopy(h, v + 3, h->sc.dbg, 8 * 16, hipMemcpyDeviceToHost));
   if (unsigned long long* cp = cp_clock_buffer())   // KSIM_CP_CLOCKS builds: the chain + pairs phase clocks
     HIPCHK(h, hcopy(h, v + 3, cp, 8 * 8, hipMemcpyDeviceToHost));
@@ -4269,7 +4323,8 @@ extern "C" int ksim_get_diag(ksim_handle* h, int64_t* out, int32_t n) {
   v[20] = h->match_ns;
   for (int k = 0; k < 4; k++) v[21 + k] = h->fw_counts[k];
   v[25] = (int64_t)batch_variant_reach();
-  const int32_t m = n < 26 ? n : 26;
+  if (h->has_cluster && h->sc.tb_vpods) HIPCHK(h, hcopy(h, v + 26, h->sc.tb_vpods, 8, hipMemcpyDeviceToHost));
+  const int32_t m = n < 27 ? n : 27;
   for (int32_t i = 0; i < m; i++) out[i] = v[i];
   return m;
 }

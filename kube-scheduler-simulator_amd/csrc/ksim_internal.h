@@ -10,7 +10,7 @@ namespace ksim {
 // libksim_engine_ab.so, every alternative form on; tests/test_gpu_ab_switches.py
 // runs it against the oracle).  The product library has none of them.
 // KSIM_AB_FORMS is a bitmask of the alternative forms (csrc/Makefile "ab":
-// 63, every one on; "abforms": one form each, checked against the product's
+// 127, every one on; "abforms": one form each, checked against the product's
 // other forms):
 constexpr unsigned kAbStab = 1;      // per-node static plugins (no static-class table)
 constexpr unsigned kAbLazy = 2;      // three-launch batches (commit as its own launch)
@@ -18,6 +18,7 @@ constexpr unsigned kAbAdaptNorm = 4; // ADAPT normalized-score pods on the per-p
 constexpr unsigned kAbTbatch = 8;    // topology pods on the per-pod path
 constexpr unsigned kAbShardGraph = 16;   // eager shard cycles (no shard-group graphs)
 constexpr unsigned kAbPtab = 32;     // per-cycle PreFilter domain sums (no persistent tables)
+constexpr unsigned kAbTbVar = 64;    // topology batches end at a zone-keyed class conflict (no zone variants)
 #ifdef KSIM_AB_FORMS
 constexpr unsigned kAbMask = KSIM_AB_FORMS;
 #else

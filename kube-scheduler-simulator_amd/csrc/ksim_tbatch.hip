@@ -18,16 +18,27 @@
 // the normalization and the spread weights were taken over; such a pod ends
 // the batch before it (pinv), and the next batch starts from it.
 //
+// Zone variants (round 6, ksim_device.h TbVar): a run may also cross the
+// class of a pod's DoNotSchedule spread constraint on a key of at most
+// kVarDom domains (zones) when one earlier pod of the run adds to it.  That
+// pod's bind moves one domain's count, which moves the skew verdict of whole
+// domains (once an app's zones are level, almost every bind of the app does),
+// so the pod is evaluated per reachable feasible-domain set: k_tb_filter
+// passes the constraint's skew and keeps counters and extrema per domain,
+// k_tb_select normalizes, keys and lists each distinct set (a slot) over its
+// domains, and the chain takes the slot the earlier pod's guess lands in.
+//
 //   k_tb_filter      grid (node blocks, pods): RunFilterPlugins and the raw
 //                    scores of pod j on every node (k_filter_score's plan
 //                    chains), feasible / ignored counts and NormalizeScore
-//                    extrema per pod (block_extrema), the critical paths and
-//                    InterPodAffinity flags from the persistent tables
+//                    extrema per pod (block_extrema; per domain for a variant
+//                    pod), the critical paths and InterPodAffinity flags from
+//                    the persistent tables; block 0 derives the pod's slots
 //   k_tb_select      grid (node blocks, pods): normalized weighted totals (as
-//                    k_select), TB keys, each block's exact top-T per pod, and
-//                    per node stat = total - (Fit + BalancedAllocation) part
-//   k_tb_merge       one wave per pod: the pod's exact top-T from its blocks'
-//   k_tb_chain_pairs the chain (ksim_chain.h), then pod j on each earlier
+//                    k_select), TB keys, each block's exact top-T per pod and
+//                    slot, and per node stat = total - (Fit + BalancedAllocation) part
+//   k_tb_merge       one wave per pod and slot: its exact top-T from its blocks'
+//   k_tb_chain_pairs the chain (tb_chain, one wave), then pod j on each earlier
 //                    guess: stat + the resource part after that bind, or pinv
 //   k_tb_commit      batch_commit, the committed pods' count-class adds and
 //                    persistent-table updates as parallel atomics, and the
@@ -37,7 +48,6 @@
 #include "ksim_wave.h"
 #include "ksim_cycle.h"
 #include "ksim_commit.h"
-#include "ksim_chain.h"
 
 namespace ksim {
 
@@ -45,10 +55,11 @@ constexpr int32_t kStatNone = INT32_MIN;       // tb_stat: not feasible at S0
 constexpr int32_t kStatOne = INT32_MIN + 1;    // tb_stat: the pod's only feasible node (chosen unscored)
 
 // The batch's pod count: the conflict-free run from the cursor, capped.
-__device__ __forceinline__ int32_t tb_count(const DevState* __restrict__ st, const DevPods& P) {
+// plain: the run without zone variants (replicated topology batches).
+__device__ __forceinline__ int32_t tb_count(const DevState* __restrict__ st, const DevPods& P, int32_t plain) {
   const int32_t base = st->cursor;
   if (base >= st->end) return 0;
-  const int32_t tlen = P.bflags[base] >> kTlenShift;
+  const int32_t tlen = (P.bflags[base] >> (plain ? kTlenPlainShift : kTlenShift)) & kTlenMask;
   return min(min(kTbPods, st->end - base), max(tlen, 1));
 }
 
@@ -58,23 +69,192 @@ struct TbSlice {
   uint8_t* ign;
   int64_t* part;
   int64_t* raw;
-  int32_t* stat;
   WinState* win;
 };
 __device__ __forceinline__ TbSlice tb_slice(const DevScratch& s, int32_t j, int32_t n) {
   const size_t N = (size_t)n;
   return TbSlice{s.tb_fail + j * N, s.tb_ign + j * N, s.tb_part + j * N, s.tb_raw + (size_t)j * KSIM_MAX_SCORE * N,
-                 s.tb_stat + j * N, s.tb_win + j};
+                 s.tb_win + j};
+}
+// Pod j's list / stat / holder slot sl (0 for a pod without variants).
+__device__ __forceinline__ size_t tb_pj(int32_t j, int32_t sl) { return (size_t)j * kVarSlots + sl; }
+
+// A variant pod's constraint skew passes on every node in k_tb_filter (the
+// slots take the verdicts per domain): a critical-path minimum no count reaches.
+constexpr int64_t kVarNoMin = 1ll << 50;
+
+// The feasible / ignored counts of pod j's slot (mask mk; the pod's tb_win
+// without variants).  Uniform.
+__device__ __forceinline__ void tb_slot_counts(const DevScratch& s, int32_t j, const TbVar& V, uint32_t mk,
+                                               int32_t& nf, int32_t& nign) {
+  if (V.use < 0) {
+    nf = s.tb_win[j].nfeas;
+    nign = s.tb_win[j].nign;
+    return;
+  }
+  nf = nign = 0;
+#pragma unroll
+  for (int d = 0; d < kVarDom; d++)
+    if (d < V.ndom && ((mk >> d) & 1u)) {
+      nf += s.tb_dom[(size_t)j * kVarDom + d].nfeas;
+      nign += s.tb_dom[(size_t)j * kVarDom + d].nign;
+    }
+}
+
+// One extremum word e of pod j's slot (mask mk) without materializing the
+// slot's record (k_tb_select keeps its registers for the node loop).  Uniform.
+__device__ __forceinline__ uint64_t tb_slot_ext(const DevScratch& s, int32_t j, const TbVar& V, uint32_t mk, int32_t nf,
+                                                int e) {
+  if (V.use < 0) return s.tb_win[j].ext[e];
+  if ((V.zmask >> (e >> 1)) & 1u) return nf > 0 ? ((e & 1) ? min_image(0) : max_image(0)) : 0ull;
+  uint64_t x = 0;
+#pragma unroll
+  for (int d = 0; d < kVarDom; d++)
+    if (d < V.ndom && ((mk >> d) & 1u)) x = umax64(x, s.tb_dom[(size_t)j * kVarDom + d].ext[e]);
+  return x;
+}
+
+// A variant pod's per-domain feasible / ignored counts and NormalizeScore
+// extrema (block_extrema per domain of the variant key; zmask slots are set
+// by tb_slot_ext).  dom: the node's value id of the key (1 .. nd when feasible).
+__device__ __forceinline__ void tb_dom_extrema(const ksim_profile& prof, TbDom* __restrict__ out, int32_t nd,
+                                               uint32_t zmask, bool feasible, bool ign, uint32_t dom,
+                                               const uint64_t (&ix)[KSIM_MAX_SCORE],
+                                               const uint64_t (&in)[KSIM_MAX_SCORE],
+                                               uint64_t (*s_red)[kVarDom][2 * KSIM_MAX_SCORE],
+                                               int32_t (*s_cnt)[kVarDom][2]) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int S = prof.n_score;
+#pragma unroll 1
+  for (int d = 0; d < nd; d++) {                  // one domain at a time (the loop body holds the VGPR peak)
+    const bool on = feasible && dom == (uint32_t)(d + 1);
+    const uint64_t fm = __ballot(on), im = __ballot(on && ign);
+    if (lane == 0) {
+      s_cnt[wv][d][0] = (int32_t)__popcll(fm);
+      s_cnt[wv][d][1] = (int32_t)__popcll(im);
+    }
+#pragma unroll
+    for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+      if (k >= S) break;
+      if (norm_kind(prof.score[k]) == kNormNone || ((zmask >> k) & 1u)) continue;
+      const uint64_t a = wave_max_u64_dpp(on ? ix[k] : 0), b = wave_max_u64_dpp(on ? in[k] : 0);
+      if (lane == 0) {
+        s_red[wv][d][2 * k] = a;
+        s_red[wv][d][2 * k + 1] = b;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < nd * 2 * KSIM_MAX_SCORE) {
+    const int d = tid / (2 * KSIM_MAX_SCORE), e = tid % (2 * KSIM_MAX_SCORE), k = e >> 1;
+    if (k < S && norm_kind(prof.score[k]) != kNormNone && !((zmask >> k) & 1u)) {
+      uint64_t m = 0;
+#pragma unroll
+      for (int w = 0; w < 4; w++) m = umax64(m, s_red[w][d][e]);
+      if (m) atomicMax(reinterpret_cast<unsigned long long*>(&out[d].ext[e]), (unsigned long long)m);
+    }
+  } else if (tid >= 128 && tid < 128 + 2 * nd) {
+    const int d = (tid - 128) >> 1, q = (tid - 128) & 1;
+    const int32_t v = s_cnt[0][d][q] + s_cnt[1][d][q] + s_cnt[2][d][q] + s_cnt[3][d][q];
+    if (v) atomicAdd(q ? &out[d].nign : &out[d].nfeas, v);
+  }
+}
+
+// Pod j's slots (one wave of block 0): the one earlier pod of the batch adding
+// to the variant use's class (its adder: exactly one add entry in the batch,
+// on the run's variant column), the S0 domain entries of the use's table, and
+// per landing domain of the adder (0: it moves no count) the domains whose
+// skew passes; equal sets share a slot.  The same verdict as pts_filter with
+// topo_block_setup's critical path over the moved counts.
+__device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods& P, const DevScratch& s,
+                                          const DevState* __restrict__ st, int32_t j, int32_t vu, uint32_t zmask) {
+  const int lane = threadIdx.x & 63;
+  TbVar* out = s.tb_var + j;
+  if (vu < 0) {
+    if (lane == 0) {
+      TbVar V{};
+      V.use = -1;
+      V.adder = -1;
+      V.nslot = 1;
+      V.col = -1;
+      V.zmask = zmask;
+      V.mask[0] = ~0u;
+      *out = V;
+    }
+    return;
+  }
+  const int32_t base = st->cursor;
+  const ksim_pod& p = P.pods[base + j];
+  const ksim_topo_use u = load_use(P.uses + p.use_first, vu);
+  const int32_t nd = c.col_nvals[u.col] - 1;        // 1 .. kVarDom (k_tb_filter)
+  const uint32_t self = (P.plans[base + j].m.self_match >> vu) & 1u;
+  const int32_t vcol = (int32_t)(P.plans[base].flags >> kPlanVcolShift) - 1;
+  int32_t ne = 0, cx = 0;
+  if (lane < j) {
+    const ksim_pod& pk = P.pods[base + lane];
+    for (int a = 0; a < pk.add_count; a++) {
+      const ksim_class_add x = P.adds[pk.add_first + a];
+      if (x.cls == u.cls) {
+        ne++;
+        cx += x.count;
+      }
+    }
+  }
+  const int64_t e = lane <= nd ? P.ptab[u._pad + lane] : 0;
+  const int32_t tot = (int32_t)wave_sum_u32_dpp((uint32_t)ne);
+  const uint64_t who = __ballot(ne > 0);
+  const int32_t adder = (tot == 1 && vcol == u.col) ? (int32_t)__builtin_ctzll(who) : -1;
+  const int32_t x = __shfl(cx, adder >= 0 ? adder : 0, 64);
+  int64_t cnt[kVarDom + 1];
+  bool mk[kVarDom + 1];
+#pragma unroll
+  for (int v = 0; v <= kVarDom; v++) {
+    const int64_t ev = (int64_t)readlane_u64((uint64_t)e, v);
+    cnt[v] = ev & kDomCountMask;
+    mk[v] = v <= nd && (ev >> kDomMarkShift) != 0;
+  }
+  if (lane != 0) return;
+  TbVar V{};
+  V.use = vu;
+  V.adder = adder;
+  V.ndom = nd;
+  V.col = u.col;
+  V.zmask = zmask;
+  V.nslot = 0;
+  const int32_t wmax = adder >= 0 ? nd : 0;
+#pragma unroll
+  for (int w = 0; w <= kVarDom; w++) {
+    V.slot_of[w] = 0;
+    if (w > wmax) continue;
+    int64_t mn = 2147483647;                       // topo_block_setup's minimum over marked domains
+#pragma unroll
+    for (int v = 0; v <= kVarDom; v++)
+      if (mk[v]) mn = min(mn, cnt[v] + (v == w && w > 0 ? x : 0));
+    uint32_t m = 0;
+#pragma unroll
+    for (int d = 1; d <= kVarDom; d++) {
+      if (d > nd) continue;
+      const int64_t c = cnt[d] + (d == w ? x : 0);
+      if (c + (int64_t)self - mn <= (int64_t)u.arg) m |= 1u << (d - 1);
+    }
+    int32_t q = 0;
+    while (q < V.nslot && V.mask[q] != m) q++;
+    if (q == V.nslot) V.mask[V.nslot++] = m;
+    V.slot_of[w] = q;
+  }
+  *out = V;
 }
 
 // Three waves per SIMD (152 VGPRs, no spills) instead of the two its 176
 // VGPRs allowed: the kernel waits on its table and row loads most of the time.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
-                                                   DevScratch s) {
+                                                   DevScratch s, int32_t plain) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
   __shared__ uint64_t s_red[4][2 * KSIM_MAX_SCORE];
+  __shared__ uint64_t s_dred[4][kVarDom][2 * KSIM_MAX_SCORE];
   __shared__ int32_t s_cnt[4][2];
+  __shared__ int32_t s_dcnt[4][kVarDom][2];
   __shared__ uint32_t s_tf;
   const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;   // replicas: their range
   const int32_t xr = node < c.eval_hi ? node : c.eval_hi - 1;
@@ -82,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const NodeRow r = load_row(c, xr);
   const double inv_c = c.inv_cpu[xr], inv_m = c.inv_mem[xr];
   const int32_t j = blockIdx.y;
-  if (j >= tb_count(st, P0)) return;                // block-uniform
+  if (j >= tb_count(st, P0, plain)) return;         // block-uniform
   const ksim_profile& prof = *prof_p;
   const int32_t pi = st->cursor + j;
   const DevPods& P = P0;
@@ -91,11 +271,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const UseMasks& m = pp.m;
   const ksim_topo_use* U = P.uses + p.use_first;
   const TbSlice q = tb_slice(s, j, c.n);
+  // the zone-variant use (plain launches and keys grown past kVarDom domains: none)
+  int32_t vu = plain ? -1 : (int32_t)((pp.flags >> kPlanVuseShift) & 31u) - 1;
+  int32_t nd = 0;
+  uint32_t vdom = 0;                               // the node's value id of the variant key
+  if (vu >= 0) {
+    const int32_t col = load_use(U, vu).col;
+    nd = c.col_nvals[col] - 1;
+    if (nd < 1 || nd > kVarDom) vu = -1;
+    else vdom = c.labels[(size_t)col * c.n + xr];
+  }
   TopoRow t;
   load_topo_row(c, U, p.use_count, m, s, P0.ptab, xr, t);
   const bool pt = (pp.flags & kPlanPtab) != 0;      // the host admits only table-read pods (tbatch_admit)
   if (m.hard || (pt && (m.aff | m.score))) {
     topo_block_setup(c, P0, s, U, m, pt, true, s_min, &s_tf, &q.win->tflags);
+    if (vu >= 0 && threadIdx.x == 0) s_min[vu] = kVarNoMin;   // after thread 0's critical paths
     __syncthreads();
   }
   const uint32_t tf = pt && (m.aff | m.score) ? s_tf : 0u;
@@ -160,7 +351,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                    (pl == KSIM_PL_POD_TOPOLOGY_SPREAD && soft < 0);
     if (z) zmask |= 1u << k;
   }
-  block_extrema(prof, q.win, ix, in, s_red, zmask, s_cnt);
+  if (vu < 0)
+    block_extrema(prof, q.win, ix, in, s_red, zmask, s_cnt);
+  else
+    tb_dom_extrema(prof, s.tb_dom + (size_t)j * kVarDom, nd, zmask, feasible, ign, vdom, ix, in, s_dred, s_dcnt);
+  if (blockIdx.x == 0 && threadIdx.x < 64) tb_var_setup(c, P0, s, st, j, vu, zmask);
 }
 
 // Each block's exact top-T keys of pod j over its 256 nodes: every wave
@@ -191,12 +386,12 @@ __device__ __forceinline__ void block_top_t(uint64_t key, uint64_t* s_cand, uint
 
 __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
-                                                   DevScratch s) {
+                                                   DevScratch s, int32_t plain) {
   __shared__ uint64_t s_cand[4 * kTopT];
   __shared__ int32_t s_hold[4][4];
   const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t j = blockIdx.y;
-  if (j >= tb_count(st, P0)) return;                // block-uniform
+  if (j >= tb_count(st, P0, plain)) return;         // block-uniform
   const ksim_profile& prof = *prof_p;
   const int32_t N = c.n;
   const int S = prof.n_score;
@@ -205,106 +400,122 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
   const UseMasks m = P0.plans[pi].m;
   const ksim_topo_use* U = P0.uses + p.use_first;
   const TbSlice q = tb_slice(s, j, N);
-  WinState* win = q.win;
-  const int32_t nf = win->nfeas;
+  const TbVar& V = s.tb_var[j];
+  const int32_t ns = V.nslot, vuse = V.use;
   const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
-  const bool has_soft = nf > 1 && soft >= 0;
-  double w_soft = 0;
-  int32_t ms = 0;
-  if (has_soft) {                                  // topologyNormalizingWeight (hostname keys only: tbatch_admit)
+  int32_t ms = 0;                                  // topologyNormalizingWeight inputs (hostname keys only: tbatch_admit)
+  bool soft_hn = false;
+  if (soft >= 0) {
     const ksim_topo_use u = load_use(U, soft);
-    w_soft = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - win->nign : 0];
+    soft_hn = (u.flags & KSIM_USEF_HOSTNAME) != 0;
     ms = u.arg;
   }
-  const bool ipa_nonempty = (win->tflags & kTopoScoreNonEmpty) != 0;
+  const bool ipa_nonempty = (q.win->tflags & kTopoScoreNonEmpty) != 0;
   const ScorePlan sp{bp->slot, bp->slot_hi};
   const int k_fit = plan_slot(sp, KSIM_PL_NODE_RESOURCES_FIT), k_ba = plan_slot(sp, KSIM_PL_BALANCED_ALLOCATION);
   const uint64_t seed = prof.tiebreak_seed;
   const int64_t seq = st->pod_seq + j;
-  uint64_t key = 0;
-  uint32_t hf = 0;                                 // holds PTS max, PTS min, IPA max, IPA min
-  if (node < c.eval_hi) {
-    int32_t stat = kStatNone;
-    if (q.fail[node] == KSIM_PASSED) {
-      if (nf > 1) {
-        const bool ign = has_soft && q.ign[node];
-        int64_t tot = S == 0 ? 1 : q.part[node];
-        for (int k = 0; k < S; k++) {
-          const int32_t kind = norm_kind(prof_score(prof, k));
-          if (kind == kNormNone) continue;
-          int64_t gmax = from_max_image(win->ext[2 * k]), gmin = from_min_image(win->ext[2 * k + 1]);
-          if (kind == kNormIPA) {                  // the holders of the extrema (k_tb_chain_pairs)
-            const int64_t x = q.raw[(size_t)k * N + node];
-            hf |= (x == gmax ? 4u : 0u) | (x == gmin ? 8u : 0u);
-          } else if (kind == kNormPTS && has_soft && !ign) {
-            const int64_t x = q.raw[(size_t)k * N + node];
-            hf |= (x == gmax ? 1u : 0u) | (x == gmin ? 2u : 0u);
-          }
-          int64_t raw;
-          if (kind == kNormPTS) {
-            raw = 0;
-            if (has_soft) {                        // counts -> scores (a non-decreasing map)
-              if (!ign) raw = soft_score(q.raw[(size_t)k * N + node], w_soft, ms);
-              if (win->ext[2 * k]) gmax = soft_score(gmax, w_soft, ms);
-              if (win->ext[2 * k + 1]) gmin = soft_score(gmin, w_soft, ms);
-            }
-          } else {
-            raw = q.raw[(size_t)k * N + node];
-          }
-          const int64_t nv = (kind == kNormPTS && ign) ? 0 : normalize_value(kind, raw, gmax, gmin, ipa_nonempty);
-          tot += nv * prof_weight(prof, k);
-        }
-        int64_t dyn0 = 0;                          // the part a bind on this node moves
-        if (k_fit >= 0) dyn0 += bp->w_fit * q.raw[(size_t)k_fit * N + node];
-        if (k_ba >= 0) dyn0 += bp->w_ba * q.raw[(size_t)k_ba * N + node];
-        stat = (int32_t)(tot - dyn0);
-        key = tb_key(tot, seed, seq, c.base + node);
-      } else {                                     // one feasible node: schedulePod takes it unscored
-        stat = kStatOne;
-        key = tb_key(0, seed, seq, c.base + node);
-      }
-    }
-    q.stat[node] = stat;
-  }
-  // holder counts (runs that cross a class conflict): one popcount per wave,
-  // one atomic per block and counter (after block_top_t's barrier)
+  const bool live = node < c.eval_hi;
+  const bool pass = live && q.fail[node] == KSIM_PASSED;
+  uint32_t dom = 0;
+  if (vuse >= 0 && live) dom = c.labels[(size_t)V.col * c.n + node];
+  const bool ign0 = pass && q.ign[node] != 0;
   const bool cross = (P0.bflags[st->cursor] & kPodTbCross) != 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (cross) {
+  for (int32_t sl = 0; sl < ns; sl++) {
+    if (sl) __syncthreads();                       // s_cand / s_hold of the last slot read
+    const uint32_t mk = vuse >= 0 ? V.mask[sl] : ~0u;
+    int32_t nf, nign;
+    tb_slot_counts(s, j, V, mk, nf, nign);
+    const bool has_soft = nf > 1 && soft >= 0;
+    const double w_soft = has_soft ? c.topo_log[soft_hn ? nf - nign : 0] : 0.0;
+    const bool feas = pass && (vuse < 0 || (dom >= 1 && dom <= (uint32_t)kVarDom && ((mk >> (dom - 1)) & 1u)));
+    uint64_t key = 0;
+    uint32_t hf = 0;                               // holds PTS max, PTS min, IPA max, IPA min
+    if (live) {
+      int32_t stat = kStatNone;
+      if (feas) {
+        if (nf > 1) {
+          const bool ign = has_soft && ign0;
+          int64_t tot = S == 0 ? 1 : q.part[node];
+          for (int k = 0; k < S; k++) {
+            const int32_t kind = norm_kind(prof_score(prof, k));
+            if (kind == kNormNone) continue;
+            const uint64_t ex = tb_slot_ext(s, j, V, mk, nf, 2 * k), en = tb_slot_ext(s, j, V, mk, nf, 2 * k + 1);
+            int64_t gmax = from_max_image(ex), gmin = from_min_image(en);
+            const int64_t x = q.raw[(size_t)k * N + node];
+            if (kind == kNormIPA) {                // the holders of the extrema (k_tb_chain_pairs)
+              hf |= (x == gmax ? 4u : 0u) | (x == gmin ? 8u : 0u);
+            } else if (kind == kNormPTS && has_soft && !ign) {
+              hf |= (x == gmax ? 1u : 0u) | (x == gmin ? 2u : 0u);
+            }
+            int64_t rv;
+            if (kind == kNormPTS) {
+              rv = 0;
+              if (has_soft) {                      // counts -> scores (a non-decreasing map)
+                if (!ign) rv = soft_score(x, w_soft, ms);
+                if (ex) gmax = soft_score(gmax, w_soft, ms);
+                if (en) gmin = soft_score(gmin, w_soft, ms);
+              }
+            } else {
+              rv = x;
+            }
+            const int64_t nv = (kind == kNormPTS && ign) ? 0 : normalize_value(kind, rv, gmax, gmin, ipa_nonempty);
+            tot += nv * prof_weight(prof, k);
+          }
+          int64_t dyn0 = 0;                        // the part a bind on this node moves
+          if (k_fit >= 0) dyn0 += bp->w_fit * q.raw[(size_t)k_fit * N + node];
+          if (k_ba >= 0) dyn0 += bp->w_ba * q.raw[(size_t)k_ba * N + node];
+          stat = (int32_t)(tot - dyn0);
+          key = tb_key(tot, seed, seq, c.base + node);
+        } else {                                   // one feasible node: schedulePod takes it unscored
+          stat = kStatOne;
+          key = tb_key(0, seed, seq, c.base + node);
+        }
+      }
+      s.tb_stat[tb_pj(j, sl) * N + node] = stat;
+    }
+    // holder counts (runs that cross a class conflict): one popcount per wave,
+    // one atomic per block and counter (after block_top_t's barrier)
+    if (cross) {
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
-      const int32_t n = (int32_t)__popcll(__ballot((hf >> h) & 1u));
-      if (lane == 0) s_hold[wv][h] = n;
+      for (int h = 0; h < 4; h++) {
+        const int32_t n = (int32_t)__popcll(__ballot((hf >> h) & 1u));
+        if (lane == 0) s_hold[wv][h] = n;
+      }
     }
-  }
-  block_top_t(key, s_cand, s.tb_clist + ((size_t)j * kTbMaxBlocks + blockIdx.x) * kTopT,
-              s.tb_ccnt + (size_t)j * kTbMaxBlocks + blockIdx.x);
-  if (cross && threadIdx.x < 4) {
-    int kp = -1, ki = -1;                          // the profile's slots (block-uniform)
-    for (int k = 0; k < S; k++) {
-      const int32_t kind = norm_kind(prof_score(prof, k));
-      if (kind == kNormPTS) kp = k;
-      if (kind == kNormIPA) ki = k;
+    block_top_t(key, s_cand, s.tb_clist + (tb_pj(j, sl) * kTbMaxBlocks + blockIdx.x) * kTopT,
+                s.tb_ccnt + tb_pj(j, sl) * kTbMaxBlocks + blockIdx.x);
+    if (cross && threadIdx.x < 4) {
+      int kp = -1, ki = -1;                        // the profile's slots (block-uniform)
+      for (int k = 0; k < S; k++) {
+        const int32_t kind = norm_kind(prof_score(prof, k));
+        if (kind == kNormPTS) kp = k;
+        if (kind == kNormIPA) ki = k;
+      }
+      const int h = threadIdx.x, k = h < 2 ? kp : ki;
+      const int32_t n = s_hold[0][h] + s_hold[1][h] + s_hold[2][h] + s_hold[3][h];
+      int32_t* hold = vuse >= 0 ? s.tb_vhold + tb_pj(j, sl) * 2 * KSIM_MAX_SCORE : q.win->hold;
+      if (k >= 0 && n) atomicAdd(&hold[2 * k + (h & 1)], n);
     }
-    const int h = threadIdx.x, k = h < 2 ? kp : ki;
-    const int32_t n = s_hold[0][h] + s_hold[1][h] + s_hold[2][h] + s_hold[3][h];
-    if (k >= 0 && n) atomicAdd(&win->hold[2 * k + (h & 1)], n);
   }
 }
 
-// Pod j's exact top-T from its blocks' exact lists (the pod's top-T lies in
-// the union of the blocks' top-T): one wave, lane b holds block b's list.
-// xsend (replicas): the record [kTbPods][kTbXRec] of this replica's range
-// (keys, count, holder counts) instead of the pod's lists.
+// Pod j's exact top-T of slot sl from its blocks' exact lists (the pod's
+// top-T lies in the union of the blocks' top-T): one wave, lane b holds block
+// b's list.  xsend (replicas, slot 0): the record [kTbPods][kTbXRec] of this
+// replica's range (keys, count, holder counts) instead of the pod's lists.
 __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const DevState* __restrict__ st,
-                                                 DevScratch s, uint64_t* __restrict__ xsend) {
+                                                 DevScratch s, uint64_t* __restrict__ xsend, int32_t plain) {
   const int lane = threadIdx.x;
-  const int32_t j = blockIdx.x;
-  if (j >= tb_count(st, P)) return;
+  const int32_t j = blockIdx.x, sl = blockIdx.y;
+  if (j >= tb_count(st, P, plain)) return;
+  if (sl >= s.tb_var[j].nslot) return;
+  const size_t pj = tb_pj(j, sl);
   const int32_t nblk = (c.eval_hi - c.eval_lo + 255) / 256;
   uint64_t L[kTopT];
   int32_t cnt = 0;
-  const size_t cl = (size_t)j * kTbMaxBlocks + lane;
+  const size_t cl = pj * kTbMaxBlocks + lane;
   if (lane < nblk) {
     cnt = s.tb_ccnt[cl];
 #pragma unroll
@@ -336,10 +547,13 @@ __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const 
                             ((uint64_t)(uint32_t)s.tb_win[j].hold[2 * lane + 1] << 32);
     return;
   }
-  if (lane < kTopT) s.topk[(size_t)j * kTopT + lane] = lane < n ? mine : 0;
+  if (lane < kTopT) s.topk[pj * kTopT + lane] = lane < n ? mine : 0;
   if (lane == 0) {
-    s.topk_cnt[j] = n;
-    s.topk_complete[j] = s.tb_win[j].nfeas <= kTopT ? 1 : 0;   // every feasible node listed
+    s.topk_cnt[pj] = n;
+    const TbVar& V = s.tb_var[j];
+    int32_t nf, nign;
+    tb_slot_counts(s, j, V, V.use >= 0 ? V.mask[sl] : ~0u, nf, nign);
+    s.topk_complete[pj] = nf <= kTopT ? 1 : 0;     // every feasible node listed
   }
 }
 
@@ -376,7 +590,8 @@ __global__ __launch_bounds__(64) void k_tb_gmerge(DevPods P, const DevState* __r
   static_assert(kTopT * kMaxShards <= 64, "k_tb_gmerge: one list entry per lane");
   const int lane = threadIdx.x;
   const int32_t j = blockIdx.x;
-  if (j >= tb_count(st, P)) return;
+  if (j >= tb_count(st, P, 1)) return;
+  const size_t pj = tb_pj(j, 0);
   const int32_t r = lane / kTopT, e = lane % kTopT;
   uint64_t key = 0;
   if (r < world) {
@@ -389,11 +604,11 @@ __global__ __launch_bounds__(64) void k_tb_gmerge(DevPods P, const DevState* __r
     rank += o > key;
   }
   const int32_t n = __popcll(__ballot(key != 0));
-  if (key != 0 && rank < kTopT) s.topk[(size_t)j * kTopT + rank] = key;
-  if (lane >= n && lane < kTopT) s.topk[(size_t)j * kTopT + lane] = 0;
+  if (key != 0 && rank < kTopT) s.topk[pj * kTopT + rank] = key;
+  if (lane >= n && lane < kTopT) s.topk[pj * kTopT + lane] = 0;
   if (lane == 0) {
-    s.topk_cnt[j] = n < kTopT ? n : kTopT;
-    s.topk_complete[j] = s.tb_win[j].nfeas <= kTopT ? 1 : 0;
+    s.topk_cnt[pj] = n < kTopT ? n : kTopT;
+    s.topk_complete[pj] = s.tb_win[j].nfeas <= kTopT ? 1 : 0;
   }
   if (lane < KSIM_MAX_SCORE) {
     uint32_t hmax = 0, hmin = 0;
@@ -419,34 +634,148 @@ __device__ __forceinline__ bool tb_keeps_extrema(int64_t x0, int64_t x1, int64_t
   return true;
 }
 
+// The topology batch's chain (tb_chain): node ids of the cluster index the
+// guess table directly (tbatch_admit: at most kTbMaxBlocks x 256 nodes).
+constexpr int kTbHoldSlots = kTbMaxBlocks * 256;
+constexpr int kTbChainRounds = kTbPods + 2;        // pod i is exact after round i + 1
+struct TbChainLds {
+  uint32_t hold[kTbHoldSlots];                     // (round << 8) | (255 - pod): the lowest pod guessing the node
+  uint64_t lst[kTbPods][kVarSlots][kTopT];         // each pod's lists per slot
+  uint8_t dom[kTbPods][kVarSlots][kTopT];          // the listed nodes' value ids of the run's variant key column
+  int32_t cnt[kTbPods][kVarSlots], comp[kTbPods][kVarSlots], slot_of[kTbPods][kVarSlots];
+  uint64_t gk[kTbPods];
+  int32_t slot[kTbPods];
+  int32_t nchain;
+};
+
+// The greedy chain of one topology batch in one wave (lane i = pod i < nb):
+// each pod takes the first entry of its current slot's list that no earlier
+// pod guesses, its slot being the one its adder's current guess lands in
+// (slot 0 without an adder).  Rounds run to the fixpoint: pod i depends only
+// on pods before it, so pods [0, r) are exact after round r.  Then the exact
+// prefix is cut before a pod whose incomplete list ran out.  Writes L.gk
+// (0: none or past the prefix), L.slot and L.nchain.
+__device__ __forceinline__ void tb_chain(TbChainLds& L, const DevCluster& c, const DevPods& P,
+                                         const DevState* __restrict__ st, const DevScratch& s, int32_t nb,
+                                         int32_t plain) {
+  const int i = threadIdx.x;                       // wave 0
+  const bool live = i < nb;
+  const int32_t vcol = plain ? -1 : (int32_t)(P.plans[st->cursor].flags >> kPlanVcolShift) - 1;
+  int32_t nslot = 0, adder = -1;
+  if (live) {
+    const TbVar& V = s.tb_var[i];
+    nslot = V.nslot;
+    adder = V.adder;
+#pragma unroll
+    for (int w = 0; w < kVarSlots; w++) L.slot_of[i][w] = V.slot_of[w];
+  }
+  // the lists, then the listed nodes' domains and their guess-table entries
+  uint64_t k0[kVarSlots][kTopT];
+  int32_t c0[kVarSlots];
+#pragma unroll
+  for (int sl = 0; sl < kVarSlots; sl++) {
+    c0[sl] = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) k0[sl][e] = 0;
+    if (sl < nslot) {
+      const size_t pj = tb_pj(i, sl);
+      c0[sl] = s.topk_cnt[pj];
+      L.comp[i][sl] = s.topk_complete[pj];
+#pragma unroll
+      for (int e = 0; e < kTopT; e++) k0[sl][e] = s.topk[pj * kTopT + e];
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < kVarSlots; sl++) {
+    if (sl >= nslot) continue;
+    L.cnt[i][sl] = c0[sl];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) {
+      L.lst[i][sl][e] = k0[sl][e];
+      uint8_t d = 0;
+      if (e < c0[sl]) {
+        const int32_t nd = key_node(k0[sl][e]);
+        L.hold[nd & (kTbHoldSlots - 1)] = 0u;
+        if (vcol >= 0) d = (uint8_t)min(c.labels[(size_t)vcol * c.n + (nd - c.base)], (uint32_t)kVarDom);
+      }
+      L.dom[i][sl][e] = d;
+    }
+  }
+  wave_lds_sync();
+  int cs = 0, ca = (live && c0[0] > 0) ? 0 : -1;   // current slot and entry
+  int32_t gnode = ca >= 0 ? key_node(k0[0][0]) : -1;
+  int32_t gdom = ca >= 0 ? L.dom[i][0][0] : 0;
+  int32_t first = nb;
+  for (int32_t r = 1; r <= kTbChainRounds; r++) {
+    if (gnode >= 0) atomicMax(&L.hold[gnode & (kTbHoldSlots - 1)], ((uint32_t)r << 8) | (uint32_t)(255 - i));
+    wave_lds_sync();
+    const int32_t ad = __shfl(gdom, adder >= 0 ? adder : 0, 64);
+    const int ns = (live && adder >= 0) ? L.slot_of[i][ad] : 0;
+    const int32_t cn = live ? L.cnt[i][ns] : 0;
+    int na = -1;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) {
+      if (e >= cn || na >= 0) continue;
+      const int32_t nd = key_node(L.lst[i][ns][e]);
+      const uint32_t h = L.hold[nd & (kTbHoldSlots - 1)];
+      const bool held = (h >> 8) == (uint32_t)r && (int)(255 - (h & 255u)) < i;
+      if (!held) na = e;
+    }
+    const uint64_t chg = __ballot(live && (ns != cs || na != ca));
+    cs = ns;
+    ca = na;
+    gnode = ca >= 0 ? key_node(L.lst[i][cs][ca]) : -1;
+    gdom = ca >= 0 ? L.dom[i][cs][ca] : 0;
+    wave_lds_sync();                               // this round's reads before the next round's registrations
+    if (!chg) {
+      first = nb;
+      break;
+    }
+    first = (int32_t)__builtin_ctzll(chg);
+  }
+  // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
+  const uint64_t bad = __ballot(live && i < first && ca < 0 && !L.comp[i][cs]);
+  const int32_t nchain = bad ? min(first, (int32_t)__builtin_ctzll(bad)) : first;
+  if (i < kTbPods) {
+    L.gk[i] = (i < nchain && ca >= 0) ? L.lst[i][cs][ca] : 0;
+    L.slot[i] = cs;
+  }
+  if (i == 0) L.nchain = nchain;
+}
+
 // Block j: the chain, then pod j's keys on the guesses of pods k < j after
 // those binds (thread k: pod k's guess), or pinv[j] when pod j's S0 lists no
 // longer describe it.  Pod k's bind moves pod j's inputs only on its guessed
 // node g: the resources and, in a run that crosses a class conflict
-// (kPodTbCross), the classes pod k adds through pod j's node-local uses.  The
-// key on g is the S0 stat with the resource part and the changed
-// PodTopologySpread / InterPodAffinity raw scores recomputed against S0's
-// extrema; pinv when a change would move an extremum, the feasible set (a
-// node's verdict) or an emptiness flag.
+// (kPodTbCross), the classes pod k adds through pod j's node-local uses (its
+// zone-variant use aside: the slot holds that move).  The key on g is the
+// slot's stat with the resource part and the changed PodTopologySpread /
+// InterPodAffinity raw scores recomputed against the slot's extrema; pinv
+// when a change would move an extremum, the feasible set (a node's verdict)
+// or an emptiness flag.
 // pp (replicas): pair maxima and pinv into pp[j] / pp[kTbPods + j], keyed
 // only on the guesses in this replica's range (the all-reduce max combines).
 __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, DevPods P,
                                                                const ksim_profile* __restrict__ prof_p,
                                                                const BatchProg* __restrict__ bp_p,
                                                                const DevState* __restrict__ st, DevScratch s,
-                                                               uint64_t* __restrict__ pp) {
-  __shared__ ChainLds L;
+                                                               uint64_t* __restrict__ pp, int32_t plain) {
+  __shared__ TbChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   __shared__ int32_t s_winv[kBatchPods / 64];
-  const int32_t nbt = tb_count(st, P);
-  uint64_t gk;
-  int32_t nchain;
-  if (!chain_block(L, st, s.topk, s.topk_cnt, s.topk_complete, &gk, &nchain, nullptr, nbt, c.n_total))
-    return;
+  const int32_t nbt = tb_count(st, P, plain);
+  if (nbt <= 0) return;                            // block-uniform
+  if (threadIdx.x < 64) tb_chain(L, c, P, st, s, nbt, plain);
+  __syncthreads();
+  const int32_t nchain = L.nchain;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
+  const uint64_t gk = k < nbt ? L.gk[k] : 0;
   if (j == 0) {
-    if (tid < nbt) s.gkey[tid] = gk;
+    if (tid < nbt) {
+      s.gkey[tid] = gk;
+      s.tb_slot[tid] = L.slot[tid];
+    }
     if (tid == 0) *s.chain_end = nchain;
   }
   if (j >= nchain) {                               // block-uniform
@@ -468,6 +797,9 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const int32_t N = c.n;
   const ksim_pod& p = P.pods[base + j];
   const bool cross = (P.bflags[base] & kPodTbCross) != 0;
+  const int32_t sj = L.slot[j];
+  const TbVar& Vj = s.tb_var[j];
+  const int32_t vskip = Vj.adder >= 0 ? Vj.use : -1;   // the use the slot accounts for
   uint64_t v = 0;
   bool inv = false;
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
@@ -490,6 +822,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
       soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
     }
     for (int i = 0; i < nu; i++) {
+      if (i == vskip) continue;
       const ksim_topo_use u = load_use(U, i);
       if (u.cls < 0) continue;
       int32_t d = 0;
@@ -514,20 +847,23 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     }
     if (hit_aff && !(tf & kTopoAffinityNonEmpty)) inv = true;   // len(affinityCounts) would change
     if (hit_score && !(tf & kTopoScoreNonEmpty)) inv = true;    // len(topologyScore) would change
-    const int32_t sv = own ? s.tb_stat[(size_t)j * N + local] : kStatNone;
+    const int32_t sv = own ? s.tb_stat[tb_pj(j, sj) * N + local] : kStatNone;
     if (!own) {
     } else if (sv != kStatNone) {
       NodeRow r = load_row(c, local);
       row_add_pod(r, pk, 1);
       if (hit_anti || (bp.has_fit_filter && fits_request(r, p, c.n_scalar, c.fit_ignore))) {
-        inv = true;                                // a node of the S0 feasible set stops passing
+        inv = true;                                // a node of the slot's feasible set stops passing
       } else {
         int64_t tot = 0;
         if (sv != kStatOne) {
           tot = sv;
-          if (d_soft || d_ipa) {                   // the changed topology scores, S0's extrema
+          if (d_soft || d_ipa) {                   // the changed topology scores, the slot's extrema
+            const uint32_t mk = Vj.use >= 0 ? Vj.mask[sj] : ~0u;
+            int32_t nf, nign;
+            tb_slot_counts(s, j, Vj, mk, nf, nign);
+            const int32_t* hold = Vj.use >= 0 ? s.tb_vhold + tb_pj(j, sj) * 2 * KSIM_MAX_SCORE : win->hold;
             const bool ipa_ne = (tf & kTopoScoreNonEmpty) != 0;
-            const int32_t nf = win->nfeas;
             for (int kk = 0; kk < prof.n_score; kk++) {
               const int32_t kind = norm_kind(prof_score(prof, kk));
               const bool pts = kind == kNormPTS && d_soft != 0 && soft >= 0 && !s.tb_ign[(size_t)j * N + local];
@@ -535,19 +871,20 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
               if (!pts && !ipa) continue;
               const int64_t x0 = s.tb_raw[((size_t)j * KSIM_MAX_SCORE + kk) * N + local];
               const int64_t x1 = x0 + (pts ? d_soft : d_ipa);
-              int64_t gmax = from_max_image(win->ext[2 * kk]), gmin = from_min_image(win->ext[2 * kk + 1]);
-              if (!tb_keeps_extrema(x0, x1, gmax, gmin, win->hold[2 * kk], win->hold[2 * kk + 1], j)) {
+              int64_t gmax = from_max_image(tb_slot_ext(s, j, Vj, mk, nf, 2 * kk));
+              int64_t gmin = from_min_image(tb_slot_ext(s, j, Vj, mk, nf, 2 * kk + 1));
+              if (!tb_keeps_extrema(x0, x1, gmax, gmin, hold[2 * kk], hold[2 * kk + 1], j)) {
                 inv = true;
                 break;
               }
               int64_t r0 = x0, r1 = x1;
               if (pts) {                           // counts -> scores (topologyNormalizingWeight, hostname)
                 const ksim_topo_use u = load_use(U, soft);
-                const double w = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - win->nign : 0];
-                r0 = soft_score(x0, w, u.arg);
-                r1 = soft_score(x1, w, u.arg);
-                gmax = soft_score(gmax, w, u.arg);
-                gmin = soft_score(gmin, w, u.arg);
+                const double wt = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - nign : 0];
+                r0 = soft_score(x0, wt, u.arg);
+                r1 = soft_score(x1, wt, u.arg);
+                gmax = soft_score(gmax, wt, u.arg);
+                gmin = soft_score(gmin, wt, u.arg);
               }
               tot += prof_weight(prof, kk) *
                      (normalize_value(kind, r1, gmax, gmin, ipa_ne) - normalize_value(kind, r0, gmax, gmin, ipa_ne));
@@ -594,7 +931,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
 constexpr int kTbAddSlots = 8;                     // adds / table updates per pod and pass
 __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
                                                           DevScratch s, int32_t* __restrict__ chosen_out,
-                                                          const uint64_t* __restrict__ pp) {
+                                                          const uint64_t* __restrict__ pp, int32_t plain) {
   __shared__ int32_t s_istar, s_sched, s_unsched;
   __shared__ int32_t s_node[kTbPods];
   const int tid = threadIdx.x;
@@ -603,8 +940,9 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
   const int32_t inv = tid < kTbPods ? (pp ? (int32_t)(pp[kTbPods + tid] != 0) : s.pinv[tid]) : 0;
   const int32_t nchain = *s.chain_end;
   const int32_t base = st->cursor;
-  const int32_t nbt = tb_count(st, P);
+  const int32_t nbt = tb_count(st, P, plain);
   if (nbt <= 0) return;
+  const int32_t vslot = tid < nbt ? s.tb_slot[tid] : 0;
   batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt,
                s_node);
   __syncthreads();
@@ -627,9 +965,15 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
                          (unsigned long long)(int64_t)t.w);
       }
   }
-  // the next batch's counters and extrema start from zero
+  // committed pods whose slot moved their zone verdicts (ksim_get_diag out[26])
+  const uint64_t vb = __ballot(tid < nbt && s_node[tid < kTbPods ? tid : 0] != -2 && vslot != 0);
+  if ((tid & 63) == 0 && vb) atomicAdd(s.tb_vpods, (unsigned long long)__popcll(vb));
+  // the next batch's counters and extrema start from zero (the rows this batch used)
   for (int x = tid; x < kTbPods * (int)(sizeof(WinState) / 4); x += blockDim.x)
     reinterpret_cast<int32_t*>(s.tb_win)[x] = 0;
+  for (int x = tid; x < nbt * kVarDom * (int)(sizeof(TbDom) / 4); x += blockDim.x)
+    reinterpret_cast<int32_t*>(s.tb_dom)[x] = 0;
+  for (int x = tid; x < nbt * kVarSlots * 2 * KSIM_MAX_SCORE; x += blockDim.x) s.tb_vhold[x] = 0;
 }
 
 const char* const kTbatchKernelNames[kKernelsPerTbatch] = {"k_tb_filter", "k_tb_select", "k_tb_merge",
@@ -638,38 +982,38 @@ const char* const kTbatchKernelNames[kKernelsPerTbatch] = {"k_tb_filter", "k_tb_
 uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs) {
   const dim3 grid((a.c.n + 255) / 256, kTbPods);
   if (evs) (void)hipEventRecord(evs[0], stream);
-  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 0);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 0);
   if (evs) (void)hipEventRecord(evs[2], stream);
-  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s, nullptr);
+  k_tb_merge<<<dim3(kTbPods, kVarSlots), 64, 0, stream>>>(a.c, a.P, a.st, a.s, nullptr, 0);
   if (evs) (void)hipEventRecord(evs[3], stream);
-  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, nullptr);
+  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, nullptr, 0);
   if (evs) (void)hipEventRecord(evs[4], stream);
-  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, nullptr);
+  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, nullptr, 0);
   if (evs) (void)hipEventRecord(evs[5], stream);
   return (1u << kKernelsPerTbatch) - 1;
 }
 
 void launch_tb_rep_filter(const LaunchArgs& a, hipStream_t stream) {
   const dim3 grid((a.c.eval_hi - a.c.eval_lo + 255) / 256, kTbPods);
-  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
+  k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 1);
 }
 
 void launch_tb_rep_select(const LaunchArgs& a, int32_t world, hipStream_t stream) {
   const dim3 grid((a.c.eval_hi - a.c.eval_lo + 255) / 256, kTbPods);
   k_tb_wmerge<<<1, kTbPods, 0, stream>>>(a.s, world);
-  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s);
-  k_tb_merge<<<kTbPods, 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.s.xsend);
+  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 1);
+  k_tb_merge<<<dim3(kTbPods, 1), 64, 0, stream>>>(a.c, a.P, a.st, a.s, a.s.xsend, 1);
 }
 
 void launch_tb_rep_pairs(const LaunchArgs& a, int32_t world, hipStream_t stream) {
   k_tb_gmerge<<<kTbPods, 64, 0, stream>>>(a.P, a.st, a.s, world);
-  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, a.s.tb_pp);
+  k_tb_chain_pairs<<<kTbPods, kBatchPods, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, a.s.tb_pp, 1);
 }
 
 void launch_tb_rep_commit(const LaunchArgs& a, hipStream_t stream) {
-  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, a.s.tb_pp);
+  k_tb_commit<<<1, kBatchPods, 0, stream>>>(a.c, a.P, a.st, a.s, a.chosen, a.s.tb_pp, 1);
 }
 
 }  // namespace ksim

@@ -474,14 +474,14 @@ class Engine:
 
     def diag(self) -> dict:
         """Batch-path diagnostics of the last schedule_loaded call."""
-        out = np.zeros(26, np.int64)
-        n = self.L.ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 26)
+        out = np.zeros(27, np.int64)
+        n = self.L.ksim_get_diag(self.h, out.ctypes.data_as(ctypes.c_void_p), 27)
         if n < 0:
             self._chk(n)
         d = {"batches": int(out[0]), "truncations": int(out[1]), "cuts": int(out[2]),
              "graph_captures": int(out[19]), "dbg": [int(x) for x in out[3:19]], "match_ns": int(out[20]),
              "fw_score_host": int(out[21]), "fw_score_device": int(out[22]), "fw_normalize_cached": int(out[23]),
-             "fw_normalize_device": int(out[24]), "variants": int(out[25])}
+             "fw_normalize_device": int(out[24]), "variants": int(out[25]), "tb_variant_pods": int(out[26])}
         if out[6]:
             d["chain_us"] = {"setup": out[3] / out[6] / 100.0, "rounds": out[4] / out[6] / 100.0,
                              "epilogue": out[5] / out[6] / 100.0, "rounds_per_batch": out[7] / out[6]}

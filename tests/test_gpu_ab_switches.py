@@ -3,7 +3,8 @@ switches (csrc/Makefile "ab": libksim_engine_ab.so, KSIM_AB_FORMS): the
 three-launch P100 / ADAPT batches (commit as its own launch) instead of the
 deferred commit, the static plugins evaluated per node instead of the
 static-class table, ADAPT normalized-score and topology pods on the per-pod
-path, per-cycle PreFilter domain sums, eager shard cycles.  A child process
+path, per-cycle PreFilter domain sums, eager shard cycles, topology batch
+runs that end at a zone-keyed class conflict (no zone variants).  A child process
 loads that library (KSIM_LIB_VARIANT=ab), schedules P100 and ADAPT batches
 and checks them against the oracle (the product forms run in every other GPU
 test)."""
@@ -48,15 +49,27 @@ ochosen, ost = Oracle(cluster, prof).schedule(pods, nthreads=8)
 np.testing.assert_array_equal(chosen, ochosen)
 assert st.evals == ost.evals and st.perpod_cycles == 0 and st.batches > 0
 eng.close()
+cluster, pods = gen.config3(n_nodes=700, pods_per_node=4, n_incoming=1500, seed=700, zone_anti_every=60)
+eng = Engine(0)
+eng.set_profile(prof)
+eng.set_cluster(cluster)
+chosen, st = eng.schedule_batch(pods)
+ora = Oracle(cluster, prof)
+ochosen, ost = ora.schedule(pods, nthreads=8)
+np.testing.assert_array_equal(chosen, ochosen)
+assert st.evals == ost.evals and eng.next_start == ora.next_start
+np.testing.assert_array_equal(eng.class_count(), ora.class_count())
+eng.close()
 print("ok")
 '''
 
 
-@pytest.mark.parametrize("flavor", ["ab", "ab1", "ab2"])
+@pytest.mark.parametrize("flavor", ["ab", "ab1", "ab2", "ab64"])
 def test_ab_forms_vs_oracle(flavor):
     """ab: every alternative form at once; ab1: only the static-class table
     off (deferred commit kept); ab2: only the three-launch batches (the table
-    kept) -- each form alone against the product's others (ADVICE r5)."""
+    kept); ab64: only the topology batches' zone variants off -- each form
+    alone against the product's others (ADVICE r5)."""
     lib = os.path.join(ROOT, "kube-scheduler-simulator_amd", "ksim", f"libksim_engine_{flavor}.so")
     assert os.path.exists(lib), "build the ab flavors: make -C kube-scheduler-simulator_amd/csrc ab abforms"
     env = dict(os.environ)

@@ -67,8 +67,10 @@ def test_nodes_fill_up():
 
 def test_one_app_serializes():
     """Every pod spreads over the same selector: each pod reads the zone
-    DoNotSchedule counts the previous one adds (a domain-keyed use), so every
-    batch holds one pod; still exact."""
+    DoNotSchedule counts the earlier ones add.  A run holds two pods (the
+    second's zone variant is taken by where the first lands, ksim_device.h
+    TbVar); a third reads a class two earlier pods add and starts the next
+    run.  Still exact."""
     nodes, bound, inc = gen.config3_objects(n_nodes=200, pods_per_node=3, n_incoming=200, seed=9)
     for p in inc:
         p.labels["app"] = "a7"
@@ -78,7 +80,8 @@ def test_one_app_serializes():
             w.term.label_selector = LabelSelector({"app": "a7"})
     cluster, _ = encode_cluster(nodes, bound)
     eng, st = _run(cluster, encode_pods(cluster, inc))
-    assert st.perpod_cycles == 0 and st.batches == 200
+    assert st.perpod_cycles == 0 and 100 <= st.batches < 200
+    assert eng.diag()["tb_variant_pods"] > 0
 
 
 def _few_apps(inc, n_apps, rng, zone=True):
@@ -173,3 +176,106 @@ def test_kernel_timing_names():
     kt = eng.time_kernels(0, pods.n_pods)
     for k in ("k_tb_filter", "k_tb_select", "k_tb_merge", "k_tb_chain_pairs", "k_tb_commit"):
         assert k in kt and kt[k][1] > 0, (k, kt)
+
+
+# ---- zone variants (round 6): runs that cross the zone DoNotSchedule class ----
+def _zone_objects(n_nodes, per_node, n_inc, seed, zones=3, zone_every=1000, max_skew=1):
+    """config3_objects with the nodes spread round-robin over ``zones`` zones
+    and the incoming pods' zone constraint at ``max_skew``."""
+    nodes, bound, inc = gen.config3_objects(n_nodes=n_nodes, pods_per_node=per_node, n_incoming=n_inc, seed=seed,
+                                            zone_anti_every=zone_every)
+    for i, n in enumerate(nodes):
+        n.labels["topology.kubernetes.io/zone"] = f"z{i % zones}"
+    for p in inc:
+        for c in p.topology_spread:
+            if c.when_unsatisfiable == "DoNotSchedule":
+                c.max_skew = max_skew
+    return nodes, bound, inc
+
+
+def _batches_without_variants(cluster, pods):
+    """The same queue on the flavor without zone variants (libksim_engine_ab64.so):
+    runs end at a zone-keyed class conflict."""
+    prof = profile.compile_profile(profile.SchedulerProfile(percentage_of_nodes_to_score=100))
+    eng = Engine(0, variant="ab64")
+    eng.set_profile(prof)
+    eng.set_cluster(cluster)
+    chosen, st = eng.schedule_batch(pods)
+    assert eng.diag()["tb_variant_pods"] == 0
+    eng.close()
+    return chosen, st
+
+
+@pytest.mark.parametrize("n_nodes,per_node,n_inc,zone_every,seed", [(900, 6, 2400, 1000, 3), (600, 4, 1600, 50, 4),
+                                                                     (5000, 10, 3000, 1000, 5)])
+def test_zone_variants_config3(n_nodes, per_node, n_inc, zone_every, seed):
+    """Config 3's queue: a pod whose app already has one pod earlier in the run
+    is evaluated per feasible-zone set that pod's landing zone gives (its
+    slots), and the chain takes the slot its guess names.  Placements equal
+    the oracle's; batches are longer than the flavor without variants, which
+    places the same pods."""
+    cluster, pods = gen.config3(n_nodes=n_nodes, pods_per_node=per_node, n_incoming=n_inc, seed=seed,
+                                zone_anti_every=zone_every)
+    eng, st = _run(cluster, pods)
+    vp = eng.diag()["tb_variant_pods"]
+    chosen0, st0 = _batches_without_variants(cluster, pods)
+    print(f"{n_inc} pods: {st.batches} batches ({vp} pods on a moved zone verdict), {st0.batches} without variants")
+    assert st.perpod_cycles == 0 and vp > 0
+    assert st.batches < st0.batches
+
+
+@pytest.mark.parametrize("zones,max_skew", [(2, 1), (4, 1), (4, 2), (5, 1), (3, 3)])
+def test_zone_variants_domains(zones, max_skew):
+    """Keys of 2 and 4 zones (kVarDom = 4: the slots of every landing zone),
+    5 zones (more domains than slots: no variants, runs end at the conflict),
+    and a wider maxSkew (fewer verdicts move)."""
+    nodes, bound, inc = _zone_objects(700, 4, 1500, seed=50 + zones, zones=zones, zone_every=70, max_skew=max_skew)
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    vp = eng.diag()["tb_variant_pods"]
+    print(f"zones {zones} maxSkew {max_skew}: {st.batches} batches, {vp} variant pods")
+    assert st.perpod_cycles == 0
+    if zones > 4:
+        assert vp == 0
+    elif max_skew == 1:
+        assert vp > 0
+
+
+def test_zone_variants_few_apps_and_full_nodes():
+    """Two apps on small nodes: most pods have an adder, guesses stop fitting
+    (pinv), adders become unschedulable (no count moves: slot 0)."""
+    nodes, bound, inc = _zone_objects(150, 2, 1800, seed=61)
+    for n in nodes:
+        n.allocatable = {"cpu": "4", "memory": "8Gi", "pods": "110"}
+    inc = _few_apps(inc, 2, np.random.default_rng(61))
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    assert st.perpod_cycles == 0 and st.unschedulable > 0
+
+
+def test_zone_variants_foreign_selector_and_two_keys():
+    """Pods whose zone constraint selects another app (they add nothing to the
+    class they read: self match 0, the adders are that app's pods), pods with a
+    second DoNotSchedule constraint on a region key (a second zone-keyed
+    conflict ends the run), and pods whose required node affinity leaves one
+    zone out (the per-pod path takes those: tbatch_admit)."""
+    from ksim.model import LabelSelector as LS, NodeSelectorTerm, Requirement, TopologySpreadConstraint
+    nodes, bound, inc = _zone_objects(600, 4, 1500, seed=71, zone_every=60)
+    for i, n in enumerate(nodes):
+        n.labels["topology.kubernetes.io/region"] = f"r{(i // 7) % 2}"
+    rng = np.random.default_rng(71)
+    for k, p in enumerate(inc):
+        if k % 5 == 1:
+            other = f"a{int(rng.integers(0, 64))}"
+            for c in p.topology_spread:
+                if c.when_unsatisfiable == "DoNotSchedule":
+                    c.label_selector = LS({"app": other})
+        elif k % 5 == 2:
+            p.topology_spread = list(p.topology_spread) + [
+                TopologySpreadConstraint(1, "topology.kubernetes.io/region", "DoNotSchedule",
+                                         LS({"app": p.labels["app"]}))]
+        elif k % 5 == 3:
+            p.required_terms = [NodeSelectorTerm([Requirement("topology.kubernetes.io/zone", "NotIn", ["z2"])])]
+    cluster, _ = encode_cluster(nodes, bound)
+    eng, st = _run(cluster, encode_pods(cluster, inc))
+    assert st.perpod_cycles == sum(1 for p in inc if p.required_terms) and eng.diag()["tb_variant_pods"] > 0

@@ -183,6 +183,7 @@ struct TbVar {
   int32_t nslot;                   // slots (1 without an adder)
   int32_t ndom;                    // domains of the key (value ids 1 .. ndom)
   int32_t col;                     // the key column
+  int32_t vcol;                    // the run's variant column (PodPlan kPlanVcolShift of its first pod; -1: none)
   uint32_t zmask;                  // score slots constant 0 for the pod (k_tb_filter)
   int32_t slot_of[kVarSlots];      // slot by the adder's landing domain (0: it moves no count)
   uint32_t mask[kVarSlots];        // feasible domains per slot (bit d - 1)
@@ -301,6 +302,10 @@ struct DevScratch {
   TbDom* tb_dom;         // [kTbPods][kVarDom] variant pods: counters and extrema per domain of the variant key
   int32_t* tb_vhold;     // [kTbPods][kVarSlots][2 * KSIM_MAX_SCORE] variant pods: extremum holders per slot
   int32_t* tb_slot;      // [kTbPods] the slot the chain took per pod (k_tb_chain_pairs block 0)
+  uint8_t* tb_vdom;      // [kTbPods][n] value ids: the pod's variant key (low nibble), the run's variant column (high)
+  uint8_t* tb_cdom;      // [kTbPods][kVarSlots][kTbMaxBlocks][T] the block lists' run-column value ids
+  uint8_t* tb_kdom;      // [kTbPods][kVarSlots][T] the merged lists' run-column value ids (the chain's slot map)
+  int32_t* tb_vnf;       // [kTbPods][kVarSlots] feasible nodes per slot (k_tb_select block 0)
   unsigned long long* tb_vpods;   // [1] committed pods whose zone verdicts moved inside their batch (ksim_get_diag)
   uint64_t* tb_clist;    // [kTbPods][kTbMaxBlocks][T] each node block's exact top-T keys
   int32_t* tb_ccnt;      // [kTbPods][kTbMaxBlocks] their counts

@@ -2172,6 +2172,10 @@ int ksim_set_cluster(ksim_handle* h, const ksim_node_table* t, const ksim_vocab*
   SCR(s.tb_dom, TbDom*, sizeof(TbDom) * (size_t)kTbPods * kVarDom);
   SCR(s.tb_vhold, int32_t*, 4 * (size_t)kTbPods * kVarSlots * 2 * KSIM_MAX_SCORE);
   SCR(s.tb_slot, int32_t*, 4 * (size_t)kTbPods);
+  SCR(s.tb_vdom, uint8_t*, (size_t)kTbPods * NT);
+  SCR(s.tb_cdom, uint8_t*, (size_t)kTbPods * kVarSlots * kTbMaxBlocks * kTopT);
+  SCR(s.tb_kdom, uint8_t*, (size_t)kTbPods * kVarSlots * kTopT);
+  SCR(s.tb_vnf, int32_t*, 4 * (size_t)kTbPods * kVarSlots);
   SCR(s.tb_vpods, unsigned long long*, 8);
   SCR(s.tb_clist, uint64_t*, 8 * (size_t)kTbPods * kVarSlots * kTbMaxBlocks * kTopT);
   SCR(s.tb_ccnt, int32_t*, 4 * (size_t)kTbPods * kVarSlots * kTbMaxBlocks);

@@ -67,17 +67,29 @@ __device__ __forceinline__ int32_t tb_count(const DevState* __restrict__ st, con
 struct TbSlice {
   uint8_t* fail;
   uint8_t* ign;
+  uint8_t* vdom;                                   // value ids: the pod's variant key | the run's variant column << 4
   int64_t* part;
   int64_t* raw;
   WinState* win;
 };
 __device__ __forceinline__ TbSlice tb_slice(const DevScratch& s, int32_t j, int32_t n) {
   const size_t N = (size_t)n;
-  return TbSlice{s.tb_fail + j * N, s.tb_ign + j * N, s.tb_part + j * N, s.tb_raw + (size_t)j * KSIM_MAX_SCORE * N,
-                 s.tb_win + j};
+  return TbSlice{s.tb_fail + j * N, s.tb_ign + j * N, s.tb_vdom + j * N, s.tb_part + j * N,
+                 s.tb_raw + (size_t)j * KSIM_MAX_SCORE * N, s.tb_win + j};
 }
 // Pod j's list / stat / holder slot sl (0 for a pod without variants).
 __device__ __forceinline__ size_t tb_pj(int32_t j, int32_t sl) { return (size_t)j * kVarSlots + sl; }
+
+// KSIM_TB_CLOCKS builds (100 MHz realtime, summed into s.dbg, ksim_get_diag
+// out[3..18]): k_tb_chain_pairs block 0 -- [0] chain prologue, [1] rounds,
+// [2] rounds run, [3] chain + pairs, [4] launches; k_tb_filter every block --
+// [5] start to the topology setup, [6] the filter and score plans, [7] the
+// extrema and slots, [8] blocks.
+#ifdef KSIM_TB_CLOCKS
+#define TB_CLOCK(var) const uint64_t var = __builtin_amdgcn_s_memrealtime()
+#else
+#define TB_CLOCK(var) do {} while (0)
+#endif
 
 // A variant pod's constraint skew passes on every node in k_tb_filter (the
 // slots take the verdicts per domain): a critical-path minimum no count reaches.
@@ -167,7 +179,8 @@ __device__ __forceinline__ void tb_dom_extrema(const ksim_profile& prof, TbDom* 
 // skew passes; equal sets share a slot.  The same verdict as pts_filter with
 // topo_block_setup's critical path over the moved counts.
 __device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods& P, const DevScratch& s,
-                                          const DevState* __restrict__ st, int32_t j, int32_t vu, uint32_t zmask) {
+                                          const DevState* __restrict__ st, int32_t j, int32_t vu, uint32_t zmask,
+                                          int32_t vcol) {
   const int lane = threadIdx.x & 63;
   TbVar* out = s.tb_var + j;
   if (vu < 0) {
@@ -177,6 +190,7 @@ __device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods&
       V.adder = -1;
       V.nslot = 1;
       V.col = -1;
+      V.vcol = vcol;
       V.zmask = zmask;
       V.mask[0] = ~0u;
       *out = V;
@@ -188,7 +202,6 @@ __device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods&
   const ksim_topo_use u = load_use(P.uses + p.use_first, vu);
   const int32_t nd = c.col_nvals[u.col] - 1;        // 1 .. kVarDom (k_tb_filter)
   const uint32_t self = (P.plans[base + j].m.self_match >> vu) & 1u;
-  const int32_t vcol = (int32_t)(P.plans[base].flags >> kPlanVcolShift) - 1;
   int32_t ne = 0, cx = 0;
   if (lane < j) {
     const ksim_pod& pk = P.pods[base + lane];
@@ -219,6 +232,7 @@ __device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods&
   V.adder = adder;
   V.ndom = nd;
   V.col = u.col;
+  V.vcol = vcol;
   V.zmask = zmask;
   V.nslot = 0;
   const int32_t wmax = adder >= 0 ? nd : 0;
@@ -245,9 +259,13 @@ __device__ __forceinline__ void tb_var_setup(const DevCluster& c, const DevPods&
   *out = V;
 }
 
-// Three waves per SIMD (152 VGPRs, no spills) instead of the two its 176
+// Three waves per SIMD (156 VGPRs, no spills) instead of the two its 176
 // VGPRs allowed: the kernel waits on its table and row loads most of the time.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
+// KSIM_TB_FILTER_WAVES builds set another occupancy (A/B flavors).
+#ifndef KSIM_TB_FILTER_WAVES
+#define KSIM_TB_FILTER_WAVES 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KSIM_TB_FILTER_WAVES))) void k_tb_filter(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
                                                    DevScratch s, int32_t plain) {
   __shared__ int64_t s_min[KSIM_MAX_USES];
@@ -256,6 +274,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   __shared__ int32_t s_cnt[4][2];
   __shared__ int32_t s_dcnt[4][kVarDom][2];
   __shared__ uint32_t s_tf;
+  TB_CLOCK(f0);
   const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;   // replicas: their range
   const int32_t xr = node < c.eval_hi ? node : c.eval_hi - 1;
   // the node's row does not depend on the pod: its loads go out first
@@ -273,14 +292,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const TbSlice q = tb_slice(s, j, c.n);
   // the zone-variant use (plain launches and keys grown past kVarDom domains: none)
   int32_t vu = plain ? -1 : (int32_t)((pp.flags >> kPlanVuseShift) & 31u) - 1;
+  const int32_t vcol = plain ? -1 : (int32_t)(P0.plans[st->cursor].flags >> kPlanVcolShift) - 1;
   int32_t nd = 0;
-  uint32_t vdom = 0;                               // the node's value id of the variant key
+  uint32_t vdom = 0, rdom = 0;                     // the node's value ids of the variant key / the run's column
   if (vu >= 0) {
     const int32_t col = load_use(U, vu).col;
     nd = c.col_nvals[col] - 1;
     if (nd < 1 || nd > kVarDom) vu = -1;
     else vdom = c.labels[(size_t)col * c.n + xr];
   }
+  if (vcol >= 0) rdom = c.labels[(size_t)vcol * c.n + xr];
   TopoRow t;
   load_topo_row(c, U, p.use_count, m, s, P0.ptab, xr, t);
   const bool pt = (pp.flags & kPlanPtab) != 0;      // the host admits only table-read pods (tbatch_admit)
@@ -289,6 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     if (vu >= 0 && threadIdx.x == 0) s_min[vu] = kVarNoMin;   // after thread 0's critical paths
     __syncthreads();
   }
+  TB_CLOCK(f1);
   const uint32_t tf = pt && (m.aff | m.score) ? s_tf : 0u;
   bool feasible = false, ign = false;
   RawScores rv{};
@@ -299,6 +321,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const uint8_t res = run_filter_plan(c, P, FilterPlan{bp->rank_lo, bp->rank_hi, pp.filter_en}, s_min, tf, p, r,
                                         U, m, t, det);
     q.fail[node] = res;
+    if (vu >= 0 || vcol >= 0) q.vdom[node] = (uint8_t)(min(vdom, 15u) | (min(rdom, 15u) << 4));
     feasible = res == KSIM_PASSED;
     if (feasible) {
 #pragma unroll
@@ -316,6 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   // feasible / ignored counts and the NormalizeScore extrema (k_filter_score's fuse_ext tail)
   const int lane = threadIdx.x & 63;
   const uint64_t fm = __ballot(feasible), im = __ballot(feasible && ign);
+  TB_CLOCK(f2);
   if (lane == 0) {
     s_cnt[threadIdx.x >> 6][0] = (int32_t)__popcll(fm);
     s_cnt[threadIdx.x >> 6][1] = (int32_t)__popcll(im);
@@ -355,19 +379,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     block_extrema(prof, q.win, ix, in, s_red, zmask, s_cnt);
   else
     tb_dom_extrema(prof, s.tb_dom + (size_t)j * kVarDom, nd, zmask, feasible, ign, vdom, ix, in, s_dred, s_dcnt);
-  if (blockIdx.x == 0 && threadIdx.x < 64) tb_var_setup(c, P0, s, st, j, vu, zmask);
+  if (blockIdx.x == 0 && threadIdx.x < 64) tb_var_setup(c, P0, s, st, j, vu, zmask, vcol);
+#ifdef KSIM_TB_CLOCKS
+  if (threadIdx.x == 0) {
+    const uint64_t f3 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&s.dbg[5], (unsigned long long)(f1 - f0));
+    atomicAdd(&s.dbg[6], (unsigned long long)(f2 - f1));
+    atomicAdd(&s.dbg[7], (unsigned long long)(f3 - f2));
+    atomicAdd(&s.dbg[8], 1ull);
+  }
+#endif
 }
 
 // Each block's exact top-T keys of pod j over its 256 nodes: every wave
 // extracts its own top-T (kTopT rounds of DPP max), wave 0 ranks the 4 T
-// candidates (keys are unique: ranks are distinct).
-__device__ __forceinline__ void block_top_t(uint64_t key, uint64_t* s_cand, uint64_t* out, int32_t* out_cnt) {
+// candidates (keys are unique: ranks are distinct).  kd / out_dom (nullable):
+// a byte carried with each key (the run-column value id of its node).
+__device__ __forceinline__ void block_top_t(uint64_t key, uint32_t kd, uint64_t* s_cand, uint8_t* s_cdom,
+                                            uint64_t* out, uint8_t* out_dom, int32_t* out_cnt) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t a = key;
 #pragma unroll 1
   for (int e = 0; e < kTopT; e++) {
     const uint64_t mx = wave_max_u64_dpp(a);
     if (lane == 0) s_cand[wv * kTopT + e] = mx;
+    if (a == mx && a != 0) s_cdom[wv * kTopT + e] = (uint8_t)kd;   // the one lane holding it
     if (a == mx) a = 0;                            // 0 stays 0: an exhausted wave lists zeros
   }
   __syncthreads();
@@ -375,33 +411,45 @@ __device__ __forceinline__ void block_top_t(uint64_t key, uint64_t* s_cand, uint
   constexpr int kC = 4 * kTopT;
   static_assert(kC <= 64, "block_top_t geometry");
   const uint64_t c0 = lane < kC ? s_cand[lane] : 0;
+  const uint8_t d0 = lane < kC ? s_cdom[lane] : 0;
   int32_t rank = 0;
 #pragma unroll
   for (int x = 0; x < kC; x++) rank += s_cand[x] > c0;
   const int32_t n = __popcll(__ballot(c0 != 0));
-  if (c0 != 0 && rank < kTopT) out[rank] = c0;
+  if (c0 != 0 && rank < kTopT) {
+    out[rank] = c0;
+    if (out_dom) out_dom[rank] = d0;
+  }
   if (lane >= n && lane < kTopT) out[lane] = 0;
   if (lane == 0) *out_cnt = n < kTopT ? n : kTopT;
 }
 
+// The filter's per-node outputs and the pod's variant record are read before
+// the batch state (they do not depend on it): a kernel that waited for the
+// state first would pay one more global round trip (data the previous launch
+// wrote sits in another XCD's L2).
 __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
                                                    DevScratch s, int32_t plain) {
   __shared__ uint64_t s_cand[4 * kTopT];
+  __shared__ uint8_t s_cdom[4 * kTopT];
   __shared__ int32_t s_hold[4][4];
   const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t j = blockIdx.y;
+  const int32_t N = c.n;
+  const TbSlice q = tb_slice(s, j, N);
+  const bool live = node < c.eval_hi;
+  const uint8_t fail = live ? q.fail[node] : (uint8_t)0;
+  const uint8_t vd = live ? q.vdom[node] : (uint8_t)0;
+  const TbVar& V = s.tb_var[j];
+  const int32_t ns = V.nslot, vuse = V.use, vcol = V.vcol;
   if (j >= tb_count(st, P0, plain)) return;         // block-uniform
   const ksim_profile& prof = *prof_p;
-  const int32_t N = c.n;
   const int S = prof.n_score;
   const int32_t pi = st->cursor + j;
   const ksim_pod& p = P0.pods[pi];
   const UseMasks m = P0.plans[pi].m;
   const ksim_topo_use* U = P0.uses + p.use_first;
-  const TbSlice q = tb_slice(s, j, N);
-  const TbVar& V = s.tb_var[j];
-  const int32_t ns = V.nslot, vuse = V.use;
   const int soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
   int32_t ms = 0;                                  // topologyNormalizingWeight inputs (hostname keys only: tbatch_admit)
   bool soft_hn = false;
@@ -415,10 +463,8 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
   const int k_fit = plan_slot(sp, KSIM_PL_NODE_RESOURCES_FIT), k_ba = plan_slot(sp, KSIM_PL_BALANCED_ALLOCATION);
   const uint64_t seed = prof.tiebreak_seed;
   const int64_t seq = st->pod_seq + j;
-  const bool live = node < c.eval_hi;
-  const bool pass = live && q.fail[node] == KSIM_PASSED;
-  uint32_t dom = 0;
-  if (vuse >= 0 && live) dom = c.labels[(size_t)V.col * c.n + node];
+  const bool pass = live && fail == KSIM_PASSED;
+  const uint32_t dom = vd & 15u, rdom = vd >> 4;
   const bool ign0 = pass && q.ign[node] != 0;
   const bool cross = (P0.bflags[st->cursor] & kPodTbCross) != 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -427,6 +473,7 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
     const uint32_t mk = vuse >= 0 ? V.mask[sl] : ~0u;
     int32_t nf, nign;
     tb_slot_counts(s, j, V, mk, nf, nign);
+    if (blockIdx.x == 0 && threadIdx.x == 0) s.tb_vnf[tb_pj(j, sl)] = nf;
     const bool has_soft = nf > 1 && soft >= 0;
     const double w_soft = has_soft ? c.topo_log[soft_hn ? nf - nign : 0] : 0.0;
     const bool feas = pass && (vuse < 0 || (dom >= 1 && dom <= (uint32_t)kVarDom && ((mk >> (dom - 1)) & 1u)));
@@ -484,8 +531,9 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
         if (lane == 0) s_hold[wv][h] = n;
       }
     }
-    block_top_t(key, s_cand, s.tb_clist + (tb_pj(j, sl) * kTbMaxBlocks + blockIdx.x) * kTopT,
-                s.tb_ccnt + tb_pj(j, sl) * kTbMaxBlocks + blockIdx.x);
+    const size_t cb = tb_pj(j, sl) * kTbMaxBlocks + blockIdx.x;
+    block_top_t(key, rdom, s_cand, s_cdom, s.tb_clist + cb * kTopT, vcol >= 0 ? s.tb_cdom + cb * kTopT : nullptr,
+                s.tb_ccnt + cb);
     if (cross && threadIdx.x < 4) {
       int kp = -1, ki = -1;                        // the profile's slots (block-uniform)
       for (int k = 0; k < S; k++) {
@@ -503,39 +551,56 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
 
 // Pod j's exact top-T of slot sl from its blocks' exact lists (the pod's
 // top-T lies in the union of the blocks' top-T): one wave, lane b holds block
-// b's list.  xsend (replicas, slot 0): the record [kTbPods][kTbXRec] of this
-// replica's range (keys, count, holder counts) instead of the pod's lists.
+// b's list (loaded before the batch state, as in k_tb_select), with the
+// run-column value id of each key.  xsend (replicas, slot 0): the record
+// [kTbPods][kTbXRec] of this replica's range (keys, count, holder counts)
+// instead of the pod's lists.
 __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const DevState* __restrict__ st,
                                                  DevScratch s, uint64_t* __restrict__ xsend, int32_t plain) {
   const int lane = threadIdx.x;
   const int32_t j = blockIdx.x, sl = blockIdx.y;
-  if (j >= tb_count(st, P, plain)) return;
-  if (sl >= s.tb_var[j].nslot) return;
   const size_t pj = tb_pj(j, sl);
   const int32_t nblk = (c.eval_hi - c.eval_lo + 255) / 256;
-  uint64_t L[kTopT];
-  int32_t cnt = 0;
   const size_t cl = pj * kTbMaxBlocks + lane;
+  uint64_t L[kTopT];
+  uint32_t Ld = 0;                                 // value ids, 4 bits per entry
+  int32_t cnt = 0;
   if (lane < nblk) {
     cnt = s.tb_ccnt[cl];
 #pragma unroll
     for (int e = 0; e < kTopT; e++) L[e] = s.tb_clist[cl * kTopT + e];
+    if (!plain) {
+      const uint64_t db = *reinterpret_cast<const uint64_t*>(s.tb_cdom + cl * kTopT);
+#pragma unroll
+      for (int e = 0; e < kTopT; e++) Ld |= (uint32_t)((db >> (8 * e)) & 15u) << (4 * e);
+    }
   }
+  const int32_t nslot = s.tb_var[j].nslot, vcol = s.tb_var[j].vcol;
+  const int32_t nf = s.tb_vnf[pj];
+  if (j >= tb_count(st, P, plain)) return;
+  if (sl >= nslot) return;
 #pragma unroll
   for (int e = 0; e < kTopT; e++)
     if (e >= cnt) L[e] = 0;
   uint64_t mine = 0;
+  uint32_t mdom = 0;
   int32_t n = 0;
 #pragma unroll 1
   for (int e = 0; e < kTopT; e++) {
     const uint64_t mx = wave_max_u64_dpp(L[0]);
     if (mx == 0) break;
-    if (lane == e) mine = mx;
+    const uint64_t own = __ballot(L[0] == mx);     // keys are unique: one lane
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)(Ld & 15u), (int)__builtin_ctzll(own));
+    if (lane == e) {
+      mine = mx;
+      mdom = d;
+    }
     n = e + 1;
     if (L[0] == mx) {                              // pop the head (a register shift)
 #pragma unroll
       for (int x = 0; x + 1 < kTopT; x++) L[x] = L[x + 1];
       L[kTopT - 1] = 0;
+      Ld >>= 4;
     }
   }
   if (xsend) {
@@ -547,12 +612,12 @@ __global__ __launch_bounds__(64) void k_tb_merge(DevCluster c, DevPods P, const 
                             ((uint64_t)(uint32_t)s.tb_win[j].hold[2 * lane + 1] << 32);
     return;
   }
-  if (lane < kTopT) s.topk[pj * kTopT + lane] = lane < n ? mine : 0;
+  if (lane < kTopT) {
+    s.topk[pj * kTopT + lane] = lane < n ? mine : 0;
+    if (vcol >= 0) s.tb_kdom[pj * kTopT + lane] = (uint8_t)(lane < n ? mdom : 0u);
+  }
   if (lane == 0) {
     s.topk_cnt[pj] = n;
-    const TbVar& V = s.tb_var[j];
-    int32_t nf, nign;
-    tb_slot_counts(s, j, V, V.use >= 0 ? V.mask[sl] : ~0u, nf, nign);
     s.topk_complete[pj] = nf <= kTopT ? 1 : 0;     // every feasible node listed
   }
 }
@@ -640,107 +705,158 @@ constexpr int kTbHoldSlots = kTbMaxBlocks * 256;
 constexpr int kTbChainRounds = kTbPods + 2;        // pod i is exact after round i + 1
 struct TbChainLds {
   uint32_t hold[kTbHoldSlots];                     // (round << 8) | (255 - pod): the lowest pod guessing the node
-  uint64_t lst[kTbPods][kVarSlots][kTopT];         // each pod's lists per slot
-  uint8_t dom[kTbPods][kVarSlots][kTopT];          // the listed nodes' value ids of the run's variant key column
-  int32_t cnt[kTbPods][kVarSlots], comp[kTbPods][kVarSlots], slot_of[kTbPods][kVarSlots];
+  uint64_t lst[kTbPods][kVarSlots][kTopT];         // each pod's lists per slot (the keys of the guesses)
   uint64_t gk[kTbPods];
   int32_t slot[kTbPods];
   int32_t nchain;
 };
+
+
+// The chain's inputs for lane i = pod i (every pod slot, every list slot:
+// none of it waits for the batch state), in registers.
+struct TbChainIn {
+  uint64_t k0[kVarSlots][kTopT];                   // the lists' keys
+  uint64_t dk[kVarSlots];                          // their run-column value ids, a byte each
+  int32_t cnt[kVarSlots], comp[kVarSlots];
+  int32_t nslot, adder;
+  uint32_t sopk;                                   // slot_of, 3 bits per landing domain
+};
+__device__ __forceinline__ void tb_chain_load(TbChainIn& in, const DevScratch& s) {
+  const int i = threadIdx.x;                       // wave 0
+  in.nslot = 0;
+  in.adder = -1;
+  in.sopk = 0;
+#pragma unroll
+  for (int sl = 0; sl < kVarSlots; sl++) {
+    in.cnt[sl] = in.comp[sl] = 0;
+    in.dk[sl] = 0;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) in.k0[sl][e] = 0;
+  }
+  if (i >= kTbPods) return;
+  const TbVar& V = s.tb_var[i];
+  in.nslot = V.nslot;
+  in.adder = V.adder;
+#pragma unroll
+  for (int w = 0; w < kVarSlots; w++) in.sopk |= (uint32_t)V.slot_of[w] << (3 * w);
+#pragma unroll
+  for (int sl = 0; sl < kVarSlots; sl++) {
+    const size_t pj = tb_pj(i, sl);
+    in.cnt[sl] = s.topk_cnt[pj];
+    in.comp[sl] = s.topk_complete[pj];
+    in.dk[sl] = *reinterpret_cast<const uint64_t*>(s.tb_kdom + pj * kTopT);
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) in.k0[sl][e] = s.topk[pj * kTopT + e];
+  }
+}
 
 // The greedy chain of one topology batch in one wave (lane i = pod i < nb):
 // each pod takes the first entry of its current slot's list that no earlier
 // pod guesses, its slot being the one its adder's current guess lands in
 // (slot 0 without an adder).  Rounds run to the fixpoint: pod i depends only
 // on pods before it, so pods [0, r) are exact after round r.  Then the exact
-// prefix is cut before a pod whose incomplete list ran out.  Writes L.gk
-// (0: none or past the prefix), L.slot and L.nchain.
-__device__ __forceinline__ void tb_chain(TbChainLds& L, const DevCluster& c, const DevPods& P,
-                                         const DevState* __restrict__ st, const DevScratch& s, int32_t nb,
-                                         int32_t plain) {
+// prefix is cut before a pod whose incomplete list ran out.  The lists' node
+// ids, value ids, counts and slot map stay in registers (a round is one LDS
+// atomic, one lane exchange and one batch of independent guess-table reads).
+// Writes L.gk (0: none or past the prefix), L.slot and L.nchain.
+__device__ __forceinline__ void tb_chain(TbChainLds& L, const TbChainIn& in, int32_t nb, int32_t vcol,
+                                         unsigned long long* __restrict__ dbg, uint64_t t0) {
   const int i = threadIdx.x;                       // wave 0
   const bool live = i < nb;
-  const int32_t vcol = plain ? -1 : (int32_t)(P.plans[st->cursor].flags >> kPlanVcolShift) - 1;
-  int32_t nslot = 0, adder = -1;
-  if (live) {
-    const TbVar& V = s.tb_var[i];
-    nslot = V.nslot;
-    adder = V.adder;
+  const int32_t nslot = live ? in.nslot : 0, adder = live ? in.adder : -1;
+  const uint32_t sopk = in.sopk;
+  uint32_t cpk = 0, comp = 0;                      // counts (4 bits per slot), complete flags (1 bit per slot)
 #pragma unroll
-    for (int w = 0; w < kVarSlots; w++) L.slot_of[i][w] = V.slot_of[w];
-  }
-  // the lists, then the listed nodes' domains and their guess-table entries
-  uint64_t k0[kVarSlots][kTopT];
-  int32_t c0[kVarSlots];
-#pragma unroll
-  for (int sl = 0; sl < kVarSlots; sl++) {
-    c0[sl] = 0;
-#pragma unroll
-    for (int e = 0; e < kTopT; e++) k0[sl][e] = 0;
+  for (int sl = 0; sl < kVarSlots; sl++)
     if (sl < nslot) {
-      const size_t pj = tb_pj(i, sl);
-      c0[sl] = s.topk_cnt[pj];
-      L.comp[i][sl] = s.topk_complete[pj];
-#pragma unroll
-      for (int e = 0; e < kTopT; e++) k0[sl][e] = s.topk[pj * kTopT + e];
+      cpk |= (uint32_t)min(in.cnt[sl], kTopT) << (4 * sl);
+      comp |= (in.comp[sl] ? 1u : 0u) << sl;
     }
-  }
+  static_assert(kTopT <= 15 && 4 * kTopT <= 32, "tb_chain packing");
+  int32_t nn[kVarSlots][kTopT];                    // node ids (-1 past the count)
+  uint32_t dpk[kVarSlots];                         // value ids, 4 bits per entry
 #pragma unroll
   for (int sl = 0; sl < kVarSlots; sl++) {
-    if (sl >= nslot) continue;
-    L.cnt[i][sl] = c0[sl];
+    dpk[sl] = 0;
+    const int32_t cn = (int32_t)((cpk >> (4 * sl)) & 15u);
 #pragma unroll
     for (int e = 0; e < kTopT; e++) {
-      L.lst[i][sl][e] = k0[sl][e];
-      uint8_t d = 0;
-      if (e < c0[sl]) {
-        const int32_t nd = key_node(k0[sl][e]);
-        L.hold[nd & (kTbHoldSlots - 1)] = 0u;
-        if (vcol >= 0) d = (uint8_t)min(c.labels[(size_t)vcol * c.n + (nd - c.base)], (uint32_t)kVarDom);
+      nn[sl][e] = e < cn ? key_node(in.k0[sl][e]) : -1;
+      if (sl < nslot) L.lst[i][sl][e] = in.k0[sl][e];
+      if (nn[sl][e] >= 0) {
+        L.hold[nn[sl][e] & (kTbHoldSlots - 1)] = 0u;
+        if (vcol >= 0) dpk[sl] |= (uint32_t)min((uint32_t)((in.dk[sl] >> (8 * e)) & 255u), (uint32_t)kVarDom) << (4 * e);
       }
-      L.dom[i][sl][e] = d;
     }
   }
   wave_lds_sync();
-  int cs = 0, ca = (live && c0[0] > 0) ? 0 : -1;   // current slot and entry
-  int32_t gnode = ca >= 0 ? key_node(k0[0][0]) : -1;
-  int32_t gdom = ca >= 0 ? L.dom[i][0][0] : 0;
-  int32_t first = nb;
+  TB_CLOCK(t1);
+  int cs = 0, ca = (live && (cpk & 15u)) ? 0 : -1;  // current slot and entry
+  int32_t gnode = ca >= 0 ? nn[0][0] : -1;
+  int32_t gdom = ca >= 0 ? (int32_t)(dpk[0] & 15u) : 0;
+  int32_t first = nb, rounds = 0;
   for (int32_t r = 1; r <= kTbChainRounds; r++) {
+    rounds = r;
     if (gnode >= 0) atomicMax(&L.hold[gnode & (kTbHoldSlots - 1)], ((uint32_t)r << 8) | (uint32_t)(255 - i));
     wave_lds_sync();
     const int32_t ad = __shfl(gdom, adder >= 0 ? adder : 0, 64);
-    const int ns = (live && adder >= 0) ? L.slot_of[i][ad] : 0;
-    const int32_t cn = live ? L.cnt[i][ns] : 0;
+    const int ns = (live && adder >= 0) ? (int)((sopk >> (3 * ad)) & 7u) : 0;
+    const int32_t cn = (int32_t)((cpk >> (4 * ns)) & 15u);
+    int32_t sel[kTopT];
+    uint32_t dsel = dpk[0];
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) sel[e] = nn[0][e];
+#pragma unroll
+    for (int sl = 1; sl < kVarSlots; sl++) {
+      const bool on = ns == sl;
+      dsel = on ? dpk[sl] : dsel;
+#pragma unroll
+      for (int e = 0; e < kTopT; e++) sel[e] = on ? nn[sl][e] : sel[e];
+    }
+    uint32_t h[kTopT];                             // independent reads, one wait
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) h[e] = L.hold[(sel[e] >= 0 ? sel[e] : 0) & (kTbHoldSlots - 1)];
     int na = -1;
 #pragma unroll
-    for (int e = 0; e < kTopT; e++) {
-      if (e >= cn || na >= 0) continue;
-      const int32_t nd = key_node(L.lst[i][ns][e]);
-      const uint32_t h = L.hold[nd & (kTbHoldSlots - 1)];
-      const bool held = (h >> 8) == (uint32_t)r && (int)(255 - (h & 255u)) < i;
-      if (!held) na = e;
+    for (int e = kTopT - 1; e >= 0; e--) {
+      const bool held = (h[e] >> 8) == (uint32_t)r && (int)(255 - (h[e] & 255u)) < i;
+      if (e < cn && !held) na = e;
     }
     const uint64_t chg = __ballot(live && (ns != cs || na != ca));
     cs = ns;
     ca = na;
-    gnode = ca >= 0 ? key_node(L.lst[i][cs][ca]) : -1;
-    gdom = ca >= 0 ? L.dom[i][cs][ca] : 0;
-    wave_lds_sync();                               // this round's reads before the next round's registrations
+    int32_t g = -1;
+#pragma unroll
+    for (int e = 0; e < kTopT; e++) g = e == na ? sel[e] : g;
+    gnode = g;
+    gdom = na >= 0 ? (int32_t)((dsel >> (4 * na)) & 15u) : 0;
     if (!chg) {
       first = nb;
       break;
     }
     first = (int32_t)__builtin_ctzll(chg);
   }
+  TB_CLOCK(t2);
   // exact prefix [0, first); an exhausted incomplete list inside it cuts the chain
-  const uint64_t bad = __ballot(live && i < first && ca < 0 && !L.comp[i][cs]);
+  const uint64_t bad = __ballot(live && i < first && ca < 0 && !((comp >> cs) & 1u));
   const int32_t nchain = bad ? min(first, (int32_t)__builtin_ctzll(bad)) : first;
   if (i < kTbPods) {
     L.gk[i] = (i < nchain && ca >= 0) ? L.lst[i][cs][ca] : 0;
     L.slot[i] = cs;
   }
   if (i == 0) L.nchain = nchain;
+#ifdef KSIM_TB_CLOCKS
+  if (i == 0 && dbg && blockIdx.x == 0) {
+    atomicAdd(&dbg[0], (unsigned long long)(t1 - t0));
+    atomicAdd(&dbg[1], (unsigned long long)(t2 - t1));
+    atomicAdd(&dbg[2], (unsigned long long)rounds);
+    atomicAdd(&dbg[4], 1ull);
+  }
+#else
+  (void)dbg;
+  (void)t0;
+  (void)rounds;
+#endif
 }
 
 // Block j: the chain, then pod j's keys on the guesses of pods k < j after
@@ -752,9 +868,11 @@ __device__ __forceinline__ void tb_chain(TbChainLds& L, const DevCluster& c, con
 // slot's stat with the resource part and the changed PodTopologySpread /
 // InterPodAffinity raw scores recomputed against the slot's extrema; pinv
 // when a change would move an extremum, the feasible set (a node's verdict)
-// or an emptiness flag.
+// or an emptiness flag.  What does not depend on the guesses (the lists, pod
+// k's requests and add entries) is loaded before the chain runs.
 // pp (replicas): pair maxima and pinv into pp[j] / pp[kTbPods + j], keyed
 // only on the guesses in this replica's range (the all-reduce max combines).
+constexpr int kPairAdds = 4;                       // pod k's add entries held in registers
 __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, DevPods P,
                                                                const ksim_profile* __restrict__ prof_p,
                                                                const BatchProg* __restrict__ bp_p,
@@ -763,13 +881,37 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   __shared__ TbChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   __shared__ int32_t s_winv[kBatchPods / 64];
+  uint64_t t0 = 0;
+#ifdef KSIM_TB_CLOCKS
+  t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  TbChainIn in;
+  if (threadIdx.x < 64) tb_chain_load(in, s);
   const int32_t nbt = tb_count(st, P, plain);
   if (nbt <= 0) return;                            // block-uniform
-  if (threadIdx.x < 64) tb_chain(L, c, P, st, s, nbt, plain);
-  __syncthreads();
-  const int32_t nchain = L.nchain;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
+  const int32_t base = st->cursor;
+  // pod k's requests and first add entries (its pair's guess-independent inputs)
+  const bool kin = k < j && k < nbt;
+  ksim_pod pk{};
+  int32_t acls[kPairAdds], acnt[kPairAdds];
+#pragma unroll
+  for (int a = 0; a < kPairAdds; a++) acls[a] = acnt[a] = 0;
+  if (kin) {
+    pk = P.pods[base + k];
+#pragma unroll
+    for (int a = 0; a < kPairAdds; a++)
+      if (a < pk.add_count) {
+        const ksim_class_add x = P.adds[pk.add_first + a];
+        acls[a] = x.cls;
+        acnt[a] = x.count;
+      }
+  }
+  if (threadIdx.x < 64)
+    tb_chain(L, in, nbt, plain ? -1 : (int32_t)(P.plans[base].flags >> kPlanVcolShift) - 1, s.dbg, t0);
+  __syncthreads();
+  const int32_t nchain = L.nchain;
   const uint64_t gk = k < nbt ? L.gk[k] : 0;
   if (j == 0) {
     if (tid < nbt) {
@@ -792,7 +934,6 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   }
   const ksim_profile& prof = *prof_p;
   const BatchProg& bp = *bp_p;
-  const int32_t base = st->cursor;
   const int64_t seq0 = st->pod_seq;
   const int32_t N = c.n;
   const ksim_pod& p = P.pods[base + j];
@@ -805,8 +946,11 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
   if (local >= 0 && local < N) {
     const bool own = local >= c.eval_lo && local < c.eval_hi;   // S0 values of g live on its replica
+    // the guess's loads first, all independent
+    const int32_t sv = own ? s.tb_stat[tb_pj(j, sj) * N + local] : kStatNone;
+    NodeRow r{};
+    if (own) r = load_row(c, local);
     // what pod k's adds change for pod j on g = local (runs that cross only)
-    const ksim_pod& pk = P.pods[base + k];
     int64_t d_soft = 0, d_ipa = 0;
     bool hit_anti = false, hit_aff = false, hit_score = false;
     UseMasks m{};
@@ -826,7 +970,9 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
       const ksim_topo_use u = load_use(U, i);
       if (u.cls < 0) continue;
       int32_t d = 0;
-      for (int a = 0; a < pk.add_count; a++) {
+#pragma unroll
+      for (int a = 0; a < kPairAdds; a++) d += acls[a] == u.cls && a < pk.add_count ? acnt[a] : 0;
+      for (int a = kPairAdds; a < pk.add_count; a++) {
         const ksim_class_add x = P.adds[pk.add_first + a];
         if (x.cls == u.cls) d += x.count;
       }
@@ -847,10 +993,8 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     }
     if (hit_aff && !(tf & kTopoAffinityNonEmpty)) inv = true;   // len(affinityCounts) would change
     if (hit_score && !(tf & kTopoScoreNonEmpty)) inv = true;    // len(topologyScore) would change
-    const int32_t sv = own ? s.tb_stat[tb_pj(j, sj) * N + local] : kStatNone;
     if (!own) {
     } else if (sv != kStatNone) {
-      NodeRow r = load_row(c, local);
       row_add_pod(r, pk, 1);
       if (hit_anti || (bp.has_fit_filter && fits_request(r, p, c.n_scalar, c.fit_ignore))) {
         inv = true;                                // a node of the slot's feasible set stops passing
@@ -921,6 +1065,9 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
         s.pmax[j] = mx;
         s.pinv[j] = any;
       }
+#ifdef KSIM_TB_CLOCKS
+      if (j == 0) atomicAdd(&s.dbg[3], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+#endif
     }
   }
 }
@@ -939,10 +1086,10 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
   const uint64_t m = pp ? (tid < kTbPods ? pp[tid] : 0) : s.pmax[tid];
   const int32_t inv = tid < kTbPods ? (pp ? (int32_t)(pp[kTbPods + tid] != 0) : s.pinv[tid]) : 0;
   const int32_t nchain = *s.chain_end;
+  const int32_t vslot = tid < kTbPods ? s.tb_slot[tid] : 0;
   const int32_t base = st->cursor;
   const int32_t nbt = tb_count(st, P, plain);
   if (nbt <= 0) return;
-  const int32_t vslot = tid < nbt ? s.tb_slot[tid] : 0;
   batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt,
                s_node);
   __syncthreads();
@@ -966,7 +1113,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
       }
   }
   // committed pods whose slot moved their zone verdicts (ksim_get_diag out[26])
-  const uint64_t vb = __ballot(tid < nbt && s_node[tid < kTbPods ? tid : 0] != -2 && vslot != 0);
+  const uint64_t vb = __ballot(tid < nbt && s_node[tid < kTbPods ? tid : 0] != -2 && vslot != 0);   // (tid < nbt)
   if ((tid & 63) == 0 && vb) atomicAdd(s.tb_vpods, (unsigned long long)__popcll(vb));
   // the next batch's counters and extrema start from zero (the rows this batch used)
   for (int x = tid; x < kTbPods * (int)(sizeof(WinState) / 4); x += blockDim.x)

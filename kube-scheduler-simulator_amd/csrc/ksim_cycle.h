@@ -45,7 +45,7 @@ __device__ __forceinline__ void block_extrema(const ksim_profile& prof, WinState
       s_red[wv][2 * k + 1] = b;
     }
   }
-  __syncthreads();
+  lds_barrier();                                   // an LDS hand-off: the caller's stores stay in flight
   if (tid < 2 * KSIM_MAX_SCORE && tid < 2 * S && norm_kind(prof.score[tid >> 1]) != kNormNone) {
     uint64_t m = 0;
     if ((zmask >> (tid >> 1)) & 1u) {

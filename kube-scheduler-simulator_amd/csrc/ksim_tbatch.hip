@@ -84,7 +84,9 @@ __device__ __forceinline__ size_t tb_pj(int32_t j, int32_t sl) { return (size_t)
 // out[3..18]): k_tb_chain_pairs block 0 -- [0] chain prologue, [1] rounds,
 // [2] rounds run, [3] chain + pairs, [4] launches; k_tb_filter every block --
 // [5] start to the topology setup, [6] the filter and score plans, [7] the
-// extrema and slots, [8] blocks.
+// extrema and slots, [8] blocks; k_tb_select every block -- [9] start to the
+// pod's inputs, [10] the slots, [11] blocks, [12] slots; k_tb_chain_pairs
+// every block that keys pairs -- [13] start to the pair maxima, [14] blocks.
 #ifdef KSIM_TB_CLOCKS
 #define TB_CLOCK(var) const uint64_t var = __builtin_amdgcn_s_memrealtime()
 #else
@@ -156,7 +158,7 @@ __device__ __forceinline__ void tb_dom_extrema(const ksim_profile& prof, TbDom* 
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < nd * 2 * KSIM_MAX_SCORE) {
     const int d = tid / (2 * KSIM_MAX_SCORE), e = tid % (2 * KSIM_MAX_SCORE), k = e >> 1;
     if (k < S && norm_kind(prof.score[k]) != kNormNone && !((zmask >> k) & 1u)) {
@@ -308,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KSIM_TB_FIL
   if (m.hard || (pt && (m.aff | m.score))) {
     topo_block_setup(c, P0, s, U, m, pt, true, s_min, &s_tf, &q.win->tflags);
     if (vu >= 0 && threadIdx.x == 0) s_min[vu] = kVarNoMin;   // after thread 0's critical paths
-    __syncthreads();
+    lds_barrier();
   }
   TB_CLOCK(f1);
   const uint32_t tf = pt && (m.aff | m.score) ? s_tf : 0u;
@@ -406,7 +408,7 @@ __device__ __forceinline__ void block_top_t(uint64_t key, uint32_t kd, uint64_t*
     if (a == mx && a != 0) s_cdom[wv * kTopT + e] = (uint8_t)kd;   // the one lane holding it
     if (a == mx) a = 0;                            // 0 stays 0: an exhausted wave lists zeros
   }
-  __syncthreads();
+  lds_barrier();
   if (wv != 0) return;
   constexpr int kC = 4 * kTopT;
   static_assert(kC <= 64, "block_top_t geometry");
@@ -424,28 +426,51 @@ __device__ __forceinline__ void block_top_t(uint64_t key, uint32_t kd, uint64_t*
   if (lane == 0) *out_cnt = n < kTopT ? n : kTopT;
 }
 
-// The filter's per-node outputs and the pod's variant record are read before
-// the batch state (they do not depend on it): a kernel that waited for the
+// The filter's per-node outputs, the pod's variant record and its counters /
+// extrema (tb_win, or per domain tb_dom, staged in LDS) are read before the
+// batch state: they do not depend on it, and a kernel that waited for the
 // state first would pay one more global round trip (data the previous launch
-// wrote sits in another XCD's L2).
+// wrote sits in another XCD's L2).  Barriers are LDS-only (lds_barrier): the
+// stat stores stay in flight across them.
 __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, const ksim_profile* __restrict__ prof_p,
                                                    const BatchProg* __restrict__ bp, const DevState* __restrict__ st,
                                                    DevScratch s, int32_t plain) {
   __shared__ uint64_t s_cand[4 * kTopT];
   __shared__ uint8_t s_cdom[4 * kTopT];
   __shared__ int32_t s_hold[4][4];
+  __shared__ TbDom s_dom[kVarDom + 1];             // the pod's domains; [kVarDom]: its tb_win counters / extrema
+  TB_CLOCK(x0);
   const int32_t node = c.eval_lo + blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t j = blockIdx.y;
+  const int32_t sl = blockIdx.z;                   // one slot per block: a pod's slots run side by side
+  if (sl > 0 && sl >= s.tb_var[j].nslot) return;   // slot 0 always runs: its loads need not wait for this
   const int32_t N = c.n;
   const TbSlice q = tb_slice(s, j, N);
   const bool live = node < c.eval_hi;
-  const uint8_t fail = live ? q.fail[node] : (uint8_t)0;
-  const uint8_t vd = live ? q.vdom[node] : (uint8_t)0;
-  const TbVar& V = s.tb_var[j];
-  const int32_t ns = V.nslot, vuse = V.use, vcol = V.vcol;
-  if (j >= tb_count(st, P0, plain)) return;         // block-uniform
   const ksim_profile& prof = *prof_p;
   const int S = prof.n_score;
+  const uint8_t fail = live ? q.fail[node] : (uint8_t)0;
+  const uint8_t vd = live ? q.vdom[node] : (uint8_t)0;
+  const bool ign0 = live && q.ign[node] != 0;
+  const int64_t part = live ? q.part[node] : 0;
+  int64_t raw[KSIM_MAX_SCORE];
+#pragma unroll
+  for (int k = 0; k < KSIM_MAX_SCORE; k++) raw[k] = (live && k < S) ? q.raw[(size_t)k * N + node] : 0;
+  {
+    constexpr int W = kVarDom * (int)(sizeof(TbDom) / 4);
+    static_assert(sizeof(TbDom) % 4 == 0, "TbDom by words");
+    const int32_t* src = reinterpret_cast<const int32_t*>(s.tb_dom + (size_t)j * kVarDom);
+    int32_t* dst = reinterpret_cast<int32_t*>(s_dom);
+    if (threadIdx.x < W) dst[threadIdx.x] = src[threadIdx.x];
+    const int x = (int)threadIdx.x - W;
+    if (x >= 0 && x < 2 * KSIM_MAX_SCORE) s_dom[kVarDom].ext[x] = q.win->ext[x];
+    if (x == 2 * KSIM_MAX_SCORE) s_dom[kVarDom].nfeas = q.win->nfeas;
+    if (x == 2 * KSIM_MAX_SCORE + 1) s_dom[kVarDom].nign = q.win->nign;
+  }
+  const TbVar& V = s.tb_var[j];
+  const int32_t ns = V.nslot, vuse = V.use, vcol = V.vcol, vnd = V.ndom;
+  const uint32_t vz = V.zmask;
+  if (j >= tb_count(st, P0, plain) || sl >= ns) return;   // block-uniform
   const int32_t pi = st->cursor + j;
   const ksim_pod& p = P0.pods[pi];
   const UseMasks m = P0.plans[pi].m;
@@ -465,14 +490,42 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
   const int64_t seq = st->pod_seq + j;
   const bool pass = live && fail == KSIM_PASSED;
   const uint32_t dom = vd & 15u, rdom = vd >> 4;
-  const bool ign0 = pass && q.ign[node] != 0;
   const bool cross = (P0.bflags[st->cursor] & kPodTbCross) != 0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int32_t sl = 0; sl < ns; sl++) {
-    if (sl) __syncthreads();                       // s_cand / s_hold of the last slot read
+  lds_barrier();                                   // s_dom
+#ifdef KSIM_TB_CLOCKS
+  const uint64_t x1 = (ms >= 0 && ipa_nonempty >= 0 && seq >= 0 && vd < 255) ? __builtin_amdgcn_s_memrealtime() : 0;
+#endif
+  {
     const uint32_t mk = vuse >= 0 ? V.mask[sl] : ~0u;
-    int32_t nf, nign;
-    tb_slot_counts(s, j, V, mk, nf, nign);
+    // the slot's counters and extrema from the staged records
+    int32_t nf = 0, nign = 0;
+    uint64_t ext[2 * KSIM_MAX_SCORE];
+    if (vuse < 0) {
+      nf = s_dom[kVarDom].nfeas;
+      nign = s_dom[kVarDom].nign;
+#pragma unroll
+      for (int e = 0; e < 2 * KSIM_MAX_SCORE; e++) ext[e] = s_dom[kVarDom].ext[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2 * KSIM_MAX_SCORE; e++) ext[e] = 0;
+#pragma unroll
+      for (int d = 0; d < kVarDom; d++) {
+        if (d >= vnd || !((mk >> d) & 1u)) continue;
+        nf += s_dom[d].nfeas;
+        nign += s_dom[d].nign;
+#pragma unroll
+        for (int e = 0; e < 2 * KSIM_MAX_SCORE; e++) ext[e] = umax64(ext[e], s_dom[d].ext[e]);
+      }
+      if (nf > 0) {                                // slots constant 0 (block_extrema's zmask)
+#pragma unroll
+        for (int k = 0; k < KSIM_MAX_SCORE; k++)
+          if ((vz >> k) & 1u) {
+            ext[2 * k] = max_image(0);
+            ext[2 * k + 1] = min_image(0);
+          }
+      }
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) s.tb_vnf[tb_pj(j, sl)] = nf;
     const bool has_soft = nf > 1 && soft >= 0;
     const double w_soft = has_soft ? c.topo_log[soft_hn ? nf - nign : 0] : 0.0;
@@ -484,13 +537,15 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
       if (feas) {
         if (nf > 1) {
           const bool ign = has_soft && ign0;
-          int64_t tot = S == 0 ? 1 : q.part[node];
-          for (int k = 0; k < S; k++) {
+          int64_t tot = S == 0 ? 1 : part;
+#pragma unroll
+          for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+            if (k >= S) break;
             const int32_t kind = norm_kind(prof_score(prof, k));
             if (kind == kNormNone) continue;
-            const uint64_t ex = tb_slot_ext(s, j, V, mk, nf, 2 * k), en = tb_slot_ext(s, j, V, mk, nf, 2 * k + 1);
+            const uint64_t ex = ext[2 * k], en = ext[2 * k + 1];
             int64_t gmax = from_max_image(ex), gmin = from_min_image(en);
-            const int64_t x = q.raw[(size_t)k * N + node];
+            const int64_t x = raw[k];
             if (kind == kNormIPA) {                // the holders of the extrema (k_tb_chain_pairs)
               hf |= (x == gmax ? 4u : 0u) | (x == gmin ? 8u : 0u);
             } else if (kind == kNormPTS && has_soft && !ign) {
@@ -511,8 +566,11 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
             tot += nv * prof_weight(prof, k);
           }
           int64_t dyn0 = 0;                        // the part a bind on this node moves
-          if (k_fit >= 0) dyn0 += bp->w_fit * q.raw[(size_t)k_fit * N + node];
-          if (k_ba >= 0) dyn0 += bp->w_ba * q.raw[(size_t)k_ba * N + node];
+#pragma unroll
+          for (int k = 0; k < KSIM_MAX_SCORE; k++) {
+            if (k == k_fit) dyn0 += bp->w_fit * raw[k];
+            if (k == k_ba) dyn0 += bp->w_ba * raw[k];
+          }
           stat = (int32_t)(tot - dyn0);
           key = tb_key(tot, seed, seq, c.base + node);
         } else {                                   // one feasible node: schedulePod takes it unscored
@@ -547,6 +605,14 @@ __global__ __launch_bounds__(256) void k_tb_select(DevCluster c, DevPods P0, con
       if (k >= 0 && n) atomicAdd(&hold[2 * k + (h & 1)], n);
     }
   }
+#ifdef KSIM_TB_CLOCKS
+  if (threadIdx.x == 0) {
+    atomicAdd(&s.dbg[9], (unsigned long long)(x1 - x0));
+    atomicAdd(&s.dbg[10], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - x1));
+    atomicAdd(&s.dbg[11], 1ull);
+    atomicAdd(&s.dbg[12], 1ull);
+  }
+#endif
 }
 
 // Pod j's exact top-T of slot sl from its blocks' exact lists (the pod's
@@ -881,17 +947,39 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   __shared__ TbChainLds L;
   __shared__ uint64_t s_wmax[kBatchPods / 64];
   __shared__ int32_t s_winv[kBatchPods / 64];
+  __shared__ TbDom s_dom[kVarDom + 1];             // pod j's domains; [kVarDom]: its tb_win counters / extrema
+  __shared__ ksim_topo_use s_use[KSIM_MAX_USES];   // pod j's uses
+  __shared__ UseMasks s_m;                         // ... and their roles
+  __shared__ int32_t s_nu;
   uint64_t t0 = 0;
 #ifdef KSIM_TB_CLOCKS
   t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  TbChainIn in;
-  if (threadIdx.x < 64) tb_chain_load(in, s);
-  const int32_t nbt = tb_count(st, P, plain);
-  if (nbt <= 0) return;                            // block-uniform
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = blockIdx.x, k = tid;
+  TbChainIn in;
+  if (threadIdx.x < 64) tb_chain_load(in, s);
+  if (tid >= 64) {                                 // pod j's counters and extrema, staged while the chain runs
+    constexpr int W = kVarDom * (int)(sizeof(TbDom) / 4);
+    const int x = tid - 64;
+    if (x < W) reinterpret_cast<int32_t*>(s_dom)[x] = reinterpret_cast<const int32_t*>(s.tb_dom + (size_t)j * kVarDom)[x];
+    const int y = x - W;
+    if (y >= 0 && y < 2 * KSIM_MAX_SCORE) s_dom[kVarDom].ext[y] = s.tb_win[j].ext[y];
+    if (y == 2 * KSIM_MAX_SCORE) s_dom[kVarDom].nfeas = s.tb_win[j].nfeas;
+    if (y == 2 * KSIM_MAX_SCORE + 1) s_dom[kVarDom].nign = s.tb_win[j].nign;
+  }
+  const int32_t nbt = tb_count(st, P, plain);
+  if (nbt <= 0) return;                            // block-uniform
   const int32_t base = st->cursor;
+  if (j < nbt && tid >= 128 && tid < 128 + KSIM_MAX_USES) {   // pod j's uses and roles, staged while the chain runs
+    const ksim_pod& pj = P.pods[base + j];
+    const int x = tid - 128;
+    if (x < pj.use_count) s_use[x] = P.uses[pj.use_first + x];
+    if (x == 0) {
+      s_m = P.plans[base + j].m;
+      s_nu = pj.use_count;
+    }
+  }
   // pod k's requests and first add entries (its pair's guess-independent inputs)
   const bool kin = k < j && k < nbt;
   ksim_pod pk{};
@@ -910,7 +998,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   }
   if (threadIdx.x < 64)
     tb_chain(L, in, nbt, plain ? -1 : (int32_t)(P.plans[base].flags >> kPlanVcolShift) - 1, s.dbg, t0);
-  __syncthreads();
+  lds_barrier();
   const int32_t nchain = L.nchain;
   const uint64_t gk = k < nbt ? L.gk[k] : 0;
   if (j == 0) {
@@ -941,33 +1029,46 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
   const int32_t sj = L.slot[j];
   const TbVar& Vj = s.tb_var[j];
   const int32_t vskip = Vj.adder >= 0 ? Vj.use : -1;   // the use the slot accounts for
+  int kp = -1, ki = -1;                            // the profile's PodTopologySpread / InterPodAffinity slots
+  for (int kk = 0; kk < prof.n_score; kk++) {
+    const int32_t kind = norm_kind(prof_score(prof, kk));
+    if (kind == kNormPTS) kp = kk;
+    if (kind == kNormIPA) ki = kk;
+  }
+  UseMasks m{};
+  const ksim_topo_use* U = s_use;                  // LDS
+  const WinState* win = s.tb_win + j;
+  uint32_t tf = 0;
+  int soft = -1, nu = 0;
+  if (cross) {
+    m = s_m;
+    nu = s_nu;
+    tf = win->tflags;
+    soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
+  }
   uint64_t v = 0;
   bool inv = false;
   const int32_t local = (k < j && gk) ? key_node(gk) - c.base : -1;
   if (local >= 0 && local < N) {
     const bool own = local >= c.eval_lo && local < c.eval_hi;   // S0 values of g live on its replica
-    // the guess's loads first, all independent
+    // the guess's loads, all independent: stat, row, the uses' values, the raw scores
     const int32_t sv = own ? s.tb_stat[tb_pj(j, sj) * N + local] : kStatNone;
     NodeRow r{};
     if (own) r = load_row(c, local);
+    uint32_t lv[KSIM_MAX_USES];
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_USES; i++) lv[i] = i < nu ? use_value(c, U[i], local) : 0u;
+    const bool ign_g = own && soft >= 0 && s.tb_ign[(size_t)j * N + local] != 0;
+    const int64_t xp0 = (own && kp >= 0) ? s.tb_raw[((size_t)j * KSIM_MAX_SCORE + kp) * N + local] : 0;
+    const int64_t xi0 = (own && ki >= 0) ? s.tb_raw[((size_t)j * KSIM_MAX_SCORE + ki) * N + local] : 0;
     // what pod k's adds change for pod j on g = local (runs that cross only)
     int64_t d_soft = 0, d_ipa = 0;
     bool hit_anti = false, hit_aff = false, hit_score = false;
-    UseMasks m{};
-    const ksim_topo_use* U = nullptr;
-    const WinState* win = s.tb_win + j;
-    uint32_t tf = 0;
-    int soft = -1, nu = 0;
-    if (cross) {
-      m = P.plans[base + j].m;
-      U = P.uses + p.use_first;
-      nu = p.use_count;
-      tf = win->tflags;
-      soft = m.soft ? 31 - __builtin_clz(m.soft) : -1;
-    }
-    for (int i = 0; i < nu; i++) {
+#pragma unroll
+    for (int i = 0; i < KSIM_MAX_USES; i++) {
+      if (i >= nu) break;
       if (i == vskip) continue;
-      const ksim_topo_use u = load_use(U, i);
+      const ksim_topo_use u = U[i];
       if (u.cls < 0) continue;
       int32_t d = 0;
 #pragma unroll
@@ -979,7 +1080,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
       if (d == 0) continue;
       const uint32_t b = 1u << i;
       if ((m.node_count & b) && !(m.hard & b)) {   // g's own count
-        if (use_value(c, u, local) == 0) continue;   // the use ignores a node without its key
+        if (lv[i] == 0) continue;                  // the use ignores a node without its key
         if ((m.anti | m.exist) & b) hit_anti = true;
         if (m.aff & b) hit_aff = true;
         if (m.score & b) {
@@ -1003,27 +1104,45 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
         if (sv != kStatOne) {
           tot = sv;
           if (d_soft || d_ipa) {                   // the changed topology scores, the slot's extrema
+            // the slot's counters and extrema from the staged records
             const uint32_t mk = Vj.use >= 0 ? Vj.mask[sj] : ~0u;
-            int32_t nf, nign;
-            tb_slot_counts(s, j, Vj, mk, nf, nign);
+            int32_t nf = 0, nign = 0;
+            if (Vj.use < 0) {
+              nf = s_dom[kVarDom].nfeas;
+              nign = s_dom[kVarDom].nign;
+            } else {
+              for (int d = 0; d < kVarDom; d++)
+                if (d < Vj.ndom && ((mk >> d) & 1u)) {
+                  nf += s_dom[d].nfeas;
+                  nign += s_dom[d].nign;
+                }
+            }
+            auto ext_of = [&](int e) -> uint64_t {
+              if (Vj.use < 0) return s_dom[kVarDom].ext[e];
+              if ((Vj.zmask >> (e >> 1)) & 1u) return nf > 0 ? ((e & 1) ? min_image(0) : max_image(0)) : 0ull;
+              uint64_t x = 0;
+              for (int d = 0; d < kVarDom; d++)
+                if (d < Vj.ndom && ((mk >> d) & 1u)) x = umax64(x, s_dom[d].ext[e]);
+              return x;
+            };
             const int32_t* hold = Vj.use >= 0 ? s.tb_vhold + tb_pj(j, sj) * 2 * KSIM_MAX_SCORE : win->hold;
             const bool ipa_ne = (tf & kTopoScoreNonEmpty) != 0;
-            for (int kk = 0; kk < prof.n_score; kk++) {
-              const int32_t kind = norm_kind(prof_score(prof, kk));
-              const bool pts = kind == kNormPTS && d_soft != 0 && soft >= 0 && !s.tb_ign[(size_t)j * N + local];
-              const bool ipa = kind == kNormIPA && d_ipa != 0;
+            for (int h = 0; h < 2; h++) {          // PodTopologySpread, then InterPodAffinity
+              const int kk = h == 0 ? kp : ki;
+              const bool pts = h == 0 && kp >= 0 && d_soft != 0 && soft >= 0 && !ign_g;
+              const bool ipa = h == 1 && ki >= 0 && d_ipa != 0;
               if (!pts && !ipa) continue;
-              const int64_t x0 = s.tb_raw[((size_t)j * KSIM_MAX_SCORE + kk) * N + local];
+              const int32_t kind = h == 0 ? kNormPTS : kNormIPA;
+              const int64_t x0 = pts ? xp0 : xi0;
               const int64_t x1 = x0 + (pts ? d_soft : d_ipa);
-              int64_t gmax = from_max_image(tb_slot_ext(s, j, Vj, mk, nf, 2 * kk));
-              int64_t gmin = from_min_image(tb_slot_ext(s, j, Vj, mk, nf, 2 * kk + 1));
+              int64_t gmax = from_max_image(ext_of(2 * kk)), gmin = from_min_image(ext_of(2 * kk + 1));
               if (!tb_keeps_extrema(x0, x1, gmax, gmin, hold[2 * kk], hold[2 * kk + 1], j)) {
                 inv = true;
                 break;
               }
               int64_t r0 = x0, r1 = x1;
               if (pts) {                           // counts -> scores (topologyNormalizingWeight, hostname)
-                const ksim_topo_use u = load_use(U, soft);
+                const ksim_topo_use u = U[soft];
                 const double wt = c.topo_log[(u.flags & KSIM_USEF_HOSTNAME) ? nf - nign : 0];
                 r0 = soft_score(x0, wt, u.arg);
                 r1 = soft_score(x1, wt, u.arg);
@@ -1049,7 +1168,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
     s_wmax[wave] = v;
     s_winv[wave] = b != 0;
   }
-  __syncthreads();
+  lds_barrier();
   if (wave == 0) {
     if (tid == 0) {
       uint64_t mx = 0;
@@ -1067,6 +1186,8 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
       }
 #ifdef KSIM_TB_CLOCKS
       if (j == 0) atomicAdd(&s.dbg[3], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+      atomicAdd(&s.dbg[13], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+      atomicAdd(&s.dbg[14], 1ull);
 #endif
     }
   }
@@ -1076,6 +1197,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_chain_pairs(DevCluster c, Dev
 // table updates as parallel atomics (one (pod, add) / (pod, table) pair per
 // thread; a pod and the pod i* that binds on its node may share entries).
 constexpr int kTbAddSlots = 8;                     // adds / table updates per pod and pass
+static_assert(kTbPods <= kBatchPods / kTbAddSlots, "k_tb_commit: one thread group per pod");
 __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods P, DevState* __restrict__ st,
                                                           DevScratch s, int32_t* __restrict__ chosen_out,
                                                           const uint64_t* __restrict__ pp, int32_t plain) {
@@ -1087,33 +1209,52 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
   const int32_t inv = tid < kTbPods ? (pp ? (int32_t)(pp[kTbPods + tid] != 0) : s.pinv[tid]) : 0;
   const int32_t nchain = *s.chain_end;
   const int32_t vslot = tid < kTbPods ? s.tb_slot[tid] : 0;
+  const int q = tid / kTbAddSlots, e = tid % kTbAddSlots;
+  const uint64_t gq = s.gkey[q];                   // pod q's guess (its node unless q is the cut pod)
   const int32_t base = st->cursor;
   const int32_t nbt = tb_count(st, P, plain);
   if (nbt <= 0) return;
+  // pod q's add / table-update entry e, and the table update's value on the
+  // guessed node: none of it waits for the commit
+  ksim_class_add x0{-1, 0};
+  int4 t0{0, 0, 0, 0};
+  uint32_t pfl = 0, v0 = 0;
+  int32_t acount = 0, afirst = 0, tcount = 0, tfirst = 0;
+  const int32_t gnode = gq ? key_node(gq) - c.base : -1;
+  if (q < nbt) {
+    const ksim_pod& pq = P.pods[base + q];
+    const PodPlan& plq = P.plans[base + q];
+    acount = pq.add_count;
+    afirst = pq.add_first;
+    pfl = plq.flags;
+    tcount = plq.tadd_count;
+    tfirst = plq.tadd_first;
+    if (e < acount) x0 = P.adds[afirst + e];
+    if ((pfl & kPlanTadds) && e < tcount) {
+      t0 = P.ptab_padd[tfirst + e];
+      if (gnode >= 0 && gnode < c.n) v0 = c.labels[(size_t)t0.y * c.n + gnode];
+    }
+  }
   batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt,
                s_node);
   __syncthreads();
-  const int q = tid / kTbAddSlots, e = tid % kTbAddSlots;
-  for (int qq = q; qq < nbt; qq += kBatchPods / kTbAddSlots) {
-    const int32_t node = s_node[qq];
-    if (node < 0) continue;
-    const ksim_pod& p = P.pods[base + qq];
-    const PodPlan& pl = P.plans[base + qq];
-    for (int a = e; a < p.add_count; a += kTbAddSlots) {
-      const ksim_class_add x = P.adds[p.add_first + a];
+  const int32_t node = q < nbt ? s_node[q] : -1;
+  if (node >= 0) {
+    for (int a = e; a < acount; a += kTbAddSlots) {
+      const ksim_class_add x = a == e ? x0 : P.adds[afirst + a];
       atomicAdd(&c.cnt[(size_t)x.cls * c.n + node], x.count);
-      if (!(pl.flags & kPlanTadds)) ptab_add(c, P, x.cls, node, (int64_t)x.count);
+      if (!(pfl & kPlanTadds)) ptab_add(c, P, x.cls, node, (int64_t)x.count);
     }
-    if (pl.flags & kPlanTadds)
-      for (int a = e; a < pl.tadd_count; a += kTbAddSlots) {
-        const int4 t = P.ptab_padd[pl.tadd_first + a];
-        const uint32_t v = c.labels[(size_t)t.y * c.n + node];
+    if (pfl & kPlanTadds)
+      for (int a = e; a < tcount; a += kTbAddSlots) {
+        const int4 t = a == e ? t0 : P.ptab_padd[tfirst + a];
+        const uint32_t v = (a == e && node == gnode) ? v0 : c.labels[(size_t)t.y * c.n + node];
         if (v) atomicAdd(reinterpret_cast<unsigned long long*>(P.ptab + t.x + (t.z == kPtabTotal ? 0u : v)),
                          (unsigned long long)(int64_t)t.w);
       }
   }
   // committed pods whose slot moved their zone verdicts (ksim_get_diag out[26])
-  const uint64_t vb = __ballot(tid < nbt && s_node[tid < kTbPods ? tid : 0] != -2 && vslot != 0);   // (tid < nbt)
+  const uint64_t vb = __ballot(tid < nbt && s_node[tid < kTbPods ? tid : 0] != -2 && vslot != 0);
   if ((tid & 63) == 0 && vb) atomicAdd(s.tb_vpods, (unsigned long long)__popcll(vb));
   // the next batch's counters and extrema start from zero (the rows this batch used)
   for (int x = tid; x < kTbPods * (int)(sizeof(WinState) / 4); x += blockDim.x)
@@ -1131,7 +1272,7 @@ uint32_t launch_tbatch(const LaunchArgs& a, hipStream_t stream, hipEvent_t* evs)
   if (evs) (void)hipEventRecord(evs[0], stream);
   k_tb_filter<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 0);
   if (evs) (void)hipEventRecord(evs[1], stream);
-  k_tb_select<<<grid, 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 0);
+  k_tb_select<<<dim3(grid.x, kTbPods, kVarSlots), 256, 0, stream>>>(a.c, a.P, a.dprof, a.dbp, a.st, a.s, 0);
   if (evs) (void)hipEventRecord(evs[2], stream);
   k_tb_merge<<<dim3(kTbPods, kVarSlots), 64, 0, stream>>>(a.c, a.P, a.st, a.s, nullptr, 0);
   if (evs) (void)hipEventRecord(evs[3], stream);

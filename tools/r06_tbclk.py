@@ -40,6 +40,13 @@ for variant in [None, "tbclk", "ab64"]:
         nb = max(fb[3], 1)
         line += (f"; filter blocks {fb[3] / n:.0f} per launch: setup {fb[0] / nb / 100:.2f} us,"
                  f" plans {fb[1] / nb / 100:.2f} us, extrema {fb[2] / nb / 100:.2f} us")
+        sb = [d["dbg"][k] - d0["dbg"][k] for k in range(9, 13)]
+        ns = max(sb[2], 1)
+        line += (f"; select blocks {sb[2] / n:.0f} per launch: inputs {sb[0] / ns / 100:.2f} us,"
+                 f" slots {sb[1] / ns / 100:.2f} us ({sb[3] / ns:.2f} slots per block)")
+        cb = [d["dbg"][k] - d0["dbg"][k] for k in (13, 14)]
+        line += f"; chain_pairs blocks {cb[1] / n:.1f} per launch, {cb[0] / max(cb[1], 1) / 100:.2f} us each"
+
     print(line, flush=True)
     if variant in (None, "ab64"):
         eng.reset_cluster()

@@ -225,7 +225,7 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
     }
     if (lane == 63) sh[wv] = x;
     if (j == 0) s_first = kBatchPods;
-    __syncthreads();
+    lds_barrier();
     int64_t before = 0;
     for (int w = 0; w < wv; w++) before += sh[w];
     const int32_t ns = (int32_t)(((int64_t)s0 + before + x - proc) % n);
@@ -233,9 +233,9 @@ __device__ __forceinline__ bool window_block(const DevState* __restrict__ st, co
       const uint64_t chg = __ballot(j < nb && ns != s);
       if (chg && lane == 0) atomicMin(&s_first, (j & ~63) + __builtin_ctzll(chg));
     }
-    __syncthreads();
+    lds_barrier();
     const int32_t f = s_first;
-    __syncthreads();                                 // sh / s_first are rewritten next round
+    lds_barrier();                                 // sh / s_first are rewritten next round
     if (f == kBatchPods) {                           // fixpoint: every window exact
       exact = nb;
       break;
@@ -376,16 +376,16 @@ __global__ __launch_bounds__(kWinBuildThreads) void k_win_build(const DevState* 
     s_pc[tid] = x - c;
     if (tid == 63) s_tot0 = x;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid >= 64 && tid < kWinSeqWords) s_pc[tid] += s_tot0;
-  __syncthreads();
+  lds_barrier();
   const int32_t total = s_pc[n_words - 1] + (int32_t)__popcll(s_w[n_words - 1]);
   for (int32_t x = tid; x < n; x += kWinBuildThreads) {         // the positions of the feasible nodes by rank
     const uint64_t w = s_w[x >> 6];
     const int b = x & 63;
     if ((w >> b) & 1ull) s_sel[s_pc[x >> 6] + (int32_t)__popcll(w & ((1ull << b) - 1ull))] = (uint16_t)x;
   }
-  __syncthreads();
+  lds_barrier();
   uint16_t* out = tab0 + (size_t)j * n;
   for (int32_t x = tid; x < n; x += kWinBuildThreads) {
     const uint64_t w = s_w[x >> 6];
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
   if (lane == 0) s_kept[wv] = kept;
-  __syncthreads();
+  lds_barrier();
   if (wv != 0) return;
   // merge: entry x = w * T + e (keys are unique per node) sits in lane x % 64, slot x / 64
   uint64_t key[kSlots];
@@ -791,19 +791,19 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
   }
   __shared__ int32_t s_lost[2];
   if (tid < 2) s_lost[tid] = 0;
-  __syncthreads();
+  lds_barrier();
   {
     const int32_t nt = __popcll(__ballot(lost_t)), na = __popcll(__ballot(lost_a));
     if (lane == 0 && nt) atomicAdd(&s_lost[0], nt);
     if (lane == 0 && na) atomicAdd(&s_lost[1], na);
   }
-  __syncthreads();
+  lds_barrier();
   if (s_lost[0] > 0 && s_lost[0] >= pnorm[4 * j + 2]) brk = true;   // every holder of a maximum left
   if (s_lost[1] > 0 && s_lost[1] >= pnorm[4 * j + 3]) brk = true;
   const bool any_brk = __syncthreads_or(brk);
   v = wave_max_u64_dpp(v);
   if (lane == 0) s_wmax[wave] = v;
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     uint64_t m = 0;
     for (int w = 0; w < kBatchPods / 64; w++) m = umax64(m, s_wmax[w]);
@@ -846,9 +846,9 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_commit(DevCluster c, DevPo
   const int32_t nchain0 = *chain_end;
   s_aw[threadIdx.x] = aw;
   if (threadIdx.x == 0) s_fb = nchain0;
-  __syncthreads();
+  lds_barrier();
   block_first_min(&s_fb, (int32_t)threadIdx.x < nchain0 && brk);
-  __syncthreads();
+  lds_barrier();
 #ifdef KSIM_ADAPT_DBG
   const int32_t nb_dbg = batch_pods(st), fb_dbg = s_fb;
   const int32_t cur_dbg = st->cursor;
@@ -916,29 +916,29 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
     s_unsched = 0;
     s_evals = 0;
   }
-  __syncthreads();
+  lds_barrier();
   // the chain ends before the first broken window
 #pragma unroll
   for (int q = 0; q < kChunks; q++) {
     const uint64_t mm = __ballot(q * 256 + tid < nchain0 && brk[q]);
     if (mm && lane == 0) atomicMin(&s_fb, q * 256 + (tid & ~63) + __builtin_ctzll(mm));
   }
-  __syncthreads();
+  lds_barrier();
   const int32_t nchain = s_fb;
   if (tid == 0) s_istar = nchain;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int q = 0; q < kChunks; q++) {
     const uint64_t mm = __ballot(q * 256 + tid < nchain && m[q] > g[q]);   // keys are unique per node
     if (mm && lane == 0) atomicMin(&s_istar, q * 256 + (tid & ~63) + __builtin_ctzll(mm));
   }
-  __syncthreads();
+  lds_barrier();
   const int32_t istar = s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
 #pragma unroll
   for (int q = 0; q < kChunks; q++)
     if (q * 256 + tid == istar && istar < nchain) s_inode = key_node(m[q]) - c.base;
-  __syncthreads();
+  lds_barrier();
   const int32_t inode = s_inode;
   // the entries whose guessed node is in this block: pod t's requests (and pod
   // i*'s when i* took the same node)
@@ -981,7 +981,7 @@ __global__ __launch_bounds__(256) void k_adapt_mask_commit(DevCluster c, DevPods
       const uint64_t gk = L.g1[k];
       if (chosen_out) chosen_out[cur0 + k] = k == istar ? inode + c.base : (gk ? key_node(gk) : -1);
     }
-  __syncthreads();
+  lds_barrier();
   if (bl == 0 && tid == 0) {
     // st[p] = st[p ^ 1] with the commit's updates, written whole: its words
     // loaded together, no store-then-reload chain (see k_batch_top_commit)

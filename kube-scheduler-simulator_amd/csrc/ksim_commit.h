@@ -37,7 +37,9 @@ struct ResCols {
 };
 
 // Validate the chain against M (pmax) and commit (one block of kBatchPods
-// threads).  Binds are applied by the shard that owns the node.  s_aw (ADAPT
+// threads).  Its barriers hand off LDS only (lds_barrier): the row loads stay
+// in flight across them and the row stores are not waited for (each committed
+// pod's node has one writer; the next launch sees them).  Binds are applied by the shard that owns the node.  s_aw (ADAPT
 // batch): per pod {scan start, cut offset or -1} (the awin pairs), staged in
 // LDS by the caller from loads issued at kernel start, so neither the
 // evaluation count nor nextStartNodeIndex waits for a global load after the
@@ -60,11 +62,11 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
   const int tid = threadIdx.x;
   if (inv_own) {                                   // block-uniform
     if (tid == 0) *s_istar = nchain;
-    __syncthreads();
+    lds_barrier();
     block_first_min(s_istar, tid < nchain && *inv_own);
-    __syncthreads();
+    lds_barrier();
     nchain = *s_istar;
-    __syncthreads();                               // every read before s_istar is reused below
+    lds_barrier();                               // every read before s_istar is reused below
   }
   const int32_t base = st->cursor;
   const int32_t nb = min(nb_cap, st->end - base);   // the batch's pods (statistics: cut or truncated)
@@ -99,9 +101,9 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     *s_unsched = 0;
     s_evals = 0;
   }
-  __syncthreads();
+  lds_barrier();
   block_first_min(s_istar, tid < nchain && mj > gj);   // keys are unique per node: never equal unless 0
-  __syncthreads();
+  lds_barrier();
   const int32_t istar = *s_istar;
   const int32_t committed = istar < nchain ? istar + 1 : nchain;
   const int32_t inode = istar < nchain ? key_node(s_m[istar]) : -1;
@@ -142,7 +144,7 @@ __device__ __forceinline__ void batch_commit(const DevCluster& c, const DevPods&
     const int2 w = s_aw[tid];
     atomicAdd(&s_evals, (int32_t)window_local(c, w.x, w.y >= 0 ? (int64_t)w.y + 1 : c.n_total));
   }
-  __syncthreads();
+  lds_barrier();
   if (tid == 0) {
     DevState ns;
     __builtin_memcpy(&ns, stw, sizeof(ns));

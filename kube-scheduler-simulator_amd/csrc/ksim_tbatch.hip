@@ -1237,7 +1237,7 @@ __global__ __launch_bounds__(kBatchPods) void k_tb_commit(DevCluster c, DevPods 
   }
   batch_commit(c, P, st, g, m, s.pmax, nchain, chosen_out, &s_istar, &s_sched, &s_unsched, nullptr, &inv, nbt,
                s_node);
-  __syncthreads();
+  lds_barrier();                                   // s_node
   const int32_t node = q < nbt ? s_node[q] : -1;
   if (node >= 0) {
     for (int a = e; a < acount; a += kTbAddSlots) {

@@ -138,7 +138,7 @@ def host_cpu() -> dict:
 
 
 def cpu_threads_sweep(arg: str) -> list:
-    """--cpu-threads: a comma list, "sweep" (1, 4, 16, 64 and every logical
+    """--cpu-threads: a comma list, "sweep" (1, 4, 8, 16, 64 and every logical
     CPU: the 1 -> 16 scaling is reported), or one count.  The sweep stops at
     4x the cgroup CPU quota when one is set: the GPU box grants 16 CPUs of its
     256, and 256 OpenMP threads time-sliced on them ran 100 cycles in 43.6 s
@@ -148,7 +148,7 @@ def cpu_threads_sweep(arg: str) -> list:
     if arg == "sweep":
         quota = host_cpu()["cgroup_cpu_quota"]
         cap = n if not quota else max(16, int(4 * quota))
-        return sorted({t for t in (1, 4, 16, 64, n) if t <= min(n, cap)} | {min(16, n)})
+        return sorted({t for t in (1, 4, 8, 16, 64, n) if t <= min(n, cap)} | {min(16, n)})
     return [int(x) for x in arg.split(",")]
 
 

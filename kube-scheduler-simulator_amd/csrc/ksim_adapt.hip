@@ -43,9 +43,17 @@
 namespace ksim {
 
 // Filter outcome of a batchable pod on a node: static filters and Fit only.
+// pi: the pod's queue index; a pod in a static class (DevPods::stab, built for
+// the loaded queue) reads its static verdict from the class row instead of
+// running the static filters (taints, node affinity: uniform loops the
+// scalar unit runs per node and pod).
 __device__ __forceinline__ bool batch_feasible(const DevCluster& c, const DevPods& P, const BatchProg& bp,
-                                               const ksim_pod& p, const NodeRow& r, bool trivial) {
-  if (!trivial && !static_filters_pass(c, P, bp, p, r)) return false;
+                                               const ksim_pod& p, const NodeRow& r, bool trivial, int32_t pi) {
+  if (!trivial) {
+    const int32_t scls = P.stab ? P.sclass[pi] : -1;   // uniform
+    if (scls >= 0 ? !stab_pass(P.stab[(size_t)scls * c.n + r.node]) : !static_filters_pass(c, P, bp, p, r))
+      return false;
+  }
   return !bp.has_fit_filter || !fits_request(r, p, c.n_scalar, c.fit_ignore);
 }
 
@@ -124,8 +132,8 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
     const int32_t jb = j + 1 < j1 ? j + 1 : j;
     const bool ta = (P.bflags[base + j] & kBatchStaticTrivial) != 0;   // uniform
     const bool tb = (P.bflags[base + jb] & kBatchStaticTrivial) != 0;
-    const bool fa = on && batch_feasible(c, P, bp, P.pods[base + j], r, ta);
-    const bool fb = on && batch_feasible(c, P, bp, P.pods[base + jb], r, tb);
+    const bool fa = on && batch_feasible(c, P, bp, P.pods[base + j], r, ta, base + j);
+    const bool fb = on && batch_feasible(c, P, bp, P.pods[base + jb], r, tb, base + jb);
     const uint64_t ma = __ballot(fa), mb = __ballot(fb);
     if (lane == 0) {
       amask[(size_t)j * n_words + w] = ma;
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
         NodeRow r = load_row(c, node);
         row_add_pod(r, P.pods[base + k], 1);
         const ksim_pod& p = P.pods[base + j];
-        const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0);
+        const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0, base + j);
         const bool was = (amask[(size_t)j * n_words + (g >> 6)] >> (g & 63)) & 1ull;
         // a window that stops before the ring's end shifts when a kept node
         // stops fitting; one that scans every node keeps its span, and for

@@ -638,6 +638,58 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       return node_key(node);
     };
     NormRaw mx{0, 0};
+    if (fk) {
+      // the FAST keys of a static class: two nodes per step with every load
+      // of both (bitmap words, class words, rows) issued before the bit tests,
+      // as the FAST loop above; the same nodes, maxima and keys as the loops below
+      const ksim_pod pf = fast_pod_fields(p);
+      const FastProg q = fast_prog(bp);
+      if (normv) {
+        NormAcc acc;
+#pragma unroll 1
+        for (int32_t off = tid; off < kend; off += 2 * NT) {
+          int32_t n1 = s + off, n2 = s + off + NT;
+          if (n1 >= n) n1 -= n;
+          if (n2 >= n) n2 -= n;
+          const bool v2 = off + NT < kend;
+          if (!v2) n2 = n1;
+          const uint64_t w1 = mask[n1 >> 6], w2 = mask[n2 >> 6], x1 = srow[n1], x2 = srow[n2];
+          __builtin_amdgcn_sched_barrier(0);
+          if ((w1 >> (n1 & 63)) & 1ull) acc.take(stab_raw(x1, P, p));
+          if (v2 && ((w2 >> (n2 & 63)) & 1ull)) acc.take(stab_raw(x2, P, p));
+        }
+        mx = norm_maxima<NT>(acc, pnorm, j);
+      }
+#pragma unroll 1
+      for (int32_t off = tid; off < kend; off += 2 * NT) {
+        int32_t n1 = s + off, n2 = s + off + NT;
+        if (n1 >= n) n1 -= n;
+        if (n2 >= n) n2 -= n;
+        const bool v2 = off + NT < kend;
+        if (!v2) n2 = n1;
+        const uint64_t w1 = mask[n1 >> 6], w2 = mask[n2 >> 6], x1 = srow[n1], x2 = srow[n2];
+        const NodeRow r1 = load_res_row_off(c, n1), r2 = load_res_row_off(c, n2);
+        const double c1 = ld_off(c.inv_cpu, (uint32_t)n1 << 3), m1 = ld_off(c.inv_mem, (uint32_t)n1 << 3);
+        const double c2 = ld_off(c.inv_cpu, (uint32_t)n2 << 3), m2 = ld_off(c.inv_mem, (uint32_t)n2 << 3);
+        __builtin_amdgcn_sched_barrier(0);
+        if ((w1 >> (n1 & 63)) & 1ull) {
+          kept++;
+          uint64_t k = dyn_key_fast_t<false>(q, pf, r1, c1, m1, hseed, c.base + n1);
+          if (normv && k) k += (uint64_t)norm_part(bp, stab_raw(x1, P, p), mx) << 44;
+          a[kTopT - 1] = umax64(a[kTopT - 1], k);
+#pragma unroll
+          for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+        }
+        if (v2 && ((w2 >> (n2 & 63)) & 1ull)) {
+          kept++;
+          uint64_t k = dyn_key_fast_t<false>(q, pf, r2, c2, m2, hseed, c.base + n2);
+          if (normv && k) k += (uint64_t)norm_part(bp, stab_raw(x2, P, p), mx) << 44;
+          a[kTopT - 1] = umax64(a[kTopT - 1], k);
+#pragma unroll
+          for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+        }
+      }
+    } else {
     if (normv) {
       // the maxima over the kept nodes and how many kept nodes hold each
       // (pnorm[4 j + 2..3]): a window that scans every node never shifts, so
@@ -664,6 +716,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       a[kTopT - 1] = umax64(a[kTopT - 1], k);
 #pragma unroll
       for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+    }
     }
   }
   // per wave: a lane can be popped at most T times and holds its T best, so
@@ -773,8 +826,13 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
       const int32_t kend = cut >= 0 ? cut : n;
       if (off < kend || off == cut) {
         NodeRow r = load_row(c, node);
+        // a static class (block-uniform): the raw normalized scores from its
+        // row, and on a run_fast cluster the FAST key (as k_adapt_top's list keys)
+        const int32_t scls = P.stab ? P.sclass[base + j] : -1;
+        const uint64_t sw = scls >= 0 ? P.stab[(size_t)scls * c.n + node] : 0;
         row_add_pod(r, P.pods[base + k], 1);
         const ksim_pod& p = P.pods[base + j];
+        auto raw = [&]() -> NormRaw { return scls >= 0 ? stab_raw(sw, P, p) : norm_raw(c, P, p, r); };
         const bool now = batch_feasible(c, P, bp, p, r, (P.bflags[base + j] & kBatchStaticTrivial) != 0, base + j);
         const bool was = (amask[(size_t)j * n_words + (g >> 6)] >> (g & 63)) & 1ull;
         // a window that stops before the ring's end shifts when a kept node
@@ -786,14 +844,19 @@ __global__ __launch_bounds__(kBatchPods) void k_adapt_pairs(DevCluster c, DevPod
           if (cut >= 0) {
             brk = true;
           } else if (normv) {
-            const NormRaw x = norm_raw(c, P, p, r);
+            const NormRaw x = raw();
             lost_t = pnorm[4 * j] > 0 && x.tt == pnorm[4 * j];
             lost_a = pnorm[4 * j + 1] > 0 && x.na == pnorm[4 * j + 1];
           }
         }
-        if (off < kend && now) v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base, c.fit_ignore);
-        if (normv && v)
-          v += (uint64_t)norm_part(bp, norm_raw(c, P, p, r), NormRaw{pnorm[4 * j], pnorm[4 * j + 1]}) << 44;
+        if (off < kend && now) {
+          if (scls >= 0 && P.stab_fast)
+            v = dyn_key_fast(bp, fast_pod_fields(p), r, c.inv_cpu[node], c.inv_mem[node],
+                             prof.tiebreak_seed ^ ((uint64_t)(st->pod_seq + j) << 20), c.base + node);
+          else
+            v = dyn_key(prof, bp, p, r, c.n_scalar, st->pod_seq + j, c.base, c.fit_ignore);
+        }
+        if (normv && v) v += (uint64_t)norm_part(bp, raw(), NormRaw{pnorm[4 * j], pnorm[4 * j + 1]}) << 44;
       }
     }
   }

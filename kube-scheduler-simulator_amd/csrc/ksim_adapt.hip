@@ -93,8 +93,9 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
   // to pass; batchable pods request no scalar resources).
   __shared__ int64_t s_pq[4][64][4];
   __shared__ uint64_t s_mk[4][64];
+  __shared__ int32_t s_cls[4][64];                 // static class, -2 trivial (static filters pass)
   const int wv = threadIdx.x >> 6;
-  bool nontriv = false;
+  bool nontriv = false, generic = false;
   if (lane < j1 - j0) {
     const ksim_pod& q = P.pods[base + j0 + lane];
     // fits_request: a pod requesting nothing (and no scalar resources) needs
@@ -104,6 +105,41 @@ __global__ __launch_bounds__(256) void k_adapt_mask_ns(DevCluster c, DevPods P, 
     s_pq[wv][lane][1] = none ? INT64_MIN : q.req_mem;
     s_pq[wv][lane][2] = none ? INT64_MIN : q.req_eph;
     nontriv = !(P.bflags[base + j0 + lane] & kBatchStaticTrivial);
+    const int32_t cls = !nontriv ? -2 : P.stab ? P.sclass[base + j0 + lane] : -1;
+    s_cls[wv][lane] = cls;
+    generic = cls == -1 || (q.flags & KSIM_POD_HAS_SCALAR);
+  }
+  if (__ballot(nontriv) != 0 && __ballot(generic) == 0) {   // wave-uniform
+    // static-class pods without scalar requests: each pod's verdict is its
+    // class row's word at this node (batch_feasible), the Fit filter the
+    // columns as below; eight pods' class words loaded before any is used
+    const int32_t np = j1 - j0;
+    const bool fit = bp.has_fit_filter != 0;
+    const uint64_t room = fit ? __ballot(on && c.num_pods[x] + 1 <= c.alloc_pods[x]) : __ballot(on);
+    const int64_t fc = c.alloc_cpu[x] - c.req_cpu[x];
+    const int64_t fm = c.alloc_mem[x] - c.req_mem[x];
+    const int64_t fe = c.alloc_eph[x] - c.req_eph[x];
+#pragma unroll 1
+    for (int32_t l0 = 0; l0 < np; l0 += 8) {
+      int32_t cl[8];
+      uint64_t sw[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        cl[t] = l0 + t < np ? s_cls[wv][l0 + t] : -2;
+        sw[t] = P.stab[(size_t)(cl[t] >= 0 ? cl[t] : 0) * c.n + x];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int32_t l = l0 + t;
+        if (l >= np) break;                          // uniform
+        const bool pass = cl[t] < 0 || stab_pass(sw[t]);
+        const bool fits = !fit || ((s_pq[wv][l][0] <= fc) & (s_pq[wv][l][1] <= fm) & (s_pq[wv][l][2] <= fe));
+        const uint64_t mk = room & __ballot(pass && fits);
+        if (lane == 0) s_mk[wv][l] = mk;
+      }
+    }
+    if (lane < np) amask[(size_t)(j0 + lane) * n_words + w] = s_mk[wv][lane];
+    return;
   }
   if (__ballot(nontriv) == 0) {                    // wave-uniform
     // only the Fit filter's columns (the table is re-read once per pod group)

@@ -514,6 +514,17 @@ static void launch_window_dbl(const LaunchArgs& a, int32_t n_words, int32_t k, h
 // (every block scans all B bitmaps: B x W words from L2 per block).
 constexpr int32_t kWinFusedWords = 256;
 
+// k_adapt_top's kept-node list (static-class FAST keys): windows with at most
+// this many kept nodes are compacted into LDS before they are keyed.
+constexpr int kAdaptList = 4096;
+// The bits of nodes [a, b) within bitmap word w.
+__device__ __forceinline__ uint64_t word_range(int32_t w, int32_t a, int32_t b) {
+  const int32_t lo = max(a - w * 64, 0), hi = min(b - w * 64, 64);
+  if (hi <= lo) return 0ull;
+  const uint64_t up = hi >= 64 ? ~0ull : (1ull << hi) - 1ull;
+  return up & ~((1ull << lo) - 1ull);
+}
+
 // One block (4 waves) per pod: the kept nodes' TB keys -> the pod's top-T
 // (complete when it lists every kept node).  Each wave keeps its lanes' best T
 // keys and extracts its own top-T; wave 0 merges the four lists.  Pods past
@@ -680,6 +691,66 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       // as the FAST loop above; the same nodes, maxima and keys as the loops below
       const ksim_pod pf = fast_pod_fields(p);
       const FastProg q = fast_prog(bp);
+      // the window's kept nodes first compacted into LDS (one bitmap word per
+      // thread, range-masked to the window's offsets [0, kend) from s), so a
+      // thread keys at most ceil(kept / NT) nodes, each with all of its loads
+      // in one round trip, instead of stepping over the window's whole span
+      __shared__ int32_t s_list[kAdaptList];
+      __shared__ int32_t s_nl;
+      if (tid == 0) s_nl = 0;
+      lds_barrier();
+      {
+        const bool wrap = s + kend > n;
+        const int32_t b1 = wrap ? n : s + kend, b2 = wrap ? s + kend - n : 0;
+        for (int32_t w = tid; w < n_words; w += NT) {
+          uint64_t bits = mask[w] & (word_range(w, s, b1) | word_range(w, 0, b2));
+          const int32_t cnt = __popcll(bits);
+          int32_t pos = cnt ? atomicAdd(&s_nl, cnt) : 0;
+          for (; bits; bits &= bits - 1, pos++)
+            if (pos < kAdaptList) s_list[pos] = w * 64 + __builtin_ctzll(bits);
+        }
+      }
+      lds_barrier();
+      const int32_t nl = s_nl;
+      if (nl <= NT) {                               // block-uniform: one kept node per thread at most
+        const bool has = tid < nl;
+        const int32_t nd = has ? s_list[tid] : 0;
+        const uint64_t x = srow[nd];
+        const NodeRow r = load_res_row_off(c, nd);
+        const double ci = ld_off(c.inv_cpu, (uint32_t)nd << 3), mi = ld_off(c.inv_mem, (uint32_t)nd << 3);
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t k = has ? dyn_key_fast_t<false>(q, pf, r, ci, mi, hseed, c.base + nd) : 0;
+        if (normv) {
+          NormAcc acc;
+          if (has) acc.take(stab_raw(x, P, p));
+          mx = norm_maxima<NT>(acc, pnorm, j);
+          if (k) k += (uint64_t)norm_part(bp, stab_raw(x, P, p), mx) << 44;
+        }
+        kept += has ? 1 : 0;
+        a[kTopT - 1] = umax64(a[kTopT - 1], k);
+#pragma unroll
+        for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+      } else if (nl <= kAdaptList) {                // block-uniform
+        if (normv) {
+          NormAcc acc;
+#pragma unroll 1
+          for (int32_t i = tid; i < nl; i += NT) acc.take(stab_raw(srow[s_list[i]], P, p));
+          mx = norm_maxima<NT>(acc, pnorm, j);
+        }
+#pragma unroll 1
+        for (int32_t i = tid; i < nl; i += NT) {
+          const int32_t nd = s_list[i];
+          const uint64_t x = srow[nd];
+          const NodeRow r = load_res_row_off(c, nd);
+          const double ci = ld_off(c.inv_cpu, (uint32_t)nd << 3), mi = ld_off(c.inv_mem, (uint32_t)nd << 3);
+          kept++;
+          uint64_t k = dyn_key_fast_t<false>(q, pf, r, ci, mi, hseed, c.base + nd);
+          if (normv && k) k += (uint64_t)norm_part(bp, stab_raw(x, P, p), mx) << 44;
+          a[kTopT - 1] = umax64(a[kTopT - 1], k);
+#pragma unroll
+          for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
+        }
+      } else {
       if (normv) {
         NormAcc acc;
 #pragma unroll 1
@@ -724,6 +795,7 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
 #pragma unroll
           for (int t = kTopT - 1; t > 0; t--) cswap_desc(a[t - 1], a[t]);
         }
+      }
       }
     } else {
     if (normv) {

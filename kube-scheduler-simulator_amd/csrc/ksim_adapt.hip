@@ -695,23 +695,29 @@ __global__ __launch_bounds__(NT) void k_adapt_top(DevCluster c, DevPods P, const
       // thread, range-masked to the window's offsets [0, kend) from s), so a
       // thread keys at most ceil(kept / NT) nodes, each with all of its loads
       // in one round trip, instead of stepping over the window's whole span
+      // (windows of at most 2 NT nodes take the stepping loop: one round trip
+      // there, two here)
       __shared__ int32_t s_list[kAdaptList];
       __shared__ int32_t s_nl;
-      if (tid == 0) s_nl = 0;
-      lds_barrier();
-      {
+      int32_t nl = kAdaptList + 1;
+      if (kend > 2 * NT) {                          // block-uniform
+        if (tid == 0) s_nl = 0;
+        lds_barrier();
+        // the window's words only: piece 1 [s, b1), piece 2 [0, b2) after the wrap
         const bool wrap = s + kend > n;
         const int32_t b1 = wrap ? n : s + kend, b2 = wrap ? s + kend - n : 0;
-        for (int32_t w = tid; w < n_words; w += NT) {
-          uint64_t bits = mask[w] & (word_range(w, s, b1) | word_range(w, 0, b2));
+        const int32_t c1 = ((b1 - 1) >> 6) - (s >> 6) + 1, c2 = b2 > 0 ? ((b2 - 1) >> 6) + 1 : 0;
+        for (int32_t t = tid; t < c1 + c2; t += NT) {
+          const int32_t w = t < c1 ? (s >> 6) + t : t - c1;
+          uint64_t bits = mask[w] & (t < c1 ? word_range(w, s, b1) : word_range(w, 0, b2));
           const int32_t cnt = __popcll(bits);
           int32_t pos = cnt ? atomicAdd(&s_nl, cnt) : 0;
           for (; bits; bits &= bits - 1, pos++)
             if (pos < kAdaptList) s_list[pos] = w * 64 + __builtin_ctzll(bits);
         }
+        lds_barrier();
+        nl = s_nl;
       }
-      lds_barrier();
-      const int32_t nl = s_nl;
       if (nl <= NT) {                               // block-uniform: one kept node per thread at most
         const bool has = tid < nl;
         const int32_t nd = has ? s_list[tid] : 0;
